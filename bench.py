@@ -1,0 +1,199 @@
+"""Benchmark: DAMA fwd+bwd frames/s at 224x224, 64 frames per GPU, dim 128
+(BASELINE.json configs[1]; configs[2] when launched with torchrun on 8 GPUs).
+
+One step = the reference training step of train.py:93-115 on synthetic data:
+``DeepfakeDetector.forward(x[8, 8, 3, 224, 224], batch_size=8, 'dynamic')`` (one
+64-frame ``_process_frame`` chunk, dama.py:179-186) under bf16 autocast,
+``combined_loss`` at epoch=1/max_epochs=1 (BCE + orthogonal term), backward,
+Adam(lr 1e-4, wd 1e-4) step.  Random-init weights, N(0,1) frames.
+
+Multi-GPU: one process per GPU (torchrun), DDP over RCCL; every rank runs its own
+64-frame chunk (weak scaling; BatchNorm statistics per rank like the reference's
+per-replica DataParallel semantics).  value = all frames / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'efficient-wavelet-vit_amd'))
+
+METRIC = 'frames/sec fwd+bwd, 224×224 bs=64 dim=128, at 1/2/4/8 MI355X'
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+BF16_PEAK_TFS = 2500.0     # dense bf16 MFMA (spec, no sparsity)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--frames', type=int, default=64, help='frames per GPU per step (one chunk)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-steps', type=int, default=4)
+    return ap.parse_args()
+
+
+def build_step(dev, frames, rank):
+    from network.model import DeepfakeDetector
+    from network.losses import combined_loss
+    torch.manual_seed(0)                                   # identical init on every rank
+    videos = 8
+    per_video = frames // videos
+    model = DeepfakeDetector(3, 128, batch_size=per_video).to(dev).to(memory_format=torch.channels_last)
+    ddp = dist.is_initialized() and dist.get_world_size() > 1
+    net = model
+    if ddp:
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], broadcast_buffers=False,
+                                                        gradient_as_bucket_view=True, bucket_cap_mb=64)
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(videos, per_video, 3, 224, 224, device=dev, generator=g)
+    gl = torch.Generator(device=dev).manual_seed(2000 + rank)
+    y = torch.bernoulli(torch.full((videos,), 0.5, device=dev), generator=gl)
+    model.train()
+
+    def step():
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = net(x, per_video, 'dynamic')
+        loss, _ = combined_loss(out, y, crit, 1, 1)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+    return step
+
+
+def kernel_table(records):
+    """Per ewvit entry point: launches, mean duration, algorithmic rate."""
+    table = {}
+    for name, recs in records.items():
+        ms = [s.elapsed_time(e) for s, e, _ in recs]
+        if not ms:
+            continue
+        tot = sum(ms)
+        byt = sum(w.get('bytes', 0.0) for _, _, w in recs)
+        fl = sum(w.get('flops', 0.0) for _, _, w in recs)
+        table[name] = {'launches': len(ms), 'total_ms': tot, 'avg_us': 1e3 * tot / len(ms),
+                       'GB/s': byt / (tot * 1e-3) / 1e9 if tot else 0.0,
+                       'TFLOP/s': fl / (tot * 1e-3) / 1e12 if tot else 0.0,
+                       'bytes_per_launch': byt / len(ms), 'flops_per_launch': fl / len(ms)}
+    return table
+
+
+def roofline_for(name, row):
+    if name == 'ewvit_gemm':
+        ach = row['TFLOP/s']
+        return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': BF16_PEAK_TFS,
+                'unit': 'TFLOP/s', 'frac': round(ach / BF16_PEAK_TFS, 5), 'traffic': None,
+                'avg_us': round(row['avg_us'], 3), 'work_per_launch': row['flops_per_launch']}
+    ach = row['GB/s']
+    return {'kernel': name, 'bound': 'hbm', 'achieved': round(ach, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(ach / HBM_PEAK_GBS, 5), 'traffic': None, 'avg_us': round(row['avg_us'], 3),
+            'work_per_launch': row['bytes_per_launch']}
+
+
+def cpu_baseline(steps):
+    """The oracle (CPU fp32 eager restatement of the reference, same op sequence)
+    timed on this host: 8-frame chunk, fwd+bwd+Adam."""
+    sys.path.insert(0, REPO)
+    from oracle import model as om
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get('OMP_NUM_THREADS', threads)))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    m = om.DeepfakeDetector(3, 128, batch_size=8)
+    m.train()
+    opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5]))
+    x = torch.randn(1, 8, 3, 224, 224)
+    y = torch.tensor([1.0])
+
+    def step():
+        out = m(x, 8, 'dynamic')
+        om.combined_loss(out, y, crit, 1, 1).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    step()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t
+    return {'value': round(8 * steps / dt, 3), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle fp32 eager, {steps} steps x 8 frames (1 chunk) fwd+bwd+Adam, after 1 warm-up'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    import ewvit
+    ewvit.load_library()                       # fail loudly if the HIP library is missing
+    step = build_step(dev, args.frames, rank)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # per-kernel timing pass (HIP events around every ewvit launch, separate from the timed loop)
+    ewvit._lib.enable_timing(True)
+    kt = max(3, min(args.steps, 5))
+    for _ in range(kt):
+        step()
+    torch.cuda.synchronize()
+    table = kernel_table(ewvit._lib.timing_records())
+    ewvit._lib.enable_timing(False)
+    for r in table.values():
+        r['per_step'] = r['launches'] / kt
+
+    if rank == 0:
+        frames = args.frames * world * args.steps
+        res = {'metric': METRIC, 'value': round(frames / elapsed, 2), 'unit': 'frames/s', 'n_gpus': world,
+               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(1e3 * elapsed / args.steps, 3),
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
+               'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
+               'config': {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
+                          'image': 224, 'frames_per_gpu': args.frames, 'dim': 128,
+                          'global_batch': args.frames * world, 'parallelism': f'ddp{world}'}}
+        dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
+        res['roofline'] = roofline_for(*dom) if dom else None
+        res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                          for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
+        if 'ewvit_dwt_haar_fwd' in table:
+            res['dwt_roofline'] = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'])
+        res['cpu_baseline'] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_steps)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,283 @@
+// Depthwise 3x3 convolution, channels-last (NHWC), forward / input-grad /
+// weight-grad (gfx950).
+//
+// EfficientNetV2-S's 30 MBConv blocks each carry one depthwise 3x3 conv
+// (groups = channels = 256..1536, stride 1 or 2, pad 1; torchvision
+// Conv2dNormActivation(groups=C), reached from the reference via
+// network/sfe.py:111-113,150).  Profiled on MI355X through MIOpen/CK these were
+// the step's dominant kernels (naive_conv fwd/bwd-data, ~12 ms per
+// grouped-conv weight-grad launch) although the op is purely HBM-bound:
+// 9 MACs per element against 2 x 2 bytes of bf16 traffic.
+//
+// Layout: x [N, H, W, C], y [N, Ho, Wo, C], w [C, 3, 3] (fp32 master weights).
+// One thread owns 8 consecutive channels (one 16-B bf16 vector); the 3x3 taps of
+// neighbouring pixels are re-read through L1/L2, so HBM traffic stays ~1x in +
+// 1x out.  The weight gradient reduces N*Ho*Wo products per (c, tap) in fp32:
+// per-block partial slabs (deterministic, no atomics) + a second reduction pass.
+#include "common.h"
+
+namespace ewvit {
+
+template <int DT>
+struct Vec8 {
+  __device__ __forceinline__ static void load(const void *p, int64_t i, float (&v)[8]) {
+    if (DT == EWVIT_BF16) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16_t *>(p) + i);
+      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+    } else {
+      const float4 *q = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + i);
+      const float4 a = q[0], b = q[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+  }
+  __device__ __forceinline__ static void store(void *p, int64_t i, const float (&v)[8]) {
+    if (DT == EWVIT_BF16) {
+      unsigned w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = (unsigned)f2bf(v[2 * j]) | ((unsigned)f2bf(v[2 * j + 1]) << 16);
+      *reinterpret_cast<uint4 *>(reinterpret_cast<bf16_t *>(p) + i) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      float4 *q = reinterpret_cast<float4 *>(reinterpret_cast<float *>(p) + i);
+      q[0] = make_float4(v[0], v[1], v[2], v[3]);
+      q[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+};
+
+struct DwShape {
+  int N, H, W, C, Ho, Wo, stride, pad;
+};
+
+template <int DT>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const void *__restrict__ x, const float *__restrict__ w,
+                                                     void *__restrict__ y, DwShape s) {
+  const int C8 = s.C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)s.N * s.Ho * s.Wo * C8;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % C8);
+  int64_t t = idx / C8;
+  const int wo = (int)(t % s.Wo);
+  t /= s.Wo;
+  const int ho = (int)(t % s.Ho);
+  const int n = (int)(t / s.Ho);
+  const int c = c8 * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int hi = ho * s.stride - s.pad + kh;
+    if (hi < 0 || hi >= s.H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int wi = wo * s.stride - s.pad + kw;
+      if (wi < 0 || wi >= s.W) continue;
+      float v[8];
+      Vec8<DT>::load(x, (((int64_t)n * s.H + hi) * s.W + wi) * s.C + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], w[(c + j) * 9 + kh * 3 + kw], acc[j]);
+    }
+  }
+  Vec8<DT>::store(y, idx * 8, acc);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void dw_bwd_data_kernel(const void *__restrict__ dy, const float *__restrict__ w,
+                                                          void *__restrict__ dx, DwShape s) {
+  const int C8 = s.C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)s.N * s.H * s.W * C8;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % C8);
+  int64_t t = idx / C8;
+  const int wi = (int)(t % s.W);
+  t /= s.W;
+  const int hi = (int)(t % s.H);
+  const int n = (int)(t / s.H);
+  const int c = c8 * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int hn = hi + s.pad - kh;           // = ho * stride
+    if (hn < 0 || hn % s.stride) continue;
+    const int ho = hn / s.stride;
+    if (ho >= s.Ho) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int wn = wi + s.pad - kw;
+      if (wn < 0 || wn % s.stride) continue;
+      const int wo = wn / s.stride;
+      if (wo >= s.Wo) continue;
+      float v[8];
+      Vec8<DT>::load(dy, (((int64_t)n * s.Ho + ho) * s.Wo + wo) * s.C + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], w[(c + j) * 9 + kh * 3 + kw], acc[j]);
+    }
+  }
+  Vec8<DT>::store(dx, idx * 8, acc);
+}
+
+// Weight gradient, pass 1: block = 64 channels x a slab of output pixels.
+// tid = pl*8 + cg: 8 channel groups (8 channels each) x 32 pixel lanes.
+constexpr int DWW_PIX_PER_BLOCK = 256;
+
+template <int DT>
+__global__ __launch_bounds__(256) void dw_bwd_weight_partial_kernel(const void *__restrict__ x,
+                                                                    const void *__restrict__ dy,
+                                                                    float *__restrict__ part, DwShape s,
+                                                                    int64_t npix) {
+  __shared__ float red[4][64 * 9];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cg = tid & 7, pl = tid >> 3;  // pl 0..31
+  const int c = blockIdx.y * 64 + cg * 8;
+  const bool cok = c < s.C;
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  const int64_t p0 = (int64_t)blockIdx.x * DWW_PIX_PER_BLOCK;
+  if (cok) {
+    for (int64_t p = p0 + pl; p < p0 + DWW_PIX_PER_BLOCK && p < npix; p += 32) {
+      const int wo = (int)(p % s.Wo);
+      const int64_t t = p / s.Wo;
+      const int ho = (int)(t % s.Ho);
+      const int n = (int)(t / s.Ho);
+      float g[8];
+      Vec8<DT>::load(dy, p * s.C + c, g);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int hi = ho * s.stride - s.pad + kh;
+        if (hi < 0 || hi >= s.H) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int wi = wo * s.stride - s.pad + kw;
+          if (wi < 0 || wi >= s.W) continue;
+          float v[8];
+          Vec8<DT>::load(x, (((int64_t)n * s.H + hi) * s.W + wi) * s.C + c, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], v[j], acc[kh * 3 + kw][j]);
+        }
+      }
+    }
+  }
+  // reduce the 8 pixel lanes of this wave (lane bits 3..5), then the 4 waves via LDS
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[k][j];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[k][j] = v;
+    }
+  if (lane < 8) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv][(cg * 8 + j) * 9 + k] = acc[k][j];
+  }
+  __syncthreads();
+  for (int i = tid; i < 64 * 9; i += 256) {
+    const int cc = blockIdx.y * 64 + i / 9;
+    if (cc < s.C)
+      part[(int64_t)blockIdx.x * s.C * 9 + (int64_t)blockIdx.y * 64 * 9 + i] =
+          red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
+__global__ __launch_bounds__(256) void dw_bwd_weight_reduce_kernel(const float *__restrict__ part,
+                                                                   float *__restrict__ dw, int64_t n,
+                                                                   int slabs, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < slabs; ++k) s += part[(int64_t)k * n + i];
+  dw[i] = accumulate ? dw[i] + s : s;
+}
+
+static int check_shape(const DwShape &s, const char *nm) {
+  EWVIT_CHECK_ARG(s.N > 0 && s.H > 0 && s.W > 0 && s.C > 0, "%s: empty shape", nm);
+  EWVIT_CHECK_ARG(s.C % 8 == 0, "%s: C=%d must be a multiple of 8 (16-B channel vectors)", nm, s.C);
+  EWVIT_CHECK_ARG(s.stride == 1 || s.stride == 2, "%s: stride %d", nm, s.stride);
+  EWVIT_CHECK_ARG(s.pad >= 0 && s.pad <= 2, "%s: pad %d", nm, s.pad);
+  EWVIT_CHECK_ARG(s.Ho == (s.H + 2 * s.pad - 3) / s.stride + 1 && s.Wo == (s.W + 2 * s.pad - 3) / s.stride + 1,
+                  "%s: output size mismatch", nm);
+  return 0;
+}
+
+}  // namespace ewvit
+
+using namespace ewvit;
+
+static DwShape mk(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int pad) {
+  DwShape s;
+  s.N = (int)N; s.H = (int)H; s.W = (int)W; s.C = (int)C; s.stride = stride; s.pad = pad;
+  s.Ho = (int)((H + 2 * pad - 3) / stride + 1);
+  s.Wo = (int)((W + 2 * pad - 3) / stride + 1);
+  return s;
+}
+
+extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,
+                                   int64_t C, int stride, int pad, int dtype, void *stream) {
+  EWVIT_CHECK_ARG(x && w && y && dtype_ok(dtype), "dwconv3x3_fwd: bad args");
+  DwShape s = mk(N, H, W, C, stride, pad);
+  if (int rc = check_shape(s, "dwconv3x3_fwd")) return rc;
+  const int64_t total = (int64_t)s.N * s.Ho * s.Wo * (s.C / 8);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(dw_fwd_kernel<EWVIT_BF16>, grid, dim3(256), 0, as_stream(stream), x, w, y, s);
+  else
+    hipLaunchKernelGGL(dw_fwd_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), x, w, y, s);
+  return launch_status("dwconv3x3_fwd");
+}
+
+extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx, int64_t N, int64_t H,
+                                        int64_t W, int64_t C, int stride, int pad, int dtype, void *stream) {
+  EWVIT_CHECK_ARG(dy && w && dx && dtype_ok(dtype), "dwconv3x3_bwd_data: bad args");
+  DwShape s = mk(N, H, W, C, stride, pad);
+  if (int rc = check_shape(s, "dwconv3x3_bwd_data")) return rc;
+  const int64_t total = (int64_t)s.N * s.H * s.W * (s.C / 8);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(dw_bwd_data_kernel<EWVIT_BF16>, grid, dim3(256), 0, as_stream(stream), dy, w, dx, s);
+  else
+    hipLaunchKernelGGL(dw_bwd_data_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), dy, w, dx, s);
+  return launch_status("dwconv3x3_bwd_data");
+}
+
+extern "C" int64_t ewvit_dwconv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t C, int stride,
+                                                        int pad) {
+  DwShape s = mk(N, H, W, C, stride, pad);
+  const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
+  const int64_t slabs = (npix + DWW_PIX_PER_BLOCK - 1) / DWW_PIX_PER_BLOCK;
+  return slabs * C * 9 * (int64_t)sizeof(float);
+}
+
+extern "C" int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
+                                          int64_t H, int64_t W, int64_t C, int stride, int pad, int dtype,
+                                          float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(x && dy && dw && workspace && dtype_ok(dtype), "dwconv3x3_bwd_weight: bad args");
+  DwShape s = mk(N, H, W, C, stride, pad);
+  if (int rc = check_shape(s, "dwconv3x3_bwd_weight")) return rc;
+  const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
+  const int slabs = (int)((npix + DWW_PIX_PER_BLOCK - 1) / DWW_PIX_PER_BLOCK);
+  EWVIT_CHECK_ARG(slabs <= 65535 * 16, "dwconv3x3_bwd_weight: too many pixels");
+  dim3 grid((unsigned)slabs, (unsigned)((s.C + 63) / 64));
+  hipStream_t st = as_stream(stream);
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_BF16>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
+  else
+    hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_F32>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
+  if (int rc = launch_status("dwconv3x3_bwd_weight")) return rc;
+  const int64_t n = (int64_t)s.C * 9;
+  hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace,
+                     dw, n, slabs, accumulate);
+  return launch_status("dwconv3x3_bwd_weight reduce");
+}

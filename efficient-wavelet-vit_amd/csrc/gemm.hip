@@ -1,0 +1,369 @@
+// bf16 MFMA GEMM with fused epilogues (gfx950).
+//
+// C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)), fp32 accumulation on
+// v_mfma_f32_16x16x32_bf16.  Serves every projection of the hot path: the ViT
+// to_qkv/to_out/FeedForward (network/sfe.py:29-55), the cross-attention
+// to_q/to_kv/to_out (network/dama.py:25-31), patch_to_embedding
+// (sfe.py:127,155; K = 62720 -> split-K) and all their backward products
+// (dX = dY W needs B n-contiguous, dW = dY^T X needs A m-contiguous).
+//
+// Tile 64x64x32, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 MFMA
+// 16x16 tiles; LDS images are [row][k] (k contiguous, padded by 8 bf16) so each
+// lane's A/B fragment (8 consecutive k) is one ds_read_b128.  Global->LDS
+// staging is double-buffered through registers: the next K-tile's loads are in
+// flight while the current one feeds the MFMAs.  Operands may be f32 (converted
+// to bf16 while staging: the fp32 master weights are consumed without a cast
+// kernel) or bf16.
+#include "common.h"
+
+namespace ewvit {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int GBM = 64, GBN = 64, GBK = 32, GPAD = 8, GLD = GBK + GPAD;
+
+struct GemmArgs {
+  const void *A; int64_t lda_m, lda_k;
+  const void *B; int64_t ldb_k, ldb_n;
+  void *C; int64_t ldc;
+  int64_t M, N, K;
+  float alpha, beta;
+  const float *bias;
+  int act;
+  void *aux;
+  float drop_p;
+  uint64_t seed;
+  const void *resid; int resid_dtype; int64_t ldr;
+  int c_dtype;
+  int64_t kper;  // K per split
+  float *ws;     // split-K slabs [splitk][M][N]
+};
+
+// Load 8 consecutive elements (along the contiguous dim) starting at flat
+// index `base`; `n_ok` of them are in range (rest zero).
+template <int DT, bool VEC>
+__device__ __forceinline__ void load8(const void *p, int64_t base, int n_ok, float (&v)[8]) {
+  if (VEC && n_ok == 8) {
+    if (DT == EWVIT_F32) {
+      const float4 *q = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + base);
+      const float4 a = q[0], b = q[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16_t *>(p) + base);
+      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (i < n_ok) ? Elem<DT>::load(p, base + i) : 0.f;
+  }
+}
+
+__device__ __forceinline__ float epilogue(const GemmArgs &g, int64_t row, int64_t col, float acc) {
+  float v = g.alpha * acc;
+  if (g.bias) v += g.bias[col];
+  if (g.act == 1) {
+    if (g.aux) reinterpret_cast<bf16_t *>(g.aux)[row * g.ldc + col] = f2bf(v);
+    v = gelu_erf(v);
+  } else if (g.act == 2) {
+    if (g.aux) reinterpret_cast<bf16_t *>(g.aux)[row * g.ldc + col] = f2bf(v);
+    v = v > 0.f ? v : 0.f;
+  } else if (g.act == 3) {
+    v *= gelu_erf_grad(bf2f(reinterpret_cast<const bf16_t *>(g.aux)[row * g.ldc + col]));
+  }
+  if (g.drop_p > 0.f) {
+    const float u = uniform01(g.seed, (uint64_t)(row * g.N + col));
+    v = (u >= g.drop_p) ? v * (1.0f / (1.0f - g.drop_p)) : 0.f;
+  }
+  if (g.resid) v += load_dt(g.resid, row * g.ldr + col, g.resid_dtype);
+  if (g.beta != 0.f) v += g.beta * reinterpret_cast<const float *>(g.C)[row * g.ldc + col];
+  return v;
+}
+
+__device__ __forceinline__ void store_c(const GemmArgs &g, int64_t row, int64_t col, float v) {
+  if (g.c_dtype == EWVIT_F32)
+    reinterpret_cast<float *>(g.C)[row * g.ldc + col] = v;
+  else
+    reinterpret_cast<bf16_t *>(g.C)[row * g.ldc + col] = f2bf(v);
+}
+
+// Stage one 64x32 operand tile into registers.  ROWS = the M (or N) index,
+// K the reduction index.  KCONTIG: element (r,k) at base + r*ld_r + k.
+// otherwise at base + r + k*ld_k (r contiguous).
+template <int DT, bool KCONTIG, bool VEC>
+struct Stager {
+  float v[8];
+  int r, k;  // first element coordinates inside the tile
+  __device__ __forceinline__ void load(const void *p, int64_t ld_r, int64_t ld_k, int64_t r0,
+                                       int64_t R, int64_t k0, int64_t kend, int tid) {
+    if (KCONTIG) {
+      r = tid >> 2; k = (tid & 3) * 8;
+      const int64_t gr = r0 + r, gk = k0 + k;
+      int n_ok = 0;
+      if (gr < R) n_ok = (int)(kend - gk > 8 ? 8 : (kend - gk > 0 ? kend - gk : 0));
+      load8<DT, VEC>(p, gr * ld_r + gk, n_ok, v);
+    } else {
+      k = tid >> 3; r = (tid & 7) * 8;
+      const int64_t gr = r0 + r, gk = k0 + k;
+      int n_ok = 0;
+      if (gk < kend) n_ok = (int)(R - gr > 8 ? 8 : (R - gr > 0 ? R - gr : 0));
+      load8<DT, VEC>(p, gr + gk * ld_k, n_ok, v);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t (*lds)[GLD]) {
+    if (KCONTIG) {
+      __attribute__((aligned(16))) bf16_t t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = f2bf(v[i]);
+      *reinterpret_cast<uint4 *>(&lds[r][k]) = *reinterpret_cast<const uint4 *>(t);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[r + i][k] = f2bf(v[i]);
+    }
+  }
+};
+
+template <int ADT, int BDT, bool AK, bool BK, bool AV, bool BV>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][GBM][GLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][GBN][GLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  const int64_t kbeg = (int64_t)blockIdx.z * g.kper;
+  const int64_t kend = (kbeg + g.kper < g.K) ? kbeg + g.kper : g.K;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<ADT, AK, AV> sa;
+  Stager<BDT, BK, BV> sb;
+  const int nk = (int)((kend - kbeg + GBK - 1) / GBK);
+  if (nk > 0) {
+    sa.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, kbeg, kend, tid);
+    sb.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, kbeg, kend, tid);
+    sa.store(As[0]);
+    sb.store(Bs[0]);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int64_t k0 = kbeg + (int64_t)(kt + 1) * GBK;
+      sa.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, k0, kend, tid);
+      sb.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, k0, kend, tid);
+    }
+    bf16x8 af[2], bfr[2];
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      af[i] = *reinterpret_cast<const bf16x8 *>(&As[cur][wm * 32 + i * 16 + fr][fk]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8 *>(&Bs[cur][wn * 32 + j * 16 + fr][fk]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      sa.store(As[cur ^ 1]);
+      sb.store(Bs[cur ^ 1]);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (row < g.M && col < g.N) {
+          if (split)
+            g.ws[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[i][j][r];
+          else
+            store_c(g, row, col, epilogue(g, row, col, acc[i][j][r]));
+        }
+      }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int splitk) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= g.M * g.N) return;
+  const int64_t row = idx / g.N, col = idx % g.N;
+  float s = 0.f;
+  for (int z = 0; z < splitk; ++z) s += g.ws[(int64_t)z * g.M * g.N + idx];
+  store_c(g, row, col, epilogue(g, row, col, s));
+}
+
+__global__ __launch_bounds__(256) void colsum_kernel(const void *X, int dt, int64_t ldx, int64_t M,
+                                                     int64_t N, float *out, int accumulate) {
+  // one thread per column, 4 row-groups per block reduced through LDS
+  __shared__ float part[4][64];
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  float s = 0.f;
+  if (col < N)
+    for (int64_t m = grp; m < M; m += 4) s += load_dt(X, m * ldx + col, dt);
+  part[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp == 0 && col < N) {
+    const float t = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    out[col] = accumulate ? out[col] + t : t;
+  }
+}
+
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(void *g, int dt, int64_t rows, int64_t cols,
+                                                          int64_t ldg, float p, uint64_t seed) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const int64_t r = idx / cols, c = idx % cols;
+  const float u = uniform01(seed, (uint64_t)idx);
+  const int64_t o = r * ldg + c;
+  const float v = load_dt(g, o, dt);
+  store_dt(g, o, u >= p ? v * (1.0f / (1.0f - p)) : 0.f, dt);
+}
+
+// g_pre = dy * keep(seed)/(1-p) * act'(aux): the backward of the GEMM epilogue
+__global__ __launch_bounds__(256) void act_bwd_kernel(const void *dy, int dydt, int64_t lddy,
+                                                      const bf16_t *aux, int act, float p, uint64_t seed,
+                                                      void *out, int odt, int64_t M, int64_t N) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int64_t r = idx / N, c = idx % N;
+  float v = load_dt(dy, r * lddy + c, dydt);
+  if (p > 0.f) v = uniform01(seed, (uint64_t)idx) >= p ? v * (1.0f / (1.0f - p)) : 0.f;
+  if (act == 1) v *= gelu_erf_grad(bf2f(aux[idx]));
+  else if (act == 2) v = bf2f(aux[idx]) > 0.f ? v : 0.f;
+  store_dt(out, idx, v, odt);
+}
+
+template <int ADT, int BDT, bool AK, bool BK>
+static void launch_typed(const GemmArgs &g, bool av, bool bv, dim3 grid, hipStream_t s) {
+  dim3 block(256);
+  if (av && bv) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
+  else if (av) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, true, false>), grid, block, 0, s, g);
+  else if (bv) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, false, true>), grid, block, 0, s, g);
+  else hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, false, false>), grid, block, 0, s, g);
+}
+
+template <int ADT, int BDT>
+static void launch_layout(const GemmArgs &g, bool ak, bool bk, bool av, bool bv, dim3 grid, hipStream_t s) {
+  if (ak && bk) launch_typed<ADT, BDT, true, true>(g, av, bv, grid, s);
+  else if (ak) launch_typed<ADT, BDT, true, false>(g, av, bv, grid, s);
+  else if (bk) launch_typed<ADT, BDT, false, true>(g, av, bv, grid, s);
+  else launch_typed<ADT, BDT, false, false>(g, av, bv, grid, s);
+}
+
+// 8 consecutive elements along the contiguous dim can be one 16/32-B load iff
+// the base and every row start are aligned.
+static bool vec_ok(const void *p, int dt, int64_t ld_other) {
+  const int64_t esz = dt == EWVIT_F32 ? 4 : 2;
+  const int64_t align = dt == EWVIT_F32 ? 16 : 16;
+  return ((uintptr_t)p % align == 0) && ((ld_other * esz) % align == 0);
+}
+
+}  // namespace ewvit
+
+using namespace ewvit;
+
+extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+                          int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
+                          int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
+                          const float *bias, int act, void *aux, float drop_p, uint64_t seed,
+                          const void *resid, int resid_dtype, int64_t ldr, int splitk,
+                          float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(A && B && C, "gemm: null operand");
+  EWVIT_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
+  EWVIT_CHECK_ARG(dtype_ok(a_dtype) && dtype_ok(b_dtype) && dtype_ok(c_dtype), "gemm: bad dtype");
+  EWVIT_CHECK_ARG(lda_m == 1 || lda_k == 1, "gemm: A needs a unit stride (lda_m=%lld lda_k=%lld)",
+                  (long long)lda_m, (long long)lda_k);
+  EWVIT_CHECK_ARG(ldb_k == 1 || ldb_n == 1, "gemm: B needs a unit stride");
+  EWVIT_CHECK_ARG(act >= 0 && act <= 3, "gemm: act=%d", act);
+  EWVIT_CHECK_ARG(act != 3 || aux, "gemm: act 3 needs aux (pre-activation)");
+  EWVIT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "gemm: drop_p=%f", (double)drop_p);
+  EWVIT_CHECK_ARG(beta == 0.f || c_dtype == EWVIT_F32, "gemm: beta needs f32 C");
+  EWVIT_CHECK_ARG(!resid || dtype_ok(resid_dtype), "gemm: bad resid dtype");
+  EWVIT_CHECK_ARG(splitk >= 1 && splitk <= 256, "gemm: splitk=%d", splitk);
+  EWVIT_CHECK_ARG(splitk == 1 || workspace, "gemm: split-K needs a workspace");
+  if (M == 0 || N == 0) return 0;
+  GemmArgs g;
+  g.A = A; g.lda_m = lda_m; g.lda_k = lda_k;
+  g.B = B; g.ldb_k = ldb_k; g.ldb_n = ldb_n;
+  g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
+  g.alpha = alpha; g.beta = beta; g.bias = bias; g.act = act; g.aux = aux;
+  g.drop_p = drop_p; g.seed = seed; g.resid = resid; g.resid_dtype = resid_dtype; g.ldr = ldr;
+  g.c_dtype = c_dtype; g.ws = workspace;
+  // K per split, a multiple of the K tile
+  int64_t kper = (K + splitk - 1) / splitk;
+  kper = ((kper + GBK - 1) / GBK) * GBK;
+  if (kper == 0) kper = GBK;
+  int sk = (int)((K + kper - 1) / kper);
+  if (sk < 1) sk = 1;
+  g.kper = kper;
+  const bool ak = (lda_k == 1), bk = (ldb_k == 1);
+  const bool av = vec_ok(A, a_dtype, ak ? lda_m : lda_k);
+  const bool bv = vec_ok(B, b_dtype, bk ? ldb_n : ldb_k);
+  dim3 grid((unsigned)((N + GBN - 1) / GBN), (unsigned)((M + GBM - 1) / GBM), (unsigned)sk);
+  EWVIT_CHECK_ARG(grid.y <= 65535, "gemm: M too large");
+  hipStream_t s = as_stream(stream);
+  if (a_dtype == EWVIT_BF16 && b_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_BF16>(g, ak, bk, av, bv, grid, s);
+  else if (a_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_F32>(g, ak, bk, av, bv, grid, s);
+  else if (b_dtype == EWVIT_BF16) launch_layout<EWVIT_F32, EWVIT_BF16>(g, ak, bk, av, bv, grid, s);
+  else launch_layout<EWVIT_F32, EWVIT_F32>(g, ak, bk, av, bv, grid, s);
+  int rc = launch_status("gemm");
+  if (rc || sk == 1) return rc;
+  const int64_t total = M * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g, sk);
+  return launch_status("gemm splitk reduce");
+}
+
+extern "C" int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N,
+                            float *out, int accumulate, void *stream) {
+  EWVIT_CHECK_ARG(X && out, "colsum: null pointer");
+  EWVIT_CHECK_ARG(dtype_ok(x_dtype) && M >= 0 && N >= 0, "colsum: bad args");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, as_stream(stream),
+                     X, x_dtype, ldx, M, N, out, accumulate);
+  return launch_status("colsum");
+}
+
+extern "C" int ewvit_dropout_bwd(void *g, int g_dtype, int64_t rows, int64_t cols, int64_t ldg,
+                                 float p, uint64_t seed, void *stream) {
+  EWVIT_CHECK_ARG(g && dtype_ok(g_dtype) && p >= 0.f && p < 1.f, "dropout_bwd: bad args");
+  const int64_t total = rows * cols;
+  if (total == 0 || p == 0.f) return 0;
+  hipLaunchKernelGGL(dropout_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), g, g_dtype, rows, cols, ldg, p, seed);
+  return launch_status("dropout_bwd");
+}
+
+extern "C" int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const void *aux, int act,
+                             float drop_p, uint64_t seed, void *out, int out_dtype, int64_t M,
+                             int64_t N, void *stream) {
+  EWVIT_CHECK_ARG(dy && out && dtype_ok(dy_dtype) && dtype_ok(out_dtype), "act_bwd: bad args");
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || aux), "act_bwd: act=%d needs aux", act);
+  EWVIT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "act_bwd: drop_p");
+  const int64_t total = M * N;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), dy, dy_dtype, lddy, (const bf16_t *)aux, act, drop_p, seed,
+                     out, out_dtype, M, N);
+  return launch_status("act_bwd");
+}

@@ -1,0 +1,139 @@
+// LayerNorm forward/backward (gfx950): one 64-lane wave per row.
+// Replaces nn.LayerNorm of network/sfe.py:23 (PreNorm, D=512) and
+// network/dama.py:62,64 (cross-attention pre-norms, D=128).  Statistics in f32
+// (two-pass mean / centred variance in registers), biased variance, eps inside
+// the rsqrt — torch's formula.
+#include "common.h"
+
+namespace ewvit {
+
+constexpr int LN_MAXV = 16;  // up to D = 1024 per wave
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void *x, int xdt, int64_t ldx,
+                                                     const float *gamma, const float *beta, void *y,
+                                                     int ydt, float *mean, float *rstd, int64_t M,
+                                                     int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = (c < D) ? load_dt(x, row * ldx + c, xdt) : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    const float d = (c < D) ? v[i] - mu : 0.f;
+    q += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) store_dt(y, row * D + c, (v[i] - mu) * rs * gamma[c] + beta[c], ydt);
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma += dy*xhat; dbeta += dy
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const void *dy, int dydt, const void *x, int xdt,
+                                                     int64_t ldx, const float *gamma, const float *mean,
+                                                     const float *rstd, float *dx, int acc_dx,
+                                                     float *dgamma, float *dbeta, int64_t M, int D,
+                                                     int rows_per_block) {
+  __shared__ float sg[4][1024];
+  __shared__ float sb[4][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pg[LN_MAXV], pb[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t row = r0 + w; row < r0 + rows_per_block && row < M; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[LN_MAXV], g[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float d = load_dt(dy, row * D + c, dydt);
+        xh[i] = (load_dt(x, row * ldx + c, xdt) - mu) * rs;
+        g[i] = d * gamma[c];
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+        pg[i] += d * xh[i];
+        pb[i] += d;
+      } else {
+        xh[i] = 0.f; g[i] = 0.f;
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float v = rs * (g[i] - m1 - xh[i] * m2);
+        const int64_t o = row * D + c;
+        dx[o] = acc_dx ? dx[o] + v : v;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) { sg[w][c] = pg[i]; sb[w][c] = pb[i]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const float a = sg[0][c] + sg[1][c] + sg[2][c] + sg[3][c];
+    const float b = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
+    if (dgamma) atomicAdd(&dgamma[c], a);
+    if (dbeta) atomicAdd(&dbeta[c], b);
+  }
+}
+
+}  // namespace ewvit
+
+using namespace ewvit;
+
+extern "C" int ewvit_layernorm_fwd(const void *x, int x_dtype, int64_t ldx, const float *gamma,
+                                   const float *beta, void *y, int y_dtype, float *mean, float *rstd,
+                                   int64_t M, int64_t D, float eps, void *stream) {
+  EWVIT_CHECK_ARG(x && gamma && beta && y, "layernorm_fwd: null pointer");
+  EWVIT_CHECK_ARG(dtype_ok(x_dtype) && dtype_ok(y_dtype), "layernorm_fwd: bad dtype");
+  EWVIT_CHECK_ARG(D > 0 && D <= 64 * LN_MAXV, "layernorm_fwd: D=%lld not in (0,1024]", (long long)D);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, as_stream(stream), x,
+                     x_dtype, ldx, gamma, beta, y, y_dtype, mean, rstd, M, (int)D, eps);
+  return launch_status("layernorm_fwd");
+}
+
+extern "C" int ewvit_layernorm_bwd(const void *dy, int dy_dtype, const void *x, int x_dtype,
+                                   int64_t ldx, const float *gamma, const float *mean,
+                                   const float *rstd, float *dx, int accumulate_dx, float *dgamma,
+                                   float *dbeta, int64_t M, int64_t D, void *stream) {
+  EWVIT_CHECK_ARG(dy && x && gamma && mean && rstd && dx, "layernorm_bwd: null pointer");
+  EWVIT_CHECK_ARG(dtype_ok(dy_dtype) && dtype_ok(x_dtype), "layernorm_bwd: bad dtype");
+  EWVIT_CHECK_ARG(D > 0 && D <= 64 * LN_MAXV, "layernorm_bwd: D=%lld not in (0,1024]", (long long)D);
+  if (M == 0) return 0;
+  const int rpb = 16;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0,
+                     as_stream(stream), dy, dy_dtype, x, x_dtype, ldx, gamma, mean, rstd, dx,
+                     accumulate_dx, dgamma, dbeta, M, (int)D, rpb);
+  return launch_status("layernorm_bwd");
+}

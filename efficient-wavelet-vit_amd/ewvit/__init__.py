@@ -1,0 +1,14 @@
+"""ewvit — MI355X (gfx950) kernels of the Efficient-Wavelet-ViT hot path.
+
+C-ABI: include/ewvit.h, built into ewvit/libewvit.so from csrc/*.hip.
+"""
+from . import _lib
+from .ops import (attention_cross, attention_packed, colsum, dwconv3x3, dwt_haar, dwt_hf_upsample, gemm,
+                  hf_upsample, layer_norm, linear, mm_nn, mm_nt, mm_tn)
+
+__all__ = ['attention_cross', 'attention_packed', 'colsum', 'dwconv3x3', 'dwt_haar', 'dwt_hf_upsample', 'gemm',
+           'hf_upsample', 'layer_norm', 'linear', 'mm_nn', 'mm_nt', 'mm_tn', 'load_library']
+
+
+def load_library():
+    return _lib.load()

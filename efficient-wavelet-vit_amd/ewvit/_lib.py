@@ -1,0 +1,124 @@
+"""ctypes binding of libewvit.so (the C-ABI declared in include/ewvit.h).
+
+The library is built in-tree (``make -C csrc`` or ``__graft_entry__.build()``)
+and loaded from this directory.  There is no fallback: if the library or a GPU
+is missing, every op raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libewvit.so')
+ABI_VERSION = 1
+F32, BF16 = 0, 1
+
+_i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
+
+# name -> argtypes (restype int for all but the two bookkeeping calls)
+SIGNATURES = {
+    'ewvit_dwt_haar_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
+    'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _vp],
+    'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
+                   _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _i32, _i64, _i32, _vp, _vp],
+    'ewvit_colsum': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
+    'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp],
+    'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _i32, _i64, _i64, _vp],
+    'ewvit_layernorm_fwd': [_vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _f32, _vp],
+    'ewvit_layernorm_bwd': [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64,
+                            _i64, _vp],
+    'ewvit_attn_fwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64,
+                       _i64, _i32, _i32, _i32, _f32, _vp],
+    'ewvit_dwconv3x3_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
+    'ewvit_dwconv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
+    'ewvit_dwconv3x3_bwd_weight': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp],
+    'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
+                       _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
+}
+
+# size queries: name -> (restype, argtypes)
+QUERIES = {
+    'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
+}
+
+_lib = None
+
+
+def load():
+    """Load and type the library; raises RuntimeError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f'ewvit: {LIB_PATH} not built — run `make -C csrc` '
+                           '(or __graft_entry__.build()); there is no CPU fallback')
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.ewvit_abi_version.restype = ctypes.c_int
+    lib.ewvit_abi_version.argtypes = []
+    lib.ewvit_last_error.restype = ctypes.c_char_p
+    lib.ewvit_last_error.argtypes = []
+    if lib.ewvit_abi_version() != ABI_VERSION:
+        raise RuntimeError(f'ewvit: ABI {lib.ewvit_abi_version()} != expected {ABI_VERSION}')
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    for name, (res, args) in QUERIES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+# Optional per-launch timing (bench.py): HIP events recorded on the current stream
+# — the stream every ewvit kernel is launched on — around each launch, with the
+# launch's algorithmic work (bytes, flops) attached.
+_timers = None
+
+
+def enable_timing(on=True):
+    global _timers
+    _timers = {} if on else None
+
+
+def timing_records():
+    return _timers or {}
+
+
+def call(name, *args, work=None):
+    rec = _timers is not None
+    if rec:
+        s = torch.cuda.Event(enable_timing=True)
+        s.record()
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f'{name} failed (rc={rc}): {_lib.ewvit_last_error().decode()}')
+    if rec:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        _timers.setdefault(name, []).append((s, e, work or {}))
+
+
+def dt(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f'ewvit: unsupported dtype {t.dtype} (f32/bf16 only)')
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('ewvit ops run on the MI355X only (tensor on %s); the product has no '
+                               'CPU path — use the oracle for CPU reference numbers' % t.device)

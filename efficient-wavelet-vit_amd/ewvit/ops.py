@@ -1,0 +1,336 @@
+"""Torch-facing ops over the C-ABI (include/ewvit.h) and their autograd Functions.
+
+torch is plumbing here: it owns device memory (caching allocator), the current
+HIP stream and autograd.  Every FLOP of these ops runs in libewvit.so; inputs
+on a non-ROCm device raise (no CPU path).
+"""
+import math
+
+import torch
+
+from . import _lib as L
+
+F32, BF16 = L.F32, L.BF16
+
+
+def _seed():
+    # CPU generator: no device sync, reproducible under torch.manual_seed
+    return int(torch.randint(1, 2 ** 62, (), dtype=torch.int64))
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ------------------------------------------------------------------- GEMM
+def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, aux=None,
+         drop_p=0.0, seed=0, resid=None, ldr=0, splitk=None):
+    """Raw C[M,N] = epi(alpha * A(M,K) @ B(K,N)).  lda = (lda_m, lda_k), ldb = (ldb_k, ldb_n).
+    C must be contiguous with row stride N (ldc = C.stride(0))."""
+    L.require_gpu(A, B, C)
+    if splitk is None:
+        tiles = ((M + 63) // 64) * ((N + 63) // 64)
+        splitk = 1
+        if tiles < 128 and K >= 2048:
+            splitk = int(max(1, min(64, 256 // max(tiles, 1), K // 1024)))
+    ws = torch.empty(splitk * M * N, dtype=torch.float32, device=C.device) if splitk > 1 else None
+    work = {'flops': 2.0 * M * N * K,
+            'bytes': M * K * A.element_size() + K * N * B.element_size() + M * N * C.element_size()}
+    L.call('ewvit_gemm', L.ptr(A), L.dt(A), lda[0], lda[1], L.ptr(B), L.dt(B), ldb[0], ldb[1],
+           L.ptr(C), L.dt(C), C.stride(0), M, N, K, float(alpha), float(beta), L.ptr(bias), act,
+           L.ptr(aux), float(drop_p), seed, L.ptr(resid), L.dt(resid) if resid is not None else 0,
+           ldr, splitk, L.ptr(ws), L.stream(C), work=work)
+    return C
+
+
+def mm_nt(X, W, out, **kw):
+    """out[M,N] = X[M,K] @ W[N,K]^T  (nn.Linear forward)."""
+    M, K = X.shape
+    N = W.shape[0]
+    assert X.stride(1) == 1 and W.stride(1) == 1
+    return gemm(X, (X.stride(0), 1), W, (1, W.stride(0)), out, M, N, K, **kw)
+
+
+def mm_nn(G, W, out, **kw):
+    """out[M,K] = G[M,N] @ W[N,K]  (input gradient of nn.Linear)."""
+    M, N = G.shape
+    K = W.shape[1]
+    assert G.stride(1) == 1 and W.stride(1) == 1
+    return gemm(G, (G.stride(0), 1), W, (W.stride(0), 1), out, M, K, N, **kw)
+
+
+def mm_tn(G, X, out, **kw):
+    """out[N,K] = G[M,N]^T @ X[M,K]  (weight gradient of nn.Linear)."""
+    M, N = G.shape
+    K = X.shape[1]
+    assert G.stride(1) == 1 and X.stride(1) == 1
+    return gemm(G, (1, G.stride(0)), X, (X.stride(0), 1), out, N, K, M, **kw)
+
+
+def colsum(X, out, accumulate=False):
+    M, N = X.shape
+    L.call('ewvit_colsum', L.ptr(X), L.dt(X), X.stride(0), M, N, L.ptr(out), int(accumulate), L.stream(X))
+    return out
+
+
+class LinearFn(torch.autograd.Function):
+    """y = dropout(act(x @ W^T + b)) + resid — nn.Linear (+ReLU/GELU/Dropout/residual)
+    of network/sfe.py:29-55,127,134-142 and network/dama.py:25-31,105-113."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act, drop_p, resid, out_dtype):
+        L.require_gpu(x, weight)
+        K = x.shape[-1]
+        lead = x.shape[:-1]
+        x2 = _c(x.reshape(-1, K))
+        M, N = x2.shape[0], weight.shape[0]
+        y = torch.empty(M, N, dtype=out_dtype, device=x.device)
+        need_aux = act in (1, 2) and any(ctx.needs_input_grad[:3])
+        aux = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if need_aux else None
+        seed = _seed() if drop_p > 0 else 0
+        r2 = _c(resid.reshape(M, N)) if resid is not None else None
+        mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, resid=r2,
+              ldr=N if r2 is not None else 0)
+        ctx.save_for_backward(x2, weight, aux)
+        ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None)
+        return y.reshape(*lead, N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, aux = ctx.saved_tensors
+        act, drop_p, seed, lead, xdt, has_res, has_bias = ctx.cfg
+        M, K = x2.shape
+        N = weight.shape[0]
+        dy2 = _c(dy.reshape(M, N))
+        if act == 0 and drop_p == 0:
+            g = dy2
+        else:
+            g = torch.empty(M, N, dtype=torch.float32, device=dy.device)
+            L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux), act, float(drop_p), seed,
+                   L.ptr(g), F32, M, N, L.stream(g))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device)).reshape(*lead, K)
+        if ctx.needs_input_grad[1]:
+            dw = mm_tn(g, x2, torch.empty(N, K, dtype=torch.float32, device=dy.device))
+        if has_bias and ctx.needs_input_grad[2]:
+            db = colsum(g, torch.empty(N, dtype=torch.float32, device=dy.device))
+        dres = dy if has_res and ctx.needs_input_grad[5] else None
+        return dx, dw, db, None, None, dres, None
+
+
+def linear(x, weight, bias=None, act=0, drop_p=0.0, resid=None, out_dtype=torch.float32):
+    return LinearFn.apply(x, weight, bias, act, float(drop_p), resid, out_dtype)
+
+
+# -------------------------------------------------------------- LayerNorm
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm over the last dim (network/sfe.py:23, network/dama.py:62,64)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, out_dtype):
+        L.require_gpu(x, gamma)
+        D = x.shape[-1]
+        x2 = _c(x.reshape(-1, D))
+        M = x2.shape[0]
+        y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        L.call('ewvit_layernorm_fwd', L.ptr(x2), L.dt(x2), D, L.ptr(gamma), L.ptr(beta), L.ptr(y),
+               L.dt(y), L.ptr(mean), L.ptr(rstd), M, D, float(eps), L.stream(y))
+        ctx.save_for_backward(x2, gamma, mean, rstd)
+        ctx.shape = x.shape
+        ctx.xdt = x.dtype
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gamma, mean, rstd = ctx.saved_tensors
+        M, D = x2.shape
+        dy2 = _c(dy.reshape(M, D))
+        dx = torch.empty(M, D, dtype=torch.float32, device=dy.device)
+        dg = torch.zeros(D, dtype=torch.float32, device=dy.device)
+        db = torch.zeros(D, dtype=torch.float32, device=dy.device)
+        L.call('ewvit_layernorm_bwd', L.ptr(dy2), L.dt(dy2), L.ptr(x2), L.dt(x2), D, L.ptr(gamma),
+               L.ptr(mean), L.ptr(rstd), L.ptr(dx), 0, L.ptr(dg), L.ptr(db), M, D, L.stream(dx))
+        dx = dx.reshape(ctx.shape)
+        if ctx.xdt != torch.float32:
+            dx = dx.to(ctx.xdt)
+        return dx, dg, db, None, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5, out_dtype=torch.bfloat16):
+    return LayerNormFn.apply(x, weight, bias, float(eps), out_dtype)
+
+
+# -------------------------------------------------------------- attention
+class AttnFn(torch.autograd.Function):
+    """Multi-head softmax attention for the hot path's short sequences.
+
+    packed (ViT, sfe.py:59-70): src = qkv [B, n, 3*H*d]  ->  o [B, n, H*d]
+    cross (dama.py:41-53):      src = (q [B, nq, H*d], kv [B, nk, 2*H*d])
+    """
+
+    @staticmethod
+    def forward(ctx, q_src, kv_src, heads, dim_head, scale):
+        packed = kv_src is None
+        qs = _c(q_src)
+        kvs = qs if packed else _c(kv_src)
+        L.require_gpu(qs, kvs)
+        if qs.dtype != torch.bfloat16 or kvs.dtype != torch.bfloat16:
+            raise TypeError('attn: q/k/v must be bf16 (projection outputs)')
+        B, nq = qs.shape[0], qs.shape[1]
+        nk = kvs.shape[1]
+        inner = heads * dim_head
+        o = torch.empty(B, nq, inner, dtype=torch.bfloat16, device=qs.device)
+        p = torch.empty(B, heads, nq, nk, dtype=torch.float32, device=qs.device)
+        esz = 2
+        q_off, k_off, v_off = (0, inner, 2 * inner) if packed else (0, 0, inner)
+        kp = kvs.data_ptr() + k_off * esz
+        vp = kvs.data_ptr() + v_off * esz
+        L.call('ewvit_attn_fwd', qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1), kp, kvs.stride(0),
+               kvs.stride(1), vp, kvs.stride(0), kvs.stride(1), L.ptr(o), o.stride(0), o.stride(1),
+               L.ptr(p), B, heads, nq, nk, dim_head, float(scale), L.stream(o))
+        ctx.save_for_backward(qs, kvs if not packed else qs, p)
+        ctx.cfg = (packed, heads, dim_head, scale, q_off, k_off, v_off)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qs, kvs, p = ctx.saved_tensors
+        packed, heads, d, scale, q_off, k_off, v_off = ctx.cfg
+        do = _c(do)
+        if do.dtype != torch.bfloat16:
+            do = do.to(torch.bfloat16)
+        B, nq, nk = qs.shape[0], qs.shape[1], kvs.shape[1]
+        dqs = torch.empty_like(qs)
+        dkvs = dqs if packed else torch.empty_like(kvs)
+        esz = 2
+        L.call('ewvit_attn_bwd', L.ptr(do), do.stride(0), do.stride(1),
+               qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1),
+               kvs.data_ptr() + k_off * esz, kvs.stride(0), kvs.stride(1),
+               kvs.data_ptr() + v_off * esz, kvs.stride(0), kvs.stride(1), L.ptr(p),
+               dqs.data_ptr() + q_off * esz, dkvs.data_ptr() + k_off * esz, dkvs.data_ptr() + v_off * esz,
+               B, heads, nq, nk, d, float(scale), L.stream(dqs))
+        return dqs, (None if packed else dkvs), None, None, None
+
+
+def attention_packed(qkv, heads, dim_head, scale):
+    return AttnFn.apply(qkv, None, heads, dim_head, scale)
+
+
+def attention_cross(q, kv, heads, dim_head, scale):
+    return AttnFn.apply(q, kv, heads, dim_head, scale)
+
+
+# -------------------------------------------------------------------- DWT
+def _level_sizes(H, W, levels):
+    out = []
+    h, w = H, W
+    for _ in range(levels):
+        h, w = (h + 1) // 2, (w + 1) // 2
+        out.append((h, w))
+    return out
+
+
+def _dwt_flat(x, levels, out_dtype):
+    L.require_gpu(x)
+    if x.requires_grad:
+        raise NotImplementedError('ewvit.dwt_haar: no backward (frames never require grad on the '
+                                  'training path, SURVEY §8a note 7)')
+    x = _c(x)
+    N, C, H, W = x.shape
+    sizes = _level_sizes(H, W, levels)
+    total = sum(N * C * 3 * h * w for h, w in sizes)
+    yh = torch.empty(total, dtype=out_dtype, device=x.device)
+    hL, wL = sizes[-1]
+    ll = torch.empty(N, C, hL, wL, dtype=out_dtype, device=x.device)
+    work = {'bytes': x.numel() * x.element_size() + (yh.numel() + ll.numel()) * ll.element_size()}
+    L.call('ewvit_dwt_haar_fwd', L.ptr(x), L.ptr(yh), L.ptr(ll), N, C, H, W, levels, L.dt(x),
+           L.dt(ll), L.stream(ll), work=work)
+    return ll, yh, sizes
+
+
+def dwt_haar(x, levels=1, out_dtype=torch.float32):
+    """Multi-level Haar DWT (pytorch_wavelets DWTForward J=1 'haar' 'zero' applied
+    `levels` times, network/mwt.py:20,76,107-111).  x [N,C,H,W] f32/bf16.
+    Returns (ll [N,C,h_L,w_L], [yh_1 .. yh_L]) with yh_l [N,C,3,h_l,w_l]."""
+    ll, yh, sizes = _dwt_flat(x, levels, out_dtype)
+    N, C = x.shape[:2]
+    outs, off = [], 0
+    for h, w in sizes:
+        n = N * C * 3 * h * w
+        outs.append(yh[off:off + n].view(N, C, 3, h, w))
+        off += n
+    return ll, outs
+
+
+def hf_upsample(yh_flat_levels, N, C, H, W, levels, out_hw, out_dtype=torch.bfloat16):
+    """Bilinear upsample of every level's bands (mwt.py:77-81) -> [L, N, OH, OW, 3C]."""
+    base = yh_flat_levels
+    OH, OW = out_hw
+    out = torch.empty(levels, N, OH, OW, 3 * C, dtype=out_dtype, device=base.device)
+    nb = sum(N * 3 * C * h * w for h, w in _level_sizes(H, W, levels))
+    work = {'bytes': nb * base.element_size() + out.numel() * out.element_size()}
+    L.call('ewvit_hf_upsample', L.ptr(base), L.ptr(out), N, C, H, W, levels, OH, OW, L.dt(base),
+           L.dt(out), L.stream(out), work=work)
+    return out
+
+
+def dwt_hf_upsample(x, levels, out_hw, out_dtype=torch.bfloat16, band_dtype=torch.bfloat16):
+    """The MWT high-frequency front end for all levels at once: DWT (one read of x)
+    then the upsampled, channel-interleaved HF input of hf_conv for every level,
+    channels-last: [L, N, OH, OW, 3C] (channel c*3+band)."""
+    ll, yh, _ = _dwt_flat(x, levels, band_dtype)
+    N, C, H, W = x.shape
+    return hf_upsample(yh, N, C, H, W, levels, out_hw, out_dtype), ll
+
+
+# ------------------------------------------------------- depthwise 3x3 conv
+class DepthwiseConv3x3Fn(torch.autograd.Function):
+    """groups=C 3x3 conv, no bias, channels-last (EfficientNetV2-S MBConv depthwise)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad):
+        L.require_gpu(x, weight)
+        N, C, H, W = x.shape
+        xc = x.contiguous(memory_format=torch.channels_last)
+        w = weight.detach().float().contiguous()
+        Ho, Wo = (H + 2 * pad - 3) // stride + 1, (W + 2 * pad - 3) // stride + 1
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        work = {'bytes': (xc.numel() + y.numel()) * x.element_size(), 'flops': 18.0 * y.numel()}
+        L.call('ewvit_dwconv3x3_fwd', L.ptr(xc), L.ptr(w), L.ptr(y), N, H, W, C, stride, pad, L.dt(xc),
+               L.stream(y), work=work)
+        ctx.save_for_backward(xc, w)
+        ctx.cfg = (stride, pad, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w = ctx.saved_tensors
+        stride, pad, wdt = ctx.cfg
+        N, C, H, W = xc.shape
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        if dyc.dtype != xc.dtype:
+            dyc = dyc.to(xc.dtype)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(xc, memory_format=torch.channels_last)
+            L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, stride, pad,
+                   L.dt(xc), L.stream(dx), work={'bytes': (dyc.numel() + dx.numel()) * dx.element_size()})
+        if ctx.needs_input_grad[1]:
+            wsb = L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, stride, pad)
+            ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
+            dw = torch.empty(C, 1, 3, 3, dtype=torch.float32, device=xc.device)
+            L.call('ewvit_dwconv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dw), 0, N, H, W, C, stride, pad,
+                   L.dt(xc), L.ptr(ws), L.stream(dw),
+                   work={'bytes': (dyc.numel() + xc.numel()) * xc.element_size()})
+            if wdt != torch.float32:
+                dw = dw.to(wdt)
+        return dx, dw, None, None
+
+
+def dwconv3x3(x, weight, stride=1, pad=1):
+    if torch.is_autocast_enabled('cuda') and x.dtype == torch.float32:
+        x = x.to(torch.get_autocast_dtype('cuda'))
+    return DepthwiseConv3x3Fn.apply(x, weight, int(stride), int(pad))

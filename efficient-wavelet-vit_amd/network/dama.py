@@ -1,0 +1,151 @@
+"""DAMA — frequency<->spatial fusion (drop-in for reference network/dama.py:15-206).
+
+Hot path on MI355X: the bidirectional cross-attention (1 query x 2 keys per
+frame, kv_include_self) runs on ewvit kernels — LayerNorm, to_q / to_kv MFMA
+GEMMs, the short-sequence attention and to_out with dropout + residual fused
+into its epilogue.  ``fusion_gate``'s 3x3 conv sees a 1x1 map with zero padding
+(dama.py:124-128 on the [N, 2D, 1, 1] concat), so only its centre tap is live:
+it runs as one GEMM on W[:, :, 1, 1] (exactly the conv's value and gradients).
+The frame-chunk loop and the per-video means keep the reference's semantics
+(pos_embedding indexed by chunk position, BatchNorm statistics per chunk).
+"""
+import os
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+import ewvit
+
+from . import load_config
+from .mwt import MWT
+from .sfe import EfficientViT, LayerNorm, Linear, _hooked
+
+
+class CrossAttention(nn.Module):                                           # dama.py:15-53
+    def __init__(self, dim, heads=8, dim_head=64, dropout=0.):
+        super().__init__()
+        inner_dim = dim_head * heads
+        project_out = not (heads == 1 and dim_head == dim)
+        self.heads = heads
+        self.dim_head = dim_head
+        self.scale = dim_head ** -0.5
+        self.attend = nn.Softmax(dim=-1)
+        self.to_q = Linear(dim, inner_dim, bias=False)
+        self.to_kv = Linear(dim, inner_dim * 2, bias=False)
+        self.to_out = nn.Sequential(Linear(inner_dim, dim), nn.Dropout(dropout)) if project_out else nn.Identity()
+
+    def forward(self, x, context=None, kv_include_self=False):
+        return self.forward_residual(x, context, kv_include_self, None)
+
+    def forward_residual(self, x, context=None, kv_include_self=False, resid=None):
+        context = context if context is not None else x
+        if kv_include_self:
+            context = torch.cat((x.float(), context.float()), dim=1)
+        q = ewvit.linear(x, self.to_q.weight, None, out_dtype=torch.bfloat16)
+        kv = ewvit.linear(context, self.to_kv.weight, None, out_dtype=torch.bfloat16)
+        o = ewvit.attention_cross(q, kv, self.heads, self.dim_head, self.scale)
+        if isinstance(self.to_out, nn.Identity):
+            o = o.float()
+            return o if resid is None else o + resid
+        lin, drop = self.to_out[0], self.to_out[1]
+        return ewvit.linear(o, lin.weight, lin.bias, drop_p=drop.p if self.training else 0.0,
+                            resid=resid, out_dtype=torch.float32)
+
+
+_CA_FORWARD = CrossAttention.forward
+
+
+class BidirectionalCrossTransformer(nn.Module):                            # dama.py:56-78
+    def __init__(self, dim, depth=1, heads=8, dim_head=64, dropout=0.):
+        super().__init__()
+        self.layers = nn.ModuleList([])
+        for _ in range(depth):
+            self.layers.append(nn.ModuleList([
+                LayerNorm(dim), CrossAttention(dim, heads=heads, dim_head=dim_head, dropout=dropout),
+                LayerNorm(dim), CrossAttention(dim, heads=heads, dim_head=dim_head, dropout=dropout)]))
+
+    @staticmethod
+    def _attend(att, xn, ctx, resid):
+        # keep module-call semantics (hooks, a class-wide patched forward) when present
+        if _hooked(att) or type(att).forward is not _CA_FORWARD:
+            return resid + att(xn, ctx, kv_include_self=True)
+        return att.forward_residual(xn, ctx, True, resid)
+
+    def forward(self, space_tokens, freq_tokens):
+        s, f = space_tokens.float(), freq_tokens.float()
+        for s_norm, s_att, f_norm, f_att in self.layers:
+            s = self._attend(s_att, s_norm(s), f, s)
+            f = self._attend(f_att, f_norm(f), s, f)
+        return s, f
+
+
+class FusionGate(nn.Sequential):
+    """Conv3x3(2D->D, pad 1) + BN + ReLU (dama.py:124-128).  On a 1x1 map the
+    zero padding leaves only the centre tap: one GEMM with W[:, :, 1, 1]."""
+
+    def forward(self, x):
+        conv, bn, act = self[0], self[1], self[2]
+        if x.shape[-2:] != (1, 1) or not x.is_cuda:
+            return super().forward(x)
+        B = x.shape[0]
+        w = conv.weight[:, :, conv.padding[0], conv.padding[1]]
+        y = ewvit.linear(x.reshape(B, -1), w, conv.bias, out_dtype=torch.float32)
+        return act(bn(y.reshape(B, -1, 1, 1)))
+
+
+class DAMA(nn.Module):                                                     # dama.py:80-206
+    def __init__(self, in_channels=3, dim=128, num_heads=4, levels=3, batch_size=16):
+        super().__init__()
+        self.dim = dim
+        self.levels = levels
+        self.batch_size = batch_size
+        self.sfe = EfficientViT(config=load_config(), channels=1280, selected_efficient_net=1,
+                                feat_dim=dim, output_mode='feature_map')
+        self.mwt = MWT(in_channels=in_channels, dama_dim=dim, levels=levels)
+        self.gate_net = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Flatten(), Linear(2 * dim, dim // 2),
+                                      nn.ReLU(), nn.Dropout(0.1), Linear(dim // 2, 3), nn.Softmax(dim=1))
+        self.cross_att = BidirectionalCrossTransformer(dim=dim, depth=2, heads=num_heads,
+                                                       dim_head=dim // num_heads, dropout=0.1)
+        self.fusion_gate = FusionGate(nn.Conv2d(dim * 2, dim, kernel_size=3, padding=1),
+                                      nn.BatchNorm2d(dim), nn.ReLU(inplace=True))
+
+    def _gate(self, cat):
+        g = self.gate_net
+        if _hooked(g) or cat.shape[-2:] != (1, 1):
+            return g(cat)
+        l1, drop, l2 = g[2], g[4], g[5]
+        h = ewvit.linear(cat.reshape(cat.shape[0], -1), l1.weight, l1.bias, act=2,
+                         drop_p=drop.p if self.training else 0.0, out_dtype=torch.float32)
+        return torch.softmax(ewvit.linear(h, l2.weight, l2.bias, out_dtype=torch.float32), dim=1)
+
+    def _process_frame(self, frame):
+        B = frame.shape[0]
+        space_feats = self.sfe(frame).float()
+        freq_feats = self.mwt(frame).float()
+        Ho, Wo = space_feats.shape[-2:]
+        s_flat = space_feats.flatten(2).transpose(1, 2)
+        f_flat = freq_feats.flatten(2).transpose(1, 2)
+        s_enh, f_enh = self.cross_att(s_flat, f_flat)
+        space_feats = s_enh.transpose(1, 2).reshape(B, -1, Ho, Wo)
+        freq_feats = f_enh.transpose(1, 2).reshape(B, -1, Ho, Wo)
+        concat = torch.cat([space_feats, freq_feats], dim=1)
+        fused_feats = self.fusion_gate(concat)
+        gw = self._gate(concat)
+        weighted = (gw[:, 0].view(B, 1, 1, 1) * space_feats + gw[:, 1].view(B, 1, 1, 1) * freq_feats +
+                    gw[:, 2].view(B, 1, 1, 1) * fused_feats)
+        return {'fused': weighted.mean(dim=[2, 3]), 'space': space_feats.mean(dim=[2, 3]),
+                'freq': freq_feats.mean(dim=[2, 3])}
+
+    def forward(self, x, batch_size=16):
+        B, K, C, H, W = x.shape
+        mean_fused = torch.zeros(B, self.dim, device=x.device)
+        mean_space = torch.zeros(B, self.dim, device=x.device)
+        mean_freq = torch.zeros(B, self.dim, device=x.device)
+        for start in range(0, K, batch_size):
+            end = min(start + batch_size, K)
+            feats = self._process_frame(x[:, start:end].flatten(0, 1))
+            mean_fused = mean_fused + feats['fused'].view(B, -1, self.dim).sum(dim=1)
+            mean_space = mean_space + feats['space'].view(B, -1, self.dim).sum(dim=1)
+            mean_freq = mean_freq + feats['freq'].view(B, -1, self.dim).sum(dim=1)
+        return {'fused': mean_fused / K, 'space': mean_space / K, 'freq': mean_freq / K}

@@ -1,0 +1,148 @@
+"""EfficientNetV2-S feature extractor — the spatial backbone DAMA builds through
+``EfficientViT(selected_efficient_net=1)`` (reference network/sfe.py:111-113, there
+``torchvision.models.efficientnet_v2_s``; torchvision is not part of this stack).
+
+Module tree and parameter names follow torchvision's published model so
+reference checkpoints load key-for-key (``features.{stage}.{block}.block.{i}...``).
+Layout: the backbone runs channels-last (NHWC), which MIOpen's bf16 implicit-GEMM
+kernels and the ewvit head both want (the 7x7x1280 map is then already the
+``(p1 p2 c)`` patch vector of sfe.py:153).
+
+Stages (expand, kernel, stride, in, out, blocks): FusedMBConv (1,3,1,24,24,2)
+(4,3,2,24,48,4) (4,3,2,48,64,4); MBConv (4,3,2,64,128,6) (6,3,1,128,160,9)
+(6,3,2,160,256,15); stem 3x3 s2 3->24, head 1x1 256->1280; BN eps 1e-3; SiLU;
+squeeze-excitation width = block input // 4; stochastic depth 0.2 * i / 40.
+"""
+import torch
+from torch import nn
+
+import ewvit
+
+STAGES = (
+    ('fused', 1, 3, 1, 24, 24, 2),
+    ('fused', 4, 3, 2, 24, 48, 4),
+    ('fused', 4, 3, 2, 48, 64, 4),
+    ('mb', 4, 3, 2, 64, 128, 6),
+    ('mb', 6, 3, 1, 128, 160, 9),
+    ('mb', 6, 3, 2, 160, 256, 15),
+)
+
+
+def _divisible(v, d=8):
+    n = max(d, int(v + d / 2) // d * d)
+    return n + d if n < 0.9 * v else n
+
+
+class DepthwiseConv2d(nn.Conv2d):
+    """3x3 depthwise conv (groups = channels) on the ewvit channels-last kernels
+    (csrc/depthwise.hip); parameters identical to nn.Conv2d."""
+
+    def forward(self, x):
+        return ewvit.dwconv3x3(x, self.weight, self.stride[0], self.padding[0])
+
+
+class ConvBNAct(nn.Sequential):
+    def __init__(self, cin, cout, k, stride=1, groups=1, act=True):
+        conv = DepthwiseConv2d if (groups == cin == cout and groups > 1 and k == 3) else nn.Conv2d
+        mods = [conv(cin, cout, k, stride, (k - 1) // 2, groups=groups, bias=False),
+                nn.BatchNorm2d(cout, eps=1e-3)]
+        if act:
+            mods.append(nn.SiLU(inplace=True))
+        super().__init__(*mods)
+
+
+class SqueezeExcitation(nn.Module):
+    def __init__(self, cin, csq):
+        super().__init__()
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc1 = nn.Conv2d(cin, csq, 1)
+        self.fc2 = nn.Conv2d(csq, cin, 1)
+        self.activation = nn.SiLU(inplace=True)
+        self.scale_activation = nn.Sigmoid()
+
+    def forward(self, x):
+        s = self.scale_activation(self.fc2(self.activation(self.fc1(self.avgpool(x)))))
+        return x * s
+
+
+def _drop_path(x, p, training):
+    """StochasticDepth(mode='row'): per-sample keep with prob 1-p, rescaled."""
+    if not training or p == 0.0:
+        return x
+    keep = torch.empty((x.shape[0], 1, 1, 1), dtype=x.dtype, device=x.device).bernoulli_(1.0 - p)
+    return x * keep.div_(1.0 - p)
+
+
+class _Block(nn.Module):
+    def forward(self, x):
+        r = self.block(x)
+        if self.use_res_connect:
+            return _drop_path(r, self.sd_prob, self.training) + x
+        return r
+
+
+class FusedMBConv(_Block):
+    def __init__(self, expand, k, stride, cin, cout, sd_prob):
+        super().__init__()
+        mid = _divisible(cin * expand)
+        self.use_res_connect = stride == 1 and cin == cout
+        if mid != cin:
+            self.block = nn.Sequential(ConvBNAct(cin, mid, k, stride), ConvBNAct(mid, cout, 1, act=False))
+        else:
+            self.block = nn.Sequential(ConvBNAct(cin, cout, k, stride))
+        self.sd_prob = sd_prob
+
+
+class MBConv(_Block):
+    def __init__(self, expand, k, stride, cin, cout, sd_prob):
+        super().__init__()
+        mid = _divisible(cin * expand)
+        self.use_res_connect = stride == 1 and cin == cout
+        mods = [ConvBNAct(cin, mid, 1)] if mid != cin else []
+        mods += [ConvBNAct(mid, mid, k, stride, groups=mid), SqueezeExcitation(mid, max(1, cin // 4)),
+                 ConvBNAct(mid, cout, 1, act=False)]
+        self.block = nn.Sequential(*mods)
+        self.sd_prob = sd_prob
+
+
+class EfficientNetV2S(nn.Module):
+    def __init__(self, num_classes=1000, stochastic_depth_prob=0.2, dropout=0.2):
+        super().__init__()
+        layers = [ConvBNAct(3, 24, 3, 2)]
+        total = sum(s[-1] for s in STAGES)
+        i = 0
+        for kind, e, k, st, cin, cout, n in STAGES:
+            blk = FusedMBConv if kind == 'fused' else MBConv
+            stage = []
+            for j in range(n):
+                stage.append(blk(e, k, st if j == 0 else 1, cin if j == 0 else cout, cout,
+                                 stochastic_depth_prob * i / total))
+                i += 1
+            layers.append(nn.Sequential(*stage))
+        layers.append(ConvBNAct(256, 1280, 1))
+        self.features = nn.Sequential(*layers)
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.classifier = nn.Sequential(nn.Dropout(p=dropout, inplace=True), nn.Linear(1280, num_classes))
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode='fan_out')
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.Linear):
+                r = 1.0 / (m.out_features ** 0.5)
+                nn.init.uniform_(m.weight, -r, r)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = torch.flatten(self.avgpool(self.features(x)), 1)
+        return self.classifier(x)
+
+
+def efficientnet_v2_s(weights=None, **kw):
+    if weights is not None:
+        raise RuntimeError('EfficientNetV2-S IMAGENET1K_V1 weights need a network fetch; load a '
+                           'state_dict instead')
+    return EfficientNetV2S(**kw)

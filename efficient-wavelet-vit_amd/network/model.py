@@ -1,0 +1,77 @@
+"""DeepfakeDetector — drop-in for reference network/model.py:9-171 ('dynamic' mode).
+
+The reference also constructs ``mwt``, ``sfe``, ``sfe_cls`` (EfficientNet-b0 via
+``efficientnet_pytorch.from_pretrained``, a network fetch) and ``fusion_gate``
+for the 'sfe_only' / 'sfe_mwt' ablations (model.py:37-58,100-161).  Those heads
+are outside the hot path (SURVEY §2 OUT rows); ``mwt``, ``fusion_gate`` and
+``feat_pooler`` are built for state-dict compatibility, the b0 heads are not.
+Load reference checkpoints with ``load_reference_state_dict`` (strips the
+DataParallel ``module.`` prefix, ignores the b0 keys).
+"""
+import torch
+from torch import nn
+
+import ewvit
+
+from . import load_config
+from .dama import DAMA
+from .mwt import MWT
+from .sfe import Linear, _hooked
+
+
+class DeepfakeDetector(nn.Module):
+    def __init__(self, in_channels=3, dama_dim=128, batch_size=16, ablation='dynamic'):
+        super().__init__()
+        self.dama_dim = dama_dim
+        self.in_channels = in_channels
+        self.batch_size = batch_size
+        self.ablation_config = ['dynamic', 'sfe_only', 'sfe_mwt']
+        self.ablation = ablation
+        self.config = load_config()
+        self.dama = DAMA(in_channels=in_channels, dim=dama_dim, num_heads=4, levels=3, batch_size=batch_size)
+        self.mwt = MWT(in_channels=in_channels, dama_dim=dama_dim)
+        self.fusion_gate = nn.Sequential(nn.Linear(dama_dim * 2, 2), nn.ReLU(), nn.Dropout(0.1))
+        self.feat_pooler = nn.AdaptiveAvgPool2d(1)
+        self.classifier = nn.Sequential(Linear(dama_dim, 64), nn.ReLU(), nn.Dropout(0.3), Linear(64, 1))
+        # the ablation-only members are unused in 'dynamic' mode (SURVEY §8a note 5)
+        # (and EfficientViT.mlp_head: output_mode='feature_map' never calls it, sfe.py:134-138,166)
+        unused = list(self.mwt.parameters()) + list(self.fusion_gate.parameters()) + \
+            list(self.dama.sfe.mlp_head.parameters())
+        for p in unused:
+            p.requires_grad_(False)
+
+    def _classify(self, f):
+        c = self.classifier
+        if _hooked(c):
+            return c(f)
+        l1, drop, l2 = c[0], c[2], c[3]
+        h = ewvit.linear(f, l1.weight, l1.bias, act=2, drop_p=drop.p if self.training else 0.0,
+                         out_dtype=torch.float32)
+        return ewvit.linear(h, l2.weight, l2.bias, out_dtype=torch.float32)
+
+    def forward(self, x, batch_size, ablation):
+        if batch_size is not None:
+            self.batch_size = batch_size
+        if ablation is not None:
+            self.ablation = ablation
+        if self.ablation != 'dynamic':
+            raise NotImplementedError(f"ablation '{self.ablation}' needs EfficientNet-b0 (network fetch); "
+                                      "only 'dynamic' (the DAMA hot path) is provided")
+        d = self.dama(x, batch_size=self.batch_size)
+        return {'logits': self._classify(d['fused']), 'fused': d['fused'], 'space': d['space'],
+                'freq': d['freq']}
+
+    def configure_ablation(self, ablation):
+        if ablation in self.ablation_config:
+            self.ablation = ablation
+        else:
+            raise ValueError(f'Invalid ablation config: {ablation}.')
+
+
+def load_reference_state_dict(model, state_dict):
+    """Load a reference (possibly DataParallel-wrapped) checkpoint; returns the
+    (missing, unexpected) key lists after dropping the b0 ablation heads."""
+    sd = {k[7:] if k.startswith('module.') else k: v for k, v in state_dict.items()}
+    sd = {k: v for k, v in sd.items() if not (k.startswith('sfe.') or k.startswith('sfe_cls.'))}
+    res = model.load_state_dict(sd, strict=False)
+    return res.missing_keys, res.unexpected_keys

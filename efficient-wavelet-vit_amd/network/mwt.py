@@ -1,0 +1,148 @@
+"""MWT — multi-level wavelet branch (drop-in for reference network/mwt.py:7-119).
+
+Hot path on MI355X:
+* one ewvit kernel pair replaces the per-level DWT + reshape + bilinear upsample
+  (mwt.py:76-81): ``dwt_haar_fwd`` reads the frames once and emits every level's
+  bands, ``hf_upsample`` writes all levels' upsampled HF input channels-last
+  ``[L, N, H/2, W/2, 3C]`` (channel c*3+band, mwt.py:77);
+* the three ``hf_conv['seperate'][i]`` convs (colour channel i's three bands,
+  mwt.py:84-86) run as ONE grouped conv (groups=3) over all levels at once
+  (weights are shared by the levels, mwt.py:108), likewise ``hf_conv['fusion']``;
+  BatchNorm statistics and running-stat updates stay per level and in the
+  reference's order, so train-mode numerics and state are the reference's.
+The conv stack itself is MIOpen (bf16 NHWC under autocast) in this round.
+
+If ``wavelet_transform`` is overridden on the instance or class (as
+utils/visualize_feature_maps.py:151-158 does), forward falls back to the
+reference's per-level loop calling ``self.wavelet_transform`` (still on GPU).
+"""
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+import ewvit
+
+
+class DWTForward(nn.Module):
+    """pytorch_wavelets.DWTForward(J, wave='haar', mode='zero') on the ewvit DWT kernel.
+    Same buffers (h0_col, h1_col, h0_row, h1_row) for state-dict compatibility."""
+
+    def __init__(self, J=1, wave='haar', mode='zero'):
+        super().__init__()
+        if wave != 'haar' or mode != 'zero':
+            raise NotImplementedError('ewvit DWT implements haar / zero padding only (mwt.py:20)')
+        self.J = J
+        s = 0.7071067811865476
+        h0 = torch.tensor([s, s], dtype=torch.float32)
+        h1 = torch.tensor([s, -s], dtype=torch.float32)
+        self.register_buffer('h0_col', h0.reshape(1, 1, 2, 1))
+        self.register_buffer('h1_col', h1.reshape(1, 1, 2, 1))
+        self.register_buffer('h0_row', h0.reshape(1, 1, 1, 2))
+        self.register_buffer('h1_row', h1.reshape(1, 1, 1, 2))
+
+    def forward(self, x):
+        odt = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        return ewvit.dwt_haar(x, self.J, out_dtype=odt)
+
+
+def _cbr(cin, cout, stride=1):
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout),
+                         nn.ReLU(inplace=True))
+
+
+def bn_groups(x, bns, training):
+    """Apply BatchNorm modules `bns` to consecutive channel groups of x with ONE
+    batch_norm launch; running stats / num_batches_tracked are updated exactly as
+    calling each module on its slice would (same momentum, same batch stats)."""
+    w = torch.cat([b.weight for b in bns])
+    bi = torch.cat([b.bias for b in bns])
+    rm = torch.cat([b.running_mean for b in bns])
+    rv = torch.cat([b.running_var for b in bns])
+    b0 = bns[0]
+    use_batch = training or rm is None
+    y = F.batch_norm(x, rm, rv, w, bi, use_batch, b0.momentum, b0.eps)
+    if training:
+        off = 0
+        for b in bns:
+            n = b.num_features
+            b.running_mean.copy_(rm[off:off + n])
+            b.running_var.copy_(rv[off:off + n])
+            b.num_batches_tracked.add_(1)
+            off += n
+    return y
+
+
+def _cdt():
+    return torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else torch.float32
+
+
+class MWT(nn.Module):
+    """Multi-level Wavelet Transformer (reference mwt.py:7-119)."""
+
+    def __init__(self, in_channels=3, dama_dim=128, levels=3):
+        super().__init__()
+        self.in_channels = in_channels
+        self.dama_dim = dama_dim
+        self.levels = levels
+        self.dwt = DWTForward(J=1, wave='haar', mode='zero')                  # mwt.py:20
+        self.freq_conv = _cbr(dama_dim, dama_dim, stride=2)                    # mwt.py:23-36
+        self.freq_pool = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2),  # mwt.py:38-44
+                                       nn.Conv2d(dama_dim, dama_dim, 3, padding=1, stride=2),
+                                       nn.BatchNorm2d(dama_dim), nn.ReLU(inplace=True),
+                                       nn.AdaptiveAvgPool2d(1))
+        self.hf_conv = nn.ModuleDict({                                         # mwt.py:47-65
+            'seperate': nn.ModuleList([_cbr(in_channels, 6 * in_channels) for _ in range(3)]),
+            'fusion': _cbr(18 * in_channels, dama_dim)})
+        self.multiscale_fusion = _cbr(levels * dama_dim, dama_dim)             # mwt.py:68-72
+
+    # ---- reference API (mwt.py:74-90), one level
+    def wavelet_transform(self, x, target_size):
+        B, C, H, W = x.shape
+        if self.levels > 1:
+            hf, ll = ewvit.dwt_hf_upsample(x, 1, tuple(target_size), out_dtype=x.dtype if x.dtype == torch.bfloat16 else torch.float32,
+                                           band_dtype=torch.float32)
+            hf = hf[0].permute(0, 3, 1, 2)
+        else:
+            ll, yh = self.dwt(x)
+            hf = yh[0].reshape(B, 3 * C, H // 2, W // 2)
+        processed = [self.hf_conv['seperate'][i](hf[:, i * C:(i + 1) * C]) for i in range(3)]
+        return ll, self.hf_conv['fusion'](torch.cat(processed, dim=1))
+
+    def _patched(self):
+        return 'wavelet_transform' in self.__dict__ or type(self).wavelet_transform is not MWT.wavelet_transform
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        target = (H // 2, W // 2)
+        if self._patched():
+            cur, highs = x, []
+            for _ in range(self.levels):
+                ll, hf = self.wavelet_transform(cur, target)
+                highs.append(hf)
+                cur = ll
+            fused = self.multiscale_fusion(torch.cat(highs, dim=1))
+            return self.freq_pool(self.freq_conv(fused))
+        return self.freq_pool(self.freq_conv(self.multiscale_fusion(self._hf_features(x))))
+
+    def _hf_features(self, x):
+        """All levels' hf_compressed, concatenated on channels: [B, L*dim, H/2, W/2]."""
+        B, C, H, W = x.shape
+        Lv = self.levels
+        OH, OW = H // 2, W // 2
+        cdt = _cdt()
+        out_hw = (OH, OW) if Lv > 1 else ((H + 1) // 2, (W + 1) // 2)
+        hf, _ = ewvit.dwt_hf_upsample(x, Lv, out_hw, out_dtype=cdt,
+                                      band_dtype=torch.bfloat16 if cdt == torch.bfloat16 else torch.float32)
+        hf = hf.view(Lv * B, out_hw[0], out_hw[1], 3 * C).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
+        sep = self.hf_conv['seperate']
+        w = torch.cat([sep[i][0].weight for i in range(3)])
+        b = torch.cat([sep[i][0].bias for i in range(3)])
+        y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1, groups=3)
+        bns = [sep[i][1] for i in range(3)]
+        y = torch.cat([bn_groups(y[l * B:(l + 1) * B], bns, self.training) for l in range(Lv)]) if Lv > 1 \
+            else bn_groups(y, bns, self.training)
+        y = F.relu_(y)
+        fus = self.hf_conv['fusion']
+        z = fus[0](y)
+        zs = [F.relu_(fus[1](z[l * B:(l + 1) * B])) for l in range(Lv)]
+        return torch.cat(zs, dim=1) if Lv > 1 else zs[0]

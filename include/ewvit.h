@@ -1,0 +1,163 @@
+/*
+ * ewvit.h — C-ABI of the MI355X (gfx950) hot path of Efficient-Wavelet-ViT.
+ *
+ * The reference (Sheldon-Xiao9/efficient-wavelet-vit) is pure Python and has
+ * no FFI; its boundary is the nn.Module surface of network/{mwt,sfe,dama}.py.
+ * Each entry point below replaces the reference operation cited next to it;
+ * the Python host side (efficient-wavelet-vit_amd/ewvit/) binds them through
+ * ctypes and keeps the reference's module/attribute/state-dict surface.
+ *
+ * Conventions (all entry points):
+ *  - plain device pointers and sizes, no framework types; every tensor is
+ *    dense in the layout stated; the caller owns all memory;
+ *  - `dtype` codes: EWVIT_F32 = 0, EWVIT_BF16 = 1;
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream); every
+ *    launch is asynchronous on it, no entry point synchronises or allocates,
+ *    so calls are capturable into a hipGraph and re-entrant across threads;
+ *  - return 0 on success, otherwise a hipError_t value or EWVIT_EINVAL for a
+ *    rejected argument; ewvit_last_error() then describes it (thread-local).
+ */
+#ifndef EWVIT_H
+#define EWVIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EWVIT_ABI_VERSION 1
+#define EWVIT_F32 0
+#define EWVIT_BF16 1
+#define EWVIT_EINVAL 1000
+
+int ewvit_abi_version(void);
+const char *ewvit_last_error(void);
+
+/* ---------------------------------------------------------------- DWT ---
+ * Multi-level 2-D Haar analysis, mode 'zero' — replaces the J=1
+ * DWTForward(wave='haar', mode='zero') built at network/mwt.py:20 and called
+ * once per level at network/mwt.py:76 inside the level loop mwt.py:107-111.
+ * One HBM read of x yields every level.
+ *   x   [N, C, H, W]                       (x_dtype)
+ *   yh  levels planes, level l (1-based) at yh + off_l:
+ *       [N, C, 3, h_l, w_l], h_l = ceil(h_{l-1}/2), band order
+ *       (W-lo,H-hi), (W-hi,H-lo), (W-hi,H-hi) = pytorch_wavelets yh[0][:, :, b]
+ *       off_1 = 0, off_{l+1} = off_l + N*C*3*h_l*w_l           (out_dtype)
+ *   ll  [N, C, h_L, w_L] the final level's low band          (out_dtype)
+ * levels in [1, 5].
+ */
+int ewvit_dwt_haar_fwd(const void *x, void *yh, void *ll, int64_t N, int64_t C, int64_t H,
+                       int64_t W, int levels, int x_dtype, int out_dtype, void *stream);
+
+/* Bilinear (align_corners=False) upsample of every level's HF bands to
+ * (OH, OW), channels-last — replaces network/mwt.py:77-81 (reshape of yh[0]
+ * to channel c*3+band, then F.interpolate(size=target_size, mode='bilinear')).
+ *   yh  as produced by ewvit_dwt_haar_fwd (in_dtype)
+ *   out [levels, N, OH, OW, 3C]  channel = c*3 + band          (out_dtype)
+ * (OH, OW) == (h_l, w_l) is an exact copy (the reference skips the interpolate
+ * when MWT.levels == 1, mwt.py:79; the caller passes (h_1, w_1) then).
+ */
+int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H, int64_t W,
+                      int levels, int64_t OH, int64_t OW, int in_dtype, int out_dtype,
+                      void *stream);
+
+/* --------------------------------------------------------------- GEMM ---
+ * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(k,n) )   bf16 MFMA, fp32 accumulate
+ * — the projection GEMMs of network/sfe.py:44-55,29-40 (to_qkv, to_out,
+ * FeedForward), network/dama.py:25-31 (to_q, to_kv, to_out),
+ * sfe.py:127,155 (patch_to_embedding, split-K) and their backward products.
+ *   A(m,k) = A[m*lda_m + k*lda_k]   (exactly one of lda_m, lda_k equals 1)
+ *   B(k,n) = B[k*ldb_k + n*ldb_n]   (exactly one of ldb_k, ldb_n equals 1)
+ *   C[m*ldc + n]                    (c_dtype)
+ * epilogue, in order: + bias[n] (f32, may be NULL)
+ *                     ; act: 0 none, 1 GELU(erf), 2 ReLU, 3 multiply by GELU'(aux[m,n])
+ *                       (act 1/2 also store the pre-activation to aux when aux != NULL)
+ *                     ; dropout: if drop_p > 0, keep with prob 1-drop_p from
+ *                       hash(seed, m*N+n), scale 1/(1-drop_p)
+ *                     ; + resid[m*ldr + n] (f32 or bf16 per resid_dtype, may be NULL)
+ *                     ; if beta != 0: C = beta*C_old + value (f32 C only)
+ *   aux[m*ldc + n] (bf16) — pre-activation for act 1/3
+ * splitk > 1 partitions K over blockIdx.z; workspace must then hold
+ * splitk*M*N floats and the epilogue runs in a second launch.
+ */
+int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+               int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype, int64_t ldc,
+               int64_t M, int64_t N, int64_t K, float alpha, float beta, const float *bias,
+               int act, void *aux, float drop_p, uint64_t seed, const void *resid,
+               int resid_dtype, int64_t ldr, int splitk, float *workspace, void *stream);
+
+/* Column sums: out[n] (+)= sum_m X[m*ldx + n]  (bias gradients).  accumulate!=0 adds. */
+int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N, float *out,
+                 int accumulate, void *stream);
+
+/* Dropout mask regeneration for backward: g[i] *= keep(seed, i)/(1-p), i < n. */
+int ewvit_dropout_bwd(void *g, int g_dtype, int64_t rows, int64_t cols, int64_t ldg, float p,
+                      uint64_t seed, void *stream);
+
+/* Backward of the GEMM epilogue: out[m*N+n] = dy[m*lddy+n] * keep(seed, m*N+n)/(1-p)
+ * * act'(aux[m*N+n]);  act 0 none, 1 GELU(erf) (aux = pre-activation), 2 ReLU. */
+int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const void *aux, int act,
+                  float drop_p, uint64_t seed, void *out, int out_dtype, int64_t M, int64_t N,
+                  void *stream);
+
+/* ---------------------------------------------------------- LayerNorm ---
+ * y = (x - mean) * rstd * gamma + beta over the last dim D, eps — nn.LayerNorm
+ * of network/sfe.py:23 (PreNorm) and network/dama.py:62,64.
+ *   x [M, D] (x_dtype, row stride ldx); y [M, D] (y_dtype); mean/rstd [M] f32.
+ */
+int ewvit_layernorm_fwd(const void *x, int x_dtype, int64_t ldx, const float *gamma,
+                        const float *beta, void *y, int y_dtype, float *mean, float *rstd,
+                        int64_t M, int64_t D, float eps, void *stream);
+/* dx = LN backward (x_dtype input, dy dy_dtype); dgamma/dbeta accumulated (+=)
+ * in f32; dx written (f32) or added to (accumulate_dx != 0). */
+int ewvit_layernorm_bwd(const void *dy, int dy_dtype, const void *x, int x_dtype, int64_t ldx,
+                        const float *gamma, const float *mean, const float *rstd, float *dx,
+                        int accumulate_dx, float *dgamma, float *dbeta, int64_t M, int64_t D,
+                        void *stream);
+
+/* ------------------------------------------------- short-sequence attention ---
+ * softmax(q k^T * scale) v per (batch, head) for the degenerate sequence
+ * lengths of this model: ViT n=2 (sfe.py:59-70: 'b n (h d) -> b h n d', einsum,
+ * Softmax(-1), einsum, merge) and the cross-attention 1 query x 2 keys
+ * (dama.py:33-53 with kv_include_self).  nq, nk <= 8, head dim d <= 128.
+ *   q (b, i, h, :) at q + b*sq_b + i*sq_n + h*d      (bf16)
+ *   k (b, j, h, :) at k + b*sk_b + j*sk_n + h*d      (bf16); v likewise (sv_*)
+ *   o (b, i, h, :) at o + b*so_b + i*so_n + h*d      (bf16)
+ *   p [B, H, nq, nk] softmax probabilities saved for backward (f32)
+ */
+int ewvit_attn_fwd(const void *q, int64_t sq_b, int64_t sq_n, const void *k, int64_t sk_b,
+                   int64_t sk_n, const void *v, int64_t sv_b, int64_t sv_n, void *o,
+                   int64_t so_b, int64_t so_n, float *p, int64_t B, int64_t H, int nq, int nk,
+                   int d, float scale, void *stream);
+/* dq, dk, dv (bf16, same strides as q/k/v; written, not accumulated) from do. */
+int ewvit_attn_bwd(const void *dout, int64_t sdo_b, int64_t sdo_n, const void *q, int64_t sq_b,
+                   int64_t sq_n, const void *k, int64_t sk_b, int64_t sk_n, const void *v,
+                   int64_t sv_b, int64_t sv_n, const float *p, void *dq, void *dk, void *dv,
+                   int64_t B, int64_t H, int nq, int nk, int d, float scale, void *stream);
+
+/* ------------------------------------------- depthwise 3x3 conv (backbone) ---
+ * The MBConv depthwise convolutions of EfficientNetV2-S (groups = channels,
+ * kernel 3, stride 1|2, pad 1, no bias) — the backbone the reference reaches
+ * through network/sfe.py:111-113,150 (torchvision Conv2dNormActivation).
+ * Channels-last: x [N, H, W, C], y [N, Ho, Wo, C] (dtype), w [C, 3, 3] f32;
+ * C % 8 == 0; Ho = (H + 2*pad - 3)/stride + 1.
+ */
+int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,
+                        int64_t C, int stride, int pad, int dtype, void *stream);
+/* dx [N, H, W, C] from dy [N, Ho, Wo, C] (written). */
+int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx, int64_t N, int64_t H, int64_t W,
+                             int64_t C, int stride, int pad, int dtype, void *stream);
+/* bytes of f32 workspace ewvit_dwconv3x3_bwd_weight needs (per-slab partials). */
+int64_t ewvit_dwconv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t C, int stride,
+                                             int pad);
+/* dw [C, 3, 3] f32 (= or += when accumulate) = sum over N*Ho*Wo of dy * x-tap;
+ * deterministic two-pass reduction through `workspace`. */
+int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
+                               int64_t H, int64_t W, int64_t C, int stride, int pad, int dtype,
+                               float *workspace, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EWVIT_H */

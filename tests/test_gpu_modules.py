@@ -1,0 +1,273 @@
+"""Module-level parity: the product (efficient-wavelet-vit_amd/network on ewvit
+kernels, MI355X) against the oracle (CPU fp32 restatement pinned to the
+reference) with identical recipe weights and inputs.
+
+Tolerance: bf16 GPU vs fp32 CPU — max |err| <= 2e-2 * scale of the
+output and cosine >= 0.999; gradients cosine >= 0.99 (bf16 operands in every
+GEMM/conv).  The fp32-conv runs (no autocast) use the same bound; the product's
+GEMMs always take bf16 operands.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def cos(a, b):
+    a = a.detach().double().flatten().cpu()
+    b = b.detach().double().flatten().cpu()
+    return float((a @ b) / (a.norm() * b.norm() + 1e-30))
+
+
+def check(a, b, tol=2e-2, cmin=0.999):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    scale = max(float(b.abs().max()), 1e-6)
+    err = float((a - b).abs().max())
+    c = cos(a, b)
+    assert err <= tol * scale and c >= cmin, f'max err {err:.3e} (scale {scale:.3e}), cos {c:.6f}'
+
+
+def no_stochastic(m):
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+        if hasattr(mod, 'sd_prob'):
+            mod.sd_prob = 0.0
+    return m
+
+
+def pair(prod_cls, oracle_cls, args, seed):
+    from oracle.weights import recipe_state_dict
+    o = no_stochastic(oracle_cls(*args))
+    sd = recipe_state_dict(o.state_dict(), seed)
+    o.load_state_dict(sd)
+    p = no_stochastic(prod_cls(*args))
+    p.load_state_dict(sd)
+    return p.to(DEV), o
+
+
+def grads_close(p, o, names, cmin=0.99):
+    pp, oo = dict(p.named_parameters()), dict(o.named_parameters())
+    for n in names:
+        assert pp[n].grad is not None, n
+        c = cos(pp[n].grad, oo[n].grad)
+        assert c >= cmin, f'{n}: grad cosine {c:.5f}'
+
+
+def test_vit_transformer_vs_oracle():
+    from network import sfe
+    from oracle import model as om
+    from oracle.weights import recipe_input
+    p, o = pair(sfe.Transformer, om.Transformer, (512, 2, 8, 64, 2048, 0.15), 13)
+    p.train(); o.train()
+    x = recipe_input((64, 2, 512), 77)
+    xo = x.clone().requires_grad_(True)
+    xp = x.to(DEV).requires_grad_(True)
+    yo, yp = o(xo), p(xp)
+    check(yp, yo)
+    w = torch.randn(yo.shape, generator=torch.Generator().manual_seed(1))
+    (yo * w).sum().backward()
+    (yp * w.to(DEV)).sum().backward()
+    assert cos(xp.grad, xo.grad) > 0.995
+    grads_close(p, o, [n for n, _ in o.named_parameters()])
+
+
+def test_vit_golden(golden):
+    """Straight against the reference-generated fixture (ref_vit.npz)."""
+    from network import sfe
+    from oracle.weights import apply_recipe
+    z = golden('ref_vit.npz')
+    tr = no_stochastic(apply_recipe(sfe.Transformer(512, 2, 8, 64, 2048, 0.15), 13)).to(DEV)
+    x = torch.from_numpy(z['x']).to(DEV).requires_grad_(True)
+    y = tr(x)
+    check(y, torch.from_numpy(z['y']))
+    (y * torch.from_numpy(z['w']).to(DEV)).sum().backward()
+    check(x.grad, torch.from_numpy(z['grad.x']), tol=3e-2, cmin=0.995)
+
+
+def test_cross_transformer_vs_golden(golden):
+    from network import dama
+    from oracle.weights import apply_recipe
+    z = golden('ref_cross.npz')
+    bct = no_stochastic(apply_recipe(dama.BidirectionalCrossTransformer(128, 2, 4, 32, 0.1), 12)).to(DEV)
+    s = torch.from_numpy(z['s']).to(DEV).requires_grad_(True)
+    f = torch.from_numpy(z['f']).to(DEV).requires_grad_(True)
+    so, fo = bct(s, f)
+    check(so, torch.from_numpy(z['s_out']))
+    check(fo, torch.from_numpy(z['f_out']))
+    ((so * torch.from_numpy(z['ws']).to(DEV)).sum() + (fo * torch.from_numpy(z['wf']).to(DEV)).sum()).backward()
+    check(s.grad, torch.from_numpy(z['grad.s']), tol=3e-2, cmin=0.995)
+    check(f.grad, torch.from_numpy(z['grad.f']), tol=3e-2, cmin=0.995)
+    for n, prm in bct.named_parameters():
+        assert cos(prm.grad, torch.from_numpy(z['grad.' + n])) > 0.99, n
+
+
+@pytest.mark.parametrize('autocast', [False, True])
+def test_mwt_config1_golden(golden, autocast):
+    """BASELINE configs[0]: MWT(3, 64, levels=2) on [4,3,64,64], eval and train."""
+    from network import mwt
+    from oracle.weights import apply_recipe
+    z = golden('ref_mwt_cfg1.npz')
+    m = apply_recipe(mwt.MWT(3, 64, 2), 11).to(DEV)
+    x = torch.from_numpy(z['x']).to(DEV)
+    tol = 3e-2 if autocast else 2e-2
+    m.eval()
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        check(m(x), torch.from_numpy(z['y_eval']), tol)
+    m.train()
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        y = m(x)
+    check(y, torch.from_numpy(z['y_train']), tol)
+    (y.float() * torch.from_numpy(z['loss_w']).to(DEV)).sum().backward()
+    assert cos(m.hf_conv['fusion'][0].weight.grad, torch.from_numpy(z['grad.hf_conv.fusion.0.weight'])) > 0.99
+    assert cos(m.hf_conv['seperate'][0][0].weight.grad, torch.from_numpy(z['grad.hf_conv.seperate.0.0.weight'])) > 0.99
+    st = m.state_dict()
+    for k in ['hf_conv.fusion.1.running_mean', 'hf_conv.fusion.1.running_var', 'multiscale_fusion.1.running_mean']:
+        check(st[k], torch.from_numpy(z['state.' + k]), tol)
+    assert int(st['hf_conv.fusion.1.num_batches_tracked']) == 2
+    assert int(st['hf_conv.seperate.1.1.num_batches_tracked']) == 2
+
+
+def test_mwt_wavelet_transform_api_and_patched_path(golden):
+    """The per-level API (mwt.py:74-90) and the monkey-patch fallback
+    (utils/visualize_feature_maps.py:151-158) give the fast path's result."""
+    from network import mwt
+    from oracle.weights import apply_recipe
+    z = golden('ref_mwt_cfg1.npz')
+    m = apply_recipe(mwt.MWT(3, 64, 2), 11).to(DEV).eval()
+    x = torch.from_numpy(z['x']).to(DEV)
+    with torch.no_grad():
+        ll, hf = m.wavelet_transform(x, (32, 32))
+        check(ll, torch.from_numpy(z['wt_ll']), 1e-5)
+        fast = m(x)
+        orig = m.wavelet_transform
+        calls = []
+
+        def spy(xx, ts):
+            calls.append(xx.shape)
+            return orig(xx, ts)
+        m.wavelet_transform = spy
+        slow = m(x)
+    assert len(calls) == 2
+    check(slow, fast, 1e-3)
+
+
+def test_dwt_module_api():
+    from network.mwt import DWTForward
+    from oracle.model import DWTForward as ODWT
+    x = torch.randn(2, 3, 32, 32)
+    ll, yh = DWTForward().to(DEV)(x.to(DEV))
+    llo, yho = ODWT()(x)
+    torch.testing.assert_close(ll.cpu(), llo, atol=1e-6, rtol=0)
+    torch.testing.assert_close(yh[0].cpu(), yho[0], atol=1e-6, rtol=0)
+    assert set(DWTForward().state_dict()) == {'h0_col', 'h1_col', 'h0_row', 'h1_row'}
+
+
+@pytest.fixture(scope='module')
+def dama_pair():
+    from network import dama
+    from oracle import model as om
+    torch.manual_seed(0)
+    return pair(dama.DAMA, om.DAMA, (3, 128, 4, 3, 8), 14)
+
+
+def test_efficientvit_head_golden(golden, dama_pair):
+    p, _ = dama_pair
+    z = golden('ref_dama.npz')
+    from oracle.weights import recipe_input
+    feat = recipe_input((4, 1280, 7, 7), seed=1005).to(DEV).to(memory_format=torch.channels_last)
+    p.eval()
+    with torch.no_grad():
+        check(p.sfe.head(feat), torch.from_numpy(z['head_out']))
+
+
+def test_dama_process_frame_eval_golden(golden, dama_pair):
+    p, _ = dama_pair
+    z = golden('ref_dama.npz')
+    from oracle.weights import recipe_input
+    xf = recipe_input((4, 3, 224, 224), seed=1006).to(DEV)
+    p.eval()
+    with torch.no_grad():
+        out = p._process_frame(xf)
+        for k in ('fused', 'space', 'freq'):
+            check(out[k], torch.from_numpy(z['pf_eval.' + k]), 3e-2)
+        check(p.mwt(xf), torch.from_numpy(z['mwt_eval']), 3e-2)
+
+
+def _max_err(a, b):
+    return float((a.detach().float().cpu() - b.detach().float().cpu()).abs().max())
+
+
+@pytest.mark.parametrize('autocast', [False, True])
+def test_dama_train_step_vs_oracle(dama_pair, autocast):
+    """Train-mode DAMA.forward over K=8 frames per video in 2 chunks + backward,
+    vs the oracle on CPU (same weights; dropout / stochastic depth off).
+
+    fp32 run: 2e-2 of scale, cosine 0.998.  bf16-autocast run: the bound is set
+    by PyTorch's own bf16 autocast of the reference op sequence (the oracle moved
+    to the GPU under autocast): the product's error vs fp32 must stay within
+    1.5x that error (+1e-2 of scale), and cosine >= 0.995."""
+    import copy
+    p0, o0 = dama_pair
+    p, o = copy.deepcopy(p0), copy.deepcopy(o0)
+    p.train(); o.train()
+    from oracle.weights import recipe_input
+    x = recipe_input((2, 8, 3, 224, 224), seed=4242)
+    ro = o(x, batch_size=4)
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        rp = p(x.to(DEV), batch_size=4)
+    if autocast:
+        og = copy.deepcopy(o0).to(DEV).train()
+        with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+            rg = og(x.to(DEV), batch_size=4)
+        for k in ro:
+            scale = float(ro[k].abs().max())
+            bound = 1.5 * _max_err(rg[k], ro[k]) + 1e-2 * scale
+            assert _max_err(rp[k], ro[k]) <= bound, (k, _max_err(rp[k], ro[k]), _max_err(rg[k], ro[k]), scale)
+            assert cos(rp[k], ro[k]) >= 0.995, k
+    else:
+        for k in ro:
+            check(rp[k], ro[k], 2e-2, 0.998)
+    tol = 4e-2 if autocast else 2e-2
+    w = {k: torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) for i, (k, v) in enumerate(sorted(ro.items()))}
+    sum((ro[k] * w[k]).sum() for k in ro).backward()
+    sum((rp[k].float() * w[k].to(DEV)).sum() for k in rp).backward()
+    names = ['sfe.patch_to_embedding.weight', 'sfe.transformer.layers.0.0.fn.to_qkv.weight',
+             'sfe.transformer.layers.1.1.fn.net.0.weight', 'cross_att.layers.1.3.to_kv.weight',
+             'cross_att.layers.0.0.weight', 'gate_net.2.weight', 'fusion_gate.0.weight',
+             'mwt.multiscale_fusion.0.weight', 'mwt.hf_conv.fusion.0.weight', 'mwt.hf_conv.seperate.1.0.weight',
+             'sfe.pos_embedding', 'sfe.cls_token', 'sfe.efficient_net.features.7.0.weight',
+             'sfe.efficient_net.features.6.3.block.1.0.weight']
+    grads_close(p, o, names, 0.98 if autocast else 0.99)
+    # BatchNorm running statistics were updated per level and per chunk like the reference
+    ps, os_ = p.state_dict(), o.state_dict()
+    for k in ['mwt.hf_conv.fusion.1.running_mean', 'mwt.hf_conv.seperate.2.1.running_var',
+              'fusion_gate.1.running_mean', 'mwt.multiscale_fusion.1.running_var']:
+        check(ps[k], os_[k], tol)
+    assert int(ps['mwt.hf_conv.fusion.1.num_batches_tracked']) == int(os_['mwt.hf_conv.fusion.1.num_batches_tracked']) == 6
+
+
+def test_chunk_over_64_frames_raises_like_reference(dama_pair):
+    p, _ = dama_pair
+    with pytest.raises(RuntimeError, match='pos_embedding'):
+        p.sfe.head(torch.randn(65, 1280, 7, 7, device=DEV))
+
+
+def test_deepfake_detector_forward_backward_runs():
+    from network.model import DeepfakeDetector
+    from network.losses import combined_loss
+    m = DeepfakeDetector(3, 128, 8).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 8, 3, 224, 224, device=DEV)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = m(x, 8, 'dynamic')
+    loss, parts = combined_loss(out, torch.tensor([0., 1.], device=DEV),
+                                torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=DEV)), 1, 1)
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert out['logits'].shape == (2, 1)
+    assert m.dama.sfe.patch_to_embedding.weight.grad is not None
+    assert m.dama.sfe.efficient_net.features[0][0].weight.grad is None      # frozen (sfe.py:115-119)
