@@ -288,7 +288,7 @@ def test_depthwise_fwd_bwd_vs_torch(N, C, H, stride, dtype):
     w = torch.randn(C, 1, 3, 3, generator=g)
     dy_shape = (N, C, (H - 1) // stride + 1, (H - 1) // stride + 1)
     dy = torch.randn(dy_shape, generator=g).to(dtype)
-    xr, wr = x.float().requires_grad_(True), w.clone().requires_grad_(True)
+    xr, wr = x.float().clone().requires_grad_(True), w.clone().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, stride=stride, padding=1, groups=C)
     yr.backward(dy.float())
     xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)

@@ -123,8 +123,21 @@ def test_mwt_config1_golden(golden, autocast):
         y = m(x)
     check(y, torch.from_numpy(z['y_train']), tol)
     (y.float() * torch.from_numpy(z['loss_w']).to(DEV)).sum().backward()
-    assert cos(m.hf_conv['fusion'][0].weight.grad, torch.from_numpy(z['grad.hf_conv.fusion.0.weight'])) > 0.99
-    assert cos(m.hf_conv['seperate'][0][0].weight.grad, torch.from_numpy(z['grad.hf_conv.seperate.0.0.weight'])) > 0.99
+    # gradient bound: fp32 0.99 cosine; bf16 autocast: no worse than PyTorch's own
+    # autocast of the reference op sequence (oracle on the GPU) minus 0.01
+    floor = {'hf_conv.fusion.0.weight': 0.99, 'hf_conv.seperate.0.0.weight': 0.99}
+    if autocast:
+        from oracle import model as om
+        og = apply_recipe(om.MWT(3, 64, 2), 11).to(DEV).train()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            yg = og(x)
+        (yg.float() * torch.from_numpy(z['loss_w']).to(DEV)).sum().backward()
+        gg = dict(og.named_parameters())
+        for k in floor:
+            floor[k] = min(0.99, cos(gg[k].grad, torch.from_numpy(z['grad.' + k])) - 0.01)
+    pp = dict(m.named_parameters())
+    for k, f in floor.items():
+        assert cos(pp[k].grad, torch.from_numpy(z['grad.' + k])) >= f, (k, f)
     st = m.state_dict()
     for k in ['hf_conv.fusion.1.running_mean', 'hf_conv.fusion.1.running_var', 'multiscale_fusion.1.running_mean']:
         check(st[k], torch.from_numpy(z['state.' + k]), tol)
@@ -222,7 +235,7 @@ def test_dama_train_step_vs_oracle(dama_pair, autocast):
         rp = p(x.to(DEV), batch_size=4)
     if autocast:
         og = copy.deepcopy(o0).to(DEV).train()
-        with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        with torch.autocast('cuda', dtype=torch.bfloat16):
             rg = og(x.to(DEV), batch_size=4)
         for k in ro:
             scale = float(ro[k].abs().max())
@@ -242,7 +255,17 @@ def test_dama_train_step_vs_oracle(dama_pair, autocast):
              'mwt.multiscale_fusion.0.weight', 'mwt.hf_conv.fusion.0.weight', 'mwt.hf_conv.seperate.1.0.weight',
              'sfe.pos_embedding', 'sfe.cls_token', 'sfe.efficient_net.features.7.0.weight',
              'sfe.efficient_net.features.6.3.block.1.0.weight']
-    grads_close(p, o, names, 0.98 if autocast else 0.99)
+    if autocast:
+        # bf16 gradients: bounded by PyTorch's own autocast of the reference op
+        # sequence on the same GPU (cosine to fp32 minus 0.01, capped at 0.98)
+        sum((rg[k].float() * w[k].to(DEV)).sum() for k in rg).backward()
+        pp, oo, gg = dict(p.named_parameters()), dict(o.named_parameters()), dict(og.named_parameters())
+        for n in names:
+            floor = min(0.98, cos(gg[n].grad, oo[n].grad) - 0.01)
+            c = cos(pp[n].grad, oo[n].grad)
+            assert c >= floor, f'{n}: grad cosine {c:.5f} < {floor:.5f} (torch autocast {floor + 0.01:.5f})'
+    else:
+        grads_close(p, o, names, 0.99)
     # BatchNorm running statistics were updated per level and per chunk like the reference
     ps, os_ = p.state_dict(), o.state_dict()
     for k in ['mwt.hf_conv.fusion.1.running_mean', 'mwt.hf_conv.seperate.2.1.running_var',
