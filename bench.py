@@ -48,11 +48,8 @@ def build_step(dev, frames, rank):
     videos = 8
     per_video = frames // videos
     model = DeepfakeDetector(3, 128, batch_size=per_video).to(dev).to(memory_format=torch.channels_last)
-    ddp = dist.is_initialized() and dist.get_world_size() > 1
-    net = model
-    if ddp:
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], broadcast_buffers=False,
-                                                        gradient_as_bucket_view=True, bucket_cap_mb=64)
+    from ewvit import dist as edist
+    net = edist.wrap(model, dev)
     params = [p for p in model.parameters() if p.requires_grad]
     opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
@@ -134,34 +131,26 @@ def cpu_baseline(steps):
 
 def main():
     args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        dist.init_process_group('nccl')
+    import ewvit
+    from ewvit import dist as edist
+    rank, world, local = edist.env_ranks()
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    import ewvit
+    edist.init_from_env('nccl')                # RCCL over xGMI
     ewvit.load_library()                       # fail loudly if the HIP library is missing
     step = build_step(dev, args.frames, rank)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    edist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    edist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = edist.max_over_ranks(time.perf_counter() - t0, dev)
 
     # per-kernel timing pass (HIP events around every ewvit launch, separate from the timed loop)
     ewvit._lib.enable_timing(True)
@@ -191,7 +180,7 @@ def main():
             res['dwt_roofline'] = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'])
         res['cpu_baseline'] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_steps)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
 
 

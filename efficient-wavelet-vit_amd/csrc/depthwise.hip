@@ -215,6 +215,94 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
   }
 }
 
+// ---- bf16 weight gradient, row form.  Thread = 8 channels; it walks whole output
+// rows (row += gridDim.x * R) accumulating its 72 (tap, channel) products in fp32
+// registers over a sliding x window (one dy + 3*s x loads per output).  The R row
+// groups of a block are summed through one LDS buffer, then the block writes one
+// partial slab [C][9]; dw_bwd_weight_reduce_kernel adds the slabs in block order
+// (deterministic).
+template <int STRIDE>
+__global__ __launch_bounds__(256) void dw_wgrad_row_bf16_kernel(const bf16_t *__restrict__ x,
+                                                                const bf16_t *__restrict__ dy,
+                                                                float *__restrict__ part, DwShape s, int R) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // C8 * 72 floats (dynamic)
+  const int C8 = s.C >> 3;
+  const int r = threadIdx.x / C8, c8 = threadIdx.x % C8;
+  const bool active = r < R;
+  const int c = c8 * 8;
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  const int64_t nrows = (int64_t)s.N * s.Ho;
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  for (int64_t row = (int64_t)blockIdx.x * R + r; active && row < nrows; row += (int64_t)gridDim.x * R) {
+    const int ho = (int)(row % s.Ho);
+    const int n = (int)(row / s.Ho);
+    bool rok[3];
+    int64_t rbase[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hi = ho * STRIDE - s.pad + kh;
+      rok[kh] = hi >= 0 && hi < s.H;
+      rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
+    }
+    auto ld = [&](int kh, int col) -> uint4 {
+      if (!rok[kh] || col < 0 || col >= s.W) return zero;
+      return *reinterpret_cast<const uint4 *>(x + rbase[kh] + (int64_t)col * s.C);
+    };
+    uint4 win[3][3];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
+    const bf16_t *gr = dy + (row * s.Wo) * s.C + c;
+    for (int wo = 0; wo < s.Wo; ++wo) {
+      float g[8];
+      bf8_unpack(*reinterpret_cast<const uint4 *>(gr + (int64_t)wo * s.C), g);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          float v[8];
+          bf8_unpack(win[kw][kh], v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], v[j], acc[kh * 3 + kw][j]);
+        }
+      const int nb = (wo + 1) * STRIDE - s.pad;
+      if (STRIDE == 1) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          win[0][kh] = win[1][kh];
+          win[1][kh] = win[2][kh];
+          win[2][kh] = ld(kh, nb + 2);
+        }
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          win[0][kh] = win[2][kh];
+          win[1][kh] = ld(kh, nb + 1);
+          win[2][kh] = ld(kh, nb + 2);
+        }
+      }
+    }
+  }
+  // sum the R row groups: group 0 stores, groups 1..R-1 add in order
+  float *mine = red + c8 * 72;  // [c8][channel j][tap k] = layout of dw [C][9]
+  for (int g = 0; g < R; ++g) {
+    if (active && r == g) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) mine[j * 9 + k] = (g == 0 ? 0.f : mine[j * 9 + k]) + acc[k][j];
+    }
+    __syncthreads();
+  }
+  float *dst = part + (int64_t)blockIdx.x * s.C * 9;
+  for (int i = threadIdx.x; i < C8 * 72; i += blockDim.x) dst[i] = red[i];
+}
+
 // Weight gradient, pass 1: block = 64 channels x a slab of output pixels.
 // tid = pl*8 + cg: 8 channel groups (8 channels each) x 32 pixel lanes.
 constexpr int DWW_PIX_PER_BLOCK = 256;
@@ -366,11 +454,30 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
   return launch_status("dwconv3x3_bwd_data");
 }
 
+// weight-gradient plan: row kernel (bf16, C/8 <= 256) with `slabs` blocks, or the
+// generic pixel-slab kernel; the workspace holds one [C][9] f32 slab per block
+static void wgrad_plan(const DwShape &s, int dtype, bool *row, int *R, int64_t *slabs) {
+  const int C8 = s.C / 8;
+  *row = dtype == EWVIT_BF16 && C8 <= 256 && (s.stride == 1 || s.stride == 2);
+  if (*row) {
+    *R = 256 / C8;
+    const int64_t nrows = (int64_t)s.N * s.Ho;
+    int64_t nb = (nrows + (int64_t)(*R) * 4 - 1) / ((int64_t)(*R) * 4);   // ~4 rows per thread
+    *slabs = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  } else {
+    *R = 0;
+    const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
+    *slabs = (npix + DWW_PIX_PER_BLOCK - 1) / DWW_PIX_PER_BLOCK;
+  }
+}
+
 extern "C" int64_t ewvit_dwconv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t C, int stride,
                                                         int pad) {
   DwShape s = mk(N, H, W, C, stride, pad);
-  const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
-  const int64_t slabs = (npix + DWW_PIX_PER_BLOCK - 1) / DWW_PIX_PER_BLOCK;
+  bool row; int R; int64_t slabs, slabs_f32;
+  wgrad_plan(s, EWVIT_BF16, &row, &R, &slabs);
+  wgrad_plan(s, EWVIT_F32, &row, &R, &slabs_f32);
+  if (slabs_f32 > slabs) slabs = slabs_f32;
   return slabs * C * 9 * (int64_t)sizeof(float);
 }
 
@@ -380,15 +487,26 @@ extern "C" int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *
   EWVIT_CHECK_ARG(x && dy && dw && workspace && dtype_ok(dtype), "dwconv3x3_bwd_weight: bad args");
   DwShape s = mk(N, H, W, C, stride, pad);
   if (int rc = check_shape(s, "dwconv3x3_bwd_weight")) return rc;
+  bool row; int R; int64_t nslab;
+  wgrad_plan(s, dtype, &row, &R, &nslab);
+  const int slabs = (int)nslab;
   const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
-  const int slabs = (int)((npix + DWW_PIX_PER_BLOCK - 1) / DWW_PIX_PER_BLOCK);
-  EWVIT_CHECK_ARG(slabs <= 65535 * 16, "dwconv3x3_bwd_weight: too many pixels");
-  dim3 grid((unsigned)slabs, (unsigned)((s.C + 63) / 64));
   hipStream_t st = as_stream(stream);
-  if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_BF16>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
-  else
-    hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_F32>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
+  if (row) {
+    const size_t lds = (size_t)(s.C / 8) * 72 * sizeof(float);
+    if (s.stride == 1)
+      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<1>, dim3((unsigned)slabs), dim3(256), lds, st,
+                         (const bf16_t *)x, (const bf16_t *)dy, workspace, s, R);
+    else
+      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<2>, dim3((unsigned)slabs), dim3(256), lds, st,
+                         (const bf16_t *)x, (const bf16_t *)dy, workspace, s, R);
+  } else {
+    dim3 grid((unsigned)slabs, (unsigned)((s.C + 63) / 64));
+    if (dtype == EWVIT_BF16)
+      hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_BF16>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
+    else
+      hipLaunchKernelGGL(dw_bwd_weight_partial_kernel<EWVIT_F32>, grid, dim3(256), 0, st, x, dy, workspace, s, npix);
+  }
   if (int rc = launch_status("dwconv3x3_bwd_weight")) return rc;
   const int64_t n = (int64_t)s.C * 9;
   hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace,

@@ -1,0 +1,101 @@
+"""The N>1 path on CPU: world_size-2 `gloo` process group driving the same
+ewvit.dist helpers bench.py uses (init from torchrun env, DDP wrap, video
+sharding, max-over-ranks timing).  The model is the oracle's MWT (BatchNorm
+inside, so per-replica statistics matter) — CPU-runnable; the product's HIP path
+itself is exercised by the -m gpu tests.
+
+Checks: DDP-averaged gradients == the gradient of the global-batch loss computed
+the reference's DataParallel way (each replica's frames normalised with its own
+BatchNorm statistics, loss = mean over all outputs); buffers of rank 0 broadcast;
+timing reduced with MAX.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+WORLD = 2
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    from oracle import model as om
+    torch.manual_seed(0)
+    return om.MWT(3, 8, 2)
+
+
+def _data():
+    g = torch.Generator().manual_seed(5)
+    return torch.randn(4, 2, 3, 16, 16, generator=g)       # [videos, frames, C, H, W]
+
+
+def _worker(rank, port, q):
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from ewvit import dist as edist
+    r, w, _ = edist.init_from_env('gloo')
+    model = _model()
+    net = edist.wrap(model)
+    assert isinstance(net, torch.nn.parallel.DistributedDataParallel)
+    x = edist.shard_videos(_data(), r, w)
+    out = net(x.flatten(0, 1))
+    out.mean().backward()
+    grads = {n: p.grad.numpy().copy() for n, p in model.named_parameters()}
+    t = edist.max_over_ranks(0.5 * (r + 1))
+    # the next forward starts by broadcasting rank 0's buffers (eval: no further update)
+    net.eval()
+    with torch.no_grad():
+        net(x.flatten(0, 1))
+    q.put((r, grads, t, model.state_dict()["multiscale_fusion.1.running_mean"].numpy().copy()))
+    edist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_gloo_world2_matches_dataparallel_semantics():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        r, g, t, rm = q.get(timeout=120)
+        res[r] = (g, t, rm)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reference: one process, replicas run separately (own BN stats), loss = global mean
+    ref = _model()
+    x = _data()
+    outs = [ref(x[2 * r:2 * r + 2].flatten(0, 1)) for r in range(WORLD)]
+    torch.cat(outs).mean().backward()
+    for n, p in ref.named_parameters():
+        for r in range(WORLD):
+            torch.testing.assert_close(torch.from_numpy(res[r][0][n]), p.grad, rtol=1e-5, atol=1e-6)
+    assert res[0][1] == res[1][1] == 1.0                      # max over ranks
+    torch.testing.assert_close(torch.from_numpy(res[0][2]), torch.from_numpy(res[1][2]))  # buffers broadcast
+
+
+def test_shard_videos_covers_batch_once():
+    sys.path.insert(0, PKG)
+    from ewvit import dist as edist
+    x = torch.arange(10).view(10, 1)
+    parts = [edist.shard_videos(x, r, 4) for r in range(4)]
+    assert torch.equal(torch.cat(parts), x)

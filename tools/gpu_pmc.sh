@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM traffic per kernel: two separate rocprofv3 counter passes (FETCH_SIZE and
+# WRITE_SIZE cannot share a pass on gfx950), each with --kernel-trace only.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_$C" -o run -- \
+      python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_$C.log" 2>&1
+  rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+F=$(ls "$O"/pmc_FETCH_SIZE/*counter_collection.csv | head -1)
+W=$(ls "$O"/pmc_WRITE_SIZE/*counter_collection.csv | head -1)
+python3 "$R/tools/pmc_summary.py" "$F" "$W" > "$O/pmc_summary.json" && echo pmc summary ok
