@@ -87,15 +87,50 @@ def kernel_table(records):
     return table
 
 
+# device kernels behind each C-ABI entry point (for the PMC traffic lookup)
+ENTRY_KERNELS = {
+    'ewvit_dwt_haar_fwd': ['dwt_multilevel_kernel'],
+    'ewvit_hf_upsample': ['hf_upsample_kernel'],
+    'ewvit_gemm': ['gemm_kernel', 'splitk_reduce_kernel'],
+    'ewvit_dwconv3x3_fwd': ['dw_row_bf16_kernel<1, false>', 'dw_row_bf16_kernel<2, false>', 'dw_fwd_kernel'],
+    'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
+    'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
+                                   'dw_bwd_weight_reduce_kernel'],
+    'ewvit_conv3x3_fwd': ['conv3x3_fwd_kernel'],
+    'ewvit_conv3x3_bwd_data': ['conv3x3_bwd_data_kernel'],
+    'ewvit_conv3x3_bwd_weight': ['conv3x3_wgrad_kernel', 'conv3x3_wgrad_reduce_kernel'],
+}
+PMC_FILE = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+
+
+def pmc_traffic(entry, per_step):
+    """HBM bytes per launch of `entry` from the committed rocprofv3 PMC passes
+    (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    if not os.path.exists(PMC_FILE) or entry not in ENTRY_KERNELS:
+        return None
+    data = json.load(open(PMC_FILE))
+    steps = data.get('_steps_executed')
+    if not steps or not per_step:
+        return None
+    tot = 0.0
+    for k, v in data.items():
+        if k.startswith('_') or not any(p in k for p in ENTRY_KERNELS[entry]):
+            continue
+        tot += v['hbm_bytes_per_launch'] * v['dispatches']
+    return round(tot / (per_step * steps), 1) if tot else None
+
+
 def roofline_for(name, row):
-    if name == 'ewvit_gemm':
+    traffic = pmc_traffic(name, row.get('per_step'))
+    if name in ('ewvit_gemm', 'ewvit_conv3x3_fwd', 'ewvit_conv3x3_bwd_data', 'ewvit_conv3x3_bwd_weight'):
         ach = row['TFLOP/s']
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': BF16_PEAK_TFS,
-                'unit': 'TFLOP/s', 'frac': round(ach / BF16_PEAK_TFS, 5), 'traffic': None,
-                'avg_us': round(row['avg_us'], 3), 'work_per_launch': row['flops_per_launch']}
+                'unit': 'TFLOP/s', 'frac': round(ach / BF16_PEAK_TFS, 5), 'traffic': traffic,
+                'avg_us': round(row['avg_us'], 3), 'work_per_launch': row['flops_per_launch'],
+                'algorithmic_bytes_per_launch': row['bytes_per_launch']}
     ach = row['GB/s']
     return {'kernel': name, 'bound': 'hbm', 'achieved': round(ach, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(ach / HBM_PEAK_GBS, 5), 'traffic': None, 'avg_us': round(row['avg_us'], 3),
+            'frac': round(ach / HBM_PEAK_GBS, 5), 'traffic': traffic, 'avg_us': round(row['avg_us'], 3),
             'work_per_launch': row['bytes_per_launch']}
 
 

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
 // partial slab [C][9]; dw_bwd_weight_reduce_kernel adds the slabs in block order
 // (deterministic).
 template <int STRIDE>
-__global__ __launch_bounds__(256) void dw_wgrad_row_bf16_kernel(const bf16_t *__restrict__ x,
+__global__ __launch_bounds__(512) void dw_wgrad_row_bf16_kernel(const bf16_t *__restrict__ x,
                                                                 const bf16_t *__restrict__ dy,
                                                                 float *__restrict__ part, DwShape s, int R) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // C8 * 72 floats (dynamic)
@@ -373,14 +373,32 @@ __global__ __launch_bounds__(256) void dw_bwd_weight_partial_kernel(const void *
   }
 }
 
+// Sum the per-block slabs: block = 64 outputs x 4 slab groups (one wave each,
+// every wave reading 256 contiguous bytes per slab, 4 loads in flight), then the
+// 4 groups are added through LDS in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void dw_bwd_weight_reduce_kernel(const float *__restrict__ part,
                                                                    float *__restrict__ dw, int64_t n,
                                                                    int slabs, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int k = 0; k < slabs; ++k) s += part[(int64_t)k * n + i];
-  dw[i] = accumulate ? dw[i] + s : s;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < n) {
+    int k = g;
+    for (; k + 12 < slabs; k += 16) {
+      s0 += part[(int64_t)k * n + i];
+      s1 += part[(int64_t)(k + 4) * n + i];
+      s2 += part[(int64_t)(k + 8) * n + i];
+      s3 += part[(int64_t)(k + 12) * n + i];
+    }
+    for (; k < slabs; k += 4) s0 += part[(int64_t)k * n + i];
+  }
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && i < n) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    dw[i] = accumulate ? dw[i] + t : t;
+  }
 }
 
 static int check_shape(const DwShape &s, const char *nm) {
@@ -460,9 +478,9 @@ static void wgrad_plan(const DwShape &s, int dtype, bool *row, int *R, int64_t *
   const int C8 = s.C / 8;
   *row = dtype == EWVIT_BF16 && C8 <= 256 && (s.stride == 1 || s.stride == 2);
   if (*row) {
-    *R = 256 / C8;
+    *R = 512 / C8;
     const int64_t nrows = (int64_t)s.N * s.Ho;
-    int64_t nb = (nrows + (int64_t)(*R) * 4 - 1) / ((int64_t)(*R) * 4);   // ~4 rows per thread
+    int64_t nb = (nrows + (int64_t)(*R) - 1) / (int64_t)(*R);   // one row per thread, 512-thread blocks
     *slabs = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   } else {
     *R = 0;
@@ -495,10 +513,10 @@ extern "C" int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *
   if (row) {
     const size_t lds = (size_t)(s.C / 8) * 72 * sizeof(float);
     if (s.stride == 1)
-      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<1>, dim3((unsigned)slabs), dim3(256), lds, st,
+      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<1>, dim3((unsigned)slabs), dim3(512), lds, st,
                          (const bf16_t *)x, (const bf16_t *)dy, workspace, s, R);
     else
-      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<2>, dim3((unsigned)slabs), dim3(256), lds, st,
+      hipLaunchKernelGGL(dw_wgrad_row_bf16_kernel<2>, dim3((unsigned)slabs), dim3(512), lds, st,
                          (const bf16_t *)x, (const bf16_t *)dy, workspace, s, R);
   } else {
     dim3 grid((unsigned)slabs, (unsigned)((s.C + 63) / 64));
@@ -509,7 +527,7 @@ extern "C" int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *
   }
   if (int rc = launch_status("dwconv3x3_bwd_weight")) return rc;
   const int64_t n = (int64_t)s.C * 9;
-  hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace,
+  hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace,
                      dw, n, slabs, accumulate);
   return launch_status("dwconv3x3_bwd_weight reduce");
 }

@@ -13,4 +13,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 F=$(ls "$O"/pmc_FETCH_SIZE/*counter_collection.csv | head -1)
 W=$(ls "$O"/pmc_WRITE_SIZE/*counter_collection.csv | head -1)
-python3 "$R/tools/pmc_summary.py" "$F" "$W" > "$O/pmc_summary.json" && echo pmc summary ok
+python3 "$R/tools/pmc_summary.py" "$F" "$W" --steps 6 > "$O/pmc_summary.json" && echo pmc summary ok

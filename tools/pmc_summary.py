@@ -23,10 +23,17 @@ def load(path, counter):
 
 
 def main():
-    fetch = load(sys.argv[1], 'FETCH_SIZE')
-    write = load(sys.argv[2], 'WRITE_SIZE')
-    pat = re.compile(sys.argv[3]) if len(sys.argv) > 3 else None
-    out = {}
+    args = sys.argv[1:]
+    steps = None
+    if '--steps' in args:
+        i = args.index('--steps')
+        steps = int(args[i + 1])
+        del args[i:i + 2]
+    fetch = load(args[0], 'FETCH_SIZE')
+    write = load(args[1], 'WRITE_SIZE')
+    pat = re.compile(args[2]) if len(args) > 2 else None
+    out = {'_steps_executed': steps,
+           '_source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate); FETCH_SIZE x2 (gfx950 correction)'}
     for k in sorted(set(fetch) | set(write)):
         if pat and not pat.search(k):
             continue
