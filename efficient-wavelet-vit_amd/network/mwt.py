@@ -45,9 +45,31 @@ class DWTForward(nn.Module):
         return ewvit.dwt_haar(x, self.J, out_dtype=odt)
 
 
-def _cbr(cin, cout, stride=1):
-    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout),
+class Conv3x3(nn.Conv2d):
+    """nn.Conv2d(k=3, pad=1) on the ewvit MFMA implicit-GEMM kernels (csrc/conv.hip)
+    for channels-last inputs whose channel count is a multiple of 8 (extra input
+    channels beyond in_channels must be zero padding); other inputs (the 3-channel
+    per-level path of `wavelet_transform`) go to the library conv."""
+
+    def forward(self, x):
+        if x.is_cuda and x.shape[1] % 8 == 0 and x.shape[1] >= self.in_channels and self.out_channels % 8 == 0:
+            return ewvit.conv3x3(x, self.weight, self.bias, self.stride[0])
+        return super().forward(x[:, :self.in_channels])
+
+
+def _cbr(cin, cout, stride=1, conv=Conv3x3):
+    return nn.Sequential(conv(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout),
                          nn.ReLU(inplace=True))
+
+
+def bn_padded(x, bns, pad, training):
+    """bn_groups over the first channels of x and an identity-like BN (weight 1,
+    bias 0) over `pad` trailing all-zero channels, which therefore stay zero."""
+    dev = x.device
+    extra = nn.BatchNorm2d(pad).to(dev)
+    extra.momentum = bns[0].momentum
+    extra.eps = bns[0].eps
+    return bn_groups(x, list(bns) + [extra], training)
 
 
 def bn_groups(x, bns, training):
@@ -87,11 +109,11 @@ class MWT(nn.Module):
         self.dwt = DWTForward(J=1, wave='haar', mode='zero')                  # mwt.py:20
         self.freq_conv = _cbr(dama_dim, dama_dim, stride=2)                    # mwt.py:23-36
         self.freq_pool = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2),  # mwt.py:38-44
-                                       nn.Conv2d(dama_dim, dama_dim, 3, padding=1, stride=2),
+                                       Conv3x3(dama_dim, dama_dim, 3, padding=1, stride=2),
                                        nn.BatchNorm2d(dama_dim), nn.ReLU(inplace=True),
                                        nn.AdaptiveAvgPool2d(1))
         self.hf_conv = nn.ModuleDict({                                         # mwt.py:47-65
-            'seperate': nn.ModuleList([_cbr(in_channels, 6 * in_channels) for _ in range(3)]),
+            'seperate': nn.ModuleList([_cbr(in_channels, 6 * in_channels, conv=nn.Conv2d) for _ in range(3)]),
             'fusion': _cbr(18 * in_channels, dama_dim)})
         self.multiscale_fusion = _cbr(levels * dama_dim, dama_dim)             # mwt.py:68-72
 
@@ -140,10 +162,19 @@ class MWT(nn.Module):
         # exact zeros): MIOpen's grouped weight-gradient kernel took ~0.3 s here.
         w = torch.cat([F.pad(sep[i][0].weight, (0, 0, 0, 0, i * C, (2 - i) * C)) for i in range(3)])
         b = torch.cat([sep[i][0].bias for i in range(3)])
+        # the fusion conv's MFMA kernel wants 8-aligned channels: emit the 18C
+        # seperate channels zero-padded to a multiple of 8 (zero weight rows and
+        # bias; an identity BN keeps them exactly 0 through BN + ReLU)
+        c18 = 18 * C
+        pad = (-c18) % 8
+        if pad:
+            w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, pad))
+            b = F.pad(b, (0, pad))
         y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
         bns = [sep[i][1] for i in range(3)]
-        y = torch.cat([bn_groups(y[l * B:(l + 1) * B], bns, self.training) for l in range(Lv)]) if Lv > 1 \
-            else bn_groups(y, bns, self.training)
+        norm = (lambda t: bn_padded(t, bns, pad, self.training)) if pad else \
+            (lambda t: bn_groups(t, bns, self.training))
+        y = torch.cat([norm(y[l * B:(l + 1) * B]) for l in range(Lv)]) if Lv > 1 else norm(y)
         y = F.relu_(y)
         fus = self.hf_conv['fusion']
         z = fus[0](y)

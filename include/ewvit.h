@@ -157,6 +157,32 @@ int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int acc
                                int64_t H, int64_t W, int64_t C, int stride, int pad, int dtype,
                                float *workspace, void *stream);
 
+/* ------------------------------------------------ 3x3 conv, implicit GEMM ---
+ * Conv2d(k=3, pad=1, stride 1|2, bias) of the MWT conv stack: hf_conv['fusion']
+ * (mwt.py:60-64), multiscale_fusion (mwt.py:68-72), freq_conv (mwt.py:23-36),
+ * freq_pool's conv (mwt.py:38-44).  bf16 MFMA, fp32 accumulate, channels-last:
+ *   x [N, H, W, Cin], y [N, Ho, Wo, Cout] (bf16); Cin, Cout % 8 == 0;
+ *   Ho = (H-1)/stride + 1.  Weights are packed once per step from the fp32
+ *   master [Cout][Cin][3][3] by ewvit_conv3x3_pack_weight:
+ *   transposed=0 -> [Cout][9][Cin_pad] (fwd), 1 -> [Cin_pad][9][Cout] (bwd_data);
+ *   input channels ci >= Cin are zero-filled up to Cin_pad.
+ */
+int ewvit_conv3x3_pack_weight(const float *w, void *wp, int64_t Cout, int64_t Cin, int64_t Cin_pad,
+                              int transposed, void *stream);
+/* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
+int ewvit_conv3x3_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                      int64_t W, int64_t Cin, int64_t Cout, int stride, void *stream);
+/* dx [N, H, W, Cin] from dy [N, Ho, Wo, Cout] and the transposed pack. */
+int ewvit_conv3x3_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
+                           int64_t Cin, int64_t Cout, int stride, void *stream);
+/* bytes of f32 split-K workspace for ewvit_conv3x3_bwd_weight. */
+int64_t ewvit_conv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                           int stride);
+/* dw [Cout][Cin][3][3] f32 (= or +=) ; deterministic split-K + reduction. */
+int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
+                             int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
+                             float *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
