@@ -68,14 +68,15 @@ __device__ __forceinline__ bool src_pixel(const FwdArgs &a, int oh, int ow, int 
   return sh >= 0 && sh < a.srcH && sw >= 0 && sw < a.srcW;
 }
 
-template <bool DGRAD>
+template <bool DGRAD, int BN_>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
+  constexpr int WN = BN_ / 2, J = WN / 16;  // per-wave columns, 16-wide MFMA tiles
   __shared__ __attribute__((aligned(16))) bf16_t As[2][CBM][CLD];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][CBN][CLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN_][CLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.x * CBM;
-  const int n0 = blockIdx.y * CBN;
+  const int n0 = blockIdx.y * BN_;
   const int K = 9 * a.KC;
   const int nk = (K + CBK - 1) / CBK;
 
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
       ra[u] = va;
       const int n = n0 + arow[u];  // B rows use the same (row, chunk) split
       uint4 vb = make_uint4(0u, 0u, 0u, 0u);
-      if (n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
+      if ((BN_ == 128 || u == 0) && n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
       rb[u] = vb;
     }
   };
@@ -119,15 +120,15 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       *reinterpret_cast<uint4 *>(&As[buf][arow[u]][ach[u]]) = ra[u];
-      *reinterpret_cast<uint4 *>(&Bs[buf][arow[u]][ach[u]]) = rb[u];
+      if (BN_ == 128 || u == 0) *reinterpret_cast<uint4 *>(&Bs[buf][arow[u]][ach[u]]) = rb[u];
     }
   };
 
-  cf32x4 acc[4][4];
+  cf32x4 acc[4][J];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
   load_tile(0);
   store_tile(0);
@@ -137,22 +138,22 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) load_tile(kt + 1);
-    cbf16x8 af[4], bfr[4];
+    cbf16x8 af[4], bfr[J];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const cbf16x8 *>(&As[cur][wm * 64 + i * 16 + fr][fk]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const cbf16x8 *>(&Bs[cur][wn * 64 + j * 16 + fr][fk]);
+    for (int j = 0; j < J; ++j) bfr[j] = *reinterpret_cast<const cbf16x8 *>(&Bs[cur][wn * WN + j * 16 + fr][fk]);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (more) store_tile(cur ^ 1);
     __syncthreads();
   }
   // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+  for (int j = 0; j < J; ++j) {
+    const int col = n0 + wn * WN + j * 16 + (lane & 15);
     if (col >= a.Ncol) continue;
     const float b = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
@@ -175,6 +176,7 @@ struct WgradArgs {
   const bf16_t *x;       // [N, H, W, Cin]
   const bf16_t *dy;      // [N, Ho, Wo, Cout]
   float *part;           // [splits][Cout][9*Cin]
+  float *dbias_part;     // [splits][Cout] partial bias gradients (sum of dy), or null
   ConvGeom g;
   int64_t M;             // N*Ho*Wo
   int64_t mper;          // pixels per split (multiple of 32)
@@ -215,6 +217,24 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
     btap[u] = bok[u] ? np / a.g.Cin : 0;
     bci[u] = bok[u] ? np % a.g.Cin : 0;
   }
+  const int bkh = 0, bkw = 0;
+  (void)bkh; (void)bkw;
+  int tkh[2], tkw[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) { tkh[u] = btap[u] / 3; tkw[u] = btap[u] % 3; }
+  // pixel coordinates of each staged row, advanced by CBK pixels per K-tile
+  // (no 64-bit div/mod in the loop)
+  int pn[2], poh[2], pow_[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t m = mbeg + vrow[u];
+    pow_[u] = (int)(m % a.g.Wo);
+    const int64_t t = m / a.g.Wo;
+    poh[u] = (int)(t % a.g.Ho);
+    pn[u] = (int)(t / a.g.Ho);
+  }
+  const bool do_bias = a.dbias_part != nullptr && blockIdx.x == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -224,17 +244,29 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
         const int co = co0 + vch[u] * 8;
         if (co < a.g.Cout) va = *reinterpret_cast<const uint4 *>(a.dy + m * a.g.Cout + co);
         if (bok[u]) {
-          const int ow = (int)(m % a.g.Wo);
-          const int64_t t = m / a.g.Wo;
-          const int oh = (int)(t % a.g.Ho);
-          const int n = (int)(t / a.g.Ho);
-          const int ih = oh * a.g.stride - 1 + btap[u] / 3, iw = ow * a.g.stride - 1 + btap[u] % 3;
+          const int ih = poh[u] * a.g.stride - 1 + tkh[u], iw = pow_[u] * a.g.stride - 1 + tkw[u];
           if (ih >= 0 && ih < a.g.H && iw >= 0 && iw < a.g.W)
-            vb = *reinterpret_cast<const uint4 *>(a.x + (((int64_t)n * a.g.H + ih) * a.g.W + iw) * a.g.Cin + bci[u]);
+            vb = *reinterpret_cast<const uint4 *>(a.x + (((int64_t)pn[u] * a.g.H + ih) * a.g.W + iw) * a.g.Cin + bci[u]);
         }
       }
       ra[u] = va;
       rb[u] = vb;
+      pow_[u] += CBK;
+      while (pow_[u] >= a.g.Wo) {
+        pow_[u] -= a.g.Wo;
+        if (++poh[u] == a.g.Ho) { poh[u] = 0; ++pn[u]; }
+      }
+    }
+  };
+  auto bias_acc = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const unsigned wv[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bsum[2 * j] += __uint_as_float(wv[j] << 16);
+        bsum[2 * j + 1] += __uint_as_float(wv[j] & 0xffff0000u);
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -262,6 +294,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
 
   if (nk > 0) {
     load_tile(0);
+    if (do_bias) bias_acc();
     store_tile(0);
   }
   __syncthreads();
@@ -269,7 +302,10 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
-    if (more) load_tile(kt + 1);
+    if (more) {
+      load_tile(kt + 1);
+      if (do_bias) bias_acc();
+    }
     cbf16x8 af[4], bfr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -292,6 +328,27 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
     if (more) store_tile(cur ^ 1);
     __syncthreads();
   }
+  if (do_bias) {
+    // threads with equal (tid & 15) hold the same 8 channels: lanes l, l^16, l^32, l^48
+    // in a wave, then the 4 waves through LDS (the staging buffers are free now)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsum[j] += __shfl_xor(bsum[j], 16, 64);
+      bsum[j] += __shfl_xor(bsum[j], 32, 64);
+    }
+    float *red = reinterpret_cast<float *>(&smem[0][0][0]);  // [4 waves][16 chunks][8]
+    if (lane < 16)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(w * 16 + lane) * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < 128) {
+      const int ch = tid >> 3, j = tid & 7;
+      const int co = co0 + ch * 8 + j;
+      const float s = (red[(0 * 16 + ch) * 8 + j] + red[(1 * 16 + ch) * 8 + j]) +
+                      (red[(2 * 16 + ch) * 8 + j] + red[(3 * 16 + ch) * 8 + j]);
+      if (co < a.g.Cout) a.dbias_part[(int64_t)blockIdx.z * a.g.Cout + co] = s;
+    }
+  }
   float *dst = a.part + (int64_t)blockIdx.z * a.g.Cout * NP;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -309,9 +366,16 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
 
 // dW[co][ci][kh][kw] (= or +=) sum over splits of part[s][co][tap*Cin + ci]
 __global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
-                                                                  int Cout, int Cin, int splits, int accumulate) {
+                                                                  int Cout, int Cin, int splits, int accumulate,
+                                                                  const float *__restrict__ dbias_part,
+                                                                  float *__restrict__ dbias) {
   const int64_t NP = 9 * (int64_t)Cin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in part layout
+  if (dbias && i < Cout) {
+    float sb = 0.f;
+    for (int k = 0; k < splits; ++k) sb += dbias_part[(int64_t)k * Cout + i];
+    dbias[i] = accumulate ? dbias[i] + sb : sb;
+  }
   if (i >= (int64_t)Cout * NP) return;
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[(int64_t)k * Cout * NP + i];
@@ -341,6 +405,18 @@ __global__ __launch_bounds__(256) void conv3x3_pack_kernel(const float *__restri
   }
   const float v = ci < Cin ? w[((int64_t)co * Cin + ci) * 9 + tap] : 0.f;
   wp[i] = f2bf(v);
+}
+
+// Ncol <= 64 (the fusion conv's input gradient: 56 channels) uses the 128x64 tile
+template <bool DGRAD>
+static void launch_fwd(const FwdArgs &a, hipStream_t s) {
+  if (a.Ncol <= 64) {
+    dim3 grid((unsigned)((a.M + CBM - 1) / CBM), 1);
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<DGRAD, 64>), grid, dim3(256), 0, s, a);
+  } else {
+    dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<DGRAD, 128>), grid, dim3(256), 0, s, a);
+  }
 }
 
 static int check_geom(const ConvGeom &g, const char *nm) {
@@ -381,8 +457,7 @@ extern "C" int ewvit_conv3x3_fwd(const void *x, const void *wp, const float *bia
   a.src = (const bf16_t *)x; a.wp = (const bf16_t *)wp; a.bias = bias; a.out = (bf16_t *)y; a.g = g;
   a.M = (int64_t)g.N * g.Ho * g.Wo; a.Ncol = g.Cout; a.KC = g.Cin;
   a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
-  dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
-  hipLaunchKernelGGL(conv3x3_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), a);
+  launch_fwd<false>(a, as_stream(stream));
   return launch_status("conv3x3_fwd");
 }
 
@@ -395,8 +470,7 @@ extern "C" int ewvit_conv3x3_bwd_data(const void *dy, const void *wp_t, void *dx
   a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx; a.g = g;
   a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
-  dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
-  hipLaunchKernelGGL(conv3x3_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), a);
+  launch_fwd<true>(a, as_stream(stream));
   return launch_status("conv3x3_bwd_data");
 }
 
@@ -413,17 +487,18 @@ static int64_t wgrad_splits(const ConvGeom &g) {
 extern "C" int64_t ewvit_conv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                                       int stride) {
   ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
-  return wgrad_splits(g) * Cout * 9 * Cin * (int64_t)sizeof(float);
+  return wgrad_splits(g) * Cout * (9 * Cin + 1) * (int64_t)sizeof(float);
 }
 
-extern "C" int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
-                                        int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
+extern "C" int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
+                                        int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
                                         float *workspace, void *stream) {
   EWVIT_CHECK_ARG(x && dy && dw && workspace, "conv3x3_bwd_weight: null pointer");
   ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
   if (int rc = check_geom(g, "conv3x3_bwd_weight")) return rc;
   WgradArgs a;
   a.x = (const bf16_t *)x; a.dy = (const bf16_t *)dy; a.part = workspace; a.g = g;
+  a.dbias_part = dbias ? workspace + wgrad_splits(g) * g.Cout * 9 * (int64_t)g.Cin : nullptr;
   a.M = (int64_t)g.N * g.Ho * g.Wo;
   const int64_t splits = wgrad_splits(g);
   int64_t mper = (a.M + splits - 1) / splits;
@@ -436,6 +511,6 @@ extern "C" int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw
   if (int rc = launch_status("conv3x3_bwd_weight")) return rc;
   const int64_t n = (int64_t)g.Cout * 9 * g.Cin;
   hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, workspace, dw,
-                     g.Cout, g.Cin, sp, accumulate);
+                     g.Cout, g.Cin, sp, accumulate, a.dbias_part, dbias);
   return launch_status("conv3x3_bwd_weight reduce");
 }

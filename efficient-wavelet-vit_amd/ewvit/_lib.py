@@ -36,7 +36,7 @@ SIGNATURES = {
     'ewvit_conv3x3_pack_weight': [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv3x3_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
-    'ewvit_conv3x3_bwd_weight': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
+    'ewvit_conv3x3_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
 }

@@ -10,7 +10,7 @@ gradient.
 import torch
 
 from . import _lib as L
-from .ops import colsum
+
 
 
 def _pack(weight, cin_pad, transposed):
@@ -59,17 +59,18 @@ class Conv3x3Fn(torch.autograd.Function):
                    L.stream(dx), work=work)
             if xdt != torch.bfloat16:
                 dx = dx.to(xdt)
-        if ctx.needs_input_grad[1]:
+        want_b = has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_b:
             wsb = L.load().ewvit_conv3x3_bwd_weight_workspace(N, H, W, Cx, Cout, stride)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
             dwf = torch.empty((Cout, Cx, 3, 3), dtype=torch.float32, device=xc.device)
+            dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device) if want_b else None
             work = {'flops': 2.0 * N * Ho * Wo * Cout * 9 * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
-            L.call('ewvit_conv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), 0, N, H, W, Cx, Cout, stride,
-                   L.ptr(ws), L.stream(dwf), work=work)
-            dw = dwf if Cx == Cin else dwf[:, :Cin].contiguous()
-        if has_bias and ctx.needs_input_grad[2]:
-            db = colsum(dyc.permute(0, 2, 3, 1).reshape(-1, Cout), torch.empty(Cout, dtype=torch.float32,
-                                                                               device=dy.device))
+            L.call('ewvit_conv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
+                   Cout, stride, L.ptr(ws), L.stream(dwf), work=work)
+            if ctx.needs_input_grad[1]:
+                dw = dwf if Cx == Cin else dwf[:, :Cin].contiguous()
+            db = dbf
         return dx, dw, db, None
 
 

@@ -178,9 +178,11 @@ int ewvit_conv3x3_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N
 /* bytes of f32 split-K workspace for ewvit_conv3x3_bwd_weight. */
 int64_t ewvit_conv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                            int stride);
-/* dw [Cout][Cin][3][3] f32 (= or +=) ; deterministic split-K + reduction. */
-int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
-                             int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
+/* dw [Cout][Cin][3][3] f32 and, when dbias != NULL, the bias gradient dbias[Cout] =
+ * sum of dy over pixels (fused: read from the dy tiles already staged), both
+ * (= or +=) ; deterministic split-K + reduction. */
+int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
+                             int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
                              float *workspace, void *stream);
 
 #ifdef __cplusplus

@@ -166,7 +166,7 @@ def test_mwt_wavelet_transform_api_and_patched_path(golden):
         m.wavelet_transform = spy
         slow = m(x)
     assert len(calls) == 2
-    check(slow, fast, 1e-3)
+    check(slow, fast, 2e-2)  # per-level path: library convs in fp32 vs the bf16 MFMA path
 
 
 def test_dwt_module_api():
