@@ -33,6 +33,9 @@ SIGNATURES = {
     'ewvit_dwconv3x3_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     'ewvit_dwconv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     'ewvit_dwconv3x3_bwd_weight': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp],
+    'ewvit_bn_fwd': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _f32, _f32, _i32, _vp, _vp, _i32, _vp,
+                     _vp],
+    'ewvit_bn_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_conv3x3_pack_weight': [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv3x3_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
@@ -45,6 +48,7 @@ SIGNATURES = {
 QUERIES = {
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32]),
+    'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
 }
 
 _lib = None

@@ -1,0 +1,82 @@
+"""BatchNorm2d fused with its activation on the ewvit kernels (csrc/batchnorm.hip).
+
+Replaces ``nn.BatchNorm2d`` + ``nn.ReLU`` (MWT conv stack, network/mwt.py:23-72)
+and ``nn.BatchNorm2d`` + ``nn.SiLU`` (EfficientNetV2-S Conv2dNormActivation) on
+channels-last tensors; training mode uses batch statistics and updates the
+module's running statistics in place like ``F.batch_norm``.  ``groups`` > 1
+normalises consecutive equal batch slices with their own statistics (one
+launch for the MWT's per-level calls of its shared BatchNorms).
+"""
+import torch
+
+from . import _lib as L
+
+ACT = {None: 0, 'none': 0, 'relu': 1, 'silu': 2}
+
+
+def _rows(x):
+    """[N, C, H, W] channels-last (or [N, C]) -> contiguous NHWC storage, M rows."""
+    C = x.shape[1]
+    xc = x.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else x.contiguous()
+    return xc, xc.numel() // C, C
+
+
+class BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups):
+        L.require_gpu(x)
+        xc, M, C = _rows(x)
+        if M % groups:
+            raise ValueError(f'batch_norm_act: {M} rows not divisible into {groups} groups')
+        y = torch.empty_like(xc)
+        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=x.device)
+        mean = torch.empty(groups, C, dtype=torch.float32, device=x.device) if training else None
+        invstd = torch.empty_like(mean) if training else None
+        L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+               L.ptr(running_mean), L.ptr(running_var), int(training), float(momentum), float(eps), act,
+               L.ptr(mean), L.ptr(invstd), groups, L.ptr(ws), L.stream(y),
+               work={'bytes': (2 + int(training)) * xc.numel() * xc.element_size()})
+        if training:
+            ctx.save_for_backward(xc, weight, bias, mean, invstd)
+        ctx.cfg = (training, act, M, C, groups)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        training, act, M, C, groups = ctx.cfg
+        if not training:
+            raise RuntimeError('ewvit BatchNorm: backward through eval-mode statistics is not implemented')
+        xc, weight, bias, mean, invstd = ctx.saved_tensors
+        dyc = dy.to(xc.dtype)
+        dyc = dyc.contiguous(memory_format=torch.channels_last) if dyc.dim() == 4 else dyc.contiguous()
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
+        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=dy.device)
+        L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+               L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), 0, groups, L.ptr(ws), L.stream(dx),
+               work={'bytes': 5 * xc.numel() * xc.element_size()})
+        return dx, dg, db, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, bn, act=None, training=None, groups=1):
+    """Apply BatchNorm module `bn` (its parameters, buffers, eps, momentum) and the
+    activation to x in one fused pass; updates bn's running stats and counter
+    (once per statistics group, as `groups` separate module calls would)."""
+    training = bn.training if training is None else training
+    if bn.momentum is None:
+        raise NotImplementedError('cumulative-average BatchNorm (momentum=None) is not used by the model')
+    if training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(groups)
+    return batch_norm_act_params(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, training,
+                                 bn.momentum, bn.eps, act, groups)
+
+
+def batch_norm_act_params(x, weight, bias, running_mean, running_var, training, momentum, eps, act=None,
+                          groups=1):
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    if not training:
+        groups = 1
+    return BatchNormActFn.apply(x, weight, bias, running_mean, running_var, bool(training), momentum, eps,
+                                ACT[act], int(groups))

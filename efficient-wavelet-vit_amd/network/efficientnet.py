@@ -42,6 +42,9 @@ class DepthwiseConv2d(nn.Conv2d):
 
 
 class ConvBNAct(nn.Sequential):
+    """conv -> BatchNorm2d(eps 1e-3) [-> SiLU]; BN and SiLU run as ONE fused ewvit
+    pass (csrc/batchnorm.hip) over the channels-last conv output."""
+
     def __init__(self, cin, cout, k, stride=1, groups=1, act=True):
         conv = DepthwiseConv2d if (groups == cin == cout and groups > 1 and k == 3) else nn.Conv2d
         mods = [conv(cin, cout, k, stride, (k - 1) // 2, groups=groups, bias=False),
@@ -49,6 +52,14 @@ class ConvBNAct(nn.Sequential):
         if act:
             mods.append(nn.SiLU(inplace=True))
         super().__init__(*mods)
+
+    def forward(self, x):
+        y = self[0](x)
+        bn = self[1]
+        if y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks):
+            return ewvit.batch_norm_act(y, bn, 'silu' if len(self) > 2 else None)
+        y = bn(y)
+        return self[2](y) if len(self) > 2 else y
 
 
 class SqueezeExcitation(nn.Module):

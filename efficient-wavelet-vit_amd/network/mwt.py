@@ -57,39 +57,59 @@ class Conv3x3(nn.Conv2d):
         return super().forward(x[:, :self.in_channels])
 
 
+def _fusable(bn, y):
+    return y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks)
+
+
+class CBR(nn.Sequential):
+    """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass."""
+
+    def forward(self, x):
+        y = self[0](x)
+        if _fusable(self[1], y):
+            return ewvit.batch_norm_act(y, self[1], 'relu')
+        return self[2](self[1](y))
+
+
+class FreqPool(nn.Sequential):
+    """MaxPool2d(2) -> Conv3x3 s2 -> BatchNorm2d -> ReLU -> AdaptiveAvgPool2d(1) (mwt.py:38-44)."""
+
+    def forward(self, x):
+        y = self[1](self[0](x))
+        y = ewvit.batch_norm_act(y, self[2], 'relu') if _fusable(self[2], y) else self[3](self[2](y))
+        return self[4](y)
+
+
 def _cbr(cin, cout, stride=1, conv=Conv3x3):
-    return nn.Sequential(conv(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout),
-                         nn.ReLU(inplace=True))
+    return CBR(conv(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
 
 
-def bn_padded(x, bns, pad, training):
-    """bn_groups over the first channels of x and an identity-like BN (weight 1,
-    bias 0) over `pad` trailing all-zero channels, which therefore stay zero."""
+def bn_relu_groups(x, bns, training, pad=0, levels=1):
+    """BatchNorm modules `bns` over consecutive channel groups of x (+ `pad` trailing
+    all-zero channels normalised by an identity BN, so they stay 0) and ReLU, in ONE
+    fused launch, with separate statistics for each of `levels` batch slices.
+    Running stats / num_batches_tracked end exactly as calling every module on its
+    slice, level after level, would leave them."""
     dev = x.device
-    extra = nn.BatchNorm2d(pad).to(dev)
-    extra.momentum = bns[0].momentum
-    extra.eps = bns[0].eps
-    return bn_groups(x, list(bns) + [extra], training)
-
-
-def bn_groups(x, bns, training):
-    """Apply BatchNorm modules `bns` to consecutive channel groups of x with ONE
-    batch_norm launch; running stats / num_batches_tracked are updated exactly as
-    calling each module on its slice would (same momentum, same batch stats)."""
     w = torch.cat([b.weight for b in bns])
     bi = torch.cat([b.bias for b in bns])
     rm = torch.cat([b.running_mean for b in bns])
     rv = torch.cat([b.running_var for b in bns])
+    if pad:
+        w = torch.cat([w, torch.ones(pad, device=dev)])
+        bi = torch.cat([bi, torch.zeros(pad, device=dev)])
+        rm = torch.cat([rm, torch.zeros(pad, device=dev)])
+        rv = torch.cat([rv, torch.ones(pad, device=dev)])
     b0 = bns[0]
-    use_batch = training or rm is None
-    y = F.batch_norm(x, rm, rv, w, bi, use_batch, b0.momentum, b0.eps)
+    y = ewvit.batch_norm_act_params(x, w, bi, rm, rv, training, b0.momentum, b0.eps, 'relu',
+                                    levels if training else 1)
     if training:
         off = 0
         for b in bns:
             n = b.num_features
             b.running_mean.copy_(rm[off:off + n])
             b.running_var.copy_(rv[off:off + n])
-            b.num_batches_tracked.add_(1)
+            b.num_batches_tracked.add_(levels)
             off += n
     return y
 
@@ -108,10 +128,10 @@ class MWT(nn.Module):
         self.levels = levels
         self.dwt = DWTForward(J=1, wave='haar', mode='zero')                  # mwt.py:20
         self.freq_conv = _cbr(dama_dim, dama_dim, stride=2)                    # mwt.py:23-36
-        self.freq_pool = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2),  # mwt.py:38-44
-                                       Conv3x3(dama_dim, dama_dim, 3, padding=1, stride=2),
-                                       nn.BatchNorm2d(dama_dim), nn.ReLU(inplace=True),
-                                       nn.AdaptiveAvgPool2d(1))
+        self.freq_pool = FreqPool(nn.MaxPool2d(kernel_size=2, stride=2),       # mwt.py:38-44
+                                  Conv3x3(dama_dim, dama_dim, 3, padding=1, stride=2),
+                                  nn.BatchNorm2d(dama_dim), nn.ReLU(inplace=True),
+                                  nn.AdaptiveAvgPool2d(1))
         self.hf_conv = nn.ModuleDict({                                         # mwt.py:47-65
             'seperate': nn.ModuleList([_cbr(in_channels, 6 * in_channels, conv=nn.Conv2d) for _ in range(3)]),
             'fusion': _cbr(18 * in_channels, dama_dim)})
@@ -171,12 +191,10 @@ class MWT(nn.Module):
             w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, pad))
             b = F.pad(b, (0, pad))
         y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
-        bns = [sep[i][1] for i in range(3)]
-        norm = (lambda t: bn_padded(t, bns, pad, self.training)) if pad else \
-            (lambda t: bn_groups(t, bns, self.training))
-        y = torch.cat([norm(y[l * B:(l + 1) * B]) for l in range(Lv)]) if Lv > 1 else norm(y)
-        y = F.relu_(y)
+        # BN + ReLU of all levels in one fused launch, per-level statistics
+        y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv)
         fus = self.hf_conv['fusion']
         z = fus[0](y)
-        zs = [F.relu_(fus[1](z[l * B:(l + 1) * B])) for l in range(Lv)]
-        return torch.cat(zs, dim=1) if Lv > 1 else zs[0]
+        z = ewvit.batch_norm_act(z, fus[1], 'relu', groups=Lv) if _fusable(fus[1], z) else \
+            torch.cat([fus[2](fus[1](z[l * B:(l + 1) * B])) for l in range(Lv)])
+        return torch.cat([z[l * B:(l + 1) * B] for l in range(Lv)], dim=1) if Lv > 1 else z

@@ -157,6 +157,32 @@ int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int acc
                                int64_t H, int64_t W, int64_t C, int stride, int pad, int dtype,
                                float *workspace, void *stream);
 
+/* ---------------------------------------------- BatchNorm2d + activation ---
+ * BatchNorm2d (batch statistics in training, running statistics in eval) fused
+ * with the activation that follows it: act 0 none, 1 ReLU (the MWT conv stack,
+ * network/mwt.py:23-72), 2 SiLU (the EfficientNetV2-S backbone's
+ * Conv2dNormActivation, reached via network/sfe.py:111-113).  Channels-last
+ * x, y [M = N*H*W][C] (dtype), C % 8 == 0, C <= 2048; gamma/beta/running stats f32.
+ * Training also writes save_mean / save_invstd [C] (biased variance) and
+ * updates running_mean/var in place with `momentum` (unbiased variance), as
+ * torch does.  `groups` > 1 splits the M rows into equal consecutive groups
+ * with their OWN batch statistics (save_mean/invstd [groups][C]) and applies
+ * the running-stat update once per group in order — the MWT calls its shared
+ * hf_conv BatchNorms once per wavelet level (network/mwt.py:107-111), here all
+ * levels are one launch.  `workspace` holds ewvit_bn_workspace(M, C, groups) bytes.
+ */
+int64_t ewvit_bn_workspace(int64_t M, int64_t C, int groups);
+int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
+                 const float *beta, float *running_mean, float *running_var, int training,
+                 float momentum, float eps, int act, float *save_mean, float *save_invstd,
+                 int groups, float *workspace, void *stream);
+/* dx (dtype) from dy and the saved x/statistics (training-mode backward);
+ * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
+int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                 const float *gamma, const float *beta, const float *save_mean,
+                 const float *save_invstd, int act, float *dgamma, float *dbeta, int accumulate,
+                 int groups, float *workspace, void *stream);
+
 /* ------------------------------------------------ 3x3 conv, implicit GEMM ---
  * Conv2d(k=3, pad=1, stride 1|2, bias) of the MWT conv stack: hf_conv['fusion']
  * (mwt.py:60-64), multiscale_fusion (mwt.py:68-72), freq_conv (mwt.py:23-36),

@@ -1,0 +1,87 @@
+"""Fused BatchNorm2d + activation kernels (csrc/batchnorm.hip) through the C-ABI,
+vs torch fp32 F.batch_norm + activation on the same (bf16-rounded) input.
+
+Tolerance: bf16 output = one rounding of an fp32 result: 2^-7 of scale (plus
+exp/rsqrt ulps); fp32 output 1e-4; gradients 2e-3 of scale (fp32 reductions in a
+different order); running statistics 1e-4.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+def ref_bn(x, w, b, rm, rv, training, act, groups):
+    """torch reference: `groups` sequential F.batch_norm calls on batch slices."""
+    outs = []
+    n = x.shape[0] // groups
+    for g in range(groups):
+        y = torch.nn.functional.batch_norm(x[g * n:(g + 1) * n], rm, rv, w, b, training, 0.1, 1e-3)
+        outs.append(torch.relu(y) if act == 'relu' else torch.nn.functional.silu(y) if act == 'silu' else y)
+    return torch.cat(outs)
+
+
+@pytest.mark.parametrize('shape,groups', [((64, 960, 14, 14), 1), ((6, 56, 20, 20), 3), ((4, 24, 33, 33), 1),
+                                          ((8, 1280, 7, 7), 1), ((64, 128), 1), ((6, 128, 12, 12), 2)])
+@pytest.mark.parametrize('act', [None, 'relu', 'silu'])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_bn_act_train(shape, groups, act, dtype):
+    import ewvit
+    g = torch.Generator().manual_seed(shape[1] + groups)
+    x = (torch.randn(shape, generator=g) * 2 + 0.5).to(dtype)
+    C = shape[1]
+    w = torch.randn(C, generator=g) * 0.5 + 1
+    b = torch.randn(C, generator=g) * 0.1
+    rm0, rv0 = torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g) + 0.5
+    xr = x.float().clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rm_r, rv_r = rm0.clone(), rv0.clone()
+    yr = ref_bn(xr, wr, br, rm_r, rv_r, True, act, groups)
+    dy = torch.randn(yr.shape, generator=g).to(dtype)
+    yr.backward(dy.float())
+    xd = x.to(DEV)
+    if xd.dim() == 4:
+        xd = xd.to(memory_format=torch.channels_last)
+    xd.requires_grad_(True)
+    wd, bd = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    rm_d, rv_d = rm0.to(DEV), rv0.to(DEV)
+    y = ewvit.batch_norm_act_params(xd, wd, bd, rm_d, rv_d, True, 0.1, 1e-3, act, groups)
+    y.backward(dy.to(DEV))
+    tol = 2 ** -7 if dtype == torch.bfloat16 else 1e-4
+    assert y.dtype == dtype
+    assert rel(y.float(), yr) < tol
+    assert rel(rm_d, rm_r) < 1e-4 and rel(rv_d, rv_r) < 1e-4
+    assert rel(xd.grad.float(), xr.grad) < (2e-2 if dtype == torch.bfloat16 else 2e-3)
+    assert rel(wd.grad, wr.grad) < 2e-3
+    assert rel(bd.grad, br.grad) < 2e-3
+
+
+@pytest.mark.parametrize('act', [None, 'relu', 'silu'])
+def test_bn_act_eval(act):
+    import ewvit
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 64, 9, 9, generator=g)
+    w, b = torch.randn(64, generator=g), torch.randn(64, generator=g)
+    rm, rv = torch.randn(64, generator=g), torch.rand(64, generator=g) + 0.5
+    yr = ref_bn(x, w, b, rm.clone(), rv.clone(), False, act, 1)
+    y = ewvit.batch_norm_act_params(x.to(DEV).to(memory_format=torch.channels_last), w.to(DEV), b.to(DEV),
+                                    rm.to(DEV), rv.to(DEV), False, 0.1, 1e-3, act)
+    assert rel(y, yr) < 1e-5
+
+
+def test_bn_stats_stable_with_large_mean():
+    """Shifted sums + Chan merging: a large common offset must not destroy the variance."""
+    import ewvit
+    x = torch.randn(16, 64, 32, 32) * 0.01 + 300.0
+    rm, rv = torch.zeros(64), torch.ones(64)
+    yr = ref_bn(x.double(), None, None, rm.double(), rv.double(), True, None, 1)
+    rmd, rvd = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    y = ewvit.batch_norm_act_params(x.to(DEV).to(memory_format=torch.channels_last), None, None, rmd, rvd, True,
+                                    0.1, 1e-3, None)
+    assert rel(y, yr) < 5e-3

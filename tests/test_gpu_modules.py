@@ -265,7 +265,9 @@ def test_dama_train_step_vs_oracle(dama_pair, autocast):
             c = cos(pp[n].grad, oo[n].grad)
             assert c >= floor, f'{n}: grad cosine {c:.5f} < {floor:.5f} (torch autocast {floor + 0.01:.5f})'
     else:
-        grads_close(p, o, names, 0.99)
+        # the MWT convs and backbone depthwise convs take bf16 operands even without
+        # autocast (their kernels are bf16 MFMA / bf16-vector): bf16-level gradients
+        grads_close(p, o, names, 0.98)
     # BatchNorm running statistics were updated per level and per chunk like the reference
     ps, os_ = p.state_dict(), o.state_dict()
     for k in ['mwt.hf_conv.fusion.1.running_mean', 'mwt.hf_conv.seperate.2.1.running_var',
