@@ -83,11 +83,12 @@ static BnPlan bn_plan(int64_t M, int64_t C) {
   BnPlan p;
   p.C8 = (int)(C / 8);
   p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
-  int64_t nb = (M + 255) / 256;           // ~256 rows per block
-  if (nb > 1024) nb = 1024;
+  // ~16 rows per thread: enough to amortise the per-thread channel constants,
+  // small enough to keep >= a few hundred blocks on the small late-stage maps
+  p.rows_per_block = (int64_t)p.R * 16;
+  int64_t nb = (M + p.rows_per_block - 1) / p.rows_per_block;
   if (nb < 1) nb = 1;
   p.nblocks = (int)nb;
-  p.rows_per_block = (M + nb - 1) / nb;
   return p;
 }
 
@@ -232,19 +233,28 @@ __global__ __launch_bounds__(256) void bn_eval_coeff_kernel(const float *__restr
 // ---- apply: y = act(x * scale + shift)
 template <int DT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ x, void *__restrict__ y,
-                                                       const float *__restrict__ ss, int64_t M, int64_t Mg, int C,
-                                                       int act) {
-  // M = rows of ALL groups; Mg = rows per statistics group (ss is [group][2][C])
+                                                       const float *__restrict__ ss, int64_t Mg, int C, int R,
+                                                       int64_t rpb, int act) {
+  // grid (blocks per group, groups); thread (row group rg, channel vector c8) walks
+  // rows rg, rg+R, ... of its block with its 16 coefficients held in registers
   const int C8 = C >> 3;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * C8) return;
-  const int c = (int)(i % C8) * 8;
-  ss += (i / C8 / Mg) * 2 * C;
-  float v[8];
-  ld8<DT>(x, i * 8, v);
+  const int rg = threadIdx.x / C8, c8 = threadIdx.x % C8;
+  if (rg >= R) return;
+  const int64_t goff = (int64_t)blockIdx.y * Mg * C;
+  ss += blockIdx.y * 2 * C;
+  const int c = c8 * 8;
+  float sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = act_fwd(fmaf(v[j], ss[c + j], ss[C + c + j]), act);
-  st8<DT>(y, i * 8, v);
+  for (int j = 0; j < 8; ++j) { sc[j] = ss[c + j]; sh[j] = ss[C + c + j]; }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
+  for (int64_t r = r0 + rg; r < r1; r += R) {
+    const int64_t i = goff + r * C + c;
+    float v[8];
+    ld8<DT>(x, i, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_fwd(fmaf(v[j], sc[j], sh[j]), act);
+    st8<DT>(y, i, v);
+  }
 }
 
 // ---- backward pass 1: per-block sums of g and g*xhat, g = dy * act'(z)
@@ -352,26 +362,38 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
                                                         const float *__restrict__ gamma,
                                                         const float *__restrict__ beta,
                                                         const float *__restrict__ coef, void *__restrict__ dx,
-                                                        int64_t M, int64_t Mg, int C, int act) {
+                                                        int64_t Mg, int C, int R, int64_t rpb, int act) {
+  // same (row group, channel vector) walk as bn_apply_kernel; per-channel
+  // constants in registers: k = gamma*invstd, mean, invstd, gamma, beta, 2 coefs
   const int C8 = C >> 3;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * C8) return;
-  const int c = (int)(i % C8) * 8;
-  const int64_t grp = i / C8 / Mg;
-  mean += grp * C;
-  invstd += grp * C;
-  coef += grp * 2 * C;
-  float vx[8], vd[8], o[8];
-  ld8<DT>(x, i * 8, vx);
-  ld8<DT>(dy, i * 8, vd);
+  const int rg = threadIdx.x / C8, c8 = threadIdx.x % C8;
+  if (rg >= R) return;
+  const int64_t goff = (int64_t)blockIdx.y * Mg * C;
+  mean += blockIdx.y * C;
+  invstd += blockIdx.y * C;
+  coef += blockIdx.y * 2 * C;
+  const int c = c8 * 8;
+  float mu[8], iv[8], ga[8], be[8], c0[8], c1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float iv = invstd[c + j], ga = gamma ? gamma[c + j] : 1.f;
-    const float xh = (vx[j] - mean[c + j]) * iv;
-    const float g = act ? vd[j] * act_grad(fmaf(xh, ga, beta ? beta[c + j] : 0.f), act) : vd[j];
-    o[j] = ga * iv * (g - coef[c + j] - xh * coef[C + c + j]);
+    mu[j] = mean[c + j]; iv[j] = invstd[c + j];
+    ga[j] = gamma ? gamma[c + j] : 1.f; be[j] = beta ? beta[c + j] : 0.f;
+    c0[j] = coef[c + j]; c1[j] = coef[C + c + j];
   }
-  st8<DT>(dx, i * 8, o);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
+  for (int64_t r = r0 + rg; r < r1; r += R) {
+    const int64_t i = goff + r * C + c;
+    float vx[8], vd[8], o[8];
+    ld8<DT>(x, i, vx);
+    ld8<DT>(dy, i, vd);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (vx[j] - mu[j]) * iv[j];
+      const float g = act ? vd[j] * act_grad(fmaf(xh, ga[j], be[j]), act) : vd[j];
+      o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
+    }
+    st8<DT>(dx, i, o);
+  }
 }
 
 }  // namespace ewvit
@@ -414,13 +436,16 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
     hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
                        running_var, gamma, beta, eps, (int)C, ss);
   }
-  const int64_t nv = M * (C / 8);
+  dim3 agrid(p.nblocks, training ? groups : 1);
+  const int64_t aMg = training ? Mg : M;
+  const BnPlan ap = training ? p : bn_plan(M, C);
+  agrid.x = ap.nblocks;
   if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_BF16>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, x, y, ss, M,
-                       Mg, (int)C, act);
+    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_BF16>, agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R,
+                       ap.rows_per_block, act);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_F32>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, x, y, ss, M,
-                       Mg, (int)C, act);
+    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_F32>, agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R,
+                       ap.rows_per_block, act);
   return launch_status("bn_fwd");
 }
 
@@ -447,12 +472,11 @@ extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, 
                        save_invstd, gamma, beta, Mg, (int)C, p.R, p.rows_per_block, act, workspace);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)C), dim3(256), 0, s, workspace, p.nblocks, groups,
                      (int)C, Mg, dgamma, dbeta, accumulate, coef);
-  const int64_t nv = M * (C / 8);
   if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_BF16>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, dy, x,
-                       save_mean, save_invstd, gamma, beta, coef, dx, M, Mg, (int)C, act);
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma,
+                       beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block, act);
   else
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_F32>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, dy, x,
-                       save_mean, save_invstd, gamma, beta, coef, dx, M, Mg, (int)C, act);
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_F32>, grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma,
+                       beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block, act);
   return launch_status("bn_bwd");
 }
