@@ -169,9 +169,14 @@ def main():
     import ewvit
     from ewvit import dist as edist
     rank, world, local = edist.env_ranks()
+    # EWVIT_BENCH_REHEARSE=1: every rank on cuda:0 over gloo — exercises the DDP path
+    # on a one-GPU box (timings meaningless); the real run is one rank per GPU on RCCL
+    rehearse = os.environ.get('EWVIT_BENCH_REHEARSE') == '1'
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    edist.init_from_env('nccl')                # RCCL over xGMI
+    edist.init_from_env('gloo' if rehearse else 'nccl')    # RCCL over xGMI
     ewvit.load_library()                       # fail loudly if the HIP library is missing
     step = build_step(dev, args.frames, rank)
     for _ in range(args.warmup):
