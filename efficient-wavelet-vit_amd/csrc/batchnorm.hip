@@ -83,9 +83,11 @@ static BnPlan bn_plan(int64_t M, int64_t C) {
   BnPlan p;
   p.C8 = (int)(C / 8);
   p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
-  // ~16 rows per thread: enough to amortise the per-thread channel constants,
-  // small enough to keep >= a few hundred blocks on the small late-stage maps
-  p.rows_per_block = (int64_t)p.R * 16;
+  // rows per thread: aim at ~1024 blocks (4 per CU) so the small late-stage maps
+  // (e.g. 64x7x7 rows x 1536 ch) still fill the chip; 1..64 rows per thread
+  int64_t rpt = (M + (int64_t)p.R * 1024 - 1) / ((int64_t)p.R * 1024);
+  rpt = rpt < 1 ? 1 : (rpt > 64 ? 64 : rpt);
+  p.rows_per_block = (int64_t)p.R * rpt;
   int64_t nb = (M + p.rows_per_block - 1) / p.rows_per_block;
   if (nb < 1) nb = 1;
   p.nblocks = (int)nb;
