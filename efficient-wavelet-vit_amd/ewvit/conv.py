@@ -69,7 +69,9 @@ class Conv3x3Fn(torch.autograd.Function):
             L.call('ewvit_conv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
                    Cout, stride, L.ptr(ws), L.stream(dwf), work=work)
             if ctx.needs_input_grad[1]:
-                dw = dwf if Cx == Cin else dwf[:, :Cin].contiguous()
+                dw = dwf if Cx == Cin else dwf[:, :Cin]
+                if dw.stride() != weight.stride():     # keep the parameter's layout (DDP bucket views)
+                    dw = torch.empty_like(weight, dtype=torch.float32).copy_(dw)
             db = dbf
         return dx, dw, db, None
 

@@ -303,6 +303,7 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                L.stream(y), work=work)
         ctx.save_for_backward(xc, w)
         ctx.cfg = (stride, pad, weight.dtype)
+        ctx.wstride = weight.stride()
         return y
 
     @staticmethod
@@ -327,6 +328,8 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                    work={'bytes': (dyc.numel() + xc.numel()) * xc.element_size()})
             if wdt != torch.float32:
                 dw = dw.to(wdt)
+            if dw.stride() != ctx.wstride:          # keep the parameter's layout (DDP bucket views)
+                dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
         return dx, dw, None, None
 
 
