@@ -10,14 +10,47 @@
 // is recomputed from it).  Layout [M = N*H*W][C], bf16 or f32; 8 channels
 // (16 B for bf16) per thread.
 //
-// Statistics are numerically stable: each thread accumulates sums shifted by its
-// first sample, converts them to (mean, M2), and (count, mean, M2) triples are
-// merged with Chan's parallel formula across lanes, waves and blocks.
+// Statistics are numerically stable and deterministic: every block accumulates
+// sums shifted by one sample per channel (row 0 of its statistics group, the
+// same shift for all blocks), so partials add exactly like plain sums while the
+// cancellation in E[(x-K)^2] - E[x-K]^2 stays at the scale of the variance even
+// for |mean| >> std.  Partial slabs are reduced in a fixed order.
 // Running stats follow torch: running = (1-m)*running + m*stat, with the unbiased
 // batch variance for running_var and the biased one for normalisation.
 #include "common.h"
 
 namespace ewvit {
+
+// raw 8-element vector of dtype DT (16 B bf16 / 32 B f32), loaded in one phase and
+// unpacked in the next so a batch of rows has its loads in flight together
+template <int DT> struct Raw8;
+template <> struct Raw8<EWVIT_BF16> { uint4 q; };
+template <> struct Raw8<EWVIT_F32> { float4 a, b; };
+
+template <int DT>
+__device__ __forceinline__ Raw8<DT> ldraw(const void *p, int64_t i) {
+  Raw8<DT> r;
+  if constexpr (DT == EWVIT_BF16) {
+    r.q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16_t *>(p) + i);
+  } else {
+    const float4 *q = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + i);
+    r.a = q[0]; r.b = q[1];
+  }
+  return r;
+}
+template <int DT>
+__device__ __forceinline__ void unpack(const Raw8<DT> &r, float (&v)[8]) {
+  if constexpr (DT == EWVIT_BF16) {
+    const unsigned w[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  } else {
+    v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w; v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+  }
+}
 
 template <int DT>
 __device__ __forceinline__ void ld8(const void *p, int64_t i, float (&v)[8]) {
@@ -49,29 +82,20 @@ __device__ __forceinline__ void st8(void *p, int64_t i, const float (&v)[8]) {
   }
 }
 
-__device__ __forceinline__ float act_fwd(float z, int act) {
-  if (act == 1) return z > 0.f ? z : 0.f;
-  if (act == 2) return z / (1.f + __expf(-z));
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float z) {
+  if (ACT == 1) return z > 0.f ? z : 0.f;
+  if (ACT == 2) return z / (1.f + __expf(-z));
   return z;
 }
-__device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == 1) return z > 0.f ? 1.f : 0.f;
-  if (act == 2) {
+template <int ACT>
+__device__ __forceinline__ float act_grad(float z) {
+  if (ACT == 1) return z > 0.f ? 1.f : 0.f;
+  if (ACT == 2) {
     const float s = 1.f / (1.f + __expf(-z));
     return s * (1.f + z * (1.f - s));
   }
   return 1.f;
-}
-
-// Chan: merge (nb, mb, M2b) into (na, ma, M2a)
-__device__ __forceinline__ void chan(float &na, float &ma, float &qa, float nb, float mb, float qb) {
-  const float n = na + nb;
-  if (n == 0.f) return;
-  const float d = mb - ma;
-  const float f = nb / n;
-  ma += d * f;
-  qa += qb + d * d * na * f;
-  na = n;
 }
 
 struct BnPlan {
@@ -79,12 +103,12 @@ struct BnPlan {
   int64_t rows_per_block;
 };
 
+// elementwise passes (apply, dx): aim at ~1024 blocks (4 per CU) so the small
+// late-stage maps (e.g. 64x7x7 rows x 1536 ch) still fill the chip; 1..64 rows/thread
 static BnPlan bn_plan(int64_t M, int64_t C) {
   BnPlan p;
   p.C8 = (int)(C / 8);
   p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
-  // rows per thread: aim at ~1024 blocks (4 per CU) so the small late-stage maps
-  // (e.g. 64x7x7 rows x 1536 ch) still fill the chip; 1..64 rows per thread
   int64_t rpt = (M + (int64_t)p.R * 1024 - 1) / ((int64_t)p.R * 1024);
   rpt = rpt < 1 ? 1 : (rpt > 64 ? 64 : rpt);
   p.rows_per_block = (int64_t)p.R * rpt;
@@ -94,128 +118,156 @@ static BnPlan bn_plan(int64_t M, int64_t C) {
   return p;
 }
 
-// ---- pass 1 (forward): per-block (mean, M2) per channel; count is rows in block
+// reduction passes (stats, bwd sums): ~512 blocks over all groups, >= 16 rows per
+// thread, so the partial slabs stay small next to the tensor they summarise
+static BnPlan bn_red_plan(int64_t M, int64_t C, int groups) {
+  BnPlan p;
+  p.C8 = (int)(C / 8);
+  p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
+  int64_t nb = (512 + groups - 1) / groups;
+  const int64_t maxnb = M / ((int64_t)p.R * 16);
+  if (nb > maxnb) nb = maxnb;
+  if (nb < 1) nb = 1;
+  int64_t rpb = (M + nb - 1) / nb;
+  rpb = (rpb + p.R - 1) / p.R * p.R;
+  p.rows_per_block = rpb;
+  p.nblocks = (int)((M + rpb - 1) / rpb);
+  if (p.nblocks < 1) p.nblocks = 1;
+  return p;
+}
+
+// workspace layout (floats): [groups][nred][2C] partials | [groups][C] shifts | [groups][2C] coefficients
+static int64_t ws_part(const BnPlan &rp, int64_t C, int groups) { return (int64_t)groups * rp.nblocks * 2 * C; }
+
+// the batched walk of a (row group, channel vector) thread over rows r0+rg,
+// r0+rg+R, ... < r1: NB rows are loaded (`load(r)` -> raw registers) before any
+// is used (`use(r, raw)`), so NB rows' loads are in flight together
+template <int NB, typename L, typename U>
+__device__ __forceinline__ void row_walk(int64_t r0, int64_t r1, int rg, int R, L &&load, U &&use) {
+  using T = decltype(load(int64_t(0)));
+  int64_t r = r0 + rg;
+  for (; r + (NB - 1) * (int64_t)R < r1; r += NB * (int64_t)R) {
+    T t[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) t[q] = load(r + q * (int64_t)R);
+    __builtin_amdgcn_sched_barrier(0);   // keep the batch's loads ahead of their uses
+#pragma unroll
+    for (int q = 0; q < NB; ++q) use(r + q * (int64_t)R, t[q]);
+  }
+  for (; r < r1; r += R) use(r, load(r));
+}
+
+template <int DT> struct Raw8x2 { Raw8<DT> x, d; };
+
+// ---- pass 1 (forward): per-block sums of (x - K) and (x - K)^2 per channel
 template <int DT>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ x, int64_t M, int C, int R,
-                                                       int64_t rpb, float *__restrict__ part) {
-  __shared__ float sm[256 * 8 * 3];
+                                                       int64_t rpb, float *__restrict__ part,
+                                                       float *__restrict__ shifts) {
+  __shared__ float sm[256 * 8 * 2];
   // blockIdx.y = statistics group (consecutive blocks of M rows, own batch stats)
   x = reinterpret_cast<const char *>(x) + (int64_t)blockIdx.y * M * C * (DT == EWVIT_BF16 ? 2 : 4);
-  part += (int64_t)blockIdx.y * gridDim.x * (2 * C + 1);
+  part += (int64_t)blockIdx.y * gridDim.x * 2 * C;
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
   const int rg = tid / C8, c8 = tid % C8;
   const bool active = rg < R && c8 < C8;
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < M ? r0 + rpb : M;
-  float n = 0.f, K[8], S[8], SS[8];
+  float K[8], S[8], SS[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { K[j] = 0.f; S[j] = 0.f; SS[j] = 0.f; }
   if (active) {
-    bool first = true;
-    for (int64_t r = r0 + rg; r < r1; r += R) {
-      float v[8];
-      ld8<DT>(x, r * C + c8 * 8, v);
-      if (first) {
+    ld8<DT>(x, (int64_t)c8 * 8, K);   // the group's shift: its row 0
+    if (blockIdx.x == 0 && rg == 0)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) K[j] = v[j];
-        first = false;
-      }
+      for (int j = 0; j < 8; ++j) shifts[blockIdx.y * C + c8 * 8 + j] = K[j];
+    row_walk<8>(r0, r1, rg, R, [&](int64_t rr) { return ldraw<DT>(x, rr * C + c8 * 8); },
+                [&](int64_t, const Raw8<DT> &raw) {
+      float v[8];
+      unpack<DT>(raw, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = v[j] - K[j];
         S[j] += d;
         SS[j] = fmaf(d, d, SS[j]);
       }
-      n += 1.f;
-    }
+    });
   }
-  // per-thread (n, mean, M2)
-  float mean[8], m2[8];
+  // sum the R row groups of each channel vector through LDS (fixed order)
+  float *s1 = sm, *s2 = sm + 256 * 8;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float mu = n > 0.f ? S[j] / n : 0.f;
-    mean[j] = K[j] + mu;
-    m2[j] = n > 0.f ? SS[j] - S[j] * mu : 0.f;
-  }
-  // merge the R row groups of each channel group through LDS (sequential, fixed order)
-  float *sn = sm, *smu = sm + 256, *sq = sm + 256 + 256 * 8;
-  if (active) {
-    sn[tid] = n;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { smu[tid * 8 + j] = mean[j]; sq[tid * 8 + j] = m2[j]; }
-  }
+  for (int j = 0; j < 8; ++j) { s1[tid * 8 + j] = S[j]; s2[tid * 8 + j] = SS[j]; }
   __syncthreads();
   if (tid < C8) {
-    float na = sn[tid];
-    float ma[8], qa[8];
+    float a[8], b[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { ma[j] = smu[tid * 8 + j]; qa[j] = sq[tid * 8 + j]; }
+    for (int j = 0; j < 8; ++j) { a[j] = s1[tid * 8 + j]; b[j] = s2[tid * 8 + j]; }
     for (int g = 1; g < R; ++g) {
       const int t = g * C8 + tid;
-      const float nb = sn[t];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float nn = na;
-        chan(nn, ma[j], qa[j], nb, smu[t * 8 + j], sq[t * 8 + j]);
-      }
-      na += nb;
+      for (int j = 0; j < 8; ++j) { a[j] += s1[t * 8 + j]; b[j] += s2[t * 8 + j]; }
     }
-    float *pb = part + (int64_t)blockIdx.x * (2 * C + 1);
+    float *pb = part + (int64_t)blockIdx.x * 2 * C;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      pb[tid * 8 + j] = ma[j];
-      pb[C + tid * 8 + j] = qa[j];
-    }
-    if (tid == 0) pb[2 * C] = na;
+    for (int j = 0; j < 8; ++j) { pb[tid * 8 + j] = a[j]; pb[C + tid * 8 + j] = b[j]; }
   }
 }
 
-// ---- finalize (forward): merge blocks; save mean / invstd; update running stats;
-// scale = gamma*invstd, shift = beta - mean*scale into ss[2][C]
+// Sum the partial slab column c over nblocks rows: 32 channels x 8 partial lanes per
+// block (coalesced 128-B rows), lanes combined in a fixed order.  Returns the two
+// sums in lane 0 of each channel.
+__device__ __forceinline__ void slab_sum(const float *__restrict__ pg, int nblocks, int C, int c, bool ok,
+                                         float *red, float &a, float &b) {
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  a = 0.f; b = 0.f;
+  if (ok)
+    for (int k = pl; k < nblocks; k += 8) {
+      a += pg[(int64_t)k * 2 * C + c];
+      b += pg[(int64_t)k * 2 * C + C + c];
+    }
+  red[threadIdx.x] = a;
+  red[256 + threadIdx.x] = b;
+  __syncthreads();
+  if (pl == 0) {
+    for (int q = 1; q < 8; ++q) { a += red[q * 32 + cl]; b += red[256 + q * 32 + cl]; }
+  }
+  __syncthreads();
+}
+
+// ---- finalize (forward): mean / invstd per group; running stats updated group by
+// group in order (the reference calls the module once per group);
+// scale = gamma*invstd, shift = beta - mean*scale into ss[groups][2][C]
 __global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(const float *__restrict__ part, int nblocks, int groups,
-                                                              int C, const float *__restrict__ gamma,
+                                                              int C, int64_t Mg, const float *__restrict__ shifts,
+                                                              const float *__restrict__ gamma,
                                                               const float *__restrict__ beta, float *running_mean,
                                                               float *running_var, float momentum, float eps,
                                                               float *save_mean, float *save_invstd,
-                                                              float *__restrict__ ss) {
-  // one block per channel: 256 threads merge strided partials, then an LDS tree;
-  // statistics groups are finalised in order, so the running stats see the
-  // groups' updates in sequence (the reference calls the module once per group)
-  __shared__ float tn[256], tm[256], tq[256];
-  const int c = blockIdx.x, t = threadIdx.x;
+                                                              int64_t *counter, float *__restrict__ ss) {
+  __shared__ float red[512];
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += groups;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool ok = c < C;
+  const float n = (float)Mg;
   for (int grp = 0; grp < groups; ++grp) {
-    const float *pg = part + (int64_t)grp * nblocks * (2 * C + 1);
-    float n = 0.f, mu = 0.f, q = 0.f;
-    for (int b = t; b < nblocks; b += 256) {
-      const float *pb = pg + (int64_t)b * (2 * C + 1);
-      chan(n, mu, q, pb[2 * C], pb[c], pb[C + c]);
-    }
-    tn[t] = n; tm[t] = mu; tq[t] = q;
-    __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-      if (t < h) {
-        float na = tn[t], ma = tm[t], qa = tq[t];
-        chan(na, ma, qa, tn[t + h], tm[t + h], tq[t + h]);
-        tn[t] = na; tm[t] = ma; tq[t] = qa;
-      }
-      __syncthreads();
-    }
-    if (t == 0) {
-      n = tn[0]; mu = tm[0]; q = tq[0];
-      const float var = n > 0.f ? q / n : 0.f;
+    float S, SS;
+    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, red, S, SS);
+    if (threadIdx.x < 32 && ok) {
+      const float d = S / n;
+      const float mu = shifts[grp * C + c] + d;
+      const float var = fmaxf(SS / n - d * d, 0.f);
       const float inv = rsqrtf(var + eps);
       if (save_mean) save_mean[grp * C + c] = mu;
       if (save_invstd) save_invstd[grp * C + c] = inv;
       if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
       if (running_var) {
-        const float unb = n > 1.f ? q / (n - 1.f) : var;
+        const float unb = Mg > 1 ? var * (n / (n - 1.f)) : var;
         running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
       }
       const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
       ss[grp * 2 * C + c] = g * inv;
       ss[grp * 2 * C + C + c] = b - mu * g * inv;
     }
-    __syncthreads();
   }
 }
 
@@ -233,10 +285,10 @@ __global__ __launch_bounds__(256) void bn_eval_coeff_kernel(const float *__restr
 }
 
 // ---- apply: y = act(x * scale + shift)
-template <int DT>
+template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ x, void *__restrict__ y,
                                                        const float *__restrict__ ss, int64_t Mg, int C, int R,
-                                                       int64_t rpb, int act) {
+                                                       int64_t rpb) {
   // grid (blocks per group, groups); thread (row group rg, channel vector c8) walks
   // rows rg, rg+R, ... of its block with its 16 coefficients held in registers
   const int C8 = C >> 3;
@@ -249,24 +301,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sc[j] = ss[c + j]; sh[j] = ss[C + c + j]; }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  for (int64_t r = r0 + rg; r < r1; r += R) {
-    const int64_t i = goff + r * C + c;
+  row_walk<8>(r0, r1, rg, R, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
+              [&](int64_t rr, const Raw8<DT> &raw) {
     float v[8];
-    ld8<DT>(x, i, v);
+    unpack<DT>(raw, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_fwd(fmaf(v[j], sc[j], sh[j]), act);
-    st8<DT>(y, i, v);
-  }
+    for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
+    st8<DT>(y, goff + rr * C + c, v);
+  });
 }
 
 // ---- backward pass 1: per-block sums of g and g*xhat, g = dy * act'(z)
-template <int DT>
+template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                             const float *__restrict__ mean,
                                                             const float *__restrict__ invstd,
                                                             const float *__restrict__ gamma,
                                                             const float *__restrict__ beta, int64_t M, int C, int R,
-                                                            int64_t rpb, int act, float *__restrict__ part) {
+                                                            int64_t rpb, float *__restrict__ part) {
   __shared__ float sm[256 * 8 * 2];
   // blockIdx.y = statistics group: its rows, saved stats and partial slab
   {
@@ -291,18 +343,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
     ga[j] = gamma ? gamma[c] : 1.f; be[j] = beta ? beta[c] : 0.f;
   }
   if (active) {
-    for (int64_t r = r0 + rg; r < r1; r += R) {
+    row_walk<8>(r0, r1, rg, R,
+                [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8)}; },
+                [&](int64_t, const Raw8x2<DT> &raw) {
       float vx[8], vd[8];
-      ld8<DT>(x, r * C + c8 * 8, vx);
-      ld8<DT>(dy, r * C + c8 * 8, vd);
+      unpack<DT>(raw.x, vx);
+      unpack<DT>(raw.d, vd);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (vx[j] - mu[j]) * iv[j];
-        const float g = act ? vd[j] * act_grad(fmaf(xh, ga[j], be[j]), act) : vd[j];
+        const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
         sg[j] += g;
         sgx[j] = fmaf(g, xh, sgx[j]);
       }
-    }
+    });
   }
   float *s1 = sm, *s2 = sm + 256 * 8;
 #pragma unroll
@@ -327,44 +381,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
 __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float *__restrict__ part, int nblocks, int groups,
                                                               int C, int64_t Mg, float *dgamma, float *dbeta,
                                                               int accumulate, float *__restrict__ coef) {
-  __shared__ float ta[256], tb[256];
-  const int c = blockIdx.x, t = threadIdx.x;
+  __shared__ float red[512];
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool ok = c < C;
   float ga = 0.f, gb = 0.f;  // sums over all groups (the parameters are shared)
   for (int grp = 0; grp < groups; ++grp) {
-    const float *pg = part + (int64_t)grp * nblocks * 2 * C;
-    float a = 0.f, b = 0.f;
-    for (int k = t; k < nblocks; k += 256) {
-      a += pg[(int64_t)k * 2 * C + c];
-      b += pg[(int64_t)k * 2 * C + C + c];
+    float a, b;
+    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, red, a, b);
+    if (threadIdx.x < 32 && ok) {
+      coef[grp * 2 * C + c] = a / (float)Mg;
+      coef[grp * 2 * C + C + c] = b / (float)Mg;
+      ga += a;
+      gb += b;
     }
-    ta[t] = a; tb[t] = b;
-    __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-      if (t < h) { ta[t] += ta[t + h]; tb[t] += tb[t + h]; }
-      __syncthreads();
-    }
-    if (t == 0) {
-      coef[grp * 2 * C + c] = ta[0] / (float)Mg;
-      coef[grp * 2 * C + C + c] = tb[0] / (float)Mg;
-      ga += ta[0];
-      gb += tb[0];
-    }
-    __syncthreads();
   }
-  if (t != 0) return;
+  if (threadIdx.x >= 32 || !ok) return;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + ga : ga;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gb : gb;
 }
 
 // dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
-template <int DT>
+template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                         const float *__restrict__ mean,
                                                         const float *__restrict__ invstd,
                                                         const float *__restrict__ gamma,
                                                         const float *__restrict__ beta,
                                                         const float *__restrict__ coef, void *__restrict__ dx,
-                                                        int64_t Mg, int C, int R, int64_t rpb, int act) {
+                                                        int64_t Mg, int C, int R, int64_t rpb) {
   // same (row group, channel vector) walk as bn_apply_kernel; per-channel
   // constants in registers: k = gamma*invstd, mean, invstd, gamma, beta, 2 coefs
   const int C8 = C >> 3;
@@ -383,35 +427,51 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
     c0[j] = coef[c + j]; c1[j] = coef[C + c + j];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  for (int64_t r = r0 + rg; r < r1; r += R) {
-    const int64_t i = goff + r * C + c;
+  row_walk<8>(r0, r1, rg, R,
+              [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c)}; },
+              [&](int64_t rr, const Raw8x2<DT> &raw) {
+    const int64_t i = goff + rr * C + c;
     float vx[8], vd[8], o[8];
-    ld8<DT>(x, i, vx);
-    ld8<DT>(dy, i, vd);
+    unpack<DT>(raw.x, vx);
+    unpack<DT>(raw.d, vd);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (vx[j] - mu[j]) * iv[j];
-      const float g = act ? vd[j] * act_grad(fmaf(xh, ga[j], be[j]), act) : vd[j];
+      const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
     }
     st8<DT>(dx, i, o);
-  }
+  });
 }
 
 }  // namespace ewvit
 
 using namespace ewvit;
 
+// instantiate launch L(dtype, act) for the runtime (dtype, act) pair
+#define BN_DISPATCH(L)                                  \
+  do {                                                  \
+    if (dtype == EWVIT_BF16) {                          \
+      if (act == 0) L(EWVIT_BF16, 0);                   \
+      else if (act == 1) L(EWVIT_BF16, 1);              \
+      else L(EWVIT_BF16, 2);                            \
+    } else {                                            \
+      if (act == 0) L(EWVIT_F32, 0);                    \
+      else if (act == 1) L(EWVIT_F32, 1);               \
+      else L(EWVIT_F32, 2);                             \
+    }                                                   \
+  } while (0)
+
 extern "C" int64_t ewvit_bn_workspace(int64_t M, int64_t C, int groups) {
   if (groups < 1) groups = 1;
-  const BnPlan p = bn_plan(M / groups, C);
-  return ((int64_t)groups * ((int64_t)p.nblocks * (2 * C + 1) + 2 * C)) * (int64_t)sizeof(float);
+  const BnPlan rp = bn_red_plan(M / groups, C, groups);
+  return (ws_part(rp, C, groups) + (int64_t)groups * 3 * C) * (int64_t)sizeof(float);
 }
 
 extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
                             const float *beta, float *running_mean, float *running_var, int training,
                             float momentum, float eps, int act, float *save_mean, float *save_invstd,
-                            int groups, float *workspace, void *stream) {
+                            int groups, int64_t *num_batches_tracked, float *workspace, void *stream) {
   EWVIT_CHECK_ARG(x && y && workspace && dtype_ok(dtype), "bn_fwd: bad args");
   EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 2048, "bn_fwd: C=%lld must be a multiple of 8, <= 2048", (long long)C);
   EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_fwd: act=%d", act);
@@ -421,33 +481,33 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const int64_t Mg = M / groups;
-  const BnPlan p = bn_plan(Mg, C);
-  float *ss = workspace + (int64_t)groups * p.nblocks * (2 * C + 1);
+  const BnPlan rp = bn_red_plan(Mg, C, groups);
+  float *shifts = workspace + ws_part(rp, C, groups);
+  float *ss = shifts + (int64_t)groups * C;
+  const unsigned cblocks = (unsigned)((C + 31) / 32);
   if (training) {
-    dim3 grid(p.nblocks, groups);
+    dim3 grid(rp.nblocks, groups);
     if (dtype == EWVIT_BF16)
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, x, Mg, (int)C, p.R,
-                         p.rows_per_block, workspace);
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, x, Mg, (int)C, rp.R,
+                         rp.rows_per_block, workspace, shifts);
     else
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(256), 0, s, x, Mg, (int)C, p.R,
-                         p.rows_per_block, workspace);
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((unsigned)C), dim3(256), 0, s, workspace, p.nblocks, groups,
-                       (int)C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, ss);
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(256), 0, s, x, Mg, (int)C, rp.R,
+                         rp.rows_per_block, workspace, shifts);
+    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(cblocks), dim3(256), 0, s, workspace, rp.nblocks, groups,
+                       (int)C, Mg, shifts, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                       save_invstd, num_batches_tracked, ss);
   } else {
     EWVIT_CHECK_ARG(groups == 1, "bn_fwd: eval mode takes one group");
     hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
                        running_var, gamma, beta, eps, (int)C, ss);
   }
-  dim3 agrid(p.nblocks, training ? groups : 1);
   const int64_t aMg = training ? Mg : M;
-  const BnPlan ap = training ? p : bn_plan(M, C);
-  agrid.x = ap.nblocks;
-  if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_BF16>, agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R,
-                       ap.rows_per_block, act);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<EWVIT_F32>, agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R,
-                       ap.rows_per_block, act);
+  const BnPlan ap = bn_plan(aMg, C);
+  dim3 agrid(ap.nblocks, training ? groups : 1);
+#define BN_APPLY(DTV, ACTV) \
+  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R, ap.rows_per_block)
+  BN_DISPATCH(BN_APPLY);
+#undef BN_APPLY
   return launch_status("bn_fwd");
 }
 
@@ -463,22 +523,22 @@ extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, 
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const int64_t Mg = M / groups;
+  const BnPlan rp = bn_red_plan(Mg, C, groups);
+  float *coef = workspace + ws_part(rp, C, groups) + (int64_t)groups * C;
+  dim3 grid(rp.nblocks, groups);
+#define BN_RED(DTV, ACTV)                                                                            \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, \
+                     gamma, beta, Mg, (int)C, rp.R, rp.rows_per_block, workspace)
+  BN_DISPATCH(BN_RED);
+#undef BN_RED
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, s, workspace,
+                     rp.nblocks, groups, (int)C, Mg, dgamma, dbeta, accumulate, coef);
   const BnPlan p = bn_plan(Mg, C);
-  float *coef = workspace + (int64_t)groups * p.nblocks * (2 * C + 1);
-  dim3 grid(p.nblocks, groups);
-  if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, dy, x, save_mean,
-                       save_invstd, gamma, beta, Mg, (int)C, p.R, p.rows_per_block, act, workspace);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<EWVIT_F32>, grid, dim3(256), 0, s, dy, x, save_mean,
-                       save_invstd, gamma, beta, Mg, (int)C, p.R, p.rows_per_block, act, workspace);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)C), dim3(256), 0, s, workspace, p.nblocks, groups,
-                     (int)C, Mg, dgamma, dbeta, accumulate, coef);
-  if (dtype == EWVIT_BF16)
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma,
-                       beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block, act);
-  else
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<EWVIT_F32>, grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma,
-                       beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block, act);
+  dim3 dgrid(p.nblocks, groups);
+#define BN_DX(DTV, ACTV)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma, \
+                     beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block)
+  BN_DISPATCH(BN_DX);
+#undef BN_DX
   return launch_status("bn_bwd");
 }

@@ -1,9 +1,11 @@
-// 3x3 convolution as an MFMA implicit GEMM, channels-last bf16 (gfx950).
+// Dense 2-D convolution (kernel 1x1 or 3x3, pad k/2, stride 1|2) as an MFMA
+// implicit GEMM, channels-last bf16 (gfx950).
 //
-// The MWT conv stack of network/mwt.py:23-72 — hf_conv['fusion'] (Cin 54 -> padded
-// 64, 112^2, all 3 levels batched), multiscale_fusion (384 -> 128, 112^2),
-// freq_conv (128 -> 128, stride 2) and freq_pool's conv (stride 2) — holds 74 % of
-// the model's FLOPs (SURVEY §8 note 3).  Three kernels:
+// Callers: the MWT conv stack of network/mwt.py:23-72 — hf_conv['fusion'] (all 3
+// levels batched), multiscale_fusion (384 -> 128, 112^2, reading the three
+// level-major fusion outputs in place), freq_conv / freq_pool (stride 2) — 74 % of
+// the model's FLOPs (SURVEY §8 note 3), and the EfficientNetV2-S backbone's dense
+// convs (FusedMBConv 3x3, MBConv expand/project 1x1, head 1x1).  Three kernels:
 //
 //   fwd    y[m, co]  = sum_{tap, ci} x[pix(m, tap), ci] * W[co, ci, tap]   (+ bias)
 //   dgrad  dx[m, ci] = sum_{tap, co} dy[pix^T(m, tap), co] * W[co, ci, tap]
@@ -11,14 +13,21 @@
 //           [ci][tap][co]; stride 2 handled by the parity test of pix^T)
 //   wgrad  dW[co, tap, ci] = sum_m dy[m, co] * x[pix(m, tap), ci]   (split over m)
 //
-// GEMM tile 128x128x32, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4
-// v_mfma_f32_16x16x32_bf16 tiles, fp32 accumulate.  Operands are staged
+// GEMM tile 128xBNx32, 256 threads = 4 waves (2x2), each wave 64x(BN/2) =
+// 4x(BN/32) v_mfma_f32_16x16x32_bf16 tiles, fp32 accumulate.  Operands are staged
 // global -> registers -> LDS with the next K-tile's loads in flight during the
-// current tile's MFMAs.  fwd/dgrad images are [row][k] (k contiguous, 16-B rows
-// chunks, padded rows) read with ds_read_b128; wgrad's operands both have the
-// reduction (pixel) index outermost in HBM, so they are staged as natural
-// [k][row] images (256-B rows, XOR-swizzled 16-B chunks) and read as MFMA
-// fragments with ds_read_b64_tr_b16 (the gfx950 transposing LDS read).
+// current tile's MFMAs.  When the per-tap channel count is a multiple of 32 every
+// K-tile lies inside one tap, so the tap (and the pixel offset it implies) is a
+// wave-uniform scalar and the gather costs a handful of VALU ops per vector.
+// fwd/dgrad images are [row][k] (k contiguous, padded 80-B rows) read with
+// ds_read_b128; wgrad's operands both have the reduction (pixel) index outermost
+// in HBM, so they are staged as natural [k][row] images (256-B rows, XOR-swizzled
+// 16-B chunks) and read as MFMA fragments with ds_read_b64_tr_b16.
+//
+// Grouped channels-last layout (gc, gs): channel c of pixel p lives at
+// (c / gc) * gs + p * gc + c % gc.  gc = C is plain NHWC; gc = 128, gs = B*H*W*128
+// is the MWT's level-major fusion output [L][B][H][W][128] read as the
+// [B][H][W][3*128] concatenation (mwt.py:112) without materialising it.
 #include "common.h"
 
 namespace ewvit {
@@ -33,56 +42,51 @@ constexpr int CLD = CBK + 8;  // padded [row][k] image row (80 B)
 struct ConvGeom {
   int N, H, W, Cin;      // x (fwd) / dx (dgrad) grid
   int Ho, Wo, Cout;      // y / dy grid
-  int stride;
+  int stride, ks, pad;   // ks 1|3, pad = ks/2
 };
 
 // ---------------------------------------------------------------- fwd / dgrad
 // A(m, k): m = pixel of the OUTPUT grid of this GEMM (y for fwd, dx for dgrad),
 // k = tap * KC + c (KC = Cin for fwd, Cout for dgrad).  B(k, n) = Wp[n][k].
 struct FwdArgs {
-  const bf16_t *src;     // gathered operand: x (fwd) or dy (dgrad), NHWC
-  const bf16_t *wp;      // packed weights [Ncol][9][KC]
+  const bf16_t *src;     // gathered operand: x (fwd) or dy (dgrad), grouped NHWC
+  const bf16_t *wp;      // packed weights [Ncol][taps][KC]
   const float *bias;     // [Ncol] or null
-  bf16_t *out;           // [M][Ncol] NHWC
+  bf16_t *out;           // [M][Ncol], grouped NHWC
   ConvGeom g;
   int64_t M;
   int Ncol, KC;          // GEMM N and per-tap K
   int srcH, srcW;        // spatial size of `src`
   int outH, outW;        // spatial size of the GEMM's output grid
+  int sgc, ogc;          // channel group widths of src / out
+  int64_t sgs, ogs;      // group strides (elements)
 };
 
-template <bool DGRAD>
-__device__ __forceinline__ bool src_pixel(const FwdArgs &a, int oh, int ow, int tap, int &sh, int &sw) {
-  const int kh = tap / 3, kw = tap % 3;
-  if (!DGRAD) {
-    sh = oh * a.g.stride - 1 + kh;
-    sw = ow * a.g.stride - 1 + kw;
-  } else {
-    // dx pixel (oh, ow) receives dy[(oh + 1 - kh)/s, (ow + 1 - kw)/s] when divisible
-    const int th = oh + 1 - kh, tw = ow + 1 - kw;
-    if (th < 0 || tw < 0) return false;
-    if (a.g.stride == 2 && ((th | tw) & 1)) return false;
-    sh = th / a.g.stride;
-    sw = tw / a.g.stride;
-  }
-  return sh >= 0 && sh < a.srcH && sw >= 0 && sw < a.srcW;
-}
-
-template <bool DGRAD, int BN_>
-__global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
+template <bool DGRAD, int BN_, int KS>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   constexpr int WN = BN_ / 2, J = WN / 16;  // per-wave columns, 16-wide MFMA tiles
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][CBM][CLD];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN_][CLD];
+  constexpr int A_EL = 2 * CBM * CLD, B_EL = 2 * BN_ * CLD;
+  constexpr int CST = BN_ + 8;               // epilogue image row (bf16)
+  static_assert(CBM * CST <= A_EL + B_EL, "epilogue tile must fit the staging LDS");
+  // one LDS array: double-buffered A / B images, reused as the output tile image
+  __shared__ __attribute__((aligned(16))) bf16_t smem[A_EL + B_EL];
+  auto As = reinterpret_cast<bf16_t (*)[CBM][CLD]>(smem);
+  auto Bs = reinterpret_cast<bf16_t (*)[BN_][CLD]>(smem + A_EL);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.x * CBM;
   const int n0 = blockIdx.y * BN_;
-  const int K = 9 * a.KC;
+  const int K = KS * KS * a.KC;
   const int nk = (K + CBK - 1) / CBK;
+  const bool fastk = (a.KC % CBK) == 0;   // every K-tile inside one tap / one src group
+  const int cbn = a.KC / CBK;             // channel blocks per tap (fastk)
+  const int ls = a.g.stride >> 1;         // log2(stride)
+  const int smask = a.g.stride - 1;
 
   // each thread stages 2 A vectors and 2 B vectors (8 bf16 each) per K-tile
   int arow[2], ach[2];
-  int an[2], aoh[2], aow[2];
+  int py[2], px[2];      // fwd: oh*s - pad, ow*s - pad;  dgrad: oh + pad, ow + pad
+  int64_t pbase[2];      // n * srcH * srcW
   bool avalid[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -92,31 +96,67 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
     const int64_t m = m0 + arow[u];
     avalid[u] = m < a.M;
     const int64_t mm = avalid[u] ? m : 0;
-    aow[u] = (int)(mm % a.outW);
+    const int ow = (int)(mm % a.outW);
     const int64_t t = mm / a.outW;
-    aoh[u] = (int)(t % a.outH);
-    an[u] = (int)(t / a.outH);
+    const int oh = (int)(t % a.outH);
+    const int n = (int)(t / a.outH);
+    if (!DGRAD) { py[u] = oh * a.g.stride - a.g.pad; px[u] = ow * a.g.stride - a.g.pad; }
+    else        { py[u] = oh + a.g.pad;               px[u] = ow + a.g.pad; }
+    pbase[u] = (int64_t)n * a.srcH * a.srcW;
   }
-  uint4 ra[2], rb[2];
-  auto load_tile = [&](int kt) {
+  // pixel index of tap (kh, kw) for staged row u, or -1 when it falls outside src
+  auto src_pix = [&](int u, int kh, int kw) -> int64_t {
+    int sh, sw;
+    if (!DGRAD) {
+      sh = py[u] + kh; sw = px[u] + kw;
+    } else {
+      const int th = py[u] - kh, tw = px[u] - kw;
+      if (th < 0 || tw < 0 || ((th | tw) & smask)) return -1;
+      sh = th >> ls; sw = tw >> ls;
+    }
+    if ((unsigned)sh >= (unsigned)a.srcH || (unsigned)sw >= (unsigned)a.srcW) return -1;
+    return pbase[u] + (int64_t)sh * a.srcW + sw;
+  };
+  int ltap = 0, lcb = 0;   // fastk: tap / channel block of the next K-tile to load
+  auto load_tile = [&](int kt, uint4 (&ra)[2], uint4 (&rb)[2]) {
+    int tap_u = 0, kh = 0, kw = 0;
+    int64_t goff = 0;      // group offset (elements) of this tile's channel block
+    int cin0 = 0;          // channel within the group for ach == 0
+    if (fastk) {
+      tap_u = ltap;
+      kh = tap_u / KS; kw = tap_u - kh * KS;
+      const int c0 = lcb * CBK;
+      const int gi = c0 / a.sgc;
+      goff = (int64_t)gi * a.sgs;
+      cin0 = c0 - gi * a.sgc;
+      if (++lcb == cbn) { lcb = 0; ++ltap; }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int k = kt * CBK + ach[u];
-      uint4 va = make_uint4(0u, 0u, 0u, 0u);
-      if (avalid[u] && k < K) {
-        const int tap = k / a.KC, c = k % a.KC;
-        int sh, sw;
-        if (src_pixel<DGRAD>(a, aoh[u], aow[u], tap, sh, sw))
-          va = *reinterpret_cast<const uint4 *>(a.src + (((int64_t)an[u] * a.srcH + sh) * a.srcW + sw) * a.KC + c);
+      int64_t off, p;
+      if (fastk) {
+        p = src_pix(u, kh, kw);
+        off = goff + p * a.sgc + cin0 + ach[u];
+      } else {   // KC % 32 != 0 (ungrouped src): per-thread tap
+        const int tap = KS == 1 ? 0 : k / a.KC;
+        const int c = k - tap * a.KC;
+        const int th = tap / KS;
+        p = src_pix(u, th, tap - th * KS);
+        off = p * a.KC + c;
       }
+      uint4 va = make_uint4(0u, 0u, 0u, 0u);
+      if (avalid[u] && k < K && p >= 0) va = *reinterpret_cast<const uint4 *>(a.src + off);
       ra[u] = va;
-      const int n = n0 + arow[u];  // B rows use the same (row, chunk) split
-      uint4 vb = make_uint4(0u, 0u, 0u, 0u);
-      if ((BN_ == 128 || u == 0) && n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
-      rb[u] = vb;
+      if (BN_ == 128 || u == 0) {
+        const int n = n0 + arow[u];  // B rows use the same (row, chunk) split
+        uint4 vb = make_uint4(0u, 0u, 0u, 0u);
+        if (n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
+        rb[u] = vb;
+      }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[2], const uint4 (&rb)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       *reinterpret_cast<uint4 *>(&As[buf][arow[u]][ach[u]]) = ra[u];
@@ -130,14 +170,13 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+  // K-tile kt+2 is loaded into registers while kt is computed from LDS and kt+1
+  // (loaded one step earlier) is written to the other LDS buffer: two K-steps of
+  // MFMA work cover each global load
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
+  auto step = [&](int kt, uint4 (&na)[2], uint4 (&nb)[2], const uint4 (&ra)[2], const uint4 (&rb)[2]) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load_tile(kt + 1);
+    if (kt + 2 < nk) load_tile(kt + 2, na, nb);
     cbf16x8 af[4], bfr[J];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const cbf16x8 *>(&As[cur][wm * 64 + i * 16 + fr][fk]);
@@ -147,22 +186,45 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) store_tile(cur ^ 1);
+    if (kt + 1 < nk) store_tile(cur ^ 1, ra, rb);
     __syncthreads();
+  };
+  uint4 pa[2], pb[2], qa[2], qb[2];
+  load_tile(0, pa, pb);
+  if (nk > 1) load_tile(1, qa, qb);
+  store_tile(0, pa, pb);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, pa, pb, qa, qb);
+    step(kt + 1, qa, qb, pa, pb);
   }
-  // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+  if (kt < nk) step(kt, pa, pb, qa, qb);
+  // epilogue: accumulators (+ bias) -> bf16 tile image in LDS (C/D map col = lane&15,
+  // row = (lane>>4)*4 + r), then 16-B row-contiguous stores of 8 output channels
+  // (the loop above ended with a barrier, so the staging images are free)
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int col = n0 + wn * WN + j * 16 + (lane & 15);
-    if (col >= a.Ncol) continue;
-    const float b = a.bias ? a.bias[col] : 0.f;
+    const int cl = wn * WN + j * 16 + (lane & 15);
+    const float b = (a.bias && n0 + cl < a.Ncol) ? a.bias[n0 + cl] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (row < a.M) a.out[row * a.Ncol + col] = f2bf(acc[i][j][r] + b);
-      }
+      for (int r = 0; r < 4; ++r) smem[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * CST + cl] = f2bf(acc[i][j][r] + b);
+  }
+  __syncthreads();
+  constexpr int VPR = BN_ / 8;               // 16-B vectors per tile row
+#pragma unroll
+  for (int k = 0; k < CBM * VPR / 256; ++k) {
+    const int v = tid + 256 * k;
+    const int rl = v / VPR, cv = v % VPR;
+    const int64_t row = m0 + rl;
+    const int col = n0 + cv * 8;
+    if (row < a.M && col < a.Ncol) {
+      const int gi = col / a.ogc;
+      *reinterpret_cast<uint4 *>(a.out + (int64_t)gi * a.ogs + row * a.ogc + (col - gi * a.ogc)) =
+          *reinterpret_cast<const uint4 *>(&smem[rl * CST + cv * 8]);
+    }
   }
 }
 
@@ -173,33 +235,35 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(FwdArgs a) {
 // 16-B chunk ch of row r lives at 256*r + 16*(ch ^ swz(r)),
 // swz(r) = ((r&3)<<2) | ((r>>2)&3)  (T10 image (b): conflict-free tr reads).
 struct WgradArgs {
-  const bf16_t *x;       // [N, H, W, Cin]
+  const bf16_t *x;       // [N, H, W, Cin], grouped (xgc, xgs)
   const bf16_t *dy;      // [N, Ho, Wo, Cout]
-  float *part;           // [splits][Cout][9*Cin]
+  float *part;           // [splits][Cout][taps*Cin]
   float *dbias_part;     // [splits][Cout] partial bias gradients (sum of dy), or null
   ConvGeom g;
   int64_t M;             // N*Ho*Wo
   int64_t mper;          // pixels per split (multiple of 32)
+  int xgc;
+  int64_t xgs;
 };
 
 __device__ __forceinline__ int swz_off(int r, int ch) {
   return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
 }
 
-__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
+template <int KS>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2][2][CBK * 256];  // [buf][A/B][32 rows x 256 B]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int co0 = blockIdx.y * CBM;
   const int np0 = blockIdx.x * CBN;
-  const int NP = 9 * a.g.Cin;
+  const int NP = KS * KS * a.g.Cin;
   const int64_t mbeg = (int64_t)blockIdx.z * a.mper;
   const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
   const int nk = (int)((mend - mbeg + CBK - 1) / CBK);
 
   // staging: 32 rows x 16 chunks per operand = 512 vectors -> 2 per thread
   // vector v: row = v >> 4, chunk = v & 15
-  uint4 ra[2], rb[2];
   int vrow[2], vch[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -208,20 +272,20 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
     vch[u] = v & 15;
   }
   // the B chunk's (tap, ci) is fixed per thread
-  int btap[2], bci[2];
+  int tkh[2], tkw[2];
+  int64_t bgoff[2];      // grouped-layout offset of this chunk's channel
   bool bok[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int np = np0 + vch[u] * 8;
     bok[u] = np < NP;
-    btap[u] = bok[u] ? np / a.g.Cin : 0;
-    bci[u] = bok[u] ? np % a.g.Cin : 0;
+    const int btap = bok[u] ? np / a.g.Cin : 0;
+    const int bci = bok[u] ? np - btap * a.g.Cin : 0;
+    tkh[u] = btap / KS - a.g.pad;
+    tkw[u] = btap % KS - a.g.pad;
+    const int gi = bci / a.xgc;
+    bgoff[u] = (int64_t)gi * a.xgs + (bci - gi * a.xgc);
   }
-  const int bkh = 0, bkw = 0;
-  (void)bkh; (void)bkw;
-  int tkh[2], tkw[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) { tkh[u] = btap[u] / 3; tkw[u] = btap[u] % 3; }
   // pixel coordinates of each staged row, advanced by CBK pixels per K-tile
   // (no 64-bit div/mod in the loop)
   int pn[2], poh[2], pow_[2];
@@ -235,20 +299,16 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
   }
   const bool do_bias = a.dbias_part != nullptr && blockIdx.x == 0;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, uint4 (&ra)[2], uint4 (&rb)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t m = mbeg + (int64_t)kt * CBK + vrow[u];
+      const int co = co0 + vch[u] * 8;
       uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = va;
-      if (m < mend) {
-        const int co = co0 + vch[u] * 8;
-        if (co < a.g.Cout) va = *reinterpret_cast<const uint4 *>(a.dy + m * a.g.Cout + co);
-        if (bok[u]) {
-          const int ih = poh[u] * a.g.stride - 1 + tkh[u], iw = pow_[u] * a.g.stride - 1 + tkw[u];
-          if (ih >= 0 && ih < a.g.H && iw >= 0 && iw < a.g.W)
-            vb = *reinterpret_cast<const uint4 *>(a.x + (((int64_t)pn[u] * a.g.H + ih) * a.g.W + iw) * a.g.Cin + bci[u]);
-        }
-      }
+      if (m < mend && co < a.g.Cout) va = *reinterpret_cast<const uint4 *>(a.dy + m * a.g.Cout + co);
+      const int ih = poh[u] * a.g.stride + tkh[u], iw = pow_[u] * a.g.stride + tkw[u];
+      if (m < mend && bok[u] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
+        vb = *reinterpret_cast<const uint4 *>(a.x + bgoff[u] + (((int64_t)pn[u] * a.g.H + ih) * a.g.W + iw) * a.xgc);
       ra[u] = va;
       rb[u] = vb;
       pow_[u] += CBK;
@@ -258,7 +318,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
       }
     }
   };
-  auto bias_acc = [&]() {
+  auto bias_acc = [&](const uint4 (&ra)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned wv[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
@@ -269,7 +329,8 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[2], const uint4 (&rb)[2]) {
+    if (do_bias) bias_acc(ra);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       *reinterpret_cast<uint4 *>(&smem[buf][0][swz_off(vrow[u], vch[u])]) = ra[u];
@@ -292,20 +353,11 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    load_tile(0);
-    if (do_bias) bias_acc();
-    store_tile(0);
-  }
-  __syncthreads();
   const int g = lane >> 4;  // k rows 8g .. 8g+7 of the 32-row tile
-  for (int kt = 0; kt < nk; ++kt) {
+  // same two-deep register prefetch as the fwd kernel
+  auto step = [&](int kt, uint4 (&na)[2], uint4 (&nb)[2], const uint4 (&ra)[2], const uint4 (&rb)[2]) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_tile(kt + 1);
-      if (do_bias) bias_acc();
-    }
+    if (kt + 2 < nk) load_tile(kt + 2, na, nb);
     cbf16x8 af[4], bfr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -325,9 +377,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) store_tile(cur ^ 1);
+    if (kt + 1 < nk) store_tile(cur ^ 1, ra, rb);
     __syncthreads();
+  };
+  uint4 pa[2], pb[2], qa[2], qb[2];
+  if (nk > 0) {
+    load_tile(0, pa, pb);
+    if (nk > 1) load_tile(1, qa, qb);
+    store_tile(0, pa, pb);
   }
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, pa, pb, qa, qb);
+    step(kt + 1, qa, qb, pa, pb);
+  }
+  if (kt < nk) step(kt, pa, pb, qa, qb);
   if (do_bias) {
     // threads with equal (tid & 15) hold the same 8 channels: lanes l, l^16, l^32, l^48
     // in a wave, then the 4 waves through LDS (the staging buffers are free now)
@@ -364,12 +429,12 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// dW[co][ci][kh][kw] (= or +=) sum over splits of part[s][co][tap*Cin + ci]
-__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
-                                                                  int Cout, int Cin, int splits, int accumulate,
-                                                                  const float *__restrict__ dbias_part,
-                                                                  float *__restrict__ dbias) {
-  const int64_t NP = 9 * (int64_t)Cin;
+// dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
+                                                                int Cout, int Cin, int taps, int splits, int accumulate,
+                                                                const float *__restrict__ dbias_part,
+                                                                float *__restrict__ dbias) {
+  const int64_t NP = taps * (int64_t)Cin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in part layout
   if (dbias && i < Cout) {
     float sb = 0.f;
@@ -382,54 +447,67 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float *
   const int co = (int)(i / NP);
   const int np = (int)(i % NP);
   const int tap = np / Cin, ci = np % Cin;
-  const int64_t o = ((int64_t)co * Cin + ci) * 9 + tap;
+  const int64_t o = ((int64_t)co * Cin + ci) * taps + tap;
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
-// pack fp32 W [Cout][Cin][3][3] -> bf16 [Cout][9][Cin] (fwd) or [Cin][9][Cout] (dgrad)
-__global__ __launch_bounds__(256) void conv3x3_pack_kernel(const float *__restrict__ w, bf16_t *__restrict__ wp,
-                                                          int Cout, int Cin, int Cin_pad, int transposed) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)Cout * Cin_pad * 9;
+// pack fp32 W (element (co, ci, tap) at co*s_co + ci*s_ci + tap*s_tap: any of the
+// parameter's memory formats) -> bf16 [Cout][taps][Cin_pad] (fwd, wp) and/or
+// [Cin_pad][taps][Cout] (dgrad, wp_t) in one pass; ci >= Cin packs zeros
+__global__ __launch_bounds__(256) void conv_pack_kernel(const float *__restrict__ w, int64_t s_co, int64_t s_ci,
+                                                        int64_t s_tap, bf16_t *__restrict__ wp,
+                                                        bf16_t *__restrict__ wp_t, int Cout, int Cin, int Cin_pad,
+                                                        int taps) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // index in the fwd layout
+  const int64_t total = (int64_t)Cout * Cin_pad * taps;
   if (i >= total) return;
-  // i enumerates the packed layout
-  int co, ci, tap;
-  if (!transposed) {            // [Cout][9][Cin_pad]
-    ci = (int)(i % Cin_pad);
-    tap = (int)((i / Cin_pad) % 9);
-    co = (int)(i / ((int64_t)Cin_pad * 9));
-  } else {                      // [Cin_pad][9][Cout]
-    co = (int)(i % Cout);
-    tap = (int)((i / Cout) % 9);
-    ci = (int)(i / ((int64_t)Cout * 9));
-  }
-  const float v = ci < Cin ? w[((int64_t)co * Cin + ci) * 9 + tap] : 0.f;
-  wp[i] = f2bf(v);
+  const int ci = (int)(i % Cin_pad);
+  const int tap = (int)((i / Cin_pad) % taps);
+  const int co = (int)(i / ((int64_t)Cin_pad * taps));
+  const bf16_t v = f2bf(ci < Cin ? w[co * s_co + ci * s_ci + tap * s_tap] : 0.f);
+  if (wp) wp[i] = v;
+  if (wp_t) wp_t[((int64_t)ci * taps + tap) * Cout + co] = v;
 }
 
-// Ncol <= 64 (the fusion conv's input gradient: 56 channels) uses the 128x64 tile
-template <bool DGRAD>
-static void launch_fwd(const FwdArgs &a, hipStream_t s) {
+// Ncol <= 64 (e.g. the fusion conv's 56-channel input gradient) uses the 128x64 tile
+template <bool DGRAD, int KS>
+static void launch_fwd_ks(const FwdArgs &a, hipStream_t s) {
   if (a.Ncol <= 64) {
     dim3 grid((unsigned)((a.M + CBM - 1) / CBM), 1);
-    hipLaunchKernelGGL((conv3x3_fwd_kernel<DGRAD, 64>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 64, KS>), grid, dim3(256), 0, s, a);
   } else {
     dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
-    hipLaunchKernelGGL((conv3x3_fwd_kernel<DGRAD, 128>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 128, KS>), grid, dim3(256), 0, s, a);
   }
+}
+
+template <bool DGRAD>
+static void launch_fwd(const FwdArgs &a, hipStream_t s) {
+  if (a.g.ks == 1) launch_fwd_ks<DGRAD, 1>(a, s);
+  else launch_fwd_ks<DGRAD, 3>(a, s);
 }
 
 static int check_geom(const ConvGeom &g, const char *nm) {
   EWVIT_CHECK_ARG(g.N > 0 && g.H > 0 && g.W > 0 && g.Cin > 0 && g.Cout > 0, "%s: empty shape", nm);
   EWVIT_CHECK_ARG(g.Cin % 8 == 0 && g.Cout % 8 == 0, "%s: Cin=%d Cout=%d must be multiples of 8", nm, g.Cin, g.Cout);
   EWVIT_CHECK_ARG(g.stride == 1 || g.stride == 2, "%s: stride %d", nm, g.stride);
-  EWVIT_CHECK_ARG(g.Ho == (g.H - 1) / g.stride + 1 && g.Wo == (g.W - 1) / g.stride + 1, "%s: output size", nm);
+  EWVIT_CHECK_ARG(g.ks == 1 || g.ks == 3, "%s: kernel size %d (1 or 3)", nm, g.ks);
   return 0;
 }
 
-static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride) {
+// grouped layout (gc, gs) for a tensor of C channels: gc == 0 means plain NHWC
+static int check_group(int64_t &gc, int64_t &gs, int64_t C, int64_t pixels, const char *nm, const char *which) {
+  if (gc == 0 || gc == C) { gc = C; gs = 0; return 0; }
+  EWVIT_CHECK_ARG(gc > 0 && gc % CBK == 0 && C % gc == 0, "%s: %s group width %lld must divide %lld and be a multiple of %d",
+                  nm, which, (long long)gc, (long long)C, CBK);
+  EWVIT_CHECK_ARG(gs >= pixels * gc, "%s: %s group stride %lld < %lld", nm, which, (long long)gs, (long long)(pixels * gc));
+  return 0;
+}
+
+static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ks, int stride) {
   ConvGeom g;
   g.N = (int)N; g.H = (int)H; g.W = (int)W; g.Cin = (int)Cin; g.Cout = (int)Cout; g.stride = stride;
+  g.ks = ks; g.pad = ks / 2;
   g.Ho = (int)((H - 1) / stride + 1);
   g.Wo = (int)((W - 1) / stride + 1);
   return g;
@@ -439,78 +517,101 @@ static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, 
 
 using namespace ewvit;
 
-extern "C" int ewvit_conv3x3_pack_weight(const float *w, void *wp, int64_t Cout, int64_t Cin, int64_t Cin_pad,
-                                         int transposed, void *stream) {
-  EWVIT_CHECK_ARG(w && wp && Cout > 0 && Cin > 0 && Cin_pad >= Cin, "conv3x3_pack_weight: bad args");
-  const int64_t total = Cout * Cin_pad * 9;
-  hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), w,
-                     (bf16_t *)wp, (int)Cout, (int)Cin, (int)Cin_pad, transposed);
-  return launch_status("conv3x3_pack_weight");
+extern "C" int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t s_tap, void *wp,
+                                        void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
+                                        void *stream) {
+  EWVIT_CHECK_ARG(w && (wp || wp_t) && Cout > 0 && Cin > 0 && Cin_pad >= Cin, "conv2d_pack_weight: bad args");
+  EWVIT_CHECK_ARG(ksize == 1 || ksize == 3, "conv2d_pack_weight: kernel size %d", ksize);
+  const int taps = ksize * ksize;
+  const int64_t total = Cout * Cin_pad * taps;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), w,
+                     s_co, s_ci, s_tap, (bf16_t *)wp, (bf16_t *)wp_t, (int)Cout, (int)Cin, (int)Cin_pad, taps);
+  return launch_status("conv2d_pack_weight");
 }
 
-extern "C" int ewvit_conv3x3_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
-                                 int64_t W, int64_t Cin, int64_t Cout, int stride, void *stream) {
-  EWVIT_CHECK_ARG(x && wp && y, "conv3x3_fwd: null pointer");
-  ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
-  if (int rc = check_geom(g, "conv3x3_fwd")) return rc;
+extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                                int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
+                                int64_t x_group_stride, void *stream) {
+  EWVIT_CHECK_ARG(x && wp && y, "conv2d_fwd: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_fwd")) return rc;
+  if (int rc = check_group(x_group_c, x_group_stride, Cin, N * H * W, "conv2d_fwd", "x")) return rc;
   FwdArgs a;
   a.src = (const bf16_t *)x; a.wp = (const bf16_t *)wp; a.bias = bias; a.out = (bf16_t *)y; a.g = g;
   a.M = (int64_t)g.N * g.Ho * g.Wo; a.Ncol = g.Cout; a.KC = g.Cin;
   a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
+  a.sgc = (int)x_group_c; a.sgs = x_group_stride; a.ogc = g.Cout; a.ogs = 0;
   launch_fwd<false>(a, as_stream(stream));
-  return launch_status("conv3x3_fwd");
+  return launch_status("conv2d_fwd");
 }
 
-extern "C" int ewvit_conv3x3_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
-                                      int64_t Cin, int64_t Cout, int stride, void *stream) {
-  EWVIT_CHECK_ARG(dy && wp_t && dx, "conv3x3_bwd_data: null pointer");
-  ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
-  if (int rc = check_geom(g, "conv3x3_bwd_data")) return rc;
+extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
+                                     int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
+                                     int64_t dx_group_stride, void *stream) {
+  EWVIT_CHECK_ARG(dy && wp_t && dx, "conv2d_bwd_data: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_bwd_data")) return rc;
+  if (int rc = check_group(dx_group_c, dx_group_stride, Cin, N * H * W, "conv2d_bwd_data", "dx")) return rc;
   FwdArgs a;
   a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx; a.g = g;
   a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
+  a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
   launch_fwd<true>(a, as_stream(stream));
-  return launch_status("conv3x3_bwd_data");
+  return launch_status("conv2d_bwd_data");
 }
 
+// split of the pixel reduction: ~768 workgroups (3 per CU), >= 32 K-tiles per split,
+// and f32 partial slabs no larger than half the bf16 operands they reduce
 static int64_t wgrad_splits(const ConvGeom &g) {
   const int64_t M = (int64_t)g.N * g.Ho * g.Wo;
-  const int64_t tiles = ((9 * (int64_t)g.Cin + CBN - 1) / CBN) * ((g.Cout + CBM - 1) / CBM);
-  int64_t s = (512 + tiles - 1) / tiles;          // aim at >= 512 workgroups
-  const int64_t maxs = (M + 32 * CBK - 1) / (32 * CBK);  // >= 32 K-tiles per split
+  const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
+  const int64_t tiles = ((NP + CBN - 1) / CBN) * ((g.Cout + CBM - 1) / CBM);
+  int64_t s = (768 + tiles - 1) / tiles;
+  const int64_t maxs = (M + 32 * CBK - 1) / (32 * CBK);
   if (s > maxs) s = maxs;
+  const int64_t cap = M * ((int64_t)g.Cin + g.Cout) / (4 * (int64_t)g.Cout * NP);
+  if (s > cap) s = cap;
   if (s < 1) s = 1;
   return s;
 }
 
-extern "C" int64_t ewvit_conv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
-                                                      int stride) {
-  ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
-  return wgrad_splits(g) * Cout * (9 * Cin + 1) * (int64_t)sizeof(float);
+extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                                     int ksize, int stride) {
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  return wgrad_splits(g) * Cout * (ksize * ksize * Cin + 1) * (int64_t)sizeof(float);
 }
 
-extern "C" int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
-                                        int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
-                                        float *workspace, void *stream) {
-  EWVIT_CHECK_ARG(x && dy && dw && workspace, "conv3x3_bwd_weight: null pointer");
-  ConvGeom g = mkg(N, H, W, Cin, Cout, stride);
-  if (int rc = check_geom(g, "conv3x3_bwd_weight")) return rc;
+extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
+                                       int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                       int stride, int64_t x_group_c, int64_t x_group_stride, float *workspace,
+                                       void *stream) {
+  EWVIT_CHECK_ARG(x && dy && dw && workspace, "conv2d_bwd_weight: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_bwd_weight")) return rc;
+  if (int rc = check_group(x_group_c, x_group_stride, Cin, N * H * W, "conv2d_bwd_weight", "x")) return rc;
+  const int taps = ksize * ksize;
   WgradArgs a;
   a.x = (const bf16_t *)x; a.dy = (const bf16_t *)dy; a.part = workspace; a.g = g;
-  a.dbias_part = dbias ? workspace + wgrad_splits(g) * g.Cout * 9 * (int64_t)g.Cin : nullptr;
-  a.M = (int64_t)g.N * g.Ho * g.Wo;
+  a.xgc = (int)x_group_c; a.xgs = x_group_stride;
   const int64_t splits = wgrad_splits(g);
+  a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
+  a.M = (int64_t)g.N * g.Ho * g.Wo;
   int64_t mper = (a.M + splits - 1) / splits;
   mper = (mper + CBK - 1) / CBK * CBK;
   a.mper = mper;
   const int sp = (int)((a.M + mper - 1) / mper);
-  dim3 grid((unsigned)((9 * g.Cin + CBN - 1) / CBN), (unsigned)((g.Cout + CBM - 1) / CBM), (unsigned)sp);
+  // one split of a 1x1 conv: the slab IS dW [Cout][Cin] (and dbias) — no reduce pass
+  const bool direct = sp == 1 && taps == 1 && !accumulate;
+  if (direct) { a.part = dw; a.dbias_part = dbias; }
+  dim3 grid((unsigned)((taps * g.Cin + CBN - 1) / CBN), (unsigned)((g.Cout + CBM - 1) / CBM), (unsigned)sp);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, grid, dim3(256), 0, s, a);
-  if (int rc = launch_status("conv3x3_bwd_weight")) return rc;
-  const int64_t n = (int64_t)g.Cout * 9 * g.Cin;
-  hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, workspace, dw,
-                     g.Cout, g.Cin, sp, accumulate, a.dbias_part, dbias);
-  return launch_status("conv3x3_bwd_weight reduce");
+  if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), 0, s, a);
+  if (int rc = launch_status("conv2d_bwd_weight")) return rc;
+  if (direct) return 0;
+  const int64_t n = (int64_t)g.Cout * taps * g.Cin;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, workspace, dw,
+                     g.Cout, g.Cin, taps, sp, accumulate, a.dbias_part, dbias);
+  return launch_status("conv2d_bwd_weight reduce");
 }

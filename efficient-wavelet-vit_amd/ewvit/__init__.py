@@ -4,11 +4,11 @@ C-ABI: include/ewvit.h, built into ewvit/libewvit.so from csrc/*.hip.
 """
 from . import _lib
 from .bn import batch_norm_act, batch_norm_act_params
-from .conv import conv3x3
+from .conv import conv2d, conv3x3
 from .ops import (attention_cross, attention_packed, colsum, dwconv3x3, dwt_haar, dwt_hf_upsample, gemm,
                   hf_upsample, layer_norm, linear, mm_nn, mm_nt, mm_tn)
 
-__all__ = ['attention_cross', 'attention_packed', 'colsum', 'conv3x3', 'dwconv3x3', 'dwt_haar', 'dwt_hf_upsample', 'gemm',
+__all__ = ['attention_cross', 'attention_packed', 'colsum', 'conv2d', 'conv3x3', 'dwconv3x3', 'dwt_haar', 'dwt_hf_upsample', 'gemm',
            'hf_upsample', 'layer_norm', 'linear', 'mm_nn', 'mm_nt', 'mm_tn', 'load_library']
 
 

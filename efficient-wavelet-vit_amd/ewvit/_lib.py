@@ -34,12 +34,13 @@ SIGNATURES = {
     'ewvit_dwconv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     'ewvit_dwconv3x3_bwd_weight': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp],
     'ewvit_bn_fwd': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _f32, _f32, _i32, _vp, _vp, _i32, _vp,
-                     _vp],
+                     _vp, _vp],
     'ewvit_bn_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
-    'ewvit_conv3x3_pack_weight': [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
-    'ewvit_conv3x3_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
-    'ewvit_conv3x3_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp],
-    'ewvit_conv3x3_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
+    'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
+    'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
+    'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
+    'ewvit_conv2d_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64,
+                                _vp, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
 }
@@ -47,7 +48,7 @@ SIGNATURES = {
 # size queries: name -> (restype, argtypes)
 QUERIES = {
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
-    'ewvit_conv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32]),
+    'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
 }
 

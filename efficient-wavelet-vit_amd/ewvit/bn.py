@@ -23,7 +23,7 @@ def _rows(x):
 
 class BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups):
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups, counter):
         L.require_gpu(x)
         xc, M, C = _rows(x)
         if M % groups:
@@ -34,7 +34,7 @@ class BatchNormActFn(torch.autograd.Function):
         invstd = torch.empty_like(mean) if training else None
         L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(running_mean), L.ptr(running_var), int(training), float(momentum), float(eps), act,
-               L.ptr(mean), L.ptr(invstd), groups, L.ptr(ws), L.stream(y),
+               L.ptr(mean), L.ptr(invstd), groups, L.ptr(counter if training else None), L.ptr(ws), L.stream(y),
                work={'bytes': (2 + int(training)) * xc.numel() * xc.element_size()})
         if training:
             ctx.save_for_backward(xc, weight, bias, mean, invstd)
@@ -56,7 +56,7 @@ class BatchNormActFn(torch.autograd.Function):
         L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), 0, groups, L.ptr(ws), L.stream(dx),
                work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return dx, dg, db, None, None, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, bn, act=None, training=None, groups=1):
@@ -66,17 +66,20 @@ def batch_norm_act(x, bn, act=None, training=None, groups=1):
     training = bn.training if training is None else training
     if bn.momentum is None:
         raise NotImplementedError('cumulative-average BatchNorm (momentum=None) is not used by the model')
-    if training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(groups)
+    counter = bn.num_batches_tracked if training and bn.track_running_stats else None
     return batch_norm_act_params(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, training,
-                                 bn.momentum, bn.eps, act, groups)
+                                 bn.momentum, bn.eps, act, groups, counter)
 
 
 def batch_norm_act_params(x, weight, bias, running_mean, running_var, training, momentum, eps, act=None,
-                          groups=1):
+                          groups=1, counter=None):
+    """`counter`: an int64 device tensor (a module's num_batches_tracked) the
+    forward kernel increments by `groups` in training, or None."""
     if x.dtype not in (torch.float32, torch.bfloat16):
         x = x.float()
     if not training:
         groups = 1
+    if counter is not None and (counter.dtype != torch.int64 or counter.device != x.device):
+        raise ValueError('batch_norm_act: counter must be an int64 tensor on the input device')
     return BatchNormActFn.apply(x, weight, bias, running_mean, running_var, bool(training), momentum, eps,
-                                ACT[act], int(groups))
+                                ACT[act], int(groups), counter)

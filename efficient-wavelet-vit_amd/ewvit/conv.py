@@ -1,81 +1,108 @@
-"""3x3 convolution (pad 1, stride 1|2, bias) on the ewvit implicit-GEMM kernels
-(csrc/conv.hip) — the MWT conv stack of network/mwt.py:23-72.
+"""Dense Conv2d (kernel 1|3, pad k/2, stride 1|2, bias) on the ewvit implicit-GEMM
+kernels (csrc/conv.hip) — the MWT conv stack of network/mwt.py:23-72 and the
+backbone's dense convs.
 
 Activations are channels-last bf16 (the MFMA operand type); weights stay fp32
-master parameters and are packed to bf16 [Cout][9][Cin] each call.  An input
+master parameters and are packed to bf16 [Cout][k*k][Cin] each call.  An input
 may carry zero-padded channels (Cin_x > weight.shape[1]): the pack fills those
 weight rows with zeros, so they contribute exactly nothing and receive no
 gradient.
+
+``levels > 1`` reads a level-major input ``z [levels*N, C, H, W]`` as the
+channel concatenation ``cat(z.chunk(levels), dim=1)`` ([N, levels*C, H, W], the
+multiscale fusion input of mwt.py:112) through the kernels' grouped layout, and
+returns the input gradient in z's layout — the concatenation is never built.
 """
 import torch
 
 from . import _lib as L
 
 
+def _pack(weight, cin_pad, fwd=True, bwd=False):
+    """bf16 packs of the fp32 weight (read in its own memory format): the fwd
+    layout [Cout][k*k][cin_pad] and/or the bwd_data layout [cin_pad][k*k][Cout],
+    one launch."""
+    Cout, Cin, k = weight.shape[0], weight.shape[1], weight.shape[2]
+    w = weight.detach()
+    if w.dtype != torch.float32:
+        w = w.float()
+    s_co, s_ci, s_kh, s_kw = w.stride()
+    if s_kh != k * s_kw:
+        w = w.contiguous()
+        s_co, s_ci, s_kh, s_kw = w.stride()
+    wp = torch.empty((Cout, k * k, cin_pad), dtype=torch.bfloat16, device=w.device) if fwd else None
+    wpt = torch.empty((cin_pad, k * k, Cout), dtype=torch.bfloat16, device=w.device) if bwd else None
+    L.call('ewvit_conv2d_pack_weight', L.ptr(w), s_co, s_ci, s_kw, L.ptr(wp), L.ptr(wpt), Cout, Cin, cin_pad, k,
+           L.stream(w))
+    return wp, wpt
 
-def _pack(weight, cin_pad, transposed):
-    Cout, Cin = weight.shape[0], weight.shape[1]
-    w = weight.detach().float().contiguous()
-    shape = (Cout, 9, cin_pad) if not transposed else (cin_pad, 9, Cout)
-    wp = torch.empty(shape, dtype=torch.bfloat16, device=weight.device)
-    L.call('ewvit_conv3x3_pack_weight', L.ptr(w), L.ptr(wp), Cout, Cin, cin_pad, int(transposed), L.stream(wp))
-    return wp
 
-
-class Conv3x3Fn(torch.autograd.Function):
+class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride):
+    def forward(ctx, x, weight, bias, stride, levels):
         L.require_gpu(x, weight)
-        N, Cx, H, W = x.shape
-        Cout, Cin = weight.shape[0], weight.shape[1]
-        if Cx < Cin or weight.shape[2:] != (3, 3):
-            raise ValueError(f'conv3x3: input has {Cx} channels, weight {tuple(weight.shape)}')
+        NL, Cz, H, W = x.shape
+        if NL % levels:
+            raise ValueError(f'conv2d: batch {NL} is not a multiple of levels={levels}')
+        N, Cx = NL // levels, Cz * levels
+        Cout, Cin, k = weight.shape[0], weight.shape[1], weight.shape[2]
+        if Cx < Cin or weight.shape[3] != k or k not in (1, 3) or (levels > 1 and Cx != Cin):
+            raise ValueError(f'conv2d: input {tuple(x.shape)} (levels={levels}), weight {tuple(weight.shape)}')
         xc = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        wp = _pack(weight, Cx, False)
+        gc, gs = (Cz, N * H * W * Cz) if levels > 1 else (0, 0)
+        wp, wpt = _pack(weight, Cx, True, ctx.needs_input_grad[0])
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = bias.detach().float().contiguous() if bias is not None else None
-        work = {'flops': 2.0 * N * Ho * Wo * Cout * 9 * Cx, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
-        L.call('ewvit_conv3x3_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, stride,
+        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
+        L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc, gs,
                L.stream(y), work=work)
-        ctx.save_for_backward(xc, weight)
-        ctx.cfg = (stride, bias is not None, x.dtype)
-        return y
+        ctx.save_for_backward(xc, weight, wpt)
+        ctx.cfg = (stride, levels, bias is not None, x.dtype)
+        # bf16 MFMA product; an fp32 caller (no autocast) gets fp32 back
+        return y if x.dtype == torch.bfloat16 else y.to(x.dtype).contiguous(memory_format=torch.channels_last)
 
     @staticmethod
     def backward(ctx, dy):
-        xc, weight = ctx.saved_tensors
-        stride, has_bias, xdt = ctx.cfg
-        N, Cx, H, W = xc.shape
-        Cout, Cin = weight.shape[0], weight.shape[1]
+        xc, weight, wpt = ctx.saved_tensors
+        stride, levels, has_bias, xdt = ctx.cfg
+        NL, Cz, H, W = xc.shape
+        N, Cx = NL // levels, Cz * levels
+        gc, gs = (Cz, N * H * W * Cz) if levels > 1 else (0, 0)
+        Cout, Cin, k = weight.shape[0], weight.shape[1], weight.shape[2]
         Ho, Wo = dy.shape[2], dy.shape[3]
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wpt = _pack(weight, Cx, True)
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
-            work = {'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            L.call('ewvit_conv3x3_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, stride,
+            work = {'flops': 2.0 * N * H * W * Cx * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
+            L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, stride, gc, gs,
                    L.stream(dx), work=work)
             if xdt != torch.bfloat16:
                 dx = dx.to(xdt)
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
-            wsb = L.load().ewvit_conv3x3_bwd_weight_workspace(N, H, W, Cx, Cout, stride)
+            wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            dwf = torch.empty((Cout, Cx, 3, 3), dtype=torch.float32, device=xc.device)
+            dwf = torch.empty((Cout, Cx, k, k), dtype=torch.float32, device=xc.device)
             dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device) if want_b else None
-            work = {'flops': 2.0 * N * Ho * Wo * Cout * 9 * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
-            L.call('ewvit_conv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
-                   Cout, stride, L.ptr(ws), L.stream(dwf), work=work)
+            work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
+            L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
+                   Cout, k, stride, gc, gs, L.ptr(ws), L.stream(dwf), work=work)
             if ctx.needs_input_grad[1]:
                 dw = dwf if Cx == Cin else dwf[:, :Cin]
                 if dw.stride() != weight.stride():     # keep the parameter's layout (DDP bucket views)
                     dw = torch.empty_like(weight, dtype=torch.float32).copy_(dw)
             db = dbf
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, levels=1):
+    """Conv2d(kernel 1|3, padding k//2, stride) — NCHW logical / channels-last bf16 output.
+    levels > 1: x is level-major [levels*N, C, H, W], convolved as cat(x.chunk(levels), 1)."""
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(levels))
 
 
 def conv3x3(x, weight, bias=None, stride=1):
-    """Conv2d(kernel 3, padding 1, stride) — NCHW logical / channels-last bf16 output."""
-    return Conv3x3Fn.apply(x, weight, bias, int(stride))
+    """Conv2d(kernel 3, padding 1, stride)."""
+    return Conv2dFn.apply(x, weight, bias, int(stride), 1)

@@ -4,8 +4,8 @@
 
 Module tree and parameter names follow torchvision's published model so
 reference checkpoints load key-for-key (``features.{stage}.{block}.block.{i}...``).
-Layout: the backbone runs channels-last (NHWC), which MIOpen's bf16 implicit-GEMM
-kernels and the ewvit head both want (the 7x7x1280 map is then already the
+Layout: the backbone runs channels-last (NHWC), which the ewvit conv / depthwise /
+BatchNorm kernels and the ewvit head all want (the 7x7x1280 map is then already the
 ``(p1 p2 c)`` patch vector of sfe.py:153).
 
 Stages (expand, kernel, stride, in, out, blocks): FusedMBConv (1,3,1,24,24,2)
@@ -41,12 +41,27 @@ class DepthwiseConv2d(nn.Conv2d):
         return ewvit.dwconv3x3(x, self.weight, self.stride[0], self.padding[0])
 
 
+class Conv2d(nn.Conv2d):
+    """Dense 1x1 / 3x3 conv (padding k//2, no dilation, groups 1) on the ewvit MFMA
+    implicit-GEMM kernels (csrc/conv.hip) when both channel counts are multiples
+    of 8; the 3-channel stem stays on the library conv.  Parameters identical to
+    nn.Conv2d."""
+
+    def forward(self, x):
+        k = self.kernel_size[0]
+        if (x.is_cuda and k in (1, 3) and self.kernel_size[1] == k and self.groups == 1 and
+                self.padding == (k // 2, k // 2) and self.dilation == (1, 1) and self.stride[0] == self.stride[1] and
+                self.in_channels % 8 == 0 and self.out_channels % 8 == 0 and x.shape[1] == self.in_channels):
+            return ewvit.conv2d(x, self.weight, self.bias, self.stride[0])
+        return super().forward(x)
+
+
 class ConvBNAct(nn.Sequential):
     """conv -> BatchNorm2d(eps 1e-3) [-> SiLU]; BN and SiLU run as ONE fused ewvit
     pass (csrc/batchnorm.hip) over the channels-last conv output."""
 
     def __init__(self, cin, cout, k, stride=1, groups=1, act=True):
-        conv = DepthwiseConv2d if (groups == cin == cout and groups > 1 and k == 3) else nn.Conv2d
+        conv = DepthwiseConv2d if (groups == cin == cout and groups > 1 and k == 3) else Conv2d
         mods = [conv(cin, cout, k, stride, (k - 1) // 2, groups=groups, bias=False),
                 nn.BatchNorm2d(cout, eps=1e-3)]
         if act:

@@ -9,8 +9,12 @@ Hot path on MI355X:
   mwt.py:84-86) run as ONE grouped conv (groups=3) over all levels at once
   (weights are shared by the levels, mwt.py:108), likewise ``hf_conv['fusion']``;
   BatchNorm statistics and running-stat updates stay per level and in the
-  reference's order, so train-mode numerics and state are the reference's.
-The conv stack itself is MIOpen (bf16 NHWC under autocast) in this round.
+  reference's order, so train-mode numerics and state are the reference's;
+* the fusion / multiscale / freq convs run on the ewvit MFMA implicit-GEMM conv
+  (csrc/conv.hip); multiscale_fusion reads the level-major fusion outputs as their
+  channel concatenation in place (no torch.cat of mwt.py:112 in HBM);
+* BatchNorm + ReLU are one fused ewvit pass (csrc/batchnorm.hip).
+The seperate conv (9 -> 54 channels) is still the library conv (MIOpen).
 
 If ``wavelet_transform`` is overridden on the instance or class (as
 utils/visualize_feature_maps.py:151-158 does), forward falls back to the
@@ -49,11 +53,17 @@ class Conv3x3(nn.Conv2d):
     """nn.Conv2d(k=3, pad=1) on the ewvit MFMA implicit-GEMM kernels (csrc/conv.hip)
     for channels-last inputs whose channel count is a multiple of 8 (extra input
     channels beyond in_channels must be zero padding); other inputs (the 3-channel
-    per-level path of `wavelet_transform`) go to the library conv."""
+    per-level path of `wavelet_transform`) go to the library conv.
+    ``levels > 1``: x is level-major [levels*B, C, H, W] and the conv input is
+    cat(x.chunk(levels), dim=1), read in place by the kernel."""
 
-    def forward(self, x):
-        if x.is_cuda and x.shape[1] % 8 == 0 and x.shape[1] >= self.in_channels and self.out_channels % 8 == 0:
-            return ewvit.conv3x3(x, self.weight, self.bias, self.stride[0])
+    def forward(self, x, levels=1):
+        C = x.shape[1] * levels
+        if x.is_cuda and C % 8 == 0 and C >= self.in_channels and self.out_channels % 8 == 0 and \
+                (levels == 1 or (x.shape[1] % 32 == 0 and C == self.in_channels)):
+            return ewvit.conv2d(x, self.weight, self.bias, self.stride[0], levels)
+        if levels > 1:
+            x = torch.cat(x.chunk(levels), dim=1)
         return super().forward(x[:, :self.in_channels])
 
 
@@ -62,10 +72,11 @@ def _fusable(bn, y):
 
 
 class CBR(nn.Sequential):
-    """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass."""
+    """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass.
+    ``levels``: see Conv3x3.forward."""
 
-    def forward(self, x):
-        y = self[0](x)
+    def forward(self, x, levels=1):
+        y = self[0](x, levels) if levels > 1 else self[0](x)
         if _fusable(self[1], y):
             return ewvit.batch_norm_act(y, self[1], 'relu')
         return self[2](self[1](y))
@@ -164,10 +175,11 @@ class MWT(nn.Module):
                 cur = ll
             fused = self.multiscale_fusion(torch.cat(highs, dim=1))
             return self.freq_pool(self.freq_conv(fused))
-        return self.freq_pool(self.freq_conv(self.multiscale_fusion(self._hf_features(x))))
+        return self.freq_pool(self.freq_conv(self.multiscale_fusion(self._hf_features(x), self.levels)))
 
     def _hf_features(self, x):
-        """All levels' hf_compressed, concatenated on channels: [B, L*dim, H/2, W/2]."""
+        """All levels' hf_compressed, level-major [L*B, dim, H/2, W/2]; multiscale_fusion
+        consumes it as the channel concatenation of mwt.py:112 (CBR(levels=L))."""
         B, C, H, W = x.shape
         Lv = self.levels
         OH, OW = H // 2, W // 2
@@ -197,4 +209,4 @@ class MWT(nn.Module):
         z = fus[0](y)
         z = ewvit.batch_norm_act(z, fus[1], 'relu', groups=Lv) if _fusable(fus[1], z) else \
             torch.cat([fus[2](fus[1](z[l * B:(l + 1) * B])) for l in range(Lv)])
-        return torch.cat([z[l * B:(l + 1) * B] for l in range(Lv)], dim=1) if Lv > 1 else z
+        return z

@@ -169,13 +169,15 @@ int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int acc
  * with their OWN batch statistics (save_mean/invstd [groups][C]) and applies
  * the running-stat update once per group in order — the MWT calls its shared
  * hf_conv BatchNorms once per wavelet level (network/mwt.py:107-111), here all
- * levels are one launch.  `workspace` holds ewvit_bn_workspace(M, C, groups) bytes.
+ * levels are one launch.  `num_batches_tracked` (int64 on the device, or NULL) is
+ * incremented by `groups` in training, like the module's counter.
+ * `workspace` holds ewvit_bn_workspace(M, C, groups) bytes.
  */
 int64_t ewvit_bn_workspace(int64_t M, int64_t C, int groups);
 int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
                  const float *beta, float *running_mean, float *running_var, int training,
                  float momentum, float eps, int act, float *save_mean, float *save_invstd,
-                 int groups, float *workspace, void *stream);
+                 int groups, int64_t *num_batches_tracked, float *workspace, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -183,33 +185,46 @@ int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, 
                  const float *save_invstd, int act, float *dgamma, float *dbeta, int accumulate,
                  int groups, float *workspace, void *stream);
 
-/* ------------------------------------------------ 3x3 conv, implicit GEMM ---
- * Conv2d(k=3, pad=1, stride 1|2, bias) of the MWT conv stack: hf_conv['fusion']
- * (mwt.py:60-64), multiscale_fusion (mwt.py:68-72), freq_conv (mwt.py:23-36),
- * freq_pool's conv (mwt.py:38-44).  bf16 MFMA, fp32 accumulate, channels-last:
- *   x [N, H, W, Cin], y [N, Ho, Wo, Cout] (bf16); Cin, Cout % 8 == 0;
- *   Ho = (H-1)/stride + 1.  Weights are packed once per step from the fp32
- *   master [Cout][Cin][3][3] by ewvit_conv3x3_pack_weight:
- *   transposed=0 -> [Cout][9][Cin_pad] (fwd), 1 -> [Cin_pad][9][Cout] (bwd_data);
- *   input channels ci >= Cin are zero-filled up to Cin_pad.
+/* ------------------------------------------ dense conv, implicit GEMM ---
+ * Conv2d(kernel 1|3, pad kernel/2, stride 1|2, bias) — the MWT conv stack:
+ * hf_conv['fusion'] (mwt.py:60-64), multiscale_fusion (mwt.py:68-72), freq_conv
+ * (mwt.py:23-36), freq_pool's conv (mwt.py:38-44) — and the EfficientNetV2-S
+ * backbone's dense convs (sfe.py:111-113 -> torchvision Conv2dNormActivation).
+ * Replaces the cuDNN nn.Conv2d calls behind those modules.
+ * bf16 MFMA, fp32 accumulate, channels-last: x [N, H, W, Cin], y [N, Ho, Wo, Cout]
+ * (bf16); Cin, Cout % 8 == 0; Ho = (H-1)/stride + 1.  Weights are packed once per
+ * step from the fp32 master [Cout][Cin][k][k] (element (co, ci, kh*k+kw) at
+ * co*s_co + ci*s_ci + (kh*k+kw)*s_tap: contiguous or channels-last parameters) by
+ * ewvit_conv2d_pack_weight into wp [Cout][k*k][Cin_pad] (fwd) and/or
+ * wp_t [Cin_pad][k*k][Cout] (bwd_data), either may be NULL; input channels
+ * ci >= Cin are zero-filled up to Cin_pad.
+ * Grouped channels-last operands (x of fwd / bwd_weight, dx of bwd_data): channel c
+ * of pixel p lives at (c / group_c) * group_stride + p * group_c + c % group_c
+ * (elements); group_c = 0 means plain NHWC.  group_c must divide Cin and be a
+ * multiple of 32 — e.g. the MWT's per-level outputs [L][N][H][W][128] consumed as
+ * their channel concatenation (mwt.py:112) without a copy.
  */
-int ewvit_conv3x3_pack_weight(const float *w, void *wp, int64_t Cout, int64_t Cin, int64_t Cin_pad,
-                              int transposed, void *stream);
+int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t s_tap, void *wp,
+                             void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
+                             void *stream);
 /* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
-int ewvit_conv3x3_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
-                      int64_t W, int64_t Cin, int64_t Cout, int stride, void *stream);
+int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                     int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
+                     int64_t x_group_stride, void *stream);
 /* dx [N, H, W, Cin] from dy [N, Ho, Wo, Cout] and the transposed pack. */
-int ewvit_conv3x3_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
-                           int64_t Cin, int64_t Cout, int stride, void *stream);
-/* bytes of f32 split-K workspace for ewvit_conv3x3_bwd_weight. */
-int64_t ewvit_conv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
-                                           int stride);
-/* dw [Cout][Cin][3][3] f32 and, when dbias != NULL, the bias gradient dbias[Cout] =
+int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
+                          int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
+                          int64_t dx_group_stride, void *stream);
+/* bytes of f32 split-K workspace for ewvit_conv2d_bwd_weight. */
+int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                          int ksize, int stride);
+/* dw [Cout][Cin][k][k] f32 and, when dbias != NULL, the bias gradient dbias[Cout] =
  * sum of dy over pixels (fused: read from the dy tiles already staged), both
  * (= or +=) ; deterministic split-K + reduction. */
-int ewvit_conv3x3_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
-                             int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int stride,
-                             float *workspace, void *stream);
+int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
+                            int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                            int stride, int64_t x_group_c, int64_t x_group_stride, float *workspace,
+                            void *stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,8 @@ def ref_bn(x, w, b, rm, rv, training, act, groups):
 
 
 @pytest.mark.parametrize('shape,groups', [((64, 960, 14, 14), 1), ((6, 56, 20, 20), 3), ((4, 24, 33, 33), 1),
-                                          ((8, 1280, 7, 7), 1), ((64, 128), 1), ((6, 128, 12, 12), 2)])
+                                          ((8, 1280, 7, 7), 1), ((64, 128), 1), ((6, 128, 12, 12), 2),
+                                          ((48, 64, 56, 56), 3), ((64, 1536, 7, 7), 1), ((2, 2048, 3, 3), 1)])
 @pytest.mark.parametrize('act', [None, 'relu', 'silu'])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
 def test_bn_act_train(shape, groups, act, dtype):
@@ -51,13 +52,23 @@ def test_bn_act_train(shape, groups, act, dtype):
     xd.requires_grad_(True)
     wd, bd = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
     rm_d, rv_d = rm0.to(DEV), rv0.to(DEV)
-    y = ewvit.batch_norm_act_params(xd, wd, bd, rm_d, rv_d, True, 0.1, 1e-3, act, groups)
+    counter = torch.full((), 7, dtype=torch.int64, device=DEV)
+    y = ewvit.batch_norm_act_params(xd, wd, bd, rm_d, rv_d, True, 0.1, 1e-3, act, groups, counter)
     y.backward(dy.to(DEV))
+    assert int(counter) == 7 + groups
     tol = 2 ** -7 if dtype == torch.bfloat16 else 1e-4
     assert y.dtype == dtype
     assert rel(y.float(), yr) < tol
     assert rel(rm_d, rm_r) < 1e-4 and rel(rv_d, rv_r) < 1e-4
-    assert rel(xd.grad.float(), xr.grad) < (2e-2 if dtype == torch.bfloat16 else 2e-3)
+    # ReLU: where the reference pre-activation is within rounding of 0 the two
+    # implementations may take different sides of the kink (dx = 0 vs dy*k);
+    # compare dx away from it
+    keep = torch.ones_like(yr, dtype=torch.bool)
+    if act == 'relu':
+        with torch.no_grad():
+            z = ref_bn(x.float(), w, b, rm0.clone(), rv0.clone(), True, None, groups)
+        keep = z.abs() > 1e-5 * float(z.abs().max())
+    assert rel(xd.grad.float().cpu()[keep], xr.grad[keep]) < (2e-2 if dtype == torch.bfloat16 else 2e-3)
     assert rel(wd.grad, wr.grad) < 2e-3
     assert rel(bd.grad, br.grad) < 2e-3
 
@@ -76,7 +87,7 @@ def test_bn_act_eval(act):
 
 
 def test_bn_stats_stable_with_large_mean():
-    """Shifted sums + Chan merging: a large common offset must not destroy the variance."""
+    """Sums shifted by a sample of each channel: a large common offset must not destroy the variance."""
     import ewvit
     x = torch.randn(16, 64, 32, 32) * 0.01 + 300.0
     rm, rv = torch.zeros(64), torch.ones(64)

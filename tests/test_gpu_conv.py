@@ -1,5 +1,5 @@
-"""Implicit-GEMM 3x3 conv kernels (csrc/conv.hip) through the C-ABI, vs torch
-fp32 conv2d on the same bf16-rounded operands.
+"""Implicit-GEMM conv kernels (csrc/conv.hip, kernel 1x1 / 3x3) through the C-ABI,
+vs torch fp32 conv2d on the same bf16-rounded operands.
 
 Tolerance: outputs / input-grads are rounded to bf16 once (fp32 accumulation of
 bf16 products, so only summation order and the final rounding differ):
@@ -17,31 +17,37 @@ def rel(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
 
 
-@pytest.mark.parametrize('N,Cx,Cin,Cout,H,W,stride', [
-    (2, 64, 64, 128, 28, 28, 1),
-    (1, 384, 384, 128, 16, 16, 1),
-    (2, 128, 128, 128, 15, 13, 2),
-    (3, 64, 54, 128, 20, 20, 1),      # fusion: 54 real channels zero-padded to 64
-    (2, 32, 32, 64, 9, 9, 2),
-    (1, 8, 8, 8, 5, 7, 1),
+@pytest.mark.parametrize('N,Cx,Cin,Cout,H,W,stride,k', [
+    (2, 64, 64, 128, 28, 28, 1, 3),
+    (1, 384, 384, 128, 16, 16, 1, 3),
+    (2, 128, 128, 128, 15, 13, 2, 3),
+    (3, 64, 54, 128, 20, 20, 1, 3),      # fusion: 54 real channels zero-padded to 64
+    (2, 56, 54, 64, 12, 12, 1, 3),       # 56-channel input: K-tiles straddle taps
+    (2, 32, 32, 64, 9, 9, 2, 3),
+    (1, 8, 8, 8, 5, 7, 1, 3),
+    (2, 24, 24, 96, 17, 17, 2, 3),       # backbone FusedMBConv expand, stride 2
+    (2, 96, 96, 48, 14, 14, 1, 1),       # backbone 1x1 project
+    (2, 64, 64, 256, 7, 9, 1, 1),        # 1x1 expand
+    (1, 256, 256, 1280, 7, 7, 1, 1),     # head 1x1
+    (2, 48, 48, 24, 10, 11, 2, 1),       # 1x1 stride 2, K-tile straddles nothing
 ])
-def test_conv3x3_fwd_bwd(N, Cx, Cin, Cout, H, W, stride):
+def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k):
     import ewvit.conv as ec
-    g = torch.Generator().manual_seed(Cx * 7 + H)
+    g = torch.Generator().manual_seed(Cx * 7 + H + k)
     x = torch.randn(N, Cx, H, W, generator=g).to(torch.bfloat16)
     if Cx > Cin:
         x[:, Cin:] = 0
-    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (k * k * Cin) ** 0.5)
     b = torch.randn(Cout, generator=g)
     xr = x[:, :Cin].float().clone().requires_grad_(True)
     wr = w.to(torch.bfloat16).float().clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)
-    yr = torch.nn.functional.conv2d(xr, wr, br, stride=stride, padding=1)
+    yr = torch.nn.functional.conv2d(xr, wr, br, stride=stride, padding=k // 2)
     dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16)
     yr.backward(dy.float())
     xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
     wd, bd = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
-    y = ec.conv3x3(xd, wd, bd, stride)
+    y = ec.conv2d(xd, wd, bd, stride)
     assert y.shape == yr.shape and y.dtype == torch.bfloat16
     assert y.is_contiguous(memory_format=torch.channels_last)
     y.backward(dy.to(DEV))
@@ -52,3 +58,27 @@ def test_conv3x3_fwd_bwd(N, Cx, Cin, Cout, H, W, stride):
     # weight grads: the kernel sees bf16 x (as torch does above) and bf16 dy
     assert rel(wd.grad, wr.grad) < 1e-3
     assert rel(bd.grad, br.grad) < 1e-3
+
+
+@pytest.mark.parametrize('levels,N,C,Cout,H,W', [(3, 2, 128, 128, 14, 14), (2, 3, 32, 64, 9, 10)])
+def test_conv_level_major_input(levels, N, C, Cout, H, W):
+    """levels > 1: the conv reads z [L*N, C, H, W] as cat(z.chunk(L), 1) in place
+    (the multiscale fusion input, mwt.py:112) and returns dz in z's layout."""
+    import ewvit.conv as ec
+    g = torch.Generator().manual_seed(levels * 100 + C)
+    z = torch.randn(levels * N, C, H, W, generator=g).to(torch.bfloat16)
+    w = torch.randn(Cout, levels * C, 3, 3, generator=g) / (9 * levels * C) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    zr = z.float().clone().requires_grad_(True)
+    wr = w.to(torch.bfloat16).float().clone().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(torch.cat(zr.chunk(levels), 1), wr, b, padding=1)
+    dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16)
+    yr.backward(dy.float())
+    zd = z.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = ec.conv2d(zd, wd, b.to(DEV), 1, levels)
+    y.backward(dy.to(DEV))
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 2 ** -7
+    assert zd.grad.shape == z.shape and rel(zd.grad, zr.grad) < 2 ** -7
+    assert rel(wd.grad, wr.grad) < 1e-3

@@ -221,10 +221,12 @@ def test_dama_train_step_vs_oracle(dama_pair, autocast):
     """Train-mode DAMA.forward over K=8 frames per video in 2 chunks + backward,
     vs the oracle on CPU (same weights; dropout / stochastic depth off).
 
-    fp32 run: 2e-2 of scale, cosine 0.998.  bf16-autocast run: the bound is set
-    by PyTorch's own bf16 autocast of the reference op sequence (the oracle moved
-    to the GPU under autocast): the product's error vs fp32 must stay within
-    1.5x that error (+1e-2 of scale), and cosine >= 0.995."""
+    The product's conv / depthwise stack computes on bf16 MFMA operands with or
+    without autocast (the bf16 contract of BASELINE.json), so both runs are
+    bounded by PyTorch's own bf16 autocast of the reference op sequence (the
+    oracle moved to the GPU under autocast): the product's error vs fp32 must stay
+    within 1.5x that error (+1e-2 of scale), cosine >= 0.995; gradient angle
+    error (1 - cosine) at most twice torch-autocast's, floor capped at 0.98."""
     import copy
     p0, o0 = dama_pair
     p, o = copy.deepcopy(p0), copy.deepcopy(o0)
@@ -234,42 +236,32 @@ def test_dama_train_step_vs_oracle(dama_pair, autocast):
     ro = o(x, batch_size=4)
     with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
         rp = p(x.to(DEV), batch_size=4)
-    if autocast:
-        og = copy.deepcopy(o0).to(DEV).train()
-        with torch.autocast('cuda', dtype=torch.bfloat16):
-            rg = og(x.to(DEV), batch_size=4)
-        for k in ro:
-            scale = float(ro[k].abs().max())
-            bound = 1.5 * _max_err(rg[k], ro[k]) + 1e-2 * scale
-            assert _max_err(rp[k], ro[k]) <= bound, (k, _max_err(rp[k], ro[k]), _max_err(rg[k], ro[k]), scale)
-            assert cos(rp[k], ro[k]) >= 0.995, k
-    else:
-        for k in ro:
-            check(rp[k], ro[k], 2e-2, 0.998)
-    tol = 4e-2 if autocast else 2e-2
+    og = copy.deepcopy(o0).to(DEV).train()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        rg = og(x.to(DEV), batch_size=4)
+    for k in ro:
+        scale = float(ro[k].abs().max())
+        bound = 1.5 * _max_err(rg[k], ro[k]) + 1e-2 * scale
+        assert _max_err(rp[k], ro[k]) <= bound, (k, _max_err(rp[k], ro[k]), _max_err(rg[k], ro[k]), scale)
+        assert cos(rp[k], ro[k]) >= 0.995, k
+    tol = 4e-2
     w = {k: torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) for i, (k, v) in enumerate(sorted(ro.items()))}
     sum((ro[k] * w[k]).sum() for k in ro).backward()
     sum((rp[k].float() * w[k].to(DEV)).sum() for k in rp).backward()
+    sum((rg[k].float() * w[k].to(DEV)).sum() for k in rg).backward()
     names = ['sfe.patch_to_embedding.weight', 'sfe.transformer.layers.0.0.fn.to_qkv.weight',
              'sfe.transformer.layers.1.1.fn.net.0.weight', 'cross_att.layers.1.3.to_kv.weight',
              'cross_att.layers.0.0.weight', 'gate_net.2.weight', 'fusion_gate.0.weight',
              'mwt.multiscale_fusion.0.weight', 'mwt.hf_conv.fusion.0.weight', 'mwt.hf_conv.seperate.1.0.weight',
              'sfe.pos_embedding', 'sfe.cls_token', 'sfe.efficient_net.features.7.0.weight',
              'sfe.efficient_net.features.6.3.block.1.0.weight']
-    if autocast:
-        # bf16 gradients: bounded by PyTorch's own autocast of the reference op
-        # sequence on the same GPU (cosine to fp32 minus 0.01, capped at 0.98)
-        sum((rg[k].float() * w[k].to(DEV)).sum() for k in rg).backward()
-        pp, oo, gg = dict(p.named_parameters()), dict(o.named_parameters()), dict(og.named_parameters())
-        for n in names:
-            ref_c = cos(gg[n].grad, oo[n].grad)
-            floor = min(0.98, ref_c - 0.02)
-            c = cos(pp[n].grad, oo[n].grad)
-            assert c >= floor, f'{n}: grad cosine {c:.5f} < {floor:.5f} (torch autocast {ref_c:.5f})'
-    else:
-        # the MWT convs and backbone depthwise convs take bf16 operands even without
-        # autocast (their kernels are bf16 MFMA / bf16-vector): bf16-level gradients
-        grads_close(p, o, names, 0.98)
+    pp, oo, gg = dict(p.named_parameters()), dict(o.named_parameters()), dict(og.named_parameters())
+    for n in names:
+        assert pp[n].grad is not None, n
+        ref_c = cos(gg[n].grad, oo[n].grad)
+        floor = min(0.98, 1.0 - 2.0 * (1.0 - ref_c))
+        c = cos(pp[n].grad, oo[n].grad)
+        assert c >= floor, f'{n}: grad cosine {c:.5f} < {floor:.5f} (torch autocast {ref_c:.5f})'
     # BatchNorm running statistics were updated per level and per chunk like the reference
     ps, os_ = p.state_dict(), o.state_dict()
     for k in ['mwt.hf_conv.fusion.1.running_mean', 'mwt.hf_conv.seperate.2.1.running_var',
