@@ -5,13 +5,17 @@ One step = the reference training step of train.py:93-115 on synthetic data:
 ``DeepfakeDetector.forward(x[8, 8, 3, 224, 224], batch_size=8, 'dynamic')`` (one
 64-frame ``_process_frame`` chunk, dama.py:179-186) under bf16 autocast,
 ``combined_loss`` at epoch=1/max_epochs=1 (BCE + orthogonal term), backward,
-Adam(lr 1e-4, wd 1e-4) step.  Random-init weights, N(0,1) frames.
+Adam(lr 1e-4, wd 1e-4) step.  Random-init weights, N(0,1) frames.  The iteration
+is recorded once into HIP graphs and replayed (ewvit/graph.py; --eager issues
+every launch from Python instead).
 
-Multi-GPU: one process per GPU (torchrun), DDP over RCCL; every rank runs its own
-64-frame chunk (weak scaling; BatchNorm statistics per rank like the reference's
-per-replica DataParallel semantics).  value = all frames / max-over-ranks time.
+Multi-GPU: one process per GPU (torchrun); each step broadcasts rank 0's BN buffers,
+replays forward+backward, all-reduces the gradients (one flat fp32 buffer, RCCL over
+xGMI) and replays the optimizer; every rank runs its own 64-frame chunk (weak
+scaling; BatchNorm statistics per rank like the reference's per-replica
+DataParallel semantics).  value = all frames / max-over-ranks time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--eager]
 """
 import argparse
 import json
@@ -38,20 +42,20 @@ def parse():
     ap.add_argument('--frames', type=int, default=64, help='frames per GPU per step (one chunk)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=4)
+    ap.add_argument('--eager', action='store_true', help='issue every launch from Python (no HIP graph)')
     return ap.parse_args()
 
 
-def build_step(dev, frames, rank):
+def build_step(dev, frames, rank, graph=True):
     from network.model import DeepfakeDetector
     from network.losses import combined_loss
+    from ewvit.graph import TrainStep
     torch.manual_seed(0)                                   # identical init on every rank
     videos = 8
     per_video = frames // videos
     model = DeepfakeDetector(3, 128, batch_size=per_video).to(dev).to(memory_format=torch.channels_last)
-    from ewvit import dist as edist
-    net = edist.wrap(model, dev)
     params = [p for p in model.parameters() if p.requires_grad]
-    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
+    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True, capturable=True)
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(videos, per_video, 3, 224, 224, device=dev, generator=g)
@@ -59,15 +63,14 @@ def build_step(dev, frames, rank):
     y = torch.bernoulli(torch.full((videos,), 0.5, device=dev), generator=gl)
     model.train()
 
-    def step():
+    def forward_loss():
         with torch.autocast('cuda', dtype=torch.bfloat16):
-            out = net(x, per_video, 'dynamic')
+            out = model(x, per_video, 'dynamic')
         loss, _ = combined_loss(out, y, crit, 1, 1)
-        loss.backward()
-        opt.step()
-        opt.zero_grad(set_to_none=True)
         return loss
-    return step
+    # gradients averaged over ranks with one RCCL all-reduce per step; the whole
+    # iteration replayed from HIP graphs (ewvit/graph.py)
+    return TrainStep(model, forward_loss, opt, graph=graph)
 
 
 def kernel_table(records):
@@ -96,10 +99,16 @@ ENTRY_KERNELS = {
     'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
     'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
                                    'dw_bwd_weight_reduce_kernel'],
-    'ewvit_conv3x3_fwd': ['conv3x3_fwd_kernel'],
-    'ewvit_conv3x3_bwd_data': ['conv3x3_bwd_data_kernel'],
-    'ewvit_conv3x3_bwd_weight': ['conv3x3_wgrad_kernel', 'conv3x3_wgrad_reduce_kernel'],
+    'ewvit_conv2d_fwd': ['conv_fwd_kernel<false'],
+    'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true'],
+    'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_reduce_kernel'],
+    'ewvit_bn_fwd': ['bn_stats_kernel', 'bn_finalize_fwd_kernel', 'bn_apply_kernel', 'bn_eval_coeff_kernel'],
+    'ewvit_bn_bwd': ['bn_bwd_reduce_kernel', 'bn_finalize_bwd_kernel', 'bn_bwd_dx_kernel'],
+    'ewvit_se_reduce': ['se_reduce_kernel', 'se_fold_kernel'],
+    'ewvit_se_scale': ['se_scale_kernel'],
+    'ewvit_scale_add': ['scale_add_kernel'],
 }
+MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data', 'ewvit_conv2d_bwd_weight')
 PMC_FILE = os.path.join(REPO, 'profiles', 'pmc_latest.json')
 
 
@@ -122,7 +131,7 @@ def pmc_traffic(entry, per_step):
 
 def roofline_for(name, row):
     traffic = pmc_traffic(name, row.get('per_step'))
-    if name in ('ewvit_gemm', 'ewvit_conv3x3_fwd', 'ewvit_conv3x3_bwd_data', 'ewvit_conv3x3_bwd_weight'):
+    if name in MFMA_ENTRIES:
         ach = row['TFLOP/s']
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': BF16_PEAK_TFS,
                 'unit': 'TFLOP/s', 'frac': round(ach / BF16_PEAK_TFS, 5), 'traffic': traffic,
@@ -178,7 +187,7 @@ def main():
     dev = torch.device('cuda', local)
     edist.init_from_env('gloo' if rehearse else 'nccl')    # RCCL over xGMI
     ewvit.load_library()                       # fail loudly if the HIP library is missing
-    step = build_step(dev, args.frames, rank)
+    step = build_step(dev, args.frames, rank, graph=not args.eager)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -192,11 +201,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = edist.max_over_ranks(time.perf_counter() - t0, dev)
 
-    # per-kernel timing pass (HIP events around every ewvit launch, separate from the timed loop)
+    # per-kernel timing pass (HIP events around every ewvit launch, separate from the timed
+    # loop): the same iteration issued eagerly, so each launch can be bracketed
     ewvit._lib.enable_timing(True)
     kt = max(3, min(args.steps, 5))
     for _ in range(kt):
-        step()
+        step._eager()
     torch.cuda.synchronize()
     table = kernel_table(ewvit._lib.timing_records())
     ewvit._lib.enable_timing(False)
@@ -211,7 +221,8 @@ def main():
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
                           'image': 224, 'frames_per_gpu': args.frames, 'dim': 128,
-                          'global_batch': args.frames * world, 'parallelism': f'ddp{world}'}}
+                          'global_batch': args.frames * world, 'parallelism': f'dp{world}',
+                          'launch': 'eager' if args.eager else 'hip-graph'}}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
         res['roofline'] = roofline_for(*dom) if dom else None
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}

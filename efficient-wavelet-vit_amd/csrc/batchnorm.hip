@@ -220,11 +220,23 @@ __device__ __forceinline__ void slab_sum(const float *__restrict__ pg, int nbloc
                                          float *red, float &a, float &b) {
   const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
   a = 0.f; b = 0.f;
-  if (ok)
-    for (int k = pl; k < nblocks; k += 8) {
+  if (ok) {
+    int k = pl;
+    for (; k + 56 < nblocks; k += 64) {      // 8 slab rows' loads in flight per thread
+      float va[8], vb[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        va[q] = pg[(int64_t)(k + 8 * q) * 2 * C + c];
+        vb[q] = pg[(int64_t)(k + 8 * q) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { a += va[q]; b += vb[q]; }
+    }
+    for (; k < nblocks; k += 8) {
       a += pg[(int64_t)k * 2 * C + c];
       b += pg[(int64_t)k * 2 * C + C + c];
     }
+  }
   red[threadIdx.x] = a;
   red[256 + threadIdx.x] = b;
   __syncthreads();

@@ -77,6 +77,12 @@ __device__ __forceinline__ void store_dt(void *p, int64_t i, float v, int dt) {
 // ---------------------------------------------------------------- RNG
 // Counter-based hash (splitmix64 finaliser) for dropout: keep(seed, i) is a
 // pure function, so backward regenerates the forward mask without storing it.
+// The effective seed of a launch is seed + *seed_offset * golden (seed_offset: a
+// device int64 advanced once per training step, or null), so a launch recorded
+// into a HIP graph draws a fresh mask on every replay.
+__device__ __forceinline__ uint64_t step_seed(uint64_t seed, const int64_t *seed_offset) {
+  return seed_offset ? seed + 0xD1B54A32D192ED03ull * (uint64_t)(*seed_offset) : seed;
+}
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
   uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -30,6 +30,8 @@
 // [B][H][W][3*128] concatenation (mwt.py:112) without materialising it.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace ewvit {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 cbf16x8;
@@ -37,7 +39,6 @@ typedef __attribute__((ext_vector_type(4))) float cf32x4;
 typedef __attribute__((ext_vector_type(4))) short cs4;
 
 constexpr int CBM = 128, CBN = 128, CBK = 32;
-constexpr int CLD = CBK + 8;  // padded [row][k] image row (80 B)
 
 struct ConvGeom {
   int N, H, W, Cin;      // x (fwd) / dx (dgrad) grid
@@ -62,37 +63,43 @@ struct FwdArgs {
   int64_t sgs, ogs;      // group strides (elements)
 };
 
-template <bool DGRAD, int BN_, int KS>
+template <bool DGRAD, int BN_, int KS, int BK, int PF>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
+  // BK: K-tile depth (32 | 64); PF: K-tiles of register prefetch (1 | 2)
   constexpr int WN = BN_ / 2, J = WN / 16;  // per-wave columns, 16-wide MFMA tiles
-  constexpr int A_EL = 2 * CBM * CLD, B_EL = 2 * BN_ * CLD;
+  constexpr int LD = BK + 8;                 // padded [row][k] image row (bf16)
+  constexpr int CPR = BK / 8;                // 16-B chunks per image row
+  constexpr int VA = CBM * CPR / 256;        // A vectors staged per thread per K-tile
+  constexpr int VB = BN_ * CPR / 256;        // B vectors
+  constexpr int A_EL = 2 * CBM * LD, B_EL = 2 * BN_ * LD;
   constexpr int CST = BN_ + 8;               // epilogue image row (bf16)
   static_assert(CBM * CST <= A_EL + B_EL, "epilogue tile must fit the staging LDS");
+  static_assert(VB >= 1, "tile too narrow for the staging map");
   // one LDS array: double-buffered A / B images, reused as the output tile image
   __shared__ __attribute__((aligned(16))) bf16_t smem[A_EL + B_EL];
-  auto As = reinterpret_cast<bf16_t (*)[CBM][CLD]>(smem);
-  auto Bs = reinterpret_cast<bf16_t (*)[BN_][CLD]>(smem + A_EL);
+  auto As = reinterpret_cast<bf16_t (*)[CBM][LD]>(smem);
+  auto Bs = reinterpret_cast<bf16_t (*)[BN_][LD]>(smem + A_EL);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.x * CBM;
   const int n0 = blockIdx.y * BN_;
   const int K = KS * KS * a.KC;
-  const int nk = (K + CBK - 1) / CBK;
-  const bool fastk = (a.KC % CBK) == 0;   // every K-tile inside one tap / one src group
-  const int cbn = a.KC / CBK;             // channel blocks per tap (fastk)
+  const int nk = (K + BK - 1) / BK;
+  const bool fastk = (a.KC % BK) == 0;    // every K-tile inside one tap / one src group
+  const int cbn = a.KC / BK;              // channel blocks per tap (fastk)
   const int ls = a.g.stride >> 1;         // log2(stride)
   const int smask = a.g.stride - 1;
 
-  // each thread stages 2 A vectors and 2 B vectors (8 bf16 each) per K-tile
-  int arow[2], ach[2];
-  int py[2], px[2];      // fwd: oh*s - pad, ow*s - pad;  dgrad: oh + pad, ow + pad
-  int64_t pbase[2];      // n * srcH * srcW
-  bool avalid[2];
+  // staged vector v = tid + 256*u covers image row v / CPR, chunk v % CPR
+  int arow[VA], ach[VA];
+  int py[VA], px[VA];    // fwd: oh*s - pad, ow*s - pad;  dgrad: oh + pad, ow + pad
+  int64_t pbase[VA];     // n * srcH * srcW
+  bool avalid[VA];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < VA; ++u) {
     const int v = tid + 256 * u;
-    arow[u] = v >> 2;
-    ach[u] = (v & 3) * 8;
+    arow[u] = v / CPR;
+    ach[u] = (v % CPR) * 8;
     const int64_t m = m0 + arow[u];
     avalid[u] = m < a.M;
     const int64_t mm = avalid[u] ? m : 0;
@@ -118,27 +125,26 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     return pbase[u] + (int64_t)sh * a.srcW + sw;
   };
   int ltap = 0, lcb = 0;   // fastk: tap / channel block of the next K-tile to load
-  auto load_tile = [&](int kt, uint4 (&ra)[2], uint4 (&rb)[2]) {
-    int tap_u = 0, kh = 0, kw = 0;
+  auto load_tile = [&](int kt, uint4 (&ra)[VA], uint4 (&rb)[VB]) {
+    int kh = 0, kw = 0;
     int64_t goff = 0;      // group offset (elements) of this tile's channel block
     int cin0 = 0;          // channel within the group for ach == 0
     if (fastk) {
-      tap_u = ltap;
-      kh = tap_u / KS; kw = tap_u - kh * KS;
-      const int c0 = lcb * CBK;
+      kh = ltap / KS; kw = ltap - kh * KS;
+      const int c0 = lcb * BK;
       const int gi = c0 / a.sgc;
       goff = (int64_t)gi * a.sgs;
       cin0 = c0 - gi * a.sgc;
       if (++lcb == cbn) { lcb = 0; ++ltap; }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = kt * CBK + ach[u];
+    for (int u = 0; u < VA; ++u) {
+      const int k = kt * BK + ach[u];
       int64_t off, p;
       if (fastk) {
         p = src_pix(u, kh, kw);
         off = goff + p * a.sgc + cin0 + ach[u];
-      } else {   // KC % 32 != 0 (ungrouped src): per-thread tap
+      } else {   // KC % BK != 0 (ungrouped src): per-thread tap
         const int tap = KS == 1 ? 0 : k / a.KC;
         const int c = k - tap * a.KC;
         const int th = tap / KS;
@@ -148,19 +154,23 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       uint4 va = make_uint4(0u, 0u, 0u, 0u);
       if (avalid[u] && k < K && p >= 0) va = *reinterpret_cast<const uint4 *>(a.src + off);
       ra[u] = va;
-      if (BN_ == 128 || u == 0) {
-        const int n = n0 + arow[u];  // B rows use the same (row, chunk) split
-        uint4 vb = make_uint4(0u, 0u, 0u, 0u);
-        if (n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
-        rb[u] = vb;
-      }
+    }
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      const int v = tid + 256 * u;
+      const int n = n0 + v / CPR, k = kt * BK + (v % CPR) * 8;
+      uint4 vb = make_uint4(0u, 0u, 0u, 0u);
+      if (n < a.Ncol && k < K) vb = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + k);
+      rb[u] = vb;
     }
   };
-  auto store_tile = [&](int buf, const uint4 (&ra)[2], const uint4 (&rb)[2]) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[VA], const uint4 (&rb)[VB]) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      *reinterpret_cast<uint4 *>(&As[buf][arow[u]][ach[u]]) = ra[u];
-      if (BN_ == 128 || u == 0) *reinterpret_cast<uint4 *>(&Bs[buf][arow[u]][ach[u]]) = rb[u];
+    for (int u = 0; u < VA; ++u) *reinterpret_cast<uint4 *>(&As[buf][arow[u]][ach[u]]) = ra[u];
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      const int v = tid + 256 * u;
+      *reinterpret_cast<uint4 *>(&Bs[buf][v / CPR][(v % CPR) * 8]) = rb[u];
     }
   };
 
@@ -170,36 +180,60 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
-  // K-tile kt+2 is loaded into registers while kt is computed from LDS and kt+1
-  // (loaded one step earlier) is written to the other LDS buffer: two K-steps of
-  // MFMA work cover each global load
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  auto step = [&](int kt, uint4 (&na)[2], uint4 (&nb)[2], const uint4 (&ra)[2], const uint4 (&rb)[2]) {
-    const int cur = kt & 1;
-    if (kt + 2 < nk) load_tile(kt + 2, na, nb);
-    cbf16x8 af[4], bfr[J];
+  auto compute = [&](int cur) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const cbf16x8 *>(&As[cur][wm * 64 + i * 16 + fr][fk]);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      cbf16x8 af[4], bfr[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) bfr[j] = *reinterpret_cast<const cbf16x8 *>(&Bs[cur][wn * WN + j * 16 + fr][fk]);
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const cbf16x8 *>(&As[cur][wm * 64 + i * 16 + fr][ks * 32 + fk]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < J; ++j)
+        bfr[j] = *reinterpret_cast<const cbf16x8 *>(&Bs[cur][wn * WN + j * 16 + fr][ks * 32 + fk]);
 #pragma unroll
-      for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) store_tile(cur ^ 1, ra, rb);
-    __syncthreads();
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
   };
-  uint4 pa[2], pb[2], qa[2], qb[2];
-  load_tile(0, pa, pb);
-  if (nk > 1) load_tile(1, qa, qb);
-  store_tile(0, pa, pb);
-  __syncthreads();
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    step(kt, pa, pb, qa, qb);
-    step(kt + 1, qa, qb, pa, pb);
+  if constexpr (PF == 1) {
+    // K-tile kt+1 is loaded into registers while kt is computed from LDS
+    uint4 ra[VA], rb[VB];
+    load_tile(0, ra, rb);
+    store_tile(0, ra, rb);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(kt + 1, ra, rb);
+      compute(cur);
+      if (more) store_tile(cur ^ 1, ra, rb);
+      __syncthreads();
+    }
+  } else {
+    // K-tile kt+2 is loaded into registers while kt is computed from LDS and kt+1
+    // (loaded one step earlier) is written to the other LDS buffer
+    auto step = [&](int kt, uint4 (&na)[VA], uint4 (&nb)[VB], const uint4 (&ra)[VA], const uint4 (&rb)[VB]) {
+      const int cur = kt & 1;
+      if (kt + 2 < nk) load_tile(kt + 2, na, nb);
+      compute(cur);
+      if (kt + 1 < nk) store_tile(cur ^ 1, ra, rb);
+      __syncthreads();
+    };
+    uint4 pa[VA], pb[VB], qa[VA], qb[VB];
+    load_tile(0, pa, pb);
+    if (nk > 1) load_tile(1, qa, qb);
+    store_tile(0, pa, pb);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, pa, pb, qa, qb);
+      step(kt + 1, qa, qb, pa, pb);
+    }
+    if (kt < nk) step(kt, pa, pb, qa, qb);
   }
-  if (kt < nk) step(kt, pa, pb, qa, qb);
   // epilogue: accumulators (+ bias) -> bf16 tile image in LDS (C/D map col = lane&15,
   // row = (lane>>4)*4 + r), then 16-B row-contiguous stores of 8 output channels
   // (the loop above ended with a barrier, so the staging images are free)
@@ -469,15 +503,45 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(const float *__restrict_
   if (wp_t) wp_t[((int64_t)ci * taps + tap) * Cout + co] = v;
 }
 
-// Ncol <= 64 (e.g. the fusion conv's 56-channel input gradient) uses the 128x64 tile
-template <bool DGRAD, int KS>
-static void launch_fwd_ks(const FwdArgs &a, hipStream_t s) {
+// Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
+// else 32; register prefetch depth from EWVIT_CONV_PF (1 or 2, default 1).
+// Ncol <= 64 (e.g. the fusion conv's 56-channel input gradient) uses the 128x64 tile.
+static int conv_pf() {
+  static int pf = [] {
+    const char *e = getenv("EWVIT_CONV_PF");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return pf;
+}
+static int conv_bk64() {
+  static int v = [] {
+    const char *e = getenv("EWVIT_CONV_BK");
+    return (e && e[0] == '3') ? 0 : 1;   // EWVIT_CONV_BK=32 disables the 64-deep tile
+  }();
+  return v;
+}
+
+template <bool DGRAD, int KS, int BK, int PF>
+static void launch_fwd_v(const FwdArgs &a, hipStream_t s) {
   if (a.Ncol <= 64) {
     dim3 grid((unsigned)((a.M + CBM - 1) / CBM), 1);
-    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 64, KS>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 64, KS, BK, PF>), grid, dim3(256), 0, s, a);
   } else {
     dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
-    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 128, KS>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 128, KS, BK, PF>), grid, dim3(256), 0, s, a);
+  }
+}
+
+template <bool DGRAD, int KS>
+static void launch_fwd_ks(const FwdArgs &a, hipStream_t s) {
+  const bool bk64 = conv_bk64() && a.KC % 64 == 0 && a.sgc % 64 == 0;
+  const int pf = conv_pf();
+  if (bk64) {
+    if (pf == 2) launch_fwd_v<DGRAD, KS, 64, 2>(a, s);
+    else launch_fwd_v<DGRAD, KS, 64, 1>(a, s);
+  } else {
+    if (pf == 2) launch_fwd_v<DGRAD, KS, 32, 2>(a, s);
+    else launch_fwd_v<DGRAD, KS, 32, 1>(a, s);
   }
 }
 

@@ -34,6 +34,7 @@ struct GemmArgs {
   void *aux;
   float drop_p;
   uint64_t seed;
+  const int64_t *seed_off;
   const void *resid; int resid_dtype; int64_t ldr;
   int c_dtype;
   int64_t kper;  // K per split
@@ -78,7 +79,7 @@ __device__ __forceinline__ float epilogue(const GemmArgs &g, int64_t row, int64_
     v *= gelu_erf_grad(bf2f(reinterpret_cast<const bf16_t *>(g.aux)[row * g.ldc + col]));
   }
   if (g.drop_p > 0.f) {
-    const float u = uniform01(g.seed, (uint64_t)(row * g.N + col));
+    const float u = uniform01(step_seed(g.seed, g.seed_off), (uint64_t)(row * g.N + col));
     v = (u >= g.drop_p) ? v * (1.0f / (1.0f - g.drop_p)) : 0.f;
   }
   if (g.resid) v += load_dt(g.resid, row * g.ldr + col, g.resid_dtype);
@@ -230,11 +231,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void *X, int dt, int6
 }
 
 __global__ __launch_bounds__(256) void dropout_bwd_kernel(void *g, int dt, int64_t rows, int64_t cols,
-                                                          int64_t ldg, float p, uint64_t seed) {
+                                                          int64_t ldg, float p, uint64_t seed,
+                                                          const int64_t *seed_off) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= rows * cols) return;
   const int64_t r = idx / cols, c = idx % cols;
-  const float u = uniform01(seed, (uint64_t)idx);
+  const float u = uniform01(step_seed(seed, seed_off), (uint64_t)idx);
   const int64_t o = r * ldg + c;
   const float v = load_dt(g, o, dt);
   store_dt(g, o, u >= p ? v * (1.0f / (1.0f - p)) : 0.f, dt);
@@ -243,12 +245,13 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(void *g, int dt, int64
 // g_pre = dy * keep(seed)/(1-p) * act'(aux): the backward of the GEMM epilogue
 __global__ __launch_bounds__(256) void act_bwd_kernel(const void *dy, int dydt, int64_t lddy,
                                                       const bf16_t *aux, int act, float p, uint64_t seed,
+                                                      const int64_t *seed_off,
                                                       void *out, int odt, int64_t M, int64_t N) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * N) return;
   const int64_t r = idx / N, c = idx % N;
   float v = load_dt(dy, r * lddy + c, dydt);
-  if (p > 0.f) v = uniform01(seed, (uint64_t)idx) >= p ? v * (1.0f / (1.0f - p)) : 0.f;
+  if (p > 0.f) v = uniform01(step_seed(seed, seed_off), (uint64_t)idx) >= p ? v * (1.0f / (1.0f - p)) : 0.f;
   if (act == 1) v *= gelu_erf_grad(bf2f(aux[idx]));
   else if (act == 2) v = bf2f(aux[idx]) > 0.f ? v : 0.f;
   store_dt(out, idx, v, odt);
@@ -287,7 +290,7 @@ extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda
                           int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
                           int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
                           const float *bias, int act, void *aux, float drop_p, uint64_t seed,
-                          const void *resid, int resid_dtype, int64_t ldr, int splitk,
+                          const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
                           float *workspace, void *stream) {
   EWVIT_CHECK_ARG(A && B && C, "gemm: null operand");
   EWVIT_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
@@ -308,7 +311,7 @@ extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda
   g.B = B; g.ldb_k = ldb_k; g.ldb_n = ldb_n;
   g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
   g.alpha = alpha; g.beta = beta; g.bias = bias; g.act = act; g.aux = aux;
-  g.drop_p = drop_p; g.seed = seed; g.resid = resid; g.resid_dtype = resid_dtype; g.ldr = ldr;
+  g.drop_p = drop_p; g.seed = seed; g.seed_off = seed_offset; g.resid = resid; g.resid_dtype = resid_dtype; g.ldr = ldr;
   g.c_dtype = c_dtype; g.ws = workspace;
   // K per split, a multiple of the K tile
   int64_t kper = (K + splitk - 1) / splitk;
@@ -345,17 +348,18 @@ extern "C" int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, 
 }
 
 extern "C" int ewvit_dropout_bwd(void *g, int g_dtype, int64_t rows, int64_t cols, int64_t ldg,
-                                 float p, uint64_t seed, void *stream) {
+                                 float p, uint64_t seed, const int64_t *seed_offset, void *stream) {
   EWVIT_CHECK_ARG(g && dtype_ok(g_dtype) && p >= 0.f && p < 1.f, "dropout_bwd: bad args");
   const int64_t total = rows * cols;
   if (total == 0 || p == 0.f) return 0;
   hipLaunchKernelGGL(dropout_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), g, g_dtype, rows, cols, ldg, p, seed);
+                     as_stream(stream), g, g_dtype, rows, cols, ldg, p, seed, seed_offset);
   return launch_status("dropout_bwd");
 }
 
 extern "C" int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const void *aux, int act,
-                             float drop_p, uint64_t seed, void *out, int out_dtype, int64_t M,
+                             float drop_p, uint64_t seed, const int64_t *seed_offset, void *out,
+                             int out_dtype, int64_t M,
                              int64_t N, void *stream) {
   EWVIT_CHECK_ARG(dy && out && dtype_ok(dy_dtype) && dtype_ok(out_dtype), "act_bwd: bad args");
   EWVIT_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || aux), "act_bwd: act=%d needs aux", act);
@@ -364,6 +368,6 @@ extern "C" int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const v
   if (total == 0) return 0;
   hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      as_stream(stream), dy, dy_dtype, lddy, (const bf16_t *)aux, act, drop_p, seed,
-                     out, out_dtype, M, N);
+                     seed_offset, out, out_dtype, M, N);
   return launch_status("act_bwd");
 }

@@ -21,10 +21,10 @@ SIGNATURES = {
     'ewvit_dwt_haar_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _vp],
     'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
-                   _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _i32, _i64, _i32, _vp, _vp],
+                   _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
     'ewvit_colsum': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
-    'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp],
-    'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _i32, _i64, _i64, _vp],
+    'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp, _vp],
+    'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _vp, _i32, _i64, _i64, _vp],
     'ewvit_layernorm_fwd': [_vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _f32, _vp],
     'ewvit_layernorm_bwd': [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64,
                             _i64, _vp],
@@ -41,6 +41,9 @@ SIGNATURES = {
     'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64,
                                 _vp, _vp],
+    'ewvit_se_reduce': [_vp, _vp, _i32, _i64, _i64, _i64, _f32, _vp, _vp, _vp],
+    'ewvit_se_scale': [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    'ewvit_scale_add': [_vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
 }
@@ -50,6 +53,7 @@ QUERIES = {
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
+    'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
 }
 
 _lib = None
@@ -117,6 +121,26 @@ def dt(t):
     if t.dtype == torch.bfloat16:
         return BF16
     raise TypeError(f'ewvit: unsupported dtype {t.dtype} (f32/bf16 only)')
+
+
+_rng_offsets = {}
+
+
+def rng_offset(device):
+    """Device int64 step counter mixed into every dropout seed (csrc/common.h
+    step_seed): a launch recorded in a HIP graph reads it on each replay, so a
+    replayed step draws fresh masks once the counter is advanced."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _rng_offsets.get(idx)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=torch.device('cuda', idx))
+        _rng_offsets[idx] = t
+    return t
+
+
+def rng_advance(device):
+    """Advance the dropout step counter (a device op: recorded into a captured step)."""
+    rng_offset(device).add_(1)
 
 
 def ptr(t):

@@ -24,7 +24,7 @@ def _c(t):
 
 # ------------------------------------------------------------------- GEMM
 def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, aux=None,
-         drop_p=0.0, seed=0, resid=None, ldr=0, splitk=None):
+         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None):
     """Raw C[M,N] = epi(alpha * A(M,K) @ B(K,N)).  lda = (lda_m, lda_k), ldb = (ldb_k, ldb_n).
     C must be contiguous with row stride N (ldc = C.stride(0))."""
     L.require_gpu(A, B, C)
@@ -38,7 +38,8 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
             'bytes': M * K * A.element_size() + K * N * B.element_size() + M * N * C.element_size()}
     L.call('ewvit_gemm', L.ptr(A), L.dt(A), lda[0], lda[1], L.ptr(B), L.dt(B), ldb[0], ldb[1],
            L.ptr(C), L.dt(C), C.stride(0), M, N, K, float(alpha), float(beta), L.ptr(bias), act,
-           L.ptr(aux), float(drop_p), seed, L.ptr(resid), L.dt(resid) if resid is not None else 0,
+           L.ptr(aux), float(drop_p), seed, L.ptr(seed_offset), L.ptr(resid),
+           L.dt(resid) if resid is not None else 0,
            ldr, splitk, L.ptr(ws), L.stream(C), work=work)
     return C
 
@@ -88,9 +89,10 @@ class LinearFn(torch.autograd.Function):
         need_aux = act in (1, 2) and any(ctx.needs_input_grad[:3])
         aux = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if need_aux else None
         seed = _seed() if drop_p > 0 else 0
+        soff = L.rng_offset(x.device) if drop_p > 0 else None
         r2 = _c(resid.reshape(M, N)) if resid is not None else None
-        mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, resid=r2,
-              ldr=N if r2 is not None else 0)
+        mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
+              resid=r2, ldr=N if r2 is not None else 0)
         ctx.save_for_backward(x2, weight, aux)
         ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None)
         return y.reshape(*lead, N)
@@ -106,8 +108,9 @@ class LinearFn(torch.autograd.Function):
             g = dy2
         else:
             g = torch.empty(M, N, dtype=torch.float32, device=dy.device)
+            soff = L.rng_offset(dy.device) if drop_p > 0 else None
             L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux), act, float(drop_p), seed,
-                   L.ptr(g), F32, M, N, L.stream(g))
+                   L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device)).reshape(*lead, K)

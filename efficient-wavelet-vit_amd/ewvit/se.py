@@ -1,0 +1,113 @@
+"""Squeeze-excitation and stochastic-depth residual add on the ewvit kernels
+(csrc/se.hip) — the MBConv block tail of the EfficientNetV2-S backbone
+(torchvision SqueezeExcitation / StochasticDepth behind network/sfe.py:111-113).
+
+SE: s = sigmoid(fc2(silu(fc1(mean_hw x)))), y = x * s.  The two HBM passes of the
+forward (squeeze, excite) and of the backward (sum_hw dy*x, dx = dy*s + dsq/HW)
+are ewvit kernels; the [N, C] squeeze MLP runs in fp32 on the library GEMM (it is
+a few KFLOP per sample).
+"""
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+
+
+def _rows(x):
+    xc = x.contiguous(memory_format=torch.channels_last)
+    N, C, H, W = xc.shape
+    return xc, N, H * W, C
+
+
+def _ws(N, HW, C, dev):
+    return torch.empty(L.load().ewvit_se_reduce_workspace(N, HW, C) // 4, dtype=torch.float32, device=dev)
+
+
+def _grad_like(g, p):
+    """gradient in the parameter's own strides (DDP bucket views)."""
+    g = g.reshape(p.shape)
+    return g if g.stride() == p.stride() else torch.empty_like(p, dtype=g.dtype).copy_(g)
+
+
+class SqueezeExciteFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        L.require_gpu(x)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        xc, N, HW, C = _rows(x)
+        Csq = w1.shape[0]
+        ws = _ws(N, HW, C, x.device)
+        s0 = torch.empty(N, C, dtype=torch.float32, device=x.device)
+        L.call('ewvit_se_reduce', L.ptr(xc), None, L.dt(xc), N, HW, C, 1.0 / HW, L.ptr(s0), L.ptr(ws), L.stream(s0),
+               work={'bytes': xc.numel() * xc.element_size()})
+        with torch.autocast('cuda', enabled=False):
+            W1, W2 = w1.detach().float().reshape(Csq, C), w2.detach().float().reshape(C, Csq)
+            h1 = torch.addmm(b1.detach().float(), s0, W1.t())
+            a1 = F.silu(h1)
+            s = torch.sigmoid(torch.addmm(b2.detach().float(), a1, W2.t()))
+        y = torch.empty_like(xc)
+        L.call('ewvit_se_scale', L.ptr(xc), L.dt(xc), L.ptr(s), None, L.ptr(y), N, HW, C, L.stream(y),
+               work={'bytes': 2 * xc.numel() * xc.element_size()})
+        ctx.save_for_backward(xc, w1, w2, s0, h1, a1, s)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w1, w2, s0, h1, a1, s = ctx.saved_tensors
+        N, C, H, W = xc.shape
+        HW, Csq = H * W, w1.shape[0]
+        dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
+        ws = _ws(N, HW, C, xc.device)
+        ds = torch.empty(N, C, dtype=torch.float32, device=xc.device)
+        L.call('ewvit_se_reduce', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, 1.0, L.ptr(ds), L.ptr(ws), L.stream(ds),
+               work={'bytes': 2 * xc.numel() * xc.element_size()})
+        with torch.autocast('cuda', enabled=False):
+            W1, W2 = w1.detach().float().reshape(Csq, C), w2.detach().float().reshape(C, Csq)
+            dh2 = ds * s * (1.0 - s)
+            dW2, db2 = dh2.t() @ a1, dh2.sum(0)
+            sg = torch.sigmoid(h1)
+            dh1 = (dh2 @ W2) * sg * (1.0 + h1 * (1.0 - sg))
+            dW1, db1 = dh1.t() @ s0, dh1.sum(0)
+            g = (dh1 @ W1) * (1.0 / HW)
+        dx = torch.empty_like(xc)
+        L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
+               work={'bytes': 2 * xc.numel() * xc.element_size()})
+        return dx, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2
+
+
+def squeeze_excite(x, w1, b1, w2, b2):
+    """torchvision SqueezeExcitation(C, Csq) with fc1 = (w1 [Csq, C, 1, 1], b1),
+    fc2 = (w2 [C, Csq, 1, 1], b2), SiLU / Sigmoid: x * sigmoid(fc2(silu(fc1(avgpool(x)))))."""
+    return SqueezeExciteFn.apply(x, w1, b1, w2, b2)
+
+
+class ScaleAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, x, scale):
+        L.require_gpu(r, x)
+        rc = r.contiguous(memory_format=torch.channels_last)
+        xc = x.to(rc.dtype).contiguous(memory_format=torch.channels_last)
+        N = rc.shape[0]
+        y = torch.empty_like(rc)
+        L.call('ewvit_scale_add', L.ptr(rc), L.ptr(xc), L.dt(rc), L.ptr(scale), L.ptr(y), N, rc.numel() // N,
+               L.stream(y), work={'bytes': 3 * rc.numel() * rc.element_size()})
+        ctx.save_for_backward(scale)
+        ctx.xdt = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        scale, = ctx.saved_tensors
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        N = dyc.shape[0]
+        dr = torch.empty_like(dyc)
+        L.call('ewvit_scale_add', L.ptr(dyc), None, L.dt(dyc), L.ptr(scale), L.ptr(dr), N, dyc.numel() // N,
+               L.stream(dr), work={'bytes': 2 * dyc.numel() * dyc.element_size()})
+        return dr, dy.to(ctx.xdt), None
+
+
+def scale_add(r, scale, x):
+    """r * scale[n] + x for [N, C, H, W] tensors (scale: f32 [N], no gradient) —
+    StochasticDepth(mode='row') fused with the residual add of an MBConv block."""
+    return ScaleAddFn.apply(r, x, scale.float().contiguous())

@@ -139,6 +139,8 @@ class DAMA(nn.Module):                                                     # dam
 
     def forward(self, x, batch_size=16):
         B, K, C, H, W = x.shape
+        if self.training and x.is_cuda:
+            ewvit._lib.rng_advance(x.device)   # fresh dropout masks per step, also under graph replay
         mean_fused = torch.zeros(B, self.dim, device=x.device)
         mean_space = torch.zeros(B, self.dim, device=x.device)
         mean_freq = torch.zeros(B, self.dim, device=x.device)

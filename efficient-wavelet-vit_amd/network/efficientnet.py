@@ -87,8 +87,13 @@ class SqueezeExcitation(nn.Module):
         self.scale_activation = nn.Sigmoid()
 
     def forward(self, x):
+        if x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0 and not self._has_hooks():
+            return ewvit.squeeze_excite(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
         s = self.scale_activation(self.fc2(self.activation(self.fc1(self.avgpool(x)))))
         return x * s
+
+    def _has_hooks(self):
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self.modules())
 
 
 def _drop_path(x, p, training):
@@ -103,6 +108,12 @@ class _Block(nn.Module):
     def forward(self, x):
         r = self.block(x)
         if self.use_res_connect:
+            if self.training and self.sd_prob > 0.0 and r.is_cuda and r.dtype in (torch.bfloat16, torch.float32) \
+                    and (r[0].numel() % 8 == 0):
+                # StochasticDepth(row) keep mask drawn as torchvision does, then ONE fused
+                # r * keep/(1-p) + x pass
+                keep = torch.empty((r.shape[0],), dtype=torch.float32, device=r.device).bernoulli_(1.0 - self.sd_prob)
+                return ewvit.scale_add(r, keep.div_(1.0 - self.sd_prob), x)
             return _drop_path(r, self.sd_prob, self.training) + x
         return r
 

@@ -74,7 +74,10 @@ int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H
  *                     ; act: 0 none, 1 GELU(erf), 2 ReLU, 3 multiply by GELU'(aux[m,n])
  *                       (act 1/2 also store the pre-activation to aux when aux != NULL)
  *                     ; dropout: if drop_p > 0, keep with prob 1-drop_p from
- *                       hash(seed, m*N+n), scale 1/(1-drop_p)
+ *                       hash(seed', m*N+n), scale 1/(1-drop_p), where
+ *                       seed' = seed + *seed_offset * 0xD1B54A32D192ED03 (seed_offset:
+ *                       device int64 advanced once per step — a graph-replayed
+ *                       launch draws a new mask each replay — or NULL: seed' = seed)
  *                     ; + resid[m*ldr + n] (f32 or bf16 per resid_dtype, may be NULL)
  *                     ; if beta != 0: C = beta*C_old + value (f32 C only)
  *   aux[m*ldc + n] (bf16) — pre-activation for act 1/3
@@ -84,22 +87,23 @@ int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H
 int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
                int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype, int64_t ldc,
                int64_t M, int64_t N, int64_t K, float alpha, float beta, const float *bias,
-               int act, void *aux, float drop_p, uint64_t seed, const void *resid,
-               int resid_dtype, int64_t ldr, int splitk, float *workspace, void *stream);
+               int act, void *aux, float drop_p, uint64_t seed, const int64_t *seed_offset,
+               const void *resid, int resid_dtype, int64_t ldr, int splitk, float *workspace,
+               void *stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n]  (bias gradients).  accumulate!=0 adds. */
 int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N, float *out,
                  int accumulate, void *stream);
 
-/* Dropout mask regeneration for backward: g[i] *= keep(seed, i)/(1-p), i < n. */
+/* Dropout mask regeneration for backward: g[i] *= keep(seed', i)/(1-p), i < n. */
 int ewvit_dropout_bwd(void *g, int g_dtype, int64_t rows, int64_t cols, int64_t ldg, float p,
-                      uint64_t seed, void *stream);
+                      uint64_t seed, const int64_t *seed_offset, void *stream);
 
-/* Backward of the GEMM epilogue: out[m*N+n] = dy[m*lddy+n] * keep(seed, m*N+n)/(1-p)
+/* Backward of the GEMM epilogue: out[m*N+n] = dy[m*lddy+n] * keep(seed', m*N+n)/(1-p)
  * * act'(aux[m*N+n]);  act 0 none, 1 GELU(erf) (aux = pre-activation), 2 ReLU. */
 int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const void *aux, int act,
-                  float drop_p, uint64_t seed, void *out, int out_dtype, int64_t M, int64_t N,
-                  void *stream);
+                  float drop_p, uint64_t seed, const int64_t *seed_offset, void *out, int out_dtype,
+                  int64_t M, int64_t N, void *stream);
 
 /* ---------------------------------------------------------- LayerNorm ---
  * y = (x - mean) * rstd * gamma + beta over the last dim D, eps — nn.LayerNorm
@@ -225,6 +229,25 @@ int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbi
                             int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                             int stride, int64_t x_group_c, int64_t x_group_stride, float *workspace,
                             void *stream);
+
+/* ------------------------------ squeeze-excitation / stochastic-depth add ---
+ * The MBConv block tail of the EfficientNetV2-S backbone (torchvision
+ * SqueezeExcitation + StochasticDepth, reached via network/sfe.py:111-113) on
+ * channels-last [N][HW][C] tensors (dtype bf16 or f32), C % 8 == 0.
+ * out[n][c] = scale * sum_hw a (b == NULL) or scale * sum_hw a*b (b != NULL), f32;
+ * deterministic; `workspace` holds ewvit_se_reduce_workspace(N, HW, C) bytes.
+ *   squeeze: a = x, scale = 1/HW;  excite backward: a = dy, b = x, scale = 1. */
+int64_t ewvit_se_reduce_workspace(int64_t N, int64_t HW, int64_t C);
+int ewvit_se_reduce(const void *a, const void *b, int dtype, int64_t N, int64_t HW, int64_t C,
+                    float scale, float *out, float *workspace, void *stream);
+/* y = x * s[n][c] (+ g[n][c] when g != NULL); s, g f32 [N][C].
+ *   excite: x, s;  backward: dx = dy * s + dsqueeze / HW. */
+int ewvit_se_scale(const void *x, int dtype, const float *s, const float *g, void *y, int64_t N,
+                   int64_t HW, int64_t C, void *stream);
+/* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
+ * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
+int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
+                    int64_t row_elems, void *stream);
 
 #ifdef __cplusplus
 }

@@ -56,7 +56,8 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc == 1000 and b'levels' in lib.ewvit_last_error()
     with pytest.raises(RuntimeError, match='unit stride'):
         _lib.call('ewvit_gemm', ctypes.c_void_p(16), 1, 7, 7, ctypes.c_void_p(16), 1, 1, 4,
-                  ctypes.c_void_p(16), 0, 4, 4, 4, 4, 1.0, 0.0, None, 0, None, 0.0, 0, None, 0, 0, 1, None, None)
+                  ctypes.c_void_p(16), 0, 4, 4, 4, 4, 1.0, 0.0, None, 0, None, 0.0, 0, None, None, 0, 0, 1, None,
+                  None)
     with pytest.raises(RuntimeError, match='nq=9'):
         _lib.call('ewvit_attn_fwd', ctypes.c_void_p(16), 0, 0, ctypes.c_void_p(16), 0, 0, ctypes.c_void_p(16),
                   0, 0, ctypes.c_void_p(16), 0, 0, None, 1, 1, 9, 2, 64, 1.0, None)

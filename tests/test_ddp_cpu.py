@@ -93,6 +93,64 @@ def test_ddp_gloo_world2_matches_dataparallel_semantics():
     torch.testing.assert_close(torch.from_numpy(res[0][2]), torch.from_numpy(res[1][2]))  # buffers broadcast
 
 
+def _trainstep_worker(rank, port, q):
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from ewvit import dist as edist
+    from ewvit.graph import TrainStep
+    r, w, _ = edist.init_from_env('gloo')
+    model = _model()
+    if r == 1:                       # rank 1 starts from different BN buffers: the step broadcasts rank 0's
+        for b in model.buffers():
+            if b.dtype.is_floating_point:
+                b.add_(3.0)
+    x = edist.shard_videos(_data(), r, w)
+    opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.5)
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    step = TrainStep(model, lambda: model(x.flatten(0, 1)).mean() / w, opt, graph=False)
+    step()
+    grads = {n: p.grad.numpy().copy() for n, p in model.named_parameters()}
+    delta = {n: (before[n] - p.detach()).numpy().copy() for n, p in model.named_parameters()}
+    q.put((r, grads, delta))
+    edist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_trainstep_gloo_world2_averages_gradients():
+    """ewvit.graph.TrainStep (the bench's data-parallel step; eager mode on CPU):
+    rank-0 buffers broadcast, one flat all-reduce, averaged gradients, identical
+    updates — equal to the DataParallel-semantics gradient of the global batch."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_trainstep_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        r, g, d = q.get(timeout=120)
+        res[r] = (g, d)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _model()
+    x = _data()
+    outs = [ref(x[2 * r:2 * r + 2].flatten(0, 1)) for r in range(WORLD)]
+    torch.cat(outs).mean().backward()
+    for n, p in ref.named_parameters():
+        for r in range(WORLD):
+            # TrainStep sums rank losses scaled by 1/world and divides the sum of
+            # gradients by world: DataParallel's mean-over-all-outputs gradient / world
+            torch.testing.assert_close(torch.from_numpy(res[r][0][n]) * WORLD, p.grad, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(res[r][1][n]), 0.5 * torch.from_numpy(res[r][0][n]),
+                                       rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(torch.from_numpy(res[0][1][n]), torch.from_numpy(res[1][1][n]))
+
+
 def test_shard_videos_covers_batch_once():
     sys.path.insert(0, PKG)
     from ewvit import dist as edist

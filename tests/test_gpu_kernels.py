@@ -169,8 +169,14 @@ def test_gemm_dropout_mask_statistics_and_backward_consistency():
     torch.testing.assert_close(y[kept], (y0 / 0.85)[kept], rtol=1e-5, atol=1e-5)
     # backward regenerates the same mask from the seed
     g = torch.ones(M, N, device=DEV)
-    L.call('ewvit_dropout_bwd', L.ptr(g), 0, M, N, N, 0.15, 1234, L.stream(g))
+    L.call('ewvit_dropout_bwd', L.ptr(g), 0, M, N, N, 0.15, 1234, None, L.stream(g))
     assert torch.equal(g != 0, kept)
+    # with a device step counter: same mask while the counter holds, a new one after it moves
+    off = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+    y5 = ewvit.mm_nt(X, W, torch.empty(M, N, device=DEV), drop_p=0.15, seed=1234, seed_offset=off)
+    g = torch.ones(M, N, device=DEV)
+    L.call('ewvit_dropout_bwd', L.ptr(g), 0, M, N, N, 0.15, 1234, L.ptr(off), L.stream(g))
+    assert torch.equal(g != 0, y5 != 0) and not torch.equal(y5 != 0, kept)
 
 
 def test_colsum():

@@ -1,0 +1,73 @@
+"""Squeeze-excitation and stochastic-depth residual kernels (csrc/se.hip) through
+the C-ABI, vs torch fp32 on the same (bf16-rounded) inputs.
+
+Tolerance: bf16 outputs are one rounding of an fp32 result (2^-7 of scale); f32
+outputs 1e-5; gradients 2e-3 of scale (fp32 reductions in another order) and
+2e-2 for bf16 input gradients (one bf16 rounding of dy*s + g).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+def ref_se(x, w1, b1, w2, b2):
+    s = x.mean((2, 3), keepdim=True)
+    s = torch.sigmoid(F.conv2d(F.silu(F.conv2d(s, w1, b1)), w2, b2))
+    return x * s
+
+
+@pytest.mark.parametrize('N,C,H,W,csq', [(4, 256, 28, 28, 16), (3, 960, 14, 14, 40), (2, 1536, 7, 7, 64),
+                                         (5, 24, 9, 11, 6), (2, 2048, 3, 3, 8)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_squeeze_excite(N, C, H, W, csq, dtype):
+    import ewvit
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randn(N, C, H, W, generator=g).to(dtype)
+    w1 = torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5
+    b1 = torch.randn(csq, generator=g) * 0.1
+    w2 = torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5
+    b2 = torch.randn(C, generator=g) * 0.1
+    ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    xr = x.float().clone().requires_grad_(True)
+    yr = ref_se(xr, *ps)
+    dy = torch.randn(yr.shape, generator=g).to(dtype)
+    yr.backward(dy.float())
+    xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    pd = [t.to(DEV).to(memory_format=torch.channels_last) if t.dim() == 4 else t.to(DEV) for t in (w1, b1, w2, b2)]
+    pd = [t.requires_grad_(True) for t in pd]
+    y = ewvit.squeeze_excite(xd, *pd)
+    y.backward(dy.to(DEV).to(memory_format=torch.channels_last))
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    assert rel(y, yr) < (2 ** -7 if dtype == torch.bfloat16 else 1e-5)
+    assert rel(xd.grad, xr.grad) < (2e-2 if dtype == torch.bfloat16 else 2e-4)
+    for a, b in zip(pd, ps):
+        assert a.grad.shape == b.shape and a.grad.stride() == a.stride()
+        assert rel(a.grad, b.grad) < 2e-3
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_scale_add(dtype):
+    import ewvit
+    g = torch.Generator().manual_seed(9)
+    r = torch.randn(6, 64, 7, 9, generator=g).to(dtype)
+    x = torch.randn(6, 64, 7, 9, generator=g).to(dtype)
+    keep = torch.tensor([1., 0., 1., 1., 0., 1.]) / 0.8
+    rr, xr = r.float().clone().requires_grad_(True), x.float().clone().requires_grad_(True)
+    yr = rr * keep.view(-1, 1, 1, 1) + xr
+    dy = torch.randn(yr.shape, generator=g).to(dtype)
+    yr.backward(dy.float())
+    rd = r.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    y = ewvit.scale_add(rd, keep.to(DEV), xd)
+    y.backward(dy.to(DEV).to(memory_format=torch.channels_last))
+    tol = 2 ** -7 if dtype == torch.bfloat16 else 1e-6
+    assert rel(y, yr) < tol
+    assert rel(rd.grad, rr.grad) < tol and rel(xd.grad, xr.grad) < tol
