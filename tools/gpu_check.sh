@@ -9,7 +9,7 @@ mkdir -p "$O"
 STEPS=${STEPS:-all}
 
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -m pytest "$R/tests" -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest "$R/tests" -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 "$O/pytest_gpu.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi

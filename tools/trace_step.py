@@ -1,0 +1,38 @@
+"""One training step from a rocprofv3 kernel trace: the kernels between the last two
+launches of the DWT kernel (the first kernel of every forward), with durations, grid
+and gaps.  Usage: python tools/trace_step.py <kernel_trace.csv> [--all] [--nth K]"""
+import csv
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    starts = [i for i, r in enumerate(rows) if 'dwt_multilevel' in r['Kernel_Name']]
+    k = int(sys.argv[sys.argv.index('--nth') + 1]) if '--nth' in sys.argv else 2
+    a, b = starts[-k], starts[-k + 1] if k > 1 else len(rows)
+    step = rows[a:b]
+    t0 = int(step[0]['Start_Timestamp'])
+    t1 = int(step[-1]['End_Timestamp'])
+    busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in step)
+    print(f'kernels {len(step)}  span {(t1 - t0) / 1e6:.3f} ms  busy {busy / 1e6:.3f} ms')
+    agg = {}
+    for r in step:
+        n = r['Kernel_Name'].split('(')[0][:90]
+        d = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+        c, t = agg.get(n, (0, 0))
+        agg[n] = (c + 1, t + d)
+    for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:40]:
+        print(f'{t / 1e3:9.1f} us {c:5d}  {n}')
+    if '--all' in sys.argv:
+        prev = t0
+        for r in step:
+            s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+            g = (r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])
+            print(f'{(s - t0) / 1e3:9.1f} gap {(s - prev) / 1e3:6.1f} dur {(e - s) / 1e3:8.1f}  {g}  {r["Kernel_Name"][:100]}')
+            prev = e
+
+
+if __name__ == '__main__':
+    main()
