@@ -465,14 +465,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
 // dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
-                                                                int Cout, int Cin, int taps, int splits, int accumulate,
-                                                                const float *__restrict__ dbias_part,
+                                                                int Cout, int Cin, int taps, int splits, int bparts,
+                                                                int accumulate, const float *__restrict__ dbias_part,
                                                                 float *__restrict__ dbias) {
   const int64_t NP = taps * (int64_t)Cin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in part layout
   if (dbias && i < Cout) {
     float sb = 0.f;
-    for (int k = 0; k < splits; ++k) sb += dbias_part[(int64_t)k * Cout + i];
+    for (int k = 0; k < bparts; ++k) sb += dbias_part[(int64_t)k * Cout + i];
     dbias[i] = accumulate ? dbias[i] + sb : sb;
   }
   if (i >= (int64_t)Cout * NP) return;
@@ -501,6 +501,346 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(const float *__restrict_
   const bf16_t v = f2bf(ci < Cin ? w[co * s_co + ci * s_ci + tap * s_tap] : 0.f);
   if (wp) wp[i] = v;
   if (wp_t) wp_t[((int64_t)ci * taps + tap) * Cout + co] = v;
+}
+
+// ---------------------------------------------------------------- LDS-DMA kernels
+// The same three GEMMs with the operands moved HBM/L2 -> LDS by buffer_load ... lds
+// (16 B per lane, no register round trip, no ds_write), for the shapes whose K-tiles
+// stay inside one tap and one channel group (fwd/dgrad: KC % 64 == 0; wgrad: Cin %
+// 128 == 0 or 1x1).  Out-of-image taps and ragged tile edges are zero-filled by the
+// buffer descriptor's range check (the lane's offset is pushed past num_records),
+// so there is no per-lane branch around a load.  The DMA writes each wave's 1 KiB
+// piece lane-linearly; the XOR swizzle that keeps the fragment reads conflict-free
+// is applied to the lane's SOURCE address and undone on the read (the swizzle is an
+// involution).  One K-tile is in flight while the previous one is multiplied; grid
+// order is remapped so that consecutive tiles (which share input halo rows and, for
+// wgrad, the same pixels) run on one XCD and meet in its L2.
+typedef __attribute__((address_space(3))) void lds_t;
+constexpr uint32_t OOB = 0x80000000u;   // any offset >= num_records reads as zero
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void *p, int64_t bytes) {
+  const uint32_t n = bytes >= (int64_t)OOB ? OOB : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, unsigned char *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t *)lds, 16, voff, 0, 0, 0);
+}
+// bijective XCD remap: blocks b, b+8, b+16 ... (one XCD) get consecutive tile ids
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// fwd / dgrad: 128 x BN_ x 64 tiles, 4 waves (2x2), [row][64 k] images of 128-B rows;
+// 16-B chunk c of row r is stored at chunk c ^ ((r >> 1) & 7): conflict-free b128 reads
+template <bool DGRAD, int BN_, int KS>
+__global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn) {
+  constexpr int BM = 128, BK = 64;
+  constexpr int WN = BN_ / 2, J = WN / 16;
+  constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
+  constexpr int PA = BM / 8 / 4, PB = BN_ / 8 / 4;   // 1 KiB pieces per wave per K-tile
+  constexpr int CST = BN_ + 8;
+  static_assert(BM * CST * 2 <= 2 * STG, "epilogue tile must fit the staging LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int n0 = (tile % ntn) * BN_;
+  const int K = KS * KS * a.KC;
+  const int nk = K / BK;
+  const int cbn = a.KC / BK;
+  const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
+  const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
+  const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
+
+  // A rows staged by this lane: piece p = w*PA + j covers rows 8p..8p+7
+  int py[PA], px[PA], lcA[PA];
+  int64_t pbase[PA];
+  bool av[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int p = w * PA + j, r = p * 8 + (lane >> 3);
+    lcA[j] = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t m = m0 + r;
+    av[j] = m < a.M;
+    const int64_t mm = av[j] ? m : 0;
+    const int ow = (int)(mm % a.outW);
+    const int64_t t = mm / a.outW;
+    const int oh = (int)(t % a.outH);
+    const int n = (int)(t / a.outH);
+    if (!DGRAD) { py[j] = oh * a.g.stride - a.g.pad; px[j] = ow * a.g.stride - a.g.pad; }
+    else        { py[j] = oh + a.g.pad;               px[j] = ow + a.g.pad; }
+    pbase[j] = (int64_t)n * a.srcH * a.srcW;
+  }
+  uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int p = w * PB + j, r = p * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    const int n = n0 + r;
+    boff[j] = n < a.Ncol ? (uint32_t)(((int64_t)n * K + lc * 8) * 2) : OOB;
+  }
+  int ltap = 0, lcb = 0;
+  auto stage = [&](int kt, int buf) {
+    const int kh = ltap / KS, kw = ltap - (ltap / KS) * KS;
+    const int c0 = lcb * BK;
+    const int gi = c0 / a.sgc;
+    const int64_t goff = (int64_t)gi * a.sgs + (c0 - gi * a.sgc);
+    if (++lcb == cbn) { lcb = 0; ++ltap; }
+    unsigned char *base = smem + buf * STG;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      int sh, sw;
+      bool ok = av[j];
+      if (!DGRAD) {
+        sh = py[j] + kh; sw = px[j] + kw;
+      } else {
+        const int th = py[j] - kh, tw = px[j] - kw;
+        ok = ok && th >= 0 && tw >= 0 && !((th | tw) & smask);
+        sh = th >> ls; sw = tw >> ls;
+      }
+      ok = ok && (unsigned)sh < (unsigned)a.srcH && (unsigned)sw < (unsigned)a.srcW;
+      const int64_t e = goff + (pbase[j] + (int64_t)sh * a.srcW + sw) * a.sgc + lcA[j] * 8;
+      glds16(rs, base + (w * PA + j) * 1024, ok ? (uint32_t)(e * 2) : OOB);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j)
+      glds16(rw, base + A_B + (w * PB + j) * 1024, boff[j] == OOB ? OOB : boff[j] + (uint32_t)(kt * BK * 2));
+  };
+
+  cf32x4 acc[4][J];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  auto frag = [&](const unsigned char *img, int r, int ch) -> cbf16x8 {
+    return *reinterpret_cast<const cbf16x8 *>(img + r * 128 + 16 * (ch ^ ((r >> 1) & 7)));
+  };
+  auto compute = [&](int buf) {
+    const unsigned char *As = smem + buf * STG, *Bs = As + A_B;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      cbf16x8 af[4], bfr[J];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(As, wm * 64 + i * 16 + fr, ks * 4 + fq);
+#pragma unroll
+      for (int j = 0; j < J; ++j) bfr[j] = frag(Bs, wn * WN + j * 16 + fr, ks * 4 + fq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: (+ bias) -> bf16 tile image -> 16-B row-contiguous stores
+  bf16_t *ep = reinterpret_cast<bf16_t *>(smem);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int cl = wn * WN + j * 16 + (lane & 15);
+    const float b = (a.bias && n0 + cl < a.Ncol) ? a.bias[n0 + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(wm * 64 + i * 16 + fq * 4 + r) * CST + cl] = f2bf(acc[i][j][r] + b);
+  }
+  __syncthreads();
+  constexpr int VPR = BN_ / 8;
+#pragma unroll
+  for (int k = 0; k < BM * VPR / 256; ++k) {
+    const int v = tid + 256 * k;
+    const int rl = v / VPR, cv = v % VPR;
+    const int64_t row = m0 + rl;
+    const int col = n0 + cv * 8;
+    if (row < a.M && col < a.Ncol) {
+      const int gi = col / a.ogc;
+      *reinterpret_cast<uint4 *>(a.out + (int64_t)gi * a.ogs + row * a.ogc + (col - gi * a.ogc)) =
+          *reinterpret_cast<const uint4 *>(&ep[rl * CST + cv * 8]);
+    }
+  }
+}
+
+// wgrad: C[co][n'] over pixel K-tiles of 64; [pixel][128] images of 256-B rows, chunk
+// c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed, ds_read_b64_tr_b16).
+// Bias gradient (sum of dy over pixels): the blocks of n'-tile t sum the dy image of
+// the K-tiles kt = t (mod n'-tiles), so the extra LDS reads are spread evenly.
+template <int KS>
+__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
+  constexpr int BK = 64, IMG = BK * 256, STG = 2 * IMG;
+  constexpr int P = BK / 4 / 4;     // pieces (4 rows x 256 B) per wave per image
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = tile / (ntx * nty);
+  const int tx = tile % ntx, ty = (tile / ntx) % nty;
+  const int co0 = ty * 128, np0 = tx * 128;
+  const int NP = KS * KS * a.g.Cin;
+  const int64_t mbeg = (int64_t)split * a.mper;
+  const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
+  const int nk = (int)((mend - mbeg + BK - 1) / BK);
+  const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, x_bytes);
+  const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * a.g.Cout * 2);
+
+  // piece p = w*P + j: rows 4p .. 4p+3; lane -> row 4p + lane/16, stored chunk lane%16
+  int lc[P], tkh[P], tkw[P], pn[P], poh[P], pw[P];
+  int64_t bgoff[P];
+  bool bok[P], aok[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int p = w * P + j, r = p * 4 + (lane >> 4);
+    lc[j] = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    aok[j] = co0 + lc[j] * 8 < a.g.Cout;
+    const int np = np0 + lc[j] * 8;
+    bok[j] = np < NP;
+    const int btap = bok[j] ? np / a.g.Cin : 0;
+    const int bci = bok[j] ? np - btap * a.g.Cin : 0;
+    tkh[j] = btap / KS - a.g.pad;
+    tkw[j] = btap % KS - a.g.pad;
+    const int gi = bci / a.xgc;
+    bgoff[j] = (int64_t)gi * a.xgs + (bci - gi * a.xgc);
+    const int64_t m = mbeg + r;
+    pw[j] = (int)(m % a.g.Wo);
+    const int64_t t = m / a.g.Wo;
+    poh[j] = (int)(t % a.g.Ho);
+    pn[j] = (int)(t / a.g.Ho);
+  }
+  auto stage = [&](int kt, int buf) {
+    unsigned char *base = smem + buf * STG;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t m = mbeg + (int64_t)kt * BK + (w * P + j) * 4 + (lane >> 4);
+      const bool mv = m < mend;
+      glds16(rd, base + (w * P + j) * 1024,
+             mv && aok[j] ? (uint32_t)((m * a.g.Cout + co0 + lc[j] * 8) * 2) : OOB);
+      const int ih = poh[j] * a.g.stride + tkh[j], iw = pw[j] * a.g.stride + tkw[j];
+      const bool ok = mv && bok[j] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W;
+      const int64_t e = bgoff[j] + (((int64_t)pn[j] * a.g.H + ih) * a.g.W + iw) * a.xgc;
+      glds16(rx, base + IMG + (w * P + j) * 1024, ok ? (uint32_t)(e * 2) : OOB);
+      pw[j] += BK;
+      while (pw[j] >= a.g.Wo) {
+        pw[j] -= a.g.Wo;
+        if (++poh[j] == a.g.Ho) { poh[j] = 0; ++pn[j]; }
+      }
+    }
+  };
+  auto tr_read = [&](const unsigned char *img, int k0, int c0) -> cs4 {
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = c0 + 4 * p;
+    const int off = swz_off(k0 + q, col >> 3) + 2 * (col & 7);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) cs4 *)(img + off));
+  };
+  const bool do_bias = a.dbias_part != nullptr;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  cf32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+  auto compute = [&](int kt, int buf) {
+    const unsigned char *As = smem + buf * STG, *Bs = As + IMG;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      cbf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const cs4 lo = tr_read(As, ks * 32 + 8 * g, wm * 64 + i * 16);
+        const cs4 hi = tr_read(As, ks * 32 + 8 * g + 4, wm * 64 + i * 16);
+        af[i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const cs4 lo = tr_read(Bs, ks * 32 + 8 * g, wn * 64 + j * 16);
+        const cs4 hi = tr_read(Bs, ks * 32 + 8 * g + 4, wn * 64 + j * 16);
+        bfr[j] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                 lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (do_bias && kt % ntx == tx) {
+      // thread t: rows (t>>4)*4 .. +3 of the dy image, chunk t & 15 (8 channels)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (tid >> 4) * 4 + q;
+        const uint4 v = *reinterpret_cast<const uint4 *>(As + swz_off(r, tid & 15));
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bsum[2 * e] += __uint_as_float(wv[e] << 16);
+          bsum[2 * e + 1] += __uint_as_float(wv[e] & 0xffff0000u);
+        }
+      }
+    }
+  };
+  if (nk > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    compute(kt, cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (do_bias) {
+    // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsum[j] += __shfl_xor(bsum[j], 16, 64);
+      bsum[j] += __shfl_xor(bsum[j], 32, 64);
+    }
+    float *red = reinterpret_cast<float *>(smem);
+    if (lane < 16)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(w * 16 + lane) * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < 128) {
+      const int ch = tid >> 3, j = tid & 7;
+      const int co = co0 + ch * 8 + j;
+      const float s = (red[(0 * 16 + ch) * 8 + j] + red[(1 * 16 + ch) * 8 + j]) +
+                      (red[(2 * 16 + ch) * 8 + j] + red[(3 * 16 + ch) * 8 + j]);
+      if (co < a.g.Cout) a.dbias_part[((int64_t)split * ntx + tx) * a.g.Cout + co] = s;
+    }
+  }
+  float *dst = a.part + (int64_t)split * a.g.Cout * NP;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = np0 + wn * 64 + j * 16 + (lane & 15);
+    if (col >= NP) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < a.g.Cout) dst[(int64_t)row * NP + col] = acc[i][j][r];
+      }
+  }
+}
+
+// EWVIT_CONV_GLDS=0 keeps every shape on the register-staged kernels (A/B runs)
+static int g_glds = -1;
+static bool use_glds() {
+  if (g_glds < 0) {
+    const char *e = getenv("EWVIT_CONV_GLDS");
+    g_glds = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_glds != 0;
 }
 
 // Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
@@ -551,6 +891,30 @@ static void launch_fwd(const FwdArgs &a, hipStream_t s) {
   else launch_fwd_ks<DGRAD, 3>(a, s);
 }
 
+// the LDS-DMA fwd/dgrad kernel when every K-tile stays in one tap and one channel
+// group and the operands fit 31-bit buffer offsets; false -> register-staged kernel
+template <bool DGRAD>
+static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
+  const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
+  if (!use_glds() || a.KC % 64 || a.sgc % 64 || src_bytes >= (int64_t)OOB || a.Ncol * K * 2 >= (int64_t)OOB ||
+      a.M * a.ogc >= (int64_t)1 << 40)
+    return false;
+  const int64_t mt = (a.M + 127) / 128;
+  if (a.Ncol <= 64) {
+    const int64_t nwg = mt;
+    if (nwg >= (int64_t)1 << 31) return false;
+    if (a.g.ks == 1) hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 1>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, 1);
+    else hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, 1);
+  } else {
+    const int ntn = (a.Ncol + 127) / 128;
+    const int64_t nwg = mt * ntn;
+    if (nwg >= (int64_t)1 << 31) return false;
+    if (a.g.ks == 1) hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 128, 1>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, ntn);
+    else hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 128, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, ntn);
+  }
+  return true;
+}
+
 static int check_geom(const ConvGeom &g, const char *nm) {
   EWVIT_CHECK_ARG(g.N > 0 && g.H > 0 && g.W > 0 && g.Cin > 0 && g.Cout > 0, "%s: empty shape", nm);
   EWVIT_CHECK_ARG(g.Cin % 8 == 0 && g.Cout % 8 == 0, "%s: Cin=%d Cout=%d must be multiples of 8", nm, g.Cin, g.Cout);
@@ -581,6 +945,12 @@ static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, 
 
 using namespace ewvit;
 
+extern "C" int ewvit_conv2d_set_glds(int on) {
+  const int prev = use_glds() ? 1 : 0;
+  g_glds = on ? 1 : 0;
+  return prev;
+}
+
 extern "C" int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t s_tap, void *wp,
                                         void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
                                         void *stream) {
@@ -605,7 +975,8 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
   a.M = (int64_t)g.N * g.Ho * g.Wo; a.Ncol = g.Cout; a.KC = g.Cin;
   a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
   a.sgc = (int)x_group_c; a.sgs = x_group_stride; a.ogc = g.Cout; a.ogs = 0;
-  launch_fwd<false>(a, as_stream(stream));
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  if (!launch_glds<false>(a, xb, as_stream(stream))) launch_fwd<false>(a, as_stream(stream));
   return launch_status("conv2d_fwd");
 }
 
@@ -621,7 +992,7 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
   a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
   a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
-  launch_fwd<true>(a, as_stream(stream));
+  if (!launch_glds<true>(a, 2 * N * (int64_t)g.Ho * g.Wo * Cout, as_stream(stream))) launch_fwd<true>(a, as_stream(stream));
   return launch_status("conv2d_bwd_data");
 }
 
@@ -643,7 +1014,8 @@ static int64_t wgrad_splits(const ConvGeom &g) {
 extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                                      int ksize, int stride) {
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
-  return wgrad_splits(g) * Cout * (ksize * ksize * Cin + 1) * (int64_t)sizeof(float);
+  const int64_t ntx = (ksize * ksize * Cin + CBN - 1) / CBN;
+  return wgrad_splits(g) * Cout * (ksize * ksize * Cin + ntx) * (int64_t)sizeof(float);
 }
 
 extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
@@ -661,21 +1033,33 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t splits = wgrad_splits(g);
   a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
   a.M = (int64_t)g.N * g.Ho * g.Wo;
+  const int ntx = (taps * g.Cin + CBN - 1) / CBN, nty = (g.Cout + CBM - 1) / CBM;
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
+  const int64_t kq = glds ? 64 : CBK;     // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
-  mper = (mper + CBK - 1) / CBK * CBK;
+  mper = (mper + kq - 1) / kq * kq;
   a.mper = mper;
   const int sp = (int)((a.M + mper - 1) / mper);
+  // the glds kernel leaves bias partials per (split, n'-tile); the old one per split
+  const int bparts = glds ? sp * ntx : sp;
   // one split of a 1x1 conv: the slab IS dW [Cout][Cin] (and dbias) — no reduce pass
-  const bool direct = sp == 1 && taps == 1 && !accumulate;
+  const bool direct = sp == 1 && taps == 1 && !accumulate && (!dbias || bparts == 1);
   if (direct) { a.part = dw; a.dbias_part = dbias; }
-  dim3 grid((unsigned)((taps * g.Cin + CBN - 1) / CBN), (unsigned)((g.Cout + CBM - 1) / CBM), (unsigned)sp);
   hipStream_t s = as_stream(stream);
-  if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), 0, s, a);
+  if (glds) {
+    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
+    if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_glds_kernel<1>, dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);
+    else hipLaunchKernelGGL(conv_wgrad_glds_kernel<3>, dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);
+  } else {
+    dim3 grid((unsigned)ntx, (unsigned)nty, (unsigned)sp);
+    if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), 0, s, a);
+  }
   if (int rc = launch_status("conv2d_bwd_weight")) return rc;
   if (direct) return 0;
   const int64_t n = (int64_t)g.Cout * taps * g.Cin;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, workspace, dw,
-                     g.Cout, g.Cin, taps, sp, accumulate, a.dbias_part, dbias);
+                     g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias);
   return launch_status("conv2d_bwd_weight reduce");
 }

@@ -36,6 +36,7 @@ SIGNATURES = {
     'ewvit_bn_fwd': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _f32, _f32, _i32, _vp, _vp, _i32, _vp,
                      _vp, _vp],
     'ewvit_bn_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
+    'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],

@@ -194,11 +194,12 @@ class MWT(nn.Module):
         # exact zeros): MIOpen's grouped weight-gradient kernel took ~0.3 s here.
         w = torch.cat([F.pad(sep[i][0].weight, (0, 0, 0, 0, i * C, (2 - i) * C)) for i in range(3)])
         b = torch.cat([sep[i][0].bias for i in range(3)])
-        # the fusion conv's MFMA kernel wants 8-aligned channels: emit the 18C
-        # seperate channels zero-padded to a multiple of 8 (zero weight rows and
-        # bias; an identity BN keeps them exactly 0 through BN + ReLU)
+        # the fusion conv's MFMA kernels want 8-aligned channels, and its LDS-DMA
+        # kernel whole 64-channel K-tiles: emit the 18C seperate channels zero-padded
+        # to a multiple of 64 (zero weight rows and bias; an identity BN keeps them
+        # exactly 0 through BN + ReLU, and the fusion weight's padded rows are zero)
         c18 = 18 * C
-        pad = (-c18) % 8
+        pad = (-c18) % 64
         if pad:
             w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, pad))
             b = F.pad(b, (0, pad))

@@ -12,6 +12,16 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
+@pytest.fixture(params=[1, 0], ids=['glds', 'regstage'])
+def glds(request):
+    """Run each case on the LDS-DMA kernels and on the register-staged ones."""
+    import ewvit
+    lib = ewvit._lib.load()
+    prev = lib.ewvit_conv2d_set_glds(request.param)
+    yield request.param
+    lib.ewvit_conv2d_set_glds(prev)
+
+
 def rel(a, b):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
@@ -30,8 +40,12 @@ def rel(a, b):
     (2, 64, 64, 256, 7, 9, 1, 1),        # 1x1 expand
     (1, 256, 256, 1280, 7, 7, 1, 1),     # head 1x1
     (2, 48, 48, 24, 10, 11, 2, 1),       # 1x1 stride 2, K-tile straddles nothing
+    (4, 128, 128, 128, 56, 56, 1, 3),    # many M tiles, split pixel reduction
+    (3, 64, 64, 384, 30, 31, 1, 3),      # 3 N tiles, ragged M
+    (2, 128, 128, 128, 57, 55, 2, 3),    # odd sizes, stride 2
+    (5, 64, 64, 64, 33, 35, 1, 1),       # 1x1, 64-wide output tile
 ])
-def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k):
+def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec
     g = torch.Generator().manual_seed(Cx * 7 + H + k)
     x = torch.randn(N, Cx, H, W, generator=g).to(torch.bfloat16)
@@ -60,8 +74,9 @@ def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k):
     assert rel(bd.grad, br.grad) < 1e-3
 
 
-@pytest.mark.parametrize('levels,N,C,Cout,H,W', [(3, 2, 128, 128, 14, 14), (2, 3, 32, 64, 9, 10)])
-def test_conv_level_major_input(levels, N, C, Cout, H, W):
+@pytest.mark.parametrize('levels,N,C,Cout,H,W', [(3, 2, 128, 128, 14, 14), (2, 3, 32, 64, 9, 10),
+                                               (3, 4, 128, 128, 40, 41)])
+def test_conv_level_major_input(levels, N, C, Cout, H, W, glds):
     """levels > 1: the conv reads z [L*N, C, H, W] as cat(z.chunk(L), 1) in place
     (the multiscale fusion input, mwt.py:112) and returns dz in z's layout."""
     import ewvit.conv as ec

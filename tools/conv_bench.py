@@ -1,5 +1,5 @@
 """Micro-benchmark of the ewvit conv kernels on the step's conv shapes.  Each phase
-(fwd, fwd+bwd) is recorded ITERS times into a HIP graph and replayed, so the
+(fwd, dgrad, wgrad: direct C-ABI calls, no autograd) is recorded ITERS times into a HIP graph and replayed, so the
 numbers are device time without Python launch overhead.  --mm also times the
 1x1 shapes as plain library GEMMs (torch.mm -> hipBLASLt) for comparison.
 Usage: python tools/conv_bench.py [--iters N] [--only NAME] [--mm]"""
@@ -49,31 +49,54 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--only', default=None)
     ap.add_argument('--mm', action='store_true')
+    ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--variants', default='1,0', help='conv kernel families to time: 1 LDS-DMA, 0 register-staged')
     a = ap.parse_args()
+    a.variants = [int(v) for v in a.variants.split(',')]
     import ewvit
     dev = torch.device('cuda', 0)
+    from ewvit import _lib as L
+    from ewvit.conv import _pack
+    lib = L.load()
     for name, (N, Cin, H, W, Cout, k, s, lv) in SHAPES.items():
         if a.only and a.only not in name:
             continue
-        x = torch.randn(N * lv, Cin, H, W, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
-        x.requires_grad_(True)
-        w = (torch.randn(Cout, Cin * lv, k, k, device=dev) / (k * k * Cin * lv) ** 0.5).requires_grad_(True)
-        y = ewvit.conv2d(x, w, None, s, lv)
+        Cx = Cin * lv
+        z = torch.randn(N * lv, Cin, H, W, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+        w = torch.randn(Cout, Cx, k, k, device=dev) / (k * k * Cx) ** 0.5
+        gc, gs = (Cin, N * H * W * Cin) if lv > 1 else (0, 0)
+        wp, wpt = _pack(w, Cx, True, True)
+        Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+        y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
         dy = torch.randn_like(y)
-        flops = 2.0 * y.numel() * Cin * lv * k * k
+        dx = torch.empty_like(z)
+        dw = torch.empty((Cout, Cx, k, k), device=dev)
+        ws = torch.empty(lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s) // 4, device=dev)
+
+        flops = 2.0 * N * Ho * Wo * Cout * k * k * Cx
 
         def fwd():
-            ewvit.conv2d(x, w, None, s, lv)
+            L.call('ewvit_conv2d_fwd', L.ptr(z), L.ptr(wp), None, L.ptr(y), N, H, W, Cx, Cout, k, s, gc, gs, L.stream(y))
 
-        def fwdbwd():
-            x.grad = None
-            w.grad = None
-            ewvit.conv2d(x, w, None, s, lv).backward(dy)
-        tf = graph_time(fwd, a.iters)
-        tb = graph_time(fwdbwd, a.iters)
-        fl_all = flops * (3 if s == 1 else 6)   # stride-2 dgrad runs the full dense tap set
-        line = (f'{name:16s} fwd {tf:8.1f} us {flops / tf / 1e6:7.1f} TF/s | fwd+bwd {tb:8.1f} us '
-                f'({fl_all / tb / 1e6:7.1f} TF/s incl. packs)')
+        def dgrad():
+            L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, s, gc, gs, L.stream(y))
+
+        def wgrad():
+            L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), None, 0, N, H, W, Cx, Cout, k, s,
+                   gc, gs, L.ptr(ws), L.stream(y))
+        rows = {}
+        for r in range(a.rounds):              # interleaved A/B rounds in one process
+            for v in a.variants:
+                lib.ewvit_conv2d_set_glds(v)
+                for pn, fn in (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad)):
+                    rows.setdefault((v, pn), []).append(graph_time(fn, a.iters))
+        lib.ewvit_conv2d_set_glds(1)
+        for v in a.variants:
+            parts = []
+            for pn in ('fwd', 'dgrad', 'wgrad'):
+                t = min(rows[(v, pn)])
+                parts.append(f'{pn} {t:8.1f} us {flops / t / 1e6:6.0f} TF/s')
+            print(f'{name:15s} [{"glds" if v else "regs"}] ' + ' | '.join(parts), flush=True)
         if a.mm and k == 1 and s == 1:
             M = N * H * W
             x2 = torch.randn(M, Cin, device=dev, dtype=torch.bfloat16)
@@ -82,8 +105,7 @@ def main():
             t1 = graph_time(lambda: torch.mm(x2, w2.t()), a.iters)
             t2 = graph_time(lambda: torch.mm(d2, w2), a.iters)
             t3 = graph_time(lambda: torch.mm(d2.t(), x2), a.iters)
-            line += f' || hipBLASLt fwd {t1:6.1f} dgrad {t2:6.1f} wgrad {t3:6.1f} us'
-        print(line, flush=True)
+            print(f'{name:15s} [hipBLASLt] fwd {t1:8.1f} us | dgrad {t2:8.1f} us | wgrad {t3:8.1f} us', flush=True)
 
 
 if __name__ == '__main__':
