@@ -531,19 +531,35 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// fwd / dgrad: 128 x BN_ x 64 tiles, 4 waves (2x2), [row][64 k] images of 128-B rows;
-// 16-B chunk c of row r is stored at chunk c ^ ((r >> 1) & 7): conflict-free b128 reads
-template <bool DGRAD, int BN_, int KS>
-__global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn) {
-  constexpr int BM = 128, BK = 64;
+// wait until at most the N youngest vector-memory ops (LDS-DMA pieces) are pending,
+// then the workgroup barrier; one asm statement, so hipcc neither drains the DMA
+// queue at the barrier nor moves LDS reads across it
+template <int N> __device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+// tile kt's pieces landed (L per tile per thread); `rem` younger tiles already issued
+// (at most NS-2 of them) may stay in flight across the barrier
+template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
+  if constexpr (NS >= 4) { if (rem >= 2) { wait_vm_barrier<2 * L>(); return; } }
+  if constexpr (NS >= 3) { if (rem >= 1) { wait_vm_barrier<L>(); return; } }
+  wait_vm_barrier<0>();
+}
+
+// fwd / dgrad: BM x BN_ x 64 tiles, BM/32 waves (BM/64 x 2), NS-deep LDS ring of
+// [row][64 k] images (128-B rows); 16-B chunk c of row r is stored at chunk
+// c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
+template <bool DGRAD, int BM, int BN_, int KS, int NS>
+__global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn) {
+  constexpr int NW = BM / 32, NT = NW * 64, BK = 64;
   constexpr int WN = BN_ / 2, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
-  constexpr int PA = BM / 8 / 4, PB = BN_ / 8 / 4;   // 1 KiB pieces per wave per K-tile
+  constexpr int PA = BM / 8 / NW, PB = BN_ / 8 / NW;   // 1 KiB pieces per wave per K-tile
   constexpr int CST = BN_ + 8;
-  static_assert(BM * CST * 2 <= 2 * STG, "epilogue tile must fit the staging LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
+  static_assert(PB >= 1 && BM * CST * 2 <= NS * STG, "tile shape");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
+  const int wm = ws >> 1, wn = ws & 1;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
@@ -554,59 +570,75 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_b
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
 
-  // A rows staged by this lane: piece p = w*PA + j covers rows 8p..8p+7
-  int py[PA], px[PA], lcA[PA];
-  int64_t pbase[PA];
-  bool av[PA];
+  // A rows staged by this lane: piece p = w*PA + j covers rows 8p..8p+7.  Every tap's
+  // source pixel is the row's base pixel plus a tap offset that is the same for all
+  // rows (fwd: +(kh*W + kw); dgrad: -(kh*W + kw), or -((kh/2)*W + kw/2) at stride 2),
+  // so a row keeps one byte offset and a mask of the taps that land inside the image
+  // (and, for stride-2 dgrad, on the stride lattice); a K-tile adds one scalar.
+  int rb[PA];
+  unsigned vmask[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
-    const int p = w * PA + j, r = p * 8 + (lane >> 3);
-    lcA[j] = (lane & 7) ^ ((r >> 1) & 7);
+    const int p = ws * PA + j, r = p * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
     const int64_t m = m0 + r;
-    av[j] = m < a.M;
-    const int64_t mm = av[j] ? m : 0;
+    const int64_t mm = m < a.M ? m : 0;
     const int ow = (int)(mm % a.outW);
     const int64_t t = mm / a.outW;
     const int oh = (int)(t % a.outH);
     const int n = (int)(t / a.outH);
-    if (!DGRAD) { py[j] = oh * a.g.stride - a.g.pad; px[j] = ow * a.g.stride - a.g.pad; }
-    else        { py[j] = oh + a.g.pad;               px[j] = ow + a.g.pad; }
-    pbase[j] = (int64_t)n * a.srcH * a.srcW;
+    int by, bx;            // base pixel (may lie outside the image)
+    unsigned msk = 0;
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        int sh, sw;
+        bool ok = m < a.M;
+        if (!DGRAD) {
+          sh = oh * a.g.stride - a.g.pad + kh; sw = ow * a.g.stride - a.g.pad + kw;
+        } else {
+          const int th = oh + a.g.pad - kh, tw = ow + a.g.pad - kw;
+          ok = ok && th >= 0 && tw >= 0 && !((th | tw) & smask);
+          sh = th >> ls; sw = tw >> ls;
+        }
+        ok = ok && (unsigned)sh < (unsigned)a.srcH && (unsigned)sw < (unsigned)a.srcW;
+        if (ok) msk |= 1u << (kh * KS + kw);
+      }
+    if (!DGRAD) { by = oh * a.g.stride - a.g.pad; bx = ow * a.g.stride - a.g.pad; }
+    else        { by = (oh + a.g.pad) >> ls;       bx = (ow + a.g.pad) >> ls; }
+    const int64_t pix = (int64_t)n * a.srcH * a.srcW + (int64_t)by * a.srcW + bx;
+    rb[j] = (int)((pix * a.sgc + lc * 8) * 2);
+    vmask[j] = msk;
   }
   uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
-    const int p = w * PB + j, r = p * 8 + (lane >> 3);
+    const int p = ws * PB + j, r = p * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((r >> 1) & 7);
     const int n = n0 + r;
     boff[j] = n < a.Ncol ? (uint32_t)(((int64_t)n * K + lc * 8) * 2) : OOB;
   }
-  int ltap = 0, lcb = 0;
+  // K-tile cursor: tap, channel block within the tap, group index / offset of the block
+  int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
   auto stage = [&](int kt, int buf) {
-    const int kh = ltap / KS, kw = ltap - (ltap / KS) * KS;
-    const int c0 = lcb * BK;
-    const int gi = c0 / a.sgc;
-    const int64_t goff = (int64_t)gi * a.sgs + (c0 - gi * a.sgc);
-    if (++lcb == cbn) { lcb = 0; ++ltap; }
-    unsigned char *base = smem + buf * STG;
+    const int kh = ltap / KS, kw = ltap - kh * KS;
+    int dpix;
+    if (!DGRAD) dpix = kh * a.srcW + kw;
+    else dpix = -((kh >> ls) * a.srcW + (kw >> ls));
+    const int sdelta = (int)(((int64_t)dpix * a.sgc + (int64_t)lgi * a.sgs + lcin) * 2);
+    const int tap = ltap;
+    lcin += BK;
+    if (lcin == a.sgc) { lcin = 0; ++lgi; }
+    if (++lcb == cbn) { lcb = 0; ++ltap; lgi = 0; lcin = 0; }
+    unsigned char *base = smem + buf * STG + ws * PA * 1024;
 #pragma unroll
-    for (int j = 0; j < PA; ++j) {
-      int sh, sw;
-      bool ok = av[j];
-      if (!DGRAD) {
-        sh = py[j] + kh; sw = px[j] + kw;
-      } else {
-        const int th = py[j] - kh, tw = px[j] - kw;
-        ok = ok && th >= 0 && tw >= 0 && !((th | tw) & smask);
-        sh = th >> ls; sw = tw >> ls;
-      }
-      ok = ok && (unsigned)sh < (unsigned)a.srcH && (unsigned)sw < (unsigned)a.srcW;
-      const int64_t e = goff + (pbase[j] + (int64_t)sh * a.srcW + sw) * a.sgc + lcA[j] * 8;
-      glds16(rs, base + (w * PA + j) * 1024, ok ? (uint32_t)(e * 2) : OOB);
-    }
+    for (int j = 0; j < PA; ++j)
+      glds16(rs, base + j * 1024, (vmask[j] >> tap) & 1u ? (uint32_t)(rb[j] + sdelta) : OOB);
+    unsigned char *bb = smem + buf * STG + A_B + ws * PB * 1024;
+    const uint32_t kb = (uint32_t)(kt * BK * 2);
 #pragma unroll
-    for (int j = 0; j < PB; ++j)
-      glds16(rw, base + A_B + (w * PB + j) * 1024, boff[j] == OOB ? OOB : boff[j] + (uint32_t)(kt * BK * 2));
+    for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
   };
 
   cf32x4 acc[4][J];
@@ -634,16 +666,23 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_b
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    compute(cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  int ld = 0, lbuf = 0;
+  for (; ld < NS - 1 && ld < nk; ++ld) {
+    stage(ld, lbuf);
+    lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
   }
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tile<PA + PB, NS>(nk - 1 - kt);
+    if (ld < nk) {           // refill the buffer every wave finished reading at kt-1
+      stage(ld, lbuf);
+      ++ld;
+      lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+    }
+    compute(cur);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  __syncthreads();
   // epilogue: (+ bias) -> bf16 tile image -> 16-B row-contiguous stores
   bf16_t *ep = reinterpret_cast<bf16_t *>(smem);
 #pragma unroll
@@ -658,8 +697,8 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_b
   __syncthreads();
   constexpr int VPR = BN_ / 8;
 #pragma unroll
-  for (int k = 0; k < BM * VPR / 256; ++k) {
-    const int v = tid + 256 * k;
+  for (int k = 0; k < BM * VPR / NT; ++k) {
+    const int v = tid + NT * k;
     const int rl = v / VPR, cv = v % VPR;
     const int64_t row = m0 + rl;
     const int col = n0 + cv * 8;
@@ -671,17 +710,16 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(FwdArgs a, int64_t src_b
   }
 }
 
-// wgrad: C[co][n'] over pixel K-tiles of 64; [pixel][128] images of 256-B rows, chunk
-// c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed, ds_read_b64_tr_b16).
-// Bias gradient (sum of dy over pixels): the blocks of n'-tile t sum the dy image of
-// the K-tiles kt = t (mod n'-tiles), so the extra LDS reads are spread evenly.
-template <int KS>
+// wgrad: C[co][n'] over pixel K-tiles of BK; NS-deep ring of [pixel][128] images of
+// 256-B rows, chunk c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed,
+// ds_read_b64_tr_b16).  Bias gradient (sum of dy over pixels): the blocks of n'-tile
+// t sum the dy image of the K-tiles kt = t (mod n'-tiles), spreading the extra reads.
+template <int KS, int BK, int NS>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
-  constexpr int BK = 64, IMG = BK * 256, STG = 2 * IMG;
-  constexpr int P = BK / 4 / 4;     // pieces (4 rows x 256 B) per wave per image
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
+  constexpr int IMG = BK * 256, STG = 2 * IMG;
+  constexpr int P = BK / 16;        // pieces (4 rows x 256 B) per wave per image
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
@@ -693,46 +731,58 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, x_bytes);
   const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * a.g.Cout * 2);
 
-  // piece p = w*P + j: rows 4p .. 4p+3; lane -> row 4p + lane/16, stored chunk lane%16
-  int lc[P], tkh[P], tkw[P], pn[P], poh[P], pw[P];
-  int64_t bgoff[P];
+  // piece p = ws*P + j: rows 4p .. 4p+3; lane -> row 4p + lane/16, stored chunk lane%16.
+  // A K-tile's first pixel (n0, oh0, ow0) is tracked in scalars; a row's pixel is that
+  // plus r, carried through (ow, oh) with exact multiply-high divisions (r < 64).
+  const int ws = __builtin_amdgcn_readfirstlane(w);
+  const int wm = ws >> 1, wn = ws & 1;
+  int rr[P], tkh[P], tkw[P], aoff[P], bgo[P];
   bool bok[P], aok[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) {
-    const int p = w * P + j, r = p * 4 + (lane >> 4);
-    lc[j] = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
-    aok[j] = co0 + lc[j] * 8 < a.g.Cout;
-    const int np = np0 + lc[j] * 8;
+    const int p = ws * P + j, r = p * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    rr[j] = r;
+    aok[j] = co0 + lc * 8 < a.g.Cout;
+    aoff[j] = (int)(((mbeg + r) * a.g.Cout + co0 + lc * 8) * 2);
+    const int np = np0 + lc * 8;
     bok[j] = np < NP;
     const int btap = bok[j] ? np / a.g.Cin : 0;
     const int bci = bok[j] ? np - btap * a.g.Cin : 0;
     tkh[j] = btap / KS - a.g.pad;
     tkw[j] = btap % KS - a.g.pad;
     const int gi = bci / a.xgc;
-    bgoff[j] = (int64_t)gi * a.xgs + (bci - gi * a.xgc);
-    const int64_t m = mbeg + r;
-    pw[j] = (int)(m % a.g.Wo);
-    const int64_t t = m / a.g.Wo;
-    poh[j] = (int)(t % a.g.Ho);
-    pn[j] = (int)(t / a.g.Ho);
+    bgo[j] = (int)(((int64_t)gi * a.xgs + (bci - gi * a.xgc)) * 2);
   }
+  // exact floor(x / d) = umulhi(x, ceil(2^32 / d)) for x < 2^32 / d
+  const uint32_t magW = (uint32_t)((0x100000000ull + a.g.Wo - 1) / a.g.Wo);
+  const uint32_t magH = (uint32_t)((0x100000000ull + a.g.Ho - 1) / a.g.Ho);
+  int sn = (int)(mbeg / ((int64_t)a.g.Ho * a.g.Wo));
+  int soh = (int)((mbeg / a.g.Wo) % a.g.Ho);
+  int sow = (int)(mbeg % a.g.Wo);
+  const int xrow = a.xgc * 2;                       // bytes per pixel step
   auto stage = [&](int kt, int buf) {
-    unsigned char *base = smem + buf * STG;
+    unsigned char *base = smem + buf * STG + ws * P * 1024;
+    const int lim = (int)(mend - mbeg) - kt * BK;   // rows r < lim are inside the split
+    const int adel = kt * BK * a.g.Cout * 2;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
-      const int64_t m = mbeg + (int64_t)kt * BK + (w * P + j) * 4 + (lane >> 4);
-      const bool mv = m < mend;
-      glds16(rd, base + (w * P + j) * 1024,
-             mv && aok[j] ? (uint32_t)((m * a.g.Cout + co0 + lc[j] * 8) * 2) : OOB);
-      const int ih = poh[j] * a.g.stride + tkh[j], iw = pw[j] * a.g.stride + tkw[j];
-      const bool ok = mv && bok[j] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W;
-      const int64_t e = bgoff[j] + (((int64_t)pn[j] * a.g.H + ih) * a.g.W + iw) * a.xgc;
-      glds16(rx, base + IMG + (w * P + j) * 1024, ok ? (uint32_t)(e * 2) : OOB);
-      pw[j] += BK;
-      while (pw[j] >= a.g.Wo) {
-        pw[j] -= a.g.Wo;
-        if (++poh[j] == a.g.Ho) { poh[j] = 0; ++pn[j]; }
-      }
+      glds16(rd, base + j * 1024, rr[j] < lim && aok[j] ? (uint32_t)(aoff[j] + adel) : OOB);
+      const uint32_t owt = (uint32_t)(sow + rr[j]);
+      const uint32_t q = __umulhi(owt, magW);
+      const int ow = (int)(owt - q * a.g.Wo);
+      const uint32_t oht = (uint32_t)soh + q;
+      const uint32_t q2 = __umulhi(oht, magH);
+      const int oh = (int)(oht - q2 * a.g.Ho);
+      const int n = sn + (int)q2;
+      const int ih = oh * a.g.stride + tkh[j], iw = ow * a.g.stride + tkw[j];
+      const bool ok = rr[j] < lim && bok[j] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W;
+      glds16(rx, base + IMG + j * 1024, ok ? (uint32_t)(((n * a.g.H + ih) * a.g.W + iw) * xrow + bgo[j]) : OOB);
+    }
+    sow += BK;                                      // next K-tile's first pixel (scalar)
+    while (sow >= a.g.Wo) {
+      sow -= a.g.Wo;
+      if (++soh == a.g.Ho) { soh = 0; ++sn; }
     }
   };
   auto tr_read = [&](const unsigned char *img, int k0, int c0) -> cs4 {
@@ -774,10 +824,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (do_bias && kt % ntx == tx) {
-      // thread t: rows (t>>4)*4 .. +3 of the dy image, chunk t & 15 (8 channels)
+      // thread t: rows (t>>4)*(BK/16) .. of the dy image, chunk t & 15 (8 channels)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = (tid >> 4) * 4 + q;
+      for (int q = 0; q < BK / 16; ++q) {
+        const int r = (tid >> 4) * (BK / 16) + q;
         const uint4 v = *reinterpret_cast<const uint4 *>(As + swz_off(r, tid & 15));
         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -788,16 +838,23 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
       }
     }
   };
-  if (nk > 0) stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    compute(kt, cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  int ld = 0, lbuf = 0;
+  for (; ld < NS - 1 && ld < nk; ++ld) {
+    stage(ld, lbuf);
+    lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
   }
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tile<2 * P, NS>(nk - 1 - kt);
+    if (ld < nk) {
+      stage(ld, lbuf);
+      ++ld;
+      lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+    }
+    compute(kt, cur);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  __syncthreads();
   if (do_bias) {
     // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves
 #pragma unroll
@@ -833,15 +890,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   }
 }
 
-// EWVIT_CONV_GLDS=0 keeps every shape on the register-staged kernels (A/B runs)
+// Kernel family: 0 register-staged everywhere; 1.. LDS-DMA configurations
+//   fwd/dgrad (rows per tile, ring depth): 1 (128, 2)  2 (128, 3)  3 (256, 2)  4 (256, 3)
+//   wgrad (pixels per K-tile, ring depth): 1 (64, 2)   2 (64, 3)   3 (32, 3)   4 (32, 4)
+// EWVIT_CONV_GLDS=<n> or ewvit_conv2d_set_glds(n) select one (A/B measurement).
 static int g_glds = -1;
-static bool use_glds() {
+static int glds_variant() {
   if (g_glds < 0) {
     const char *e = getenv("EWVIT_CONV_GLDS");
-    g_glds = (e && e[0] == '0') ? 0 : 1;
+    g_glds = e && e[0] >= '0' && e[0] <= '4' ? e[0] - '0' : 1;
   }
-  return g_glds != 0;
+  return g_glds;
 }
+static bool use_glds() { return glds_variant() != 0; }
 
 // Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
 // else 32; register prefetch depth from EWVIT_CONV_PF (1 or 2, default 1).
@@ -899,19 +960,37 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   if (!use_glds() || a.KC % 64 || a.sgc % 64 || src_bytes >= (int64_t)OOB || a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
-  const int64_t mt = (a.M + 127) / 128;
-  if (a.Ncol <= 64) {
-    const int64_t nwg = mt;
-    if (nwg >= (int64_t)1 << 31) return false;
-    if (a.g.ks == 1) hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 1>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, 1);
-    else hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, 1);
+  const int v = glds_variant();
+  const int BM = v >= 3 ? 256 : 128;
+  const int64_t mt = (a.M + BM - 1) / BM;
+  const int bn = a.Ncol <= 64 ? 64 : 128;
+  const int ntn = (a.Ncol + bn - 1) / bn;
+  const int64_t nwg = mt * ntn;
+  if (nwg >= (int64_t)1 << 31) return false;
+  const dim3 grid((unsigned)nwg);
+#define EWVIT_GLDS_FWD(BM_, BN__, NS_)                                                                              \
+  do {                                                                                                            \
+    if (a.g.ks == 1)                                                                                              \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn); \
+  } while (0)
+  if (bn == 64) {
+    switch (v) {
+      case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
+      case 3: EWVIT_GLDS_FWD(256, 64, 2); break;
+      case 4: EWVIT_GLDS_FWD(256, 64, 3); break;
+      default: EWVIT_GLDS_FWD(128, 64, 2); break;
+    }
   } else {
-    const int ntn = (a.Ncol + 127) / 128;
-    const int64_t nwg = mt * ntn;
-    if (nwg >= (int64_t)1 << 31) return false;
-    if (a.g.ks == 1) hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 128, 1>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, ntn);
-    else hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 128, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, src_bytes, ntn);
+    switch (v) {
+      case 2: EWVIT_GLDS_FWD(128, 128, 3); break;
+      case 3: EWVIT_GLDS_FWD(256, 128, 2); break;
+      case 4: EWVIT_GLDS_FWD(256, 128, 3); break;
+      default: EWVIT_GLDS_FWD(128, 128, 2); break;
+    }
   }
+#undef EWVIT_GLDS_FWD
   return true;
 }
 
@@ -945,9 +1024,9 @@ static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, 
 
 using namespace ewvit;
 
-extern "C" int ewvit_conv2d_set_glds(int on) {
-  const int prev = use_glds() ? 1 : 0;
-  g_glds = on ? 1 : 0;
+extern "C" int ewvit_conv2d_set_glds(int variant) {
+  const int prev = glds_variant();
+  g_glds = variant >= 0 && variant <= 4 ? variant : 1;
   return prev;
 }
 
@@ -1036,7 +1115,8 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int ntx = (taps * g.Cin + CBN - 1) / CBN, nty = (g.Cout + CBM - 1) / CBM;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
-  const int64_t kq = glds ? 64 : CBK;     // K-tile depth (pixels)
+  const int gv = glds_variant();
+  const int64_t kq = !glds ? CBK : (gv >= 3 ? 32 : 64);     // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
   mper = (mper + kq - 1) / kq * kq;
   a.mper = mper;
@@ -1049,8 +1129,18 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   hipStream_t s = as_stream(stream);
   if (glds) {
     const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
-    if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_glds_kernel<1>, dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);
-    else hipLaunchKernelGGL(conv_wgrad_glds_kernel<3>, dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);
+#define EWVIT_GLDS_WG(BK_, NS_)                                                                             \
+  do {                                                                                                    \
+    if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
+    else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
+  } while (0)
+    switch (gv) {
+      case 2: EWVIT_GLDS_WG(64, 3); break;
+      case 3: EWVIT_GLDS_WG(32, 3); break;
+      case 4: EWVIT_GLDS_WG(32, 4); break;
+      default: EWVIT_GLDS_WG(64, 2); break;
+    }
+#undef EWVIT_GLDS_WG
   } else {
     dim3 grid((unsigned)ntx, (unsigned)nty, (unsigned)sp);
     if (ksize == 1) hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), 0, s, a);

@@ -211,10 +211,11 @@ int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, 
 int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t s_tap, void *wp,
                              void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
                              void *stream);
-/* Kernel-family switch for A/B measurement (not needed for correctness): 1 (default,
- * or EWVIT_CONV_GLDS unset/!=0) stages operands by LDS-DMA where the shape allows,
- * 0 uses the register-staged kernels everywhere.  Returns the previous setting. */
-int ewvit_conv2d_set_glds(int on);
+/* Kernel-family switch for A/B measurement (not needed for correctness): 0 uses the
+ * register-staged kernels everywhere; 1..4 (default 1, or EWVIT_CONV_GLDS) select an
+ * LDS-DMA tile / ring-depth configuration where the shape allows (csrc/conv.hip).
+ * Returns the previous setting. */
+int ewvit_conv2d_set_glds(int variant);
 /* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
 int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                      int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,

@@ -12,9 +12,9 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.fixture(params=[1, 0], ids=['glds', 'regstage'])
+@pytest.fixture(params=[1, 2, 3, 4, 0], ids=['glds1', 'glds2', 'glds3', 'glds4', 'regstage'])
 def glds(request):
-    """Run each case on the LDS-DMA kernels and on the register-staged ones."""
+    """Run each case on every LDS-DMA configuration and on the register-staged kernels."""
     import ewvit
     lib = ewvit._lib.load()
     prev = lib.ewvit_conv2d_set_glds(request.param)

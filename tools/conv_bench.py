@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, 'efficient-wavelet-vit_amd'))
 
 # name: (N, Cin, H, W, Cout, k, stride, levels)
 SHAPES = {
-    'mwt_fusion': (192, 56, 112, 112, 128, 3, 1, 1),
+    'mwt_fusion': (192, 64, 112, 112, 128, 3, 1, 1),
     'mwt_multiscale': (64, 128, 112, 112, 128, 3, 1, 3),
     'mwt_freq_conv': (64, 128, 112, 112, 128, 3, 2, 1),
     'bb_s2_fused': (64, 48, 56, 56, 192, 3, 1, 1),
@@ -50,7 +50,7 @@ def main():
     ap.add_argument('--only', default=None)
     ap.add_argument('--mm', action='store_true')
     ap.add_argument('--rounds', type=int, default=3)
-    ap.add_argument('--variants', default='1,0', help='conv kernel families to time: 1 LDS-DMA, 0 register-staged')
+    ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged')
     a = ap.parse_args()
     a.variants = [int(v) for v in a.variants.split(',')]
     import ewvit
@@ -96,7 +96,7 @@ def main():
             for pn in ('fwd', 'dgrad', 'wgrad'):
                 t = min(rows[(v, pn)])
                 parts.append(f'{pn} {t:8.1f} us {flops / t / 1e6:6.0f} TF/s')
-            print(f'{name:15s} [{"glds" if v else "regs"}] ' + ' | '.join(parts), flush=True)
+            print(f'{name:15s} [{f"glds{v}" if v else "regs "}] ' + ' | '.join(parts), flush=True)
         if a.mm and k == 1 and s == 1:
             M = N * H * W
             x2 = torch.randn(M, Cin, device=dev, dtype=torch.bfloat16)
