@@ -77,6 +77,8 @@ def kernel_table(records):
     """Per ewvit entry point: launches, mean duration, algorithmic rate."""
     table = {}
     for name, recs in records.items():
+        if name.startswith('__'):
+            continue
         ms = [s.elapsed_time(e) for s, e, _ in recs]
         if not ms:
             continue

@@ -463,26 +463,46 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]
+// dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]; a thread
+// sums 4 consecutive slab elements (one 16-B load per split, 4 splits in flight)
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
                                                                 int Cout, int Cin, int taps, int splits, int bparts,
                                                                 int accumulate, const float *__restrict__ dbias_part,
                                                                 float *__restrict__ dbias) {
   const int64_t NP = taps * (int64_t)Cin;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in part layout
-  if (dbias && i < Cout) {
+  const int64_t n = (int64_t)Cout * NP;                                // n % 4 == 0 (Cin % 8 == 0)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (dbias && t < Cout) {
     float sb = 0.f;
-    for (int k = 0; k < bparts; ++k) sb += dbias_part[(int64_t)k * Cout + i];
-    dbias[i] = accumulate ? dbias[i] + sb : sb;
+    for (int k = 0; k < bparts; ++k) sb += dbias_part[(int64_t)k * Cout + t];
+    dbias[t] = accumulate ? dbias[t] + sb : sb;
   }
-  if (i >= (int64_t)Cout * NP) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * Cout * NP + i];
+  const int64_t i = t * 4;
+  if (i >= n) return;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+  int k = 0;
+  for (; k + 3 < splits; k += 4) {
+    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + i);
+    const float4 b = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 1) * n + i);
+    const float4 c = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 2) * n + i);
+    const float4 d = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 3) * n + i);
+    s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+    s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
+    s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
+  }
+  for (; k < splits; ++k) {
+    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + i);
+    s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+  }
+  const float r[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                      (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w)};
   const int co = (int)(i / NP);
   const int np = (int)(i % NP);
   const int tap = np / Cin, ci = np % Cin;
   const int64_t o = ((int64_t)co * Cin + ci) * taps + tap;
-  dw[o] = accumulate ? dw[o] + s : s;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dw[o + e * taps] = accumulate ? dw[o + e * taps] + r[e] : r[e];
 }
 
 // pack fp32 W (element (co, ci, tap) at co*s_co + ci*s_ci + tap*s_tap: any of the
@@ -549,7 +569,7 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // [row][64 k] images (128-B rows); 16-B chunk c of row r is stored at chunk
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
 template <bool DGRAD, int BM, int BN_, int KS, int NS>
-__global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn) {
+__global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn, int tap_inner) {
   constexpr int NW = BM / 32, NT = NW * 64, BK = 64;
   constexpr int WN = BN_ / 2, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
@@ -619,7 +639,10 @@ __global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t sr
     const int n = n0 + r;
     boff[j] = n < a.Ncol ? (uint32_t)(((int64_t)n * K + lc * 8) * 2) : OOB;
   }
-  // K-tile cursor: tap, channel block within the tap, group index / offset of the block
+  // K-tile cursor: tap, channel block, group index / offset of the block.  With
+  // tap_inner the 9 taps of one 64-channel block are consecutive K-tiles, so a block's
+  // live input window (its pixels + halo, 64 channels) stays small enough for the
+  // XCD's L2 to serve the tap re-reads; otherwise taps are outer.
   int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
   auto stage = [&](int kt, int buf) {
     const int kh = ltap / KS, kw = ltap - kh * KS;
@@ -628,15 +651,23 @@ __global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t sr
     else dpix = -((kh >> ls) * a.srcW + (kw >> ls));
     const int sdelta = (int)(((int64_t)dpix * a.sgc + (int64_t)lgi * a.sgs + lcin) * 2);
     const int tap = ltap;
-    lcin += BK;
-    if (lcin == a.sgc) { lcin = 0; ++lgi; }
-    if (++lcb == cbn) { lcb = 0; ++ltap; lgi = 0; lcin = 0; }
+    const uint32_t kb = (uint32_t)((ltap * a.KC + lcb * BK) * 2);
+    if (tap_inner) {
+      if (++ltap == KS * KS) {
+        ltap = 0; ++lcb;
+        lcin += BK;
+        if (lcin == a.sgc) { lcin = 0; ++lgi; }
+      }
+    } else {
+      lcin += BK;
+      if (lcin == a.sgc) { lcin = 0; ++lgi; }
+      if (++lcb == cbn) { lcb = 0; ++ltap; lgi = 0; lcin = 0; }
+    }
     unsigned char *base = smem + buf * STG + ws * PA * 1024;
 #pragma unroll
     for (int j = 0; j < PA; ++j)
       glds16(rs, base + j * 1024, (vmask[j] >> tap) & 1u ? (uint32_t)(rb[j] + sdelta) : OOB);
     unsigned char *bb = smem + buf * STG + A_B + ws * PB * 1024;
-    const uint32_t kb = (uint32_t)(kt * BK * 2);
 #pragma unroll
     for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
   };
@@ -893,16 +924,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
 // Kernel family: 0 register-staged everywhere; 1.. LDS-DMA configurations
 //   fwd/dgrad (rows per tile, ring depth): 1 (128, 2)  2 (128, 3)  3 (256, 2)  4 (256, 3)
 //   wgrad (pixels per K-tile, ring depth): 1 (64, 2)   2 (64, 3)   3 (32, 3)   4 (32, 4)
+// +8: fwd/dgrad K-tiles ordered channel-block outer, tap inner.
 // EWVIT_CONV_GLDS=<n> or ewvit_conv2d_set_glds(n) select one (A/B measurement).
 static int g_glds = -1;
 static int glds_variant() {
   if (g_glds < 0) {
     const char *e = getenv("EWVIT_CONV_GLDS");
-    g_glds = e && e[0] >= '0' && e[0] <= '4' ? e[0] - '0' : 1;
+    g_glds = e ? atoi(e) : 9;
+    if ((g_glds & 7) > 4 || g_glds < 0 || g_glds > 15) g_glds = 9;
   }
   return g_glds;
 }
-static bool use_glds() { return glds_variant() != 0; }
+static bool use_glds() { return (glds_variant() & 7) != 0; }
 
 // Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
 // else 32; register prefetch depth from EWVIT_CONV_PF (1 or 2, default 1).
@@ -960,7 +993,8 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   if (!use_glds() || a.KC % 64 || a.sgc % 64 || src_bytes >= (int64_t)OOB || a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
-  const int v = glds_variant();
+  const int v = glds_variant() & 7;
+  const int tap_inner = (glds_variant() & 8) ? 1 : 0;
   const int BM = v >= 3 ? 256 : 128;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int bn = a.Ncol <= 64 ? 64 : 128;
@@ -971,9 +1005,9 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
 #define EWVIT_GLDS_FWD(BM_, BN__, NS_)                                                                              \
   do {                                                                                                            \
     if (a.g.ks == 1)                                                                                              \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn); \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn, tap_inner); \
     else                                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn); \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn, tap_inner); \
   } while (0)
   if (bn == 64) {
     switch (v) {
@@ -1026,7 +1060,7 @@ using namespace ewvit;
 
 extern "C" int ewvit_conv2d_set_glds(int variant) {
   const int prev = glds_variant();
-  g_glds = variant >= 0 && variant <= 4 ? variant : 1;
+  g_glds = variant >= 0 && variant <= 15 && (variant & 7) <= 4 ? variant : 9;
   return prev;
 }
 
@@ -1077,14 +1111,17 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
 
 // split of the pixel reduction: ~768 workgroups (3 per CU), >= 32 K-tiles per split,
 // and f32 partial slabs no larger than half the bf16 operands they reduce
+// split of the pixel reduction: at most 512 workgroups — the 2 per CU that registers
+// and LDS allow, so every split runs in the first (only) round — >= 4 K-tiles of 64
+// pixels per split, and f32 partial slabs no larger than 4x the bf16 operands
 static int64_t wgrad_splits(const ConvGeom &g) {
   const int64_t M = (int64_t)g.N * g.Ho * g.Wo;
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
   const int64_t tiles = ((NP + CBN - 1) / CBN) * ((g.Cout + CBM - 1) / CBM);
-  int64_t s = (768 + tiles - 1) / tiles;
-  const int64_t maxs = (M + 32 * CBK - 1) / (32 * CBK);
+  int64_t s = 512 / tiles;
+  const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;
-  const int64_t cap = M * ((int64_t)g.Cin + g.Cout) / (4 * (int64_t)g.Cout * NP);
+  const int64_t cap = 2 * M * ((int64_t)g.Cin + g.Cout) / ((int64_t)g.Cout * NP);
   if (s > cap) s = cap;
   if (s < 1) s = 1;
   return s;
@@ -1115,7 +1152,7 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int ntx = (taps * g.Cin + CBN - 1) / CBN, nty = (g.Cout + CBM - 1) / CBM;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
-  const int gv = glds_variant();
+  const int gv = glds_variant() & 7;
   const int64_t kq = !glds ? CBK : (gv >= 3 ? 32 : 64);     // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
   mper = (mper + kq - 1) / kq * kq;
@@ -1148,8 +1185,9 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   }
   if (int rc = launch_status("conv2d_bwd_weight")) return rc;
   if (direct) return 0;
-  const int64_t n = (int64_t)g.Cout * taps * g.Cin;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, workspace, dw,
+  const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
+  const int64_t nt = n4 > g.Cout ? n4 : g.Cout;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, workspace, dw,
                      g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias);
   return launch_status("conv2d_bwd_weight reduce");
 }

@@ -102,6 +102,11 @@ def timing_records():
     return _timers or {}
 
 
+def timing_detail():
+    """[(entry, integer args, start event, end event)] in launch order (layer attribution)."""
+    return (_timers or {}).get('__detail__', [])
+
+
 def call(name, *args, work=None):
     rec = _timers is not None
     if rec:
@@ -114,6 +119,8 @@ def call(name, *args, work=None):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         _timers.setdefault(name, []).append((s, e, work or {}))
+        ints = tuple(a for a in args if isinstance(a, int) and not isinstance(a, bool))
+        _timers.setdefault('__detail__', []).append((name, ints, s, e))
 
 
 def dt(t):

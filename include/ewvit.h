@@ -212,7 +212,8 @@ int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t
                              void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
                              void *stream);
 /* Kernel-family switch for A/B measurement (not needed for correctness): 0 uses the
- * register-staged kernels everywhere; 1..4 (default 1, or EWVIT_CONV_GLDS) select an
+ * register-staged kernels everywhere; 1..4 (+8: tap-inner K order; default 9, or
+ * EWVIT_CONV_GLDS) select an
  * LDS-DMA tile / ring-depth configuration where the shape allows (csrc/conv.hip).
  * Returns the previous setting. */
 int ewvit_conv2d_set_glds(int variant);

@@ -22,6 +22,7 @@ SHAPES = {
     'bb_s5_expand': (64, 160, 14, 14, 960, 1, 1, 1),
     'bb_s5_project': (64, 960, 14, 14, 160, 1, 1, 1),
     'bb_s6_expand': (64, 256, 7, 7, 1536, 1, 1, 1),
+    'bb_s6_project': (64, 1536, 7, 7, 256, 1, 1, 1),
     'bb_head': (64, 256, 7, 7, 1280, 1, 1, 1),
 }
 
