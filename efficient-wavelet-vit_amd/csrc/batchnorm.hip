@@ -85,32 +85,40 @@ __device__ __forceinline__ void st8(void *p, int64_t i, const float (&v)[8]) {
 template <int ACT>
 __device__ __forceinline__ float act_fwd(float z) {
   if (ACT == 1) return z > 0.f ? z : 0.f;
-  if (ACT == 2) return z / (1.f + __expf(-z));
+  if (ACT == 2) return z * __builtin_amdgcn_rcpf(1.f + __expf(-z));   // v_rcp_f32 (1 ulp), not IEEE div
   return z;
 }
 template <int ACT>
 __device__ __forceinline__ float act_grad(float z) {
   if (ACT == 1) return z > 0.f ? 1.f : 0.f;
   if (ACT == 2) {
-    const float s = 1.f / (1.f + __expf(-z));
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-z));
     return s * (1.f + z * (1.f - s));
   }
   return 1.f;
 }
 
 struct BnPlan {
-  int C8, R, nblocks;
+  int C8, R, threads, nblocks;
   int64_t rows_per_block;
 };
 
-// elementwise passes (apply, dx): aim at ~1024 blocks (4 per CU) so the small
-// late-stage maps (e.g. 64x7x7 rows x 1536 ch) still fill the chip; 1..64 rows/thread
-static BnPlan bn_plan(int64_t M, int64_t C) {
-  BnPlan p;
+// R row groups of C8 channel-vector threads per block; the block is R*C8 threads
+// rounded up to whole waves (no idle quarter-blocks when C8 does not divide 256)
+static void bn_shape(BnPlan &p, int64_t C) {
   p.C8 = (int)(C / 8);
   p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
+  p.threads = (p.R * p.C8 + 63) / 64 * 64;
+}
+
+// elementwise passes (apply, dx): ~1024 blocks (4 per CU) for the large maps, but at
+// least 8 rows per thread, so the per-channel constants a thread loads are amortised
+// over its rows on the small late-stage maps (e.g. 64x7x7 rows x 1536 ch); <= 64 rows
+static BnPlan bn_plan(int64_t M, int64_t C) {
+  BnPlan p;
+  bn_shape(p, C);
   int64_t rpt = (M + (int64_t)p.R * 1024 - 1) / ((int64_t)p.R * 1024);
-  rpt = rpt < 1 ? 1 : (rpt > 64 ? 64 : rpt);
+  rpt = rpt < 8 ? 8 : (rpt > 64 ? 64 : rpt);
   p.rows_per_block = (int64_t)p.R * rpt;
   int64_t nb = (M + p.rows_per_block - 1) / p.rows_per_block;
   if (nb < 1) nb = 1;
@@ -118,13 +126,14 @@ static BnPlan bn_plan(int64_t M, int64_t C) {
   return p;
 }
 
-// reduction passes (stats, bwd sums): ~512 blocks over all groups, >= 16 rows per
+// reduction passes (stats, bwd sums): <= 256 blocks per group (the finalize sums a
+// group's partial rows in one batch of loads), ~512 over all groups, >= 16 rows per
 // thread, so the partial slabs stay small next to the tensor they summarise
 static BnPlan bn_red_plan(int64_t M, int64_t C, int groups) {
   BnPlan p;
-  p.C8 = (int)(C / 8);
-  p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
+  bn_shape(p, C);
   int64_t nb = (512 + groups - 1) / groups;
+  if (nb > 256) nb = 256;
   const int64_t maxnb = M / ((int64_t)p.R * 16);
   if (nb > maxnb) nb = maxnb;
   if (nb < 1) nb = 1;
@@ -213,37 +222,32 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ 
   }
 }
 
-// Sum the partial slab column c over nblocks rows: 32 channels x 8 partial lanes per
-// block (coalesced 128-B rows), lanes combined in a fixed order.  Returns the two
-// sums in lane 0 of each channel.
+// Sum the partial slab column c over nblocks rows: a block is 8 channels x 32 lanes;
+// lane l loads rows l, l+32, ... (up to 256 rows in one batch of loads in flight —
+// the slab was just written by other XCDs, so each dependent round trip is costly),
+// then the 32 lanes combine in a fixed shuffle tree.  Every lane returns the sums.
 __device__ __forceinline__ void slab_sum(const float *__restrict__ pg, int nblocks, int C, int c, bool ok,
-                                         float *red, float &a, float &b) {
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+                                         float &a, float &b) {
+  const int l = threadIdx.x & 31;
   a = 0.f; b = 0.f;
   if (ok) {
-    int k = pl;
-    for (; k + 56 < nblocks; k += 64) {      // 8 slab rows' loads in flight per thread
+    for (int k0 = 0; k0 < nblocks; k0 += 256) {
       float va[8], vb[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        va[q] = pg[(int64_t)(k + 8 * q) * 2 * C + c];
-        vb[q] = pg[(int64_t)(k + 8 * q) * 2 * C + C + c];
+        const int k = k0 + l + 32 * q;
+        va[q] = k < nblocks ? pg[(int64_t)k * 2 * C + c] : 0.f;
+        vb[q] = k < nblocks ? pg[(int64_t)k * 2 * C + C + c] : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) { a += va[q]; b += vb[q]; }
     }
-    for (; k < nblocks; k += 8) {
-      a += pg[(int64_t)k * 2 * C + c];
-      b += pg[(int64_t)k * 2 * C + C + c];
-    }
   }
-  red[threadIdx.x] = a;
-  red[256 + threadIdx.x] = b;
-  __syncthreads();
-  if (pl == 0) {
-    for (int q = 1; q < 8; ++q) { a += red[q * 32 + cl]; b += red[256 + q * 32 + cl]; }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  __syncthreads();
 }
 
 // ---- finalize (forward): mean / invstd per group; running stats updated group by
@@ -256,15 +260,14 @@ __global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(const float *__res
                                                               float *running_var, float momentum, float eps,
                                                               float *save_mean, float *save_invstd,
                                                               int64_t *counter, float *__restrict__ ss) {
-  __shared__ float red[512];
   if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += groups;
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
   const bool ok = c < C;
   const float n = (float)Mg;
   for (int grp = 0; grp < groups; ++grp) {
     float S, SS;
-    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, red, S, SS);
-    if (threadIdx.x < 32 && ok) {
+    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, S, SS);
+    if ((threadIdx.x & 31) == 0 && ok) {
       const float d = S / n;
       const float mu = shifts[grp * C + c] + d;
       const float var = fmaxf(SS / n - d * d, 0.f);
@@ -393,21 +396,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
 __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float *__restrict__ part, int nblocks, int groups,
                                                               int C, int64_t Mg, float *dgamma, float *dbeta,
                                                               int accumulate, float *__restrict__ coef) {
-  __shared__ float red[512];
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
   const bool ok = c < C;
   float ga = 0.f, gb = 0.f;  // sums over all groups (the parameters are shared)
   for (int grp = 0; grp < groups; ++grp) {
     float a, b;
-    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, red, a, b);
-    if (threadIdx.x < 32 && ok) {
+    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, a, b);
+    if ((threadIdx.x & 31) == 0 && ok) {
       coef[grp * 2 * C + c] = a / (float)Mg;
       coef[grp * 2 * C + C + c] = b / (float)Mg;
       ga += a;
       gb += b;
     }
   }
-  if (threadIdx.x >= 32 || !ok) return;
+  if ((threadIdx.x & 31) != 0 || !ok) return;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + ga : ga;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gb : gb;
 }
@@ -496,14 +498,14 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
   const BnPlan rp = bn_red_plan(Mg, C, groups);
   float *shifts = workspace + ws_part(rp, C, groups);
   float *ss = shifts + (int64_t)groups * C;
-  const unsigned cblocks = (unsigned)((C + 31) / 32);
+  const unsigned cblocks = (unsigned)((C + 7) / 8);
   if (training) {
     dim3 grid(rp.nblocks, groups);
     if (dtype == EWVIT_BF16)
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(256), 0, s, x, Mg, (int)C, rp.R,
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(rp.threads), 0, s, x, Mg, (int)C, rp.R,
                          rp.rows_per_block, workspace, shifts);
     else
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(256), 0, s, x, Mg, (int)C, rp.R,
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(rp.threads), 0, s, x, Mg, (int)C, rp.R,
                          rp.rows_per_block, workspace, shifts);
     hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(cblocks), dim3(256), 0, s, workspace, rp.nblocks, groups,
                        (int)C, Mg, shifts, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
@@ -517,7 +519,7 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
   const BnPlan ap = bn_plan(aMg, C);
   dim3 agrid(ap.nblocks, training ? groups : 1);
 #define BN_APPLY(DTV, ACTV) \
-  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(256), 0, s, x, y, ss, aMg, (int)C, ap.R, ap.rows_per_block)
+  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(ap.threads), 0, s, x, y, ss, aMg, (int)C, ap.R, ap.rows_per_block)
   BN_DISPATCH(BN_APPLY);
 #undef BN_APPLY
   return launch_status("bn_fwd");
@@ -539,16 +541,16 @@ extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, 
   float *coef = workspace + ws_part(rp, C, groups) + (int64_t)groups * C;
   dim3 grid(rp.nblocks, groups);
 #define BN_RED(DTV, ACTV)                                                                            \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(256), 0, s, dy, x, save_mean, save_invstd, \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(rp.threads), 0, s, dy, x, save_mean, save_invstd, \
                      gamma, beta, Mg, (int)C, rp.R, rp.rows_per_block, workspace)
   BN_DISPATCH(BN_RED);
 #undef BN_RED
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, s, workspace,
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, s, workspace,
                      rp.nblocks, groups, (int)C, Mg, dgamma, dbeta, accumulate, coef);
   const BnPlan p = bn_plan(Mg, C);
   dim3 dgrid(p.nblocks, groups);
 #define BN_DX(DTV, ACTV)                                                                                  \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(256), 0, s, dy, x, save_mean, save_invstd, gamma, \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(p.threads), 0, s, dy, x, save_mean, save_invstd, gamma, \
                      beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block)
   BN_DISPATCH(BN_DX);
 #undef BN_DX
