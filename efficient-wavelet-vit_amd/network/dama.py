@@ -22,6 +22,24 @@ from .mwt import MWT
 from .sfe import EfficientViT, LayerNorm, Linear, _hooked
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE.get(idx)
+    if st is None:
+        st = _SIDE[idx] = torch.cuda.Stream(device=torch.device('cuda', idx))
+    return st
+
+
+def _branch_streams():
+    """EWVIT_BRANCH_STREAMS=1 runs the MWT branch on a second stream.  Off by default:
+    measured on MI355X (graph-replayed step) it was 1-1.5 % slower — the MWT's large
+    convs occupy every CU, so the backbone's small kernels gain nothing beside them."""
+    return os.environ.get('EWVIT_BRANCH_STREAMS', '0') == '1'
+
+
 class CrossAttention(nn.Module):                                           # dama.py:15-53
     def __init__(self, dim, heads=8, dim_head=64, dropout=0.):
         super().__init__()
@@ -119,10 +137,30 @@ class DAMA(nn.Module):                                                     # dam
                          drop_p=drop.p if self.training else 0.0, out_dtype=torch.float32)
         return torch.softmax(ewvit.linear(h, l2.weight, l2.bias, out_dtype=torch.float32), dim=1)
 
+    def _branches(self, frame):
+        """space = sfe(frame), freq = mwt(frame) (dama.py:135-136).  The two branches are
+        independent until the cross-attention, so on the GPU the MWT runs on a second
+        stream: its large MFMA convs overlap the backbone's many small, latency-bound
+        kernels.  Autograd replays each backward op on its forward op's stream, so the
+        backward passes overlap the same way; a captured HIP graph keeps both streams."""
+        if not (frame.is_cuda and _branch_streams()):
+            return self.sfe(frame).float(), self.mwt(frame).float()
+        main = torch.cuda.current_stream(frame.device)
+        side = _side_stream(frame.device)
+        side.wait_stream(main)             # fork before the SFE work is issued on main
+        space = self.sfe(frame).float()
+        # the MWT ops are recorded after the SFE ops: autograd runs ready backward nodes
+        # latest-first, so the MWT backward is issued (on `side`) before the SFE backward
+        # fills `main`, and its wait on main covers only the cross-attention backward
+        with torch.cuda.stream(side):
+            freq = self.mwt(frame).float()
+        main.wait_stream(side)
+        freq.record_stream(main)
+        return space, freq
+
     def _process_frame(self, frame):
         B = frame.shape[0]
-        space_feats = self.sfe(frame).float()
-        freq_feats = self.mwt(frame).float()
+        space_feats, freq_feats = self._branches(frame)
         Ho, Wo = space_feats.shape[-2:]
         s_flat = space_feats.flatten(2).transpose(1, 2)
         f_flat = freq_feats.flatten(2).transpose(1, 2)
