@@ -172,6 +172,228 @@ __global__ __launch_bounds__(256) void scale_add_kernel(const void *__restrict__
   se_st8<DT>(y, v * 8, vr);
 }
 
+// ---------------------------------------------------------------- squeeze MLP
+// s0 [N, C] -> h1 = W1 s0 + b1 [N, Csq] -> a1 = silu(h1) -> s = sigmoid(W2 a1 + b2) [N, C]
+// (torchvision SqueezeExcitation fc1 / fc2 as 1x1 convs, fp32 like the reference).
+// The vectors are tiny (N = 64 frames); what costs is load latency, so every kernel
+// spreads a frame over many blocks and issues all of a thread's loads back to back.
+// Reductions over c go through fixed-order partial slabs (deterministic).
+//   F1 se_mlp_h1_part  grid (N, C/64):  part[n][cb][j] = sum_{c in cb} W1[j][c] s0[n][c]
+//   F2 se_mlp_gate     grid (N, C/256): h1 = b1 + sum_cb part; s = sigmoid(W2 silu(h1) + b2)
+//   B1 se_mlp_dh_part  grid (N, C/64):  dz2 = ds s(1-s); part[n][cb][j] = sum_c W2[c][j] dz2
+//   B2 se_mlp_g        grid (N, C/256): dz1 = (sum_cb part) silu'(h1); g = W1^T dz1 / HW
+//   B3 se_mlp_wgrad    one thread per dW1 / dW2 / db element, sums over n
+constexpr int SE_CB = 64;
+
+// lanes = 64 consecutive channels of chunk cb, waves take outputs j = w, w+4, ...
+__global__ __launch_bounds__(256) void se_mlp_h1_part_kernel(const float *__restrict__ s0,
+                                                             const float *__restrict__ w1, int C, int Csq,
+                                                             float *__restrict__ part) {
+  const int n = blockIdx.x, cb = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = cb * SE_CB + lane;
+  const float xv = c < C ? s0[(int64_t)n * C + c] : 0.f;
+  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = w; j0 < Csq; j0 += 16) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 4 * q;
+      v[q] = (j < Csq && c < C) ? w1[(int64_t)j * C + c] * xv : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      const int j = j0 + 4 * q;
+      if (lane == 0 && j < Csq) pp[j] = v[q];
+    }
+  }
+}
+
+__device__ __forceinline__ float silu_f(float h) { return h * __builtin_amdgcn_rcpf(1.f + __expf(-h)); }
+__device__ __forceinline__ float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
+// sum the nb partial rows of output j (up to 32 loads in flight per thread)
+__device__ __forceinline__ float se_part_sum(const float *__restrict__ pp, int nb, int Csq, int j) {
+  float acc = 0.f;
+  for (int k0 = 0; k0 < nb; k0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = k0 + q < nb ? pp[(int64_t)(k0 + q) * Csq + j] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc += v[q];
+  }
+  return acc;
+}
+
+// a thread's dot of a contiguous fp32 row with the LDS vector a (16-B loads when the
+// rows are 16-B aligned, Csq % 4 == 0)
+__device__ __forceinline__ float se_row_dot(const float *__restrict__ row, const float *a, int Csq) {
+  float acc0 = 0.f, acc1 = 0.f;
+  if (Csq & 3) {
+    for (int j0 = 0; j0 < Csq; j0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = j0 + q < Csq ? row[j0 + q] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        if (j0 + q < Csq) acc0 = fmaf(v[q], a[j0 + q], acc0);
+        if (j0 + q + 1 < Csq) acc1 = fmaf(v[q + 1], a[j0 + q + 1], acc1);
+      }
+    }
+    return acc0 + acc1;
+  }
+  for (int j0 = 0; j0 < Csq; j0 += 32) {
+    float4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] = j0 + 4 * q < Csq ? *reinterpret_cast<const float4 *>(row + j0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = j0 + 4 * q;
+      if (j < Csq) {
+        acc0 = fmaf(v[q].x, a[j], acc0);
+        acc1 = fmaf(v[q].y, a[j + 1], acc1);
+        acc0 = fmaf(v[q].z, a[j + 2], acc0);
+        acc1 = fmaf(v[q].w, a[j + 3], acc1);
+      }
+    }
+  }
+  return acc0 + acc1;
+}
+
+__global__ __launch_bounds__(256) void se_mlp_gate_kernel(const float *__restrict__ part, int nb,
+                                                          const float *__restrict__ b1,
+                                                          const float *__restrict__ w2,
+                                                          const float *__restrict__ b2, int C, int Csq,
+                                                          float *__restrict__ h1_out, float *__restrict__ s_out) {
+  extern __shared__ float a1[];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float *pp = part + (int64_t)n * nb * Csq;
+  for (int j = tid; j < Csq; j += 256) {
+    const float h = se_part_sum(pp, nb, Csq, j) + (b1 ? b1[j] : 0.f);
+    a1[j] = silu_f(h);
+    if (blockIdx.y == 0) h1_out[(int64_t)n * Csq + j] = h;
+  }
+  __syncthreads();
+  const int c = blockIdx.y * 256 + tid;
+  if (c >= C) return;
+  const float z = se_row_dot(w2 + (int64_t)c * Csq, a1, Csq) + (b2 ? b2[c] : 0.f);
+  s_out[(int64_t)n * C + c] = sigmoid_f(z);
+}
+
+__global__ __launch_bounds__(256) void se_mlp_dh_part_kernel(const float *__restrict__ ds,
+                                                             const float *__restrict__ s,
+                                                             const float *__restrict__ w2, int C, int Csq,
+                                                             float *__restrict__ dz2_out, float *__restrict__ part) {
+  const int n = blockIdx.x, cb = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = cb * SE_CB + lane;
+  float d = 0.f;
+  if (c < C) {
+    const float sv = s[(int64_t)n * C + c];
+    d = ds[(int64_t)n * C + c] * sv * (1.f - sv);
+    if (w == 0) dz2_out[(int64_t)n * C + c] = d;
+  }
+  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = w; j0 < Csq; j0 += 16) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 4 * q;
+      v[q] = (j < Csq && c < C) ? w2[(int64_t)c * Csq + j] * d : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      const int j = j0 + 4 * q;
+      if (lane == 0 && j < Csq) pp[j] = v[q];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__ part, int nb,
+                                                       const float *__restrict__ h1,
+                                                       const float *__restrict__ w1, int C, int Csq, float inv_hw,
+                                                       float *__restrict__ dz1_out, float *__restrict__ g_out) {
+  extern __shared__ float dz1[];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float *pp = part + (int64_t)n * nb * Csq;
+  for (int j = tid; j < Csq; j += 256) {
+    const float dh = se_part_sum(pp, nb, Csq, j);
+    const float h = h1[(int64_t)n * Csq + j];
+    const float sg = sigmoid_f(h);
+    const float d = dh * sg * (1.f + h * (1.f - sg));
+    dz1[j] = d;
+    if (blockIdx.y == 0) dz1_out[(int64_t)n * Csq + j] = d;
+  }
+  __syncthreads();
+  const int c = blockIdx.y * 256 + tid;
+  if (c >= C) return;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int j0 = 0; j0 < Csq; j0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = j0 + q < Csq ? w1[(int64_t)(j0 + q) * C + c] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      if (j0 + q < Csq) acc0 = fmaf(v[q], dz1[j0 + q], acc0);
+      if (j0 + q + 1 < Csq) acc1 = fmaf(v[q + 1], dz1[j0 + q + 1], acc1);
+    }
+  }
+  g_out[(int64_t)n * C + c] = (acc0 + acc1) * inv_hw;
+}
+
+// dW2[c][j] = sum_n dz2[n][c] silu(h1[n][j]),  db2[c] = sum_n dz2[n][c]
+// dW1[j][c] = sum_n dz1[n][j] s0[n][c],        db1[j] = sum_n dz1[n][j]
+__global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restrict__ dz2,
+                                                           const float *__restrict__ dz1,
+                                                           const float *__restrict__ h1,
+                                                           const float *__restrict__ s0, int N, int C, int Csq,
+                                                           float *__restrict__ dw1, float *__restrict__ db1,
+                                                           float *__restrict__ dw2, float *__restrict__ db2) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t P = (int64_t)C * Csq;
+  const float *pa, *pb;
+  int64_t sa, sb;                 // strides over n of the two factors
+  bool silu_b = false;
+  float *dst;
+  if (i < P) {                    // dW2[c][j], j fastest
+    const int c = (int)(i / Csq), j = (int)(i % Csq);
+    pa = dz2 + c; sa = C; pb = h1 + j; sb = Csq; silu_b = true; dst = dw2 + i;
+  } else if (i < 2 * P) {         // dW1[j][c], c fastest
+    const int64_t k = i - P;
+    const int j = (int)(k / C), c = (int)(k % C);
+    pa = dz1 + j; sa = Csq; pb = s0 + c; sb = C; dst = dw1 + k;
+  } else if (i < 2 * P + C) {
+    const int c = (int)(i - 2 * P);
+    pa = dz2 + c; sa = C; pb = nullptr; sb = 0; dst = db2 ? db2 + c : nullptr;
+  } else if (i < 2 * P + C + Csq) {
+    const int j = (int)(i - 2 * P - C);
+    pa = dz1 + j; sa = Csq; pb = nullptr; sb = 0; dst = db1 ? db1 + j : nullptr;
+  } else {
+    return;
+  }
+  if (!dst) return;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int n0 = 0; n0 < N; n0 += 16) {
+    float va[16], vb[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const bool ok = n0 + q < N;
+      va[q] = ok ? pa[(int64_t)(n0 + q) * sa] : 0.f;
+      vb[q] = ok ? (pb ? pb[(int64_t)(n0 + q) * sb] : 1.f) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      const float b0 = silu_b ? silu_f(vb[q]) : vb[q], b1v = silu_b ? silu_f(vb[q + 1]) : vb[q + 1];
+      acc0 = fmaf(va[q], b0, acc0);
+      acc1 = fmaf(va[q + 1], b1v, acc1);
+    }
+  }
+  *dst = acc0 + acc1;
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -236,4 +458,52 @@ extern "C" int ewvit_scale_add(const void *r, const void *x, int dtype, const fl
     hipLaunchKernelGGL(scale_add_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), r, x, scale, y, nvec,
                        row_elems / 8);
   return launch_status("scale_add");
+}
+
+static int se_mlp_check(int64_t N, int64_t C, int64_t Csq, const char *nm) {
+  EWVIT_CHECK_ARG(N > 0 && C > 0 && Csq > 0 && C <= 65535 * 64 && Csq <= 8192, "%s: N=%lld C=%lld Csq=%lld", nm,
+                  (long long)N, (long long)C, (long long)Csq);
+  return 0;
+}
+
+static int se_nb(int64_t C) { return (int)((C + SE_CB - 1) / SE_CB); }
+
+extern "C" int64_t ewvit_se_mlp_fwd_workspace(int64_t N, int64_t C, int64_t Csq) {
+  return N * se_nb(C) * Csq * (int64_t)sizeof(float);
+}
+
+extern "C" int ewvit_se_mlp_fwd(const float *s0, const float *w1, const float *b1, const float *w2, const float *b2,
+                                float *h1, float *s, int64_t N, int64_t C, int64_t Csq, float *workspace,
+                                void *stream) {
+  if (int rc = se_mlp_check(N, C, Csq, "se_mlp_fwd")) return rc;
+  EWVIT_CHECK_ARG(s0 && w1 && w2 && h1 && s && workspace, "se_mlp_fwd: null pointer");
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  hipLaunchKernelGGL(se_mlp_h1_part_kernel, dim3((unsigned)N, (unsigned)nb), dim3(256), 0, st, s0, w1, (int)C,
+                     (int)Csq, workspace);
+  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+                     (size_t)Csq * sizeof(float), st, workspace, nb, b1, w2, b2, (int)C, (int)Csq, h1, s);
+  return launch_status("se_mlp_fwd");
+}
+
+extern "C" int64_t ewvit_se_mlp_bwd_workspace(int64_t N, int64_t C, int64_t Csq) {
+  return N * (C + Csq + se_nb(C) * Csq) * (int64_t)sizeof(float);
+}
+
+extern "C" int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const float *s0, const float *w1,
+                                const float *w2, float inv_hw, float *g, float *dw1, float *db1, float *dw2,
+                                float *db2, int64_t N, int64_t C, int64_t Csq, float *workspace, void *stream) {
+  if (int rc = se_mlp_check(N, C, Csq, "se_mlp_bwd")) return rc;
+  EWVIT_CHECK_ARG(ds && s && h1 && s0 && w1 && w2 && g && dw1 && dw2 && workspace, "se_mlp_bwd: null pointer");
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  float *dz2 = workspace, *dz1 = workspace + N * C, *part = dz1 + N * Csq;
+  hipLaunchKernelGGL(se_mlp_dh_part_kernel, dim3((unsigned)N, (unsigned)nb), dim3(256), 0, st, ds, s, w2, (int)C,
+                     (int)Csq, dz2, part);
+  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+                     (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, inv_hw, dz1, g);
+  const int64_t tot = 2 * C * Csq + C + Csq;
+  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
+                     (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
+  return launch_status("se_mlp_bwd");
 }

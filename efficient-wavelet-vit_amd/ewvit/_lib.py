@@ -44,6 +44,8 @@ SIGNATURES = {
                                 _vp, _vp],
     'ewvit_se_reduce': [_vp, _vp, _i32, _i64, _i64, _i64, _f32, _vp, _vp, _vp],
     'ewvit_se_scale': [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    'ewvit_se_mlp_fwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    'ewvit_se_mlp_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     'ewvit_scale_add': [_vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
@@ -55,6 +57,8 @@ QUERIES = {
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
     'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
+    'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),
+    'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
 }
 
 _lib = None

@@ -4,8 +4,9 @@
 
 SE: s = sigmoid(fc2(silu(fc1(mean_hw x)))), y = x * s.  The two HBM passes of the
 forward (squeeze, excite) and of the backward (sum_hw dy*x, dx = dy*s + dsq/HW)
-are ewvit kernels; the [N, C] squeeze MLP runs in fp32 on the library GEMM (it is
-a few KFLOP per sample).
+are ewvit kernels, and so is the fp32 [N, C] squeeze MLP: one launch forward
+(fc1 + SiLU + fc2 + sigmoid), two backward (per-frame vectors; weight/bias sums)
+in place of the ~15 small library/elementwise kernels of the reference block.
 """
 import torch
 import torch.nn.functional as F
@@ -23,10 +24,24 @@ def _ws(N, HW, C, dev):
     return torch.empty(L.load().ewvit_se_reduce_workspace(N, HW, C) // 4, dtype=torch.float32, device=dev)
 
 
+def _mat(w, r, c):
+    """fp32 [r, c] matrix over a 1x1 conv weight's memory (no copy for fp32 weights)."""
+    return w.detach().float().reshape(r, c).contiguous()
+
+
+def _vec(b):
+    return None if b is None else b.detach().float().contiguous()
+
+
 def _grad_like(g, p):
-    """gradient in the parameter's own strides (DDP bucket views)."""
+    """gradient in the parameter's own strides (DDP bucket views); size-1 dims' strides
+    are free, so a 1x1 conv weight's channels-last gradient is a view, not a copy."""
     g = g.reshape(p.shape)
-    return g if g.stride() == p.stride() else torch.empty_like(p, dtype=g.dtype).copy_(g)
+    if g.stride() == p.stride():
+        return g
+    if all(a == b for a, b, n in zip(g.stride(), p.stride(), p.shape) if n != 1) and g.is_contiguous():
+        return g.as_strided(p.shape, p.stride())
+    return torch.empty_like(p, dtype=g.dtype).copy_(g)
 
 
 class SqueezeExciteFn(torch.autograd.Function):
@@ -41,35 +56,39 @@ class SqueezeExciteFn(torch.autograd.Function):
         s0 = torch.empty(N, C, dtype=torch.float32, device=x.device)
         L.call('ewvit_se_reduce', L.ptr(xc), None, L.dt(xc), N, HW, C, 1.0 / HW, L.ptr(s0), L.ptr(ws), L.stream(s0),
                work={'bytes': xc.numel() * xc.element_size()})
-        with torch.autocast('cuda', enabled=False):
-            W1, W2 = w1.detach().float().reshape(Csq, C), w2.detach().float().reshape(C, Csq)
-            h1 = torch.addmm(b1.detach().float(), s0, W1.t())
-            a1 = F.silu(h1)
-            s = torch.sigmoid(torch.addmm(b2.detach().float(), a1, W2.t()))
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        h1 = torch.empty(N, Csq, dtype=torch.float32, device=x.device)
+        s = torch.empty(N, C, dtype=torch.float32, device=x.device)
+        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=x.device)
+        L.call('ewvit_se_mlp_fwd', L.ptr(s0), L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2), L.ptr(_vec(b2)), L.ptr(h1),
+               L.ptr(s), N, C, Csq, L.ptr(fws), L.stream(s))
         y = torch.empty_like(xc)
         L.call('ewvit_se_scale', L.ptr(xc), L.dt(xc), L.ptr(s), None, L.ptr(y), N, HW, C, L.stream(y),
                work={'bytes': 2 * xc.numel() * xc.element_size()})
-        ctx.save_for_backward(xc, w1, w2, s0, h1, a1, s)
+        ctx.save_for_backward(xc, w1, w2, s0, h1, s)
+        ctx.has_b = (b1 is not None, b2 is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xc, w1, w2, s0, h1, a1, s = ctx.saved_tensors
+        xc, w1, w2, s0, h1, s = ctx.saved_tensors
         N, C, H, W = xc.shape
         HW, Csq = H * W, w1.shape[0]
+        dev = xc.device
         dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
-        ws = _ws(N, HW, C, xc.device)
-        ds = torch.empty(N, C, dtype=torch.float32, device=xc.device)
+        ws = _ws(N, HW, C, dev)
+        ds = torch.empty(N, C, dtype=torch.float32, device=dev)
         L.call('ewvit_se_reduce', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, 1.0, L.ptr(ds), L.ptr(ws), L.stream(ds),
                work={'bytes': 2 * xc.numel() * xc.element_size()})
-        with torch.autocast('cuda', enabled=False):
-            W1, W2 = w1.detach().float().reshape(Csq, C), w2.detach().float().reshape(C, Csq)
-            dh2 = ds * s * (1.0 - s)
-            dW2, db2 = dh2.t() @ a1, dh2.sum(0)
-            sg = torch.sigmoid(h1)
-            dh1 = (dh2 @ W2) * sg * (1.0 + h1 * (1.0 - sg))
-            dW1, db1 = dh1.t() @ s0, dh1.sum(0)
-            g = (dh1 @ W1) * (1.0 / HW)
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        g = torch.empty(N, C, dtype=torch.float32, device=dev)
+        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
+        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
+        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if ctx.has_b[0] else None
+        db2 = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b[1] else None
+        mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_se_mlp_bwd', L.ptr(ds), L.ptr(s), L.ptr(h1), L.ptr(s0), L.ptr(W1), L.ptr(W2), 1.0 / HW,
+               L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), N, C, Csq, L.ptr(mws), L.stream(g))
         dx = torch.empty_like(xc)
         L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
                work={'bytes': 2 * xc.numel() * xc.element_size()})

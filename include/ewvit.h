@@ -250,6 +250,21 @@ int ewvit_se_reduce(const void *a, const void *b, int dtype, int64_t N, int64_t 
  *   excite: x, s;  backward: dx = dy * s + dsqueeze / HW. */
 int ewvit_se_scale(const void *x, int dtype, const float *s, const float *g, void *y, int64_t N,
                    int64_t HW, int64_t C, void *stream);
+
+/* Squeeze MLP of SqueezeExcitation (torchvision fc1/fc2 1x1 convs + SiLU + Sigmoid on the
+ * squeezed [N, C] vector, fp32): h1 = W1 s0 + b1 [N, Csq], s = sigmoid(W2 silu(h1) + b2)
+ * [N, C].  W1 [Csq][C], W2 [C][Csq] (the conv weights' memory), b1/b2 may be NULL.
+ * Replaces addmm + silu + addmm + sigmoid of the reference block. */
+int64_t ewvit_se_mlp_fwd_workspace(int64_t N, int64_t C, int64_t Csq);
+int ewvit_se_mlp_fwd(const float *s0, const float *w1, const float *b1, const float *w2, const float *b2,
+                     float *h1, float *s, int64_t N, int64_t C, int64_t Csq, float *workspace, void *stream);
+int64_t ewvit_se_mlp_bwd_workspace(int64_t N, int64_t C, int64_t Csq);
+/* Backward of the squeeze MLP given ds[n, c] = sum_hw dy * x: g = (dL/ds0) * inv_hw (the
+ * squeeze's share of dx, consumed by ewvit_se_scale), dW1 [Csq][C], db1, dW2 [C][Csq],
+ * db2 (overwritten; db1/db2 may be NULL).  Deterministic (fixed-order sums over N). */
+int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const float *s0, const float *w1,
+                     const float *w2, float inv_hw, float *g, float *dw1, float *db1, float *dw2, float *db2,
+                     int64_t N, int64_t C, int64_t Csq, float *workspace, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
