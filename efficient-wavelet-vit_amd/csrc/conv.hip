@@ -923,6 +923,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
 
 // Kernel family: 0 register-staged everywhere; 1.. LDS-DMA configurations
 //   fwd/dgrad (rows per tile, ring depth): 1 (128, 2)  2 (128, 3)  3 (256, 2)  4 (256, 3)
+//     5 (128; ring 4 when the grid is <= 256 workgroups, else 2)
 //   wgrad (pixels per K-tile, ring depth): 1 (64, 2)   2 (64, 3)   3 (32, 3)   4 (32, 4)
 // +8: fwd/dgrad K-tiles ordered channel-block outer, tap inner.
 // EWVIT_CONV_GLDS=<n> or ewvit_conv2d_set_glds(n) select one (A/B measurement).
@@ -931,7 +932,7 @@ static int glds_variant() {
   if (g_glds < 0) {
     const char *e = getenv("EWVIT_CONV_GLDS");
     g_glds = e ? atoi(e) : 9;
-    if ((g_glds & 7) > 4 || g_glds < 0 || g_glds > 15) g_glds = 9;
+    if ((g_glds & 7) > 5 || g_glds < 0 || g_glds > 15) g_glds = 9;
   }
   return g_glds;
 }
@@ -995,7 +996,7 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     return false;
   const int v = glds_variant() & 7;
   const int tap_inner = (glds_variant() & 8) ? 1 : 0;
-  const int BM = v >= 3 ? 256 : 128;
+  const int BM = (v == 3 || v == 4) ? 256 : 128;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int bn = a.Ncol <= 64 ? 64 : 128;
   const int ntn = (a.Ncol + bn - 1) / bn;
@@ -1009,18 +1010,23 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     else                                                                                                          \
       hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn, tap_inner); \
   } while (0)
+  // variant 5: a grid of at most one workgroup per CU cannot hide the operand latency
+  // behind a second resident block, so it gets a 4-deep LDS ring (3 K-tiles in flight)
+  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : v;
   if (bn == 64) {
-    switch (v) {
+    switch (vv) {
       case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
       case 3: EWVIT_GLDS_FWD(256, 64, 2); break;
       case 4: EWVIT_GLDS_FWD(256, 64, 3); break;
+      case 6: EWVIT_GLDS_FWD(128, 64, 4); break;
       default: EWVIT_GLDS_FWD(128, 64, 2); break;
     }
   } else {
-    switch (v) {
+    switch (vv) {
       case 2: EWVIT_GLDS_FWD(128, 128, 3); break;
       case 3: EWVIT_GLDS_FWD(256, 128, 2); break;
       case 4: EWVIT_GLDS_FWD(256, 128, 3); break;
+      case 6: EWVIT_GLDS_FWD(128, 128, 4); break;
       default: EWVIT_GLDS_FWD(128, 128, 2); break;
     }
   }
@@ -1060,7 +1066,7 @@ using namespace ewvit;
 
 extern "C" int ewvit_conv2d_set_glds(int variant) {
   const int prev = glds_variant();
-  g_glds = variant >= 0 && variant <= 15 && (variant & 7) <= 4 ? variant : 9;
+  g_glds = variant >= 0 && variant <= 15 && (variant & 7) <= 5 ? variant : 9;
   return prev;
 }
 
@@ -1153,7 +1159,7 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
   const int gv = glds_variant() & 7;
-  const int64_t kq = !glds ? CBK : (gv >= 3 ? 32 : 64);     // K-tile depth (pixels)
+  const int64_t kq = !glds ? CBK : ((gv == 3 || gv == 4) ? 32 : 64);     // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
   mper = (mper + kq - 1) / kq * kq;
   a.mper = mper;
