@@ -463,12 +463,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// where dW element (co, ci, tap), ci < cin, lives: the parameter's strides
+struct WOut {
+  int64_t s_co, s_ci, s_tap;
+  int cin;
+};
+
 // dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]; a thread
 // sums 4 consecutive slab elements (one 16-B load per split, 4 splits in flight)
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
                                                                 int Cout, int Cin, int taps, int splits, int bparts,
                                                                 int accumulate, const float *__restrict__ dbias_part,
-                                                                float *__restrict__ dbias) {
+                                                                float *__restrict__ dbias, WOut wo) {
   const int64_t NP = taps * (int64_t)Cin;
   const int64_t n = (int64_t)Cout * NP;                                // n % 4 == 0 (Cin % 8 == 0)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -500,9 +506,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__r
   const int co = (int)(i / NP);
   const int np = (int)(i % NP);
   const int tap = np / Cin, ci = np % Cin;
-  const int64_t o = ((int64_t)co * Cin + ci) * taps + tap;
+  // the parameter's own layout (strides), only its real input channels
+  const int64_t o = co * wo.s_co + ci * wo.s_ci + tap * wo.s_tap;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) dw[o + e * taps] = accumulate ? dw[o + e * taps] + r[e] : r[e];
+  for (int e = 0; e < 4; ++e)
+    if (ci + e < wo.cin) dw[o + e * wo.s_ci] = accumulate ? dw[o + e * wo.s_ci] + r[e] : r[e];
 }
 
 // pack fp32 W (element (co, ci, tap) at co*s_co + ci*s_ci + tap*s_tap: any of the
@@ -1142,7 +1150,8 @@ extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64
 
 extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
                                        int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
-                                       int stride, int64_t x_group_c, int64_t x_group_stride, float *workspace,
+                                       int stride, int64_t x_group_c, int64_t x_group_stride, int64_t dw_cin,
+                                       int64_t dw_s_co, int64_t dw_s_ci, int64_t dw_s_tap, float *workspace,
                                        void *stream) {
   EWVIT_CHECK_ARG(x && dy && dw && workspace, "conv2d_bwd_weight: null pointer");
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
@@ -1166,8 +1175,14 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int sp = (int)((a.M + mper - 1) / mper);
   // the glds kernel leaves bias partials per (split, n'-tile); the old one per split
   const int bparts = glds ? sp * ntx : sp;
-  // one split of a 1x1 conv: the slab IS dW [Cout][Cin] (and dbias) — no reduce pass
-  const bool direct = sp == 1 && taps == 1 && !accumulate && (!dbias || bparts == 1);
+  EWVIT_CHECK_ARG(dw_cin > 0 && dw_cin <= Cin, "conv2d_bwd_weight: dw_cin %lld not in (0, %lld]", (long long)dw_cin,
+                  (long long)Cin);
+  WOut wo;
+  wo.s_co = dw_s_co; wo.s_ci = dw_s_ci; wo.s_tap = dw_s_tap; wo.cin = (int)dw_cin;
+  // one split of a 1x1 conv whose dW is [Cout][Cin] row-major: the slab IS dW (and
+  // dbias) — no reduce pass
+  const bool direct = sp == 1 && taps == 1 && !accumulate && (!dbias || bparts == 1) && dw_cin == Cin &&
+                      dw_s_ci == 1 && dw_s_co == Cin;
   if (direct) { a.part = dw; a.dbias_part = dbias; }
   hipStream_t s = as_stream(stream);
   if (glds) {
@@ -1194,6 +1209,6 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
   const int64_t nt = n4 > g.Cout ? n4 : g.Cout;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, workspace, dw,
-                     g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias);
+                     g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias, wo);
   return launch_status("conv2d_bwd_weight reduce");
 }

@@ -41,7 +41,7 @@ SIGNATURES = {
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64,
-                                _vp, _vp],
+                                _i64, _i64, _i64, _i64, _vp, _vp],
     'ewvit_se_reduce': [_vp, _vp, _i32, _i64, _i64, _i64, _f32, _vp, _vp, _vp],
     'ewvit_se_scale': [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     'ewvit_se_mlp_fwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],

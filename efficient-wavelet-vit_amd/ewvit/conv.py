@@ -84,15 +84,18 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or want_b:
             wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            dwf = torch.empty((Cout, Cx, k, k), dtype=torch.float32, device=xc.device)
+            # dW in the parameter's own memory format (DDP bucket views, no layout copy)
+            dwf = torch.empty_like(weight, dtype=torch.float32)
+            s_co, s_ci, s_kh, s_kw = dwf.stride()
+            if s_kh != k * s_kw:
+                dwf = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=xc.device)
+                s_co, s_ci, s_kh, s_kw = dwf.stride()
             dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device) if want_b else None
             work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
             L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
-                   Cout, k, stride, gc, gs, L.ptr(ws), L.stream(dwf), work=work)
+                   Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
             if ctx.needs_input_grad[1]:
-                dw = dwf if Cx == Cin else dwf[:, :Cin]
-                if dw.stride() != weight.stride():     # keep the parameter's layout (DDP bucket views)
-                    dw = torch.empty_like(weight, dtype=torch.float32).copy_(dw)
+                dw = dwf
             db = dbf
         return dx, dw, db, None, None
 

@@ -228,13 +228,16 @@ int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N,
 /* bytes of f32 split-K workspace for ewvit_conv2d_bwd_weight. */
 int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                           int ksize, int stride);
-/* dw [Cout][Cin][k][k] f32 and, when dbias != NULL, the bias gradient dbias[Cout] =
- * sum of dy over pixels (fused: read from the dy tiles already staged), both
- * (= or +=) ; deterministic split-K + reduction. */
+/* dw f32 and, when dbias != NULL, the bias gradient dbias[Cout] = sum of dy over
+ * pixels (fused: read from the dy tiles already staged), both (= or +=);
+ * deterministic split-K + reduction.  dW element (co, ci, kh*k + kw) for the first
+ * dw_cin input channels (the rest are zero padding of x) is written at
+ * co*dw_s_co + ci*dw_s_ci + tap*dw_s_tap: the weight parameter's own memory format
+ * (contiguous or channels-last), so no layout copy follows. */
 int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
                             int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
-                            int stride, int64_t x_group_c, int64_t x_group_stride, float *workspace,
-                            void *stream);
+                            int stride, int64_t x_group_c, int64_t x_group_stride, int64_t dw_cin,
+                            int64_t dw_s_co, int64_t dw_s_ci, int64_t dw_s_tap, float *workspace, void *stream);
 
 /* ------------------------------ squeeze-excitation / stochastic-depth add ---
  * The MBConv block tail of the EfficientNetV2-S backbone (torchvision

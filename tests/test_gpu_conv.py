@@ -97,3 +97,25 @@ def test_conv_level_major_input(levels, N, C, Cout, H, W, glds):
     assert rel(y, yr) < 2 ** -7
     assert zd.grad.shape == z.shape and rel(zd.grad, zr.grad) < 2 ** -7
     assert rel(wd.grad, wr.grad) < 1e-3
+
+
+@pytest.mark.parametrize('Cx,Cin,k', [(64, 64, 3), (64, 54, 3), (96, 96, 1), (64, 60, 1)])
+def test_conv_weight_grad_in_param_layout(Cx, Cin, k):
+    """dW is written straight into the parameter's memory format (channels-last conv
+    weights, as the model holds them) and only for the real input channels."""
+    import ewvit.conv as ec
+    g = torch.Generator().manual_seed(Cx + Cin + k)
+    x = torch.randn(3, Cx, 13, 11, generator=g).to(torch.bfloat16)
+    x[:, Cin:] = 0
+    w = torch.randn(48, Cin, k, k, generator=g) / (k * k * Cin) ** 0.5
+    xr = x[:, :Cin].float().clone().requires_grad_(True)
+    wr = w.to(torch.bfloat16).float().clone().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, padding=k // 2)
+    dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16)
+    yr.backward(dy.float())
+    xd = x.to(DEV).to(memory_format=torch.channels_last)
+    wd = w.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    y = ec.conv2d(xd, wd, None, 1)
+    y.backward(dy.to(DEV))
+    assert wd.grad.stride() == wd.stride()
+    assert rel(wd.grad, wr.grad) < 1e-3

@@ -84,7 +84,7 @@ def main():
 
         def wgrad():
             L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), None, 0, N, H, W, Cx, Cout, k, s,
-                   gc, gs, L.ptr(ws), L.stream(y))
+                   gc, gs, Cx, dw.stride(0), dw.stride(1), dw.stride(3), L.ptr(ws), L.stream(y))
         rows = {}
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
