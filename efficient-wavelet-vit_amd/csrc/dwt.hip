@@ -104,7 +104,7 @@ template <int IDT, int ODT, int CH>
 __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict__ yh,
                                                           void *__restrict__ out, int N, int C,
                                                           int H, int W, int levels, int OH,
-                                                          int OW, int64_t total) {
+                                                          int OW, int64_t total, int ocs) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int ox = (int)(idx % OW);
@@ -134,7 +134,28 @@ __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict
   const int64_t p00 = (int64_t)y0 * wl + x0;
   const int64_t base = off + (int64_t)n * 3 * C * hw;
   const int nch = (CH > 0) ? CH : 3 * C;
-  const int64_t obase = idx * nch;
+  const int64_t obase = idx * ocs;          // ocs >= 3C: padded channel stride, pad = 0
+  if (CH == 9 && ODT == EWVIT_BF16 && ocs == 16) {
+    // the 9 bands + 7 zero channels of the hf_conv input: two 16-B stores per pixel
+    float v[9];
+#pragma unroll
+    for (int ch = 0; ch < 9; ++ch) {
+      const int64_t pb = base + ch * hw + p00;
+      const float v00 = Elem<IDT>::load(yh, pb), v01 = Elem<IDT>::load(yh, pb + xp);
+      const float v10 = Elem<IDT>::load(yh, pb + yp * wl), v11 = Elem<IDT>::load(yh, pb + yp * wl + xp);
+      v[ch] = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+    }
+    unsigned w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = 2 * k < 9 ? v[2 * k] : 0.f, b = 2 * k + 1 < 9 ? v[2 * k + 1] : 0.f;
+      w[k] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+    }
+    uint4 *o = reinterpret_cast<uint4 *>(reinterpret_cast<bf16_t *>(out) + obase);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    return;
+  }
   for (int ch = 0; ch < nch; ++ch) {
     const int64_t pb = base + ch * hw + p00;
     const float v00 = Elem<IDT>::load(yh, pb), v01 = Elem<IDT>::load(yh, pb + xp);
@@ -142,6 +163,7 @@ __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict
     const float v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
     Elem<ODT>::store(out, obase + ch, v);
   }
+  for (int ch = nch; ch < ocs; ++ch) Elem<ODT>::store(out, obase + ch, 0.f);
 }
 
 }  // namespace ewvit
@@ -176,8 +198,11 @@ extern "C" int ewvit_dwt_haar_fwd(const void *x, void *yh, void *ll, int64_t N, 
 
 extern "C" int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H,
                                  int64_t W, int levels, int64_t OH, int64_t OW, int in_dtype,
-                                 int out_dtype, void *stream) {
+                                 int out_dtype, int64_t out_channels, void *stream) {
   EWVIT_CHECK_ARG(yh && out, "hf_upsample: null pointer");
+  if (out_channels == 0) out_channels = 3 * C;
+  EWVIT_CHECK_ARG(out_channels >= 3 * C && out_channels <= 4096, "hf_upsample: out_channels %lld < 3C",
+                  (long long)out_channels);
   EWVIT_CHECK_ARG(N > 0 && C > 0 && H > 0 && W > 0 && OH > 0 && OW > 0, "hf_upsample: empty shape");
   EWVIT_CHECK_ARG(levels >= 1 && levels <= 5, "hf_upsample: levels=%d not in [1,5]", levels);
   EWVIT_CHECK_ARG(dtype_ok(in_dtype) && dtype_ok(out_dtype), "hf_upsample: bad dtype");
@@ -186,7 +211,7 @@ extern "C" int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C
   hipStream_t s = as_stream(stream);
 #define UP_LAUNCH(ID, OD, CHN)                                                                  \
   hipLaunchKernelGGL((hf_upsample_kernel<ID, OD, CHN>), grid, block, 0, s, yh, out, (int)N,    \
-                     (int)C, (int)H, (int)W, levels, (int)OH, (int)OW, total)
+                     (int)C, (int)H, (int)W, levels, (int)OH, (int)OW, total, (int)out_channels)
   const bool c3 = (C == 3);
   if (in_dtype == EWVIT_F32 && out_dtype == EWVIT_F32) { if (c3) UP_LAUNCH(EWVIT_F32, EWVIT_F32, 9); else UP_LAUNCH(EWVIT_F32, EWVIT_F32, 0); }
   else if (in_dtype == EWVIT_F32) { if (c3) UP_LAUNCH(EWVIT_F32, EWVIT_BF16, 9); else UP_LAUNCH(EWVIT_F32, EWVIT_BF16, 0); }

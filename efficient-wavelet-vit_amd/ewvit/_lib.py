@@ -19,7 +19,7 @@ _i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctyp
 # name -> argtypes (restype int for all but the two bookkeeping calls)
 SIGNATURES = {
     'ewvit_dwt_haar_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
-    'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _vp],
+    'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _i64, _vp],
     'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
                    _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
     'ewvit_colsum': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],

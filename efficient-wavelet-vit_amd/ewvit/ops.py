@@ -268,25 +268,27 @@ def dwt_haar(x, levels=1, out_dtype=torch.float32):
     return ll, outs
 
 
-def hf_upsample(yh_flat_levels, N, C, H, W, levels, out_hw, out_dtype=torch.bfloat16):
-    """Bilinear upsample of every level's bands (mwt.py:77-81) -> [L, N, OH, OW, 3C]."""
+def hf_upsample(yh_flat_levels, N, C, H, W, levels, out_hw, out_dtype=torch.bfloat16, out_channels=0):
+    """Bilinear upsample of every level's bands (mwt.py:77-81) -> [L, N, OH, OW, Cout]
+    with Cout = out_channels (>= 3C; channels past 3C are zero) or 3C."""
     base = yh_flat_levels
     OH, OW = out_hw
-    out = torch.empty(levels, N, OH, OW, 3 * C, dtype=out_dtype, device=base.device)
+    oc = out_channels or 3 * C
+    out = torch.empty(levels, N, OH, OW, oc, dtype=out_dtype, device=base.device)
     nb = sum(N * 3 * C * h * w for h, w in _level_sizes(H, W, levels))
     work = {'bytes': nb * base.element_size() + out.numel() * out.element_size()}
     L.call('ewvit_hf_upsample', L.ptr(base), L.ptr(out), N, C, H, W, levels, OH, OW, L.dt(base),
-           L.dt(out), L.stream(out), work=work)
+           L.dt(out), oc, L.stream(out), work=work)
     return out
 
 
-def dwt_hf_upsample(x, levels, out_hw, out_dtype=torch.bfloat16, band_dtype=torch.bfloat16):
+def dwt_hf_upsample(x, levels, out_hw, out_dtype=torch.bfloat16, band_dtype=torch.bfloat16, out_channels=0):
     """The MWT high-frequency front end for all levels at once: DWT (one read of x)
     then the upsampled, channel-interleaved HF input of hf_conv for every level,
-    channels-last: [L, N, OH, OW, 3C] (channel c*3+band)."""
+    channels-last: [L, N, OH, OW, 3C] (channel c*3+band; zero-padded to out_channels)."""
     ll, yh, _ = _dwt_flat(x, levels, band_dtype)
     N, C, H, W = x.shape
-    return hf_upsample(yh, N, C, H, W, levels, out_hw, out_dtype), ll
+    return hf_upsample(yh, N, C, H, W, levels, out_hw, out_dtype, out_channels), ll
 
 
 # ------------------------------------------------------- depthwise 3x3 conv
@@ -332,7 +334,10 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
             if wdt != torch.float32:
                 dw = dw.to(wdt)
             if dw.stride() != ctx.wstride:          # keep the parameter's layout (DDP bucket views)
-                dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
+                if all(a == b for a, b, n in zip(dw.stride(), ctx.wstride, dw.shape) if n != 1):
+                    dw = dw.as_strided(dw.shape, ctx.wstride)      # same memory, size-1 dims differ only
+                else:
+                    dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
         return dx, dw, None, None
 
 

@@ -14,7 +14,8 @@ Hot path on MI355X:
   (csrc/conv.hip); multiscale_fusion reads the level-major fusion outputs as their
   channel concatenation in place (no torch.cat of mwt.py:112 in HBM);
 * BatchNorm + ReLU are one fused ewvit pass (csrc/batchnorm.hip).
-The seperate conv (9 -> 54 channels) is still the library conv (MIOpen).
+The seperate conv (9 band channels, zero-padded to 16 by the upsample pass -> 54
+channels, zero-padded to 64) runs on the same MFMA conv (one block-diagonal conv).
 
 If ``wavelet_transform`` is overridden on the instance or class (as
 utils/visualize_feature_maps.py:151-158 does), forward falls back to the
@@ -185,14 +186,19 @@ class MWT(nn.Module):
         OH, OW = H // 2, W // 2
         cdt = _cdt()
         out_hw = (OH, OW) if Lv > 1 else ((H + 1) // 2, (W + 1) // 2)
+        # bf16: the 3C band channels zero-padded to a multiple of 16 in the same pass, so
+        # the seperate conv runs on the ewvit MFMA conv (K = 9 taps x 16 channels)
+        cin = 3 * C
+        cpad = (cin + 15) // 16 * 16 if cdt == torch.bfloat16 else cin
         hf, _ = ewvit.dwt_hf_upsample(x, Lv, out_hw, out_dtype=cdt,
-                                      band_dtype=torch.bfloat16 if cdt == torch.bfloat16 else torch.float32)
-        hf = hf.view(Lv * B, out_hw[0], out_hw[1], 3 * C).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
+                                      band_dtype=torch.bfloat16 if cdt == torch.bfloat16 else torch.float32,
+                                      out_channels=cpad)
+        hf = hf.view(Lv * B, out_hw[0], out_hw[1], cpad).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
         sep = self.hf_conv['seperate']
         # seperate[i] sees colour i's 3C/3 = C band channels: a groups=3 conv.  It is
         # issued as ONE dense conv with a block-diagonal weight (zeros contribute
         # exact zeros): MIOpen's grouped weight-gradient kernel took ~0.3 s here.
-        w = torch.cat([F.pad(sep[i][0].weight, (0, 0, 0, 0, i * C, (2 - i) * C)) for i in range(3)])
+        w = torch.cat([F.pad(sep[i][0].weight, (0, 0, 0, 0, i * C, (2 - i) * C + cpad - cin)) for i in range(3)])
         b = torch.cat([sep[i][0].bias for i in range(3)])
         # the fusion conv's MFMA kernels want 8-aligned channels, and its LDS-DMA
         # kernel whole 64-channel K-tiles: emit the 18C seperate channels zero-padded
@@ -203,7 +209,10 @@ class MWT(nn.Module):
         if pad:
             w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, pad))
             b = F.pad(b, (0, pad))
-        y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
+        if cpad % 8 == 0 and hf.is_cuda:
+            y = ewvit.conv2d(hf, w, b, 1)
+        else:
+            y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
         # BN + ReLU of all levels in one fused launch, per-level statistics
         y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv)
         fus = self.hf_conv['fusion']

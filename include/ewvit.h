@@ -60,7 +60,9 @@ int ewvit_dwt_haar_fwd(const void *x, void *yh, void *ll, int64_t N, int64_t C, 
  */
 int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H, int64_t W,
                       int levels, int64_t OH, int64_t OW, int in_dtype, int out_dtype,
-                      void *stream);
+                      int64_t out_channels, void *stream);
+/* out_channels: channel stride of `out` (0 = 3C); channels 3C .. out_channels-1 are
+ * written as zeros (the 16-channel-aligned input of the hf_conv MFMA conv). */
 
 /* --------------------------------------------------------------- GEMM ---
  * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(k,n) )   bf16 MFMA, fp32 accumulate

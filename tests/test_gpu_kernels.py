@@ -306,3 +306,18 @@ def test_depthwise_fwd_bwd_vs_torch(N, C, H, stride, dtype):
     assert rel_err(y.float(), yr) < tol
     assert rel_err(xd.grad.float(), xr.grad) < tol
     assert rel_err(wd.grad, wr.grad) < 1e-5 if dtype == torch.float32 else rel_err(wd.grad, wr.grad) < 1e-4
+
+
+def test_hf_upsample_padded_channels():
+    """out_channels > 3C: the bands in channels 0..3C-1 (the unpadded result up to one
+    bf16 rounding: the vectorised store path may contract the lerp differently),
+    exact zeros after — the 16-channel input of the MWT seperate conv."""
+    import ewvit
+    x = torch.randn(3, 3, 40, 36, generator=torch.Generator().manual_seed(5)).to(DEV)
+    a, _ = ewvit.dwt_hf_upsample(x, 3, (20, 18), out_dtype=torch.bfloat16, band_dtype=torch.bfloat16)
+    b, _ = ewvit.dwt_hf_upsample(x, 3, (20, 18), out_dtype=torch.bfloat16, band_dtype=torch.bfloat16,
+                                 out_channels=16)
+    assert b.shape[-1] == 16
+    d = (b[..., :9].float() - a.float()).abs()
+    assert float((d / a.float().abs().clamp_min(1e-3)).max()) <= 2 ** -7
+    assert float(b[..., 9:].abs().max()) == 0.0
