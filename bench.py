@@ -101,11 +101,11 @@ ENTRY_KERNELS = {
     'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
     'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
                                    'dw_bwd_weight_reduce_kernel'],
-    'ewvit_conv2d_fwd': ['conv_fwd_kernel<false'],
-    'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true'],
-    'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_reduce_kernel'],
-    'ewvit_bn_fwd': ['bn_stats_kernel', 'bn_finalize_fwd_kernel', 'bn_apply_kernel', 'bn_eval_coeff_kernel'],
-    'ewvit_bn_bwd': ['bn_bwd_reduce_kernel', 'bn_finalize_bwd_kernel', 'bn_bwd_dx_kernel'],
+    'ewvit_conv2d_fwd': ['conv_fwd_kernel<false', 'conv_glds_kernel<false'],
+    'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true', 'conv_glds_kernel<true'],
+    'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_glds_kernel', 'conv_wgrad_reduce_kernel'],
+    'ewvit_bn_fwd': ['bn_stats_kernel', 'bn_apply_kernel'],
+    'ewvit_bn_bwd': ['bn_bwd_reduce_kernel', 'bn_bwd_dx_kernel'],
     'ewvit_se_reduce': ['se_reduce_kernel', 'se_fold_kernel'],
     'ewvit_se_scale': ['se_scale_kernel'],
     'ewvit_scale_add': ['scale_add_kernel'],

@@ -4,11 +4,17 @@
 // MWT stack (network/mwt.py:23-72), SiLU / none in the EfficientNetV2-S backbone
 // (torchvision Conv2dNormActivation, reached from network/sfe.py:111-113).  On
 // MIOpen that was 3 BN kernels + a separate activation kernel each way, per layer.
-// Here: forward = statistics pass + finalize + one apply pass writing act(bn(x));
-// backward = one reduction pass (sum g, sum g*xhat with g = dy * act'(z)) +
-// finalize + one dx pass.  x is the only saved activation (the pre-activation z
-// is recomputed from it).  Layout [M = N*H*W][C], bf16 or f32; 8 channels
-// (16 B for bf16) per thread.
+// Here: forward = statistics pass + one apply pass writing act(bn(x)); backward =
+// one reduction pass (sum g, sum g*xhat with g = dy * act'(z)) + one dx pass.  x is
+// the only saved activation (the pre-activation z is recomputed from it).  Layout
+// [M = N*H*W][C], bf16 or f32; 8 channels (16 B for bf16) per thread.
+//
+// Blocks own a CHANNEL CHUNK (<= 8 channel vectors = 64 channels, 128 B of a row)
+// and a range of rows.  The reduction pass leaves at most 32 partial rows per
+// chunk, so the elementwise pass finalises its own chunk's statistics from them
+// (a few KB read by the block, from L2) — no separate finalize launch — and the
+// blocks of row range 0 keep the books (running stats, saved mean / invstd,
+// counter, dgamma / dbeta) for their chunk.
 //
 // Statistics are numerically stable and deterministic: every block accumulates
 // sums shifted by one sample per channel (row 0 of its statistics group, the
@@ -18,6 +24,8 @@
 // Running stats follow torch: running = (1-m)*running + m*stat, with the unbiased
 // batch variance for running_var and the biased one for normalisation.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace ewvit {
 
@@ -98,55 +106,56 @@ __device__ __forceinline__ float act_grad(float z) {
   return 1.f;
 }
 
-struct BnPlan {
-  int C8, R, threads, nblocks;
-  int64_t rows_per_block;
+// ---------------------------------------------------------------- geometry
+struct BnGeo {
+  int C8;       // channel vectors (8 channels) per row
+  int CC8;      // channel vectors per block (chunk)
+  int RG;       // row groups per block
+  int threads;  // CC8 * RG rounded up to whole waves
+  int nch;      // channel chunks
 };
 
-// R row groups of C8 channel-vector threads per block; the block is R*C8 threads
-// rounded up to whole waves (no idle quarter-blocks when C8 does not divide 256)
-static void bn_shape(BnPlan &p, int64_t C) {
-  p.C8 = (int)(C / 8);
-  p.R = p.C8 >= 256 ? 1 : 256 / p.C8;
-  p.threads = (p.R * p.C8 + 63) / 64 * 64;
+static BnGeo bn_geo(int64_t C) {
+  BnGeo g;
+  g.C8 = (int)(C / 8);
+  g.CC8 = g.C8 < 8 ? g.C8 : 8;
+  g.RG = 256 / g.CC8;
+  g.threads = (g.CC8 * g.RG + 63) / 64 * 64;
+  if (g.threads > 256) g.threads = 256;
+  g.nch = (g.C8 + g.CC8 - 1) / g.CC8;
+  return g;
 }
 
-// elementwise passes (apply, dx): ~1024 blocks (4 per CU) for the large maps, but at
-// least 8 rows per thread, so the per-channel constants a thread loads are amortised
-// over its rows on the small late-stage maps (e.g. 64x7x7 rows x 1536 ch); <= 64 rows
-static BnPlan bn_plan(int64_t M, int64_t C) {
-  BnPlan p;
-  bn_shape(p, C);
-  int64_t rpt = (M + (int64_t)p.R * 1024 - 1) / ((int64_t)p.R * 1024);
+// reduction passes: row chunks per (channel chunk, group) — ~512 blocks in all,
+// >= 16 rows per thread, <= 256 partial rows (what an elementwise block finalises
+// from: <= 128 KB of L2 reads next to the rows it streams)
+static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
+  static const int cap = [] {
+    const char *e = getenv("EWVIT_BN_NRC_CAP");
+    const int v = e ? atoi(e) : 256;
+    return v < 1 ? 1 : (v > 256 ? 256 : v);
+  }();
+  int64_t nrc = (512 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
+  if (nrc > cap) nrc = cap;
+  const int64_t maxr = M / ((int64_t)g.RG * 16);
+  if (nrc > maxr) nrc = maxr;
+  if (nrc < 1) nrc = 1;
+  return (int)nrc;
+}
+
+// elementwise passes: ~1024 blocks in all, 8..64 rows per thread
+static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
+  int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
+  int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
   rpt = rpt < 8 ? 8 : (rpt > 64 ? 64 : rpt);
-  p.rows_per_block = (int64_t)p.R * rpt;
-  int64_t nb = (M + p.rows_per_block - 1) / p.rows_per_block;
-  if (nb < 1) nb = 1;
-  p.nblocks = (int)nb;
-  return p;
+  return (int64_t)g.RG * rpt;
 }
 
-// reduction passes (stats, bwd sums): <= 256 blocks per group (the finalize sums a
-// group's partial rows in one batch of loads), ~512 over all groups, >= 16 rows per
-// thread, so the partial slabs stay small next to the tensor they summarise
-static BnPlan bn_red_plan(int64_t M, int64_t C, int groups) {
-  BnPlan p;
-  bn_shape(p, C);
-  int64_t nb = (512 + groups - 1) / groups;
-  if (nb > 256) nb = 256;
-  const int64_t maxnb = M / ((int64_t)p.R * 16);
-  if (nb > maxnb) nb = maxnb;
-  if (nb < 1) nb = 1;
-  int64_t rpb = (M + nb - 1) / nb;
-  rpb = (rpb + p.R - 1) / p.R * p.R;
-  p.rows_per_block = rpb;
-  p.nblocks = (int)((M + rpb - 1) / rpb);
-  if (p.nblocks < 1) p.nblocks = 1;
-  return p;
+// workspace (floats): [groups][nrc][2C] partial sums | [groups][C] shifts
+static int64_t bn_ws_floats(int64_t M, int64_t C, int groups) {
+  const BnGeo g = bn_geo(C);
+  return (int64_t)groups * bn_nrc(g, M, groups) * 2 * C + (int64_t)groups * C;
 }
-
-// workspace layout (floats): [groups][nred][2C] partials | [groups][C] shifts | [groups][2C] coefficients
-static int64_t ws_part(const BnPlan &rp, int64_t C, int groups) { return (int64_t)groups * rp.nblocks * 2 * C; }
 
 // the batched walk of a (row group, channel vector) thread over rows r0+rg,
 // r0+rg+R, ... < r1: NB rows are loaded (`load(r)` -> raw registers) before any
@@ -168,29 +177,55 @@ __device__ __forceinline__ void row_walk(int64_t r0, int64_t r1, int rg, int R, 
 
 template <int DT> struct Raw8x2 { Raw8<DT> x, d; };
 
-// ---- pass 1 (forward): per-block sums of (x - K) and (x - K)^2 per channel
-template <int DT>
-__global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ x, int64_t M, int C, int R,
-                                                       int64_t rpb, float *__restrict__ part,
-                                                       float *__restrict__ shifts) {
-  __shared__ float sm[256 * 8 * 2];
-  // blockIdx.y = statistics group (consecutive blocks of M rows, own batch stats)
-  x = reinterpret_cast<const char *>(x) + (int64_t)blockIdx.y * M * C * (DT == EWVIT_BF16 ? 2 : 4);
-  part += (int64_t)blockIdx.y * gridDim.x * 2 * C;
-  const int C8 = C >> 3;
+
+
+// block-reduce the (CC8 x 8) pairs of sums held by every thread over its RG row
+// groups (fixed order) and store them to partial row `pr` (2C floats: a | b)
+__device__ __forceinline__ void bn_block_sums(float *sm, const float (&a)[8], const float (&b)[8], int cl, int rg,
+                                              int CC8, int RG, int c8, int C8, int C, float *pr) {
   const int tid = threadIdx.x;
-  const int rg = tid / C8, c8 = tid % C8;
-  const bool active = rg < R && c8 < C8;
-  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < M ? r0 + rpb : M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sm[tid * 16 + j] = a[j]; sm[tid * 16 + 8 + j] = b[j]; }
+  __syncthreads();
+  if (rg == 0 && c8 < C8) {
+    float sa[8], sb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+    for (int g = 0; g < RG; ++g) {
+      const float *q = sm + (g * CC8 + cl) * 16;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sa[j] += q[j]; sb[j] += q[8 + j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { pr[c8 * 8 + j] = sa[j]; pr[C + c8 * 8 + j] = sb[j]; }
+  }
+}
+
+// ---- pass 1 (forward): partial sums of (x - K) and (x - K)^2 per channel;
+// grid (row chunks, channel chunks, groups).  K = row 0 of the group (one sample per
+// channel, the same for every block): partials add like plain sums while the
+// cancellation of E[(x-K)^2] - E[x-K]^2 stays at the scale of the variance.
+template <int DT>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ x, int64_t M, int C, int CC8, int RG,
+                                                       int64_t rpc, float *__restrict__ part,
+                                                       float *__restrict__ shifts) {
+  __shared__ float sm[256 * 16];
+  const int grp = blockIdx.z, nrc = gridDim.x;
+  x = reinterpret_cast<const char *>(x) + (int64_t)grp * M * C * (DT == EWVIT_BF16 ? 2 : 4);
+  const int C8 = C >> 3;
+  const int tid = threadIdx.x, cl = tid % CC8, rg = tid / CC8;
+  const int c8 = blockIdx.y * CC8 + cl;
+  const bool active = rg < RG && c8 < C8;
+  const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = r0 + rpc < M ? r0 + rpc : M;
   float K[8], S[8], SS[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { K[j] = 0.f; S[j] = 0.f; SS[j] = 0.f; }
   if (active) {
-    ld8<DT>(x, (int64_t)c8 * 8, K);   // the group's shift: its row 0
+    ld8<DT>(x, (int64_t)c8 * 8, K);
     if (blockIdx.x == 0 && rg == 0)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) shifts[blockIdx.y * C + c8 * 8 + j] = K[j];
-    row_walk<8>(r0, r1, rg, R, [&](int64_t rr) { return ldraw<DT>(x, rr * C + c8 * 8); },
+      for (int j = 0; j < 8; ++j) shifts[grp * C + c8 * 8 + j] = K[j];
+    row_walk<8>(r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, rr * C + c8 * 8); },
                 [&](int64_t, const Raw8<DT> &raw) {
       float v[8];
       unpack<DT>(raw, v);
@@ -202,121 +237,120 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ 
       }
     });
   }
-  // sum the R row groups of each channel vector through LDS (fixed order)
-  float *s1 = sm, *s2 = sm + 256 * 8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[tid * 8 + j] = S[j]; s2[tid * 8 + j] = SS[j]; }
-  __syncthreads();
-  if (tid < C8) {
-    float a[8], b[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { a[j] = s1[tid * 8 + j]; b[j] = s2[tid * 8 + j]; }
-    for (int g = 1; g < R; ++g) {
-      const int t = g * C8 + tid;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { a[j] += s1[t * 8 + j]; b[j] += s2[t * 8 + j]; }
-    }
-    float *pb = part + (int64_t)blockIdx.x * 2 * C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { pb[tid * 8 + j] = a[j]; pb[C + tid * 8 + j] = b[j]; }
-  }
+  bn_block_sums(sm, S, SS, cl, rg, CC8, RG, c8, C8, C, part + ((int64_t)grp * nrc + blockIdx.x) * 2 * C);
 }
 
-// Sum the partial slab column c over nblocks rows: a block is 8 channels x 32 lanes;
-// lane l loads rows l, l+32, ... (up to 256 rows in one batch of loads in flight —
-// the slab was just written by other XCDs, so each dependent round trip is costly),
-// then the 32 lanes combine in a fixed shuffle tree.  Every lane returns the sums.
-__device__ __forceinline__ void slab_sum(const float *__restrict__ pg, int nblocks, int C, int c, bool ok,
-                                         float &a, float &b) {
-  const int l = threadIdx.x & 31;
-  a = 0.f; b = 0.f;
-  if (ok) {
-    for (int k0 = 0; k0 < nblocks; k0 += 256) {
+// the chunk's per-channel sums over the nrc partial rows of group grp, into LDS
+// red[0][ch], red[1][ch] (ch < 8*CC8): 64 channels x 4 lanes, fixed order
+__device__ __forceinline__ void bn_chunk_sums(const float *__restrict__ part, int grp, int nrc, int C, int ch0,
+                                              int nch_c, float *red) {
+  const int tid = threadIdx.x, j = tid & 63, q = tid >> 6;
+  float a = 0.f, b = 0.f;
+  if (j < nch_c && q * 64 < (int)blockDim.x) {
+    const float *pg = part + (int64_t)grp * nrc * 2 * C + ch0 + j;
+    for (int k0 = q; k0 < nrc; k0 += 32) {      // 8 partial rows' loads in flight
       float va[8], vb[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = k0 + l + 32 * q;
-        va[q] = k < nblocks ? pg[(int64_t)k * 2 * C + c] : 0.f;
-        vb[q] = k < nblocks ? pg[(int64_t)k * 2 * C + C + c] : 0.f;
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 4 * u;
+        va[u] = k < nrc ? pg[(int64_t)k * 2 * C] : 0.f;
+        vb[u] = k < nrc ? pg[(int64_t)k * 2 * C + C] : 0.f;
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) { a += va[q]; b += vb[q]; }
+      for (int u = 0; u < 8; ++u) { a += va[u]; b += vb[u]; }
     }
   }
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
+  float *ra = red, *rb = red + 256;
+  ra[tid] = a;
+  rb[tid] = b;
+  __syncthreads();
+  if (tid < 64) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k * 64 < (int)blockDim.x; ++k) { sa += ra[k * 64 + tid]; sb += rb[k * 64 + tid]; }
+    ra[tid] = sa;
+    rb[tid] = sb;
   }
+  __syncthreads();
 }
 
-// ---- finalize (forward): mean / invstd per group; running stats updated group by
-// group in order (the reference calls the module once per group);
-// scale = gamma*invstd, shift = beta - mean*scale into ss[groups][2][C]
-__global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(const float *__restrict__ part, int nblocks, int groups,
-                                                              int C, int64_t Mg, const float *__restrict__ shifts,
-                                                              const float *__restrict__ gamma,
-                                                              const float *__restrict__ beta, float *running_mean,
-                                                              float *running_var, float momentum, float eps,
-                                                              float *save_mean, float *save_invstd,
-                                                              int64_t *counter, float *__restrict__ ss) {
-  if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += groups;
-  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
-  const bool ok = c < C;
-  const float n = (float)Mg;
-  for (int grp = 0; grp < groups; ++grp) {
-    float S, SS;
-    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, S, SS);
-    if ((threadIdx.x & 31) == 0 && ok) {
-      const float d = S / n;
-      const float mu = shifts[grp * C + c] + d;
-      const float var = fmaxf(SS / n - d * d, 0.f);
-      const float inv = rsqrtf(var + eps);
-      if (save_mean) save_mean[grp * C + c] = mu;
-      if (save_invstd) save_invstd[grp * C + c] = inv;
-      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
-      if (running_var) {
-        const float unb = Mg > 1 ? var * (n / (n - 1.f)) : var;
-        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
-      }
-      const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-      ss[grp * 2 * C + c] = g * inv;
-      ss[grp * 2 * C + C + c] = b - mu * g * inv;
-    }
-  }
-}
-
-// eval: scale/shift from running stats
-__global__ __launch_bounds__(256) void bn_eval_coeff_kernel(const float *__restrict__ rm, const float *__restrict__ rv,
-                                                            const float *__restrict__ gamma,
-                                                            const float *__restrict__ beta, float eps, int C,
-                                                            float *__restrict__ ss) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float inv = rsqrtf(rv[c] + eps);
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  ss[c] = g * inv;
-  ss[C + c] = b - rm[c] * g * inv;
-}
-
-// ---- apply: y = act(x * scale + shift)
+// ---- apply: y = act(x * scale + shift).  Training: the block finalises its chunk's
+// batch statistics from the partial rows; blocks of row range 0 of group 0 update
+// the running statistics group after group (the reference calls the module once per
+// group) and save mean / invstd.  Eval: coefficients from the running statistics.
 template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ x, void *__restrict__ y,
-                                                       const float *__restrict__ ss, int64_t Mg, int C, int R,
-                                                       int64_t rpb) {
-  // grid (blocks per group, groups); thread (row group rg, channel vector c8) walks
-  // rows rg, rg+R, ... of its block with its 16 coefficients held in registers
-  const int C8 = C >> 3;
-  const int rg = threadIdx.x / C8, c8 = threadIdx.x % C8;
-  if (rg >= R) return;
-  const int64_t goff = (int64_t)blockIdx.y * Mg * C;
-  ss += blockIdx.y * 2 * C;
+                                                       const float *__restrict__ part,
+                                                       const float *__restrict__ shifts, int nrc, int64_t Mg, int C,
+                                                       int CC8, int RG, int64_t rpb, int training,
+                                                       const float *__restrict__ gamma,
+                                                       const float *__restrict__ beta, float *running_mean,
+                                                       float *running_var, float momentum, float eps, float *save_mean,
+                                                       float *save_invstd, int64_t *counter) {
+  __shared__ float red[512];
+  __shared__ float coef[2][64];
+  const int grp = blockIdx.z, groups = gridDim.z;
+  const int tid = threadIdx.x, C8 = C >> 3;
+  const int ch0 = blockIdx.y * CC8 * 8;
+  const int nch_c = (C - ch0) < CC8 * 8 ? (C - ch0) : CC8 * 8;
+  const float n = (float)Mg;
+  if (training) {
+    if (blockIdx.x == 0 && grp == 0) {
+      if (counter && blockIdx.y == 0 && tid == 0) *counter += groups;
+      float rm = 0.f, rv = 0.f;
+      const int c = ch0 + tid;
+      if (tid < nch_c) { rm = running_mean ? running_mean[c] : 0.f; rv = running_var ? running_var[c] : 0.f; }
+      for (int g = 0; g < groups; ++g) {
+        bn_chunk_sums(part, g, nrc, C, ch0, nch_c, red);
+        if (tid < nch_c) {
+          const float d = red[tid] / n, mu = shifts[g * C + c] + d;
+          const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
+          if (save_mean) save_mean[g * C + c] = mu;
+          if (save_invstd) save_invstd[g * C + c] = rsqrtf(var + eps);
+          rm = (1.f - momentum) * rm + momentum * mu;
+          rv = (1.f - momentum) * rv + momentum * (Mg > 1 ? var * (n / (n - 1.f)) : var);
+          if (g == grp) {
+            const float inv = rsqrtf(var + eps);
+            const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+            coef[0][tid] = ga * inv;
+            coef[1][tid] = be - mu * ga * inv;
+          }
+        }
+        __syncthreads();
+      }
+      if (tid < nch_c) {
+        if (running_mean) running_mean[c] = rm;
+        if (running_var) running_var[c] = rv;
+      }
+    } else {
+      bn_chunk_sums(part, grp, nrc, C, ch0, nch_c, red);
+      if (tid < nch_c) {
+        const int c = ch0 + tid;
+        const float d = red[tid] / n, mu = shifts[grp * C + c] + d;
+        const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
+        const float inv = rsqrtf(var + eps);
+        const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+        coef[0][tid] = ga * inv;
+        coef[1][tid] = be - mu * ga * inv;
+      }
+    }
+  } else if (tid < nch_c) {
+    const int c = ch0 + tid;
+    const float inv = rsqrtf(running_var[c] + eps);
+    const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+    coef[0][tid] = ga * inv;
+    coef[1][tid] = be - running_mean[c] * ga * inv;
+  }
+  __syncthreads();
+  const int cl = tid % CC8, rg = tid / CC8;
+  const int c8 = blockIdx.y * CC8 + cl;
+  if (rg >= RG || c8 >= C8) return;
+  const int64_t goff = (int64_t)grp * Mg * C;
   const int c = c8 * 8;
   float sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = ss[c + j]; sh[j] = ss[C + c + j]; }
+  for (int j = 0; j < 8; ++j) { sc[j] = coef[0][cl * 8 + j]; sh[j] = coef[1][cl * 8 + j]; }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  row_walk<8>(r0, r1, rg, R, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
+  row_walk<8>(r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
               [&](int64_t rr, const Raw8<DT> &raw) {
     float v[8];
     unpack<DT>(raw, v);
@@ -326,29 +360,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
   });
 }
 
-// ---- backward pass 1: per-block sums of g and g*xhat, g = dy * act'(z)
+// ---- backward pass 1: partial sums of g and g*xhat, g = dy * act'(z)
 template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                             const float *__restrict__ mean,
                                                             const float *__restrict__ invstd,
                                                             const float *__restrict__ gamma,
-                                                            const float *__restrict__ beta, int64_t M, int C, int R,
-                                                            int64_t rpb, float *__restrict__ part) {
-  __shared__ float sm[256 * 8 * 2];
-  // blockIdx.y = statistics group: its rows, saved stats and partial slab
+                                                            const float *__restrict__ beta, int64_t M, int C, int CC8,
+                                                            int RG, int64_t rpc, float *__restrict__ part) {
+  __shared__ float sm[256 * 16];
+  const int grp = blockIdx.z, nrc = gridDim.x;
   {
-    const int64_t off = (int64_t)blockIdx.y * M * C * (DT == EWVIT_BF16 ? 2 : 4);
+    const int64_t off = (int64_t)grp * M * C * (DT == EWVIT_BF16 ? 2 : 4);
     x = reinterpret_cast<const char *>(x) + off;
     dy = reinterpret_cast<const char *>(dy) + off;
-    mean += blockIdx.y * C;
-    invstd += blockIdx.y * C;
-    part += (int64_t)blockIdx.y * gridDim.x * 2 * C;
+    mean += grp * C;
+    invstd += grp * C;
   }
   const int C8 = C >> 3;
-  const int tid = threadIdx.x;
-  const int rg = tid / C8, c8 = tid % C8;
-  const bool active = rg < R && c8 < C8;
-  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < M ? r0 + rpb : M;
+  const int tid = threadIdx.x, cl = tid % CC8, rg = tid / CC8;
+  const int c8 = blockIdx.y * CC8 + cl;
+  const bool active = rg < RG && c8 < C8;
+  const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = r0 + rpc < M ? r0 + rpc : M;
   float sg[8], sgx[8], mu[8], iv[8], ga[8], be[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -358,7 +391,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
     ga[j] = gamma ? gamma[c] : 1.f; be[j] = beta ? beta[c] : 0.f;
   }
   if (active) {
-    row_walk<8>(r0, r1, rg, R,
+    row_walk<8>(r0, r1, rg, RG,
                 [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8)}; },
                 [&](int64_t, const Raw8x2<DT> &raw) {
       float vx[8], vd[8];
@@ -373,78 +406,67 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
       }
     });
   }
-  float *s1 = sm, *s2 = sm + 256 * 8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[tid * 8 + j] = sg[j]; s2[tid * 8 + j] = sgx[j]; }
-  __syncthreads();
-  if (tid < C8) {
-    float a[8], b[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { a[j] = s1[tid * 8 + j]; b[j] = s2[tid * 8 + j]; }
-    for (int g = 1; g < R; ++g) {
-      const int t = g * C8 + tid;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { a[j] += s1[t * 8 + j]; b[j] += s2[t * 8 + j]; }
-    }
-    float *pb = part + (int64_t)blockIdx.x * 2 * C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { pb[tid * 8 + j] = a[j]; pb[C + tid * 8 + j] = b[j]; }
-  }
+  bn_block_sums(sm, sg, sgx, cl, rg, CC8, RG, c8, C8, C, part + ((int64_t)grp * nrc + blockIdx.x) * 2 * C);
 }
 
-// finalize (backward): dgamma = sum g*xhat, dbeta = sum g; coefficients for dx
-__global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float *__restrict__ part, int nblocks, int groups,
-                                                              int C, int64_t Mg, float *dgamma, float *dbeta,
-                                                              int accumulate, float *__restrict__ coef) {
-  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
-  const bool ok = c < C;
-  float ga = 0.f, gb = 0.f;  // sums over all groups (the parameters are shared)
-  for (int grp = 0; grp < groups; ++grp) {
-    float a, b;
-    slab_sum(part + (int64_t)grp * nblocks * 2 * C, nblocks, C, c, ok, a, b);
-    if ((threadIdx.x & 31) == 0 && ok) {
-      coef[grp * 2 * C + c] = a / (float)Mg;
-      coef[grp * 2 * C + C + c] = b / (float)Mg;
-      ga += a;
-      gb += b;
-    }
-  }
-  if ((threadIdx.x & 31) != 0 || !ok) return;
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + ga : ga;
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gb : gb;
-}
-
-// dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+// dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); the block finalises its chunk's
+// two means from the partial rows; blocks of row range 0 of group 0 write
+// dgamma = sum g*xhat, dbeta = sum g (over all groups: the parameters are shared)
 template <int DT, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                         const float *__restrict__ mean,
                                                         const float *__restrict__ invstd,
                                                         const float *__restrict__ gamma,
                                                         const float *__restrict__ beta,
-                                                        const float *__restrict__ coef, void *__restrict__ dx,
-                                                        int64_t Mg, int C, int R, int64_t rpb) {
-  // same (row group, channel vector) walk as bn_apply_kernel; per-channel
-  // constants in registers: k = gamma*invstd, mean, invstd, gamma, beta, 2 coefs
-  const int C8 = C >> 3;
-  const int rg = threadIdx.x / C8, c8 = threadIdx.x % C8;
-  if (rg >= R) return;
-  const int64_t goff = (int64_t)blockIdx.y * Mg * C;
-  mean += blockIdx.y * C;
-  invstd += blockIdx.y * C;
-  coef += blockIdx.y * 2 * C;
+                                                        const float *__restrict__ part, int nrc,
+                                                        void *__restrict__ dx, int64_t Mg, int C, int CC8, int RG,
+                                                        int64_t rpb, float *dgamma, float *dbeta, int accumulate) {
+  __shared__ float red[512];
+  __shared__ float coef[2][64];
+  const int grp = blockIdx.z, groups = gridDim.z;
+  const int tid = threadIdx.x, C8 = C >> 3;
+  const int ch0 = blockIdx.y * CC8 * 8;
+  const int nch_c = (C - ch0) < CC8 * 8 ? (C - ch0) : CC8 * 8;
+  const float n = (float)Mg;
+  if (blockIdx.x == 0 && grp == 0) {
+    float ga = 0.f, gb = 0.f;
+    for (int g = 0; g < groups; ++g) {
+      bn_chunk_sums(part, g, nrc, C, ch0, nch_c, red);
+      if (tid < nch_c) {
+        ga += red[tid];
+        gb += red[256 + tid];
+        if (g == grp) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
+      }
+      __syncthreads();
+    }
+    if (tid < nch_c) {
+      const int c = ch0 + tid;
+      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + ga : ga;
+      if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gb : gb;
+    }
+  } else {
+    bn_chunk_sums(part, grp, nrc, C, ch0, nch_c, red);
+    if (tid < nch_c) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
+  }
+  __syncthreads();
+  const int cl = tid % CC8, rg = tid / CC8;
+  const int c8 = blockIdx.y * CC8 + cl;
+  if (rg >= RG || c8 >= C8) return;
+  const int64_t goff = (int64_t)grp * Mg * C;
+  mean += grp * C;
+  invstd += grp * C;
   const int c = c8 * 8;
   float mu[8], iv[8], ga[8], be[8], c0[8], c1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = mean[c + j]; iv[j] = invstd[c + j];
     ga[j] = gamma ? gamma[c + j] : 1.f; be[j] = beta ? beta[c + j] : 0.f;
-    c0[j] = coef[c + j]; c1[j] = coef[C + c + j];
+    c0[j] = coef[0][cl * 8 + j]; c1[j] = coef[1][cl * 8 + j];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  row_walk<8>(r0, r1, rg, R,
+  row_walk<8>(r0, r1, rg, RG,
               [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c)}; },
               [&](int64_t rr, const Raw8x2<DT> &raw) {
-    const int64_t i = goff + rr * C + c;
     float vx[8], vd[8], o[8];
     unpack<DT>(raw.x, vx);
     unpack<DT>(raw.d, vd);
@@ -454,7 +476,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
       const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
     }
-    st8<DT>(dx, i, o);
+    st8<DT>(dx, goff + rr * C + c, o);
   });
 }
 
@@ -478,8 +500,7 @@ using namespace ewvit;
 
 extern "C" int64_t ewvit_bn_workspace(int64_t M, int64_t C, int groups) {
   if (groups < 1) groups = 1;
-  const BnPlan rp = bn_red_plan(M / groups, C, groups);
-  return (ws_part(rp, C, groups) + (int64_t)groups * 3 * C) * (int64_t)sizeof(float);
+  return bn_ws_floats(M / groups, C, groups) * (int64_t)sizeof(float);
 }
 
 extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
@@ -487,39 +508,34 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
                             float momentum, float eps, int act, float *save_mean, float *save_invstd,
                             int groups, int64_t *num_batches_tracked, float *workspace, void *stream) {
   EWVIT_CHECK_ARG(x && y && workspace && dtype_ok(dtype), "bn_fwd: bad args");
-  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 2048, "bn_fwd: C=%lld must be a multiple of 8, <= 2048", (long long)C);
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_fwd: C=%lld must be a multiple of 8, <= 4096", (long long)C);
   EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_fwd: act=%d", act);
   EWVIT_CHECK_ARG(training || (running_mean && running_var), "bn_fwd: eval needs running stats");
   EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M % groups == 0, "bn_fwd: M=%lld not divisible into %d groups",
                   (long long)M, groups);
   if (M == 0) return 0;
+  if (!training) groups = 1;
   hipStream_t s = as_stream(stream);
   const int64_t Mg = M / groups;
-  const BnPlan rp = bn_red_plan(Mg, C, groups);
-  float *shifts = workspace + ws_part(rp, C, groups);
-  float *ss = shifts + (int64_t)groups * C;
-  const unsigned cblocks = (unsigned)((C + 7) / 8);
+  const BnGeo geo = bn_geo(C);
+  const int nrc = bn_nrc(geo, Mg, groups);
+  float *part = workspace, *shifts = workspace + (int64_t)groups * nrc * 2 * C;
   if (training) {
-    dim3 grid(rp.nblocks, groups);
+    const int64_t rpc = (Mg + nrc - 1) / nrc;
+    dim3 grid(nrc, geo.nch, groups);
     if (dtype == EWVIT_BF16)
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(rp.threads), 0, s, x, Mg, (int)C, rp.R,
-                         rp.rows_per_block, workspace, shifts);
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(geo.threads), 0, s, x, Mg, (int)C, geo.CC8, geo.RG,
+                         rpc, part, shifts);
     else
-      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(rp.threads), 0, s, x, Mg, (int)C, rp.R,
-                         rp.rows_per_block, workspace, shifts);
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(cblocks), dim3(256), 0, s, workspace, rp.nblocks, groups,
-                       (int)C, Mg, shifts, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
-                       save_invstd, num_batches_tracked, ss);
-  } else {
-    EWVIT_CHECK_ARG(groups == 1, "bn_fwd: eval mode takes one group");
-    hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
-                       running_var, gamma, beta, eps, (int)C, ss);
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(geo.threads), 0, s, x, Mg, (int)C, geo.CC8, geo.RG,
+                         rpc, part, shifts);
   }
-  const int64_t aMg = training ? Mg : M;
-  const BnPlan ap = bn_plan(aMg, C);
-  dim3 agrid(ap.nblocks, training ? groups : 1);
-#define BN_APPLY(DTV, ACTV) \
-  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(ap.threads), 0, s, x, y, ss, aMg, (int)C, ap.R, ap.rows_per_block)
+  const int64_t rpb = bn_rows_per_block(geo, Mg, groups);
+  dim3 agrid((unsigned)((Mg + rpb - 1) / rpb), geo.nch, groups);
+#define BN_APPLY(DTV, ACTV)                                                                                          \
+  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc, Mg,     \
+                     (int)C, geo.CC8, geo.RG, rpb, training, gamma, beta, running_mean, running_var, momentum, eps, \
+                     save_mean, save_invstd, num_batches_tracked)
   BN_DISPATCH(BN_APPLY);
 #undef BN_APPLY
   return launch_status("bn_fwd");
@@ -530,28 +546,27 @@ extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, 
                             const float *save_invstd, int act, float *dgamma, float *dbeta, int accumulate,
                             int groups, float *workspace, void *stream) {
   EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && workspace && dtype_ok(dtype), "bn_bwd: bad args");
-  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 2048, "bn_bwd: C=%lld must be a multiple of 8, <= 2048", (long long)C);
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd: C=%lld must be a multiple of 8, <= 4096", (long long)C);
   EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd: act=%d", act);
   EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M % groups == 0, "bn_bwd: M=%lld not divisible into %d groups",
                   (long long)M, groups);
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const int64_t Mg = M / groups;
-  const BnPlan rp = bn_red_plan(Mg, C, groups);
-  float *coef = workspace + ws_part(rp, C, groups) + (int64_t)groups * C;
-  dim3 grid(rp.nblocks, groups);
-#define BN_RED(DTV, ACTV)                                                                            \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(rp.threads), 0, s, dy, x, save_mean, save_invstd, \
-                     gamma, beta, Mg, (int)C, rp.R, rp.rows_per_block, workspace)
+  const BnGeo geo = bn_geo(C);
+  const int nrc = bn_nrc(geo, Mg, groups);
+  const int64_t rpc = (Mg + nrc - 1) / nrc;
+  dim3 grid(nrc, geo.nch, groups);
+#define BN_RED(DTV, ACTV)                                                                                           \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,           \
+                     save_invstd, gamma, beta, Mg, (int)C, geo.CC8, geo.RG, rpc, workspace)
   BN_DISPATCH(BN_RED);
 #undef BN_RED
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, s, workspace,
-                     rp.nblocks, groups, (int)C, Mg, dgamma, dbeta, accumulate, coef);
-  const BnPlan p = bn_plan(Mg, C);
-  dim3 dgrid(p.nblocks, groups);
-#define BN_DX(DTV, ACTV)                                                                                  \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(p.threads), 0, s, dy, x, save_mean, save_invstd, gamma, \
-                     beta, coef, dx, Mg, (int)C, p.R, p.rows_per_block)
+  const int64_t rpb = bn_rows_per_block(geo, Mg, groups);
+  dim3 dgrid((unsigned)((Mg + rpb - 1) / rpb), geo.nch, groups);
+#define BN_DX(DTV, ACTV)                                                                                              \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean, save_invstd,   \
+                     gamma, beta, workspace, nrc, dx, Mg, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, accumulate)
   BN_DISPATCH(BN_DX);
 #undef BN_DX
   return launch_status("bn_bwd");
