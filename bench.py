@@ -92,6 +92,26 @@ def kernel_table(records):
     return table
 
 
+def shape_table(detail):
+    """Per (entry point, integer arguments = one launch configuration): launches,
+    total, mean duration and algorithmic rate — the hottest single kernel configuration."""
+    rows = {}
+    for name, ints, s, e, w in detail:
+        r = rows.setdefault((name, ints), {'ms': [], 'bytes': 0.0, 'flops': 0.0})
+        r['ms'].append(s.elapsed_time(e))
+        r['bytes'] += w.get('bytes', 0.0)
+        r['flops'] += w.get('flops', 0.0)
+    out = []
+    for (name, ints), r in rows.items():
+        tot = sum(r['ms'])
+        out.append({'entry': name, 'args': list(ints), 'launches': len(r['ms']), 'total_ms': tot,
+                    'avg_us': 1e3 * tot / len(r['ms']),
+                    'GB/s': r['bytes'] / (tot * 1e-3) / 1e9 if tot else 0.0,
+                    'TFLOP/s': r['flops'] / (tot * 1e-3) / 1e12 if tot else 0.0,
+                    'bytes_per_launch': r['bytes'] / len(r['ms']), 'flops_per_launch': r['flops'] / len(r['ms'])})
+    return sorted(out, key=lambda r: -r['total_ms'])
+
+
 # device kernels behind each C-ABI entry point (for the PMC traffic lookup)
 ENTRY_KERNELS = {
     'ewvit_dwt_haar_fwd': ['dwt_multilevel_kernel'],
@@ -211,6 +231,7 @@ def main():
         step._eager()
     torch.cuda.synchronize()
     table = kernel_table(ewvit._lib.timing_records())
+    shapes = shape_table(ewvit._lib.timing_detail())
     ewvit._lib.enable_timing(False)
     for r in table.values():
         r['per_step'] = r['launches'] / kt
@@ -227,6 +248,16 @@ def main():
                           'launch': 'eager' if args.eager else 'hip-graph'}}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
         res['roofline'] = roofline_for(*dom) if dom else None
+        if shapes:
+            # the hottest single launch configuration (entry point + shape arguments)
+            h = dict(shapes[0])
+            h['per_step'] = h['launches'] / kt
+            hot = roofline_for(h['entry'], h)
+            hot['traffic'] = None      # the PMC passes are summarised per kernel symbol, not per shape
+            hot['args'] = h['args']
+            res['roofline_hot'] = hot
+            res['top_launch_configs'] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+                                         for r in shapes[:12]]
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                           for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
         if 'ewvit_dwt_haar_fwd' in table:

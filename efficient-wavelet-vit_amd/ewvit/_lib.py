@@ -124,7 +124,7 @@ def call(name, *args, work=None):
         e.record()
         _timers.setdefault(name, []).append((s, e, work or {}))
         ints = tuple(a for a in args if isinstance(a, int) and not isinstance(a, bool))
-        _timers.setdefault('__detail__', []).append((name, ints, s, e))
+        _timers.setdefault('__detail__', []).append((name, ints, s, e, work or {}))
 
 
 def dt(t):

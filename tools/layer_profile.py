@@ -37,7 +37,7 @@ def main():
     ewvit._lib.enable_timing(False)
     agg = {}
     tot = 0.0
-    for name, ints, s, e in det:
+    for name, ints, s, e, _ in det:
         t = s.elapsed_time(e) * 1e3
         tot += t
         k = (name, ints)
