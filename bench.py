@@ -49,13 +49,14 @@ def parse():
 def build_step(dev, frames, rank, graph=True):
     from network.model import DeepfakeDetector
     from network.losses import combined_loss
+    import ewvit
     from ewvit.graph import TrainStep
     torch.manual_seed(0)                                   # identical init on every rank
     videos = 8
     per_video = frames // videos
     model = DeepfakeDetector(3, 128, batch_size=per_video).to(dev).to(memory_format=torch.channels_last)
     params = [p for p in model.parameters() if p.requires_grad]
-    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True, capturable=True)
+    opt = ewvit.optim.Adam(params, lr=1e-4, weight_decay=1e-4)      # train.py:273-275 on csrc/optim.hip
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(videos, per_video, 3, 224, 224, device=dev, generator=g)

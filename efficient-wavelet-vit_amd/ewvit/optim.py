@@ -1,0 +1,83 @@
+"""Adam on the ewvit multi-tensor kernel (csrc/optim.hip) — the optimizer of the
+reference's training step (train.py:273-275: ``optim.Adam(params, lr, weight_decay)``).
+
+Same constructor, update rule and state layout as ``torch.optim.Adam`` (per-parameter
+state ``step`` / ``exp_avg`` / ``exp_avg_sq``, so checkpoints load either way), for
+amsgrad=False / maximize=False.  ``step()`` issues one launch per 48 tensors with the
+pointers passed by value — graph-capturable although autograd allocates fresh gradients
+every eager step — plus one foreach increment of the per-parameter device step counters.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _dense(t):
+    """True when t's elements fill exactly numel() consecutive slots (any dim order)."""
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False,
+                 maximize=False, **_ignored):
+        if amsgrad or maximize:
+            raise NotImplementedError('ewvit.optim.Adam: amsgrad / maximize are not used by the reference')
+        if lr < 0 or eps < 0 or not 0 <= betas[0] < 1 or not 0 <= betas[1] < 1 or weight_decay < 0:
+            raise ValueError('ewvit.optim.Adam: invalid hyper-parameters')
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    def _group_step(self, group):
+        items = []
+        for p in group['params']:
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse:
+                raise RuntimeError('ewvit.optim.Adam: sparse gradients are not supported')
+            if p.dtype != torch.float32 or not p.is_cuda:
+                raise RuntimeError('ewvit.optim.Adam: fp32 parameters on the GPU only')
+            if not _dense(p):
+                raise RuntimeError('ewvit.optim.Adam: parameters must be dense (no gaps or overlap)')
+            st = self.state[p]
+            if not st:
+                st['step'] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            elif st['step'].device != p.device:          # a loaded torch checkpoint keeps it on the host
+                st['step'] = st['step'].to(device=p.device, dtype=torch.float32)
+            g = p.grad
+            if g.stride() != p.stride():
+                g = torch.empty_like(p).copy_(g)          # same element order as p / m / v
+            items.append((p, g, st))
+        if not items:
+            return
+        torch._foreach_add_([c[2]['step'] for c in items], 1.0)   # torch semantics: per-parameter steps
+        b1, b2 = group['betas']
+        stream = L.stream(items[0][0])
+        for k in range(0, len(items), L.ADAM_MAX):
+            chunk = items[k:k + L.ADAM_MAX]
+            n = len(chunk)
+            cols = ([c[0] for c in chunk], [c[1] for c in chunk], [c[2]['exp_avg'] for c in chunk],
+                    [c[2]['exp_avg_sq'] for c in chunk], [c[2]['step'] for c in chunk])
+            ptrs = [(ctypes.c_void_p * n)(*[t.data_ptr() for t in col]) for col in cols]
+            numel = (ctypes.c_int64 * n)(*[c[0].numel() for c in chunk])
+            L.call('ewvit_adam_step', n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, ptrs[4],
+                   float(group['lr']), float(b1), float(b2), float(group['eps']), float(group['weight_decay']),
+                   stream, work={'bytes': 28.0 * sum(c[0].numel() for c in chunk)})
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            self._group_step(group)
+        return loss

@@ -30,6 +30,7 @@ extern "C" {
 #define EWVIT_F32 0
 #define EWVIT_BF16 1
 #define EWVIT_EINVAL 1000
+#define EWVIT_ADAM_MAX 48   /* tensors per ewvit_adam_step launch */
 
 int ewvit_abi_version(void);
 const char *ewvit_last_error(void);
@@ -274,6 +275,17 @@ int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const flo
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
                     int64_t row_elems, void *stream);
+
+/* ------------------------------------------------------ optimizer ---
+ * Adam exactly as torch.optim.Adam (amsgrad=False, maximize=False): g += wd*p;
+ * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ * with t = *steps[i] (per-tensor device f32, advanced by the caller first) — the optimizer of the
+ * reference's training step (train.py:273-275).  n <= EWVIT_ADAM_MAX f32 tensors per
+ * launch (pointers by value: capturable although autograd reallocates the gradients);
+ * p, g, m, v of a tensor share one memory order (any dense layout), numel elements. */
+int ewvit_adam_step(int n, float *const *params, const float *const *grads, float *const *exp_avg,
+                    float *const *exp_avg_sq, const int64_t *numel, const float *const *steps, double lr,
+                    double beta1, double beta2, float eps, float weight_decay, void *stream);
 
 #ifdef __cplusplus
 }
