@@ -1,6 +1,6 @@
 """One training step from a rocprofv3 kernel trace: the kernels between the last two
 launches of the DWT kernel (the first kernel of every forward), with durations, grid
-and gaps.  Usage: python tools/trace_step.py <kernel_trace.csv> [--all] [--nth K]"""
+and gaps.  Usage: python tools/trace_step.py <kernel_trace.csv> [--all] [--by-grid] [--nth K]"""
 import csv
 import sys
 
@@ -25,6 +25,18 @@ def main():
         agg[n] = (c + 1, t + d)
     for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:40]:
         print(f'{t / 1e3:9.1f} us {c:5d}  {n}')
+    if '--by-grid' in sys.argv:
+        # one row per (kernel, grid): the launch configurations of the step by total time
+        agg = {}
+        for r in step:
+            n = r['Kernel_Name'].split('(')[0][:70]
+            g = (r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'], r['Workgroup_Size_X'])
+            d = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+            c, t = agg.get((n, g), (0, 0))
+            agg[(n, g)] = (c + 1, t + d)
+        print()
+        for (n, g), (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:120]:
+            print(f'{t / 1e3:9.1f} us {c:4d}x {t / 1e3 / c:8.1f} us  {str(g):32s} {n}')
     if '--all' in sys.argv:
         prev = t0
         for r in step:
