@@ -531,6 +531,51 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(const float *__restrict_
   if (wp_t) wp_t[((int64_t)ci * taps + tap) * Cout + co] = v;
 }
 
+// multi-tensor pack: up to EWVIT_PACK_MAX weights per launch.  A workgroup packs one
+// (weight, tap, 64-co x 64-ci) tile: read once, written row-contiguous to the fwd
+// layout [co][tap][ci] and, through an LDS transpose, to the bwd_data layout
+// [ci][tap][co] (tensor found by a uniform prefix-sum search over tile counts)
+struct PackArgs {
+  int n;
+  int chunk0[EWVIT_PACK_MAX + 1];
+  const float *w[EWVIT_PACK_MAX];
+  bf16_t *wp[EWVIT_PACK_MAX];
+  bf16_t *wpt[EWVIT_PACK_MAX];
+  int64_t s_co[EWVIT_PACK_MAX], s_ci[EWVIT_PACK_MAX], s_tap[EWVIT_PACK_MAX];
+  int cout[EWVIT_PACK_MAX], cin[EWVIT_PACK_MAX], cin_pad[EWVIT_PACK_MAX], taps[EWVIT_PACK_MAX];
+};
+
+__global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackArgs a) {
+  __shared__ bf16_t tile[64][66];
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  int t = 0;
+  while (t + 1 < a.n && a.chunk0[t + 1] <= blk) ++t;
+  const int Cout = a.cout[t], Cin = a.cin[t], Cin_pad = a.cin_pad[t], taps = a.taps[t];
+  const int nco = (Cout + 63) >> 6, nci = (Cin_pad + 63) >> 6;
+  const int local = blk - a.chunk0[t];
+  const int tap = local / (nco * nci), rem = local - tap * nco * nci;
+  const int co0 = (rem / nci) * 64, ci0 = (rem % nci) * 64;
+  const float *w = a.w[t];
+  bf16_t *wp = a.wp[t], *wpt = a.wpt[t];
+  const int64_t sco = a.s_co[t], sci = a.s_ci[t], stap = a.s_tap[t];
+#pragma unroll 4
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    const int co = co0 + r, ci = ci0 + c;
+    const bf16_t v = f2bf(co < Cout && ci < Cin ? w[co * sco + ci * sci + tap * stap] : 0.f);
+    tile[r][c] = v;
+    if (wp && co < Cout && ci < Cin_pad) wp[((int64_t)co * taps + tap) * Cin_pad + ci] = v;
+  }
+  if (!wpt) return;
+  __syncthreads();
+#pragma unroll 4
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    const int ci = ci0 + r, co = co0 + c;
+    if (ci < Cin_pad && co < Cout) wpt[((int64_t)ci * taps + tap) * Cout + co] = tile[c][r];
+  }
+}
+
 // ---------------------------------------------------------------- LDS-DMA kernels
 // The same three GEMMs with the operands moved HBM/L2 -> LDS by buffer_load ... lds
 // (16 B per lane, no register round trip, no ds_write), for the shapes whose K-tiles
@@ -578,12 +623,11 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
 template <bool DGRAD, int BM, int BN_, int KS, int NS>
 __global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn, int tap_inner) {
-  constexpr int NW = BM / 32, NT = NW * 64, BK = 64;
+  constexpr int NW = BM / 32, BK = 64;
   constexpr int WN = BN_ / 2, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
   constexpr int PA = BM / 8 / NW, PB = BN_ / 8 / NW;   // 1 KiB pieces per wave per K-tile
-  constexpr int CST = BN_ + 8;
-  static_assert(PB >= 1 && BM * CST * 2 <= NS * STG, "tile shape");
+  static_assert(PB >= 1, "tile shape");
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
@@ -702,7 +746,10 @@ __global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t sr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < J; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          // operands swapped (B first): the lane holds 4 consecutive output COLUMNS of
+          // one row, acc[i][j][r] = C[i*16 + (lane&15)][j*16 + 4*(lane>>4) + r], so the
+          // epilogue stores 8 B per lane straight from registers (no LDS image)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   };
   int ld = 0, lbuf = 0;
@@ -721,30 +768,25 @@ __global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t sr
     compute(cur);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
-  __syncthreads();
-  // epilogue: (+ bias) -> bf16 tile image -> 16-B row-contiguous stores
-  bf16_t *ep = reinterpret_cast<bf16_t *>(smem);
+  // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
+  // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int cl = wn * WN + j * 16 + (lane & 15);
-    const float b = (a.bias && n0 + cl < a.Ncol) ? a.bias[n0 + cl] : 0.f;
+    const int col = n0 + wn * WN + j * 16 + fq * 4;
+    if (col >= a.Ncol) continue;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) bv = *reinterpret_cast<const float4 *>(a.bias + col);
+    const int gi = col / a.ogc;
+    bf16_t *ob = a.out + (int64_t)gi * a.ogs + (col - gi * a.ogc);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ep[(wm * 64 + i * 16 + fq * 4 + r) * CST + cl] = f2bf(acc[i][j][r] + b);
-  }
-  __syncthreads();
-  constexpr int VPR = BN_ / 8;
-#pragma unroll
-  for (int k = 0; k < BM * VPR / NT; ++k) {
-    const int v = tid + NT * k;
-    const int rl = v / VPR, cv = v % VPR;
-    const int64_t row = m0 + rl;
-    const int col = n0 + cv * 8;
-    if (row < a.M && col < a.Ncol) {
-      const int gi = col / a.ogc;
-      *reinterpret_cast<uint4 *>(a.out + (int64_t)gi * a.ogs + row * a.ogc + (col - gi * a.ogc)) =
-          *reinterpret_cast<const uint4 *>(&ep[rl * CST + cv * 8]);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = m0 + wm * 64 + i * 16 + fr;
+      if (row < a.M) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(acc[i][j][0] + bv.x) | ((uint32_t)f2bf(acc[i][j][1] + bv.y) << 16);
+        pk.y = (uint32_t)f2bf(acc[i][j][2] + bv.z) | ((uint32_t)f2bf(acc[i][j][3] + bv.w) << 16);
+        *reinterpret_cast<uint2 *>(ob + row * a.ogc) = pk;
+      }
     }
   }
 }
@@ -1088,6 +1130,33 @@ extern "C" int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_
   hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), w,
                      s_co, s_ci, s_tap, (bf16_t *)wp, (bf16_t *)wp_t, (int)Cout, (int)Cin, (int)Cin_pad, taps);
   return launch_status("conv2d_pack_weight");
+}
+
+extern "C" int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co, const int64_t *s_ci,
+                                         const int64_t *s_tap, void *const *wp, void *const *wp_t,
+                                         const int64_t *Cout, const int64_t *Cin, const int64_t *Cin_pad,
+                                         const int *ksize, void *stream) {
+  EWVIT_CHECK_ARG(n >= 0 && n <= EWVIT_PACK_MAX, "conv2d_pack_weights: %d weights (max %d per launch)", n,
+                  EWVIT_PACK_MAX);
+  if (n == 0) return 0;
+  PackArgs a;
+  a.n = n;
+  int64_t chunks = 0;
+  for (int i = 0; i < n; ++i) {
+    EWVIT_CHECK_ARG(w[i] && (wp[i] || wp_t[i]) && Cout[i] > 0 && Cin[i] > 0 && Cin_pad[i] >= Cin[i] &&
+                        (ksize[i] == 1 || ksize[i] == 3),
+                    "conv2d_pack_weights: weight %d", i);
+    const int taps = ksize[i] * ksize[i];
+    a.chunk0[i] = (int)chunks;
+    chunks += (int64_t)taps * ((Cout[i] + 63) / 64) * ((Cin_pad[i] + 63) / 64);
+    EWVIT_CHECK_ARG(chunks < ((int64_t)1 << 30), "conv2d_pack_weights: too many elements");
+    a.w[i] = w[i]; a.wp[i] = (bf16_t *)wp[i]; a.wpt[i] = (bf16_t *)wp_t[i];
+    a.s_co[i] = s_co[i]; a.s_ci[i] = s_ci[i]; a.s_tap[i] = s_tap[i];
+    a.cout[i] = (int)Cout[i]; a.cin[i] = (int)Cin[i]; a.cin_pad[i] = (int)Cin_pad[i]; a.taps[i] = taps;
+  }
+  a.chunk0[n] = (int)chunks;
+  hipLaunchKernelGGL(conv_pack_multi_kernel, dim3((unsigned)chunks), dim3(256), 0, as_stream(stream), a);
+  return launch_status("conv2d_pack_weights");
 }
 
 extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, 'libewvit.so')
 ABI_VERSION = 1
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
+PACK_MAX = 32          # EWVIT_PACK_MAX
 
 _i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 _f64 = ctypes.c_double
@@ -40,6 +41,7 @@ SIGNATURES = {
     'ewvit_bn_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
+    'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],

@@ -3,7 +3,8 @@ kernels (csrc/conv.hip) — the MWT conv stack of network/mwt.py:23-72 and the
 backbone's dense convs.
 
 Activations are channels-last bf16 (the MFMA operand type); weights stay fp32
-master parameters and are packed to bf16 [Cout][k*k][Cin] each call.  An input
+master parameters and are packed to bf16 [Cout][k*k][Cin] each call — or, inside
+``packed()`` (the training step), once per step for all convs by one launch.  An input
 may carry zero-padded channels (Cin_x > weight.shape[1]): the pack fills those
 weight rows with zeros, so they contribute exactly nothing and receive no
 gradient.
@@ -13,9 +14,87 @@ channel concatenation ``cat(z.chunk(levels), dim=1)`` ([N, levels*C, H, W], the
 multiscale fusion input of mwt.py:112) through the kernels' grouped layout, and
 returns the input gradient in z's layout — the concatenation is never built.
 """
+import contextlib
+import ctypes
+import weakref
+
 import torch
 
 from . import _lib as L
+
+# ---- step-wide weight packing: every conv weight the model used is packed by ONE
+# multi-tensor launch per 32 weights at the start of a training step (`packed()`),
+# into persistent bf16 buffers, instead of one pack launch per conv call.
+_registry = {}      # id(weight) -> {'ref', 'cin_pad', 'wp', 'wpt', 'bwd'}
+_active = False
+
+
+def _register(weight, cin_pad, bwd):
+    e = _registry.get(id(weight))
+    if e is not None and e['ref']() is weight and e['cin_pad'] == cin_pad:
+        e['bwd'] = e['bwd'] or bwd
+        return
+    _registry[id(weight)] = {'ref': weakref.ref(weight), 'cin_pad': cin_pad, 'wp': None, 'wpt': None, 'bwd': bwd}
+
+
+def prepack():
+    """Pack every registered conv weight into its persistent buffers (allocated on
+    first use); Conv2dFn reads them while `packed()` is active."""
+    items = []
+    for key in list(_registry):
+        e = _registry[key]
+        w = e['ref']()
+        if w is None or not w.is_cuda or w.dtype != torch.float32:
+            del _registry[key]
+            continue
+        Cout, k = w.shape[0], w.shape[2]
+        if e['wp'] is None or e['wp'].device != w.device:
+            e['wp'] = torch.empty((Cout, k * k, e['cin_pad']), dtype=torch.bfloat16, device=w.device)
+        if e['bwd'] and (e['wpt'] is None or e['wpt'].device != w.device):
+            e['wpt'] = torch.empty((e['cin_pad'], k * k, Cout), dtype=torch.bfloat16, device=w.device)
+        s_co, s_ci, s_kh, s_kw = w.stride()
+        if s_kh != k * s_kw:
+            e['wp'] = None          # not packable in place: this weight is packed per call
+            continue
+        items.append((w, e, (s_co, s_ci, s_kw)))
+    if not items:
+        return
+    stream = L.stream(items[0][0])
+    for i in range(0, len(items), L.PACK_MAX):
+        ch = items[i:i + L.PACK_MAX]
+        n = len(ch)
+        vp = ctypes.c_void_p * n
+        i64 = ctypes.c_int64 * n
+        L.call('ewvit_conv2d_pack_weights', n, vp(*[w.data_ptr() for w, _, _ in ch]),
+               i64(*[st[0] for _, _, st in ch]), i64(*[st[1] for _, _, st in ch]), i64(*[st[2] for _, _, st in ch]),
+               vp(*[e['wp'].data_ptr() for _, e, _ in ch]),
+               vp(*[(e['wpt'].data_ptr() if e['bwd'] else None) for _, e, _ in ch]),
+               i64(*[w.shape[0] for w, _, _ in ch]), i64(*[w.shape[1] for w, _, _ in ch]),
+               i64(*[e['cin_pad'] for _, e, _ in ch]), (ctypes.c_int * n)(*[w.shape[2] for w, _, _ in ch]),
+               stream, work={'bytes': sum(w.numel() * 8.0 for w, _, _ in ch)})
+
+
+@contextlib.contextmanager
+def packed():
+    """Scope of one forward(+backward) with the weights fixed: packs all registered
+    conv weights once on entry; convs inside read the packs."""
+    global _active
+    prepack()
+    prev, _active = _active, True
+    try:
+        yield
+    finally:
+        _active = prev
+
+
+def _cached_pack(weight, cin_pad, bwd):
+    if not _active:
+        return None
+    e = _registry.get(id(weight))
+    if e is None or e['ref']() is not weight or e['cin_pad'] != cin_pad or e['wp'] is None or \
+            (bwd and e['wpt'] is None):
+        return None
+    return e['wp'], (e['wpt'] if bwd else None)
 
 
 def _pack(weight, cin_pad, fwd=True, bwd=False):
@@ -50,7 +129,14 @@ class Conv2dFn(torch.autograd.Function):
             raise ValueError(f'conv2d: input {tuple(x.shape)} (levels={levels}), weight {tuple(weight.shape)}')
         xc = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         gc, gs = (Cz, N * H * W * Cz) if levels > 1 else (0, 0)
-        wp, wpt = _pack(weight, Cx, True, ctx.needs_input_grad[0])
+        bwd = ctx.needs_input_grad[0]
+        cached = _cached_pack(weight, Cx, bwd) if weight.dtype == torch.float32 else None
+        if cached is None:
+            wp, wpt = _pack(weight, Cx, True, bwd)
+            if weight.dtype == torch.float32:
+                _register(weight, Cx, bwd)
+        else:
+            wp, wpt = cached
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = bias.detach().float().contiguous() if bias is not None else None

@@ -56,8 +56,10 @@ class TrainStep:
             dist._broadcast_coalesced(self.group or dist.group.WORLD, self.buffers, 64 << 20, 0)
 
     def _fwd_bwd(self):
-        loss = self.forward_loss()
-        loss.backward()
+        from . import conv
+        with conv.packed():          # every conv weight packed to bf16 by one launch
+            loss = self.forward_loss()
+            loss.backward()
         if self.world > 1:
             torch._foreach_copy_(self.views, [p.grad for p in self.params])
         return loss

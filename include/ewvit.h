@@ -31,6 +31,7 @@ extern "C" {
 #define EWVIT_BF16 1
 #define EWVIT_EINVAL 1000
 #define EWVIT_ADAM_MAX 48   /* tensors per ewvit_adam_step launch */
+#define EWVIT_PACK_MAX 32   /* weights per ewvit_conv2d_pack_weights launch */
 
 int ewvit_abi_version(void);
 const char *ewvit_last_error(void);
@@ -214,6 +215,12 @@ int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, 
 int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t s_tap, void *wp,
                              void *wp_t, int64_t Cout, int64_t Cin, int64_t Cin_pad, int ksize,
                              void *stream);
+/* ewvit_conv2d_pack_weight for n <= EWVIT_PACK_MAX weights in ONE launch (arrays of the
+ * same per-weight arguments; ksize[i] 1 or 3): the training step packs every conv
+ * weight of the model once, after the optimizer update, instead of once per conv. */
+int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co, const int64_t *s_ci,
+                              const int64_t *s_tap, void *const *wp, void *const *wp_t, const int64_t *Cout,
+                              const int64_t *Cin, const int64_t *Cin_pad, const int *ksize, void *stream);
 /* Kernel-family switch for A/B measurement (not needed for correctness): 0 uses the
  * register-staged kernels everywhere; 1..4 (+8: tap-inner K order; default 9, or
  * EWVIT_CONV_GLDS) select an

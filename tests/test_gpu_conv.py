@@ -44,6 +44,9 @@ def rel(a, b):
     (3, 64, 64, 384, 30, 31, 1, 3),      # 3 N tiles, ragged M
     (2, 128, 128, 128, 57, 55, 2, 3),    # odd sizes, stride 2
     (5, 64, 64, 64, 33, 35, 1, 1),       # 1x1, 64-wide output tile
+    (4, 1536, 1536, 256, 7, 7, 1, 1),    # 1x1 project: long K, few tiles
+    (3, 256, 256, 1536, 7, 7, 1, 1),     # 1x1 expand: long-K dgrad
+    (2, 192, 192, 160, 9, 9, 1, 3),      # 3x3, few tiles, 27 K-tiles
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec
@@ -119,3 +122,46 @@ def test_conv_weight_grad_in_param_layout(Cx, Cin, k):
     y.backward(dy.to(DEV))
     assert wd.grad.stride() == wd.stride()
     assert rel(wd.grad, wr.grad) < 1e-3
+
+
+def test_step_wide_weight_packing():
+    """conv.packed(): every registered weight packed by one multi-tensor launch; the
+    convs inside read those packs (bitwise the per-call packs), and a weight updated
+    between steps is re-packed at the next scope entry."""
+    import ewvit.conv as ec
+    g = torch.Generator().manual_seed(11)
+    shapes = [(64, 64, 3), (128, 54, 3), (256, 1536, 1), (40, 24, 1)]
+    ws = [(torch.randn(co, ci, k, k, generator=g) * 0.1).to(DEV).requires_grad_(True) for co, ci, k in shapes]
+    ws[1].data = ws[1].data.contiguous(memory_format=torch.channels_last)
+    xs = [torch.randn(2, (ci + 7) // 8 * 8 if ci % 8 else ci, 9, 9, generator=g).to(torch.bfloat16).to(DEV)
+          .contiguous(memory_format=torch.channels_last).requires_grad_(True) for _, ci, _ in shapes]
+    for x, (_, ci, _) in zip(xs, shapes):
+        with torch.no_grad():
+            x[:, ci:] = 0
+
+    def run():
+        outs = []
+        for x, w in zip(xs, ws):
+            y = ec.conv2d(x, w, None, 1)
+            y.float().square().sum().backward()
+            outs.append((y.detach().clone(), x.grad.clone(), w.grad.clone()))
+            x.grad = None
+            w.grad = None
+        return outs
+    ref = run()                        # per-call packs; registers the weights
+    with ec.packed():
+        assert all(ec._cached_pack(w, x.shape[1], True) is not None for x, w in zip(xs, ws))
+        got = run()
+    for a, b in zip(ref, got):
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-0.5)
+    ref2 = run()
+    with ec.packed():
+        got2 = run()
+    for a, b in zip(ref2, got2):
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+    assert not torch.equal(ref[0][0], ref2[0][0])

@@ -51,6 +51,8 @@ def main():
     ap.add_argument('--only', default=None)
     ap.add_argument('--mm', action='store_true')
     ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--shape', action='append', default=[],
+                    help='extra shape N,Cin,H,W,Cout,k,stride,levels (repeatable; replaces the table)')
     ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged')
     a = ap.parse_args()
     a.variants = [int(v) for v in a.variants.split(',')]
@@ -59,7 +61,10 @@ def main():
     from ewvit import _lib as L
     from ewvit.conv import _pack
     lib = L.load()
-    for name, (N, Cin, H, W, Cout, k, s, lv) in SHAPES.items():
+    shapes = SHAPES
+    if a.shape:
+        shapes = {f'shape{i}': tuple(int(v) for v in sh.split(',')) for i, sh in enumerate(a.shape)}
+    for name, (N, Cin, H, W, Cout, k, s, lv) in shapes.items():
         if a.only and a.only not in name:
             continue
         Cx = Cin * lv
@@ -77,10 +82,12 @@ def main():
         flops = 2.0 * N * Ho * Wo * Cout * k * k * Cx
 
         def fwd():
-            L.call('ewvit_conv2d_fwd', L.ptr(z), L.ptr(wp), None, L.ptr(y), N, H, W, Cx, Cout, k, s, gc, gs, L.stream(y))
+            L.call('ewvit_conv2d_fwd', L.ptr(z), L.ptr(wp), None, L.ptr(y), N, H, W, Cx, Cout, k, s, gc, gs,
+                   L.stream(y))
 
         def dgrad():
-            L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, s, gc, gs, L.stream(y))
+            L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, s, gc, gs,
+                   L.stream(y))
 
         def wgrad():
             L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), None, 0, N, H, W, Cx, Cout, k, s,
