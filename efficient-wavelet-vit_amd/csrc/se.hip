@@ -172,6 +172,28 @@ __global__ __launch_bounds__(256) void scale_add_kernel(const void *__restrict__
   se_st8<DT>(y, v * 8, vr);
 }
 
+// StochasticDepth(row) drawn in-kernel: scale[n] = (u(n) < keep) / keep with u the
+// counter hash of (seed, step counter, n) — every thread draws its row's value, the
+// thread holding the row's first vector stores it for the backward pass
+template <int DT>
+__global__ __launch_bounds__(256) void scale_add_drop_kernel(const void *__restrict__ r, const void *__restrict__ x,
+                                                             float keep, uint64_t seed,
+                                                             const int64_t *__restrict__ seed_offset,
+                                                             float *__restrict__ scale_out, void *__restrict__ y,
+                                                             int64_t nvec, int64_t row_vec) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nvec) return;
+  const int64_t n = v / row_vec;
+  const float sc = uniform01(step_seed(seed, seed_offset), (uint64_t)n) < keep ? 1.f / keep : 0.f;
+  if (v == n * row_vec) scale_out[n] = sc;
+  float vr[8], vx[8];
+  se_ld8<DT>(r, v * 8, vr);
+  se_ld8<DT>(x, v * 8, vx);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vr[j] = fmaf(vr[j], sc, vx[j]);
+  se_st8<DT>(y, v * 8, vr);
+}
+
 // ---------------------------------------------------------------- squeeze MLP
 // s0 [N, C] -> h1 = W1 s0 + b1 [N, Csq] -> a1 = silu(h1) -> s = sigmoid(W2 a1 + b2) [N, C]
 // (torchvision SqueezeExcitation fc1 / fc2 as 1x1 convs, fp32 like the reference).
@@ -458,6 +480,24 @@ extern "C" int ewvit_scale_add(const void *r, const void *x, int dtype, const fl
     hipLaunchKernelGGL(scale_add_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), r, x, scale, y, nvec,
                        row_elems / 8);
   return launch_status("scale_add");
+}
+
+extern "C" int ewvit_scale_add_drop(const void *r, const void *x, int dtype, float keep_prob, uint64_t seed,
+                                    const int64_t *seed_offset, float *scale_out, void *y, int64_t N,
+                                    int64_t row_elems, void *stream) {
+  EWVIT_CHECK_ARG(dtype_ok(dtype), "scale_add_drop: dtype %d", dtype);
+  EWVIT_CHECK_ARG(r && x && scale_out && y && N > 0 && row_elems > 0 && row_elems % 8 == 0,
+                  "scale_add_drop: bad args (row_elems %% 8 == 0)");
+  EWVIT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "scale_add_drop: keep_prob %g", (double)keep_prob);
+  const int64_t nvec = N * row_elems / 8;
+  dim3 grid((unsigned)((nvec + 255) / 256));
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(scale_add_drop_kernel<EWVIT_BF16>, grid, dim3(256), 0, as_stream(stream), r, x, keep_prob,
+                       seed, seed_offset, scale_out, y, nvec, row_elems / 8);
+  else
+    hipLaunchKernelGGL(scale_add_drop_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), r, x, keep_prob,
+                       seed, seed_offset, scale_out, y, nvec, row_elems / 8);
+  return launch_status("scale_add_drop");
 }
 
 static int se_mlp_check(int64_t N, int64_t C, int64_t Csq, const char *nm) {

@@ -126,6 +126,33 @@ class ScaleAddFn(torch.autograd.Function):
         return dr, dy.to(ctx.xdt), None
 
 
+class DropAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, x, keep_prob):
+        from .ops import _seed
+        L.require_gpu(r, x)
+        rc = r.contiguous(memory_format=torch.channels_last)
+        xc = x.to(rc.dtype).contiguous(memory_format=torch.channels_last)
+        N = rc.shape[0]
+        y = torch.empty_like(rc)
+        scale = torch.empty(N, dtype=torch.float32, device=r.device)
+        L.call('ewvit_scale_add_drop', L.ptr(rc), L.ptr(xc), L.dt(rc), float(keep_prob), _seed(),
+               L.ptr(L.rng_offset(r.device)), L.ptr(scale), L.ptr(y), N, rc.numel() // N, L.stream(y),
+               work={'bytes': 3 * rc.numel() * rc.element_size()})
+        ctx.save_for_backward(scale)
+        ctx.xdt = x.dtype
+        return y
+
+    backward = ScaleAddFn.backward
+
+
+def drop_add(r, x, drop_prob):
+    """StochasticDepth(p=drop_prob, mode='row')(r) + x in one pass, the per-sample keep
+    mask drawn in the kernel (counter hash of a per-call seed and the ewvit step
+    counter, as ewvit dropout draws; advanced by _lib.rng_advance once per step)."""
+    return DropAddFn.apply(r, x, 1.0 - float(drop_prob))
+
+
 def scale_add(r, scale, x):
     """r * scale[n] + x for [N, C, H, W] tensors (scale: f32 [N], no gradient) —
     StochasticDepth(mode='row') fused with the residual add of an MBConv block."""

@@ -110,10 +110,10 @@ class _Block(nn.Module):
         if self.use_res_connect:
             if self.training and self.sd_prob > 0.0 and r.is_cuda and r.dtype in (torch.bfloat16, torch.float32) \
                     and (r[0].numel() % 8 == 0):
-                # StochasticDepth(row) keep mask drawn as torchvision does, then ONE fused
-                # r * keep/(1-p) + x pass
-                keep = torch.empty((r.shape[0],), dtype=torch.float32, device=r.device).bernoulli_(1.0 - self.sd_prob)
-                return ewvit.scale_add(r, keep.div_(1.0 - self.sd_prob), x)
+                # StochasticDepth(row) + skip add in ONE pass, the keep mask drawn in the
+                # kernel (counter-hash RNG like ewvit dropout: same distribution as
+                # torchvision's bernoulli_, not its random stream)
+                return ewvit.drop_add(r, x, self.sd_prob)
             return _drop_path(r, self.sd_prob, self.training) + x
         return r
 

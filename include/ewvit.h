@@ -282,6 +282,13 @@ int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const flo
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
                     int64_t row_elems, void *stream);
+/* The same add with the StochasticDepth(row) keep mask drawn in-kernel: scale[n] =
+ * (u < keep_prob) / keep_prob, u uniform in [0,1) from the counter hash of (seed +
+ * *seed_offset * golden, n) as ewvit dropout draws it; scale_out[n] receives the
+ * factors (the backward's ewvit_scale_add scale). */
+int ewvit_scale_add_drop(const void *r, const void *x, int dtype, float keep_prob, uint64_t seed,
+                         const int64_t *seed_offset, float *scale_out, void *y, int64_t N, int64_t row_elems,
+                         void *stream);
 
 /* ------------------------------------------------------ optimizer ---
  * Adam exactly as torch.optim.Adam (amsgrad=False, maximize=False): g += wd*p;

@@ -71,3 +71,34 @@ def test_scale_add(dtype):
     tol = 2 ** -7 if dtype == torch.bfloat16 else 1e-6
     assert rel(y, yr) < tol
     assert rel(rd.grad, rr.grad) < tol and rel(xd.grad, xr.grad) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_drop_add(dtype):
+    """StochasticDepth(row) + skip add with the keep mask drawn in-kernel: y and the
+    gradients follow r * scale[n] + x for the 0 / 1/keep factors the kernel drew;
+    the kept fraction matches keep over many rows; a new step counter redraws."""
+    import ewvit
+    from ewvit import _lib as L
+    g = torch.Generator().manual_seed(10)
+    N, p = 4096, 0.3
+    r = torch.randn(N, 16, 3, 3, generator=g).to(dtype).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(N, 16, 3, 3, generator=g).to(dtype).to(DEV).to(memory_format=torch.channels_last)
+    rd, xd = r.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    y = ewvit.drop_add(rd, xd, p)
+    dy = torch.randn(y.shape, generator=g).to(dtype).to(DEV).to(memory_format=torch.channels_last)
+    y.backward(dy)
+    # recover the factors from the rows: kept rows have y - x = r / (1-p)
+    kept = ((y.float() - x.float()).abs().flatten(1).amax(1) > 0)
+    sc = kept.float() / (1 - p)
+    yr = r.float() * sc.view(-1, 1, 1, 1) + x.float()
+    tol = 2 ** -7 if dtype == torch.bfloat16 else 1e-6
+    assert rel(y, yr) < tol
+    assert rel(rd.grad, dy.float() * sc.view(-1, 1, 1, 1)) < tol and rel(xd.grad, dy) < tol
+    frac = float(kept.float().mean())
+    assert abs(frac - (1 - p)) < 4 * ((p * (1 - p) / N) ** 0.5)
+    L.rng_advance(r.device)
+    with torch.no_grad():
+        y2 = ewvit.drop_add(r, x, p)
+    kept2 = ((y2.float() - x.float()).abs().flatten(1).amax(1) > 0)
+    assert not torch.equal(kept, kept2)
