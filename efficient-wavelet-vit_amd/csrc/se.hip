@@ -52,27 +52,37 @@ struct SePlan {
   int rows_per_split;
 };
 
-// block = LC channel vectors x R row groups; grid (N * S, cblocks)
+// block = LC channel vectors x R row groups; grid (N * S, cblocks).  Narrow channel
+// chunks (LC <= 32 vectors, R >= 8 row groups) give >= 2 blocks per frame and short
+// per-thread row walks; the rows are split (S > 1, then a fold launch sums the
+// slabs) only when a thread would otherwise walk more than 32 rows — never for the
+// backbone's SE shapes (HW <= 196), which therefore take one launch.
 static SePlan se_plan(int64_t N, int64_t HW, int64_t C) {
   SePlan p;
   p.C8 = (int)(C / 8);
-  p.LC = p.C8 < 256 ? p.C8 : 256;
+  p.LC = p.C8 < 32 ? p.C8 : 32;
   p.R = 256 / p.LC;
   p.cblocks = (p.C8 + p.LC - 1) / p.LC;
-  int64_t s = (512 + N * p.cblocks - 1) / (N * p.cblocks);     // ~512 blocks
-  const int64_t maxs = HW / (4 * p.R);                          // >= 4 rows per thread
-  if (s > maxs) s = maxs;
+  int64_t s = (HW + 32 * p.R - 1) / (32 * p.R);                 // <= 32 rows per thread
+  if (N * p.cblocks * s < 256) {                                // fill the chip when rows allow
+    int64_t want = (256 + N * p.cblocks - 1) / (N * p.cblocks);
+    const int64_t maxs = HW / (8 * p.R);                        // >= 8 rows per thread
+    if (want > maxs) want = maxs;
+    if (want > s) s = want;
+  }
   if (s < 1) s = 1;
   p.S = (int)s;
   p.rows_per_split = (int)((HW + s - 1) / s);
   return p;
 }
 
-// part[split][n][c] = sum over this split's rows of a (PROD=0) or a*b (PROD=1)
+// part[split][n][c] = sum over this split's rows of a (PROD=0) or a*b (PROD=1);
+// with one split the block writes out[n][c] = scale * sum directly
 template <int DT, int PROD>
 __global__ __launch_bounds__(256) void se_reduce_kernel(const void *__restrict__ a, const void *__restrict__ b,
                                                         int HW, int C, int R, int LC, int S, int rps,
-                                                        float *__restrict__ part, int N) {
+                                                        float *__restrict__ part, int N, float scale,
+                                                        float *__restrict__ out) {
   __shared__ float sm[256 * 8];
   const int n = blockIdx.x / S, split = blockIdx.x % S;
   const int tid = threadIdx.x, rg = tid / LC, cl = tid % LC;
@@ -85,15 +95,15 @@ __global__ __launch_bounds__(256) void se_reduce_kernel(const void *__restrict__
   if (active) {
     const int64_t base = (int64_t)n * HW * C + c8 * 8;
     int h = h0 + rg;
-    for (; h + 3 * R < h1; h += 4 * R) {     // 4 rows' loads in flight
-      float va[4][8], vb[4][8];
+    for (; h + 7 * R < h1; h += 8 * R) {     // 8 rows' loads in flight
+      float va[8][8], vb[8][8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 8; ++q) {
         se_ld8<DT>(a, base + (int64_t)(h + q * R) * C, va[q]);
         if (PROD) se_ld8<DT>(b, base + (int64_t)(h + q * R) * C, vb[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = PROD ? fmaf(va[q][j], vb[q][j], acc[j]) : acc[j] + va[q][j];
     }
@@ -112,9 +122,15 @@ __global__ __launch_bounds__(256) void se_reduce_kernel(const void *__restrict__
     for (int g = 1; g < R; ++g)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += sm[(g * LC + cl) * 8 + j];
-    float *dst = part + ((int64_t)split * N + n) * C + c8 * 8;
+    if (S == 1) {
+      float *dst = out + (int64_t)n * C + c8 * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j] = acc[j];
+      for (int j = 0; j < 8; ++j) dst[j] = acc[j] * scale;
+    } else {
+      float *dst = part + ((int64_t)split * N + n) * C + c8 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j] = acc[j];
+    }
   }
 }
 
@@ -441,13 +457,15 @@ extern "C" int ewvit_se_reduce(const void *a, const void *b, int dtype, int64_t 
   dim3 grid((unsigned)(N * p.S), (unsigned)p.cblocks);
 #define SE_RED(DTV, PV)                                                                                        \
   hipLaunchKernelGGL((se_reduce_kernel<DTV, PV>), grid, dim3(256), 0, s, a, b, (int)HW, (int)C, p.R, p.LC, p.S, \
-                     p.rows_per_split, workspace, (int)N)
+                     p.rows_per_split, workspace, (int)N, scale, out)
   if (dtype == EWVIT_BF16) { if (b) SE_RED(EWVIT_BF16, 1); else SE_RED(EWVIT_BF16, 0); }
   else { if (b) SE_RED(EWVIT_F32, 1); else SE_RED(EWVIT_F32, 0); }
 #undef SE_RED
-  const int64_t NC = N * C;
-  hipLaunchKernelGGL(se_fold_kernel, dim3((unsigned)((NC + 255) / 256)), dim3(256), 0, s, workspace, p.S, NC, scale,
-                     out);
+  if (p.S > 1) {
+    const int64_t NC = N * C;
+    hipLaunchKernelGGL(se_fold_kernel, dim3((unsigned)((NC + 255) / 256)), dim3(256), 0, s, workspace, p.S, NC,
+                       scale, out);
+  }
   return launch_status("se_reduce");
 }
 

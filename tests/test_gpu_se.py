@@ -25,7 +25,7 @@ def ref_se(x, w1, b1, w2, b2):
 
 
 @pytest.mark.parametrize('N,C,H,W,csq', [(4, 256, 28, 28, 16), (3, 960, 14, 14, 40), (2, 1536, 7, 7, 64),
-                                         (5, 24, 9, 11, 6), (2, 2048, 3, 3, 8)])
+                                         (5, 24, 9, 11, 6), (2, 2048, 3, 3, 8), (64, 960, 14, 14, 40)])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
 def test_squeeze_excite(N, C, H, W, csq, dtype):
     import ewvit
