@@ -621,17 +621,18 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // fwd / dgrad: BM x BN_ x 64 tiles, BM/32 waves (BM/64 x 2), NS-deep LDS ring of
 // [row][64 k] images (128-B rows); 16-B chunk c of row r is stored at chunk
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
-template <bool DGRAD, int BM, int BN_, int KS, int NS>
-__global__ __launch_bounds__(BM * 2) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn, int tap_inner) {
-  constexpr int NW = BM / 32, BK = 64;
-  constexpr int WN = BN_ / 2, J = WN / 16;
+template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2>
+__global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn,
+                                                                      int tap_inner) {
+  constexpr int NW = BM / 64 * WC, BK = 64;      // waves: BM/64 rows x WC columns
+  constexpr int WN = BN_ / WC, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
   constexpr int PA = BM / 8 / NW, PB = BN_ / 8 / NW;   // 1 KiB pieces per wave per K-tile
   static_assert(PB >= 1, "tile shape");
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
-  const int wm = ws >> 1, wn = ws & 1;
+  const int wm = ws / WC, wn = ws % WC;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
@@ -973,7 +974,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
 
 // Kernel family: 0 register-staged everywhere; 1.. LDS-DMA configurations
 //   fwd/dgrad (rows per tile, ring depth): 1 (128, 2)  2 (128, 3)  3 (256, 2)  4 (256, 3)
-//     5 (128; ring 4 when the grid is <= 256 workgroups, else 2)
+//     5 (128; ring 4 when the grid is <= 256 workgroups, else 2)  7 (128, 2, 8 waves)
+//     1 takes 7's 8-wave blocks for grids of <= 1024 workgroups
 //   wgrad (pixels per K-tile, ring depth): 1 (64, 2)   2 (64, 3)   3 (32, 3)   4 (32, 4)
 // +8: fwd/dgrad K-tiles ordered channel-block outer, tap inner.
 // EWVIT_CONV_GLDS=<n> or ewvit_conv2d_set_glds(n) select one (A/B measurement).
@@ -982,7 +984,7 @@ static int glds_variant() {
   if (g_glds < 0) {
     const char *e = getenv("EWVIT_CONV_GLDS");
     g_glds = e ? atoi(e) : 9;
-    if ((g_glds & 7) > 5 || g_glds < 0 || g_glds > 15) g_glds = 9;
+    if (g_glds < 0 || g_glds > 15) g_glds = 9;
   }
   return g_glds;
 }
@@ -1053,22 +1055,30 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   const int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
   const dim3 grid((unsigned)nwg);
-#define EWVIT_GLDS_FWD(BM_, BN__, NS_)                                                                              \
+#define EWVIT_GLDS_FWDW(BM_, BN__, NS_, WC_)                                                                        \
   do {                                                                                                            \
     if (a.g.ks == 1)                                                                                              \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn, tap_inner); \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
+                         src_bytes, ntn, tap_inner);                                                              \
     else                                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_>), grid, dim3(BM_ * 2), 0, s, a, src_bytes, ntn, tap_inner); \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
+                         src_bytes, ntn, tap_inner);                                                              \
   } while (0)
+#define EWVIT_GLDS_FWD(BM_, BN__, NS_) EWVIT_GLDS_FWDW(BM_, BN__, NS_, 2)
   // variant 5: a grid of at most one workgroup per CU cannot hide the operand latency
   // behind a second resident block, so it gets a 4-deep LDS ring (3 K-tiles in flight)
-  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : v;
+  // variant 1 (the default family): grids of <= 1024 workgroups (the backbone's 7x7 /
+  // 14x14 / 28x28 convs) take 8-wave blocks (64 x BN/4 per wave) — twice the waves per
+  // CU to hide the latency of their short K loops; big grids keep 4 waves (fewer LDS
+  // reads per MFMA)
+  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && nwg <= 1024 ? 7 : v);
   if (bn == 64) {
     switch (vv) {
       case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
       case 3: EWVIT_GLDS_FWD(256, 64, 2); break;
       case 4: EWVIT_GLDS_FWD(256, 64, 3); break;
       case 6: EWVIT_GLDS_FWD(128, 64, 4); break;
+      case 7: EWVIT_GLDS_FWDW(128, 64, 2, 4); break;
       default: EWVIT_GLDS_FWD(128, 64, 2); break;
     }
   } else {
@@ -1077,10 +1087,12 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
       case 3: EWVIT_GLDS_FWD(256, 128, 2); break;
       case 4: EWVIT_GLDS_FWD(256, 128, 3); break;
       case 6: EWVIT_GLDS_FWD(128, 128, 4); break;
+      case 7: EWVIT_GLDS_FWDW(128, 128, 2, 4); break;
       default: EWVIT_GLDS_FWD(128, 128, 2); break;
     }
   }
 #undef EWVIT_GLDS_FWD
+#undef EWVIT_GLDS_FWDW
   return true;
 }
 
@@ -1116,7 +1128,7 @@ using namespace ewvit;
 
 extern "C" int ewvit_conv2d_set_glds(int variant) {
   const int prev = glds_variant();
-  g_glds = variant >= 0 && variant <= 15 && (variant & 7) <= 5 ? variant : 9;
+  g_glds = variant >= 0 && variant <= 15 ? variant : 9;
   return prev;
 }
 

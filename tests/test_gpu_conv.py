@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.fixture(params=[1, 9, 13, 2, 3, 4, 0], ids=['glds1', 'glds9', 'glds13', 'glds2', 'glds3', 'glds4', 'regstage'])
+@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0], ids=['glds1', 'glds9', 'glds13', 'glds15', 'glds2', 'glds3', 'glds4', 'regstage'])
 def glds(request):
     """Run each case on every LDS-DMA configuration and on the register-staged kernels."""
     import ewvit

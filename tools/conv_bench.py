@@ -27,7 +27,15 @@ SHAPES = {
 }
 
 
+EAGER = False
+
+
 def graph_time(fn, iters):
+    if EAGER:                      # plain launches (PMC passes): time is not meaningful
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        return 1.0
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
@@ -54,7 +62,10 @@ def main():
     ap.add_argument('--shape', action='append', default=[],
                     help='extra shape N,Cin,H,W,Cout,k,stride,levels (repeatable; replaces the table)')
     ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged')
+    ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
+    global EAGER
+    EAGER = a.eager
     a.variants = [int(v) for v in a.variants.split(',')]
     import ewvit
     dev = torch.device('cuda', 0)
