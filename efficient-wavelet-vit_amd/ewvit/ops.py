@@ -31,8 +31,10 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
     if splitk is None:
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
         splitk = 1
-        if tiles < 128 and K >= 2048:
-            splitk = int(max(1, min(64, 256 // max(tiles, 1), K // 1024)))
+        # small grids (the ViT / DAMA token GEMMs: M, N <= 512) are latency-bound on
+        # their serial K loop: split K so ~256 workgroups run >= 8 K-steps of 32 each
+        if tiles < 128 and K >= 256:
+            splitk = int(max(1, min(64, 512 // max(tiles, 1), K // 128)))
     ws = torch.empty(splitk * M * N, dtype=torch.float32, device=C.device) if splitk > 1 else None
     work = {'flops': 2.0 * M * N * K,
             'bytes': M * K * A.element_size() + K * N * B.element_size() + M * N * C.element_size()}
