@@ -469,40 +469,67 @@ struct WOut {
   int cin;
 };
 
-// dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci]; a thread
-// sums 4 consecutive slab elements (one 16-B load per split, 4 splits in flight)
+// dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci].  T lanes of a
+// wave share one 4-element output (T = splits fan-in, a power of two <= 64 chosen so
+// ~64K threads run): lane l sums splits l, l+T, ... (4 loads in flight), then an xor
+// tree over the T lanes — fixed order, deterministic.  Blocks >= nmain reduce the bias
+// partials: 64 channels per block, 4 waves over the partial rows, fixed-order combine.
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__restrict__ part, float *__restrict__ dw,
                                                                 int Cout, int Cin, int taps, int splits, int bparts,
                                                                 int accumulate, const float *__restrict__ dbias_part,
-                                                                float *__restrict__ dbias, WOut wo) {
+                                                                float *__restrict__ dbias, WOut wo, int T, int nmain) {
+  __shared__ float red[4][64];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= nmain) {
+    const int c = ((int)blockIdx.x - nmain) * 64 + (tid & 63), q = tid >> 6;
+    float sb = 0.f;
+    if (c < Cout) {
+      int k = q;
+      for (; k + 12 < bparts; k += 16) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = dbias_part[(int64_t)(k + 4 * u) * Cout + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sb += v[u];
+      }
+      for (; k < bparts; k += 4) sb += dbias_part[(int64_t)k * Cout + c];
+    }
+    red[q][tid & 63] = sb;
+    __syncthreads();
+    if (tid < 64 && c < Cout) {
+      const float r = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+      dbias[c] = accumulate ? dbias[c] + r : r;
+    }
+    return;
+  }
   const int64_t NP = taps * (int64_t)Cin;
   const int64_t n = (int64_t)Cout * NP;                                // n % 4 == 0 (Cin % 8 == 0)
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (dbias && t < Cout) {
-    float sb = 0.f;
-    for (int k = 0; k < bparts; ++k) sb += dbias_part[(int64_t)k * Cout + t];
-    dbias[t] = accumulate ? dbias[t] + sb : sb;
-  }
-  const int64_t i = t * 4;
-  if (i >= n) return;
+  const int sl = tid & (T - 1);
+  const int64_t i = ((int64_t)blockIdx.x * (256 / T) + tid / T) * 4;
+  const bool ok = i < n;
+  const int64_t ii = ok ? i : 0;
   float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-  int k = 0;
-  for (; k + 3 < splits; k += 4) {
-    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + i);
-    const float4 b = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 1) * n + i);
-    const float4 c = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 2) * n + i);
-    const float4 d = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 3) * n + i);
+  int k = sl;
+  for (; k + 3 * T < splits; k += 4 * T) {
+    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + ii);
+    const float4 b = *reinterpret_cast<const float4 *>(part + (int64_t)(k + T) * n + ii);
+    const float4 c = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 2 * T) * n + ii);
+    const float4 d = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 3 * T) * n + ii);
     s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
     s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
     s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
     s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
   }
-  for (; k < splits; ++k) {
-    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + i);
+  for (; k < splits; k += T) {
+    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + ii);
     s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
   }
-  const float r[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
-                      (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w)};
+  float r[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w)};
+  for (int o = T >> 1; o >= 1; o >>= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] += __shfl_xor(r[e], o, 64);
+  if (!ok || sl != 0) return;
   const int co = (int)(i / NP);
   const int np = (int)(i % NP);
   const int tap = np / Cin, ci = np % Cin;
@@ -1288,8 +1315,11 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   if (int rc = launch_status("conv2d_bwd_weight")) return rc;
   if (direct) return 0;
   const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
-  const int64_t nt = n4 > g.Cout ? n4 : g.Cout;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, workspace, dw,
-                     g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias, wo);
+  int T = 1;                       // split lanes per output: ~64K threads, <= splits, <= 64
+  while (T < 64 && T * 2 <= sp && n4 * T * 2 <= 65536) T *= 2;
+  const int64_t nmain = (n4 * T + 255) / 256;
+  const int64_t nbias = dbias ? (g.Cout + 63) / 64 : 0;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,
+                     g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias, wo, T, (int)nmain);
   return launch_status("conv2d_bwd_weight reduce");
 }
