@@ -131,7 +131,9 @@ extern "C" int ewvit_layernorm_bwd(const void *dy, int dy_dtype, const void *x, 
   EWVIT_CHECK_ARG(dtype_ok(dy_dtype) && dtype_ok(x_dtype), "layernorm_bwd: bad dtype");
   EWVIT_CHECK_ARG(D > 0 && D <= 64 * LN_MAXV, "layernorm_bwd: D=%lld not in (0,1024]", (long long)D);
   if (M == 0) return 0;
-  const int rpb = 16;
+  // one row per wave: the token counts here are small (M = 128..512), so the grid,
+  // not per-block atomics, sets the time
+  const int rpb = M >= 16384 ? 16 : 4;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0,
                      as_stream(stream), dy, dy_dtype, x, x_dtype, ldx, gamma, mean, rstd, dx,
                      accumulate_dx, dgamma, dbeta, M, (int)D, rpb);
