@@ -541,6 +541,33 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
   return launch_status("bn_fwd");
 }
 
+// training forward from precomputed partial statistics (nrc rows of shifted sums +
+// the shift, e.g. left by ewvit_conv2d_fwd_bn in the producing conv's epilogue):
+// the apply pass only (it finalises from the partial rows), one group
+extern "C" int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
+                                     const float *beta, float *running_mean, float *running_var, float momentum,
+                                     float eps, int act, float *save_mean, float *save_invstd,
+                                     int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
+                                     void *stream) {
+  EWVIT_CHECK_ARG(x && y && part && shifts && dtype_ok(dtype), "bn_fwd_partials: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_fwd_partials: C=%lld must be a multiple of 8, <= 4096",
+                  (long long)C);
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_fwd_partials: act=%d", act);
+  EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 4096, "bn_fwd_partials: %d partial rows", nrc);
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const BnGeo geo = bn_geo(C);
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 agrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+#define BN_APPLY(DTV, ACTV)                                                                                          \
+  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc, M,      \
+                     (int)C, geo.CC8, geo.RG, rpb, 1, gamma, beta, running_mean, running_var, momentum, eps,        \
+                     save_mean, save_invstd, num_batches_tracked)
+  BN_DISPATCH(BN_APPLY);
+#undef BN_APPLY
+  return launch_status("bn_fwd_partials");
+}
+
 extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
                             const float *gamma, const float *beta, const float *save_mean,
                             const float *save_invstd, int act, float *dgamma, float *dbeta, int accumulate,

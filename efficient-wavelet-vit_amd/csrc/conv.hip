@@ -61,6 +61,12 @@ struct FwdArgs {
   int outH, outW;        // spatial size of the GEMM's output grid
   int sgc, ogc;          // channel group widths of src / out
   int64_t sgs, ogs;      // group strides (elements)
+  // optional BatchNorm statistics of the (bf16-rounded) output, LDS-DMA fwd only:
+  // per m-tile t and column c, bn_part[t][c] = sum (y - K[c]), bn_part[t][Ncol + c] =
+  // sum (y - K[c])^2 with K = bn_shift (or 0); tile 0 copies K to bn_shift_out
+  const float *bn_shift = nullptr;
+  float *bn_part = nullptr;
+  float *bn_shift_out = nullptr;
 };
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
@@ -798,23 +804,73 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   }
   // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
   // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
+  const bool stats = a.bn_part != nullptr;
+  float cs[J][4], cq[J][4];     // this lane's column sums over its 4 rows (BN statistics)
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int col = n0 + wn * WN + j * 16 + fq * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
     if (col >= a.Ncol) continue;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (a.bias) bv = *reinterpret_cast<const float4 *>(a.bias + col);
+    float4 kv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (stats && a.bn_shift) kv = *reinterpret_cast<const float4 *>(a.bn_shift + col);
     const int gi = col / a.ogc;
     bf16_t *ob = a.out + (int64_t)gi * a.ogs + (col - gi * a.ogc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = m0 + wm * 64 + i * 16 + fr;
       if (row < a.M) {
+        const bf16_t h0 = f2bf(acc[i][j][0] + bv.x), h1 = f2bf(acc[i][j][1] + bv.y);
+        const bf16_t h2 = f2bf(acc[i][j][2] + bv.z), h3 = f2bf(acc[i][j][3] + bv.w);
         uint2 pk;
-        pk.x = (uint32_t)f2bf(acc[i][j][0] + bv.x) | ((uint32_t)f2bf(acc[i][j][1] + bv.y) << 16);
-        pk.y = (uint32_t)f2bf(acc[i][j][2] + bv.z) | ((uint32_t)f2bf(acc[i][j][3] + bv.w) << 16);
+        pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
         *reinterpret_cast<uint2 *>(ob + row * a.ogc) = pk;
+        if (stats) {
+          const float d0 = bf2f(h0) - kv.x, d1 = bf2f(h1) - kv.y, d2 = bf2f(h2) - kv.z, d3 = bf2f(h3) - kv.w;
+          cs[j][0] += d0; cs[j][1] += d1; cs[j][2] += d2; cs[j][3] += d3;
+          cq[j][0] = fmaf(d0, d0, cq[j][0]); cq[j][1] = fmaf(d1, d1, cq[j][1]);
+          cq[j][2] = fmaf(d2, d2, cq[j][2]); cq[j][3] = fmaf(d3, d3, cq[j][3]);
+        }
       }
+    }
+  }
+  if (!stats) return;
+  // BatchNorm partial statistics of this m-tile: the 16 row lanes of each column
+  // (xor tree), then the BM/64 waves that share a column block through LDS, in order
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        cs[j][r] += __shfl_xor(cs[j][r], o, 64);
+        cq[j][r] += __shfl_xor(cq[j][r], o, 64);
+      }
+  __syncthreads();                         // every wave is done reading the staging ring
+  float *red = reinterpret_cast<float *>(smem);   // [BM/64][BN_][2]
+  if (fr == 0)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = wn * WN + j * 16 + fq * 4 + r;
+        red[(wm * BN_ + cl) * 2] = cs[j][r];
+        red[(wm * BN_ + cl) * 2 + 1] = cq[j][r];
+      }
+  __syncthreads();
+  if (tid < BN_) {
+    const int col = n0 + tid;
+    if (col < a.Ncol) {
+      float S = 0.f, Q = 0.f;
+#pragma unroll
+      for (int q = 0; q < BM / 64; ++q) { S += red[(q * BN_ + tid) * 2]; Q += red[(q * BN_ + tid) * 2 + 1]; }
+      const int64_t t = m0 / BM;
+      a.bn_part[t * 2 * a.Ncol + col] = S;
+      a.bn_part[t * 2 * a.Ncol + a.Ncol + col] = Q;
+      if (t == 0 && a.bn_shift_out) a.bn_shift_out[col] = a.bn_shift ? a.bn_shift[col] : 0.f;
     }
   }
 }
@@ -1196,6 +1252,42 @@ extern "C" int ewvit_conv2d_pack_weights(int n, const float *const *w, const int
   a.chunk0[n] = (int)chunks;
   hipLaunchKernelGGL(conv_pack_multi_kernel, dim3((unsigned)chunks), dim3(256), 0, as_stream(stream), a);
   return launch_status("conv2d_pack_weights");
+}
+
+// rows per BatchNorm partial that ewvit_conv2d_fwd_bn leaves for this shape (the
+// LDS-DMA kernel's m-tile), or 0 when the shape takes the register-staged kernel
+static int fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
+  if (!use_glds() || Cin % 64 || Cout % 8 || Cout > 65536) return 0;
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t K = (int64_t)ksize * ksize * Cin;
+  if (2 * N * H * W * Cin >= (int64_t)OOB || Cout * K * 2 >= (int64_t)OOB || N * Ho * Wo * Cout >= (int64_t)1 << 40)
+    return 0;
+  const int v = glds_variant() & 7;
+  return (v == 3 || v == 4) ? 256 : 128;
+}
+
+extern "C" int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                           int stride) {
+  return fwd_bn_rows(N, H, W, Cin, Cout, ksize, stride);
+}
+
+extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                                   int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                                   const float *bn_shift, float *bn_part, float *bn_shift_out, void *stream) {
+  EWVIT_CHECK_ARG(x && wp && y && bn_part && bn_shift_out, "conv2d_fwd_bn: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_fwd_bn")) return rc;
+  EWVIT_CHECK_ARG(fwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) > 0,
+                  "conv2d_fwd_bn: shape takes the register-staged kernel (query ewvit_conv2d_fwd_bn_rows)");
+  FwdArgs a;
+  a.src = (const bf16_t *)x; a.wp = (const bf16_t *)wp; a.bias = bias; a.out = (bf16_t *)y; a.g = g;
+  a.M = (int64_t)g.N * g.Ho * g.Wo; a.Ncol = g.Cout; a.KC = g.Cin;
+  a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
+  a.sgc = (int)Cin; a.sgs = 0; a.ogc = g.Cout; a.ogs = 0;
+  a.bn_shift = bn_shift; a.bn_part = bn_part; a.bn_shift_out = bn_shift_out;
+  EWVIT_CHECK_ARG(launch_glds<false>(a, 2 * N * H * W * Cin, as_stream(stream)),
+                  "conv2d_fwd_bn: LDS-DMA kernel refused the shape");
+  return launch_status("conv2d_fwd_bn");
 }
 
 extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,

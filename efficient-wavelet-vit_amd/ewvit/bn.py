@@ -23,19 +23,30 @@ def _rows(x):
 
 class BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups, counter):
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups, counter,
+                partials=None):
         L.require_gpu(x)
         xc, M, C = _rows(x)
         if M % groups:
             raise ValueError(f'batch_norm_act: {M} rows not divisible into {groups} groups')
         y = torch.empty_like(xc)
-        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=x.device)
         mean = torch.empty(groups, C, dtype=torch.float32, device=x.device) if training else None
         invstd = torch.empty_like(mean) if training else None
-        L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
-               L.ptr(running_mean), L.ptr(running_var), int(training), float(momentum), float(eps), act,
-               L.ptr(mean), L.ptr(invstd), groups, L.ptr(counter if training else None), L.ptr(ws), L.stream(y),
-               work={'bytes': (2 + int(training)) * xc.numel() * xc.element_size()})
+        if partials is not None:
+            # statistics already summed by the producing conv's epilogue: apply pass only
+            part, shifts, nrc = partials
+            if not training or groups != 1:
+                raise ValueError('batch_norm_act: partial statistics need training mode and one group')
+            L.call('ewvit_bn_fwd_partials', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.stream(y),
+                   work={'bytes': 2 * xc.numel() * xc.element_size()})
+        else:
+            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=x.device)
+            L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+                   L.ptr(running_mean), L.ptr(running_var), int(training), float(momentum), float(eps), act,
+                   L.ptr(mean), L.ptr(invstd), groups, L.ptr(counter if training else None), L.ptr(ws),
+                   L.stream(y), work={'bytes': (2 + int(training)) * xc.numel() * xc.element_size()})
         if training:
             ctx.save_for_backward(xc, weight, bias, mean, invstd)
         ctx.cfg = (training, act, M, C, groups)
@@ -56,23 +67,25 @@ class BatchNormActFn(torch.autograd.Function):
         L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), 0, groups, L.ptr(ws), L.stream(dx),
                work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return dx, dg, db, None, None, None, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, None, None, None
 
 
-def batch_norm_act(x, bn, act=None, training=None, groups=1):
+def batch_norm_act(x, bn, act=None, training=None, groups=1, partials=None):
     """Apply BatchNorm module `bn` (its parameters, buffers, eps, momentum) and the
     activation to x in one fused pass; updates bn's running stats and counter
-    (once per statistics group, as `groups` separate module calls would)."""
+    (once per statistics group, as `groups` separate module calls would).
+    `partials` = (part, shifts, nrc) from ewvit.conv.conv2d_bn_stats: the batch
+    statistics were summed by the conv's epilogue (training, one group)."""
     training = bn.training if training is None else training
     if bn.momentum is None:
         raise NotImplementedError('cumulative-average BatchNorm (momentum=None) is not used by the model')
     counter = bn.num_batches_tracked if training and bn.track_running_stats else None
     return batch_norm_act_params(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, training,
-                                 bn.momentum, bn.eps, act, groups, counter)
+                                 bn.momentum, bn.eps, act, groups, counter, partials)
 
 
 def batch_norm_act_params(x, weight, bias, running_mean, running_var, training, momentum, eps, act=None,
-                          groups=1, counter=None):
+                          groups=1, counter=None, partials=None):
     """`counter`: an int64 device tensor (a module's num_batches_tracked) the
     forward kernel increments by `groups` in training, or None."""
     if x.dtype not in (torch.float32, torch.bfloat16):
@@ -82,4 +95,4 @@ def batch_norm_act_params(x, weight, bias, running_mean, running_var, training, 
     if counter is not None and (counter.dtype != torch.int64 or counter.device != x.device):
         raise ValueError('batch_norm_act: counter must be an int64 tensor on the input device')
     return BatchNormActFn.apply(x, weight, bias, running_mean, running_var, bool(training), momentum, eps,
-                                ACT[act], int(groups), counter)
+                                ACT[act], int(groups), counter, partials)

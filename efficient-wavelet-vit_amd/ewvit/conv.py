@@ -118,7 +118,7 @@ def _pack(weight, cin_pad, fwd=True, bwd=False):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, levels):
+    def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
         L.require_gpu(x, weight)
         NL, Cz, H, W = x.shape
         if NL % levels:
@@ -141,8 +141,14 @@ class Conv2dFn(torch.autograd.Function):
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = bias.detach().float().contiguous() if bias is not None else None
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
-        L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc, gs,
-               L.stream(y), work=work)
+        if bn_stats is not None:
+            # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
+            shift, part, shift_out = bn_stats
+            L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
+                   L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
+        else:
+            L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc,
+                   gs, L.stream(y), work=work)
         ctx.save_for_backward(xc, weight, wpt)
         ctx.cfg = (stride, levels, bias is not None, x.dtype)
         # bf16 MFMA product; an fp32 caller (no autocast) gets fp32 back
@@ -183,13 +189,43 @@ class Conv2dFn(torch.autograd.Function):
             if ctx.needs_input_grad[1]:
                 dw = dwf
             db = dbf
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, levels=1):
     """Conv2d(kernel 1|3, padding k//2, stride) — NCHW logical / channels-last bf16 output.
     levels > 1: x is level-major [levels*N, C, H, W], convolved as cat(x.chunk(levels), 1)."""
     return Conv2dFn.apply(x, weight, bias, int(stride), int(levels))
+
+
+def bn_stat_rows(x, weight, stride=1):
+    """Rows per BatchNorm partial that `conv2d_bn_stats` leaves for this conv (the LDS-DMA
+    kernel's m-tile), or 0 when the conv cannot produce them (then use conv2d + BN)."""
+    N, C, H, W = x.shape
+    k = weight.shape[2]
+    if (not x.is_cuda or C != weight.shape[1] or k not in (1, 3) or weight.shape[3] != k
+            or weight.shape[0] % 8):
+        return 0
+    return int(L.load().ewvit_conv2d_fwd_bn_rows(N, H, W, C, weight.shape[0], k, int(stride)))
+
+
+def conv2d_bn_stats(x, weight, bias, stride, shift):
+    """conv2d whose epilogue also leaves the BatchNorm partial statistics of its bf16
+    output: returns (y, part [nrc, 2*Cout], shifts [Cout], nrc) for
+    ewvit.bn.batch_norm_act(..., partials=(part, shifts, nrc)).  `shift` (the BN
+    running mean) centres the sums.  Requires bn_stat_rows(x, weight, stride) > 0."""
+    rows = bn_stat_rows(x, weight, stride)
+    if rows <= 0:
+        raise ValueError('conv2d_bn_stats: shape not supported (check bn_stat_rows)')
+    N, _, H, W = x.shape
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    Cout = weight.shape[0]
+    nrc = (N * Ho * Wo + rows - 1) // rows
+    part = torch.empty(nrc, 2 * Cout, dtype=torch.float32, device=x.device)
+    shifts = torch.empty(Cout, dtype=torch.float32, device=x.device)
+    sh = shift.detach().float().contiguous() if shift is not None else None
+    y = Conv2dFn.apply(x, weight, bias, int(stride), 1, (sh, part, shifts))
+    return y, part, shifts, nrc
 
 
 def conv3x3(x, weight, bias=None, stride=1):

@@ -13,10 +13,17 @@ Stages (expand, kernel, stride, in, out, blocks): FusedMBConv (1,3,1,24,24,2)
 (6,3,2,160,256,15); stem 3x3 s2 3->24, head 1x1 256->1280; BN eps 1e-3; SiLU;
 squeeze-excitation width = block input // 4; stochastic depth 0.2 * i / 40.
 """
+import os
+
 import torch
 from torch import nn
 
 import ewvit
+
+# BatchNorm statistics summed in the producing conv's epilogue when the conv has at
+# most this many 128-row output tiles: every BN apply block re-reads all partial rows
+# while finalising, so the fusion pays only for small maps
+_EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '32'))
 
 STAGES = (
     ('fused', 1, 3, 1, 24, 24, 2),
@@ -69,10 +76,22 @@ class ConvBNAct(nn.Sequential):
         super().__init__(*mods)
 
     def forward(self, x):
-        y = self[0](x)
-        bn = self[1]
+        conv, bn = self[0], self[1]
+        act = 'silu' if len(self) > 2 else None
+        hooks = bn._forward_hooks or bn._forward_pre_hooks or conv._forward_hooks or conv._forward_pre_hooks
+        if (type(conv) is Conv2d and bn.training and bn.track_running_stats and bn.momentum is not None
+                and not hooks and x.is_cuda and conv.groups == 1 and conv.padding[0] == conv.kernel_size[0] // 2
+                and conv.stride[0] == conv.stride[1] and conv.out_channels <= 2048):
+            rows = ewvit.conv.bn_stat_rows(x, conv.weight, conv.stride[0])
+            if rows and (x.shape[0] * ((x.shape[2] - 1) // conv.stride[0] + 1) *
+                         ((x.shape[3] - 1) // conv.stride[0] + 1) + rows - 1) // rows <= _EPI_STATS_MAX_TILES:
+                # the conv's epilogue sums the batch statistics: BN runs its apply pass only
+                y, part, shifts, nrc = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0],
+                                                                  bn.running_mean)
+                return ewvit.batch_norm_act(y, bn, act, partials=(part, shifts, nrc))
+        y = conv(x)
         if y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks):
-            return ewvit.batch_norm_act(y, bn, 'silu' if len(self) > 2 else None)
+            return ewvit.batch_norm_act(y, bn, act)
         y = bn(y)
         return self[2](y) if len(self) > 2 else y
 

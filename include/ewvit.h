@@ -186,6 +186,14 @@ int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_t C, const 
                  const float *beta, float *running_mean, float *running_var, int training,
                  float momentum, float eps, int act, float *save_mean, float *save_invstd,
                  int groups, int64_t *num_batches_tracked, float *workspace, void *stream);
+/* Training forward from precomputed partial statistics: part [nrc][2C] rows of
+ * (sum (x-K), sum (x-K)^2) and shifts K [C] — what ewvit_conv2d_fwd_bn leaves in
+ * its epilogue — so only the apply pass runs (one group). */
+int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
+                          const float *beta, float *running_mean, float *running_var, float momentum,
+                          float eps, int act, float *save_mean, float *save_invstd,
+                          int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
+                          void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -228,6 +236,16 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
  * Returns the previous setting. */
 int ewvit_conv2d_set_glds(int variant);
 /* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
+/* ewvit_conv2d_fwd (plain NHWC x, Cin % 64 == 0) that also leaves the BatchNorm
+ * statistics of its bf16 output for ewvit_bn_fwd_partials: per tile of R output rows
+ * (R = ewvit_conv2d_fwd_bn_rows(...), 0 when the shape is not supported) bn_part[t]
+ * gets (sum (y - K), sum (y - K)^2) over its rows per channel, K = bn_shift[c] (a
+ * running-mean estimate; NULL: 0), and bn_shift_out receives K. */
+int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                 int stride);
+int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                        int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, const float *bn_shift,
+                        float *bn_part, float *bn_shift_out, void *stream);
 int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                      int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
                      int64_t x_group_stride, void *stream);

@@ -96,3 +96,36 @@ def test_bn_stats_stable_with_large_mean():
     y = ewvit.batch_norm_act_params(x.to(DEV).to(memory_format=torch.channels_last), None, None, rmd, rvd, True,
                                     0.1, 1e-3, None)
     assert rel(y, yr) < 5e-3
+
+
+@pytest.mark.parametrize('cin,cout,k,stride,hw', [(256, 512, 1, 1, 7), (64, 256, 1, 1, 14), (128, 160, 3, 2, 13),
+                                                 (64, 64, 3, 1, 9)])
+def test_conv_bn_stats_in_epilogue(cin, cout, k, stride, hw):
+    """ConvBNAct training forward with the BatchNorm batch statistics summed in the
+    conv's epilogue (ewvit_conv2d_fwd_bn + ewvit_bn_fwd_partials) matches the unfused
+    conv -> BN(+SiLU) path: output, running stats, counter, and all gradients."""
+    import ewvit
+    from network.efficientnet import ConvBNAct
+    torch.manual_seed(cin + cout + k)
+    m1 = ConvBNAct(cin, cout, k, stride).to(DEV)
+    m2 = ConvBNAct(cin, cout, k, stride).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    with torch.no_grad():
+        for m in (m1, m2):
+            m[1].running_mean.copy_(torch.linspace(-0.5, 0.5, cout))   # shift used by the fused sums
+    x = (torch.randn(6, cin, hw, hw) * 1.5 + 0.3).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+    assert ewvit.conv.bn_stat_rows(x, m1[0].weight, stride) > 0
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    y1 = m1(x1)                                   # fused statistics path
+    y2 = ewvit.batch_norm_act(m2[0](x2), m2[1], 'silu')   # conv, then the full BN
+    dy = torch.randn(y1.shape, device=DEV).to(torch.bfloat16)
+    y1.backward(dy)
+    y2.backward(dy)
+    assert rel(y1.float(), y2.float()) < 2 ** -7
+    assert rel(m1[1].running_mean, m2[1].running_mean) < 1e-4
+    assert rel(m1[1].running_var, m2[1].running_var) < 1e-4
+    assert int(m1[1].num_batches_tracked) == int(m2[1].num_batches_tracked) == 1
+    assert rel(x1.grad.float(), x2.grad.float()) < 2e-2
+    assert rel(m1[0].weight.grad, m2[0].weight.grad) < 1e-2
+    assert rel(m1[1].weight.grad, m2[1].weight.grad) < 1e-2
+    assert rel(m1[1].bias.grad, m2[1].bias.grad) < 1e-2
