@@ -541,26 +541,64 @@ extern "C" int ewvit_bn_fwd(const void *x, void *y, int dtype, int64_t M, int64_
   return launch_status("bn_fwd");
 }
 
-// training forward from precomputed partial statistics (nrc rows of shifted sums +
-// the shift, e.g. left by ewvit_conv2d_fwd_bn in the producing conv's epilogue):
-// the apply pass only (it finalises from the partial rows), one group
+// sum consecutive chunks of a group's partial rows: out[g][k][:] = sum of in[g][k*ch ..
+// k*ch + ch - 1][:] (fixed order), and the shift [C] replicated per group
+__global__ __launch_bounds__(256) void bn_fold_kernel(const float *__restrict__ in, int nin, const float *shift_in,
+                                                      float *__restrict__ out, int nout, float *__restrict__ shift_out,
+                                                      int C) {
+  const int c2 = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y, g = blockIdx.z;
+  if (c2 >= 2 * C) return;
+  const int ch = (nin + nout - 1) / nout;
+  const int r0 = k * ch, r1 = r0 + ch < nin ? r0 + ch : nin;
+  const float *p = in + ((int64_t)g * nin) * 2 * C + c2;
+  float acc = 0.f;
+  int r = r0;
+  for (; r + 7 < r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(r + u) * 2 * C];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; r < r1; ++r) acc += p[(int64_t)r * 2 * C];
+  out[((int64_t)g * nout + k) * 2 * C + c2] = acc;
+  if (k == 0 && c2 < C) shift_out[g * C + c2] = shift_in[c2];
+}
+
+extern "C" int ewvit_bn_fold_partials(const float *part_in, int nin, const float *shift_in, float *part_out,
+                                      int nout, float *shift_out, int64_t C, int groups, void *stream) {
+  EWVIT_CHECK_ARG(part_in && shift_in && part_out && shift_out && nin >= 1 && nout >= 1 && groups >= 1 &&
+                      C > 0 && C <= 4096 && groups <= 65535 && nout <= 65535,
+                  "bn_fold_partials: bad args");
+  dim3 grid((unsigned)((2 * C + 255) / 256), (unsigned)nout, (unsigned)groups);
+  hipLaunchKernelGGL(bn_fold_kernel, grid, dim3(256), 0, as_stream(stream), part_in, nin, shift_in, part_out, nout,
+                     shift_out, (int)C);
+  return launch_status("bn_fold_partials");
+}
+
+// training forward from precomputed partial statistics (per group nrc rows of shifted
+// sums [groups][nrc][2C] + the shifts [groups][C], e.g. left by ewvit_conv2d_fwd_bn in
+// the producing conv's epilogue): the apply pass only (it finalises from the rows)
 extern "C" int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
                                      const float *beta, float *running_mean, float *running_var, float momentum,
                                      float eps, int act, float *save_mean, float *save_invstd,
                                      int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
-                                     void *stream) {
+                                     int groups, void *stream) {
   EWVIT_CHECK_ARG(x && y && part && shifts && dtype_ok(dtype), "bn_fwd_partials: bad args");
   EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_fwd_partials: C=%lld must be a multiple of 8, <= 4096",
                   (long long)C);
   EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_fwd_partials: act=%d", act);
   EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 4096, "bn_fwd_partials: %d partial rows", nrc);
+  EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M % groups == 0, "bn_fwd_partials: M=%lld, %d groups",
+                  (long long)M, groups);
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const BnGeo geo = bn_geo(C);
-  const int64_t rpb = bn_rows_per_block(geo, M, 1);
-  dim3 agrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+  const int64_t Mg = M / groups;
+  const int64_t rpb = bn_rows_per_block(geo, Mg, groups);
+  dim3 agrid((unsigned)((Mg + rpb - 1) / rpb), geo.nch, groups);
 #define BN_APPLY(DTV, ACTV)                                                                                          \
-  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc, M,      \
+  hipLaunchKernelGGL((bn_apply_kernel<DTV, ACTV>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc, Mg,     \
                      (int)C, geo.CC8, geo.RG, rpb, 1, gamma, beta, running_mean, running_var, momentum, eps,        \
                      save_mean, save_invstd, num_batches_tracked)
   BN_DISPATCH(BN_APPLY);

@@ -1272,21 +1272,23 @@ extern "C" int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int
 }
 
 extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
-                                   int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
-                                   const float *bn_shift, float *bn_part, float *bn_shift_out, void *stream) {
+                                   int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
+                                   int64_t x_group_stride, const float *bn_shift, float *bn_part,
+                                   float *bn_shift_out, void *stream) {
   EWVIT_CHECK_ARG(x && wp && y && bn_part && bn_shift_out, "conv2d_fwd_bn: null pointer");
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
   if (int rc = check_geom(g, "conv2d_fwd_bn")) return rc;
-  EWVIT_CHECK_ARG(fwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) > 0,
+  if (int rc = check_group(x_group_c, x_group_stride, Cin, N * H * W, "conv2d_fwd_bn", "x")) return rc;
+  EWVIT_CHECK_ARG(fwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) > 0 && x_group_c % 64 == 0,
                   "conv2d_fwd_bn: shape takes the register-staged kernel (query ewvit_conv2d_fwd_bn_rows)");
   FwdArgs a;
   a.src = (const bf16_t *)x; a.wp = (const bf16_t *)wp; a.bias = bias; a.out = (bf16_t *)y; a.g = g;
   a.M = (int64_t)g.N * g.Ho * g.Wo; a.Ncol = g.Cout; a.KC = g.Cin;
   a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
-  a.sgc = (int)Cin; a.sgs = 0; a.ogc = g.Cout; a.ogs = 0;
+  a.sgc = (int)x_group_c; a.sgs = x_group_stride; a.ogc = g.Cout; a.ogs = 0;
   a.bn_shift = bn_shift; a.bn_part = bn_part; a.bn_shift_out = bn_shift_out;
-  EWVIT_CHECK_ARG(launch_glds<false>(a, 2 * N * H * W * Cin, as_stream(stream)),
-                  "conv2d_fwd_bn: LDS-DMA kernel refused the shape");
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd_bn: LDS-DMA kernel refused the shape");
   return launch_status("conv2d_fwd_bn");
 }
 

@@ -35,11 +35,11 @@ class BatchNormActFn(torch.autograd.Function):
         if partials is not None:
             # statistics already summed by the producing conv's epilogue: apply pass only
             part, shifts, nrc = partials
-            if not training or groups != 1:
-                raise ValueError('batch_norm_act: partial statistics need training mode and one group')
+            if not training:
+                raise ValueError('batch_norm_act: partial statistics need training mode')
             L.call('ewvit_bn_fwd_partials', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                    L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
-                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.stream(y),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), groups, L.stream(y),
                    work={'bytes': 2 * xc.numel() * xc.element_size()})
         else:
             ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=x.device)
@@ -75,7 +75,7 @@ def batch_norm_act(x, bn, act=None, training=None, groups=1, partials=None):
     activation to x in one fused pass; updates bn's running stats and counter
     (once per statistics group, as `groups` separate module calls would).
     `partials` = (part, shifts, nrc) from ewvit.conv.conv2d_bn_stats: the batch
-    statistics were summed by the conv's epilogue (training, one group)."""
+    statistics were summed by the conv's epilogue (training)."""
     training = bn.training if training is None else training
     if bn.momentum is None:
         raise NotImplementedError('cumulative-average BatchNorm (momentum=None) is not used by the model')

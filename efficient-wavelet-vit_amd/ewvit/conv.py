@@ -145,7 +145,7 @@ class Conv2dFn(torch.autograd.Function):
             # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
             shift, part, shift_out = bn_stats
             L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
-                   L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
+                   gc, gs, L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
         else:
             L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc,
                    gs, L.stream(y), work=work)
@@ -198,33 +198,47 @@ def conv2d(x, weight, bias=None, stride=1, levels=1):
     return Conv2dFn.apply(x, weight, bias, int(stride), int(levels))
 
 
-def bn_stat_rows(x, weight, stride=1):
+def bn_stat_rows(x, weight, stride=1, levels=1):
     """Rows per BatchNorm partial that `conv2d_bn_stats` leaves for this conv (the LDS-DMA
     kernel's m-tile), or 0 when the conv cannot produce them (then use conv2d + BN)."""
-    N, C, H, W = x.shape
+    NL, Cz, H, W = x.shape
     k = weight.shape[2]
-    if (not x.is_cuda or C != weight.shape[1] or k not in (1, 3) or weight.shape[3] != k
-            or weight.shape[0] % 8):
+    Cx = Cz * levels
+    if (not x.is_cuda or Cx < weight.shape[1] or (levels > 1 and Cx != weight.shape[1]) or k not in (1, 3)
+            or weight.shape[3] != k or weight.shape[0] % 8 or NL % levels or (levels > 1 and Cz % 64)):
         return 0
-    return int(L.load().ewvit_conv2d_fwd_bn_rows(N, H, W, C, weight.shape[0], k, int(stride)))
+    return int(L.load().ewvit_conv2d_fwd_bn_rows(NL // levels, H, W, Cz * levels, weight.shape[0], k, int(stride)))
 
 
-def conv2d_bn_stats(x, weight, bias, stride, shift):
+def conv2d_bn_stats(x, weight, bias, stride, shift, levels=1, groups=1, max_rows=256):
     """conv2d whose epilogue also leaves the BatchNorm partial statistics of its bf16
-    output: returns (y, part [nrc, 2*Cout], shifts [Cout], nrc) for
-    ewvit.bn.batch_norm_act(..., partials=(part, shifts, nrc)).  `shift` (the BN
-    running mean) centres the sums.  Requires bn_stat_rows(x, weight, stride) > 0."""
-    rows = bn_stat_rows(x, weight, stride)
+    output: returns (y, part [groups, nrc, 2*Cout], shifts [groups, Cout], nrc) for
+    ewvit.bn.batch_norm_act(..., partials=(part, shifts, nrc)), or None when the shape
+    is not supported.  `shift` (the BN running mean) centres the sums; `groups` equal
+    batch slices get separate statistics (each must be whole output tiles); more than
+    `max_rows` tile rows per group are folded by one extra launch."""
+    rows = bn_stat_rows(x, weight, stride, levels)
     if rows <= 0:
-        raise ValueError('conv2d_bn_stats: shape not supported (check bn_stat_rows)')
-    N, _, H, W = x.shape
+        return None
+    NL, _, H, W = x.shape
+    N = NL // levels
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    M = N * Ho * Wo
+    if M % groups or (groups > 1 and (M // groups) % rows):
+        return None
     Cout = weight.shape[0]
-    nrc = (N * Ho * Wo + rows - 1) // rows
-    part = torch.empty(nrc, 2 * Cout, dtype=torch.float32, device=x.device)
+    nrc = (M // groups + rows - 1) // rows
+    part = torch.empty(groups * nrc, 2 * Cout, dtype=torch.float32, device=x.device)
     shifts = torch.empty(Cout, dtype=torch.float32, device=x.device)
     sh = shift.detach().float().contiguous() if shift is not None else None
-    y = Conv2dFn.apply(x, weight, bias, int(stride), 1, (sh, part, shifts))
+    y = Conv2dFn.apply(x, weight, bias, int(stride), int(levels), (sh, part, shifts))
+    if nrc > max_rows or groups > 1:
+        nout = min(nrc, max_rows)
+        part2 = torch.empty(groups, nout, 2 * Cout, dtype=torch.float32, device=x.device)
+        shifts2 = torch.empty(groups, Cout, dtype=torch.float32, device=x.device)
+        L.call('ewvit_bn_fold_partials', L.ptr(part), nrc, L.ptr(shifts), L.ptr(part2), nout, L.ptr(shifts2), Cout,
+               groups, L.stream(y))
+        part, shifts, nrc = part2, shifts2, nout
     return y, part, shifts, nrc
 
 

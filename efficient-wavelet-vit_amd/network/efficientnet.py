@@ -86,9 +86,10 @@ class ConvBNAct(nn.Sequential):
             if rows and (x.shape[0] * ((x.shape[2] - 1) // conv.stride[0] + 1) *
                          ((x.shape[3] - 1) // conv.stride[0] + 1) + rows - 1) // rows <= _EPI_STATS_MAX_TILES:
                 # the conv's epilogue sums the batch statistics: BN runs its apply pass only
-                y, part, shifts, nrc = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0],
-                                                                  bn.running_mean)
-                return ewvit.batch_norm_act(y, bn, act, partials=(part, shifts, nrc))
+                r = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0], bn.running_mean)
+                if r is not None:
+                    y, part, shifts, nrc = r
+                    return ewvit.batch_norm_act(y, bn, act, partials=(part, shifts, nrc))
         y = conv(x)
         if y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks):
             return ewvit.batch_norm_act(y, bn, act)

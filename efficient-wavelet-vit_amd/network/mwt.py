@@ -72,11 +72,26 @@ def _fusable(bn, y):
     return y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks)
 
 
+def _epi_stats(conv, bn, x, levels=1, groups=1):
+    """Conv with the BatchNorm batch statistics summed in its epilogue ->
+    (y, partials) for ewvit.batch_norm_act, or None (the plain conv + BN path)."""
+    if (type(conv) is not Conv3x3 or not bn.training or not bn.track_running_stats or bn.momentum is None
+            or conv._forward_hooks or conv._forward_pre_hooks or bn._forward_hooks or bn._forward_pre_hooks
+            or not x.is_cuda or bn.num_features > 2048):
+        return None
+    r = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0], bn.running_mean, levels, groups)
+    return None if r is None else (r[0], r[1:])
+
+
 class CBR(nn.Sequential):
-    """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass.
+    """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass, its batch
+    statistics summed in the conv's epilogue where the conv kernel allows.
     ``levels``: see Conv3x3.forward."""
 
     def forward(self, x, levels=1):
+        r = _epi_stats(self[0], self[1], x, levels)
+        if r is not None:
+            return ewvit.batch_norm_act(r[0], self[1], 'relu', partials=r[1])
         y = self[0](x, levels) if levels > 1 else self[0](x)
         if _fusable(self[1], y):
             return ewvit.batch_norm_act(y, self[1], 'relu')
@@ -87,7 +102,11 @@ class FreqPool(nn.Sequential):
     """MaxPool2d(2) -> Conv3x3 s2 -> BatchNorm2d -> ReLU -> AdaptiveAvgPool2d(1) (mwt.py:38-44)."""
 
     def forward(self, x):
-        y = self[1](self[0](x))
+        p = self[0](x)
+        r = _epi_stats(self[1], self[2], p)
+        if r is not None:
+            return self[4](ewvit.batch_norm_act(r[0], self[2], 'relu', partials=r[1]))
+        y = self[1](p)
         y = ewvit.batch_norm_act(y, self[2], 'relu') if _fusable(self[2], y) else self[3](self[2](y))
         return self[4](y)
 
@@ -216,6 +235,9 @@ class MWT(nn.Module):
         # BN + ReLU of all levels in one fused launch, per-level statistics
         y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv)
         fus = self.hf_conv['fusion']
+        r = _epi_stats(fus[0], fus[1], y, groups=Lv)
+        if r is not None:
+            return ewvit.batch_norm_act(r[0], fus[1], 'relu', groups=Lv, partials=r[1])
         z = fus[0](y)
         z = ewvit.batch_norm_act(z, fus[1], 'relu', groups=Lv) if _fusable(fus[1], z) else \
             torch.cat([fus[2](fus[1](z[l * B:(l + 1) * B])) for l in range(Lv)])

@@ -193,7 +193,12 @@ int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t 
                           const float *beta, float *running_mean, float *running_var, float momentum,
                           float eps, int act, float *save_mean, float *save_invstd,
                           int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
-                          void *stream);
+                          int groups, void *stream);
+/* part_out[g][k] = sum of part_in[g][k*ch .. k*ch + ch - 1] (ch = ceil(nin / nout); rows
+ * of 2C floats, fixed order) and shift_out[g][:] = shift_in[:]: brings a large conv's
+ * per-tile partial rows down to what the apply pass finalises from. */
+int ewvit_bn_fold_partials(const float *part_in, int nin, const float *shift_in, float *part_out, int nout,
+                           float *shift_out, int64_t C, int groups, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -237,15 +242,17 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
 int ewvit_conv2d_set_glds(int variant);
 /* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
 /* ewvit_conv2d_fwd (plain NHWC x, Cin % 64 == 0) that also leaves the BatchNorm
- * statistics of its bf16 output for ewvit_bn_fwd_partials: per tile of R output rows
+ * statistics of its bf16 output for ewvit_bn_fwd_partials (grouped x as in ewvit_conv2d_fwd,
+ * group width a multiple of 64): per tile of R output rows
  * (R = ewvit_conv2d_fwd_bn_rows(...), 0 when the shape is not supported) bn_part[t]
  * gets (sum (y - K), sum (y - K)^2) over its rows per channel, K = bn_shift[c] (a
  * running-mean estimate; NULL: 0), and bn_shift_out receives K. */
 int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                                  int stride);
 int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
-                        int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, const float *bn_shift,
-                        float *bn_part, float *bn_shift_out, void *stream);
+                        int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
+                        int64_t x_group_stride, const float *bn_shift, float *bn_part, float *bn_shift_out,
+                        void *stream);
 int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                      int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
                      int64_t x_group_stride, void *stream);

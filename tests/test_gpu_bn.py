@@ -129,3 +129,43 @@ def test_conv_bn_stats_in_epilogue(cin, cout, k, stride, hw):
     assert rel(m1[0].weight.grad, m2[0].weight.grad) < 1e-2
     assert rel(m1[1].weight.grad, m2[1].weight.grad) < 1e-2
     assert rel(m1[1].bias.grad, m2[1].bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize('hw', [64, 40])
+def test_mwt_epilogue_stats_match_plain(hw, monkeypatch):
+    """MWT forward/backward with the BN statistics of its convs summed in the conv
+    epilogues (per-level groups for the fusion conv, folded partial rows) equals the
+    plain conv -> BN path: outputs, running stats and parameter gradients."""
+    import network.mwt as mw
+    torch.manual_seed(3)
+    m1 = mw.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last)
+    m2 = mw.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last)
+    m2.load_state_dict(m1.state_dict())
+    x = torch.randn(2, 3, hw, hw, device=DEV)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y1 = m1(x)
+    calls = []
+    real = mw._epi_stats
+    monkeypatch.setattr(mw, '_epi_stats', lambda *a, **k: calls.append(1))
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y2 = m2(x)
+    monkeypatch.setattr(mw, '_epi_stats', real)
+    assert len(calls) >= 3
+    g = torch.randn(y1.shape, device=DEV)
+    y1.float().mul(g).sum().backward()
+    y2.float().mul(g).sum().backward()
+    assert rel(y1.float(), y2.float()) < 2e-2
+    for (n, b1), b2 in zip(m1.named_buffers(), m2.buffers()):
+        if b1.dtype.is_floating_point:
+            assert rel(b1, b2) < 1e-3, n
+        else:
+            assert torch.equal(b1, b2), n
+    # gradients pass the freq_pool max-pool, whose bf16 near-ties may route a pixel's
+    # gradient differently once the statistics' summation order changes: compare by
+    # direction, not elementwise
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        # a conv bias in front of a BatchNorm has an exactly-zero true gradient: its
+        # computed value is rounding noise, not compared
+        if p1.grad is not None and not (n.endswith('0.bias') or n.endswith('1.bias') and 'freq_pool' in n):
+            cos = torch.nn.functional.cosine_similarity(p1.grad.flatten().double(), p2.grad.flatten().double(), 0)
+            assert float(cos) > 0.995, (n, float(cos))
