@@ -67,6 +67,10 @@ struct FwdArgs {
   const float *bn_shift = nullptr;
   float *bn_part = nullptr;
   float *bn_shift_out = nullptr;
+  // LDS-DMA fwd over a plain NHWC x whose channel count is not a multiple of 64: KC is
+  // the per-tap K padded up to 64 (the weights packed with that many input channels)
+  // and the staging lanes of channels >= KCr (the real count) read zeros
+  int KCr = 0;
 };
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
@@ -681,8 +685,9 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // rows (fwd: +(kh*W + kw); dgrad: -(kh*W + kw), or -((kh/2)*W + kw/2) at stride 2),
   // so a row keeps one byte offset and a mask of the taps that land inside the image
   // (and, for stride-2 dgrad, on the stride lattice); a K-tile adds one scalar.
-  int rb[PA];
+  int rb[PA], lc8[PA];
   unsigned vmask[PA];
+  const int kcr = a.KCr ? a.KCr : a.KC;
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int p = ws * PA + j, r = p * 8 + (lane >> 3);
@@ -716,6 +721,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     const int64_t pix = (int64_t)n * a.srcH * a.srcW + (int64_t)by * a.srcW + bx;
     rb[j] = (int)((pix * a.sgc + lc * 8) * 2);
     vmask[j] = msk;
+    lc8[j] = lc * 8;
   }
   uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
 #pragma unroll
@@ -736,7 +742,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     if (!DGRAD) dpix = kh * a.srcW + kw;
     else dpix = -((kh >> ls) * a.srcW + (kw >> ls));
     const int sdelta = (int)(((int64_t)dpix * a.sgc + (int64_t)lgi * a.sgs + lcin) * 2);
-    const int tap = ltap;
+    const int tap = ltap, c0 = lcin;
     const uint32_t kb = (uint32_t)((ltap * a.KC + lcb * BK) * 2);
     if (tap_inner) {
       if (++ltap == KS * KS) {
@@ -752,7 +758,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     unsigned char *base = smem + buf * STG + ws * PA * 1024;
 #pragma unroll
     for (int j = 0; j < PA; ++j)
-      glds16(rs, base + j * 1024, (vmask[j] >> tap) & 1u ? (uint32_t)(rb[j] + sdelta) : OOB);
+      glds16(rs, base + j * 1024,
+             ((vmask[j] >> tap) & 1u) && c0 + lc8[j] < kcr ? (uint32_t)(rb[j] + sdelta) : OOB);
     unsigned char *bb = smem + buf * STG + A_B + ws * PB * 1024;
 #pragma unroll
     for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
@@ -1126,7 +1133,9 @@ static void launch_fwd(const FwdArgs &a, hipStream_t s) {
 template <bool DGRAD>
 static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
-  if (!use_glds() || a.KC % 64 || a.sgc % 64 || src_bytes >= (int64_t)OOB || a.Ncol * K * 2 >= (int64_t)OOB ||
+  const bool padded = a.KCr && a.KCr != a.KC;     // plain x, channels padded to 64 per tap
+  if (!use_glds() || a.KC % 64 || (padded ? a.sgc != a.KCr : a.sgc % 64) || src_bytes >= (int64_t)OOB ||
+      a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
   const int v = glds_variant() & 7;
@@ -1292,6 +1301,28 @@ extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *b
   return launch_status("conv2d_fwd_bn");
 }
 
+// input channels per tap the fwd expects its weight pack to have: Cin rounded up to 64
+// when Cin % 64 != 0 (Cin % 16 == 0) and the padded LDS-DMA kernel takes the shape
+static int64_t fwd_pack_cin(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
+  static const int on = [] {
+    const char *e = getenv("EWVIT_CONV_PAD_K");     // 0: never pad (A/B measurement)
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || Cin % 64 == 0 || Cin % 16 || !use_glds()) return Cin;
+  const int64_t Cp = (Cin + 63) / 64 * 64;
+  if (4 * Cp > 5 * Cin) return Cin;      // > 25 % zero K (48 -> 64 measured slower): exact-K kernel
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  if (2 * N * H * W * Cin >= (int64_t)OOB || Cout * ksize * ksize * Cp * 2 >= (int64_t)OOB ||
+      N * Ho * Wo * Cout >= (int64_t)1 << 40)
+    return Cin;
+  return Cp;
+}
+
+extern "C" int64_t ewvit_conv2d_fwd_pack_cin(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                            int stride) {
+  return fwd_pack_cin(N, H, W, Cin, Cout, ksize, stride);
+}
+
 extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                                 int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
                                 int64_t x_group_stride, void *stream) {
@@ -1305,7 +1336,14 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
   a.srcH = g.H; a.srcW = g.W; a.outH = g.Ho; a.outW = g.Wo;
   a.sgc = (int)x_group_c; a.sgs = x_group_stride; a.ogc = g.Cout; a.ogs = 0;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
-  if (!launch_glds<false>(a, xb, as_stream(stream))) launch_fwd<false>(a, as_stream(stream));
+  const int64_t cp = x_group_stride ? Cin : fwd_pack_cin(N, H, W, Cin, Cout, ksize, stride);
+  if (cp != Cin) {
+    // the weights were packed with cp input channels (ewvit_conv2d_fwd_pack_cin)
+    a.KC = (int)cp; a.KCr = (int)Cin;
+    EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd: padded LDS-DMA kernel refused");
+  } else if (!launch_glds<false>(a, xb, as_stream(stream))) {
+    launch_fwd<false>(a, as_stream(stream));
+  }
   return launch_status("conv2d_fwd");
 }
 

@@ -67,6 +67,7 @@ QUERIES = {
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_conv2d_fwd_pack_cin': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
     'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),

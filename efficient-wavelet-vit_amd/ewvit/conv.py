@@ -130,11 +130,14 @@ class Conv2dFn(torch.autograd.Function):
         xc = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         gc, gs = (Cz, N * H * W * Cz) if levels > 1 else (0, 0)
         bwd = ctx.needs_input_grad[0]
-        cached = _cached_pack(weight, Cx, bwd) if weight.dtype == torch.float32 else None
+        # per-tap input channels of the fwd pack: Cx, or Cx padded to 64 when the LDS-DMA
+        # kernel runs a non-multiple-of-64 input with zero lanes (wpt shares the rows)
+        cp = Cx if levels > 1 else int(L.load().ewvit_conv2d_fwd_pack_cin(N, H, W, Cx, Cout, k, stride))
+        cached = _cached_pack(weight, cp, bwd) if weight.dtype == torch.float32 else None
         if cached is None:
-            wp, wpt = _pack(weight, Cx, True, bwd)
+            wp, wpt = _pack(weight, cp, True, bwd)
             if weight.dtype == torch.float32:
-                _register(weight, Cx, bwd)
+                _register(weight, cp, bwd)
         else:
             wp, wpt = cached
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1

@@ -240,7 +240,14 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
  * LDS-DMA tile / ring-depth configuration where the shape allows (csrc/conv.hip).
  * Returns the previous setting. */
 int ewvit_conv2d_set_glds(int variant);
-/* y = conv(x, W) + bias (bias f32 [Cout] or NULL). */
+/* Input channels per tap the forward expects its packed weights to have (the Cin_pad
+ * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
+ * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs
+ * the shape with zero lanes for the missing channels. */
+int64_t ewvit_conv2d_fwd_pack_cin(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                  int stride);
+/* y = conv(x, W) + bias (bias f32 [Cout] or NULL); wp packed with
+ * ewvit_conv2d_fwd_pack_cin(...) input channels (grouped x: Cin). */
 /* ewvit_conv2d_fwd (plain NHWC x, Cin % 64 == 0) that also leaves the BatchNorm
  * statistics of its bf16 output for ewvit_bn_fwd_partials (grouped x as in ewvit_conv2d_fwd,
  * group width a multiple of 64): per tile of R output rows

@@ -47,6 +47,8 @@ def rel(a, b):
     (4, 1536, 1536, 256, 7, 7, 1, 1),    # 1x1 project: long K, few tiles
     (3, 256, 256, 1536, 7, 7, 1, 1),     # 1x1 expand: long-K dgrad
     (2, 192, 192, 160, 9, 9, 1, 3),      # 3x3, few tiles, 27 K-tiles
+    (2, 160, 160, 64, 9, 9, 1, 1),       # Cin 160: LDS-DMA fwd with K padded to 192 per tap
+    (2, 160, 160, 48, 11, 10, 2, 3),     # the same, 3x3 stride 2
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec

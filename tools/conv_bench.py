@@ -82,7 +82,8 @@ def main():
         z = torch.randn(N * lv, Cin, H, W, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
         w = torch.randn(Cout, Cx, k, k, device=dev) / (k * k * Cx) ** 0.5
         gc, gs = (Cin, N * H * W * Cin) if lv > 1 else (0, 0)
-        wp, wpt = _pack(w, Cx, True, True)
+        cp = Cx if lv > 1 else int(lib.ewvit_conv2d_fwd_pack_cin(N, H, W, Cx, Cout, k, s))
+        wp, wpt = _pack(w, cp, True, True)
         Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
         dy = torch.randn_like(y)
