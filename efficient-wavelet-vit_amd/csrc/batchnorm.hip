@@ -176,6 +176,19 @@ __device__ __forceinline__ void row_walk(int64_t r0, int64_t r1, int rg, int R, 
 }
 
 template <int DT> struct Raw8x2 { Raw8<DT> x, d; };
+template <int DT> struct Raw8x2s { Raw8<DT> x, d; float s; };
+
+// StochasticDepth(row) + skip add fused into the apply pass (MBConv block tail):
+// y = bn(x) * scale[n] + skip with scale[n] = (u(n) < keep) / keep, n = row / HW, u the
+// counter hash of ewvit dropout (common.h); scale_out[n] keeps the factors for backward
+struct BnDrop {
+  const void *skip = nullptr;
+  float keep = 1.f;
+  uint64_t seed = 0;
+  const int64_t *seed_offset = nullptr;
+  float *scale_out = nullptr;
+  int HW = 0;
+};
 
 
 
@@ -277,7 +290,7 @@ __device__ __forceinline__ void bn_chunk_sums(const float *__restrict__ part, in
 // batch statistics from the partial rows; blocks of row range 0 of group 0 update
 // the running statistics group after group (the reference calls the module once per
 // group) and save mean / invstd.  Eval: coefficients from the running statistics.
-template <int DT, int ACT>
+template <int DT, int ACT, bool DROP = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ x, void *__restrict__ y,
                                                        const float *__restrict__ part,
                                                        const float *__restrict__ shifts, int nrc, int64_t Mg, int C,
@@ -285,7 +298,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
                                                        const float *__restrict__ gamma,
                                                        const float *__restrict__ beta, float *running_mean,
                                                        float *running_var, float momentum, float eps, float *save_mean,
-                                                       float *save_invstd, int64_t *counter) {
+                                                       float *save_invstd, int64_t *counter, BnDrop dr = BnDrop()) {
   __shared__ float red[512];
   __shared__ float coef[2][64];
   const int grp = blockIdx.z, groups = gridDim.z;
@@ -350,24 +363,42 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sc[j] = coef[0][cl * 8 + j]; sh[j] = coef[1][cl * 8 + j]; }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  row_walk<8>(r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
-              [&](int64_t rr, const Raw8<DT> &raw) {
+  auto apply_row = [&](int64_t rr, const Raw8<DT> &raw) {
     float v[8];
     unpack<DT>(raw, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
     st8<DT>(y, goff + rr * C + c, v);
-  });
+  };
+  if constexpr (!DROP) {
+    row_walk<8>(r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); }, apply_row);
+  } else {
+    const uint64_t sd = step_seed(dr.seed, dr.seed_offset);
+    row_walk<8>(r0, r1, rg, RG,
+                [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c), ldraw<DT>(dr.skip, rr * C + c)}; },
+                [&](int64_t rr, const Raw8x2<DT> &raw) {
+      const int n = (int)rr / dr.HW;
+      const float ks = uniform01(sd, (uint64_t)n) < dr.keep ? 1.f / dr.keep : 0.f;
+      if (dr.scale_out && (int)rr == n * dr.HW && c8 == 0) dr.scale_out[n] = ks;
+      float v[8], vs[8];
+      unpack<DT>(raw.x, v);
+      unpack<DT>(raw.d, vs);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(act_fwd<ACT>(fmaf(v[j], sc[j], sh[j])), ks, vs[j]);
+      st8<DT>(y, rr * C + c, v);
+    });
+  }
 }
 
 // ---- backward pass 1: partial sums of g and g*xhat, g = dy * act'(z)
-template <int DT, int ACT>
+template <int DT, int ACT, bool SC = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                             const float *__restrict__ mean,
                                                             const float *__restrict__ invstd,
                                                             const float *__restrict__ gamma,
                                                             const float *__restrict__ beta, int64_t M, int C, int CC8,
-                                                            int RG, int64_t rpc, float *__restrict__ part) {
+                                                            int RG, int64_t rpc, float *__restrict__ part,
+                                                            const float *__restrict__ rscale = nullptr, int HW = 1) {
   __shared__ float sm[256 * 16];
   const int grp = blockIdx.z, nrc = gridDim.x;
   {
@@ -392,13 +423,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
   }
   if (active) {
     row_walk<8>(r0, r1, rg, RG,
-                [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8)}; },
-                [&](int64_t, const Raw8x2<DT> &raw) {
+                [&](int64_t rr) {
+                  return Raw8x2s<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8),
+                                     SC ? rscale[(int)rr / HW] : 1.f};
+                },
+                [&](int64_t, const Raw8x2s<DT> &raw) {
       float vx[8], vd[8];
       unpack<DT>(raw.x, vx);
       unpack<DT>(raw.d, vd);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        if (SC) vd[j] *= raw.s;
         const float xh = (vx[j] - mu[j]) * iv[j];
         const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
         sg[j] += g;
@@ -412,7 +447,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
 // dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); the block finalises its chunk's
 // two means from the partial rows; blocks of row range 0 of group 0 write
 // dgamma = sum g*xhat, dbeta = sum g (over all groups: the parameters are shared)
-template <int DT, int ACT>
+template <int DT, int ACT, bool SC = false>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                         const float *__restrict__ mean,
                                                         const float *__restrict__ invstd,
@@ -420,7 +455,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
                                                         const float *__restrict__ beta,
                                                         const float *__restrict__ part, int nrc,
                                                         void *__restrict__ dx, int64_t Mg, int C, int CC8, int RG,
-                                                        int64_t rpb, float *dgamma, float *dbeta, int accumulate) {
+                                                        int64_t rpb, float *dgamma, float *dbeta, int accumulate,
+                                                        const float *__restrict__ rscale = nullptr, int HW = 1) {
   __shared__ float red[512];
   __shared__ float coef[2][64];
   const int grp = blockIdx.z, groups = gridDim.z;
@@ -465,13 +501,17 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
   row_walk<8>(r0, r1, rg, RG,
-              [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c)}; },
-              [&](int64_t rr, const Raw8x2<DT> &raw) {
+              [&](int64_t rr) {
+                return Raw8x2s<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c),
+                                   SC ? rscale[(int)rr / HW] : 1.f};
+              },
+              [&](int64_t rr, const Raw8x2s<DT> &raw) {
     float vx[8], vd[8], o[8];
     unpack<DT>(raw.x, vx);
     unpack<DT>(raw.d, vd);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+      if (SC) vd[j] *= raw.s;
       const float xh = (vx[j] - mu[j]) * iv[j];
       const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
@@ -604,6 +644,91 @@ extern "C" int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t 
   BN_DISPATCH(BN_APPLY);
 #undef BN_APPLY
   return launch_status("bn_fwd_partials");
+}
+
+// BatchNorm (no activation) + StochasticDepth(row) + skip add, training, one group:
+// y = bn(x) * scale[n] + skip (BnDrop); statistics from `part`/`shifts` (nrc rows, e.g.
+// the conv epilogue's) or, when part is NULL, by the stats pass into `workspace`
+extern "C" int ewvit_bn_fwd_drop_add(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
+                                     const float *beta, float *running_mean, float *running_var, float momentum,
+                                     float eps, float *save_mean, float *save_invstd, int64_t *num_batches_tracked,
+                                     const float *part, const float *shifts, int nrc, const void *skip, int64_t HW,
+                                     float keep_prob, uint64_t seed, const int64_t *seed_offset, float *scale_out,
+                                     float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(x && y && skip && scale_out && dtype_ok(dtype), "bn_fwd_drop_add: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_fwd_drop_add: C=%lld must be a multiple of 8, <= 4096",
+                  (long long)C);
+  EWVIT_CHECK_ARG(HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31), "bn_fwd_drop_add: M=%lld rows of %lld", (long long)M,
+                  (long long)HW);
+  EWVIT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "bn_fwd_drop_add: keep_prob %g", (double)keep_prob);
+  EWVIT_CHECK_ARG(part ? (shifts && nrc >= 1 && nrc <= 4096) : workspace != nullptr,
+                  "bn_fwd_drop_add: partial statistics or a workspace");
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const BnGeo geo = bn_geo(C);
+  if (!part) {
+    nrc = bn_nrc(geo, M, 1);
+    float *wpart = workspace, *wshift = workspace + (int64_t)nrc * 2 * C;
+    const int64_t rpc = (M + nrc - 1) / nrc;
+    dim3 grid(nrc, geo.nch, 1);
+    if (dtype == EWVIT_BF16)
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_BF16>, grid, dim3(geo.threads), 0, s, x, M, (int)C, geo.CC8, geo.RG,
+                         rpc, wpart, wshift);
+    else
+      hipLaunchKernelGGL(bn_stats_kernel<EWVIT_F32>, grid, dim3(geo.threads), 0, s, x, M, (int)C, geo.CC8, geo.RG,
+                         rpc, wpart, wshift);
+    part = wpart;
+    shifts = wshift;
+  }
+  BnDrop dr;
+  dr.skip = skip; dr.keep = keep_prob; dr.seed = seed; dr.seed_offset = seed_offset; dr.scale_out = scale_out;
+  dr.HW = (int)HW;
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 agrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL((bn_apply_kernel<EWVIT_BF16, 0, true>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc,
+                       M, (int)C, geo.CC8, geo.RG, rpb, 1, gamma, beta, running_mean, running_var, momentum, eps,
+                       save_mean, save_invstd, num_batches_tracked, dr);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<EWVIT_F32, 0, true>), agrid, dim3(geo.threads), 0, s, x, y, part, shifts, nrc,
+                       M, (int)C, geo.CC8, geo.RG, rpb, 1, gamma, beta, running_mean, running_var, momentum, eps,
+                       save_mean, save_invstd, num_batches_tracked, dr);
+  return launch_status("bn_fwd_drop_add");
+}
+
+// backward of ewvit_bn_fwd_drop_add's BatchNorm: g = dy * row_scale[row / HW] (the skip
+// gradient is dy itself, no kernel); dgamma / dbeta overwritten
+extern "C" int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                                   const float *gamma, const float *beta, const float *save_mean,
+                                   const float *save_invstd, float *dgamma, float *dbeta, const float *row_scale,
+                                   int64_t HW, float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && row_scale && workspace && dtype_ok(dtype),
+                  "bn_bwd_scaled: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_scaled: C=%lld", (long long)C);
+  EWVIT_CHECK_ARG(HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31), "bn_bwd_scaled: M=%lld rows of %lld", (long long)M,
+                  (long long)HW);
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const BnGeo geo = bn_geo(C);
+  const int nrc = bn_nrc(geo, M, 1);
+  const int64_t rpc = (M + nrc - 1) / nrc;
+  dim3 grid(nrc, geo.nch, 1);
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+  if (dtype == EWVIT_BF16) {
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_BF16, 0, true>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
+                       save_invstd, gamma, beta, M, (int)C, geo.CC8, geo.RG, rpc, workspace, row_scale, (int)HW);
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_BF16, 0, true>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
+                       save_invstd, gamma, beta, workspace, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0,
+                       row_scale, (int)HW);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_F32, 0, true>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
+                       save_invstd, gamma, beta, M, (int)C, geo.CC8, geo.RG, rpc, workspace, row_scale, (int)HW);
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_F32, 0, true>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
+                       save_invstd, gamma, beta, workspace, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0,
+                       row_scale, (int)HW);
+  }
+  return launch_status("bn_bwd_scaled");
 }
 
 extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,

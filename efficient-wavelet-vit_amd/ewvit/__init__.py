@@ -3,7 +3,7 @@
 C-ABI: include/ewvit.h, built into ewvit/libewvit.so from csrc/*.hip.
 """
 from . import _lib, optim
-from .bn import batch_norm_act, batch_norm_act_params
+from .bn import batch_norm_act, batch_norm_act_params, batch_norm_drop_add
 from .conv import conv2d, conv3x3
 from .se import drop_add, scale_add, squeeze_excite
 from .ops import (attention_cross, attention_packed, colsum, dwconv3x3, dwt_haar, dwt_hf_upsample, gemm,

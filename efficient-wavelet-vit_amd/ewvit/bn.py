@@ -96,3 +96,59 @@ def batch_norm_act_params(x, weight, bias, running_mean, running_var, training, 
         raise ValueError('batch_norm_act: counter must be an int64 tensor on the input device')
     return BatchNormActFn.apply(x, weight, bias, running_mean, running_var, bool(training), momentum, eps,
                                 ACT[act], int(groups), counter, partials)
+
+
+class BNDropAddFn(torch.autograd.Function):
+    """y = BatchNorm(x) * scale[n] + skip (StochasticDepth(row) drawn in the kernel),
+    training mode, one group: the MBConv block tail in one pass each way."""
+    @staticmethod
+    def forward(ctx, x, skip, weight, bias, running_mean, running_var, momentum, eps, counter, keep, partials):
+        from .ops import _seed
+        L.require_gpu(x, skip)
+        xc, M, C = _rows(x)
+        sk = skip.to(xc.dtype).contiguous(memory_format=torch.channels_last)
+        N = xc.shape[0]
+        y = torch.empty_like(xc)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        scale = torch.empty(N, dtype=torch.float32, device=x.device)
+        if partials is not None:
+            part, shifts, nrc = partials
+            ws = None
+        else:
+            part = shifts = None
+            nrc = 0
+            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=x.device)
+        L.call('ewvit_bn_fwd_drop_add', L.ptr(xc), L.ptr(y), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+               L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), L.ptr(mean), L.ptr(invstd),
+               L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.ptr(sk), M // N, float(keep), _seed(),
+               L.ptr(L.rng_offset(x.device)), L.ptr(scale), L.ptr(ws), L.stream(y),
+               work={'bytes': (3 + int(partials is None)) * xc.numel() * xc.element_size()})
+        ctx.save_for_backward(xc, weight, bias, mean, invstd, scale)
+        ctx.cfg = (M, C, M // N, skip.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, weight, bias, mean, invstd, scale = ctx.saved_tensors
+        M, C, HW, sdt = ctx.cfg
+        dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
+        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dy.device)
+        L.call('ewvit_bn_bwd_scaled', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
+               L.ptr(mean), L.ptr(invstd), L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(ws), L.stream(dx),
+               work={'bytes': 5 * xc.numel() * xc.element_size()})
+        return dx, dy.to(sdt), dg, db, None, None, None, None, None, None, None
+
+
+def batch_norm_drop_add(x, bn, skip, drop_prob, partials=None):
+    """StochasticDepth(p=drop_prob, mode='row')(bn(x)) + skip in one pass (training):
+    the keep mask is drawn in the kernel (ewvit dropout's counter hash of a per-call
+    seed and the step counter); `partials` as in batch_norm_act."""
+    if bn.momentum is None or not bn.training:
+        raise ValueError('batch_norm_drop_add: training-mode BatchNorm with a momentum only')
+    counter = bn.num_batches_tracked if bn.track_running_stats else None
+    return BNDropAddFn.apply(x, skip, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                             counter, 1.0 - float(drop_prob), partials)

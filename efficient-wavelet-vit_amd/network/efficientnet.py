@@ -75,21 +75,44 @@ class ConvBNAct(nn.Sequential):
             mods.append(nn.SiLU(inplace=True))
         super().__init__(*mods)
 
-    def forward(self, x):
+    def _hooked(self):
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self)
+
+    def _conv_stats(self, x):
+        """(y, partials) with the BatchNorm statistics summed in the conv's epilogue, or None."""
         conv, bn = self[0], self[1]
-        act = 'silu' if len(self) > 2 else None
-        hooks = bn._forward_hooks or bn._forward_pre_hooks or conv._forward_hooks or conv._forward_pre_hooks
         if (type(conv) is Conv2d and bn.training and bn.track_running_stats and bn.momentum is not None
-                and not hooks and x.is_cuda and conv.groups == 1 and conv.padding[0] == conv.kernel_size[0] // 2
-                and conv.stride[0] == conv.stride[1] and conv.out_channels <= 2048):
+                and not self._hooked() and x.is_cuda and conv.groups == 1
+                and conv.padding[0] == conv.kernel_size[0] // 2 and conv.stride[0] == conv.stride[1]
+                and conv.out_channels <= 2048):
             rows = ewvit.conv.bn_stat_rows(x, conv.weight, conv.stride[0])
             if rows and (x.shape[0] * ((x.shape[2] - 1) // conv.stride[0] + 1) *
                          ((x.shape[3] - 1) // conv.stride[0] + 1) + rows - 1) // rows <= _EPI_STATS_MAX_TILES:
-                # the conv's epilogue sums the batch statistics: BN runs its apply pass only
                 r = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0], bn.running_mean)
                 if r is not None:
-                    y, part, shifts, nrc = r
-                    return ewvit.batch_norm_act(y, bn, act, partials=(part, shifts, nrc))
+                    return r[0], r[1:]
+        return None
+
+    def can_drop_add(self, x):
+        bn = self[1]
+        return (len(self) == 2 and type(self[0]) is Conv2d and bn.training and bn.momentum is not None
+                and x.is_cuda and not self._hooked() and self[0].out_channels % 8 == 0
+                and self[0].out_channels <= 4096)
+
+    def forward_drop_add(self, x, skip, drop_prob):
+        """StochasticDepth(bn(conv(x))) + skip: BN, drop-path and the skip add in one pass."""
+        r = self._conv_stats(x)
+        if r is not None:
+            return ewvit.batch_norm_drop_add(r[0], self[1], skip, drop_prob, partials=r[1])
+        return ewvit.batch_norm_drop_add(self[0](x), self[1], skip, drop_prob)
+
+    def forward(self, x):
+        conv, bn = self[0], self[1]
+        act = 'silu' if len(self) > 2 else None
+        r = self._conv_stats(x)
+        if r is not None:
+            # the conv's epilogue summed the batch statistics: BN runs its apply pass only
+            return ewvit.batch_norm_act(r[0], bn, act, partials=r[1])
         y = conv(x)
         if y.is_cuda and y.shape[1] % 8 == 0 and y.shape[1] <= 2048 and not (bn._forward_hooks or bn._forward_pre_hooks):
             return ewvit.batch_norm_act(y, bn, act)
@@ -124,8 +147,20 @@ def _drop_path(x, p, training):
     return x * keep.div_(1.0 - p)
 
 
+def r_ok(x):
+    return x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.shape[1] % 8 == 0
+
+
 class _Block(nn.Module):
     def forward(self, x):
+        last = self.block[-1]
+        if (self.use_res_connect and self.training and isinstance(last, ConvBNAct) and last.can_drop_add(x)
+                and r_ok(x) and not self._forward_hooks and not self.block._forward_hooks):
+            # the block tail (project BN + drop-path + skip add) as one pass each way
+            h = x
+            for m in list(self.block)[:-1]:
+                h = m(h)
+            return last.forward_drop_add(h, x, self.sd_prob)
         r = self.block(x)
         if self.use_res_connect:
             if self.training and self.sd_prob > 0.0 and r.is_cuda and r.dtype in (torch.bfloat16, torch.float32) \

@@ -199,6 +199,24 @@ int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t 
  * per-tile partial rows down to what the apply pass finalises from. */
 int ewvit_bn_fold_partials(const float *part_in, int nin, const float *shift_in, float *part_out, int nout,
                            float *shift_out, int64_t C, int groups, void *stream);
+/* MBConv block tail in one pass (training, no activation, one group): y = bn(x) *
+ * scale[n] + skip, n = row / HW, scale[n] = (u < keep_prob) / keep_prob with u the
+ * counter hash of (seed + *seed_offset * golden, n) as ewvit dropout draws it;
+ * scale_out[n] receives the factors.  Statistics from part/shifts/nrc (as
+ * ewvit_bn_fwd_partials) or, with part == NULL, computed into `workspace`
+ * (ewvit_bn_workspace(M, C, 1) bytes). */
+int ewvit_bn_fwd_drop_add(const void *x, void *y, int dtype, int64_t M, int64_t C, const float *gamma,
+                          const float *beta, float *running_mean, float *running_var, float momentum, float eps,
+                          float *save_mean, float *save_invstd, int64_t *num_batches_tracked, const float *part,
+                          const float *shifts, int nrc, const void *skip, int64_t HW, float keep_prob,
+                          uint64_t seed, const int64_t *seed_offset, float *scale_out, float *workspace,
+                          void *stream);
+/* Its backward: dx of the BatchNorm for g = dy * row_scale[row / HW]; dgamma / dbeta
+ * overwritten (may be NULL); the skip's gradient is dy. */
+int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                        const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
+                        float *dgamma, float *dbeta, const float *row_scale, int64_t HW, float *workspace,
+                        void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,

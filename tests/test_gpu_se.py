@@ -102,3 +102,37 @@ def test_drop_add(dtype):
         y2 = ewvit.drop_add(r, x, p)
     kept2 = ((y2.float() - x.float()).abs().flatten(1).amax(1) > 0)
     assert not torch.equal(kept, kept2)
+
+
+@pytest.mark.parametrize('kind,hw', [('mb', 7), ('mb', 14), ('fused', 12)])
+def test_block_tail_bn_drop_add(kind, hw, monkeypatch):
+    """MBConv / FusedMBConv training forward+backward with the block tail (project BN,
+    StochasticDepth, skip add) as one ewvit_bn_fwd_drop_add pass matches the separate
+    BN + drop_add path under the same seed (same in-kernel keep mask)."""
+    import network.efficientnet as en
+    torch.manual_seed(7)
+    if kind == 'mb':
+        b1, b2 = en.MBConv(6, 3, 1, 64, 64, 0.5), en.MBConv(6, 3, 1, 64, 64, 0.5)
+    else:
+        b1, b2 = en.FusedMBConv(4, 3, 1, 64, 64, 0.5), en.FusedMBConv(4, 3, 1, 64, 64, 0.5)
+    b1, b2 = b1.to(DEV), b2.to(DEV)
+    b2.load_state_dict(b1.state_dict())
+    x = torch.randn(16, 64, hw, hw, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    torch.manual_seed(11)
+    y1 = b1(x1)
+    monkeypatch.setattr(en.ConvBNAct, 'can_drop_add', lambda self, x: False)
+    torch.manual_seed(11)
+    y2 = b2(x2)
+    kept = ((y2.float() - x.float()).abs().flatten(1).amax(1) > 0)
+    assert 0 < int(kept.sum()) < 16                        # the mask is exercised
+    dy = torch.randn(y1.shape, device=DEV).to(torch.bfloat16)
+    y1.backward(dy)
+    y2.backward(dy)
+    assert rel(y1.float(), y2.float()) < 2 ** -6
+    assert rel(x1.grad.float(), x2.grad.float()) < 2e-2
+    for (n, p1), p2 in zip(b1.named_parameters(), b2.parameters()):
+        if p1.grad is not None and p2.grad is not None:
+            assert rel(p1.grad, p2.grad) < 3e-2, n
+    for (n, q1), q2 in zip(b1.named_buffers(), b2.buffers()):
+        assert torch.allclose(q1.float(), q2.float(), rtol=1e-3, atol=1e-5), n
