@@ -253,15 +253,20 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const void *__restrict__ 
   bn_block_sums(sm, S, SS, cl, rg, CC8, RG, c8, C8, C, part + ((int64_t)grp * nrc + blockIdx.x) * 2 * C);
 }
 
-// the chunk's per-channel sums over the nrc partial rows of group grp, into LDS
-// red[0][ch], red[1][ch] (ch < 8*CC8): 64 channels x 4 lanes, fixed order
-__device__ __forceinline__ void bn_chunk_sums(const float *__restrict__ part, int grp, int nrc, int C, int ch0,
-                                              int nch_c, float *red) {
+// LDS-only workgroup barrier: waits for this wave's LDS ops, not for its global loads
+// (a __syncthreads() fence would also drain the row loads issued ahead of the finalize)
+__device__ __forceinline__ void bn_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// the chunk's per-channel sums over the nrc partial rows of group grp: 64 channels x 4
+// lanes, each lane its slice of rows (8 loads in flight) -> (a, b); bn_chunk_reduce
+// combines the 4 lanes in fixed order into LDS red[0][ch], red[1][ch] (ch < 8*CC8)
+__device__ __forceinline__ void bn_chunk_load(const float *__restrict__ part, int grp, int nrc, int C, int ch0,
+                                              int nch_c, float &a, float &b) {
   const int tid = threadIdx.x, j = tid & 63, q = tid >> 6;
-  float a = 0.f, b = 0.f;
+  a = 0.f; b = 0.f;
   if (j < nch_c && q * 64 < (int)blockDim.x) {
     const float *pg = part + (int64_t)grp * nrc * 2 * C + ch0 + j;
-    for (int k0 = q; k0 < nrc; k0 += 32) {      // 8 partial rows' loads in flight
+    for (int k0 = q; k0 < nrc; k0 += 32) {
       float va[8], vb[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -273,17 +278,57 @@ __device__ __forceinline__ void bn_chunk_sums(const float *__restrict__ part, in
       for (int u = 0; u < 8; ++u) { a += va[u]; b += vb[u]; }
     }
   }
+}
+__device__ __forceinline__ void bn_chunk_reduce(float *red, float a, float b) {
+  const int tid = threadIdx.x;
   float *ra = red, *rb = red + 256;
   ra[tid] = a;
   rb[tid] = b;
-  __syncthreads();
+  bn_sync();
   if (tid < 64) {
     float sa = 0.f, sb = 0.f;
     for (int k = 0; k * 64 < (int)blockDim.x; ++k) { sa += ra[k * 64 + tid]; sb += rb[k * 64 + tid]; }
     ra[tid] = sa;
     rb[tid] = sb;
   }
-  __syncthreads();
+  bn_sync();
+}
+__device__ __forceinline__ void bn_chunk_sums(const float *__restrict__ part, int grp, int nrc, int C, int ch0,
+                                              int nch_c, float *red) {
+  float a, b;
+  bn_chunk_load(part, grp, nrc, C, ch0, nch_c, a, b);
+  bn_chunk_reduce(red, a, b);
+}
+
+// row_walk whose first batch of NB rows is loaded BEFORE fin() (the block's statistics
+// finalize, run by every thread) so the two latency chains overlap
+template <int NB, typename L, typename U, typename F>
+__device__ __forceinline__ void row_walk_pf(bool active, int64_t r0, int64_t r1, int rg, int R, L &&load, U &&use,
+                                            F &&fin) {
+  using T = decltype(load(int64_t(0)));
+  int64_t r = r0 + rg;
+  T t[NB];
+  const bool full = active && r + (NB - 1) * (int64_t)R < r1;
+  if (full) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) t[q] = load(r + q * (int64_t)R);
+  }
+  fin();
+  if (!active) return;
+  if (full) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) use(r + q * (int64_t)R, t[q]);
+    r += NB * (int64_t)R;
+  }
+  for (; r + (NB - 1) * (int64_t)R < r1; r += NB * (int64_t)R) {
+    T u[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) u[q] = load(r + q * (int64_t)R);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NB; ++q) use(r + q * (int64_t)R, u[q]);
+  }
+  for (; r < r1; r += R) use(r, load(r));
 }
 
 // ---- apply: y = act(x * scale + shift).  Training: the block finalises its chunk's
@@ -306,87 +351,94 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
   const int ch0 = blockIdx.y * CC8 * 8;
   const int nch_c = (C - ch0) < CC8 * 8 ? (C - ch0) : CC8 * 8;
   const float n = (float)Mg;
-  if (training) {
-    if (blockIdx.x == 0 && grp == 0) {
-      if (counter && blockIdx.y == 0 && tid == 0) *counter += groups;
-      float rm = 0.f, rv = 0.f;
-      const int c = ch0 + tid;
-      if (tid < nch_c) { rm = running_mean ? running_mean[c] : 0.f; rv = running_var ? running_var[c] : 0.f; }
-      for (int g = 0; g < groups; ++g) {
-        bn_chunk_sums(part, g, nrc, C, ch0, nch_c, red);
-        if (tid < nch_c) {
-          const float d = red[tid] / n, mu = shifts[g * C + c] + d;
-          const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
-          if (save_mean) save_mean[g * C + c] = mu;
-          if (save_invstd) save_invstd[g * C + c] = rsqrtf(var + eps);
-          rm = (1.f - momentum) * rm + momentum * mu;
-          rv = (1.f - momentum) * rv + momentum * (Mg > 1 ? var * (n / (n - 1.f)) : var);
-          if (g == grp) {
-            const float inv = rsqrtf(var + eps);
-            const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
-            coef[0][tid] = ga * inv;
-            coef[1][tid] = be - mu * ga * inv;
-          }
-        }
-        __syncthreads();
-      }
-      if (tid < nch_c) {
-        if (running_mean) running_mean[c] = rm;
-        if (running_var) running_var[c] = rv;
-      }
-    } else {
-      bn_chunk_sums(part, grp, nrc, C, ch0, nch_c, red);
-      if (tid < nch_c) {
-        const int c = ch0 + tid;
-        const float d = red[tid] / n, mu = shifts[grp * C + c] + d;
-        const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
-        const float inv = rsqrtf(var + eps);
-        const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
-        coef[0][tid] = ga * inv;
-        coef[1][tid] = be - mu * ga * inv;
-      }
-    }
-  } else if (tid < nch_c) {
-    const int c = ch0 + tid;
-    const float inv = rsqrtf(running_var[c] + eps);
-    const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
-    coef[0][tid] = ga * inv;
-    coef[1][tid] = be - running_mean[c] * ga * inv;
-  }
-  __syncthreads();
+  const bool book = training && blockIdx.x == 0 && grp == 0;
+  // this block's partial-row loads first, then its first batch of rows (row_walk_pf)
+  float pa = 0.f, pb = 0.f;
+  if (training && !(book && groups > 1)) bn_chunk_load(part, grp, nrc, C, ch0, nch_c, pa, pb);
   const int cl = tid % CC8, rg = tid / CC8;
   const int c8 = blockIdx.y * CC8 + cl;
-  if (rg >= RG || c8 >= C8) return;
+  const bool active = rg < RG && c8 < C8;
   const int64_t goff = (int64_t)grp * Mg * C;
-  const int c = c8 * 8;
+  const int c = active ? c8 * 8 : 0;
   float sc[8], sh[8];
+  auto fin = [&]() {
+    if (training) {
+      if (book) {
+        if (counter && blockIdx.y == 0 && tid == 0) *counter += groups;
+        float rm = 0.f, rv = 0.f;
+        const int cc = ch0 + tid;
+        if (tid < nch_c) { rm = running_mean ? running_mean[cc] : 0.f; rv = running_var ? running_var[cc] : 0.f; }
+        for (int g = 0; g < groups; ++g) {
+          if (groups > 1) bn_chunk_load(part, g, nrc, C, ch0, nch_c, pa, pb);
+          bn_chunk_reduce(red, pa, pb);
+          if (tid < nch_c) {
+            const float d = red[tid] / n, mu = shifts[g * C + cc] + d;
+            const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
+            if (save_mean) save_mean[g * C + cc] = mu;
+            if (save_invstd) save_invstd[g * C + cc] = rsqrtf(var + eps);
+            rm = (1.f - momentum) * rm + momentum * mu;
+            rv = (1.f - momentum) * rv + momentum * (Mg > 1 ? var * (n / (n - 1.f)) : var);
+            if (g == grp) {
+              const float inv = rsqrtf(var + eps);
+              const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
+              coef[0][tid] = ga * inv;
+              coef[1][tid] = be - mu * ga * inv;
+            }
+          }
+          bn_sync();
+        }
+        if (tid < nch_c) {
+          if (running_mean) running_mean[cc] = rm;
+          if (running_var) running_var[cc] = rv;
+        }
+      } else {
+        bn_chunk_reduce(red, pa, pb);
+        if (tid < nch_c) {
+          const int cc = ch0 + tid;
+          const float d = red[tid] / n, mu = shifts[grp * C + cc] + d;
+          const float var = fmaxf(red[256 + tid] / n - d * d, 0.f);
+          const float inv = rsqrtf(var + eps);
+          const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
+          coef[0][tid] = ga * inv;
+          coef[1][tid] = be - mu * ga * inv;
+        }
+      }
+    } else if (tid < nch_c) {
+      const int cc = ch0 + tid;
+      const float inv = rsqrtf(running_var[cc] + eps);
+      const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
+      coef[0][tid] = ga * inv;
+      coef[1][tid] = be - running_mean[cc] * ga * inv;
+    }
+    bn_sync();
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = coef[0][cl * 8 + j]; sh[j] = coef[1][cl * 8 + j]; }
-  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  auto apply_row = [&](int64_t rr, const Raw8<DT> &raw) {
-    float v[8];
-    unpack<DT>(raw, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
-    st8<DT>(y, goff + rr * C + c, v);
+    for (int j = 0; j < 8; ++j) { sc[j] = coef[0][cl * 8 + j]; sh[j] = coef[1][cl * 8 + j]; }
   };
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
   if constexpr (!DROP) {
-    row_walk<8>(r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); }, apply_row);
+    row_walk_pf<8>(active, r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
+                   [&](int64_t rr, const Raw8<DT> &raw) {
+      float v[8];
+      unpack<DT>(raw, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
+      st8<DT>(y, goff + rr * C + c, v);
+    }, fin);
   } else {
     const uint64_t sd = step_seed(dr.seed, dr.seed_offset);
-    row_walk<8>(r0, r1, rg, RG,
-                [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c), ldraw<DT>(dr.skip, rr * C + c)}; },
-                [&](int64_t rr, const Raw8x2<DT> &raw) {
-      const int n = (int)rr / dr.HW;
-      const float ks = uniform01(sd, (uint64_t)n) < dr.keep ? 1.f / dr.keep : 0.f;
-      if (dr.scale_out && (int)rr == n * dr.HW && c8 == 0) dr.scale_out[n] = ks;
+    row_walk_pf<8>(active, r0, r1, rg, RG,
+                   [&](int64_t rr) { return Raw8x2<DT>{ldraw<DT>(x, rr * C + c), ldraw<DT>(dr.skip, rr * C + c)}; },
+                   [&](int64_t rr, const Raw8x2<DT> &raw) {
+      const int nn = (int)rr / dr.HW;
+      const float ks = uniform01(sd, (uint64_t)nn) < dr.keep ? 1.f / dr.keep : 0.f;
+      if (dr.scale_out && (int)rr == nn * dr.HW && c8 == 0) dr.scale_out[nn] = ks;
       float v[8], vs[8];
       unpack<DT>(raw.x, v);
       unpack<DT>(raw.d, vs);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaf(act_fwd<ACT>(fmaf(v[j], sc[j], sh[j])), ks, vs[j]);
       st8<DT>(y, rr * C + c, v);
-    });
+    }, fin);
   }
 }
 
