@@ -516,48 +516,54 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
   const int ch0 = blockIdx.y * CC8 * 8;
   const int nch_c = (C - ch0) < CC8 * 8 ? (C - ch0) : CC8 * 8;
   const float n = (float)Mg;
-  if (blockIdx.x == 0 && grp == 0) {
-    float ga = 0.f, gb = 0.f;
-    for (int g = 0; g < groups; ++g) {
-      bn_chunk_sums(part, g, nrc, C, ch0, nch_c, red);
-      if (tid < nch_c) {
-        ga += red[tid];
-        gb += red[256 + tid];
-        if (g == grp) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
-      }
-      __syncthreads();
-    }
-    if (tid < nch_c) {
-      const int c = ch0 + tid;
-      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + ga : ga;
-      if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gb : gb;
-    }
-  } else {
-    bn_chunk_sums(part, grp, nrc, C, ch0, nch_c, red);
-    if (tid < nch_c) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
-  }
-  __syncthreads();
+  const bool book = blockIdx.x == 0 && grp == 0;
+  // partial-row loads first, then the first batch of rows (row_walk_pf), then finalize
+  float pa = 0.f, pb = 0.f;
+  if (!(book && groups > 1)) bn_chunk_load(part, grp, nrc, C, ch0, nch_c, pa, pb);
   const int cl = tid % CC8, rg = tid / CC8;
   const int c8 = blockIdx.y * CC8 + cl;
-  if (rg >= RG || c8 >= C8) return;
+  const bool active = rg < RG && c8 < C8;
   const int64_t goff = (int64_t)grp * Mg * C;
-  mean += grp * C;
-  invstd += grp * C;
-  const int c = c8 * 8;
+  const int c = active ? c8 * 8 : 0;
   float mu[8], iv[8], ga[8], be[8], c0[8], c1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    mu[j] = mean[c + j]; iv[j] = invstd[c + j];
+    mu[j] = mean[grp * C + c + j]; iv[j] = invstd[grp * C + c + j];
     ga[j] = gamma ? gamma[c + j] : 1.f; be[j] = beta ? beta[c + j] : 0.f;
-    c0[j] = coef[0][cl * 8 + j]; c1[j] = coef[1][cl * 8 + j];
   }
+  auto fin = [&]() {
+    if (book) {
+      float sa = 0.f, sb = 0.f;
+      for (int g = 0; g < groups; ++g) {
+        if (groups > 1) bn_chunk_load(part, g, nrc, C, ch0, nch_c, pa, pb);
+        bn_chunk_reduce(red, pa, pb);
+        if (tid < nch_c) {
+          sa += red[tid];
+          sb += red[256 + tid];
+          if (g == grp) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
+        }
+        bn_sync();
+      }
+      if (tid < nch_c) {
+        const int cc = ch0 + tid;
+        if (dbeta) dbeta[cc] = accumulate ? dbeta[cc] + sa : sa;
+        if (dgamma) dgamma[cc] = accumulate ? dgamma[cc] + sb : sb;
+      }
+    } else {
+      bn_chunk_reduce(red, pa, pb);
+      if (tid < nch_c) { coef[0][tid] = red[tid] / n; coef[1][tid] = red[256 + tid] / n; }
+    }
+    bn_sync();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { c0[j] = coef[0][cl * 8 + j]; c1[j] = coef[1][cl * 8 + j]; }
+  };
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
-  row_walk<8>(r0, r1, rg, RG,
-              [&](int64_t rr) {
-                return Raw8x2s<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c),
-                                   SC ? rscale[(int)rr / HW] : 1.f};
-              },
-              [&](int64_t rr, const Raw8x2s<DT> &raw) {
+  row_walk_pf<8>(active, r0, r1, rg, RG,
+                 [&](int64_t rr) {
+                   return Raw8x2s<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c),
+                                      SC ? rscale[(int)rr / HW] : 1.f};
+                 },
+                 [&](int64_t rr, const Raw8x2s<DT> &raw) {
     float vx[8], vd[8], o[8];
     unpack<DT>(raw.x, vx);
     unpack<DT>(raw.d, vd);
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
     }
     st8<DT>(dx, goff + rr * C + c, o);
-  });
+  }, fin);
 }
 
 }  // namespace ewvit
