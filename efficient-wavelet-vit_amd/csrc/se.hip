@@ -432,6 +432,117 @@ __global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restri
   *dst = acc0 + acc1;
 }
 
+// The squeeze folded into the MLP's first kernel: block (n, chunk) reduces its 64
+// channels of frame n over the HW rows itself (8 channel vectors x 32 row groups, 4
+// rows' loads in flight, fixed-order tree) instead of reading a vector a separate
+// launch produced.  PROD = 0: mean_hw a (the forward squeeze s0, written out for the
+// backward); PROD = 1: sum_hw a * b (the backward's ds = sum dy * x).
+template <int DT, int PROD>
+__device__ __forceinline__ float se_chunk_squeeze(const void *__restrict__ a, const void *__restrict__ b, int n,
+                                                  int cb, int HW, int C, float scale, float *sm) {
+  const int tid = threadIdx.x, cv = tid & 7, rg = tid >> 3;
+  const int c = cb * SE_CB + cv * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (c < C) {
+    const int64_t base = (int64_t)n * HW * C + c;
+    int h = rg;
+    for (; h + 96 < HW; h += 128) {
+      float va[4][8], vb[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        se_ld8<DT>(a, base + (int64_t)(h + 32 * q) * C, va[q]);
+        if (PROD) se_ld8<DT>(b, base + (int64_t)(h + 32 * q) * C, vb[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = PROD ? fmaf(va[q][j], vb[q][j], acc[j]) : acc[j] + va[q][j];
+    }
+    for (; h < HW; h += 32) {
+      float va[8], vb[8];
+      se_ld8<DT>(a, base + (int64_t)h * C, va);
+      if (PROD) se_ld8<DT>(b, base + (int64_t)h * C, vb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = PROD ? fmaf(va[j], vb[j], acc[j]) : acc[j] + va[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sm[j * 256 + tid] = acc[j];
+  __syncthreads();
+  for (int st = 16; st >= 1; st >>= 1) {
+    if (rg < st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm[j * 256 + tid] += sm[j * 256 + tid + st * 8];
+    __syncthreads();
+  }
+  // lane l of every wave: channel cb*64 + l = vector l>>3, element l&7
+  const int l = tid & 63;
+  return sm[(l & 7) * 256 + (l >> 3)] * scale;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void se_sq_h1_part_kernel(const void *__restrict__ x, int HW, float inv_hw,
+                                                            const float *__restrict__ w1, int C, int Csq,
+                                                            float *__restrict__ s0_out, float *__restrict__ part) {
+  __shared__ float sm[8 * 256];
+  const int n = blockIdx.x, cb = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = cb * SE_CB + lane;
+  const float sq = se_chunk_squeeze<DT, 0>(x, nullptr, n, cb, HW, C, inv_hw, sm);
+  const float xv = c < C ? sq : 0.f;
+  if (w == 0 && c < C) s0_out[(int64_t)n * C + c] = xv;
+  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = w; j0 < Csq; j0 += 16) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 4 * q;
+      v[q] = (j < Csq && c < C) ? w1[(int64_t)j * C + c] * xv : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      const int j = j0 + 4 * q;
+      if (lane == 0 && j < Csq) pp[j] = v[q];
+    }
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restrict__ dy, const void *__restrict__ x,
+                                                            int HW, const float *__restrict__ s,
+                                                            const float *__restrict__ w2, int C, int Csq,
+                                                            float *__restrict__ dz2_out, float *__restrict__ part) {
+  __shared__ float sm[8 * 256];
+  const int n = blockIdx.x, cb = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = cb * SE_CB + lane;
+  const float dsv = se_chunk_squeeze<DT, 1>(dy, x, n, cb, HW, C, 1.f, sm);
+  float d = 0.f;
+  if (c < C) {
+    const float sv = s[(int64_t)n * C + c];
+    d = dsv * sv * (1.f - sv);
+    if (w == 0) dz2_out[(int64_t)n * C + c] = d;
+  }
+  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = w; j0 < Csq; j0 += 16) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 4 * q;
+      v[q] = (j < Csq && c < C) ? w2[(int64_t)c * Csq + j] * d : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      const int j = j0 + 4 * q;
+      if (lane == 0 && j < Csq) pp[j] = v[q];
+    }
+  }
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -564,4 +675,54 @@ extern "C" int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1
   hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
                      (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
   return launch_status("se_mlp_bwd");
+}
+
+// squeeze + MLP forward: s0 = mean_hw x (written out), then h1 and s as ewvit_se_mlp_fwd;
+// the squeeze runs inside the MLP's first kernel (2 launches for the excite vector)
+extern "C" int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1,
+                                        const float *b1, const float *w2, const float *b2, int64_t Csq, float *s0,
+                                        float *h1, float *s, float *workspace, void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "se_squeeze_mlp_fwd")) return rc;
+  if (int rc = se_mlp_check(N, C, Csq, "se_squeeze_mlp_fwd")) return rc;
+  EWVIT_CHECK_ARG(x && w1 && w2 && s0 && h1 && s && workspace && HW < (1 << 30), "se_squeeze_mlp_fwd: bad args");
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  const dim3 g1((unsigned)N, (unsigned)nb);
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_BF16>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
+                       (int)C, (int)Csq, s0, workspace);
+  else
+    hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_F32>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
+                       (int)C, (int)Csq, s0, workspace);
+  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+                     (size_t)Csq * sizeof(float), st, workspace, nb, b1, w2, b2, (int)C, (int)Csq, h1, s);
+  return launch_status("se_squeeze_mlp_fwd");
+}
+
+// squeeze-excite backward of the excite vector: ds = sum_hw dy * x inside the first
+// kernel, then g / dW1 / db1 / dW2 / db2 as ewvit_se_mlp_bwd (3 launches)
+extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,
+                                        const float *s, const float *h1, const float *s0, const float *w1,
+                                        const float *w2, int64_t Csq, float *g, float *dw1, float *db1, float *dw2,
+                                        float *db2, float *workspace, void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "se_squeeze_mlp_bwd")) return rc;
+  if (int rc = se_mlp_check(N, C, Csq, "se_squeeze_mlp_bwd")) return rc;
+  EWVIT_CHECK_ARG(dy && x && s && h1 && s0 && w1 && w2 && g && dw1 && dw2 && workspace && HW < (1 << 30),
+                  "se_squeeze_mlp_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  float *dz2 = workspace, *dz1 = workspace + N * C, *part = dz1 + N * Csq;
+  const dim3 g1((unsigned)N, (unsigned)nb);
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(se_sq_dh_part_kernel<EWVIT_BF16>, g1, dim3(256), 0, st, dy, x, (int)HW, s, w2, (int)C,
+                       (int)Csq, dz2, part);
+  else
+    hipLaunchKernelGGL(se_sq_dh_part_kernel<EWVIT_F32>, g1, dim3(256), 0, st, dy, x, (int)HW, s, w2, (int)C,
+                       (int)Csq, dz2, part);
+  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+                     (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, 1.f / (float)HW, dz1, g);
+  const int64_t tot = 2 * C * Csq + C + Csq;
+  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
+                     (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
+  return launch_status("se_squeeze_mlp_bwd");
 }

@@ -59,6 +59,9 @@ SIGNATURES = {
     'ewvit_se_scale': [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     'ewvit_se_mlp_fwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     'ewvit_se_mlp_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    'ewvit_se_squeeze_mlp_fwd': [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_se_squeeze_mlp_bwd': [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                 _vp, _vp, _vp],
     'ewvit_scale_add': [_vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp],
     'ewvit_scale_add_drop': [_vp, _vp, _i32, _f32, _u64, _vp, _vp, _vp, _i64, _i64, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,

@@ -52,16 +52,15 @@ class SqueezeExciteFn(torch.autograd.Function):
             x = x.float()
         xc, N, HW, C = _rows(x)
         Csq = w1.shape[0]
-        ws = _ws(N, HW, C, x.device)
         s0 = torch.empty(N, C, dtype=torch.float32, device=x.device)
-        L.call('ewvit_se_reduce', L.ptr(xc), None, L.dt(xc), N, HW, C, 1.0 / HW, L.ptr(s0), L.ptr(ws), L.stream(s0),
-               work={'bytes': xc.numel() * xc.element_size()})
         W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
         h1 = torch.empty(N, Csq, dtype=torch.float32, device=x.device)
         s = torch.empty(N, C, dtype=torch.float32, device=x.device)
         fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=x.device)
-        L.call('ewvit_se_mlp_fwd', L.ptr(s0), L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2), L.ptr(_vec(b2)), L.ptr(h1),
-               L.ptr(s), N, C, Csq, L.ptr(fws), L.stream(s))
+        # squeeze (mean over HW) inside the MLP's first kernel
+        L.call('ewvit_se_squeeze_mlp_fwd', L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
+               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(s), L.ptr(fws), L.stream(s),
+               work={'bytes': xc.numel() * xc.element_size()})
         y = torch.empty_like(xc)
         L.call('ewvit_se_scale', L.ptr(xc), L.dt(xc), L.ptr(s), None, L.ptr(y), N, HW, C, L.stream(y),
                work={'bytes': 2 * xc.numel() * xc.element_size()})
@@ -76,10 +75,6 @@ class SqueezeExciteFn(torch.autograd.Function):
         HW, Csq = H * W, w1.shape[0]
         dev = xc.device
         dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
-        ws = _ws(N, HW, C, dev)
-        ds = torch.empty(N, C, dtype=torch.float32, device=dev)
-        L.call('ewvit_se_reduce', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, 1.0, L.ptr(ds), L.ptr(ws), L.stream(ds),
-               work={'bytes': 2 * xc.numel() * xc.element_size()})
         W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
         g = torch.empty(N, C, dtype=torch.float32, device=dev)
         dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
@@ -87,8 +82,10 @@ class SqueezeExciteFn(torch.autograd.Function):
         db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if ctx.has_b[0] else None
         db2 = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b[1] else None
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-        L.call('ewvit_se_mlp_bwd', L.ptr(ds), L.ptr(s), L.ptr(h1), L.ptr(s0), L.ptr(W1), L.ptr(W2), 1.0 / HW,
-               L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), N, C, Csq, L.ptr(mws), L.stream(g))
+        # ds = sum_hw dy * x inside the backward MLP's first kernel
+        L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(s), L.ptr(h1), L.ptr(s0),
+               L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
+               L.stream(g), work={'bytes': 2 * xc.numel() * xc.element_size()})
         dx = torch.empty_like(xc)
         L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
                work={'bytes': 2 * xc.numel() * xc.element_size()})

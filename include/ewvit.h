@@ -328,6 +328,17 @@ int64_t ewvit_se_mlp_bwd_workspace(int64_t N, int64_t C, int64_t Csq);
 int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const float *s0, const float *w1,
                      const float *w2, float inv_hw, float *g, float *dw1, float *db1, float *dw2, float *db2,
                      int64_t N, int64_t C, int64_t Csq, float *workspace, void *stream);
+/* The squeeze folded into the MLP: s0 = mean_hw x (written out) -> h1, s exactly as
+ * ewvit_se_mlp_fwd (workspace ewvit_se_mlp_fwd_workspace bytes), 2 launches; and the
+ * backward with ds = sum_hw dy * x computed inside its first kernel, then g, dW1, db1,
+ * dW2, db2 as ewvit_se_mlp_bwd (workspace ewvit_se_mlp_bwd_workspace bytes). */
+int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1,
+                             const float *b1, const float *w2, const float *b2, int64_t Csq, float *s0, float *h1,
+                             float *s, float *workspace, void *stream);
+int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,
+                             const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
+                             int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,
+                             float *workspace, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
