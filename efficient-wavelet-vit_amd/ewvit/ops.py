@@ -347,3 +347,35 @@ def dwconv3x3(x, weight, stride=1, pad=1):
     if torch.is_autocast_enabled('cuda') and x.dtype == torch.float32:
         x = x.to(torch.get_autocast_dtype('cuda'))
     return DepthwiseConv3x3Fn.apply(x, weight, int(stride), int(pad))
+
+
+# ------------------------------------------------------------------- pooling
+class MaxPool2Fn(torch.autograd.Function):
+    """MaxPool2d(kernel 2, stride 2) on a channels-last tensor (csrc/pool.hip)."""
+    @staticmethod
+    def forward(ctx, x):
+        L.require_gpu(x)
+        xc = x.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = xc.shape
+        y = torch.empty((N, C, H // 2, W // 2), dtype=xc.dtype, device=x.device, memory_format=torch.channels_last)
+        arg = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8, device=x.device)
+        L.call('ewvit_maxpool2_fwd', L.ptr(xc), L.ptr(y), L.ptr(arg), L.dt(xc), N, H, W, C, L.stream(y),
+               work={'bytes': (xc.numel() + y.numel()) * xc.element_size() + arg.numel()})
+        ctx.save_for_backward(arg)
+        ctx.shape = (N, C, H, W, xc.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        arg, = ctx.saved_tensors
+        N, C, H, W, dt = ctx.shape
+        dyc = dy.to(dt).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, C, H, W), dtype=dt, device=dy.device, memory_format=torch.channels_last)
+        L.call('ewvit_maxpool2_bwd', L.ptr(dyc), L.ptr(arg), L.ptr(dx), L.dt(dyc), N, H, W, C, L.stream(dx),
+               work={'bytes': (dx.numel() + dyc.numel()) * dyc.element_size() + arg.numel()})
+        return dx
+
+
+def maxpool2(x):
+    """nn.MaxPool2d(2) (stride 2, floor mode) for [N, C, H, W] with C % 8 == 0, f32/bf16."""
+    return MaxPool2Fn.apply(x)

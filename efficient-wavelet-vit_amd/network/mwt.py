@@ -102,7 +102,14 @@ class FreqPool(nn.Sequential):
     """MaxPool2d(2) -> Conv3x3 s2 -> BatchNorm2d -> ReLU -> AdaptiveAvgPool2d(1) (mwt.py:38-44)."""
 
     def forward(self, x):
-        p = self[0](x)
+        mp = self[0]
+        if (x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32)
+                and mp.kernel_size in (2, (2, 2)) and mp.stride in (2, (2, 2)) and mp.padding in (0, (0, 0))
+                and mp.dilation in (1, (1, 1)) and not mp.ceil_mode and not mp.return_indices
+                and not (mp._forward_hooks or mp._forward_pre_hooks)):
+            p = ewvit.maxpool2(x)               # csrc/pool.hip
+        else:
+            p = mp(x)
         r = _epi_stats(self[1], self[2], p)
         if r is not None:
             return self[4](ewvit.batch_norm_act(r[0], self[2], 'relu', partials=r[1]))

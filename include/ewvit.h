@@ -351,6 +351,16 @@ int ewvit_scale_add_drop(const void *r, const void *x, int dtype, float keep_pro
                          const int64_t *seed_offset, float *scale_out, void *y, int64_t N, int64_t row_elems,
                          void *stream);
 
+/* ------------------------------------------------------ pooling ---
+ * MaxPool2d(2) (kernel 2, stride 2, floor mode) of the MWT freq_pool (mwt.py:38-44) on
+ * channels-last [N, H, W, C] (C % 8 == 0): y [N, H/2, W/2, C] and argmax (uint8 window
+ * slot 0..3 per output element, torch's first-maximum / NaN rule); the backward writes
+ * every dx element once (dy at the slot, 0 elsewhere and in a floor-mode remainder). */
+int ewvit_maxpool2_fwd(const void *x, void *y, uint8_t *argmax, int dtype, int64_t N, int64_t H, int64_t W,
+                       int64_t C, void *stream);
+int ewvit_maxpool2_bwd(const void *dy, const uint8_t *argmax, void *dx, int dtype, int64_t N, int64_t H, int64_t W,
+                       int64_t C, void *stream);
+
 /* ------------------------------------------------------ optimizer ---
  * Adam exactly as torch.optim.Adam (amsgrad=False, maximize=False): g += wd*p;
  * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)

@@ -321,3 +321,25 @@ def test_hf_upsample_padded_channels():
     d = (b[..., :9].float() - a.float()).abs()
     assert float((d / a.float().abs().clamp_min(1e-3)).max()) <= 2 ** -7
     assert float(b[..., 9:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize('shape,dtype', [((4, 128, 56, 56), torch.bfloat16), ((3, 16, 9, 11), torch.float32),
+                                         ((2, 64, 8, 8), torch.bfloat16)])
+def test_maxpool2_matches_torch(shape, dtype):
+    """ewvit.maxpool2 (csrc/pool.hip) vs nn.MaxPool2d(2): outputs bitwise, and the
+    gradient routed to the same window element (ties included: integer-valued inputs
+    make many; torch keeps the first maximum), odd sizes in floor mode."""
+    import ewvit
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randint(-3, 4, shape, generator=g).to(dtype)           # many ties
+    x[0, 0, 0, 0] = float('nan')
+    xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.clone().to(DEV).requires_grad_(True)
+    y = ewvit.maxpool2(xd)
+    yr = torch.nn.functional.max_pool2d(xr, 2)
+    assert y.shape == yr.shape
+    assert torch.equal(torch.nan_to_num(y.float(), 99.0), torch.nan_to_num(yr.float(), 99.0))
+    dy = torch.randn(y.shape, generator=g).to(dtype).to(DEV)
+    y.backward(dy)
+    yr.backward(dy)
+    assert torch.equal(xd.grad.float(), xr.grad.float())
