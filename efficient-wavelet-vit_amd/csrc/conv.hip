@@ -71,6 +71,9 @@ struct FwdArgs {
   // the per-tap K padded up to 64 (the weights packed with that many input channels)
   // and the staging lanes of channels >= KCr (the real count) read zeros
   int KCr = 0;
+  // optional addend of the output (same layout as out, bf16), added before rounding —
+  // the skip connection's gradient folded into the block input's dgrad
+  const bf16_t *addend = nullptr;
 };
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
@@ -829,8 +832,14 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     for (int i = 0; i < 4; ++i) {
       const int64_t row = m0 + wm * 64 + i * 16 + fr;
       if (row < a.M) {
-        const bf16_t h0 = f2bf(acc[i][j][0] + bv.x), h1 = f2bf(acc[i][j][1] + bv.y);
-        const bf16_t h2 = f2bf(acc[i][j][2] + bv.z), h3 = f2bf(acc[i][j][3] + bv.w);
+        float4 av = bv;
+        if (a.addend) {
+          const uint2 q = *reinterpret_cast<const uint2 *>(a.addend + (ob - a.out) + row * a.ogc);
+          av.x += __uint_as_float(q.x << 16); av.y += __uint_as_float(q.x & 0xffff0000u);
+          av.z += __uint_as_float(q.y << 16); av.w += __uint_as_float(q.y & 0xffff0000u);
+        }
+        const bf16_t h0 = f2bf(acc[i][j][0] + av.x), h1 = f2bf(acc[i][j][1] + av.y);
+        const bf16_t h2 = f2bf(acc[i][j][2] + av.z), h3 = f2bf(acc[i][j][3] + av.w);
         uint2 pk;
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
@@ -1345,6 +1354,37 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
     launch_fwd<false>(a, as_stream(stream));
   }
   return launch_status("conv2d_fwd");
+}
+
+// 1 when ewvit_conv2d_bwd_data_add can run this shape (the LDS-DMA dgrad kernel)
+extern "C" int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                               int stride) {
+  if (!use_glds() || Cout % 64 || Cin % 8 || 2 * N * H * W * Cout >= (int64_t)OOB ||
+      Cin * ksize * ksize * Cout * 2 >= (int64_t)OOB)
+    return 0;
+  (void)stride;
+  return 1;
+}
+
+// dx = dgrad(dy) + addend (plain NHWC, bf16): the skip connection's gradient of a
+// residual block added in the dgrad epilogue of the block's first conv
+extern "C" int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N,
+                                         int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                                         void *stream) {
+  EWVIT_CHECK_ARG(dy && wp_t && dx && addend, "conv2d_bwd_data_add: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_bwd_data_add")) return rc;
+  EWVIT_CHECK_ARG(ewvit_conv2d_bwd_data_add_ok(N, H, W, Cin, Cout, ksize, stride),
+                  "conv2d_bwd_data_add: shape not supported (query ewvit_conv2d_bwd_data_add_ok)");
+  FwdArgs a;
+  a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx; a.g = g;
+  a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
+  a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
+  a.sgc = g.Cout; a.sgs = 0; a.ogc = g.Cin; a.ogs = 0;
+  a.addend = (const bf16_t *)addend;
+  EWVIT_CHECK_ARG(launch_glds<true>(a, 2 * N * (int64_t)g.Ho * g.Wo * Cout, as_stream(stream)),
+                  "conv2d_bwd_data_add: LDS-DMA kernel refused the shape");
+  return launch_status("conv2d_bwd_data_add");
 }
 
 extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,

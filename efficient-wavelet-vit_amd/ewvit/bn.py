@@ -102,7 +102,8 @@ class BNDropAddFn(torch.autograd.Function):
     """y = BatchNorm(x) * scale[n] + skip (StochasticDepth(row) drawn in the kernel),
     training mode, one group: the MBConv block tail in one pass each way."""
     @staticmethod
-    def forward(ctx, x, skip, weight, bias, running_mean, running_var, momentum, eps, counter, keep, partials):
+    def forward(ctx, x, skip, weight, bias, running_mean, running_var, momentum, eps, counter, keep, partials,
+                link=None):
         from .ops import _seed
         L.require_gpu(x, skip)
         xc, M, C = _rows(x)
@@ -126,6 +127,7 @@ class BNDropAddFn(torch.autograd.Function):
                work={'bytes': (3 + int(partials is None)) * xc.numel() * xc.element_size()})
         ctx.save_for_backward(xc, weight, bias, mean, invstd, scale)
         ctx.cfg = (M, C, M // N, skip.dtype)
+        ctx.link = link if link is not None and link.armed else None
         return y
 
     @staticmethod
@@ -140,10 +142,17 @@ class BNDropAddFn(torch.autograd.Function):
         L.call('ewvit_bn_bwd_scaled', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(mean), L.ptr(invstd), L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(ws), L.stream(dx),
                work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return dx, dy.to(sdt), dg, db, None, None, None, None, None, None, None
+        if ctx.link is not None:
+            # the skip gradient goes to the block's first conv (ewvit.conv.SkipLink), which
+            # adds it to its input gradient in the dgrad epilogue
+            ctx.link.grad = dy
+            dskip = None
+        else:
+            dskip = dy.to(sdt)
+        return dx, dskip, dg, db, None, None, None, None, None, None, None, None
 
 
-def batch_norm_drop_add(x, bn, skip, drop_prob, partials=None):
+def batch_norm_drop_add(x, bn, skip, drop_prob, partials=None, link=None):
     """StochasticDepth(p=drop_prob, mode='row')(bn(x)) + skip in one pass (training):
     the keep mask is drawn in the kernel (ewvit dropout's counter hash of a per-call
     seed and the step counter); `partials` as in batch_norm_act."""
@@ -151,4 +160,4 @@ def batch_norm_drop_add(x, bn, skip, drop_prob, partials=None):
         raise ValueError('batch_norm_drop_add: training-mode BatchNorm with a momentum only')
     counter = bn.num_batches_tracked if bn.track_running_stats else None
     return BNDropAddFn.apply(x, skip, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
-                             counter, 1.0 - float(drop_prob), partials)
+                             counter, 1.0 - float(drop_prob), partials, link)

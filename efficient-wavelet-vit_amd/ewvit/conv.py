@@ -29,6 +29,39 @@ _registry = {}      # id(weight) -> {'ref', 'cin_pad', 'wp', 'wpt', 'bwd'}
 _active = False
 
 
+class SkipLink:
+    """Folds a residual block's skip gradient into its first conv's input gradient.
+    The block offers the link for its input x (`offer`); the conv whose input IS x takes it
+    in forward (`armed`); in backward the block tail (ewvit.bn.BNDropAddFn) leaves dy in
+    `grad` instead of returning it, and the conv's dgrad adds it in its epilogue — no
+    separate accumulation add for x."""
+    __slots__ = ('key', 'armed', 'grad')
+
+    def __init__(self, x):
+        self.key = (x.data_ptr(), tuple(x.shape), x.dtype)
+        self.armed = False
+        self.grad = None
+
+
+_offered = None
+
+
+def offer_skip_link(x):
+    global _offered
+    _offered = SkipLink(x)
+    return _offered
+
+
+def _take_link(x):
+    global _offered
+    link = _offered
+    if link is not None and link.key == (x.data_ptr(), tuple(x.shape), x.dtype):
+        _offered = None
+        link.armed = True
+        return link
+    return None
+
+
 def _register(weight, cin_pad, bwd):
     e = _registry.get(id(weight))
     if e is not None and e['ref']() is weight and e['cin_pad'] == cin_pad:
@@ -120,6 +153,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
         L.require_gpu(x, weight)
+        ctx.link = _take_link(x) if levels == 1 else None
         NL, Cz, H, W = x.shape
         if NL % levels:
             raise ValueError(f'conv2d: batch {NL} is not a multiple of levels={levels}')
@@ -168,13 +202,26 @@ class Conv2dFn(torch.autograd.Function):
         Ho, Wo = dy.shape[2], dy.shape[3]
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
+        link = ctx.link
+        skip = link.grad if link is not None else None
+        if link is not None:
+            link.grad = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * H * W * Cx * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, stride, gc, gs,
-                   L.stream(dx), work=work)
+            if skip is not None and L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
+                # the residual block's skip gradient added in the dgrad epilogue
+                sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                L.call('ewvit_conv2d_bwd_data_add', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), L.ptr(sk), N, H, W, Cx, Cout,
+                       k, stride, L.stream(dx), work=work)
+                skip = None
+            else:
+                L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, stride, gc,
+                       gs, L.stream(dx), work=work)
             if xdt != torch.bfloat16:
                 dx = dx.to(xdt)
+            if skip is not None:
+                dx = dx + skip.to(dx.dtype)
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
             wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
@@ -192,6 +239,8 @@ class Conv2dFn(torch.autograd.Function):
             if ctx.needs_input_grad[1]:
                 dw = dwf
             db = dbf
+        if dx is None and skip is not None:       # x needs no gradient through the conv, only the skip's
+            dx = skip
         return dx, dw, db, None, None, None
 
 

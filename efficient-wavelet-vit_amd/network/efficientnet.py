@@ -24,6 +24,8 @@ import ewvit
 # most this many 128-row output tiles: every BN apply block re-reads all partial rows
 # while finalising, so the fusion pays only for small maps
 _EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '32'))
+# residual blocks hand their skip gradient to the first conv's dgrad epilogue (SkipLink)
+_SKIP_LINK = os.environ.get('EWVIT_SKIP_LINK', '1') != '0'
 
 STAGES = (
     ('fused', 1, 3, 1, 24, 24, 2),
@@ -99,12 +101,12 @@ class ConvBNAct(nn.Sequential):
                 and x.is_cuda and not self._hooked() and self[0].out_channels % 8 == 0
                 and self[0].out_channels <= 4096)
 
-    def forward_drop_add(self, x, skip, drop_prob):
+    def forward_drop_add(self, x, skip, drop_prob, link=None):
         """StochasticDepth(bn(conv(x))) + skip: BN, drop-path and the skip add in one pass."""
         r = self._conv_stats(x)
         if r is not None:
-            return ewvit.batch_norm_drop_add(r[0], self[1], skip, drop_prob, partials=r[1])
-        return ewvit.batch_norm_drop_add(self[0](x), self[1], skip, drop_prob)
+            return ewvit.batch_norm_drop_add(r[0], self[1], skip, drop_prob, partials=r[1], link=link)
+        return ewvit.batch_norm_drop_add(self[0](x), self[1], skip, drop_prob, link=link)
 
     def forward(self, x):
         conv, bn = self[0], self[1]
@@ -156,11 +158,14 @@ class _Block(nn.Module):
         last = self.block[-1]
         if (self.use_res_connect and self.training and isinstance(last, ConvBNAct) and last.can_drop_add(x)
                 and r_ok(x) and not self._forward_hooks and not self.block._forward_hooks):
-            # the block tail (project BN + drop-path + skip add) as one pass each way
+            # the block tail (project BN + drop-path + skip add) as one pass each way; the
+            # skip's gradient is added in the first conv's dgrad epilogue (SkipLink)
+            link = ewvit.conv.offer_skip_link(x) if torch.is_grad_enabled() and _SKIP_LINK else None
             h = x
             for m in list(self.block)[:-1]:
                 h = m(h)
-            return last.forward_drop_add(h, x, self.sd_prob)
+            ewvit.conv._offered = None
+            return last.forward_drop_add(h, x, self.sd_prob, link)
         r = self.block(x)
         if self.use_res_connect:
             if self.training and self.sd_prob > 0.0 and r.is_cuda and r.dtype in (torch.bfloat16, torch.float32) \

@@ -285,6 +285,13 @@ int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, 
 int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
                           int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
                           int64_t dx_group_stride, void *stream);
+/* dx = dgrad(dy) + addend (plain NHWC bf16, same layout as dx): a residual block's skip
+ * gradient added in the epilogue of its first conv's input gradient (no separate add).
+ * Supported when ewvit_conv2d_bwd_data_add_ok(...) returns 1 (the LDS-DMA kernel). */
+int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                     int stride);
+int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N, int64_t H,
+                              int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, void *stream);
 /* bytes of f32 split-K workspace for ewvit_conv2d_bwd_weight. */
 int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                           int ksize, int stride);
