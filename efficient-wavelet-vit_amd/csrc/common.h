@@ -91,6 +91,29 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// Cross-lane sums on DPP / v_permlane*_swap (VALU) instead of ds_bpermute: every
+// lane of the group ends with the group's sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// the 16 lanes of a DPP row (lanes 16r .. 16r+15)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_mov<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);    // row_half_mirror
+  v += dpp_mov<0x140>(v);    // row_mirror
+  return v;
+}
+// lanes l, l^16, l^32, l^48 (the 4 rows of the wave)
+__device__ __forceinline__ float rows_sum4(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = __int_as_float(a[0]) + __int_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(b[0]) + __int_as_float(b[1]);
+}
+__device__ __forceinline__ float wave_sum(float v) { return rows_sum4(row_sum16(v)); }
+
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }

@@ -445,8 +445,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     // in a wave, then the 4 waves through LDS (the staging buffers are free now)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bsum[j] += __shfl_xor(bsum[j], 16, 64);
-      bsum[j] += __shfl_xor(bsum[j], 32, 64);
+      bsum[j] = rows_sum4(bsum[j]);
     }
     float *red = reinterpret_cast<float *>(&smem[0][0][0]);  // [4 waves][16 chunks][8]
     if (lane < 16)
@@ -855,16 +854,14 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   }
   if (!stats) return;
   // BatchNorm partial statistics of this m-tile: the 16 row lanes of each column
-  // (xor tree), then the BM/64 waves that share a column block through LDS, in order
+  // (DPP row sums), then the BM/64 waves that share a column block through LDS, in order
 #pragma unroll
   for (int j = 0; j < J; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        cs[j][r] += __shfl_xor(cs[j][r], o, 64);
-        cq[j][r] += __shfl_xor(cq[j][r], o, 64);
-      }
+    for (int r = 0; r < 4; ++r) {
+      cs[j][r] = row_sum16(cs[j][r]);
+      cq[j][r] = row_sum16(cq[j][r]);
+    }
   __syncthreads();                         // every wave is done reading the staging ring
   float *red = reinterpret_cast<float *>(smem);   // [BM/64][BN_][2]
   if (fr == 0)
@@ -1040,8 +1037,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
     // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bsum[j] += __shfl_xor(bsum[j], 16, 64);
-      bsum[j] += __shfl_xor(bsum[j], 32, 64);
+      bsum[j] = rows_sum4(bsum[j]);
     }
     float *red = reinterpret_cast<float *>(smem);
     if (lane < 16)

@@ -353,9 +353,8 @@ __global__ __launch_bounds__(256) void dw_bwd_weight_partial_kernel(const void *
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = acc[k][j];
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+      v += dpp_mov<0x128>(v);   // row_ror:8 = lane ^ 8 within the row
+      v = rows_sum4(v);
       acc[k][j] = v;
     }
   if (lane < 8) {

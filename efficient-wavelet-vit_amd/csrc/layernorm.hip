@@ -9,12 +9,6 @@ namespace ewvit {
 
 constexpr int LN_MAXV = 16;  // up to D = 1024 per wave
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *x, int xdt, int64_t ldx,
                                                      const float *gamma, const float *beta, void *y,
                                                      int ydt, float *mean, float *rstd, int64_t M,

@@ -240,8 +240,7 @@ __global__ __launch_bounds__(256) void se_mlp_h1_part_kernel(const float *__rest
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      v[q] = wave_sum(v[q]);
       const int j = j0 + 4 * q;
       if (lane == 0 && j < Csq) pp[j] = v[q];
     }
@@ -342,8 +341,7 @@ __global__ __launch_bounds__(256) void se_mlp_dh_part_kernel(const float *__rest
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      v[q] = wave_sum(v[q]);
       const int j = j0 + 4 * q;
       if (lane == 0 && j < Csq) pp[j] = v[q];
     }
@@ -502,8 +500,7 @@ __global__ __launch_bounds__(256) void se_sq_h1_part_kernel(const void *__restri
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      v[q] = wave_sum(v[q]);
       const int j = j0 + 4 * q;
       if (lane == 0 && j < Csq) pp[j] = v[q];
     }
@@ -535,8 +532,7 @@ __global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restri
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+      v[q] = wave_sum(v[q]);
       const int j = j0 + 4 * q;
       if (lane == 0 && j < Csq) pp[j] = v[q];
     }

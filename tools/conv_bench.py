@@ -62,6 +62,7 @@ def main():
     ap.add_argument('--shape', action='append', default=[],
                     help='extra shape N,Cin,H,W,Cout,k,stride,levels (repeatable; replaces the table)')
     ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged')
+    ap.add_argument('--bnstats', action='store_true', help='time fwd against fwd with BN statistics in the epilogue')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
     global EAGER
@@ -101,6 +102,15 @@ def main():
             L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, s, gc, gs,
                    L.stream(y))
 
+        rows_bn = int(lib.ewvit_conv2d_fwd_bn_rows(N, H, W, Cx, Cout, k, s))
+        part = torch.empty(max(1, (N * Ho * Wo + max(rows_bn, 1) - 1) // max(rows_bn, 1)), 2 * Cout, device=dev)
+        shift = torch.zeros(Cout, device=dev)
+        shift_out = torch.empty(Cout, device=dev)
+
+        def fwd_bn():
+            L.call('ewvit_conv2d_fwd_bn', L.ptr(z), L.ptr(wp), None, L.ptr(y), N, H, W, Cx, Cout, k, s, gc, gs,
+                   L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y))
+
         def wgrad():
             L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), None, 0, N, H, W, Cx, Cout, k, s,
                    gc, gs, Cx, dw.stride(0), dw.stride(1), dw.stride(3), L.ptr(ws), L.stream(y))
@@ -108,12 +118,15 @@ def main():
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
                 lib.ewvit_conv2d_set_glds(v)
-                for pn, fn in (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad)):
+                phases = (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad))
+                if a.bnstats and rows_bn > 0:
+                    phases = (('fwd', fwd), ('fwd_bn', fwd_bn))
+                for pn, fn in phases:
                     rows.setdefault((v, pn), []).append(graph_time(fn, a.iters))
         lib.ewvit_conv2d_set_glds(1)
         for v in a.variants:
             parts = []
-            for pn in ('fwd', 'dgrad', 'wgrad'):
+            for pn in (('fwd', 'fwd_bn') if a.bnstats and rows_bn > 0 else ('fwd', 'dgrad', 'wgrad')):
                 t = min(rows[(v, pn)])
                 parts.append(f'{pn} {t:8.1f} us {flops / t / 1e6:6.0f} TF/s')
             print(f'{name:15s} [{f"glds{v}" if v else "regs "}] ' + ' | '.join(parts), flush=True)
