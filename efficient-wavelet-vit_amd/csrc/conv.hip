@@ -676,8 +676,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
   const int K = KS * KS * a.KC;
-  const int nk = K / BK;
-  const int cbn = a.KC / BK;
+  const int cbn = (a.KC + BK - 1) / BK;   // ragged KC: the last block's lanes >= KC read zeros
+  const int nk = KS * KS * cbn;
   const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
@@ -1133,13 +1133,31 @@ static void launch_fwd(const FwdArgs &a, hipStream_t s) {
   else launch_fwd_ks<DGRAD, 3>(a, s);
 }
 
+static int conv_ragged() {
+  static int v = [] {
+    const char *e = getenv("EWVIT_CONV_RAGGED");   // 0: K % 64 != 0 takes the register-staged kernel
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // the LDS-DMA fwd/dgrad kernel when every K-tile stays in one tap and one channel
 // group and the operands fit 31-bit buffer offsets; false -> register-staged kernel
 template <bool DGRAD>
 static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
   const bool padded = a.KCr && a.KCr != a.KC;     // plain x, channels padded to 64 per tap
-  if (!use_glds() || a.KC % 64 || (padded ? a.sgc != a.KCr : a.sgc % 64) || src_bytes >= (int64_t)OOB ||
+  // ragged: plain (ungrouped) x whose per-tap K is not a multiple of 64 — the last
+  // 64-channel block of each tap zero-fills its A lanes >= KC and reads finite weights
+  // of the next tap / row (or zeros past the end) for B, which meet only zeros
+  // (only while the zero lanes stay <= 20 % of K: K = 48 per tap measured slower than
+  // the register-staged kernel, K = 160 -> 3 blocks 17 % faster)
+  const bool ragged = !padded && a.KC % 64 != 0;
+  if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 ||
+                 5 * ((a.KC + 63) / 64 * 64) > 6 * a.KC))
+    return false;
+  if (!use_glds() || (!ragged && a.KC % 64) || (padded ? a.sgc != a.KCr : (!ragged && a.sgc % 64)) ||
+      src_bytes >= (int64_t)OOB ||
       a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
@@ -1355,7 +1373,8 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
 // 1 when ewvit_conv2d_bwd_data_add can run this shape (the LDS-DMA dgrad kernel)
 extern "C" int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                                                int stride) {
-  if (!use_glds() || Cout % 64 || Cin % 8 || 2 * N * H * W * Cout >= (int64_t)OOB ||
+  if (!use_glds() || (Cout % 64 && (!conv_ragged() || Cout % 8 || 5 * ((Cout + 63) / 64 * 64) > 6 * Cout)) ||
+      Cin % 8 || 2 * N * H * W * Cout >= (int64_t)OOB ||
       Cin * ksize * ksize * Cout * 2 >= (int64_t)OOB)
     return 0;
   (void)stride;

@@ -49,6 +49,10 @@ def rel(a, b):
     (2, 192, 192, 160, 9, 9, 1, 3),      # 3x3, few tiles, 27 K-tiles
     (2, 160, 160, 64, 9, 9, 1, 1),       # Cin 160: LDS-DMA fwd with K padded to 192 per tap
     (2, 160, 160, 48, 11, 10, 2, 3),     # the same, 3x3 stride 2
+    (2, 960, 960, 160, 7, 7, 1, 1),      # 1x1 project: dgrad K = 160 per tap (ragged last K-tile)
+    (2, 192, 192, 48, 14, 14, 1, 1),     # dgrad K = 48: one ragged K-tile
+    (2, 48, 48, 192, 15, 14, 1, 3),      # 3x3 fwd Cin 48: ragged K-tile in every tap
+    (1, 16, 16, 64, 20, 19, 1, 3),       # Cin 16 (the MWT seperate conv's input)
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec
