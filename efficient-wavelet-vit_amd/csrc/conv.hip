@@ -74,6 +74,13 @@ struct FwdArgs {
   // optional addend of the output (same layout as out, bf16), added before rounding —
   // the skip connection's gradient folded into the block input's dgrad
   const bf16_t *addend = nullptr;
+  // stride-2 3x3 dgrad by output parity class (LDS-DMA kernel): the GEMM rows are the
+  // dx pixels (2i + py, 2j + px) of class pc = 2*py + px on an outH x outW grid, and
+  // only the class's ntap live taps tapl[] run (dy pixel (i + dh, j + dw)); the
+  // epilogue scatters row (n, i, j) to dx pixel (n, 2i + py, 2j + px) of dstH x dstW
+  int pc = -1, ntap = 0;
+  int tapl[4] = {0, 0, 0, 0};
+  int dstH = 0, dstW = 0;
 };
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
@@ -677,7 +684,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const int n0 = (tile % ntn) * BN_;
   const int K = KS * KS * a.KC;
   const int cbn = (a.KC + BK - 1) / BK;   // ragged KC: the last block's lanes >= KC read zeros
-  const int nk = KS * KS * cbn;
+  const bool cls = DGRAD && KS == 3 && a.pc >= 0;
+  const int py = a.pc >> 1, px = a.pc & 1;
+  const int ntaps = cls ? a.ntap : KS * KS;
+  const int nk = ntaps * cbn;
   const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
@@ -702,6 +712,14 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     const int n = (int)(t / a.outH);
     int by, bx;            // base pixel (may lie outside the image)
     unsigned msk = 0;
+    if (cls) {
+      // class taps: dy pixel (oh + dh, ow + dw), dh = (py + 1 - kh) / 2 in {0, 1}
+      for (int lt = 0; lt < a.ntap; ++lt) {
+        const int tp = a.tapl[lt], kh = tp / 3, kw = tp - kh * 3;
+        const int sh = oh + ((py + 1 - kh) >> 1), sw = ow + ((px + 1 - kw) >> 1);
+        if (m < a.M && sh < a.srcH && sw < a.srcW) msk |= 1u << lt;
+      }
+    } else
 #pragma unroll
     for (int kh = 0; kh < KS; ++kh)
 #pragma unroll
@@ -719,6 +737,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
         if (ok) msk |= 1u << (kh * KS + kw);
       }
     if (!DGRAD) { by = oh * a.g.stride - a.g.pad; bx = ow * a.g.stride - a.g.pad; }
+    else if (cls) { by = oh; bx = ow; }
     else        { by = (oh + a.g.pad) >> ls;       bx = (ow + a.g.pad) >> ls; }
     const int64_t pix = (int64_t)n * a.srcH * a.srcW + (int64_t)by * a.srcW + bx;
     rb[j] = (int)((pix * a.sgc + lc * 8) * 2);
@@ -739,15 +758,17 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // XCD's L2 to serve the tap re-reads; otherwise taps are outer.
   int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
   auto stage = [&](int kt, int buf) {
-    const int kh = ltap / KS, kw = ltap - kh * KS;
+    const int rt = cls ? a.tapl[ltap] : ltap;      // the weight tap
+    const int kh = rt / KS, kw = rt - kh * KS;
     int dpix;
     if (!DGRAD) dpix = kh * a.srcW + kw;
+    else if (cls) dpix = ((py + 1 - kh) >> 1) * a.srcW + ((px + 1 - kw) >> 1);
     else dpix = -((kh >> ls) * a.srcW + (kw >> ls));
     const int sdelta = (int)(((int64_t)dpix * a.sgc + (int64_t)lgi * a.sgs + lcin) * 2);
     const int tap = ltap, c0 = lcin;
-    const uint32_t kb = (uint32_t)((ltap * a.KC + lcb * BK) * 2);
+    const uint32_t kb = (uint32_t)((rt * a.KC + lcb * BK) * 2);
     if (tap_inner) {
-      if (++ltap == KS * KS) {
+      if (++ltap == ntaps) {
         ltap = 0; ++lcb;
         lcin += BK;
         if (lcin == a.sgc) { lcin = 0; ++lgi; }
@@ -814,6 +835,19 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
   // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
   const bool stats = a.bn_part != nullptr;
+  int64_t opx[4];               // parity-class dgrad: the dx pixel of each of this lane's rows
+  if (cls) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = m0 + wm * 64 + i * 16 + fr;
+      const int64_t rr = row < a.M ? row : 0;
+      const int ow = (int)(rr % a.outW);
+      const int64_t t = rr / a.outW;
+      const int oh = (int)(t % a.outH);
+      const int64_t n = t / a.outH;
+      opx[i] = (n * a.dstH + 2 * oh + py) * a.dstW + 2 * ow + px;
+    }
+  }
   float cs[J][4], cq[J][4];     // this lane's column sums over its 4 rows (BN statistics)
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -831,9 +865,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     for (int i = 0; i < 4; ++i) {
       const int64_t row = m0 + wm * 64 + i * 16 + fr;
       if (row < a.M) {
+        const int64_t opix = cls ? opx[i] : row;
         float4 av = bv;
         if (a.addend) {
-          const uint2 q = *reinterpret_cast<const uint2 *>(a.addend + (ob - a.out) + row * a.ogc);
+          const uint2 q = *reinterpret_cast<const uint2 *>(a.addend + (ob - a.out) + opix * a.ogc);
           av.x += __uint_as_float(q.x << 16); av.y += __uint_as_float(q.x & 0xffff0000u);
           av.z += __uint_as_float(q.y << 16); av.w += __uint_as_float(q.y & 0xffff0000u);
         }
@@ -842,7 +877,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
         uint2 pk;
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
-        *reinterpret_cast<uint2 *>(ob + row * a.ogc) = pk;
+        *reinterpret_cast<uint2 *>(ob + opix * a.ogc) = pk;
         if (stats) {
           const float d0 = bf2f(h0) - kv.x, d1 = bf2f(h1) - kv.y, d2 = bf2f(h2) - kv.z, d3 = bf2f(h3) - kv.w;
           cs[j][0] += d0; cs[j][1] += d1; cs[j][2] += d2; cs[j][3] += d3;
@@ -1153,8 +1188,9 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   // (only while the zero lanes stay <= 20 % of K: K = 48 per tap measured slower than
   // the register-staged kernel, K = 160 -> 3 blocks 17 % faster)
   const bool ragged = !padded && a.KC % 64 != 0;
+  // (a parity-class dgrad, which already skips 3/4 of the taps, up to 1/3)
   if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 ||
-                 5 * ((a.KC + 63) / 64 * 64) > 6 * a.KC))
+                 (a.pc >= 0 ? 2 * ((a.KC + 63) / 64 * 64) > 3 * a.KC : 5 * ((a.KC + 63) / 64 * 64) > 6 * a.KC)))
     return false;
   if (!use_glds() || (!ragged && a.KC % 64) || (padded ? a.sgc != a.KCr : (!ragged && a.sgc % 64)) ||
       src_bytes >= (int64_t)OOB ||
@@ -1370,6 +1406,51 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
   return launch_status("conv2d_fwd");
 }
 
+static int dgrad_parity() {
+  static int v = [] {
+    const char *e = getenv("EWVIT_DGRAD_PARITY");   // 0: stride-2 dgrad masks 3/4 of 9 taps per row
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// stride-2 3x3 dgrad as 4 launches, one per output parity class (py, px), each over
+// only its live taps (1, 2, 2 and 4 of the 9); false when the LDS-DMA kernel cannot
+// take the class launches (nothing launched)
+static bool dgrad_by_parity(FwdArgs a, int64_t src_bytes, hipStream_t s) {
+  if (!dgrad_parity() || a.g.ks != 3 || a.g.stride != 2 || a.g.pad != 1 || a.ogs != 0 || a.sgs != 0 ||
+      !use_glds() || (glds_variant() & 7) == 0)
+    return false;
+  const int H = a.outH, W = a.outW;
+  FwdArgs c[4];
+  for (int pc = 0; pc < 4; ++pc) {
+    const int py = pc >> 1, px = pc & 1;
+    c[pc] = a;
+    c[pc].pc = pc;
+    c[pc].dstH = H; c[pc].dstW = W;
+    c[pc].outH = (H - py + 1) / 2; c[pc].outW = (W - px + 1) / 2;
+    c[pc].M = (int64_t)a.g.N * c[pc].outH * c[pc].outW;
+    int nt = 0;
+    for (int kh = 0; kh < 3; ++kh)
+      for (int kw = 0; kw < 3; ++kw)
+        if (((py + 1 - kh) & 1) == 0 && ((px + 1 - kw) & 1) == 0) c[pc].tapl[nt++] = kh * 3 + kw;
+    c[pc].ntap = nt;
+  }
+  // the KC / layout checks of launch_glds do not depend on the class: probe class 3's
+  // shape first so a refusal launches nothing
+  int order[4] = {3, 0, 1, 2};
+  for (int q = 0; q < 4; ++q) {
+    const int pc = order[q];
+    if (c[pc].M == 0) continue;
+    if (!launch_glds<true>(c[pc], src_bytes, s)) {
+      if (q == 0) return false;
+      set_error("conv2d_bwd_data: parity class %d refused after class 3 ran", pc);
+      return false;
+    }
+  }
+  return true;
+}
+
 // 1 when ewvit_conv2d_bwd_data_add can run this shape (the LDS-DMA dgrad kernel)
 extern "C" int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                                                int stride) {
@@ -1397,7 +1478,8 @@ extern "C" int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void 
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
   a.sgc = g.Cout; a.sgs = 0; a.ogc = g.Cin; a.ogs = 0;
   a.addend = (const bf16_t *)addend;
-  EWVIT_CHECK_ARG(launch_glds<true>(a, 2 * N * (int64_t)g.Ho * g.Wo * Cout, as_stream(stream)),
+  const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
+  EWVIT_CHECK_ARG(dgrad_by_parity(a, sb, as_stream(stream)) || launch_glds<true>(a, sb, as_stream(stream)),
                   "conv2d_bwd_data_add: LDS-DMA kernel refused the shape");
   return launch_status("conv2d_bwd_data_add");
 }
@@ -1414,7 +1496,9 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
   a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
   a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
-  if (!launch_glds<true>(a, 2 * N * (int64_t)g.Ho * g.Wo * Cout, as_stream(stream))) launch_fwd<true>(a, as_stream(stream));
+  const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
+  if (!dgrad_by_parity(a, sb, as_stream(stream)) && !launch_glds<true>(a, sb, as_stream(stream)))
+    launch_fwd<true>(a, as_stream(stream));
   return launch_status("conv2d_bwd_data");
 }
 
