@@ -6,6 +6,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
+# a counter pass serialises ~1500 dispatches per step and prints nothing until it ends:
+# report the growth of its output directory once a minute so the run is seen alive
+( while sleep 60; do du -sk "$O"/pmc_* 2>/dev/null | tr '\n' ' ' >> "$O/pmc_progress.log"; echo >> "$O/pmc_progress.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_$C" -o run -- \
       python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_$C.log" 2>&1
