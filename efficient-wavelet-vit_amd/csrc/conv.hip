@@ -927,16 +927,17 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 // 256-B rows, chunk c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed,
 // ds_read_b64_tr_b16).  Bias gradient (sum of dy over pixels): the blocks of n'-tile
 // t sum the dy image of the K-tiles kt = t (mod n'-tiles), spreading the extra reads.
-template <int KS, int BK, int NS>
+template <int KS, int BK, int NS, int WJ = 4>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
-  constexpr int IMG = BK * 256, STG = 2 * IMG;
+  constexpr int NB = WJ / 4;         // 128-column x images per stage (n'-tile of 128 * NB)
+  constexpr int IMG = BK * 256, STG = (1 + NB) * IMG;
   constexpr int P = BK / 16;        // pieces (4 rows x 256 B) per wave per image
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
-  const int co0 = ty * 128, np0 = tx * 128;
+  const int co0 = ty * 128, np0 = tx * 128 * NB;
   const int NP = KS * KS * a.g.Cin;
   const int64_t mbeg = (int64_t)split * a.mper;
   const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
@@ -949,8 +950,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   // plus r, carried through (ow, oh) with exact multiply-high divisions (r < 64).
   const int ws = __builtin_amdgcn_readfirstlane(w);
   const int wm = ws >> 1, wn = ws & 1;
-  int rr[P], tkh[P], tkw[P], aoff[P], bgo[P];
-  bool bok[P], aok[P];
+  int rr[P], aoff[P], tkh[NB * P], tkw[NB * P], bgo[NB * P];
+  bool aok[P], bok[NB * P];
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const int p = ws * P + j, r = p * 4 + (lane >> 4);
@@ -958,14 +959,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
     rr[j] = r;
     aok[j] = co0 + lc * 8 < a.g.Cout;
     aoff[j] = (int)(((mbeg + r) * a.g.Cout + co0 + lc * 8) * 2);
-    const int np = np0 + lc * 8;
-    bok[j] = np < NP;
-    const int btap = bok[j] ? np / a.g.Cin : 0;
-    const int bci = bok[j] ? np - btap * a.g.Cin : 0;
-    tkh[j] = btap / KS - a.g.pad;
-    tkw[j] = btap % KS - a.g.pad;
-    const int gi = bci / a.xgc;
-    bgo[j] = (int)(((int64_t)gi * a.xgs + (bci - gi * a.xgc)) * 2);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int e = b * P + j;
+      const int np = np0 + b * 128 + lc * 8;
+      bok[e] = np < NP;
+      const int btap = bok[e] ? np / a.g.Cin : 0;
+      const int bci = bok[e] ? np - btap * a.g.Cin : 0;
+      tkh[e] = btap / KS - a.g.pad;
+      tkw[e] = btap % KS - a.g.pad;
+      const int gi = bci / a.xgc;
+      bgo[e] = (int)(((int64_t)gi * a.xgs + (bci - gi * a.xgc)) * 2);
+    }
   }
   // exact floor(x / d) = umulhi(x, ceil(2^32 / d)) for x < 2^32 / d
   const uint32_t magW = (uint32_t)((0x100000000ull + a.g.Wo - 1) / a.g.Wo);
@@ -988,9 +993,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
       const uint32_t q2 = __umulhi(oht, magH);
       const int oh = (int)(oht - q2 * a.g.Ho);
       const int n = sn + (int)q2;
-      const int ih = oh * a.g.stride + tkh[j], iw = ow * a.g.stride + tkw[j];
-      const bool ok = rr[j] < lim && bok[j] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W;
-      glds16(rx, base + IMG + j * 1024, ok ? (uint32_t)(((n * a.g.H + ih) * a.g.W + iw) * xrow + bgo[j]) : OOB);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int e = b * P + j;
+        const int ih = oh * a.g.stride + tkh[e], iw = ow * a.g.stride + tkw[e];
+        const bool ok = rr[j] < lim && bok[e] && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W;
+        glds16(rx, base + (1 + b) * IMG + j * 1024,
+               ok ? (uint32_t)(((n * a.g.H + ih) * a.g.W + iw) * xrow + bgo[e]) : OOB);
+      }
     }
     sow += BK;                                      // next K-tile's first pixel (scalar)
     while (sow >= a.g.Wo) {
@@ -1006,17 +1016,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   };
   const bool do_bias = a.dbias_part != nullptr;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  cf32x4 acc[4][4];
+  cf32x4 acc[4][WJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WJ; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4;
   auto compute = [&](int kt, int buf) {
-    const unsigned char *As = smem + buf * STG, *Bs = As + IMG;
+    const unsigned char *As = smem + buf * STG;
+    // wave column wn: 64 columns of the one x image (WJ 4), or a whole image (WJ 8)
+    const unsigned char *Bs = As + IMG + (NB > 1 ? wn * IMG : 0);
+    const int bc0 = NB > 1 ? 0 : wn * 64;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      cbf16x8 af[4], bfr[4];
+      cbf16x8 af[4], bfr[WJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const cs4 lo = tr_read(As, ks * 32 + 8 * g, wm * 64 + i * 16);
@@ -1025,16 +1038,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
                                                 lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const cs4 lo = tr_read(Bs, ks * 32 + 8 * g, wn * 64 + j * 16);
-        const cs4 hi = tr_read(Bs, ks * 32 + 8 * g + 4, wn * 64 + j * 16);
+      for (int j = 0; j < WJ; ++j) {
+        const cs4 lo = tr_read(Bs, ks * 32 + 8 * g, bc0 + j * 16);
+        const cs4 hi = tr_read(Bs, ks * 32 + 8 * g + 4, bc0 + j * 16);
         bfr[j] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
                                                  lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < WJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (do_bias && kt % ntx == tx) {
       // thread t: rows (t>>4)*(BK/16) .. of the dy image, chunk t & 15 (8 channels)
@@ -1058,7 +1071,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   }
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    wait_tile<2 * P, NS>(nk - 1 - kt);
+    wait_tile<(1 + NB) * P, NS>(nk - 1 - kt);
     if (ld < nk) {
       stage(ld, lbuf);
       ++ld;
@@ -1089,8 +1102,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   }
   float *dst = a.part + (int64_t)split * a.g.Cout * NP;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = np0 + wn * 64 + j * 16 + (lane & 15);
+  for (int j = 0; j < WJ; ++j) {
+    const int col = np0 + wn * 16 * WJ + j * 16 + (lane & 15);
     if (col >= NP) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1507,11 +1520,34 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
 // split of the pixel reduction: at most 512 workgroups — the 2 per CU that registers
 // and LDS allow, so every split runs in the first (only) round — >= 4 K-tiles of 64
 // pixels per split, and f32 partial slabs no larger than 4x the bf16 operands
-static int64_t wgrad_splits(const ConvGeom &g) {
+// Wide n'-tiles (128 x 256 per block, each wave 64 x 128: a quarter fewer LDS and L2
+// bytes per MFMA): EWVIT_CONV_WGW = 0 off, 1 (64 pixels, ring 2; 96 KB LDS, 1 block
+// per CU), 2 (32, 2; 48 KB), 3 (32, 3; 72 KB), taken when n' >= 256 and the last
+// 256-column tile wastes <= 1/8 of n'; 4 (default) = 2 for n' >= 2048 over >= 64K pixels
+// (multiscale_fusion 384 -> 128, 3x3, 64 x 112^2: 951 -> 850 us; measured slower on
+// freq_conv's n' = 1152 and on every backbone 1x1, which keep the 128-column tiles).
+static int g_wgw = -1;
+static int wgw_variant() {
+  if (g_wgw < 0) {
+    const char *e = getenv("EWVIT_CONV_WGW");
+    const int x = e ? atoi(e) : 4;
+    g_wgw = (x < 0 || x > 4) ? 4 : x;
+  }
+  return g_wgw;
+}
+static int wgrad_wide(const ConvGeom &g) {
+  const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
+  int v = wgw_variant();
+  if (v == 4) v = (NP >= 2048 && (int64_t)g.N * g.Ho * g.Wo >= 65536) ? 2 : 0;
+  if (!v || NP < 256 || ((NP + 255) / 256 * 256 - NP) * 8 > NP) return 0;
+  return v;
+}
+static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   const int64_t M = (int64_t)g.N * g.Ho * g.Wo;
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
-  const int64_t tiles = ((NP + CBN - 1) / CBN) * ((g.Cout + CBM - 1) / CBM);
-  int64_t s = 512 / tiles;
+  const int64_t tn = wide ? 2 * CBN : CBN;
+  const int64_t tiles = ((NP + tn - 1) / tn) * ((g.Cout + CBM - 1) / CBM);
+  int64_t s = (wide == 1 ? 256 : 512) / tiles;
   const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;
   const int64_t cap = 2 * M * ((int64_t)g.Cin + g.Cout) / ((int64_t)g.Cout * NP);
@@ -1520,11 +1556,22 @@ static int64_t wgrad_splits(const ConvGeom &g) {
   return s;
 }
 
+extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {
+  const int prev = wgw_variant();
+  g_wgw = variant >= 0 && variant <= 4 ? variant : 4;
+  return prev;
+}
+
 extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                                      int ksize, int stride) {
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
   const int64_t ntx = (ksize * ksize * Cin + CBN - 1) / CBN;
-  return wgrad_splits(g) * Cout * (ksize * ksize * Cin + ntx) * (int64_t)sizeof(float);
+  const int64_t narrow = wgrad_splits(g) * Cout * (ksize * ksize * Cin + ntx) * (int64_t)sizeof(float);
+  const int wide = wgrad_wide(g);
+  if (!wide) return narrow;
+  const int64_t ntw = (ksize * ksize * Cin + 2 * CBN - 1) / (2 * CBN);
+  const int64_t wb = wgrad_splits(g, wide) * Cout * (ksize * ksize * Cin + ntw) * (int64_t)sizeof(float);
+  return wb > narrow ? wb : narrow;
 }
 
 extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
@@ -1540,14 +1587,16 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   WgradArgs a;
   a.x = (const bf16_t *)x; a.dy = (const bf16_t *)dy; a.part = workspace; a.g = g;
   a.xgc = (int)x_group_c; a.xgs = x_group_stride;
-  const int64_t splits = wgrad_splits(g);
-  a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
   a.M = (int64_t)g.N * g.Ho * g.Wo;
-  const int ntx = (taps * g.Cin + CBN - 1) / CBN, nty = (g.Cout + CBM - 1) / CBM;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
+  const int wide = glds ? wgrad_wide(g) : 0;
+  const int64_t splits = wgrad_splits(g, wide);
+  a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
+  const int tnw = wide ? 2 * CBN : CBN;
+  const int ntx = (taps * g.Cin + tnw - 1) / tnw, nty = (g.Cout + CBM - 1) / CBM;
   const int gv = glds_variant() & 7;
-  const int64_t kq = !glds ? CBK : ((gv == 3 || gv == 4) ? 32 : 64);     // K-tile depth (pixels)
+  const int64_t kq = !glds ? CBK : wide ? (wide == 1 ? 64 : 32) : ((gv == 3 || gv == 4) ? 32 : 64);  // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
   mper = (mper + kq - 1) / kq * kq;
   a.mper = mper;
@@ -1566,16 +1615,19 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   hipStream_t s = as_stream(stream);
   if (glds) {
     const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
-#define EWVIT_GLDS_WG(BK_, NS_)                                                                             \
+#define EWVIT_GLDS_WG(BK_, NS_, WJ_)                                                                        \
   do {                                                                                                    \
-    if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
-    else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
+    if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
+    else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
   } while (0)
-    switch (gv) {
-      case 2: EWVIT_GLDS_WG(64, 3); break;
-      case 3: EWVIT_GLDS_WG(32, 3); break;
-      case 4: EWVIT_GLDS_WG(32, 4); break;
-      default: EWVIT_GLDS_WG(64, 2); break;
+    if (wide == 1) EWVIT_GLDS_WG(64, 2, 8);
+    else if (wide == 2) EWVIT_GLDS_WG(32, 2, 8);
+    else if (wide == 3) EWVIT_GLDS_WG(32, 3, 8);
+    else switch (gv) {
+      case 2: EWVIT_GLDS_WG(64, 3, 4); break;
+      case 3: EWVIT_GLDS_WG(32, 3, 4); break;
+      case 4: EWVIT_GLDS_WG(32, 4, 4); break;
+      default: EWVIT_GLDS_WG(64, 2, 4); break;
     }
 #undef EWVIT_GLDS_WG
   } else {

@@ -258,6 +258,12 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
  * LDS-DMA tile / ring-depth configuration where the shape allows (csrc/conv.hip).
  * Returns the previous setting. */
 int ewvit_conv2d_set_glds(int variant);
+/* Weight-gradient n'-tile width (A/B measurement; default from EWVIT_CONV_WGW, else 4):
+ * 0 = 128-column tiles; 1/2/3 = 256-column tiles (each wave 64 x 128) with 64/32/32 pixels
+ * per K-tile and ring depth 2/2/3, taken when n' = k*k*Cin >= 256 and the last tile wastes
+ * <= 1/8 of it; 4 = auto (2 for n' >= 2048 over >= 64K output pixels, else 0).  Replaces nothing in the reference (tuning knob of csrc/conv.hip).
+ * Returns the previous setting. */
+int ewvit_conv2d_set_wgrad_wide(int variant);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs

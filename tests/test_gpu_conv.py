@@ -12,14 +12,20 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0], ids=['glds1', 'glds9', 'glds13', 'glds15', 'glds2', 'glds3', 'glds4', 'regstage'])
+@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0, 'w1', 'w2', 'w3'],
+                ids=['glds1', 'glds9', 'glds13', 'glds15', 'glds2', 'glds3', 'glds4', 'regstage',
+                     'glds9-wgw1', 'glds9-wgw2', 'glds9-wgw3'])
 def glds(request):
-    """Run each case on every LDS-DMA configuration and on the register-staged kernels."""
+    """Run each case on every LDS-DMA configuration and on the register-staged kernels;
+    'wN': glds9 with 256-column weight-gradient tiles of variant N (the others: auto, 4)."""
     import ewvit
     lib = ewvit._lib.load()
-    prev = lib.ewvit_conv2d_set_glds(request.param)
-    yield request.param
+    v, w = (9, int(request.param[1])) if isinstance(request.param, str) else (request.param, 4)
+    prev = lib.ewvit_conv2d_set_glds(v)
+    prevw = lib.ewvit_conv2d_set_wgrad_wide(w)
+    yield v
     lib.ewvit_conv2d_set_glds(prev)
+    lib.ewvit_conv2d_set_wgrad_wide(prevw)
 
 
 def rel(a, b):

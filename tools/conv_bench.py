@@ -61,7 +61,8 @@ def main():
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--shape', action='append', default=[],
                     help='extra shape N,Cin,H,W,Cout,k,stride,levels (repeatable; replaces the table)')
-    ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged')
+    ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged; '
+                    '+100*w: 256-column wgrad tiles of variant w (e.g. 209)')
     ap.add_argument('--bnstats', action='store_true', help='time fwd against fwd with BN statistics in the epilogue')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
@@ -90,7 +91,12 @@ def main():
         dy = torch.randn_like(y)
         dx = torch.empty_like(z)
         dw = torch.empty((Cout, Cx, k, k), device=dev)
-        ws = torch.empty(lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s) // 4, device=dev)
+        wsb = 0
+        for wv in range(5):                    # largest workspace over the wgrad tile widths
+            lib.ewvit_conv2d_set_wgrad_wide(wv)
+            wsb = max(wsb, lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s))
+        lib.ewvit_conv2d_set_wgrad_wide(4)
+        ws = torch.empty(wsb // 4, device=dev)
 
         flops = 2.0 * N * Ho * Wo * Cout * k * k * Cx
 
@@ -117,13 +123,15 @@ def main():
         rows = {}
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
-                lib.ewvit_conv2d_set_glds(v)
+                lib.ewvit_conv2d_set_glds(v % 100)
+                lib.ewvit_conv2d_set_wgrad_wide(v // 100)     # 0 = 128-column tiles, 4 = auto
                 phases = (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad))
                 if a.bnstats and rows_bn > 0:
                     phases = (('fwd', fwd), ('fwd_bn', fwd_bn))
                 for pn, fn in phases:
                     rows.setdefault((v, pn), []).append(graph_time(fn, a.iters))
         lib.ewvit_conv2d_set_glds(1)
+        lib.ewvit_conv2d_set_wgrad_wide(4)
         for v in a.variants:
             parts = []
             for pn in (('fwd', 'fwd_bn') if a.bnstats and rows_bn > 0 else ('fwd', 'dgrad', 'wgrad')):
