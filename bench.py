@@ -262,7 +262,23 @@ def main():
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                           for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
         if 'ewvit_dwt_haar_fwd' in table:
-            res['dwt_roofline'] = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'])
+            dr = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'])
+            # the per-launch events of the eager pass add ~10 us around a ~15 us kernel: the
+            # achieved rate is taken from back-to-back launches on the same frames replayed
+            # from one HIP graph (tools/dwt_bench.py; matches rocprofv3's kernel duration)
+            sys.path.insert(0, os.path.join(REPO, 'tools'))
+            import dwt_bench
+            iso = dwt_bench.measure(n=args.frames, hw=224, levels=3)
+            dr['event_avg_us'] = dr['avg_us']
+            dr['avg_us'] = round(iso['dwt_us'], 3)
+            dr['work_per_launch'] = iso['dwt_bytes']
+            dr['achieved'] = round(iso['dwt_bytes'] / iso['dwt_us'] / 1e3, 2)
+            dr['frac'] = round(dr['achieved'] / HBM_PEAK_GBS, 5)
+            dr['timing'] = 'HIP graph of 50 back-to-back launches, events around the replay'
+            dr['hf_upsample'] = {'avg_us': round(iso['up_us'], 3), 'work_per_launch': iso['up_bytes'],
+                                 'achieved': round(iso['up_bytes'] / iso['up_us'] / 1e3, 2),
+                                 'frac': round(iso['up_bytes'] / iso['up_us'] / 1e3 / HBM_PEAK_GBS, 5)}
+            res['dwt_roofline'] = dr
         res['cpu_baseline'] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_steps)
         print(json.dumps(res), flush=True)
     if world > 1 and dist.is_initialized():

@@ -3,8 +3,8 @@
 // Replaces network/mwt.py:20,76-81 (pytorch_wavelets DWTForward(J=1,'haar','zero')
 // per level + reshape + F.interpolate(bilinear, align_corners=False)).
 //
-// dwt_multilevel_kernel: one workgroup = one 32x32 input tile of one (n,c)
-// plane.  The tile is read from HBM once (coalesced 16-B loads) into LDS; every
+// dwt_multilevel_kernel: one workgroup = one 32-row strip (up to 256 columns) of one
+// (n,c) plane.  The strip is read from HBM once (coalesced 16-B loads) into LDS; every
 // level is then an LDS-staged row pass followed by a column pass, its LL
 // written back to LDS for the next level, its three HF bands stored straight to
 // their planes.  Algorithmic HBM traffic = one read of x + one write of every
@@ -13,86 +13,160 @@
 
 namespace ewvit {
 
-constexpr int DWT_TILE = 32;
+constexpr int DWT_TH = 32;      // strip height: a multiple of 2^levels (levels <= 5)
+constexpr int DWT_TWMAX = 256;  // strip width (runtime, a multiple of 32)
 // float32(1/sqrt(2)), the haar dec_lo/dec_hi magnitude pytorch_wavelets stores
 constexpr float HAAR_S = 0.70710677f;
 
+// store v[0..1] at o, o+1 (second only if two): one 4-B bf16x2 / 8-B f32x2 store
+// when both are present and the pair is aligned
+template <int ODT>
+__device__ __forceinline__ void store_pair(void *p, int64_t o, float v0, float v1, bool two) {
+  if (two && (o & 1) == 0) {
+    if (ODT == EWVIT_BF16) {
+      const uint32_t w = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      *reinterpret_cast<uint32_t *>(reinterpret_cast<bf16_t *>(p) + o) = w;
+    } else {
+      *reinterpret_cast<float2 *>(reinterpret_cast<float *>(p) + o) = make_float2(v0, v1);
+    }
+    return;
+  }
+  Elem<ODT>::store(p, o, v0);
+  if (two) Elem<ODT>::store(p, o + 1, v1);
+}
+
+// 4 consecutive pixels of row gy from column gx (zero outside the plane)
+template <int XDT>
+__device__ __forceinline__ float4 load4(const void *x, int64_t plane, int gy, int gx, int H, int W) {
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (gy >= H || gx >= W) return r;
+  const int64_t base = (plane * H + gy) * (int64_t)W + gx;
+  if (XDT == EWVIT_F32 && gx + 3 < W && ((base & 3) == 0))
+    return *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(x) + base);
+  if (XDT == EWVIT_BF16 && gx + 3 < W && ((base & 3) == 0)) {
+    const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const bf16_t *>(x) + base);
+    return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                       __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+  }
+  r.x = Elem<XDT>::load(x, base);
+  if (gx + 1 < W) r.y = Elem<XDT>::load(x, base + 1);
+  if (gx + 2 < W) r.z = Elem<XDT>::load(x, base + 2);
+  if (gx + 3 < W) r.w = Elem<XDT>::load(x, base + 3);
+  return r;
+}
+
+// one Haar 2x2 step, AFB2D's two fp32 passes in their order: row pass (dim 3) over
+// (a b / c d), then the column pass (dim 2)
+__device__ __forceinline__ void haar2x2(float a, float b, float cc, float d, float &LL, float &B0, float &B1,
+                                        float &B2) {
+  const float s = HAAR_S;
+  const float lo0 = __fadd_rn(__fmul_rn(s, a), __fmul_rn(s, b));
+  const float hi0 = __fsub_rn(__fmul_rn(s, a), __fmul_rn(s, b));
+  const float lo1 = __fadd_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
+  const float hi1 = __fsub_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
+  LL = __fadd_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));
+  B0 = __fsub_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));  // (W-lo,H-hi)
+  B1 = __fadd_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-lo)
+  B2 = __fsub_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-hi)
+}
+
+// One workgroup = one 32-row x tw-column strip of one (n,c) plane (tw = the whole
+// 224-pixel row at config 2: 1344 workgroups).  Level 1 runs from registers: an item
+// is a 2-row x 4-column patch (two coalesced 16-B loads, up to 4 items = 8 loads in
+// flight per thread) -> 2 output pixels, bands stored as 4-B bf16x2 pairs along output
+// rows, LL to LDS.  Levels 2.. run over LDS (<= 10 KB per workgroup, so ~8 resident per
+// CU and the whole grid in one round), ping-ponging between two LL buffers.
 template <int XDT, int ODT>
 __global__ __launch_bounds__(256) void dwt_multilevel_kernel(const void *__restrict__ x,
                                                              void *__restrict__ yh,
                                                              void *__restrict__ ll, int H,
                                                              int W, int C, int levels,
-                                                             int64_t nplanes) {
-  __shared__ float tile[2][DWT_TILE][DWT_TILE + 1];
+                                                             int64_t nplanes, int tw) {
+  __shared__ float bufB[(DWT_TH / 2) * (DWT_TWMAX / 2 + 1)];
+  __shared__ float bufA[(DWT_TH / 4) * (DWT_TWMAX / 4 + 1)];
   const int tid = threadIdx.x;
   const int64_t plane = blockIdx.z;  // n*C + c
-  const int y0 = blockIdx.y * DWT_TILE, x0 = blockIdx.x * DWT_TILE;
+  const int y0 = blockIdx.y * DWT_TH, x0 = blockIdx.x * tw;
+  const int n = (int)(plane / C), c = (int)(plane % C);
 
-  // ---- load: 32 rows x 32 cols, 4 consecutive pixels per thread
+  // ---- level 1 from registers
+  int hl = H, wl = W;
+  int ho = (hl + 1) >> 1, wo = (wl + 1) >> 1;
   {
-    const int r = tid >> 3, c4 = (tid & 7) * 4;
-    const int gy = y0 + r, gx = x0 + c4;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (gy < H) {
-      const int64_t base = (plane * H + gy) * (int64_t)W + gx;
-      if (XDT == EWVIT_F32 && gx + 3 < W && ((base & 3) == 0)) {
-        const float4 q = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(x) + base);
-        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-      } else if (XDT == EWVIT_BF16 && gx + 3 < W && ((base & 3) == 0)) {
-        const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const bf16_t *>(x) + base);
-        v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-        v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
-      } else {
+    const int nq = tw >> 2, items = (DWT_TH / 2) * nq, dp = (tw >> 1) + 1;
+    float4 r0[4], r1[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (gx + i < W) v[i] = Elem<XDT>::load(x, base + i);
+    for (int k = 0; k < 4; ++k) {
+      const int it = tid + k * 256;
+      if (it < items) {
+        const int i = it / nq, q = it - i * nq;
+        r0[k] = load4<XDT>(x, plane, y0 + 2 * i, x0 + 4 * q, H, W);
+        r1[k] = load4<XDT>(x, plane, y0 + 2 * i + 1, x0 + 4 * q, H, W);
       }
     }
+    const int64_t hw = (int64_t)ho * wo;
+    const int64_t ob = ((int64_t)(n * C + c) * 3) * hw;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tile[0][r][c4 + i] = v[i];
+    for (int k = 0; k < 4; ++k) {
+      const int it = tid + k * 256;
+      if (it >= items) continue;
+      const int i = it / nq, q = it - i * nq;
+      float L0, L1, a0, a1, b0, b1, c0, c1;
+      haar2x2(r0[k].x, r0[k].y, r1[k].x, r1[k].y, L0, a0, b0, c0);
+      haar2x2(r0[k].z, r0[k].w, r1[k].z, r1[k].w, L1, a1, b1, c1);
+      bufB[i * dp + 2 * q] = L0;
+      bufB[i * dp + 2 * q + 1] = L1;
+      const int gy = (y0 >> 1) + i, gx = (x0 >> 1) + 2 * q;
+      if (gy < ho && gx < wo) {
+        const bool two = gx + 1 < wo;
+        const int64_t o = ob + (int64_t)gy * wo + gx;
+        store_pair<ODT>(yh, o, a0, a1, two);
+        store_pair<ODT>(yh, o + hw, b0, b1, two);
+        store_pair<ODT>(yh, o + 2 * hw, c0, c1, two);
+        if (levels == 1) store_pair<ODT>(ll, plane * hw + (int64_t)gy * wo + gx, L0, L1, two);
+      }
+    }
   }
   __syncthreads();
 
-  // ---- levels: row pass then column pass, exactly AFB2D's two fp32 passes
-  const int n = (int)(plane / C), c = (int)(plane % C);
-  int hl = H, wl = W;     // size of this level's input plane
-  int64_t yh_off = 0;     // offset of this level's yh block
-  int S = DWT_TILE;       // tile extent at this level's input
-  int ty = y0, tx = x0;   // tile origin at this level's input resolution
-  int buf = 0;
-  for (int lv = 0; lv < levels; ++lv) {
-    const int ho = (hl + 1) >> 1, wo = (wl + 1) >> 1;
-    const int So = S >> 1;
+  // ---- levels 2..: row pass then column pass over LDS
+  int64_t yh_off = nplanes * 3 * (int64_t)ho * wo;   // offset of this level's yh block
+  hl = ho; wl = wo;
+  int Sh = DWT_TH / 2, Sw = tw >> 1;   // strip extent at this level's input
+  int ty = y0 >> 1, tx = x0 >> 1;      // strip origin at this level's input resolution
+  for (int lv = 1; lv < levels; ++lv) {
+    const float *src = (lv & 1) ? bufB : bufA;
+    float *dst = (lv & 1) ? bufA : bufB;
+    const int sp = Sw + 1, Soh = Sh >> 1, Sow = Sw >> 1, dp = Sow + 1;
+    ho = (hl + 1) >> 1; wo = (wl + 1) >> 1;
     const int oy0 = ty >> 1, ox0 = tx >> 1;
-    if (tid < So * So) {
-      const int i = tid / So, j = tid % So;
-      const float a = tile[buf][2 * i][2 * j], b = tile[buf][2 * i][2 * j + 1];
-      const float cc = tile[buf][2 * i + 1][2 * j], d = tile[buf][2 * i + 1][2 * j + 1];
-      const float s = HAAR_S;
-      // row pass (dim 3): even row 2i and odd row 2i+1
-      const float lo0 = __fadd_rn(__fmul_rn(s, a), __fmul_rn(s, b));
-      const float hi0 = __fsub_rn(__fmul_rn(s, a), __fmul_rn(s, b));
-      const float lo1 = __fadd_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
-      const float hi1 = __fsub_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
-      // column pass (dim 2)
-      const float LL = __fadd_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));
-      const float B0 = __fsub_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));  // (W-lo,H-hi)
-      const float B1 = __fadd_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-lo)
-      const float B2 = __fsub_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-hi)
-      tile[buf ^ 1][i][j] = LL;
-      const int gy = oy0 + i, gx = ox0 + j;
+    const int npair = (Sow + 1) >> 1, items = Soh * npair;
+    const int64_t hw = (int64_t)ho * wo;
+    const int64_t ob = yh_off + ((int64_t)(n * C + c) * 3) * hw;
+    for (int it = tid; it < items; it += 256) {
+      const int i = it / npair, j0 = (it - i * npair) * 2;
+      float L[2], B0[2], B1[2], B2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = j0 + e < Sow ? j0 + e : j0;
+        haar2x2(src[(2 * i) * sp + 2 * j], src[(2 * i) * sp + 2 * j + 1], src[(2 * i + 1) * sp + 2 * j],
+                src[(2 * i + 1) * sp + 2 * j + 1], L[e], B0[e], B1[e], B2[e]);
+      }
+      dst[i * dp + j0] = L[0];
+      if (j0 + 1 < Sow) dst[i * dp + j0 + 1] = L[1];
+      const int gy = oy0 + i, gx = ox0 + j0;
       if (gy < ho && gx < wo) {
-        const int64_t hw = (int64_t)ho * wo;
-        const int64_t o = yh_off + ((int64_t)(n * C + c) * 3) * hw + (int64_t)gy * wo + gx;
-        Elem<ODT>::store(yh, o, B0);
-        Elem<ODT>::store(yh, o + hw, B1);
-        Elem<ODT>::store(yh, o + 2 * hw, B2);
-        if (lv == levels - 1) Elem<ODT>::store(ll, plane * hw + (int64_t)gy * wo + gx, LL);
+        const bool two = j0 + 1 < Sow && gx + 1 < wo;
+        const int64_t o = ob + (int64_t)gy * wo + gx;
+        store_pair<ODT>(yh, o, B0[0], B0[1], two);
+        store_pair<ODT>(yh, o + hw, B1[0], B1[1], two);
+        store_pair<ODT>(yh, o + 2 * hw, B2[0], B2[1], two);
+        if (lv == levels - 1) store_pair<ODT>(ll, plane * hw + (int64_t)gy * wo + gx, L[0], L[1], two);
       }
     }
     __syncthreads();
     yh_off += nplanes * 3 * (int64_t)ho * wo;
-    hl = ho; wl = wo; S = So; ty = oy0; tx = ox0; buf ^= 1;
+    hl = ho; wl = wo; Sh = Soh; Sw = Sow; ty = oy0; tx = ox0;
   }
 }
 
@@ -181,13 +255,22 @@ extern "C" int ewvit_dwt_haar_fwd(const void *x, void *yh, void *ll, int64_t N, 
   EWVIT_CHECK_ARG(H < (1 << 30) && W < (1 << 30), "dwt_haar_fwd: plane too large");
   const int64_t planes = N * C;
   EWVIT_CHECK_ARG(planes <= 65535, "dwt_haar_fwd: N*C=%lld exceeds 65535", (long long)planes);
+  // strip width: the whole row when it fits (rounded up to 32), else the multiple of 32 in
+  // [128, 256] that wastes the fewest columns
+  int tw = (int)((W + 31) / 32 * 32);
+  if (tw > DWT_TWMAX) {
+    int64_t best = -1;
+    for (int c = DWT_TWMAX; c >= 128; c -= 32) {
+      const int64_t waste = (W + c - 1) / c * c - W;
+      if (best < 0 || waste < best) { best = waste; tw = c; }
+    }
+  }
   dim3 block(256);
-  dim3 grid((unsigned)((W + DWT_TILE - 1) / DWT_TILE), (unsigned)((H + DWT_TILE - 1) / DWT_TILE),
-            (unsigned)planes);
+  dim3 grid((unsigned)((W + tw - 1) / tw), (unsigned)((H + DWT_TH - 1) / DWT_TH), (unsigned)planes);
   hipStream_t s = as_stream(stream);
 #define DWT_LAUNCH(XD, OD)                                                                     \
   hipLaunchKernelGGL((dwt_multilevel_kernel<XD, OD>), grid, block, 0, s, x, yh, ll, (int)H,   \
-                     (int)W, (int)C, levels, planes)
+                     (int)W, (int)C, levels, planes, tw)
   if (x_dtype == EWVIT_F32 && out_dtype == EWVIT_F32) DWT_LAUNCH(EWVIT_F32, EWVIT_F32);
   else if (x_dtype == EWVIT_F32 && out_dtype == EWVIT_BF16) DWT_LAUNCH(EWVIT_F32, EWVIT_BF16);
   else if (x_dtype == EWVIT_BF16 && out_dtype == EWVIT_F32) DWT_LAUNCH(EWVIT_BF16, EWVIT_F32);
