@@ -135,9 +135,14 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
     const int v = e ? atoi(e) : 256;
     return v < 1 ? 1 : (v > 256 ? 256 : v);
   }();
+  static const int minr = [] {      // rows per thread at least (A/B: EWVIT_BN_MINRPT)
+    const char *e = getenv("EWVIT_BN_MINRPT");
+    const int v = e ? atoi(e) : 16;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
   int64_t nrc = (512 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   if (nrc > cap) nrc = cap;
-  const int64_t maxr = M / ((int64_t)g.RG * 16);
+  const int64_t maxr = M / ((int64_t)g.RG * minr);
   if (nrc > maxr) nrc = maxr;
   if (nrc < 1) nrc = 1;
   return (int)nrc;
@@ -145,9 +150,14 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
 
 // elementwise passes: ~1024 blocks in all, 8..64 rows per thread
 static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
+  static const int minr = [] {      // rows per thread at least (A/B: EWVIT_BN_MINRPE)
+    const char *e = getenv("EWVIT_BN_MINRPE");
+    const int v = e ? atoi(e) : 8;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
   int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
-  rpt = rpt < 8 ? 8 : (rpt > 64 ? 64 : rpt);
+  rpt = rpt < minr ? minr : (rpt > 64 ? 64 : rpt);
   return (int64_t)g.RG * rpt;
 }
 
