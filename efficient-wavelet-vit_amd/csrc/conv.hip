@@ -1235,7 +1235,14 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   // 14x14 / 28x28 convs) take 8-wave blocks (64 x BN/4 per wave) — twice the waves per
   // CU to hide the latency of their short K loops; big grids keep 4 waves (fewer LDS
   // reads per MFMA)
-  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && nwg <= 1024 ? 7 : v);
+  // — and every dgrad with 128-wide column tiles (freq_conv's parity-class dgrad 185 -> 162 us,
+  // multiscale 834 -> 820; the 56-column fusion dgrad is slower on 8 waves and keeps 4)
+  static const int dg8 = [] {
+    const char *e = getenv("EWVIT_CONV_DG8");
+    return e ? atoi(e) : 1;
+  }();
+  const bool wide8 = nwg <= 1024 || (DGRAD && bn == 128 && dg8);
+  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && wide8 ? 7 : v);
   if (bn == 64) {
     switch (vv) {
       case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
