@@ -1210,12 +1210,19 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
       a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
-  const int v = glds_variant() & 7;
+  int v = glds_variant() & 7;
   const int tap_inner = (glds_variant() & 8) ? 1 : 0;
-  const int BM = (v == 3 || v == 4) ? 256 : 128;
-  const int64_t mt = (a.M + BM - 1) / BM;
   const int bn = a.Ncol <= 64 ? 64 : 128;
   const int ntn = (a.Ncol + bn - 1) / bn;
+  // a <= 64-column dgrad over a big map (the MWT fusion conv's 56-channel input gradient,
+  // 2.4 M pixels): 256-row blocks, 535 -> 505 us (EWVIT_CONV_DG256=0 keeps 128)
+  static const int dg256 = [] {
+    const char *e = getenv("EWVIT_CONV_DG256");
+    return e ? atoi(e) : 1;
+  }();
+  if (DGRAD && v == 1 && bn == 64 && dg256 && (a.M + 127) / 128 * ntn > 4096) v = 3;
+  const int BM = (v == 3 || v == 4) ? 256 : 128;
+  const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
   const dim3 grid((unsigned)nwg);
