@@ -1248,7 +1248,11 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     const char *e = getenv("EWVIT_CONV_DG8");
     return e ? atoi(e) : 1;
   }();
-  const bool wide8 = nwg <= 1024 || (DGRAD && bn == 128 && dg8);
+  static const int w8max = [] {      // grids up to this many blocks take 8 waves
+    const char *e = getenv("EWVIT_CONV_W8MAX");
+    return e ? atoi(e) : 2048;
+  }();
+  const bool wide8 = nwg <= w8max || (DGRAD && bn == 128 && dg8);
   const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && wide8 ? 7 : v);
   if (bn == 64) {
     switch (vv) {
