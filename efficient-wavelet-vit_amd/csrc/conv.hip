@@ -1215,12 +1215,13 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   const int bn = a.Ncol <= 64 ? 64 : 128;
   const int ntn = (a.Ncol + bn - 1) / bn;
   // a <= 64-column dgrad over a big map (the MWT fusion conv's 56-channel input gradient,
-  // 2.4 M pixels): 256-row blocks, 535 -> 505 us (EWVIT_CONV_DG256=0 keeps 128)
+  // 2.4 M pixels): 256-row blocks, 535 -> 505 us; likewise stage 2's 48-channel 3x3 dgrad
+  // (1568 row tiles) 71 -> 65 us.  EWVIT_CONV_DG256 = the row-tile count above which (0: never)
   static const int dg256 = [] {
     const char *e = getenv("EWVIT_CONV_DG256");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 1024;
   }();
-  if (DGRAD && v == 1 && bn == 64 && dg256 && (a.M + 127) / 128 * ntn > 4096) v = 3;
+  if (DGRAD && v == 1 && bn == 64 && dg256 > 0 && (a.M + 127) / 128 * ntn > dg256) v = 3;
   const int BM = (v == 3 || v == 4) ? 256 : 128;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
