@@ -522,20 +522,26 @@ __global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restri
     d = dsv * sv * (1.f - sv);
     if (w == 0) dz2_out[(int64_t)n * C + c] = d;
   }
+  // part[j] = sum_c w2[c][j] * d[c] over the chunk's channels: w2 is [C][Csq], so lanes run
+  // over j (coalesced rows of w2) and the 4 waves over interleaved channels, d from LDS
+  __shared__ float dsh[SE_CB];
+  __shared__ float red[4][64];
+  if (w == 0) dsh[lane] = d;
+  __syncthreads();
   float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
-  for (int j0 = w; j0 < Csq; j0 += 16) {
-    float v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = j0 + 4 * q;
-      v[q] = (j < Csq && c < C) ? w2[(int64_t)c * Csq + j] * d : 0.f;
+  const int c0 = cb * SE_CB;
+  const int nc = C - c0 < SE_CB ? C - c0 : SE_CB;
+  for (int j0 = 0; j0 < Csq; j0 += 64) {
+    const int j = j0 + lane;
+    float acc = 0.f;
+    if (j < Csq) {
+      const float *wr = w2 + (int64_t)c0 * Csq + j;
+      for (int k = w; k < nc; k += 4) acc = fmaf(wr[(int64_t)k * Csq], dsh[k], acc);
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      v[q] = wave_sum(v[q]);
-      const int j = j0 + 4 * q;
-      if (lane == 0 && j < Csq) pp[j] = v[q];
-    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && j < Csq) pp[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
   }
 }
 
