@@ -139,12 +139,18 @@ __device__ __forceinline__ void bf8_unpack(const uint4 &q, float (&v)[8]) {
 
 template <int STRIDE, bool ROT>
 __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restrict__ x, const float *__restrict__ w,
-                                                          bf16_t *__restrict__ y, DwShape s, int rows_per_block) {
+                                                          bf16_t *__restrict__ y, DwShape s, int rows_per_block,
+                                                          int segs) {
   const int C8 = s.C >> 3;
   const int r = threadIdx.x / C8, c8 = threadIdx.x % C8;
   if (r >= rows_per_block) return;
-  const int64_t row = (int64_t)blockIdx.x * rows_per_block + r;   // n*Ho + ho
-  if (row >= (int64_t)s.N * s.Ho) return;
+  // a thread walks one column segment of one output row (segs segments per row)
+  const int64_t vrow = (int64_t)blockIdx.x * rows_per_block + r;
+  if (vrow >= (int64_t)s.N * s.Ho * segs) return;
+  const int64_t row = vrow / segs;                                   // n*Ho + ho
+  const int wseg = (s.Wo + segs - 1) / segs;
+  const int wo0 = (int)(vrow - row * segs) * wseg;
+  const int wo1 = wo0 + wseg < s.Wo ? wo0 + wseg : s.Wo;
   const int ho = (int)(row % s.Ho);
   const int n = (int)(row / s.Ho);
   const int c = c8 * 8;
@@ -179,9 +185,9 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
+    for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, wo0 * STRIDE - s.pad + kw);
   bf16_t *yrow = y + (row * s.Wo) * s.C + c;
-  for (int wo = 0; wo < s.Wo; ++wo) {
+  for (int wo = wo0; wo < wo1; ++wo) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw)
@@ -422,6 +428,22 @@ static DwShape mk(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int pa
   return s;
 }
 
+// column segments per output row for the row kernels (EWVIT_DW_SEGS = the most segments):
+// the backbone's 7^2 / 14^2 maps give only ~448 blocks of whole rows, but splitting each row
+// in 2 (<= 2048 blocks, one more 3x3 window fill per row) measured slower in the step
+// (2682 vs 2703 frames/s), so the default is 1 — whole rows
+static int dw_segs(const DwShape &s, int rpb) {
+  static const int maxs = [] {
+    const char *e = getenv("EWVIT_DW_SEGS");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
+  const int64_t nb = ((int64_t)s.N * s.Ho + rpb - 1) / rpb;
+  int segs = 1;
+  while (segs * 2 <= maxs && nb * segs * 2 <= 2048 && s.Wo / (segs * 2) >= 3) segs *= 2;
+  return segs;
+}
+
 extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,
                                    int64_t C, int stride, int pad, int dtype, void *stream) {
   EWVIT_CHECK_ARG(x && w && y && dtype_ok(dtype), "dwconv3x3_fwd: bad args");
@@ -429,13 +451,14 @@ extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64
   if (int rc = check_shape(s, "dwconv3x3_fwd")) return rc;
   if (dtype == EWVIT_BF16 && s.C / 8 <= 256 && (s.stride == 1 || s.stride == 2)) {
     const int rpb = 256 / (s.C / 8);
-    dim3 grid((unsigned)(((int64_t)s.N * s.Ho + rpb - 1) / rpb));
+    const int segs = dw_segs(s, rpb);
+    dim3 grid((unsigned)(((int64_t)s.N * s.Ho * segs + rpb - 1) / rpb));
     if (s.stride == 1)
       hipLaunchKernelGGL((dw_row_bf16_kernel<1, false>), grid, dim3(256), 0, as_stream(stream),
-                         (const bf16_t *)x, w, (bf16_t *)y, s, rpb);
+                         (const bf16_t *)x, w, (bf16_t *)y, s, rpb, segs);
     else
       hipLaunchKernelGGL((dw_row_bf16_kernel<2, false>), grid, dim3(256), 0, as_stream(stream),
-                         (const bf16_t *)x, w, (bf16_t *)y, s, rpb);
+                         (const bf16_t *)x, w, (bf16_t *)y, s, rpb, segs);
   } else {
     const int64_t total = (int64_t)s.N * s.Ho * s.Wo * (s.C / 8);
     dim3 grid((unsigned)((total + 255) / 256));
@@ -457,9 +480,10 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
     DwShape t = s;
     t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
     const int rpb = 256 / (s.C / 8);
-    dim3 grid((unsigned)(((int64_t)t.N * t.Ho + rpb - 1) / rpb));
+    const int segs = dw_segs(t, rpb);
+    dim3 grid((unsigned)(((int64_t)t.N * t.Ho * segs + rpb - 1) / rpb));
     hipLaunchKernelGGL((dw_row_bf16_kernel<1, true>), grid, dim3(256), 0, as_stream(stream),
-                       (const bf16_t *)dy, w, (bf16_t *)dx, t, rpb);
+                       (const bf16_t *)dy, w, (bf16_t *)dx, t, rpb, segs);
   } else {
     const int64_t total = (int64_t)s.N * s.H * s.W * (s.C / 8);
     dim3 grid((unsigned)((total + 255) / 256));
