@@ -1,5 +1,5 @@
 """Benchmark: DAMA fwd+bwd frames/s at 224x224, 64 frames per GPU, dim 128
-(BASELINE.json configs[1]; configs[2] when launched with torchrun on 8 GPUs).
+(BASELINE.json configs[1]; configs[2] with --gpus N / torchrun on N GPUs).
 
 One step = the reference training step of train.py:93-115 on synthetic data:
 ``DeepfakeDetector.forward(x[8, 8, 3, 224, 224], batch_size=8, 'dynamic')`` (one
@@ -9,17 +9,24 @@ Adam(lr 1e-4, wd 1e-4) step.  Random-init weights, N(0,1) frames.  The iteration
 is recorded once into HIP graphs and replayed (ewvit/graph.py; --eager issues
 every launch from Python instead).
 
-Multi-GPU: one process per GPU (torchrun); each step broadcasts rank 0's BN buffers,
-replays forward+backward, all-reduces the gradients (one flat fp32 buffer, RCCL over
-xGMI) and replays the optimizer; every rank runs its own 64-frame chunk (weak
-scaling; BatchNorm statistics per rank like the reference's per-replica
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (no torchrun env) starts N
+ranks itself through torch.distributed.run before touching the GPU and relays rank 0's
+line; under torchrun it checks WORLD_SIZE == N.  Each replayed step broadcasts rank 0's
+BN buffers, runs forward + backward with the gradient all-reduces (RCCL over xGMI,
+bucketed, issued as buckets fill so they overlap the rest of the backward) and the
+optimizer — all in one HIP graph (ewvit/graph.py); every rank runs its own 64-frame chunk
+(weak scaling; BatchNorm statistics per rank like the reference's per-replica
 DataParallel semantics).  value = all frames / max-over-ranks time.
+EWVIT_BENCH_REHEARSE=1 puts every rank on cuda:0 over gloo (eager; timings meaningless):
+the one-GPU rehearsal of the N-rank path.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--eager]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,7 +55,7 @@ def parse():
 
 def build_step(dev, frames, rank, graph=True):
     from network.model import DeepfakeDetector
-    from network.losses import combined_loss
+    from network.losses import combined_loss, orth_weight
     import ewvit
     from ewvit.graph import TrainStep
     torch.manual_seed(0)                                   # identical init on every rank
@@ -64,13 +71,17 @@ def build_step(dev, frames, rank, graph=True):
     y = torch.bernoulli(torch.full((videos,), 0.5, device=dev), generator=gl)
     model.train()
 
+    # the curriculum weight of the orthogonality term as a device scalar (epoch 1 of 1: 1.0),
+    # so a replayed step would follow an epoch schedule written in place
+    orth_w = torch.full((), orth_weight(1, 1), device=dev)
+
     def forward_loss():
         with torch.autocast('cuda', dtype=torch.bfloat16):
             out = model(x, per_video, 'dynamic')
-        loss, _ = combined_loss(out, y, crit, 1, 1)
+        loss, _ = combined_loss(out, y, crit, 1, 1, weight=orth_w)
         return loss
-    # gradients averaged over ranks with one RCCL all-reduce per step; the whole
-    # iteration replayed from HIP graphs (ewvit/graph.py)
+    # gradients averaged over ranks by bucketed RCCL all-reduces issued during backward;
+    # the whole iteration replayed from one HIP graph (ewvit/graph.py)
     return TrainStep(model, forward_loss, opt, graph=graph)
 
 
@@ -196,11 +207,37 @@ def cpu_baseline(steps):
             'sample': f'oracle fp32 eager, {steps} steps x 8 frames (1 chunk) fwd+bwd+Adam, after 1 warm-up'}
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus N outside torchrun: start N ranks (one process per GPU) as a child
+    torch.distributed.run — before this process touches the GPU — and exit with its code.
+    Rank 0's JSON line reaches stdout through the inherited file descriptors."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    os.environ.setdefault('TORCH_NCCL_AVOID_RECORD_STREAMS', '1')   # buckets are persistent buffers
     import ewvit
     from ewvit import dist as edist
     rank, world, local = edist.env_ranks()
+    if world != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled '
+              f'n_gpus', file=sys.stderr, flush=True)
+        sys.exit(2)
     # EWVIT_BENCH_REHEARSE=1: every rank on cuda:0 over gloo — exercises the DDP path
     # on a one-GPU box (timings meaningless); the real run is one rank per GPU on RCCL
     rehearse = os.environ.get('EWVIT_BENCH_REHEARSE') == '1'
@@ -246,7 +283,7 @@ def main():
                'config': {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
                           'image': 224, 'frames_per_gpu': args.frames, 'dim': 128,
                           'global_batch': args.frames * world, 'parallelism': f'dp{world}',
-                          'launch': 'eager' if args.eager else 'hip-graph'}}
+                          'launch': step.mode}}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
         res['roofline'] = roofline_for(*dom) if dom else None
         if shapes:
@@ -279,7 +316,8 @@ def main():
                                  'achieved': round(iso['up_bytes'] / iso['up_us'] / 1e3, 2),
                                  'frac': round(iso['up_bytes'] / iso['up_us'] / 1e3 / HBM_PEAK_GBS, 5)}
             res['dwt_roofline'] = dr
-        res['cpu_baseline'] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_steps)
+        res['allreduce'] = step.describe() if hasattr(step, 'describe') else None
+        res['cpu_baseline'] = None if args.no_cpu_baseline else cpu_baseline(args.cpu_steps)
         print(json.dumps(res), flush=True)
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()

@@ -38,8 +38,8 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
   p = p + neg_step_size * (m / denom);
 }
 
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr, double b1, double b2, float eps,
-                                                         float wd) {
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr_host, const double *lr_dev, double b1,
+                                                         double b2, float eps, float wd) {
   // tensor of this workgroup: scalar search over the prefix sums (uniform)
   const int blk = blockIdx.x;
   int t = 0;
@@ -53,6 +53,9 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr, 
   // bias corrections in double, as torch computes them on the host (1 - 0.999^t cancels
   // badly in f32), then rounded once to the f32 scalars the element update uses
   const double st = (double)*a.step[t];
+  // the learning rate from device memory when given (a replayed graph follows the caller's
+  // LR schedule, train.py:274,300), else the launch-time constant
+  const double lr = lr_dev ? *lr_dev : lr_host;
   const float neg_step_size = (float)(-(lr / (1.0 - pow(b1, st))));
   const float bc2s = (float)sqrt(1.0 - pow(b2, st));
   const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2), fb2 = (float)b2;
@@ -96,7 +99,7 @@ using namespace ewvit;
 
 extern "C" int ewvit_adam_step(int n, float *const *params, const float *const *grads, float *const *exp_avg,
                                float *const *exp_avg_sq, const int64_t *numel, const float *const *steps, double lr,
-                               double beta1, double beta2, float eps, float weight_decay, void *stream) {
+                               const double *lr_dev, double beta1, double beta2, float eps, float weight_decay, void *stream) {
   EWVIT_CHECK_ARG(n >= 0 && n <= EWVIT_ADAM_MAX, "adam_step: %d tensors (max %d per launch)", n, EWVIT_ADAM_MAX);
   if (n == 0) return 0;
   AdamArgs a;
@@ -116,7 +119,7 @@ extern "C" int ewvit_adam_step(int n, float *const *params, const float *const *
     a.step[i] = steps[i];
   }
   a.chunk0[n] = (int)chunks;
-  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)chunks), dim3(256), 0, as_stream(stream), a, lr, beta1, beta2, eps,
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)chunks), dim3(256), 0, as_stream(stream), a, lr, lr_dev, beta1, beta2, eps,
                      weight_decay);
   return launch_status("adam_step");
 }

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libewvit.so')
-ABI_VERSION = 1
+ABI_VERSION = 2
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
 PACK_MAX = 32          # EWVIT_PACK_MAX
@@ -41,7 +41,7 @@ SIGNATURES = {
     'ewvit_bn_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_maxpool2_fwd': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp],
     'ewvit_maxpool2_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp],
-    'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _f32, _f32, _vp],
+    'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

@@ -21,6 +21,7 @@ import weakref
 import torch
 
 from . import _lib as L
+from .grads import grad_out
 
 # ---- step-wide weight packing: every conv weight the model used is packed by ONE
 # multi-tensor launch per 32 weights at the start of a training step (`packed()`),
@@ -187,6 +188,7 @@ class Conv2dFn(torch.autograd.Function):
             L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc,
                    gs, L.stream(y), work=work)
         ctx.save_for_backward(xc, weight, wpt)
+        ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
         ctx.cfg = (stride, levels, bias is not None, x.dtype)
         # bf16 MFMA product; an fp32 caller (no autocast) gets fp32 back
         return y if x.dtype == torch.bfloat16 else y.to(x.dtype).contiguous(memory_format=torch.channels_last)
@@ -226,13 +228,19 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or want_b:
             wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            # dW in the parameter's own memory format (DDP bucket views, no layout copy)
-            dwf = torch.empty_like(weight, dtype=torch.float32)
+            # dW in the parameter's own memory format — the data-parallel flat buffer's view
+            # when the step provides one (ewvit.grads), so no copy or layout change follows
+            wparam, bparam = ctx.params
+            dwf = grad_out(wparam) if ctx.needs_input_grad[1] else torch.empty_like(weight, dtype=torch.float32)
             s_co, s_ci, s_kh, s_kw = dwf.stride()
             if s_kh != k * s_kw:
                 dwf = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=xc.device)
                 s_co, s_ci, s_kh, s_kw = dwf.stride()
-            dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device) if want_b else None
+            dbf = None
+            if want_b:
+                dbf = grad_out(bparam)
+                if dbf.dim() != 1 or not dbf.is_contiguous():
+                    dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
             work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
             L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
                    Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)

@@ -1,122 +1,348 @@
-"""A static-shape data-parallel training step, replayed from captured HIP graphs.
+"""A static-shape data-parallel training step, replayed from one captured HIP graph.
 
 The reference's training iteration (train.py:93-115: DeepfakeDetector forward over
-the chunk, combined_loss, backward, optimizer step) issues ~2000 kernel launches;
-issued from Python each costs 10-50 us of host time, which is more than the GPU
-needs for most of them.  `TrainStep` records the iteration once into HIP graphs
-(torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it: one host call per step.
+the chunk, combined_loss, backward, optimizer step; `nn.DataParallel` at train.py:249-251
+for --multi-gpu) issues ~1500 kernel launches; issued from Python each costs 10-50 us of
+host time, more than the GPU needs for most of them.  `TrainStep` records the whole
+iteration once into a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it:
+one host call per step.
 
-Data parallel (one process per GPU): the gradient all-reduce runs between two
-graphs — g1 = forward + loss + backward + pack of all gradients into ONE flat fp32
-buffer; then a single RCCL all-reduce of that buffer over xGMI; g2 = average +
-optimizer step reading the gradients as views of the flat buffer.  Before g1 the
-module buffers (BatchNorm running statistics and counters) are broadcast from
-rank 0, which is what DistributedDataParallel(broadcast_buffers=True) does and what
-the reference's nn.DataParallel replicas see (train.py:136-139).  `graph=False`
-runs the identical sequence eagerly (the path the CPU gloo tests drive).
+Data parallel (one process per GPU, RCCL over xGMI) — `GradBuckets`:
 
-Requirements of graph mode: every input of `forward_loss` is a static tensor
-updated in place, the model issues no host synchronisation, and random draws use
-the device generator (torch ops) or the ewvit dropout step counter
-(_lib.rng_advance, advanced inside the recorded forward).
+* every trainable gradient lives in ONE flat fp32 buffer, laid out in the order backward
+  produces the gradients (observed on the first step and agreed from rank 0, as DDP
+  rebuilds its buckets) and cut into ~`bucket_mb` buckets;
+* the conv / linear wgrad kernels write their gradient straight into the buffer
+  (ewvit.grads slots); the few gradients autograd allocates itself are copied in by the
+  parameter's post-accumulate hook;
+* as soon as a bucket's last gradient lands, its all-reduce (average) is issued — in
+  bucket order — on the process group's stream, so the ring over xGMI runs under the rest
+  of the backward (the patch_to_embedding bucket, 128 MB, under the backbone's backward);
+* the optimizer waits for the buckets and reads the gradients as views of the buffer.
+
+With a capturable backend (RCCL) the collectives are recorded in the same graph as
+forward, backward and the optimizer.  The module buffers (BatchNorm running statistics
+and counters) are re-pointed into flat buffers and broadcast from rank 0 at the start of
+every step — inside the graph — which is what DistributedDataParallel(broadcast_buffers=
+True) does and what the reference's DataParallel replicas see (the replicas copy device
+0's buffers every forward).  BN batch statistics and the `pos_embedding[0:N]` chunk
+position stay per replica.  gloo (the CPU tests, the one-GPU rehearsal) runs the same
+sequence eagerly.
+
+Replay-time inputs: the optimizer's learning rate is a device scalar refreshed before each
+replay (ewvit.optim.Adam.sync_hyper) so an LR scheduler keeps working; other per-step
+values (e.g. the curriculum weight of combined_loss, train.py:76-86: pass `weight=` a device
+tensor the caller updates in place) must be device tensors too; betas / eps / weight decay
+are launch constants and a change raises.  `accum_steps=k` records k forward/backward
+passes (forward_loss(micro) for micro in 0..k-1, each loss / k, train.py:110-115) before
+the reduction and the optimizer step.
+
+Requirements of graph mode: every input of `forward_loss` is a static tensor updated in
+place, the model issues no host synchronisation, and random draws use the device
+generator (torch ops) or the ewvit dropout step counter (_lib.rng_advance, advanced
+inside the recorded forward).
 """
 import torch
 import torch.distributed as dist
+
+from .grads import clear_slot, set_slot
 
 
 def _world(group):
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+def _backend(group):
+    return dist.get_backend(group) if _world(group) > 1 else None
+
+
+class GradBuckets:
+    """Flat, bucketed gradient buffer with all-reduces issued as buckets fill."""
+
+    def __init__(self, params, group=None, bucket_mb=32, first_bucket_mb=4):
+        self.params = list(params)
+        self.group = group
+        self.world = _world(group)
+        self.avg_op = _backend(group) != 'gloo'          # gloo has no AVG: SUM, then divide
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.first_bytes = min(int(first_bucket_mb * (1 << 20)), self.bucket_bytes)
+        self.order = None          # parameter indices in gradient-ready order
+        self.observed = []
+        self.collect = True        # only the last micro-batch of a step reduces
+        self.defer = False         # True: no collectives from the hooks (all-reduce_all() after)
+        self.flat = None
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i)) for i, p in enumerate(self.params)]
+        self._layout(list(range(len(self.params)))[::-1])      # DDP's first guess: reverse registration
+
+    # ---- layout
+    def _layout(self, order):
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.order = list(order)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = [None] * len(self.params)
+        self.bucket_of = [0] * len(self.params)
+        self.buckets = []          # [(start, end, [param idx])]
+        off, start, cur, cap = 0, 0, [], self.first_bytes
+        for i in self.order:
+            p = self.params[i]
+            self.views[i] = self.flat.as_strided(p.shape, p.stride(), off)    # the parameter's own strides
+            set_slot(p, self.views[i])
+            if cur and (off - start + p.numel()) * 4 > cap:
+                self.buckets.append((start, off, cur))
+                start, cur, cap = off, [], self.bucket_bytes
+            cur.append(i)
+            self.bucket_of[i] = len(self.buckets)
+            off += p.numel()
+        if cur:
+            self.buckets.append((start, off, cur))
+
+    def relayout(self):
+        """Re-cut the buffer in the order the last backward produced the gradients
+        (rank 0's order, so every rank issues the same collectives in the same order)."""
+        seen = list(dict.fromkeys(self.observed))
+        order = seen + [i for i in reversed(range(len(self.params))) if i not in set(seen)]
+        if self.world > 1:
+            t = torch.tensor(order, dtype=torch.int64, device=self.flat.device)
+            dist.broadcast(t, 0, group=self.group)
+            order = t.tolist()
+        if order != self.order:
+            self._layout(order)
+
+    # ---- one step
+    def begin(self):
+        self.pending = [len(b[2]) for b in self.buckets]
+        self.next = 0
+        self.works = []
+        self.observed = []
+
+    def _hook(self, i):
+        def hook(p):
+            if not self.collect:
+                return
+            self.observed.append(i)
+            v = self.views[i]
+            if p.grad is not v:
+                if p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+                p.grad = v
+            b = self.bucket_of[i]
+            self.pending[b] -= 1
+            self._fire_ready()
+        return hook
+
+    def _fire(self, b):
+        s, e, _ = self.buckets[b]
+        if self.world > 1 and not self.defer:
+            op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
+            self.works.append(dist.all_reduce(self.flat[s:e], op=op, group=self.group, async_op=True))
+
+    def _fire_ready(self):
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._fire(self.next)
+            self.next += 1
+
+    def finish(self):
+        """After backward: zero the slots of parameters that got no gradient, issue the
+        remaining buckets, wait for all of them (a stream wait under RCCL)."""
+        for b in range(self.next, len(self.buckets)):
+            if self.pending[b]:
+                for i in self.buckets[b][2]:
+                    p = self.params[i]
+                    if p.grad is None:
+                        self.views[i].zero_()
+                self.pending[b] = 0
+        self._fire_ready()
+        for w in self.works:
+            w.wait()
+        self.works = []
+        if self.world > 1 and not self.avg_op and not self.defer:
+            self.flat.div_(self.world)
+
+    def allreduce_all(self):
+        """The deferred form: one all-reduce of the whole buffer (between two graphs)."""
+        if self.world > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM, group=self.group)
+            if not self.avg_op:
+                self.flat.div_(self.world)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        for p in self.params:
+            clear_slot(p)
+
+
+class BufferSync:
+    """Module buffers re-pointed into one flat tensor per dtype, broadcast from rank 0."""
+
+    def __init__(self, model, group=None):
+        self.group = group
+        by_dt = {}
+        for mod in model.modules():
+            for name, b in mod._buffers.items():
+                if b is not None:
+                    by_dt.setdefault(b.dtype, []).append((mod, name, b))
+        self.flats = []
+        for dt, items in by_dt.items():
+            n = sum(b.numel() for _, _, b in items)
+            flat = torch.empty(n, dtype=dt, device=items[0][2].device)
+            off = 0
+            for mod, name, b in items:
+                v = flat[off:off + b.numel()].view(b.shape)
+                v.copy_(b)
+                mod._buffers[name] = v
+                off += b.numel()
+            self.flats.append(flat)
+
+    def __call__(self):
+        for f in self.flats:
+            dist.broadcast(f, 0, group=self.group)
+
+
 class TrainStep:
-    def __init__(self, model, forward_loss, optimizer, graph=True, warmup=3, group=None):
+    def __init__(self, model, forward_loss, optimizer, graph=True, warmup=3, group=None, bucket_mb=32,
+                 accum_steps=1, overlap=True):
         self.model, self.forward_loss, self.opt, self.group = model, forward_loss, optimizer, group
         self.world = _world(group)
+        self.accum = int(accum_steps)
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.buffers = [b for b in model.buffers()]
         dev = self.params[0].device
-        self.graph = bool(graph) and dev.type == 'cuda'
-        self.flat = None
-        if self.world > 1:
-            n = sum(p.numel() for p in self.params)
-            self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-            self.views, off = [], 0
-            for p in self.params:
-                # the parameter's own strides (channels-last conv weights included), so
-                # the fused optimizer pairs gradient and parameter memory element-wise
-                self.views.append(self.flat.as_strided(p.shape, p.stride(), off))
-                off += p.numel()
+        capturable = _backend(group) in (None, 'nccl')
+        self.graph = bool(graph) and dev.type == 'cuda' and capturable
+        self.buckets = GradBuckets(self.params, group, bucket_mb) if self.world > 1 else None
+        if self.buckets is not None:
+            self.buckets.defer = not overlap
+        self.bufsync = BufferSync(model, group) if self.world > 1 else None
         self.loss = None
-        if self.graph:
-            self._capture(warmup)
+        self.mode = 'graph' if self.graph else 'eager'
+        self._hyper = optimizer.hyper_signature() if hasattr(optimizer, 'hyper_signature') else None
+        self._started = False
+        self.g2 = None
+        if self.graph and self.buckets is not None and self.buckets.defer:
+            self._capture_split(warmup)
+        elif self.graph:
+            try:
+                self._capture(warmup)
+            except Exception as e:          # noqa: BLE001 — a backend that cannot record collectives
+                if self.world == 1:
+                    raise
+                import sys
+                print(f'TrainStep: capturing the collectives failed ({type(e).__name__}: {e}); falling back to '
+                      f'forward/backward and optimizer graphs around one all-reduce', file=sys.stderr, flush=True)
+                torch.cuda.synchronize()
+                self.buckets.defer = True
+                self._capture_split(warmup)
 
-    # ---- pieces of one iteration
-    def _sync_buffers(self):
-        if self.world > 1 and self.buffers:
-            dist._broadcast_coalesced(self.group or dist.group.WORLD, self.buffers, 64 << 20, 0)
+    def describe(self):
+        d = {'launch': 'hip-graph' if self.graph else 'eager', 'world': self.world}
+        if self.buckets is not None:
+            d.update({'buckets': len(self.buckets.buckets), 'bucket_mb': self.buckets.bucket_bytes / (1 << 20),
+                      'grad_bytes': 4 * self.buckets.flat.numel(),
+                      'overlap': 'per-bucket all-reduce issued during backward' + (
+                          ', recorded in the step graph' if self.graph else '')
+                      if not self.buckets.defer else 'one all-reduce between two graphs'})
+        return d
 
+    def _first(self):
+        self._eager()                        # first step: observes the gradient order
+        if self.buckets is not None:
+            self.buckets.relayout()
+        self._started = True
+        return self.loss
+
+    # ---- one iteration
     def _fwd_bwd(self):
         from . import conv
+        loss = None
         with conv.packed():          # every conv weight packed to bf16 by one launch
-            loss = self.forward_loss()
-            loss.backward()
-        if self.world > 1:
-            torch._foreach_copy_(self.views, [p.grad for p in self.params])
+            for k in range(self.accum):
+                if self.buckets is not None:
+                    self.buckets.collect = k == self.accum - 1
+                lk = self.forward_loss(k) if self.accum > 1 else self.forward_loss()
+                if self.accum > 1:
+                    lk = lk / self.accum                                   # train.py:110
+                lk.backward()
+                loss = lk.detach() if loss is None else loss + lk.detach()
         return loss
 
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat, group=self.group)
-
-    def _update(self):
-        if self.world > 1:
-            self.flat.div_(self.world)
+    def _iteration(self):
+        self.opt.zero_grad(set_to_none=True)
+        if self.buckets is not None:
+            self.bufsync()
+            self.buckets.begin()
+        loss = self._fwd_bwd()
+        if self.buckets is not None:
+            self.buckets.finish()
         self.opt.step()
+        return loss
 
     def _eager(self):
-        self.opt.zero_grad(set_to_none=True)
-        self._sync_buffers()
-        loss = self._fwd_bwd()
-        self._allreduce()
-        if self.world > 1:
-            for p, v in zip(self.params, self.views):
-                p.grad = v
-        self._update()
-        return loss
+        self.loss = self._split_eager() if (self.buckets is not None and self.buckets.defer) else self._iteration()
+        return self.loss
 
-    # ---- capture
+    # ---- capture: warm-up and capture on one side stream (the AccumulateGrad nodes keep
+    # the stream they were created on), no autograd graph kept alive across them
     def _capture(self, warmup):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(warmup):          # lazy inits (library handles, caches) happen here
-                self._eager()
+            self._first()
+            for _ in range(max(0, warmup - 1)):       # lazy inits (library handles, caches, RCCL comms)
+                self._iteration()
+            self.loss = None
+            torch.cuda.synchronize()
+            self.g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g, stream=side):
+                self.loss = self._iteration()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        self.opt.zero_grad(set_to_none=True)
-        self._sync_buffers()
-        self.g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g1):
-            self.loss = self._fwd_bwd()
-            if self.world == 1:
-                self._update()
-        self.g2 = None
-        if self.world > 1:
-            for p, v in zip(self.params, self.views):
-                p.grad = v
+
+    def _capture_split(self, warmup):
+        """Fallback: g1 = forward + backward (+ gradient slots), the all-reduce issued
+        eagerly, g2 = optimizer."""
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self._split_eager()
+            self.loss = None
+            torch.cuda.synchronize()
+            self.opt.zero_grad(set_to_none=True)
+            self.g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g, stream=side):
+                self.buckets.begin()
+                self.loss = self._fwd_bwd()
+                self.buckets.finish()
             self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2, pool=self.g1.pool()):
-                self._update()
+            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool()):
+                self.opt.step()
+        torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
 
+    def _split_eager(self):
+        self.opt.zero_grad(set_to_none=True)
+        self.bufsync()
+        self.buckets.begin()
+        loss = self._fwd_bwd()
+        self.buckets.finish()
+        self.buckets.allreduce_all()
+        self.opt.step()
+        return loss
+
     def __call__(self):
-        """One training iteration; returns the (static) loss tensor."""
+        """One training iteration; returns the (static, detached) loss tensor."""
         if not self.graph:
-            self.loss = self._eager()
-            return self.loss
-        self._sync_buffers()
-        self.g1.replay()
+            return self._eager() if self._started else self._first()
+        if self._hyper is not None and self.opt.hyper_signature() != self._hyper:
+            raise RuntimeError('TrainStep: betas / eps / weight_decay changed after capture; build a new TrainStep')
+        if hasattr(self.opt, 'sync_hyper'):
+            self.opt.sync_hyper()            # LR schedule -> the device scalar the graph reads
         if self.g2 is not None:
-            self._allreduce()
+            self.bufsync()
+            self.g.replay()
+            self.buckets.allreduce_all()
             self.g2.replay()
+            return self.loss
+        self.g.replay()
         return self.loss

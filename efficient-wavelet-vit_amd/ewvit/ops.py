@@ -9,6 +9,7 @@ import math
 import torch
 
 from . import _lib as L
+from .grads import grad_out
 
 F32, BF16 = L.F32, L.BF16
 
@@ -96,6 +97,7 @@ class LinearFn(torch.autograd.Function):
         mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
               resid=r2, ldr=N if r2 is not None else 0)
         ctx.save_for_backward(x2, weight, aux)
+        ctx.params = (weight, bias)          # gradient slots (ewvit.grads)
         ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None)
         return y.reshape(*lead, N)
 
@@ -117,9 +119,12 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device)).reshape(*lead, K)
         if ctx.needs_input_grad[1]:
-            dw = mm_tn(g, x2, torch.empty(N, K, dtype=torch.float32, device=dy.device))
+            dw = grad_out(ctx.params[0])
+            if not dw.is_contiguous():
+                dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+            dw = mm_tn(g, x2, dw)
         if has_bias and ctx.needs_input_grad[2]:
-            db = colsum(g, torch.empty(N, dtype=torch.float32, device=dy.device))
+            db = colsum(g, grad_out(ctx.params[1]))
         dres = dy if has_res and ctx.needs_input_grad[5] else None
         return dx, dw, db, None, None, dres, None
 

@@ -6,6 +6,12 @@ state ``step`` / ``exp_avg`` / ``exp_avg_sq``, so checkpoints load either way), 
 amsgrad=False / maximize=False.  ``step()`` issues one launch per 48 tensors with the
 pointers passed by value — graph-capturable although autograd allocates fresh gradients
 every eager step — plus one foreach increment of the per-parameter device step counters.
+
+The learning rate is read by the kernel from a per-group device scalar (``self._lr_dev``),
+written from ``group['lr']`` by ``sync_hyper()`` — called by every eager ``step()`` and, for
+a step recorded in a HIP graph, by ``ewvit.graph.TrainStep`` before each replay — so an LR
+scheduler (train.py:274,300: CosineAnnealingLR) drives a replayed step too.  betas, eps and
+weight_decay are launch constants: ``hyper_signature()`` lets a graph owner detect a change.
 """
 import ctypes
 
@@ -34,6 +40,26 @@ class Adam(torch.optim.Optimizer):
             raise ValueError('ewvit.optim.Adam: invalid hyper-parameters')
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
 
+    def sync_hyper(self):
+        """Write each group's current lr into its device scalar (outside any graph capture)."""
+        if not hasattr(self, '_lr_dev'):
+            self._lr_dev = {}           # id(group) -> [device f64 scalar, value last written]
+        for group in self.param_groups:
+            lr = float(group['lr'])
+            dev = next((p.device for p in group['params'] if p.is_cuda), None)
+            if dev is None:
+                continue
+            e = self._lr_dev.get(id(group))
+            if e is None or e[0].device != dev:
+                e = self._lr_dev[id(group)] = [torch.empty((), dtype=torch.float64, device=dev), None]
+            if e[1] != lr:
+                e[0].fill_(lr)
+                e[1] = lr
+
+    def hyper_signature(self):
+        """The hyper-parameters a recorded step bakes in as launch constants."""
+        return tuple((tuple(g['betas']), float(g['eps']), float(g['weight_decay'])) for g in self.param_groups)
+
     def _group_step(self, group):
         items = []
         for p in group['params']:
@@ -60,6 +86,9 @@ class Adam(torch.optim.Optimizer):
             return
         torch._foreach_add_([c[2]['step'] for c in items], 1.0)   # torch semantics: per-parameter steps
         b1, b2 = group['betas']
+        if id(group) not in getattr(self, '_lr_dev', {}):
+            self.sync_hyper()
+        lr_dev = L.ptr(self._lr_dev[id(group)][0])
         stream = L.stream(items[0][0])
         for k in range(0, len(items), L.ADAM_MAX):
             chunk = items[k:k + L.ADAM_MAX]
@@ -69,8 +98,8 @@ class Adam(torch.optim.Optimizer):
             ptrs = [(ctypes.c_void_p * n)(*[t.data_ptr() for t in col]) for col in cols]
             numel = (ctypes.c_int64 * n)(*[c[0].numel() for c in chunk])
             L.call('ewvit_adam_step', n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, ptrs[4],
-                   float(group['lr']), float(b1), float(b2), float(group['eps']), float(group['weight_decay']),
-                   stream, work={'bytes': 28.0 * sum(c[0].numel() for c in chunk)})
+                   float(group['lr']), lr_dev, float(b1), float(b2), float(group['eps']),
+                   float(group['weight_decay']), stream, work={'bytes': 28.0 * sum(c[0].numel() for c in chunk)})
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -78,6 +107,8 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_hyper()           # a captured step reads the scalar its owner refreshes
         for group in self.param_groups:
             self._group_step(group)
         return loss

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EWVIT_ABI_VERSION 1
+#define EWVIT_ABI_VERSION 2
 #define EWVIT_F32 0
 #define EWVIT_BF16 1
 #define EWVIT_EINVAL 1000
@@ -377,13 +377,15 @@ int ewvit_maxpool2_bwd(const void *dy, const uint8_t *argmax, void *dx, int dtyp
 /* ------------------------------------------------------ optimizer ---
  * Adam exactly as torch.optim.Adam (amsgrad=False, maximize=False): g += wd*p;
  * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
- * with t = *steps[i] (per-tensor device f32, advanced by the caller first) — the optimizer of the
+ * with t = *steps[i] (per-tensor device f32, advanced by the caller first) and lr = *lr_dev when
+ * lr_dev is non-null (device f64, so a replayed HIP graph follows an LR schedule the caller
+ * writes between replays: CosineAnnealingLR of train.py:274,300), else `lr` — the optimizer of the
  * reference's training step (train.py:273-275).  n <= EWVIT_ADAM_MAX f32 tensors per
  * launch (pointers by value: capturable although autograd reallocates the gradients);
  * p, g, m, v of a tensor share one memory order (any dense layout), numel elements. */
 int ewvit_adam_step(int n, float *const *params, const float *const *grads, float *const *exp_avg,
                     float *const *exp_avg_sq, const int64_t *numel, const float *const *steps, double lr,
-                    double beta1, double beta2, float eps, float weight_decay, void *stream);
+                    const double *lr_dev, double beta1, double beta2, float eps, float weight_decay, void *stream);
 
 #ifdef __cplusplus
 }

@@ -93,7 +93,7 @@ def test_ddp_gloo_world2_matches_dataparallel_semantics():
     torch.testing.assert_close(torch.from_numpy(res[0][2]), torch.from_numpy(res[1][2]))  # buffers broadcast
 
 
-def _trainstep_worker(rank, port, q):
+def _trainstep_worker(rank, port, q, accum=1, overlap=True):
     for p in (REPO, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -111,32 +111,80 @@ def _trainstep_worker(rank, port, q):
     x = edist.shard_videos(_data(), r, w)
     opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.5)
     before = {n: p.detach().clone() for n, p in model.named_parameters()}
-    step = TrainStep(model, lambda: model(x.flatten(0, 1)).mean() / w, opt, graph=False)
-    step()
+    if accum == 1:
+        def fl():
+            return model(x.flatten(0, 1)).mean() / w
+    else:                            # micro-batch k = frame k of every video
+        def fl(k):
+            return model(x[:, k]).mean() / w
+    # 4 KB buckets: the MWT's ~40 gradients go out in many all-reduces, issued from the
+    # post-accumulate hooks while backward is still running
+    step = TrainStep(model, fl, opt, graph=False, bucket_mb=4 / 1024, accum_steps=accum, overlap=overlap)
+    fired_in_backward = []
+    orig_fire = step.buckets._fire
+
+    def spy(b):
+        fired_in_backward.append(b)
+        return orig_fire(b)
+    step.buckets._fire = spy
+    at_finish = []
+    orig_finish = step.buckets.finish
+
+    def finish_spy():
+        at_finish.append(len(fired_in_backward))      # buckets already issued while backward ran
+        return orig_finish()
+    step.buckets.finish = finish_spy
+    step()                           # first step: initial layout, observes the gradient order
+    assert fired_in_backward == list(range(len(fired_in_backward)))
+    fired_in_backward.clear()
+    for p, b in zip(model.parameters(), before.values()):    # replay the step from the same start
+        p.data.copy_(b)
+    step()                           # second step: the buffer re-cut in the observed order
+    nb = len(step.buckets.buckets)
+    first_order = list(step.buckets.order)
     grads = {n: p.grad.numpy().copy() for n, p in model.named_parameters()}
     delta = {n: (before[n] - p.detach()).numpy().copy() for n, p in model.named_parameters()}
-    q.put((r, grads, delta))
+    # every gradient is a view of the flat buffer after the step
+    flat_ptrs = all(step.buckets.flat.data_ptr() <= p.grad.data_ptr() <
+                    step.buckets.flat.data_ptr() + 4 * step.buckets.flat.numel() for p in model.parameters())
+    if overlap:
+        assert at_finish[-1] >= nb - 1, f'only {at_finish[-1]} of {nb} buckets issued during backward'
+    q.put((r, grads, delta, nb, fired_in_backward, first_order, flat_ptrs))
     edist.barrier()
     torch.distributed.destroy_process_group()
 
 
-def test_trainstep_gloo_world2_averages_gradients():
-    """ewvit.graph.TrainStep (the bench's data-parallel step; eager mode on CPU):
-    rank-0 buffers broadcast, one flat all-reduce, averaged gradients, identical
-    updates — equal to the DataParallel-semantics gradient of the global batch."""
+def _run_trainstep(accum, overlap=True):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_trainstep_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_trainstep_worker, args=(r, port, q, accum, overlap)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(WORLD):
-        r, g, d = q.get(timeout=120)
-        res[r] = (g, d)
+        r, g, d, nb, fired, order, flat_ptrs = q.get(timeout=120)
+        res[r] = (g, d, nb, fired, order, flat_ptrs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    for r in range(WORLD):
+        g, d, nb, fired, order, flat_ptrs = res[r]
+        assert nb > 4, 'expected several buckets'
+        assert fired == list(range(nb)), 'buckets must be issued in order, each once'   # (no-ops when deferred)
+        assert flat_ptrs, 'gradients must be views of the flat all-reduce buffer'
+    assert res[0][4] == res[1][4], 'bucket layout agreed across ranks'
+    return res
+
+
+@pytest.mark.parametrize('overlap', [True, False])
+def test_trainstep_gloo_world2_averages_gradients(overlap):
+    """ewvit.graph.TrainStep (the bench's data-parallel step; eager mode on CPU):
+    rank-0 buffers broadcast, bucketed all-reduces issued from the gradient hooks during
+    backward in bucket order (overlap=False: the fallback's one all-reduce after backward),
+    averaged gradients, identical updates — equal to the DataParallel-semantics gradient
+    of the global batch."""
+    res = _run_trainstep(1, overlap)
     ref = _model()
     x = _data()
     outs = [ref(x[2 * r:2 * r + 2].flatten(0, 1)) for r in range(WORLD)]
@@ -149,6 +197,23 @@ def test_trainstep_gloo_world2_averages_gradients():
             torch.testing.assert_close(torch.from_numpy(res[r][1][n]), 0.5 * torch.from_numpy(res[r][0][n]),
                                        rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(torch.from_numpy(res[0][1][n]), torch.from_numpy(res[1][1][n]))
+
+
+def test_trainstep_gloo_world2_grad_accumulation():
+    """accum_steps=2 (train.py:110-115: loss / accum_steps, backward per micro-batch, one
+    optimizer step): the reduction runs once, after the last micro-batch, over the
+    accumulated gradients."""
+    res = _run_trainstep(2)
+    ref = _model()
+    x = _data()
+    loss = 0
+    for k in range(2):
+        outs = [ref(x[2 * r:2 * r + 2, k]) for r in range(WORLD)]
+        loss = loss + torch.cat(outs).mean() / 2
+    loss.backward()
+    for n, p in ref.named_parameters():
+        for r in range(WORLD):
+            torch.testing.assert_close(torch.from_numpy(res[r][0][n]) * WORLD, p.grad, rtol=1e-5, atol=1e-6)
 
 
 def test_shard_videos_covers_batch_once():

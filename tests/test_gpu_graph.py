@@ -46,6 +46,55 @@ def test_trainstep_graph_replay_equals_eager():
     assert float(sb.loss) == pytest.approx(float(sa.loss), rel=1e-3)
 
 
+def _adam_pair(sched_steps_after=3, accum=1):
+    """Eager vs graph TrainStep with ewvit.optim.Adam (the bench's optimizer): 3 steps at
+    the initial lr, then 3 steps each followed by a CosineAnnealingLR step."""
+    import ewvit
+    from ewvit.graph import TrainStep
+    a, b = _mwt_pair()
+    xs = torch.randn(accum, 4, 3, 64, 64, device=DEV)
+
+    def make(m):
+        opt = ewvit.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=3e-3, weight_decay=1e-4)
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=4)
+
+        def fl(k=0):
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                return m(xs[k]).float().square().mean()
+        return fl, opt, sched
+    fa, oa, sa_ = make(a)
+    fb, ob, sb_ = make(b)
+    sa = TrainStep(a, fa, oa, graph=False, accum_steps=accum)
+    for _ in range(3):
+        sa()
+    for _ in range(3):
+        sa()
+        sa_.step()
+    sb = TrainStep(b, fb, ob, graph=True, warmup=3, accum_steps=accum)      # 3 steps run while capturing
+    for _ in range(3):
+        sb()
+        sb_.step()
+    torch.cuda.synchronize()
+    assert oa.param_groups[0]['lr'] < 3e-3 * 0.9            # the schedule moved the lr
+    return a, b, sa, sb
+
+
+def test_trainstep_graph_follows_lr_schedule():
+    """a replayed step must read the scheduler's lr (device scalar refreshed
+    before each replay), not the lr baked in at capture."""
+    a, b, sa, sb = _adam_pair()
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(q, p, rtol=2e-4, atol=2e-5, msg=n)
+    assert float(sb.loss) == pytest.approx(float(sa.loss), rel=1e-3)
+
+
+def test_trainstep_graph_grad_accumulation():
+    """accum_steps=2 recorded in the graph (train.py:110-115) equals the eager loop."""
+    a, b, sa, sb = _adam_pair(accum=2)
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(q, p, rtol=2e-4, atol=2e-5, msg=n)
+
+
 def test_dropout_mask_changes_per_replay():
     import ewvit
     x = torch.randn(64, 128, device=DEV)
