@@ -4,10 +4,16 @@ The reference also constructs ``mwt``, ``sfe``, ``sfe_cls`` (EfficientNet-b0 via
 ``efficientnet_pytorch.from_pretrained``, a network fetch) and ``fusion_gate``
 for the 'sfe_only' / 'sfe_mwt' ablations (model.py:37-58,100-161).  Those heads
 are outside the hot path (SURVEY §2 OUT rows); ``mwt``, ``fusion_gate`` and
-``feat_pooler`` are built for state-dict compatibility, the b0 heads are not.
-Load reference checkpoints with ``load_reference_state_dict`` (strips the
-DataParallel ``module.`` prefix, ignores the b0 keys).
+``feat_pooler`` are built for state-dict compatibility, the b0 heads are not built up
+front.  ``load_state_dict`` accepts reference checkpoints unchanged — so the reference's
+``eval.py:60-77`` (strict ``model.load_state_dict(torch.load(path))``) works as is: the
+DataParallel ``module.`` prefix (train.py:309,315) is stripped, and every ``sfe.*`` /
+``sfe_cls.*`` tensor of the b0 heads is kept in a parameter-free placeholder under the
+same key, so it loads strictly and is saved back by ``state_dict()`` (round trip), while
+no compute ever touches it.
 """
+from collections import OrderedDict
+
 import torch
 from torch import nn
 
@@ -61,6 +67,32 @@ class DeepfakeDetector(nn.Module):
         return {'logits': self._classify(d['fused']), 'fused': d['fused'], 'space': d['space'],
                 'freq': d['freq']}
 
+    _ABLATION_HEADS = ('sfe', 'sfe_cls')
+
+    def _hold_ablation_tensor(self, key, value):
+        """Register `value`'s shape under `key` (e.g. sfe.efficient_net._fc.weight) in
+        placeholder modules — buffers, not parameters: they never train."""
+        parts = key.split('.')
+        mod = self
+        for name in parts[:-1]:
+            child = mod._modules.get(name)
+            if child is None:
+                child = _AblationHeadState()
+                mod.add_module(name, child)
+            mod = child
+        dev = self.classifier[0].weight.device
+        if not isinstance(mod, _AblationHeadState):
+            raise KeyError(f'{key}: not an ablation-head key')
+        mod.register_buffer(parts[-1], torch.empty(value.shape, dtype=value.dtype, device=dev))
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        """nn.Module.load_state_dict accepting the reference's checkpoints (see module doc)."""
+        sd = OrderedDict((k[7:] if k.startswith('module.') else k, v) for k, v in state_dict.items())
+        for k, v in sd.items():
+            if k.split('.', 1)[0] in self._ABLATION_HEADS and torch.is_tensor(v):
+                self._hold_ablation_tensor(k, v)
+        return super().load_state_dict(sd, strict=strict, assign=assign)
+
     def configure_ablation(self, ablation):
         if ablation in self.ablation_config:
             self.ablation = ablation
@@ -68,10 +100,18 @@ class DeepfakeDetector(nn.Module):
             raise ValueError(f'Invalid ablation config: {ablation}.')
 
 
+class _AblationHeadState(nn.Module):
+    """Holds checkpoint tensors of the reference's b0 ablation heads (model.py:37-51); no forward."""
+
+    def forward(self, *_):
+        raise NotImplementedError("the 'sfe_only' / 'sfe_mwt' ablation heads need EfficientNet-b0 "
+                                  "(a network fetch); only their checkpoint tensors are kept")
+
+
 def load_reference_state_dict(model, state_dict):
-    """Load a reference (possibly DataParallel-wrapped) checkpoint; returns the
-    (missing, unexpected) key lists after dropping the b0 ablation heads."""
+    """Load a reference (possibly DataParallel-wrapped) checkpoint without the b0 ablation
+    heads; returns the (missing, unexpected) key lists."""
     sd = {k[7:] if k.startswith('module.') else k: v for k, v in state_dict.items()}
-    sd = {k: v for k, v in sd.items() if not (k.startswith('sfe.') or k.startswith('sfe_cls.'))}
-    res = model.load_state_dict(sd, strict=False)
+    sd = {k: v for k, v in sd.items() if k.split('.', 1)[0] not in DeepfakeDetector._ABLATION_HEADS}
+    res = nn.Module.load_state_dict(model, sd, strict=False)
     return res.missing_keys, res.unexpected_keys

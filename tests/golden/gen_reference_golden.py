@@ -11,7 +11,8 @@ are provided as restatements (the same ones the oracle uses):
                                           see gen_pywt_golden.py)
 * ``torchvision.models.efficientnet_v2_s`` -> oracle.effnetv2 (random init; the
                                           IMAGENET1K_V1 weights are unreachable)
-* ``efficientnet_pytorch.EfficientNet`` -> raises (only the out-of-scope b0 path uses it)
+* ``efficientnet_pytorch.EfficientNet`` -> an empty placeholder module (only the out-of-scope
+                                          b0 ablation heads use it; its weights are a fetch)
 * ``cv2``                              -> empty module (imported but unused by sfe.py)
 
 Usage:  python tests/golden/gen_reference_golden.py
@@ -57,9 +58,14 @@ def install_stubs():
 
     ep = types.ModuleType('efficientnet_pytorch')
 
-    class EfficientNet:
+    class EfficientNet(torch.nn.Module):
+        """Parameter-free stand-in: the b0 heads (model.py:38-51) are built but never
+        called in 'dynamic' mode; their backbone keys are not part of any fixture."""
         @staticmethod
         def from_pretrained(name):
+            return EfficientNet()
+
+        def extract_features(self, img):
             raise RuntimeError('efficientnet_pytorch b0 is out of scope (network fetch)')
     ep.EfficientNet = EfficientNet
     sys.modules['efficientnet_pytorch'] = ep
@@ -73,6 +79,20 @@ def load_reference():
     import network.sfe as rsfe
     import network.dama as rdama
     return rmwt, rsfe, rdama
+
+
+def reference_losses():
+    """orthogonal_loss / combined_loss from the reference's train.py:55-91.  train.py
+    itself cannot be imported here (its module level needs the dataset stack: cv2,
+    facenet, sklearn's data loaders), so the two function definitions are taken from its
+    source text and executed alone."""
+    import ast
+    src = open(os.path.join(REF, 'train.py')).read()
+    tree = ast.parse(src)
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in ('orthogonal_loss', 'combined_loss')]
+    ns = {'torch': torch, 'F': torch.nn.functional}
+    exec(compile(ast.Module(body=fns, type_ignores=[]), os.path.join(REF, 'train.py'), 'exec'), ns)
+    return ns['orthogonal_loss'], ns['combined_loss']
 
 
 def no_stochastic(module):
@@ -204,6 +224,49 @@ def main():
                                    'sfe.efficient_net.features.6.14.block.2.fc1.weight']))
         out['grad.sfe.patch_to_embedding.weight.rowsum'] = dama.sfe.patch_to_embedding.weight.grad.sum(1)
         save('ref_dama.npz', out)
+
+        # ---- G7: DeepfakeDetector 'dynamic' (model.py:70-99): logits in eval and train mode,
+        # classifier gradients, and the reference state-dict key/shape manifest
+        import network.model as rmodel
+        det = no_stochastic(apply_recipe(rmodel.DeepfakeDetector(3, 128, batch_size=4), seed=15))
+        xd = recipe_input((2, 4, 3, 224, 224), seed=1008)
+        det.eval()
+        with torch.no_grad():
+            ev = det(xd, 4, 'dynamic')
+        det.train()
+        tr = det(xd, 4, 'dynamic')
+        wlog = loss_weights(tuple(tr['logits'].shape), 30)
+        (tr['logits'] * wlog).sum().backward()
+        out = {'x': xd, 'eval.logits': ev['logits'], 'eval.fused': ev['fused'], 'train.logits': tr['logits'],
+               'train.fused': tr['fused'], 'train.space': tr['space'], 'train.freq': tr['freq'], 'lw': wlog}
+        out.update(grads_of(det, ['classifier.0.weight', 'classifier.0.bias', 'classifier.3.weight',
+                                  'classifier.3.bias', 'dama.gate_net.5.weight']))
+        sd = det.state_dict()
+        keys = list(sd.keys())
+        out['manifest.keys'] = np.array(keys)
+        out['manifest.shapes'] = np.array([list(sd[k].shape) + [-1] * (4 - sd[k].dim()) for k in keys], dtype=np.int64)
+        save('ref_detector.npz', out)
+
+        # ---- G8: combined_loss / orthogonal_loss (train.py:55-91) at three curriculum points
+        r_orth, r_comb = reference_losses()
+        crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5]))
+        out = {}
+        logits0 = recipe_input((8, 1), seed=1009)
+        space0 = recipe_input((8, 128), seed=1010)
+        freq0 = recipe_input((8, 128), seed=1011) + 0.3 * space0
+        labels = torch.tensor([1., 0., 1., 1., 0., 0., 1., 0.])
+        out.update({'logits': logits0, 'space': space0, 'freq': freq0, 'labels': labels,
+                    'orth': r_orth(space0, freq0)})
+        for epoch, maxe in ((1, 10), (4, 10), (9, 10)):
+            lg, sp, fq = (t.clone().requires_grad_(True) for t in (logits0, space0, freq0))
+            loss, _ = r_comb({'logits': lg, 'space': sp, 'freq': fq}, labels, crit, epoch, maxe)
+            loss.backward()
+            tag = f'e{epoch}of{maxe}'
+            out[f'{tag}.loss'] = loss.detach()
+            out[f'{tag}.grad.logits'] = lg.grad
+            out[f'{tag}.grad.space'] = sp.grad if sp.grad is not None else torch.zeros_like(sp)
+            out[f'{tag}.grad.freq'] = fq.grad if fq.grad is not None else torch.zeros_like(fq)
+        save('ref_loss.npz', out)
     finally:
         os.chdir(cwd)
 

@@ -278,6 +278,45 @@ def test_chunk_over_64_frames_raises_like_reference(dama_pair):
         p.sfe.head(torch.randn(65, 1280, 7, 7, device=DEV))
 
 
+@pytest.fixture(scope='module')
+def detector_golden():
+    """The product DeepfakeDetector with the recipe weights of ref_detector.npz (seed 15;
+    the recipe is keyed by state-dict name, and the product's keys are the reference's)."""
+    from network.model import DeepfakeDetector
+    from oracle.weights import recipe_state_dict
+    m = DeepfakeDetector(3, 128, batch_size=4)
+    m.load_state_dict(recipe_state_dict(m.state_dict(), 15))
+    return no_stochastic(m).to(DEV).to(memory_format=torch.channels_last)
+
+
+def test_deepfake_detector_eval_vs_reference_golden(golden, detector_golden):
+    """A13: DeepfakeDetector.forward(x, batch_size, 'dynamic') (model.py:70-99) in eval mode,
+    against the reference's own output (ref_detector.npz, 2 videos x 4 frames, one chunk)."""
+    z = golden('ref_detector.npz')
+    m = detector_golden.eval()
+    x = torch.from_numpy(z['x']).to(DEV)
+    with torch.no_grad():
+        out = m(x, 4, 'dynamic')
+    check(out['fused'], torch.from_numpy(z['eval.fused']))
+    check(out['logits'], torch.from_numpy(z['eval.logits']))
+
+
+def test_deepfake_detector_train_vs_reference_golden(golden, detector_golden):
+    """A13 in train mode (BatchNorm batch statistics, dropout p=0) + classifier gradients."""
+    import copy
+    z = golden('ref_detector.npz')
+    m = copy.deepcopy(detector_golden).train()
+    x = torch.from_numpy(z['x']).to(DEV)
+    out = m(x, 4, 'dynamic')
+    for k in ('fused', 'space', 'freq', 'logits'):
+        check(out[k], torch.from_numpy(z['train.' + k]))
+    (out['logits'].float() * torch.from_numpy(z['lw']).to(DEV)).sum().backward()
+    pp = dict(m.named_parameters())
+    for n in ('classifier.0.weight', 'classifier.0.bias', 'classifier.3.weight', 'classifier.3.bias',
+              'dama.gate_net.5.weight'):
+        check(pp[n].grad, torch.from_numpy(z['grad.' + n]))
+
+
 def test_deepfake_detector_forward_backward_runs():
     from network.model import DeepfakeDetector
     from network.losses import combined_loss
