@@ -46,22 +46,62 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--frames', type=int, default=64, help='frames per GPU per step (one chunk)')
+    ap.add_argument('--config', type=int, default=2, choices=(2, 3, 4, 5),
+                    help='BASELINE.json configs[k-1]: 2 = 224^2 64 frames dim 128 (3 = the same per GPU on '
+                         'N GPUs), 4 = MWT branch at 384^2 32 frames dim 256, 5 = fp8 token GEMMs, 128 frames')
+    ap.add_argument('--frames', type=int, default=None, help='frames per GPU per step (config default)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=4)
     ap.add_argument('--eager', action='store_true', help='issue every launch from Python (no HIP graph)')
     return ap.parse_args()
 
 
-def build_step(dev, frames, rank, graph=True):
+CONFIGS = {
+    # BASELINE.json configs[1] / [2]: one 64-frame _process_frame chunk (8 videos x 8 frames)
+    2: dict(image=224, dim=128, frames=64, videos=8, chunk=8, gemm='bf16'),
+    3: dict(image=224, dim=128, frames=64, videos=8, chunk=8, gemm='bf16'),
+    # configs[4]: 128 frames = 16 videos x 8 frames in 2 chunks of 64 (batch_size=4: a
+    # 128-frame chunk overflows pos_embedding[0:N] in the reference, sfe.py:126,158-159)
+    5: dict(image=224, dim=128, frames=128, videos=16, chunk=4, gemm='fp8'),
+}
+
+
+def build_mwt_step(dev, frames, rank, graph=True):
+    """BASELINE.json configs[3]: the MWT branch (mwt.py:92-119) at 384^2, 32 frames, dim 256,
+    3 DWT levels — the reference's SFE cannot run at 384^2 (its 12x12 backbone map is not
+    divisible by the 7x7 patch, sfe.py:153), so the step is MWT forward + a mean-square loss
+    on its [N, 256, 1, 1] features + backward + Adam, bf16 autocast."""
+    from network.mwt import MWT
+    import ewvit
+    from ewvit.graph import TrainStep
+    torch.manual_seed(0)
+    model = MWT(3, 256, 3).to(dev).to(memory_format=torch.channels_last).train()
+    opt = ewvit.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(frames, 3, 384, 384, device=dev, generator=g)
+
+    def forward_loss():
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y = model(x)
+        return y.float().square().mean()
+    return TrainStep(model, forward_loss, opt, graph=graph)
+
+
+def build_step(dev, frames, rank, graph=True, config=2):
+    if config == 4:
+        return build_mwt_step(dev, frames, rank, graph)
     from network.model import DeepfakeDetector
     from network.losses import combined_loss, orth_weight
     import ewvit
     from ewvit.graph import TrainStep
     torch.manual_seed(0)                                   # identical init on every rank
-    videos = 8
+    cfg = CONFIGS[config]
+    videos = cfg['videos'] * frames // cfg['frames']
     per_video = frames // videos
-    model = DeepfakeDetector(3, 128, batch_size=per_video).to(dev).to(memory_format=torch.channels_last)
+    chunk = cfg['chunk']                                   # frames per video per _process_frame call
+    model = DeepfakeDetector(3, 128, batch_size=chunk).to(dev).to(memory_format=torch.channels_last)
+    if cfg['gemm'] != 'bf16':
+        ewvit.set_gemm_precision(model, cfg['gemm'])
     params = [p for p in model.parameters() if p.requires_grad]
     opt = ewvit.optim.Adam(params, lr=1e-4, weight_decay=1e-4)      # train.py:273-275 on csrc/optim.hip
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
@@ -77,7 +117,7 @@ def build_step(dev, frames, rank, graph=True):
 
     def forward_loss():
         with torch.autocast('cuda', dtype=torch.bfloat16):
-            out = model(x, per_video, 'dynamic')
+            out = model(x, chunk, 'dynamic')
         loss, _ = combined_loss(out, y, crit, 1, 1, weight=orth_w)
         return loss
     # gradients averaged over ranks by bucketed RCCL all-reduces issued during backward;
@@ -143,15 +183,19 @@ ENTRY_KERNELS = {
     'ewvit_scale_add': ['scale_add_kernel'],
 }
 MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data', 'ewvit_conv2d_bwd_weight')
-PMC_FILE = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+def pmc_file(config):
+    return os.path.join(REPO, 'profiles', 'pmc_latest.json' if config in (2, 3) else f'pmc_latest_c{config}.json')
 
 
-def pmc_traffic(entry, per_step):
-    """HBM bytes per launch of `entry` from the committed rocprofv3 PMC passes
-    (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None."""
-    if not os.path.exists(PMC_FILE) or entry not in ENTRY_KERNELS:
+def pmc_traffic(entry, per_step, config=2):
+    """HBM bytes per launch of `entry` from the committed rocprofv3 PMC passes of the same
+    bench config (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    path = pmc_file(config)
+    if not os.path.exists(path) or entry not in ENTRY_KERNELS:
         return None
-    data = json.load(open(PMC_FILE))
+    data = json.load(open(path))
+    if data.get('_config', 2) not in ((2, 3) if config in (2, 3) else (config,)):
+        return None
     steps = data.get('_steps_executed')
     if not steps or not per_step:
         return None
@@ -163,8 +207,8 @@ def pmc_traffic(entry, per_step):
     return round(tot / (per_step * steps), 1) if tot else None
 
 
-def roofline_for(name, row):
-    traffic = pmc_traffic(name, row.get('per_step'))
+def roofline_for(name, row, config=2):
+    traffic = pmc_traffic(name, row.get('per_step'), config)
     if name in MFMA_ENTRIES:
         ach = row['TFLOP/s']
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': BF16_PEAK_TFS,
@@ -177,15 +221,33 @@ def roofline_for(name, row):
             'work_per_launch': row['bytes_per_launch']}
 
 
-def cpu_baseline(steps):
+def cpu_baseline(steps, config=2):
     """The oracle (CPU fp32 eager restatement of the reference, same op sequence)
-    timed on this host: 8-frame chunk, fwd+bwd+Adam."""
+    timed on this host: 8-frame chunk, fwd+bwd+Adam; config 4: the MWT
+    branch at 384^2 dim 256 on 2-frame steps."""
     sys.path.insert(0, REPO)
     from oracle import model as om
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get('OMP_NUM_THREADS', threads)))
     torch.set_num_threads(threads)
     torch.manual_seed(0)
+    if config == 4:
+        m = om.MWT(3, 256, 3).train()
+        opt = torch.optim.Adam(m.parameters(), lr=1e-4, weight_decay=1e-4)
+        x = torch.randn(2, 3, 384, 384)
+
+        def mstep():
+            m(x).square().mean().backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        mstep()
+        n = max(1, steps // 2)
+        t = time.perf_counter()
+        for _ in range(n):
+            mstep()
+        dt = time.perf_counter() - t
+        return {'value': round(2 * n / dt, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+                'sample': f'oracle fp32 eager MWT(3,256,3) at 384^2, {n} steps x 2 frames fwd+bwd+Adam, after 1 warm-up'}
     m = om.DeepfakeDetector(3, 128, batch_size=8)
     m.train()
     opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
@@ -205,6 +267,19 @@ def cpu_baseline(steps):
     dt = time.perf_counter() - t
     return {'value': round(8 * steps / dt, 3), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
             'sample': f'oracle fp32 eager, {steps} steps x 8 frames (1 chunk) fwd+bwd+Adam, after 1 warm-up'}
+
+
+def workload(args, world, step):
+    if args.config == 4:
+        return {'workload': 'BASELINE configs[3]: MWT branch train step (mwt.py:92-119) fwd + mean-square loss + '
+                            'bwd + Adam at 384x384, 3 DWT levels', 'image': 384, 'frames_per_gpu': args.frames,
+                'dim': 256, 'levels': 3, 'global_batch': args.frames * world, 'parallelism': f'dp{world}',
+                'launch': step.mode, 'baseline_config': 4}
+    cfg = CONFIGS[args.config]
+    return {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
+            'image': 224, 'frames_per_gpu': args.frames, 'dim': 128, 'chunk_frames': 8 * cfg['chunk'],
+            'token_gemms': cfg['gemm'], 'global_batch': args.frames * world, 'parallelism': f'dp{world}',
+            'launch': step.mode, 'baseline_config': 3 if world > 1 else args.config}
 
 
 def _free_port():
@@ -247,7 +322,9 @@ def main():
     dev = torch.device('cuda', local)
     edist.init_from_env('gloo' if rehearse else 'nccl')    # RCCL over xGMI
     ewvit.load_library()                       # fail loudly if the HIP library is missing
-    step = build_step(dev, args.frames, rank, graph=not args.eager)
+    if args.frames is None:
+        args.frames = 32 if args.config == 4 else CONFIGS[args.config]['frames']
+    step = build_step(dev, args.frames, rank, graph=not args.eager, config=args.config)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -276,21 +353,21 @@ def main():
 
     if rank == 0:
         frames = args.frames * world * args.steps
-        res = {'metric': METRIC, 'value': round(frames / elapsed, 2), 'unit': 'frames/s', 'n_gpus': world,
+        metric = METRIC if args.config in (2, 3) else {
+            4: 'frames/sec fwd+bwd, 384×384 bs=32 dim=256 3-level DWT, MWT branch, MI355X',
+            5: 'frames/sec fwd+bwd, 224×224 bs=128 dim=128, fp8 e4m3 token GEMMs, MI355X'}[args.config]
+        res = {'metric': metric, 'value': round(frames / elapsed, 2), 'unit': 'frames/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(1e3 * elapsed / args.steps, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
-               'config': {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
-                          'image': 224, 'frames_per_gpu': args.frames, 'dim': 128,
-                          'global_batch': args.frames * world, 'parallelism': f'dp{world}',
-                          'launch': step.mode}}
+               'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
-        res['roofline'] = roofline_for(*dom) if dom else None
+        res['roofline'] = roofline_for(*dom, config=args.config) if dom else None
         if shapes:
             # the hottest single launch configuration (entry point + shape arguments)
             h = dict(shapes[0])
             h['per_step'] = h['launches'] / kt
-            hot = roofline_for(h['entry'], h)
+            hot = roofline_for(h['entry'], h, args.config)
             hot['traffic'] = None      # the PMC passes are summarised per kernel symbol, not per shape
             hot['args'] = h['args']
             res['roofline_hot'] = hot
@@ -299,13 +376,13 @@ def main():
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                           for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
         if 'ewvit_dwt_haar_fwd' in table:
-            dr = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'])
+            dr = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'], args.config)
             # the per-launch events of the eager pass add ~10 us around a ~15 us kernel: the
             # achieved rate is taken from back-to-back launches on the same frames replayed
             # from one HIP graph (tools/dwt_bench.py; matches rocprofv3's kernel duration)
             sys.path.insert(0, os.path.join(REPO, 'tools'))
             import dwt_bench
-            iso = dwt_bench.measure(n=args.frames, hw=224, levels=3)
+            iso = dwt_bench.measure(n=args.frames, hw=384 if args.config == 4 else 224, levels=3)
             dr['event_avg_us'] = dr['avg_us']
             dr['avg_us'] = round(iso['dwt_us'], 3)
             dr['work_per_launch'] = iso['dwt_bytes']
@@ -317,7 +394,7 @@ def main():
                                  'frac': round(iso['up_bytes'] / iso['up_us'] / 1e3 / HBM_PEAK_GBS, 5)}
             res['dwt_roofline'] = dr
         res['allreduce'] = step.describe() if hasattr(step, 'describe') else None
-        res['cpu_baseline'] = None if args.no_cpu_baseline else cpu_baseline(args.cpu_steps)
+        res['cpu_baseline'] = None if args.no_cpu_baseline else cpu_baseline(args.cpu_steps, args.config)
         print(json.dumps(res), flush=True)
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()

@@ -29,10 +29,15 @@ def main():
         i = args.index('--steps')
         steps = int(args[i + 1])
         del args[i:i + 2]
+    config = 2
+    if '--config' in args:
+        i = args.index('--config')
+        config = int(args[i + 1])
+        del args[i:i + 2]
     fetch = load(args[0], 'FETCH_SIZE')
     write = load(args[1], 'WRITE_SIZE')
     pat = re.compile(args[2]) if len(args) > 2 else None
-    out = {'_steps_executed': steps,
+    out = {'_steps_executed': steps, '_config': config,
            '_source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate); FETCH_SIZE x2 (gfx950 correction)'}
     for k in sorted(set(fetch) | set(write)):
         if pat and not pat.search(k):
