@@ -101,7 +101,8 @@ def build_step(dev, frames, rank, graph=True, config=2):
     chunk = cfg['chunk']                                   # frames per video per _process_frame call
     model = DeepfakeDetector(3, 128, batch_size=chunk).to(dev).to(memory_format=torch.channels_last)
     if cfg['gemm'] != 'bf16':
-        ewvit.set_gemm_precision(model, cfg['gemm'])
+        from network import set_gemm_precision
+        set_gemm_precision(model, cfg['gemm'])
     params = [p for p in model.parameters() if p.requires_grad]
     opt = ewvit.optim.Adam(params, lr=1e-4, weight_decay=1e-4)      # train.py:273-275 on csrc/optim.hip
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))

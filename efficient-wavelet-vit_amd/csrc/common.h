@@ -113,6 +113,17 @@ __device__ __forceinline__ float rows_sum4(float v) {
   return __int_as_float(b[0]) + __int_as_float(b[1]);
 }
 __device__ __forceinline__ float wave_sum(float v) { return rows_sum4(row_sum16(v)); }
+// the same butterfly with max (every lane ends with the wave's maximum)
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = fmaxf(__int_as_float(a[0]), __int_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(b[0]), __int_as_float(b[1]));
+}
 
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));

@@ -22,6 +22,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int GBM = 64, GBN = 64, GBK = 32, GPAD = 8, GLD = GBK + GPAD;
+constexpr int GLD8 = GBK + 16;   // fp8 LDS image row: 32 k bytes + 16 pad (48-B rows)
 
 struct GemmArgs {
   const void *A; int64_t lda_m, lda_k;
@@ -39,6 +40,9 @@ struct GemmArgs {
   int c_dtype;
   int64_t kper;  // K per split
   float *ws;     // split-K slabs [splitk][M][N]
+  // fp8 path: per-tensor amax of A and B as partial maxima (ewvit_amax_partials)
+  const float *a_amax; int a_nparts;
+  const float *b_amax; int b_nparts;
 };
 
 // Load 8 consecutive elements (along the contiguous dim) starting at flat
@@ -115,6 +119,27 @@ struct Stager {
       int n_ok = 0;
       if (gk < kend) n_ok = (int)(R - gr > 8 ? 8 : (R - gr > 0 ? R - gr : 0));
       load8<DT, VEC>(p, gr + gk * ld_k, n_ok, v);
+    }
+  }
+  // fp8 e4m3 (OCP) image: v * scale clamped to +-448 (per-tensor scaling keeps |v*scale| <=
+  // 448 up to rounding), round-to-nearest-even by v_cvt_pk_fp8_f32
+  __device__ __forceinline__ void store_q8(uint8_t (*lds)[GLD8], float scale) {
+    unsigned w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float a = __builtin_amdgcn_fmed3f(v[4 * h] * scale, 448.f, -448.f);
+      const float b = __builtin_amdgcn_fmed3f(v[4 * h + 1] * scale, 448.f, -448.f);
+      const float c = __builtin_amdgcn_fmed3f(v[4 * h + 2] * scale, 448.f, -448.f);
+      const float d = __builtin_amdgcn_fmed3f(v[4 * h + 3] * scale, 448.f, -448.f);
+      int q = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+      q = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, q, true);
+      w[h] = (unsigned)q;
+    }
+    if (KCONTIG) {
+      *reinterpret_cast<uint2 *>(&lds[r][k]) = make_uint2(w[0], w[1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[r + i][k] = (uint8_t)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
     }
   }
   __device__ __forceinline__ void store(bf16_t (*lds)[GLD]) {
@@ -204,6 +229,115 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       }
 }
 
+// Per-tensor amax: each of `nparts` workgroups reduces a contiguous range of rows of the
+// [rows x cols] (row stride ld) matrix to one partial maximum; consumers fold the partials.
+template <int DT>
+__global__ __launch_bounds__(256) void amax_partial_kernel(const void *x, int64_t rows, int64_t cols, int64_t ld,
+                                                          float *part) {
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
+  float m = 0.f;
+  for (int64_t r = r0; r < r1; ++r)
+    for (int64_t c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, r * ld + c)));
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// fold the partial maxima into the e4m3 scale 448 / amax (1 for an all-zero tensor)
+__device__ __forceinline__ float fp8_scale(const float *part, int n, float *red) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, part[i]);
+  m = wave_max(m);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  return m > 0.f ? 448.f / m : 1.f;
+}
+
+// The gemm_kernel structure with fp8 e4m3 operands (BASELINE configs[4]): operands staged
+// from f32/bf16 memory, multiplied by their per-tensor scale and rounded to OCP e4m3 into
+// the LDS images, v_mfma_f32_16x16x32_fp8_fp8 (8 fp8 of A and of B per lane, the bf16
+// lane map), fp32 accumulation, the product descaled by 1/(sa*sb) before the epilogue.
+template <int ADT, int BDT, bool AK, bool BK, bool AV, bool BV>
+__global__ __launch_bounds__(256) void gemm_fp8_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) uint8_t As[2][GBM][GLD8];
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][GBN][GLD8];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  const int64_t kbeg = (int64_t)blockIdx.z * g.kper;
+  const int64_t kend = (kbeg + g.kper < g.K) ? kbeg + g.kper : g.K;
+  const float sa = fp8_scale(g.a_amax, g.a_nparts, red);
+  const float sb = fp8_scale(g.b_amax, g.b_nparts, red);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<ADT, AK, AV> st_a;
+  Stager<BDT, BK, BV> st_b;
+  const int nk = (int)((kend - kbeg + GBK - 1) / GBK);
+  if (nk > 0) {
+    st_a.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, kbeg, kend, tid);
+    st_b.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, kbeg, kend, tid);
+    st_a.store_q8(As[0], sa);
+    st_b.store_q8(Bs[0], sb);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int64_t k0 = kbeg + (int64_t)(kt + 1) * GBK;
+      st_a.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, k0, kend, tid);
+      st_b.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, k0, kend, tid);
+    }
+    long af[2], bfr[2];
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const long *>(&As[cur][wm * 32 + i * 16 + fr][fk]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const long *>(&Bs[cur][wn * 32 + j * 16 + fr][fk]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      st_a.store_q8(As[cur ^ 1], sa);
+      st_b.store_q8(Bs[cur ^ 1], sb);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  const float descale = 1.f / (sa * sb);
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (row < g.M && col < g.N) {
+          const float v = acc[i][j][r] * descale;
+          if (split)
+            g.ws[((int64_t)blockIdx.z * g.M + row) * g.N + col] = v;
+          else
+            store_c(g, row, col, epilogue(g, row, col, v));
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int splitk) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= g.M * g.N) return;
@@ -258,8 +392,15 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const void *dy, int dydt, 
 }
 
 template <int ADT, int BDT, bool AK, bool BK>
-static void launch_typed(const GemmArgs &g, bool av, bool bv, dim3 grid, hipStream_t s) {
+static void launch_typed(const GemmArgs &g, bool av, bool bv, bool q8, dim3 grid, hipStream_t s) {
   dim3 block(256);
+  if (q8) {
+    if (av && bv) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
+    else if (av) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, true, false>), grid, block, 0, s, g);
+    else if (bv) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, false, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, false, false>), grid, block, 0, s, g);
+    return;
+  }
   if (av && bv) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
   else if (av) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, true, false>), grid, block, 0, s, g);
   else if (bv) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, false, true>), grid, block, 0, s, g);
@@ -267,11 +408,12 @@ static void launch_typed(const GemmArgs &g, bool av, bool bv, dim3 grid, hipStre
 }
 
 template <int ADT, int BDT>
-static void launch_layout(const GemmArgs &g, bool ak, bool bk, bool av, bool bv, dim3 grid, hipStream_t s) {
-  if (ak && bk) launch_typed<ADT, BDT, true, true>(g, av, bv, grid, s);
-  else if (ak) launch_typed<ADT, BDT, true, false>(g, av, bv, grid, s);
-  else if (bk) launch_typed<ADT, BDT, false, true>(g, av, bv, grid, s);
-  else launch_typed<ADT, BDT, false, false>(g, av, bv, grid, s);
+static void launch_layout(const GemmArgs &g, bool ak, bool bk, bool av, bool bv, bool q8, dim3 grid,
+                          hipStream_t s) {
+  if (ak && bk) launch_typed<ADT, BDT, true, true>(g, av, bv, q8, grid, s);
+  else if (ak) launch_typed<ADT, BDT, true, false>(g, av, bv, q8, grid, s);
+  else if (bk) launch_typed<ADT, BDT, false, true>(g, av, bv, q8, grid, s);
+  else launch_typed<ADT, BDT, false, false>(g, av, bv, q8, grid, s);
 }
 
 // 8 consecutive elements along the contiguous dim can be one 16/32-B load iff
@@ -286,12 +428,13 @@ static bool vec_ok(const void *p, int dt, int64_t ld_other) {
 
 using namespace ewvit;
 
-extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
-                          int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
-                          int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
-                          const float *bias, int act, void *aux, float drop_p, uint64_t seed,
-                          const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
-                          float *workspace, void *stream) {
+static int gemm_impl(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+                     int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
+                     int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
+                     const float *bias, int act, void *aux, float drop_p, uint64_t seed,
+                     const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
+                     float *workspace, const float *a_amax, int a_nparts, const float *b_amax, int b_nparts,
+                     bool q8, void *stream) {
   EWVIT_CHECK_ARG(A && B && C, "gemm: null operand");
   EWVIT_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   EWVIT_CHECK_ARG(dtype_ok(a_dtype) && dtype_ok(b_dtype) && dtype_ok(c_dtype), "gemm: bad dtype");
@@ -313,6 +456,7 @@ extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda
   g.alpha = alpha; g.beta = beta; g.bias = bias; g.act = act; g.aux = aux;
   g.drop_p = drop_p; g.seed = seed; g.seed_off = seed_offset; g.resid = resid; g.resid_dtype = resid_dtype; g.ldr = ldr;
   g.c_dtype = c_dtype; g.ws = workspace;
+  g.a_amax = a_amax; g.a_nparts = a_nparts; g.b_amax = b_amax; g.b_nparts = b_nparts;
   // K per split, a multiple of the K tile
   int64_t kper = (K + splitk - 1) / splitk;
   kper = ((kper + GBK - 1) / GBK) * GBK;
@@ -326,15 +470,53 @@ extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda
   dim3 grid((unsigned)((N + GBN - 1) / GBN), (unsigned)((M + GBM - 1) / GBM), (unsigned)sk);
   EWVIT_CHECK_ARG(grid.y <= 65535, "gemm: M too large");
   hipStream_t s = as_stream(stream);
-  if (a_dtype == EWVIT_BF16 && b_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_BF16>(g, ak, bk, av, bv, grid, s);
-  else if (a_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_F32>(g, ak, bk, av, bv, grid, s);
-  else if (b_dtype == EWVIT_BF16) launch_layout<EWVIT_F32, EWVIT_BF16>(g, ak, bk, av, bv, grid, s);
-  else launch_layout<EWVIT_F32, EWVIT_F32>(g, ak, bk, av, bv, grid, s);
-  int rc = launch_status("gemm");
+  if (a_dtype == EWVIT_BF16 && b_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_BF16>(g, ak, bk, av, bv, q8, grid, s);
+  else if (a_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_F32>(g, ak, bk, av, bv, q8, grid, s);
+  else if (b_dtype == EWVIT_BF16) launch_layout<EWVIT_F32, EWVIT_BF16>(g, ak, bk, av, bv, q8, grid, s);
+  else launch_layout<EWVIT_F32, EWVIT_F32>(g, ak, bk, av, bv, q8, grid, s);
+  int rc = launch_status(q8 ? "gemm_fp8" : "gemm");
   if (rc || sk == 1) return rc;
   const int64_t total = M * N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g, sk);
   return launch_status("gemm splitk reduce");
+}
+
+extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+                          int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
+                          int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
+                          const float *bias, int act, void *aux, float drop_p, uint64_t seed,
+                          const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
+                          float *workspace, void *stream) {
+  return gemm_impl(A, a_dtype, lda_m, lda_k, B, b_dtype, ldb_k, ldb_n, C, c_dtype, ldc, M, N, K, alpha, beta, bias,
+                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, nullptr, 0,
+                   nullptr, 0, false, stream);
+}
+
+extern "C" int ewvit_gemm_fp8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+                              int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
+                              int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
+                              const float *bias, int act, void *aux, float drop_p, uint64_t seed,
+                              const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr,
+                              int splitk, float *workspace, const float *a_amax, int a_nparts,
+                              const float *b_amax, int b_nparts, void *stream) {
+  EWVIT_CHECK_ARG(a_amax && b_amax && a_nparts >= 1 && b_nparts >= 1 && a_nparts <= EWVIT_AMAX_PARTS &&
+                  b_nparts <= EWVIT_AMAX_PARTS, "gemm_fp8: amax partials (%d, %d)", a_nparts, b_nparts);
+  return gemm_impl(A, a_dtype, lda_m, lda_k, B, b_dtype, ldb_k, ldb_n, C, c_dtype, ldc, M, N, K, alpha, beta, bias,
+                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, a_amax, a_nparts,
+                   b_amax, b_nparts, true, stream);
+}
+
+extern "C" int ewvit_amax_partials(const void *x, int dtype, int64_t rows, int64_t cols, int64_t ld, float *part,
+                                   int nparts, void *stream) {
+  EWVIT_CHECK_ARG(x && part && dtype_ok(dtype) && rows >= 0 && cols >= 0, "amax_partials: bad args");
+  EWVIT_CHECK_ARG(nparts >= 1 && nparts <= EWVIT_AMAX_PARTS, "amax_partials: nparts=%d", nparts);
+  if (dtype == EWVIT_F32)
+    hipLaunchKernelGGL(amax_partial_kernel<EWVIT_F32>, dim3(nparts), dim3(256), 0, as_stream(stream), x, rows, cols, ld,
+                       part);
+  else
+    hipLaunchKernelGGL(amax_partial_kernel<EWVIT_BF16>, dim3(nparts), dim3(256), 0, as_stream(stream), x, rows, cols,
+                       ld, part);
+  return launch_status("amax_partials");
 }
 
 extern "C" int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N,

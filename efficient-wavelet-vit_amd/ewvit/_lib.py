@@ -15,6 +15,7 @@ ABI_VERSION = 2
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
 PACK_MAX = 32          # EWVIT_PACK_MAX
+AMAX_PARTS = 256       # EWVIT_AMAX_PARTS
 
 _i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 _f64 = ctypes.c_double
@@ -25,6 +26,10 @@ SIGNATURES = {
     'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _i64, _vp],
     'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
                    _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
+    'ewvit_gemm_fp8': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
+                       _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp,
+                       _vp, _i32, _vp, _i32, _vp],
+    'ewvit_amax_partials': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
     'ewvit_colsum': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
     'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp, _vp],
     'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _vp, _i32, _i64, _i64, _vp],

@@ -24,10 +24,29 @@ def _c(t):
 
 
 # ------------------------------------------------------------------- GEMM
+def amax_partials(X, rows, cols, ld, nparts=None):
+    """Partial maxima of |X| over a [rows x cols] (row stride ld) matrix (ewvit_amax_partials)."""
+    n = nparts or int(max(1, min(L.AMAX_PARTS, rows)))
+    part = torch.empty(n, dtype=torch.float32, device=X.device)
+    L.call('ewvit_amax_partials', L.ptr(X), L.dt(X), rows, cols, ld, L.ptr(part), n, L.stream(X),
+           work={'bytes': rows * cols * X.element_size()})
+    return part, n
+
+
+def _operand_amax(X, rows_dim, k_dim, ld):
+    """amax partials of a GEMM operand with logical shape (rows_dim, k_dim) and strides ld =
+    (ld_rows, ld_k) — one of them 1."""
+    if ld[1] == 1:
+        return amax_partials(X, rows_dim, k_dim, ld[0])
+    return amax_partials(X, k_dim, rows_dim, ld[1])
+
+
 def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, aux=None,
-         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None):
+         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None, fp8=False):
     """Raw C[M,N] = epi(alpha * A(M,K) @ B(K,N)).  lda = (lda_m, lda_k), ldb = (ldb_k, ldb_n).
-    C must be contiguous with row stride N (ldc = C.stride(0))."""
+    C must be contiguous with row stride N (ldc = C.stride(0)).
+    fp8=True: both operands rounded to OCP e4m3 after per-tensor scaling 448/amax (the amax of
+    each operand is reduced by one launch first; ewvit_gemm_fp8)."""
     L.require_gpu(A, B, C)
     if splitk is None:
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
@@ -39,11 +58,16 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
     ws = torch.empty(splitk * M * N, dtype=torch.float32, device=C.device) if splitk > 1 else None
     work = {'flops': 2.0 * M * N * K,
             'bytes': M * K * A.element_size() + K * N * B.element_size() + M * N * C.element_size()}
-    L.call('ewvit_gemm', L.ptr(A), L.dt(A), lda[0], lda[1], L.ptr(B), L.dt(B), ldb[0], ldb[1],
-           L.ptr(C), L.dt(C), C.stride(0), M, N, K, float(alpha), float(beta), L.ptr(bias), act,
-           L.ptr(aux), float(drop_p), seed, L.ptr(seed_offset), L.ptr(resid),
-           L.dt(resid) if resid is not None else 0,
-           ldr, splitk, L.ptr(ws), L.stream(C), work=work)
+    args = (L.ptr(A), L.dt(A), lda[0], lda[1], L.ptr(B), L.dt(B), ldb[0], ldb[1],
+            L.ptr(C), L.dt(C), C.stride(0), M, N, K, float(alpha), float(beta), L.ptr(bias), act,
+            L.ptr(aux), float(drop_p), seed, L.ptr(seed_offset), L.ptr(resid),
+            L.dt(resid) if resid is not None else 0, ldr, splitk, L.ptr(ws))
+    if fp8:
+        pa, na = _operand_amax(A, M, K, lda)
+        pb, nb = _operand_amax(B, N, K, (ldb[1], ldb[0]))
+        L.call('ewvit_gemm_fp8', *args, L.ptr(pa), na, L.ptr(pb), nb, L.stream(C), work=work)
+    else:
+        L.call('ewvit_gemm', *args, L.stream(C), work=work)
     return C
 
 
@@ -82,7 +106,7 @@ class LinearFn(torch.autograd.Function):
     of network/sfe.py:29-55,127,134-142 and network/dama.py:25-31,105-113."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, act, drop_p, resid, out_dtype):
+    def forward(ctx, x, weight, bias, act, drop_p, resid, out_dtype, fp8=False):
         L.require_gpu(x, weight)
         K = x.shape[-1]
         lead = x.shape[:-1]
@@ -95,16 +119,16 @@ class LinearFn(torch.autograd.Function):
         soff = L.rng_offset(x.device) if drop_p > 0 else None
         r2 = _c(resid.reshape(M, N)) if resid is not None else None
         mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
-              resid=r2, ldr=N if r2 is not None else 0)
+              resid=r2, ldr=N if r2 is not None else 0, fp8=fp8)
         ctx.save_for_backward(x2, weight, aux)
         ctx.params = (weight, bias)          # gradient slots (ewvit.grads)
-        ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None)
+        ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None, fp8)
         return y.reshape(*lead, N)
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight, aux = ctx.saved_tensors
-        act, drop_p, seed, lead, xdt, has_res, has_bias = ctx.cfg
+        act, drop_p, seed, lead, xdt, has_res, has_bias, fp8 = ctx.cfg
         M, K = x2.shape
         N = weight.shape[0]
         dy2 = _c(dy.reshape(M, N))
@@ -117,20 +141,22 @@ class LinearFn(torch.autograd.Function):
                    L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device)).reshape(*lead, K)
+            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device), fp8=fp8).reshape(*lead, K)
         if ctx.needs_input_grad[1]:
             dw = grad_out(ctx.params[0])
             if not dw.is_contiguous():
                 dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-            dw = mm_tn(g, x2, dw)
+            dw = mm_tn(g, x2, dw, fp8=fp8)
         if has_bias and ctx.needs_input_grad[2]:
             db = colsum(g, grad_out(ctx.params[1]))
         dres = dy if has_res and ctx.needs_input_grad[5] else None
-        return dx, dw, db, None, None, dres, None
+        return dx, dw, db, None, None, dres, None, None
 
 
-def linear(x, weight, bias=None, act=0, drop_p=0.0, resid=None, out_dtype=torch.float32):
-    return LinearFn.apply(x, weight, bias, act, float(drop_p), resid, out_dtype)
+def linear(x, weight, bias=None, act=0, drop_p=0.0, resid=None, out_dtype=torch.float32, fp8=False):
+    """fp8=True: the forward and both backward GEMMs take OCP e4m3 operands with per-tensor
+    scaling (BASELINE configs[4]); the epilogue (bias, activation, dropout, residual) is fp32."""
+    return LinearFn.apply(x, weight, bias, act, float(drop_p), resid, out_dtype, bool(fp8))
 
 
 # -------------------------------------------------------------- LayerNorm

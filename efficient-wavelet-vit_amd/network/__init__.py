@@ -17,3 +17,26 @@ def load_config(path='config/architecture.yaml'):
     p = path if os.path.exists(path) else _PKG_CONFIG
     with open(p, 'r') as f:
         return yaml.safe_load(f)
+
+
+def set_gemm_precision(model, precision='bf16'):
+    """BASELINE.json configs[4]: run the attention / MLP GEMMs — the ViT's to_qkv, to_out and
+    FeedForward (sfe.py:29-70), patch_to_embedding and feat_map (sfe.py:127,140,155), the
+    cross-attention's to_q, to_kv, to_out (dama.py:15-53) — on fp8 e4m3 operands with
+    per-tensor scaling ('fp8'), or back on bf16 ('bf16').  The conv stacks, the DWT, the
+    gates and the classifier keep bf16.  Returns the number of Linear modules switched."""
+    from .dama import CrossAttention
+    from .sfe import Attention, EfficientViT, FeedForward, Linear
+    if precision not in ('bf16', 'fp8'):
+        raise ValueError(f'gemm precision {precision!r}: bf16 or fp8')
+    n = 0
+    for m in model.modules():
+        targets = []
+        if isinstance(m, (Attention, FeedForward, CrossAttention)):
+            targets = [c for c in m.modules() if isinstance(c, Linear)]
+        elif isinstance(m, EfficientViT):
+            targets = [m.patch_to_embedding, m.feat_map[0]]
+        for t in targets:
+            t.gemm_precision = precision
+            n += 1
+    return n

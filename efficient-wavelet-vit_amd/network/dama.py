@@ -19,7 +19,7 @@ import ewvit
 
 from . import load_config
 from .mwt import MWT
-from .sfe import EfficientViT, LayerNorm, Linear, _hooked
+from .sfe import EfficientViT, LayerNorm, Linear, _fp8, _hooked
 
 
 _SIDE = {}
@@ -60,15 +60,15 @@ class CrossAttention(nn.Module):                                           # dam
         context = context if context is not None else x
         if kv_include_self:
             context = torch.cat((x.float(), context.float()), dim=1)
-        q = ewvit.linear(x, self.to_q.weight, None, out_dtype=torch.bfloat16)
-        kv = ewvit.linear(context, self.to_kv.weight, None, out_dtype=torch.bfloat16)
+        q = ewvit.linear(x, self.to_q.weight, None, out_dtype=torch.bfloat16, fp8=_fp8(self.to_q))
+        kv = ewvit.linear(context, self.to_kv.weight, None, out_dtype=torch.bfloat16, fp8=_fp8(self.to_kv))
         o = ewvit.attention_cross(q, kv, self.heads, self.dim_head, self.scale)
         if isinstance(self.to_out, nn.Identity):
             o = o.float()
             return o if resid is None else o + resid
         lin, drop = self.to_out[0], self.to_out[1]
         return ewvit.linear(o, lin.weight, lin.bias, drop_p=drop.p if self.training else 0.0,
-                            resid=resid, out_dtype=torch.float32)
+                            resid=resid, out_dtype=torch.float32, fp8=_fp8(lin))
 
 
 _CA_FORWARD = CrossAttention.forward

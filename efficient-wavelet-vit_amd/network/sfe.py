@@ -31,6 +31,11 @@ def _hooked(m):
     return bool(m._forward_hooks or m._forward_pre_hooks or m._backward_hooks)
 
 
+def _fp8(m):
+    """True when network.set_gemm_precision put this Linear's GEMMs on fp8 e4m3."""
+    return getattr(m, 'gemm_precision', 'bf16') == 'fp8'
+
+
 class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm on the ewvit kernel; output in `out_dtype` (default: fp32)."""
 
@@ -44,7 +49,7 @@ class Linear(nn.Linear):
     """nn.Linear on the ewvit MFMA GEMM (fp32 master weights read directly)."""
 
     def forward(self, x):
-        return ewvit.linear(x, self.weight, self.bias, out_dtype=torch.float32)
+        return ewvit.linear(x, self.weight, self.bias, out_dtype=torch.float32, fp8=_fp8(self))
 
 
 class Residual(nn.Module):                                                 # sfe.py:12-18
@@ -86,8 +91,9 @@ class FeedForward(nn.Module):                                              # sfe
 
     def forward_residual(self, x, resid):
         l1, l2 = self.net[0], self.net[3]
-        h = ewvit.linear(x, l1.weight, l1.bias, act=1, drop_p=self._p(2), out_dtype=torch.bfloat16)
-        return ewvit.linear(h, l2.weight, l2.bias, drop_p=self._p(4), resid=resid, out_dtype=torch.float32)
+        h = ewvit.linear(x, l1.weight, l1.bias, act=1, drop_p=self._p(2), out_dtype=torch.bfloat16, fp8=_fp8(l1))
+        return ewvit.linear(h, l2.weight, l2.bias, drop_p=self._p(4), resid=resid, out_dtype=torch.float32,
+                            fp8=_fp8(l2))
 
 
 class Attention(nn.Module):                                                # sfe.py:42-70
@@ -106,14 +112,14 @@ class Attention(nn.Module):                                                # sfe
         return self.forward_residual(x, None)
 
     def forward_residual(self, x, resid):
-        qkv = ewvit.linear(x, self.to_qkv.weight, None, out_dtype=torch.bfloat16)
+        qkv = ewvit.linear(x, self.to_qkv.weight, None, out_dtype=torch.bfloat16, fp8=_fp8(self.to_qkv))
         o = ewvit.attention_packed(qkv, self.heads, self.dim_head, self.scale)
         if isinstance(self.to_out, nn.Identity):
             o = o.float()
             return o if resid is None else o + resid
         lin, drop = self.to_out[0], self.to_out[1]
         return ewvit.linear(o, lin.weight, lin.bias, drop_p=drop.p if self.training else 0.0,
-                            resid=resid, out_dtype=torch.float32)
+                            resid=resid, out_dtype=torch.float32, fp8=_fp8(lin))
 
 
 class Transformer(nn.Module):                                              # sfe.py:72-85
@@ -181,7 +187,7 @@ class EfficientViT(nn.Module):                                             # sfe
                                f'({self.pos_embedding.shape[0]}) — the reference fails here too (sfe.py:158-159)')
         y = self.patches(x)
         pe = self.patch_to_embedding
-        y = ewvit.linear(y, pe.weight, pe.bias, out_dtype=torch.float32)
+        y = ewvit.linear(y, pe.weight, pe.bias, out_dtype=torch.float32, fp8=_fp8(pe))
         tok = torch.cat((self.cls_token.expand(B, -1, -1), y), 1) + self.pos_embedding[0:B]
         tok = self.dropout(tok)
         tok = self.transformer(tok)
@@ -190,7 +196,7 @@ class EfficientViT(nn.Module):                                             # sfe
         Bn, N, D = tok.shape
         H = W = int(math.sqrt(N - 1))
         fm = self.feat_map[0]
-        f = ewvit.linear(tok[:, 1:], fm.weight, fm.bias, act=2, out_dtype=torch.float32)
+        f = ewvit.linear(tok[:, 1:], fm.weight, fm.bias, act=2, out_dtype=torch.float32, fp8=_fp8(fm))
         return f.reshape(Bn, H, W, -1).permute(0, 3, 1, 2)
 
     def forward(self, img, mask=None):

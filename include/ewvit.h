@@ -32,6 +32,7 @@ extern "C" {
 #define EWVIT_EINVAL 1000
 #define EWVIT_ADAM_MAX 48   /* tensors per ewvit_adam_step launch */
 #define EWVIT_PACK_MAX 32   /* weights per ewvit_conv2d_pack_weights launch */
+#define EWVIT_AMAX_PARTS 256 /* partial maxima per ewvit_amax_partials result */
 
 int ewvit_abi_version(void);
 const char *ewvit_last_error(void);
@@ -94,6 +95,26 @@ int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const v
                int act, void *aux, float drop_p, uint64_t seed, const int64_t *seed_offset,
                const void *resid, int resid_dtype, int64_t ldr, int splitk, float *workspace,
                void *stream);
+
+/* fp8 (BASELINE configs[4]): ewvit_gemm with both operands rounded to OCP e4m3fn
+ * (v_mfma_f32_16x16x32_fp8_fp8, fp32 accumulation) after per-tensor scaling s = 448 / amax:
+ * C = epi(alpha * sum_k q(A*sa) q(B*sb) / (sa*sb)).  a_amax / b_amax: partial maxima of |A|
+ * and |B| over the whole operand (ewvit_amax_partials, <= EWVIT_AMAX_PARTS each), folded by
+ * every workgroup in its prologue — so the scaling is current (this call's operands) and the
+ * call stays graph-capturable.  Replaces the bf16 GEMMs of the ViT attention / MLP
+ * (sfe.py:29-70), the cross-attention projections (dama.py:15-53) and patch_to_embedding
+ * (sfe.py:127,155) when the model runs in fp8 (ewvit.set_gemm_precision). */
+int ewvit_gemm_fp8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B, int b_dtype,
+                   int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                   float alpha, float beta, const float *bias, int act, void *aux, float drop_p, uint64_t seed,
+                   const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
+                   float *workspace, const float *a_amax, int a_nparts, const float *b_amax, int b_nparts,
+                   void *stream);
+
+/* max |x| over a [rows x cols] matrix (row stride ld, f32/bf16) as `nparts` partial maxima
+ * (workgroup i reduces rows [i*ceil(rows/nparts), ...)); nparts <= EWVIT_AMAX_PARTS. */
+int ewvit_amax_partials(const void *x, int dtype, int64_t rows, int64_t cols, int64_t ld, float *part, int nparts,
+                        void *stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n]  (bias gradients).  accumulate!=0 adds. */
 int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N, float *out,

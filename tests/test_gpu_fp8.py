@@ -1,0 +1,156 @@
+"""fp8 e4m3 GEMMs (BASELINE.json configs[4]: "fp8 (e4m3) MFMA for attention/MLP GEMMs, bf16
+DWT, 224x224 bs=128").
+
+Kernel level (ewvit_gemm_fp8 through the C-ABI):
+* the lane maps of v_mfma_f32_16x16x32_fp8_fp8 in all three operand layouts, with exact
+  integer data whose amax is 448 (scale 1: every value is exact in e4m3 and every sum exact
+  in fp32) — the result must be bit-exact;
+* random operands against an emulation built on torch's own float8_e4m3fn cast (CPU):
+  C = (q(A*sa) @ q(B*sb)) / (sa*sb) with sa = 448/amax(A) in float64 — only the fp32
+  accumulation order differs (<= 1e-5 of scale), which also pins the rounding (RNE) of the
+  hardware conversion to OCP e4m3fn (not the MI300 fnuz encoding);
+* split-K at the patch_to_embedding shape (M=64, N=512, K=62720).
+
+Module level: the DAMA train step with network.set_gemm_precision(model, 'fp8') against the
+fp32 oracle, with the stated fp8 bound; and the config-5 chunking (16 videos x 8 frames,
+batch_size=4 -> two 64-frame chunks) equal to composing _process_frame per chunk.
+"""
+import pytest
+import torch
+
+from test_gpu_modules import check, cos, log
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _q(x, s):
+    return (x.double() * s).float().clamp(-448, 448).to(torch.float8_e4m3fn).double()
+
+
+def _emulate(A, B):
+    """A [M,K], B [K,N] fp32 CPU -> fp8 e4m3 per-tensor-scaled product in float64."""
+    sa = 448.0 / float(A.abs().max())
+    sb = 448.0 / float(B.abs().max())
+    sa32, sb32 = torch.tensor(sa, dtype=torch.float32).item(), torch.tensor(sb, dtype=torch.float32).item()
+    return (_q(A, sa32) @ _q(B, sb32)) / (sa32 * sb32)
+
+
+@pytest.mark.parametrize('layout', ['nt', 'nn', 'tn'])
+def test_fp8_gemm_lane_maps_exact_integers(layout):
+    import ewvit
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 96, 80, 160
+    A = torch.randint(-8, 9, (M, K), generator=g).float()
+    B = torch.randint(-8, 9, (K, N), generator=g).float()
+    A[3, 7] = 448.0                       # amax 448 -> scale 1: all values exact in e4m3
+    B[5, 2] = -448.0
+    ref = A.double() @ B.double()
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    out = torch.empty(M, N, device=DEV)
+    if layout == 'nt':       # B given as W[N, K] (nn.Linear forward)
+        ewvit.mm_nt(Ad, Bd.t().contiguous(), out, fp8=True)
+    elif layout == 'nn':     # dX = G[M, N'] @ W[N', K']
+        ewvit.mm_nn(Ad, Bd.contiguous(), out, fp8=True)
+    else:                    # dW = G^T X: A given m-contiguous
+        ewvit.mm_tn(Ad.t().contiguous(), Bd.contiguous(), out, fp8=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu().double(), ref)
+
+
+@pytest.mark.parametrize('M,N,K', [(128, 1536, 512), (64, 512, 2048), (37, 100, 70)])
+def test_fp8_gemm_vs_torch_e4m3_emulation(M, N, K):
+    import ewvit
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g) * 3
+    W = torch.randn(N, K, generator=g) * 0.05
+    ref = _emulate(A, W.t())
+    out = torch.empty(M, N, device=DEV)
+    ewvit.mm_nt(A.to(DEV), W.to(DEV), out, fp8=True)
+    err = float((out.cpu().double() - ref).abs().max()) / float(ref.abs().max())
+    log('fp8_vs_emulation', err, 1e-5)
+    assert err <= 1e-5, err
+    # and the e4m3 product is an approximation of the exact one (sanity of the scaling)
+    exact = A.double() @ W.t().double()
+    assert cos(out.cpu(), exact) > 0.995
+
+
+def test_fp8_gemm_splitk_patch_embedding_shape():
+    import ewvit
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 64, 512, 62720
+    X = torch.randn(M, K, generator=g).relu()          # backbone map after SiLU/ReLU-like
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    out = torch.empty(M, N, device=DEV)
+    ewvit.mm_nt(X.to(DEV).bfloat16(), W.to(DEV), out, fp8=True)   # bf16 activations, fp32 master weight
+    ref = _emulate(X.bfloat16().float(), W.t())
+    err = float((out.cpu().double() - ref).abs().max()) / float(ref.abs().max())
+    log('fp8_splitk_vs_emulation', err, 1e-5)
+    assert err <= 1e-5, err
+
+
+# fp8 bound of the DAMA train step: the token GEMMs carry 3-bit mantissas, so the SFE /
+# cross-attention outputs move by about the e4m3 step (2^-4 relative) averaged over K;
+# set from the measured values (profiles/r02/parity_fp8.jsonl), fixed.
+FP8_OUT_TOL, FP8_OUT_COS, FP8_GRAD_COS = 8e-2, 0.997, 0.93
+
+
+def test_dama_train_step_fp8_vs_oracle():
+    import copy
+    from network import dama, set_gemm_precision
+    from oracle import model as om
+    from oracle.weights import recipe_input
+    from test_gpu_modules import pair
+    torch.manual_seed(0)
+    p, o = pair(dama.DAMA, om.DAMA, (3, 128, 4, 3, 8), 14)
+    assert set_gemm_precision(p, 'fp8') == 22
+    p.train(); o.train()
+    x = recipe_input((2, 8, 3, 224, 224), seed=4242)
+    ro = o(x, batch_size=4)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        rp = p(x.to(DEV), batch_size=4)
+    for k in ro:
+        check(rp[k], ro[k], FP8_OUT_TOL, FP8_OUT_COS)
+    w = {k: torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) for i, (k, v) in enumerate(sorted(ro.items()))}
+    sum((ro[k] * w[k]).sum() for k in ro).backward()
+    sum((rp[k].float() * w[k].to(DEV)).sum() for k in rp).backward()
+    pp, oo = dict(p.named_parameters()), dict(o.named_parameters())
+    for n in ('sfe.patch_to_embedding.weight', 'sfe.transformer.layers.0.0.fn.to_qkv.weight',
+              'sfe.transformer.layers.1.1.fn.net.0.weight', 'cross_att.layers.1.3.to_kv.weight',
+              'cross_att.layers.0.1.to_out.0.weight', 'sfe.feat_map.0.weight'):
+        c = cos(pp[n].grad, oo[n].grad)
+        log('fp8_grad_cos:' + n, c, FP8_GRAD_COS)
+        assert c >= FP8_GRAD_COS, (n, c)
+
+
+def test_set_gemm_precision_targets():
+    from network import set_gemm_precision
+    from network.model import DeepfakeDetector
+    m = DeepfakeDetector(3, 128, 4)
+    assert set_gemm_precision(m, 'fp8') == 22
+    assert m.dama.sfe.patch_to_embedding.gemm_precision == 'fp8'
+    assert getattr(m.classifier[0], 'gemm_precision', 'bf16') == 'bf16'
+    assert getattr(m.dama.gate_net[2], 'gemm_precision', 'bf16') == 'bf16'
+    with pytest.raises(ValueError):
+        set_gemm_precision(m, 'fp4')
+
+
+def test_config5_two_chunks_equal_per_chunk_composition():
+    """x [16, 8, 3, 224, 224], batch_size=4 (dama.py:179-199): two 64-frame chunks, per-video
+    sums over chunks / K — equal to composing _process_frame on each chunk by hand."""
+    from network import dama, set_gemm_precision
+    torch.manual_seed(0)
+    m = dama.DAMA(3, 128, 4, 3, 4).to(DEV).to(memory_format=torch.channels_last).eval()
+    set_gemm_precision(m, 'fp8')
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(16, 8, 3, 224, 224, device=DEV, generator=g)
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        out = m(x, batch_size=4)
+        acc = None
+        for s in (0, 4):
+            f = m._process_frame(x[:, s:s + 4].flatten(0, 1))
+            part = {k: v.float().view(16, -1, 128).sum(1) for k, v in f.items()}
+            acc = part if acc is None else {k: acc[k] + part[k] for k in acc}
+    for k in out:
+        assert out[k].shape == (16, 128)
+        torch.testing.assert_close(out[k].float(), acc[k] / 8, rtol=1e-5, atol=1e-6)
