@@ -278,7 +278,7 @@ def workload(args, world, step):
                 'launch': step.mode, 'baseline_config': 4}
     cfg = CONFIGS[args.config]
     return {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
-            'image': 224, 'frames_per_gpu': args.frames, 'dim': 128, 'chunk_frames': 8 * cfg['chunk'],
+            'image': 224, 'frames_per_gpu': args.frames, 'dim': 128, 'chunk_frames': cfg['videos'] * cfg['chunk'],
             'token_gemms': cfg['gemm'], 'global_batch': args.frames * world, 'parallelism': f'dp{world}',
             'launch': step.mode, 'baseline_config': 3 if world > 1 else args.config}
 

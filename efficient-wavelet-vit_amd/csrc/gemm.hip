@@ -234,11 +234,34 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 template <int DT>
 __global__ __launch_bounds__(256) void amax_partial_kernel(const void *x, int64_t rows, int64_t cols, int64_t ld,
                                                           float *part) {
-  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
-  const int64_t r0 = (int64_t)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
   float m = 0.f;
-  for (int64_t r = r0; r < r1; ++r)
-    for (int64_t c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, r * ld + c)));
+  if (ld == cols && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // dense: the flat range split evenly over the workgroups, 16-B loads
+    constexpr int V = DT == EWVIT_F32 ? 4 : 8;
+    const int64_t nv = rows * cols / V;
+    const int64_t per = (nv + gridDim.x - 1) / gridDim.x;
+    const int64_t v0 = (int64_t)blockIdx.x * per, v1 = v0 + per < nv ? v0 + per : nv;
+    for (int64_t v = v0 + threadIdx.x; v < v1; v += 256) {
+      const uint4 q = reinterpret_cast<const uint4 *>(x)[v];
+      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (DT == EWVIT_F32) {
+          m = fmaxf(m, fabsf(__uint_as_float(w[i])));
+        } else {
+          m = fmaxf(m, fabsf(__uint_as_float(w[i] << 16)));
+          m = fmaxf(m, fabsf(__uint_as_float(w[i] & 0xffff0000u)));
+        }
+      }
+    }
+    if (blockIdx.x == gridDim.x - 1)          // the tail past the last whole vector
+      for (int64_t i = nv * V + threadIdx.x; i < rows * cols; i += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, i)));
+  } else {
+    const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
+    for (int64_t r = r0; r < r1; ++r)
+      for (int64_t c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, r * ld + c)));
+  }
   __shared__ float red[4];
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;

@@ -113,12 +113,15 @@ def packed():
     """Scope of one forward(+backward) with the weights fixed: packs all registered
     conv weights once on entry; convs inside read the packs."""
     global _active
+    from . import ops
     prepack()
     prev, _active = _active, True
+    prev_amax, ops._weight_amax = ops._weight_amax, {}     # fp8 weight amax: once per step
     try:
         yield
     finally:
         _active = prev
+        ops._weight_amax = prev_amax
 
 
 def _cached_pack(weight, cin_pad, bwd):

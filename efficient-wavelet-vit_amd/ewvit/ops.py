@@ -25,8 +25,9 @@ def _c(t):
 
 # ------------------------------------------------------------------- GEMM
 def amax_partials(X, rows, cols, ld, nparts=None):
-    """Partial maxima of |X| over a [rows x cols] (row stride ld) matrix (ewvit_amax_partials)."""
-    n = nparts or int(max(1, min(L.AMAX_PARTS, rows)))
+    """Partial maxima of |X| over a [rows x cols] (row stride ld) matrix (ewvit_amax_partials):
+    one workgroup per ~16K elements, at most EWVIT_AMAX_PARTS."""
+    n = nparts or int(max(1, min(L.AMAX_PARTS, (rows * cols + 16383) // 16384)))
     part = torch.empty(n, dtype=torch.float32, device=X.device)
     L.call('ewvit_amax_partials', L.ptr(X), L.dt(X), rows, cols, ld, L.ptr(part), n, L.stream(X),
            work={'bytes': rows * cols * X.element_size()})
@@ -41,12 +42,32 @@ def _operand_amax(X, rows_dim, k_dim, ld):
     return amax_partials(X, k_dim, rows_dim, ld[1])
 
 
+# amax partials of fp32 master weights, reused by every fp8 GEMM of one training step (the
+# weights are fixed between optimizer steps): valid inside ewvit.conv.packed() only
+_weight_amax = None
+
+
+def weight_amax(W):
+    """amax partials of a whole weight tensor (any layout: the partition does not matter)."""
+    if _weight_amax is not None:
+        e = _weight_amax.get(id(W))
+        if e is not None and e[0] is W:
+            return e[1]
+    r = amax_partials(W, 1, W.numel(), W.numel()) if W.is_contiguous() else \
+        amax_partials(W.contiguous(), 1, W.numel(), W.numel())
+    if _weight_amax is not None:
+        _weight_amax[id(W)] = (W, r)
+    return r
+
+
 def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, aux=None,
-         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None, fp8=False):
+         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None, fp8=False,
+         amax_a=None, amax_b=None):
     """Raw C[M,N] = epi(alpha * A(M,K) @ B(K,N)).  lda = (lda_m, lda_k), ldb = (ldb_k, ldb_n).
     C must be contiguous with row stride N (ldc = C.stride(0)).
     fp8=True: both operands rounded to OCP e4m3 after per-tensor scaling 448/amax (the amax of
-    each operand is reduced by one launch first; ewvit_gemm_fp8)."""
+    each operand is reduced by one launch first unless its partials are given as amax_a /
+    amax_b = (partials, count); ewvit_gemm_fp8)."""
     L.require_gpu(A, B, C)
     if splitk is None:
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
@@ -63,8 +84,8 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
             L.ptr(aux), float(drop_p), seed, L.ptr(seed_offset), L.ptr(resid),
             L.dt(resid) if resid is not None else 0, ldr, splitk, L.ptr(ws))
     if fp8:
-        pa, na = _operand_amax(A, M, K, lda)
-        pb, nb = _operand_amax(B, N, K, (ldb[1], ldb[0]))
+        pa, na = amax_a if amax_a is not None else _operand_amax(A, M, K, lda)
+        pb, nb = amax_b if amax_b is not None else _operand_amax(B, N, K, (ldb[1], ldb[0]))
         L.call('ewvit_gemm_fp8', *args, L.ptr(pa), na, L.ptr(pb), nb, L.stream(C), work=work)
     else:
         L.call('ewvit_gemm', *args, L.stream(C), work=work)
@@ -118,8 +139,13 @@ class LinearFn(torch.autograd.Function):
         seed = _seed() if drop_p > 0 else 0
         soff = L.rng_offset(x.device) if drop_p > 0 else None
         r2 = _c(resid.reshape(M, N)) if resid is not None else None
+        # fp8: the operands' amax partials are taken once and shared — X's by the forward and
+        # the weight gradient, the weight's by every GEMM of the step, dY's by both backward GEMMs
+        xa = amax_partials(x2, M, K, K) if fp8 else None
         mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
-              resid=r2, ldr=N if r2 is not None else 0, fp8=fp8)
+              resid=r2, ldr=N if r2 is not None else 0, fp8=fp8, amax_a=xa,
+              amax_b=weight_amax(weight) if fp8 else None)
+        ctx.xa = xa
         ctx.save_for_backward(x2, weight, aux)
         ctx.params = (weight, bias)          # gradient slots (ewvit.grads)
         ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None, fp8)
@@ -140,13 +166,15 @@ class LinearFn(torch.autograd.Function):
             L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux), act, float(drop_p), seed,
                    L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
         dx = dw = db = None
+        ga = amax_partials(g, M, N, N) if fp8 and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
         if ctx.needs_input_grad[0]:
-            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device), fp8=fp8).reshape(*lead, K)
+            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device), fp8=fp8, amax_a=ga,
+                       amax_b=weight_amax(weight) if fp8 else None).reshape(*lead, K)
         if ctx.needs_input_grad[1]:
             dw = grad_out(ctx.params[0])
             if not dw.is_contiguous():
                 dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-            dw = mm_tn(g, x2, dw, fp8=fp8)
+            dw = mm_tn(g, x2, dw, fp8=fp8, amax_a=ga, amax_b=ctx.xa)
         if has_bias and ctx.needs_input_grad[2]:
             db = colsum(g, grad_out(ctx.params[1]))
         dres = dy if has_res and ctx.needs_input_grad[5] else None
