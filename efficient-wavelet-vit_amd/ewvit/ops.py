@@ -5,6 +5,7 @@ HIP stream and autograd.  Every FLOP of these ops runs in libewvit.so; inputs
 on a non-ROCm device raise (no CPU path).
 """
 import math
+from typing import Optional, Tuple
 
 import torch
 
@@ -122,169 +123,292 @@ def colsum(X, out, accumulate=False):
     return out
 
 
-class LinearFn(torch.autograd.Function):
-    """y = dropout(act(x @ W^T + b)) + resid — nn.Linear (+ReLU/GELU/Dropout/residual)
-    of network/sfe.py:29-55,127,134-142 and network/dama.py:25-31,105-113."""
+# ------------------------------------------------------------- custom ops
+# The hot-path ops of the north_star (projection / MLP GEMMs, LayerNorm, attention, the DWT
+# front end) are torch.library custom ops in the `ewvit` namespace (torch.ops.ewvit.*): a real
+# implementation launching the C-ABI, a fake (meta) implementation so FakeTensor and
+# torch.compile trace through them without running kernels, and autograd registered with
+# torch.library.register_autograd whose backward is itself made of ewvit custom ops.
 
-    @staticmethod
-    def forward(ctx, x, weight, bias, act, drop_p, resid, out_dtype, fp8=False):
-        L.require_gpu(x, weight)
-        K = x.shape[-1]
-        lead = x.shape[:-1]
-        x2 = _c(x.reshape(-1, K))
-        M, N = x2.shape[0], weight.shape[0]
-        y = torch.empty(M, N, dtype=out_dtype, device=x.device)
-        need_aux = act in (1, 2) and any(ctx.needs_input_grad[:3])
-        aux = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if need_aux else None
-        seed = _seed() if drop_p > 0 else 0
-        soff = L.rng_offset(x.device) if drop_p > 0 else None
-        r2 = _c(resid.reshape(M, N)) if resid is not None else None
-        # fp8: the operands' amax partials are taken once and shared — X's by the forward and
-        # the weight gradient, the weight's by every GEMM of the step, dY's by both backward GEMMs
-        xa = amax_partials(x2, M, K, K) if fp8 else None
-        mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
-              resid=r2, ldr=N if r2 is not None else 0, fp8=fp8, amax_a=xa,
-              amax_b=weight_amax(weight) if fp8 else None)
-        ctx.xa = xa
-        ctx.save_for_backward(x2, weight, aux)
-        ctx.params = (weight, bias)          # gradient slots (ewvit.grads)
-        ctx.cfg = (act, drop_p, seed, lead, x.dtype, resid is not None, bias is not None, fp8)
-        return y.reshape(*lead, N)
+_EMPTY = (0,)
 
-    @staticmethod
-    def backward(ctx, dy):
-        x2, weight, aux = ctx.saved_tensors
-        act, drop_p, seed, lead, xdt, has_res, has_bias, fp8 = ctx.cfg
-        M, K = x2.shape
-        N = weight.shape[0]
-        dy2 = _c(dy.reshape(M, N))
-        if act == 0 and drop_p == 0:
-            g = dy2
-        else:
-            g = torch.empty(M, N, dtype=torch.float32, device=dy.device)
-            soff = L.rng_offset(dy.device) if drop_p > 0 else None
-            L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux), act, float(drop_p), seed,
-                   L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
-        dx = dw = db = None
-        ga = amax_partials(g, M, N, N) if fp8 and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
-        if ctx.needs_input_grad[0]:
-            dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=xdt, device=dy.device), fp8=fp8, amax_a=ga,
-                       amax_b=weight_amax(weight) if fp8 else None).reshape(*lead, K)
-        if ctx.needs_input_grad[1]:
-            dw = grad_out(ctx.params[0])
-            if not dw.is_contiguous():
-                dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-            dw = mm_tn(g, x2, dw, fp8=fp8, amax_a=ga, amax_b=ctx.xa)
-        if has_bias and ctx.needs_input_grad[2]:
-            db = colsum(g, grad_out(ctx.params[1]))
-        dres = dy if has_res and ctx.needs_input_grad[5] else None
-        return dx, dw, db, None, None, dres, None, None
+
+def _seed_for(drop_p):
+    return _seed() if drop_p > 0 else 0
+
+
+@torch.library.custom_op('ewvit::linear', mutates_args=())
+def _linear_op(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], act: int, drop_p: float,
+               seed: int, resid: Optional[torch.Tensor], out_dtype: torch.dtype, fp8: bool,
+               need_aux: bool) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """y = dropout(act(x @ W^T + b)) + resid — nn.Linear (+ReLU/GELU/Dropout/residual) of
+    network/sfe.py:29-55,127,134-142 and network/dama.py:25-31,105-113.
+    -> (y [*, N], aux = bf16 pre-activation [M, N] (act 1/2 with need_aux, else empty),
+        x amax partials (fp8, else empty))."""
+    L.require_gpu(x, weight)
+    K = x.shape[-1]
+    lead = x.shape[:-1]
+    x2 = _c(x.reshape(-1, K))
+    M, N = x2.shape[0], weight.shape[0]
+    y = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if (need_aux and act in (1, 2)) else None
+    soff = L.rng_offset(x.device) if drop_p > 0 else None
+    r2 = _c(resid.reshape(M, N)) if resid is not None else None
+    # fp8: the operands' amax partials are taken once and shared — X's by the forward and
+    # the weight gradient, the weight's by every GEMM of the step, dY's by both backward GEMMs
+    xa = amax_partials(x2, M, K, K) if fp8 else None
+    mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
+          resid=r2, ldr=N if r2 is not None else 0, fp8=fp8, amax_a=xa,
+          amax_b=weight_amax(weight) if fp8 else None)
+    e = x.new_empty(_EMPTY, dtype=torch.float32)
+    return y.reshape(*lead, N), (aux if aux is not None else e.to(torch.bfloat16)), (xa[0] if fp8 else e.clone())
+
+
+@_linear_op.register_fake
+def _(x, weight, bias, act, drop_p, seed, resid, out_dtype, fp8, need_aux):
+    M = x.numel() // x.shape[-1]
+    N = weight.shape[0]
+    aux = x.new_empty((M, N) if (need_aux and act in (1, 2)) else _EMPTY, dtype=torch.bfloat16)
+    xa = x.new_empty((int(max(1, min(L.AMAX_PARTS, (x.numel() + 16383) // 16384))),) if fp8 else _EMPTY,
+                     dtype=torch.float32)
+    return x.new_empty((*x.shape[:-1], N), dtype=out_dtype), aux, xa
+
+
+@torch.library.custom_op('ewvit::linear_backward', mutates_args=('dw_out', 'db_out'))
+def _linear_backward_op(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, aux: torch.Tensor,
+                        xa: torch.Tensor, act: int, drop_p: float, seed: int, need_dx: bool, fp8: bool,
+                        dw_out: Optional[torch.Tensor], db_out: Optional[torch.Tensor]) -> torch.Tensor:
+    """dX (x's dtype; empty unless need_dx), dW into dw_out and db into db_out when given
+    (gradient slots of the data-parallel flat buffer, ewvit.grads)."""
+    K = x.shape[-1]
+    x2 = _c(x.reshape(-1, K))
+    M, N = x2.shape[0], weight.shape[0]
+    dy2 = _c(dy.reshape(M, N))
+    if act == 0 and drop_p == 0:
+        g = dy2
+    else:
+        g = torch.empty(M, N, dtype=torch.float32, device=dy.device)
+        soff = L.rng_offset(dy.device) if drop_p > 0 else None
+        L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux) if aux.numel() else None, act,
+               float(drop_p), seed, L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
+    ga = amax_partials(g, M, N, N) if fp8 and (need_dx or dw_out is not None) else None
+    dx = dy.new_empty(_EMPTY, dtype=x.dtype)
+    if need_dx:
+        dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=x.dtype, device=dy.device), fp8=fp8, amax_a=ga,
+                   amax_b=weight_amax(weight) if fp8 else None).reshape(x.shape)
+    if dw_out is not None:
+        dw = dw_out if dw_out.is_contiguous() else torch.empty(N, K, dtype=torch.float32, device=dy.device)
+        mm_tn(g, x2, dw, fp8=fp8, amax_a=ga, amax_b=(xa, xa.numel()) if fp8 else None)
+        if dw is not dw_out:
+            dw_out.copy_(dw)
+    if db_out is not None:
+        colsum(g, db_out)
+    return dx
+
+
+@_linear_backward_op.register_fake
+def _(dy, x, weight, aux, xa, act, drop_p, seed, need_dx, fp8, dw_out, db_out):
+    return dy.new_empty(x.shape if need_dx else _EMPTY, dtype=x.dtype)
+
+
+def _linear_setup(ctx, inputs, output):
+    x, weight, bias, act, drop_p, seed, resid, out_dtype, fp8, need_aux = inputs
+    _, aux, xa = output
+    ctx.mark_non_differentiable(aux, xa)
+    ctx.save_for_backward(x, weight, aux, xa)
+    ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
+    ctx.cfg = (act, drop_p, seed, resid is not None, bias is not None, fp8)
+
+
+def _linear_backward(ctx, dy, _daux, _dxa):
+    x, weight, aux, xa = ctx.saved_tensors
+    act, drop_p, seed, has_res, has_bias, fp8 = ctx.cfg
+    need = ctx.needs_input_grad
+    dw = db = None
+    if need[1]:
+        dw = grad_out(ctx.params[0])
+    if has_bias and need[2]:
+        db = grad_out(ctx.params[1])
+        if db.dim() != 1 or not db.is_contiguous():
+            db = torch.empty(db.shape[0], dtype=torch.float32, device=dy.device)
+    dx = torch.ops.ewvit.linear_backward(dy, x, weight, aux, xa, act, drop_p, seed, bool(need[0]), fp8, dw, db)
+    dres = dy if has_res and need[6] else None
+    return (dx if need[0] else None), dw, db, None, None, None, dres, None, None, None
+
+
+_linear_op.register_autograd(_linear_backward, setup_context=_linear_setup)
 
 
 def linear(x, weight, bias=None, act=0, drop_p=0.0, resid=None, out_dtype=torch.float32, fp8=False):
-    """fp8=True: the forward and both backward GEMMs take OCP e4m3 operands with per-tensor
-    scaling (BASELINE configs[4]); the epilogue (bias, activation, dropout, residual) is fp32."""
-    return LinearFn.apply(x, weight, bias, act, float(drop_p), resid, out_dtype, bool(fp8))
+    """torch.ops.ewvit.linear with autograd.  act 0 none / 1 GELU(erf) / 2 ReLU; dropout and
+    the residual add fused in the GEMM epilogue.  fp8=True: the forward and both backward
+    GEMMs take OCP e4m3 operands with per-tensor scaling (BASELINE configs[4]); the epilogue
+    (bias, activation, dropout, residual) is fp32."""
+    drop_p = float(drop_p)
+    need_aux = act in (1, 2) and torch.is_grad_enabled() and (
+        x.requires_grad or weight.requires_grad or (bias is not None and bias.requires_grad))
+    y, _, _ = torch.ops.ewvit.linear(x, weight, bias, int(act), drop_p, _seed_for(drop_p), resid, out_dtype,
+                                     bool(fp8), bool(need_aux))
+    return y
 
 
 # -------------------------------------------------------------- LayerNorm
-class LayerNormFn(torch.autograd.Function):
-    """nn.LayerNorm over the last dim (network/sfe.py:23, network/dama.py:62,64)."""
+@torch.library.custom_op('ewvit::layer_norm', mutates_args=())
+def _layer_norm_op(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
+                   out_dtype: torch.dtype) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """nn.LayerNorm over the last dim (network/sfe.py:23, network/dama.py:62,64) -> (y, mean, rstd)."""
+    L.require_gpu(x, weight)
+    D = x.shape[-1]
+    x2 = _c(x.reshape(-1, D))
+    M = x2.shape[0]
+    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    L.call('ewvit_layernorm_fwd', L.ptr(x2), L.dt(x2), D, L.ptr(weight), L.ptr(bias), L.ptr(y),
+           L.dt(y), L.ptr(mean), L.ptr(rstd), M, D, float(eps), L.stream(y))
+    return y.reshape(x.shape), mean, rstd
 
-    @staticmethod
-    def forward(ctx, x, gamma, beta, eps, out_dtype):
-        L.require_gpu(x, gamma)
-        D = x.shape[-1]
-        x2 = _c(x.reshape(-1, D))
-        M = x2.shape[0]
-        y = torch.empty(M, D, dtype=out_dtype, device=x.device)
-        mean = torch.empty(M, dtype=torch.float32, device=x.device)
-        rstd = torch.empty_like(mean)
-        L.call('ewvit_layernorm_fwd', L.ptr(x2), L.dt(x2), D, L.ptr(gamma), L.ptr(beta), L.ptr(y),
-               L.dt(y), L.ptr(mean), L.ptr(rstd), M, D, float(eps), L.stream(y))
-        ctx.save_for_backward(x2, gamma, mean, rstd)
-        ctx.shape = x.shape
-        ctx.xdt = x.dtype
-        return y.reshape(x.shape)
 
-    @staticmethod
-    def backward(ctx, dy):
-        x2, gamma, mean, rstd = ctx.saved_tensors
-        M, D = x2.shape
-        dy2 = _c(dy.reshape(M, D))
-        dx = torch.empty(M, D, dtype=torch.float32, device=dy.device)
-        dg = torch.zeros(D, dtype=torch.float32, device=dy.device)
-        db = torch.zeros(D, dtype=torch.float32, device=dy.device)
-        L.call('ewvit_layernorm_bwd', L.ptr(dy2), L.dt(dy2), L.ptr(x2), L.dt(x2), D, L.ptr(gamma),
-               L.ptr(mean), L.ptr(rstd), L.ptr(dx), 0, L.ptr(dg), L.ptr(db), M, D, L.stream(dx))
-        dx = dx.reshape(ctx.shape)
-        if ctx.xdt != torch.float32:
-            dx = dx.to(ctx.xdt)
-        return dx, dg, db, None, None
+@_layer_norm_op.register_fake
+def _(x, weight, bias, eps, out_dtype):
+    M = x.numel() // x.shape[-1]
+    return (x.new_empty(x.shape, dtype=out_dtype), x.new_empty((M,), dtype=torch.float32),
+            x.new_empty((M,), dtype=torch.float32))
+
+
+@torch.library.custom_op('ewvit::layer_norm_backward', mutates_args=())
+def _layer_norm_backward_op(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, mean: torch.Tensor,
+                            rstd: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    D = x.shape[-1]
+    x2 = _c(x.reshape(-1, D))
+    M = x2.shape[0]
+    dy2 = _c(dy.reshape(M, D))
+    dx = torch.empty(M, D, dtype=torch.float32, device=dy.device)
+    dg = torch.zeros(D, dtype=torch.float32, device=dy.device)
+    db = torch.zeros(D, dtype=torch.float32, device=dy.device)
+    L.call('ewvit_layernorm_bwd', L.ptr(dy2), L.dt(dy2), L.ptr(x2), L.dt(x2), D, L.ptr(weight),
+           L.ptr(mean), L.ptr(rstd), L.ptr(dx), 0, L.ptr(dg), L.ptr(db), M, D, L.stream(dx))
+    dx = dx.reshape(x.shape)
+    return (dx if x.dtype == torch.float32 else dx.to(x.dtype)), dg, db
+
+
+@_layer_norm_backward_op.register_fake
+def _(dy, x, weight, mean, rstd):
+    D = x.shape[-1]
+    return (x.new_empty(x.shape), x.new_empty((D,), dtype=torch.float32), x.new_empty((D,), dtype=torch.float32))
+
+
+def _ln_setup(ctx, inputs, output):
+    x, weight, _, _, _ = inputs
+    _, mean, rstd = output
+    ctx.mark_non_differentiable(mean, rstd)
+    ctx.save_for_backward(x, weight, mean, rstd)
+
+
+def _ln_backward(ctx, dy, _dm, _dr):
+    x, weight, mean, rstd = ctx.saved_tensors
+    dx, dg, db = torch.ops.ewvit.layer_norm_backward(dy, x, weight, mean, rstd)
+    return dx, dg, db, None, None
+
+
+_layer_norm_op.register_autograd(_ln_backward, setup_context=_ln_setup)
 
 
 def layer_norm(x, weight, bias, eps=1e-5, out_dtype=torch.bfloat16):
-    return LayerNormFn.apply(x, weight, bias, float(eps), out_dtype)
+    return torch.ops.ewvit.layer_norm(x, weight, bias, float(eps), out_dtype)[0]
 
 
 # -------------------------------------------------------------- attention
-class AttnFn(torch.autograd.Function):
-    """Multi-head softmax attention for the hot path's short sequences.
+@torch.library.custom_op('ewvit::attention', mutates_args=())
+def _attention_op(q_src: torch.Tensor, kv_src: Optional[torch.Tensor], heads: int, dim_head: int,
+                  scale: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Multi-head softmax attention for the hot path's short sequences -> (o, softmax p).
 
-    packed (ViT, sfe.py:59-70): src = qkv [B, n, 3*H*d]  ->  o [B, n, H*d]
-    cross (dama.py:41-53):      src = (q [B, nq, H*d], kv [B, nk, 2*H*d])
+    packed (ViT, sfe.py:59-70): q_src = qkv [B, n, 3*H*d], kv_src None -> o [B, n, H*d]
+    cross (dama.py:41-53):      q_src = q [B, nq, H*d], kv_src = kv [B, nk, 2*H*d]
     """
+    packed = kv_src is None
+    qs = _c(q_src)
+    kvs = qs if packed else _c(kv_src)
+    L.require_gpu(qs, kvs)
+    if qs.dtype != torch.bfloat16 or kvs.dtype != torch.bfloat16:
+        raise TypeError('attn: q/k/v must be bf16 (projection outputs)')
+    B, nq = qs.shape[0], qs.shape[1]
+    nk = kvs.shape[1]
+    inner = heads * dim_head
+    o = torch.empty(B, nq, inner, dtype=torch.bfloat16, device=qs.device)
+    p = torch.empty(B, heads, nq, nk, dtype=torch.float32, device=qs.device)
+    esz = 2
+    q_off, k_off, v_off = (0, inner, 2 * inner) if packed else (0, 0, inner)
+    L.call('ewvit_attn_fwd', qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1), kvs.data_ptr() + k_off * esz,
+           kvs.stride(0), kvs.stride(1), kvs.data_ptr() + v_off * esz, kvs.stride(0), kvs.stride(1), L.ptr(o),
+           o.stride(0), o.stride(1), L.ptr(p), B, heads, nq, nk, dim_head, float(scale), L.stream(o))
+    return o, p
 
-    @staticmethod
-    def forward(ctx, q_src, kv_src, heads, dim_head, scale):
-        packed = kv_src is None
-        qs = _c(q_src)
-        kvs = qs if packed else _c(kv_src)
-        L.require_gpu(qs, kvs)
-        if qs.dtype != torch.bfloat16 or kvs.dtype != torch.bfloat16:
-            raise TypeError('attn: q/k/v must be bf16 (projection outputs)')
-        B, nq = qs.shape[0], qs.shape[1]
-        nk = kvs.shape[1]
-        inner = heads * dim_head
-        o = torch.empty(B, nq, inner, dtype=torch.bfloat16, device=qs.device)
-        p = torch.empty(B, heads, nq, nk, dtype=torch.float32, device=qs.device)
-        esz = 2
-        q_off, k_off, v_off = (0, inner, 2 * inner) if packed else (0, 0, inner)
-        kp = kvs.data_ptr() + k_off * esz
-        vp = kvs.data_ptr() + v_off * esz
-        L.call('ewvit_attn_fwd', qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1), kp, kvs.stride(0),
-               kvs.stride(1), vp, kvs.stride(0), kvs.stride(1), L.ptr(o), o.stride(0), o.stride(1),
-               L.ptr(p), B, heads, nq, nk, dim_head, float(scale), L.stream(o))
-        ctx.save_for_backward(qs, kvs if not packed else qs, p)
-        ctx.cfg = (packed, heads, dim_head, scale, q_off, k_off, v_off)
-        return o
 
-    @staticmethod
-    def backward(ctx, do):
-        qs, kvs, p = ctx.saved_tensors
-        packed, heads, d, scale, q_off, k_off, v_off = ctx.cfg
-        do = _c(do)
-        if do.dtype != torch.bfloat16:
-            do = do.to(torch.bfloat16)
-        B, nq, nk = qs.shape[0], qs.shape[1], kvs.shape[1]
-        dqs = torch.empty_like(qs)
-        dkvs = dqs if packed else torch.empty_like(kvs)
-        esz = 2
-        L.call('ewvit_attn_bwd', L.ptr(do), do.stride(0), do.stride(1),
-               qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1),
-               kvs.data_ptr() + k_off * esz, kvs.stride(0), kvs.stride(1),
-               kvs.data_ptr() + v_off * esz, kvs.stride(0), kvs.stride(1), L.ptr(p),
-               dqs.data_ptr() + q_off * esz, dkvs.data_ptr() + k_off * esz, dkvs.data_ptr() + v_off * esz,
-               B, heads, nq, nk, d, float(scale), L.stream(dqs))
-        return dqs, (None if packed else dkvs), None, None, None
+@_attention_op.register_fake
+def _(q_src, kv_src, heads, dim_head, scale):
+    B, nq = q_src.shape[0], q_src.shape[1]
+    nk = nq if kv_src is None else kv_src.shape[1]
+    return (q_src.new_empty((B, nq, heads * dim_head), dtype=torch.bfloat16),
+            q_src.new_empty((B, heads, nq, nk), dtype=torch.float32))
+
+
+@torch.library.custom_op('ewvit::attention_backward', mutates_args=())
+def _attention_backward_op(do: torch.Tensor, q_src: torch.Tensor, kv_src: Optional[torch.Tensor],
+                           p: torch.Tensor, heads: int, dim_head: int,
+                           scale: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> (d q_src, d kv_src) — the packed form returns its whole qkv gradient first and an
+    empty second tensor."""
+    packed = kv_src is None
+    qs = _c(q_src)
+    kvs = qs if packed else _c(kv_src)
+    do = _c(do)
+    if do.dtype != torch.bfloat16:
+        do = do.to(torch.bfloat16)
+    inner = heads * dim_head
+    q_off, k_off, v_off = (0, inner, 2 * inner) if packed else (0, 0, inner)
+    B, nq, nk = qs.shape[0], qs.shape[1], kvs.shape[1]
+    dqs = torch.empty_like(qs)
+    dkvs = dqs if packed else torch.empty_like(kvs)
+    esz = 2
+    L.call('ewvit_attn_bwd', L.ptr(do), do.stride(0), do.stride(1),
+           qs.data_ptr() + q_off * esz, qs.stride(0), qs.stride(1),
+           kvs.data_ptr() + k_off * esz, kvs.stride(0), kvs.stride(1),
+           kvs.data_ptr() + v_off * esz, kvs.stride(0), kvs.stride(1), L.ptr(p),
+           dqs.data_ptr() + q_off * esz, dkvs.data_ptr() + k_off * esz, dkvs.data_ptr() + v_off * esz,
+           B, heads, nq, nk, dim_head, float(scale), L.stream(dqs))
+    return dqs, (qs.new_empty(_EMPTY) if packed else dkvs)
+
+
+@_attention_backward_op.register_fake
+def _(do, q_src, kv_src, p, heads, dim_head, scale):
+    return (torch.empty_like(q_src), q_src.new_empty(_EMPTY) if kv_src is None else torch.empty_like(kv_src))
+
+
+def _attn_setup(ctx, inputs, output):
+    q_src, kv_src, heads, dim_head, scale = inputs
+    _, p = output
+    ctx.mark_non_differentiable(p)
+    ctx.save_for_backward(q_src, kv_src, p)
+    ctx.cfg = (heads, dim_head, scale)
+
+
+def _attn_backward(ctx, do, _dp):
+    q_src, kv_src, p = ctx.saved_tensors
+    dq, dkv = torch.ops.ewvit.attention_backward(do, q_src, kv_src, p, *ctx.cfg)
+    return dq, (dkv if kv_src is not None else None), None, None, None
+
+
+_attention_op.register_autograd(_attn_backward, setup_context=_attn_setup)
 
 
 def attention_packed(qkv, heads, dim_head, scale):
-    return AttnFn.apply(qkv, None, heads, dim_head, scale)
+    return torch.ops.ewvit.attention(qkv, None, int(heads), int(dim_head), float(scale))[0]
 
 
 def attention_cross(q, kv, heads, dim_head, scale):
-    return AttnFn.apply(q, kv, heads, dim_head, scale)
+    return torch.ops.ewvit.attention(q, kv, int(heads), int(dim_head), float(scale))[0]
 
 
 # -------------------------------------------------------------------- DWT
@@ -297,11 +421,15 @@ def _level_sizes(H, W, levels):
     return out
 
 
-def _dwt_flat(x, levels, out_dtype):
-    L.require_gpu(x)
-    if x.requires_grad:
+def _no_grad_input(x):
+    if x.requires_grad and torch.is_grad_enabled():
         raise NotImplementedError('ewvit.dwt_haar: no backward (frames never require grad on the '
                                   'training path, SURVEY §8a note 7)')
+
+
+def _dwt_flat(x, levels, out_dtype):
+    """Raw launch: (ll, all levels' bands flat, level sizes)."""
+    L.require_gpu(x)
     x = _c(x)
     N, C, H, W = x.shape
     sizes = _level_sizes(H, W, levels)
@@ -315,12 +443,46 @@ def _dwt_flat(x, levels, out_dtype):
     return ll, yh, sizes
 
 
+@torch.library.custom_op('ewvit::dwt_haar', mutates_args=())
+def _dwt_haar_op(x: torch.Tensor, levels: int, out_dtype: torch.dtype) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> (ll [N, C, h_L, w_L], every level's bands flat: level l as [N, C, 3, h_l, w_l])."""
+    ll, yh, _ = _dwt_flat(x, levels, out_dtype)
+    return ll, yh
+
+
+@_dwt_haar_op.register_fake
+def _(x, levels, out_dtype):
+    N, C, H, W = x.shape
+    sizes = _level_sizes(H, W, levels)
+    return (x.new_empty((N, C) + sizes[-1], dtype=out_dtype),
+            x.new_empty((sum(N * C * 3 * h * w for h, w in sizes),), dtype=out_dtype))
+
+
+@torch.library.custom_op('ewvit::hf_upsample', mutates_args=())
+def _hf_upsample_op(yh: torch.Tensor, n: int, c: int, h: int, w: int, levels: int, oh: int, ow: int,
+                    out_dtype: torch.dtype, out_channels: int) -> torch.Tensor:
+    oc = out_channels or 3 * c
+    out = torch.empty(levels, n, oh, ow, oc, dtype=out_dtype, device=yh.device)
+    nb = sum(n * 3 * c * hh * ww for hh, ww in _level_sizes(h, w, levels))
+    work = {'bytes': nb * yh.element_size() + out.numel() * out.element_size()}
+    L.call('ewvit_hf_upsample', L.ptr(yh), L.ptr(out), n, c, h, w, levels, oh, ow, L.dt(yh),
+           L.dt(out), oc, L.stream(out), work=work)
+    return out
+
+
+@_hf_upsample_op.register_fake
+def _(yh, n, c, h, w, levels, oh, ow, out_dtype, out_channels):
+    return yh.new_empty((levels, n, oh, ow, out_channels or 3 * c), dtype=out_dtype)
+
+
 def dwt_haar(x, levels=1, out_dtype=torch.float32):
     """Multi-level Haar DWT (pytorch_wavelets DWTForward J=1 'haar' 'zero' applied
     `levels` times, network/mwt.py:20,76,107-111).  x [N,C,H,W] f32/bf16.
     Returns (ll [N,C,h_L,w_L], [yh_1 .. yh_L]) with yh_l [N,C,3,h_l,w_l]."""
-    ll, yh, sizes = _dwt_flat(x, levels, out_dtype)
+    _no_grad_input(x)
+    ll, yh = torch.ops.ewvit.dwt_haar(x, int(levels), out_dtype)
     N, C = x.shape[:2]
+    sizes = _level_sizes(x.shape[2], x.shape[3], levels)
     outs, off = [], 0
     for h, w in sizes:
         n = N * C * 3 * h * w
@@ -332,22 +494,16 @@ def dwt_haar(x, levels=1, out_dtype=torch.float32):
 def hf_upsample(yh_flat_levels, N, C, H, W, levels, out_hw, out_dtype=torch.bfloat16, out_channels=0):
     """Bilinear upsample of every level's bands (mwt.py:77-81) -> [L, N, OH, OW, Cout]
     with Cout = out_channels (>= 3C; channels past 3C are zero) or 3C."""
-    base = yh_flat_levels
-    OH, OW = out_hw
-    oc = out_channels or 3 * C
-    out = torch.empty(levels, N, OH, OW, oc, dtype=out_dtype, device=base.device)
-    nb = sum(N * 3 * C * h * w for h, w in _level_sizes(H, W, levels))
-    work = {'bytes': nb * base.element_size() + out.numel() * out.element_size()}
-    L.call('ewvit_hf_upsample', L.ptr(base), L.ptr(out), N, C, H, W, levels, OH, OW, L.dt(base),
-           L.dt(out), oc, L.stream(out), work=work)
-    return out
+    return torch.ops.ewvit.hf_upsample(yh_flat_levels, int(N), int(C), int(H), int(W), int(levels),
+                                       int(out_hw[0]), int(out_hw[1]), out_dtype, int(out_channels))
 
 
 def dwt_hf_upsample(x, levels, out_hw, out_dtype=torch.bfloat16, band_dtype=torch.bfloat16, out_channels=0):
     """The MWT high-frequency front end for all levels at once: DWT (one read of x)
     then the upsampled, channel-interleaved HF input of hf_conv for every level,
     channels-last: [L, N, OH, OW, 3C] (channel c*3+band; zero-padded to out_channels)."""
-    ll, yh, _ = _dwt_flat(x, levels, band_dtype)
+    _no_grad_input(x)
+    ll, yh = torch.ops.ewvit.dwt_haar(x, int(levels), band_dtype)
     N, C, H, W = x.shape
     return hf_upsample(yh, N, C, H, W, levels, out_hw, out_dtype, out_channels), ll
 
