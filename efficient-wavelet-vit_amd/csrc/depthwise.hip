@@ -432,16 +432,28 @@ static DwShape mk(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int pa
 // the backbone's 7^2 / 14^2 maps give only ~448 blocks of whole rows, but splitting each row
 // in 2 (<= 2048 blocks, one more 3x3 window fill per row) measured slower in the step
 // (2682 vs 2703 frames/s), so the default is 1 — whole rows
-static int dw_segs(const DwShape &s, int rpb) {
-  static const int maxs = [] {
+static int g_dw_maxsegs = -1;      // -1: not read from EWVIT_DW_SEGS yet
+static int dw_max_segs() {
+  if (g_dw_maxsegs < 0) {
     const char *e = getenv("EWVIT_DW_SEGS");
     const int v = e ? atoi(e) : 1;
-    return v < 1 ? 1 : (v > 8 ? 8 : v);
-  }();
+    g_dw_maxsegs = v < 1 ? 1 : (v > 8 ? 8 : v);
+  }
+  return g_dw_maxsegs;
+}
+static int dw_segs(const DwShape &s, int rpb) {
+  const int maxs = dw_max_segs();
   const int64_t nb = ((int64_t)s.N * s.Ho + rpb - 1) / rpb;
   int segs = 1;
   while (segs * 2 <= maxs && nb * segs * 2 <= 2048 && s.Wo / (segs * 2) >= 3) segs *= 2;
   return segs;
+}
+
+// A/B and test knob: the most column segments per row (1 = whole rows, the default; <= 8)
+extern "C" int ewvit_dwconv3x3_set_segs(int max_segs) {
+  EWVIT_CHECK_ARG(max_segs >= 1 && max_segs <= 8, "dwconv3x3_set_segs: %d (1..8)", max_segs);
+  g_dw_maxsegs = max_segs;
+  return 0;
 }
 
 extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,

@@ -48,6 +48,7 @@ SIGNATURES = {
     'ewvit_maxpool2_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp],
     'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
+    'ewvit_dwconv3x3_set_segs': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],

@@ -165,6 +165,11 @@ int ewvit_attn_bwd(const void *dout, int64_t sdo_b, int64_t sdo_n, const void *q
                    int64_t sv_b, int64_t sv_n, const float *p, void *dq, void *dk, void *dv,
                    int64_t B, int64_t H, int nq, int nk, int d, float scale, void *stream);
 
+/* Most column segments per output row the depthwise row kernels may use (1..8; default 1 or
+ * EWVIT_DW_SEGS): an A/B and test knob, not a numerics switch (every split computes the
+ * same sums in the same order). */
+int ewvit_dwconv3x3_set_segs(int max_segs);
+
 /* ------------------------------------------- depthwise 3x3 conv (backbone) ---
  * The MBConv depthwise convolutions of EfficientNetV2-S (groups = channels,
  * kernel 3, stride 1|2, pad 1, no bias) — the backbone the reference reaches

@@ -308,6 +308,30 @@ def test_depthwise_fwd_bwd_vs_torch(N, C, H, stride, dtype):
     assert rel_err(wd.grad, wr.grad) < 1e-5 if dtype == torch.float32 else rel_err(wd.grad, wr.grad) < 1e-4
 
 
+@pytest.mark.parametrize('segs', [2, 4])
+@pytest.mark.parametrize('N,C,H,stride', [(8, 64, 7, 1), (8, 64, 9, 1), (8, 32, 14, 1), (4, 32, 28, 2)])
+def test_depthwise_column_segments_identical(segs, N, C, H, stride):
+    """the column-segment split of the row kernels (ewvit_dwconv3x3_set_segs) gives
+    bit-identical results to whole rows, fwd and input gradient, for Wo in {7, 9, 14}."""
+    import ewvit
+    from ewvit import _lib
+    g = torch.Generator().manual_seed(H * 10 + segs)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().to(DEV).to(memory_format=torch.channels_last)
+    w = torch.randn(C, 1, 3, 3, generator=g).to(DEV)
+    dy = torch.randn(N, C, (H - 1) // stride + 1, (H - 1) // stride + 1, generator=g).bfloat16().to(DEV)
+    outs = []
+    try:
+        for s in (1, segs):
+            _lib.call('ewvit_dwconv3x3_set_segs', s)
+            xd = x.clone().requires_grad_(True)
+            y = ewvit.dwconv3x3(xd, w, stride, 1)
+            y.backward(dy)
+            outs.append((y.detach().clone(), xd.grad.clone()))
+    finally:
+        _lib.call('ewvit_dwconv3x3_set_segs', 1)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_hf_upsample_padded_channels():
     """out_channels > 3C: the bands in channels 0..3C-1 (the unpadded result up to one
     bf16 rounding: the vectorised store path may contract the lerp differently),
