@@ -1254,7 +1254,37 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     return e ? atoi(e) : 2048;
   }();
   const bool wide8 = nwg <= w8max || (DGRAD && bn == 128 && dg8);
-  const int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && wide8 ? 7 : v);
+  int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && wide8 ? 7 : v);
+  // grids of at most EWVIT_CONV_SGMAX blocks (the backbone's long-K 1x1 convs at 7^2 / 14^2:
+  // 50-196 blocks of 15-24 K-tiles — at most one block per CU, so occupancy hides nothing):
+  // EWVIT_CONV_SG = 8: 8 waves with a 4-deep ring (3 K-tiles in flight); 9: 64-row tiles
+  // (twice the blocks), 4 waves, 4-deep ring; 0: as above
+  static const int sg = [] {
+    const char *e = getenv("EWVIT_CONV_SG");
+    return e ? atoi(e) : 8;
+  }();
+  static const int sgmax = [] {
+    const char *e = getenv("EWVIT_CONV_SGMAX");
+    return e ? atoi(e) : 256;
+  }();
+  // (64-row tiles would change the BatchNorm partial rows fwd_bn_rows promised: not with bn_part)
+  if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part)) && nwg <= sgmax) vv = sg;
+  if (vv == 9) {
+    const int64_t mt64 = (a.M + 63) / 64;
+    const dim3 grid9((unsigned)(mt64 * ntn));
+    if (bn == 64) {
+      if (a.g.ks == 1)
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+      else
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+    } else {
+      if (a.g.ks == 1)
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+      else
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+    }
+    return true;
+  }
   if (bn == 64) {
     switch (vv) {
       case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
@@ -1262,6 +1292,7 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
       case 4: EWVIT_GLDS_FWD(256, 64, 3); break;
       case 6: EWVIT_GLDS_FWD(128, 64, 4); break;
       case 7: EWVIT_GLDS_FWDW(128, 64, 2, 4); break;
+      case 8: EWVIT_GLDS_FWDW(128, 64, 4, 4); break;
       default: EWVIT_GLDS_FWD(128, 64, 2); break;
     }
   } else {
@@ -1271,6 +1302,7 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
       case 4: EWVIT_GLDS_FWD(256, 128, 3); break;
       case 6: EWVIT_GLDS_FWD(128, 128, 4); break;
       case 7: EWVIT_GLDS_FWDW(128, 128, 2, 4); break;
+      case 8: EWVIT_GLDS_FWDW(128, 128, 4, 4); break;
       default: EWVIT_GLDS_FWD(128, 128, 2); break;
     }
   }
