@@ -1666,6 +1666,17 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   hipStream_t s = as_stream(stream);
   if (glds) {
     const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
+    // small grids (<= EWVIT_CONV_WSGMAX blocks, at most one per CU): EWVIT_CONV_WSG picks a
+    // deeper-ring family for them (2: 64 pixels, ring 3; 4: 32 pixels, ring 4; 0 keep)
+    static const int wsg = [] {
+      const char *e = getenv("EWVIT_CONV_WSG");
+      return e ? atoi(e) : 0;
+    }();
+    static const int wsgmax = [] {
+      const char *e = getenv("EWVIT_CONV_WSGMAX");
+      return e ? atoi(e) : 256;
+    }();
+    const int gvs = (!wide && gv == 1 && (wsg == 2 || wsg == 4) && (int64_t)nwg <= wsgmax) ? wsg : gv;
 #define EWVIT_GLDS_WG(BK_, NS_, WJ_)                                                                        \
   do {                                                                                                    \
     if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
@@ -1674,7 +1685,7 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
     if (wide == 1) EWVIT_GLDS_WG(64, 2, 8);
     else if (wide == 2) EWVIT_GLDS_WG(32, 2, 8);
     else if (wide == 3) EWVIT_GLDS_WG(32, 3, 8);
-    else switch (gv) {
+    else switch (gvs) {
       case 2: EWVIT_GLDS_WG(64, 3, 4); break;
       case 3: EWVIT_GLDS_WG(32, 3, 4); break;
       case 4: EWVIT_GLDS_WG(32, 4, 4); break;

@@ -44,11 +44,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *x, int xdt, int
   }
 }
 
-// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma += dy*xhat; dbeta += dy
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma = sum dy*xhat; dbeta = sum dy.
+// Each block leaves its dgamma / dbeta partial sums in part[block][2][D]; ln_bwd_fold_kernel
+// adds them in block order (deterministic, no zero-filled accumulator, no float atomics).
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void *dy, int dydt, const void *x, int xdt,
                                                      int64_t ldx, const float *gamma, const float *mean,
                                                      const float *rstd, float *dx, int acc_dx,
-                                                     float *dgamma, float *dbeta, int64_t M, int D,
+                                                     float *part, int64_t M, int D,
                                                      int rows_per_block) {
   __shared__ float sg[4][1024];
   __shared__ float sb[4][1024];
@@ -93,12 +95,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void *dy, int dydt, c
     if (c < D) { sg[w][c] = pg[i]; sb[w][c] = pb[i]; }
   }
   __syncthreads();
+  float *pp = part + (int64_t)blockIdx.x * 2 * D;
   for (int c = threadIdx.x; c < D; c += 256) {
-    const float a = sg[0][c] + sg[1][c] + sg[2][c] + sg[3][c];
-    const float b = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
-    if (dgamma) atomicAdd(&dgamma[c], a);
-    if (dbeta) atomicAdd(&dbeta[c], b);
+    pp[c] = (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]);
+    pp[D + c] = (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]);
   }
+}
+
+// dgamma / dbeta from the per-block partials: thread per column, blocks in order
+__global__ __launch_bounds__(256) void ln_bwd_fold_kernel(const float *part, int nblk, int D, float *dgamma,
+                                                          float *dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 2 * D) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * 2 * D + c];
+  if (c < D) { if (dgamma) dgamma[c] = s; }
+  else if (dbeta) dbeta[c - D] = s;
 }
 
 }  // namespace ewvit
@@ -117,19 +129,30 @@ extern "C" int ewvit_layernorm_fwd(const void *x, int x_dtype, int64_t ldx, cons
   return launch_status("layernorm_fwd");
 }
 
+static int ln_bwd_rpb(int64_t M) { return M >= 16384 ? 16 : 4; }
+
+extern "C" int64_t ewvit_layernorm_bwd_workspace(int64_t M, int64_t D) {
+  return (M + ln_bwd_rpb(M) - 1) / ln_bwd_rpb(M) * 2 * D * (int64_t)sizeof(float);
+}
+
 extern "C" int ewvit_layernorm_bwd(const void *dy, int dy_dtype, const void *x, int x_dtype,
                                    int64_t ldx, const float *gamma, const float *mean,
                                    const float *rstd, float *dx, int accumulate_dx, float *dgamma,
-                                   float *dbeta, int64_t M, int64_t D, void *stream) {
-  EWVIT_CHECK_ARG(dy && x && gamma && mean && rstd && dx, "layernorm_bwd: null pointer");
+                                   float *dbeta, float *workspace, int64_t M, int64_t D, void *stream) {
+  EWVIT_CHECK_ARG(dy && x && gamma && mean && rstd && dx && workspace, "layernorm_bwd: null pointer");
   EWVIT_CHECK_ARG(dtype_ok(dy_dtype) && dtype_ok(x_dtype), "layernorm_bwd: bad dtype");
   EWVIT_CHECK_ARG(D > 0 && D <= 64 * LN_MAXV, "layernorm_bwd: D=%lld not in (0,1024]", (long long)D);
   if (M == 0) return 0;
   // one row per wave: the token counts here are small (M = 128..512), so the grid,
   // not per-block atomics, sets the time
-  const int rpb = M >= 16384 ? 16 : 4;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0,
+  const int rpb = ln_bwd_rpb(M);
+  const int nblk = (int)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nblk), dim3(256), 0,
                      as_stream(stream), dy, dy_dtype, x, x_dtype, ldx, gamma, mean, rstd, dx,
-                     accumulate_dx, dgamma, dbeta, M, (int)D, rpb);
-  return launch_status("layernorm_bwd");
+                     accumulate_dx, workspace, M, (int)D, rpb);
+  if (int rc = launch_status("layernorm_bwd")) return rc;
+  if (!dgamma && !dbeta) return 0;
+  hipLaunchKernelGGL(ln_bwd_fold_kernel, dim3((unsigned)((2 * D + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     workspace, nblk, (int)D, dgamma, dbeta);
+  return launch_status("layernorm_bwd fold");
 }

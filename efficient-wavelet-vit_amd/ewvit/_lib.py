@@ -34,7 +34,7 @@ SIGNATURES = {
     'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp, _vp],
     'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _vp, _i32, _i64, _i64, _vp],
     'ewvit_layernorm_fwd': [_vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _f32, _vp],
-    'ewvit_layernorm_bwd': [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64,
+    'ewvit_layernorm_bwd': [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64,
                             _i64, _vp],
     'ewvit_attn_fwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64,
                        _i64, _i32, _i32, _i32, _f32, _vp],
@@ -80,6 +80,7 @@ SIGNATURES = {
 
 # size queries: name -> (restype, argtypes)
 QUERIES = {
+    'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),

@@ -215,12 +215,15 @@ def _linear_setup(ctx, inputs, output):
     x, weight, bias, act, drop_p, seed, resid, out_dtype, fp8, need_aux = inputs
     _, aux, xa = output
     ctx.mark_non_differentiable(aux, xa)
+    ctx.set_materialize_grads(False)     # no zero-filled gradients for aux / xa
     ctx.save_for_backward(x, weight, aux, xa)
     ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
     ctx.cfg = (act, drop_p, seed, resid is not None, bias is not None, fp8)
 
 
 def _linear_backward(ctx, dy, _daux, _dxa):
+    if dy is None:
+        return (None,) * 10
     x, weight, aux, xa = ctx.saved_tensors
     act, drop_p, seed, has_res, has_bias, fp8 = ctx.cfg
     need = ctx.needs_input_grad
@@ -284,10 +287,11 @@ def _layer_norm_backward_op(dy: torch.Tensor, x: torch.Tensor, weight: torch.Ten
     M = x2.shape[0]
     dy2 = _c(dy.reshape(M, D))
     dx = torch.empty(M, D, dtype=torch.float32, device=dy.device)
-    dg = torch.zeros(D, dtype=torch.float32, device=dy.device)
-    db = torch.zeros(D, dtype=torch.float32, device=dy.device)
+    dg = torch.empty(D, dtype=torch.float32, device=dy.device)
+    db = torch.empty(D, dtype=torch.float32, device=dy.device)
+    ws = torch.empty(L.load().ewvit_layernorm_bwd_workspace(M, D) // 4, dtype=torch.float32, device=dy.device)
     L.call('ewvit_layernorm_bwd', L.ptr(dy2), L.dt(dy2), L.ptr(x2), L.dt(x2), D, L.ptr(weight),
-           L.ptr(mean), L.ptr(rstd), L.ptr(dx), 0, L.ptr(dg), L.ptr(db), M, D, L.stream(dx))
+           L.ptr(mean), L.ptr(rstd), L.ptr(dx), 0, L.ptr(dg), L.ptr(db), L.ptr(ws), M, D, L.stream(dx))
     dx = dx.reshape(x.shape)
     return (dx if x.dtype == torch.float32 else dx.to(x.dtype)), dg, db
 
@@ -302,10 +306,13 @@ def _ln_setup(ctx, inputs, output):
     x, weight, _, _, _ = inputs
     _, mean, rstd = output
     ctx.mark_non_differentiable(mean, rstd)
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(x, weight, mean, rstd)
 
 
 def _ln_backward(ctx, dy, _dm, _dr):
+    if dy is None:
+        return (None,) * 5
     x, weight, mean, rstd = ctx.saved_tensors
     dx, dg, db = torch.ops.ewvit.layer_norm_backward(dy, x, weight, mean, rstd)
     return dx, dg, db, None, None
@@ -390,11 +397,14 @@ def _attn_setup(ctx, inputs, output):
     q_src, kv_src, heads, dim_head, scale = inputs
     _, p = output
     ctx.mark_non_differentiable(p)
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(q_src, kv_src, p)
     ctx.cfg = (heads, dim_head, scale)
 
 
 def _attn_backward(ctx, do, _dp):
+    if do is None:
+        return (None,) * 5
     q_src, kv_src, p = ctx.saved_tensors
     dq, dkv = torch.ops.ewvit.attention_backward(do, q_src, kv_src, p, *ctx.cfg)
     return dq, (dkv if kv_src is not None else None), None, None, None

@@ -98,6 +98,14 @@ class BidirectionalCrossTransformer(nn.Module):                            # dam
         return s, f
 
 
+def _spatial_mean(t):
+    """mean over H, W (dama.py:165-169); over a 1x1 map the mean of one element is that
+    element exactly, so no reduction launch is needed."""
+    if t.shape[-2:] == (1, 1):
+        return t.reshape(t.shape[0], t.shape[1])
+    return t.mean(dim=[2, 3])
+
+
 class FusionGate(nn.Sequential):
     """Conv3x3(2D->D, pad 1) + BN + ReLU (dama.py:124-128).  On a 1x1 map the
     zero padding leaves only the centre tap: one GEMM with W[:, :, 1, 1]."""
@@ -172,20 +180,19 @@ class DAMA(nn.Module):                                                     # dam
         gw = self._gate(concat)
         weighted = (gw[:, 0].view(B, 1, 1, 1) * space_feats + gw[:, 1].view(B, 1, 1, 1) * freq_feats +
                     gw[:, 2].view(B, 1, 1, 1) * fused_feats)
-        return {'fused': weighted.mean(dim=[2, 3]), 'space': space_feats.mean(dim=[2, 3]),
-                'freq': freq_feats.mean(dim=[2, 3])}
+        return {'fused': _spatial_mean(weighted), 'space': _spatial_mean(space_feats),
+                'freq': _spatial_mean(freq_feats)}
 
     def forward(self, x, batch_size=16):
         B, K, C, H, W = x.shape
         if self.training and x.is_cuda:
             ewvit._lib.rng_advance(x.device)   # fresh dropout masks per step, also under graph replay
-        mean_fused = torch.zeros(B, self.dim, device=x.device)
-        mean_space = torch.zeros(B, self.dim, device=x.device)
-        mean_freq = torch.zeros(B, self.dim, device=x.device)
+        # per-video sums over the chunks (fp32, dama.py:174-199); the reference starts from
+        # zeros — 0 + s == s exactly, so the first chunk's sums are taken as they are
+        acc = None
         for start in range(0, K, batch_size):
             end = min(start + batch_size, K)
             feats = self._process_frame(x[:, start:end].flatten(0, 1))
-            mean_fused = mean_fused + feats['fused'].view(B, -1, self.dim).sum(dim=1)
-            mean_space = mean_space + feats['space'].view(B, -1, self.dim).sum(dim=1)
-            mean_freq = mean_freq + feats['freq'].view(B, -1, self.dim).sum(dim=1)
-        return {'fused': mean_fused / K, 'space': mean_space / K, 'freq': mean_freq / K}
+            part = {k: feats[k].float().view(B, -1, self.dim).sum(dim=1) for k in ('fused', 'space', 'freq')}
+            acc = part if acc is None else {k: acc[k] + part[k] for k in acc}
+        return {k: acc[k] / K for k in ('fused', 'space', 'freq')}

@@ -122,34 +122,50 @@ def _cbr(cin, cout, stride=1, conv=Conv3x3):
     return CBR(conv(cin, cout, 3, padding=1, stride=stride), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
 
 
-def bn_relu_groups(x, bns, training, pad=0, levels=1):
-    """BatchNorm modules `bns` over consecutive channel groups of x (+ `pad` trailing
-    all-zero channels normalised by an identity BN, so they stay 0) and ReLU, in ONE
-    fused launch, with separate statistics for each of `levels` batch slices.
-    Running stats / num_batches_tracked end exactly as calling every module on its
-    slice, level after level, would leave them."""
-    dev = x.device
-    w = torch.cat([b.weight for b in bns])
-    bi = torch.cat([b.bias for b in bns])
-    rm = torch.cat([b.running_mean for b in bns])
-    rv = torch.cat([b.running_var for b in bns])
-    if pad:
-        w = torch.cat([w, torch.ones(pad, device=dev)])
-        bi = torch.cat([bi, torch.zeros(pad, device=dev)])
-        rm = torch.cat([rm, torch.zeros(pad, device=dev)])
-        rv = torch.cat([rv, torch.ones(pad, device=dev)])
-    b0 = bns[0]
-    y = ewvit.batch_norm_act_params(x, w, bi, rm, rv, training, b0.momentum, b0.eps, 'relu',
-                                    levels if training else 1)
-    if training:
-        off = 0
-        for b in bns:
-            n = b.num_features
-            b.running_mean.copy_(rm[off:off + n])
-            b.running_var.copy_(rv[off:off + n])
-            b.num_batches_tracked.add_(levels)
-            off += n
-    return y
+class _GroupBN:
+    """The seperate convs' three BatchNorms (plus `pad` identity channels) as ONE fused BN
+    + ReLU launch.  Each of weight, bias, running_mean, running_var is concatenated with its
+    cached constant identity padding by one cat (autograd routes the affine gradients back
+    through the cat), the updated running statistics go back to the modules by one
+    multi-tensor copy and num_batches_tracked advances by one multi-tensor add: 6 launches
+    around the BN instead of ~20 (the modules' own buffers are left in place, so state_dict,
+    .to() and the data-parallel buffer broadcast see ordinary buffers)."""
+
+    def __init__(self):
+        self.pads = {}
+
+    def _pad(self, n, dev):
+        p = self.pads.get((n, dev))
+        if p is None:
+            p = self.pads[(n, dev)] = (torch.ones(n, device=dev), torch.zeros(n, device=dev))
+        return p
+
+    def __call__(self, x, bns, training, pad=0, levels=1):
+        ones, zeros = self._pad(pad, x.device) if pad else (None, None)
+        ext = (lambda ts, c: ts + [c]) if pad else (lambda ts, c: ts)
+        w = torch.cat(ext([b.weight for b in bns], ones))
+        bi = torch.cat(ext([b.bias for b in bns], zeros))
+        rm = torch.cat(ext([b.running_mean for b in bns], zeros))
+        rv = torch.cat(ext([b.running_var for b in bns], ones))
+        b0 = bns[0]
+        y = ewvit.batch_norm_act_params(x, w, bi, rm, rv, training, b0.momentum, b0.eps, 'relu',
+                                        levels if training else 1)
+        if training:
+            dst, src, off = [], [], 0
+            for b in bns:
+                n = b.num_features
+                dst += [b.running_mean, b.running_var]
+                src += [rm[off:off + n], rv[off:off + n]]
+                off += n
+            torch._foreach_copy_(dst, src)
+            torch._foreach_add_([b.num_batches_tracked for b in bns], levels)
+        return y
+
+
+def bn_relu_groups(x, bns, training, pad=0, levels=1, state=None):
+    """One fused BN + ReLU over the channel groups of `bns` (see _GroupBN); `state` keeps the
+    grouped buffers between calls."""
+    return (state if state is not None else _GroupBN())(x, bns, training, pad, levels)
 
 
 def _cdt():
@@ -240,7 +256,9 @@ class MWT(nn.Module):
         else:
             y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
         # BN + ReLU of all levels in one fused launch, per-level statistics
-        y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv)
+        if not hasattr(self, '_sep_bn'):
+            self._sep_bn = _GroupBN()
+        y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv, self._sep_bn)
         fus = self.hf_conv['fusion']
         r = _epi_stats(fus[0], fus[1], y, groups=Lv)
         if r is not None:

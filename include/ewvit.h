@@ -138,12 +138,15 @@ int ewvit_act_bwd(const void *dy, int dy_dtype, int64_t lddy, const void *aux, i
 int ewvit_layernorm_fwd(const void *x, int x_dtype, int64_t ldx, const float *gamma,
                         const float *beta, void *y, int y_dtype, float *mean, float *rstd,
                         int64_t M, int64_t D, float eps, void *stream);
-/* dx = LN backward (x_dtype input, dy dy_dtype); dgamma/dbeta accumulated (+=)
- * in f32; dx written (f32) or added to (accumulate_dx != 0). */
+/* dx = LN backward (x_dtype input, dy dy_dtype); dgamma/dbeta written (=) in f32 (either may be
+ * null); dx written (f32) or added to (accumulate_dx != 0). */
 int ewvit_layernorm_bwd(const void *dy, int dy_dtype, const void *x, int x_dtype, int64_t ldx,
                         const float *gamma, const float *mean, const float *rstd, float *dx,
-                        int accumulate_dx, float *dgamma, float *dbeta, int64_t M, int64_t D,
+                        int accumulate_dx, float *dgamma, float *dbeta, float *workspace, int64_t M, int64_t D,
                         void *stream);
+/* bytes of `workspace` ewvit_layernorm_bwd needs: per-block dgamma / dbeta partials, added in
+ * block order by a second launch (deterministic; dgamma / dbeta need no zero-fill) */
+int64_t ewvit_layernorm_bwd_workspace(int64_t M, int64_t D);
 
 /* ------------------------------------------------- short-sequence attention ---
  * softmax(q k^T * scale) v per (batch, head) for the degenerate sequence
