@@ -1598,7 +1598,19 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
   const int64_t tn = wide ? 2 * CBN : CBN;
   const int64_t tiles = ((NP + tn - 1) / tn) * ((g.Cout + CBM - 1) / CBM);
-  int64_t s = (wide == 1 ? 256 : 512) / tiles;
+  // target workgroups over splits x tiles (A/B: EWVIT_CONV_WSPLIT, default 512; the 1x1
+  // convs of <= 4096 pixels use EWVIT_CONV_WSPLIT_SMALL when set)
+  static const int target = [] {
+    const char *e = getenv("EWVIT_CONV_WSPLIT");
+    const int v = e ? atoi(e) : 512;
+    return v < 16 ? 16 : v;
+  }();
+  static const int target_small = [] {
+    const char *e = getenv("EWVIT_CONV_WSPLIT_SMALL");
+    return e ? atoi(e) : 0;
+  }();
+  const int tg = (target_small > 0 && g.ks == 1 && M <= 4096) ? target_small : target;
+  int64_t s = (wide == 1 ? tg / 2 : tg) / tiles;
   const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;
   const int64_t cap = 2 * M * ((int64_t)g.Cin + g.Cout) / ((int64_t)g.Cout * NP);
