@@ -5,6 +5,7 @@
 
 namespace ewvit {
 static thread_local char g_err[512] = "";
+int g_grid_cap = 0;
 
 void set_error(const char *fmt, ...) {
   va_list ap;
@@ -16,3 +17,11 @@ void set_error(const char *fmt, ...) {
 
 extern "C" int ewvit_abi_version(void) { return EWVIT_ABI_VERSION; }
 extern "C" const char *ewvit_last_error(void) { return ewvit::g_err; }
+
+// workgroups at most per launch of the big-grid kernels (LDS-DMA convs, BatchNorm passes);
+// 0 = no cap.  Set around a branch that shares the GPU with another stream.
+extern "C" int ewvit_set_grid_cap(int max_workgroups) {
+  const int prev = ewvit::g_grid_cap;
+  ewvit::g_grid_cap = max_workgroups > 0 ? (max_workgroups + 7) / 8 * 8 : 0;   // whole XCD rounds
+  return prev;
+}

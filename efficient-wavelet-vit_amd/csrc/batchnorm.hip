@@ -144,6 +144,7 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
   if (nrc > cap) nrc = cap;
   const int64_t maxr = M / ((int64_t)g.RG * minr);
   if (nrc > maxr) nrc = maxr;
+  if (g_grid_cap > 0 && nrc * g.nch * groups > g_grid_cap) nrc = g_grid_cap / ((int64_t)g.nch * groups);
   if (nrc < 1) nrc = 1;
   return (int)nrc;
 }
@@ -158,6 +159,12 @@ static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
   int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
   rpt = rpt < minr ? minr : (rpt > 64 ? 64 : rpt);
+  if (g_grid_cap > 0) {          // capped grid: more rows per block, at most cap blocks in all
+    int64_t nb = g_grid_cap / ((int64_t)g.nch * groups);
+    if (nb < 1) nb = 1;
+    const int64_t need = (M + (int64_t)g.RG * nb - 1) / ((int64_t)g.RG * nb);
+    if (rpt < need) rpt = need;
+  }
   return (int64_t)g.RG * rpt;
 }
 

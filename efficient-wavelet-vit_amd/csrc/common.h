@@ -136,4 +136,7 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
 
 inline bool dtype_ok(int dt) { return dt == EWVIT_F32 || dt == EWVIT_BF16; }
 
+// workgroup cap of the big-grid launches (abi.hip, ewvit_set_grid_cap); 0 = none
+extern int g_grid_cap;
+
 }  // namespace ewvit

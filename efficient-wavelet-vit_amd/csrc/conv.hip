@@ -669,7 +669,7 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
 template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2>
 __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn,
-                                                                      int tap_inner) {
+                                                                      int tap_inner, int ntiles) {
   constexpr int NW = BM / 64 * WC, BK = 64;      // waves: BM/64 rows x WC columns
   constexpr int WN = BN_ / WC, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
@@ -679,7 +679,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
   const int wm = ws / WC, wn = ws % WC;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // tile loop: one tile per workgroup, or — with a capped grid (ewvit_conv2d_set_grid_cap,
+  // a branch sharing the GPU with another stream) — a persistent walk over the tiles
+  for (int ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+  const int tile = xcd_remap(ti, ntiles);
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
   const int K = KS * KS * a.KC;
@@ -887,7 +890,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
       }
     }
   }
-  if (!stats) return;
+  if (stats) {
   // BatchNorm partial statistics of this m-tile: the 16 row lanes of each column
   // (DPP row sums), then the BM/64 waves that share a column block through LDS, in order
 #pragma unroll
@@ -920,6 +923,11 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
       a.bn_part[t * 2 * a.Ncol + a.Ncol + col] = Q;
       if (t == 0 && a.bn_shift_out) a.bn_shift_out[col] = a.bn_shift ? a.bn_shift[col] : 0.f;
     }
+  }
+  }
+  // every wave is done with the LDS ring (and the statistics image) before the next tile
+  // stages into it; the epilogue's stores stay in flight (no vmcnt wait)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 }
 
@@ -1226,15 +1234,16 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
-  const dim3 grid((unsigned)nwg);
+  const int ntiles = (int)nwg;
+  const dim3 grid((unsigned)(g_grid_cap > 0 && nwg > g_grid_cap ? g_grid_cap : nwg));
 #define EWVIT_GLDS_FWDW(BM_, BN__, NS_, WC_)                                                                        \
   do {                                                                                                            \
     if (a.g.ks == 1)                                                                                              \
       hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
-                         src_bytes, ntn, tap_inner);                                                              \
+                         src_bytes, ntn, tap_inner, ntiles);                                                      \
     else                                                                                                          \
       hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
-                         src_bytes, ntn, tap_inner);                                                              \
+                         src_bytes, ntn, tap_inner, ntiles);                                                      \
   } while (0)
 #define EWVIT_GLDS_FWD(BM_, BN__, NS_) EWVIT_GLDS_FWDW(BM_, BN__, NS_, 2)
   // variant 5: a grid of at most one workgroup per CU cannot hide the operand latency
@@ -1271,17 +1280,18 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part)) && nwg <= sgmax) vv = sg;
   if (vv == 9) {
     const int64_t mt64 = (a.M + 63) / 64;
-    const dim3 grid9((unsigned)(mt64 * ntn));
+    const int nt9 = (int)(mt64 * ntn);
+    const dim3 grid9((unsigned)nt9);
     if (bn == 64) {
       if (a.g.ks == 1)
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
       else
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
     } else {
       if (a.g.ks == 1)
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
       else
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner);
+        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
     }
     return true;
   }
@@ -1340,6 +1350,9 @@ static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, 
 }  // namespace ewvit
 
 using namespace ewvit;
+
+extern "C" int ewvit_set_grid_cap(int max_workgroups);
+extern "C" int ewvit_conv2d_set_grid_cap(int max_workgroups) { return ewvit_set_grid_cap(max_workgroups); }
 
 extern "C" int ewvit_conv2d_set_glds(int variant) {
   const int prev = glds_variant();
@@ -1611,6 +1624,7 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   }();
   const int tg = (target_small > 0 && g.ks == 1 && M <= 4096) ? target_small : target;
   int64_t s = (wide == 1 ? tg / 2 : tg) / tiles;
+  if (g_grid_cap > 0 && s * tiles > g_grid_cap) s = g_grid_cap / tiles;
   const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;
   const int64_t cap = 2 * M * ((int64_t)g.Cin + g.Cout) / ((int64_t)g.Cout * NP);

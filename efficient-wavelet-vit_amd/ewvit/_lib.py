@@ -4,6 +4,7 @@ The library is built in-tree (``make -C csrc`` or ``__graft_entry__.build()``)
 and loaded from this directory.  There is no fallback: if the library or a GPU
 is missing, every op raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -48,6 +49,8 @@ SIGNATURES = {
     'ewvit_maxpool2_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp],
     'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
+    'ewvit_conv2d_set_grid_cap': [_i32],
+    'ewvit_set_grid_cap': [_i32],
     'ewvit_dwconv3x3_set_segs': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -184,6 +187,40 @@ def rng_offset(device):
 def rng_advance(device):
     """Advance the dropout step counter (a device op: recorded into a captured step)."""
     rng_offset(device).add_(1)
+
+
+# Workgroup cap of the big-grid launches (LDS-DMA convs, BatchNorm passes) while
+# `grid_cap(n)` is active: a branch that runs on its own stream beside another (DAMA's MWT
+# beside the backbone) walks its tiles / rows on part of the CUs instead of filling the whole
+# GPU.  Ops remember the cap of their forward for their backward launches (`launch_cap`).
+_cap = 0
+
+
+@contextlib.contextmanager
+def grid_cap(n):
+    global _cap
+    prev, _cap = _cap, int(n)
+    try:
+        yield
+    finally:
+        _cap = prev
+
+
+def current_cap():
+    return _cap
+
+
+@contextlib.contextmanager
+def launch_cap(n):
+    """The C-side cap for the launches issued inside (ewvit_set_grid_cap)."""
+    if not n:
+        yield
+        return
+    prev = load().ewvit_set_grid_cap(int(n))
+    try:
+        yield
+    finally:
+        load().ewvit_set_grid_cap(prev)
 
 
 def ptr(t):

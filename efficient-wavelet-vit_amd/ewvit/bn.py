@@ -25,6 +25,14 @@ class BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups, counter,
                 partials=None):
+        ctx.cap = L.current_cap()          # a stream branch's workgroup cap (ewvit._lib.grid_cap)
+        with L.launch_cap(ctx.cap):
+            return BatchNormActFn._forward(ctx, x, weight, bias, running_mean, running_var, training, momentum,
+                                           eps, act, groups, counter, partials)
+
+    @staticmethod
+    def _forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, groups, counter,
+                 partials):
         L.require_gpu(x)
         xc, M, C = _rows(x)
         if M % groups:
@@ -54,6 +62,11 @@ class BatchNormActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        with L.launch_cap(ctx.cap):
+            return BatchNormActFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         training, act, M, C, groups = ctx.cfg
         if not training:
             raise RuntimeError('ewvit BatchNorm: backward through eval-mode statistics is not implemented')

@@ -46,6 +46,8 @@ class SkipLink:
 
 _offered = None
 
+grid_cap = L.grid_cap            # (ewvit._lib: the big-grid workgroup cap of a stream branch)
+
 
 def offer_skip_link(x):
     global _offered
@@ -182,14 +184,16 @@ class Conv2dFn(torch.autograd.Function):
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = bias.detach().float().contiguous() if bias is not None else None
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
-        if bn_stats is not None:
-            # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
-            shift, part, shift_out = bn_stats
-            L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
-                   gc, gs, L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
-        else:
-            L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc,
-                   gs, L.stream(y), work=work)
+        ctx.cap = L.current_cap()
+        with L.launch_cap(ctx.cap):
+            if bn_stats is not None:
+                # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
+                shift, part, shift_out = bn_stats
+                L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
+                       gc, gs, L.ptr(shift), L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
+            else:
+                L.call('ewvit_conv2d_fwd', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride, gc,
+                       gs, L.stream(y), work=work)
         ctx.save_for_backward(xc, weight, wpt)
         ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
         ctx.cfg = (stride, levels, bias is not None, x.dtype)
@@ -198,6 +202,11 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        with L.launch_cap(ctx.cap):
+            return Conv2dFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         xc, weight, wpt = ctx.saved_tensors
         stride, levels, has_bias, xdt = ctx.cfg
         NL, Cz, H, W = xc.shape

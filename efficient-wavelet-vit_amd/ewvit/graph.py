@@ -115,6 +115,7 @@ class GradBuckets:
         self.next = 0
         self.works = []
         self.observed = []
+        self.streams = [set() for _ in self.buckets]     # streams that wrote each bucket
 
     def _hook(self, i):
         def hook(p):
@@ -127,6 +128,8 @@ class GradBuckets:
                     v.copy_(p.grad)
                 p.grad = v
             b = self.bucket_of[i]
+            if v.is_cuda:
+                self.streams[b].add(torch.cuda.current_stream(v.device))
             self.pending[b] -= 1
             self._fire_ready()
         return hook
@@ -134,6 +137,13 @@ class GradBuckets:
     def _fire(self, b):
         s, e, _ = self.buckets[b]
         if self.world > 1 and not self.defer:
+            if self.flat.is_cuda:
+                # the gradients of a bucket may come from several streams (DAMA's MWT branch
+                # runs on its own): the collective, issued on the current stream, waits for all
+                cur = torch.cuda.current_stream(self.flat.device)
+                for st in self.streams[b]:
+                    if st != cur:
+                        cur.wait_stream(st)
             op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
             self.works.append(dist.all_reduce(self.flat[s:e], op=op, group=self.group, async_op=True))
 

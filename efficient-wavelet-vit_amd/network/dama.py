@@ -34,10 +34,20 @@ def _side_stream(device):
 
 
 def _branch_streams():
-    """EWVIT_BRANCH_STREAMS=1 runs the MWT branch on a second stream.  Off by default:
-    measured on MI355X (graph-replayed step) it was 1-1.5 % slower — the MWT's large
-    convs occupy every CU, so the backbone's small kernels gain nothing beside them."""
-    return os.environ.get('EWVIT_BRANCH_STREAMS', '0') == '1'
+    """The MWT branch runs on a second stream beside the backbone (EWVIT_BRANCH_STREAMS=0:
+    one stream).  Uncapped, the MWT's big convs and BatchNorm passes take every CU and the
+    two streams gain ~1 %; with their grids capped (_mwt_grid_cap) the backbone's
+    latency-bound kernels keep most CUs: 2754 -> 2952 frames/s (tools/cap_ab.sh)."""
+    return os.environ.get('EWVIT_BRANCH_STREAMS', '1') == '1'
+
+
+def _mwt_grid_cap():
+    """Workgroups per big-grid MWT launch (LDS-DMA convs, BatchNorm passes) while the MWT
+    shares the GPU with the backbone (EWVIT_MWT_GRID_CAP, 0 = uncapped): the MWT walks its
+    tiles / rows on ~160 of the 256 CUs and the backbone's latency-bound kernels keep the
+    rest.  Measured (config 2, graph replay, 3 rounds): cap 0 2754, 144 2919, 160 2952,
+    192 2910, 224 2870 frames/s; 64 / 96 make the MWT the critical path (1747 / 2300)."""
+    return int(os.environ.get('EWVIT_MWT_GRID_CAP', '160'))
 
 
 class CrossAttention(nn.Module):                                           # dama.py:15-53
@@ -160,7 +170,7 @@ class DAMA(nn.Module):                                                     # dam
         # the MWT ops are recorded after the SFE ops: autograd runs ready backward nodes
         # latest-first, so the MWT backward is issued (on `side`) before the SFE backward
         # fills `main`, and its wait on main covers only the cross-attention backward
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), ewvit._lib.grid_cap(_mwt_grid_cap()):
             freq = self.mwt(frame).float()
         main.wait_stream(side)
         freq.record_stream(main)

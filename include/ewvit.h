@@ -281,6 +281,16 @@ int ewvit_conv2d_pack_weight(const float *w, int64_t s_co, int64_t s_ci, int64_t
 int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co, const int64_t *s_ci,
                               const int64_t *s_tap, void *const *wp, void *const *wp_t, const int64_t *Cout,
                               const int64_t *Cin, const int64_t *Cin_pad, const int *ksize, void *stream);
+/* At most `max_workgroups` (rounded up to a multiple of 8; 0 = no cap, the default) per
+ * launch of the big-grid kernels from now on: LDS-DMA conv fwd / dgrad walk their tiles
+ * persistently, conv wgrad uses fewer pixel splits, the BatchNorm passes take more rows per
+ * workgroup.  For a branch sharing the GPU with another stream (DAMA's MWT beside the
+ * backbone: its big launches then leave most CUs to the backbone's latency-bound kernels).
+ * Host-side state read at launch time (so a HIP graph records the capped grids).  Returns the
+ * previous cap.  ewvit_conv2d_set_grid_cap is the same call. */
+int ewvit_set_grid_cap(int max_workgroups);
+int ewvit_conv2d_set_grid_cap(int max_workgroups);
+
 /* Kernel-family switch for A/B measurement (not needed for correctness): 0 uses the
  * register-staged kernels everywhere; 1..4 (+8: tap-inner K order; default 9, or
  * EWVIT_CONV_GLDS) select an
