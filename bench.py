@@ -351,6 +351,29 @@ def main():
     ewvit._lib.enable_timing(False)
     for r in table.values():
         r['per_step'] = r['launches'] / kt
+    # the same pass with the MWT on the main stream and uncapped grids: each kernel on the
+    # whole chip (the timed step runs the MWT's big launches on 160 of the 256 CUs, beside
+    # the backbone — network/dama.py _mwt_grid_cap — so their as-run durations are longer)
+    iso_table = None
+    if rank == 0 and args.config in (2, 3, 5):
+        saved = {k: os.environ.get(k) for k in ('EWVIT_BRANCH_STREAMS', 'EWVIT_MWT_GRID_CAP')}
+        os.environ['EWVIT_BRANCH_STREAMS'] = '0'
+        os.environ['EWVIT_MWT_GRID_CAP'] = '0'
+        try:
+            ewvit._lib.enable_timing(True)
+            for _ in range(kt):
+                step._eager()
+            torch.cuda.synchronize()
+            iso_table = kernel_table(ewvit._lib.timing_records())
+            ewvit._lib.enable_timing(False)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        for r in iso_table.values():
+            r['per_step'] = r['launches'] / kt
 
     if rank == 0:
         frames = args.frames * world * args.steps
@@ -364,6 +387,13 @@ def main():
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
         res['roofline'] = roofline_for(*dom, config=args.config) if dom else None
+        if res['roofline'] is not None:
+            res['roofline']['timing'] = ('HIP events around every launch of an eager pass of the step as it runs '
+                                         '(MWT on its own stream, its big grids capped at 160 workgroups)')
+        if iso_table and dom and dom[0] in iso_table:
+            iso = roofline_for(dom[0], iso_table[dom[0]], config=args.config)
+            iso['timing'] = 'same pass with one stream and uncapped grids (each kernel on the whole chip)'
+            res['roofline_isolated'] = iso
         if shapes:
             # the hottest single launch configuration (entry point + shape arguments)
             h = dict(shapes[0])

@@ -101,7 +101,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   auto Bs = reinterpret_cast<bf16_t (*)[BN_][LD]>(smem + A_EL);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * CBM;
+  const int64_t ntm = (a.M + CBM - 1) / CBM;
+  // one M-tile per workgroup, or a grid-stride walk when the grid is capped (g_grid_cap)
+  for (int64_t mt = blockIdx.x; mt < ntm; mt += gridDim.x) {
+  const int64_t m0 = mt * CBM;
   const int n0 = blockIdx.y * BN_;
   const int K = KS * KS * a.KC;
   const int nk = (K + BK - 1) / BK;
@@ -279,6 +282,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       *reinterpret_cast<uint4 *>(a.out + (int64_t)gi * a.ogs + row * a.ogc + (col - gi * a.ogc)) =
           *reinterpret_cast<const uint4 *>(&smem[rl * CST + cv * 8]);
     }
+  }
+  __syncthreads();         // the output image is read before the next tile stages into smem
   }
 }
 
@@ -1159,13 +1164,21 @@ static int conv_bk64() {
   return v;
 }
 
+// M-tiles of the register-staged grid: all, or (g_grid_cap) at most cap / N-tiles of them
+static unsigned capped_mtiles(int64_t M, int ntn) {
+  int64_t gx = (M + CBM - 1) / CBM;
+  if (g_grid_cap > 0 && gx * ntn > g_grid_cap) gx = g_grid_cap / ntn > 0 ? g_grid_cap / ntn : 1;
+  return (unsigned)gx;
+}
+
 template <bool DGRAD, int KS, int BK, int PF>
 static void launch_fwd_v(const FwdArgs &a, hipStream_t s) {
   if (a.Ncol <= 64) {
-    dim3 grid((unsigned)((a.M + CBM - 1) / CBM), 1);
+    dim3 grid(capped_mtiles(a.M, 1), 1);
     hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 64, KS, BK, PF>), grid, dim3(256), 0, s, a);
   } else {
-    dim3 grid((unsigned)((a.M + CBM - 1) / CBM), (unsigned)((a.Ncol + CBN - 1) / CBN));
+    const int ntn = (a.Ncol + CBN - 1) / CBN;
+    dim3 grid(capped_mtiles(a.M, ntn), (unsigned)ntn);
     hipLaunchKernelGGL((conv_fwd_kernel<DGRAD, 128, KS, BK, PF>), grid, dim3(256), 0, s, a);
   }
 }
