@@ -680,16 +680,12 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
   constexpr int PA = BM / 8 / NW, PB = BN_ / 8 / NW;   // 1 KiB pieces per wave per K-tile
   static_assert(PB >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
+  constexpr int RED_B = DGRAD ? 0 : BM / 64 * BN_ * 2 * 4;   // fwd BN statistics image, after the ring
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG + RED_B];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
   const int wm = ws / WC, wn = ws % WC;
-  // tile loop: one tile per workgroup, or — with a capped grid (ewvit_conv2d_set_grid_cap,
-  // a branch sharing the GPU with another stream) — a persistent walk over the tiles
-  for (int ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
-  const int tile = xcd_remap(ti, ntiles);
-  const int64_t m0 = (int64_t)(tile / ntn) * BM;
-  const int n0 = (tile % ntn) * BN_;
+  if ((int)blockIdx.x >= ntiles) return;
   const int K = KS * KS * a.KC;
   const int cbn = (a.KC + BK - 1) / BK;   // ragged KC: the last block's lanes >= KC read zeros
   const bool cls = DGRAD && KS == 3 && a.pc >= 0;
@@ -705,9 +701,25 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // rows (fwd: +(kh*W + kw); dgrad: -(kh*W + kw), or -((kh/2)*W + kw/2) at stride 2),
   // so a row keeps one byte offset and a mask of the taps that land inside the image
   // (and, for stride-2 dgrad, on the stride lattice); a K-tile adds one scalar.
+  //
+  // Tile loop: one tile per workgroup, or — with a capped grid (ewvit_set_grid_cap: a
+  // branch sharing the GPU with another stream) — a persistent walk over the tiles.  The
+  // staging cursor runs ahead of the compute cursor across tile boundaries: the next
+  // tile's first K-tiles are in flight while this tile's last ones are multiplied and its
+  // epilogue stores, so a walk pays the ring's fill latency once, not once per tile.
   int rb[PA], lc8[PA];
   unsigned vmask[PA];
+  uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
   const int kcr = a.KCr ? a.KCr : a.KC;
+  // K-tile cursor: tap, channel block, group index / offset of the block.  With
+  // tap_inner the 9 taps of one 64-channel block are consecutive K-tiles, so a block's
+  // live input window (its pixels + halo, 64 channels) stays small enough for the
+  // XCD's L2 to serve the tap re-reads; otherwise taps are outer.
+  int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
+  auto setup = [&](int tile) {          // the staged tile's row / column offsets
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int n0 = (tile % ntn) * BN_;
+  ltap = 0; lcb = 0; lgi = 0; lcin = 0;
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int p = ws * PA + j, r = p * 8 + (lane >> 3);
@@ -752,7 +764,6 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     vmask[j] = msk;
     lc8[j] = lc * 8;
   }
-  uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
     const int p = ws * PB + j, r = p * 8 + (lane >> 3);
@@ -760,12 +771,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     const int n = n0 + r;
     boff[j] = n < a.Ncol ? (uint32_t)(((int64_t)n * K + lc * 8) * 2) : OOB;
   }
-  // K-tile cursor: tap, channel block, group index / offset of the block.  With
-  // tap_inner the 9 taps of one 64-channel block are consecutive K-tiles, so a block's
-  // live input window (its pixels + halo, 64 channels) stays small enough for the
-  // XCD's L2 to serve the tap re-reads; otherwise taps are outer.
-  int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
-  auto stage = [&](int kt, int buf) {
+  };
+  auto stage = [&](int buf) {
     const int rt = cls ? a.tapl[ltap] : ltap;      // the weight tap
     const int kh = rt / KS, kw = rt - kh * KS;
     int dpix;
@@ -797,10 +804,6 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   };
 
   cf32x4 acc[4][J];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
   auto frag = [&](const unsigned char *img, int r, int ch) -> cbf16x8 {
     return *reinterpret_cast<const cbf16x8 *>(img + r * 128 + 16 * (ch ^ ((r >> 1) & 7)));
@@ -824,25 +827,56 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   };
-  int ld = 0, lbuf = 0;
-  for (; ld < NS - 1 && ld < nk; ++ld) {
-    stage(ld, lbuf);
+  // `inflight` counts issued K-tiles not yet multiplied (<= NS-1); the buffer refilled is
+  // always the one every wave finished reading before the last barrier
+  int ts = blockIdx.x, ld = 0, lbuf = 0, inflight = 0, cur = 0;
+  setup(xcd_remap(ts, ntiles));
+  for (; ld < NS - 1 && ld < nk; ++ld, ++inflight) {
+    stage(lbuf);
     lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
   }
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    wait_tile<PA + PB, NS>(nk - 1 - kt);
-    if (ld < nk) {           // refill the buffer every wave finished reading at kt-1
-      stage(ld, lbuf);
+  for (int ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+  const int tile = xcd_remap(ti, ntiles);
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int n0 = (tile % ntn) * BN_;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  int kt = 0;
+  for (; ld < nk; ++kt) {     // steady state: refill with this tile's K-tiles
+    // K-tile kt landed; the inflight-1 younger ones may stay in flight (the previous
+    // tile's epilogue stores, issued after them, only make this wait conservative)
+    wait_tile<PA + PB, NS>(inflight - 1);
+    stage(lbuf);
+    ++ld;
+    lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+    compute(cur);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  // this tile is fully issued: the remaining (<= NS-1) iterations refill with the next
+  // tile's first K-tiles, so they are in flight during this tile's tail and epilogue
+  const bool nxt = ts + (int)gridDim.x < ntiles;
+  if (nxt) {
+    ts += gridDim.x;
+    setup(xcd_remap(ts, ntiles));
+  }
+  ld = 0;
+  for (; kt < nk; ++kt) {
+    wait_tile<PA + PB, NS>(inflight - 1);
+    if (nxt) {
+      stage(lbuf);
       ++ld;
       lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+    } else {
+      --inflight;
     }
     compute(cur);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
   // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
   // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
-  const bool stats = a.bn_part != nullptr;
+  const bool stats = !DGRAD && a.bn_part != nullptr;
   int64_t opx[4];               // parity-class dgrad: the dx pixel of each of this lane's rows
   if (cls) {
 #pragma unroll
@@ -905,8 +939,9 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
       cs[j][r] = row_sum16(cs[j][r]);
       cq[j][r] = row_sum16(cq[j][r]);
     }
-  __syncthreads();                         // every wave is done reading the staging ring
-  float *red = reinterpret_cast<float *>(smem);   // [BM/64][BN_][2]
+  // [BM/64][BN_][2] after the ring (the next tile's K-tiles are landing in it); its
+  // previous tile's readers finished before this tile's K-loop barriers
+  float *red = reinterpret_cast<float *>(smem + NS * STG);
   if (fr == 0)
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -916,7 +951,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
         red[(wm * BN_ + cl) * 2] = cs[j][r];
         red[(wm * BN_ + cl) * 2 + 1] = cq[j][r];
       }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // no vmcnt drain
   if (tid < BN_) {
     const int col = n0 + tid;
     if (col < a.Ncol) {
@@ -930,9 +965,6 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     }
   }
   }
-  // every wave is done with the LDS ring (and the statistics image) before the next tile
-  // stages into it; the epilogue's stores stay in flight (no vmcnt wait)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 }
 

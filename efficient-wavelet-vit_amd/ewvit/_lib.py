@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libewvit.so')
+# EWVIT_LIB: another build of the library (A/B measurements of two kernel versions)
+LIB_PATH = os.environ.get('EWVIT_LIB') or os.path.join(_HERE, 'libewvit.so')
 ABI_VERSION = 2
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
