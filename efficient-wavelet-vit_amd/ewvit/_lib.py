@@ -65,6 +65,8 @@ SIGNATURES = {
     'ewvit_bn_bwd_scaled': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     'ewvit_bn_fold_partials': [_vp, _i32, _vp, _vp, _i32, _vp, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
+    'ewvit_conv2d_stem_fwd': [_vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64,
+                              _i32, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_bwd_data_add': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp],
     'ewvit_conv2d_bwd_data': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_bwd_weight': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64,
@@ -88,6 +90,7 @@ QUERIES = {
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_conv2d_stem_parts': (_i64, [_i64, _i64, _i64, _i32]),
     'ewvit_conv2d_fwd_pack_cin': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_data_add_ok': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),

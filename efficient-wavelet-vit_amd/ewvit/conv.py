@@ -314,6 +314,69 @@ def conv2d_bn_stats(x, weight, bias, stride, shift, levels=1, groups=1, max_rows
     return y, part, shifts, nrc
 
 
+def stem_ok(x, weight, bias, stride):
+    """The frozen backbone stem's shape class (ewvit_conv2d_stem_fwd): 3x3, pad 1, stride
+    1|2, Cin 1..4, Cout 8/16/24/32, f32 / bf16 input, no gradient needed anywhere."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16) and weight.dim() == 4
+            and tuple(weight.shape[2:]) == (3, 3) and 1 <= weight.shape[1] <= 4 and x.shape[1] == weight.shape[1]
+            and weight.shape[0] in (8, 16, 24, 32) and weight.dtype == torch.float32 and stride in (1, 2)
+            and not (torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad
+                                                  or (bias is not None and bias.requires_grad))))
+
+
+_stem_bufs = {}       # id(weight) -> (weakref(weight), padded buffer)
+
+
+def _stem_weight(weight, bias):
+    """The weight as the stem kernel reads it: tap-major [Cin*9][Cout] fp32, the bias as
+    one more row (if any), then 64 padding floats (its scalar loads take 64 bytes at a
+    time).  The buffer persists per parameter; the permuting copy into it is one small
+    launch per call (two with a bias), so a graph-replayed step always reads the
+    parameters' current values."""
+    Cout, n = weight.shape[0], weight.numel()
+    size = n + (Cout if bias is not None else 0) + 64
+    e = _stem_bufs.get(id(weight))
+    buf = e[1] if e is not None and e[0]() is weight else None
+    if buf is None or buf.device != weight.device or buf.numel() != size:
+        buf = torch.zeros(size, dtype=torch.float32, device=weight.device)
+        _stem_bufs[id(weight)] = (weakref.ref(weight), buf)
+    buf[:n].view(n // Cout, Cout).copy_(weight.detach().permute(1, 2, 3, 0).reshape(n // Cout, Cout))
+    if bias is not None:
+        buf[n:n + Cout].copy_(bias.detach())
+    return buf
+
+
+def stem_conv2d(x, weight, bias, stride, shift=None, stats=False, max_rows=256):
+    """Forward-only direct conv of the backbone stem (csrc/stem.hip; reference
+    sfe.py:111-119 freezes it): y bf16 channels-last.  stats=True also returns the
+    BatchNorm partial statistics of y centred on `shift` — (y, part, shifts, nrc) as
+    conv2d_bn_stats — folded to <= max_rows rows."""
+    assert stem_ok(x, weight, bias, stride), 'stem_conv2d: unsupported shape or a gradient is required'
+    N, Cin, H, W = x.shape
+    Cout = weight.shape[0]
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    part = shifts = sh = None
+    nrc = 0
+    if stats:
+        nrc = int(L.load().ewvit_conv2d_stem_parts(N, H, W, int(stride)))
+        part = torch.empty(nrc, 2 * Cout, dtype=torch.float32, device=x.device)
+        shifts = torch.empty(Cout, dtype=torch.float32, device=x.device)
+        sh = shift.detach().float().contiguous() if shift is not None else None
+    w = _stem_weight(weight, bias)
+    L.call('ewvit_conv2d_stem_fwd', L.ptr(x), L.dt(x), N, Cin, H, W, *x.stride(), L.ptr(w), int(bias is not None),
+           L.ptr(y), Cout, int(stride), L.ptr(sh), L.ptr(part), L.ptr(shifts), L.stream(x))
+    if not stats:
+        return y
+    if nrc > max_rows:
+        part2 = torch.empty(1, max_rows, 2 * Cout, dtype=torch.float32, device=x.device)
+        shifts2 = torch.empty(1, Cout, dtype=torch.float32, device=x.device)
+        L.call('ewvit_bn_fold_partials', L.ptr(part), nrc, L.ptr(shifts), L.ptr(part2), max_rows, L.ptr(shifts2),
+               Cout, 1, L.stream(y))
+        part, shifts, nrc = part2, shifts2, max_rows
+    return y, part, shifts, nrc
+
+
 def conv3x3(x, weight, bias=None, stride=1):
     """Conv2d(kernel 3, padding 1, stride)."""
     return Conv2dFn.apply(x, weight, bias, int(stride), 1)

@@ -26,6 +26,8 @@ import ewvit
 _EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '32'))
 # residual blocks hand their skip gradient to the first conv's dgrad epilogue (SkipLink)
 _SKIP_LINK = os.environ.get('EWVIT_SKIP_LINK', '1') != '0'
+# the frozen 3-channel stem on the ewvit direct conv (0: the library conv, A/B)
+_STEM = os.environ.get('EWVIT_STEM', '1') != '0'
 
 STAGES = (
     ('fused', 1, 3, 1, 24, 24, 2),
@@ -53,8 +55,9 @@ class DepthwiseConv2d(nn.Conv2d):
 class Conv2d(nn.Conv2d):
     """Dense 1x1 / 3x3 conv (padding k//2, no dilation, groups 1) on the ewvit MFMA
     implicit-GEMM kernels (csrc/conv.hip) when both channel counts are multiples
-    of 8; the 3-channel stem stays on the library conv.  Parameters identical to
-    nn.Conv2d."""
+    of 8.  The 3-channel stem, frozen on the training path, runs the ewvit direct conv
+    through ConvBNAct._stem; a stem that takes a gradient stays on the library conv.
+    Parameters identical to nn.Conv2d."""
 
     def forward(self, x):
         k = self.kernel_size[0]
@@ -108,9 +111,27 @@ class ConvBNAct(nn.Sequential):
             return ewvit.batch_norm_drop_add(r[0], self[1], skip, drop_prob, partials=r[1], link=link)
         return ewvit.batch_norm_drop_add(self[0](x), self[1], skip, drop_prob, link=link)
 
+    def _stem(self, x, act):
+        """The frozen 3-channel stem (sfe.py:115-119 freezes backbone parameters 0-5): the
+        forward-only ewvit direct conv reading the fp32 NCHW frames, with the BatchNorm
+        statistics summed on the way in training; None when it does not apply."""
+        conv, bn = self[0], self[1]
+        if not (type(conv) is Conv2d and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+                and conv.stride[0] == conv.stride[1] and not self._hooked()
+                and ewvit.conv.stem_ok(x, conv.weight, conv.bias, conv.stride[0])):
+            return None
+        if bn.training and bn.track_running_stats and bn.momentum is not None:
+            r = ewvit.conv.stem_conv2d(x, conv.weight, conv.bias, conv.stride[0], bn.running_mean, stats=True)
+            return ewvit.batch_norm_act(r[0], bn, act, partials=r[1:])
+        return ewvit.batch_norm_act(ewvit.conv.stem_conv2d(x, conv.weight, conv.bias, conv.stride[0]), bn, act)
+
     def forward(self, x):
         conv, bn = self[0], self[1]
         act = 'silu' if len(self) > 2 else None
+        if _STEM and x.is_cuda and x.shape[1] <= 4:
+            y = self._stem(x, act)
+            if y is not None:
+                return y
         r = self._conv_stats(x)
         if r is not None:
             # the conv's epilogue summed the batch statistics: BN runs its apply pass only

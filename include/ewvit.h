@@ -326,6 +326,21 @@ int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *
 int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                      int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
                      int64_t x_group_stride, void *stream);
+/* The backbone stem, forward only (replaces the library conv of the frozen
+ * features.0.0 = Conv2d(3, 24, 3, stride 2, pad 1), reference network/sfe.py:111-119):
+ * y [N, Ho, Wo, Cout] bf16 channels-last = conv(x, w) + bias (fp32 operands and accumulation,
+ * the output rounded once) for x f32 or bf16 at any element strides (sx_*: the frames'
+ * NCHW; x spans < 2 GiB).  w: fp32 tap-major [Cin*9][Cout] (the weight permuted to
+ * [Cin][3][3][Cout]), then, if has_bias, one more row [Cout] holding the bias, then >= 64
+ * readable floats (scalar loads read 64 bytes at a time).  Cin 1..4, Cout 8/16/24/32,
+ * stride 1|2.  bn_part (or NULL) [P][2][Cout] receives per workgroup the shifted
+ * BatchNorm sums of the bf16 output as ewvit_conv2d_fwd_bn leaves them,
+ * P = ewvit_conv2d_stem_parts(N, H, W, stride); bn_shift_out receives K. */
+int64_t ewvit_conv2d_stem_parts(int64_t N, int64_t H, int64_t W, int stride);
+int ewvit_conv2d_stem_fwd(const void *x, int x_dtype, int64_t N, int64_t Cin, int64_t H, int64_t W,
+                          int64_t sx_n, int64_t sx_c, int64_t sx_h, int64_t sx_w, const float *w,
+                          int has_bias, void *y, int64_t Cout, int stride, const float *bn_shift,
+                          float *bn_part, float *bn_shift_out, void *stream);
 /* dx [N, H, W, Cin] from dy [N, Ho, Wo, Cout] and the transposed pack. */
 int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
                           int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
