@@ -188,28 +188,37 @@ def pmc_file(config):
     return os.path.join(REPO, 'profiles', 'pmc_latest.json' if config in (2, 3) else f'pmc_latest_c{config}.json')
 
 
-def pmc_traffic(entry, per_step, config=2):
+# entry points that launch exactly one kernel per call: traffic per call = bytes per dispatch
+PER_DISPATCH = ('ewvit_dwt_haar_fwd', 'ewvit_hf_upsample')
+
+
+def pmc_traffic(entry, per_step, config=2, adam_per_step=None):
     """HBM bytes per launch of `entry` from the committed rocprofv3 PMC passes of the same
-    bench config (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    bench config (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None.  The profiled bench
+    run also executes the eager timing passes and the DWT loop, so the number of step
+    equivalents it ran is counted from the Adam launches it made (Adam runs once per step in
+    every pass; `adam_per_step` multi-tensor launches each), not from the command line."""
     path = pmc_file(config)
     if not os.path.exists(path) or entry not in ENTRY_KERNELS:
         return None
     data = json.load(open(path))
     if data.get('_config', 2) not in ((2, 3) if config in (2, 3) else (config,)):
         return None
-    steps = data.get('_steps_executed')
+    ks = [v for k, v in data.items() if not k.startswith('_') and any(p in k for p in ENTRY_KERNELS[entry])]
+    if not ks:
+        return None
+    tot = sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in ks)
+    if entry in PER_DISPATCH:
+        return round(tot / sum(v['dispatches'] for v in ks), 1)
+    adam = [v['dispatches'] for k, v in data.items() if 'adam_multi_kernel' in k]
+    steps = adam[0] / adam_per_step if adam and adam_per_step else data.get('_steps_executed')
     if not steps or not per_step:
         return None
-    tot = 0.0
-    for k, v in data.items():
-        if k.startswith('_') or not any(p in k for p in ENTRY_KERNELS[entry]):
-            continue
-        tot += v['hbm_bytes_per_launch'] * v['dispatches']
-    return round(tot / (per_step * steps), 1) if tot else None
+    return round(tot / (per_step * steps), 1)
 
 
-def roofline_for(name, row, config=2):
-    traffic = pmc_traffic(name, row.get('per_step'), config)
+def roofline_for(name, row, config=2, adam_per_step=None):
+    traffic = pmc_traffic(name, row.get('per_step'), config, adam_per_step)
     if name in MFMA_ENTRIES:
         ach = row['TFLOP/s']
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': BF16_PEAK_TFS,
@@ -386,19 +395,20 @@ def main():
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
-        res['roofline'] = roofline_for(*dom, config=args.config) if dom else None
+        aps = table.get('ewvit_adam_step', {}).get('per_step')
+        res['roofline'] = roofline_for(*dom, config=args.config, adam_per_step=aps) if dom else None
         if res['roofline'] is not None:
             res['roofline']['timing'] = ('HIP events around every launch of an eager pass of the step as it runs '
                                          '(MWT on its own stream, its big grids capped at 160 workgroups)')
         if iso_table and dom and dom[0] in iso_table:
-            iso = roofline_for(dom[0], iso_table[dom[0]], config=args.config)
+            iso = roofline_for(dom[0], iso_table[dom[0]], config=args.config, adam_per_step=aps)
             iso['timing'] = 'same pass with one stream and uncapped grids (each kernel on the whole chip)'
             res['roofline_isolated'] = iso
         if shapes:
             # the hottest single launch configuration (entry point + shape arguments)
             h = dict(shapes[0])
             h['per_step'] = h['launches'] / kt
-            hot = roofline_for(h['entry'], h, args.config)
+            hot = roofline_for(h['entry'], h, args.config, aps)
             hot['traffic'] = None      # the PMC passes are summarised per kernel symbol, not per shape
             hot['args'] = h['args']
             res['roofline_hot'] = hot
@@ -407,7 +417,7 @@ def main():
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                           for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
         if 'ewvit_dwt_haar_fwd' in table:
-            dr = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'], args.config)
+            dr = roofline_for('ewvit_dwt_haar_fwd', table['ewvit_dwt_haar_fwd'], args.config, aps)
             # the per-launch events of the eager pass add ~10 us around a ~15 us kernel: the
             # achieved rate is taken from back-to-back launches on the same frames replayed
             # from one HIP graph (tools/dwt_bench.py; matches rocprofv3's kernel duration)

@@ -91,7 +91,7 @@ def test_fp8_gemm_splitk_patch_embedding_shape():
     assert err <= 1e-4, err
 
 
-# fp8 bound of the DAMA train step (fixed; measured values in profiles/r02/parity_fp8.jsonl):
+# fp8 bound of the DAMA train step (fixed; measured values in profiles/r02/parity_all.jsonl):
 # the 22 token GEMMs take 3-bit-mantissa operands (e4m3 step 2^-4 relative), on top of the
 # bf16 conv stack.  Measured: outputs 0.055-0.086 of scale / cosine 0.9966-0.9983 (bf16 run:
 # 0.021-0.035 / 0.9994), gradient cosines 0.964-0.994 (bf16: 0.977-0.999).

@@ -9,7 +9,8 @@ mkdir -p "$O"
 STEPS=${STEPS:-all}
 
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -u -m pytest "$R/tests" -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1
+  rm -f "$O/parity.jsonl"
+  EWVIT_PARITY_LOG="$O/parity.jsonl" timeout -k 10 900 python -u -m pytest "$R/tests" -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 "$O/pytest_gpu.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
@@ -18,8 +19,9 @@ if [[ $STEPS == all || $STEPS == *smoke* ]]; then
   rc=$?; echo "smoke rc=$rc"; tail -2 "$O/smoke.log"; [ $rc -eq 0 ] || exit $rc
 fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
-  timeout -k 10 600 python "$R/bench.py" ${BENCH_ARGS:-} > "$O/bench.log" 2>&1
-  rc=$?; echo "bench rc=$rc"; tail -1 "$O/bench.log" | cut -c1-400; [ $rc -eq 0 ] || exit $rc
+  BL=${BENCH_LOG:-bench.log}
+  timeout -k 10 600 python "$R/bench.py" ${BENCH_ARGS:-} > "$O/$BL" 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -1 "$O/$BL" | cut -c1-400; [ $rc -eq 0 ] || exit $rc
 fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
