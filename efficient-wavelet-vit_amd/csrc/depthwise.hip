@@ -221,6 +221,83 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
   }
 }
 
+// ---- bf16 input gradient of a STRIDE-2 pad-1 conv, row form (the first block of stages 4
+// and 6).  dx[hi][wi] only meets the taps with kh = hi+1 (mod 2), kw = wi+1 (mod 2): an even
+// dx row one dy row (kh = 1), an odd one two (kh = 0, 2); likewise along the row, so a thread
+// (8 channels x one dx row segment) walks dx columns in pairs (2j, 2j+1): the even column
+// takes dy column j (kw = 1), the odd one dy columns j+1 (kw = 0) and j (kw = 2) — one new
+// 16-B dy load per dy row per pair, the 72 weights in registers.  (The generic kernel this
+// replaces gathered its weights per lane and tested every tap: 0.5 TB/s.)
+__global__ __launch_bounds__(256) void dw_row_s2_bwd_kernel(const bf16_t *__restrict__ dy, const float *__restrict__ w,
+                                                            bf16_t *__restrict__ dx, DwShape s, int rows_per_block,
+                                                            int segs) {
+  const int C8 = s.C >> 3;
+  const int r = threadIdx.x / C8, c8 = threadIdx.x % C8;
+  if (r >= rows_per_block) return;
+  const int64_t vrow = (int64_t)blockIdx.x * rows_per_block + r;
+  if (vrow >= (int64_t)s.N * s.H * segs) return;
+  const int64_t row = vrow / segs;                                   // n*H + hi
+  const int npair = (s.W + 1) / 2;                                   // dx column pairs
+  const int pseg = (npair + segs - 1) / segs;
+  const int j0 = (int)(vrow - row * segs) * pseg;
+  const int j1 = j0 + pseg < npair ? j0 + pseg : npair;
+  const int hi = (int)(row % s.H);
+  const int n = (int)(row / s.H);
+  const int c = c8 * 8;
+  float wr[9][8];  // [tap][channel]
+  {
+    const float4 *wp = reinterpret_cast<const float4 *>(w + (int64_t)c * 9);
+    float t[72];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+      const float4 q = wp[i];
+      t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wr[k][j] = t[j * 9 + k];
+  }
+  // dy rows: even hi -> ho = hi/2 (kh 1); odd hi -> ho = (hi+1)/2 (kh 0), (hi-1)/2 (kh 2)
+  const bool odd = hi & 1;
+  const int hoA = odd ? (hi + 1) >> 1 : hi >> 1, khA = odd ? 0 : 1;
+  const int hoB = (hi - 1) >> 1, khB = 2;                            // odd rows only
+  const bool okA = hoA < s.Ho, okB = odd && hoB >= 0;
+  const bf16_t *rA = dy + (((int64_t)n * s.Ho + (okA ? hoA : 0)) * s.Wo) * s.C + c;
+  const bf16_t *rB = dy + (((int64_t)n * s.Ho + (okB ? hoB : 0)) * s.Wo) * s.C + c;
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  auto ld = [&](const bf16_t *rp, bool ok, int col) -> uint4 {
+    if (!ok || col < 0 || col >= s.Wo) return zero;
+    return *reinterpret_cast<const uint4 *>(rp + (int64_t)col * s.C);
+  };
+  uint4 a0 = ld(rA, okA, j0), b0 = ld(rB, okB, j0);                  // dy column j of rows A, B
+  bf16_t *xrow = dx + (row * s.W) * s.C + c;
+  for (int j = j0; j < j1; ++j) {
+    const uint4 a1 = ld(rA, okA, j + 1), b1 = ld(rB, okB, j + 1);    // dy column j+1
+    float va0[8], va1[8], vb0[8], vb1[8];
+    bf8_unpack(a0, va0); bf8_unpack(a1, va1); bf8_unpack(b0, vb0); bf8_unpack(b1, vb1);
+    float e[8], o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      // even column 2j: kw = 1 on dy column j;  odd column 2j+1: kw = 0 on j+1, kw = 2 on j
+      // (row B is all zeros for an even dx row: its terms add nothing, no branch)
+      e[q] = fmaf(vb0[q], wr[khB * 3 + 1][q], va0[q] * wr[khA * 3 + 1][q]);
+      o[q] = fmaf(va1[q], wr[khA * 3 + 0][q], va0[q] * wr[khA * 3 + 2][q]);
+      o[q] = fmaf(vb1[q], wr[khB * 3 + 0][q], fmaf(vb0[q], wr[khB * 3 + 2][q], o[q]));
+    }
+    unsigned pe[4], po[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pe[q] = (unsigned)f2bf(e[2 * q]) | ((unsigned)f2bf(e[2 * q + 1]) << 16);
+      po[q] = (unsigned)f2bf(o[2 * q]) | ((unsigned)f2bf(o[2 * q + 1]) << 16);
+    }
+    *reinterpret_cast<uint4 *>(xrow + (int64_t)(2 * j) * s.C) = make_uint4(pe[0], pe[1], pe[2], pe[3]);
+    if (2 * j + 1 < s.W)
+      *reinterpret_cast<uint4 *>(xrow + (int64_t)(2 * j + 1) * s.C) = make_uint4(po[0], po[1], po[2], po[3]);
+    a0 = a1; b0 = b1;
+  }
+}
+
 // ---- bf16 weight gradient, row form.  Thread = 8 channels; it walks whole output
 // rows (row += gridDim.x * R) accumulating its 72 (tap, channel) products in fp32
 // registers over a sliding x window (one dy + 3*s x loads per output).  The R row
@@ -441,6 +518,12 @@ static int dw_max_segs() {
   }
   return g_dw_maxsegs;
 }
+// A/B knob: stride-2 input gradients on the row kernel (1) or the generic per-pixel one (0)
+static int g_dw_s2_rows = [] {
+  const char *e = getenv("EWVIT_DW_S2_ROWS");
+  return e ? atoi(e) : 1;
+}();
+
 static int dw_segs(const DwShape &s, int rpb) {
   const int maxs = dw_max_segs();
   const int64_t nb = ((int64_t)s.N * s.Ho + rpb - 1) / rpb;
@@ -496,6 +579,17 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
     dim3 grid((unsigned)(((int64_t)t.N * t.Ho * segs + rpb - 1) / rpb));
     hipLaunchKernelGGL((dw_row_bf16_kernel<1, true>), grid, dim3(256), 0, as_stream(stream),
                        (const bf16_t *)dy, w, (bf16_t *)dx, t, rpb, segs);
+  } else if (dtype == EWVIT_BF16 && s.stride == 2 && s.pad == 1 && s.C / 8 <= 256 && s.Ho == (s.H + 1) / 2 &&
+             s.Wo == (s.W + 1) / 2 && g_dw_s2_rows) {
+    // stride 2: dx rows in column pairs (dw_row_s2_bwd_kernel); column segments while the
+    // grid is small, as for the forward rows
+    DwShape t = s;
+    t.Ho = s.H; t.Wo = (s.W + 1) / 2;        // rows = dx rows, "columns" = column pairs
+    const int rpb = 256 / (s.C / 8);
+    const int segs = dw_segs(t, rpb);
+    dim3 grid((unsigned)(((int64_t)s.N * s.H * segs + rpb - 1) / rpb));
+    hipLaunchKernelGGL(dw_row_s2_bwd_kernel, grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
+                       (bf16_t *)dx, s, rpb, segs);
   } else {
     const int64_t total = (int64_t)s.N * s.H * s.W * (s.C / 8);
     dim3 grid((unsigned)((total + 255) / 256));

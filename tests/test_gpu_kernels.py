@@ -284,7 +284,7 @@ def test_bad_arguments_raise_on_gpu():
 
 # ---------------------------------------------------------------- depthwise conv
 @pytest.mark.parametrize('N,C,H,stride', [(64, 960, 14, 1), (4, 256, 28, 2), (3, 1536, 7, 1), (2, 64, 15, 2),
-                                          (1, 8, 5, 1)])
+                                          (1, 8, 5, 1), (8, 960, 14, 2), (2, 48, 9, 2), (3, 16, 3, 2)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_depthwise_fwd_bwd_vs_torch(N, C, H, stride, dtype):
     """vs torch fp32 conv2d(groups=C) on the same (rounded) values."""
