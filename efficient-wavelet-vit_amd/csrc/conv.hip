@@ -672,9 +672,17 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // fwd / dgrad: BM x BN_ x 64 tiles, BM/32 waves (BM/64 x 2), NS-deep LDS ring of
 // [row][64 k] images (128-B rows); 16-B chunk c of row r is stored at chunk
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
-template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2>
+// DENSE (forward, plain NHWC x, Cin % 8 == 0 and not a multiple of 64: the backbone's 24 /
+// 48 / 96-channel inputs, the MWT seperate conv's 16): the K axis is taps x Cin flattened
+// ([Cout][taps][Cin] packs are exactly that), so a 64-wide K-tile spans several taps —
+// each 16-B chunk of a row is (tap, 8 channels), with its own tap offset and in-image test.
+// A lane's chunk index is fixed per row, so it advances by 8 chunks per K-tile: tap +=
+// 8 / CC, cc += 8 % CC (CC = Cin / 8).  Zero waste but the last K-tile's tail (A past the
+// last tap reads through the OOB offset, B's tail meets only those zeros).
+template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2, bool DENSE = false>
 __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn,
                                                                       int tap_inner, int ntiles) {
+  static_assert(!(DENSE && DGRAD), "dense K: forward only");
   constexpr int NW = BM / 64 * WC, BK = 64;      // waves: BM/64 rows x WC columns
   constexpr int WN = BN_ / WC, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
@@ -691,7 +699,9 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const bool cls = DGRAD && KS == 3 && a.pc >= 0;
   const int py = a.pc >> 1, px = a.pc & 1;
   const int ntaps = cls ? a.ntap : KS * KS;
-  const int nk = ntaps * cbn;
+  const int CC = a.KC >> 3;                // DENSE: 8-channel chunks per tap
+  const int nk = DENSE ? (K + BK - 1) / BK : ntaps * cbn;
+  const int tq = DENSE ? 8 / CC : 0, tr = DENSE ? 8 % CC : 0;   // DENSE: per-K-tile tap / chunk advance
   const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
@@ -709,6 +719,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // epilogue stores, so a walk pays the ring's fill latency once, not once per tile.
   int rb[PA], lc8[PA];
   unsigned vmask[PA];
+  int dtap[PA], dcc[PA];  // DENSE: the (tap, chunk) each piece stages next
   uint32_t boff[PB];      // B (packed weights) byte offset of K-tile 0, or OOB
   const int kcr = a.KCr ? a.KCr : a.KC;
   // K-tile cursor: tap, channel block, group index / offset of the block.  With
@@ -760,9 +771,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     else if (cls) { by = oh; bx = ow; }
     else        { by = (oh + a.g.pad) >> ls;       bx = (ow + a.g.pad) >> ls; }
     const int64_t pix = (int64_t)n * a.srcH * a.srcW + (int64_t)by * a.srcW + bx;
-    rb[j] = (int)((pix * a.sgc + lc * 8) * 2);
+    rb[j] = (int)((pix * a.sgc + (DENSE ? 0 : lc * 8)) * 2);
     vmask[j] = msk;
     lc8[j] = lc * 8;
+    if (DENSE) { dtap[j] = lc / CC; dcc[j] = lc - dtap[j] * CC; }
   }
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
@@ -772,7 +784,27 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     boff[j] = n < a.Ncol ? (uint32_t)(((int64_t)n * K + lc * 8) * 2) : OOB;
   }
   };
+  int ld = 0;             // K-tiles of the staged tile issued so far
   auto stage = [&](int buf) {
+    if constexpr (DENSE) {
+      unsigned char *base = smem + buf * STG + ws * PA * 1024;
+#pragma unroll
+      for (int j = 0; j < PA; ++j) {
+        const int tp = dtap[j];
+        const int kh = (tp * 11) >> 5, kw = tp - kh * 3;     // tp / 3 for tp < 32 (KS == 3)
+        const int dpix = KS == 3 ? kh * a.srcW + kw : 0;
+        const bool ok = tp < KS * KS && ((vmask[j] >> tp) & 1u);
+        glds16(rs, base + j * 1024, ok ? (uint32_t)(rb[j] + (dpix * a.sgc + dcc[j] * 8) * 2) : OOB);
+        dtap[j] += tq;
+        dcc[j] += tr;
+        if (dcc[j] >= CC) { dcc[j] -= CC; ++dtap[j]; }
+      }
+      unsigned char *bb = smem + buf * STG + A_B + ws * PB * 1024;
+      const uint32_t kb = (uint32_t)(ld * BK * 2);
+#pragma unroll
+      for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
+      return;
+    }
     const int rt = cls ? a.tapl[ltap] : ltap;      // the weight tap
     const int kh = rt / KS, kw = rt - kh * KS;
     int dpix;
@@ -829,7 +861,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   };
   // `inflight` counts issued K-tiles not yet multiplied (<= NS-1); the buffer refilled is
   // always the one every wave finished reading before the last barrier
-  int ts = blockIdx.x, ld = 0, lbuf = 0, inflight = 0, cur = 0;
+  int ts = blockIdx.x, lbuf = 0, inflight = 0, cur = 0;
+  ld = 0;
   setup(xcd_remap(ts, ntiles));
   for (; ld < NS - 1 && ld < nk; ++ld, ++inflight) {
     stage(lbuf);
@@ -1242,6 +1275,41 @@ static int conv_ragged() {
   return v;
 }
 
+// EWVIT_CONV_DENSE: forward convs of a plain input whose channels are not a multiple of 64
+// take the dense-K LDS-DMA kernel (1, the default) instead of the ragged-K / register-staged
+// paths (0)
+static int conv_dense() {
+  static int v = [] {
+    const char *e = getenv("EWVIT_CONV_DENSE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// the dense-K forward (conv_glds_kernel<false, ..., DENSE>): 128-row tiles, 8 waves with a
+// 2-deep ring for grids of <= 2048 blocks, 4 waves beyond, the 4-deep ring for <= 256
+static void launch_glds_dense(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
+  const int bn = 128;
+  const int ntn = (a.Ncol + bn - 1) / bn;
+  const int64_t nwg = (a.M + 127) / 128 * ntn;
+  const int ntiles = (int)nwg;
+  const dim3 grid((unsigned)(g_grid_cap > 0 && nwg > g_grid_cap ? g_grid_cap : nwg));
+#define EWVIT_GLDS_DENSE(BN__, NS_, WC_)                                                                            \
+  do {                                                                                                            \
+    if (a.g.ks == 1)                                                                                              \
+      hipLaunchKernelGGL((conv_glds_kernel<false, 128, BN__, 1, NS_, WC_, true>), grid, dim3(128 / 64 * WC_ * 64), \
+                         0, s, a, src_bytes, ntn, 0, ntiles);                                                     \
+    else                                                                                                          \
+      hipLaunchKernelGGL((conv_glds_kernel<false, 128, BN__, 3, NS_, WC_, true>), grid, dim3(128 / 64 * WC_ * 64), \
+                         0, s, a, src_bytes, ntn, 0, ntiles);                                                     \
+  } while (0)
+  (void)bn;                                // Ncol > 64: 128-wide column tiles
+  if (nwg <= 256) EWVIT_GLDS_DENSE(128, 4, 4);
+  else if (nwg <= 2048) EWVIT_GLDS_DENSE(128, 2, 4);
+  else EWVIT_GLDS_DENSE(128, 2, 2);
+#undef EWVIT_GLDS_DENSE
+}
+
 // the LDS-DMA fwd/dgrad kernel when every K-tile stays in one tap and one channel
 // group and the operands fit 31-bit buffer offsets; false -> register-staged kernel
 template <bool DGRAD>
@@ -1254,6 +1322,16 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   // (only while the zero lanes stay <= 20 % of K: K = 48 per tap measured slower than
   // the register-staged kernel, K = 160 -> 3 blocks 17 % faster)
   const bool ragged = !padded && a.KC % 64 != 0;
+  // (only with 128-wide column tiles: for Cout <= 64 — stage 1's 24 -> 24 at 112^2, the MWT
+  // seperate conv's 16 -> 64, the 96 -> 48 projects — the register-staged kernel measured
+  // as fast or faster: 62 vs 64, 166 vs 199, 15 vs 16 us; Cout 96 / 192: 39 -> 32, 106 -> 81,
+  // 34 -> 27 us, tools/conv_bench.py)
+  if (!DGRAD && ragged && conv_dense() && use_glds() && a.Ncol > 64 && a.sgs == 0 && a.sgc == a.KC && a.KC % 8 == 0 &&
+      src_bytes < (int64_t)OOB && a.Ncol * K * 2 < (int64_t)OOB && a.M * a.ogc < ((int64_t)1 << 40) &&
+      (a.g.ks == 1 || a.g.ks == 3)) {
+    launch_glds_dense(a, src_bytes, s);
+    return true;
+  }
   // (a parity-class dgrad, which already skips 3/4 of the taps, up to 1/3)
   if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 ||
                  (a.pc >= 0 ? 2 * ((a.KC + 63) / 64 * 64) > 3 * a.KC : 5 * ((a.KC + 63) / 64 * 64) > 6 * a.KC)))
