@@ -21,6 +21,7 @@ import weakref
 import torch
 
 from . import _lib as L
+from . import grads
 from .grads import grad_out
 
 # ---- step-wide weight packing: every conv weight the model used is packed by ONE
@@ -159,6 +160,10 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
         L.require_gpu(x, weight)
+        if ctx.needs_input_grad[1]:
+            grads.note_use(weight)
+        if ctx.needs_input_grad[2]:
+            grads.note_use(bias)
         ctx.link = _take_link(x) if levels == 1 else None
         NL, Cz, H, W = x.shape
         if NL % levels:
@@ -238,30 +243,49 @@ class Conv2dFn(torch.autograd.Function):
                 dx = dx + skip.to(dx.dtype)
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
-            wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
-            ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            # dW in the parameter's own memory format — the data-parallel flat buffer's view
-            # when the step provides one (ewvit.grads), so no copy or layout change follows
             wparam, bparam = ctx.params
-            dwf = grad_out(wparam) if ctx.needs_input_grad[1] else torch.empty_like(weight, dtype=torch.float32)
-            s_co, s_ci, s_kh, s_kw = dwf.stride()
-            if s_kh != k * s_kw:
-                dwf = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=xc.device)
-                s_co, s_ci, s_kh, s_kw = dwf.stride()
-            dbf = None
-            if want_b:
-                dbf = grad_out(bparam)
-                if dbf.dim() != 1 or not dbf.is_contiguous():
-                    dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
-            work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
-            L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
-                   Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
-            if ctx.needs_input_grad[1]:
-                dw = dwf
-            db = dbf
+            dev = xc.device
+            # the weight gradient on the wgrad stream (ewvit.grads) when the weights were used
+            # once and hold no gradient; the MWT branch (capped grids, its own stream) keeps it
+            s_kh, s_kw = wparam.stride()[2:]
+            defer = ctx.cap == 0 and s_kh == k * s_kw and 2.0 * N * Ho * Wo * Cout * k * k * Cx >= grads.DEFER_MIN_FLOPS and \
+                grads.deferrable(wparam if ctx.needs_input_grad[1] else None, bparam if want_b else None)
+            if defer:
+                with torch.cuda.stream(grads.defer_begin(dev, xc, dyc)):
+                    dw, db = Conv2dFn._wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin,
+                                             k, stride, Ho, Wo, gc, gs)
+                for t in (dw, db):
+                    if t is not None:
+                        grads.defer_output(t, dev)
+            else:
+                grads.wgrad_wait(dev)
+                dw, db = Conv2dFn._wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin, k,
+                                         stride, Ho, Wo, gc, gs)
         if dx is None and skip is not None:       # x needs no gradient through the conv, only the skip's
             dx = skip
         return dx, dw, db, None, None, None
+
+    @staticmethod
+    def _wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin, k, stride, Ho, Wo, gc, gs):
+        """dW (and db) on the current stream."""
+        wsb = L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, stride)
+        ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
+        # dW in the parameter's own memory format — the data-parallel flat buffer's view
+        # when the step provides one (ewvit.grads), so no copy or layout change follows
+        dwf = grad_out(wparam) if ctx.needs_input_grad[1] else torch.empty_like(weight, dtype=torch.float32)
+        s_co, s_ci, s_kh, s_kw = dwf.stride()
+        if s_kh != k * s_kw:
+            dwf = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=xc.device)
+            s_co, s_ci, s_kh, s_kw = dwf.stride()
+        dbf = None
+        if want_b:
+            dbf = grad_out(bparam)
+            if dbf.dim() != 1 or not dbf.is_contiguous():
+                dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
+        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
+        L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
+               Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
+        return (dwf if ctx.needs_input_grad[1] else None), dbf
 
 
 def conv2d(x, weight, bias=None, stride=1, levels=1):

@@ -42,9 +42,12 @@ place, the model issues no host synchronisation, and random draws use the device
 generator (torch ops) or the ewvit dropout step counter (_lib.rng_advance, advanced
 inside the recorded forward).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
+from . import grads
 from .grads import clear_slot, set_slot
 
 
@@ -87,7 +90,7 @@ class GradBuckets:
         for i in self.order:
             p = self.params[i]
             self.views[i] = self.flat.as_strided(p.shape, p.stride(), off)    # the parameter's own strides
-            set_slot(p, self.views[i])
+            set_slot(p, self.flat, off)
             if cur and (off - start + p.numel()) * 4 > cap:
                 self.buckets.append((start, off, cur))
                 start, cur, cap = off, [], self.bucket_bytes
@@ -139,7 +142,9 @@ class GradBuckets:
         if self.world > 1 and not self.defer:
             if self.flat.is_cuda:
                 # the gradients of a bucket may come from several streams (DAMA's MWT branch
-                # runs on its own): the collective, issued on the current stream, waits for all
+                # runs on its own, deferred weight gradients on the wgrad stream): the
+                # collective, issued on the current stream, waits for all
+                grads.wgrad_wait(self.flat.device)
                 cur = torch.cuda.current_stream(self.flat.device)
                 for st in self.streams[b]:
                     if st != cur:
@@ -224,6 +229,8 @@ class TrainStep:
         if self.buckets is not None:
             self.buckets.defer = not overlap
         self.bufsync = BufferSync(model, group) if self.world > 1 else None
+        # single-use weights' gradients on a second stream, beside the input-gradient chain
+        grads.set_wgrad_stream(dev.type == 'cuda' and os.environ.get('EWVIT_WGRAD_STREAM', '0') == '1')
         self.loss = None
         self.mode = 'graph' if self.graph else 'eager'
         self._hyper = optimizer.hyper_signature() if hasattr(optimizer, 'hyper_signature') else None
@@ -269,10 +276,12 @@ class TrainStep:
             for k in range(self.accum):
                 if self.buckets is not None:
                     self.buckets.collect = k == self.accum - 1
+                grads.begin_step()           # parameter use counts (ewvit.grads)
                 lk = self.forward_loss(k) if self.accum > 1 else self.forward_loss()
                 if self.accum > 1:
                     lk = lk / self.accum                                   # train.py:110
                 lk.backward()
+                grads.wgrad_join()           # deferred weight gradients complete
                 loss = lk.detach() if loss is None else loss + lk.detach()
         return loss
 

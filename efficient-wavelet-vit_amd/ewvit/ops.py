@@ -10,7 +10,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib as L
-from .grads import grad_out
+from .grads import grad_out, note_use
 
 F32, BF16 = L.F32, L.BF16
 
@@ -218,6 +218,8 @@ def _linear_setup(ctx, inputs, output):
     ctx.set_materialize_grads(False)     # no zero-filled gradients for aux / xa
     ctx.save_for_backward(x, weight, aux, xa)
     ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
+    note_use(weight)
+    note_use(bias)
     ctx.cfg = (act, drop_p, seed, resid is not None, bias is not None, fp8)
 
 

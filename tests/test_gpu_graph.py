@@ -115,3 +115,53 @@ def test_dropout_mask_changes_per_replay():
     m2 = (out == 0).clone()
     assert 0.4 < float(m1.float().mean()) < 0.6
     assert not torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize('wgrad_stream', [False, True])
+def test_grad_slots_adopted_and_multi_use(wgrad_stream):
+    """ewvit.grads slots: a conv / linear weight used once gets its gradient written into the
+    flat buffer and ADOPTED by AccumulateGrad (no clone: the gradient's storage is the slot's
+    when the first post-accumulate hook sees it); a weight used twice in one forward gets the
+    sum of both uses (fresh outputs, not one shared slot).  With the wgrad stream on, the conv
+    wgrads run on the side stream and must give the same gradients."""
+    from ewvit import grads, ops
+    from ewvit.conv import conv2d
+    from ewvit.graph import GradBuckets
+    torch.manual_seed(5)
+    w1 = torch.nn.Parameter(torch.randn(64, 32, 3, 3, device=DEV) * 0.1)
+    w2 = torch.nn.Parameter(torch.randn(64, 64, 1, 1, device=DEV) * 0.1)     # used twice
+    lw = torch.nn.Parameter(torch.randn(48, 64, device=DEV) * 0.1)
+    lb = torch.nn.Parameter(torch.randn(48, device=DEV) * 0.1)
+    params = [w1, w2, lw, lb]
+    x = torch.randn(4, 32, 16, 16, device=DEV).to(memory_format=torch.channels_last)
+
+    def fwd():
+        y = conv2d(x, w1, None, 1)
+        y = conv2d(conv2d(y, w2, None, 1), w2, None, 1)
+        t = y.float().mean((2, 3))
+        return ops.linear(t, lw, lb).square().sum()
+
+    fwd().backward()                         # reference gradients, no slots
+    ref = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
+    stolen = {}
+    for i, p in enumerate(params):           # registered before GradBuckets' hooks: runs first
+        p.register_post_accumulate_grad_hook(lambda q, i=i: stolen.__setitem__(i, q.grad.data_ptr()))
+    gb = GradBuckets(params)
+    prev = grads.set_wgrad_stream(wgrad_stream)
+    try:
+        gb.begin()
+        grads.begin_step()
+        fwd().backward()
+        grads.wgrad_join()
+        torch.cuda.synchronize()
+    finally:
+        grads.set_wgrad_stream(prev)
+        gb.remove()
+    for i, (p, r) in enumerate(zip(params, ref)):
+        assert p.grad.data_ptr() == gb.views[i].data_ptr()
+        torch.testing.assert_close(p.grad, r, rtol=1e-5, atol=1e-6)
+    for i in (0, 2, 3):                      # single use: written in place, adopted without a clone
+        assert stolen[i] == gb.views[i].data_ptr(), i
+    assert stolen[1] != gb.views[1].data_ptr()       # two uses: summed by autograd, copied in
