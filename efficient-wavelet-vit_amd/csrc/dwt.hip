@@ -56,18 +56,20 @@ __device__ __forceinline__ float4 load4(const void *x, int64_t plane, int gy, in
 }
 
 // one Haar 2x2 step, AFB2D's two fp32 passes in their order: row pass (dim 3) over
-// (a b / c d), then the column pass (dim 2)
+// (a b / c d), then the column pass (dim 2).  Every product rounded before its sum (no FMA
+// contraction: the result must not depend on the calling kernel)
 __device__ __forceinline__ void haar2x2(float a, float b, float cc, float d, float &LL, float &B0, float &B1,
                                         float &B2) {
+#pragma clang fp contract(off)
   const float s = HAAR_S;
-  const float lo0 = __fadd_rn(__fmul_rn(s, a), __fmul_rn(s, b));
-  const float hi0 = __fsub_rn(__fmul_rn(s, a), __fmul_rn(s, b));
-  const float lo1 = __fadd_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
-  const float hi1 = __fsub_rn(__fmul_rn(s, cc), __fmul_rn(s, d));
-  LL = __fadd_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));
-  B0 = __fsub_rn(__fmul_rn(s, lo0), __fmul_rn(s, lo1));  // (W-lo,H-hi)
-  B1 = __fadd_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-lo)
-  B2 = __fsub_rn(__fmul_rn(s, hi0), __fmul_rn(s, hi1));  // (W-hi,H-hi)
+  const float lo0 = s * a + s * b;
+  const float hi0 = s * a - s * b;
+  const float lo1 = s * cc + s * d;
+  const float hi1 = s * cc - s * d;
+  LL = s * lo0 + s * lo1;
+  B0 = s * lo0 - s * lo1;  // (W-lo,H-hi)
+  B1 = s * hi0 + s * hi1;  // (W-hi,H-lo)
+  B2 = s * hi0 - s * hi1;  // (W-hi,H-hi)
 }
 
 // One workgroup = one 32-row x tw-column strip of one (n,c) plane (tw = the whole
@@ -170,6 +172,30 @@ __global__ __launch_bounds__(256) void dwt_multilevel_kernel(const void *__restr
   }
 }
 
+// PyTorch upsample_bilinear2d (align_corners=False) source coordinate of output index o:
+// src = max(scale*(o+0.5)-0.5, 0), scale = in/out in f32; explicit FMAs so the two-launch
+// path and the fused kernel below round identically
+struct Lerp {
+  int i0, ip;      // first source index, step to the second (0 at the last index)
+  float w0, w1;
+};
+__device__ __forceinline__ Lerp lerp_src(int o, int in, int out) {
+  const float sc = (float)in / (float)out;
+  float f = fmaf(sc, (float)o + 0.5f, -0.5f);
+  f = f < 0.f ? 0.f : f;
+  Lerp l;
+  l.i0 = (int)f;
+  l.ip = l.i0 < in - 1 ? 1 : 0;
+  l.w1 = f - (float)l.i0;
+  l.w0 = 1.f - l.w1;
+  return l;
+}
+__device__ __forceinline__ float bilerp(float v00, float v01, float v10, float v11, const Lerp &ly, const Lerp &lx) {
+  const float r0 = fmaf(lx.w0, v00, lx.w1 * v01);
+  const float r1 = fmaf(lx.w0, v10, lx.w1 * v11);
+  return fmaf(ly.w0, r0, ly.w1 * r1);
+}
+
 // ---- fused HF reshape + bilinear upsample to (OH, OW), channels-last output.
 // One thread = one output pixel of one level, all 3C channels.  Source index
 // arithmetic is PyTorch's upsample_bilinear2d (align_corners=False): src =
@@ -195,17 +221,10 @@ __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict
     off += (int64_t)N * C * 3 * hl * wl;
   }
   hl = (hl + 1) >> 1; wl = (wl + 1) >> 1;
-  const float sh = (float)hl / (float)OH, sw = (float)wl / (float)OW;
-  float fy = sh * ((float)oy + 0.5f) - 0.5f;
-  float fx = sw * ((float)ox + 0.5f) - 0.5f;
-  fy = fy < 0.f ? 0.f : fy;
-  fx = fx < 0.f ? 0.f : fx;
-  const int y0 = (int)fy, x0 = (int)fx;
-  const int yp = y0 < hl - 1 ? 1 : 0, xp = x0 < wl - 1 ? 1 : 0;
-  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-  const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  const Lerp ly = lerp_src(oy, hl, OH), lx = lerp_src(ox, wl, OW);
+  const int yp = ly.ip, xp = lx.ip;
   const int64_t hw = (int64_t)hl * wl;
-  const int64_t p00 = (int64_t)y0 * wl + x0;
+  const int64_t p00 = (int64_t)ly.i0 * wl + lx.i0;
   const int64_t base = off + (int64_t)n * 3 * C * hw;
   const int nch = (CH > 0) ? CH : 3 * C;
   const int64_t obase = idx * ocs;          // ocs >= 3C: padded channel stride, pad = 0
@@ -217,7 +236,7 @@ __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict
       const int64_t pb = base + ch * hw + p00;
       const float v00 = Elem<IDT>::load(yh, pb), v01 = Elem<IDT>::load(yh, pb + xp);
       const float v10 = Elem<IDT>::load(yh, pb + yp * wl), v11 = Elem<IDT>::load(yh, pb + yp * wl + xp);
-      v[ch] = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+      v[ch] = bilerp(v00, v01, v10, v11, ly, lx);
     }
     unsigned w[8];
 #pragma unroll
@@ -234,10 +253,166 @@ __global__ __launch_bounds__(256) void hf_upsample_kernel(const void *__restrict
     const int64_t pb = base + ch * hw + p00;
     const float v00 = Elem<IDT>::load(yh, pb), v01 = Elem<IDT>::load(yh, pb + xp);
     const float v10 = Elem<IDT>::load(yh, pb + yp * wl), v11 = Elem<IDT>::load(yh, pb + yp * wl + xp);
-    const float v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
-    Elem<ODT>::store(out, obase + ch, v);
+    Elem<ODT>::store(out, obase + ch, bilerp(v00, v01, v10, v11, ly, lx));
   }
   for (int ch = nch; ch < ocs; ++ch) Elem<ODT>::store(out, obase + ch, 0.f);
+}
+
+// ---- fused DWT -> HF bilinear upsample (3 colour planes): the MWT's hf_conv
+// input of every level, [levels][N][H/2][W/2][ocs] channels-last (9 band channels, the rest
+// zero), straight from the frames — the bands never go to HBM.  Same values, bit for bit,
+// as dwt_multilevel_kernel (bands rounded to the output type) + hf_upsample_kernel.
+//
+// One workgroup = 16 level-1 output rows of one frame, full width.  Level l's bilinear
+// upsample to level-1 resolution (scale 2^(1-l)) reads one level-l row beyond the strip on
+// each side, so the workgroup computes a window of 16 + 2*HALO level-1 rows (HALO = 2^(L-1)
+// level-1 rows = one level-L row): 48 input rows for L = 3, the halo rows' loads mostly
+// L2 hits of the neighbouring strips.  Level 1 runs from registers (a thread = one level-1
+// pixel of all 3 planes: six 8-B loads, 9 bands -> one 32-B store for the strip's own rows,
+// LL to LDS); levels 2..L run over LDS (bands rounded to the output type, LL in fp32); the
+// upsample pass then gathers 4 x 9 band values per output pixel from LDS.
+constexpr int DWTF_ROWS = 16;       // level-1 output rows per workgroup
+
+template <int ODT>
+__device__ __forceinline__ float rnd_out(float v) {
+  return ODT == EWVIT_BF16 ? bf2f(f2bf(v)) : v;
+}
+
+// 9 (or 16 with zero padding) channels of one output pixel
+template <int ODT>
+__device__ __forceinline__ void store_px9(void *out, int64_t o, const float (&v)[9], int ocs) {
+  if (ODT == EWVIT_BF16 && ocs == 16) {
+    unsigned w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = 2 * k < 9 ? v[2 * k] : 0.f, b = 2 * k + 1 < 9 ? v[2 * k + 1] : 0.f;
+      w[k] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+    }
+    uint4 *q = reinterpret_cast<uint4 *>(reinterpret_cast<bf16_t *>(out) + o);
+    q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    return;
+  }
+#pragma unroll
+  for (int ch = 0; ch < 9; ++ch) Elem<ODT>::store(out, o + ch, v[ch]);
+  for (int ch = 9; ch < ocs; ++ch) Elem<ODT>::store(out, o + ch, 0.f);
+}
+
+// two consecutive pixels of a row (an 8-B / 4-B load: W even, column even)
+template <int XDT>
+__device__ __forceinline__ float2 load2(const void *x, int64_t i) {
+  if (XDT == EWVIT_F32) return *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(x) + i);
+  const unsigned q = *reinterpret_cast<const unsigned *>(reinterpret_cast<const bf16_t *>(x) + i);
+  return make_float2(__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u));
+}
+
+template <int XDT, int ODT, int L, int OWMAX>
+__global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restrict__ x, void *__restrict__ out,
+                                                           int N, int H, int W, int ocs) {
+  constexpr int HALO = L > 1 ? (1 << (L - 1)) : 0;      // level-1 rows
+  constexpr int R1 = DWTF_ROWS + 2 * HALO;              // level-1 window rows
+  constexpr int R2 = L >= 2 ? R1 / 2 : 1, R3 = L >= 3 ? R1 / 4 : 1;
+  constexpr int O2 = OWMAX / 2, O3 = OWMAX / 4;
+  __shared__ float ll1[L >= 2 ? R1 * OWMAX * 3 : 1];
+  __shared__ float b2[L >= 2 ? R2 * O2 * 9 : 1];
+  __shared__ float ll2[L >= 3 ? R2 * O2 * 3 : 1];
+  __shared__ float b3[L >= 3 ? R3 * O3 * 9 : 1];
+  const int tid = threadIdx.x, n = blockIdx.y;
+  const int OH = H >> 1, OW = W >> 1;
+  const int y0 = blockIdx.x * DWTF_ROWS;                // first level-1 output row
+  const int ws1 = y0 - HALO;                            // window origin, level-1 rows
+  const int64_t plane = (int64_t)H * W;
+  const char *xn = reinterpret_cast<const char *>(x) + (int64_t)n * 3 * plane * (XDT == EWVIT_BF16 ? 2 : 4);
+  const int64_t lvl = (int64_t)N * OH * OW * ocs;       // one level's output block
+
+  // ---- level 1 (registers): 4 pixels per thread in flight
+  {
+    const int items = R1 * OW;
+    for (int i0 = tid; i0 < items; i0 += 4 * 256) {
+      float2 r[4][3][2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int it = i0 + k * 256;
+        const int i = it / OW, j = it - i * OW, y = ws1 + i;
+        if (it < items && y >= 0 && y < OH) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int64_t b = c * plane + (int64_t)(2 * y) * W + 2 * j;
+            r[k][c][0] = load2<XDT>(xn, b);
+            r[k][c][1] = load2<XDT>(xn, b + W);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int it = i0 + k * 256;
+        const int i = it / OW, j = it - i * OW, y = ws1 + i;
+        if (!(it < items && y >= 0 && y < OH)) continue;
+        float v[9];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float LL, B0, B1, B2;
+          haar2x2(r[k][c][0].x, r[k][c][0].y, r[k][c][1].x, r[k][c][1].y, LL, B0, B1, B2);
+          v[3 * c] = B0; v[3 * c + 1] = B1; v[3 * c + 2] = B2;
+          if (L >= 2) ll1[(i * OWMAX + j) * 3 + c] = LL;
+        }
+        if (i >= HALO && i < HALO + DWTF_ROWS)
+          store_px9<ODT>(out, (((int64_t)n * OH + y) * OW + j) * ocs, v, ocs);
+      }
+    }
+  }
+  if constexpr (L >= 2) {
+    __syncthreads();
+    // ---- level 2 over LDS: window rows ws2 .. ws2 + R2
+    const int OH2 = OH >> 1, OW2 = OW >> 1, ws2 = ws1 >> 1;
+    for (int it = tid; it < R2 * OW2; it += 256) {
+      const int i = it / OW2, j = it - i * OW2, y = ws2 + i;
+      if (y < 0 || y >= OH2) continue;
+      const float *p0 = ll1 + ((2 * i) * OWMAX + 2 * j) * 3, *p1 = p0 + OWMAX * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float LL, B0, B1, B2;
+        haar2x2(p0[c], p0[3 + c], p1[c], p1[3 + c], LL, B0, B1, B2);
+        float *q = b2 + (i * O2 + j) * 9 + 3 * c;
+        q[0] = rnd_out<ODT>(B0); q[1] = rnd_out<ODT>(B1); q[2] = rnd_out<ODT>(B2);
+        if (L >= 3) ll2[(i * O2 + j) * 3 + c] = LL;
+      }
+    }
+    if constexpr (L >= 3) {
+      __syncthreads();
+      const int OH3 = OH2 >> 1, OW3 = OW2 >> 1, ws3 = ws2 >> 1;
+      for (int it = tid; it < R3 * OW3; it += 256) {
+        const int i = it / OW3, j = it - i * OW3, y = ws3 + i;
+        if (y < 0 || y >= OH3) continue;
+        const float *p0 = ll2 + ((2 * i) * O2 + 2 * j) * 3, *p1 = p0 + O2 * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float LL, B0, B1, B2;
+          haar2x2(p0[c], p0[3 + c], p1[c], p1[3 + c], LL, B0, B1, B2);
+          float *q = b3 + (i * O3 + j) * 9 + 3 * c;
+          q[0] = rnd_out<ODT>(B0); q[1] = rnd_out<ODT>(B1); q[2] = rnd_out<ODT>(B2);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- levels 2..L upsampled to the strip's level-1 rows
+    const int rows = OH - y0 < DWTF_ROWS ? OH - y0 : DWTF_ROWS;
+    const int items = rows * OW;
+    for (int it = tid; it < (L - 1) * items; it += 256) {
+      const int l = 2 + it / items, r = it - (l - 2) * items;
+      const int oy = y0 + r / OW, ox = r - (r / OW) * OW;
+      const int hl = OH >> (l - 1), wl = OW >> (l - 1);
+      const Lerp ly = lerp_src(oy, hl, OH), lx = lerp_src(ox, wl, OW);
+      const float *bb = l == 2 ? b2 : b3;
+      const int ow = l == 2 ? O2 : O3, ws = l == 2 ? ws2 : (ws1 >> 2);
+      const float *q00 = bb + ((ly.i0 - ws) * ow + lx.i0) * 9;
+      const float *q01 = q00 + lx.ip * 9, *q10 = q00 + ly.ip * ow * 9, *q11 = q10 + lx.ip * 9;
+      float v[9];
+#pragma unroll
+      for (int ch = 0; ch < 9; ++ch) v[ch] = bilerp(q00[ch], q01[ch], q10[ch], q11[ch], ly, lx);
+      store_px9<ODT>(out, (l - 1) * lvl + (((int64_t)n * OH + oy) * OW + ox) * ocs, v, ocs);
+    }
+  }
 }
 
 }  // namespace ewvit
@@ -302,4 +477,44 @@ extern "C" int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C
   else { if (c3) UP_LAUNCH(EWVIT_BF16, EWVIT_BF16, 9); else UP_LAUNCH(EWVIT_BF16, EWVIT_BF16, 0); }
 #undef UP_LAUNCH
   return launch_status("hf_upsample");
+}
+
+// the fused DWT -> HF upsample applies: 3 planes, every level halves exactly (H, W multiples
+// of 2^levels), output at level-1 resolution, levels <= 3, W/2 <= 112, 9..16 output channels.
+// (A 192-column form for config 4's 384^2 frames needed 121 KB of LDS — one workgroup per CU
+// — and ran 61 us against the two launches' 58 us: wider frames keep the two launches.)
+extern "C" int ewvit_dwt_hf_fused_ok(int64_t N, int64_t C, int64_t H, int64_t W, int levels, int64_t OH, int64_t OW,
+                                     int64_t out_channels) {
+  const int64_t m = (int64_t)1 << (levels < 1 ? 1 : levels);
+  return N > 0 && N <= 65535 && C == 3 && levels >= 1 && levels <= 3 && H > 0 && W > 0 && H % m == 0 &&
+         W % m == 0 && OH == H / 2 && OW == W / 2 && OW <= 112 && out_channels >= 9 && out_channels <= 16;
+}
+
+extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, int64_t C, int64_t H, int64_t W,
+                                           int levels, int x_dtype, int out_dtype, int64_t out_channels,
+                                           void *stream) {
+  EWVIT_CHECK_ARG(x && out, "dwt_hf_upsample_fused: null pointer");
+  EWVIT_CHECK_ARG(dtype_ok(x_dtype) && dtype_ok(out_dtype), "dwt_hf_upsample_fused: bad dtype");
+  EWVIT_CHECK_ARG(ewvit_dwt_hf_fused_ok(N, C, H, W, levels, H / 2, W / 2, out_channels),
+                  "dwt_hf_upsample_fused: unsupported shape [%lld,%lld,%lld,%lld] levels=%d channels=%lld",
+                  (long long)N, (long long)C, (long long)H, (long long)W, levels, (long long)out_channels);
+  const int OH = (int)(H / 2);
+  dim3 grid((unsigned)((OH + DWTF_ROWS - 1) / DWTF_ROWS), (unsigned)N), block(256);
+  hipStream_t s = as_stream(stream);
+#define DWTF_L(XD, OD, LV)                                                                                \
+  hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112>), grid, block, 0, s, x, out, (int)N, (int)H, (int)W, \
+                     (int)out_channels)
+#define DWTF_D(XD, OD)                        \
+  do {                                        \
+    if (levels == 1) DWTF_L(XD, OD, 1);       \
+    else if (levels == 2) DWTF_L(XD, OD, 2);  \
+    else DWTF_L(XD, OD, 3);                   \
+  } while (0)
+  if (x_dtype == EWVIT_F32 && out_dtype == EWVIT_BF16) DWTF_D(EWVIT_F32, EWVIT_BF16);
+  else if (x_dtype == EWVIT_F32) DWTF_D(EWVIT_F32, EWVIT_F32);
+  else if (out_dtype == EWVIT_BF16) DWTF_D(EWVIT_BF16, EWVIT_BF16);
+  else DWTF_D(EWVIT_BF16, EWVIT_F32);
+#undef DWTF_D
+#undef DWTF_L
+  return launch_status("dwt_hf_upsample_fused");
 }

@@ -26,6 +26,7 @@ _f64 = ctypes.c_double
 SIGNATURES = {
     'ewvit_dwt_haar_fwd': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     'ewvit_hf_upsample': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i64, _i64, _i32, _i32, _i64, _vp],
+    'ewvit_dwt_hf_upsample_fused': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i64, _vp],
     'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
                    _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
     'ewvit_gemm_fp8': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
@@ -91,6 +92,7 @@ QUERIES = {
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_stem_parts': (_i64, [_i64, _i64, _i64, _i32]),
+    'ewvit_dwt_hf_fused_ok': (_i32, [_i64, _i64, _i64, _i64, _i32, _i64, _i64, _i64]),
     'ewvit_conv2d_fwd_pack_cin': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_data_add_ok': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),

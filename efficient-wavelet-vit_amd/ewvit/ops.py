@@ -5,6 +5,7 @@ HIP stream and autograd.  Every FLOP of these ops runs in libewvit.so; inputs
 on a non-ROCm device raise (no CPU path).
 """
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -518,6 +519,41 @@ def dwt_hf_upsample(x, levels, out_hw, out_dtype=torch.bfloat16, band_dtype=torc
     ll, yh = torch.ops.ewvit.dwt_haar(x, int(levels), band_dtype)
     N, C, H, W = x.shape
     return hf_upsample(yh, N, C, H, W, levels, out_hw, out_dtype, out_channels), ll
+
+
+@torch.library.custom_op('ewvit::dwt_hf_fused', mutates_args=())
+def _dwt_hf_fused_op(x: torch.Tensor, levels: int, out_dtype: torch.dtype, out_channels: int) -> torch.Tensor:
+    L.require_gpu(x)
+    x = _c(x)
+    N, C, H, W = x.shape
+    out = torch.empty(levels, N, H // 2, W // 2, out_channels, dtype=out_dtype, device=x.device)
+    work = {'bytes': x.numel() * x.element_size() + out.numel() * out.element_size()}
+    L.call('ewvit_dwt_hf_upsample_fused', L.ptr(x), L.ptr(out), N, C, H, W, levels, L.dt(x), L.dt(out),
+           out_channels, L.stream(out), work=work)
+    return out
+
+
+@_dwt_hf_fused_op.register_fake
+def _(x, levels, out_dtype, out_channels):
+    N, C, H, W = x.shape
+    return x.new_empty((levels, N, H // 2, W // 2, out_channels), dtype=out_dtype)
+
+
+_DWT_FUSED = os.environ.get('EWVIT_DWT_FUSED', '1') != '0'
+
+
+def dwt_hf_features(x, levels, out_hw, out_dtype=torch.bfloat16, out_channels=0):
+    """The MWT's hf_conv input of every level, [L, N, OH, OW, out_channels or 3C] channels-last
+    (bands rounded to out_dtype, as dwt_hf_upsample with band_dtype = out_dtype).  ONE launch
+    (ewvit_dwt_hf_upsample_fused: the bands stay on chip) when the shape allows it (3 colour
+    planes, levels <= 3, H and W multiples of 2^levels, out_hw = (H/2, W/2), W <= 224,
+    9-16 channels), otherwise the DWT + upsample launches."""
+    _no_grad_input(x)
+    N, C, H, W = x.shape
+    oc = int(out_channels) or 3 * C
+    if _DWT_FUSED and L.load().ewvit_dwt_hf_fused_ok(N, C, H, W, int(levels), int(out_hw[0]), int(out_hw[1]), oc):
+        return torch.ops.ewvit.dwt_hf_fused(x, int(levels), out_dtype, oc)
+    return dwt_hf_upsample(x, levels, out_hw, out_dtype, out_dtype, out_channels)[0]
 
 
 # ------------------------------------------------------- depthwise 3x3 conv

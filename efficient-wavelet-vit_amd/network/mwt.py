@@ -232,9 +232,7 @@ class MWT(nn.Module):
         # the seperate conv runs on the ewvit MFMA conv (K = 9 taps x 16 channels)
         cin = 3 * C
         cpad = (cin + 15) // 16 * 16 if cdt == torch.bfloat16 else cin
-        hf, _ = ewvit.dwt_hf_upsample(x, Lv, out_hw, out_dtype=cdt,
-                                      band_dtype=torch.bfloat16 if cdt == torch.bfloat16 else torch.float32,
-                                      out_channels=cpad)
+        hf = ewvit.dwt_hf_features(x, Lv, out_hw, out_dtype=cdt, out_channels=cpad)
         hf = hf.view(Lv * B, out_hw[0], out_hw[1], cpad).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
         sep = self.hf_conv['seperate']
         # seperate[i] sees colour i's 3C/3 = C band channels: a groups=3 conv.  It is

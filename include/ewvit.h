@@ -67,6 +67,20 @@ int ewvit_hf_upsample(const void *yh, void *out, int64_t N, int64_t C, int64_t H
 /* out_channels: channel stride of `out` (0 = 3C); channels 3C .. out_channels-1 are
  * written as zeros (the 16-channel-aligned input of the hf_conv MFMA conv). */
 
+/* Fused ewvit_dwt_haar_fwd + ewvit_hf_upsample for the MWT's hf_conv input (SURVEY §7.4;
+ * network/mwt.py:76-81 per level, all levels at once as mwt.py:101-110 loops them): x
+ * [N, 3, H, W] (fp32/bf16) -> out [levels, N, H/2, W/2, out_channels] channels-last, the 9
+ * band channels (colour-major, bands LH/HL/HH) bilinearly upsampled to level-1 resolution
+ * and channels 9.. zero.  Bit-identical to the two-launch path with band_dtype = out_dtype;
+ * the bands never reach HBM (one launch, 1 x frames in + the output).  Applies when
+ * ewvit_dwt_hf_fused_ok(): C == 3, levels <= 3, H and W multiples of 2^levels,
+ * (OH, OW) == (H/2, W/2), W/2 <= 112, 9 <= out_channels <= 16 (wider frames: the two
+ * launches measured faster). */
+int ewvit_dwt_hf_fused_ok(int64_t N, int64_t C, int64_t H, int64_t W, int levels, int64_t OH, int64_t OW,
+                          int64_t out_channels);
+int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, int64_t C, int64_t H, int64_t W,
+                                int levels, int x_dtype, int out_dtype, int64_t out_channels, void *stream);
+
 /* --------------------------------------------------------------- GEMM ---
  * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(k,n) )   bf16 MFMA, fp32 accumulate
  * — the projection GEMMs of network/sfe.py:44-55,29-40 (to_qkv, to_out,

@@ -99,6 +99,50 @@ def test_hf_upsample_bf16_is_rounded_fp32():
     assert rel_err(b.float(), a) < 2 ** -7
 
 
+@pytest.mark.parametrize('shape,levels,odt,oc,xdt', [
+    ((64, 3, 224, 224), 3, torch.bfloat16, 16, torch.float32),     # config 2's MWT front end
+    ((6, 3, 96, 224), 3, torch.bfloat16, 16, torch.float32),
+    ((4, 3, 224, 224), 3, torch.bfloat16, 16, torch.bfloat16),
+    ((4, 3, 64, 64), 2, torch.float32, 9, torch.float32),
+    ((2, 3, 40, 72), 3, torch.bfloat16, 16, torch.float32),        # 20 level-1 rows: a ragged strip
+    ((2, 3, 32, 48), 1, torch.float32, 9, torch.float32),
+    ((3, 3, 8, 200), 3, torch.float32, 12, torch.float32)])
+def test_dwt_hf_fused_equals_two_launch_path(shape, levels, odt, oc, xdt):
+    """ewvit_dwt_hf_upsample_fused (one launch, bands on chip) gives exactly the values of
+    dwt_haar_fwd (bands rounded to the output type) + hf_upsample."""
+    import ewvit
+    from ewvit import _lib as L
+    N, C, H, W = shape
+    assert L.load().ewvit_dwt_hf_fused_ok(N, C, H, W, levels, H // 2, W // 2, oc)
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(11)).to(DEV, xdt)
+    got = torch.ops.ewvit.dwt_hf_fused(x, levels, odt, oc)
+    ref, _ = ewvit.dwt_hf_upsample(x, levels, (H // 2, W // 2), out_dtype=odt, band_dtype=odt, out_channels=oc)
+    assert got.shape == ref.shape == (levels, N, H // 2, W // 2, oc)
+    assert torch.equal(got, ref)
+
+
+def test_dwt_hf_fused_vs_oracle_and_dispatch():
+    """The fused path against the oracle (fp32), and dwt_hf_features' dispatch: shapes the
+    fused kernel does not take (odd sizes, 4 levels, C != 3) run the two launches."""
+    import ewvit
+    from ewvit import _lib as L
+    from oracle import dwt as odwt
+    x = torch.randn(8, 3, 224, 224, generator=torch.Generator().manual_seed(3))
+    up = ewvit.dwt_hf_features(x.to(DEV), 3, (112, 112), out_dtype=torch.float32)
+    ref = odwt.hf_upsampled(x.numpy(), 3)
+    np.testing.assert_allclose(up.permute(0, 1, 4, 2, 3).cpu().numpy(), ref, atol=2e-6, rtol=0)
+    lib = L.load()
+    for shape, lv, oc in [((2, 3, 42, 40), 3, 16), ((2, 3, 64, 64), 4, 16), ((2, 2, 64, 64), 2, 6),
+                          ((1, 3, 16, 416), 3, 16), ((2, 3, 384, 384), 3, 16)]:
+        N, C, H, W = shape
+        assert not lib.ewvit_dwt_hf_fused_ok(N, C, H, W, lv, H // 2, W // 2, oc)
+        xs = torch.randn(*shape, device=DEV)
+        a = ewvit.dwt_hf_features(xs, lv, (H // 2, W // 2), out_dtype=torch.bfloat16, out_channels=oc)
+        b, _ = ewvit.dwt_hf_upsample(xs, lv, (H // 2, W // 2), out_dtype=torch.bfloat16, band_dtype=torch.bfloat16,
+                                     out_channels=oc)
+        assert torch.equal(a, b)
+
+
 # ---------------------------------------------------------------- GEMM
 def _bf(t):
     return t.to(torch.bfloat16).float()

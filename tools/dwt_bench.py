@@ -1,6 +1,6 @@
-"""Isolated timing of the MWT front end (ewvit_dwt_haar_fwd, ewvit_hf_upsample) at the
-bench shape (config 2: 64 x 3 x 224^2 fp32 frames, 3 levels, bf16 bands): ITERS
-back-to-back launches captured in one HIP graph, timed by events around the replay,
+"""Isolated timing of the MWT front end (the fused ewvit_dwt_hf_upsample_fused, and the
+two-launch ewvit_dwt_haar_fwd + ewvit_hf_upsample it replaces) at the bench shape
+(config 2: 64 x 3 x 224^2 fp32 frames, 3 levels, bf16 bands): ITERS back-to-back launches captured in one HIP graph, timed by events around the replay,
 so the per-launch figure is the kernel duration (as rocprofv3 reports it) without
 the per-launch event gaps of bench.py's eager pass.
 
@@ -38,7 +38,8 @@ def graph_us(fn, iters):
 
 
 def measure(n=64, hw=224, levels=3, iters=50):
-    """-> {'dwt_us', 'dwt_bytes', 'up_us', 'up_bytes'} (algorithmic bytes per launch)."""
+    """-> {'dwt_us', 'dwt_bytes', 'up_us', 'up_bytes', 'fused_us', 'fused_bytes'} (algorithmic
+    bytes per launch)."""
     from ewvit import ops
     dev = torch.device('cuda', 0)
     x = torch.randn(n, 3, hw, hw, device=dev)
@@ -49,7 +50,12 @@ def measure(n=64, hw=224, levels=3, iters=50):
     up_bytes = yh.numel() * 2 + out.numel() * 2
     up_us = graph_us(lambda: ops.hf_upsample(yh, n, 3, hw, hw, levels, (hw // 2, hw // 2), torch.bfloat16, 16),
                      iters)
-    return {'dwt_us': dwt_us, 'dwt_bytes': dwt_bytes, 'up_us': up_us, 'up_bytes': up_bytes}
+    fused_us = fused_bytes = None                      # the fused launch takes W <= 224
+    if ops.L.load().ewvit_dwt_hf_fused_ok(n, 3, hw, hw, levels, hw // 2, hw // 2, 16):
+        fused_us = graph_us(lambda: ops._dwt_hf_fused_op(x, levels, torch.bfloat16, 16), iters)
+        fused_bytes = x.numel() * 4 + out.numel() * 2  # frames in + hf_conv input out
+    return {'dwt_us': dwt_us, 'dwt_bytes': dwt_bytes, 'up_us': up_us, 'up_bytes': up_bytes,
+            'fused_us': fused_us, 'fused_bytes': fused_bytes}
 
 
 def main():
@@ -60,9 +66,11 @@ def main():
     ap.add_argument('--iters', type=int, default=50)
     a = ap.parse_args()
     r = measure(a.n, a.hw, a.levels, a.iters)
-    for k in ('dwt', 'up'):
+    for k in ('dwt', 'up', 'fused'):
         us, b = r[k + '_us'], r[k + '_bytes']
-        print(f'{k:4s} {us:8.2f} us  {b / 1e6:7.2f} MB  {b / us / 1e3:7.1f} GB/s', flush=True)
+        if us is None:
+            continue
+        print(f'{k:5s} {us:8.2f} us  {b / 1e6:7.2f} MB  {b / us / 1e3:7.1f} GB/s', flush=True)
 
 
 if __name__ == '__main__':
