@@ -459,15 +459,61 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
   }
 }
 
-// ---- backward pass 1: partial sums of g and g*xhat, g = dy * act'(z)
-template <int DT, int ACT, bool SC = false>
+// SC == 2: the BatchNorm's output gradient is the squeeze-excitation input gradient
+// dy * s[n][c] + g[n][c] (ewvit_se_scale's backward, s the excitation, g the squeeze term),
+// formed on the fly from the SE output gradient
+__device__ __forceinline__ void se_affine(float (&v)[8], const float *__restrict__ s, const float *__restrict__ g,
+                                          int64_t n, int C, int c) {
+  const float4 *sp = reinterpret_cast<const float4 *>(s + n * C + c);
+  const float4 *gp = reinterpret_cast<const float4 *>(g + n * C + c);
+  const float4 s0 = sp[0], s1 = sp[1], g0 = gp[0], g1 = gp[1];
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sv[j], gv[j]);
+}
+
+// the se_affine tables of the frames of rows [r0, r1) and the block's channel chunk, staged in
+// LDS (tab[0][f][ch] = s, tab[1][f][ch] = g, f relative to frame f0): a row then reads its 8
+// channels' factors from LDS instead of four 16-B global loads.  Returns false (use global
+// loads) when the rows span more than SE_MAXF frames.
+constexpr int SE_MAXF = 16;
+__device__ __forceinline__ bool se_stage(float *tab, const float *__restrict__ s, const float *__restrict__ g,
+                                         int64_t r0, int64_t r1, int HW, int C, int ch0, int nch_c, int64_t &f0) {
+  f0 = r0 / HW;
+  const int nf = r1 > r0 ? (int)((r1 - 1) / HW - f0 + 1) : 0;
+  if (nf > SE_MAXF) return false;
+  for (int i = threadIdx.x; i < nf * 64; i += blockDim.x) {
+    const int f = i >> 6, ch = i & 63;
+    if (ch < nch_c) {
+      tab[f * 64 + ch] = s[(f0 + f) * C + ch0 + ch];
+      tab[SE_MAXF * 64 + f * 64 + ch] = g[(f0 + f) * C + ch0 + ch];
+    }
+  }
+  __syncthreads();
+  return true;
+}
+__device__ __forceinline__ void se_affine_lds(float (&v)[8], const float *tab, int f, int cl) {
+  const float4 *sp = reinterpret_cast<const float4 *>(tab + f * 64 + cl * 8);
+  const float4 *gp = reinterpret_cast<const float4 *>(tab + SE_MAXF * 64 + f * 64 + cl * 8);
+  const float4 s0 = sp[0], s1 = sp[1], g0 = gp[0], g1 = gp[1];
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sv[j], gv[j]);
+}
+
+// ---- backward pass 1: partial sums of g and g*xhat, g = dy * act'(z); SC 1: dy scaled
+// per row group (rscale[row / HW], the drop-path tail), SC 2: dy -> dy * s + g (se_affine)
+template <int DT, int ACT, int SC = 0>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                             const float *__restrict__ mean,
                                                             const float *__restrict__ invstd,
                                                             const float *__restrict__ gamma,
                                                             const float *__restrict__ beta, int64_t M, int C, int CC8,
                                                             int RG, int64_t rpc, float *__restrict__ part,
-                                                            const float *__restrict__ rscale = nullptr, int HW = 1) {
+                                                            const float *__restrict__ rscale = nullptr, int HW = 1,
+                                                            const float *__restrict__ se_g = nullptr) {
   __shared__ float sm[256 * 16];
   const int grp = blockIdx.z, nrc = gridDim.x;
   {
@@ -482,6 +528,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
   const int c8 = blockIdx.y * CC8 + cl;
   const bool active = rg < RG && c8 < C8;
   const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = r0 + rpc < M ? r0 + rpc : M;
+  __shared__ __attribute__((aligned(16))) float tab[SC == 2 ? 2 * SE_MAXF * 64 : 4];
+  int64_t f0 = 0;
+  bool ltab = false;
+  if constexpr (SC == 2) {
+    const int ch0 = blockIdx.y * CC8 * 8;
+    ltab = se_stage(tab, rscale, se_g, r0, r1, HW, C, ch0, (C - ch0) < CC8 * 8 ? (C - ch0) : CC8 * 8, f0);
+  }
   float sg[8], sgx[8], mu[8], iv[8], ga[8], be[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -494,15 +547,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
     row_walk<8>(r0, r1, rg, RG,
                 [&](int64_t rr) {
                   return Raw8x2s<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8),
-                                     SC ? rscale[(int)rr / HW] : 1.f};
+                                     SC == 1 ? rscale[(int)rr / HW] : 1.f};
                 },
-                [&](int64_t, const Raw8x2s<DT> &raw) {
+                [&](int64_t rr, const Raw8x2s<DT> &raw) {
       float vx[8], vd[8];
       unpack<DT>(raw.x, vx);
       unpack<DT>(raw.d, vd);
+      if (SC == 2) {
+        if (ltab) se_affine_lds(vd, tab, (int)(rr / HW - f0), cl);
+        else se_affine(vd, rscale, se_g, rr / HW, C, c8 * 8);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (SC) vd[j] *= raw.s;
+        if (SC == 1) vd[j] *= raw.s;
         const float xh = (vx[j] - mu[j]) * iv[j];
         const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
         sg[j] += g;
@@ -516,7 +573,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
 // dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); the block finalises its chunk's
 // two means from the partial rows; blocks of row range 0 of group 0 write
 // dgamma = sum g*xhat, dbeta = sum g (over all groups: the parameters are shared)
-template <int DT, int ACT, bool SC = false>
+template <int DT, int ACT, int SC = 0>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__ dy, const void *__restrict__ x,
                                                         const float *__restrict__ mean,
                                                         const float *__restrict__ invstd,
@@ -525,7 +582,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
                                                         const float *__restrict__ part, int nrc,
                                                         void *__restrict__ dx, int64_t Mg, int C, int CC8, int RG,
                                                         int64_t rpb, float *dgamma, float *dbeta, int accumulate,
-                                                        const float *__restrict__ rscale = nullptr, int HW = 1) {
+                                                        const float *__restrict__ rscale = nullptr, int HW = 1,
+                                                        const float *__restrict__ se_g = nullptr) {
   __shared__ float red[512];
   __shared__ float coef[2][64];
   const int grp = blockIdx.z, groups = gridDim.z;
@@ -575,18 +633,26 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
     for (int j = 0; j < 8; ++j) { c0[j] = coef[0][cl * 8 + j]; c1[j] = coef[1][cl * 8 + j]; }
   };
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
+  __shared__ __attribute__((aligned(16))) float tab[SC == 2 ? 2 * SE_MAXF * 64 : 4];
+  int64_t f0 = 0;
+  bool ltab = false;
+  if constexpr (SC == 2) ltab = se_stage(tab, rscale, se_g, r0, r1, HW, C, ch0, nch_c, f0);
   row_walk_pf<8>(active, r0, r1, rg, RG,
                  [&](int64_t rr) {
                    return Raw8x2s<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c),
-                                      SC ? rscale[(int)rr / HW] : 1.f};
+                                      SC == 1 ? rscale[(int)rr / HW] : 1.f};
                  },
                  [&](int64_t rr, const Raw8x2s<DT> &raw) {
     float vx[8], vd[8], o[8];
     unpack<DT>(raw.x, vx);
     unpack<DT>(raw.d, vd);
+    if (SC == 2) {
+      if (ltab) se_affine_lds(vd, tab, (int)(rr / HW - f0), cl);
+      else se_affine(vd, rscale, se_g, rr / HW, C, c);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (SC) vd[j] *= raw.s;
+      if (SC == 1) vd[j] *= raw.s;
       const float xh = (vx[j] - mu[j]) * iv[j];
       const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
@@ -791,19 +857,54 @@ extern "C" int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int 
   const int64_t rpb = bn_rows_per_block(geo, M, 1);
   dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
   if (dtype == EWVIT_BF16) {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_BF16, 0, true>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_BF16, 0, 1>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
                        save_invstd, gamma, beta, M, (int)C, geo.CC8, geo.RG, rpc, workspace, row_scale, (int)HW);
-    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_BF16, 0, true>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_BF16, 0, 1>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
                        save_invstd, gamma, beta, workspace, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0,
                        row_scale, (int)HW);
   } else {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_F32, 0, true>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<EWVIT_F32, 0, 1>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,
                        save_invstd, gamma, beta, M, (int)C, geo.CC8, geo.RG, rpc, workspace, row_scale, (int)HW);
-    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_F32, 0, true>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_F32, 0, 1>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
                        save_invstd, gamma, beta, workspace, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0,
                        row_scale, (int)HW);
   }
   return launch_status("bn_bwd_scaled");
+}
+
+// backward of BatchNorm(+act) followed by squeeze-excitation (the MBConv depthwise BN + SiLU,
+// then SE): the BatchNorm's output gradient dy * s[n][c] + g[n][c] is formed from the SE
+// output gradient dy inside both passes (s: the excitation [N][C], g: the squeeze term from
+// ewvit_se_squeeze_mlp_bwd), so the SE input-gradient pass (ewvit_se_scale) never runs
+extern "C" int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                               const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
+                               int act, float *dgamma, float *dbeta, const float *se_s, const float *se_g, int64_t HW,
+                               float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && se_s && se_g && workspace && dtype_ok(dtype),
+                  "bn_bwd_se: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_se: C=%lld", (long long)C);
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd_se: act=%d", act);
+  EWVIT_CHECK_ARG(HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31), "bn_bwd_se: M=%lld rows of %lld", (long long)M,
+                  (long long)HW);
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const BnGeo geo = bn_geo(C);
+  const int nrc = bn_nrc(geo, M, 1);
+  const int64_t rpc = (M + nrc - 1) / nrc;
+  dim3 grid(nrc, geo.nch, 1);
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+#define BN_SE(DTV, ACTV)                                                                                            \
+  do {                                                                                                              \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV, 2>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,      \
+                       save_invstd, gamma, beta, M, (int)C, geo.CC8, geo.RG, rpc, workspace, se_s, (int)HW, se_g);  \
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV, 2>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,         \
+                       save_invstd, gamma, beta, workspace, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, \
+                       0, se_s, (int)HW, se_g);                                                                     \
+  } while (0)
+  BN_DISPATCH(BN_SE);
+#undef BN_SE
+  return launch_status("bn_bwd_se");
 }
 
 extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,

@@ -64,6 +64,7 @@ SIGNATURES = {
     'ewvit_bn_fwd_drop_add': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64, _f32, _u64, _vp, _vp, _vp, _vp],
     'ewvit_bn_bwd_scaled': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
+    'ewvit_bn_bwd_se': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     'ewvit_bn_fold_partials': [_vp, _i32, _vp, _vp, _i32, _vp, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_stem_fwd': [_vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64,

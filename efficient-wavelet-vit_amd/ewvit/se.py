@@ -7,6 +7,8 @@ forward (squeeze, excite) and of the backward (sum_hw dy*x, dx = dy*s + dsq/HW)
 are ewvit kernels, and so is the fp32 [N, C] squeeze MLP: one launch forward
 (fc1 + SiLU + fc2 + sigmoid), two backward (per-frame vectors; weight/bias sums)
 in place of the ~15 small library/elementwise kernels of the reference block.
+``bn_act_se`` takes the BatchNorm + SiLU before the SE as well: its backward folds the SE
+input-gradient pass into the BatchNorm backward.
 """
 import torch
 import torch.nn.functional as F
@@ -90,6 +92,84 @@ class SqueezeExciteFn(torch.autograd.Function):
         L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
                work={'bytes': 2 * xc.numel() * xc.element_size()})
         return dx, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2
+
+
+class BnActSEFn(torch.autograd.Function):
+    """SE(act(BatchNorm(x))) in training mode — MBConv's depthwise BN + SiLU followed by its
+    squeeze-excitation.  Forward: the BatchNorm statistics + apply passes, then the SE's squeeze
+    MLP and excite pass (the same kernels as batch_norm_act + squeeze_excite).  Backward: the SE
+    MLP backward gives the squeeze term g, and the BatchNorm backward forms its output gradient
+    dy*s + g itself (ewvit_bn_bwd_se) — the SE input-gradient pass and its tensor never exist."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2):
+        L.require_gpu(x)
+        xc, N, HW, C = _rows(x)
+        M = N * HW
+        dev = x.device
+        x2 = torch.empty_like(xc)
+        mean = torch.empty(1, C, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta), L.ptr(running_mean),
+               L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean), L.ptr(invstd), 1, L.ptr(counter),
+               L.ptr(ws), L.stream(x2), work={'bytes': 3 * xc.numel() * xc.element_size()})
+        Csq = w1.shape[0]
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
+        h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
+        sc = torch.empty(N, C, dtype=torch.float32, device=dev)
+        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_se_squeeze_mlp_fwd', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
+               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(fws), L.stream(sc),
+               work={'bytes': x2.numel() * x2.element_size()})
+        y = torch.empty_like(x2)
+        L.call('ewvit_se_scale', L.ptr(x2), L.dt(x2), L.ptr(sc), None, L.ptr(y), N, HW, C, L.stream(y),
+               work={'bytes': 2 * x2.numel() * x2.element_size()})
+        ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
+        ctx.cfg = (act, b1 is not None, b2 is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc = ctx.saved_tensors
+        act, has_b1, has_b2 = ctx.cfg
+        N, C, H, W = xc.shape
+        HW, M, Csq = H * W, N * H * W, w1.shape[0]
+        dev = xc.device
+        dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        g = torch.empty(N, C, dtype=torch.float32, device=dev)
+        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
+        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
+        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if has_b1 else None
+        db2 = torch.empty(C, dtype=torch.float32, device=dev) if has_b2 else None
+        mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
+               L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
+               L.stream(g), work={'bytes': 2 * x2.numel() * x2.element_size()})
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
+        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_bn_bwd_se', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
+               L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW, L.ptr(ws),
+               L.stream(dx), work={'bytes': 5 * xc.numel() * xc.element_size()})
+        return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2)
+
+
+def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2):
+    """SE(act(bn(x))) for a training-mode BatchNorm module `bn` (batch statistics, running
+    statistics and counter updated like batch_norm_act) and the SE's 1x1 conv parameters
+    (fc1 = (se_w1, se_b1), fc2 = (se_w2, se_b2)) — see BnActSEFn."""
+    from .bn import ACT
+    if not bn.training or bn.momentum is None:
+        raise ValueError('bn_act_se: training-mode BatchNorm with a momentum only')
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    counter = bn.num_batches_tracked if bn.track_running_stats else None
+    return BnActSEFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, counter,
+                           ACT[act], se_w1, se_b1, se_w2, se_b2)
 
 
 def squeeze_excite(x, w1, b1, w2, b2):

@@ -28,6 +28,8 @@ _EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '32'))
 _SKIP_LINK = os.environ.get('EWVIT_SKIP_LINK', '1') != '0'
 # the frozen 3-channel stem on the ewvit direct conv (0: the library conv, A/B)
 _STEM = os.environ.get('EWVIT_STEM', '1') != '0'
+# MBConv's depthwise BN + SiLU and its squeeze-excitation as one ewvit.bn_act_se (0: A/B)
+_BN_SE = os.environ.get('EWVIT_BN_SE', '1') != '0'
 
 STAGES = (
     ('fused', 1, 3, 1, 24, 24, 2),
@@ -97,6 +99,14 @@ class ConvBNAct(nn.Sequential):
                 if r is not None:
                     return r[0], r[1:]
         return None
+
+    def can_bn_se(self, x, se):
+        """This block's BatchNorm + act on input x's conv output, then `se`, as one
+        ewvit.bn_act_se."""
+        bn, c = self[1], self[0].out_channels
+        return (_BN_SE and bn.training and bn.track_running_stats and bn.momentum is not None and x.is_cuda
+                and x.dim() == 4 and c % 8 == 0 and c <= 4096 and not self._hooked()
+                and isinstance(se, SqueezeExcitation) and not se._has_hooks())
 
     def can_drop_add(self, x):
         bn = self[1]
@@ -170,6 +180,24 @@ def _drop_path(x, p, training):
     return x * keep.div_(1.0 - p)
 
 
+def _seq(mods, h):
+    """Run a block's modules in order; a depthwise ConvBNAct followed by its SqueezeExcitation
+    runs as conv + ewvit.bn_act_se (the SE input-gradient pass folded into the BatchNorm
+    backward)."""
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, ConvBNAct) and i + 1 < len(mods) and m.can_bn_se(h, mods[i + 1]):
+            se = mods[i + 1]
+            h = ewvit.bn_act_se(m[0](h), m[1], 'silu' if len(m) > 2 else None, se.fc1.weight, se.fc1.bias,
+                                se.fc2.weight, se.fc2.bias)
+            i += 2
+            continue
+        h = m(h)
+        i += 1
+    return h
+
+
 def r_ok(x):
     return x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.shape[1] % 8 == 0
 
@@ -182,12 +210,10 @@ class _Block(nn.Module):
             # the block tail (project BN + drop-path + skip add) as one pass each way; the
             # skip's gradient is added in the first conv's dgrad epilogue (SkipLink)
             link = ewvit.conv.offer_skip_link(x) if torch.is_grad_enabled() and _SKIP_LINK else None
-            h = x
-            for m in list(self.block)[:-1]:
-                h = m(h)
+            h = _seq(list(self.block)[:-1], x)
             ewvit.conv._offered = None
             return last.forward_drop_add(h, x, self.sd_prob, link)
-        r = self.block(x)
+        r = self.block(x) if self.block._forward_hooks or self.block._forward_pre_hooks else _seq(list(self.block), x)
         if self.use_res_connect:
             if self.training and self.sd_prob > 0.0 and r.is_cuda and r.dtype in (torch.bfloat16, torch.float32) \
                     and (r[0].numel() % 8 == 0):

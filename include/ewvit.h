@@ -260,6 +260,15 @@ int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int6
                         const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
                         float *dgamma, float *dbeta, const float *row_scale, int64_t HW, float *workspace,
                         void *stream);
+/* Backward of BatchNorm(+act) followed by squeeze-excitation (MBConv's depthwise BN + SiLU
+ * then SE, torchvision Conv2dNormActivation + SqueezeExcitation, network/sfe.py:111-113):
+ * the BatchNorm's output gradient dy*se_s[n][c] + se_g[n][c] (se_s the excitation [N][C],
+ * se_g the squeeze term from ewvit_se_squeeze_mlp_bwd, HW rows per frame) is formed from the
+ * SE output gradient dy inside both passes — the SE input-gradient pass never runs.
+ * dgamma / dbeta overwritten. */
+int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
+                    const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
+                    float *dbeta, const float *se_s, const float *se_g, int64_t HW, float *workspace, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,

@@ -136,3 +136,77 @@ def test_block_tail_bn_drop_add(kind, hw, monkeypatch):
             assert rel(p1.grad, p2.grad) < 3e-2, n
     for (n, q1), q2 in zip(b1.named_buffers(), b2.buffers()):
         assert torch.allclose(q1.float(), q2.float(), rtol=1e-3, atol=1e-5), n
+
+
+@pytest.mark.parametrize('N,C,H,W,csq', [(64, 1536, 7, 7, 64), (64, 960, 14, 14, 40), (4, 256, 28, 28, 16),
+                                         (5, 24, 9, 11, 6)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_bn_act_se(N, C, H, W, csq, dtype):
+    """ewvit.bn_act_se = SE(SiLU(BatchNorm(x))) in training mode (MBConv's depthwise BN + SE), its
+    backward forming the BN output gradient dy*s + g inside the BN passes: against torch fp32
+    BatchNorm2d + SiLU + SE on the same inputs, and the running statistics / counter against
+    the module's."""
+    import ewvit
+    g = torch.Generator().manual_seed(C + W)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.5).to(dtype)
+    w1 = torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5
+    b1 = torch.randn(csq, generator=g) * 0.1
+    w2 = torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5
+    b2 = torch.randn(C, generator=g) * 0.1
+    bn_r = torch.nn.BatchNorm2d(C, eps=1e-3).train()
+    with torch.no_grad():
+        bn_r.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn_r.bias.copy_(torch.randn(C, generator=g) * 0.2)
+    bn_d = torch.nn.BatchNorm2d(C, eps=1e-3).train().to(DEV)
+    bn_d.load_state_dict(bn_r.state_dict())
+    ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    xr = x.float().clone().requires_grad_(True)
+    yr = ref_se(F.silu(bn_r(xr)), *ps)
+    dy = torch.randn(yr.shape, generator=g).to(dtype)
+    yr.backward(dy.float())
+    xd = x.to(DEV).to(memory_format=torch.channels_last).requires_grad_(True)
+    pd = [t.to(DEV).to(memory_format=torch.channels_last) if t.dim() == 4 else t.to(DEV) for t in (w1, b1, w2, b2)]
+    pd = [t.requires_grad_(True) for t in pd]
+    y = ewvit.bn_act_se(xd, bn_d, 'silu', *pd)
+    y.backward(dy.to(DEV).to(memory_format=torch.channels_last))
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    bf = dtype == torch.bfloat16
+    assert rel(y, yr) < (2e-2 if bf else 1e-4)              # bf16: BN output and y each rounded once
+    assert rel(xd.grad, xr.grad) < (3e-2 if bf else 5e-4)
+    assert rel(bn_d.weight.grad, bn_r.weight.grad) < (2e-2 if bf else 5e-4)
+    assert rel(bn_d.bias.grad, bn_r.bias.grad) < (2e-2 if bf else 5e-4)
+    for a, b in zip(pd, ps):
+        assert a.grad.shape == b.shape
+        assert rel(a.grad, b.grad) < (2e-2 if bf else 1e-3)
+    assert rel(bn_d.running_mean, bn_r.running_mean) < 1e-3 and rel(bn_d.running_var, bn_r.running_var) < 1e-3
+    assert int(bn_d.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
+
+
+def test_bn_act_se_matches_two_step_path():
+    """bn_act_se against the unfused product path (batch_norm_act, then squeeze_excite): same
+    forward bits; the input gradient differs only by the unfused path's bf16 rounding of the SE
+    input gradient (dy*s + g)."""
+    import ewvit
+    g = torch.Generator().manual_seed(4)
+    N, C, H, W, csq = 64, 1536, 7, 7, 64
+    x = (torch.randn(N, C, H, W, generator=g)).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    w1 = (torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5).to(DEV)
+    b1 = (torch.randn(csq, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5).to(DEV)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    dy = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    outs = []
+    for fused in (True, False):
+        bn = torch.nn.BatchNorm2d(C, eps=1e-3).train().to(DEV)
+        xd = x.clone().requires_grad_(True)
+        ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+        y = ewvit.bn_act_se(xd, bn, 'silu', *ps) if fused else \
+            ewvit.squeeze_excite(ewvit.batch_norm_act(xd, bn, 'silu'), *ps)
+        y.backward(dy)
+        outs.append((y, xd.grad, bn.weight.grad, bn.bias.grad, [p.grad for p in ps], bn.running_var.clone()))
+    a, b = outs
+    assert torch.equal(a[0], b[0]) and torch.equal(a[5], b[5])
+    assert rel(a[1], b[1]) < 1e-2
+    assert rel(a[2], b[2]) < 1e-2 and rel(a[3], b[3]) < 1e-2
+    for p, q in zip(a[4], b[4]):
+        assert torch.equal(p, q)
