@@ -213,6 +213,16 @@ def grid_cap(n):
         _cap = prev
 
 
+# the backward launches of a capped branch take EWVIT_MWT_GRID_CAP_BWD when set (> 0) instead
+# of their forward's cap: the two phases balance against different backbone chains
+_BWD_CAP = int(os.environ.get('EWVIT_MWT_GRID_CAP_BWD', '0'))
+
+
+def bwd_cap(n):
+    """The cap for the backward of an op whose forward ran under cap n (0: uncapped stays)."""
+    return _BWD_CAP if (n and _BWD_CAP > 0) else n
+
+
 def current_cap():
     return _cap
 

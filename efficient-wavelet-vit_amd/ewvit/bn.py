@@ -62,7 +62,7 @@ class BatchNormActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        with L.launch_cap(ctx.cap):
+        with L.launch_cap(L.bwd_cap(ctx.cap)):
             return BatchNormActFn._backward(ctx, dy)
 
     @staticmethod

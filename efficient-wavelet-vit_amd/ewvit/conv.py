@@ -207,7 +207,7 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        with L.launch_cap(ctx.cap):
+        with L.launch_cap(L.bwd_cap(ctx.cap)):
             return Conv2dFn._backward(ctx, dy)
 
     @staticmethod
