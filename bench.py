@@ -364,8 +364,10 @@ def main():
     # the same pass with the MWT on the main stream and uncapped grids: each kernel on the
     # whole chip (the timed step runs the MWT's big launches on 160 of the 256 CUs, beside
     # the backbone — network/dama.py _mwt_grid_cap — so their as-run durations are longer)
+    # (every rank runs it: the eager step issues the gradient all-reduces and the buffer
+    # broadcast, so a rank-0-only pass would wait on its peers forever)
     iso_table = None
-    if rank == 0 and args.config in (2, 3, 5):
+    if args.config in (2, 3, 5):
         saved = {k: os.environ.get(k) for k in ('EWVIT_BRANCH_STREAMS', 'EWVIT_MWT_GRID_CAP')}
         os.environ['EWVIT_BRANCH_STREAMS'] = '0'
         os.environ['EWVIT_MWT_GRID_CAP'] = '0'
