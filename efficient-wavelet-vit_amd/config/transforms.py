@@ -115,6 +115,14 @@ class FrameTransform:
             off += h * w * 3
         return np.asarray(geom, np.int64).reshape(-1, 10), off
 
+    def plan(self, geom, nbytes):
+        """ewvit_frames_plan: validate the geometry on the host, the launch shape (int[4])."""
+        lib = _lib.load()
+        plan = (ctypes.c_int * 4)()
+        if lib.ewvit_frames_plan(geom.ctypes.data_as(ctypes.c_void_p), len(geom), self.crop, nbytes, plan):
+            raise ValueError(f'ewvit_frames_plan: {lib.ewvit_last_error().decode()}')
+        return plan
+
     def batch(self, frames, boxes=None):
         """frames: sequence of HWC uint8 RGB arrays / tensors (any sizes) -> [N, 3, crop, crop]."""
         frames = [f if isinstance(f, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(f)) for f in frames]
@@ -126,10 +134,7 @@ class FrameTransform:
         dev = self.device or (frames[0].device if frames[0].is_cuda else torch.device('cuda'))
         geom, nbytes = self.geometry(frames, boxes)
         n, S = len(frames), self.crop
-        lib = _lib.load()
-        rb = lib.ewvit_frames_plan(geom.ctypes.data_as(ctypes.c_void_p), n, S, nbytes)
-        if rb < 0:
-            raise ValueError(f'ewvit_frames_plan: {lib.ewvit_last_error().decode()}')
+        plan = self.plan(geom, nbytes)
         if all(f.is_cuda for f in frames):
             buf = torch.cat([f.reshape(-1) for f in frames])
         else:
@@ -146,13 +151,13 @@ class FrameTransform:
         with torch.cuda.device(dev):
             stream = _lib.stream(out)
             if self.jitter is None:
-                _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), n, S, rb, 1, self.mean_std,
+                _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), n, S, plan, 1, self.mean_std,
                           _lib.ptr(out), stream)
             else:
                 img = torch.empty(n, S, S, 3, dtype=torch.uint8, device=dev)
                 jit = torch.tensor([self._jitter_params() for _ in range(n)], dtype=torch.float32)
                 jit = jit.pin_memory().to(dev, non_blocking=True)
-                _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), n, S, rb, 0, None,
+                _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), n, S, plan, 0, None,
                           _lib.ptr(img), stream)
                 _lib.call('ewvit_frames_jitter_normalize', _lib.ptr(img), _lib.ptr(jit), n, S, self.mean_std,
                           _lib.ptr(out), stream)

@@ -25,7 +25,7 @@ namespace ewvit {
 
 constexpr int FR_KMAX = 17;            // taps per output sample: 2 * ceil(support) + 1, scale <= 8
 constexpr int FR_SMAX = 256;           // output size S (CenterCrop) at most
-constexpr int FR_TMP = 40 * 1024;      // LDS bytes of the horizontal pass's rows (2 workgroups per CU)
+constexpr int FR_LDS = 64 * 1024;      // dynamic LDS per workgroup (2 workgroups per CU)
 constexpr int FR_PREC = 22;            // Pillow PRECISION_BITS for 8-bpc images
 constexpr int FR_GEOM = 10;            // int64 per frame (include/ewvit.h)
 
@@ -84,17 +84,41 @@ __device__ __forceinline__ FrGeom fr_geom(const int64_t *g, int n) {
 
 struct FrNorm { float mean[3], inv[3]; };   // inv = std (division, as torchvision)
 
-// grid (ceil(S / rb), N), 256 threads.  out: TO_F32 -> [N][3][S][S] normalised fp32,
-// else [N][S][S][3] uint8.
-template <bool TO_F32>
+// LDS layout of a resize workgroup (ints, then pixels): hk [kmax][S] column weights, hx / hn [S]
+// first tap / taps per column, vk [kmax][rb], vy / vn [rb]; then the horizontal pass's rows
+// tmp [rmax][S] and, when the plan stages the source (pitch > 0), the source rows
+// src [rmax][pitch] — one 4-byte word per RGB pixel (R | G << 8 | B << 16), so a tap is one LDS
+// read and three byte extracts.
+struct FrPlan { int rb, kmax, rmax, pitch; };
+
+__host__ __device__ inline int fr_ints(int S, const FrPlan &p) { return (p.kmax + 2) * (S + p.rb); }
+__host__ __device__ inline int fr_lds_bytes(int S, const FrPlan &p) {
+  return (fr_ints(S, p) + p.rmax * S + p.rmax * p.pitch) * 4;
+}
+
+// acc += weight * (8-bit channels of a packed pixel); weights and bytes fit the 24-bit multiply
+__device__ __forceinline__ void fr_tap(uint32_t px, uint32_t w, uint32_t &a0, uint32_t &a1, uint32_t &a2) {
+  a0 += __umul24(px & 0xffu, w);   // (Pillow's weights are >= 0 and <= 2^22)
+  a1 += __umul24((px >> 8) & 0xffu, w);
+  a2 += __umul24(px >> 16, w);
+}
+__device__ __forceinline__ uint32_t fr_pack(uint32_t a0, uint32_t a1, uint32_t a2) {
+  const uint32_t r = min(a0 >> FR_PREC, 255u), g = min(a1 >> FR_PREC, 255u), b = min(a2 >> FR_PREC, 255u);
+  return r | (g << 8) | (b << 16);
+}
+
+// grid (ceil(S / rb), N), 256 threads, fr_lds_bytes of dynamic LDS; KT >= the plan's taps.
+// out: TO_F32 -> [N][3][S][S] normalised fp32, else [N][S][S][3] uint8.
+template <int KT, bool TO_F32>
 __global__ __launch_bounds__(256) void frames_resize_crop_kernel(const uint8_t *__restrict__ src,
-                                                                 const int64_t *__restrict__ geom, int S, int rb,
+                                                                 const int64_t *__restrict__ geom, int S, FrPlan pl,
                                                                  FrNorm nm, void *__restrict__ out) {
-  __shared__ int hk[FR_KMAX * FR_SMAX];      // [k][column] (lanes read consecutive columns)
-  __shared__ int hx[FR_SMAX], hn[FR_SMAX];
-  __shared__ int vk[FR_KMAX * 64];
-  __shared__ int vy[64], vn[64];
-  __shared__ __attribute__((aligned(16))) uint8_t tmp[FR_TMP];
+  extern __shared__ __attribute__((aligned(16))) int fr_smem[];
+  const int rb = pl.rb, kmax = pl.kmax;
+  int *hk = fr_smem, *hx = hk + kmax * S, *hn = hx + S;
+  int *vk = hn + S, *vy = vk + kmax * rb, *vn = vy + rb;
+  uint32_t *tmp = reinterpret_cast<uint32_t *>(fr_smem + fr_ints(S, pl));
+  uint32_t *stg = tmp + pl.rmax * S;
   const int tid = threadIdx.x, n = blockIdx.y;
   const int y_beg = blockIdx.x * rb;
   const int rows = S - y_beg < rb ? S - y_beg : rb;
@@ -102,60 +126,92 @@ __global__ __launch_bounds__(256) void frames_resize_crop_kernel(const uint8_t *
   const FrGeom g = fr_geom(geom, n);
   for (int c = tid; c < S; c += blockDim.x) {
     int cnt;
-    hx[c] = fr_coeffs(g.w, g.nw, g.ox + c, hk + c, FR_SMAX, cnt);
+    hx[c] = fr_coeffs(g.w, g.nw, g.ox + c, hk + c, S, cnt);
     hn[c] = cnt;
   }
   for (int r = tid; r < rows; r += blockDim.x) {
     int cnt;
-    vy[r] = fr_coeffs(g.h, g.nh, g.oy + y_beg + r, vk + r, 64, cnt);
+    vy[r] = fr_coeffs(g.h, g.nh, g.oy + y_beg + r, vk + r, rb, cnt);
     vn[r] = cnt;
   }
   __syncthreads();
-  const int y0 = vy[0], y1 = vy[rows - 1] + vn[rows - 1];   // both monotone in the row
-  const int R = y1 - y0;
-  if (R * S * 3 > FR_TMP) return;                           // the planner keeps R within LDS
-  // horizontal pass: source rows y0 .. y1 of the crop, the S output columns
-  const uint8_t *base = src + g.off + (int64_t)g.t * g.stride + (int64_t)g.l * 3;
-  for (int i = tid; i < R * S; i += blockDim.x) {
-    const int r = i / S, c = i - r * S;
-    const uint8_t *p = base + (int64_t)(y0 + r) * g.stride + hx[c] * 3;
-    int a0 = 1 << (FR_PREC - 1), a1 = a0, a2 = a0;
-    const int cnt = hn[c];
-    for (int k = 0; k < cnt; ++k) {
-      const int w = hk[k * FR_SMAX + c];
-      a0 += (int)p[3 * k] * w;
-      a1 += (int)p[3 * k + 1] * w;
-      a2 += (int)p[3 * k + 2] * w;
+  const int y0 = vy[0], R = vy[rows - 1] + vn[rows - 1] - y0;   // both bounds monotone in the row
+  const int x0 = hx[0], npx = hx[S - 1] + hn[S - 1] - x0;
+  if (R > pl.rmax) return;                                       // the planner bounds R
+  const uint8_t *base = src + g.off + (int64_t)(g.t + y0) * g.stride + (int64_t)(g.l + x0) * 3;
+  const bool staged = npx <= pl.pitch;
+  if (staged) {
+    // 4 pixels (12 bytes) per item from the 4 aligned dwords that hold them (a dword holding
+    // one of the frame's bytes never leaves its allocation; dwords past the span are not read)
+    const int groups = (npx + 3) >> 2, items = R * groups;
+    for (int i = tid; i < items; i += blockDim.x) {
+      const int r = i / groups, j = i - r * groups;
+      const uintptr_t a = (uintptr_t)(base + (int64_t)r * g.stride);
+      const uintptr_t al = a & ~(uintptr_t)3, last = (a + 3 * npx - 1) & ~(uintptr_t)3;
+      const uint32_t lead = (uint32_t)(a & 3);
+      uint32_t d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uintptr_t ad = al + 12 * j + 4 * q;
+        d[q] = ad <= last ? *reinterpret_cast<const uint32_t *>(ad) : 0u;
+      }
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(d[1], d[0], lead);
+      const uint32_t w1 = __builtin_amdgcn_alignbyte(d[2], d[1], lead);
+      const uint32_t w2 = __builtin_amdgcn_alignbyte(d[3], d[2], lead);
+      uint4 v;
+      v.x = w0 & 0xffffffu;
+      v.y = (w0 >> 24) | ((w1 & 0xffffu) << 8);
+      v.z = (w1 >> 16) | ((w2 & 0xffu) << 16);
+      v.w = w2 >> 8;
+      *reinterpret_cast<uint4 *>(stg + r * pl.pitch + 4 * j) = v;
     }
-    uint8_t *q = tmp + i * 3;
-    q[0] = (uint8_t)fr_clip8(a0);
-    q[1] = (uint8_t)fr_clip8(a1);
-    q[2] = (uint8_t)fr_clip8(a2);
+    __syncthreads();
+  }
+  // horizontal pass, a thread per output column: its taps in registers, down the R rows
+  for (int c = tid; c < S; c += blockDim.x) {
+    const int cnt = hn[c], xo = hx[c] - x0;
+    uint32_t w[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) w[k] = k < cnt ? (uint32_t)hk[k * S + c] : 0u;
+    for (int r = 0; r < R; ++r) {
+      uint32_t a0 = 1u << (FR_PREC - 1), a1 = a0, a2 = a0;
+      if (staged) {
+        const uint32_t *p = stg + r * pl.pitch + xo;
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+          if (k < cnt) fr_tap(p[k], w[k], a0, a1, a2);
+      } else {
+        const uint8_t *p = base + (int64_t)r * g.stride + xo * 3;
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+          if (k < cnt) fr_tap(p[3 * k] | (p[3 * k + 1] << 8) | (p[3 * k + 2] << 16), w[k], a0, a1, a2);
+      }
+      tmp[r * S + c] = fr_pack(a0, a1, a2);
+    }
   }
   __syncthreads();
-  // vertical pass from LDS
-  for (int i = tid; i < rows * S; i += blockDim.x) {
-    const int r = i / S, c = i - r * S;
-    const uint8_t *p = tmp + ((vy[r] - y0) * S + c) * 3;
-    int a0 = 1 << (FR_PREC - 1), a1 = a0, a2 = a0;
-    const int cnt = vn[r];
-    for (int k = 0; k < cnt; ++k) {
-      const int w = vk[k * 64 + r];
-      a0 += (int)p[k * S * 3] * w;
-      a1 += (int)p[k * S * 3 + 1] * w;
-      a2 += (int)p[k * S * 3 + 2] * w;
-    }
-    const unsigned u[3] = {fr_clip8(a0), fr_clip8(a1), fr_clip8(a2)};
-    const int y = y_beg + r;
-    if (TO_F32) {
-      float *o = reinterpret_cast<float *>(out) + (int64_t)n * 3 * S * S + (int64_t)y * S + c;
+  // vertical pass from LDS, a thread per output column
+  for (int c = tid; c < S; c += blockDim.x) {
+    for (int r = 0; r < rows; ++r) {
+      const int cnt = vn[r];
+      const uint32_t *p = tmp + (vy[r] - y0) * S + c;
+      uint32_t a0 = 1u << (FR_PREC - 1), a1 = a0, a2 = a0;
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) o[(int64_t)ch * S * S] = ((float)u[ch] / 255.0f - nm.mean[ch]) / nm.inv[ch];
-    } else {
-      uint8_t *o = reinterpret_cast<uint8_t *>(out) + (((int64_t)n * S + y) * S + c) * 3;
-      o[0] = (uint8_t)u[0];
-      o[1] = (uint8_t)u[1];
-      o[2] = (uint8_t)u[2];
+      for (int k = 0; k < KT; ++k)
+        if (k < cnt) fr_tap(p[k * S], (uint32_t)vk[k * rb + r], a0, a1, a2);
+      const uint32_t px = fr_pack(a0, a1, a2);
+      const int y = y_beg + r;
+      if (TO_F32) {
+        float *o = reinterpret_cast<float *>(out) + (int64_t)n * 3 * S * S + (int64_t)y * S + c;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          o[(int64_t)ch * S * S] = ((float)((px >> (8 * ch)) & 0xffu) / 255.0f - nm.mean[ch]) / nm.inv[ch];
+      } else {
+        uint8_t *o = reinterpret_cast<uint8_t *>(out) + (((int64_t)n * S + y) * S + c) * 3;
+        o[0] = (uint8_t)px;
+        o[1] = (uint8_t)(px >> 8);
+        o[2] = (uint8_t)(px >> 16);
+      }
     }
   }
 }
@@ -234,12 +290,12 @@ static FrNorm fr_norm(const float *mean_std) {
 
 using namespace ewvit;
 
-extern "C" int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t nbytes) {
-  if (!geom || n <= 0 || S <= 0 || S > FR_SMAX) {
+extern "C" int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t nbytes, int *plan) {
+  if (!geom || !plan || n <= 0 || S <= 0 || S > FR_SMAX) {
     set_error("frames_plan: bad arguments (n %lld, S %d; S <= %d)", (long long)n, S, FR_SMAX);
-    return -EWVIT_EINVAL;
+    return EWVIT_EINVAL;
   }
-  int rb = 16;   // 14 bands of a 224-row output: ~900 workgroups for 64 frames
+  int kmax = 3, words = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t *p = geom + i * FR_GEOM;
     const int l = (int)p[2], t = (int)p[3], w = (int)p[4], h = (int)p[5];
@@ -248,36 +304,69 @@ extern "C" int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t 
         ox < 0 || oy < 0 || ox + S > nw || oy + S > nh || p[0] + (t + h - 1) * p[1] + 3 * (int64_t)(l + w) > nbytes) {
       set_error("frames_plan: frame %lld: bad geometry (box %d,%d %dx%d, resize %dx%d, crop at %d,%d, S %d)",
                 (long long)i, l, t, w, h, nw, nh, ox, oy, S);
-      return -EWVIT_EINVAL;
+      return EWVIT_EINVAL;
     }
     // taps per output sample: support = max(scale, 1) -> 2 * ceil(support) + 1 <= FR_KMAX
     if (w > 8 * (int64_t)nw || h > 8 * (int64_t)nh) {
       set_error("frames_plan: frame %lld: downscale %dx%d -> %dx%d beyond 8x", (long long)i, w, h, nw, nh);
-      return -EWVIT_EINVAL;
+      return EWVIT_EINVAL;
     }
-    while (rb > 1 && fr_band_rows(h, nh, oy, S, rb) * S * 3 > FR_TMP) rb >>= 1;
-    if (fr_band_rows(h, nh, oy, S, rb) * S * 3 > FR_TMP) {
-      set_error("frames_plan: frame %lld: one output row needs more source rows than LDS holds", (long long)i);
-      return -EWVIT_EINVAL;
-    }
+    const int kx = 2 * ((w + nw - 1) / nw) + 1, ky = 2 * ((h + nh - 1) / nh) + 1;
+    kmax = kx > kmax ? kx : kmax;
+    kmax = ky > kmax ? ky : kmax;
+    int n0, n1;
+    const int a = fr_coeffs(w, nw, ox, nullptr, 0, n0), b = fr_coeffs(w, nw, ox + S - 1, nullptr, 0, n1);
+    const int wd = (b + n1 - a + 3) / 4 * 4;       // staged pixels per source row (16-B rows)
+    words = wd > words ? wd : words;
   }
-  return rb;
+  auto rmax_of = [&](int rb) {
+    int r = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t *p = geom + i * FR_GEOM;
+      const int v = fr_band_rows((int)p[5], (int)p[7], (int)p[9], S, rb);
+      r = v > r ? v : r;
+    }
+    return r;
+  };
+  // staged source rows at the tallest band that fits, else bands read the source from global
+  for (int staged = 1; staged >= 0; --staged)
+    for (int rb = 16; rb >= 1; rb >>= 1) {
+      const FrPlan pl{rb, kmax, rmax_of(rb), staged ? words : 0};
+      if (fr_lds_bytes(S, pl) <= FR_LDS) {
+        plan[0] = pl.rb; plan[1] = pl.kmax; plan[2] = pl.rmax; plan[3] = pl.pitch;
+        return 0;
+      }
+    }
+  set_error("frames_plan: one output row needs more source rows than LDS holds");
+  return EWVIT_EINVAL;
 }
 
-extern "C" int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *geom, int64_t n, int S, int rb,
+extern "C" int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *geom, int64_t n, int S, const int *plan,
                                         int to_f32, const float *mean_std, void *out, void *stream) {
-  EWVIT_CHECK_ARG(frames && geom && out && n > 0, "frames_resize_crop: null pointer or empty batch");
-  EWVIT_CHECK_ARG(S > 0 && S <= FR_SMAX && rb >= 1 && rb <= 64, "frames_resize_crop: S %d / rb %d out of range", S, rb);
+  EWVIT_CHECK_ARG(frames && geom && out && plan && n > 0, "frames_resize_crop: null pointer or empty batch");
+  const FrPlan pl{plan[0], plan[1], plan[2], plan[3]};
+  EWVIT_CHECK_ARG(S > 0 && S <= FR_SMAX && pl.rb >= 1 && pl.rb <= 64 && pl.kmax >= 1 && pl.kmax <= FR_KMAX &&
+                      pl.rmax >= 1 && pl.pitch >= 0 && fr_lds_bytes(S, pl) <= FR_LDS,
+                  "frames_resize_crop: S %d / plan (%d, %d, %d, %d) out of range (use ewvit_frames_plan)", S, pl.rb,
+                  pl.kmax, pl.rmax, pl.pitch);
   EWVIT_CHECK_ARG(!to_f32 || mean_std, "frames_resize_crop: normalised output needs mean_std");
   const float one[6] = {0.f, 0.f, 0.f, 1.f, 1.f, 1.f};
   const FrNorm nm = fr_norm(mean_std ? mean_std : one);
-  const dim3 grid((unsigned)((S + rb - 1) / rb), (unsigned)n);
-  if (to_f32)
-    hipLaunchKernelGGL(frames_resize_crop_kernel<true>, grid, dim3(256), 0, as_stream(stream), frames, geom, S, rb, nm,
-                       out);
-  else
-    hipLaunchKernelGGL(frames_resize_crop_kernel<false>, grid, dim3(256), 0, as_stream(stream), frames, geom, S, rb, nm,
-                       out);
+  EWVIT_CHECK_ARG(pl.pitch % 4 == 0, "frames_resize_crop: plan pitch %d not a multiple of 4", pl.pitch);
+  const dim3 grid((unsigned)((S + pl.rb - 1) / pl.rb), (unsigned)n);
+  const size_t lds = (size_t)fr_lds_bytes(S, pl);
+  hipStream_t st = as_stream(stream);
+#define EWVIT_FR_LAUNCH(KT_)                                                                                        \
+  do {                                                                                                            \
+    if (to_f32)                                                                                                   \
+      hipLaunchKernelGGL((frames_resize_crop_kernel<KT_, true>), grid, dim3(256), lds, st, frames, geom, S, pl, nm, out); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((frames_resize_crop_kernel<KT_, false>), grid, dim3(256), lds, st, frames, geom, S, pl, nm, out); \
+  } while (0)
+  if (pl.kmax <= 5) EWVIT_FR_LAUNCH(5);
+  else if (pl.kmax <= 9) EWVIT_FR_LAUNCH(9);
+  else EWVIT_FR_LAUNCH(FR_KMAX);
+#undef EWVIT_FR_LAUNCH
   return launch_status("frames_resize_crop");
 }
 

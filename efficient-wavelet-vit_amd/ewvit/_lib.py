@@ -84,7 +84,7 @@ SIGNATURES = {
     'ewvit_scale_add_drop': [_vp, _vp, _i32, _f32, _u64, _vp, _vp, _vp, _i64, _i64, _vp],
     'ewvit_attn_bwd': [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp,
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
-    'ewvit_frames_resize_crop': [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+    'ewvit_frames_resize_crop': [_vp, _vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp],
     'ewvit_frames_jitter_normalize': [_vp, _vp, _i64, _i32, _vp, _vp, _vp],
 }
 
@@ -102,7 +102,7 @@ QUERIES = {
     'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
-    'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64]),
+    'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64, _vp]),
 }
 
 _lib = None

@@ -477,17 +477,18 @@ int ewvit_adam_step(int n, float *const *params, const float *const *grads, floa
  *           short-side rule), CenterCrop offsets x, y (round((size - S) / 2))
  *   mean_std  host float[6]: mean[3], std[3]
  * ewvit_frames_plan (host-only, geom in HOST memory): validates every frame (box inside the
- * buffer, S <= 256, crop inside the resized image, downscale <= 8x) and returns the output
- * rows per workgroup `rb` for ewvit_frames_resize_crop, or -EWVIT_EINVAL.
- * ewvit_frames_resize_crop (geom in DEVICE memory): out = to_f32 ? [n][3][S][S] normalised
- * f32 : [n][S][S][3] uint8 (the PIL image after CenterCrop).
+ * buffer, S <= 256, crop inside the resized image, downscale <= 8x) and fills plan[4] (output
+ * rows per workgroup, taps, source rows per workgroup, staged dwords per source row) for
+ * ewvit_frames_resize_crop; returns 0 or EWVIT_EINVAL.
+ * ewvit_frames_resize_crop (geom in DEVICE memory, plan in host memory): out = to_f32 ?
+ * [n][3][S][S] normalised f32 : [n][S][S][3] uint8 (the PIL image after CenterCrop).
  * ewvit_frames_jitter_normalize: ColorJitter + ToTensor + Normalize of that uint8 image;
  * jitter [n][4] f32 device: brightness factor, contrast factor (< 0: absent), order (0:
  * brightness first, 1: contrast first — torchvision's randperm(4) restricted to ids 0 / 1),
  * unused; out [n][3][S][S] f32. */
-int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t nbytes);
-int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *geom, int64_t n, int S, int rb, int to_f32,
-                             const float *mean_std, void *out, void *stream);
+int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t nbytes, int *plan);
+int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *geom, int64_t n, int S, const int *plan,
+                             int to_f32, const float *mean_std, void *out, void *stream);
 int ewvit_frames_jitter_normalize(const uint8_t *img, const float *jitter, int64_t n, int S, const float *mean_std,
                                   float *out, void *stream);
 

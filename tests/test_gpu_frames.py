@@ -47,21 +47,23 @@ def test_uint8_image_bit_exact():
     boxes = _boxes(frames, BOXES)
     t = _transform()
     geom, nbytes = t.geometry(frames, boxes)
-    rb = _lib.load().ewvit_frames_plan(geom.ctypes.data_as(ctypes.c_void_p), len(frames), 224, nbytes)
-    assert rb >= 1
+    plan = t.plan(geom, nbytes)
+    assert 1 <= plan[0] <= 16 and plan[3] > 0      # source rows staged in LDS
     buf = torch.from_numpy(np.concatenate([f.reshape(-1) for f in frames])).cuda()
     g = torch.from_numpy(geom).cuda()
     img = torch.empty(len(frames), 224, 224, 3, dtype=torch.uint8, device='cuda')
-    _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), len(frames), 224, rb, 0, None,
+    _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), len(frames), 224, plan, 0, None,
               _lib.ptr(img), _lib.stream(img))
     img = img.cpu().numpy()
     for i, (f, b) in enumerate(zip(frames, boxes)):
         np.testing.assert_array_equal(img[i], T.resize_center_crop(f, b))
-    # a smaller band height computes the same pixels
-    img2 = torch.empty_like(torch.from_numpy(img)).cuda()
-    _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), len(frames), 224, 1, 0, None,
-              _lib.ptr(img2), _lib.stream(img2))
-    np.testing.assert_array_equal(img2.cpu().numpy(), img)
+    # one output row per workgroup, and source rows read from global memory (no staging):
+    # the same pixels
+    for alt in ((1, plan[1], plan[2], plan[3]), (plan[0], plan[1], plan[2], 0)):
+        img2 = torch.zeros(len(frames), 224, 224, 3, dtype=torch.uint8, device='cuda')
+        _lib.call('ewvit_frames_resize_crop', _lib.ptr(buf), _lib.ptr(g), len(frames), 224, (ctypes.c_int * 4)(*alt),
+                  0, None, _lib.ptr(img2), _lib.stream(img2))
+        np.testing.assert_array_equal(img2.cpu().numpy(), img, err_msg=str(alt))
 
 
 def test_train_batch_jitter_bit_exact():

@@ -103,24 +103,26 @@ def test_product_geometry_matches_oracle():
 
 
 def test_planner_validates_on_the_host():
-    """ewvit_frames_plan runs on the host: band height and argument checks, no GPU."""
+    """ewvit_frames_plan runs on the host: launch shape and argument checks, no GPU."""
     from config.transforms import FrameTransform
     from ewvit import _lib
     lib = _lib.load()
-    t = FrameTransform()
 
     def plan(frames, nbytes=None, S=224):
+        t = FrameTransform(crop=S)
         geom, nb = t.geometry(frames)
-        return lib.ewvit_frames_plan(geom.ctypes.data_as(ctypes.c_void_p), len(frames), S,
-                                     nb if nbytes is None else nbytes), geom
+        out = (ctypes.c_int * 4)()
+        rc = lib.ewvit_frames_plan(geom.ctypes.data_as(ctypes.c_void_p), len(frames), S,
+                                   nb if nbytes is None else nbytes, out)
+        return rc, list(out)
 
-    rb, _ = plan([np.zeros((480, 640, 3), np.uint8)])
-    assert rb == 16
-    rb, _ = plan([np.zeros((1080, 1920, 3), np.uint8), np.zeros((2000, 3000, 3), np.uint8)])
-    assert 1 <= rb < 16          # 4.4x down: fewer output rows per workgroup
-    rb, _ = plan([np.zeros((480, 640, 3), np.uint8)], nbytes=1000)
-    assert rb < 0 and b'bad geometry' in lib.ewvit_last_error()
-    rb, _ = plan([np.zeros((4000, 4000, 3), np.uint8)])
-    assert rb < 0 and b'beyond 8x' in lib.ewvit_last_error()
-    rb, _ = plan([np.zeros((480, 640, 3), np.uint8)], S=300)
-    assert rb < 0
+    rc, p = plan([np.zeros((480, 640, 3), np.uint8)])
+    assert rc == 0 and p[0] == 16 and p[1] == 5 and p[3] > 0           # staged; 480 -> 450: support 2
+    rc, p = plan([np.zeros((1080, 1920, 3), np.uint8), np.zeros((2000, 3000, 3), np.uint8)])
+    assert rc == 0 and 1 <= p[0] < 16 and p[1] == 2 * 5 + 1             # 4.4x down: 11 taps
+    rc, _ = plan([np.zeros((480, 640, 3), np.uint8)], nbytes=1000)
+    assert rc != 0 and b'bad geometry' in lib.ewvit_last_error()
+    rc, _ = plan([np.zeros((4000, 4000, 3), np.uint8)])
+    assert rc != 0 and b'beyond 8x' in lib.ewvit_last_error()
+    rc, _ = plan([np.zeros((480, 640, 3), np.uint8)], S=300)
+    assert rc != 0
