@@ -86,6 +86,7 @@ SIGNATURES = {
                        _vp, _vp, _i64, _i64, _i32, _i32, _i32, _f32, _vp],
     'ewvit_frames_resize_crop': [_vp, _vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp],
     'ewvit_frames_jitter_normalize': [_vp, _vp, _i64, _i32, _vp, _vp, _vp],
+    'ewvit_combined_loss': [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp],
 }
 
 # size queries: name -> (restype, argtypes)

@@ -22,12 +22,58 @@ def orth_weight(epoch, max_epochs):
     return min(1.0, (epoch - 0.2 * max_epochs) / (0.5 * max_epochs))
 
 
+class _CombinedLoss(torch.autograd.Function):
+    """ewvit_combined_loss: the loss and every input gradient in one launch on the GPU (the
+    torch form below is ~40 small launches between the forward and the backward); the
+    backward scales the saved gradients by the incoming one."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, space, freq, pos_weight, weight, lam):
+        from ewvit import _lib as L
+        B, D = space.shape
+        lg = logits.detach().float().reshape(B).contiguous()
+        lb = labels.detach().float().reshape(B).contiguous()
+        s, f = space.detach().float().contiguous(), freq.detach().float().contiguous()
+        out = torch.empty(3, dtype=torch.float32, device=space.device)
+        dl, ds, df = torch.empty_like(lg), torch.empty_like(s), torch.empty_like(f)
+        pw = pos_weight.detach().float().reshape(1).contiguous() if pos_weight is not None else None
+        w = weight.detach().float().reshape(1).contiguous() if weight is not None else None
+        L.require_gpu(lg, s, f)
+        L.call('ewvit_combined_loss', L.ptr(lg), L.ptr(lb), L.ptr(s), L.ptr(f), B, D, L.ptr(pw), L.ptr(w),
+               float(lam), L.ptr(out), L.ptr(dl), L.ptr(ds), L.ptr(df), L.stream(out))
+        ctx.save_for_backward(dl, ds, df)
+        ctx.logit_shape = logits.shape
+        total, parts = out[0], out[1:]
+        ctx.mark_non_differentiable(parts)
+        return total, parts
+
+    @staticmethod
+    def backward(ctx, g, _):
+        dl, ds, df = ctx.saved_tensors
+        dl, ds, df = torch._foreach_mul([dl, ds, df], g)
+        return dl.view(ctx.logit_shape), None, ds, df, None, None, None
+
+
+def _fused_ok(logits, space, freq, criterion):
+    return (logits.is_cuda and type(criterion) is torch.nn.BCEWithLogitsLoss and criterion.reduction == 'mean'
+            and criterion.weight is None and (criterion.pos_weight is None or criterion.pos_weight.numel() == 1)
+            and space.dim() == 2 and space.shape == freq.shape and logits.numel() == space.shape[0]
+            and 1 <= space.shape[0] <= 64 and 4 * space.numel() + 2 * space.shape[0] + 8 <= 16384)
+
+
 def combined_loss(outputs, labels, criterion, epoch, max_epochs, weight=None):  # train.py:69-91
     """weight: optional device tensor holding orth_weight(epoch, max_epochs), updated in place
     by the caller each epoch — the form a step replayed from a HIP graph needs (the
     epoch / max_epochs arguments are then ignored; a zero weight gives the reference's
-    cls-only loss value and gradients)."""
+    cls-only loss value and gradients).  On the GPU with the reference's criterion
+    (BCEWithLogitsLoss, mean, scalar pos_weight) the whole objective is one ewvit launch."""
     logits = outputs['logits']
+    if _fused_ok(logits, outputs['space'], outputs['freq'], criterion):
+        lam = 0.0 if weight is not None else orth_weight(epoch, max_epochs)
+        total, parts = _CombinedLoss.apply(logits, labels, outputs['space'], outputs['freq'], criterion.pos_weight,
+                                           weight, lam)
+        orth = parts[1] if (weight is not None or lam != 0.0) else 0.0
+        return total, {'cls_loss': parts[0], 'orth_loss': orth}
     labels = labels.view(-1, 1).float()
     cls_loss = criterion(logits, labels)
     if weight is not None:

@@ -464,6 +464,18 @@ int ewvit_adam_step(int n, float *const *params, const float *const *grads, floa
                     float *const *exp_avg_sq, const int64_t *numel, const float *const *steps, double lr,
                     const double *lr_dev, double beta1, double beta2, float eps, float weight_decay, void *stream);
 
+/* ------------------------------------------------------ loss ---
+ * combined_loss of train.py:69-91 with orthogonal_loss of train.py:55-67, forward and all input
+ * gradients in one launch: out[0] = cls + w * orth, out[1] = cls = BCEWithLogits(logits, labels,
+ * pos_weight, mean), out[2] = orth = ||offdiag(normalize(space)^T normalize(freq))||_F^2 /
+ * (D (D - 1)); d_logits / d_space / d_freq = d out[0] / d input.  w = *weight (device f32) when
+ * weight is non-null (the curriculum weight a replayed step reads), else lam.  logits / labels
+ * [B], space / freq / d_* [B, D] f32 row-major, pos_weight device f32[1] or NULL (1);
+ * 1 <= B <= 64, 4 * B * D floats <= 64 KB. */
+int ewvit_combined_loss(const float *logits, const float *labels, const float *space, const float *freq, int64_t B,
+                        int64_t D, const float *pos_weight, const float *weight, float lam, float *out,
+                        float *d_logits, float *d_space, float *d_freq, void *stream);
+
 /* ------------------------------------------------------ frames (input side) ---
  * The per-frame transform chain of config/transforms.py:81-113 applied by the datasets'
  * __getitem__ (config/data_loader.py:325-337: cv2.imread -> BGR2RGB -> transform(frame) per

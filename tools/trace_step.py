@@ -9,9 +9,12 @@ def main():
     path = sys.argv[1]
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    starts = [i for i, r in enumerate(rows) if 'dwt_multilevel' in r['Kernel_Name']]
+    starts = [i for i, r in enumerate(rows) if 'dwt_multilevel' in r['Kernel_Name'] or 'dwt_hf_fused' in r['Kernel_Name']]
     k = int(sys.argv[sys.argv.index('--nth') + 1]) if '--nth' in sys.argv else 2
     a, b = starts[-k], starts[-k + 1] if k > 1 else len(rows)
+    if '--largest' in sys.argv:     # the delimited span with the most kernels (a whole step)
+        spans = [(starts[i + 1] - starts[i], starts[i], starts[i + 1]) for i in range(len(starts) - 1)]
+        _, a, b = max(spans)
     step = rows[a:b]
     t0 = int(step[0]['Start_Timestamp'])
     t1 = int(step[-1]['End_Timestamp'])
