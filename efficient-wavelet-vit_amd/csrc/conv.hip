@@ -1304,8 +1304,22 @@ static void launch_glds_dense(const FwdArgs &a, int64_t src_bytes, hipStream_t s
                          0, s, a, src_bytes, ntn, 0, ntiles);                                                     \
   } while (0)
   (void)bn;                                // Ncol > 64: 128-wide column tiles
+  // A/B knobs: EWVIT_CONV_DENSE_W8MAX (grids up to this many blocks take 8 waves; 4096 covers
+  // stage 2's 48 -> 192 expands, 3136 blocks: 81 -> 75 us), EWVIT_CONV_DENSE_NS (ring depth of
+  // the big-grid form; 3 measured 30-60 % slower)
+  static const int w8max = [] {
+    const char *e = getenv("EWVIT_CONV_DENSE_W8MAX");
+    return e ? atoi(e) : 4096;
+  }();
+  static const int dns = [] {
+    const char *e = getenv("EWVIT_CONV_DENSE_NS");
+    return e ? atoi(e) : 2;
+  }();
   if (nwg <= 256) EWVIT_GLDS_DENSE(128, 4, 4);
-  else if (nwg <= 2048) EWVIT_GLDS_DENSE(128, 2, 4);
+  else if (nwg <= w8max) {
+    if (dns == 3) EWVIT_GLDS_DENSE(128, 3, 4);
+    else EWVIT_GLDS_DENSE(128, 2, 4);
+  } else if (dns == 3) EWVIT_GLDS_DENSE(128, 3, 2);
   else EWVIT_GLDS_DENSE(128, 2, 2);
 #undef EWVIT_GLDS_DENSE
 }
@@ -1343,14 +1357,21 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     return false;
   int v = glds_variant() & 7;
   const int tap_inner = (glds_variant() & 8) ? 1 : 0;
-  const int bn = a.Ncol <= 64 ? 64 : 128;
+  // <= 32 columns (stage 2's entry-conv input gradient, 24 channels): 32-wide column tiles
+  // (EWVIT_CONV_BN32 = 0: the 64-wide ones)
+  static const int bn32 = [] {
+    const char *e = getenv("EWVIT_CONV_BN32");
+    return e ? atoi(e) : 1;
+  }();
+  const int bn = (bn32 && a.Ncol <= 32 && v != 3 && v != 4) ? 32 : a.Ncol <= 64 ? 64 : 128;
   const int ntn = (a.Ncol + bn - 1) / bn;
   // a <= 64-column dgrad over a big map (the MWT fusion conv's 56-channel input gradient,
-  // 2.4 M pixels): 256-row blocks, 535 -> 505 us; likewise stage 2's 48-channel 3x3 dgrad
-  // (1568 row tiles) 71 -> 65 us.  EWVIT_CONV_DG256 = the row-tile count above which (0: never)
+  // 2.4 M pixels): 256-row blocks, 535 -> 505 us.  Stage 2's 48-channel 3x3 dgrad (1568 row
+  // tiles) now runs faster on 8-wave 128-row blocks (96 -> 75 us, tools/dgrad_ab.sh), so the
+  // threshold is 4096.  EWVIT_CONV_DG256 = the row-tile count above which (0: never)
   static const int dg256 = [] {
     const char *e = getenv("EWVIT_CONV_DG256");
-    return e ? atoi(e) : 1024;
+    return e ? atoi(e) : 4096;
   }();
   if (DGRAD && v == 1 && bn == 64 && dg256 > 0 && (a.M + 127) / 128 * ntn > dg256) v = 3;
   const int BM = (v == 3 || v == 4) ? 256 : 128;
@@ -1401,6 +1422,10 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   }();
   // (64-row tiles would change the BatchNorm partial rows fwd_bn_rows promised: not with bn_part)
   if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part)) && nwg <= sgmax) vv = sg;
+  if (bn == 32) {
+    EWVIT_GLDS_FWD(128, 32, 2);
+    return true;
+  }
   if (vv == 9) {
     const int64_t mt64 = (a.M + 63) / 64;
     const int nt9 = (int)(mt64 * ntn);

@@ -59,6 +59,8 @@ def rel(a, b):
     (2, 192, 192, 48, 14, 14, 1, 1),     # dgrad K = 48: one ragged K-tile
     (2, 48, 48, 192, 15, 14, 1, 3),      # 3x3 fwd Cin 48: ragged K-tile in every tap
     (1, 16, 16, 64, 20, 19, 1, 3),       # Cin 16 (the MWT seperate conv's input)
+    (2, 24, 24, 96, 24, 24, 2, 3),       # stage-2 entry: parity-class dgrad into 24 channels (32-wide tiles)
+    (1, 32, 32, 64, 18, 18, 2, 3),       # dgrad into exactly 32 channels
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec

@@ -94,4 +94,5 @@ def test_fused_loss_grad_scale_and_graph():
     w.fill_(1.0)
     graph.replay()
     torch.cuda.synchronize()
-    np.testing.assert_allclose(float(lv), float(parts[0]) + float(parts[1]), rtol=1e-6)
+    np.testing.assert_allclose(float(lv), float(parts['cls_loss']) + float(parts['orth_loss']), rtol=1e-6)
+    assert float(parts['orth_loss']) > 0

@@ -18,6 +18,8 @@ SHAPES = {
     'mwt_multiscale': (64, 128, 112, 112, 128, 3, 1, 3),
     'mwt_freq_conv': (64, 128, 112, 112, 128, 3, 2, 1),
     'bb_s2_fused': (64, 48, 56, 56, 192, 3, 1, 1),
+    'bb_s2_entry': (64, 24, 112, 112, 96, 3, 2, 1),
+    'bb_s3_entry': (64, 48, 56, 56, 192, 3, 2, 1),
     'bb_s4_expand': (64, 128, 28, 28, 512, 1, 1, 1),
     'bb_s5_expand': (64, 160, 14, 14, 960, 1, 1, 1),
     'bb_s5_project': (64, 960, 14, 14, 160, 1, 1, 1),
