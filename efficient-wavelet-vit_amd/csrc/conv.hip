@@ -1236,6 +1236,138 @@ static unsigned capped_mtiles(int64_t M, int ntn) {
   return (unsigned)gx;
 }
 
+// ---------------------------------------------------------------- small-channel 3x3
+// 3x3 stride-1 convs over few channels (KC = 16 / 24 per tap, <= 64 outputs): stage 1 of the
+// backbone (24 -> 24 at 112^2, forward and input gradient) and the MWT seperate conv
+// (16 -> 64).  A GEMM tile of 128 pixels re-gathers its 9 taps from L2 per K-tile; here a
+// workgroup stages the input rows its TH output rows need ONCE in LDS ([TH+2][W+2][KC] bf16,
+// zero halo — no bounds tests in the loop), keeps the packed weights of all taps in
+// registers (they are the MFMA A operand: K = 9*KC padded to k-steps of 32, N = Ncol padded
+// to 16-wide tiles), and walks 16-pixel groups: per group, KSTEPS ds_read_b128 of the pixel
+// operand and NT*KSTEPS v_mfma_f32_16x16x32_bf16.  Operands weights-first, so a lane ends
+// with 4 consecutive output channels of one pixel (8-byte stores).  FLIP: the input gradient
+// (taps mirrored; weights packed [Cin][taps][Cout]).  Grid: (N * ceil(H/TH)) workgroups,
+// walked persistently when the launch is capped.
+template <int KC, int NT, bool FLIP>
+__global__ __launch_bounds__(256) void conv3x3_small_kernel(FwdArgs a, int TH, int nblk) {
+  constexpr int CC = KC / 8, NCH = 9 * CC, KSTEPS = (NCH + 3) / 4, K = 9 * KC;
+  extern __shared__ __attribute__((aligned(16))) unsigned char cs_smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = a.outH, W = a.outW, Wp = W + 2;
+  const int rowb = Wp * KC * 2;                  // bytes per staged row
+  // weights (MFMA A operand): lane -> output channel (lane & 15) of each 16-wide tile,
+  // k chunk 4*s + (lane >> 4)
+  cbf16x8 wf[NT][KSTEPS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      const int n = t * 16 + (lane & 15), kc = 4 * s + (lane >> 4);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (n < a.Ncol && kc < NCH) v = *reinterpret_cast<const uint4 *>(a.wp + (int64_t)n * K + kc * 8);
+      wf[t][s] = __builtin_bit_cast(cbf16x8, v);
+    }
+  float bias[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = t * 16 + 4 * (lane >> 4) + i;
+      bias[t][i] = (a.bias && n < a.Ncol) ? a.bias[n] : 0.f;
+    }
+  const int nbh = (H + TH - 1) / TH;
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int img = blk / nbh, r0 = (blk - img * nbh) * TH;
+    const int rows = H - r0 < TH ? H - r0 : TH;
+    // stage input rows r0-1 .. r0+TH, cols -1 .. W, 16 B (8 channels) per item
+    const int items = (TH + 2) * Wp * CC;
+    __syncthreads();                             // the previous tile's readers are done
+    for (int i = tid; i < items; i += 256) {
+      const int c8 = i % CC, px = i / CC;
+      const int tr = px / Wp, tc = px - tr * Wp;
+      const int ir = r0 - 1 + tr, ic = tc - 1;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if ((unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W)
+        v = *reinterpret_cast<const uint4 *>(a.src + (((int64_t)img * H + ir) * W + ic) * KC + c8 * 8);
+      *reinterpret_cast<uint4 *>(cs_smem + (size_t)tr * rowb + (tc * KC + c8 * 8) * 2) = v;
+    }
+    __syncthreads();
+    const int npx = rows * W, ngr = (npx + 15) / 16;
+    for (int gi = w; gi < ngr; gi += 4) {
+      const int q = gi * 16 + (lane & 15);
+      const int qq = q < npx ? q : npx - 1;
+      const int r = qq / W, c = qq - r * W;
+      cf32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = cf32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const int kc = 4 * s + (lane >> 4);
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (kc < NCH) {
+          const int tap = kc / CC, c8 = kc - tap * CC;
+          const int kh = tap / 3, kw = tap - kh * 3;
+          const int tr = FLIP ? r + 2 - kh : r + kh, tc = FLIP ? c + 2 - kw : c + kw;
+          v = *reinterpret_cast<const uint4 *>(cs_smem + (size_t)tr * rowb + (tc * KC + c8 * 8) * 2);
+        }
+        const cbf16x8 xf = __builtin_bit_cast(cbf16x8, v);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][s], xf, acc[t], 0, 0, 0);
+      }
+      if (q < npx) {
+        bf16_t *o = a.out + (((int64_t)img * H + r0 + r) * W + c) * a.Ncol;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int n = t * 16 + 4 * (lane >> 4);
+          if (n < a.Ncol) {
+            const uint32_t lo = (uint32_t)f2bf(acc[t][0] + bias[t][0]) | ((uint32_t)f2bf(acc[t][1] + bias[t][1]) << 16);
+            const uint32_t hi = (uint32_t)f2bf(acc[t][2] + bias[t][2]) | ((uint32_t)f2bf(acc[t][3] + bias[t][3]) << 16);
+            *reinterpret_cast<uint2 *>(o + n) = make_uint2(lo, hi);
+          }
+        }
+      }
+    }
+  }
+}
+
+// EWVIT_CONV_SMALL = 0: those convs take the GEMM-tiled kernels
+static bool launch_small(const FwdArgs &a, bool dgrad, hipStream_t s) {
+  static const int on = [] {
+    const char *e = getenv("EWVIT_CONV_SMALL");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || a.g.ks != 3 || a.g.stride != 1 || a.sgs != 0 || a.ogs != 0 || a.sgc != a.KC || a.ogc != a.Ncol ||
+      a.KCr || a.addend || a.bn_part || a.pc >= 0 || a.outH != a.srcH || a.outW != a.srcW || a.outW > 256 ||
+      a.Ncol % 8)
+    return false;
+  const int KC = a.KC, NT = (a.Ncol + 15) / 16;
+  if (!((KC == 24 && NT <= 2) || (KC == 16 && NT <= 4))) return false;
+  const int H = a.outH, W = a.outW;
+  int TH = 4;                                     // rows per workgroup: LDS <= 40 KB
+  while (TH > 1 && (TH + 2) * (W + 2) * KC * 2 > 40 * 1024) --TH;
+  const size_t lds = (size_t)(TH + 2) * (W + 2) * KC * 2;
+  const int64_t nblk64 = (int64_t)a.g.N * ((H + TH - 1) / TH);
+  if (nblk64 >= (1ll << 31)) return false;
+  const int nblk = (int)nblk64;
+  const dim3 grid((unsigned)(g_grid_cap > 0 && nblk > g_grid_cap ? g_grid_cap : nblk));
+#define EWVIT_SMALL(KC_, NT_)                                                                                     \
+  do {                                                                                                          \
+    if (dgrad)                                                                                                  \
+      hipLaunchKernelGGL((conv3x3_small_kernel<KC_, NT_, true>), grid, dim3(256), lds, s, a, TH, nblk);        \
+    else                                                                                                        \
+      hipLaunchKernelGGL((conv3x3_small_kernel<KC_, NT_, false>), grid, dim3(256), lds, s, a, TH, nblk);       \
+  } while (0)
+  if (KC == 24) {
+    if (NT == 1) EWVIT_SMALL(24, 1);
+    else EWVIT_SMALL(24, 2);
+  } else {
+    if (NT <= 2) EWVIT_SMALL(16, 2);
+    else EWVIT_SMALL(16, 4);
+  }
+#undef EWVIT_SMALL
+  return true;
+}
+
 template <bool DGRAD, int KS, int BK, int PF>
 static void launch_fwd_v(const FwdArgs &a, hipStream_t s) {
   if (a.Ncol <= 64) {
@@ -1625,7 +1757,7 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
     // the weights were packed with cp input channels (ewvit_conv2d_fwd_pack_cin)
     a.KC = (int)cp; a.KCr = (int)Cin;
     EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd: padded LDS-DMA kernel refused");
-  } else if (!launch_glds<false>(a, xb, as_stream(stream))) {
+  } else if (!launch_small(a, false, as_stream(stream)) && !launch_glds<false>(a, xb, as_stream(stream))) {
     launch_fwd<false>(a, as_stream(stream));
   }
   return launch_status("conv2d_fwd");
@@ -1722,7 +1854,8 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
   a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
   const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
-  if (!dgrad_by_parity(a, sb, as_stream(stream)) && !launch_glds<true>(a, sb, as_stream(stream)))
+  if (!launch_small(a, true, as_stream(stream)) && !dgrad_by_parity(a, sb, as_stream(stream)) &&
+      !launch_glds<true>(a, sb, as_stream(stream)))
     launch_fwd<true>(a, as_stream(stream));
   return launch_status("conv2d_bwd_data");
 }

@@ -61,6 +61,10 @@ def rel(a, b):
     (1, 16, 16, 64, 20, 19, 1, 3),       # Cin 16 (the MWT seperate conv's input)
     (2, 24, 24, 96, 24, 24, 2, 3),       # stage-2 entry: parity-class dgrad into 24 channels (32-wide tiles)
     (1, 32, 32, 64, 18, 18, 2, 3),       # dgrad into exactly 32 channels
+    (2, 24, 24, 24, 21, 19, 1, 3),       # stage 1 (24 -> 24): small-channel direct conv fwd + dgrad
+    (1, 24, 24, 24, 112, 112, 1, 3),     # the same at 112^2 (TH-row bands, full-width LDS tiles)
+    (2, 16, 16, 16, 9, 13, 1, 3),        # Cin / Cout 16: both directions on the small-channel kernel
+    (1, 24, 24, 8, 7, 5, 1, 3),          # one 16-wide output tile, rows < the band height
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec
