@@ -1343,8 +1343,20 @@ static bool launch_small(const FwdArgs &a, bool dgrad, hipStream_t s) {
   const int KC = a.KC, NT = (a.Ncol + 15) / 16;
   if (!((KC == 24 && NT <= 2) || (KC == 16 && NT <= 4))) return false;
   const int H = a.outH, W = a.outW;
-  int TH = 4;                                     // rows per workgroup: LDS <= 40 KB
-  while (TH > 1 && (TH + 2) * (W + 2) * KC * 2 > 40 * 1024) --TH;
+  // rows per workgroup (at most; EWVIT_CONV_SMALL_TH overrides), LDS <= EWVIT_CONV_SMALL_LDS KB:
+  // 4 rows for 24 channels (stage 1: 29 us; 2 / 6 / 8 rows 34 / 31 / 33 us), 8 for 16 (the
+  // seperate conv: 119 us; 4 / 6 / 12 rows 129 / 123 / 133 us), tools/small_ab.sh
+  static const int thenv = [] {
+    const char *e = getenv("EWVIT_CONV_SMALL_TH");
+    return e ? atoi(e) : 0;
+  }();
+  static const int ldsmax = [] {
+    const char *e = getenv("EWVIT_CONV_SMALL_LDS");
+    return (e ? atoi(e) : 64) * 1024;
+  }();
+  const int thmax = thenv > 0 ? thenv : (KC == 16 ? 8 : 4);
+  int TH = thmax;
+  while (TH > 1 && (TH + 2) * (W + 2) * KC * 2 > ldsmax) --TH;
   const size_t lds = (size_t)(TH + 2) * (W + 2) * KC * 2;
   const int64_t nblk64 = (int64_t)a.g.N * ((H + TH - 1) / TH);
   if (nblk64 >= (1ll << 31)) return false;
