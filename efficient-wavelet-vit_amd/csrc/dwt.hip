@@ -306,11 +306,11 @@ __device__ __forceinline__ float2 load2(const void *x, int64_t i) {
   return make_float2(__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u));
 }
 
-template <int XDT, int ODT, int L, int OWMAX>
-__global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restrict__ x, void *__restrict__ out,
+template <int XDT, int ODT, int L, int OWMAX, int NT, int ROWS = DWTF_ROWS>
+__global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict__ x, void *__restrict__ out,
                                                            int N, int H, int W, int ocs) {
   constexpr int HALO = L > 1 ? (1 << (L - 1)) : 0;      // level-1 rows
-  constexpr int R1 = DWTF_ROWS + 2 * HALO;              // level-1 window rows
+  constexpr int R1 = ROWS + 2 * HALO;              // level-1 window rows
   constexpr int R2 = L >= 2 ? R1 / 2 : 1, R3 = L >= 3 ? R1 / 4 : 1;
   constexpr int O2 = OWMAX / 2, O3 = OWMAX / 4;
   __shared__ float ll1[L >= 2 ? R1 * OWMAX * 3 : 1];
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
   __shared__ float b3[L >= 3 ? R3 * O3 * 9 : 1];
   const int tid = threadIdx.x, n = blockIdx.y;
   const int OH = H >> 1, OW = W >> 1;
-  const int y0 = blockIdx.x * DWTF_ROWS;                // first level-1 output row
+  const int y0 = blockIdx.x * ROWS;                // first level-1 output row
   const int ws1 = y0 - HALO;                            // window origin, level-1 rows
   const int64_t plane = (int64_t)H * W;
   const char *xn = reinterpret_cast<const char *>(x) + (int64_t)n * 3 * plane * (XDT == EWVIT_BF16 ? 2 : 4);
@@ -328,11 +328,11 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
   // ---- level 1 (registers): 4 pixels per thread in flight
   {
     const int items = R1 * OW;
-    for (int i0 = tid; i0 < items; i0 += 4 * 256) {
+    for (int i0 = tid; i0 < items; i0 += 4 * NT) {
       float2 r[4][3][2];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int it = i0 + k * 256;
+        const int it = i0 + k * NT;
         const int i = it / OW, j = it - i * OW, y = ws1 + i;
         if (it < items && y >= 0 && y < OH) {
 #pragma unroll
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int it = i0 + k * 256;
+        const int it = i0 + k * NT;
         const int i = it / OW, j = it - i * OW, y = ws1 + i;
         if (!(it < items && y >= 0 && y < OH)) continue;
         float v[9];
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
           v[3 * c] = B0; v[3 * c + 1] = B1; v[3 * c + 2] = B2;
           if (L >= 2) ll1[(i * OWMAX + j) * 3 + c] = LL;
         }
-        if (i >= HALO && i < HALO + DWTF_ROWS)
+        if (i >= HALO && i < HALO + ROWS)
           store_px9<ODT>(out, (((int64_t)n * OH + y) * OW + j) * ocs, v, ocs);
       }
     }
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
     __syncthreads();
     // ---- level 2 over LDS: window rows ws2 .. ws2 + R2
     const int OH2 = OH >> 1, OW2 = OW >> 1, ws2 = ws1 >> 1;
-    for (int it = tid; it < R2 * OW2; it += 256) {
+    for (int it = tid; it < R2 * OW2; it += NT) {
       const int i = it / OW2, j = it - i * OW2, y = ws2 + i;
       if (y < 0 || y >= OH2) continue;
       const float *p0 = ll1 + ((2 * i) * OWMAX + 2 * j) * 3, *p1 = p0 + OWMAX * 3;
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
     if constexpr (L >= 3) {
       __syncthreads();
       const int OH3 = OH2 >> 1, OW3 = OW2 >> 1, ws3 = ws2 >> 1;
-      for (int it = tid; it < R3 * OW3; it += 256) {
+      for (int it = tid; it < R3 * OW3; it += NT) {
         const int i = it / OW3, j = it - i * OW3, y = ws3 + i;
         if (y < 0 || y >= OH3) continue;
         const float *p0 = ll2 + ((2 * i) * O2 + 2 * j) * 3, *p1 = p0 + O2 * 3;
@@ -396,9 +396,9 @@ __global__ __launch_bounds__(256) void dwt_hf_fused_kernel(const void *__restric
     }
     __syncthreads();
     // ---- levels 2..L upsampled to the strip's level-1 rows
-    const int rows = OH - y0 < DWTF_ROWS ? OH - y0 : DWTF_ROWS;
+    const int rows = OH - y0 < ROWS ? OH - y0 : ROWS;
     const int items = rows * OW;
-    for (int it = tid; it < (L - 1) * items; it += 256) {
+    for (int it = tid; it < (L - 1) * items; it += NT) {
       const int l = 2 + it / items, r = it - (l - 2) * items;
       const int oy = y0 + r / OW, ox = r - (r / OW) * OW;
       const int hl = OH >> (l - 1), wl = OW >> (l - 1);
@@ -499,11 +499,38 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
                   "dwt_hf_upsample_fused: unsupported shape [%lld,%lld,%lld,%lld] levels=%d channels=%lld",
                   (long long)N, (long long)C, (long long)H, (long long)W, levels, (long long)out_channels);
   const int OH = (int)(H / 2);
-  dim3 grid((unsigned)((OH + DWTF_ROWS - 1) / DWTF_ROWS), (unsigned)N), block(256);
+  // threads per workgroup / level-1 rows per workgroup (EWVIT_DWTF_THREADS, EWVIT_DWTF_ROWS A/B):
+  // 512 threads over 16-row strips (29.9 -> 26.5 us at config 2 against 256 threads; 1024: 29.7)
+  static const int nt = [] {
+    const char *e = getenv("EWVIT_DWTF_THREADS");
+    const int v = e ? atoi(e) : 512;
+    return v == 256 || v == 1024 ? v : 512;
+  }();
+  static const int rows = [] {
+    const char *e = getenv("EWVIT_DWTF_ROWS");
+    const int v = e ? atoi(e) : 16;
+    return v == 8 || v == 32 ? v : 16;
+  }();
+  dim3 grid((unsigned)((OH + rows - 1) / rows), (unsigned)N), block(nt);
   hipStream_t s = as_stream(stream);
-#define DWTF_L(XD, OD, LV)                                                                                \
-  hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112>), grid, block, 0, s, x, out, (int)N, (int)H, (int)W, \
-                     (int)out_channels)
+#define DWTF_R(XD, OD, LV, NT_)                                                                                 \
+  do {                                                                                                        \
+    if (rows == 8)                                                                                            \
+      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 8>), grid, block, 0, s, x, out, (int)N, (int)H, \
+                         (int)W, (int)out_channels);                                                          \
+    else if (rows == 32)                                                                                      \
+      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 32>), grid, block, 0, s, x, out, (int)N,     \
+                         (int)H, (int)W, (int)out_channels);                                                  \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 16>), grid, block, 0, s, x, out, (int)N,     \
+                         (int)H, (int)W, (int)out_channels);                                                  \
+  } while (0)
+#define DWTF_L(XD, OD, LV)                \
+  do {                                    \
+    if (nt == 1024) DWTF_R(XD, OD, LV, 1024); \
+    else if (nt == 256) DWTF_R(XD, OD, LV, 256); \
+    else DWTF_R(XD, OD, LV, 512);         \
+  } while (0)
 #define DWTF_D(XD, OD)                        \
   do {                                        \
     if (levels == 1) DWTF_L(XD, OD, 1);       \
@@ -516,5 +543,6 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
   else DWTF_D(EWVIT_BF16, EWVIT_F32);
 #undef DWTF_D
 #undef DWTF_L
+#undef DWTF_R
   return launch_status("dwt_hf_upsample_fused");
 }
