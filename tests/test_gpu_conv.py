@@ -65,6 +65,8 @@ def rel(a, b):
     (1, 24, 24, 24, 112, 112, 1, 3),     # the same at 112^2 (TH-row bands, full-width LDS tiles)
     (2, 16, 16, 16, 9, 13, 1, 3),        # Cin / Cout 16: both directions on the small-channel kernel
     (1, 24, 24, 8, 7, 5, 1, 3),          # one 16-wide output tile, rows < the band height
+    (2, 16, 16, 64, 10, 16, 1, 3),       # small-channel wgrad (W % 8 == 0): 16 -> 64 with bias
+    (3, 24, 24, 24, 7, 24, 1, 3),        # small-channel wgrad, odd H (a 1-row tail band)
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec

@@ -18,6 +18,11 @@ SHAPES = {
     'mwt_multiscale': (64, 128, 112, 112, 128, 3, 1, 3),
     'mwt_freq_conv': (64, 128, 112, 112, 128, 3, 2, 1),
     'bb_s2_fused': (64, 48, 56, 56, 192, 3, 1, 1),
+    'bb_s1_fused': (64, 24, 112, 112, 24, 3, 1, 1),
+    'mwt_seperate': (192, 16, 112, 112, 64, 3, 1, 1),
+    'bb_s2_project': (64, 192, 56, 56, 48, 1, 1, 1),
+    'bb_s3_fused': (64, 64, 28, 28, 256, 3, 1, 1),
+    'bb_s3_project': (64, 256, 28, 28, 64, 1, 1, 1),
     'bb_s2_entry': (64, 24, 112, 112, 96, 3, 2, 1),
     'bb_s3_entry': (64, 48, 56, 56, 192, 3, 2, 1),
     'bb_s4_expand': (64, 128, 28, 28, 512, 1, 1, 1),
