@@ -25,7 +25,7 @@ namespace ewvit {
 
 constexpr int FR_KMAX = 17;            // taps per output sample: 2 * ceil(support) + 1, scale <= 8
 constexpr int FR_SMAX = 256;           // output size S (CenterCrop) at most
-constexpr int FR_LDS = 64 * 1024;      // dynamic LDS per workgroup (2 workgroups per CU)
+constexpr int FR_LDS_CAP = 160 * 1024; // the most dynamic LDS one workgroup may be given (gfx950)
 constexpr int FR_PREC = 22;            // Pillow PRECISION_BITS for 8-bpc images
 constexpr int FR_GEOM = 10;            // int64 per frame (include/ewvit.h)
 
@@ -280,6 +280,16 @@ static int fr_band_rows(int h, int nh, int oy, int S, int rb) {
   return worst;
 }
 
+// dynamic LDS budget per workgroup (EWVIT_FRAMES_LDS, KB)
+static int fr_lds_max() {
+  static const int v = [] {
+    const char *e = getenv("EWVIT_FRAMES_LDS");
+    const int kb = e ? atoi(e) : 64;
+    return (kb < 16 ? 16 : kb > 160 ? 160 : kb) * 1024;
+  }();
+  return v;
+}
+
 static FrNorm fr_norm(const float *mean_std) {
   FrNorm nm;
   for (int c = 0; c < 3; ++c) { nm.mean[c] = mean_std[c]; nm.inv[c] = mean_std[3 + c]; }
@@ -329,10 +339,18 @@ extern "C" int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t 
     return r;
   };
   // staged source rows at the tallest band that fits, else bands read the source from global
+  // the tallest band (<= EWVIT_FRAMES_RB, default 4) whose LDS fits: 64-frame 720p clip with face
+  // boxes, 2 / 4 / 8 / 16-row bands 38.5 / 31.7 / 32.6 / 44.4 us (tools/frames_lds_ab.sh: the
+  // column-per-thread horizontal pass walks the band's source rows serially)
+  static const int rbmax = [] {
+    const char *e = getenv("EWVIT_FRAMES_RB");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
+  }();
   for (int staged = 1; staged >= 0; --staged)
-    for (int rb = 16; rb >= 1; rb >>= 1) {
+    for (int rb = rbmax; rb >= 1; rb >>= 1) {
       const FrPlan pl{rb, kmax, rmax_of(rb), staged ? words : 0};
-      if (fr_lds_bytes(S, pl) <= FR_LDS) {
+      if (fr_lds_bytes(S, pl) <= fr_lds_max()) {
         plan[0] = pl.rb; plan[1] = pl.kmax; plan[2] = pl.rmax; plan[3] = pl.pitch;
         return 0;
       }
@@ -346,7 +364,7 @@ extern "C" int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *ge
   EWVIT_CHECK_ARG(frames && geom && out && plan && n > 0, "frames_resize_crop: null pointer or empty batch");
   const FrPlan pl{plan[0], plan[1], plan[2], plan[3]};
   EWVIT_CHECK_ARG(S > 0 && S <= FR_SMAX && pl.rb >= 1 && pl.rb <= 64 && pl.kmax >= 1 && pl.kmax <= FR_KMAX &&
-                      pl.rmax >= 1 && pl.pitch >= 0 && fr_lds_bytes(S, pl) <= FR_LDS,
+                      pl.rmax >= 1 && pl.pitch >= 0 && fr_lds_bytes(S, pl) <= FR_LDS_CAP,
                   "frames_resize_crop: S %d / plan (%d, %d, %d, %d) out of range (use ewvit_frames_plan)", S, pl.rb,
                   pl.kmax, pl.rmax, pl.pitch);
   EWVIT_CHECK_ARG(!to_f32 || mean_std, "frames_resize_crop: normalised output needs mean_std");
@@ -358,6 +376,13 @@ extern "C" int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *ge
   hipStream_t st = as_stream(stream);
 #define EWVIT_FR_LAUNCH(KT_)                                                                                        \
   do {                                                                                                            \
+    static const bool attr = [] {      /* more than 64 KB of dynamic LDS needs the attribute */                  \
+      return hipFuncSetAttribute(reinterpret_cast<const void *>(frames_resize_crop_kernel<KT_, true>),            \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_CAP) == hipSuccess &&         \
+             hipFuncSetAttribute(reinterpret_cast<const void *>(frames_resize_crop_kernel<KT_, false>),           \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_CAP) == hipSuccess;           \
+    }();                                                                                                          \
+    (void)attr;                                                                                                   \
     if (to_f32)                                                                                                   \
       hipLaunchKernelGGL((frames_resize_crop_kernel<KT_, true>), grid, dim3(256), lds, st, frames, geom, S, pl, nm, out); \
     else                                                                                                          \

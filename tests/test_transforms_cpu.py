@@ -117,7 +117,7 @@ def test_planner_validates_on_the_host():
         return rc, list(out)
 
     rc, p = plan([np.zeros((480, 640, 3), np.uint8)])
-    assert rc == 0 and p[0] == 16 and p[1] == 5 and p[3] > 0           # staged; 480 -> 450: support 2
+    assert rc == 0 and p[0] == 4 and p[1] == 5 and p[3] > 0            # staged; 480 -> 450: support 2
     rc, p = plan([np.zeros((1080, 1920, 3), np.uint8), np.zeros((2000, 3000, 3), np.uint8)])
     assert rc == 0 and 1 <= p[0] < 16 and p[1] == 2 * 5 + 1             # 4.4x down: 11 taps
     rc, _ = plan([np.zeros((480, 640, 3), np.uint8)], nbytes=1000)
