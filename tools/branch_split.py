@@ -9,7 +9,7 @@ import re
 import sys
 
 TOKEN = re.compile(r'gemm_kernel|splitk_reduce|attn_|ln_fwd|ln_bwd|act_bwd|colsum|softmax|dropout|amax|'
-                   r'log_sigmoid|sigmoid_kernel|neg_kernel|CatArray|at::native::reduce_kernel')
+                   r'log_sigmoid|sigmoid_kernel|neg_kernel|CatArray|at::native::reduce_kernel|combined_loss')
 CONV_BB = re.compile(r'bn_|conv_|dw_|se_|stem_|scale_add|drop_add|pool')
 
 
