@@ -1490,9 +1490,16 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     launch_glds_dense(a, src_bytes, s);
     return true;
   }
-  // (a parity-class dgrad, which already skips 3/4 of the taps, up to 1/3)
-  if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 ||
-                 (a.pc >= 0 ? 2 * ((a.KC + 63) / 64 * 64) > 3 * a.KC : 5 * ((a.KC + 63) / 64 * 64) > 6 * a.KC)))
+  // (a parity-class dgrad, which already skips 3/4 of the taps, up to 1/3; EWVIT_CONV_RAGGED_1X1 = 1:
+  // a 1x1 input gradient with up to 1/3 zero lanes too — stage 2's projects, K = 48)
+  static const int r1x1 = [] {
+    const char *e = getenv("EWVIT_CONV_RAGGED_1X1");
+    return e ? atoi(e) : 0;
+  }();
+  const int kpad = (a.KC + 63) / 64 * 64;
+  const bool ragged_ok = a.pc >= 0 ? 2 * kpad <= 3 * a.KC
+                                   : (5 * kpad <= 6 * a.KC || (r1x1 && DGRAD && a.g.ks == 1 && 2 * kpad <= 3 * a.KC));
+  if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 || !ragged_ok))
     return false;
   if (!use_glds() || (!ragged && a.KC % 64) || (padded ? a.sgc != a.KCr : (!ragged && a.sgc % 64)) ||
       src_bytes >= (int64_t)OOB ||

@@ -21,6 +21,7 @@ SHAPES = {
     'bb_s1_fused': (64, 24, 112, 112, 24, 3, 1, 1),
     'mwt_seperate': (192, 16, 112, 112, 64, 3, 1, 1),
     'bb_s2_project': (64, 192, 56, 56, 48, 1, 1, 1),
+    'bb_s2e_project': (64, 96, 56, 56, 48, 1, 1, 1),
     'bb_s3_fused': (64, 64, 28, 28, 256, 3, 1, 1),
     'bb_s3_project': (64, 256, 28, 28, 64, 1, 1, 1),
     'bb_s2_entry': (64, 24, 112, 112, 96, 3, 2, 1),
