@@ -38,21 +38,14 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
   p = p + neg_step_size * (m / denom);
 }
 
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr_host, const double *lr_dev, double b1,
-                                                         double b2, float eps, float wd) {
-  // tensor of this workgroup: scalar search over the prefix sums (uniform)
-  const int blk = blockIdx.x;
-  int t = 0;
-  while (t + 1 < a.n && a.chunk0[t + 1] <= blk) ++t;
-  const int64_t base = (int64_t)(blk - a.chunk0[t]) * ADAM_CHUNK;
-  const int64_t n = a.numel[t];
-  float *__restrict__ P = a.p[t];
-  const float *__restrict__ G = a.g[t];
-  float *__restrict__ M = a.m[t];
-  float *__restrict__ V = a.v[t];
+// one 4096-element chunk of one tensor (both launch forms)
+__device__ __forceinline__ void adam_chunk(float *__restrict__ P, const float *__restrict__ G, float *__restrict__ M,
+                                          float *__restrict__ V, int64_t n, int64_t base, const float *step_ptr,
+                                          double lr_host, const double *lr_dev, double b1, double b2, float eps,
+                                          float wd) {
   // bias corrections in double, as torch computes them on the host (1 - 0.999^t cancels
   // badly in f32), then rounded once to the f32 scalars the element update uses
-  const double st = (double)*a.step[t];
+  const double st = (double)*step_ptr;
   // the learning rate from device memory when given (a replayed graph follows the caller's
   // LR schedule, train.py:274,300), else the launch-time constant
   const double lr = lr_dev ? *lr_dev : lr_host;
@@ -93,6 +86,35 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr_h
   }
 }
 
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamArgs a, double lr_host, const double *lr_dev, double b1,
+                                                         double b2, float eps, float wd) {
+  // tensor of this workgroup: scalar search over the prefix sums (uniform)
+  const int blk = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.n && a.chunk0[t + 1] <= blk) ++t;
+  adam_chunk(a.p[t], a.g[t], a.m[t], a.v[t], a.numel[t], (int64_t)(blk - a.chunk0[t]) * ADAM_CHUNK, a.step[t],
+             lr_host, lr_dev, b1, b2, eps, wd);
+}
+
+// every tensor of a parameter group in ONE launch: a device table of entries {p, g, m, v,
+// step, numel, first chunk} (int64 words, EWVIT_ADAM_ENTRY of them per tensor); a workgroup
+// finds its tensor by binary search over the first-chunk column (read-only table)
+__global__ __launch_bounds__(256) void adam_table_kernel(const int64_t *__restrict__ tab, int n, double lr_host,
+                                                         const double *lr_dev, double b1, double b2, float eps,
+                                                         float wd) {
+  const int64_t blk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[(int64_t)mid * EWVIT_ADAM_ENTRY + 6] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const int64_t *e = tab + (int64_t)lo * EWVIT_ADAM_ENTRY;
+  adam_chunk(reinterpret_cast<float *>(e[0]), reinterpret_cast<const float *>(e[1]), reinterpret_cast<float *>(e[2]),
+             reinterpret_cast<float *>(e[3]), e[5], (blk - e[6]) * ADAM_CHUNK, reinterpret_cast<const float *>(e[4]),
+             lr_host, lr_dev, b1, b2, eps, wd);
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -122,4 +144,14 @@ extern "C" int ewvit_adam_step(int n, float *const *params, const float *const *
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)chunks), dim3(256), 0, as_stream(stream), a, lr, lr_dev, beta1, beta2, eps,
                      weight_decay);
   return launch_status("adam_step");
+}
+
+extern "C" int64_t ewvit_adam_chunks(int64_t numel) { return (numel + ADAM_CHUNK - 1) / ADAM_CHUNK; }
+
+extern "C" int ewvit_adam_step_table(const int64_t *table, int n, int64_t nchunks, double lr, const double *lr_dev,
+                                     double beta1, double beta2, float eps, float weight_decay, void *stream) {
+  EWVIT_CHECK_ARG(table && n > 0 && nchunks > 0 && nchunks < ((int64_t)1 << 31), "adam_step_table: bad table");
+  hipLaunchKernelGGL(adam_table_kernel, dim3((unsigned)nchunks), dim3(256), 0, as_stream(stream), table, n, lr, lr_dev,
+                     beta1, beta2, eps, weight_decay);
+  return launch_status("adam_step_table");
 }

@@ -18,6 +18,7 @@ F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
 PACK_MAX = 32          # EWVIT_PACK_MAX
 AMAX_PARTS = 256       # EWVIT_AMAX_PARTS
+ADAM_ENTRY = 7         # EWVIT_ADAM_ENTRY
 
 _i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 _f64 = ctypes.c_double
@@ -87,6 +88,7 @@ SIGNATURES = {
     'ewvit_frames_resize_crop': [_vp, _vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp],
     'ewvit_frames_jitter_normalize': [_vp, _vp, _i64, _i32, _vp, _vp, _vp],
     'ewvit_combined_loss': [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
 }
 
 # size queries: name -> (restype, argtypes)
@@ -104,6 +106,7 @@ QUERIES = {
     'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64, _vp]),
+    'ewvit_adam_chunks': (_i64, [_i64]),
 }
 
 _lib = None

@@ -3,9 +3,11 @@ reference's training step (train.py:273-275: ``optim.Adam(params, lr, weight_dec
 
 Same constructor, update rule and state layout as ``torch.optim.Adam`` (per-parameter
 state ``step`` / ``exp_avg`` / ``exp_avg_sq``, so checkpoints load either way), for
-amsgrad=False / maximize=False.  ``step()`` issues one launch per 48 tensors with the
-pointers passed by value — graph-capturable although autograd allocates fresh gradients
-every eager step — plus one foreach increment of the per-parameter device step counters.
+amsgrad=False / maximize=False.  ``step()`` issues ONE launch per parameter group from a
+device table of the tensors' addresses (rebuilt when they change, outside graph capture), or
+— when the addresses changed while a graph is being captured, or with EWVIT_ADAM_TABLE=0 —
+one launch per 48 tensors with the pointers passed by value; plus one foreach increment of
+the per-parameter device step counters.
 
 The learning rate is read by the kernel from a per-group device scalar (``self._lr_dev``),
 written from ``group['lr']`` by ``sync_hyper()`` — called by every eager ``step()`` and, for
@@ -39,6 +41,8 @@ class Adam(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or not 0 <= betas[0] < 1 or not 0 <= betas[1] < 1 or weight_decay < 0:
             raise ValueError('ewvit.optim.Adam: invalid hyper-parameters')
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        import os
+        self.table = os.environ.get('EWVIT_ADAM_TABLE', '1') != '0'   # one launch per group
 
     def sync_hyper(self):
         """Write each group's current lr into its device scalar (outside any graph capture)."""
@@ -90,6 +94,8 @@ class Adam(torch.optim.Optimizer):
             self.sync_hyper()
         lr_dev = L.ptr(self._lr_dev[id(group)][0])
         stream = L.stream(items[0][0])
+        if self._table_step(group, items, lr_dev, stream):
+            return
         for k in range(0, len(items), L.ADAM_MAX):
             chunk = items[k:k + L.ADAM_MAX]
             n = len(chunk)
@@ -100,6 +106,34 @@ class Adam(torch.optim.Optimizer):
             L.call('ewvit_adam_step', n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, ptrs[4],
                    float(group['lr']), lr_dev, float(b1), float(b2), float(group['eps']),
                    float(group['weight_decay']), stream, work={'bytes': 28.0 * sum(c[0].numel() for c in chunk)})
+
+    def _table_step(self, group, items, lr_dev, stream):
+        """The whole group in one launch (ewvit_adam_step_table) from a device table of its
+        tensors' addresses, built when they change — never while a graph is being captured
+        (a changed layout then takes the launches above).  EWVIT_ADAM_TABLE=0: off."""
+        if not self.table:
+            return False
+        key = tuple((c[0].data_ptr(), c[1].data_ptr(), c[2]['exp_avg'].data_ptr(), c[2]['exp_avg_sq'].data_ptr(),
+                     c[2]['step'].data_ptr(), c[0].numel()) for c in items)
+        if not hasattr(self, '_tables'):
+            self._tables = {}
+        cached = self._tables.get(id(group))
+        if cached is None or cached[0] != key:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            lib, rows, chunk0 = L.load(), [], 0
+            for k in key:
+                rows.append(list(k) + [chunk0])
+                chunk0 += int(lib.ewvit_adam_chunks(k[5]))
+            tab = torch.tensor(rows, dtype=torch.int64).to(items[0][0].device)
+            cached = self._tables[id(group)] = (key, tab, chunk0)
+            # a step captured earlier may still replay the previous table: keep every table
+            self.__dict__.setdefault('_table_keep', []).append(tab)
+        b1, b2 = group['betas']
+        L.call('ewvit_adam_step_table', L.ptr(cached[1]), len(key), cached[2], float(group['lr']), lr_dev, float(b1),
+               float(b2), float(group['eps']), float(group['weight_decay']), stream,
+               work={'bytes': 28.0 * sum(k[5] for k in key)})
+        return True
 
     @torch.no_grad()
     def step(self, closure=None):

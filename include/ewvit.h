@@ -463,6 +463,15 @@ int ewvit_maxpool2_bwd(const void *dy, const uint8_t *argmax, void *dx, int dtyp
 int ewvit_adam_step(int n, float *const *params, const float *const *grads, float *const *exp_avg,
                     float *const *exp_avg_sq, const int64_t *numel, const float *const *steps, double lr,
                     const double *lr_dev, double beta1, double beta2, float eps, float weight_decay, void *stream);
+/* The same update for any number of tensors in ONE launch: `table` is a DEVICE array of n
+ * entries of EWVIT_ADAM_ENTRY int64 words {p, g, m, v, step (pointers), numel, first chunk},
+ * first chunks ascending from 0 with ewvit_adam_chunks(numel) chunks per tensor, nchunks the
+ * total.  A caller whose tensors keep their addresses builds the table once (a replayed HIP
+ * graph then runs the whole group as one kernel). */
+#define EWVIT_ADAM_ENTRY 7
+int64_t ewvit_adam_chunks(int64_t numel);
+int ewvit_adam_step_table(const int64_t *table, int n, int64_t nchunks, double lr, const double *lr_dev, double beta1,
+                          double beta2, float eps, float weight_decay, void *stream);
 
 /* ------------------------------------------------------ loss ---
  * combined_loss of train.py:69-91 with orthogonal_loss of train.py:55-67, forward and all input
