@@ -198,7 +198,8 @@ def pmc_traffic(entry, per_step, config=2, adam_per_step=None):
     bench config (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE), or None.  The profiled bench
     run also executes the eager timing passes and the DWT loop, so the number of step
     equivalents it ran is counted from the Adam launches it made (Adam runs once per step in
-    every pass; `adam_per_step` multi-tensor launches each), not from the command line."""
+    every pass; `adam_per_step` maps each Adam kernel name to its launches per step, so a
+    PMC file from either launch form counts right), not from the command line."""
     path = pmc_file(config)
     if not os.path.exists(path) or entry not in ENTRY_KERNELS:
         return None
@@ -211,8 +212,12 @@ def pmc_traffic(entry, per_step, config=2, adam_per_step=None):
     tot = sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in ks)
     if entry in PER_DISPATCH:
         return round(tot / sum(v['dispatches'] for v in ks), 1)
-    adam = [v['dispatches'] for k, v in data.items() if 'adam_multi_kernel' in k]
-    steps = adam[0] / adam_per_step if adam and adam_per_step else data.get('_steps_executed')
+    steps = data.get('_steps_executed')
+    for kname, per in (adam_per_step or {}).items():      # {kernel name: launches per step}
+        adam = [v['dispatches'] for k, v in data.items() if kname in k]
+        if adam and per:
+            steps = adam[0] / per
+            break
     if not steps or not per_step:
         return None
     return round(tot / (per_step * steps), 1)
@@ -398,7 +403,8 @@ def main():
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
-        aps = table.get('ewvit_adam_step', {}).get('per_step')
+        opt = getattr(step, 'opt', None)
+        aps = opt.launches_per_step() if hasattr(opt, 'launches_per_step') else None
         res['roofline'] = roofline_for(*dom, config=args.config, adam_per_step=aps) if dom else None
         if res['roofline'] is not None:
             res['roofline']['timing'] = ('HIP events around every launch of an eager pass of the step as it runs '

@@ -135,6 +135,13 @@ class Adam(torch.optim.Optimizer):
                work={'bytes': 28.0 * sum(k[5] for k in key)})
         return True
 
+    def launches_per_step(self):
+        """Adam kernel launches one step makes, by kernel name, in either launch form (the
+        profilers count step equivalents from them, whichever form the profiled build took)."""
+        groups = [sum(1 for p in g['params'] if p.requires_grad) for g in self.param_groups]
+        return {'adam_table_kernel': sum(1 for n in groups if n),
+                'adam_multi_kernel': sum(-(-n // L.ADAM_MAX) for n in groups)}
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

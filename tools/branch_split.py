@@ -2,7 +2,7 @@
 (`bench.py --eager`: the MWT runs on its own HIP stream, so the trace's Stream_Id separates
 it; graph replay shows one queue).  Branches: MWT (side stream), backbone and token path
 (main stream, told apart by kernel family), optimizer.  Step = the kernels between two
-groups of Adam launches.  Usage: python tools/branch_split.py <run_kernel_trace.csv> [adam_per_step]"""
+groups of Adam launches.  Usage: python tools/branch_split.py <run_kernel_trace.csv> [multi_adam_launches_per_step]"""
 import collections
 import csv
 import re
@@ -21,9 +21,12 @@ def branch_of(name):
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    aps = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    adam = [i for i, r in enumerate(rows) if 'adam_multi' in r['Kernel_Name']]
+    adam = [i for i, r in enumerate(rows) if 'adam_table' in r['Kernel_Name']]
+    aps = 1                                  # the single-launch Adam: one launch per step
+    if not adam:                             # the per-48-tensor launches
+        adam = [i for i, r in enumerate(rows) if 'adam_multi' in r['Kernel_Name']]
+        aps = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     ends = [adam[i] for i in range(aps - 1, len(adam), aps)]
     main_stream = collections.Counter(r['Stream_Id'] for r in rows).most_common(1)[0][0]
     # the last complete step that ran the MWT on its side stream (the bench's isolated
