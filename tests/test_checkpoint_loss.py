@@ -136,3 +136,14 @@ def test_orthogonal_loss_vs_reference(golden):
     np.testing.assert_allclose(float(v), float(z['orth']), rtol=1e-6)
     assert losses.orth_weight(1, 10) == 0.0 and losses.orth_weight(4, 10) == pytest.approx(0.4)
     assert losses.orth_weight(9, 10) == 1.0
+
+
+def test_adam_launches_per_step_counts_both_forms():
+    """The profilers' step-equivalent count (bench.py pmc_traffic): one table launch per
+    parameter group, ceil(n / ADAM_MAX) launches per group in the per-48-tensor form."""
+    from ewvit import _lib
+    from ewvit.optim import Adam
+    ps = [torch.nn.Parameter(torch.zeros(2)) for _ in range(2 * _lib.ADAM_MAX + 1)]
+    frozen = torch.nn.Parameter(torch.zeros(2), requires_grad=False)
+    opt = Adam([{'params': ps}, {'params': [frozen]}], lr=1e-3)
+    assert opt.launches_per_step() == {'adam_table_kernel': 1, 'adam_multi_kernel': 3}
