@@ -58,7 +58,7 @@ def _fused_ok(logits, space, freq, criterion):
     return (logits.is_cuda and type(criterion) is torch.nn.BCEWithLogitsLoss and criterion.reduction == 'mean'
             and criterion.weight is None and (criterion.pos_weight is None or criterion.pos_weight.numel() == 1)
             and space.dim() == 2 and space.shape == freq.shape and logits.numel() == space.shape[0]
-            and 1 <= space.shape[0] <= 64 and 4 * space.numel() + 2 * space.shape[0] + 8 <= 16384)
+            and 1 <= space.shape[0] <= 64 and 4 * space.numel() + 2 * space.shape[0] + 16 <= 16384)
 
 
 def combined_loss(outputs, labels, criterion, epoch, max_epochs, weight=None):  # train.py:69-91

@@ -3,7 +3,9 @@ loss value and the logits / space / freq gradients against the reference's own o
 (tests/golden/ref_loss.npz) and against the torch formulation of network/losses.py on the
 same device, at the curriculum points, with a device weight, without pos_weight, and for a
 zero-norm row (F.normalize's eps branch).  fp32 throughout: bounds 2e-6 relative on the
-value, 2e-5 relative on gradients (a different summation order of the same fp32 terms)."""
+value, 2e-5 relative on gradients (a different summation order of the same fp32 terms; per
+row, 1e-5 of the row's largest gradient absolute, x sqrt(D / 128) past D = 128: g - u (u . g)
+cancels, and its rounding grows with the length of the D-term sums)."""
 import numpy as np
 import pytest
 import torch
@@ -42,7 +44,8 @@ def test_fused_loss_vs_reference_golden(golden, epoch, maxe):
             torch.testing.assert_close(g, torch.from_numpy(z[f'{tag}.grad.{name}']), rtol=2e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize('B,D,pw', [(8, 128, 0.5), (3, 64, None), (16, 192, 2.0), (1, 8, 0.5)])
+@pytest.mark.parametrize('B,D,pw', [(8, 128, 0.5), (3, 64, None), (16, 192, 2.0), (1, 8, 0.5),
+                                         (40, 80, 0.5), (4, 512, 1.5), (32, 96, None)])
 def test_fused_loss_vs_torch(B, D, pw):
     g = torch.Generator().manual_seed(B * 131 + D)
     logits = torch.randn(B, 1, generator=g) * 3
@@ -60,7 +63,7 @@ def test_fused_loss_vs_torch(B, D, pw):
     for a, b in zip(got[2], ref[2]):
         for r in range(B):                  # per row: the zero row's gradient is ~1e12 larger
             scale = float(b[r].abs().max()) + 1e-30
-            torch.testing.assert_close(a[r], b[r], rtol=2e-5, atol=1e-5 * scale)
+            torch.testing.assert_close(a[r], b[r], rtol=2e-5, atol=1e-5 * max(1.0, (D / 128) ** 0.5) * scale)
 
 
 def test_fused_loss_grad_scale_and_graph():
