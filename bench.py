@@ -212,12 +212,11 @@ def pmc_traffic(entry, per_step, config=2, adam_per_step=None):
     tot = sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in ks)
     if entry in PER_DISPATCH:
         return round(tot / sum(v['dispatches'] for v in ks), 1)
-    steps = data.get('_steps_executed')
-    for kname, per in (adam_per_step or {}).items():      # {kernel name: launches per step}
-        adam = [v['dispatches'] for k, v in data.items() if kname in k]
-        if adam and per:
-            steps = adam[0] / per
-            break
+    # {kernel name: launches per step}; a run may mix the forms (eager passes vs a graph
+    # captured with the other), so the step equivalents of each form add up
+    counted = [sum(v['dispatches'] for k, v in data.items() if kname in k) / per
+               for kname, per in (adam_per_step or {}).items() if per]
+    steps = sum(counted) if any(counted) else data.get('_steps_executed')
     if not steps or not per_step:
         return None
     return round(tot / (per_step * steps), 1)

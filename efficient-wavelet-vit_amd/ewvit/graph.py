@@ -314,6 +314,7 @@ class TrainStep:
             self.g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g, stream=side):
                 self.loss = self._iteration()
+            self._finish_capture()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
 
@@ -336,7 +337,14 @@ class TrainStep:
             self.g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool()):
                 self.opt.step()
+            self._finish_capture()
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+
+    def _finish_capture(self):
+        fin = getattr(self.opt, 'finish_capture', None)
+        if fin is not None:
+            fin()                            # device tables the captured optimizer launches read
         torch.cuda.synchronize()
 
     def _split_eager(self):

@@ -4,9 +4,9 @@ reference's training step (train.py:273-275: ``optim.Adam(params, lr, weight_dec
 Same constructor, update rule and state layout as ``torch.optim.Adam`` (per-parameter
 state ``step`` / ``exp_avg`` / ``exp_avg_sq``, so checkpoints load either way), for
 amsgrad=False / maximize=False.  ``step()`` issues ONE launch per parameter group from a
-device table of the tensors' addresses (rebuilt when they change, outside graph capture), or
-— when the addresses changed while a graph is being captured, or with EWVIT_ADAM_TABLE=0 —
-one launch per 48 tensors with the pointers passed by value; plus one foreach increment of
+device table of the tensors' addresses (rebuilt when they change; a graph capture's table is
+allocated before it and filled after it, ``finish_capture()``), or — with EWVIT_ADAM_TABLE=0
+or no such table — one launch per 48 tensors with the pointers passed by value; plus one foreach increment of
 the per-parameter device step counters.
 
 The learning rate is read by the kernel from a per-group device scalar (``self._lr_dev``),
@@ -110,7 +110,8 @@ class Adam(torch.optim.Optimizer):
     def _table_step(self, group, items, lr_dev, stream):
         """The whole group in one launch (ewvit_adam_step_table) from a device table of its
         tensors' addresses, built when they change — never while a graph is being captured
-        (a changed layout then takes the launches above).  EWVIT_ADAM_TABLE=0: off."""
+        (a captured step takes a table allocated by the eager step before it and filled by
+        finish_capture(); without one, the launches above).  EWVIT_ADAM_TABLE=0: off."""
         if not self.table:
             return False
         key = tuple((c[0].data_ptr(), c[1].data_ptr(), c[2]['exp_avg'].data_ptr(), c[2]['exp_avg_sq'].data_ptr(),
@@ -119,21 +120,38 @@ class Adam(torch.optim.Optimizer):
             self._tables = {}
         cached = self._tables.get(id(group))
         if cached is None or cached[0] != key:
-            if torch.cuda.is_current_stream_capturing():
-                return False
             lib, rows, chunk0 = L.load(), [], 0
             for k in key:
                 rows.append(list(k) + [chunk0])
                 chunk0 += int(lib.ewvit_adam_chunks(k[5]))
-            tab = torch.tensor(rows, dtype=torch.int64).to(items[0][0].device)
+            spares = self.__dict__.setdefault('_spare', {})
+            if torch.cuda.is_current_stream_capturing():
+                # the captured step's gradients are new tensors of the graph's pool: the launch
+                # reads a table allocated before the capture (outside the graph's pool, so no
+                # captured temporary can alias it), filled once the capture has ended
+                tab = spares.pop(id(group), None)
+                if tab is None or tab.shape[0] != len(rows):
+                    return False
+                self.__dict__.setdefault('_fill_after_capture', []).append((tab, rows))
+            else:
+                tab = torch.tensor(rows, dtype=torch.int64).to(items[0][0].device)
+                spares[id(group)] = torch.empty_like(tab)
             cached = self._tables[id(group)] = (key, tab, chunk0)
-            # a step captured earlier may still replay the previous table: keep every table
-            self.__dict__.setdefault('_table_keep', []).append(tab)
+        if torch.cuda.is_current_stream_capturing():
+            # the graph replays this table for its lifetime: keep it past later rebuilds (an
+            # eager step's table is freed stream-ordered when the next one replaces it)
+            self.__dict__.setdefault('_table_keep', []).append(cached[1])
         b1, b2 = group['betas']
         L.call('ewvit_adam_step_table', L.ptr(cached[1]), len(key), cached[2], float(group['lr']), lr_dev, float(b1),
                float(b2), float(group['eps']), float(group['weight_decay']), stream,
                work={'bytes': 28.0 * sum(k[5] for k in key)})
         return True
+
+    def finish_capture(self):
+        """Fill the tables a graph capture launched Adam on (their rows are host data; the
+        replays only read them).  Called by ewvit.graph.TrainStep after every capture."""
+        for tab, rows in self.__dict__.pop('_fill_after_capture', []):
+            tab.copy_(torch.tensor(rows, dtype=torch.int64))
 
     def launches_per_step(self):
         """Adam kernel launches one step makes, by kernel name, in either launch form (the

@@ -79,6 +79,36 @@ def _adam_pair(sched_steps_after=3, accum=1):
     return a, b, sa, sb
 
 
+def test_trainstep_graph_single_launch_adam_equals_eager():
+    """ewvit Adam inside the captured step: the capture launches the one-launch form on a
+    table allocated before the capture and filled after it (Adam.finish_capture); the replays
+    match the same steps run eagerly"""
+    import ewvit
+    from ewvit.graph import TrainStep
+    a, b = _mwt_pair()
+    x = torch.randn(4, 3, 64, 64, device=DEV)
+
+    def make(m):
+        opt = ewvit.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-4)
+
+        def fl():
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                return m(x).float().square().mean()
+        return fl, opt
+    fa, oa = make(a)
+    fb, ob = make(b)
+    sa = TrainStep(a, fa, oa, graph=False)
+    for _ in range(6):
+        sa()
+    sb = TrainStep(b, fb, ob, graph=True, warmup=3)
+    assert len(ob._table_keep) == 1 and not getattr(ob, '_fill_after_capture', [])
+    for _ in range(3):
+        sb()
+    torch.cuda.synchronize()
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(q, p, rtol=2e-4, atol=2e-5, msg=n)
+
+
 def test_trainstep_graph_follows_lr_schedule():
     """a replayed step must read the scheduler's lr (device scalar refreshed
     before each replay), not the lr baked in at capture."""
