@@ -87,7 +87,9 @@ def build_mwt_step(dev, frames, rank, graph=True):
     return TrainStep(model, forward_loss, opt, graph=graph)
 
 
-def build_step(dev, frames, rank, graph=True, config=2):
+def build_step(dev, frames, rank, graph=True, config=2, force_collectives=False):
+    """The config's TrainStep (force_collectives: the test switch that issues the bucket
+    all-reduces and the buffer broadcast in a world of one, ewvit/graph.py)."""
     if config == 4:
         return build_mwt_step(dev, frames, rank, graph)
     from network.model import DeepfakeDetector
@@ -123,7 +125,7 @@ def build_step(dev, frames, rank, graph=True, config=2):
         return loss
     # gradients averaged over ranks by bucketed RCCL all-reduces issued during backward;
     # the whole iteration replayed from one HIP graph (ewvit/graph.py)
-    return TrainStep(model, forward_loss, opt, graph=graph)
+    return TrainStep(model, forward_loss, opt, graph=graph, force_collectives=force_collectives)
 
 
 def kernel_table(records):
@@ -398,7 +400,9 @@ def main():
             5: 'frames/sec fwd+bwd, 224×224 bs=128 dim=128, fp8 e4m3 token GEMMs, MI355X'}[args.config]
         res = {'metric': metric, 'value': round(frames / elapsed, 2), 'unit': 'frames/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(1e3 * elapsed / args.steps, 3),
-               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+               # config 5: the attention / MLP token GEMMs on fp8 e4m3 operands, everything else bf16
+               'dtype': 'fp8e4m3+bf16' if CONFIGS.get(args.config, {}).get('gemm') == 'fp8' else 'bf16',
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None

@@ -60,13 +60,17 @@ def _backend(group):
 
 
 class GradBuckets:
-    """Flat, bucketed gradient buffer with all-reduces issued as buckets fill."""
+    """Flat, bucketed gradient buffer with all-reduces issued as buckets fill.
 
-    def __init__(self, params, group=None, bucket_mb=32, first_bucket_mb=4):
+    ``force=True`` issues the collectives even in a world of one process (a test switch: it
+    puts the RCCL calls inside the captured step graph on a one-GPU box)."""
+
+    def __init__(self, params, group=None, bucket_mb=32, first_bucket_mb=4, force=False):
         self.params = list(params)
         self.group = group
         self.world = _world(group)
-        self.avg_op = _backend(group) != 'gloo'          # gloo has no AVG: SUM, then divide
+        self.reduce = self.world > 1 or (force and dist.is_available() and dist.is_initialized())
+        self.avg_op = not self.reduce or dist.get_backend(group) != 'gloo'   # gloo has no AVG: SUM, then divide
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.first_bytes = min(int(first_bucket_mb * (1 << 20)), self.bucket_bytes)
         self.order = None          # parameter indices in gradient-ready order
@@ -105,7 +109,7 @@ class GradBuckets:
         (rank 0's order, so every rank issues the same collectives in the same order)."""
         seen = list(dict.fromkeys(self.observed))
         order = seen + [i for i in reversed(range(len(self.params))) if i not in set(seen)]
-        if self.world > 1:
+        if self.reduce:
             t = torch.tensor(order, dtype=torch.int64, device=self.flat.device)
             dist.broadcast(t, 0, group=self.group)
             order = t.tolist()
@@ -139,7 +143,7 @@ class GradBuckets:
 
     def _fire(self, b):
         s, e, _ = self.buckets[b]
-        if self.world > 1 and not self.defer:
+        if self.reduce and not self.defer:
             if self.flat.is_cuda:
                 # the gradients of a bucket may come from several streams (DAMA's MWT branch
                 # runs on its own, deferred weight gradients on the wgrad stream): the
@@ -171,12 +175,12 @@ class GradBuckets:
         for w in self.works:
             w.wait()
         self.works = []
-        if self.world > 1 and not self.avg_op and not self.defer:
+        if self.reduce and not self.avg_op and not self.defer:
             self.flat.div_(self.world)
 
     def allreduce_all(self):
         """The deferred form: one all-reduce of the whole buffer (between two graphs)."""
-        if self.world > 1:
+        if self.reduce:
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM, group=self.group)
             if not self.avg_op:
                 self.flat.div_(self.world)
@@ -189,12 +193,19 @@ class GradBuckets:
 
 
 class BufferSync:
-    """Module buffers re-pointed into one flat tensor per dtype, broadcast from rank 0."""
+    """Module buffers re-pointed into one flat tensor per dtype, broadcast from rank 0.
+
+    Modules whose class sets ``ewvit_buffer_sync = False`` (the checkpoint placeholders of
+    the reference's unused ablation heads, network/model.py) and everything below them are
+    left out: nothing updates them, and they can hold hundreds of MB."""
 
     def __init__(self, model, group=None):
         self.group = group
         by_dt = {}
-        for mod in model.modules():
+        skip = [n for n, m in model.named_modules() if getattr(type(m), 'ewvit_buffer_sync', True) is False]
+        for mname, mod in model.named_modules():
+            if any(mname == s or mname.startswith(s + '.') for s in skip):
+                continue
             for name, b in mod._buffers.items():
                 if b is not None:
                     by_dt.setdefault(b.dtype, []).append((mod, name, b))
@@ -209,6 +220,7 @@ class BufferSync:
                 mod._buffers[name] = v
                 off += b.numel()
             self.flats.append(flat)
+        self.bytes = sum(f.numel() * f.element_size() for f in self.flats)
 
     def __call__(self):
         for f in self.flats:
@@ -217,18 +229,27 @@ class BufferSync:
 
 class TrainStep:
     def __init__(self, model, forward_loss, optimizer, graph=True, warmup=3, group=None, bucket_mb=32,
-                 accum_steps=1, overlap=True):
+                 accum_steps=1, overlap=True, force_collectives=False):
+        """``force_collectives``: issue the bucket all-reduces and the buffer broadcast even in
+        a world of one (test switch; needs an initialised process group).  A failure to
+        capture the collectives raises, unless EWVIT_GRAPH_SPLIT_FALLBACK=1 allows the split,
+        non-overlapped form (graphs around one all-reduce) — never silently."""
         self.model, self.forward_loss, self.opt, self.group = model, forward_loss, optimizer, group
         self.world = _world(group)
+        forced = bool(force_collectives) and dist.is_available() and dist.is_initialized()
+        if force_collectives and not forced:
+            raise RuntimeError('TrainStep(force_collectives=True) needs an initialised process group')
         self.accum = int(accum_steps)
         self.params = [p for p in model.parameters() if p.requires_grad]
         dev = self.params[0].device
-        capturable = _backend(group) in (None, 'nccl')
+        backend = dist.get_backend(group) if (self.world > 1 or forced) else None
+        capturable = backend in (None, 'nccl')
         self.graph = bool(graph) and dev.type == 'cuda' and capturable
-        self.buckets = GradBuckets(self.params, group, bucket_mb) if self.world > 1 else None
+        dp = self.world > 1 or forced
+        self.buckets = GradBuckets(self.params, group, bucket_mb, force=forced) if dp else None
         if self.buckets is not None:
             self.buckets.defer = not overlap
-        self.bufsync = BufferSync(model, group) if self.world > 1 else None
+        self.bufsync = BufferSync(model, group) if dp else None
         # single-use weights' gradients on a second stream, beside the input-gradient chain
         grads.set_wgrad_stream(dev.type == 'cuda' and os.environ.get('EWVIT_WGRAD_STREAM', '0') == '1')
         self.loss = None
@@ -236,26 +257,38 @@ class TrainStep:
         self._hyper = optimizer.hyper_signature() if hasattr(optimizer, 'hyper_signature') else None
         self._started = False
         self.g2 = None
+        self.fallback = None
         if self.graph and self.buckets is not None and self.buckets.defer:
             self._capture_split(warmup)
         elif self.graph:
             try:
                 self._capture(warmup)
             except Exception as e:          # noqa: BLE001 — a backend that cannot record collectives
-                if self.world == 1:
+                if self.buckets is None or os.environ.get('EWVIT_GRAPH_SPLIT_FALLBACK', '0') != '1':
+                    self.close()             # no gradient hooks / slots left behind on the parameters
                     raise
                 import sys
-                print(f'TrainStep: capturing the collectives failed ({type(e).__name__}: {e}); falling back to '
-                      f'forward/backward and optimizer graphs around one all-reduce', file=sys.stderr, flush=True)
+                print(f'TrainStep: capturing the collectives failed ({type(e).__name__}: {e}); '
+                      f'EWVIT_GRAPH_SPLIT_FALLBACK=1: forward/backward and optimizer graphs around one '
+                      f'all-reduce', file=sys.stderr, flush=True)
                 torch.cuda.synchronize()
                 self.buckets.defer = True
+                self.fallback = f'{type(e).__name__}: {e}'
                 self._capture_split(warmup)
+
+    def close(self):
+        """Detach from the model: remove the gradient hooks and slots of the buckets."""
+        if self.buckets is not None:
+            self.buckets.remove()
+            self.buckets = None
 
     def describe(self):
         d = {'launch': 'hip-graph' if self.graph else 'eager', 'world': self.world}
+        if self.fallback is not None:
+            d['capture_fallback'] = self.fallback
         if self.buckets is not None:
             d.update({'buckets': len(self.buckets.buckets), 'bucket_mb': self.buckets.bucket_bytes / (1 << 20),
-                      'grad_bytes': 4 * self.buckets.flat.numel(),
+                      'grad_bytes': 4 * self.buckets.flat.numel(), 'buffer_bytes': self.bufsync.bytes,
                       'overlap': 'per-bucket all-reduce issued during backward' + (
                           ', recorded in the step graph' if self.graph else '')
                       if not self.buckets.defer else 'one all-reduce between two graphs'})
@@ -312,9 +345,12 @@ class TrainStep:
             self.loss = None
             torch.cuda.synchronize()
             self.g = torch.cuda.CUDAGraph()
+            # the host seeds the recorded dropout launches bake in come from the CPU generator
+            # (ewvit.ops._seed); its state at capture lets a caller reproduce a replay eagerly
+            self.capture_cpu_rng = torch.get_rng_state()
             with torch.cuda.graph(self.g, stream=side):
                 self.loss = self._iteration()
-            self._finish_capture()
+            self._finish_capture(self.g)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
 
@@ -337,15 +373,15 @@ class TrainStep:
             self.g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool()):
                 self.opt.step()
-            self._finish_capture()
+            self._finish_capture(self.g2)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
 
-    def _finish_capture(self):
+    def _finish_capture(self, graph):
         fin = getattr(self.opt, 'finish_capture', None)
         if fin is not None:
-            fin()                            # device tables the captured optimizer launches read
-        torch.cuda.synchronize()
+            fin(graph)                       # device tables the captured optimizer launches read,
+        torch.cuda.synchronize()             # owned by the graph that reads them
 
     def _split_eager(self):
         self.opt.zero_grad(set_to_none=True)

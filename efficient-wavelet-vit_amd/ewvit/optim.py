@@ -45,26 +45,48 @@ class Adam(torch.optim.Optimizer):
         self.table = os.environ.get('EWVIT_ADAM_TABLE', '1') != '0'   # one launch per group
 
     def sync_hyper(self):
-        """Write each group's current lr into its device scalar (outside any graph capture)."""
-        if not hasattr(self, '_lr_dev'):
-            self._lr_dev = {}           # id(group) -> [device f64 scalar, value last written]
-        for group in self.param_groups:
+        """Write each group's current lr into its device scalar (outside any graph capture).
+
+        The scalars are keyed by group INDEX and refilled in place: ``load_state_dict``
+        replaces every param_group dict, and a graph captured before it keeps reading the
+        tensor it was recorded with."""
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError('ewvit.optim.Adam.sync_hyper: called inside a graph capture (the fill '
+                               'would be recorded and override the schedule on every replay)')
+        lrs = self.__dict__.setdefault('_lr_dev', {})      # group index -> [device f64 scalar, value]
+        for gi, group in enumerate(self.param_groups):
             lr = float(group['lr'])
             dev = next((p.device for p in group['params'] if p.is_cuda), None)
             if dev is None:
                 continue
-            e = self._lr_dev.get(id(group))
+            e = lrs.get(gi)
             if e is None or e[0].device != dev:
-                e = self._lr_dev[id(group)] = [torch.empty((), dtype=torch.float64, device=dev), None]
+                e = lrs[gi] = [torch.empty((), dtype=torch.float64, device=dev), None]
             if e[1] != lr:
                 e[0].fill_(lr)
                 e[1] = lr
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict, keeping the device tensors a captured step
+        reads: the loaded ``step`` / ``exp_avg`` / ``exp_avg_sq`` are copied INTO the existing
+        state tensors (torch would replace them, and a HIP graph recorded before the load would
+        keep updating the old ones), and the lr scalars stay keyed by group index."""
+        old = {p: dict(st) for p, st in self.state.items()}
+        super().load_state_dict(state_dict)
+        for p, st in self.state.items():
+            o = old.get(p)
+            if not o:
+                continue
+            for k in ('step', 'exp_avg', 'exp_avg_sq'):
+                if k in o and k in st and torch.is_tensor(st[k]) and o[k].shape == st[k].shape:
+                    o[k].copy_(st[k])
+                    st[k] = o[k]
 
     def hyper_signature(self):
         """The hyper-parameters a recorded step bakes in as launch constants."""
         return tuple((tuple(g['betas']), float(g['eps']), float(g['weight_decay'])) for g in self.param_groups)
 
-    def _group_step(self, group):
+    def _group_step(self, gi, group):
         items = []
         for p in group['params']:
             if p.grad is None:
@@ -90,11 +112,11 @@ class Adam(torch.optim.Optimizer):
             return
         torch._foreach_add_([c[2]['step'] for c in items], 1.0)   # torch semantics: per-parameter steps
         b1, b2 = group['betas']
-        if id(group) not in getattr(self, '_lr_dev', {}):
-            self.sync_hyper()
-        lr_dev = L.ptr(self._lr_dev[id(group)][0])
+        if gi not in self.__dict__.get('_lr_dev', {}):
+            self.sync_hyper()           # raises inside a capture: never record the scalar's fill
+        lr_dev = L.ptr(self._lr_dev[gi][0])
         stream = L.stream(items[0][0])
-        if self._table_step(group, items, lr_dev, stream):
+        if self._table_step(gi, group, items, lr_dev, stream):
             return
         for k in range(0, len(items), L.ADAM_MAX):
             chunk = items[k:k + L.ADAM_MAX]
@@ -107,51 +129,86 @@ class Adam(torch.optim.Optimizer):
                    float(group['lr']), lr_dev, float(b1), float(b2), float(group['eps']),
                    float(group['weight_decay']), stream, work={'bytes': 28.0 * sum(c[0].numel() for c in chunk)})
 
-    def _table_step(self, group, items, lr_dev, stream):
+    def _table_step(self, gi, group, items, lr_dev, stream):
         """The whole group in one launch (ewvit_adam_step_table) from a device table of its
-        tensors' addresses, built when they change — never while a graph is being captured
-        (a captured step takes a table allocated by the eager step before it and filled by
-        finish_capture(); without one, the launches above).  EWVIT_ADAM_TABLE=0: off."""
+        tensors' addresses, rebuilt when they change.
+
+        Eager: one device table per group, refilled in place from a pinned host buffer
+        (stream-ordered after the launches that read it) while its row count holds.  Capture:
+        the launch reads a spare table allocated by the eager step before it (outside the
+        graph's pool, so no captured temporary can alias it), filled by finish_capture() and
+        owned by the graph from then on (finish_capture(graph) ties it to the graph's
+        lifetime).  Without a spare, the per-48-tensor launches above.  EWVIT_ADAM_TABLE=0: off."""
         if not self.table:
             return False
         key = tuple((c[0].data_ptr(), c[1].data_ptr(), c[2]['exp_avg'].data_ptr(), c[2]['exp_avg_sq'].data_ptr(),
                      c[2]['step'].data_ptr(), c[0].numel()) for c in items)
-        if not hasattr(self, '_tables'):
-            self._tables = {}
-        cached = self._tables.get(id(group))
+        tables = self.__dict__.setdefault('_tables', {})   # gi -> [key, device table, chunks, graph-owned]
+        spares = self.__dict__.setdefault('_spare', {})
+        capturing = torch.cuda.is_current_stream_capturing()
+        cached = tables.get(gi)
         if cached is None or cached[0] != key:
             lib, rows, chunk0 = L.load(), [], 0
             for k in key:
                 rows.append(list(k) + [chunk0])
                 chunk0 += int(lib.ewvit_adam_chunks(k[5]))
-            spares = self.__dict__.setdefault('_spare', {})
-            if torch.cuda.is_current_stream_capturing():
-                # the captured step's gradients are new tensors of the graph's pool: the launch
-                # reads a table allocated before the capture (outside the graph's pool, so no
-                # captured temporary can alias it), filled once the capture has ended
-                tab = spares.pop(id(group), None)
+            if capturing:
+                tab = spares.pop(gi, None)
                 if tab is None or tab.shape[0] != len(rows):
                     return False
                 self.__dict__.setdefault('_fill_after_capture', []).append((tab, rows))
+                cached = tables[gi] = [key, tab, chunk0, True]
             else:
-                tab = torch.tensor(rows, dtype=torch.int64).to(items[0][0].device)
-                spares[id(group)] = torch.empty_like(tab)
-            cached = self._tables[id(group)] = (key, tab, chunk0)
-        if torch.cuda.is_current_stream_capturing():
-            # the graph replays this table for its lifetime: keep it past later rebuilds (an
-            # eager step's table is freed stream-ordered when the next one replaces it)
-            self.__dict__.setdefault('_table_keep', []).append(cached[1])
+                dev = items[0][0].device
+                if cached is not None and not cached[3] and cached[1].shape[0] == len(rows):
+                    tab = cached[1]                     # refill in place (same stream as its readers)
+                else:
+                    tab = torch.empty((len(rows), 7), dtype=torch.int64, device=dev)
+                pin = self.__dict__.get('_pin', {}).get(gi)
+                if pin is None or pin[0].shape[0] != len(rows):
+                    pin = self.__dict__.setdefault('_pin', {})[gi] = [
+                        torch.empty((len(rows), 7), dtype=torch.int64, pin_memory=True), None]
+                if pin[1] is not None:
+                    pin[1].synchronize()               # the previous copy out of it has finished
+                pin[0].copy_(torch.tensor(rows, dtype=torch.int64))
+                tab.copy_(pin[0], non_blocking=True)
+                pin[1] = torch.cuda.Event()
+                pin[1].record()
+                if spares.get(gi) is None or spares[gi].shape[0] != len(rows):
+                    spares[gi] = torch.empty_like(tab)
+                cached = tables[gi] = [key, tab, chunk0, False]
+        elif capturing and not cached[3]:
+            # the same addresses as the eager table: the graph must not share a table an
+            # eager rebuild may refill, so it takes the spare with the same rows
+            tab = spares.pop(gi, None)
+            if tab is None or tab.shape != cached[1].shape:
+                return False
+            self.__dict__.setdefault('_fill_after_capture', []).append((tab, None, cached[1]))
+            cached = tables[gi] = [key, tab, cached[2], True]
         b1, b2 = group['betas']
         L.call('ewvit_adam_step_table', L.ptr(cached[1]), len(key), cached[2], float(group['lr']), lr_dev, float(b1),
                float(b2), float(group['eps']), float(group['weight_decay']), stream,
                work={'bytes': 28.0 * sum(k[5] for k in key)})
         return True
 
-    def finish_capture(self):
+    def finish_capture(self, graph=None):
         """Fill the tables a graph capture launched Adam on (their rows are host data; the
-        replays only read them).  Called by ewvit.graph.TrainStep after every capture."""
-        for tab, rows in self.__dict__.pop('_fill_after_capture', []):
-            tab.copy_(torch.tensor(rows, dtype=torch.int64))
+        replays only read them) and hand them to the graph: with ``graph`` given they live as
+        long as it does (ewvit.graph.TrainStep passes its graphs), else the optimizer keeps
+        them.  Returns the tables."""
+        out = []
+        for item in self.__dict__.pop('_fill_after_capture', []):
+            tab = item[0]
+            if item[1] is not None:
+                tab.copy_(torch.tensor(item[1], dtype=torch.int64))
+            else:
+                tab.copy_(item[2])
+            out.append(tab)
+        if graph is not None:
+            graph.__dict__.setdefault('_ewvit_adam_tables', []).extend(out)
+        else:
+            self.__dict__.setdefault('_table_keep', []).extend(out)
+        return out
 
     def launches_per_step(self):
         """Adam kernel launches one step makes, by kernel name, in either launch form (the
@@ -168,6 +225,6 @@ class Adam(torch.optim.Optimizer):
                 loss = closure()
         if not torch.cuda.is_current_stream_capturing():
             self.sync_hyper()           # a captured step reads the scalar its owner refreshes
-        for group in self.param_groups:
-            self._group_step(group)
+        for gi, group in enumerate(self.param_groups):
+            self._group_step(gi, group)
         return loss

@@ -31,14 +31,22 @@ class _CombinedLoss(torch.autograd.Function):
     def forward(ctx, logits, labels, space, freq, pos_weight, weight, lam):
         from ewvit import _lib as L
         B, D = space.shape
+        dev = space.device
+
+        def on_dev(t, n):
+            # labels / pos_weight / the curriculum weight may be CPU tensors (torch accepts a
+            # 0-dim CPU weight): the kernel dereferences them, so they move to the GPU first
+            return t.detach().to(device=dev, dtype=torch.float32).reshape(n).contiguous()
         lg = logits.detach().float().reshape(B).contiguous()
-        lb = labels.detach().float().reshape(B).contiguous()
+        lb = on_dev(labels, B)
         s, f = space.detach().float().contiguous(), freq.detach().float().contiguous()
-        out = torch.empty(3, dtype=torch.float32, device=space.device)
+        out = torch.empty(3, dtype=torch.float32, device=dev)
         dl, ds, df = torch.empty_like(lg), torch.empty_like(s), torch.empty_like(f)
-        pw = pos_weight.detach().float().reshape(1).contiguous() if pos_weight is not None else None
-        w = weight.detach().float().reshape(1).contiguous() if weight is not None else None
-        L.require_gpu(lg, s, f)
+        pw = on_dev(pos_weight, 1) if pos_weight is not None else None
+        w = on_dev(weight, 1) if weight is not None else None
+        L.require_gpu(lg, lb, s, f, pw, w)
+        if any(t is not None and t.device != dev for t in (lg, lb, f, pw, w)):
+            raise RuntimeError('combined_loss: inputs on different GPUs')
         L.call('ewvit_combined_loss', L.ptr(lg), L.ptr(lb), L.ptr(s), L.ptr(f), B, D, L.ptr(pw), L.ptr(w),
                float(lam), L.ptr(out), L.ptr(dl), L.ptr(ds), L.ptr(df), L.stream(out))
         ctx.save_for_backward(dl, ds, df)
@@ -54,8 +62,9 @@ class _CombinedLoss(torch.autograd.Function):
         return dl.view(ctx.logit_shape), None, ds, df, None, None, None
 
 
-def _fused_ok(logits, space, freq, criterion):
-    return (logits.is_cuda and type(criterion) is torch.nn.BCEWithLogitsLoss and criterion.reduction == 'mean'
+def _fused_ok(logits, labels, space, freq, criterion):
+    return (logits.is_cuda and space.is_cuda and freq.is_cuda and logits.device == space.device == freq.device
+            and torch.is_tensor(labels) and labels.numel() == logits.numel() and type(criterion) is torch.nn.BCEWithLogitsLoss and criterion.reduction == 'mean'
             and criterion.weight is None and (criterion.pos_weight is None or criterion.pos_weight.numel() == 1)
             and space.dim() == 2 and space.shape == freq.shape and logits.numel() == space.shape[0]
             and 1 <= space.shape[0] <= 64 and 4 * space.numel() + 2 * space.shape[0] + 16 <= 16384)
@@ -68,7 +77,7 @@ def combined_loss(outputs, labels, criterion, epoch, max_epochs, weight=None):  
     cls-only loss value and gradients).  On the GPU with the reference's criterion
     (BCEWithLogitsLoss, mean, scalar pos_weight) the whole objective is one ewvit launch."""
     logits = outputs['logits']
-    if _fused_ok(logits, outputs['space'], outputs['freq'], criterion):
+    if _fused_ok(logits, labels, outputs['space'], outputs['freq'], criterion):
         lam = 0.0 if weight is not None else orth_weight(epoch, max_epochs)
         total, parts = _CombinedLoss.apply(logits, labels, outputs['space'], outputs['freq'], criterion.pos_weight,
                                            weight, lam)

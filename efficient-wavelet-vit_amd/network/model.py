@@ -101,7 +101,13 @@ class DeepfakeDetector(nn.Module):
 
 
 class _AblationHeadState(nn.Module):
-    """Holds checkpoint tensors of the reference's b0 ablation heads (model.py:37-51); no forward."""
+    """Holds checkpoint tensors of the reference's b0 ablation heads (model.py:37-51); no forward.
+
+    Nothing trains or updates them, so the data-parallel buffer broadcast leaves them out
+    (ewvit.graph.BufferSync: a resumed reference checkpoint would otherwise broadcast two
+    128 MB patch_to_embedding weights every step)."""
+
+    ewvit_buffer_sync = False
 
     def forward(self, *_):
         raise NotImplementedError("the 'sfe_only' / 'sfe_mwt' ablation heads need EfficientNet-b0 "

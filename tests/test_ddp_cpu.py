@@ -222,3 +222,62 @@ def test_shard_videos_covers_batch_once():
     x = torch.arange(10).view(10, 1)
     parts = [edist.shard_videos(x, r, 4) for r in range(4)]
     assert torch.equal(torch.cat(parts), x)
+
+
+def _forced_worker(port, q):
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    torch.set_num_threads(1)
+    import torch.distributed as tdist
+    from ewvit.graph import TrainStep
+    tdist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
+    model = _model()
+    ref = _model()
+    x = _data()[:2].flatten(0, 1)
+    opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.5)
+    step = TrainStep(model, lambda: model(x).mean(), opt, graph=False, bucket_mb=4 / 1024, force_collectives=True)
+    fired = []
+    orig = step.buckets._fire
+    step.buckets._fire = lambda b: (fired.append(b), orig(b))[1]
+    step()
+    ref(x).mean().backward()
+    ok = all(torch.allclose(p.grad, r.grad, rtol=1e-6, atol=1e-7) for p, r in zip(model.parameters(), ref.parameters()))
+    q.put((fired, len(step.buckets.buckets), step.buckets.reduce, ok, step.describe()))
+    tdist.destroy_process_group()
+
+
+def test_force_collectives_world1_issues_bucket_allreduces():
+    """TrainStep(force_collectives=True) in a world of one (the switch the GPU test uses to put
+    RCCL calls in the captured step on a one-GPU box): the buckets are laid out and each one's
+    all-reduce is issued, in order; the averaged gradient of one rank is its own gradient."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(_port(), q))
+    p.start()
+    fired, nb, reduce, ok, desc = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    # (the first step runs on the initial layout; the buffer is re-cut after it)
+    assert reduce and nb > 4 and len(fired) > 4 and fired == list(range(len(fired))), (fired, nb)
+    assert ok
+    assert desc['world'] == 1 and desc['buckets'] == nb
+
+
+def test_buffer_sync_skips_ablation_head_placeholders():
+    """the checkpoint placeholders of the unused b0 heads (network/model.py
+    _AblationHeadState) are never broadcast; BatchNorm running statistics are."""
+    sys.path.insert(0, PKG)
+    from ewvit.graph import BufferSync
+    from network.model import _AblationHeadState
+    m = torch.nn.Module()
+    m.bn = torch.nn.BatchNorm2d(8)
+    m.sfe = _AblationHeadState()
+    m.sfe.inner = _AblationHeadState()
+    m.sfe.inner.register_buffer('weight', torch.zeros(512, 1024))
+    m.sfe.register_buffer('bias', torch.zeros(16))
+    bs = BufferSync(m)
+    # bn: running_mean + running_var (fp32) and num_batches_tracked (int64)
+    assert bs.bytes == 2 * 8 * 4 + 8
+    assert m.bn.running_mean.data_ptr() in {f.data_ptr() for f in bs.flats}
+    assert m.sfe.inner.weight.numel() == 512 * 1024

@@ -139,3 +139,38 @@ def test_max_output_size():
     out = t.batch(frames).cpu().numpy()
     for i, f in enumerate(frames):
         np.testing.assert_array_equal(out[i], T.transform_frame(f, None, size=300, crop=256))
+
+
+def test_dataset_clip_through_gpu_transform(tmp_path):
+    """config/data_loader.py with the GPU transforms (get_transforms()): a FaceForensics++ clip
+    is ONE transform.batch launch and equals the reference's per-frame call + torch.stack
+    (data_loader.py:333-337) — with the train split's ColorJitter draws in the same order — and
+    the oracle (Pillow-pinned) per frame, the blank frame of an unreadable file included."""
+    import random
+    import loader_tree
+    from config import data_loader as D
+    from config.transforms import get_transforms
+    root = loader_tree.build(str(tmp_path / 'data'))
+    tr = get_transforms(device='cuda')
+    random.seed(0)
+    ds = D.FaceForensicsLoader(root, split='train', frame_count=8, transform=tr['train'])
+    for i in (0, 3, len(ds.real_videos) + 1, len(ds) - 1):
+        d, _ = ds.video_dir(i)
+        frames = D.read_frames(D.select_frames(D.frame_files(d), 8))
+        torch.manual_seed(100 + i)
+        clip, _ = ds[i]
+        torch.manual_seed(100 + i)
+        ref = torch.stack([tr['train'](f) for f in frames])
+        assert clip.shape == (8, 3, 224, 224) and clip.is_cuda
+        assert torch.equal(clip, ref), i
+    random.seed(0)
+    dv = D.FaceForensicsLoader(root, split='val', frame_count=6, transform=tr['val'])
+    blank_seen = False
+    for i in range(len(dv)):
+        d, _ = dv.video_dir(i)
+        frames = D.read_frames(D.select_frames(D.frame_files(d), 6))
+        blank_seen |= any(f.shape == (224, 224, 3) and not f.any() for f in frames)
+        clip = dv[i][0].cpu().numpy()
+        for k, f in enumerate(frames):
+            np.testing.assert_array_equal(clip[k], T.transform_frame(f, None), err_msg=f'{i}/{k}')
+    assert blank_seen

@@ -35,7 +35,7 @@ def test_fused_loss_vs_reference_golden(golden, epoch, maxe):
     logits, space, freq = (torch.from_numpy(z[k]) for k in ('logits', 'space', 'freq'))
     labels = torch.from_numpy(z['labels'])
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=DEV))
-    assert losses._fused_ok(logits.to(DEV), space, freq, crit)
+    assert losses._fused_ok(logits.to(DEV), labels, space.to(DEV), freq.to(DEV), crit)
     tag = f'e{epoch}of{maxe}'
     for weight in (None, torch.tensor(losses.orth_weight(epoch, maxe), device=DEV)):
         loss, parts, grads = _run(crit, logits, space, freq, labels, epoch, maxe, weight)
@@ -99,3 +99,26 @@ def test_fused_loss_grad_scale_and_graph():
     torch.cuda.synchronize()
     np.testing.assert_allclose(float(lv), float(parts['cls_loss']) + float(parts['orth_loss']), rtol=1e-6)
     assert float(parts['orth_loss']) > 0
+
+
+def test_fused_loss_host_operands():
+    """labels, pos_weight and a 0-dim curriculum weight given as CPU tensors (torch
+    accepts them) go to the GPU before the launch — the kernel must never read a host
+    address.  Same values as the all-device call."""
+    from network import losses
+    g = torch.Generator().manual_seed(11)
+    logits, space, freq = torch.randn(8, 1, generator=g), torch.randn(8, 128, generator=g), torch.randn(8, 128,
+                                                                                                        generator=g)
+    labels = (torch.rand(8, generator=g) > 0.5).float()
+    dev_crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=DEV))
+    host_crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor(0.5))
+    ref = _run(dev_crit, logits, space, freq, labels.to(DEV), weight=torch.tensor(0.7, device=DEV))
+    out = {'logits': logits.to(DEV).requires_grad_(True), 'space': space.to(DEV).requires_grad_(True),
+           'freq': freq.to(DEV).requires_grad_(True)}
+    assert losses._fused_ok(out['logits'], labels, out['space'], out['freq'], host_crit)
+    loss, _ = losses.combined_loss(out, labels, host_crit, 1, 1, weight=torch.tensor(0.7))
+    loss.backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss.detach().cpu(), ref[0], rtol=0, atol=0)
+    for t, r in zip((out['logits'], out['space'], out['freq']), ref[2]):
+        torch.testing.assert_close(t.grad.cpu(), r, rtol=0, atol=0)

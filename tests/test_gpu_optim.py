@@ -97,6 +97,7 @@ def test_adam_table_launch_matches_per_tensor_launches():
     ob = ewvit.optim.Adam(pb, lr=1e-3, weight_decay=1e-4)
     oa.table, ob.table = True, False
     g = torch.Generator().manual_seed(6)
+    tab_ptrs = []
     for step in range(3):
         for a, b in zip(pa, pb):
             gr = torch.randn(a.shape, generator=g).to(DEV)
@@ -104,8 +105,12 @@ def test_adam_table_launch_matches_per_tensor_launches():
             b.grad = gr.clone().contiguous(memory_format=torch.channels_last) if b.dim() == 4 else gr.clone()
         oa.step()
         ob.step()
+        tab_ptrs.append(oa._tables[0][1].data_ptr())
     torch.cuda.synchronize()
     assert len(oa._tables) == 1 and not getattr(oa, '_table_keep', [])   # eager tables are not kept
+    # new gradient addresses every step: the one device table is refilled in place (pinned
+    # host staging), not reallocated
+    assert len(set(tab_ptrs)) == 1
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
         assert torch.equal(oa.state[a]['exp_avg'], ob.state[b]['exp_avg'])
