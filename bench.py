@@ -454,7 +454,10 @@ def main():
         res['allreduce'] = step.describe() if hasattr(step, 'describe') else None
         res['cpu_baseline'] = None if args.no_cpu_baseline else cpu_baseline(args.cpu_steps, args.config)
         print(json.dumps(res), flush=True)
+    if hasattr(step, 'close'):
+        step.close()                 # graphs holding RCCL collectives released before the communicator
     if world > 1 and dist.is_initialized():
+        edist.barrier()
         dist.destroy_process_group()
 
 

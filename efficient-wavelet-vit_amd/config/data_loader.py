@@ -56,7 +56,7 @@ def imread_rgb(path):
     try:
         with Image.open(path) as im:
             im = ImageOps.exif_transpose(im)
-            return np.asarray(im.convert('RGB'))
+            return np.array(im.convert("RGB"))
     except Exception:     # noqa: BLE001 — unreadable / not an image: the caller's blank frame
         return None
 
@@ -116,10 +116,6 @@ class _ClipDataset(Dataset):
 
 
 # ------------------------------------------------------------------ FaceForensics++
-def _pair_key(pair):
-    return f'{pair[0]}_{pair[1]}'
-
-
 def _fake_candidates(root, methods, video_ids):
     """{target_source: [candidate videos in method order]} (data_loader.py:118-137)."""
     by_pair = {}

@@ -89,6 +89,8 @@ SIGNATURES = {
     'ewvit_frames_jitter_normalize': [_vp, _vp, _i64, _i32, _vp, _vp, _vp],
     'ewvit_combined_loss': [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp],
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
+    'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 
 # size queries: name -> (restype, argtypes)
@@ -107,6 +109,8 @@ QUERIES = {
     'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64, _vp]),
     'ewvit_adam_chunks': (_i64, [_i64]),
+    'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
+    'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
 }
 
 _lib = None

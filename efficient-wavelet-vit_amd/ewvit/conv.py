@@ -188,7 +188,9 @@ class Conv2dFn(torch.autograd.Function):
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = bias.detach().float().contiguous() if bias is not None else None
-        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
+        # algorithmic work over the REAL input channels (weight.shape[1]): zero-padded input
+        # channels (the MWT fusion conv's 54 -> 64) are not counted
+        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
         ctx.cap = L.current_cap()
         with L.launch_cap(ctx.cap):
             if bn_stats is not None:
@@ -227,7 +229,7 @@ class Conv2dFn(torch.autograd.Function):
             link.grad = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
-            work = {'flops': 2.0 * N * H * W * Cx * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
+            work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
             if skip is not None and L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
                 # the residual block's skip gradient added in the dgrad epilogue
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -248,7 +250,7 @@ class Conv2dFn(torch.autograd.Function):
             # the weight gradient on the wgrad stream (ewvit.grads) when the weights were used
             # once and hold no gradient; the MWT branch (capped grids, its own stream) keeps it
             s_kh, s_kw = wparam.stride()[2:]
-            defer = ctx.cap == 0 and s_kh == k * s_kw and 2.0 * N * Ho * Wo * Cout * k * k * Cx >= grads.DEFER_MIN_FLOPS and \
+            defer = ctx.cap == 0 and s_kh == k * s_kw and 2.0 * N * Ho * Wo * Cout * k * k * Cin >= grads.DEFER_MIN_FLOPS and \
                 grads.deferrable(wparam if ctx.needs_input_grad[1] else None, bparam if want_b else None)
             if defer:
                 with torch.cuda.stream(grads.defer_begin(dev, xc, dyc)):
@@ -282,7 +284,7 @@ class Conv2dFn(torch.autograd.Function):
             dbf = grad_out(bparam)
             if dbf.dim() != 1 or not dbf.is_contiguous():
                 dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
-        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cx, 'bytes': (dyc.numel() + xc.numel()) * 2}
+        work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (dyc.numel() + xc.numel()) * 2}
         L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
                Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
         return (dwf if ctx.needs_input_grad[1] else None), dbf

@@ -258,6 +258,7 @@ class TrainStep:
         self._started = False
         self.g2 = None
         self.fallback = None
+        self._capturing = False
         if self.graph and self.buckets is not None and self.buckets.defer:
             self._capture_split(warmup)
         elif self.graph:
@@ -265,7 +266,13 @@ class TrainStep:
                 self._capture(warmup)
             except Exception as e:          # noqa: BLE001 — a backend that cannot record collectives
                 if self.buckets is None or os.environ.get('EWVIT_GRAPH_SPLIT_FALLBACK', '0') != '1':
-                    self.close()             # no gradient hooks / slots left behind on the parameters
+                    import sys
+                    import traceback
+                    print('TrainStep: graph capture failed:', file=sys.stderr)
+                    traceback.print_exc()
+                    sys.stderr.flush()
+                    if not self._capturing:  # (inside a failed capture, freeing memory can abort)
+                        self.close()         # no gradient hooks / slots left behind on the parameters
                     raise
                 import sys
                 print(f'TrainStep: capturing the collectives failed ({type(e).__name__}: {e}); '
@@ -277,7 +284,18 @@ class TrainStep:
                 self._capture_split(warmup)
 
     def close(self):
-        """Detach from the model: remove the gradient hooks and slots of the buckets."""
+        """Release the captured graphs (after the device has drained them) and detach from the
+        model: remove the gradient hooks and slots of the buckets.  Call it while the process
+        group is still alive — a graph holding RCCL collectives releases communicator
+        resources when it is destroyed — before ``destroy_process_group``."""
+        if getattr(self, 'g', None) is not None or getattr(self, 'g2', None) is not None:
+            torch.cuda.synchronize()
+            for name in ('g', 'g2'):
+                gr = getattr(self, name, None)
+                if gr is not None:
+                    gr.reset()
+                    setattr(self, name, None)
+            torch.cuda.synchronize()
         if self.buckets is not None:
             self.buckets.remove()
             self.buckets = None
@@ -348,8 +366,13 @@ class TrainStep:
             # the host seeds the recorded dropout launches bake in come from the CPU generator
             # (ewvit.ops._seed); its state at capture lets a caller reproduce a replay eagerly
             self.capture_cpu_rng = torch.get_rng_state()
-            with torch.cuda.graph(self.g, stream=side):
+            # thread-local capture: CUDA calls of other threads (the process group's watchdog
+            # querying its collectives' events, a data-loader thread) neither fail nor
+            # invalidate the capture, as they can in the default global mode
+            self._capturing = True
+            with torch.cuda.graph(self.g, stream=side, capture_error_mode='thread_local'):
                 self.loss = self._iteration()
+            self._capturing = False
             self._finish_capture(self.g)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -366,13 +389,15 @@ class TrainStep:
             torch.cuda.synchronize()
             self.opt.zero_grad(set_to_none=True)
             self.g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g, stream=side):
+            self._capturing = True
+            with torch.cuda.graph(self.g, stream=side, capture_error_mode='thread_local'):
                 self.buckets.begin()
                 self.loss = self._fwd_bwd()
                 self.buckets.finish()
             self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool()):
+            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool(), capture_error_mode='thread_local'):
                 self.opt.step()
+            self._capturing = False
             self._finish_capture(self.g2)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()

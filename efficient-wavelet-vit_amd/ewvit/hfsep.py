@@ -1,0 +1,103 @@
+"""The MWT seperate convs on csrc/hfsep.hip (reference network/mwt.py:48-59, 84-86).
+
+``hf_conv['seperate'][g]`` is Conv2d(3, 18, 3, padding=1) on colour g's three HF bands, the
+weights shared by every DWT level (mwt.py:108): a grouped conv, 3 x (3 -> 18), 1458 MACs per
+pixel.  ``seperate_conv`` runs all levels in one launch, reading the three modules' fp32
+weights and biases directly, and — in training — leaves the per-level BatchNorm partial
+statistics of its output for the grouped BN + ReLU that follows (network/mwt.py), so that BN
+runs its apply pass only.  The backward computes the six parameter gradients (the HF input
+never needs one: the frames do not require grad, SURVEY §8a note 7) in one pass over dy and x
+plus a small fixed-order reduce.
+"""
+import torch
+
+from . import _lib as L
+from . import grads
+from .grads import grad_out
+
+MACS_PER_PIXEL = 3 * 18 * 27
+
+
+class SeperateConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, levels, shift, w0, w1, w2, b0, b1, b2):
+        L.require_gpu(x, w0)
+        params = (w0, w1, w2, b0, b1, b2)
+        for i, p in enumerate(params):
+            if ctx.needs_input_grad[3 + i]:
+                grads.note_use(p)
+        NL, C, H, W = x.shape
+        if C != 16 or NL % levels or x.dtype != torch.bfloat16:
+            raise ValueError(f'seperate_conv: input {tuple(x.shape)} {x.dtype} (want [L*N, 16, H, W] bf16)')
+        for w in (w0, w1, w2):
+            if tuple(w.shape) != (18, 3, 3, 3) or w.dtype != torch.float32:
+                raise ValueError(f'seperate_conv: weight {tuple(w.shape)} {w.dtype}')
+        xc = x.contiguous(memory_format=torch.channels_last)
+        N = NL // levels
+        ws = [t.detach().contiguous() for t in params]
+        y = torch.empty((NL, 64, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        ctx.cap = L.current_cap()
+        with L.launch_cap(ctx.cap):
+            part = shifts = sh = None
+            nparts = 0
+            if shift is not None:
+                nparts = int(L.load().ewvit_hfsep_fwd_parts(levels, N, H, W))
+                part = torch.empty(levels, nparts, 128, dtype=torch.float32, device=x.device)
+                shifts = torch.empty(levels, 64, dtype=torch.float32, device=x.device)
+                sh = shift.detach().float().contiguous()
+            npx = NL * H * W
+            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, *[L.ptr(t) for t in ws], L.ptr(sh),
+                   L.ptr(part), L.ptr(shifts), nparts, L.stream(y),
+                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+        ctx.save_for_backward(xc)
+        ctx.params = params
+        outs = (y,) if shift is None else (y, part, shifts)
+        for t in outs[1:]:
+            ctx.mark_non_differentiable(t)
+        return outs if shift is not None else y
+
+    @staticmethod
+    def backward(ctx, dy, *_):
+        with L.launch_cap(L.bwd_cap(ctx.cap)):
+            (xc,) = ctx.saved_tensors
+            NL, _, H, W = xc.shape
+            dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            outs = []
+            for i, p in enumerate(ctx.params):
+                if ctx.needs_input_grad[3 + i]:
+                    g = grad_out(p)
+                    if not g.is_contiguous():
+                        g = torch.empty_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+                    outs.append(g)
+                else:
+                    outs.append(None)
+            ws = torch.empty(int(L.load().ewvit_hfsep_bwd_weight_workspace(NL, H, W)) // 4, dtype=torch.float32,
+                             device=xc.device)
+            npx = NL * H * W
+            L.call('ewvit_hfsep_bwd_weight', L.ptr(xc), L.ptr(dyc), NL, H, W, *[L.ptr(t) for t in outs], L.ptr(ws),
+                   L.stream(dyc), work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+        return (None, None, None) + tuple(outs)
+
+
+def seperate_conv(x, levels, convs, shift=None):
+    """x [levels*N, 16, H, W] bf16 (channels-last storage; channel 3g+ci of colour g) ->
+    y [levels*N, 64, H, W] bf16 (channel 18g+o, 54..63 zero) with the three Conv2d modules'
+    parameters; with ``shift`` (the concatenated BatchNorm running means, training) also
+    (part [levels, nparts, 128], shifts [levels, 64], nparts) for ewvit.bn partials."""
+    ws = [c.weight for c in convs]
+    bs = [c.bias for c in convs]
+    if shift is None:
+        return SeperateConvFn.apply(x, int(levels), None, *ws, *bs)
+    y, part, shifts = SeperateConvFn.apply(x, int(levels), shift, *ws, *bs)
+    return y, (part, shifts, part.shape[1])
+
+
+def applies(x, convs):
+    """The shape class of seperate_conv: bf16 16-channel HF input on the GPU, three
+    Conv2d(3, 18, 3, padding=1) with biases, no hooks."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 16 and x.shape[3] <= 200
+            and len(convs) == 3 and all(
+                type(c) is torch.nn.Conv2d and tuple(c.weight.shape) == (18, 3, 3, 3) and c.bias is not None
+                and c.stride == (1, 1) and c.padding == (1, 1) and c.dilation == (1, 1) and c.groups == 1
+                and c.weight.dtype == torch.float32 and not (c._forward_hooks or c._forward_pre_hooks)
+                for c in convs))

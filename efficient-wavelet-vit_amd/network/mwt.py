@@ -15,7 +15,9 @@ Hot path on MI355X:
   channel concatenation in place (no torch.cat of mwt.py:112 in HBM);
 * BatchNorm + ReLU are one fused ewvit pass (csrc/batchnorm.hip).
 The seperate conv (9 band channels, zero-padded to 16 by the upsample pass -> 54
-channels, zero-padded to 64) runs on the same MFMA conv (one block-diagonal conv).
+channels, zero-padded to 64) runs as the grouped conv it is on csrc/hfsep.hip, its
+BatchNorm statistics summed in the same pass (ewvit.hfsep); fp32 / other shapes take one
+block-diagonal conv.
 
 If ``wavelet_transform`` is overridden on the instance or class (as
 utils/visualize_feature_maps.py:151-158 does), forward falls back to the
@@ -140,16 +142,19 @@ class _GroupBN:
             p = self.pads[(n, dev)] = (torch.ones(n, device=dev), torch.zeros(n, device=dev))
         return p
 
-    def __call__(self, x, bns, training, pad=0, levels=1):
-        ones, zeros = self._pad(pad, x.device) if pad else (None, None)
+    def params(self, bns, pad, dev):
+        """(weight, bias, running_mean, running_var) of the grouped BN: the modules' tensors
+        concatenated with the identity padding."""
+        ones, zeros = self._pad(pad, dev) if pad else (None, None)
         ext = (lambda ts, c: ts + [c]) if pad else (lambda ts, c: ts)
-        w = torch.cat(ext([b.weight for b in bns], ones))
-        bi = torch.cat(ext([b.bias for b in bns], zeros))
-        rm = torch.cat(ext([b.running_mean for b in bns], zeros))
-        rv = torch.cat(ext([b.running_var for b in bns], ones))
+        return (torch.cat(ext([b.weight for b in bns], ones)), torch.cat(ext([b.bias for b in bns], zeros)),
+                torch.cat(ext([b.running_mean for b in bns], zeros)), torch.cat(ext([b.running_var for b in bns], ones)))
+
+    def __call__(self, x, bns, training, pad=0, levels=1, partials=None, cat=None):
+        w, bi, rm, rv = cat if cat is not None else self.params(bns, pad, x.device)
         b0 = bns[0]
         y = ewvit.batch_norm_act_params(x, w, bi, rm, rv, training, b0.momentum, b0.eps, 'relu',
-                                        levels if training else 1)
+                                        levels if training else 1, partials=partials if training else None)
         if training:
             dst, src, off = [], [], 0
             for b in bns:
@@ -162,10 +167,11 @@ class _GroupBN:
         return y
 
 
-def bn_relu_groups(x, bns, training, pad=0, levels=1, state=None):
+def bn_relu_groups(x, bns, training, pad=0, levels=1, state=None, partials=None, cat=None):
     """One fused BN + ReLU over the channel groups of `bns` (see _GroupBN); `state` keeps the
-    grouped buffers between calls."""
-    return (state if state is not None else _GroupBN())(x, bns, training, pad, levels)
+    grouped buffers between calls; `partials` (training): the batch statistics summed by the
+    producing conv, with `cat` the grouped parameters the conv centred them on."""
+    return (state if state is not None else _GroupBN())(x, bns, training, pad, levels, partials, cat)
 
 
 def _cdt():
@@ -235,6 +241,23 @@ class MWT(nn.Module):
         hf = ewvit.dwt_hf_features(x, Lv, out_hw, out_dtype=cdt, out_channels=cpad)
         hf = hf.view(Lv * B, out_hw[0], out_hw[1], cpad).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
         sep = self.hf_conv['seperate']
+        if not hasattr(self, '_sep_bn'):
+            self._sep_bn = _GroupBN()
+        c18 = 18 * C
+        pad = (-c18) % 64
+        convs = [sep[i][0] for i in range(3)]
+        if C == 3 and cpad == 16 and ewvit.hfsep.applies(hf, convs):
+            # the grouped conv on csrc/hfsep.hip: 3 x (3 -> 18) for all levels in one launch,
+            # 54 channels + 10 zero channels out (whole 64-channel K slices for the fusion
+            # conv), the BatchNorm statistics per level summed on the way (training)
+            bns = [sep[i][1] for i in range(3)]
+            cat = self._sep_bn.params(bns, pad, hf.device)
+            if self.training:
+                y, partials = ewvit.hfsep.seperate_conv(hf, Lv, convs, shift=cat[2])
+            else:
+                y, partials = ewvit.hfsep.seperate_conv(hf, Lv, convs), None
+            y = bn_relu_groups(y, bns, self.training, pad, Lv, self._sep_bn, partials, cat)
+            return self._fusion(y, Lv, B)
         # seperate[i] sees colour i's 3C/3 = C band channels: a groups=3 conv.  It is
         # issued as ONE dense conv with a block-diagonal weight (zeros contribute
         # exact zeros): MIOpen's grouped weight-gradient kernel took ~0.3 s here.
@@ -244,8 +267,6 @@ class MWT(nn.Module):
         # kernel whole 64-channel K-tiles: emit the 18C seperate channels zero-padded
         # to a multiple of 64 (zero weight rows and bias; an identity BN keeps them
         # exactly 0 through BN + ReLU, and the fusion weight's padded rows are zero)
-        c18 = 18 * C
-        pad = (-c18) % 64
         if pad:
             w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, pad))
             b = F.pad(b, (0, pad))
@@ -254,9 +275,11 @@ class MWT(nn.Module):
         else:
             y = F.conv2d(hf, w.to(hf.dtype), b.to(hf.dtype), padding=1)
         # BN + ReLU of all levels in one fused launch, per-level statistics
-        if not hasattr(self, '_sep_bn'):
-            self._sep_bn = _GroupBN()
         y = bn_relu_groups(y, [sep[i][1] for i in range(3)], self.training, pad, Lv, self._sep_bn)
+        return self._fusion(y, Lv, B)
+
+    def _fusion(self, y, Lv, B):
+        """hf_conv['fusion'] (mwt.py:60-65, 87-88) over all levels, per-level BN statistics."""
         fus = self.hf_conv['fusion']
         r = _epi_stats(fus[0], fus[1], y, groups=Lv)
         if r is not None:

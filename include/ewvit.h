@@ -485,6 +485,29 @@ int ewvit_combined_loss(const float *logits, const float *labels, const float *s
                         int64_t D, const float *pos_weight, const float *weight, float lam, float *out,
                         float *d_logits, float *d_space, float *d_freq, void *stream);
 
+/* ----------------------------------------------------- MWT seperate convs (csrc/hfsep.hip) ---
+ * hf_conv['seperate'][g] for g = 0..2 (reference network/mwt.py:48-59: Conv2d(3, 18, 3, pad 1) per
+ * colour, applied to channels 3g..3g+2 of the level's HF input at mwt.py:84-86, weights shared by the
+ * levels, mwt.py:108) for every level in one launch — the grouped conv it is (1458 MACs per pixel).
+ *   x   [L*N][H][W][16] bf16 channels-last, level-major (ewvit_dwt_hf_upsample_fused with 16 output
+ *       channels: channel 3g+ci real for g, ci < 3, channels 9..15 zero)
+ *   y   [L*N][H][W][64] bf16: channel 18g+o for o < 18; channels 54..63 written as zero
+ *   w_g [18][3][3][3] fp32, b_g [18] fp32 (the three modules' parameters, contiguous)
+ * ewvit_hfsep_fwd also leaves, when bn_part is not NULL, the BatchNorm partial statistics of the
+ * bf16 y per level for ewvit_bn_fwd_partials (groups = L): bn_part [L][nparts][128] (sum (y - K),
+ * sum (y - K)^2 per channel, K = bn_shift[c] for c < 54 (NULL: 0), else 0) and bn_shift_out [L][64]
+ * = K; nparts must equal ewvit_hfsep_fwd_parts(L, N, H, W) under the same grid cap.
+ * ewvit_hfsep_bwd_weight overwrites dw_g [18][3][3][3] and db_g [18] (any may be NULL) from dy
+ * [L*N][H][W][64] bf16 and x; workspace: ewvit_hfsep_bwd_weight_workspace(L*N, H, W) bytes.
+ * W <= 512. */
+int64_t ewvit_hfsep_fwd_parts(int64_t L, int64_t N, int64_t H, int64_t W);
+int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int64_t H, int64_t W, const float *w0,
+                    const float *w1, const float *w2, const float *b0, const float *b1, const float *b2,
+                    const float *bn_shift, float *bn_part, float *bn_shift_out, int nparts, void *stream);
+int64_t ewvit_hfsep_bwd_weight_workspace(int64_t NI, int64_t H, int64_t W);
+int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, float *dw0, float *dw1,
+                           float *dw2, float *db0, float *db1, float *db2, float *workspace, void *stream);
+
 /* ------------------------------------------------------ frames (input side) ---
  * The per-frame transform chain of config/transforms.py:81-113 applied by the datasets'
  * __getitem__ (config/data_loader.py:325-337: cv2.imread -> BGR2RGB -> transform(frame) per

@@ -89,6 +89,8 @@ def test_rccl_collectives_recorded_in_step_graph(nccl_world1):
     flat = sb.buckets.flat
     assert all(flat.data_ptr() <= p.grad.data_ptr() < flat.data_ptr() + 4 * flat.numel()
                for p in b.parameters() if p.requires_grad)
+    sa.close()
+    sb.close()                                # the RCCL-holding graph released while the group lives
 
 
 def test_capture_failure_raises_without_opt_in(nccl_world1, monkeypatch):
@@ -116,6 +118,7 @@ def test_capture_failure_raises_without_opt_in(nccl_world1, monkeypatch):
     assert 'simulated' in d['capture_fallback'] and d['overlap'] == 'one all-reduce between two graphs'
     s()
     torch.cuda.synchronize()
+    s.close()
 
 
 def _snapshot(step):
@@ -200,6 +203,7 @@ def test_bench_shape_graph_step_equals_eager(nccl_world1):
     assert g is not None and g.shape == pe.shape
     rows = g.reshape(64, -1).abs().amax(1)
     assert bool((rows > 0).all()), f'rows without gradient: {(rows == 0).nonzero().flatten().tolist()}'
+    step.close()
 
 
 def test_adam_load_state_dict_after_capture_follows_loaded_state():
