@@ -426,6 +426,13 @@ def main():
             res['roofline_hot'] = hot
             res['top_launch_configs'] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
                                          for r in shapes[:12]]
+        if 'ewvit_gemm' in table:
+            # MFMA utilisation of the token path's GEMMs (ViT attention / MLP projections,
+            # cross-attention, patch_to_embedding, heads: north_star's attention/MLP figure)
+            tg = roofline_for('ewvit_gemm', table['ewvit_gemm'], args.config, aps)
+            tg['timing'] = res['roofline']['timing'] if res.get('roofline') else None
+            tg['launches_per_step'] = table['ewvit_gemm']['per_step']
+            res['token_gemm_roofline'] = tg
         res['kernels'] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                           for k, v in sorted(table.items(), key=lambda kv: -kv[1]['total_ms'])}
         fe = next((e for e in ('ewvit_dwt_hf_upsample_fused', 'ewvit_dwt_haar_fwd') if e in table), None)

@@ -183,16 +183,21 @@ __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict
 }
 
 // ---------------------------------------------------------------- weight gradient
-// dy image: rows of the band's pixels (Pk = TH*W rounded up to 32; rows past the band are
-// zero), 128 B each, 16-B chunk c of row r at chunk c ^ dsw(r): the transposed reads of one
-// 32-lane half (rows k0 + q and k0 + 8 + q, q < 4, of one 16-channel column pair) hit 64
-// distinct banks.  x image: the band's rows plus a halo row above and below, each with a
-// zero column either side, 32 B per pixel, halo pixel h at slot h + 8 (h >> 4) + 4 ((h >> 3)
-// & 1) (pixels 8 apart land 32 banks apart), then one zero pixel for the padding rows.
-__device__ __forceinline__ int hs_dsw(int r) { return (((r >> 1) & 1) | ((r >> 2) & 2)) << 1; }
-__device__ __forceinline__ int hs_slot(int h) { return h + 8 * (h >> 4) + 4 * ((h >> 3) & 1); }
+// GEMM view: C[co][tap*16 + c] = sum_p dy[p][co] x[pix(p, tap)][c] over the band's pixels.
+// K order inside a 32-pixel K-step: MFMA k = 8g + 4hh + q (g = lane >> 4, hh = lo / hi
+// read, q < 4) is pixel p0 + 4g + 16hh + q, so the two 16-lane groups of a 32-lane half
+// read 8 consecutive pixels — x rows (32 B) then hit 64 distinct banks without a swizzle,
+// and the dy rows (128 B) with the chunk XOR dsw(r) = 2((r >> 1) & 3).
+// dy image: Pk rows (the band's TH*W pixels rounded up to 32; rows past the band zero).
+// x image: the band's rows plus a halo row above and below, each W + 2 pixels with a zero
+// column either side, 32 B per pixel; one zero pixel after them for the padding rows.
+// The next band's global loads are issued into registers before the current band's MFMAs
+// (one register stage), then written to LDS after them.
+__device__ __forceinline__ int hs_dsw(int r) { return ((r >> 1) & 3) << 1; }
 
-template <int TH>
+// DYI / XI: register-staged 16-B pieces per thread (dy, x): 7 / 4 cover W <= 112 at TH = 2
+// (the MWT's 112^2 levels), 13 / 7 cover W <= 200 (config 4's 192^2)
+template <int TH, int DYI, int XI>
 __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy,
                                                           float *__restrict__ part, int NI, int H, int W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char hs_smem[];
@@ -201,74 +206,102 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
   const int Wp = W + 2;
   const int Pk = (TH * W + 31) & ~31;
   const int nhalo = (TH + 2) * Wp;
-  const int zslot = hs_slot(nhalo - 1) + 1;                   // the zero pixel
   unsigned char *dimg = hs_smem;
   unsigned char *ximg = hs_smem + Pk * 128;
-  // transposed-read lane roles (T10): lane 4q + pp of each 16-lane group gives row q,
-  // columns 4pp .. 4pp + 3 of a 4 x 16 block
+  const int zoff = nhalo * 32;                                // the zero pixel
   const int gq = (lane & 15) >> 2, gp = lane & 3, grp = lane >> 4;
+  const int chk = 2 * wv + (gp >> 1);
   hf32x4 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = hf32x4{0.f, 0.f, 0.f, 0.f};
-  if (tid < 2) *reinterpret_cast<uint4 *>(ximg + zslot * 32 + tid * 16) = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < 2) *reinterpret_cast<uint4 *>(ximg + zoff + tid * 16) = make_uint4(0u, 0u, 0u, 0u);
   const int nbh = (H + TH - 1) / TH, nbands = NI * nbh;
-  for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
+  const int ndy = Pk * 8, nx = nhalo * 2;
+  uint4 rd[DYI], rx[XI];
+  auto fetch = [&](int band) {
     const int img = band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
     const int Pb = rows * W;
-    __syncthreads();                               // the previous band's readers are done
     const bf16_t *dsrc = dy + ((int64_t)img * H + r0) * W * HS_COUT;
-    for (int i = tid; i < Pk * 8; i += 256) {
-      const int r = i >> 3, c = i & 7;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (r < Pb) v = *reinterpret_cast<const uint4 *>(dsrc + (int64_t)r * HS_COUT + c * 8);
-      *reinterpret_cast<uint4 *>(dimg + r * 128 + 16 * (c ^ hs_dsw(r))) = v;
-    }
-    for (int i = tid; i < nhalo * 2; i += 256) {
-      const int h = i >> 1, c = i & 1;
-      const int hr = h / Wp, hc = h - hr * Wp;
-      const int ir = r0 - 1 + hr, ic = hc - 1;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if ((unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && hr < rows + 2) {
-        v = *reinterpret_cast<const uint4 *>(x + (((int64_t)img * H + ir) * W + ic) * HS_CIN + c * 8);
-        if (c == 1) v.w = (v.w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
-      }
-      *reinterpret_cast<uint4 *>(ximg + hs_slot(h) * 32 + c * 16) = v;
-    }
-    __syncthreads();
-    for (int k0 = 0; k0 < Pk; k0 += 32) {
-      // rows of this lane's two transposed reads: pixels k0 + 8 grp + gq (+ 4)
-      hs4 alo, ahi;
-      int xs[2];
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int pr = k0 + 8 * grp + 4 * hh + gq;
-        const int chk = 2 * wv + (gp >> 1);
-        const hs4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) hs4 *)(dimg + pr * 128 + 16 * (chk ^ hs_dsw(pr)) + 8 * (gp & 1)));
-        if (hh == 0) alo = v; else ahi = v;
-        if (pr < Pb) {
-          const int rr = pr / W, cc = pr - rr * W;
-          xs[hh] = rr * Wp + cc;                   // halo pixel of tap (0, 0)
-        } else {
-          xs[hh] = -1;
+    for (int k = 0; k < DYI; ++k) {
+      const int i = tid + 256 * k;
+      rd[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < ndy && (i >> 3) < Pb) rd[k] = *reinterpret_cast<const uint4 *>(dsrc + (int64_t)(i >> 3) * HS_COUT + (i & 7) * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + 256 * k;
+      rx[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < nx) {
+        const int h = i >> 1, c = i & 1;
+        const int hr = h / Wp, hc = h - hr * Wp;
+        const int ir = r0 - 1 + hr, ic = hc - 1;
+        if ((unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && hr < rows + 2) {
+          rx[k] = *reinterpret_cast<const uint4 *>(x + (((int64_t)img * H + ir) * W + ic) * HS_CIN + c * 8);
+          if (c == 1) rx[k].w = (rx[k].w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
         }
       }
+    }
+  };
+  if ((int)blockIdx.x < nbands) fetch(blockIdx.x);
+  for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
+    const int rows = H - (band % nbh) * TH < TH ? H - (band % nbh) * TH : TH;
+    const int Pb = rows * W;
+    __syncthreads();                               // the previous band's readers are done
+#pragma unroll
+    for (int k = 0; k < DYI; ++k) {
+      const int i = tid + 256 * k;
+      if (i < ndy) *reinterpret_cast<uint4 *>(dimg + (i >> 3) * 128 + 16 * ((i & 7) ^ hs_dsw(i >> 3))) = rd[k];
+    }
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + 256 * k;
+      if (i < nx) *reinterpret_cast<uint4 *>(ximg + i * 16) = rx[k];
+    }
+    __syncthreads();
+    if (band + (int)gridDim.x < nbands) fetch(band + gridDim.x);   // in flight under the MFMAs
+    // this lane's pixels of K-step 0: lo p = 4 grp + gq, hi p + 16; tracked as (row, col)
+    int pr[2], rr[2], cc[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      pr[hh] = 4 * grp + 16 * hh + gq;
+      rr[hh] = pr[hh] / W;
+      cc[hh] = pr[hh] - rr[hh] * W;
+    }
+    for (int k0 = 0; k0 < Pk; k0 += 32) {
+      hs4 av[2];
+      int xb[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = pr[hh];
+        av[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) hs4 *)(dimg + r * 128 + 16 * (chk ^ hs_dsw(r)) + 8 * (gp & 1)));
+        xb[hh] = r < Pb ? (rr[hh] * Wp + cc[hh]) * 32 + 8 * gp : zoff + 8 * gp;   // tap (0, 0)
+      }
       const hbf16x8 af = __builtin_bit_cast(hbf16x8, (__attribute__((ext_vector_type(8))) short){
-                                                         alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]});
+                                                         av[0][0], av[0][1], av[0][2], av[0][3], av[1][0], av[1][1], av[1][2], av[1][3]});
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int kh = tap / 3, kw = tap - kh * 3;
+        const int toff = (kh * Wp + kw) * 32;
         hs4 b[2];
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int s = xs[hh] >= 0 ? hs_slot(xs[hh] + kh * Wp + kw) : zslot;
+        for (int hh = 0; hh < 2; ++hh)
           b[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) hs4 *)(ximg + s * 32 + 8 * gp));
-        }
+              (__attribute__((address_space(3))) hs4 *)(ximg + (pr[hh] < Pb ? xb[hh] + toff : xb[hh])));
         const hbf16x8 bf = __builtin_bit_cast(hbf16x8, (__attribute__((ext_vector_type(8))) short){
                                                            b[0][0], b[0][1], b[0][2], b[0][3], b[1][0], b[1][1], b[1][2], b[1][3]});
         acc[tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[tap], 0, 0, 0);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        pr[hh] += 32;
+        cc[hh] += 32;
+        while (cc[hh] >= W) {
+          cc[hh] -= W;
+          ++rr[hh];
+        }
       }
     }
   }
@@ -328,15 +361,15 @@ static int hs_wg_th() {
   static const int th = [] {
     const char *e = getenv("EWVIT_HFSEP_WG_TH");
     const int v = e ? atoi(e) : 2;
-    return v == 4 ? 4 : 2;
+    return v == 1 ? 1 : 2;
   }();
   return th;
 }
 static int hs_wg_blocks(int64_t NI, int64_t H) {
   static const int maxb = [] {
     const char *e = getenv("EWVIT_HFSEP_WG_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v > 0 && v <= 4096 ? v : 512;
+    const int v = e ? atoi(e) : 768;          // 3 resident per CU
+    return v > 0 && v <= 4096 ? v : 768;
   }();
   const int th = hs_wg_th();
   return hs_blocks(NI * ((H + th - 1) / th), maxb);
@@ -355,8 +388,17 @@ extern "C" int64_t ewvit_hfsep_fwd_parts(int64_t L, int64_t N, int64_t H, int64_
   const int th = hs_fwd_th();
   const int64_t bands = N * ((H + th - 1) / th);
   // one partial row per workgroup of the level (<= 256: the BatchNorm apply pass finalises
-  // from them directly); under a grid cap the levels share it
-  int64_t g = bands < 256 ? bands : 256;
+  // from them directly); all levels together one round of resident workgroups (2 per CU at
+  // this kernel's register use), so no level's tail waits for a second round; under a grid
+  // cap the levels share it
+  static const int fwdb = [] {
+    const char *e = getenv("EWVIT_HFSEP_FWD_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 && v <= 4096 ? v : 512;
+  }();
+  int64_t g = fwdb / L > 0 ? fwdb / L : 1;
+  if (g > 256) g = 256;
+  if (g > bands) g = bands;
   if (g_grid_cap > 0 && g * L > g_grid_cap) g = g_grid_cap / L > 0 ? g_grid_cap / L : 1;
   return g;
 }
@@ -393,22 +435,26 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
   const int th = hs_wg_th();
   const int G = hs_wg_blocks(NI, H);
   const int Pk = (int)((th * W + 31) & ~31);
-  const size_t lds = (size_t)Pk * 128 + (size_t)(((th + 2) * (W + 2) - 1) + 8 * (((th + 2) * (W + 2) - 1) >> 4) + 4 + 2) * 32;
-  EWVIT_CHECK_ARG(lds <= 96 * 1024, "hfsep_bwd_weight: W=%lld too wide", (long long)W);
+  // the register stage holds a band's pieces: DYI x 256 dy pieces, XI x 256 x pieces
+  const bool small = Pk * 8 <= 7 * 256 && (th + 2) * (W + 2) * 2 <= 4 * 256;
+  EWVIT_CHECK_ARG(small || (Pk * 8 <= 13 * 256 && (th + 2) * (W + 2) * 2 <= 7 * 256),
+                  "hfsep_bwd_weight: W=%lld too wide for TH=%d", (long long)W, th);
+  const size_t lds = (size_t)Pk * 128 + ((size_t)(th + 2) * (W + 2) + 1) * 32;
   hipStream_t s = as_stream(stream);
-  static const bool attr = [] {          // more than 64 KB of dynamic LDS needs the attribute
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<4>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
-           hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<2>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
-  }();
-  (void)attr;
-  if (th == 4)
-    hipLaunchKernelGGL(hfsep_wgrad_kernel<4>, dim3(G), dim3(256), lds, s, (const bf16_t *)x, (const bf16_t *)dy,
-                       workspace, (int)NI, (int)H, (int)W);
-  else
-    hipLaunchKernelGGL(hfsep_wgrad_kernel<2>, dim3(G), dim3(256), lds, s, (const bf16_t *)x, (const bf16_t *)dy,
-                       workspace, (int)NI, (int)H, (int)W);
+#define EWVIT_HS_WG(TH_, D_, X_)                                                                                 \
+  do {                                                                                                           \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_>), \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
+    (void)attr;                                                                                                  \
+    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,           \
+                       (const bf16_t *)dy, workspace, (int)NI, (int)H, (int)W);                                  \
+  } while (0)
+  if (th == 1) {
+    if (small) EWVIT_HS_WG(1, 7, 4); else EWVIT_HS_WG(1, 13, 7);
+  } else {
+    if (small) EWVIT_HS_WG(2, 7, 4); else EWVIT_HS_WG(2, 13, 7);
+  }
+#undef EWVIT_HS_WG
   int rc = launch_status("hfsep_bwd_weight");
   if (rc) return rc;
   HsParams out{{dw0, dw1, dw2}, {db0, db1, db2}};

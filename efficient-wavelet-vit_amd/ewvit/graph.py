@@ -259,6 +259,7 @@ class TrainStep:
         self.g2 = None
         self.fallback = None
         self._capturing = False
+        self._capture_mode = os.environ.get('EWVIT_CAPTURE_MODE', 'relaxed')
         if self.graph and self.buckets is not None and self.buckets.defer:
             self._capture_split(warmup)
         elif self.graph:
@@ -362,15 +363,18 @@ class TrainStep:
                 self._iteration()
             self.loss = None
             torch.cuda.synchronize()
+            self._drain_watchdog()
             self.g = torch.cuda.CUDAGraph()
             # the host seeds the recorded dropout launches bake in come from the CPU generator
             # (ewvit.ops._seed); its state at capture lets a caller reproduce a replay eagerly
             self.capture_cpu_rng = torch.get_rng_state()
-            # thread-local capture: CUDA calls of other threads (the process group's watchdog
-            # querying its collectives' events, a data-loader thread) neither fail nor
-            # invalidate the capture, as they can in the default global mode
+            # relaxed capture: CUDA calls of other threads — the process group's watchdog
+            # polling the events of the eager collectives that preceded the capture, a
+            # data-loader thread — must neither fail nor invalidate the capture.  In the
+            # default global mode the watchdog's event query errors and it aborts the process
+            # (seen intermittently on the GPU box; TORCH_NCCL_ASYNC_ERROR_HANDLING=0 hides it)
             self._capturing = True
-            with torch.cuda.graph(self.g, stream=side, capture_error_mode='thread_local'):
+            with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
                 self.loss = self._iteration()
             self._capturing = False
             self._finish_capture(self.g)
@@ -387,20 +391,30 @@ class TrainStep:
                 self._split_eager()
             self.loss = None
             torch.cuda.synchronize()
+            self._drain_watchdog()
             self.opt.zero_grad(set_to_none=True)
             self.g = torch.cuda.CUDAGraph()
             self._capturing = True
-            with torch.cuda.graph(self.g, stream=side, capture_error_mode='thread_local'):
+            with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
                 self.buckets.begin()
                 self.loss = self._fwd_bwd()
                 self.buckets.finish()
             self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool(), capture_error_mode='thread_local'):
+            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool(), capture_error_mode=self._capture_mode):
                 self.opt.step()
             self._capturing = False
             self._finish_capture(self.g2)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+
+    def _drain_watchdog(self):
+        """Before a capture with RCCL collectives: the process group's watchdog thread polls
+        the events of the eager collectives issued before it (every ~100 ms) and drops them
+        once it has seen them complete; give it that poll after the device has drained, so
+        it has nothing to query while the capture runs."""
+        if self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl':
+            import time
+            time.sleep(float(os.environ.get('EWVIT_CAPTURE_DRAIN_S', '0.3')))
 
     def _finish_capture(self, graph):
         fin = getattr(self.opt, 'finish_capture', None)
