@@ -9,6 +9,8 @@ runs its apply pass only.  The backward computes the six parameter gradients (th
 never needs one: the frames do not require grad, SURVEY §8a note 7) in one pass over dy and x
 plus a small fixed-order reduce.
 """
+import os
+
 import torch
 
 from . import _lib as L
@@ -92,10 +94,13 @@ def seperate_conv(x, levels, convs, shift=None):
     return y, (part, shifts, part.shape[1])
 
 
+_ON = os.environ.get('EWVIT_HFSEP', '1') != '0'      # 0: the block-diagonal dense conv (A/B)
+
+
 def applies(x, convs):
     """The shape class of seperate_conv: bf16 16-channel HF input on the GPU, three
     Conv2d(3, 18, 3, padding=1) with biases, no hooks."""
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 16 and x.shape[3] <= 200
+    return (_ON and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 16 and x.shape[3] <= 200
             and len(convs) == 3 and all(
                 type(c) is torch.nn.Conv2d and tuple(c.weight.shape) == (18, 3, 3, 3) and c.bias is not None
                 and c.stride == (1, 1) and c.padding == (1, 1) and c.dilation == (1, 1) and c.groups == 1
