@@ -22,8 +22,15 @@ sys.path.insert(0, os.path.join(REPO, 'efficient-wavelet-vit_amd'))
 
 
 class _NoOpt:
+    """No update; zero_grad drops the gradients like the real optimizer (else every replay
+    would add into .grad: ~480 accumulation kernels in the SFE piece)."""
+
+    def __init__(self, params=()):
+        self.params = list(params)
+
     def zero_grad(self, set_to_none=True):
-        pass
+        for p in self.params:
+            p.grad = None
 
     def step(self):
         pass
@@ -62,7 +69,7 @@ def main():
             with torch.autocast('cuda', dtype=torch.bfloat16):
                 y = fn()
             return y.float().square().mean()
-        return TrainStep(model, fl, _NoOpt(), graph=True)
+        return TrainStep(model, fl, _NoOpt(model.parameters()), graph=True)
     dama = model.dama
     out['mwt_ms'] = _time(piece(lambda: dama.mwt(x)), args.reps)
     cap = _mwt_grid_cap()

@@ -43,7 +43,7 @@ def main():
             with torch.autocast('cuda', dtype=torch.bfloat16):
                 y = fn()
             return y.float().square().mean()
-        return TrainStep(model, fl, _NoOpt(), graph=True)
+        return TrainStep(model, fl, _NoOpt(model.parameters()), graph=True)
 
     def capped():
         with ewvit._lib.grid_cap(160):

@@ -9,7 +9,8 @@ def main():
     path = sys.argv[1]
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    starts = [i for i, r in enumerate(rows) if 'dwt_multilevel' in r['Kernel_Name'] or 'dwt_hf_fused' in r['Kernel_Name']]
+    marks = [sys.argv[sys.argv.index('--marker') + 1]] if '--marker' in sys.argv else ['dwt_multilevel', 'dwt_hf_fused']
+    starts = [i for i, r in enumerate(rows) if any(m in r['Kernel_Name'] for m in marks)]
     k = int(sys.argv[sys.argv.index('--nth') + 1]) if '--nth' in sys.argv else 2
     a, b = starts[-k], starts[-k + 1] if k > 1 else len(rows)
     if '--largest' in sys.argv:     # the delimited span with the most kernels (a whole step)
@@ -19,7 +20,19 @@ def main():
     t0 = int(step[0]['Start_Timestamp'])
     t1 = int(step[-1]['End_Timestamp'])
     busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in step)
-    print(f'kernels {len(step)}  span {(t1 - t0) / 1e6:.3f} ms  busy {busy / 1e6:.3f} ms')
+    # busy = sum of kernel durations; union = time at least one kernel runs (overlap counted once)
+    union, cur_s, cur_e = 0, None, None
+    for r in sorted(step, key=lambda r: int(r['Start_Timestamp'])):
+        s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                union += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    union += (cur_e - cur_s) if cur_e is not None else 0
+    print(f'kernels {len(step)}  span {(t1 - t0) / 1e6:.3f} ms  busy {busy / 1e6:.3f} ms  union {union / 1e6:.3f} ms '
+          f'(idle {(t1 - t0 - union) / 1e6:.3f} ms)')
     agg = {}
     for r in step:
         n = r['Kernel_Name'].split('(')[0][:90]
