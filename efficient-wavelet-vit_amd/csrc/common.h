@@ -134,6 +134,31 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
+// derivative of a BatchNorm's activation at its pre-activation z (act 1 ReLU, 2 SiLU, else
+// identity) — the same operations as batchnorm.hip's act_grad, so producers that sum the
+// backward statistics in their epilogue round exactly as bn_bwd_reduce_kernel would
+__device__ __forceinline__ float bn_act_grad(int act, float z) {
+  if (act == 1) return z > 0.f ? 1.f : 0.f;
+  if (act == 2) {
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-z));
+    return s * (1.f + z * (1.f - s));
+  }
+  return 1.f;
+}
+
+// BatchNorm backward statistics left by the kernel that produces the BN output's gradient
+// (the consumer conv's input gradient): per partial row t and channel c, part[t][c] = sum g,
+// part[t][C + c] = sum g * xhat over the producer's tile rows, with xhat = (x - mean) * invstd
+// (x: the BN input, same layout as the gradient), g = d * act'(xhat * gamma + beta) (act) or
+// g = d * rscale[row / hw] (rscale: the drop-path factor of the MBConv tail); what
+// bn_bwd_dx_kernel finalises from (ewvit_bn_bwd_partials)
+struct BnBwdStats {
+  float *part = nullptr;
+  const bf16_t *x = nullptr;
+  const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr, *rscale = nullptr;
+  int act = 0, hw = 1;
+};
+
 inline bool dtype_ok(int dt) { return dt == EWVIT_F32 || dt == EWVIT_BF16; }
 
 // workgroup cap of the big-grid launches (abi.hip, ewvit_set_grid_cap); 0 = none

@@ -81,6 +81,10 @@ struct FwdArgs {
   int pc = -1, ntap = 0;
   int tapl[4] = {0, 0, 0, 0};
   int dstH = 0, dstW = 0;
+  // optional (LDS-DMA dgrad, plain NHWC dx, uncapped grid): the backward statistics of the
+  // BatchNorm(+act) whose output this conv read, summed over the bf16-rounded dx per m-tile
+  // (common.h BnBwdStats; bwd.part [m-tiles][2 Ncol])
+  BnBwdStats bwd;
 };
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
@@ -679,10 +683,13 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
 // A lane's chunk index is fixed per row, so it advances by 8 chunks per K-tile: tap +=
 // 8 / CC, cc += 8 % CC (CC = Cin / 8).  Zero waste but the last K-tile's tail (A past the
 // last tap reads through the OOB offset, B's tail meets only those zeros).
-template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2, bool DENSE = false>
+// BST (dgrad): the backward statistics of the BatchNorm before the conv (FwdArgs::bwd) in
+// the epilogue — its own instantiation, so the plain dgrad keeps its register budget
+template <bool DGRAD, int BM, int BN_, int KS, int NS, int WC = 2, bool DENSE = false, bool BST = false>
 __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a, int64_t src_bytes, int ntn,
                                                                       int tap_inner, int ntiles) {
   static_assert(!(DENSE && DGRAD), "dense K: forward only");
+  static_assert(!BST || DGRAD, "backward statistics: dgrad only");
   constexpr int NW = BM / 64 * WC, BK = 64;      // waves: BM/64 rows x WC columns
   constexpr int WN = BN_ / WC, J = WN / 16;
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
@@ -910,6 +917,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
   // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
   const bool stats = !DGRAD && a.bn_part != nullptr;
+  constexpr bool bstats = BST;
   int64_t opx[4];               // parity-class dgrad: the dx pixel of each of this lane's rows
   if (cls) {
 #pragma unroll
@@ -924,6 +932,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     }
   }
   float cs[J][4], cq[J][4];     // this lane's column sums over its 4 rows (BN statistics)
+  // BST: the stored bf16 values, kept for the statistics pass after the stores
+  uint2 hpk[BST ? J : 1][4];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int col = n0 + wn * WN + j * 16 + fq * 4;
@@ -953,6 +963,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
         *reinterpret_cast<uint2 *>(ob + opix * a.ogc) = pk;
+        if constexpr (BST) hpk[j][i] = pk;
         if (stats) {
           const float d0 = bf2f(h0) - kv.x, d1 = bf2f(h1) - kv.y, d2 = bf2f(h2) - kv.z, d3 = bf2f(h3) - kv.w;
           cs[j][0] += d0; cs[j][1] += d1; cs[j][2] += d2; cs[j][3] += d3;
@@ -962,7 +973,51 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
       }
     }
   }
-  if (stats) {
+  if constexpr (BST) {
+    // g = dx * act'(xhat * gamma + beta) (act) or dx * rscale[frame]; sums of g and g * xhat
+    // over the stored values, one column block at a time: its 4 BN-input loads and the BN
+    // parameters are issued together, so their latencies overlap
+    float brs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = m0 + wm * 64 + i * 16 + fr;
+      brs[i] = a.bwd.rscale && row < a.M ? a.bwd.rscale[row / a.bwd.hw] : 1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int col = n0 + wn * WN + j * 16 + fq * 4;
+      if (col >= a.Ncol) continue;
+      uint2 xq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + wm * 64 + i * 16 + fr;
+        xq[i] = row < a.M ? *reinterpret_cast<const uint2 *>(a.bwd.x + row * a.ogc + col) : make_uint2(0u, 0u);
+      }
+      const float4 mu4 = *reinterpret_cast<const float4 *>(a.bwd.mean + col);
+      const float4 iv4 = *reinterpret_cast<const float4 *>(a.bwd.invstd + col);
+      const float4 ga4 = a.bwd.gamma ? *reinterpret_cast<const float4 *>(a.bwd.gamma + col) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 be4 = a.bwd.beta ? *reinterpret_cast<const float4 *>(a.bwd.beta + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, iv[4] = {iv4.x, iv4.y, iv4.z, iv4.w};
+      const float ga[4] = {ga4.x, ga4.y, ga4.z, ga4.w}, be[4] = {be4.x, be4.y, be4.z, be4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + wm * 64 + i * 16 + fr;
+        if (row >= a.M) continue;
+        const float xv[4] = {__uint_as_float(xq[i].x << 16), __uint_as_float(xq[i].x & 0xffff0000u),
+                             __uint_as_float(xq[i].y << 16), __uint_as_float(xq[i].y & 0xffff0000u)};
+        const float hv[4] = {__uint_as_float(hpk[j][i].x << 16), __uint_as_float(hpk[j][i].x & 0xffff0000u),
+                             __uint_as_float(hpk[j][i].y << 16), __uint_as_float(hpk[j][i].y & 0xffff0000u)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xh = (xv[r] - mu[r]) * iv[r];
+          const float g = a.bwd.act ? hv[r] * bn_act_grad(a.bwd.act, fmaf(xh, ga[r], be[r])) : hv[r] * brs[i];
+          cs[j][r] += g;
+          cq[j][r] = fmaf(g, xh, cq[j][r]);
+        }
+      }
+    }
+  }
+  if (stats || bstats) {
   // BatchNorm partial statistics of this m-tile: the 16 row lanes of each column
   // (DPP row sums), then the BM/64 waves that share a column block through LDS, in order
 #pragma unroll
@@ -974,7 +1029,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     }
   // [BM/64][BN_][2] after the ring (the next tile's K-tiles are landing in it); its
   // previous tile's readers finished before this tile's K-loop barriers
-  float *red = reinterpret_cast<float *>(smem + NS * STG);
+  // (dgrad: no image after the ring — its partials go into ring slot 0 once every wave has
+  // finished reading it; an uncapped grid, so no next tile's K-tiles are landing there)
+  float *red = reinterpret_cast<float *>(smem + (DGRAD ? 0 : NS * STG));
+  if (DGRAD) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (fr == 0)
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -992,9 +1050,10 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 #pragma unroll
       for (int q = 0; q < BM / 64; ++q) { S += red[(q * BN_ + tid) * 2]; Q += red[(q * BN_ + tid) * 2 + 1]; }
       const int64_t t = m0 / BM;
-      a.bn_part[t * 2 * a.Ncol + col] = S;
-      a.bn_part[t * 2 * a.Ncol + a.Ncol + col] = Q;
-      if (t == 0 && a.bn_shift_out) a.bn_shift_out[col] = a.bn_shift ? a.bn_shift[col] : 0.f;
+      float *dst = DGRAD ? a.bwd.part : a.bn_part;
+      dst[t * 2 * a.Ncol + col] = S;
+      dst[t * 2 * a.Ncol + a.Ncol + col] = Q;
+      if (!DGRAD && t == 0 && a.bn_shift_out) a.bn_shift_out[col] = a.bn_shift ? a.bn_shift[col] : 0.f;
     }
   }
   }
@@ -1471,7 +1530,7 @@ static void launch_glds_dense(const FwdArgs &a, int64_t src_bytes, hipStream_t s
 // the LDS-DMA fwd/dgrad kernel when every K-tile stays in one tap and one channel
 // group and the operands fit 31-bit buffer offsets; false -> register-staged kernel
 template <bool DGRAD>
-static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
+static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int *bm_out = nullptr) {
   const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
   const bool padded = a.KCr && a.KCr != a.KC;     // plain x, channels padded to 64 per tap
   // ragged: plain (ungrouped) x whose per-tap K is not a multiple of 64 — the last
@@ -1526,6 +1585,7 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
   }();
   if (DGRAD && v == 1 && bn == 64 && dg256 > 0 && (a.M + 127) / 128 * ntn > dg256) v = 3;
   const int BM = (v == 3 || v == 4) ? 256 : 128;
+  if (bm_out) *bm_out = BM;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
@@ -1572,7 +1632,40 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s) {
     return e ? atoi(e) : 256;
   }();
   // (64-row tiles would change the BatchNorm partial rows fwd_bn_rows promised: not with bn_part)
-  if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part)) && nwg <= sgmax) vv = sg;
+  if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part && !a.bwd.part)) && nwg <= sgmax) vv = sg;
+  if constexpr (DGRAD) {
+    if (a.bwd.part) {
+      // the backward-statistics epilogue (its own instantiations): 128-row tiles always (the
+      // partial rows ewvit_conv2d_bwd_bn_rows promised), uncapped; the same tile / ring / wave
+      // choice as below otherwise
+      if (bm_out) *bm_out = 128;
+      const int64_t nt = (a.M + 127) / 128 * ntn;
+      if (nt >= (int64_t)1 << 31) return false;
+      const dim3 g1((unsigned)nt);
+#define EWVIT_GLDS_BST(BN__, NS_, WC_)                                                                              \
+  do {                                                                                                            \
+    if (a.g.ks == 1)                                                                                              \
+      hipLaunchKernelGGL((conv_glds_kernel<true, 128, BN__, 1, NS_, WC_, false, true>), g1, dim3(2 * WC_ * 64), 0, s, \
+                         a, src_bytes, ntn, tap_inner, (int)nt);                                                  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((conv_glds_kernel<true, 128, BN__, 3, NS_, WC_, false, true>), g1, dim3(2 * WC_ * 64), 0, s, \
+                         a, src_bytes, ntn, tap_inner, (int)nt);                                                  \
+  } while (0)
+      const bool w8 = nt <= w8max || (bn == 128 && dg8);
+      if (bn == 32) EWVIT_GLDS_BST(32, 2, 2);
+      else if (bn == 64) {
+        if (nt <= sgmax) EWVIT_GLDS_BST(64, 4, 4);
+        else if (w8) EWVIT_GLDS_BST(64, 2, 4);
+        else EWVIT_GLDS_BST(64, 2, 2);
+      } else {
+        if (nt <= sgmax) EWVIT_GLDS_BST(128, 4, 4);
+        else if (w8) EWVIT_GLDS_BST(128, 2, 4);
+        else EWVIT_GLDS_BST(128, 2, 2);
+      }
+#undef EWVIT_GLDS_BST
+      return true;
+    }
+  }
   if (bn == 32) {
     EWVIT_GLDS_FWD(128, 32, 2);
     return true;
@@ -1858,6 +1951,51 @@ extern "C" int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void 
   EWVIT_CHECK_ARG(dgrad_by_parity(a, sb, as_stream(stream)) || launch_glds<true>(a, sb, as_stream(stream)),
                   "conv2d_bwd_data_add: LDS-DMA kernel refused the shape");
   return launch_status("conv2d_bwd_data_add");
+}
+
+// partial rows ewvit_conv2d_bwd_data_bn leaves for this shape at most (one per 128 dx rows;
+// the launch reports the exact count), or 0 when the shape does not take it: stride 1, the
+// LDS-DMA dgrad (ewvit_conv2d_bwd_data_add_ok), no workgroup cap in force
+extern "C" int64_t ewvit_conv2d_bwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                           int stride) {
+  if (stride != 1 || g_grid_cap > 0 || !ewvit_conv2d_bwd_data_add_ok(N, H, W, Cin, Cout, ksize, stride) ||
+      Cin > 65536)
+    return 0;
+  return (N * H * W + 127) / 128;
+}
+
+// dx = dgrad(dy) (+ addend, when not null) and the backward statistics of the BatchNorm
+// whose output was this conv's input (bx: that BN's input [N,H,W,Cin] bf16; mean / invstd its
+// saved statistics; gamma / beta or null; act 0/1/2; rscale [N] with act 0: the drop-path
+// factor per frame of the MBConv tail, or null): part [ewvit_conv2d_bwd_bn_rows][2 Cin] gets
+// per 128- or 256-row m-tile (sum g, sum g * xhat) of the bf16-rounded dx; *nrc_out = the
+// partial rows written (what ewvit_bn_bwd_partials is given)
+extern "C" int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N,
+                                        int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                                        const void *bx, const float *mean, const float *invstd, const float *gamma,
+                                        const float *beta, int act, const float *rscale, float *part, int *nrc_out,
+                                        void *stream) {
+  EWVIT_CHECK_ARG(dy && wp_t && dx && bx && mean && invstd && part && nrc_out && act >= 0 && act <= 2 &&
+                      !(rscale && act),
+                  "conv2d_bwd_data_bn: bad args");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  if (int rc = check_geom(g, "conv2d_bwd_data_bn")) return rc;
+  EWVIT_CHECK_ARG(ewvit_conv2d_bwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) > 0,
+                  "conv2d_bwd_data_bn: shape not supported (query ewvit_conv2d_bwd_bn_rows)");
+  FwdArgs a;
+  a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx; a.g = g;
+  a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
+  a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
+  a.sgc = g.Cout; a.sgs = 0; a.ogc = g.Cin; a.ogs = 0;
+  a.addend = (const bf16_t *)addend;
+  a.bwd.part = part; a.bwd.x = (const bf16_t *)bx; a.bwd.mean = mean; a.bwd.invstd = invstd; a.bwd.gamma = gamma;
+  a.bwd.beta = beta; a.bwd.rscale = rscale; a.bwd.act = act; a.bwd.hw = (int)(H * W);
+  const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
+  int bm = 0;
+  EWVIT_CHECK_ARG(launch_glds<true>(a, sb, as_stream(stream), &bm) && bm > 0,
+                  "conv2d_bwd_data_bn: LDS-DMA kernel refused the shape");
+  *nrc_out = (int)((a.M + bm - 1) / bm);
+  return launch_status("conv2d_bwd_data_bn");
 }
 
 extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,

@@ -221,6 +221,162 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
   }
 }
 
+// ---- the row kernel with the BatchNorm sums of what it stores (MBConv: the BN after the
+// depthwise conv in the forward, the BN before it in the backward), so the BN needs no
+// statistics pass of its own.  Block = 32 output rows (n*Ho + ho, across frames) x 64
+// channels: thread tid walks row tid / 8 for channel vector tid % 8, exactly as
+// dw_row_bf16_kernel walks a row, and keeps its 8 channels' sums of the bf16-rounded
+// outputs; the block leaves ONE partial row (its 64 channels) at part[blockIdx.x]:
+//   ST 1 (forward): sum (y - K), sum (y - K)^2 with K = shift (or 0) — the shifted sums
+//        ewvit_bn_fwd_partials finalises; block row 0 copies K to shift_out
+//   ST 2 (input gradient of a stride-1 conv, ROT): sum g, sum g * xhat (BnBwdStats: g =
+//        dx * act'(xhat * gamma + beta), the gradient of the BN(+act) whose output the conv
+//        read) — what ewvit_bn_bwd_partials finalises
+// The 32 row sums of a channel are added in row order through LDS (deterministic).
+struct DwBnFwd {
+  float *part = nullptr;
+  const float *shift = nullptr;
+  float *shift_out = nullptr;
+};
+template <int STRIDE, bool ROT, int ST>
+__global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict__ x, const float *__restrict__ w,
+                                                        bf16_t *__restrict__ y, DwShape s, DwBnFwd f, BnBwdStats b) {
+  __shared__ float red[32 * 8 * 16];
+  const int tid = threadIdx.x, cv = tid & 7, r = tid >> 3;
+  const int C8 = s.C >> 3;
+  const int c8 = blockIdx.y * 8 + cv;
+  const int64_t row = (int64_t)blockIdx.x * 32 + r;          // n*Ho + ho
+  const bool active = c8 < C8 && row < (int64_t)s.N * s.Ho;
+  float sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+  if (active) {
+    const int ho = (int)(row % s.Ho);
+    const int n = (int)(row / s.Ho);
+    const int c = c8 * 8;
+    float wr[9][8];
+    {
+      const float4 *wp = reinterpret_cast<const float4 *>(w + (int64_t)c * 9);
+      float t[72];
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        const float4 q = wp[i];
+        t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wr[ROT ? 8 - k : k][j] = t[j * 9 + k];
+    }
+    float p0[8], p1[8], p2[8], p3[8];     // ST 1: K | ST 2: mean, invstd, gamma, beta
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (ST == 1) {
+        p0[j] = f.shift ? f.shift[c + j] : 0.f;
+      } else {
+        p0[j] = b.mean[c + j]; p1[j] = b.invstd[c + j];
+        p2[j] = b.gamma ? b.gamma[c + j] : 1.f; p3[j] = b.beta ? b.beta[c + j] : 0.f;
+      }
+    }
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    bool rok[3];
+    int64_t rbase[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hi = ho * STRIDE - s.pad + kh;
+      rok[kh] = hi >= 0 && hi < s.H;
+      rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
+    }
+    auto ld = [&](int kh, int col) -> uint4 {
+      if (!rok[kh] || col < 0 || col >= s.W) return zero;
+      return *reinterpret_cast<const uint4 *>(x + rbase[kh] + (int64_t)col * s.C);
+    };
+    uint4 win[3][3];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
+    const int64_t ybase = (row * s.Wo) * s.C + c;
+    // ST 2: the BN input at this output pixel, loaded one column ahead with the window's
+    // next column (a load consumed in the same iteration would expose its latency per column)
+    uint4 bxq = zero;
+    if (ST == 2) bxq = *reinterpret_cast<const uint4 *>(b.x + ybase);
+    for (int wo = 0; wo < s.Wo; ++wo) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          float v[8];
+          bf8_unpack(win[kw][kh], v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[j]);
+        }
+      unsigned o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (unsigned)f2bf(acc[2 * j]) | ((unsigned)f2bf(acc[2 * j + 1]) << 16);
+      const uint4 oq = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4 *>(y + ybase + (int64_t)wo * s.C) = oq;
+      float v[8];
+      bf8_unpack(oq, v);
+      if (ST == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[j] - p0[j];
+          sa[j] += d;
+          sb[j] = fmaf(d, d, sb[j]);
+        }
+      } else {
+        float xv[8];
+        bf8_unpack(bxq, xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - p0[j]) * p1[j];
+          const float g = b.act ? v[j] * bn_act_grad(b.act, fmaf(xh, p2[j], p3[j])) : v[j];
+          sa[j] += g;
+          sb[j] = fmaf(g, xh, sb[j]);
+        }
+      }
+      const int nb = (wo + 1) * STRIDE - s.pad;
+      if (STRIDE == 1) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          win[0][kh] = win[1][kh];
+          win[1][kh] = win[2][kh];
+          win[2][kh] = ld(kh, nb + 2);
+        }
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          win[0][kh] = win[2][kh];
+          win[1][kh] = ld(kh, nb + 1);
+          win[2][kh] = ld(kh, nb + 2);
+        }
+      }
+      if (ST == 2 && wo + 1 < s.Wo) bxq = *reinterpret_cast<const uint4 *>(b.x + ybase + (int64_t)(wo + 1) * s.C);
+    }
+  }
+  float *q = red + (r * 8 + cv) * 16;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { q[j] = sa[j]; q[8 + j] = sb[j]; }
+  __syncthreads();
+  if (tid < 64) {
+    const int v = tid >> 3, j = tid & 7;
+    const int c = (blockIdx.y * 8 + v) * 8 + j;
+    float A = 0.f, B = 0.f;
+    for (int rr = 0; rr < 32; ++rr) {
+      A += red[(rr * 8 + v) * 16 + j];
+      B += red[(rr * 8 + v) * 16 + 8 + j];
+    }
+    if (c < s.C) {
+      float *pr = (ST == 1 ? f.part : b.part) + (int64_t)blockIdx.x * 2 * s.C;
+      pr[c] = A;
+      pr[s.C + c] = B;
+      if (ST == 1 && blockIdx.x == 0 && f.shift_out) f.shift_out[c] = f.shift ? f.shift[c] : 0.f;
+    }
+  }
+}
+
 // ---- bf16 input gradient of a STRIDE-2 pad-1 conv, row form (the first block of stages 4
 // and 6).  dx[hi][wi] only meets the taps with kh = hi+1 (mod 2), kw = wi+1 (mod 2): an even
 // dx row one dy row (kh = 1), an odd one two (kh = 0, 2); likewise along the row, so a thread
@@ -599,6 +755,66 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
       hipLaunchKernelGGL(dw_bwd_data_kernel<EWVIT_F32>, grid, dim3(256), 0, as_stream(stream), dy, w, dx, s);
   }
   return launch_status("dwconv3x3_bwd_data");
+}
+
+// partial rows the BatchNorm-sum forms below leave (one per 32 output rows n*Ho + ho of
+// the output they store), or 0 when the shape does not take them (bf16 only, pad 1,
+// stride 1 | 2 forward / stride 1 input gradient, C % 8 == 0)
+extern "C" int64_t ewvit_dwconv3x3_bn_rows(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int bwd) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || C > 65536 * 8 || (stride != 1 && stride != 2) ||
+      (bwd && stride != 1))
+    return 0;
+  const int64_t rows = bwd ? N * H : N * ((H - 1) / stride + 1);
+  return (rows + 31) / 32;
+}
+
+// forward + the BatchNorm statistics of y (shifted sums, ewvit_bn_fwd_partials): part
+// [ewvit_dwconv3x3_bn_rows(..., 0)][2C], shift_out [C] (= shift, or zeros)
+extern "C" int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,
+                                      int64_t C, int stride, const float *shift, float *part, float *shift_out,
+                                      void *stream) {
+  EWVIT_CHECK_ARG(x && w && y && part && shift_out, "dwconv3x3_fwd_bn: null pointer");
+  const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 0);
+  EWVIT_CHECK_ARG(nrc > 0 && nrc < 65536, "dwconv3x3_fwd_bn: shape not supported");
+  DwShape s = mk(N, H, W, C, stride, 1);
+  if (int rc = check_shape(s, "dwconv3x3_fwd_bn")) return rc;
+  DwBnFwd f;
+  f.part = part; f.shift = shift; f.shift_out = shift_out;
+  BnBwdStats b;
+  dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
+  if (stride == 1)
+    hipLaunchKernelGGL((dw_row_bn_kernel<1, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
+                       (bf16_t *)y, s, f, b);
+  else
+    hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
+                       (bf16_t *)y, s, f, b);
+  return launch_status("dwconv3x3_fwd_bn");
+}
+
+// stride-1 input gradient + the backward statistics of the BatchNorm(+act) whose output the
+// conv read (bx: that BN's input, mean / invstd its saved batch statistics, gamma / beta its
+// affine parameters or null, act 0 / 1 / 2): part [ewvit_dwconv3x3_bn_rows(..., 1)][2C]
+// for ewvit_bn_bwd_partials
+extern "C" int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void *dx, int64_t N, int64_t H, int64_t W,
+                                           int64_t C, const void *bx, const float *mean, const float *invstd,
+                                           const float *gamma, const float *beta, int act, float *part,
+                                           void *stream) {
+  EWVIT_CHECK_ARG(dy && w && dx && bx && mean && invstd && part && act >= 0 && act <= 2,
+                  "dwconv3x3_bwd_data_bn: bad args");
+  const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1);
+  EWVIT_CHECK_ARG(nrc > 0 && nrc < 65536, "dwconv3x3_bwd_data_bn: shape not supported");
+  DwShape s = mk(N, H, W, C, 1, 1);
+  if (int rc = check_shape(s, "dwconv3x3_bwd_data_bn")) return rc;
+  DwShape t = s;                               // the rotated-kernel conv over dy
+  t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
+  DwBnFwd f;
+  BnBwdStats b;
+  b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
+  b.act = act;
+  dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
+  hipLaunchKernelGGL((dw_row_bn_kernel<1, true, 2>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
+                     (bf16_t *)dx, t, f, b);
+  return launch_status("dwconv3x3_bwd_data_bn");
 }
 
 // weight-gradient plan: row kernel (bf16, C/8 <= 256) with `slabs` blocks, or the

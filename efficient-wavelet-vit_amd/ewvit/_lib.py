@@ -91,6 +91,13 @@ SIGNATURES = {
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_dwconv3x3_fwd_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    'ewvit_dwconv3x3_bwd_data_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                    _vp],
+    'ewvit_bn_bwd_partials': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp,
+                              _i32, _vp],
+    'ewvit_conv2d_bwd_data_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
+                                 _vp, _i32, _vp, _vp, _vp, _vp],
 }
 
 # size queries: name -> (restype, argtypes)
@@ -111,6 +118,8 @@ QUERIES = {
     'ewvit_adam_chunks': (_i64, [_i64]),
     'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
+    'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
 }
 
 _lib = None

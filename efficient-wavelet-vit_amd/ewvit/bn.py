@@ -7,11 +7,77 @@ module's running statistics in place like ``F.batch_norm``.  ``groups`` > 1
 normalises consecutive equal batch slices with their own statistics (one
 launch for the MWT's per-level calls of its shared BatchNorms).
 """
+import os
+
 import torch
 
 from . import _lib as L
 
 ACT = {None: 0, 'none': 0, 'relu': 1, 'silu': 2}
+
+# BatchNorm backward statistics summed by the op that produces the BN output's gradient
+# (EWVIT_BN_BWD_LINK=0: every BN backward runs its own reduction pass, A/B)
+_BWD_LINK = os.environ.get('EWVIT_BN_BWD_LINK', '1') != '0'
+# the most partial rows a linked producer may leave (the dx pass reads them all per block)
+BWD_LINK_MAX_ROWS = 512
+
+
+class BwdStatsLink:
+    """The reduction pass of a training-mode BatchNorm backward, done by the kernel that
+    produces the gradient of the BN's output — the input gradient of the op that consumed it
+    (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn).  The BN forward offers a link for
+    its output (`offer`); the consuming op takes it in its forward (`take_bwd_link`); its
+    backward `fulfil`s it with the partial sums and the gradient tensor it produced.  The BN
+    backward uses the partials only if the gradient it receives IS that tensor, unmodified
+    (`partials_for`): a second consumer's gradient added by autograd gives a new tensor (the
+    link holds a reference to the produced one, so autograd cannot accumulate into it in
+    place) and the BN runs its own reduction."""
+    __slots__ = ('key', 'x', 'mean', 'invstd', 'gamma', 'beta', 'act', 'rscale', 'part', 'nrc', 'dx', 'ver')
+
+    def __init__(self, y, x, mean, invstd, gamma, beta, act, rscale=None):
+        self.key = (y.data_ptr(), tuple(y.shape), y.dtype)
+        self.x, self.mean, self.invstd, self.gamma, self.beta = x, mean, invstd, gamma, beta
+        self.act, self.rscale = act, rscale
+        self.part = self.dx = None
+        self.nrc = 0
+        self.ver = -1
+
+    def fulfil(self, part, nrc, dx):
+        self.part, self.nrc, self.dx, self.ver = part, int(nrc), dx, dx._version
+
+    def partials_for(self, dy):
+        """(part, nrc) when dy is the fulfilling op's gradient tensor, else None; releases
+        the link's references either way."""
+        dx, part, nrc, ver = self.dx, self.part, self.nrc, self.ver
+        self.dx = self.part = self.x = None
+        if (dx is None or dy.data_ptr() != dx.data_ptr() or dy.shape != dx.shape or dy.dtype != dx.dtype
+                or dy.stride() != dx.stride() or dx._version != ver):
+            return None
+        return part, nrc
+
+
+_bwd_offered = None
+
+
+def offer_bwd_link(y, x, mean, invstd, gamma, beta, act, rscale=None):
+    """Offer the backward statistics of the BN that produced y (4-D NHWC bf16, one group) to
+    y's consumer; returns the link (kept by the BN's backward), or None."""
+    global _bwd_offered
+    if not (_BWD_LINK and y.dim() == 4 and y.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
+        _bwd_offered = None
+        return None
+    _bwd_offered = BwdStatsLink(y, x, mean, invstd, gamma, beta, act, rscale)
+    return _bwd_offered
+
+
+def take_bwd_link(x):
+    """The link offered for x (the consumer's input), if any; one taker."""
+    global _bwd_offered
+    link = _bwd_offered
+    if link is not None and link.key == (x.data_ptr(), tuple(x.shape), x.dtype):
+        _bwd_offered = None
+        return link
+    return None
 
 
 def _rows(x):
@@ -58,6 +124,8 @@ class BatchNormActFn(torch.autograd.Function):
         if training:
             ctx.save_for_backward(xc, weight, bias, mean, invstd)
         ctx.cfg = (training, act, M, C, groups)
+        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, act) \
+            if training and groups == 1 and ctx.cap == 0 else None
         return y
 
     @staticmethod
@@ -76,6 +144,14 @@ class BatchNormActFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
         db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
+        pr = ctx.bnlink.partials_for(dyc) if ctx.bnlink is not None else None
+        ctx.bnlink = None
+        if pr is not None:
+            # the reduction was summed by the kernel that produced dy: the dx pass only
+            L.call('ewvit_bn_bwd_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
+                   L.ptr(bias), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), None, 1, L.ptr(pr[0]), pr[1],
+                   L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+            return dx, dg, db, None, None, None, None, None, None, None, None, None
         ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=dy.device)
         L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), 0, groups, L.ptr(ws), L.stream(dx),
@@ -141,6 +217,7 @@ class BNDropAddFn(torch.autograd.Function):
         ctx.save_for_backward(xc, weight, bias, mean, invstd, scale)
         ctx.cfg = (M, C, M // N, skip.dtype)
         ctx.link = link if link is not None and link.armed else None
+        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, 0, scale) if L.current_cap() == 0 else None
         return y
 
     @staticmethod
@@ -151,10 +228,18 @@ class BNDropAddFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
         db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
-        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dy.device)
-        L.call('ewvit_bn_bwd_scaled', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
-               L.ptr(mean), L.ptr(invstd), L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(ws), L.stream(dx),
-               work={'bytes': 5 * xc.numel() * xc.element_size()})
+        pr = ctx.bnlink.partials_for(dyc) if ctx.bnlink is not None else None
+        ctx.bnlink = None
+        if pr is not None:
+            # g = dy * scale[n] summed by the next conv's input-gradient epilogue: dx pass only
+            L.call('ewvit_bn_bwd_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
+                   L.ptr(bias), L.ptr(mean), L.ptr(invstd), 0, L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(pr[0]),
+                   pr[1], L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+        else:
+            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dy.device)
+            L.call('ewvit_bn_bwd_scaled', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
+                   L.ptr(bias), L.ptr(mean), L.ptr(invstd), L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(ws),
+                   L.stream(dx), work={'bytes': 5 * xc.numel() * xc.element_size()})
         if ctx.link is not None:
             # the skip gradient goes to the block's first conv (ewvit.conv.SkipLink), which
             # adds it to its input gradient in the dgrad epilogue

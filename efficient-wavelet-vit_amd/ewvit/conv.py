@@ -21,6 +21,7 @@ import weakref
 import torch
 
 from . import _lib as L
+from . import bn as bnmod
 from . import grads
 from .grads import grad_out
 
@@ -165,6 +166,8 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             grads.note_use(bias)
         ctx.link = _take_link(x) if levels == 1 else None
+        # the backward statistics of the BatchNorm that produced x, summed by the dgrad epilogue
+        ctx.bnlink = bnmod.take_bwd_link(x) if levels == 1 and ctx.needs_input_grad[0] else None
         NL, Cz, H, W = x.shape
         if NL % levels:
             raise ValueError(f'conv2d: batch {NL} is not a multiple of levels={levels}')
@@ -227,10 +230,25 @@ class Conv2dFn(torch.autograd.Function):
         skip = link.grad if link is not None else None
         if link is not None:
             link.grad = None
+        bl = ctx.bnlink
+        ctx.bnlink = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            if skip is not None and L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
+            rows = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cx, Cout, k, stride)) \
+                if bl is not None and xdt == torch.bfloat16 and bl.x.shape == xc.shape else 0
+            if 0 < rows <= bnmod.BWD_LINK_MAX_ROWS and (
+                    skip is None or L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride)):
+                # dx (+ the skip gradient) and the producing BatchNorm's backward sums in one epilogue
+                sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if skip is not None else None
+                part = torch.empty(rows, 2 * Cx, dtype=torch.float32, device=xc.device)
+                nrc = ctypes.c_int(0)
+                L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), L.ptr(sk), N, H, W, Cx, Cout,
+                       k, stride, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta),
+                       bl.act, L.ptr(bl.rscale), L.ptr(part), ctypes.byref(nrc), L.stream(dx), work=work)
+                bl.fulfil(part, nrc.value, dx)
+                skip = None
+            elif skip is not None and L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
                 # the residual block's skip gradient added in the dgrad epilogue
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
                 L.call('ewvit_conv2d_bwd_data_add', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), L.ptr(sk), N, H, W, Cx, Cout,

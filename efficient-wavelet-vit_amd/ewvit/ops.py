@@ -11,6 +11,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib as L
+from . import bn as _bn
 from .grads import grad_out, note_use
 
 F32, BF16 = L.F32, L.BF16
@@ -557,11 +558,16 @@ def dwt_hf_features(x, levels, out_hw, out_dtype=torch.bfloat16, out_channels=0)
 
 
 # ------------------------------------------------------- depthwise 3x3 conv
+# the stride-1 input gradient sums the backward statistics of the BatchNorm before the conv
+# (ewvit_dwconv3x3_bwd_data_bn; 0: that BN runs its own reduction pass, A/B)
+_DW_BWD_LINK = os.environ.get('EWVIT_DW_BWD_LINK', '1') != '0'
+
+
 class DepthwiseConv3x3Fn(torch.autograd.Function):
     """groups=C 3x3 conv, no bias, channels-last (EfficientNetV2-S MBConv depthwise)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad):
+    def forward(ctx, x, weight, stride, pad, bn_stats=None):
         L.require_gpu(x, weight)
         N, C, H, W = x.shape
         xc = x.contiguous(memory_format=torch.channels_last)
@@ -569,11 +575,20 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         Ho, Wo = (H + 2 * pad - 3) // stride + 1, (W + 2 * pad - 3) // stride + 1
         y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         work = {'bytes': (xc.numel() + y.numel()) * x.element_size(), 'flops': 18.0 * y.numel()}
-        L.call('ewvit_dwconv3x3_fwd', L.ptr(xc), L.ptr(w), L.ptr(y), N, H, W, C, stride, pad, L.dt(xc),
-               L.stream(y), work=work)
+        if bn_stats is not None:
+            # the BatchNorm statistics of y summed on the way (ewvit_bn_fwd_partials)
+            shift, part, shift_out = bn_stats
+            L.call('ewvit_dwconv3x3_fwd_bn', L.ptr(xc), L.ptr(w), L.ptr(y), N, H, W, C, stride, L.ptr(shift),
+                   L.ptr(part), L.ptr(shift_out), L.stream(y), work=work)
+        else:
+            L.call('ewvit_dwconv3x3_fwd', L.ptr(xc), L.ptr(w), L.ptr(y), N, H, W, C, stride, pad, L.dt(xc),
+                   L.stream(y), work=work)
         ctx.save_for_backward(xc, w)
         ctx.cfg = (stride, pad, weight.dtype)
         ctx.wstride = weight.stride()
+        # the backward statistics of the BatchNorm that produced x, summed by the input gradient
+        ctx.bnlink = _bn.take_bwd_link(x) if (_DW_BWD_LINK and stride == 1 and pad == 1
+                                             and ctx.needs_input_grad[0]) else None
         return y
 
     @staticmethod
@@ -585,10 +600,22 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         if dyc.dtype != xc.dtype:
             dyc = dyc.to(xc.dtype)
         dx = dw = None
+        bl = ctx.bnlink
+        ctx.bnlink = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
-            L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, stride, pad,
-                   L.dt(xc), L.stream(dx), work={'bytes': (dyc.numel() + dx.numel()) * dx.element_size()})
+            rows = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 1)) \
+                if bl is not None and xc.dtype == torch.bfloat16 and bl.x.shape == xc.shape else 0
+            if 0 < rows <= _bn.BWD_LINK_MAX_ROWS:
+                # dx and the producing BatchNorm(+SiLU)'s backward sums in one pass
+                part = torch.empty(rows, 2 * C, dtype=torch.float32, device=xc.device)
+                L.call('ewvit_dwconv3x3_bwd_data_bn', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, L.ptr(bl.x),
+                       L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta), bl.act, L.ptr(part),
+                       L.stream(dx), work={'bytes': (dyc.numel() + 2 * dx.numel()) * dx.element_size()})
+                bl.fulfil(part, rows, dx)
+            else:
+                L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, stride, pad,
+                       L.dt(xc), L.stream(dx), work={'bytes': (dyc.numel() + dx.numel()) * dx.element_size()})
         if ctx.needs_input_grad[1]:
             wsb = L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, stride, pad)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
@@ -603,13 +630,33 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                     dw = dw.as_strided(dw.shape, ctx.wstride)      # same memory, size-1 dims differ only
                 else:
                     dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def dwconv3x3(x, weight, stride=1, pad=1):
     if torch.is_autocast_enabled('cuda') and x.dtype == torch.float32:
         x = x.to(torch.get_autocast_dtype('cuda'))
     return DepthwiseConv3x3Fn.apply(x, weight, int(stride), int(pad))
+
+
+def dwconv3x3_bn_stats(x, weight, stride, shift):
+    """dwconv3x3 (pad 1, bf16) whose kernel also leaves the BatchNorm partial statistics of
+    its output centred on `shift` (the BN running mean): (y, part, shifts, nrc) for
+    ewvit.bn.batch_norm_act / bn_act_se(..., partials=(part, shifts, nrc)), or None when the
+    shape does not take it."""
+    if torch.is_autocast_enabled('cuda') and x.dtype == torch.float32:
+        x = x.to(torch.get_autocast_dtype('cuda'))
+    if x.dtype != torch.bfloat16 or x.dim() != 4 or not x.is_cuda:
+        return None
+    N, C, H, W = x.shape
+    nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, int(stride), 0))
+    if not 0 < nrc <= 256:
+        return None
+    part = torch.empty(nrc, 2 * C, dtype=torch.float32, device=x.device)
+    shifts = torch.empty(C, dtype=torch.float32, device=x.device)
+    sh = shift.detach().float().contiguous() if shift is not None else None
+    y = DepthwiseConv3x3Fn.apply(x, weight, int(stride), 1, (sh, part, shifts))
+    return y, part, shifts, nrc
 
 
 # ------------------------------------------------------------------- pooling

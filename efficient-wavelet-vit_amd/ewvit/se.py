@@ -102,7 +102,8 @@ class BnActSEFn(torch.autograd.Function):
     dy*s + g itself (ewvit_bn_bwd_se) — the SE input-gradient pass and its tensor never exist."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2,
+                partials=None):
         L.require_gpu(x)
         xc, N, HW, C = _rows(x)
         M = N * HW
@@ -110,10 +111,19 @@ class BnActSEFn(torch.autograd.Function):
         x2 = torch.empty_like(xc)
         mean = torch.empty(1, C, dtype=torch.float32, device=dev)
         invstd = torch.empty_like(mean)
-        ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
-        L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta), L.ptr(running_mean),
-               L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean), L.ptr(invstd), 1, L.ptr(counter),
-               L.ptr(ws), L.stream(x2), work={'bytes': 3 * xc.numel() * xc.element_size()})
+        if partials is not None:
+            # statistics summed by the depthwise conv that produced x: the apply pass only
+            part, shifts, nrc = partials
+            L.call('ewvit_bn_fwd_partials', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), 1, L.stream(x2),
+                   work={'bytes': 2 * xc.numel() * xc.element_size()})
+        else:
+            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
+            L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), 1, L.ptr(counter), L.ptr(ws), L.stream(x2),
+                   work={'bytes': 3 * xc.numel() * xc.element_size()})
         Csq = w1.shape[0]
         W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
         s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
@@ -155,13 +165,16 @@ class BnActSEFn(torch.autograd.Function):
         L.call('ewvit_bn_bwd_se', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW, L.ptr(ws),
                L.stream(dx), work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2)
+        return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2,
+                None)
 
 
-def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2):
+def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2, partials=None):
     """SE(act(bn(x))) for a training-mode BatchNorm module `bn` (batch statistics, running
     statistics and counter updated like batch_norm_act) and the SE's 1x1 conv parameters
-    (fc1 = (se_w1, se_b1), fc2 = (se_w2, se_b2)) — see BnActSEFn."""
+    (fc1 = (se_w1, se_b1), fc2 = (se_w2, se_b2)) — see BnActSEFn.  `partials` = (part,
+    shifts, nrc): x's batch statistics already summed by its producer
+    (ewvit.ops.dwconv3x3_bn_stats)."""
     from .bn import ACT
     if not bn.training or bn.momentum is None:
         raise ValueError('bn_act_se: training-mode BatchNorm with a momentum only')
@@ -169,7 +182,7 @@ def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2):
         x = x.float()
     counter = bn.num_batches_tracked if bn.track_running_stats else None
     return BnActSEFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, counter,
-                           ACT[act], se_w1, se_b1, se_w2, se_b2)
+                           ACT[act], se_w1, se_b1, se_w2, se_b2, partials)
 
 
 def squeeze_excite(x, w1, b1, w2, b2):

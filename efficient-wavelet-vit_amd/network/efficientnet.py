@@ -30,6 +30,8 @@ _SKIP_LINK = os.environ.get('EWVIT_SKIP_LINK', '1') != '0'
 _STEM = os.environ.get('EWVIT_STEM', '1') != '0'
 # MBConv's depthwise BN + SiLU and its squeeze-excitation as one ewvit.bn_act_se (0: A/B)
 _BN_SE = os.environ.get('EWVIT_BN_SE', '1') != '0'
+# the depthwise conv sums its BatchNorm's statistics (0: a statistics pass, A/B)
+_DW_STATS = os.environ.get('EWVIT_DW_STATS', '1') != '0'
 
 STAGES = (
     ('fused', 1, 3, 1, 24, 24, 2),
@@ -99,6 +101,15 @@ class ConvBNAct(nn.Sequential):
                 if r is not None:
                     return r[0], r[1:]
         return None
+
+    def dw_stats(self, x):
+        """(y, part, shifts, nrc): the depthwise conv with its BatchNorm's statistics summed by
+        the conv kernel (ewvit.ops.dwconv3x3_bn_stats), or None."""
+        conv, bn = self[0], self[1]
+        if not (_DW_STATS and type(conv) is DepthwiseConv2d and conv.padding == (1, 1) and bn.training
+                and bn.track_running_stats and bn.momentum is not None and x.is_cuda and not self._hooked()):
+            return None
+        return ewvit.ops.dwconv3x3_bn_stats(x, conv.weight, conv.stride[0], bn.running_mean)
 
     def can_bn_se(self, x, se):
         """This block's BatchNorm + act on input x's conv output, then `se`, as one
@@ -189,8 +200,10 @@ def _seq(mods, h):
         m = mods[i]
         if isinstance(m, ConvBNAct) and i + 1 < len(mods) and m.can_bn_se(h, mods[i + 1]):
             se = mods[i + 1]
-            h = ewvit.bn_act_se(m[0](h), m[1], 'silu' if len(m) > 2 else None, se.fc1.weight, se.fc1.bias,
-                                se.fc2.weight, se.fc2.bias)
+            r = m.dw_stats(h)
+            y, part = (r[0], r[1:]) if r is not None else (m[0](h), None)
+            h = ewvit.bn_act_se(y, m[1], 'silu' if len(m) > 2 else None, se.fc1.weight, se.fc1.bias,
+                                se.fc2.weight, se.fc2.bias, partials=part)
             i += 2
             continue
         h = m(h)

@@ -207,6 +207,23 @@ int64_t ewvit_dwconv3x3_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, in
 int ewvit_dwconv3x3_bwd_weight(const void *x, const void *dy, float *dw, int accumulate, int64_t N,
                                int64_t H, int64_t W, int64_t C, int stride, int pad, int dtype,
                                float *workspace, void *stream);
+/* The same convs with the training-mode BatchNorm sums of what they store (bf16, pad 1),
+ * so the MBConv block's BatchNorm around the depthwise conv (torchvision
+ * Conv2dNormActivation, sfe.py:111-113,150) runs no statistics pass of its own.  One partial
+ * row per 32 output rows n*Ho + ho: ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, bwd) rows
+ * (0 = shape not supported; bwd: the stride-1 input gradient, rows of dx).
+ * fwd_bn: part [rows][2C] = (sum (y - K), sum (y - K)^2) per channel, K = shift (a running
+ *   mean estimate, NULL: 0), shift_out [C] = K — what ewvit_bn_fwd_partials finalises.
+ * bwd_data_bn (stride 1): dx as ewvit_dwconv3x3_bwd_data, and part [rows][2C] = (sum g,
+ *   sum g*xhat) of the BatchNorm(+act) that produced the conv's input: xhat = (bx - mean)
+ *   * invstd (bx: that BN's input [N, H, W, C] bf16), g = dx * act'(xhat*gamma + beta)
+ *   (act 0/1/2; gamma / beta NULL = 1 / 0) — what ewvit_bn_bwd_partials finalises. */
+int64_t ewvit_dwconv3x3_bn_rows(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int bwd);
+int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W, int64_t C,
+                           int stride, const float *shift, float *part, float *shift_out, void *stream);
+int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void *dx, int64_t N, int64_t H, int64_t W,
+                                int64_t C, const void *bx, const float *mean, const float *invstd,
+                                const float *gamma, const float *beta, int act, float *part, void *stream);
 
 /* ---------------------------------------------- BatchNorm2d + activation ---
  * BatchNorm2d (batch statistics in training, running statistics in eval) fused
@@ -269,6 +286,16 @@ int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int6
 int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
                     const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
                     float *dbeta, const float *se_s, const float *se_g, int64_t HW, float *workspace, void *stream);
+/* Training-mode backward whose reduction pass already ran in the kernel that produced dy
+ * (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [nrc][2C] rows of (sum g,
+ * sum g*xhat), g = dy * act'(...) or, with row_scale [M / HW] (act 0: the MBConv tail of
+ * ewvit_bn_fwd_drop_add), g = dy * row_scale[row / HW].  Only the dx pass runs; one group;
+ * dgamma / dbeta overwritten (may be NULL).  Replaces the reduce launch of ewvit_bn_bwd /
+ * ewvit_bn_bwd_scaled (torchvision BatchNorm2d backward behind sfe.py:111-113). */
+int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                          const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
+                          int act, float *dgamma, float *dbeta, const float *row_scale, int64_t HW,
+                          const float *part, int nrc, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -375,6 +402,20 @@ int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Ci
                                      int stride);
 int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N, int64_t H,
                               int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, void *stream);
+/* Stride-1 input gradient (+ addend when not NULL, as ewvit_conv2d_bwd_data_add) that also
+ * sums, over its bf16-rounded dx, the backward statistics of the BatchNorm whose output was
+ * this conv's input (the MBConv tail / Conv2dNormActivation before the next block's first
+ * conv, sfe.py:111-113): bx [N, H, W, Cin] bf16 that BN's input, mean / invstd its saved
+ * statistics, gamma / beta or NULL, act 0/1/2, rscale [N] (act 0) the drop-path factor per
+ * frame or NULL.  part [ewvit_conv2d_bwd_bn_rows(...)][2 Cin] gets per m-tile (sum g, sum
+ * g*xhat) as ewvit_dwconv3x3_bwd_data_bn defines them; *nrc_out = rows written (for
+ * ewvit_bn_bwd_partials).  ewvit_conv2d_bwd_bn_rows: the most rows (0 = shape not
+ * supported, or a workgroup cap is in force). */
+int64_t ewvit_conv2d_bwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride);
+int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N, int64_t H,
+                             int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, const void *bx,
+                             const float *mean, const float *invstd, const float *gamma, const float *beta, int act,
+                             const float *rscale, float *part, int *nrc_out, void *stream);
 /* bytes of f32 split-K workspace for ewvit_conv2d_bwd_weight. */
 int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                           int ksize, int stride);

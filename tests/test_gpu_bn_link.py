@@ -1,0 +1,326 @@
+"""BatchNorm statistics summed by the neighbouring kernels (csrc/depthwise.hip
+dw_row_bn_kernel, csrc/conv.hip dgrad epilogue, csrc/batchnorm.hip ewvit_bn_bwd_partials):
+the MBConv block's BatchNorms with no statistics / reduction pass of their own.
+
+Kernel level (through the C-ABI): the stored outputs are bit-identical to the plain kernels
+(the sums are an epilogue on the same values), and the partial rows add up to the fp64 sums
+of those stored values (1e-5 of the sum of magnitudes: fp32 adds in a fixed order).
+ewvit_bn_bwd_partials vs ewvit_bn_bwd: dx within 2 bf16 ulps (the two reductions add the same
+terms in different orders, so the finalised means differ in the last fp32 bits).
+Module level: four MBConv blocks with the links on vs off (the A/B switches) — outputs,
+running statistics and every gradient equal to the tolerance of those orders (outputs cosine
+>= 0.99999 and max 2e-2 of scale, gradients cosine >= 0.999); all 30 MBConv blocks of stages
+4-6: the fused launches are the ones that ran, one per BatchNorm the links can serve.
+"""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _L():
+    import ewvit
+    return ewvit._lib
+
+
+def bf(t):
+    return t.to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def sums_close(part, ref_a, ref_b, mag_a, mag_b):
+    """part [rows][2C] summed over rows vs fp64 references (per channel)."""
+    p = part.double().sum(0).cpu()
+    C = ref_a.numel()
+    ea = float(((p[:C] - ref_a).abs() / (mag_a + 1e-30)).max())
+    eb = float(((p[C:] - ref_b).abs() / (mag_b + 1e-30)).max())
+    return ea, eb
+
+
+DW_SHAPES = [(16, 1536, 7, 7, 1), (16, 960, 14, 14, 1), (8, 256, 28, 28, 2), (4, 200, 9, 11, 1), (3, 64, 5, 5, 2)]
+
+
+@pytest.mark.parametrize('N,C,H,W,stride', DW_SHAPES)
+def test_dw_fwd_bn(N, C, H, W, stride):
+    L = _L()
+    g = torch.Generator().manual_seed(C + H)
+    x = bf(torch.randn(N, C, H, W, generator=g))
+    w = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV).contiguous()
+    shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y0 = torch.empty(N, C, Ho, Wo, dtype=torch.bfloat16, device=DEV, memory_format=torch.channels_last)
+    y1 = torch.empty_like(y0)
+    L.call('ewvit_dwconv3x3_fwd', L.ptr(x), L.ptr(w), L.ptr(y0), N, H, W, C, stride, 1, L.BF16, L.stream(x))
+    nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 0))
+    assert nrc == (N * Ho + 31) // 32
+    part = torch.full((nrc, 2 * C), float('nan'), device=DEV)
+    so = torch.full((C,), float('nan'), device=DEV)
+    L.call('ewvit_dwconv3x3_fwd_bn', L.ptr(x), L.ptr(w), L.ptr(y1), N, H, W, C, stride, L.ptr(shift), L.ptr(part),
+           L.ptr(so), L.stream(x))
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(so, shift)
+    d = (y1.double().cpu() - shift.double().cpu().view(1, C, 1, 1))
+    ra, rb = d.sum((0, 2, 3)), (d * d).sum((0, 2, 3))
+    ea, eb = sums_close(part, ra, rb, d.abs().sum((0, 2, 3)), rb)
+    assert ea < 1e-5 and eb < 1e-5, (ea, eb)
+
+
+def _bwd_ref(dx, bx, mean, invstd, gamma, beta, act, rscale=None, hw=1):
+    """fp64 g and g*xhat sums per channel of the stored dx (bf16) — bn_bwd_reduce_kernel's terms."""
+    d, x = dx.double().cpu(), bx.double().cpu()
+    C = d.shape[1]
+    xh = (x - mean.double().cpu().view(1, C, 1, 1)) * invstd.double().cpu().view(1, C, 1, 1)
+    if act == 2:
+        z = xh * gamma.double().cpu().view(1, C, 1, 1) + beta.double().cpu().view(1, C, 1, 1)
+        s = torch.sigmoid(z)
+        gr = d * s * (1 + z * (1 - s))
+    else:
+        gr = d
+    if rscale is not None:
+        gr = gr * rscale.double().cpu().view(-1, 1, 1, 1)
+    return gr.sum((0, 2, 3)), (gr * xh).sum((0, 2, 3)), gr.abs().sum((0, 2, 3)), (gr * xh).abs().sum((0, 2, 3))
+
+
+def _bn_stats(bx):
+    x = bx.float()
+    mean = x.mean((0, 2, 3))
+    invstd = torch.rsqrt(x.var((0, 2, 3), unbiased=False) + 1e-3)
+    return mean.contiguous(), invstd.contiguous()
+
+
+@pytest.mark.parametrize('N,C,H,W', [(16, 1536, 7, 7), (16, 960, 14, 14), (4, 200, 9, 11), (2, 64, 30, 30)])
+def test_dw_bwd_data_bn(N, C, H, W):
+    L = _L()
+    g = torch.Generator().manual_seed(C * 3 + H)
+    dy = bf(torch.randn(N, C, H, W, generator=g))
+    bx = bf(torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3)
+    w = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV).contiguous()
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    mean, invstd = _bn_stats(bx)
+    dx0 = torch.empty_like(dy)
+    dx1 = torch.empty_like(dy)
+    L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dy), L.ptr(w), L.ptr(dx0), N, H, W, C, 1, 1, L.BF16, L.stream(dy))
+    nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1))
+    assert nrc == (N * H + 31) // 32
+    part = torch.full((nrc, 2 * C), float('nan'), device=DEV)
+    L.call('ewvit_dwconv3x3_bwd_data_bn', L.ptr(dy), L.ptr(w), L.ptr(dx1), N, H, W, C, L.ptr(bx), L.ptr(mean),
+           L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 2, L.ptr(part), L.stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    ra, rb, ma, mb = _bwd_ref(dx1, bx, mean, invstd, gamma, beta, 2)
+    ea, eb = sums_close(part, ra, rb, ma, mb)
+    assert ea < 1e-5 and eb < 1e-5, (ea, eb)
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,act,addend,scaled', [
+    (64, 7, 7, 256, 1536, 0, True, True),      # stage-6 expand dgrad + skip: the project BN of the block before
+    (64, 14, 14, 160, 960, 0, True, True),     # stage 5 (Ncol 160: a half-empty column tile)
+    (64, 7, 7, 256, 1280, 0, False, True),     # the head conv's dgrad: the last block's tail
+    (64, 14, 14, 128, 768, 0, False, False),   # a non-residual tail (BatchNorm, no activation)
+    (16, 14, 14, 64, 256, 2, False, False),    # a BN + SiLU before a 1x1 conv
+])
+def test_conv_dgrad_bn(N, H, W, Cin, Cout, act, addend, scaled):
+    L = _L()
+    g = torch.Generator().manual_seed(Cin + Cout)
+    dy = bf(torch.randn(N, Cout, H, W, generator=g))
+    wt = torch.randn(Cout, Cin, 1, 1, generator=g) * 0.05
+    wpt = wt.reshape(Cout, Cin).t().contiguous().to(DEV, torch.bfloat16)      # [Cin][1][Cout]
+    bx = bf(torch.randn(N, Cin, H, W, generator=g) * 1.2 - 0.1)
+    gamma = (torch.randn(Cin, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(Cin, generator=g) * 0.2).to(DEV)
+    mean, invstd = _bn_stats(bx)
+    sk = bf(torch.randn(N, Cin, H, W, generator=g)) if addend else None
+    rs = ((torch.rand(N, generator=g) < 0.8).float() / 0.8).to(DEV) if scaled else None
+    dx0, dx1 = torch.empty_like(bx), torch.empty_like(bx)
+    if addend:
+        L.call('ewvit_conv2d_bwd_data_add', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), L.ptr(sk), N, H, W, Cin, Cout, 1, 1,
+               L.stream(dy))
+    else:
+        L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Cin, Cout, 1, 1, 0, 0,
+               L.stream(dy))
+    rows = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cin, Cout, 1, 1))
+    assert rows == (N * H * W + 127) // 128
+    part = torch.full((rows, 2 * Cin), float('nan'), device=DEV)
+    nrc = ctypes.c_int(0)
+    L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), L.ptr(sk), N, H, W, Cin, Cout, 1, 1,
+           L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma if act else None), L.ptr(beta if act else None), act,
+           L.ptr(rs), L.ptr(part), ctypes.byref(nrc), L.stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    assert 1 <= nrc.value <= rows
+    ra, rb, ma, mb = _bwd_ref(dx1, bx, mean, invstd, gamma, beta, act, rs)
+    ea, eb = sums_close(part[:nrc.value], ra, rb, ma, mb)
+    assert ea < 1e-5 and eb < 1e-5, (ea, eb)
+
+
+@pytest.mark.parametrize('act,scaled', [(2, False), (0, True), (0, False)])
+def test_bn_bwd_partials_matches_reduce(act, scaled):
+    """ewvit_bn_bwd_partials from a producer's partial rows == ewvit_bn_bwd(_scaled) (which
+    sums the same terms itself), to the fp32 summation order."""
+    L = _L()
+    N, C, H, W = 32, 512, 14, 14
+    M = N * H * W
+    g = torch.Generator().manual_seed(act + 10 * scaled)
+    dy = bf(torch.randn(N, C, H, W, generator=g))
+    bx = bf(torch.randn(N, C, H, W, generator=g) + 0.2)
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    mean, invstd = _bn_stats(bx)
+    rs = ((torch.rand(N, generator=g) < 0.75).float() / 0.75).to(DEV) if scaled else None
+    ra, rb, _, _ = _bwd_ref(dy, bx, mean, invstd, gamma, beta, act, rs)
+    part = torch.stack([ra, rb]).reshape(1, 2 * C).float().to(DEV)     # one exact partial row
+    dx0, dx1 = torch.empty_like(dy), torch.empty_like(dy)
+    dg0, db0, dg1, db1 = (torch.empty(C, device=DEV) for _ in range(4))
+    ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, device=DEV)
+    if scaled:
+        L.call('ewvit_bn_bwd_scaled', L.ptr(dy), L.ptr(bx), L.ptr(dx0), L.BF16, M, C, L.ptr(gamma), L.ptr(beta),
+               L.ptr(mean), L.ptr(invstd), L.ptr(dg0), L.ptr(db0), L.ptr(rs), H * W, L.ptr(ws), L.stream(dy))
+    else:
+        L.call('ewvit_bn_bwd', L.ptr(dy), L.ptr(bx), L.ptr(dx0), L.BF16, M, C, L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+               L.ptr(invstd), act, L.ptr(dg0), L.ptr(db0), 0, 1, L.ptr(ws), L.stream(dy))
+    L.call('ewvit_bn_bwd_partials', L.ptr(dy), L.ptr(bx), L.ptr(dx1), L.BF16, M, C, L.ptr(gamma), L.ptr(beta),
+           L.ptr(mean), L.ptr(invstd), act, L.ptr(dg1), L.ptr(db1), L.ptr(rs), H * W, L.ptr(part), 1, L.stream(dy))
+    torch.cuda.synchronize()
+    d = (dx0.float() - dx1.float()).abs()
+    assert float(d.max()) <= 2 ** -6 * float(dx0.float().abs().max()), float(d.max())
+    assert float((d > 0).float().mean()) < 0.02
+    for a, b in ((dg0, dg1), (db0, db1)):
+        assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max()) + 1e-6
+
+
+def _run(mods, x0, dyo, linked, monkeypatch):
+    import ewvit
+    import ewvit.bn as ebn
+    import network.efficientnet as en
+    L = ewvit._lib
+    monkeypatch.setattr(ebn, '_BWD_LINK', linked)
+    monkeypatch.setattr(en, '_DW_STATS', linked)
+    m = mods().to(DEV).to(memory_format=torch.channels_last).train()
+    for mod in m.modules():
+        if hasattr(mod, 'sd_prob'):
+            mod.sd_prob = 0.0          # no drop-path draw: both runs see the same keep masks
+    x = x0.clone().requires_grad_(True)
+    calls = {}
+    real = L.call
+
+    def count(name, *a, **k):
+        calls[name] = calls.get(name, 0) + 1
+        return real(name, *a, **k)
+    monkeypatch.setattr(L, 'call', count)
+    try:
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y = m(x)
+        y.backward(dyo)
+    finally:
+        monkeypatch.setattr(L, 'call', real)
+    torch.cuda.synchronize()
+    return (y.detach().float(), x.grad.float(), {n: p.grad.float() for n, p in m.named_parameters()},
+            {n: b.float() for n, b in m.named_buffers() if 'running' in n}, calls)
+
+
+def _features(sl):
+    def make():
+        from network.efficientnet import EfficientNetV2S
+        torch.manual_seed(1)
+        f = EfficientNetV2S().features
+        return torch.nn.Sequential(*[f[s][b] for s, b in sl])
+    return make
+
+
+def _cos(a, b):
+    return float(torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0))
+
+
+def test_mbconv_blocks_linked_vs_unlinked(monkeypatch):
+    """Four MBConv blocks (5.7, 5.8 at 14^2, the stride-2 6.0, 6.1 at 7^2) train step with the
+    BN links on and off: the same numbers to fp32 summation order (a short chain, so bf16
+    rounding differences cannot compound much), and the linked run launched the fused kernels.
+    Measured (tools/diag_link.py): the forward drifts only through the depthwise BN statistics
+    (other fp32 summation order), 1 - cos = 1e-8 after one block, 7e-7 after two, 2.4e-5 after
+    four — the amplification any two bf16 runs of this random-init stack show; the backward
+    links alone leave the forward bit-identical (input-gradient cosine 0.99999)."""
+    g = torch.Generator().manual_seed(5)
+    N = 32
+    x0 = torch.randn(N, 160, 14, 14, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyo = torch.randn(N, 256, 7, 7, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mods = _features([(5, 7), (5, 8), (6, 0), (6, 1)])
+    y0, gx0, gp0, bf0, c0 = _run(mods, x0, dyo, False, monkeypatch)
+    y1, gx1, gp1, bf1, c1 = _run(mods, x0, dyo, True, monkeypatch)
+    assert c0.get('ewvit_bn_bwd_partials', 0) == 0
+    assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == 4
+    assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == 3          # 6.0's depthwise is stride 2
+    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 3             # tails of 5.7, 5.8, 6.0
+    assert c1.get('ewvit_bn_bwd_partials', 0) == 6
+    assert _cos(y0, y1) > 0.9999 and float((y0 - y1).abs().max()) <= 5e-2 * float(y0.abs().max())
+    assert _cos(gx0, gx1) > 0.9995
+    # a BatchNorm bias whose output gradient passes only through train-mode BatchNorms (and
+    # skips of them) has an exactly zero true gradient — its computed one is rounding noise in
+    # both runs (cosine ~0.1): biases are held to an absolute bound instead
+    worst = min((_cos(gp0[n], gp1[n]), n) for n in gp0 if gp0[n].abs().max() > 0 and not n.endswith('bias'))
+    assert worst[0] > 0.995, worst
+    top = max(float(v.abs().max()) for v in gp0.values())
+    for n in gp0:
+        if n.endswith('bias'):
+            assert float((gp0[n] - gp1[n]).abs().max()) <= 1e-2 * top, n
+    # running statistics after one update (0.9 * init + 0.1 * batch): 1e-3 relative, or 2e-4
+    # absolute for a mean that is itself a near-zero cancellation (a project conv's output)
+    for n in bf0:
+        assert float((bf0[n] - bf1[n]).abs().max()) <= 1e-3 * float(bf0[n].abs().max()) + 2e-4, n
+
+
+def test_mbconv_stages_link_count(monkeypatch):
+    """Stages 4-6 (all 30 MBConv blocks): every BN the links can serve is served — the
+    depthwise BNs' statistics in the conv, each stride-1 block's expand-BN reduction in its
+    depthwise input gradient, each tail's reduction in the next block's first input gradient —
+    and the step stays finite (the numbers are compared on the short chain above; over 30
+    blocks two bf16 implementations drift apart like any two bf16 runs)."""
+    g = torch.Generator().manual_seed(9)
+    N = 16
+    x0 = torch.randn(N, 64, 28, 28, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyo = torch.randn(N, 256, 7, 7, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    sl = [(4, b) for b in range(6)] + [(5, b) for b in range(9)] + [(6, b) for b in range(15)]
+    y1, gx1, gp1, _, c1 = _run(_features(sl), x0, dyo, True, monkeypatch)
+    nblk = 30
+    assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == nblk
+    assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == nblk - 2          # blocks 4.0 / 6.0 are stride 2
+    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == nblk - 1              # the last tail has no conv after it
+    assert c1.get('ewvit_bn_bwd_partials', 0) == 2 * nblk - 3
+    assert c1.get('ewvit_bn_bwd', 0) == 2 and c1.get('ewvit_bn_bwd_scaled', 0) == 1
+    assert bool(torch.isfinite(y1).all()) and bool(torch.isfinite(gx1).all())
+    assert all(bool(torch.isfinite(v).all()) for v in gp1.values())
+
+
+@pytest.mark.parametrize('N,C,H', [(32, 960, 14), (32, 1536, 7)])
+def test_dw_stats_bn_act_se_matches(N, C, H, monkeypatch):
+    """One depthwise conv + BN + SiLU + SE (ewvit.bn_act_se) with the statistics from the conv
+    kernel vs from the BN's own statistics pass: same batch statistics to fp32 rounding, same
+    outputs up to the bf16 rounding those last bits can flip."""
+    import ewvit
+    from network.efficientnet import ConvBNAct, SqueezeExcitation
+    torch.manual_seed(C)
+    blk = ConvBNAct(C, C, 3, 1, groups=C).to(DEV).train()
+    se = SqueezeExcitation(C, C // 24).to(DEV)
+    x = (torch.randn(N, C, H, H) * 0.8 + 0.3).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for linked in (False, True):
+        rm0, rv0 = blk[1].running_mean.clone(), blk[1].running_var.clone()
+        r = blk.dw_stats(x) if linked else None
+        if linked:
+            assert r is not None
+        y = r[0] if linked else blk[0](x)
+        o = ewvit.bn_act_se(y, blk[1], 'silu', se.fc1.weight, se.fc1.bias, se.fc2.weight, se.fc2.bias,
+                            partials=r[1:] if linked else None)
+        outs.append((y, o, blk[1].running_mean.clone(), blk[1].running_var.clone()))
+        blk[1].running_mean.copy_(rm0)
+        blk[1].running_var.copy_(rv0)
+    (y0, o0, m0, v0), (y1, o1, m1, v1) = outs
+    assert torch.equal(y0, y1)
+    assert float((m0 - m1).abs().max()) <= 1e-6 * float(m0.abs().max()) + 1e-7
+    assert float((v0 - v1).abs().max()) <= 1e-5 * float(v0.abs().max())
+    d = (o0.float() - o1.float()).abs()
+    assert float((d > 0).float().mean()) < 0.01, float((d > 0).float().mean())
+    assert float(d.max()) <= 2 ** -7 * float(o0.float().abs().max())
