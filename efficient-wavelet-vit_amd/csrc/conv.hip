@@ -1064,13 +1064,19 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 // 256-B rows, chunk c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed,
 // ds_read_b64_tr_b16).  Bias gradient (sum of dy over pixels): the blocks of n'-tile
 // t sum the dy image of the K-tiles kt = t (mod n'-tiles), spreading the extra reads.
-template <int KS, int BK, int NS, int WJ = 4>
-__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
+// KG = 2: two K-groups of 4 waves share a workgroup — group g multiplies the split's K-tiles
+// g, g + 2, ... through its own LDS ring, and group 1 hands its accumulators to group 0
+// through LDS at the end (fixed order: group 0 + group 1), so a workgroup covers twice the
+// pixels of a split and the fp32 partial slabs (and their reduce) halve at the same wave count
+template <int KS, int BK, int NS, int WJ = 4, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
   constexpr int NB = WJ / 4;         // 128-column x images per stage (n'-tile of 128 * NB)
   constexpr int IMG = BK * 256, STG = (1 + NB) * IMG;
   constexpr int P = BK / 16;        // pieces (4 rows x 256 B) per wave per image
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  static_assert(KG == 1 || (KG == 2 && NS * STG * 2 >= 4 * 64 * 4 * WJ * 16 + 8 * 16 * 8 * 4), "K-group LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[KG * NS * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3;
+  const int kg = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
@@ -1078,7 +1084,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   const int NP = KS * KS * a.g.Cin;
   const int64_t mbeg = (int64_t)split * a.mper;
   const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
-  const int nk = (int)((mend - mbeg + BK - 1) / BK);
+  // K-tiles per group (both groups run the same count: a group past the split's end stages
+  // zero tiles, which keeps every wave's LDS-DMA accounting uniform)
+  const int nk = (int)((mend - mbeg + (int64_t)BK * KG - 1) / ((int64_t)BK * KG));
   const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, x_bytes);
   const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * a.g.Cout * 2);
 
@@ -1112,12 +1120,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   // exact floor(x / d) = umulhi(x, ceil(2^32 / d)) for x < 2^32 / d
   const uint32_t magW = (uint32_t)((0x100000000ull + a.g.Wo - 1) / a.g.Wo);
   const uint32_t magH = (uint32_t)((0x100000000ull + a.g.Ho - 1) / a.g.Ho);
-  int sn = (int)(mbeg / ((int64_t)a.g.Ho * a.g.Wo));
-  int soh = (int)((mbeg / a.g.Wo) % a.g.Ho);
-  int sow = (int)(mbeg % a.g.Wo);
+  const int64_t gbeg = mbeg + (int64_t)kg * BK;    // this K-group's first pixel
+  int sn = (int)(gbeg / ((int64_t)a.g.Ho * a.g.Wo));
+  int soh = (int)((gbeg / a.g.Wo) % a.g.Ho);
+  int sow = (int)(gbeg % a.g.Wo);
   const int xrow = a.xgc * 2;                       // bytes per pixel step
-  auto stage = [&](int kt, int buf) {
-    unsigned char *base = smem + buf * STG + ws * P * 1024;
+  auto stage = [&](int kl, int buf) {               // kl: the group's K-tile index
+    const int kt = kl * KG + kg;                    // the split's K-tile index
+    unsigned char *base = smem + (kg * NS + buf) * STG + ws * P * 1024;
     const int lim = (int)(mend - mbeg) - kt * BK;   // rows r < lim are inside the split
     const int adel = kt * BK * a.g.Cout * 2;
 #pragma unroll
@@ -1139,7 +1149,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
                ok ? (uint32_t)(((n * a.g.H + ih) * a.g.W + iw) * xrow + bgo[e]) : OOB);
       }
     }
-    sow += BK;                                      // next K-tile's first pixel (scalar)
+    sow += BK * KG;                                 // the group's next K-tile (scalar)
     while (sow >= a.g.Wo) {
       sow -= a.g.Wo;
       if (++soh == a.g.Ho) { soh = 0; ++sn; }
@@ -1159,8 +1169,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
 #pragma unroll
     for (int j = 0; j < WJ; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4;
-  auto compute = [&](int kt, int buf) {
-    const unsigned char *As = smem + buf * STG;
+  auto compute = [&](int kl, int buf) {
+    const int kt = kl * KG + kg;
+    const unsigned char *As = smem + (kg * NS + buf) * STG;
     // wave column wn: 64 columns of the one x image (WJ 4), or a whole image (WJ 8)
     const unsigned char *Bs = As + IMG + (NB > 1 ? wn * IMG : 0);
     const int bc0 = NB > 1 ? 0 : wn * 64;
@@ -1187,10 +1198,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
         for (int j = 0; j < WJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (do_bias && kt % ntx == tx) {
-      // thread t: rows (t>>4)*(BK/16) .. of the dy image, chunk t & 15 (8 channels)
+      // thread t of a K-group: rows (t>>4)*(BK/16) .. of its dy image, chunk t & 15 (8 channels)
 #pragma unroll
       for (int q = 0; q < BK / 16; ++q) {
-        const int r = (tid >> 4) * (BK / 16) + q;
+        const int r = ((tid & 255) >> 4) * (BK / 16) + q;    // the K-group's own 256 threads
         const uint4 v = *reinterpret_cast<const uint4 *>(As + swz_off(r, tid & 15));
         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1219,7 +1230,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   }
   __syncthreads();
   if (do_bias) {
-    // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves
+    // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves (of
+    // each K-group, groups in order)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bsum[j] = rows_sum4(bsum[j]);
@@ -1227,15 +1239,40 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
     float *red = reinterpret_cast<float *>(smem);
     if (lane < 16)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[(w * 16 + lane) * 8 + j] = bsum[j];
+      for (int j = 0; j < 8; ++j) red[((kg * 4 + w) * 16 + lane) * 8 + j] = bsum[j];
     __syncthreads();
     if (tid < 128) {
       const int ch = tid >> 3, j = tid & 7;
       const int co = co0 + ch * 8 + j;
-      const float s = (red[(0 * 16 + ch) * 8 + j] + red[(1 * 16 + ch) * 8 + j]) +
-                      (red[(2 * 16 + ch) * 8 + j] + red[(3 * 16 + ch) * 8 + j]);
+      float s = (red[(0 * 16 + ch) * 8 + j] + red[(1 * 16 + ch) * 8 + j]) +
+                (red[(2 * 16 + ch) * 8 + j] + red[(3 * 16 + ch) * 8 + j]);
+      if (KG > 1)
+        s += (red[(4 * 16 + ch) * 8 + j] + red[(5 * 16 + ch) * 8 + j]) +
+             (red[(6 * 16 + ch) * 8 + j] + red[(7 * 16 + ch) * 8 + j]);
       if (co < a.g.Cout) a.dbias_part[((int64_t)split * ntx + tx) * a.g.Cout + co] = s;
     }
+    if (KG > 1) __syncthreads();
+  }
+  if constexpr (KG > 1) {
+    // group 1's accumulators to group 0 through LDS ([wave][i][j][r][lane] floats, each
+    // 64-lane row contiguous), added in a fixed order
+    float *xa = reinterpret_cast<float *>(smem);
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xa[(((w * 4 + i) * WJ + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (kg == 1) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += xa[(((w * 4 + i) * WJ + j) * 4 + r) * 64 + lane];
   }
   float *dst = a.part + (int64_t)split * a.g.Cout * NP;
 #pragma unroll
@@ -2071,6 +2108,20 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   return s;
 }
 
+static int g_wkg = -1;
+static int wgrad_kgroups() {
+  if (g_wkg < 0) {
+    const char *e = getenv("EWVIT_CONV_WKG");
+    g_wkg = e && atoi(e) == 2 ? 2 : 1;
+  }
+  return g_wkg;
+}
+extern "C" int ewvit_conv2d_set_wgrad_kgroups(int kgroups) {
+  const int prev = wgrad_kgroups();
+  g_wkg = kgroups == 2 ? 2 : 1;
+  return prev;
+}
+
 extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {
   const int prev = wgw_variant();
   g_wgw = variant >= 0 && variant <= 4 ? variant : 4;
@@ -2106,14 +2157,20 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
   const int wide = glds ? wgrad_wide(g) : 0;
-  const int64_t splits = wgrad_splits(g, wide);
+  // two K-groups per workgroup (conv_wgrad_glds_kernel KG = 2) for the default 128-column
+  // family on an uncapped grid: half the splits (and fp32 slabs) at the same wave count.
+  // Measured slower (SFE piece 14.27-14.29 -> 14.45-14.47 ms, tools/piece_ab.sh): the two
+  // groups' lockstep barriers at one workgroup per CU cost more than the halved slabs save —
+  // off unless EWVIT_CONV_WKG = 2 (A/B)
+  const int kgrp = (glds && !wide && (glds_variant() & 7) == 1 && g_grid_cap == 0 && wgrad_kgroups() == 2) ? 2 : 1;
+  const int64_t splits = (wgrad_splits(g, wide) + kgrp - 1) / kgrp;
   a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
   const int tnw = wide ? 2 * CBN : CBN;
   const int ntx = (taps * g.Cin + tnw - 1) / tnw, nty = (g.Cout + CBM - 1) / CBM;
   const int gv = glds_variant() & 7;
   const int64_t kq = !glds ? CBK : wide ? (wide == 1 ? 64 : 32) : ((gv == 3 || gv == 4) ? 32 : 64);  // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
-  mper = (mper + kq - 1) / kq * kq;
+  mper = (mper + kq * kgrp - 1) / (kq * kgrp) * (kq * kgrp);
   a.mper = mper;
   const int sp = (int)((a.M + mper - 1) / mper);
   // the glds kernel leaves bias partials per (split, n'-tile); the old one per split
@@ -2146,7 +2203,10 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
     if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
     else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
   } while (0)
-    if (wide == 1) EWVIT_GLDS_WG(64, 2, 8);
+    if (kgrp == 2) {
+      if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, 64, 2, 4, 2>), dim3(nwg), dim3(512), 0, s, a, xb, ntx, nty);
+      else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, 64, 2, 4, 2>), dim3(nwg), dim3(512), 0, s, a, xb, ntx, nty);
+    } else if (wide == 1) EWVIT_GLDS_WG(64, 2, 8);
     else if (wide == 2) EWVIT_GLDS_WG(32, 2, 8);
     else if (wide == 3) EWVIT_GLDS_WG(32, 3, 8);
     else switch (gvs) {

@@ -319,6 +319,75 @@ __global__ __launch_bounds__(256) void se_mlp_gate_kernel(const float *__restric
   s_out[(int64_t)n * C + c] = sigmoid_f(z);
 }
 
+// F2 + the excite pass in one launch: block (n, 256-channel chunk) forms the frame's hidden
+// vector and its chunk's gates exactly as se_mlp_gate_kernel does, then scales the chunk's
+// HW rows of x (y = x * s, as se_scale_kernel) — 32 channel vectors x 8 row groups, the first
+// 4 rows of every thread loaded before the gate is known (they do not depend on it)
+template <int DT>
+__global__ __launch_bounds__(256) void se_gate_scale_kernel(const float *__restrict__ part, int nb,
+                                                            const float *__restrict__ b1,
+                                                            const float *__restrict__ w2,
+                                                            const float *__restrict__ b2, int C, int Csq,
+                                                            float *__restrict__ h1_out, float *__restrict__ s_out,
+                                                            const void *__restrict__ x, void *__restrict__ y, int HW) {
+  extern __shared__ float gsm[];
+  float *a1 = gsm, *sv = gsm + ((Csq + 3) & ~3);
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const int cv = tid & 31, rg = tid >> 5;
+  const int c0 = blockIdx.y * 256 + cv * 8;
+  const bool active = c0 < C;
+  const int64_t base = (int64_t)n * HW * C + c0;
+  constexpr int PF = 4;
+  float pre[PF][8];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) {
+    const int r = rg + 8 * q;
+    if (active && r < HW) se_ld8<DT>(x, base + (int64_t)r * C, pre[q]);
+  }
+  const float *pp = part + (int64_t)n * nb * Csq;
+  for (int j = tid; j < Csq; j += 256) {
+    const float h = se_part_sum(pp, nb, Csq, j) + (b1 ? b1[j] : 0.f);
+    a1[j] = silu_f(h);
+    if (blockIdx.y == 0) h1_out[(int64_t)n * Csq + j] = h;
+  }
+  __syncthreads();
+  const int c = blockIdx.y * 256 + tid;
+  if (c < C) {
+    const float z = se_row_dot(w2 + (int64_t)c * Csq, a1, Csq) + (b2 ? b2[c] : 0.f);
+    const float sg = sigmoid_f(z);
+    s_out[(int64_t)n * C + c] = sg;
+    sv[tid] = sg;
+  }
+  __syncthreads();
+  if (!active) return;
+  float sc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sc[j] = sv[cv * 8 + j];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) {
+    const int r = rg + 8 * q;
+    if (r < HW) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pre[q][j] = fmaf(pre[q][j], sc[j], 0.f);
+      se_st8<DT>(y, base + (int64_t)r * C, pre[q]);
+    }
+  }
+  for (int r0 = rg + 8 * PF; r0 < HW; r0 += 8 * PF) {
+    float v[PF][8];
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+      if (r0 + 8 * q < HW) se_ld8<DT>(x, base + (int64_t)(r0 + 8 * q) * C, v[q]);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      if (r0 + 8 * q < HW) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[q][j] = fmaf(v[q][j], sc[j], 0.f);
+        se_st8<DT>(y, base + (int64_t)(r0 + 8 * q) * C, v[q]);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void se_mlp_dh_part_kernel(const float *__restrict__ ds,
                                                              const float *__restrict__ s,
                                                              const float *__restrict__ w2, int C, int Csq,
@@ -699,6 +768,33 @@ extern "C" int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int
   hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
                      (size_t)Csq * sizeof(float), st, workspace, nb, b1, w2, b2, (int)C, (int)Csq, h1, s);
   return launch_status("se_squeeze_mlp_fwd");
+}
+
+// the whole squeeze-excitation forward in two launches: ewvit_se_squeeze_mlp_fwd's squeeze +
+// hidden-partials kernel, then the gate and the excite pass y = x * s together
+extern "C" int ewvit_se_forward(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1,
+                                const float *b1, const float *w2, const float *b2, int64_t Csq, float *s0, float *h1,
+                                float *s, void *y, float *workspace, void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "se_forward")) return rc;
+  if (int rc = se_mlp_check(N, C, Csq, "se_forward")) return rc;
+  EWVIT_CHECK_ARG(x && w1 && w2 && s0 && h1 && s && y && workspace && HW < (1 << 30), "se_forward: bad args");
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  const dim3 g1((unsigned)N, (unsigned)nb);
+  const dim3 g2((unsigned)N, (unsigned)((C + 255) / 256));
+  const size_t lds = (size_t)(((Csq + 3) & ~3) + 256) * sizeof(float);
+  if (dtype == EWVIT_BF16) {
+    hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_BF16>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
+                       (int)C, (int)Csq, s0, workspace);
+    hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_BF16>, g2, dim3(256), lds, st, workspace, nb, b1, w2, b2, (int)C,
+                       (int)Csq, h1, s, x, y, (int)HW);
+  } else {
+    hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_F32>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
+                       (int)C, (int)Csq, s0, workspace);
+    hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_F32>, g2, dim3(256), lds, st, workspace, nb, b1, w2, b2, (int)C,
+                       (int)Csq, h1, s, x, y, (int)HW);
+  }
+  return launch_status("se_forward");
 }
 
 // squeeze-excite backward of the excite vector: ds = sum_hw dy * x inside the first

@@ -56,6 +56,7 @@ SIGNATURES = {
     'ewvit_set_grid_cap': [_i32],
     'ewvit_dwconv3x3_set_segs': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
+    'ewvit_conv2d_set_wgrad_kgroups': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -91,6 +92,7 @@ SIGNATURES = {
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_se_forward': [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_dwconv3x3_fwd_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     'ewvit_dwconv3x3_bwd_data_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp],

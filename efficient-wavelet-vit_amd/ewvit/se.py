@@ -59,13 +59,11 @@ class SqueezeExciteFn(torch.autograd.Function):
         h1 = torch.empty(N, Csq, dtype=torch.float32, device=x.device)
         s = torch.empty(N, C, dtype=torch.float32, device=x.device)
         fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=x.device)
-        # squeeze (mean over HW) inside the MLP's first kernel
-        L.call('ewvit_se_squeeze_mlp_fwd', L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
-               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(s), L.ptr(fws), L.stream(s),
-               work={'bytes': xc.numel() * xc.element_size()})
         y = torch.empty_like(xc)
-        L.call('ewvit_se_scale', L.ptr(xc), L.dt(xc), L.ptr(s), None, L.ptr(y), N, HW, C, L.stream(y),
-               work={'bytes': 2 * xc.numel() * xc.element_size()})
+        # squeeze (mean over HW) inside the MLP's first kernel; gates + excite pass in the second
+        L.call('ewvit_se_forward', L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
+               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(s), L.ptr(y), L.ptr(fws), L.stream(y),
+               work={'bytes': 3 * xc.numel() * xc.element_size()})
         ctx.save_for_backward(xc, w1, w2, s0, h1, s)
         ctx.has_b = (b1 is not None, b2 is not None)
         return y
@@ -130,12 +128,11 @@ class BnActSEFn(torch.autograd.Function):
         h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
         sc = torch.empty(N, C, dtype=torch.float32, device=dev)
         fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-        L.call('ewvit_se_squeeze_mlp_fwd', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
-               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(fws), L.stream(sc),
-               work={'bytes': x2.numel() * x2.element_size()})
         y = torch.empty_like(x2)
-        L.call('ewvit_se_scale', L.ptr(x2), L.dt(x2), L.ptr(sc), None, L.ptr(y), N, HW, C, L.stream(y),
-               work={'bytes': 2 * x2.numel() * x2.element_size()})
+        # squeeze + MLP hidden partials, then the gates and the excite pass in one launch
+        L.call('ewvit_se_forward', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
+               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(y), L.ptr(fws), L.stream(y),
+               work={'bytes': 3 * x2.numel() * x2.element_size()})
         ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
         ctx.cfg = (act, b1 is not None, b2 is not None)
         return y

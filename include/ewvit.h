@@ -353,6 +353,12 @@ int ewvit_conv2d_set_glds(int variant);
  * <= 1/8 of it; 4 = auto (2 for n' >= 2048 over >= 64K output pixels, else 0).  Replaces nothing in the reference (tuning knob of csrc/conv.hip).
  * Returns the previous setting. */
 int ewvit_conv2d_set_wgrad_wide(int variant);
+/* Weight-gradient K-groups (A/B measurement; default from EWVIT_CONV_WKG, else 1): 2 = two
+ * groups of 4 waves per workgroup, each multiplying every other K-tile of a pixel split and
+ * summed through LDS (half the splits and fp32 slabs), for the default 128-column family on
+ * an uncapped grid; 1 = one group.  Replaces nothing in the reference.  Returns the previous
+ * setting. */
+int ewvit_conv2d_set_wgrad_kgroups(int kgroups);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs
@@ -466,6 +472,13 @@ int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1, const flo
 int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1,
                              const float *b1, const float *w2, const float *b2, int64_t Csq, float *s0, float *h1,
                              float *s, float *workspace, void *stream);
+/* The whole squeeze-excitation forward (torchvision SqueezeExcitation, sfe.py:111-113): the
+ * squeeze + MLP of ewvit_se_squeeze_mlp_fwd (s0, h1, s written out for the backward) and the
+ * excite pass y = x * s[n, c] ([N][HW][C], dtype) — the gates and the excite pass share one
+ * launch (2 in all; bit-identical to ewvit_se_squeeze_mlp_fwd + ewvit_se_scale). */
+int ewvit_se_forward(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1, const float *b1,
+                     const float *w2, const float *b2, int64_t Csq, float *s0, float *h1, float *s, void *y,
+                     float *workspace, void *stream);
 int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,
                              const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
                              int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,

@@ -12,20 +12,24 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0, 'w1', 'w2', 'w3'],
+@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0, 'w1', 'w2', 'w3', 'k2'],
                 ids=['glds1', 'glds9', 'glds13', 'glds15', 'glds2', 'glds3', 'glds4', 'regstage',
-                     'glds9-wgw1', 'glds9-wgw2', 'glds9-wgw3'])
+                     'glds9-wgw1', 'glds9-wgw2', 'glds9-wgw3', 'glds9-wkg2'])
 def glds(request):
     """Run each case on every LDS-DMA configuration and on the register-staged kernels;
-    'wN': glds9 with 256-column weight-gradient tiles of variant N (the others: auto, 4)."""
+    'wN': glds9 with 256-column weight-gradient tiles of variant N (the others: auto, 4);
+    'k2': glds9 with two K-groups per weight-gradient workgroup (off by default)."""
     import ewvit
     lib = ewvit._lib.load()
-    v, w = (9, int(request.param[1])) if isinstance(request.param, str) else (request.param, 4)
+    p = request.param
+    v, w = (9, int(p[1])) if isinstance(p, str) and p[0] == 'w' else ((9, 4) if p == 'k2' else (p, 4))
     prev = lib.ewvit_conv2d_set_glds(v)
     prevw = lib.ewvit_conv2d_set_wgrad_wide(w)
+    prevk = lib.ewvit_conv2d_set_wgrad_kgroups(2 if p == 'k2' else 1)
     yield v
     lib.ewvit_conv2d_set_glds(prev)
     lib.ewvit_conv2d_set_wgrad_wide(prevw)
+    lib.ewvit_conv2d_set_wgrad_kgroups(prevk)
 
 
 def rel(a, b):
@@ -67,6 +71,8 @@ def rel(a, b):
     (1, 24, 24, 8, 7, 5, 1, 3),          # one 16-wide output tile, rows < the band height
     (2, 16, 16, 64, 10, 16, 1, 3),       # small-channel wgrad (W % 8 == 0): 16 -> 64 with bias
     (3, 24, 24, 24, 7, 24, 1, 3),        # small-channel wgrad, odd H (a 1-row tail band)
+    (64, 160, 160, 960, 14, 14, 1, 1),   # bench-size stage-5 expand: many pixel splits (two K-groups)
+    (64, 256, 256, 1536, 7, 7, 1, 1),    # bench-size stage-6 expand
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
     import ewvit.conv as ec

@@ -210,3 +210,36 @@ def test_bn_act_se_matches_two_step_path():
     assert rel(a[2], b[2]) < 1e-2 and rel(a[3], b[3]) < 1e-2
     for p, q in zip(a[4], b[4]):
         assert torch.equal(p, q)
+
+
+@pytest.mark.parametrize('N,C,HW,csq,dtype', [(64, 1536, 49, 64, torch.bfloat16), (64, 960, 196, 40, torch.bfloat16),
+                                              (3, 200, 9, 6, torch.bfloat16), (5, 264, 30, 16, torch.float32)])
+def test_se_forward_matches_two_launch_path(N, C, HW, csq, dtype):
+    """ewvit_se_forward (gates + excite pass in one launch) is bit-identical to
+    ewvit_se_squeeze_mlp_fwd + ewvit_se_scale (the same operations in the same order)."""
+    import ewvit
+    L = ewvit._lib
+    g = torch.Generator().manual_seed(C + HW)
+    x = torch.randn(N, HW, C, generator=g).to(DEV, dtype)
+    w1 = (torch.randn(csq, C, generator=g) / C ** 0.5).to(DEV)
+    b1 = (torch.randn(csq, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(C, csq, generator=g) / csq ** 0.5).to(DEV)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    ws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, csq) // 4, device=DEV)
+    out = []
+    for fused in (False, True):
+        s0, h1, s = torch.empty(N, C, device=DEV), torch.empty(N, csq, device=DEV), torch.empty(N, C, device=DEV)
+        y = torch.empty_like(x)
+        if fused:
+            L.call('ewvit_se_forward', L.ptr(x), L.dt(x), N, HW, C, L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), csq,
+                   L.ptr(s0), L.ptr(h1), L.ptr(s), L.ptr(y), L.ptr(ws), L.stream(x))
+        else:
+            L.call('ewvit_se_squeeze_mlp_fwd', L.ptr(x), L.dt(x), N, HW, C, L.ptr(w1), L.ptr(b1), L.ptr(w2),
+                   L.ptr(b2), csq, L.ptr(s0), L.ptr(h1), L.ptr(s), L.ptr(ws), L.stream(x))
+            L.call('ewvit_se_scale', L.ptr(x), L.dt(x), L.ptr(s), None, L.ptr(y), N, HW, C, L.stream(x))
+        out.append((s0, h1, s, y))
+    torch.cuda.synchronize()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    ref = x.float() * out[0][2].view(N, 1, C)
+    assert float((out[1][3].float() - ref).abs().max()) <= 2 ** -7 * float(ref.abs().max())
