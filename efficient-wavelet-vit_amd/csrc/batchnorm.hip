@@ -915,18 +915,22 @@ extern "C" int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtyp
 extern "C" int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
                                      const float *gamma, const float *beta, const float *save_mean,
                                      const float *save_invstd, int act, float *dgamma, float *dbeta,
-                                     const float *row_scale, int64_t HW, const float *part, int nrc, void *stream) {
+                                     const float *row_scale, int64_t HW, const float *part, int nrc, int groups,
+                                     void *stream) {
   EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && part && dtype_ok(dtype), "bn_bwd_partials: bad args");
   EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_partials: C=%lld", (long long)C);
   EWVIT_CHECK_ARG(act >= 0 && act <= 2 && !(row_scale && act), "bn_bwd_partials: act=%d (row_scale needs act 0)", act);
   EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 65535, "bn_bwd_partials: %d partial rows", nrc);
   EWVIT_CHECK_ARG(!row_scale || (HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31)), "bn_bwd_partials: M=%lld rows of %lld",
                   (long long)M, (long long)HW);
+  EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M % groups == 0 && (groups == 1 || !row_scale),
+                  "bn_bwd_partials: %d groups", groups);
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const BnGeo geo = bn_geo(C);
-  const int64_t rpb = bn_rows_per_block(geo, M, 1);
-  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+  const int64_t Mg = M / groups;
+  const int64_t rpb = bn_rows_per_block(geo, Mg, groups);
+  dim3 dgrid((unsigned)((Mg + rpb - 1) / rpb), geo.nch, groups);
   if (row_scale) {
     if (dtype == EWVIT_BF16)
       hipLaunchKernelGGL((bn_bwd_dx_kernel<EWVIT_BF16, 0, 1>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean,
@@ -940,7 +944,7 @@ extern "C" int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, in
   }
 #define BN_DX(DTV, ACTV)                                                                                              \
   hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean, save_invstd,   \
-                     gamma, beta, part, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0)
+                     gamma, beta, part, nrc, dx, Mg, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0)
   BN_DISPATCH(BN_DX);
 #undef BN_DX
   return launch_status("bn_bwd_partials");

@@ -157,6 +157,8 @@ struct BnBwdStats {
   const bf16_t *x = nullptr;
   const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr, *rscale = nullptr;
   int act = 0, hw = 1;
+  int64_t grows = 0;   // rows per BatchNorm row group (consecutive batch slices with their own
+                       // statistics: mean / invstd [group][C]); 0 = one group
 };
 
 inline bool dtype_ok(int dt) { return dt == EWVIT_F32 || dt == EWVIT_BF16; }

@@ -695,7 +695,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   constexpr int A_B = BM * BK * 2, B_B = BN_ * BK * 2, STG = A_B + B_B;
   constexpr int PA = BM / 8 / NW, PB = BN_ / 8 / NW;   // 1 KiB pieces per wave per K-tile
   static_assert(PB >= 1, "tile shape");
-  constexpr int RED_B = DGRAD ? 0 : BM / 64 * BN_ * 2 * 4;   // fwd BN statistics image, after the ring
+  // BatchNorm statistics image (fwd, or dgrad with BST), after the ring
+  constexpr int RED_B = (DGRAD && !BST) ? 0 : BM / 64 * BN_ * 2 * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG + RED_B];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ws = __builtin_amdgcn_readfirstlane(w);   // wave id, provably uniform
@@ -987,16 +988,22 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     for (int j = 0; j < J; ++j) {
       const int col = n0 + wn * WN + j * 16 + fq * 4;
       if (col >= a.Ncol) continue;
+      const int gi = col / a.ogc;
+      const bf16_t *xg = a.bwd.x + (int64_t)gi * a.ogs + (col - gi * a.ogc);   // the BN input, dx's layout
       uint2 xq[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t row = m0 + wm * 64 + i * 16 + fr;
-        xq[i] = row < a.M ? *reinterpret_cast<const uint2 *>(a.bwd.x + row * a.ogc + col) : make_uint2(0u, 0u);
+        xq[i] = row < a.M ? *reinterpret_cast<const uint2 *>(xg + row * a.ogc) : make_uint2(0u, 0u);
       }
-      const float4 mu4 = *reinterpret_cast<const float4 *>(a.bwd.mean + col);
-      const float4 iv4 = *reinterpret_cast<const float4 *>(a.bwd.invstd + col);
-      const float4 ga4 = a.bwd.gamma ? *reinterpret_cast<const float4 *>(a.bwd.gamma + col) : make_float4(1.f, 1.f, 1.f, 1.f);
-      const float4 be4 = a.bwd.beta ? *reinterpret_cast<const float4 *>(a.bwd.beta + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      // statistics: [row group][C] of a row-grouped BN, [channel group][C] = col of a grouped dx;
+      // the affine parameters are shared by the groups
+      const int64_t sidx = (a.bwd.grows ? m0 / a.bwd.grows * a.ogc : 0) + col;
+      const int pidx = col - gi * a.ogc;
+      const float4 mu4 = *reinterpret_cast<const float4 *>(a.bwd.mean + sidx);
+      const float4 iv4 = *reinterpret_cast<const float4 *>(a.bwd.invstd + sidx);
+      const float4 ga4 = a.bwd.gamma ? *reinterpret_cast<const float4 *>(a.bwd.gamma + pidx) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 be4 = a.bwd.beta ? *reinterpret_cast<const float4 *>(a.bwd.beta + pidx) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, iv[4] = {iv4.x, iv4.y, iv4.z, iv4.w};
       const float ga[4] = {ga4.x, ga4.y, ga4.z, ga4.w}, be[4] = {be4.x, be4.y, be4.z, be4.w};
 #pragma unroll
@@ -1031,8 +1038,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // previous tile's readers finished before this tile's K-loop barriers
   // (dgrad: no image after the ring — its partials go into ring slot 0 once every wave has
   // finished reading it; an uncapped grid, so no next tile's K-tiles are landing there)
-  float *red = reinterpret_cast<float *>(smem + (DGRAD ? 0 : NS * STG));
-  if (DGRAD) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float *red = reinterpret_cast<float *>(smem + NS * STG);
   if (fr == 0)
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -1050,9 +1056,16 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 #pragma unroll
       for (int q = 0; q < BM / 64; ++q) { S += red[(q * BN_ + tid) * 2]; Q += red[(q * BN_ + tid) * 2 + 1]; }
       const int64_t t = m0 / BM;
-      float *dst = DGRAD ? a.bwd.part : a.bn_part;
-      dst[t * 2 * a.Ncol + col] = S;
-      dst[t * 2 * a.Ncol + a.Ncol + col] = Q;
+      if (DGRAD) {
+        // channel group gi of a grouped dx is its own BatchNorm group: rows [gi][m-tile][2 ogc]
+        const int gi = col / a.ogc, cl = col - gi * a.ogc;
+        float *pr = a.bwd.part + ((int64_t)gi * ((a.M + BM - 1) / BM) + t) * 2 * a.ogc;
+        pr[cl] = S;
+        pr[a.ogc + cl] = Q;
+      } else {
+        a.bn_part[t * 2 * a.Ncol + col] = S;
+        a.bn_part[t * 2 * a.Ncol + a.Ncol + col] = Q;
+      }
       if (!DGRAD && t == 0 && a.bn_shift_out) a.bn_shift_out[col] = a.bn_shift ? a.bn_shift[col] : 0.f;
     }
   }
@@ -1678,7 +1691,7 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
       if (bm_out) *bm_out = 128;
       const int64_t nt = (a.M + 127) / 128 * ntn;
       if (nt >= (int64_t)1 << 31) return false;
-      const dim3 g1((unsigned)nt);
+      const dim3 g1((unsigned)(g_grid_cap > 0 && nt > g_grid_cap ? g_grid_cap : nt));
 #define EWVIT_GLDS_BST(BN__, NS_, WC_)                                                                              \
   do {                                                                                                            \
     if (a.g.ks == 1)                                                                                              \
@@ -1990,48 +2003,59 @@ extern "C" int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void 
   return launch_status("conv2d_bwd_data_add");
 }
 
-// partial rows ewvit_conv2d_bwd_data_bn leaves for this shape at most (one per 128 dx rows;
-// the launch reports the exact count), or 0 when the shape does not take it: stride 1, the
-// LDS-DMA dgrad (ewvit_conv2d_bwd_data_add_ok), no workgroup cap in force
+// partial rows per channel group ewvit_conv2d_bwd_data_bn leaves for this shape (one per 128
+// dx rows), or 0 when the shape does not take it: stride 1, the LDS-DMA dgrad
+// (ewvit_conv2d_bwd_data_add_ok)
 extern "C" int64_t ewvit_conv2d_bwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                                            int stride) {
-  if (stride != 1 || g_grid_cap > 0 || !ewvit_conv2d_bwd_data_add_ok(N, H, W, Cin, Cout, ksize, stride) ||
+  if (stride != 1 || !ewvit_conv2d_bwd_data_add_ok(N, H, W, Cin, Cout, ksize, stride) ||
       Cin > 65536)
     return 0;
   return (N * H * W + 127) / 128;
 }
 
-// dx = dgrad(dy) (+ addend, when not null) and the backward statistics of the BatchNorm
-// whose output was this conv's input (bx: that BN's input [N,H,W,Cin] bf16; mean / invstd its
-// saved statistics; gamma / beta or null; act 0/1/2; rscale [N] with act 0: the drop-path
-// factor per frame of the MBConv tail, or null): part [ewvit_conv2d_bwd_bn_rows][2 Cin] gets
-// per 128- or 256-row m-tile (sum g, sum g * xhat) of the bf16-rounded dx; *nrc_out = the
-// partial rows written (what ewvit_bn_bwd_partials is given)
+// dx = dgrad(dy) (+ addend, when not null; plain dx only) and the backward statistics of the
+// BatchNorm whose output was this conv's input (bx: that BN's input, dx's layout, bf16; mean /
+// invstd its saved statistics; gamma / beta or null; act 0/1/2; rscale [N] with act 0: the
+// drop-path factor per frame of the MBConv tail, or null).  BatchNorm groups: a grouped dx
+// (dx_group_c, dx_group_stride: the multiscale conv's level-major input) has one per channel
+// group, mean / invstd [groups][group_c]; a plain dx with bn_group_rows > 0 (a multiple of 128
+// dividing N*H*W) one per slice of that many rows, mean / invstd [groups][Cin].  part
+// [groups][ewvit_conv2d_bwd_bn_rows per channel group or ... / groups per row group][2 C]
+// gets per 128-row m-tile (sum g, sum g * xhat) of the bf16-rounded dx; *nrc_out = the partial
+// rows per BatchNorm group (what ewvit_bn_bwd_partials is given)
 extern "C" int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N,
                                         int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
-                                        const void *bx, const float *mean, const float *invstd, const float *gamma,
-                                        const float *beta, int act, const float *rscale, float *part, int *nrc_out,
-                                        void *stream) {
+                                        int64_t dx_group_c, int64_t dx_group_stride, const void *bx,
+                                        const float *mean, const float *invstd, const float *gamma, const float *beta,
+                                        int act, const float *rscale, int64_t bn_group_rows, float *part,
+                                        int *nrc_out, void *stream) {
   EWVIT_CHECK_ARG(dy && wp_t && dx && bx && mean && invstd && part && nrc_out && act >= 0 && act <= 2 &&
                       !(rscale && act),
                   "conv2d_bwd_data_bn: bad args");
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
   if (int rc = check_geom(g, "conv2d_bwd_data_bn")) return rc;
+  if (int rc = check_group(dx_group_c, dx_group_stride, Cin, N * H * W, "conv2d_bwd_data_bn", "dx")) return rc;
   EWVIT_CHECK_ARG(ewvit_conv2d_bwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) > 0,
                   "conv2d_bwd_data_bn: shape not supported (query ewvit_conv2d_bwd_bn_rows)");
+  EWVIT_CHECK_ARG(!(addend && dx_group_stride), "conv2d_bwd_data_bn: an addend needs a plain dx");
+  EWVIT_CHECK_ARG(bn_group_rows == 0 || (!dx_group_stride && bn_group_rows % 128 == 0 &&
+                                         (N * H * W) % bn_group_rows == 0),
+                  "conv2d_bwd_data_bn: BatchNorm row groups of %lld rows", (long long)bn_group_rows);
   FwdArgs a;
   a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx; a.g = g;
   a.M = (int64_t)g.N * g.H * g.W; a.Ncol = g.Cin; a.KC = g.Cout;
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
-  a.sgc = g.Cout; a.sgs = 0; a.ogc = g.Cin; a.ogs = 0;
+  a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
   a.addend = (const bf16_t *)addend;
   a.bwd.part = part; a.bwd.x = (const bf16_t *)bx; a.bwd.mean = mean; a.bwd.invstd = invstd; a.bwd.gamma = gamma;
-  a.bwd.beta = beta; a.bwd.rscale = rscale; a.bwd.act = act; a.bwd.hw = (int)(H * W);
+  a.bwd.beta = beta; a.bwd.rscale = rscale; a.bwd.act = act; a.bwd.hw = (int)(H * W); a.bwd.grows = bn_group_rows;
   const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
   int bm = 0;
   EWVIT_CHECK_ARG(launch_glds<true>(a, sb, as_stream(stream), &bm) && bm > 0,
                   "conv2d_bwd_data_bn: LDS-DMA kernel refused the shape");
-  *nrc_out = (int)((a.M + bm - 1) / bm);
+  const int64_t ntm = (a.M + bm - 1) / bm;
+  *nrc_out = (int)(bn_group_rows ? bn_group_rows / bm : ntm);
   return launch_status("conv2d_bwd_data_bn");
 }
 

@@ -97,9 +97,9 @@ SIGNATURES = {
     'ewvit_dwconv3x3_bwd_data_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp],
     'ewvit_bn_bwd_partials': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp,
-                              _i32, _vp],
-    'ewvit_conv2d_bwd_data_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
-                                 _vp, _i32, _vp, _vp, _vp, _vp],
+                              _i32, _i32, _vp],
+    'ewvit_conv2d_bwd_data_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
+                                 _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
 }
 
 # size queries: name -> (restype, argtypes)

@@ -32,12 +32,12 @@ class BwdStatsLink:
     (`partials_for`): a second consumer's gradient added by autograd gives a new tensor (the
     link holds a reference to the produced one, so autograd cannot accumulate into it in
     place) and the BN runs its own reduction."""
-    __slots__ = ('key', 'x', 'mean', 'invstd', 'gamma', 'beta', 'act', 'rscale', 'part', 'nrc', 'dx', 'ver')
+    __slots__ = ('key', 'x', 'mean', 'invstd', 'gamma', 'beta', 'act', 'rscale', 'groups', 'part', 'nrc', 'dx', 'ver')
 
-    def __init__(self, y, x, mean, invstd, gamma, beta, act, rscale=None):
+    def __init__(self, y, x, mean, invstd, gamma, beta, act, rscale=None, groups=1):
         self.key = (y.data_ptr(), tuple(y.shape), y.dtype)
         self.x, self.mean, self.invstd, self.gamma, self.beta = x, mean, invstd, gamma, beta
-        self.act, self.rscale = act, rscale
+        self.act, self.rscale, self.groups = act, rscale, groups
         self.part = self.dx = None
         self.nrc = 0
         self.ver = -1
@@ -57,16 +57,36 @@ class BwdStatsLink:
 
 
 _bwd_offered = None
+_zeros = {}
 
 
-def offer_bwd_link(y, x, mean, invstd, gamma, beta, act, rscale=None):
-    """Offer the backward statistics of the BN that produced y (4-D NHWC bf16, one group) to
-    y's consumer; returns the link (kept by the BN's backward), or None."""
+def fold_bwd_partials(part, nrc, groups, C):
+    """(part, nrc) with at most BWD_LINK_MAX_ROWS partial rows per group: a producer over a big
+    map (the MWT's 2.4 M-row convs: 6272 m-tiles per level) leaves more than the dx pass should
+    finalise from per block, so one launch folds them in a fixed order (ewvit_bn_fold_partials)."""
+    if nrc <= BWD_LINK_MAX_ROWS:
+        return part, nrc
+    nout = 256
+    dev = part.device
+    z = _zeros.get((dev, C))
+    if z is None:
+        z = _zeros[(dev, C)] = torch.zeros(C, dtype=torch.float32, device=dev)
+    out = torch.empty(groups * nout, 2 * C, dtype=torch.float32, device=dev)
+    sh = torch.empty(groups, C, dtype=torch.float32, device=dev)
+    L.call('ewvit_bn_fold_partials', L.ptr(part), nrc, L.ptr(z), L.ptr(out), nout, L.ptr(sh), C, groups,
+           L.stream(part), work={'bytes': part.numel() * 4})
+    return out, nout
+
+
+def offer_bwd_link(y, x, mean, invstd, gamma, beta, act, rscale=None, groups=1):
+    """Offer the backward statistics of the BN that produced y (4-D NHWC bf16; `groups`
+    consecutive batch slices with their own statistics) to y's consumer; returns the link
+    (kept by the BN's backward), or None."""
     global _bwd_offered
     if not (_BWD_LINK and y.dim() == 4 and y.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
         _bwd_offered = None
         return None
-    _bwd_offered = BwdStatsLink(y, x, mean, invstd, gamma, beta, act, rscale)
+    _bwd_offered = BwdStatsLink(y, x, mean, invstd, gamma, beta, act, rscale, groups)
     return _bwd_offered
 
 
@@ -124,8 +144,7 @@ class BatchNormActFn(torch.autograd.Function):
         if training:
             ctx.save_for_backward(xc, weight, bias, mean, invstd)
         ctx.cfg = (training, act, M, C, groups)
-        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, act) \
-            if training and groups == 1 and ctx.cap == 0 else None
+        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, act, None, groups) if training else None
         return y
 
     @staticmethod
@@ -150,7 +169,7 @@ class BatchNormActFn(torch.autograd.Function):
             # the reduction was summed by the kernel that produced dy: the dx pass only
             L.call('ewvit_bn_bwd_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
                    L.ptr(bias), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), None, 1, L.ptr(pr[0]), pr[1],
-                   L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+                   groups, L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
             return dx, dg, db, None, None, None, None, None, None, None, None, None
         ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=dy.device)
         L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
@@ -217,7 +236,7 @@ class BNDropAddFn(torch.autograd.Function):
         ctx.save_for_backward(xc, weight, bias, mean, invstd, scale)
         ctx.cfg = (M, C, M // N, skip.dtype)
         ctx.link = link if link is not None and link.armed else None
-        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, 0, scale) if L.current_cap() == 0 else None
+        ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, 0, scale)
         return y
 
     @staticmethod
@@ -234,7 +253,7 @@ class BNDropAddFn(torch.autograd.Function):
             # g = dy * scale[n] summed by the next conv's input-gradient epilogue: dx pass only
             L.call('ewvit_bn_bwd_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
                    L.ptr(bias), L.ptr(mean), L.ptr(invstd), 0, L.ptr(dg), L.ptr(db), L.ptr(scale), HW, L.ptr(pr[0]),
-                   pr[1], L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+                   pr[1], 1, L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
         else:
             ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dy.device)
             L.call('ewvit_bn_bwd_scaled', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),

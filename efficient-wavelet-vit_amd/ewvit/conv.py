@@ -157,6 +157,29 @@ def _pack(weight, cin_pad, fwd=True, bwd=False):
     return wp, wpt
 
 
+def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
+    """(groups, rows per group's slice, partial rows per group, channels per group) when this
+    conv's input gradient can sum the backward statistics of the BatchNorm that produced its
+    input (link `bl`), else None.  The BN's groups are either the input's levels (the level-
+    major input read as a channel concatenation: channel groups of dx) or equal row slices of a
+    plain input (per-level statistics of the MWT's shared BatchNorms); 128-row m-tiles."""
+    if bl is None or xdt != torch.bfloat16 or bl.x.shape != xc.shape:
+        return None
+    tiles = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cx, Cout, k, stride))
+    if tiles <= 0 or (skip is not None and levels > 1):
+        return None
+    if skip is not None and not L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
+        return None
+    if levels > 1:
+        if bl.groups != levels:
+            return None
+        return levels, 0, tiles, Cx // levels
+    M = N * H * W
+    if bl.groups > 1 and (M % bl.groups or (M // bl.groups) % 128):
+        return None
+    return bl.groups, (M // bl.groups if bl.groups > 1 else 0), tiles // bl.groups, Cx
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
@@ -167,7 +190,7 @@ class Conv2dFn(torch.autograd.Function):
             grads.note_use(bias)
         ctx.link = _take_link(x) if levels == 1 else None
         # the backward statistics of the BatchNorm that produced x, summed by the dgrad epilogue
-        ctx.bnlink = bnmod.take_bwd_link(x) if levels == 1 and ctx.needs_input_grad[0] else None
+        ctx.bnlink = bnmod.take_bwd_link(x) if ctx.needs_input_grad[0] else None
         NL, Cz, H, W = x.shape
         if NL % levels:
             raise ValueError(f'conv2d: batch {NL} is not a multiple of levels={levels}')
@@ -235,18 +258,18 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            rows = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cx, Cout, k, stride)) \
-                if bl is not None and xdt == torch.bfloat16 and bl.x.shape == xc.shape else 0
-            if 0 < rows <= bnmod.BWD_LINK_MAX_ROWS and (
-                    skip is None or L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride)):
+            lk = _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            if lk is not None:
                 # dx (+ the skip gradient) and the producing BatchNorm's backward sums in one epilogue
+                groups, grows, rows, Cg = lk
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if skip is not None else None
-                part = torch.empty(rows, 2 * Cx, dtype=torch.float32, device=xc.device)
+                part = torch.empty(groups * rows, 2 * Cg, dtype=torch.float32, device=xc.device)
                 nrc = ctypes.c_int(0)
                 L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), L.ptr(sk), N, H, W, Cx, Cout,
-                       k, stride, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta),
-                       bl.act, L.ptr(bl.rscale), L.ptr(part), ctypes.byref(nrc), L.stream(dx), work=work)
-                bl.fulfil(part, nrc.value, dx)
+                       k, stride, gc, gs, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma),
+                       L.ptr(bl.beta), bl.act, L.ptr(bl.rscale), grows, L.ptr(part), ctypes.byref(nrc), L.stream(dx),
+                       work=work)
+                bl.fulfil(*bnmod.fold_bwd_partials(part, nrc.value, groups, Cg), dx)
                 skip = None
             elif skip is not None and L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
                 # the residual block's skip gradient added in the dgrad epilogue

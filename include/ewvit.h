@@ -287,15 +287,17 @@ int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t 
                     const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
                     float *dbeta, const float *se_s, const float *se_g, int64_t HW, float *workspace, void *stream);
 /* Training-mode backward whose reduction pass already ran in the kernel that produced dy
- * (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [nrc][2C] rows of (sum g,
- * sum g*xhat), g = dy * act'(...) or, with row_scale [M / HW] (act 0: the MBConv tail of
- * ewvit_bn_fwd_drop_add), g = dy * row_scale[row / HW].  Only the dx pass runs; one group;
- * dgamma / dbeta overwritten (may be NULL).  Replaces the reduce launch of ewvit_bn_bwd /
- * ewvit_bn_bwd_scaled (torchvision BatchNorm2d backward behind sfe.py:111-113). */
+ * (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [groups][nrc][2C] rows of
+ * (sum g, sum g*xhat), g = dy * act'(...) or, with row_scale [M / HW] (act 0, one group: the
+ * MBConv tail of ewvit_bn_fwd_drop_add), g = dy * row_scale[row / HW].  `groups` as in
+ * ewvit_bn_bwd (consecutive row slices with their own statistics).  Only the dx pass runs;
+ * dgamma / dbeta summed over the groups, overwritten (may be NULL).  Replaces the reduce
+ * launch of ewvit_bn_bwd / ewvit_bn_bwd_scaled (BatchNorm2d backward of the backbone,
+ * sfe.py:111-113, and of the MWT's hf_conv / multiscale_fusion, mwt.py:60-72). */
 int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
                           const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
                           int act, float *dgamma, float *dbeta, const float *row_scale, int64_t HW,
-                          const float *part, int nrc, void *stream);
+                          const float *part, int nrc, int groups, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -408,20 +410,26 @@ int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Ci
                                      int stride);
 int ewvit_conv2d_bwd_data_add(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N, int64_t H,
                               int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, void *stream);
-/* Stride-1 input gradient (+ addend when not NULL, as ewvit_conv2d_bwd_data_add) that also
- * sums, over its bf16-rounded dx, the backward statistics of the BatchNorm whose output was
- * this conv's input (the MBConv tail / Conv2dNormActivation before the next block's first
- * conv, sfe.py:111-113): bx [N, H, W, Cin] bf16 that BN's input, mean / invstd its saved
+/* Stride-1 input gradient (+ addend when not NULL, plain dx, as ewvit_conv2d_bwd_data_add;
+ * dx_group_c / dx_group_stride as ewvit_conv2d_bwd_data) that also sums, over its
+ * bf16-rounded dx, the backward statistics of the BatchNorm whose output was this conv's
+ * input — the MBConv tail / Conv2dNormActivation before the next block's first conv
+ * (sfe.py:111-113), the MWT's seperate / fusion BatchNorms before the fusion / multiscale
+ * convs (mwt.py:60-72, 112): bx that BN's input in dx's layout (bf16), mean / invstd its saved
  * statistics, gamma / beta or NULL, act 0/1/2, rscale [N] (act 0) the drop-path factor per
- * frame or NULL.  part [ewvit_conv2d_bwd_bn_rows(...)][2 Cin] gets per m-tile (sum g, sum
- * g*xhat) as ewvit_dwconv3x3_bwd_data_bn defines them; *nrc_out = rows written (for
- * ewvit_bn_bwd_partials).  ewvit_conv2d_bwd_bn_rows: the most rows (0 = shape not
- * supported, or a workgroup cap is in force). */
+ * frame or NULL.  BatchNorm groups: one per channel group of a grouped dx (mean / invstd
+ * [groups][group_c]), or, plain dx with bn_group_rows > 0 (a multiple of 128 dividing
+ * N*H*W), one per slice of that many rows (mean / invstd [groups][Cin]).  part [groups][rows
+ * per group][2 C] gets per 128-row m-tile (sum g, sum g*xhat) as ewvit_dwconv3x3_bwd_data_bn
+ * defines them; *nrc_out = rows per group (for ewvit_bn_bwd_partials; fold them with
+ * ewvit_bn_fold_partials beyond a few hundred).  Works under a workgroup cap (the persistent
+ * walk).  ewvit_conv2d_bwd_bn_rows: m-tiles of 128 dx rows, 0 = shape not supported. */
 int64_t ewvit_conv2d_bwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride);
 int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *dx, const void *addend, int64_t N, int64_t H,
-                             int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, const void *bx,
-                             const float *mean, const float *invstd, const float *gamma, const float *beta, int act,
-                             const float *rscale, float *part, int *nrc_out, void *stream);
+                             int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
+                             int64_t dx_group_stride, const void *bx, const float *mean, const float *invstd,
+                             const float *gamma, const float *beta, int act, const float *rscale,
+                             int64_t bn_group_rows, float *part, int *nrc_out, void *stream);
 /* bytes of f32 split-K workspace for ewvit_conv2d_bwd_weight. */
 int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                           int ksize, int stride);

@@ -146,9 +146,9 @@ def test_conv_dgrad_bn(N, H, W, Cin, Cout, act, addend, scaled):
     assert rows == (N * H * W + 127) // 128
     part = torch.full((rows, 2 * Cin), float('nan'), device=DEV)
     nrc = ctypes.c_int(0)
-    L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), L.ptr(sk), N, H, W, Cin, Cout, 1, 1,
+    L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), L.ptr(sk), N, H, W, Cin, Cout, 1, 1, 0, 0,
            L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma if act else None), L.ptr(beta if act else None), act,
-           L.ptr(rs), L.ptr(part), ctypes.byref(nrc), L.stream(dy))
+           L.ptr(rs), 0, L.ptr(part), ctypes.byref(nrc), L.stream(dy))
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1)
     assert 1 <= nrc.value <= rows
@@ -183,7 +183,7 @@ def test_bn_bwd_partials_matches_reduce(act, scaled):
         L.call('ewvit_bn_bwd', L.ptr(dy), L.ptr(bx), L.ptr(dx0), L.BF16, M, C, L.ptr(gamma), L.ptr(beta), L.ptr(mean),
                L.ptr(invstd), act, L.ptr(dg0), L.ptr(db0), 0, 1, L.ptr(ws), L.stream(dy))
     L.call('ewvit_bn_bwd_partials', L.ptr(dy), L.ptr(bx), L.ptr(dx1), L.BF16, M, C, L.ptr(gamma), L.ptr(beta),
-           L.ptr(mean), L.ptr(invstd), act, L.ptr(dg1), L.ptr(db1), L.ptr(rs), H * W, L.ptr(part), 1, L.stream(dy))
+           L.ptr(mean), L.ptr(invstd), act, L.ptr(dg1), L.ptr(db1), L.ptr(rs), H * W, L.ptr(part), 1, 1, L.stream(dy))
     torch.cuda.synchronize()
     d = (dx0.float() - dx1.float()).abs()
     assert float(d.max()) <= 2 ** -6 * float(dx0.float().abs().max()), float(d.max())
@@ -324,3 +324,147 @@ def test_dw_stats_bn_act_se_matches(N, C, H, monkeypatch):
     d = (o0.float() - o1.float()).abs()
     assert float((d > 0).float().mean()) < 0.01, float((d > 0).float().mean())
     assert float(d.max()) <= 2 ** -7 * float(o0.float().abs().max())
+
+
+def _wpack_t(w):
+    """[Cout][Cin][k][k] fp32 -> the bwd_data pack [Cin][k*k][Cout] bf16 (ewvit_conv2d_pack_weight)."""
+    Cout, Cin, k, _ = w.shape
+    return w.permute(1, 2, 3, 0).reshape(Cin, k * k, Cout).contiguous().to(DEV, torch.bfloat16)
+
+
+@pytest.mark.parametrize('cap', [0, 24])
+def test_conv_dgrad_bn_channel_groups(cap):
+    """The multiscale_fusion shape class: a level-major input read as its channel concatenation
+    (grouped dx), one BatchNorm group per level (the fusion BN's per-level statistics), the MWT
+    under a workgroup cap (persistent walk): dx bit-identical to ewvit_conv2d_bwd_data, each
+    level's partial rows = fp64 sums of its own g terms."""
+    L = _L()
+    lib = L.load()
+    Lv, N, C, Cout, H, W = 3, 2, 128, 128, 20, 18
+    g = torch.Generator().manual_seed(11)
+    dy = bf(torch.randn(N, Cout, H, W, generator=g))
+    w = torch.randn(Cout, Lv * C, 3, 3, generator=g) / (9 * Lv * C) ** 0.5
+    wpt = _wpack_t(w)
+    bxz = bf(torch.randn(Lv * N, C, H, W, generator=g) + 0.2)           # level-major BN input
+    mean = torch.stack([bxz[l * N:(l + 1) * N].float().mean((0, 2, 3)) for l in range(Lv)]).contiguous()
+    invstd = torch.stack([torch.rsqrt(bxz[l * N:(l + 1) * N].float().var((0, 2, 3), unbiased=False) + 1e-5)
+                          for l in range(Lv)]).contiguous()
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    gs = N * H * W * C
+    dx0, dx1 = torch.empty_like(bxz), torch.empty_like(bxz)
+    prev = lib.ewvit_set_grid_cap(cap)
+    try:
+        L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Lv * C, Cout, 3, 1, C, gs,
+               L.stream(dy))
+        tiles = int(lib.ewvit_conv2d_bwd_bn_rows(N, H, W, Lv * C, Cout, 3, 1))
+        assert tiles == (N * H * W + 127) // 128
+        part = torch.full((Lv * tiles, 2 * C), float('nan'), device=DEV)
+        nrc = ctypes.c_int(0)
+        L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), None, N, H, W, Lv * C, Cout, 3, 1, C,
+               gs, L.ptr(bxz), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, None, 0, L.ptr(part),
+               ctypes.byref(nrc), L.stream(dy))
+    finally:
+        lib.ewvit_set_grid_cap(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    assert nrc.value == tiles
+    for lv in range(Lv):
+        sl = slice(lv * N, (lv + 1) * N)
+        # ReLU: g = dx where the BN output is positive
+        d, x = dx1[sl].double().cpu(), bxz[sl].double().cpu()
+        xh = (x - mean[lv].double().cpu().view(1, C, 1, 1)) * invstd[lv].double().cpu().view(1, C, 1, 1)
+        z = xh * gamma.double().cpu().view(1, C, 1, 1) + beta.double().cpu().view(1, C, 1, 1)
+        gr = torch.where(z > 0, d, torch.zeros_like(d))
+        ra, rb = gr.sum((0, 2, 3)), (gr * xh).sum((0, 2, 3))
+        ma, mb = gr.abs().sum((0, 2, 3)), (gr * xh).abs().sum((0, 2, 3))
+        ea, eb = sums_close(part[lv * tiles:(lv + 1) * tiles], ra, rb, ma, mb)
+        assert ea < 1e-5 and eb < 1e-5, (lv, ea, eb)
+
+
+@pytest.mark.parametrize('cap', [0, 16])
+def test_conv_dgrad_bn_row_groups(cap):
+    """The hf_conv fusion shape class: a plain input whose BatchNorm has one statistics group
+    per level (consecutive batch slices, mean / invstd [groups][C]): partial rows grouped by
+    level, each = fp64 sums of its slice's g terms; dx bit-identical; capped walk too."""
+    L = _L()
+    lib = L.load()
+    Lv, N, C, Cout, H, W = 3, 2, 64, 128, 16, 16       # N*H*W = 512 rows per level (4 m-tiles)
+    g = torch.Generator().manual_seed(12)
+    dy = bf(torch.randn(Lv * N, Cout, H, W, generator=g))
+    w = torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    wpt = _wpack_t(w)
+    bx = bf(torch.randn(Lv * N, C, H, W, generator=g) * 0.7 + 0.1)
+    mean = torch.stack([bx[l * N:(l + 1) * N].float().mean((0, 2, 3)) for l in range(Lv)]).contiguous()
+    invstd = torch.stack([torch.rsqrt(bx[l * N:(l + 1) * N].float().var((0, 2, 3), unbiased=False) + 1e-5)
+                          for l in range(Lv)]).contiguous()
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    dx0, dx1 = torch.empty_like(bx), torch.empty_like(bx)
+    M = Lv * N * H * W
+    prev = lib.ewvit_set_grid_cap(cap)
+    try:
+        L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), Lv * N, H, W, C, Cout, 3, 1, 0, 0,
+               L.stream(dy))
+        tiles = int(lib.ewvit_conv2d_bwd_bn_rows(Lv * N, H, W, C, Cout, 3, 1))
+        part = torch.full((tiles, 2 * C), float('nan'), device=DEV)
+        nrc = ctypes.c_int(0)
+        L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), None, Lv * N, H, W, C, Cout, 3, 1, 0,
+               0, L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, None, M // Lv, L.ptr(part),
+               ctypes.byref(nrc), L.stream(dy))
+    finally:
+        lib.ewvit_set_grid_cap(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    per = M // Lv // 128
+    assert nrc.value == per and tiles == Lv * per
+    for lv in range(Lv):
+        sl = slice(lv * N, (lv + 1) * N)
+        d, x = dx1[sl].double().cpu(), bx[sl].double().cpu()
+        xh = (x - mean[lv].double().cpu().view(1, C, 1, 1)) * invstd[lv].double().cpu().view(1, C, 1, 1)
+        z = xh * gamma.double().cpu().view(1, C, 1, 1) + beta.double().cpu().view(1, C, 1, 1)
+        gr = torch.where(z > 0, d, torch.zeros_like(d))
+        ea, eb = sums_close(part[lv * per:(lv + 1) * per], gr.sum((0, 2, 3)), (gr * xh).sum((0, 2, 3)),
+                            gr.abs().sum((0, 2, 3)), (gr * xh).abs().sum((0, 2, 3)))
+        assert ea < 1e-5 and eb < 1e-5, (lv, ea, eb)
+
+
+def test_mwt_linked_vs_unlinked(monkeypatch):
+    """The MWT branch (training step of MWT(3, 128, 3) with its convs capped as in DAMA): with
+    the links its hf_conv seperate and fusion BatchNorms (per-level statistics) take their
+    backward sums from the fusion / multiscale convs' input gradients; forward bit-identical,
+    gradients equal to the fp32 summation order."""
+    import ewvit
+    import ewvit.bn as ebn
+    from network.mwt import MWT
+    L = ewvit._lib
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 3, 64, 64, generator=g).to(DEV)
+    res = {}
+    for linked in (False, True):
+        monkeypatch.setattr(ebn, '_BWD_LINK', linked)
+        torch.manual_seed(2)
+        m = MWT(3, 128, 3).to(DEV).train()
+        calls = {}
+        real = L.call
+
+        def count(name, *a, **k):
+            calls[name] = calls.get(name, 0) + 1
+            return real(name, *a, **k)
+        monkeypatch.setattr(L, 'call', count)
+        try:
+            with torch.autocast('cuda', dtype=torch.bfloat16), ewvit._lib.grid_cap(24):
+                y = m(x)
+            y.float().square().mean().backward()
+        finally:
+            monkeypatch.setattr(L, 'call', real)
+        torch.cuda.synchronize()
+        res[linked] = (y.detach().float(), {n: p.grad.float() for n, p in m.named_parameters() if p.grad is not None},
+                       calls)
+    y0, g0, c0 = res[False]
+    y1, g1, c1 = res[True]
+    assert torch.equal(y0, y1)
+    assert c0.get('ewvit_bn_bwd_partials', 0) == 0 and c1.get('ewvit_bn_bwd_partials', 0) == 2
+    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 2
+    worst = min((_cos(g0[n], g1[n]), n) for n in g0 if g0[n].abs().max() > 0 and not n.endswith('bias'))
+    assert worst[0] > 0.999, worst
