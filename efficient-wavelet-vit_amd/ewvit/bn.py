@@ -20,6 +20,10 @@ ACT = {None: 0, 'none': 0, 'relu': 1, 'silu': 2}
 _BWD_LINK = os.environ.get('EWVIT_BN_BWD_LINK', '1') != '0'
 # the most partial rows a linked producer may leave (the dx pass reads them all per block)
 BWD_LINK_MAX_ROWS = 512
+# links for big maps too (the MWT's 2.4 M-row convs, partials folded): measured slower — the
+# input-gradient epilogue's BN-input reads under the capped walk cost more than the reduction
+# pass they replace (MWT capped 14.0 -> 15.6 ms) — so A/B only (EWVIT_BN_LINK_BIG=1)
+BWD_LINK_BIG = os.environ.get('EWVIT_BN_LINK_BIG', '0') != '0'
 
 
 class BwdStatsLink:

@@ -168,6 +168,8 @@ def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     tiles = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cx, Cout, k, stride))
     if tiles <= 0 or (skip is not None and levels > 1):
         return None
+    if tiles > bnmod.BWD_LINK_MAX_ROWS * (levels if levels > 1 else 1) and not bnmod.BWD_LINK_BIG:
+        return None
     if skip is not None and not L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
         return None
     if levels > 1:

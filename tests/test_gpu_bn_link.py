@@ -441,6 +441,7 @@ def test_mwt_linked_vs_unlinked(monkeypatch):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(4, 3, 64, 64, generator=g).to(DEV)
     res = {}
+    monkeypatch.setattr(ebn, 'BWD_LINK_BIG', True)       # off by default (measured slower); the path is kept
     for linked in (False, True):
         monkeypatch.setattr(ebn, '_BWD_LINK', linked)
         torch.manual_seed(2)
