@@ -121,6 +121,7 @@ QUERIES = {
     'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_dwconv3x3_set_pix': (_i64, [_i64]),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
 }
 

@@ -186,6 +186,12 @@ int ewvit_attn_bwd(const void *dout, int64_t sdo_b, int64_t sdo_n, const void *q
  * EWVIT_DW_SEGS): an A/B and test knob, not a numerics switch (every split computes the
  * same sums in the same order). */
 int ewvit_dwconv3x3_set_segs(int max_segs);
+/* Output maps of at most max_pixels per frame (default 0 = never, or EWVIT_DW_PIX) run the
+ * depthwise convs on the per-pixel kernel (all 9 taps of a pixel loaded at once, the block's
+ * weights staged in LDS) instead of the row kernels: an A/B and test knob (the two compute
+ * every output with the same operations in the same order; the per-pixel form measured slower on
+ * the backbone's 7^2 / 14^2 maps).  Returns the previous setting. */
+int64_t ewvit_dwconv3x3_set_pix(int64_t max_pixels);
 
 /* ------------------------------------------- depthwise 3x3 conv (backbone) ---
  * The MBConv depthwise convolutions of EfficientNetV2-S (groups = channels,

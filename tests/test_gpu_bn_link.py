@@ -54,7 +54,7 @@ def test_dw_fwd_bn(N, C, H, W, stride):
     y1 = torch.empty_like(y0)
     L.call('ewvit_dwconv3x3_fwd', L.ptr(x), L.ptr(w), L.ptr(y0), N, H, W, C, stride, 1, L.BF16, L.stream(x))
     nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 0))
-    assert nrc == (N * Ho + 31) // 32
+    assert nrc == (N * Ho + 31) // 32          # row kernel (the per-pixel form is off by default)
     part = torch.full((nrc, 2 * C), float('nan'), device=DEV)
     so = torch.full((C,), float('nan'), device=DEV)
     L.call('ewvit_dwconv3x3_fwd_bn', L.ptr(x), L.ptr(w), L.ptr(y1), N, H, W, C, stride, L.ptr(shift), L.ptr(part),
