@@ -661,6 +661,132 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
   }, fin);
 }
 
+// MBConv's depthwise BatchNorm + SiLU (training, statistics from partial rows, one group)
+// and the squeeze of the squeeze-excitation after it in ONE pass: block (frame n, 64-channel
+// chunk) finalises its chunk's statistics from the partial rows (the depthwise conv's,
+// ewvit_dwconv3x3_fwd_bn) as bn_apply_kernel does (blocks of frame 0 keep the books), applies
+// BN + act to the frame's HW rows of its chunk, and sums the stored (rounded) outputs per
+// channel — the squeeze s0 = mean_hw y — then leaves the chunk's partial of the SE MLP's
+// first layer, part[n][chunk][j] = sum_{c in chunk} W1[j][c] s0[n][c].  The same operations
+// in the same order as bn_apply_kernel + se_sq_h1_part_kernel (8 channel vectors x 32 row
+// groups, rows rg, rg + 32, ... added in order, then the fixed tree over the row groups), so
+// the same bits, one launch and one pass over the tensor fewer.
+template <int DT, int ACT>
+__global__ __launch_bounds__(256) void bn_act_squeeze_kernel(const void *__restrict__ x, void *__restrict__ y,
+                                                             const float *__restrict__ part,
+                                                             const float *__restrict__ shifts, int nrc, int HW, int C,
+                                                             const float *__restrict__ gamma,
+                                                             const float *__restrict__ beta, float *running_mean,
+                                                             float *running_var, float momentum, float eps,
+                                                             float *save_mean, float *save_invstd, int64_t *counter,
+                                                             float inv_hw, const float *__restrict__ w1, int Csq,
+                                                             float *__restrict__ s0_out, float *__restrict__ hpart) {
+  __shared__ float red[512];
+  __shared__ float coef[2][64];
+  __shared__ float sm[8 * 256];
+  const int tid = threadIdx.x, C8 = C >> 3, nfr = gridDim.x, n = blockIdx.x, cb = blockIdx.y;
+  const int ch0 = cb * 64;
+  const int nch_c = (C - ch0) < 64 ? (C - ch0) : 64;
+  const int64_t Mg = (int64_t)nfr * HW;
+  const float nf = (float)Mg;
+  const bool book = n == 0;
+  float pa = 0.f, pb = 0.f;
+  bn_chunk_load(part, 0, nrc, C, ch0, nch_c, pa, pb);
+  const int cv = tid & 7, rg = tid >> 3;
+  const int c8 = cb * 8 + cv;
+  const bool active = c8 < C8;
+  const int c = active ? c8 * 8 : 0;
+  const int64_t base = (int64_t)n * HW * C + c;
+  // first batch of this thread's rows in flight before the statistics finalise
+  constexpr int PF = 4;
+  Raw8<DT> pre[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+    if (active && rg + 32 * q < HW) pre[q] = ldraw<DT>(x, base + (int64_t)(rg + 32 * q) * C);
+  bn_chunk_reduce(red, pa, pb);
+  if (tid < nch_c) {
+    const int cc = ch0 + tid;
+    const float d = red[tid] / nf, mu = shifts[cc] + d;
+    const float var = fmaxf(red[256 + tid] / nf - d * d, 0.f);
+    const float inv = rsqrtf(var + eps);
+    const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
+    coef[0][tid] = ga * inv;
+    coef[1][tid] = be - mu * ga * inv;
+    if (book) {
+      if (counter && cb == 0 && tid == 0) *counter += 1;
+      if (save_mean) save_mean[cc] = mu;
+      if (save_invstd) save_invstd[cc] = inv;
+      if (running_mean) running_mean[cc] = (1.f - momentum) * running_mean[cc] + momentum * mu;
+      if (running_var)
+        running_var[cc] = (1.f - momentum) * running_var[cc] + momentum * (Mg > 1 ? var * (nf / (nf - 1.f)) : var);
+    }
+  }
+  bn_sync();
+  float sc[8], sh[8], acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = coef[0][cv * 8 + j]; sh[j] = coef[1][cv * 8 + j]; acc[j] = 0.f; }
+  auto apply = [&](int h, const Raw8<DT> &raw) {
+    float v[8];
+    unpack<DT>(raw, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
+    st8<DT>(y, base + (int64_t)h * C, v);
+    float r[8];                                        // the stored values, as the squeeze reads them
+    if constexpr (DT == EWVIT_BF16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = bf2f(f2bf(v[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += r[j];
+  };
+  if (active) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+      if (rg + 32 * q < HW) apply(rg + 32 * q, pre[q]);
+    for (int h0 = rg + 32 * PF; h0 < HW; h0 += 32 * PF) {
+      Raw8<DT> t[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q)
+        if (h0 + 32 * q < HW) t[q] = ldraw<DT>(x, base + (int64_t)(h0 + 32 * q) * C);
+#pragma unroll
+      for (int q = 0; q < PF; ++q)
+        if (h0 + 32 * q < HW) apply(h0 + 32 * q, t[q]);
+    }
+  }
+  // squeeze: the fixed tree of se_chunk_squeeze over the 32 row groups
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sm[j * 256 + tid] = acc[j];
+  __syncthreads();
+  for (int st = 16; st >= 1; st >>= 1) {
+    if (rg < st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm[j * 256 + tid] += sm[j * 256 + tid + st * 8];
+    __syncthreads();
+  }
+  const int l = tid & 63, w = tid >> 6;
+  const int cl = ch0 + l;
+  const float xv = cl < C ? sm[(l & 7) * 256 + (l >> 3)] * inv_hw : 0.f;
+  if (w == 0 && cl < C) s0_out[(int64_t)n * C + cl] = xv;
+  float *pp = hpart + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = w; j0 < Csq; j0 += 16) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 4 * q;
+      v[q] = (j < Csq && cl < C) ? w1[(int64_t)j * C + cl] * xv : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = wave_sum(v[q]);
+      const int j = j0 + 4 * q;
+      if (l == 0 && j < Csq) pp[j] = v[q];
+    }
+  }
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -979,4 +1105,28 @@ extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, 
   BN_DISPATCH(BN_DX);
 #undef BN_DX
   return launch_status("bn_bwd");
+}
+
+// MBConv depthwise BatchNorm(+act) from the depthwise conv's partial statistics, fused with the
+// SE squeeze and the MLP's first-layer partials (bn_act_squeeze_kernel): x, y [N][HW][C];
+// s0 [N][C]; part [N][ceil(C / 64)][Csq] (what ewvit_se_gate_excite finishes); one launch
+extern "C" int ewvit_bn_act_se_squeeze(const void *x, void *y, int dtype, int64_t N, int64_t HW, int64_t C,
+                                       const float *gamma, const float *beta, float *running_mean, float *running_var,
+                                       float momentum, float eps, int act, float *save_mean, float *save_invstd,
+                                       int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
+                                       const float *w1, int64_t Csq, float *s0, float *hpart, void *stream) {
+  EWVIT_CHECK_ARG(x && y && part && shifts && w1 && s0 && hpart && dtype_ok(dtype), "bn_act_se_squeeze: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096 && N > 0 && N <= 65535 && HW > 0 && HW < (1 << 30),
+                  "bn_act_se_squeeze: N=%lld HW=%lld C=%lld", (long long)N, (long long)HW, (long long)C);
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2 && nrc >= 1 && nrc <= 65535 && Csq >= 1 && Csq <= 4096,
+                  "bn_act_se_squeeze: act=%d nrc=%d Csq=%lld", act, nrc, (long long)Csq);
+  const dim3 grid((unsigned)N, (unsigned)((C + 63) / 64));
+  hipStream_t s = as_stream(stream);
+#define BN_SQ(DTV, ACTV)                                                                                             \
+  hipLaunchKernelGGL((bn_act_squeeze_kernel<DTV, ACTV>), grid, dim3(256), 0, s, x, y, part, shifts, nrc, (int)HW,   \
+                     (int)C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,         \
+                     num_batches_tracked, 1.f / (float)HW, w1, (int)Csq, s0, hpart)
+  BN_DISPATCH(BN_SQ);
+#undef BN_SQ
+  return launch_status("bn_act_se_squeeze");
 }

@@ -797,6 +797,25 @@ extern "C" int ewvit_se_forward(const void *x, int dtype, int64_t N, int64_t HW,
   return launch_status("se_forward");
 }
 
+// the second half of ewvit_se_forward alone: the gates from the MLP's first-layer partials
+// (part [N][ceil(C / 64)][Csq], e.g. from ewvit_bn_act_se_squeeze) and the excite pass
+extern "C" int ewvit_se_gate_excite(const float *part, const float *b1, const float *w2, const float *b2,
+                                    const void *x, int dtype, int64_t N, int64_t HW, int64_t C, int64_t Csq, float *h1,
+                                    float *s, void *y, void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "se_gate_excite")) return rc;
+  if (int rc = se_mlp_check(N, C, Csq, "se_gate_excite")) return rc;
+  EWVIT_CHECK_ARG(part && w2 && h1 && s && x && y && HW < (1 << 30), "se_gate_excite: bad args");
+  const dim3 g2((unsigned)N, (unsigned)((C + 255) / 256));
+  const size_t lds = (size_t)(((Csq + 3) & ~3) + 256) * sizeof(float);
+  if (dtype == EWVIT_BF16)
+    hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_BF16>, g2, dim3(256), lds, as_stream(stream), part, se_nb(C), b1, w2,
+                       b2, (int)C, (int)Csq, h1, s, x, y, (int)HW);
+  else
+    hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_F32>, g2, dim3(256), lds, as_stream(stream), part, se_nb(C), b1, w2,
+                       b2, (int)C, (int)Csq, h1, s, x, y, (int)HW);
+  return launch_status("se_gate_excite");
+}
+
 // squeeze-excite backward of the excite vector: ds = sum_hw dy * x inside the first
 // kernel, then g / dW1 / db1 / dW2 / db2 as ewvit_se_mlp_bwd (3 launches)
 extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,

@@ -92,6 +92,9 @@ SIGNATURES = {
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_bn_act_se_squeeze': [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp,
+                                _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
+    'ewvit_se_gate_excite': [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     'ewvit_se_forward': [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_dwconv3x3_fwd_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     'ewvit_dwconv3x3_bwd_data_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp,

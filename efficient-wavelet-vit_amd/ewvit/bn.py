@@ -8,6 +8,7 @@ normalises consecutive equal batch slices with their own statistics (one
 launch for the MWT's per-level calls of its shared BatchNorms).
 """
 import os
+import weakref
 
 import torch
 
@@ -36,10 +37,14 @@ class BwdStatsLink:
     (`partials_for`): a second consumer's gradient added by autograd gives a new tensor (the
     link holds a reference to the produced one, so autograd cannot accumulate into it in
     place) and the BN runs its own reduction."""
-    __slots__ = ('key', 'x', 'mean', 'invstd', 'gamma', 'beta', 'act', 'rscale', 'groups', 'part', 'nrc', 'dx', 'ver')
+    __slots__ = ('key', 'yref', 'x', 'mean', 'invstd', 'gamma', 'beta', 'act', 'rscale', 'groups', 'part', 'nrc',
+                 'dx', 'ver')
 
     def __init__(self, y, x, mean, invstd, gamma, beta, act, rscale=None, groups=1):
         self.key = (y.data_ptr(), tuple(y.shape), y.dtype)
+        # the offer holds only while y lives: after y is freed another tensor can take its
+        # address and shape, and must not pick up this BatchNorm's link
+        self.yref = weakref.ref(y)
         self.x, self.mean, self.invstd, self.gamma, self.beta = x, mean, invstd, gamma, beta
         self.act, self.rscale, self.groups = act, rscale, groups
         self.part = self.dx = None
@@ -100,7 +105,8 @@ def take_bwd_link(x):
     link = _bwd_offered
     if link is not None and link.key == (x.data_ptr(), tuple(x.shape), x.dtype):
         _bwd_offered = None
-        return link
+        if link.yref() is not None and link.x is not None:
+            return link
     return None
 
 

@@ -10,10 +10,16 @@ in place of the ~15 small library/elementwise kernels of the reference block.
 ``bn_act_se`` takes the BatchNorm + SiLU before the SE as well: its backward folds the SE
 input-gradient pass into the BatchNorm backward.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _lib as L
+
+# the depthwise BatchNorm's apply pass and the SE squeeze as one kernel when the statistics come
+# from the depthwise conv (ewvit_bn_act_se_squeeze; 0: separate passes, A/B)
+_BN_SQUEEZE = os.environ.get('EWVIT_BN_SQUEEZE', '1') != '0'
 
 
 def _rows(x):
@@ -109,6 +115,27 @@ class BnActSEFn(torch.autograd.Function):
         x2 = torch.empty_like(xc)
         mean = torch.empty(1, C, dtype=torch.float32, device=dev)
         invstd = torch.empty_like(mean)
+        Csq = w1.shape[0]
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
+        h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
+        sc = torch.empty(N, C, dtype=torch.float32, device=dev)
+        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        y = torch.empty_like(x2)
+        if partials is not None and _BN_SQUEEZE and N <= 65535:
+            # BatchNorm apply + SiLU + the SE squeeze (+ the MLP's first-layer partials) in one
+            # pass, then the gates + excite: 2 launches for the BN and the SE forward
+            part, shifts, nrc = partials
+            L.call('ewvit_bn_act_se_squeeze', L.ptr(xc), L.ptr(x2), L.dt(xc), N, HW, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.ptr(W1), Csq, L.ptr(s0),
+                   L.ptr(fws), L.stream(x2), work={'bytes': 2 * xc.numel() * xc.element_size()})
+            L.call('ewvit_se_gate_excite', L.ptr(fws), L.ptr(_vec(b1)), L.ptr(W2), L.ptr(_vec(b2)), L.ptr(x2),
+                   L.dt(x2), N, HW, C, Csq, L.ptr(h1), L.ptr(sc), L.ptr(y), L.stream(y),
+                   work={'bytes': 2 * x2.numel() * x2.element_size()})
+            ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
+            ctx.cfg = (act, b1 is not None, b2 is not None)
+            return y
         if partials is not None:
             # statistics summed by the depthwise conv that produced x: the apply pass only
             part, shifts, nrc = partials
@@ -122,13 +149,6 @@ class BnActSEFn(torch.autograd.Function):
                    L.ptr(running_mean), L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean),
                    L.ptr(invstd), 1, L.ptr(counter), L.ptr(ws), L.stream(x2),
                    work={'bytes': 3 * xc.numel() * xc.element_size()})
-        Csq = w1.shape[0]
-        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
-        s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
-        h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
-        sc = torch.empty(N, C, dtype=torch.float32, device=dev)
-        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-        y = torch.empty_like(x2)
         # squeeze + MLP hidden partials, then the gates and the excite pass in one launch
         L.call('ewvit_se_forward', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
                L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(y), L.ptr(fws), L.stream(y),

@@ -304,6 +304,19 @@ int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, int dtype, in
                           const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
                           int act, float *dgamma, float *dbeta, const float *row_scale, int64_t HW,
                           const float *part, int nrc, int groups, void *stream);
+/* MBConv's depthwise BatchNorm + act (training, statistics from partial rows as
+ * ewvit_bn_fwd_partials: the depthwise conv's, ewvit_dwconv3x3_fwd_bn) and the squeeze of the
+ * squeeze-excitation after it (torchvision Conv2dNormActivation + SqueezeExcitation,
+ * sfe.py:111-113) in one pass over x [N][HW][C]: y = act(bn(x)), s0[n][c] = mean_hw y (of
+ * the stored values), part [N][ceil(C / 64)][Csq] = the SE MLP's first-layer partials
+ * sum_{c in chunk} w1[j][c] s0[n][c] (w1 [Csq][C] f32) for ewvit_se_gate_excite; running
+ * statistics / saved mean, invstd / counter as ewvit_bn_fwd_partials.  The same bits as
+ * ewvit_bn_fwd_partials + ewvit_se_squeeze_mlp_fwd's first launch. */
+int ewvit_bn_act_se_squeeze(const void *x, void *y, int dtype, int64_t N, int64_t HW, int64_t C, const float *gamma,
+                            const float *beta, float *running_mean, float *running_var, float momentum, float eps,
+                            int act, float *save_mean, float *save_invstd, int64_t *num_batches_tracked,
+                            const float *part, const float *shifts, int nrc, const float *w1, int64_t Csq, float *s0,
+                            float *hpart, void *stream);
 /* dx (dtype) from dy and the saved x/statistics (training-mode backward);
  * dgamma/dbeta f32 summed over groups (= or += when accumulate), either may be NULL. */
 int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
@@ -493,6 +506,11 @@ int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int64_t HW, in
 int ewvit_se_forward(const void *x, int dtype, int64_t N, int64_t HW, int64_t C, const float *w1, const float *b1,
                      const float *w2, const float *b2, int64_t Csq, float *s0, float *h1, float *s, void *y,
                      float *workspace, void *stream);
+/* ewvit_se_forward's second launch alone: the SE gates from the MLP's first-layer partials part
+ * [N][ceil(C / 64)][Csq] (h1, s written out) and the excite pass y = x * s[n, c]. */
+int ewvit_se_gate_excite(const float *part, const float *b1, const float *w2, const float *b2, const void *x,
+                         int dtype, int64_t N, int64_t HW, int64_t C, int64_t Csq, float *h1, float *s, void *y,
+                         void *stream);
 int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,
                              const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
                              int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,

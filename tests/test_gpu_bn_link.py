@@ -469,3 +469,19 @@ def test_mwt_linked_vs_unlinked(monkeypatch):
     assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 2
     worst = min((_cos(g0[n], g1[n]), n) for n in g0 if g0[n].abs().max() > 0 and not n.endswith('bias'))
     assert worst[0] > 0.999, worst
+
+
+def test_stale_offer_not_taken():
+    """A BatchNorm's link offer dies with its output: a later tensor at the same address and
+    shape (the caching allocator reuses blocks) does not pick it up."""
+    import ewvit.bn as ebn
+    y = torch.empty(2, 8, 4, 4, dtype=torch.bfloat16, device=DEV)
+    x = torch.empty_like(y)
+    m = torch.zeros(1, 8, device=DEV)
+    ebn.offer_bwd_link(y, x, m, m, None, None, 0)
+    key = ebn._bwd_offered.key
+    del y
+    z = torch.empty(2, 8, 4, 4, dtype=torch.bfloat16, device=DEV)
+    if (z.data_ptr(), tuple(z.shape), z.dtype) == key:
+        assert ebn.take_bwd_link(z) is None
+    ebn._bwd_offered = None

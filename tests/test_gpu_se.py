@@ -243,3 +243,38 @@ def test_se_forward_matches_two_launch_path(N, C, HW, csq, dtype):
         assert torch.equal(a, b)
     ref = x.float() * out[0][2].view(N, 1, C)
     assert float((out[1][3].float() - ref).abs().max()) <= 2 ** -7 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize('N,C,H,csq', [(64, 1536, 7, 64), (64, 960, 14, 40), (3, 200, 5, 6)])
+def test_bn_act_se_squeeze_matches_separate_passes(N, C, H, csq, monkeypatch):
+    """bn_act_se with the depthwise conv's partial statistics: the fused BatchNorm apply + SE
+    squeeze (ewvit_bn_act_se_squeeze + ewvit_se_gate_excite) gives the separate passes' bits —
+    output, saved statistics, running statistics, counter — and the same gradients."""
+    import ewvit
+    import ewvit.se as ese
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(N, C, H, H, generator=g) * 0.7 + 0.2).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    wd = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV)
+    w1 = (torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5).to(DEV)
+    b1 = (torch.randn(csq, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5).to(DEV)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    dy = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(ese, '_BN_SQUEEZE', fused)
+        bn = torch.nn.BatchNorm2d(C, eps=1e-3).train().to(DEV)
+        xd = x.clone().requires_grad_(True)
+        ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+        r = ewvit.ops.dwconv3x3_bn_stats(xd, wd, 1, bn.running_mean)
+        assert r is not None
+        y = ewvit.bn_act_se(r[0], bn, 'silu', *ps, partials=r[1:])
+        y.backward(dy)
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xd.grad, bn.running_mean.clone(), bn.running_var.clone(),
+                     bn.num_batches_tracked.clone(), bn.weight.grad, [p.grad for p in ps]))
+    a, b = outs
+    for u, v in zip(a[:6], b[:6]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[6], b[6]):
+        assert torch.equal(u, v)
