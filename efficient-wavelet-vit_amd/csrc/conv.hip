@@ -1320,6 +1320,39 @@ static int glds_variant() {
 }
 static bool use_glds() { return (glds_variant() & 7) != 0; }
 
+// Wide-wave blocks for the big 128-column grids (the MWT's multiscale / fusion convs and the
+// multiscale input gradient): each wave owns 64 x 128 of the tile instead of 64 x 64, so it
+// reads (64 + 128) / (64 * 128) LDS bytes per MFMA flop instead of (64 + 64) / (64 * 64) —
+// 3/4 of the fragment traffic that bounds the 4-wave 128 x 128 block.
+//   1: 256 x 128 tiles, 4 waves, 2-deep ring (96 KB: one block per CU)
+//   2: 128 x 128 tiles, 2 waves, 2-deep ring (64 KB: two blocks per CU)
+//   3: 256 x 128 tiles, 4 waves, 3-deep ring (144 KB)
+// for grids of more than EWVIT_CONV_WWMIN (default 4096) 128 x 128 tiles; 0 = off.
+// EWVIT_CONV_WW or ewvit_conv2d_set_ww (A/B measurement).
+static int g_ww = -1;
+static int ww_variant() {
+  if (g_ww < 0) {
+    const char *e = getenv("EWVIT_CONV_WW");
+    g_ww = e ? atoi(e) : 0;
+    if (g_ww < 0 || g_ww > 3) g_ww = 0;
+  }
+  return g_ww;
+}
+static int64_t g_wwmin = -1;
+static int64_t ww_min() {
+  if (g_wwmin < 0) {
+    const char *e = getenv("EWVIT_CONV_WWMIN");
+    g_wwmin = e ? (int64_t)atoll(e) : (int64_t)4096;
+    if (g_wwmin < 0) g_wwmin = 4096;
+  }
+  return g_wwmin;
+}
+static int ww_pick(int64_t M, int Ncol, int bn) {
+  if (bn != 128 || !ww_variant()) return 0;
+  const int64_t nwg = (M + 127) / 128 * ((Ncol + 127) / 128);
+  return nwg > ww_min() ? ww_variant() : 0;
+}
+
 // Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
 // else 32; register prefetch depth from EWVIT_CONV_PF (1 or 2, default 1).
 // Ncol <= 64 (e.g. the fusion conv's 56-channel input gradient) uses the 128x64 tile.
@@ -1683,6 +1716,31 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
   }();
   // (64-row tiles would change the BatchNorm partial rows fwd_bn_rows promised: not with bn_part)
   if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part && !a.bwd.part)) && nwg <= sgmax) vv = sg;
+  const int ww = (v == 1 && a.pc < 0 && !a.bwd.part) ? ww_pick(a.M, a.Ncol, bn) : 0;
+  if (ww) {
+    // (fwd_bn_rows promises 256-row BatchNorm partials for variants 1 / 3)
+    const int wbm = ww == 2 ? 128 : 256;
+    if (bm_out) *bm_out = wbm;
+    const int64_t nt = (a.M + wbm - 1) / wbm * ntn;
+    if (nt >= (int64_t)1 << 31) return false;
+    // a capped grid: one 256-row block fills a CU, so half the workgroups of the cap
+    const int64_t capw = g_grid_cap > 0 ? (wbm == 256 ? (g_grid_cap + 1) / 2 : g_grid_cap) : 0;
+    const dim3 gw((unsigned)(capw > 0 && nt > capw ? capw : nt));
+#define EWVIT_GLDS_WW(BM_, NS_)                                                                                   \
+  do {                                                                                                            \
+    if (a.g.ks == 1)                                                                                              \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, 128, 1, NS_, 1>), gw, dim3(BM_), 0, s, a, src_bytes, ntn,   \
+                         tap_inner, (int)nt);                                                                     \
+    else                                                                                                          \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, 128, 3, NS_, 1>), gw, dim3(BM_), 0, s, a, src_bytes, ntn,   \
+                         tap_inner, (int)nt);                                                                     \
+  } while (0)
+    if (ww == 1) EWVIT_GLDS_WW(256, 2);
+    else if (ww == 2) EWVIT_GLDS_WW(128, 2);
+    else EWVIT_GLDS_WW(256, 3);
+#undef EWVIT_GLDS_WW
+    return true;
+  }
   if constexpr (DGRAD) {
     if (a.bwd.part) {
       // the backward-statistics epilogue (its own instantiations): 128-row tiles always (the
@@ -1850,6 +1908,10 @@ static int fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cou
   if (2 * N * H * W * Cin >= (int64_t)OOB || Cout * K * 2 >= (int64_t)OOB || N * Ho * Wo * Cout >= (int64_t)1 << 40)
     return 0;
   const int v = glds_variant() & 7;
+  if (v == 1) {
+    const int ww = ww_pick(N * Ho * Wo, (int)Cout, Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128);
+    if (ww == 1 || ww == 3) return 256;
+  }
   return (v == 3 || v == 4) ? 256 : 128;
 }
 
@@ -2144,6 +2206,18 @@ extern "C" int ewvit_conv2d_set_wgrad_kgroups(int kgroups) {
   const int prev = wgrad_kgroups();
   g_wkg = kgroups == 2 ? 2 : 1;
   return prev;
+}
+
+extern "C" int ewvit_conv2d_set_ww(int variant) {
+  const int old = ww_variant();
+  g_ww = variant < 0 || variant > 3 ? 0 : variant;
+  return old;
+}
+
+extern "C" int64_t ewvit_conv2d_set_ww_min(int64_t min_tiles) {
+  const int64_t old = ww_min();
+  g_wwmin = min_tiles < 0 ? 4096 : min_tiles;
+  return old;
 }
 
 extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {

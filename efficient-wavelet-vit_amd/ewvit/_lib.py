@@ -57,6 +57,7 @@ SIGNATURES = {
     'ewvit_dwconv3x3_set_segs': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_set_wgrad_kgroups': [_i32],
+    'ewvit_conv2d_set_ww': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -110,6 +111,7 @@ QUERIES = {
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_conv2d_set_ww_min': (_i64, [_i64]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_stem_parts': (_i64, [_i64, _i64, _i64, _i32]),
     'ewvit_dwt_hf_fused_ok': (_i32, [_i64, _i64, _i64, _i64, _i32, _i64, _i64, _i64]),

@@ -374,6 +374,15 @@ int ewvit_conv2d_set_glds(int variant);
  * <= 1/8 of it; 4 = auto (2 for n' >= 2048 over >= 64K output pixels, else 0).  Replaces nothing in the reference (tuning knob of csrc/conv.hip).
  * Returns the previous setting. */
 int ewvit_conv2d_set_wgrad_wide(int variant);
+/* Wide-wave fwd / input-gradient blocks for grids of > 4096 128 x 128 tiles with 128-column
+ * tiles (A/B measurement; default from EWVIT_CONV_WW, else 0): each wave 64 x 128 of the tile;
+ * 1 = 256 x 128 tiles with a 2-deep ring, 2 = 128 x 128 tiles, 3 = 256 x 128 with a 3-deep
+ * ring; 0 = off.  Variants 1 / 3 change ewvit_conv2d_fwd_bn_rows to 256.  Replaces nothing in
+ * the reference.  Returns the previous setting. */
+int ewvit_conv2d_set_ww(int variant);
+/* The grid size (128 x 128 tiles) above which ewvit_conv2d_set_ww's variant applies (default
+ * from EWVIT_CONV_WWMIN, else 4096; tests lower it).  Returns the previous setting. */
+int64_t ewvit_conv2d_set_ww_min(int64_t min_tiles);
 /* Weight-gradient K-groups (A/B measurement; default from EWVIT_CONV_WKG, else 1): 2 = two
  * groups of 4 waves per workgroup, each multiplying every other K-tile of a pixel split and
  * summed through LDS (half the splits and fp32 slabs), for the default 128-column family on

@@ -71,12 +71,15 @@ def main():
                     help='extra shape N,Cin,H,W,Cout,k,stride,levels (repeatable; replaces the table)')
     ap.add_argument('--variants', default='1,2,3,4,0', help='conv kernel families to time: 1-4 LDS-DMA configs, 0 register-staged; '
                     '+100*w: 256-column wgrad tiles of variant w (e.g. 209)')
+    ap.add_argument('--ww', default=None, help='wide-wave fwd/dgrad variants to time per kernel family (ewvit_conv2d_set_ww), e.g. 0,1,2,3')
     ap.add_argument('--bnstats', action='store_true', help='time fwd against fwd with BN statistics in the epilogue')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
     a.variants = [int(v) for v in a.variants.split(',')]
+    if a.ww is not None:      # variant v + 1000 * ww
+        a.variants = [v + 1000 * int(w) for v in a.variants for w in a.ww.split(',')]
     import ewvit
     dev = torch.device('cuda', 0)
     from ewvit import _lib as L
@@ -132,7 +135,9 @@ def main():
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
                 lib.ewvit_conv2d_set_glds(v % 100)
-                lib.ewvit_conv2d_set_wgrad_wide(v // 100)     # 0 = 128-column tiles, 4 = auto
+                lib.ewvit_conv2d_set_wgrad_wide(v % 1000 // 100)     # 0 = 128-column tiles, 4 = auto
+                if a.ww is not None:
+                    lib.ewvit_conv2d_set_ww(v // 1000)
                 phases = (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad))
                 if a.bnstats and rows_bn > 0:
                     phases = (('fwd', fwd), ('fwd_bn', fwd_bn))
@@ -140,6 +145,8 @@ def main():
                     rows.setdefault((v, pn), []).append(graph_time(fn, a.iters))
         lib.ewvit_conv2d_set_glds(1)
         lib.ewvit_conv2d_set_wgrad_wide(4)
+        if a.ww is not None:
+            lib.ewvit_conv2d_set_ww(0)
         for v in a.variants:
             parts = []
             for pn in (('fwd', 'fwd_bn') if a.bnstats and rows_bn > 0 else ('fwd', 'dgrad', 'wgrad')):

@@ -25,6 +25,8 @@ sys.path.insert(0, os.path.join(REPO, 'tools'))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--prio', action='store_true', help='stream priorities instead of CU masks: the SFE graph '
+                    'on a high-priority stream beside the MWT graph on a normal one')
     args = ap.parse_args()
     import bench
     import ewvit
@@ -75,6 +77,15 @@ def main():
     out['serial_ms'] = pair(plain1, plain1, st_mwt, st_sfe, args.reps)
     out['plain_overlap_uncapped_ms'] = pair(plain1, plain2, st_mwt, st_sfe, args.reps)
     out['plain_overlap_cap160_ms'] = pair(plain1, plain2, st_cap, st_sfe, args.reps)
+    if args.prio:
+        lo, hi = torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)
+        out['prio_sfe_hi_uncapped_ms'] = pair(lo, hi, st_mwt, st_sfe, args.reps)
+        out['prio_sfe_hi_cap160_ms'] = pair(lo, hi, st_cap, st_sfe, args.reps)
+        out['prio_mwt_hi_uncapped_ms'] = pair(hi, lo, st_mwt, st_sfe, args.reps)
+        out['plain_overlap_cap160_again_ms'] = pair(plain1, plain2, st_cap, st_sfe, args.reps)
+        out['prio_sfe_hi_cap160_again_ms'] = pair(lo, hi, st_cap, st_sfe, args.reps)
+        print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
+        return
     for k in (96, 128, 160, 192):
         m = masked_stream(k, total)
         # the complement mask for the SFE stream
