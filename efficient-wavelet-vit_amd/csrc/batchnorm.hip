@@ -129,6 +129,18 @@ static BnGeo bn_geo(int64_t C) {
 // reduction passes: row chunks per (channel chunk, group) — ~512 blocks in all,
 // >= 16 rows per thread, <= 256 partial rows (what an elementwise block finalises
 // from: <= 128 KB of L2 reads next to the rows it streams)
+// workgroup cap of the BatchNorm passes under ewvit_set_grid_cap: the same cap, or
+// EWVIT_BN_CAP (> 0) instead — HBM-bound passes beside the backbone's latency-bound kernels
+// may want more bytes in flight than the convs' cap allows (A/B measurement)
+static int bn_cap() {
+  static const int env = [] {
+    const char *e = getenv("EWVIT_BN_CAP");
+    return e ? atoi(e) : 0;
+  }();
+  if (g_grid_cap <= 0) return 0;
+  return env > 0 ? (env + 7) / 8 * 8 : g_grid_cap;
+}
+
 static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
   static const int cap = [] {
     const char *e = getenv("EWVIT_BN_NRC_CAP");
@@ -144,7 +156,7 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
   if (nrc > cap) nrc = cap;
   const int64_t maxr = M / ((int64_t)g.RG * minr);
   if (nrc > maxr) nrc = maxr;
-  if (g_grid_cap > 0 && nrc * g.nch * groups > g_grid_cap) nrc = g_grid_cap / ((int64_t)g.nch * groups);
+  if (bn_cap() > 0 && nrc * g.nch * groups > bn_cap()) nrc = bn_cap() / ((int64_t)g.nch * groups);
   if (nrc < 1) nrc = 1;
   return (int)nrc;
 }
@@ -159,8 +171,8 @@ static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
   int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
   rpt = rpt < minr ? minr : (rpt > 64 ? 64 : rpt);
-  if (g_grid_cap > 0) {          // capped grid: more rows per block, at most cap blocks in all
-    int64_t nb = g_grid_cap / ((int64_t)g.nch * groups);
+  if (bn_cap() > 0) {            // capped grid: more rows per block, at most cap blocks in all
+    int64_t nb = bn_cap() / ((int64_t)g.nch * groups);
     if (nb < 1) nb = 1;
     const int64_t need = (M + (int64_t)g.RG * nb - 1) / ((int64_t)g.RG * nb);
     if (rpt < need) rpt = need;
