@@ -1045,6 +1045,35 @@ extern "C" int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtyp
   return launch_status("bn_bwd_se");
 }
 
+// ewvit_bn_bwd_se's dx pass only, from partial rows its producer left (ewvit_se_squeeze_mlp_bwd_bn:
+// one row per frame, part [nrc][2C] = (sum g, sum g * xhat), g = (dy * s + se_g) * act'(z));
+// dgamma / dbeta overwritten
+extern "C" int ewvit_bn_bwd_se_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                                        const float *gamma, const float *beta, const float *save_mean,
+                                        const float *save_invstd, int act, float *dgamma, float *dbeta,
+                                        const float *se_s, const float *se_g, int64_t HW, const float *part, int nrc,
+                                        void *stream) {
+  EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && se_s && se_g && part && dtype_ok(dtype),
+                  "bn_bwd_se_partials: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_se_partials: C=%lld", (long long)C);
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd_se_partials: act=%d", act);
+  EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 65535, "bn_bwd_se_partials: %d partial rows", nrc);
+  EWVIT_CHECK_ARG(HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31), "bn_bwd_se_partials: M=%lld rows of %lld",
+                  (long long)M, (long long)HW);
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const BnGeo geo = bn_geo(C);
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+#define BN_SEP(DTV, ACTV)                                                                                           \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV, 2>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean, save_invstd, \
+                     gamma, beta, part, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0, se_s, (int)HW,    \
+                     se_g)
+  BN_DISPATCH(BN_SEP);
+#undef BN_SEP
+  return launch_status("bn_bwd_se_partials");
+}
+
 // backward from partial sums left by the kernel that produced dy (the consumer conv's input
 // gradient: ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [nrc][2C] = per
 // partial row (sum g, sum g * xhat) with g = dy * act'(...) or, row_scale given (the MBConv

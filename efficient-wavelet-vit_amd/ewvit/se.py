@@ -20,6 +20,13 @@ from . import _lib as L
 # the depthwise BatchNorm's apply pass and the SE squeeze as one kernel when the statistics come
 # from the depthwise conv (ewvit_bn_act_se_squeeze; 0: separate passes, A/B)
 _BN_SQUEEZE = os.environ.get('EWVIT_BN_SQUEEZE', '1') != '0'
+# the BatchNorm backward's sums taken by the SE backward's squeeze kernel, per frame
+# (ewvit_se_squeeze_mlp_bwd_bn + ewvit_bn_bwd_se_partials; EWVIT_SE_BN_SUMS=1).  Off: measured
+# slower (SFE piece 14.22-14.25 -> 14.28-14.32 ms, profiles/r03/ab/se_bn_sums_ab.txt) — the
+# squeeze kernel walks one frame's 49-196 rows per block, 1-6 rows per thread, so the third
+# operand's loads, act' and the five-fold LDS tree land on its latency path, while the
+# reduction pass they replace streams the whole map
+_SE_BN_SUMS = os.environ.get('EWVIT_SE_BN_SUMS', '0') == '1'
 
 
 def _rows(x):
@@ -171,13 +178,27 @@ class BnActSEFn(torch.autograd.Function):
         dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
         db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if has_b1 else None
         db2 = torch.empty(C, dtype=torch.float32, device=dev) if has_b2 else None
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
+        if _SE_BN_SUMS:
+            # the SE backward's squeeze kernel also sums the BatchNorm backward's terms per frame
+            # (ewvit_se_squeeze_mlp_bwd_bn): the BatchNorm backward is its dx pass alone
+            mws = torch.empty(L.load().ewvit_se_mlp_bwd_bn_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+            bnpart = torch.empty(N, 2 * C, dtype=torch.float32, device=dev)
+            L.call('ewvit_se_squeeze_mlp_bwd_bn', L.ptr(dyc), L.ptr(x2), L.ptr(xc), L.dt(x2), N, HW, C, L.ptr(sc),
+                   L.ptr(h1), L.ptr(s0), L.ptr(W1), L.ptr(W2), Csq, L.ptr(mean), L.ptr(invstd), L.ptr(gamma),
+                   L.ptr(beta), act, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(bnpart),
+                   L.ptr(mws), L.stream(g), work={'bytes': 3 * x2.numel() * x2.element_size()})
+            L.call('ewvit_bn_bwd_se_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma),
+                   L.ptr(beta), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW,
+                   L.ptr(bnpart), N, L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+            return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2),
+                    db2, None)
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
                L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
                L.stream(g), work={'bytes': 2 * x2.numel() * x2.element_size()})
-        dx = torch.empty_like(xc)
-        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
         ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_bn_bwd_se', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW, L.ptr(ws),

@@ -292,6 +292,13 @@ int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int6
 int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
                     const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
                     float *dbeta, const float *se_s, const float *se_g, int64_t HW, float *workspace, void *stream);
+/* ewvit_bn_bwd_se's dx pass alone, from the partial rows [nrc][2C] of (sum g, sum g*xhat),
+ * g = (dy*se_s + se_g) * act'(z), that ewvit_se_squeeze_mlp_bwd_bn left (one per frame) — the
+ * same backward (network/sfe.py:111-113 via torchvision MBConv) without its reduction pass. */
+int ewvit_bn_bwd_se_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
+                             const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
+                             int act, float *dgamma, float *dbeta, const float *se_s, const float *se_g, int64_t HW,
+                             const float *part, int nrc, void *stream);
 /* Training-mode backward whose reduction pass already ran in the kernel that produced dy
  * (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [groups][nrc][2C] rows of
  * (sum g, sum g*xhat), g = dy * act'(...) or, with row_scale [M / HW] (act 0, one group: the
@@ -524,6 +531,19 @@ int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N
                              const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
                              int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,
                              float *workspace, void *stream);
+/* ewvit_se_squeeze_mlp_bwd for an SE whose input a = act(BatchNorm(xb)) (training mode: mean /
+ * invstd saved by the forward, affine gamma / beta, act 0/1/2): the same outputs (ds, so g and
+ * the MLP gradients, bit-identical), plus that BatchNorm's backward partial rows bnpart [N][2C]
+ * (sum g, sum g*xhat per frame, g = (dy*s + g_se) * act'(z)) for ewvit_bn_bwd_se_partials —
+ * its first kernel sums the BatchNorm terms over the frame's rows as it reads dy, so the
+ * BatchNorm backward's reduction pass never runs (MBConv depthwise BN + SiLU -> SE,
+ * network/sfe.py:111-113).  Workspace: ewvit_se_mlp_bwd_bn_workspace bytes. */
+int64_t ewvit_se_mlp_bwd_bn_workspace(int64_t N, int64_t C, int64_t Csq);
+int ewvit_se_squeeze_mlp_bwd_bn(const void *dy, const void *a, const void *xb, int dtype, int64_t N, int64_t HW,
+                                int64_t C, const float *s, const float *h1, const float *s0, const float *w1,
+                                const float *w2, int64_t Csq, const float *mean, const float *invstd,
+                                const float *gamma, const float *beta, int act, float *g, float *dw1, float *db1,
+                                float *dw2, float *db2, float *bnpart, float *workspace, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,
