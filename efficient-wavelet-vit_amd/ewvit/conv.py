@@ -157,6 +157,25 @@ def _pack(weight, cin_pad, fwd=True, bwd=False):
     return wp, wpt
 
 
+# 1x1 stride-1 convs whose implicit GEMM has at most 64 128x128 tiles over a K of >= 1024 (the
+# backbone's stage-6 project forward, 1536 -> 256 at 7^2, and stage-6 expand input gradient,
+# K = 1536): the LDS-DMA kernel runs them on 50 workgroups, each walking 24 K-tiles, and
+# hipBLASLt (torch.mm, a plain library GEMM: the 1x1 conv over channels-last pixels IS one)
+# splits them over the chip — 20.4 -> 9.2 and 19.0 -> 11.2 us (tools/conv_bench.py --mm,
+# profiles/r03/ab/conv_mm.log).  Such a forward leaves no BatchNorm partials and such an input
+# gradient no backward sums (their BatchNorms run their own reduction passes).  Off by default
+# (EWVIT_CONV_LIBGEMM=1 enables it): the SFE branch alone gains 14.25-14.28 -> 14.09-14.12 ms,
+# but the two-branch step is unchanged (bench 3116-3126 vs 3119-3124 frames/s over 4 interleaved
+# rounds, profiles/r03/ab/conv_libgemm_*): those 50-workgroup launches left CUs to the capped
+# MWT branch, which the library GEMM's wider grids now take.
+import os as _os
+_LIBGEMM = _os.environ.get('EWVIT_CONV_LIBGEMM', '0') == '1'
+
+
+def _libgemm(M, ncol, K):
+    return _LIBGEMM and -(-M // 128) * -(-ncol // 128) <= 64 and K >= 1024 and K % 8 == 0 and ncol % 8 == 0
+
+
 def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     """(groups, rows per group's slice, partial rows per group, channels per group) when this
     conv's input gradient can sum the backward statistics of the BatchNorm that produced its
@@ -220,8 +239,14 @@ class Conv2dFn(torch.autograd.Function):
         # channels (the MWT fusion conv's 54 -> 64) are not counted
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
         ctx.cap = L.current_cap()
+        ctx.libgemm_dx = k == 1 and stride == 1 and levels == 1 and _libgemm(N * H * W, Cx, Cout)
         with L.launch_cap(ctx.cap):
-            if bn_stats is not None:
+            if bn_stats is None and b is None and k == 1 and stride == 1 and levels == 1 and \
+                    _libgemm(N * Ho * Wo, Cout, Cx):
+                # hipBLASLt: y[pixels, Cout] = x[pixels, Cx] @ W[Cout, Cx]^T on the channels-last views
+                torch.mm(xc.permute(0, 2, 3, 1).reshape(-1, Cx), wp.view(Cout, -1)[:, :Cx].t(),
+                         out=y.permute(0, 2, 3, 1).view(-1, Cout))
+            elif bn_stats is not None:
                 # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
                 shift, part, shift_out = bn_stats
                 L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
@@ -260,8 +285,19 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            lk = _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
-            if lk is not None:
+            lk = None if ctx.libgemm_dx else _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            if ctx.libgemm_dx:
+                # hipBLASLt: dx[pixels, Cx] = dy[pixels, Cout] @ W[Cout, Cx] (+ the skip gradient,
+                # added before the bf16 rounding as the dgrad epilogue adds it)
+                d2, w2 = dyc.permute(0, 2, 3, 1).reshape(-1, Cout), wpt.view(-1, Cout)[:Cx].t()
+                x2 = dx.permute(0, 2, 3, 1).view(-1, Cx)
+                if skip is not None:
+                    sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                    torch.addmm(sk.permute(0, 2, 3, 1).reshape(-1, Cx), d2, w2, out=x2)
+                    skip = None
+                else:
+                    torch.mm(d2, w2, out=x2)
+            elif lk is not None:
                 # dx (+ the skip gradient) and the producing BatchNorm's backward sums in one epilogue
                 groups, grows, rows, Cg = lk
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if skip is not None else None
@@ -348,6 +384,8 @@ def bn_stat_rows(x, weight, stride=1, levels=1):
     if (not x.is_cuda or Cx < weight.shape[1] or (levels > 1 and Cx != weight.shape[1]) or k not in (1, 3)
             or weight.shape[3] != k or weight.shape[0] % 8 or NL % levels or (levels > 1 and Cz % 64)):
         return 0
+    if k == 1 and stride == 1 and levels == 1 and _libgemm(NL * H * W, weight.shape[0], Cx):
+        return 0                 # the library GEMM's shape: conv, then the BatchNorm's own statistics
     return int(L.load().ewvit_conv2d_fwd_bn_rows(NL // levels, H, W, Cz * levels, weight.shape[0], k, int(stride)))
 
 

@@ -191,3 +191,28 @@ def test_step_wide_weight_packing():
         for u, v in zip(a, b):
             assert torch.equal(u, v)
     assert not torch.equal(ref[0][0], ref2[0][0])
+
+
+@pytest.mark.parametrize('N,Cin,Cout,H', [(64, 1536, 256, 7), (64, 256, 1536, 7), (8, 1024, 64, 14)])
+def test_conv_1x1_library_gemm_route(N, Cin, Cout, H, monkeypatch):
+    """1x1 stride-1 convs with <= 64 128x128 tiles over K >= 1024 (the stage-6 project forward,
+    the stage-6 expand input gradient) run as hipBLASLt GEMMs on the channels-last views: the
+    same results as the LDS-DMA kernel up to fp32 summation order and the bf16 rounding, the skip
+    gradient added before the rounding, and no BatchNorm partial rows offered for the forward."""
+    import ewvit.conv as ec
+    g = torch.Generator().manual_seed(Cin + Cout)
+    x = torch.randn(N, Cin, H, H, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).to(DEV)
+    dy = torch.randn(N, Cout, H, H, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+    outs = []
+    for lib in (False, True):
+        monkeypatch.setattr(ec, '_LIBGEMM', lib)
+        xd, wd = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        y = ec.conv2d(xd, wd, None, 1)
+        y.backward(dy)
+        outs.append((y.float(), xd.grad.float(), wd.grad))
+        routed_fwd = ec._libgemm(N * H * H, Cout, Cin)
+        assert (ec.bn_stat_rows(x, w, 1) == 0) == (lib and routed_fwd)
+    for a, b in zip(*outs):
+        assert rel(a, b) < 2 ** -7
+    assert ec._libgemm(N * H * H, Cout, Cin) or ec._libgemm(N * H * H, Cin, Cout)

@@ -161,7 +161,14 @@ def main():
             t1 = graph_time(lambda: torch.mm(x2, w2.t()), a.iters)
             t2 = graph_time(lambda: torch.mm(d2, w2), a.iters)
             t3 = graph_time(lambda: torch.mm(d2.t(), x2), a.iters)
-            print(f'{name:15s} [hipBLASLt] fwd {t1:8.1f} us | dgrad {t2:8.1f} us | wgrad {t3:8.1f} us', flush=True)
+            dwo = torch.empty(Cout, Cin, device=dev)
+            try:
+                t4 = graph_time(lambda: torch.mm(d2.t(), x2, out_dtype=torch.float32, out=dwo), a.iters)
+            except Exception as e:          # out_dtype not supported on this build
+                print(f'{name:15s} [hipBLASLt] fp32-out wgrad: {type(e).__name__}: {e}', flush=True)
+                t4 = float('nan')
+            print(f'{name:15s} [hipBLASLt] fwd {t1:8.1f} us | dgrad {t2:8.1f} us | wgrad {t3:8.1f} us | '
+                  f'wgrad fp32 out {t4:8.1f} us', flush=True)
 
 
 if __name__ == '__main__':
