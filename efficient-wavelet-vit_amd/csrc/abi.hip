@@ -5,7 +5,9 @@
 
 namespace ewvit {
 static thread_local char g_err[512] = "";
-int g_grid_cap = 0;
+// per host thread: nn.DataParallel runs its replicas in threads (reference train.py:249-251),
+// and a cap set around one replica's branch must not reach another's launches
+thread_local int g_grid_cap = 0;
 
 void set_error(const char *fmt, ...) {
   va_list ap;
@@ -19,7 +21,8 @@ extern "C" int ewvit_abi_version(void) { return EWVIT_ABI_VERSION; }
 extern "C" const char *ewvit_last_error(void) { return ewvit::g_err; }
 
 // workgroups at most per launch of the big-grid kernels (LDS-DMA convs, BatchNorm passes);
-// 0 = no cap.  Set around a branch that shares the GPU with another stream.
+// 0 = no cap.  Set around a branch that shares the GPU with another stream; the cap is the
+// calling thread's (launches issued by other threads keep their own).
 extern "C" int ewvit_set_grid_cap(int max_workgroups) {
   const int prev = ewvit::g_grid_cap;
   ewvit::g_grid_cap = max_workgroups > 0 ? (max_workgroups + 7) / 8 * 8 : 0;   // whole XCD rounds

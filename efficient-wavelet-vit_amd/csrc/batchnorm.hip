@@ -129,29 +129,13 @@ static BnGeo bn_geo(int64_t C) {
 // reduction passes: row chunks per (channel chunk, group) — ~512 blocks in all,
 // >= 16 rows per thread, <= 256 partial rows (what an elementwise block finalises
 // from: <= 128 KB of L2 reads next to the rows it streams)
-// workgroup cap of the BatchNorm passes under ewvit_set_grid_cap: the same cap, or
-// EWVIT_BN_CAP (> 0) instead — HBM-bound passes beside the backbone's latency-bound kernels
-// may want more bytes in flight than the convs' cap allows (A/B measurement)
-static int bn_cap() {
-  static const int env = [] {
-    const char *e = getenv("EWVIT_BN_CAP");
-    return e ? atoi(e) : 0;
-  }();
-  if (g_grid_cap <= 0) return 0;
-  return env > 0 ? (env + 7) / 8 * 8 : g_grid_cap;
-}
+// workgroup cap of the BatchNorm passes under ewvit_set_grid_cap: the convs' cap (a separate
+// BatchNorm cap, 64 - 640 workgroups, measured no better: DESIGN §5.6)
+static int bn_cap() { return g_grid_cap > 0 ? g_grid_cap : 0; }
 
 static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
-  static const int cap = [] {
-    const char *e = getenv("EWVIT_BN_NRC_CAP");
-    const int v = e ? atoi(e) : 256;
-    return v < 1 ? 1 : (v > 256 ? 256 : v);
-  }();
-  static const int minr = [] {      // rows per thread at least (A/B: EWVIT_BN_MINRPT)
-    const char *e = getenv("EWVIT_BN_MINRPT");
-    const int v = e ? atoi(e) : 16;
-    return v < 1 ? 1 : (v > 64 ? 64 : v);
-  }();
+  // <= 256 partial rows, >= 16 rows per thread (8 / 32 measured 0.3-2 % slower on the SFE)
+  constexpr int cap = 256, minr = 16;
   int64_t nrc = (512 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   if (nrc > cap) nrc = cap;
   const int64_t maxr = M / ((int64_t)g.RG * minr);
@@ -163,11 +147,7 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
 
 // elementwise passes: ~1024 blocks in all, 8..64 rows per thread
 static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
-  static const int minr = [] {      // rows per thread at least (A/B: EWVIT_BN_MINRPE)
-    const char *e = getenv("EWVIT_BN_MINRPE");
-    const int v = e ? atoi(e) : 8;
-    return v < 1 ? 1 : (v > 64 ? 64 : v);
-  }();
+  constexpr int minr = 8;          // rows per thread at least (4 / 16 measured slower)
   int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
   rpt = rpt < minr ? minr : (rpt > 64 ? 64 : rpt);
@@ -1043,35 +1023,6 @@ extern "C" int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtyp
   BN_DISPATCH(BN_SE);
 #undef BN_SE
   return launch_status("bn_bwd_se");
-}
-
-// ewvit_bn_bwd_se's dx pass only, from partial rows its producer left (ewvit_se_squeeze_mlp_bwd_bn:
-// one row per frame, part [nrc][2C] = (sum g, sum g * xhat), g = (dy * s + se_g) * act'(z));
-// dgamma / dbeta overwritten
-extern "C" int ewvit_bn_bwd_se_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
-                                        const float *gamma, const float *beta, const float *save_mean,
-                                        const float *save_invstd, int act, float *dgamma, float *dbeta,
-                                        const float *se_s, const float *se_g, int64_t HW, const float *part, int nrc,
-                                        void *stream) {
-  EWVIT_CHECK_ARG(dy && x && dx && save_mean && save_invstd && se_s && se_g && part && dtype_ok(dtype),
-                  "bn_bwd_se_partials: bad args");
-  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_se_partials: C=%lld", (long long)C);
-  EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd_se_partials: act=%d", act);
-  EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 65535, "bn_bwd_se_partials: %d partial rows", nrc);
-  EWVIT_CHECK_ARG(HW > 0 && M % HW == 0 && M < ((int64_t)1 << 31), "bn_bwd_se_partials: M=%lld rows of %lld",
-                  (long long)M, (long long)HW);
-  if (M == 0) return 0;
-  hipStream_t s = as_stream(stream);
-  const BnGeo geo = bn_geo(C);
-  const int64_t rpb = bn_rows_per_block(geo, M, 1);
-  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
-#define BN_SEP(DTV, ACTV)                                                                                           \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV, 2>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean, save_invstd, \
-                     gamma, beta, part, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0, se_s, (int)HW,    \
-                     se_g)
-  BN_DISPATCH(BN_SEP);
-#undef BN_SEP
-  return launch_status("bn_bwd_se_partials");
 }
 
 // backward from partial sums left by the kernel that produced dy (the consumer conv's input

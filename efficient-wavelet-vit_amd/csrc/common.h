@@ -163,7 +163,7 @@ struct BnBwdStats {
 
 inline bool dtype_ok(int dt) { return dt == EWVIT_F32 || dt == EWVIT_BF16; }
 
-// workgroup cap of the big-grid launches (abi.hip, ewvit_set_grid_cap); 0 = none
-extern int g_grid_cap;
+// workgroup cap of the big-grid launches (abi.hip, ewvit_set_grid_cap); 0 = none; per host thread
+extern thread_local int g_grid_cap;
 
 }  // namespace ewvit

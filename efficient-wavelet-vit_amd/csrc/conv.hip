@@ -1077,19 +1077,13 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 // 256-B rows, chunk c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)) (read transposed,
 // ds_read_b64_tr_b16).  Bias gradient (sum of dy over pixels): the blocks of n'-tile
 // t sum the dy image of the K-tiles kt = t (mod n'-tiles), spreading the extra reads.
-// KG = 2: two K-groups of 4 waves share a workgroup — group g multiplies the split's K-tiles
-// g, g + 2, ... through its own LDS ring, and group 1 hands its accumulators to group 0
-// through LDS at the end (fixed order: group 0 + group 1), so a workgroup covers twice the
-// pixels of a split and the fp32 partial slabs (and their reduce) halve at the same wave count
-template <int KS, int BK, int NS, int WJ = 4, int KG = 1>
-__global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
+template <int KS, int BK, int NS, int WJ = 4>
+__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
   constexpr int NB = WJ / 4;         // 128-column x images per stage (n'-tile of 128 * NB)
   constexpr int IMG = BK * 256, STG = (1 + NB) * IMG;
   constexpr int P = BK / 16;        // pieces (4 rows x 256 B) per wave per image
-  static_assert(KG == 1 || (KG == 2 && NS * STG * 2 >= 4 * 64 * 4 * WJ * 16 + 8 * 16 * 8 * 4), "K-group LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[KG * NS * STG];
-  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3;
-  const int kg = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
@@ -1097,9 +1091,7 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
   const int NP = KS * KS * a.g.Cin;
   const int64_t mbeg = (int64_t)split * a.mper;
   const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
-  // K-tiles per group (both groups run the same count: a group past the split's end stages
-  // zero tiles, which keeps every wave's LDS-DMA accounting uniform)
-  const int nk = (int)((mend - mbeg + (int64_t)BK * KG - 1) / ((int64_t)BK * KG));
+  const int nk = (int)((mend - mbeg + BK - 1) / BK);
   const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, x_bytes);
   const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * a.g.Cout * 2);
 
@@ -1133,14 +1125,12 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
   // exact floor(x / d) = umulhi(x, ceil(2^32 / d)) for x < 2^32 / d
   const uint32_t magW = (uint32_t)((0x100000000ull + a.g.Wo - 1) / a.g.Wo);
   const uint32_t magH = (uint32_t)((0x100000000ull + a.g.Ho - 1) / a.g.Ho);
-  const int64_t gbeg = mbeg + (int64_t)kg * BK;    // this K-group's first pixel
-  int sn = (int)(gbeg / ((int64_t)a.g.Ho * a.g.Wo));
-  int soh = (int)((gbeg / a.g.Wo) % a.g.Ho);
-  int sow = (int)(gbeg % a.g.Wo);
+  int sn = (int)(mbeg / ((int64_t)a.g.Ho * a.g.Wo));
+  int soh = (int)((mbeg / a.g.Wo) % a.g.Ho);
+  int sow = (int)(mbeg % a.g.Wo);
   const int xrow = a.xgc * 2;                       // bytes per pixel step
-  auto stage = [&](int kl, int buf) {               // kl: the group's K-tile index
-    const int kt = kl * KG + kg;                    // the split's K-tile index
-    unsigned char *base = smem + (kg * NS + buf) * STG + ws * P * 1024;
+  auto stage = [&](int kt, int buf) {               // kt: the split's K-tile index
+    unsigned char *base = smem + buf * STG + ws * P * 1024;
     const int lim = (int)(mend - mbeg) - kt * BK;   // rows r < lim are inside the split
     const int adel = kt * BK * a.g.Cout * 2;
 #pragma unroll
@@ -1162,7 +1152,7 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
                ok ? (uint32_t)(((n * a.g.H + ih) * a.g.W + iw) * xrow + bgo[e]) : OOB);
       }
     }
-    sow += BK * KG;                                 // the group's next K-tile (scalar)
+    sow += BK;                                      // the next K-tile (scalar)
     while (sow >= a.g.Wo) {
       sow -= a.g.Wo;
       if (++soh == a.g.Ho) { soh = 0; ++sn; }
@@ -1182,9 +1172,8 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
 #pragma unroll
     for (int j = 0; j < WJ; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4;
-  auto compute = [&](int kl, int buf) {
-    const int kt = kl * KG + kg;
-    const unsigned char *As = smem + (kg * NS + buf) * STG;
+  auto compute = [&](int kt, int buf) {
+    const unsigned char *As = smem + buf * STG;
     // wave column wn: 64 columns of the one x image (WJ 4), or a whole image (WJ 8)
     const unsigned char *Bs = As + IMG + (NB > 1 ? wn * IMG : 0);
     const int bc0 = NB > 1 ? 0 : wn * 64;
@@ -1214,7 +1203,7 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
       // thread t of a K-group: rows (t>>4)*(BK/16) .. of its dy image, chunk t & 15 (8 channels)
 #pragma unroll
       for (int q = 0; q < BK / 16; ++q) {
-        const int r = ((tid & 255) >> 4) * (BK / 16) + q;    // the K-group's own 256 threads
+        const int r = (tid >> 4) * (BK / 16) + q;
         const uint4 v = *reinterpret_cast<const uint4 *>(As + swz_off(r, tid & 15));
         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1243,8 +1232,7 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
   }
   __syncthreads();
   if (do_bias) {
-    // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves (of
-    // each K-group, groups in order)
+    // threads t, t^16, t^32, t^48 of a wave hold the same 8 channels; then the 4 waves
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bsum[j] = rows_sum4(bsum[j]);
@@ -1252,40 +1240,15 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
     float *red = reinterpret_cast<float *>(smem);
     if (lane < 16)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[((kg * 4 + w) * 16 + lane) * 8 + j] = bsum[j];
+      for (int j = 0; j < 8; ++j) red[(w * 16 + lane) * 8 + j] = bsum[j];
     __syncthreads();
     if (tid < 128) {
       const int ch = tid >> 3, j = tid & 7;
       const int co = co0 + ch * 8 + j;
       float s = (red[(0 * 16 + ch) * 8 + j] + red[(1 * 16 + ch) * 8 + j]) +
                 (red[(2 * 16 + ch) * 8 + j] + red[(3 * 16 + ch) * 8 + j]);
-      if (KG > 1)
-        s += (red[(4 * 16 + ch) * 8 + j] + red[(5 * 16 + ch) * 8 + j]) +
-             (red[(6 * 16 + ch) * 8 + j] + red[(7 * 16 + ch) * 8 + j]);
       if (co < a.g.Cout) a.dbias_part[((int64_t)split * ntx + tx) * a.g.Cout + co] = s;
     }
-    if (KG > 1) __syncthreads();
-  }
-  if constexpr (KG > 1) {
-    // group 1's accumulators to group 0 through LDS ([wave][i][j][r][lane] floats, each
-    // 64-lane row contiguous), added in a fixed order
-    float *xa = reinterpret_cast<float *>(smem);
-    if (kg == 1) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < WJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) xa[(((w * 4 + i) * WJ + j) * 4 + r) * 64 + lane] = acc[i][j][r];
-    }
-    __syncthreads();
-    if (kg == 1) return;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += xa[(((w * 4 + i) * WJ + j) * 4 + r) * 64 + lane];
   }
   float *dst = a.part + (int64_t)split * a.g.Cout * NP;
 #pragma unroll
@@ -1302,74 +1265,15 @@ __global__ __launch_bounds__(256 * KG) void conv_wgrad_glds_kernel(WgradArgs a, 
   }
 }
 
-// Kernel family: 0 register-staged everywhere; 1.. LDS-DMA configurations
-//   fwd/dgrad (rows per tile, ring depth): 1 (128, 2)  2 (128, 3)  3 (256, 2)  4 (256, 3)
-//     5 (128; ring 4 when the grid is <= 256 workgroups, else 2)  7 (128, 2, 8 waves)
-//     1 takes 7's 8-wave blocks for grids of <= 1024 workgroups
-//   wgrad (pixels per K-tile, ring depth): 1 (64, 2)   2 (64, 3)   3 (32, 3)   4 (32, 4)
-// +8: fwd/dgrad K-tiles ordered channel-block outer, tap inner.
-// EWVIT_CONV_GLDS=<n> or ewvit_conv2d_set_glds(n) select one (A/B measurement).
-static int g_glds = -1;
-static int glds_variant() {
-  if (g_glds < 0) {
-    const char *e = getenv("EWVIT_CONV_GLDS");
-    g_glds = e ? atoi(e) : 9;
-    if (g_glds < 0 || g_glds > 15) g_glds = 9;
-  }
-  return g_glds;
-}
-static bool use_glds() { return (glds_variant() & 7) != 0; }
-
-// Wide-wave blocks for the big 128-column grids (the MWT's multiscale / fusion convs and the
-// multiscale input gradient): each wave owns 64 x 128 of the tile instead of 64 x 64, so it
-// reads (64 + 128) / (64 * 128) LDS bytes per MFMA flop instead of (64 + 64) / (64 * 64) —
-// 3/4 of the fragment traffic that bounds the 4-wave 128 x 128 block.
-//   1: 256 x 128 tiles, 4 waves, 2-deep ring (96 KB: one block per CU)
-//   2: 128 x 128 tiles, 2 waves, 2-deep ring (64 KB: two blocks per CU)
-//   3: 256 x 128 tiles, 4 waves, 3-deep ring (144 KB)
-// for grids of more than EWVIT_CONV_WWMIN (default 4096) 128 x 128 tiles; 0 = off.
-// EWVIT_CONV_WW or ewvit_conv2d_set_ww (A/B measurement).
-static int g_ww = -1;
-static int ww_variant() {
-  if (g_ww < 0) {
-    const char *e = getenv("EWVIT_CONV_WW");
-    g_ww = e ? atoi(e) : 0;
-    if (g_ww < 0 || g_ww > 3) g_ww = 0;
-  }
-  return g_ww;
-}
-static int64_t g_wwmin = -1;
-static int64_t ww_min() {
-  if (g_wwmin < 0) {
-    const char *e = getenv("EWVIT_CONV_WWMIN");
-    g_wwmin = e ? (int64_t)atoll(e) : (int64_t)4096;
-    if (g_wwmin < 0) g_wwmin = 4096;
-  }
-  return g_wwmin;
-}
-static int ww_pick(int64_t M, int Ncol, int bn) {
-  if (bn != 128 || !ww_variant()) return 0;
-  const int64_t nwg = (M + 127) / 128 * ((Ncol + 127) / 128);
-  return nwg > ww_min() ? ww_variant() : 0;
-}
-
-// Variant: K-tile depth 64 when every K-tile can stay inside one tap (KC % 64 == 0),
-// else 32; register prefetch depth from EWVIT_CONV_PF (1 or 2, default 1).
-// Ncol <= 64 (e.g. the fusion conv's 56-channel input gradient) uses the 128x64 tile.
-static int conv_pf() {
-  static int pf = [] {
-    const char *e = getenv("EWVIT_CONV_PF");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  return pf;
-}
-static int conv_bk64() {
-  static int v = [] {
-    const char *e = getenv("EWVIT_CONV_BK");
-    return (e && e[0] == '3') ? 0 : 1;   // EWVIT_CONV_BK=32 disables the 64-deep tile
-  }();
-  return v;
-}
+// Kernel family: 1 (default) the LDS-DMA kernels wherever the shape allows them, the
+// register-staged kernels elsewhere; 0 the register-staged kernels everywhere — a test
+// switch (ewvit_conv2d_set_glds): they are the fallback of the shapes the LDS-DMA kernels
+// refuse, so the tests run every case through both.  (The other tile / ring-depth families
+// measured while tuning — 3-deep rings, 256-row tiles everywhere, 64-row tiles for small
+// grids, wide 64 x 128 waves, two K-groups per wgrad workgroup — were slower and are gone;
+// their numbers are in DESIGN.md §5.)
+static int g_glds = 1;
+static bool use_glds() { return g_glds != 0; }
 
 // M-tiles of the register-staged grid: all, or (g_grid_cap) at most cap / N-tiles of them
 static unsigned capped_mtiles(int64_t M, int ntn) {
@@ -1472,31 +1376,19 @@ __global__ __launch_bounds__(256) void conv3x3_small_kernel(FwdArgs a, int TH, i
   }
 }
 
-// EWVIT_CONV_SMALL = 0: those convs take the GEMM-tiled kernels
 static bool launch_small(const FwdArgs &a, bool dgrad, hipStream_t s) {
-  static const int on = [] {
-    const char *e = getenv("EWVIT_CONV_SMALL");
-    return e ? atoi(e) : 1;
-  }();
-  if (!on || a.g.ks != 3 || a.g.stride != 1 || a.sgs != 0 || a.ogs != 0 || a.sgc != a.KC || a.ogc != a.Ncol ||
+  if (a.g.ks != 3 || a.g.stride != 1 || a.sgs != 0 || a.ogs != 0 || a.sgc != a.KC || a.ogc != a.Ncol ||
       a.KCr || a.addend || a.bn_part || a.pc >= 0 || a.outH != a.srcH || a.outW != a.srcW || a.outW > 256 ||
       a.Ncol % 8)
     return false;
   const int KC = a.KC, NT = (a.Ncol + 15) / 16;
   if (!((KC == 24 && NT <= 2) || (KC == 16 && NT <= 4))) return false;
   const int H = a.outH, W = a.outW;
-  // rows per workgroup (at most; EWVIT_CONV_SMALL_TH overrides), LDS <= EWVIT_CONV_SMALL_LDS KB:
-  // 4 rows for 24 channels (stage 1: 29 us; 2 / 6 / 8 rows 34 / 31 / 33 us), 8 for 16 (the
-  // seperate conv: 119 us; 4 / 6 / 12 rows 129 / 123 / 133 us), tools/small_ab.sh
-  static const int thenv = [] {
-    const char *e = getenv("EWVIT_CONV_SMALL_TH");
-    return e ? atoi(e) : 0;
-  }();
-  static const int ldsmax = [] {
-    const char *e = getenv("EWVIT_CONV_SMALL_LDS");
-    return (e ? atoi(e) : 64) * 1024;
-  }();
-  const int thmax = thenv > 0 ? thenv : (KC == 16 ? 8 : 4);
+  // rows per workgroup, LDS <= 64 KB: 4 rows for 24 channels (stage 1: 29 us; 2 / 6 / 8 rows
+  // 34 / 31 / 33 us), 8 for 16 (the seperate conv: 119 us; 4 / 6 / 12 rows 129 / 123 / 133 us),
+  // tools/small_ab.sh
+  const int ldsmax = 64 * 1024;
+  const int thmax = KC == 16 ? 8 : 4;
   int TH = thmax;
   while (TH > 1 && (TH + 2) * (W + 2) * KC * 2 > ldsmax) --TH;
   const size_t lds = (size_t)(TH + 2) * (W + 2) * KC * 2;
@@ -1536,40 +1428,14 @@ static void launch_fwd_v(const FwdArgs &a, hipStream_t s) {
 
 template <bool DGRAD, int KS>
 static void launch_fwd_ks(const FwdArgs &a, hipStream_t s) {
-  const bool bk64 = conv_bk64() && a.KC % 64 == 0 && a.sgc % 64 == 0;
-  const int pf = conv_pf();
-  if (bk64) {
-    if (pf == 2) launch_fwd_v<DGRAD, KS, 64, 2>(a, s);
-    else launch_fwd_v<DGRAD, KS, 64, 1>(a, s);
-  } else {
-    if (pf == 2) launch_fwd_v<DGRAD, KS, 32, 2>(a, s);
-    else launch_fwd_v<DGRAD, KS, 32, 1>(a, s);
-  }
+  if (a.KC % 64 == 0 && a.sgc % 64 == 0) launch_fwd_v<DGRAD, KS, 64, 1>(a, s);
+  else launch_fwd_v<DGRAD, KS, 32, 1>(a, s);
 }
 
 template <bool DGRAD>
 static void launch_fwd(const FwdArgs &a, hipStream_t s) {
   if (a.g.ks == 1) launch_fwd_ks<DGRAD, 1>(a, s);
   else launch_fwd_ks<DGRAD, 3>(a, s);
-}
-
-static int conv_ragged() {
-  static int v = [] {
-    const char *e = getenv("EWVIT_CONV_RAGGED");   // 0: K % 64 != 0 takes the register-staged kernel
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// EWVIT_CONV_DENSE: forward convs of a plain input whose channels are not a multiple of 64
-// take the dense-K LDS-DMA kernel (1, the default) instead of the ragged-K / register-staged
-// paths (0)
-static int conv_dense() {
-  static int v = [] {
-    const char *e = getenv("EWVIT_CONV_DENSE");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
 }
 
 // the dense-K forward (conv_glds_kernel<false, ..., DENSE>): 128-row tiles, 8 waves with a
@@ -1590,22 +1456,10 @@ static void launch_glds_dense(const FwdArgs &a, int64_t src_bytes, hipStream_t s
                          0, s, a, src_bytes, ntn, 0, ntiles);                                                     \
   } while (0)
   (void)bn;                                // Ncol > 64: 128-wide column tiles
-  // A/B knobs: EWVIT_CONV_DENSE_W8MAX (grids up to this many blocks take 8 waves; 4096 covers
-  // stage 2's 48 -> 192 expands, 3136 blocks: 81 -> 75 us), EWVIT_CONV_DENSE_NS (ring depth of
-  // the big-grid form; 3 measured 30-60 % slower)
-  static const int w8max = [] {
-    const char *e = getenv("EWVIT_CONV_DENSE_W8MAX");
-    return e ? atoi(e) : 4096;
-  }();
-  static const int dns = [] {
-    const char *e = getenv("EWVIT_CONV_DENSE_NS");
-    return e ? atoi(e) : 2;
-  }();
+  // grids up to 4096 blocks take 8 waves (stage 2's 48 -> 192 expands, 3136 blocks: 81 -> 75
+  // us); a 3-deep ring for the big grids measured 30-60 % slower
   if (nwg <= 256) EWVIT_GLDS_DENSE(128, 4, 4);
-  else if (nwg <= w8max) {
-    if (dns == 3) EWVIT_GLDS_DENSE(128, 3, 4);
-    else EWVIT_GLDS_DENSE(128, 2, 4);
-  } else if (dns == 3) EWVIT_GLDS_DENSE(128, 3, 2);
+  else if (nwg <= 4096) EWVIT_GLDS_DENSE(128, 2, 4);
   else EWVIT_GLDS_DENSE(128, 2, 2);
 #undef EWVIT_GLDS_DENSE
 }
@@ -1626,197 +1480,79 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
   // seperate conv's 16 -> 64, the 96 -> 48 projects — the register-staged kernel measured
   // as fast or faster: 62 vs 64, 166 vs 199, 15 vs 16 us; Cout 96 / 192: 39 -> 32, 106 -> 81,
   // 34 -> 27 us, tools/conv_bench.py)
-  if (!DGRAD && ragged && conv_dense() && use_glds() && a.Ncol > 64 && a.sgs == 0 && a.sgc == a.KC && a.KC % 8 == 0 &&
+  if (!DGRAD && ragged && use_glds() && a.Ncol > 64 && a.sgs == 0 && a.sgc == a.KC && a.KC % 8 == 0 &&
       src_bytes < (int64_t)OOB && a.Ncol * K * 2 < (int64_t)OOB && a.M * a.ogc < ((int64_t)1 << 40) &&
       (a.g.ks == 1 || a.g.ks == 3)) {
     launch_glds_dense(a, src_bytes, s);
     return true;
   }
-  // (a parity-class dgrad, which already skips 3/4 of the taps, up to 1/3; EWVIT_CONV_RAGGED_1X1 = 1:
-  // a 1x1 input gradient with up to 1/3 zero lanes too — stage 2's projects, K = 48)
-  static const int r1x1 = [] {
-    const char *e = getenv("EWVIT_CONV_RAGGED_1X1");
-    return e ? atoi(e) : 0;
-  }();
+  // a parity-class dgrad, which already skips 3/4 of the taps, takes up to 1/3 zero lanes
   const int kpad = (a.KC + 63) / 64 * 64;
-  const bool ragged_ok = a.pc >= 0 ? 2 * kpad <= 3 * a.KC
-                                   : (5 * kpad <= 6 * a.KC || (r1x1 && DGRAD && a.g.ks == 1 && 2 * kpad <= 3 * a.KC));
-  if (ragged && (!conv_ragged() || a.sgs != 0 || a.sgc != a.KC || a.KC % 8 || !ragged_ok))
+  const bool ragged_ok = a.pc >= 0 ? 2 * kpad <= 3 * a.KC : 5 * kpad <= 6 * a.KC;
+  if (ragged && (a.sgs != 0 || a.sgc != a.KC || a.KC % 8 || !ragged_ok))
     return false;
   if (!use_glds() || (!ragged && a.KC % 64) || (padded ? a.sgc != a.KCr : (!ragged && a.sgc % 64)) ||
       src_bytes >= (int64_t)OOB ||
       a.Ncol * K * 2 >= (int64_t)OOB ||
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
-  int v = glds_variant() & 7;
-  const int tap_inner = (glds_variant() & 8) ? 1 : 0;
+  const int tap_inner = 1;           // the 9 taps of a 64-channel block are consecutive K-tiles
   // <= 32 columns (stage 2's entry-conv input gradient, 24 channels): 32-wide column tiles
-  // (EWVIT_CONV_BN32 = 0: the 64-wide ones)
-  static const int bn32 = [] {
-    const char *e = getenv("EWVIT_CONV_BN32");
-    return e ? atoi(e) : 1;
-  }();
-  const int bn = (bn32 && a.Ncol <= 32 && v != 3 && v != 4) ? 32 : a.Ncol <= 64 ? 64 : 128;
+  const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
   const int ntn = (a.Ncol + bn - 1) / bn;
-  // a <= 64-column dgrad over a big map (the MWT fusion conv's 56-channel input gradient,
-  // 2.4 M pixels): 256-row blocks, 535 -> 505 us.  Stage 2's 48-channel 3x3 dgrad (1568 row
-  // tiles) now runs faster on 8-wave 128-row blocks (96 -> 75 us, tools/dgrad_ab.sh), so the
-  // threshold is 4096.  EWVIT_CONV_DG256 = the row-tile count above which (0: never)
-  static const int dg256 = [] {
-    const char *e = getenv("EWVIT_CONV_DG256");
-    return e ? atoi(e) : 4096;
-  }();
-  if (DGRAD && v == 1 && bn == 64 && dg256 > 0 && (a.M + 127) / 128 * ntn > dg256) v = 3;
-  const int BM = (v == 3 || v == 4) ? 256 : 128;
+  // a <= 64-column dgrad over > 4096 row tiles (the MWT fusion conv's 56-channel input
+  // gradient, 2.4 M pixels): 256-row blocks, 535 -> 505 us.  Stage 2's 48-channel 3x3 dgrad
+  // (1568 row tiles) runs faster on 8-wave 128-row blocks (96 -> 75 us, tools/dgrad_ab.sh)
+  const bool big = DGRAD && bn == 64 && (a.M + 127) / 128 * ntn > 4096 && !a.bwd.part;
+  const int BM = big ? 256 : 128;
   if (bm_out) *bm_out = BM;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
   const int ntiles = (int)nwg;
   const dim3 grid((unsigned)(g_grid_cap > 0 && nwg > g_grid_cap ? g_grid_cap : nwg));
-#define EWVIT_GLDS_FWDW(BM_, BN__, NS_, WC_)                                                                        \
+#define EWVIT_GLDS_FWDW(BM_, BN__, NS_, WC_, BST_)                                                                  \
   do {                                                                                                            \
     if (a.g.ks == 1)                                                                                              \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
-                         src_bytes, ntn, tap_inner, ntiles);                                                      \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 1, NS_, WC_, false, BST_>), grid,                     \
+                         dim3(BM_ / 64 * WC_ * 64), 0, s, a, src_bytes, ntn, tap_inner, ntiles);                  \
     else                                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_, WC_>), grid, dim3(BM_ / 64 * WC_ * 64), 0, s, a, \
-                         src_bytes, ntn, tap_inner, ntiles);                                                      \
+      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, BN__, 3, NS_, WC_, false, BST_>), grid,                     \
+                         dim3(BM_ / 64 * WC_ * 64), 0, s, a, src_bytes, ntn, tap_inner, ntiles);                  \
   } while (0)
-#define EWVIT_GLDS_FWD(BM_, BN__, NS_) EWVIT_GLDS_FWDW(BM_, BN__, NS_, 2)
-  // variant 5: a grid of at most one workgroup per CU cannot hide the operand latency
-  // behind a second resident block, so it gets a 4-deep LDS ring (3 K-tiles in flight)
-  // variant 1 (the default family): grids of <= 1024 workgroups (the backbone's 7x7 /
-  // 14x14 / 28x28 convs) take 8-wave blocks (64 x BN/4 per wave) — twice the waves per
-  // CU to hide the latency of their short K loops; big grids keep 4 waves (fewer LDS
-  // reads per MFMA)
-  // — and every dgrad with 128-wide column tiles (freq_conv's parity-class dgrad 185 -> 162 us,
-  // multiscale 834 -> 820; the 56-column fusion dgrad is slower on 8 waves and keeps 4)
-  static const int dg8 = [] {
-    const char *e = getenv("EWVIT_CONV_DG8");
-    return e ? atoi(e) : 1;
-  }();
-  static const int w8max = [] {      // grids up to this many blocks take 8 waves
-    const char *e = getenv("EWVIT_CONV_W8MAX");
-    return e ? atoi(e) : 2048;
-  }();
-  const bool wide8 = nwg <= w8max || (DGRAD && bn == 128 && dg8);
-  int vv = v == 5 ? (nwg <= 256 ? 6 : 1) : (v == 1 && wide8 ? 7 : v);
-  // grids of at most EWVIT_CONV_SGMAX blocks (the backbone's long-K 1x1 convs at 7^2 / 14^2:
-  // 50-196 blocks of 15-24 K-tiles — at most one block per CU, so occupancy hides nothing):
-  // EWVIT_CONV_SG = 8: 8 waves with a 4-deep ring (3 K-tiles in flight); 9: 64-row tiles
-  // (twice the blocks), 4 waves, 4-deep ring; 0: as above
-  static const int sg = [] {
-    const char *e = getenv("EWVIT_CONV_SG");
-    return e ? atoi(e) : 8;
-  }();
-  static const int sgmax = [] {
-    const char *e = getenv("EWVIT_CONV_SGMAX");
-    return e ? atoi(e) : 256;
-  }();
-  // (64-row tiles would change the BatchNorm partial rows fwd_bn_rows promised: not with bn_part)
-  if (v == 1 && (sg == 8 || (sg == 9 && !a.bn_part && !a.bwd.part)) && nwg <= sgmax) vv = sg;
-  const int ww = (v == 1 && a.pc < 0 && !a.bwd.part) ? ww_pick(a.M, a.Ncol, bn) : 0;
-  if (ww) {
-    // (fwd_bn_rows promises 256-row BatchNorm partials for variants 1 / 3)
-    const int wbm = ww == 2 ? 128 : 256;
-    if (bm_out) *bm_out = wbm;
-    const int64_t nt = (a.M + wbm - 1) / wbm * ntn;
-    if (nt >= (int64_t)1 << 31) return false;
-    // a capped grid: one 256-row block fills a CU, so half the workgroups of the cap
-    const int64_t capw = g_grid_cap > 0 ? (wbm == 256 ? (g_grid_cap + 1) / 2 : g_grid_cap) : 0;
-    const dim3 gw((unsigned)(capw > 0 && nt > capw ? capw : nt));
-#define EWVIT_GLDS_WW(BM_, NS_)                                                                                   \
-  do {                                                                                                            \
-    if (a.g.ks == 1)                                                                                              \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, 128, 1, NS_, 1>), gw, dim3(BM_), 0, s, a, src_bytes, ntn,   \
-                         tap_inner, (int)nt);                                                                     \
-    else                                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<DGRAD, BM_, 128, 3, NS_, 1>), gw, dim3(BM_), 0, s, a, src_bytes, ntn,   \
-                         tap_inner, (int)nt);                                                                     \
-  } while (0)
-    if (ww == 1) EWVIT_GLDS_WW(256, 2);
-    else if (ww == 2) EWVIT_GLDS_WW(128, 2);
-    else EWVIT_GLDS_WW(256, 3);
-#undef EWVIT_GLDS_WW
-    return true;
-  }
-  if constexpr (DGRAD) {
-    if (a.bwd.part) {
-      // the backward-statistics epilogue (its own instantiations): 128-row tiles always (the
-      // partial rows ewvit_conv2d_bwd_bn_rows promised), uncapped; the same tile / ring / wave
-      // choice as below otherwise
-      if (bm_out) *bm_out = 128;
-      const int64_t nt = (a.M + 127) / 128 * ntn;
-      if (nt >= (int64_t)1 << 31) return false;
-      const dim3 g1((unsigned)(g_grid_cap > 0 && nt > g_grid_cap ? g_grid_cap : nt));
-#define EWVIT_GLDS_BST(BN__, NS_, WC_)                                                                              \
-  do {                                                                                                            \
-    if (a.g.ks == 1)                                                                                              \
-      hipLaunchKernelGGL((conv_glds_kernel<true, 128, BN__, 1, NS_, WC_, false, true>), g1, dim3(2 * WC_ * 64), 0, s, \
-                         a, src_bytes, ntn, tap_inner, (int)nt);                                                  \
-    else                                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<true, 128, BN__, 3, NS_, WC_, false, true>), g1, dim3(2 * WC_ * 64), 0, s, \
-                         a, src_bytes, ntn, tap_inner, (int)nt);                                                  \
-  } while (0)
-      const bool w8 = nt <= w8max || (bn == 128 && dg8);
-      if (bn == 32) EWVIT_GLDS_BST(32, 2, 2);
-      else if (bn == 64) {
-        if (nt <= sgmax) EWVIT_GLDS_BST(64, 4, 4);
-        else if (w8) EWVIT_GLDS_BST(64, 2, 4);
-        else EWVIT_GLDS_BST(64, 2, 2);
-      } else {
-        if (nt <= sgmax) EWVIT_GLDS_BST(128, 4, 4);
-        else if (w8) EWVIT_GLDS_BST(128, 2, 4);
-        else EWVIT_GLDS_BST(128, 2, 2);
-      }
-#undef EWVIT_GLDS_BST
-      return true;
-    }
-  }
-  if (bn == 32) {
-    EWVIT_GLDS_FWD(128, 32, 2);
-    return true;
-  }
-  if (vv == 9) {
-    const int64_t mt64 = (a.M + 63) / 64;
-    const int nt9 = (int)(mt64 * ntn);
-    const dim3 grid9((unsigned)nt9);
-    if (bn == 64) {
-      if (a.g.ks == 1)
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
-      else
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 64, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
+  // Blocks: grids of <= 2048 workgroups (the backbone's 7^2 - 28^2 convs) and every dgrad with
+  // 128-wide column tiles (freq_conv's parity-class dgrad 185 -> 162 us, multiscale 834 -> 820)
+  // take 8 waves (64 x BN/4 each) — twice the waves per CU to hide the latency of short K
+  // loops; big grids keep 4 waves (64 x BN/2 each: fewer LDS reads per MFMA).  Grids of <= 256
+  // workgroups (the backbone's long-K 1x1 convs at 7^2 / 14^2: at most one block per CU, so
+  // occupancy hides nothing) take 8 waves with a 4-deep ring (3 K-tiles in flight).
+  const bool w8 = nwg <= 2048 || (DGRAD && bn == 128);
+  const bool sg = nwg <= 256;
+  constexpr bool BST = DGRAD;      // (the statistics epilogue is a separate instantiation)
+  if (DGRAD && a.bwd.part) {
+    // the backward-statistics epilogue: 128-row tiles always (the partial rows
+    // ewvit_conv2d_bwd_bn_rows promised)
+    if (bn == 32) EWVIT_GLDS_FWDW(128, 32, 2, 2, BST);
+    else if (bn == 64) {
+      if (sg) EWVIT_GLDS_FWDW(128, 64, 4, 4, BST);
+      else if (w8) EWVIT_GLDS_FWDW(128, 64, 2, 4, BST);
+      else EWVIT_GLDS_FWDW(128, 64, 2, 2, BST);
     } else {
-      if (a.g.ks == 1)
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 1, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
-      else
-        hipLaunchKernelGGL((conv_glds_kernel<DGRAD, 64, 128, 3, 4, 4>), grid9, dim3(256), 0, s, a, src_bytes, ntn, tap_inner, nt9);
+      if (sg) EWVIT_GLDS_FWDW(128, 128, 4, 4, BST);
+      else if (w8) EWVIT_GLDS_FWDW(128, 128, 2, 4, BST);
+      else EWVIT_GLDS_FWDW(128, 128, 2, 2, BST);
     }
-    return true;
-  }
-  if (bn == 64) {
-    switch (vv) {
-      case 2: EWVIT_GLDS_FWD(128, 64, 3); break;
-      case 3: EWVIT_GLDS_FWD(256, 64, 2); break;
-      case 4: EWVIT_GLDS_FWD(256, 64, 3); break;
-      case 6: EWVIT_GLDS_FWD(128, 64, 4); break;
-      case 7: EWVIT_GLDS_FWDW(128, 64, 2, 4); break;
-      case 8: EWVIT_GLDS_FWDW(128, 64, 4, 4); break;
-      default: EWVIT_GLDS_FWD(128, 64, 2); break;
-    }
+  } else if (bn == 32) EWVIT_GLDS_FWDW(128, 32, 2, 2, false);
+  else if (bn == 64) {
+    if (big) EWVIT_GLDS_FWDW(256, 64, 2, 2, false);
+    else if (sg) EWVIT_GLDS_FWDW(128, 64, 4, 4, false);
+    else if (w8) EWVIT_GLDS_FWDW(128, 64, 2, 4, false);
+    else EWVIT_GLDS_FWDW(128, 64, 2, 2, false);
   } else {
-    switch (vv) {
-      case 2: EWVIT_GLDS_FWD(128, 128, 3); break;
-      case 3: EWVIT_GLDS_FWD(256, 128, 2); break;
-      case 4: EWVIT_GLDS_FWD(256, 128, 3); break;
-      case 6: EWVIT_GLDS_FWD(128, 128, 4); break;
-      case 7: EWVIT_GLDS_FWDW(128, 128, 2, 4); break;
-      case 8: EWVIT_GLDS_FWDW(128, 128, 4, 4); break;
-      default: EWVIT_GLDS_FWD(128, 128, 2); break;
-    }
+    if (sg) EWVIT_GLDS_FWDW(128, 128, 4, 4, false);
+    else if (w8) EWVIT_GLDS_FWDW(128, 128, 2, 4, false);
+    else EWVIT_GLDS_FWDW(128, 128, 2, 2, false);
   }
-#undef EWVIT_GLDS_FWD
 #undef EWVIT_GLDS_FWDW
   return true;
 }
@@ -1855,8 +1591,8 @@ extern "C" int ewvit_set_grid_cap(int max_workgroups);
 extern "C" int ewvit_conv2d_set_grid_cap(int max_workgroups) { return ewvit_set_grid_cap(max_workgroups); }
 
 extern "C" int ewvit_conv2d_set_glds(int variant) {
-  const int prev = glds_variant();
-  g_glds = variant >= 0 && variant <= 15 ? variant : 9;
+  const int prev = g_glds;
+  g_glds = variant ? 1 : 0;
   return prev;
 }
 
@@ -1907,12 +1643,7 @@ static int fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cou
   const int64_t K = (int64_t)ksize * ksize * Cin;
   if (2 * N * H * W * Cin >= (int64_t)OOB || Cout * K * 2 >= (int64_t)OOB || N * Ho * Wo * Cout >= (int64_t)1 << 40)
     return 0;
-  const int v = glds_variant() & 7;
-  if (v == 1) {
-    const int ww = ww_pick(N * Ho * Wo, (int)Cout, Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128);
-    if (ww == 1 || ww == 3) return 256;
-  }
-  return (v == 3 || v == 4) ? 256 : 128;
+  return 128;
 }
 
 extern "C" int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
@@ -1944,11 +1675,7 @@ extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *b
 // input channels per tap the fwd expects its weight pack to have: Cin rounded up to 64
 // when Cin % 64 != 0 (Cin % 16 == 0) and the padded LDS-DMA kernel takes the shape
 static int64_t fwd_pack_cin(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
-  static const int on = [] {
-    const char *e = getenv("EWVIT_CONV_PAD_K");     // 0: never pad (A/B measurement)
-    return e ? atoi(e) : 1;
-  }();
-  if (!on || Cin % 64 == 0 || Cin % 16 || !use_glds()) return Cin;
+  if (Cin % 64 == 0 || Cin % 16 || !use_glds()) return Cin;
   const int64_t Cp = (Cin + 63) / 64 * 64;
   if (4 * Cp > 5 * Cin) return Cin;      // > 25 % zero K (48 -> 64 measured slower): exact-K kernel
   const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
@@ -1987,20 +1714,11 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
   return launch_status("conv2d_fwd");
 }
 
-static int dgrad_parity() {
-  static int v = [] {
-    const char *e = getenv("EWVIT_DGRAD_PARITY");   // 0: stride-2 dgrad masks 3/4 of 9 taps per row
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 // stride-2 3x3 dgrad as 4 launches, one per output parity class (py, px), each over
 // only its live taps (1, 2, 2 and 4 of the 9); false when the LDS-DMA kernel cannot
 // take the class launches (nothing launched)
 static bool dgrad_by_parity(FwdArgs a, int64_t src_bytes, hipStream_t s) {
-  if (!dgrad_parity() || a.g.ks != 3 || a.g.stride != 2 || a.g.pad != 1 || a.ogs != 0 || a.sgs != 0 ||
-      !use_glds() || (glds_variant() & 7) == 0)
+  if (a.g.ks != 3 || a.g.stride != 2 || a.g.pad != 1 || a.ogs != 0 || a.sgs != 0 || !use_glds())
     return false;
   const int H = a.outH, W = a.outW;
   FwdArgs c[4];
@@ -2035,7 +1753,7 @@ static bool dgrad_by_parity(FwdArgs a, int64_t src_bytes, hipStream_t s) {
 // 1 when ewvit_conv2d_bwd_data_add can run this shape (the LDS-DMA dgrad kernel)
 extern "C" int64_t ewvit_conv2d_bwd_data_add_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
                                                int stride) {
-  if (!use_glds() || (Cout % 64 && (!conv_ragged() || Cout % 8 || 5 * ((Cout + 63) / 64 * 64) > 6 * Cout)) ||
+  if (!use_glds() || (Cout % 64 && (Cout % 8 || 5 * ((Cout + 63) / 64 * 64) > 6 * Cout)) ||
       Cin % 8 || 2 * N * H * W * Cout >= (int64_t)OOB ||
       Cin * ksize * ksize * Cout * 2 >= (int64_t)OOB)
     return 0;
@@ -2140,51 +1858,29 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
   return launch_status("conv2d_bwd_data");
 }
 
-// split of the pixel reduction: ~768 workgroups (3 per CU), >= 32 K-tiles per split,
-// and f32 partial slabs no larger than half the bf16 operands they reduce
 // split of the pixel reduction: at most 512 workgroups — the 2 per CU that registers
 // and LDS allow, so every split runs in the first (only) round — >= 4 K-tiles of 64
-// pixels per split, and f32 partial slabs no larger than 4x the bf16 operands
-// Wide n'-tiles (128 x 256 per block, each wave 64 x 128: a quarter fewer LDS and L2
-// bytes per MFMA): EWVIT_CONV_WGW = 0 off, 1 (64 pixels, ring 2; 96 KB LDS, 1 block
-// per CU), 2 (32, 2; 48 KB), 3 (32, 3; 72 KB), taken when n' >= 256 and the last
-// 256-column tile wastes <= 1/8 of n'; 4 (default) = 2 for n' >= 2048 over >= 64K pixels
+// pixels per split, and f32 partial slabs no larger than 4x the bf16 operands.
+// Wide n'-tiles (128 x 256 per block, each wave 64 x 128: a quarter fewer LDS and L2 bytes
+// per MFMA; 32 pixels per K-tile, 2-deep ring, 48 KB) for n' >= 2048 over >= 64K pixels
 // (multiscale_fusion 384 -> 128, 3x3, 64 x 112^2: 951 -> 850 us; measured slower on
-// freq_conv's n' = 1152 and on every backbone 1x1, which keep the 128-column tiles).
-static int g_wgw = -1;
-static int wgw_variant() {
-  if (g_wgw < 0) {
-    const char *e = getenv("EWVIT_CONV_WGW");
-    const int x = e ? atoi(e) : 4;
-    g_wgw = (x < 0 || x > 4) ? 4 : x;
-  }
-  return g_wgw;
-}
+// freq_conv's n' = 1152 and on every backbone 1x1, which keep the 128-column tiles; the
+// 64-pixel / 96 KB form ran 1233 us).  ewvit_conv2d_set_wgrad_wide: 4 auto (default), 2 wide
+// whenever the shape allows it, 0 never (test switches).
+static int g_wgw = 4;
 static int wgrad_wide(const ConvGeom &g) {
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
-  int v = wgw_variant();
+  int v = g_wgw;
   if (v == 4) v = (NP >= 2048 && (int64_t)g.N * g.Ho * g.Wo >= 65536) ? 2 : 0;
   if (!v || NP < 256 || ((NP + 255) / 256 * 256 - NP) * 8 > NP) return 0;
-  return v;
+  return 2;
 }
 static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   const int64_t M = (int64_t)g.N * g.Ho * g.Wo;
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
   const int64_t tn = wide ? 2 * CBN : CBN;
   const int64_t tiles = ((NP + tn - 1) / tn) * ((g.Cout + CBM - 1) / CBM);
-  // target workgroups over splits x tiles (A/B: EWVIT_CONV_WSPLIT, default 512; the 1x1
-  // convs of <= 4096 pixels use EWVIT_CONV_WSPLIT_SMALL when set)
-  static const int target = [] {
-    const char *e = getenv("EWVIT_CONV_WSPLIT");
-    const int v = e ? atoi(e) : 512;
-    return v < 16 ? 16 : v;
-  }();
-  static const int target_small = [] {
-    const char *e = getenv("EWVIT_CONV_WSPLIT_SMALL");
-    return e ? atoi(e) : 0;
-  }();
-  const int tg = (target_small > 0 && g.ks == 1 && M <= 4096) ? target_small : target;
-  int64_t s = (wide == 1 ? tg / 2 : tg) / tiles;
+  int64_t s = 512 / tiles;        // (fewer, longer splits measured slower)
   if (g_grid_cap > 0 && s * tiles > g_grid_cap) s = g_grid_cap / tiles;
   const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;
@@ -2194,35 +1890,9 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   return s;
 }
 
-static int g_wkg = -1;
-static int wgrad_kgroups() {
-  if (g_wkg < 0) {
-    const char *e = getenv("EWVIT_CONV_WKG");
-    g_wkg = e && atoi(e) == 2 ? 2 : 1;
-  }
-  return g_wkg;
-}
-extern "C" int ewvit_conv2d_set_wgrad_kgroups(int kgroups) {
-  const int prev = wgrad_kgroups();
-  g_wkg = kgroups == 2 ? 2 : 1;
-  return prev;
-}
-
-extern "C" int ewvit_conv2d_set_ww(int variant) {
-  const int old = ww_variant();
-  g_ww = variant < 0 || variant > 3 ? 0 : variant;
-  return old;
-}
-
-extern "C" int64_t ewvit_conv2d_set_ww_min(int64_t min_tiles) {
-  const int64_t old = ww_min();
-  g_wwmin = min_tiles < 0 ? 4096 : min_tiles;
-  return old;
-}
-
 extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {
-  const int prev = wgw_variant();
-  g_wgw = variant >= 0 && variant <= 4 ? variant : 4;
+  const int prev = g_wgw;
+  g_wgw = variant == 0 || variant == 2 ? variant : 4;
   return prev;
 }
 
@@ -2255,20 +1925,13 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
   const int wide = glds ? wgrad_wide(g) : 0;
-  // two K-groups per workgroup (conv_wgrad_glds_kernel KG = 2) for the default 128-column
-  // family on an uncapped grid: half the splits (and fp32 slabs) at the same wave count.
-  // Measured slower (SFE piece 14.27-14.29 -> 14.45-14.47 ms, tools/piece_ab.sh): the two
-  // groups' lockstep barriers at one workgroup per CU cost more than the halved slabs save —
-  // off unless EWVIT_CONV_WKG = 2 (A/B)
-  const int kgrp = (glds && !wide && (glds_variant() & 7) == 1 && g_grid_cap == 0 && wgrad_kgroups() == 2) ? 2 : 1;
-  const int64_t splits = (wgrad_splits(g, wide) + kgrp - 1) / kgrp;
+  const int64_t splits = wgrad_splits(g, wide);
   a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;
   const int tnw = wide ? 2 * CBN : CBN;
   const int ntx = (taps * g.Cin + tnw - 1) / tnw, nty = (g.Cout + CBM - 1) / CBM;
-  const int gv = glds_variant() & 7;
-  const int64_t kq = !glds ? CBK : wide ? (wide == 1 ? 64 : 32) : ((gv == 3 || gv == 4) ? 32 : 64);  // K-tile depth (pixels)
+  const int64_t kq = !glds ? CBK : wide ? 32 : 64;  // K-tile depth (pixels)
   int64_t mper = (a.M + splits - 1) / splits;
-  mper = (mper + kq * kgrp - 1) / (kq * kgrp) * (kq * kgrp);
+  mper = (mper + kq - 1) / kq * kq;
   a.mper = mper;
   const int sp = (int)((a.M + mper - 1) / mper);
   // the glds kernel leaves bias partials per (split, n'-tile); the old one per split
@@ -2285,34 +1948,13 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   hipStream_t s = as_stream(stream);
   if (glds) {
     const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
-    // small grids (<= EWVIT_CONV_WSGMAX blocks, at most one per CU): EWVIT_CONV_WSG picks a
-    // deeper-ring family for them (2: 64 pixels, ring 3; 4: 32 pixels, ring 4; 0 keep)
-    static const int wsg = [] {
-      const char *e = getenv("EWVIT_CONV_WSG");
-      return e ? atoi(e) : 0;
-    }();
-    static const int wsgmax = [] {
-      const char *e = getenv("EWVIT_CONV_WSGMAX");
-      return e ? atoi(e) : 256;
-    }();
-    const int gvs = (!wide && gv == 1 && (wsg == 2 || wsg == 4) && (int64_t)nwg <= wsgmax) ? wsg : gv;
 #define EWVIT_GLDS_WG(BK_, NS_, WJ_)                                                                        \
   do {                                                                                                    \
     if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
     else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
   } while (0)
-    if (kgrp == 2) {
-      if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, 64, 2, 4, 2>), dim3(nwg), dim3(512), 0, s, a, xb, ntx, nty);
-      else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, 64, 2, 4, 2>), dim3(nwg), dim3(512), 0, s, a, xb, ntx, nty);
-    } else if (wide == 1) EWVIT_GLDS_WG(64, 2, 8);
-    else if (wide == 2) EWVIT_GLDS_WG(32, 2, 8);
-    else if (wide == 3) EWVIT_GLDS_WG(32, 3, 8);
-    else switch (gvs) {
-      case 2: EWVIT_GLDS_WG(64, 3, 4); break;
-      case 3: EWVIT_GLDS_WG(32, 3, 4); break;
-      case 4: EWVIT_GLDS_WG(32, 4, 4); break;
-      default: EWVIT_GLDS_WG(64, 2, 4); break;
-    }
+    if (wide) EWVIT_GLDS_WG(32, 2, 8);
+    else EWVIT_GLDS_WG(64, 2, 4);
 #undef EWVIT_GLDS_WG
   } else {
     dim3 grid((unsigned)ntx, (unsigned)nty, (unsigned)sp);

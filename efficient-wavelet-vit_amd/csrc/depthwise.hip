@@ -377,147 +377,6 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
   }
 }
 
-// ---- per-pixel form of dw_row_bn_kernel (the backbone's 7^2 / 14^2 maps).  The row kernel
-// walks a row's columns one after another, each waiting on the loads of its new window
-// column; here a thread owns DW_PPT output pixels of 8 channels and issues all 9 tap loads of
-// a pixel at once (the taps' re-reads by the neighbouring threads hit L1/L2), so a pixel costs
-// one load round.  The block's 64 channels' weights are staged in LDS once ([ch][tap], the
-// rotated kernel for ROT) and read back as 18 ds_read_b128 per thread; block = 8 channel
-// vectors x 32 pixel slots, DW_PPT pixels per slot.  Sums: as dw_row_bn_kernel (ST 0: none),
-// one partial row per block of 32 * DW_PPT consecutive output pixels, the slots added in order.
-// Same multiply-add order per output as the row kernel (kw outer, kh inner): same bits.
-constexpr int DW_PPT = 2;
-template <int STRIDE, bool ROT, int ST>
-__global__ __launch_bounds__(256) void dw_pix_kernel(const bf16_t *__restrict__ x, const float *__restrict__ w,
-                                                     bf16_t *__restrict__ y, DwShape s, DwBnFwd f, BnBwdStats b) {
-  __shared__ __attribute__((aligned(16))) float wl[64 * 9];
-  __shared__ float red[ST ? 32 * 8 * 16 : 4];
-  const int tid = threadIdx.x, cv = tid & 7, ps = tid >> 3;
-  const int C8 = s.C >> 3;
-  const int cb = blockIdx.y * 64;
-  const int nch = s.C - cb < 64 ? s.C - cb : 64;
-  for (int i = tid; i < nch * 9; i += 256) {
-    const int ch = i / 9, k = i - ch * 9;
-    wl[ch * 9 + (ROT ? 8 - k : k)] = w[(int64_t)(cb + ch) * 9 + k];
-  }
-  __syncthreads();
-  const int c8 = blockIdx.y * 8 + cv;
-  const int c = c8 * 8;
-  const int64_t npix = (int64_t)s.N * s.Ho * s.Wo;
-  float sa[8], sb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
-  if (c8 < C8) {
-    float wr[9][8];
-    {
-      const float4 *wq = reinterpret_cast<const float4 *>(wl + cv * 72);
-      float t[72];
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        const float4 q = wq[i];
-        t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int k = 0; k < 9; ++k) wr[k][j] = t[j * 9 + k];
-    }
-    float p0[8], p1[8], p2[8], p3[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      p0[j] = p1[j] = p2[j] = p3[j] = 0.f;
-      if (ST == 1) {
-        p0[j] = f.shift ? f.shift[c + j] : 0.f;
-      } else if (ST == 2) {
-        p0[j] = b.mean[c + j]; p1[j] = b.invstd[c + j];
-        p2[j] = b.gamma ? b.gamma[c + j] : 1.f; p3[j] = b.beta ? b.beta[c + j] : 0.f;
-      }
-    }
-    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int q = 0; q < DW_PPT; ++q) {
-      const int64_t pix = (int64_t)blockIdx.x * (32 * DW_PPT) + q * 32 + ps;
-      if (pix >= npix) break;
-      const int wo = (int)(pix % s.Wo);
-      const int64_t t = pix / s.Wo;
-      const int ho = (int)(t % s.Ho);
-      const int n = (int)(t / s.Ho);
-      uint4 win[3][3];     // [kw][kh]
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int hi = ho * STRIDE - s.pad + kh;
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int wi = wo * STRIDE - s.pad + kw;
-          win[kw][kh] = (hi >= 0 && hi < s.H && wi >= 0 && wi < s.W)
-                            ? *reinterpret_cast<const uint4 *>(x + (((int64_t)n * s.H + hi) * s.W + wi) * s.C + c)
-                            : zero;
-        }
-      }
-      uint4 bxq = zero;
-      if (ST == 2) bxq = *reinterpret_cast<const uint4 *>(b.x + pix * s.C + c);
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-          float v[8];
-          bf8_unpack(win[kw][kh], v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[j]);
-        }
-      unsigned o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (unsigned)f2bf(acc[2 * j]) | ((unsigned)f2bf(acc[2 * j + 1]) << 16);
-      const uint4 oq = make_uint4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<uint4 *>(y + pix * s.C + c) = oq;
-      if (ST) {
-        float v[8];
-        bf8_unpack(oq, v);
-        if (ST == 1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = v[j] - p0[j];
-            sa[j] += d;
-            sb[j] = fmaf(d, d, sb[j]);
-          }
-        } else {
-          float xv[8];
-          bf8_unpack(bxq, xv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xh = (xv[j] - p0[j]) * p1[j];
-            const float g = b.act ? v[j] * bn_act_grad(b.act, fmaf(xh, p2[j], p3[j])) : v[j];
-            sa[j] += g;
-            sb[j] = fmaf(g, xh, sb[j]);
-          }
-        }
-      }
-    }
-  }
-  if constexpr (ST != 0) {
-    float *q = red + (ps * 8 + cv) * 16;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { q[j] = sa[j]; q[8 + j] = sb[j]; }
-    __syncthreads();
-    if (tid < 64) {
-      const int v = tid >> 3, j = tid & 7;
-      const int cc = (blockIdx.y * 8 + v) * 8 + j;
-      float A = 0.f, B = 0.f;
-      for (int rr = 0; rr < 32; ++rr) {
-        A += red[(rr * 8 + v) * 16 + j];
-        B += red[(rr * 8 + v) * 16 + 8 + j];
-      }
-      if (cc < s.C) {
-        float *pr = (ST == 1 ? f.part : b.part) + (int64_t)blockIdx.x * 2 * s.C;
-        pr[cc] = A;
-        pr[s.C + cc] = B;
-        if (ST == 1 && blockIdx.x == 0 && f.shift_out) f.shift_out[cc] = f.shift ? f.shift[cc] : 0.f;
-      }
-    }
-  }
-}
-
 // ---- bf16 input gradient of a STRIDE-2 pad-1 conv, row form (the first block of stages 4
 // and 6).  dx[hi][wi] only meets the taps with kh = hi+1 (mod 2), kw = wi+1 (mod 2): an even
 // dx row one dy row (kh = 1), an odd one two (kh = 0, 2); likewise along the row, so a thread
@@ -802,82 +661,19 @@ static DwShape mk(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int pa
   return s;
 }
 
-// column segments per output row for the row kernels (EWVIT_DW_SEGS = the most segments):
-// the backbone's 7^2 / 14^2 maps give only ~448 blocks of whole rows, but splitting each row
-// in 2 (<= 2048 blocks, one more 3x3 window fill per row) measured slower in the step
-// (2682 vs 2703 frames/s), so the default is 1 — whole rows
-static int g_dw_maxsegs = -1;      // -1: not read from EWVIT_DW_SEGS yet
-static int dw_max_segs() {
-  if (g_dw_maxsegs < 0) {
-    const char *e = getenv("EWVIT_DW_SEGS");
-    const int v = e ? atoi(e) : 1;
-    g_dw_maxsegs = v < 1 ? 1 : (v > 8 ? 8 : v);
-  }
-  return g_dw_maxsegs;
-}
-// A/B knob: stride-2 input gradients on the row kernel (1) or the generic per-pixel one (0)
-static int g_dw_s2_rows = [] {
-  const char *e = getenv("EWVIT_DW_S2_ROWS");
-  return e ? atoi(e) : 1;
-}();
-
-static int dw_segs(const DwShape &s, int rpb) {
-  const int maxs = dw_max_segs();
-  const int64_t nb = ((int64_t)s.N * s.Ho + rpb - 1) / rpb;
-  int segs = 1;
-  while (segs * 2 <= maxs && nb * segs * 2 <= 2048 && s.Wo / (segs * 2) >= 3) segs *= 2;
-  return segs;
-}
-
-// A/B and test knob: the most column segments per row (1 = whole rows, the default; <= 8)
-extern "C" int ewvit_dwconv3x3_set_segs(int max_segs) {
-  EWVIT_CHECK_ARG(max_segs >= 1 && max_segs <= 8, "dwconv3x3_set_segs: %d (1..8)", max_segs);
-  g_dw_maxsegs = max_segs;
-  return 0;
-}
-
-// the per-pixel kernels (dw_pix_kernel) for maps of at most this many pixels per frame
-// (EWVIT_DW_PIX).  Measured slower than the row kernels on the 7^2 / 14^2 maps (SFE piece
-// 14.29-14.32 -> 15.09-15.12 ms, tools/piece_ab.sh: the 9 tap loads per pixel re-read each
-// input vector 9 times through L1/L2 where the row kernel's window re-reads it 3 times), so the
-// default is 0 — row kernels everywhere; kept as an A/B knob
-static int64_t g_dw_pix = -1;
-static int64_t dw_pix_max() {
-  if (g_dw_pix < 0) {
-    const char *e = getenv("EWVIT_DW_PIX");
-    g_dw_pix = e ? (int64_t)atoll(e) : (int64_t)0;
-    if (g_dw_pix < 0) g_dw_pix = 0;
-  }
-  return g_dw_pix;
-}
-// A/B and test knob: the per-pixel kernels for output maps of at most max_pixels per frame
-// (0: row kernels everywhere); returns the previous setting
-extern "C" int64_t ewvit_dwconv3x3_set_pix(int64_t max_pixels) {
-  const int64_t prev = dw_pix_max();
-  g_dw_pix = max_pixels < 0 ? 0 : max_pixels;
-  return prev;
-}
-static bool dw_pix(int64_t Ho, int64_t Wo) { return Ho * Wo <= dw_pix_max(); }
-
+// The row kernels walk whole output rows (segs = 1).  Measured and removed: column segments
+// per row for the 7^2 / 14^2 maps (2682 vs 2703 frames/s: one more 3x3 window fill per
+// segment) and a per-pixel kernel for them (SFE piece 14.29-14.32 -> 15.09-15.12 ms: the 9 tap
+// loads of a pixel re-read each input vector 9 times through L1/L2 where the row kernel's
+// window re-reads it 3 times).
 extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64_t N, int64_t H, int64_t W,
                                    int64_t C, int stride, int pad, int dtype, void *stream) {
   EWVIT_CHECK_ARG(x && w && y && dtype_ok(dtype), "dwconv3x3_fwd: bad args");
   DwShape s = mk(N, H, W, C, stride, pad);
   if (int rc = check_shape(s, "dwconv3x3_fwd")) return rc;
-  if (dtype == EWVIT_BF16 && (s.stride == 1 || s.stride == 2) && dw_pix(s.Ho, s.Wo)) {
-    const dim3 grid((unsigned)(((int64_t)s.N * s.Ho * s.Wo + 32 * DW_PPT - 1) / (32 * DW_PPT)), (unsigned)((C / 8 + 7) / 8));
-    DwBnFwd f;
-    BnBwdStats b;
-    if (s.stride == 1)
-      hipLaunchKernelGGL((dw_pix_kernel<1, false, 0>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                         (bf16_t *)y, s, f, b);
-    else
-      hipLaunchKernelGGL((dw_pix_kernel<2, false, 0>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                         (bf16_t *)y, s, f, b);
-  } else if (dtype == EWVIT_BF16 && s.C / 8 <= 256 && (s.stride == 1 || s.stride == 2)) {
-    const int rpb = 256 / (s.C / 8);
-    const int segs = dw_segs(s, rpb);
-    dim3 grid((unsigned)(((int64_t)s.N * s.Ho * segs + rpb - 1) / rpb));
+  if (dtype == EWVIT_BF16 && s.C / 8 <= 256 && (s.stride == 1 || s.stride == 2)) {
+    const int rpb = 256 / (s.C / 8), segs = 1;
+    dim3 grid((unsigned)(((int64_t)s.N * s.Ho + rpb - 1) / rpb));
     if (s.stride == 1)
       hipLaunchKernelGGL((dw_row_bf16_kernel<1, false>), grid, dim3(256), 0, as_stream(stream),
                          (const bf16_t *)x, w, (bf16_t *)y, s, rpb, segs);
@@ -900,33 +696,19 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
   EWVIT_CHECK_ARG(dy && w && dx && dtype_ok(dtype), "dwconv3x3_bwd_data: bad args");
   DwShape s = mk(N, H, W, C, stride, pad);
   if (int rc = check_shape(s, "dwconv3x3_bwd_data")) return rc;
-  if (dtype == EWVIT_BF16 && s.stride == 1 && s.pad == 1 && dw_pix(s.H, s.W)) {
+  if (dtype == EWVIT_BF16 && s.stride == 1 && s.pad == 1 && s.C / 8 <= 256) {
     // input gradient of a stride-1 pad-1 conv = stride-1 pad-1 conv of dy with the rotated kernel
     DwShape t = s;
     t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
-    const dim3 grid((unsigned)(((int64_t)t.N * t.Ho * t.Wo + 32 * DW_PPT - 1) / (32 * DW_PPT)), (unsigned)((C / 8 + 7) / 8));
-    DwBnFwd f;
-    BnBwdStats b;
-    hipLaunchKernelGGL((dw_pix_kernel<1, true, 0>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
-                       (bf16_t *)dx, t, f, b);
-  } else if (dtype == EWVIT_BF16 && s.stride == 1 && s.pad == 1 && s.C / 8 <= 256) {
-    // input gradient of a stride-1 pad-1 conv = stride-1 pad-1 conv of dy with the rotated kernel
-    DwShape t = s;
-    t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
-    const int rpb = 256 / (s.C / 8);
-    const int segs = dw_segs(t, rpb);
-    dim3 grid((unsigned)(((int64_t)t.N * t.Ho * segs + rpb - 1) / rpb));
+    const int rpb = 256 / (s.C / 8), segs = 1;
+    dim3 grid((unsigned)(((int64_t)t.N * t.Ho + rpb - 1) / rpb));
     hipLaunchKernelGGL((dw_row_bf16_kernel<1, true>), grid, dim3(256), 0, as_stream(stream),
                        (const bf16_t *)dy, w, (bf16_t *)dx, t, rpb, segs);
   } else if (dtype == EWVIT_BF16 && s.stride == 2 && s.pad == 1 && s.C / 8 <= 256 && s.Ho == (s.H + 1) / 2 &&
-             s.Wo == (s.W + 1) / 2 && g_dw_s2_rows) {
-    // stride 2: dx rows in column pairs (dw_row_s2_bwd_kernel); column segments while the
-    // grid is small, as for the forward rows
-    DwShape t = s;
-    t.Ho = s.H; t.Wo = (s.W + 1) / 2;        // rows = dx rows, "columns" = column pairs
-    const int rpb = 256 / (s.C / 8);
-    const int segs = dw_segs(t, rpb);
-    dim3 grid((unsigned)(((int64_t)s.N * s.H * segs + rpb - 1) / rpb));
+             s.Wo == (s.W + 1) / 2) {
+    // stride 2: dx rows in column pairs (dw_row_s2_bwd_kernel)
+    const int rpb = 256 / (s.C / 8), segs = 1;
+    dim3 grid((unsigned)(((int64_t)s.N * s.H + rpb - 1) / rpb));
     hipLaunchKernelGGL(dw_row_s2_bwd_kernel, grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
                        (bf16_t *)dx, s, rpb, segs);
   } else {
@@ -948,8 +730,7 @@ extern "C" int64_t ewvit_dwconv3x3_bn_rows(int64_t N, int64_t H, int64_t W, int6
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || C > 65536 * 8 || (stride != 1 && stride != 2) ||
       (bwd && stride != 1))
     return 0;
-  const int64_t Ho = bwd ? H : (H - 1) / stride + 1, Wo = bwd ? W : (W - 1) / stride + 1;
-  if (dw_pix(Ho, Wo)) return (N * Ho * Wo + 32 * DW_PPT - 1) / (32 * DW_PPT);
+  const int64_t Ho = bwd ? H : (H - 1) / stride + 1;
   return (N * Ho + 31) / 32;
 }
 
@@ -967,18 +748,12 @@ extern "C" int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, in
   f.part = part; f.shift = shift; f.shift_out = shift_out;
   BnBwdStats b;
   dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
-  const bool pix = dw_pix(s.Ho, s.Wo);
-  if (stride == 1) {
-    if (pix) hipLaunchKernelGGL((dw_pix_kernel<1, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                                (bf16_t *)y, s, f, b);
-    else hipLaunchKernelGGL((dw_row_bn_kernel<1, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                            (bf16_t *)y, s, f, b);
-  } else {
-    if (pix) hipLaunchKernelGGL((dw_pix_kernel<2, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                                (bf16_t *)y, s, f, b);
-    else hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                            (bf16_t *)y, s, f, b);
-  }
+  if (stride == 1)
+    hipLaunchKernelGGL((dw_row_bn_kernel<1, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
+                       (bf16_t *)y, s, f, b);
+  else
+    hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
+                       (bf16_t *)y, s, f, b);
   return launch_status("dwconv3x3_fwd_bn");
 }
 
@@ -1003,11 +778,7 @@ extern "C" int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void 
   b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
   b.act = act;
   dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
-  if (dw_pix(t.Ho, t.Wo))
-    hipLaunchKernelGGL((dw_pix_kernel<1, true, 2>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
-                       (bf16_t *)dx, t, f, b);
-  else
-    hipLaunchKernelGGL((dw_row_bn_kernel<1, true, 2>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
+  hipLaunchKernelGGL((dw_row_bn_kernel<1, true, 2>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
                        (bf16_t *)dx, t, f, b);
   return launch_status("dwconv3x3_bwd_data_bn");
 }

@@ -499,38 +499,14 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
                   "dwt_hf_upsample_fused: unsupported shape [%lld,%lld,%lld,%lld] levels=%d channels=%lld",
                   (long long)N, (long long)C, (long long)H, (long long)W, levels, (long long)out_channels);
   const int OH = (int)(H / 2);
-  // threads per workgroup / level-1 rows per workgroup (EWVIT_DWTF_THREADS, EWVIT_DWTF_ROWS A/B):
-  // 512 threads over 16-row strips (29.9 -> 26.5 us at config 2 against 256 threads; 1024: 29.7)
-  static const int nt = [] {
-    const char *e = getenv("EWVIT_DWTF_THREADS");
-    const int v = e ? atoi(e) : 512;
-    return v == 256 || v == 1024 ? v : 512;
-  }();
-  static const int rows = [] {
-    const char *e = getenv("EWVIT_DWTF_ROWS");
-    const int v = e ? atoi(e) : 16;
-    return v == 8 || v == 32 ? v : 16;
-  }();
+  // 512 threads over 16-row strips (29.9 -> 26.5 us at config 2 against 256 threads; 1024: 29.7;
+  // 8-row strips 31-33 us, 32-row strips on 1024 threads 26.3 us: profiles/r02/ab/dwtf_rows.log)
+  constexpr int nt = 512, rows = 16;
   dim3 grid((unsigned)((OH + rows - 1) / rows), (unsigned)N), block(nt);
   hipStream_t s = as_stream(stream);
-#define DWTF_R(XD, OD, LV, NT_)                                                                                 \
-  do {                                                                                                        \
-    if (rows == 8)                                                                                            \
-      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 8>), grid, block, 0, s, x, out, (int)N, (int)H, \
-                         (int)W, (int)out_channels);                                                          \
-    else if (rows == 32)                                                                                      \
-      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 32>), grid, block, 0, s, x, out, (int)N,     \
-                         (int)H, (int)W, (int)out_channels);                                                  \
-    else                                                                                                      \
-      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, NT_, 16>), grid, block, 0, s, x, out, (int)N,     \
-                         (int)H, (int)W, (int)out_channels);                                                  \
-  } while (0)
-#define DWTF_L(XD, OD, LV)                \
-  do {                                    \
-    if (nt == 1024) DWTF_R(XD, OD, LV, 1024); \
-    else if (nt == 256) DWTF_R(XD, OD, LV, 256); \
-    else DWTF_R(XD, OD, LV, 512);         \
-  } while (0)
+#define DWTF_L(XD, OD, LV)                                                                                    \
+  hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, nt, rows>), grid, block, 0, s, x, out, (int)N, (int)H, \
+                     (int)W, (int)out_channels)
 #define DWTF_D(XD, OD)                        \
   do {                                        \
     if (levels == 1) DWTF_L(XD, OD, 1);       \
@@ -543,6 +519,5 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
   else DWTF_D(EWVIT_BF16, EWVIT_F32);
 #undef DWTF_D
 #undef DWTF_L
-#undef DWTF_R
   return launch_status("dwt_hf_upsample_fused");
 }

@@ -280,15 +280,8 @@ static int fr_band_rows(int h, int nh, int oy, int S, int rb) {
   return worst;
 }
 
-// dynamic LDS budget per workgroup (EWVIT_FRAMES_LDS, KB)
-static int fr_lds_max() {
-  static const int v = [] {
-    const char *e = getenv("EWVIT_FRAMES_LDS");
-    const int kb = e ? atoi(e) : 64;
-    return (kb < 16 ? 16 : kb > 160 ? 160 : kb) * 1024;
-  }();
-  return v;
-}
+// dynamic LDS budget per workgroup
+static int fr_lds_max() { return 64 * 1024; }
 
 static FrNorm fr_norm(const float *mean_std) {
   FrNorm nm;
@@ -339,14 +332,10 @@ extern "C" int ewvit_frames_plan(const int64_t *geom, int64_t n, int S, int64_t 
     return r;
   };
   // staged source rows at the tallest band that fits, else bands read the source from global
-  // the tallest band (<= EWVIT_FRAMES_RB, default 4) whose LDS fits: 64-frame 720p clip with face
-  // boxes, 2 / 4 / 8 / 16-row bands 38.5 / 31.7 / 32.6 / 44.4 us (tools/frames_lds_ab.sh: the
-  // column-per-thread horizontal pass walks the band's source rows serially)
-  static const int rbmax = [] {
-    const char *e = getenv("EWVIT_FRAMES_RB");
-    const int v = e ? atoi(e) : 4;
-    return v >= 1 && v <= 16 ? v : 4;
-  }();
+  // the tallest band (<= 4 rows) whose LDS fits: 64-frame 720p clip with face boxes, 2 / 4 / 8 /
+  // 16-row bands 38.5 / 31.7 / 32.6 / 44.4 us (tools/frames_lds_ab.sh: the column-per-thread
+  // horizontal pass walks the band's source rows serially)
+  constexpr int rbmax = 4;
   for (int staged = 1; staged >= 0; --staged)
     for (int rb = rbmax; rb >= 1; rb >>= 1) {
       const FrPlan pl{rb, kmax, rmax_of(rb), staged ? words : 0};

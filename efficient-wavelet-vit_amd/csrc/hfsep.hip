@@ -357,20 +357,9 @@ static int hs_blocks(int64_t work, int cap_default) {
 }
 
 static int hs_fwd_th() { return 8; }
-static int hs_wg_th() {
-  static const int th = [] {
-    const char *e = getenv("EWVIT_HFSEP_WG_TH");
-    const int v = e ? atoi(e) : 2;
-    return v == 1 ? 1 : 2;
-  }();
-  return th;
-}
+static int hs_wg_th() { return 2; }        // rows per band (1-row bands measured slower)
 static int hs_wg_blocks(int64_t NI, int64_t H) {
-  static const int maxb = [] {
-    const char *e = getenv("EWVIT_HFSEP_WG_BLOCKS");
-    const int v = e ? atoi(e) : 768;          // 3 resident per CU
-    return v > 0 && v <= 4096 ? v : 768;
-  }();
+  constexpr int maxb = 768;                     // 3 resident per CU
   const int th = hs_wg_th();
   return hs_blocks(NI * ((H + th - 1) / th), maxb);
 }
@@ -391,11 +380,7 @@ extern "C" int64_t ewvit_hfsep_fwd_parts(int64_t L, int64_t N, int64_t H, int64_
   // from them directly); all levels together one round of resident workgroups (2 per CU at
   // this kernel's register use), so no level's tail waits for a second round; under a grid
   // cap the levels share it
-  static const int fwdb = [] {
-    const char *e = getenv("EWVIT_HFSEP_FWD_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v > 0 && v <= 4096 ? v : 512;
-  }();
+  constexpr int fwdb = 512;
   int64_t g = fwdb / L > 0 ? fwdb / L : 1;
   if (g > 256) g = 256;
   if (g > bands) g = bands;
@@ -449,11 +434,7 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
     hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,           \
                        (const bf16_t *)dy, workspace, (int)NI, (int)H, (int)W);                                  \
   } while (0)
-  if (th == 1) {
-    if (small) EWVIT_HS_WG(1, 7, 4); else EWVIT_HS_WG(1, 13, 7);
-  } else {
-    if (small) EWVIT_HS_WG(2, 7, 4); else EWVIT_HS_WG(2, 13, 7);
-  }
+  if (small) EWVIT_HS_WG(2, 7, 4); else EWVIT_HS_WG(2, 13, 7);
 #undef EWVIT_HS_WG
   int rc = launch_status("hfsep_bwd_weight");
   if (rc) return rc;

@@ -417,17 +417,10 @@ __global__ __launch_bounds__(256) void se_mlp_dh_part_kernel(const float *__rest
   }
 }
 
-// bnsum given (ewvit_se_squeeze_mlp_bwd_bn): also the BatchNorm-before-the-SE's backward partial
-// row of frame n, bnpart[n] = (sum g_bn, sum g_bn * xhat) with g_bn = (dy * s + g) * act'(z) over
-// the frame's rows — s and g are constant over a frame, so it is s * A1 + g * A2 and s * A3 +
-// g * A4 from the frame sums se_sq_dh_part_bn_kernel left (bnsum [4][N][C])
 __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__ part, int nb,
                                                        const float *__restrict__ h1,
                                                        const float *__restrict__ w1, int C, int Csq, float inv_hw,
-                                                       float *__restrict__ dz1_out, float *__restrict__ g_out,
-                                                       const float *__restrict__ s = nullptr,
-                                                       const float *__restrict__ bnsum = nullptr, int N = 0,
-                                                       float *__restrict__ bnpart = nullptr) {
+                                                       float *__restrict__ dz1_out, float *__restrict__ g_out) {
   extern __shared__ float dz1[];
   const int n = blockIdx.x, tid = threadIdx.x;
   const float *pp = part + (int64_t)n * nb * Csq;
@@ -455,12 +448,6 @@ __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__
   }
   const float gq = (acc0 + acc1) * inv_hw;
   g_out[(int64_t)n * C + c] = gq;
-  if (bnsum) {
-    const int64_t NC = (int64_t)N * C, i = (int64_t)n * C + c;
-    const float sv = s[i];
-    bnpart[(int64_t)n * 2 * C + c] = fmaf(sv, bnsum[i], gq * bnsum[NC + i]);
-    bnpart[(int64_t)n * 2 * C + C + c] = fmaf(sv, bnsum[2 * NC + i], gq * bnsum[3 * NC + i]);
-  }
 }
 
 // dW2[c][j] = sum_n dz2[n][c] silu(h1[n][j]),  db2[c] = sum_n dz2[n][c]
@@ -607,128 +594,6 @@ __global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restri
   }
   // part[j] = sum_c w2[c][j] * d[c] over the chunk's channels: w2 is [C][Csq], so lanes run
   // over j (coalesced rows of w2) and the 4 waves over interleaved channels, d from LDS
-  __shared__ float dsh[SE_CB];
-  __shared__ float red[4][64];
-  if (w == 0) dsh[lane] = d;
-  __syncthreads();
-  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
-  const int c0 = cb * SE_CB;
-  const int nc = C - c0 < SE_CB ? C - c0 : SE_CB;
-  for (int j0 = 0; j0 < Csq; j0 += 64) {
-    const int j = j0 + lane;
-    float acc = 0.f;
-    if (j < Csq) {
-      const float *wr = w2 + (int64_t)c0 * Csq + j;
-      for (int k = w; k < nc; k += 4) acc = fmaf(wr[(int64_t)k * Csq], dsh[k], acc);
-    }
-    red[w][lane] = acc;
-    __syncthreads();
-    if (w == 0 && j < Csq) pp[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-    __syncthreads();
-  }
-}
-
-// se_sq_dh_part_kernel for the SE after a BatchNorm(+act) (BnActSEFn): besides ds = sum_hw dy * a
-// (a: the SE input, bit-identical to se_chunk_squeeze<DT, 1> — same loads, same fma order, same
-// tree), the frame sums of the BatchNorm backward's terms, per channel over the frame's rows:
-//   A1 = sum dy act'(z),  A2 = sum act'(z),  A3 = sum dy act'(z) xhat,  A4 = sum act'(z) xhat
-// (xb: the BatchNorm input, xhat = (xb - mean) invstd, z = xhat gamma + beta) — the terms
-// bn_bwd_reduce_kernel<., ., 2> would sum from dy * s + g, which se_mlp_g_kernel forms from them
-// once g is known, so that pass (and its reads of dy and xb) goes away
-template <int DT, int ACT>
-__global__ __launch_bounds__(256) void se_sq_dh_part_bn_kernel(const void *__restrict__ dy, const void *__restrict__ a,
-                                                               const void *__restrict__ xb, int HW,
-                                                               const float *__restrict__ s,
-                                                               const float *__restrict__ w2, int C, int Csq,
-                                                               const float *__restrict__ mean,
-                                                               const float *__restrict__ invstd,
-                                                               const float *__restrict__ gamma,
-                                                               const float *__restrict__ beta, int N,
-                                                               float *__restrict__ dz2_out, float *__restrict__ part,
-                                                               float *__restrict__ bnsum) {
-  __shared__ float sm[5 * 8 * 256];
-  const int n = blockIdx.x, cb = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tid = threadIdx.x, cv = tid & 7, rg = tid >> 3;
-  {
-    const int cc = cb * SE_CB + cv * 8;
-    float acc[8], A[4][8], mu[8], iv[8], ga[8], be[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      acc[j] = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) A[q][j] = 0.f;
-      const int ch = cc < C ? cc + j : 0;
-      mu[j] = mean[ch]; iv[j] = invstd[ch];
-      ga[j] = gamma ? gamma[ch] : 1.f; be[j] = beta ? beta[ch] : 0.f;
-    }
-    auto bnacc = [&](const float (&vd)[8], const float (&vx)[8]) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (vx[j] - mu[j]) * iv[j];
-        const float ag = bn_act_grad(ACT, fmaf(xh, ga[j], be[j]));
-        const float dg = vd[j] * ag;
-        A[0][j] += dg;
-        A[1][j] += ag;
-        A[2][j] = fmaf(dg, xh, A[2][j]);
-        A[3][j] = fmaf(ag, xh, A[3][j]);
-      }
-    };
-    if (cc < C) {
-      const int64_t base = (int64_t)n * HW * C + cc;
-      int h = rg;
-      // two rows' loads in flight (the register budget of the extra sums; the rows are still
-      // added in the order rg, rg + 32, ... so ds rounds as se_chunk_squeeze's)
-      for (; h + 32 < HW; h += 64) {
-        float va[2][8], vb[2][8], vx[2][8];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          se_ld8<DT>(dy, base + (int64_t)(h + 32 * q) * C, va[q]);
-          se_ld8<DT>(a, base + (int64_t)(h + 32 * q) * C, vb[q]);
-          se_ld8<DT>(xb, base + (int64_t)(h + 32 * q) * C, vx[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = fmaf(va[q][j], vb[q][j], acc[j]);
-          bnacc(va[q], vx[q]);
-        }
-      }
-      for (; h < HW; h += 32) {
-        float va[8], vb[8], vx[8];
-        se_ld8<DT>(dy, base + (int64_t)h * C, va);
-        se_ld8<DT>(a, base + (int64_t)h * C, vb);
-        se_ld8<DT>(xb, base + (int64_t)h * C, vx);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = fmaf(va[j], vb[j], acc[j]);
-        bnacc(va, vx);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sm[j * 256 + tid] = acc[j];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sm[(q + 1) * 2048 + j * 256 + tid] = A[q][j];
-    }
-  }
-  __syncthreads();
-  for (int st = 16; st >= 1; st >>= 1) {
-    if (rg < st)
-#pragma unroll
-      for (int j = 0; j < 40; ++j) sm[j * 256 + tid] += sm[j * 256 + tid + st * 8];
-    __syncthreads();
-  }
-  // lane l of every wave: channel cb*64 + l = vector l>>3, element l&7
-  const int c = cb * SE_CB + lane;
-  const float dsv = sm[(lane & 7) * 256 + (lane >> 3)];
-  float d = 0.f;
-  if (c < C) {
-    const float sv = s[(int64_t)n * C + c];
-    d = dsv * sv * (1.f - sv);
-    if (w == 0) dz2_out[(int64_t)n * C + c] = d;
-    // wave q writes the frame sum A(q+1)
-    const int q = w;
-    bnsum[((int64_t)q * N + n) * C + c] = sm[(q + 1) * 2048 + (lane & 7) * 256 + (lane >> 3)];
-  }
   __shared__ float dsh[SE_CB];
   __shared__ float red[4][64];
   if (w == 0) dsh[lane] = d;
@@ -950,48 +815,6 @@ extern "C" int ewvit_se_gate_excite(const float *part, const float *b1, const fl
     hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_F32>, g2, dim3(256), lds, as_stream(stream), part, se_nb(C), b1, w2,
                        b2, (int)C, (int)Csq, h1, s, x, y, (int)HW);
   return launch_status("se_gate_excite");
-}
-
-// squeeze-excite backward of the excite vector: ds = sum_hw dy * x inside the first
-// kernel, then g / dW1 / db1 / dW2 / db2 as ewvit_se_mlp_bwd (3 launches)
-extern "C" int64_t ewvit_se_mlp_bwd_bn_workspace(int64_t N, int64_t C, int64_t Csq) {
-  return ewvit_se_mlp_bwd_workspace(N, C, Csq) + 4 * N * C * (int64_t)sizeof(float);
-}
-
-// ewvit_se_squeeze_mlp_bwd for the SE after a training-mode BatchNorm(+act) whose input is xb:
-// also leaves that BatchNorm's backward partial rows bnpart [N][2C] (one per frame) for
-// ewvit_bn_bwd_se_partials (workspace: ewvit_se_mlp_bwd_bn_workspace bytes)
-extern "C" int ewvit_se_squeeze_mlp_bwd_bn(const void *dy, const void *a, const void *xb, int dtype, int64_t N,
-                                           int64_t HW, int64_t C, const float *s, const float *h1, const float *s0,
-                                           const float *w1, const float *w2, int64_t Csq, const float *mean,
-                                           const float *invstd, const float *gamma, const float *beta, int act,
-                                           float *g, float *dw1, float *db1, float *dw2, float *db2, float *bnpart,
-                                           float *workspace, void *stream) {
-  if (int rc = se_check(dtype, N, HW, C, "se_squeeze_mlp_bwd_bn")) return rc;
-  if (int rc = se_mlp_check(N, C, Csq, "se_squeeze_mlp_bwd_bn")) return rc;
-  EWVIT_CHECK_ARG(dy && a && xb && s && h1 && s0 && w1 && w2 && mean && invstd && g && dw1 && dw2 && bnpart &&
-                      workspace && HW < (1 << 30) && act >= 0 && act <= 2,
-                  "se_squeeze_mlp_bwd_bn: bad args");
-  hipStream_t st = as_stream(stream);
-  const int nb = se_nb(C);
-  float *dz2 = workspace, *dz1 = workspace + N * C, *part = dz1 + N * Csq, *bnsum = part + N * nb * Csq;
-  const dim3 g1((unsigned)N, (unsigned)nb);
-#define SE_DH_BN(DTV, ACTV)                                                                                          \
-  hipLaunchKernelGGL((se_sq_dh_part_bn_kernel<DTV, ACTV>), g1, dim3(256), 0, st, dy, a, xb, (int)HW, s, w2, (int)C,  \
-                     (int)Csq, mean, invstd, gamma, beta, (int)N, dz2, part, bnsum)
-  if (dtype == EWVIT_BF16) {
-    if (act == 2) SE_DH_BN(EWVIT_BF16, 2); else if (act == 1) SE_DH_BN(EWVIT_BF16, 1); else SE_DH_BN(EWVIT_BF16, 0);
-  } else {
-    if (act == 2) SE_DH_BN(EWVIT_F32, 2); else if (act == 1) SE_DH_BN(EWVIT_F32, 1); else SE_DH_BN(EWVIT_F32, 0);
-  }
-#undef SE_DH_BN
-  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
-                     (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, 1.f / (float)HW, dz1, g, s,
-                     bnsum, (int)N, bnpart);
-  const int64_t tot = 2 * C * Csq + C + Csq;
-  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
-                     (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
-  return launch_status("se_squeeze_mlp_bwd_bn");
 }
 
 extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N, int64_t HW, int64_t C,

@@ -183,10 +183,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(StemArgs a) {
 }
 
 static int stem_grid(int64_t ntiles) {
-  static const int cap = [] {
-    const char *e = getenv("EWVIT_STEM_GRID");     // workgroups (A/B); each walks its tiles
-    return e ? atoi(e) : 1024;
-  }();
+  constexpr int64_t cap = 1024;                  // workgroups; each walks its tiles
   const int64_t g = ntiles < cap ? ntiles : cap;
   return (int)(g < 1 ? 1 : g);
 }

@@ -7,6 +7,7 @@ is missing, every op raises.
 import contextlib
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -54,10 +55,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
-    'ewvit_dwconv3x3_set_segs': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
-    'ewvit_conv2d_set_wgrad_kgroups': [_i32],
-    'ewvit_conv2d_set_ww': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -67,10 +65,6 @@ SIGNATURES = {
     'ewvit_bn_fwd_drop_add': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64, _f32, _u64, _vp, _vp, _vp, _vp],
     'ewvit_bn_bwd_scaled': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
-    'ewvit_bn_bwd_se_partials': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64,
-                                 _vp, _i32, _vp],
-    'ewvit_se_squeeze_mlp_bwd_bn': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
-                                    _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_bn_bwd_se': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     'ewvit_bn_fold_partials': [_vp, _i32, _vp, _vp, _i32, _vp, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
@@ -115,7 +109,6 @@ QUERIES = {
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
-    'ewvit_conv2d_set_ww_min': (_i64, [_i64]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_stem_parts': (_i64, [_i64, _i64, _i64, _i32]),
     'ewvit_dwt_hf_fused_ok': (_i32, [_i64, _i64, _i64, _i64, _i32, _i64, _i64, _i64]),
@@ -124,14 +117,12 @@ QUERIES = {
     'ewvit_bn_workspace': (_i64, [_i64, _i64, _i32]),
     'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),
-    'ewvit_se_mlp_bwd_bn_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64, _vp]),
     'ewvit_adam_chunks': (_i64, [_i64]),
     'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
-    'ewvit_dwconv3x3_set_pix': (_i64, [_i64]),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
 }
 
@@ -233,31 +224,29 @@ def rng_advance(device):
 # `grid_cap(n)` is active: a branch that runs on its own stream beside another (DAMA's MWT
 # beside the backbone) walks its tiles / rows on part of the CUs instead of filling the whole
 # GPU.  Ops remember the cap of their forward for their backward launches (`launch_cap`).
-_cap = 0
+# Per thread, like the C side (ewvit_set_grid_cap): nn.DataParallel runs its replicas in
+# threads (reference train.py:249-251), and one replica's branch cap must not leak into another.
+_tls = threading.local()
 
 
 @contextlib.contextmanager
 def grid_cap(n):
-    global _cap
-    prev, _cap = _cap, int(n)
+    prev = getattr(_tls, 'cap', 0)
+    _tls.cap = int(n)
     try:
         yield
     finally:
-        _cap = prev
-
-
-# the backward launches of a capped branch take EWVIT_MWT_GRID_CAP_BWD when set (> 0) instead
-# of their forward's cap: the two phases balance against different backbone chains
-_BWD_CAP = int(os.environ.get('EWVIT_MWT_GRID_CAP_BWD', '0'))
+        _tls.cap = prev
 
 
 def bwd_cap(n):
-    """The cap for the backward of an op whose forward ran under cap n (0: uncapped stays)."""
-    return _BWD_CAP if (n and _BWD_CAP > 0) else n
+    """The cap for the backward of an op whose forward ran under cap n: the same (one cap of
+    160 balances both phases)."""
+    return n
 
 
 def current_cap():
-    return _cap
+    return getattr(_tls, 'cap', 0)
 
 
 @contextlib.contextmanager

@@ -8,6 +8,7 @@ normalises consecutive equal batch slices with their own statistics (one
 launch for the MWT's per-level calls of its shared BatchNorms).
 """
 import os
+import threading
 import weakref
 
 import torch
@@ -19,12 +20,11 @@ ACT = {None: 0, 'none': 0, 'relu': 1, 'silu': 2}
 # BatchNorm backward statistics summed by the op that produces the BN output's gradient
 # (EWVIT_BN_BWD_LINK=0: every BN backward runs its own reduction pass, A/B)
 _BWD_LINK = os.environ.get('EWVIT_BN_BWD_LINK', '1') != '0'
-# the most partial rows a linked producer may leave (the dx pass reads them all per block)
-BWD_LINK_MAX_ROWS = 512
-# links for big maps too (the MWT's 2.4 M-row convs, partials folded): measured slower — the
+# the most partial rows a linked producer may leave (the dx pass reads them all per block).
+# Links over bigger maps (the MWT's 2.4 M-row convs, partials folded) measured slower — the
 # input-gradient epilogue's BN-input reads under the capped walk cost more than the reduction
-# pass they replace (MWT capped 14.0 -> 15.6 ms) — so A/B only (EWVIT_BN_LINK_BIG=1)
-BWD_LINK_BIG = os.environ.get('EWVIT_BN_LINK_BIG', '0') != '0'
+# pass they replace (MWT capped 14.0 -> 15.6 ms) — so those BNs reduce themselves.
+BWD_LINK_MAX_ROWS = 512
 
 
 class BwdStatsLink:
@@ -65,7 +65,9 @@ class BwdStatsLink:
         return part, nrc
 
 
-_bwd_offered = None
+# the offered link, per thread (nn.DataParallel replicas run in threads, reference
+# train.py:249-251): a replica's consumer must only ever see its own BatchNorm's offer
+_tls = threading.local()
 _zeros = {}
 
 
@@ -91,21 +93,23 @@ def offer_bwd_link(y, x, mean, invstd, gamma, beta, act, rscale=None, groups=1):
     """Offer the backward statistics of the BN that produced y (4-D NHWC bf16; `groups`
     consecutive batch slices with their own statistics) to y's consumer; returns the link
     (kept by the BN's backward), or None."""
-    global _bwd_offered
     if not (_BWD_LINK and y.dim() == 4 and y.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
-        _bwd_offered = None
+        _tls.offered = None
         return None
-    _bwd_offered = BwdStatsLink(y, x, mean, invstd, gamma, beta, act, rscale, groups)
-    return _bwd_offered
+    _tls.offered = BwdStatsLink(y, x, mean, invstd, gamma, beta, act, rscale, groups)
+    return _tls.offered
 
 
-def take_bwd_link(x):
-    """The link offered for x (the consumer's input), if any; one taker."""
-    global _bwd_offered
-    link = _bwd_offered
+def take_bwd_link(x, grouped=True, scaled=True):
+    """The link offered for x (the consumer's input), if any; one taker.  A consumer whose
+    backward kernel sums over whole maps only (no per-group partial rows) passes
+    grouped=False, one that cannot apply a per-frame row scale (the drop-path factor of
+    BNDropAddFn) scaled=False: such links are left to the BatchNorm's own reduction pass."""
+    link = getattr(_tls, 'offered', None)
     if link is not None and link.key == (x.data_ptr(), tuple(x.shape), x.dtype):
-        _bwd_offered = None
-        if link.yref() is not None and link.x is not None:
+        _tls.offered = None
+        if link.yref() is not None and link.x is not None and (grouped or link.groups == 1) and \
+                (scaled or link.rscale is None):
             return link
     return None
 

@@ -16,6 +16,7 @@ returns the input gradient in z's layout — the concatenation is never built.
 """
 import contextlib
 import ctypes
+import threading
 import weakref
 
 import torch
@@ -29,7 +30,9 @@ from .grads import grad_out
 # multi-tensor launch per 32 weights at the start of a training step (`packed()`),
 # into persistent bf16 buffers, instead of one pack launch per conv call.
 _registry = {}      # id(weight) -> {'ref', 'cin_pad', 'wp', 'wpt', 'bwd'}
-_active = False
+# per thread (nn.DataParallel replicas run in threads, reference train.py:249-251): the
+# `packed()` scope, the fp8 weight-amax cache of that scope and the offered skip link
+_tls = threading.local()
 
 
 class SkipLink:
@@ -46,22 +49,22 @@ class SkipLink:
         self.grad = None
 
 
-_offered = None
-
 grid_cap = L.grid_cap            # (ewvit._lib: the big-grid workgroup cap of a stream branch)
 
 
 def offer_skip_link(x):
-    global _offered
-    _offered = SkipLink(x)
-    return _offered
+    _tls.offered = SkipLink(x)
+    return _tls.offered
+
+
+def clear_skip_link():
+    _tls.offered = None
 
 
 def _take_link(x):
-    global _offered
-    link = _offered
+    link = getattr(_tls, 'offered', None)
     if link is not None and link.key == (x.data_ptr(), tuple(x.shape), x.dtype):
-        _offered = None
+        _tls.offered = None
         link.armed = True
         return link
     return None
@@ -116,20 +119,22 @@ def prepack():
 def packed():
     """Scope of one forward(+backward) with the weights fixed: packs all registered
     conv weights once on entry; convs inside read the packs."""
-    global _active
-    from . import ops
     prepack()
-    prev, _active = _active, True
-    prev_amax, ops._weight_amax = ops._weight_amax, {}     # fp8 weight amax: once per step
+    prev, prev_amax = getattr(_tls, 'active', False), getattr(_tls, 'weight_amax', None)
+    _tls.active, _tls.weight_amax = True, {}     # fp8 weight amax: once per step
     try:
         yield
     finally:
-        _active = prev
-        ops._weight_amax = prev_amax
+        _tls.active, _tls.weight_amax = prev, prev_amax
+
+
+def weight_amax_cache():
+    """The fp8 weight-amax cache of the calling thread's `packed()` scope, or None."""
+    return getattr(_tls, 'weight_amax', None)
 
 
 def _cached_pack(weight, cin_pad, bwd):
-    if not _active:
+    if not getattr(_tls, 'active', False):
         return None
     e = _registry.get(id(weight))
     if e is None or e['ref']() is not weight or e['cin_pad'] != cin_pad or e['wp'] is None or \
@@ -157,25 +162,6 @@ def _pack(weight, cin_pad, fwd=True, bwd=False):
     return wp, wpt
 
 
-# 1x1 stride-1 convs whose implicit GEMM has at most 64 128x128 tiles over a K of >= 1024 (the
-# backbone's stage-6 project forward, 1536 -> 256 at 7^2, and stage-6 expand input gradient,
-# K = 1536): the LDS-DMA kernel runs them on 50 workgroups, each walking 24 K-tiles, and
-# hipBLASLt (torch.mm, a plain library GEMM: the 1x1 conv over channels-last pixels IS one)
-# splits them over the chip — 20.4 -> 9.2 and 19.0 -> 11.2 us (tools/conv_bench.py --mm,
-# profiles/r03/ab/conv_mm.log).  Such a forward leaves no BatchNorm partials and such an input
-# gradient no backward sums (their BatchNorms run their own reduction passes).  Off by default
-# (EWVIT_CONV_LIBGEMM=1 enables it): the SFE branch alone gains 14.25-14.28 -> 14.09-14.12 ms,
-# but the two-branch step is unchanged (bench 3116-3126 vs 3119-3124 frames/s over 4 interleaved
-# rounds, profiles/r03/ab/conv_libgemm_*): those 50-workgroup launches left CUs to the capped
-# MWT branch, which the library GEMM's wider grids now take.
-import os as _os
-_LIBGEMM = _os.environ.get('EWVIT_CONV_LIBGEMM', '0') == '1'
-
-
-def _libgemm(M, ncol, K):
-    return _LIBGEMM and -(-M // 128) * -(-ncol // 128) <= 64 and K >= 1024 and K % 8 == 0 and ncol % 8 == 0
-
-
 def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     """(groups, rows per group's slice, partial rows per group, channels per group) when this
     conv's input gradient can sum the backward statistics of the BatchNorm that produced its
@@ -187,7 +173,7 @@ def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     tiles = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cx, Cout, k, stride))
     if tiles <= 0 or (skip is not None and levels > 1):
         return None
-    if tiles > bnmod.BWD_LINK_MAX_ROWS * (levels if levels > 1 else 1) and not bnmod.BWD_LINK_BIG:
+    if tiles > bnmod.BWD_LINK_MAX_ROWS * (levels if levels > 1 else 1):
         return None
     if skip is not None and not L.load().ewvit_conv2d_bwd_data_add_ok(N, H, W, Cx, Cout, k, stride):
         return None
@@ -205,8 +191,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
         L.require_gpu(x, weight)
-        if ctx.needs_input_grad[1]:
-            grads.note_use(weight)
+        ctx.gen = grads.note_use(weight if ctx.needs_input_grad[1] else None)
         if ctx.needs_input_grad[2]:
             grads.note_use(bias)
         ctx.link = _take_link(x) if levels == 1 else None
@@ -239,14 +224,8 @@ class Conv2dFn(torch.autograd.Function):
         # channels (the MWT fusion conv's 54 -> 64) are not counted
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (xc.numel() + y.numel() + wp.numel()) * 2}
         ctx.cap = L.current_cap()
-        ctx.libgemm_dx = k == 1 and stride == 1 and levels == 1 and _libgemm(N * H * W, Cx, Cout)
         with L.launch_cap(ctx.cap):
-            if bn_stats is None and b is None and k == 1 and stride == 1 and levels == 1 and \
-                    _libgemm(N * Ho * Wo, Cout, Cx):
-                # hipBLASLt: y[pixels, Cout] = x[pixels, Cx] @ W[Cout, Cx]^T on the channels-last views
-                torch.mm(xc.permute(0, 2, 3, 1).reshape(-1, Cx), wp.view(Cout, -1)[:, :Cx].t(),
-                         out=y.permute(0, 2, 3, 1).view(-1, Cout))
-            elif bn_stats is not None:
+            if bn_stats is not None:
                 # BatchNorm statistics of y left by the epilogue (ewvit_bn_fwd_partials)
                 shift, part, shift_out = bn_stats
                 L.call('ewvit_conv2d_fwd_bn', L.ptr(xc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, k, stride,
@@ -285,19 +264,8 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            lk = None if ctx.libgemm_dx else _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
-            if ctx.libgemm_dx:
-                # hipBLASLt: dx[pixels, Cx] = dy[pixels, Cout] @ W[Cout, Cx] (+ the skip gradient,
-                # added before the bf16 rounding as the dgrad epilogue adds it)
-                d2, w2 = dyc.permute(0, 2, 3, 1).reshape(-1, Cout), wpt.view(-1, Cout)[:Cx].t()
-                x2 = dx.permute(0, 2, 3, 1).view(-1, Cx)
-                if skip is not None:
-                    sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-                    torch.addmm(sk.permute(0, 2, 3, 1).reshape(-1, Cx), d2, w2, out=x2)
-                    skip = None
-                else:
-                    torch.mm(d2, w2, out=x2)
-            elif lk is not None:
+            lk = _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            if lk is not None:
                 # dx (+ the skip gradient) and the producing BatchNorm's backward sums in one epilogue
                 groups, grows, rows, Cg = lk
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if skip is not None else None
@@ -325,23 +293,8 @@ class Conv2dFn(torch.autograd.Function):
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
             wparam, bparam = ctx.params
-            dev = xc.device
-            # the weight gradient on the wgrad stream (ewvit.grads) when the weights were used
-            # once and hold no gradient; the MWT branch (capped grids, its own stream) keeps it
-            s_kh, s_kw = wparam.stride()[2:]
-            defer = ctx.cap == 0 and s_kh == k * s_kw and 2.0 * N * Ho * Wo * Cout * k * k * Cin >= grads.DEFER_MIN_FLOPS and \
-                grads.deferrable(wparam if ctx.needs_input_grad[1] else None, bparam if want_b else None)
-            if defer:
-                with torch.cuda.stream(grads.defer_begin(dev, xc, dyc)):
-                    dw, db = Conv2dFn._wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin,
-                                             k, stride, Ho, Wo, gc, gs)
-                for t in (dw, db):
-                    if t is not None:
-                        grads.defer_output(t, dev)
-            else:
-                grads.wgrad_wait(dev)
-                dw, db = Conv2dFn._wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin, k,
-                                         stride, Ho, Wo, gc, gs)
+            dw, db = Conv2dFn._wgrad(ctx, xc, dyc, weight, wparam, bparam, want_b, N, H, W, Cx, Cout, Cin, k,
+                                     stride, Ho, Wo, gc, gs)
         if dx is None and skip is not None:       # x needs no gradient through the conv, only the skip's
             dx = skip
         return dx, dw, db, None, None, None
@@ -353,14 +306,14 @@ class Conv2dFn(torch.autograd.Function):
         ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
         # dW in the parameter's own memory format — the data-parallel flat buffer's view
         # when the step provides one (ewvit.grads), so no copy or layout change follows
-        dwf = grad_out(wparam) if ctx.needs_input_grad[1] else torch.empty_like(weight, dtype=torch.float32)
+        dwf = grad_out(wparam, ctx.gen) if ctx.needs_input_grad[1] else torch.empty_like(weight, dtype=torch.float32)
         s_co, s_ci, s_kh, s_kw = dwf.stride()
         if s_kh != k * s_kw:
             dwf = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=xc.device)
             s_co, s_ci, s_kh, s_kw = dwf.stride()
         dbf = None
         if want_b:
-            dbf = grad_out(bparam)
+            dbf = grad_out(bparam, ctx.gen)
             if dbf.dim() != 1 or not dbf.is_contiguous():
                 dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (dyc.numel() + xc.numel()) * 2}
@@ -384,8 +337,6 @@ def bn_stat_rows(x, weight, stride=1, levels=1):
     if (not x.is_cuda or Cx < weight.shape[1] or (levels > 1 and Cx != weight.shape[1]) or k not in (1, 3)
             or weight.shape[3] != k or weight.shape[0] % 8 or NL % levels or (levels > 1 and Cz % 64)):
         return 0
-    if k == 1 and stride == 1 and levels == 1 and _libgemm(NL * H * W, weight.shape[0], Cx):
-        return 0                 # the library GEMM's shape: conv, then the BatchNorm's own statistics
     return int(L.load().ewvit_conv2d_fwd_bn_rows(NL // levels, H, W, Cz * levels, weight.shape[0], k, int(stride)))
 
 

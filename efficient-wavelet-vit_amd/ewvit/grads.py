@@ -16,58 +16,57 @@ autograd sums the uses' gradients before AccumulateGrad, so two uses must not sh
 slot) a fresh tensor is returned and AccumulateGrad adds it as usual.  The uses are
 counted per step: ``begin_step`` opens a step, the ops' forwards call ``note_use``.
 
-**Weight-gradient stream.**  A weight gradient is off the backward's critical path: only
-the optimizer (and the data-parallel all-reduce) reads it, while the input gradient feeds
-the next layer's backward.  With ``set_wgrad_stream(True)`` (``ewvit.graph.TrainStep``
-with ``EWVIT_WGRAD_STREAM=1``) a conv whose weight is used once in the step issues its
-wgrad (if at least ``EWVIT_WGRAD_MIN_FLOPS``) on a second stream, to fill the CUs the
-latency-bound input-gradient chain leaves idle.  The stream waits for the main stream at
-the point of issue (dy and x are ready), the tensors it reads are recorded on it (the
-caching allocator keeps them until it is done), and every consumer joins it: the bucket
-all-reduces (``wgrad_wait``), any synchronous gradient of a parameter that might already
-hold a deferred one (``wgrad_wait``), and the end of each backward (``wgrad_join``), which
-also rejoins the stream before a HIP-graph capture ends.  OFF by default: measured on the
-config-2 step it loses — 2958 vs 2956 frames/s deferring nothing (threshold 1e12), 2901 at
-5e9 FLOPs, 2268-2281 at 2e9 and below: the concurrent wgrads lengthen the
-dgrad chain more than they save.
+Use counts are per thread: nn.DataParallel runs its replicas' forwards in threads
+(reference train.py:249-251), each with its own parameters.
+
+(A second stream for the weight gradients was built and measured slower — 2958 vs 2956
+frames/s deferring nothing, 2268-2281 deferring the small wgrads, DESIGN §5.5 — and removed.)
 """
-import os
+import itertools
+import threading
 
 import torch
 
-DEFER_MIN_FLOPS = float(os.environ.get('EWVIT_WGRAD_MIN_FLOPS', '0'))
-_gen = 0
-_enabled = False
-_streams = {}
-_issued = set()          # devices with wgrad work issued since the last join
+_tls = threading.local()
+_steps = itertools.count(1)     # step ids unique across threads
 
 
 def begin_step():
-    """A new forward: use counts restart."""
-    global _gen
-    _gen += 1
+    """A new forward (of the calling thread): use counts restart."""
+    _tls.gen = next(_steps)
+
+
+def _gen():
+    return getattr(_tls, 'gen', 0)
 
 
 def note_use(param):
+    """Count one use of `param` in the calling thread's current step; returns the step id,
+    which the op keeps for its backward (autograd runs backward nodes on its own device
+    threads, so the backward cannot read the forward thread's step)."""
+    g = _gen()
     if param is None:
-        return
-    if getattr(param, '_ewvit_gen', None) != _gen:
-        param._ewvit_gen = _gen
+        return g
+    if getattr(param, '_ewvit_gen', None) != g:
+        param._ewvit_gen = g
         param._ewvit_uses = 1
     else:
         param._ewvit_uses += 1
+    return g
 
 
-def single_use(param):
-    """True when `param` entered the current step's forward exactly once (never noted:
-    False — unknown use counts take the conservative path)."""
-    return getattr(param, '_ewvit_gen', None) == _gen and param._ewvit_uses == 1
+def single_use(param, gen=None):
+    """True when `param` entered step `gen`'s forward (default: the calling thread's current
+    step) exactly once (never noted: False — unknown use counts take the conservative path)."""
+    g = _gen() if gen is None else gen
+    return g != 0 and getattr(param, '_ewvit_gen', None) == g and param._ewvit_uses == 1
 
 
-def grad_out(param, dtype=torch.float32):
-    """Output tensor for `param`'s gradient (shape and strides of `param`)."""
+def grad_out(param, gen=None, dtype=torch.float32):
+    """Output tensor for `param`'s gradient (shape and strides of `param`); `gen`: the step id
+    `note_use` returned in the op's forward."""
     slot = getattr(param, '_ewvit_grad_slot', None)
-    if slot is not None and param.is_leaf and param.grad is None and slot[0].dtype == dtype and single_use(param):
+    if slot is not None and param.is_leaf and param.grad is None and slot[0].dtype == dtype and single_use(param, gen):
         return slot[0].as_strided(param.shape, param.stride(), slot[1])
     return torch.empty_like(param, dtype=dtype, memory_format=torch.preserve_format)
 
@@ -80,62 +79,3 @@ def set_slot(param, flat, offset):
 def clear_slot(param):
     if hasattr(param, '_ewvit_grad_slot'):
         del param._ewvit_grad_slot
-
-
-# ---------------------------------------------------------------- weight-gradient stream
-def set_wgrad_stream(on):
-    global _enabled
-    prev, _enabled = _enabled, bool(on)
-    return prev
-
-
-def wgrad_stream(device):
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _streams.get(idx)
-    if st is None:
-        st = _streams[idx] = torch.cuda.Stream(device=torch.device('cuda', idx))
-    return st
-
-
-def deferrable(*params):
-    """The weight gradient of these parameters may go to the wgrad stream: the stream is
-    on, and each parameter (None = no gradient wanted) holds no gradient and was used once
-    — so AccumulateGrad adopts the deferred tensor without a kernel of its own on the
-    main stream (the op's output must keep the parameter's layout for that)."""
-    if not _enabled:
-        return False
-    return all(p is None or (p.is_leaf and p.grad is None and single_use(p)) for p in params)
-
-
-def defer_begin(device, *reads):
-    """Fork: the wgrad stream waits for the current stream; `reads` (dy, x, …) are kept
-    alive for it.  Returns the stream (use it as the current stream for the launches)."""
-    cur = torch.cuda.current_stream(device)
-    st = wgrad_stream(device)
-    st.wait_stream(cur)
-    for t in reads:
-        if t is not None:
-            t.record_stream(st)
-    _issued.add(st.device.index)
-    return st
-
-
-def defer_output(t, device):
-    """A gradient tensor written on the wgrad stream and handed to autograd on the
-    current one: its memory is in use on both."""
-    t.record_stream(torch.cuda.current_stream(device))
-
-
-def wgrad_wait(device):
-    """The current stream waits for every wgrad issued so far (a consumer, or a synchronous
-    gradient that AccumulateGrad may add to a deferred one)."""
-    if device.type == 'cuda' and (device.index if device.index is not None else torch.cuda.current_device()) in _issued:
-        torch.cuda.current_stream(device).wait_stream(wgrad_stream(device))
-
-
-def wgrad_join():
-    """End of a backward: the current stream joins the wgrad stream of every device used."""
-    for idx in list(_issued):
-        dev = torch.device('cuda', idx)
-        torch.cuda.current_stream(dev).wait_stream(wgrad_stream(dev))
-    _issued.clear()

@@ -59,6 +59,35 @@ def _backend(group):
     return dist.get_backend(group) if _world(group) > 1 else None
 
 
+def _pg_status():
+    import json
+    from torch._C import _distributed_c10d as c10d
+    d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=False, onlyActive=True))
+    return d.get('pg_status') or {}
+
+
+def retire_eager_collectives(timeout_s=60.0):
+    """Block until ProcessGroupNCCL's watchdog has retired every collective issued so far
+    (device synchronised first).  Raises if the status is unavailable or the watchdog does
+    not catch up within `timeout_s`."""
+    import time
+    torch.cuda.synchronize()
+    t0 = time.monotonic()
+    while True:
+        st = _pg_status()
+        if not st:
+            raise RuntimeError('TrainStep: the process-group status (flight recorder pg_status) is unavailable, '
+                               'so the watchdog queue cannot be drained before a global-mode capture; use '
+                               'EWVIT_CAPTURE_MODE=relaxed')
+        behind = {k: v for k, v in st.items()
+                  if int(v.get('last_completed_collective', -1)) < int(v.get('last_enqueued_collective', -1))}
+        if not behind:
+            return
+        if time.monotonic() - t0 > timeout_s:
+            raise RuntimeError(f'TrainStep: the NCCL watchdog did not retire the eager collectives: {behind}')
+        time.sleep(0.005)
+
+
 class GradBuckets:
     """Flat, bucketed gradient buffer with all-reduces issued as buckets fill.
 
@@ -146,9 +175,7 @@ class GradBuckets:
         if self.reduce and not self.defer:
             if self.flat.is_cuda:
                 # the gradients of a bucket may come from several streams (DAMA's MWT branch
-                # runs on its own, deferred weight gradients on the wgrad stream): the
-                # collective, issued on the current stream, waits for all
-                grads.wgrad_wait(self.flat.device)
+                # runs on its own): the collective, issued on the current stream, waits for all
                 cur = torch.cuda.current_stream(self.flat.device)
                 for st in self.streams[b]:
                     if st != cur:
@@ -250,8 +277,6 @@ class TrainStep:
         if self.buckets is not None:
             self.buckets.defer = not overlap
         self.bufsync = BufferSync(model, group) if dp else None
-        # single-use weights' gradients on a second stream, beside the input-gradient chain
-        grads.set_wgrad_stream(dev.type == 'cuda' and os.environ.get('EWVIT_WGRAD_STREAM', '0') == '1')
         self.loss = None
         self.mode = 'graph' if self.graph else 'eager'
         self._hyper = optimizer.hyper_signature() if hasattr(optimizer, 'hyper_signature') else None
@@ -266,14 +291,14 @@ class TrainStep:
             try:
                 self._capture(warmup)
             except Exception as e:          # noqa: BLE001 — a backend that cannot record collectives
+                self.g = None                # a failed capture's graph is never replayed
                 if self.buckets is None or os.environ.get('EWVIT_GRAPH_SPLIT_FALLBACK', '0') != '1':
                     import sys
                     import traceback
                     print('TrainStep: graph capture failed:', file=sys.stderr)
                     traceback.print_exc()
                     sys.stderr.flush()
-                    if not self._capturing:  # (inside a failed capture, freeing memory can abort)
-                        self.close()         # no gradient hooks / slots left behind on the parameters
+                    self.close()             # no gradient hooks / slots left behind on the parameters
                     raise
                 import sys
                 print(f'TrainStep: capturing the collectives failed ({type(e).__name__}: {e}); '
@@ -333,7 +358,6 @@ class TrainStep:
                 if self.accum > 1:
                     lk = lk / self.accum                                   # train.py:110
                 lk.backward()
-                grads.wgrad_join()           # deferred weight gradients complete
                 loss = lk.detach() if loss is None else loss + lk.detach()
         return loss
 
@@ -374,9 +398,11 @@ class TrainStep:
             # default global mode the watchdog's event query errors and it aborts the process
             # (seen intermittently on the GPU box; TORCH_NCCL_ASYNC_ERROR_HANDLING=0 hides it)
             self._capturing = True
-            with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
-                self.loss = self._iteration()
-            self._capturing = False
+            try:
+                with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
+                    self.loss = self._iteration()
+            finally:
+                self._capturing = False      # the capture has ended (the context closed it)
             self._finish_capture(self.g)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -395,26 +421,37 @@ class TrainStep:
             self.opt.zero_grad(set_to_none=True)
             self.g = torch.cuda.CUDAGraph()
             self._capturing = True
-            with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
-                self.buckets.begin()
-                self.loss = self._fwd_bwd()
-                self.buckets.finish()
-            self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool(), capture_error_mode=self._capture_mode):
-                self.opt.step()
-            self._capturing = False
+            try:
+                with torch.cuda.graph(self.g, stream=side, capture_error_mode=self._capture_mode):
+                    self.buckets.begin()
+                    self.loss = self._fwd_bwd()
+                    self.buckets.finish()
+                self.g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g2, stream=side, pool=self.g.pool(), capture_error_mode=self._capture_mode):
+                    self.opt.step()
+            finally:
+                self._capturing = False
             self._finish_capture(self.g2)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
 
     def _drain_watchdog(self):
-        """Before a capture with RCCL collectives: the process group's watchdog thread polls
-        the events of the eager collectives issued before it (every ~100 ms) and drops them
-        once it has seen them complete; give it that poll after the device has drained, so
-        it has nothing to query while the capture runs."""
-        if self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl':
-            import time
-            time.sleep(float(os.environ.get('EWVIT_CAPTURE_DRAIN_S', '0.3')))
+        """Before a capture that records RCCL collectives.  Every EAGER collective (the warm-up
+        steps' bucket all-reduces and buffer broadcasts, the layout broadcast) is queued to
+        ProcessGroupNCCL's watchdog thread, which polls the collective's end event
+        (hipEventQuery) until it sees it complete and then drops it.  Collectives issued
+        during a capture are never queued.  Such a poll from another thread while this one
+        captures is illegal in the GLOBAL capture mode (the watchdog's query fails and it
+        aborts the process); in the default RELAXED mode (`EWVIT_CAPTURE_MODE`) it is legal,
+        so nothing has to be drained.  In global mode: after the device has drained, wait
+        until the watchdog has retired every collective enqueued so far — its own progress
+        marker, `last_completed_collective == last_enqueued_collective` of each process group
+        in the flight-recorder status — so its queue is empty when the capture begins."""
+        if not (self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl'):
+            return
+        if self._capture_mode != 'global':
+            return
+        retire_eager_collectives()
 
     def _finish_capture(self, graph):
         fin = getattr(self.opt, 'finish_capture', None)

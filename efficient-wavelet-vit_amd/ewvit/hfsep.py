@@ -25,6 +25,7 @@ class SeperateConvFn(torch.autograd.Function):
     def forward(ctx, x, levels, shift, w0, w1, w2, b0, b1, b2):
         L.require_gpu(x, w0)
         params = (w0, w1, w2, b0, b1, b2)
+        ctx.gen = grads.note_use(None)
         for i, p in enumerate(params):
             if ctx.needs_input_grad[3 + i]:
                 grads.note_use(p)
@@ -67,7 +68,7 @@ class SeperateConvFn(torch.autograd.Function):
             outs = []
             for i, p in enumerate(ctx.params):
                 if ctx.needs_input_grad[3 + i]:
-                    g = grad_out(p)
+                    g = grad_out(p, ctx.gen)
                     if not g.is_contiguous():
                         g = torch.empty_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
                     outs.append(g)

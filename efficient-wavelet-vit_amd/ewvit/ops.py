@@ -45,21 +45,20 @@ def _operand_amax(X, rows_dim, k_dim, ld):
     return amax_partials(X, k_dim, rows_dim, ld[1])
 
 
-# amax partials of fp32 master weights, reused by every fp8 GEMM of one training step (the
-# weights are fixed between optimizer steps): valid inside ewvit.conv.packed() only
-_weight_amax = None
-
-
 def weight_amax(W):
-    """amax partials of a whole weight tensor (any layout: the partition does not matter)."""
-    if _weight_amax is not None:
-        e = _weight_amax.get(id(W))
+    """amax partials of a whole weight tensor (any layout: the partition does not matter);
+    reused by every fp8 GEMM of one training step (the weights are fixed between optimizer
+    steps) inside ewvit.conv.packed()."""
+    from .conv import weight_amax_cache
+    cache = weight_amax_cache()
+    if cache is not None:
+        e = cache.get(id(W))
         if e is not None and e[0] is W:
             return e[1]
     r = amax_partials(W, 1, W.numel(), W.numel()) if W.is_contiguous() else \
         amax_partials(W.contiguous(), 1, W.numel(), W.numel())
-    if _weight_amax is not None:
-        _weight_amax[id(W)] = (W, r)
+    if cache is not None:
+        cache[id(W)] = (W, r)
     return r
 
 
@@ -220,7 +219,7 @@ def _linear_setup(ctx, inputs, output):
     ctx.set_materialize_grads(False)     # no zero-filled gradients for aux / xa
     ctx.save_for_backward(x, weight, aux, xa)
     ctx.params = (weight, bias)          # gradient slots (ewvit.grads) are looked up on these
-    note_use(weight)
+    ctx.gen = note_use(weight)
     note_use(bias)
     ctx.cfg = (act, drop_p, seed, resid is not None, bias is not None, fp8)
 
@@ -233,9 +232,9 @@ def _linear_backward(ctx, dy, _daux, _dxa):
     need = ctx.needs_input_grad
     dw = db = None
     if need[1]:
-        dw = grad_out(ctx.params[0])
+        dw = grad_out(ctx.params[0], ctx.gen)
     if has_bias and need[2]:
-        db = grad_out(ctx.params[1])
+        db = grad_out(ctx.params[1], ctx.gen)
         if db.dim() != 1 or not db.is_contiguous():
             db = torch.empty(db.shape[0], dtype=torch.float32, device=dy.device)
     dx = torch.ops.ewvit.linear_backward(dy, x, weight, aux, xa, act, drop_p, seed, bool(need[0]), fp8, dw, db)
@@ -586,9 +585,11 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         ctx.save_for_backward(xc, w)
         ctx.cfg = (stride, pad, weight.dtype)
         ctx.wstride = weight.stride()
-        # the backward statistics of the BatchNorm that produced x, summed by the input gradient
-        ctx.bnlink = _bn.take_bwd_link(x) if (_DW_BWD_LINK and stride == 1 and pad == 1
-                                             and ctx.needs_input_grad[0]) else None
+        # the backward statistics of the BatchNorm that produced x, summed by the input gradient:
+        # ewvit_dwconv3x3_bwd_data_bn leaves whole-map sums with no row scale, so only the link
+        # of a one-group BatchNorm without a drop-path scale
+        ctx.bnlink = _bn.take_bwd_link(x, grouped=False, scaled=False) if (
+            _DW_BWD_LINK and stride == 1 and pad == 1 and ctx.needs_input_grad[0]) else None
         return y
 
     @staticmethod

@@ -72,7 +72,19 @@ class Adam(torch.optim.Optimizer):
         state tensors (torch would replace them, and a HIP graph recorded before the load would
         keep updating the old ones), and the lr scalars stay keyed by group index."""
         old = {p: dict(st) for p, st in self.state.items()}
+        prev_state, prev_groups = self.state, self.param_groups
         super().load_state_dict(state_dict)
+        # a parameter a captured step updates must keep its tensors, else the graph would go on
+        # updating the old ones while the optimizer shows the loaded, never-updated ones
+        captured = self.__dict__.get('_captured_params', ())
+        bad = [i for i, p in enumerate(captured)
+               if not all(k in old.get(p, {}) and torch.is_tensor(self.state.get(p, {}).get(k))
+                          and old[p][k].shape == self.state[p][k].shape for k in ('step', 'exp_avg', 'exp_avg_sq'))]
+        if bad:
+            self.__setstate__({'state': prev_state, 'param_groups': prev_groups})
+            raise RuntimeError(f'ewvit.optim.Adam.load_state_dict: {len(bad)} parameter(s) a captured step updates '
+                               'have no matching state in the loaded dict; re-capture the step (build a new '
+                               'TrainStep) after loading such a state')
         for p, st in self.state.items():
             o = old.get(p)
             if not o:
@@ -197,6 +209,9 @@ class Adam(torch.optim.Optimizer):
         long as it does (ewvit.graph.TrainStep passes its graphs), else the optimizer keeps
         them.  Returns the tables."""
         out = []
+        cap = self.__dict__.setdefault('_captured_params', [])
+        have = set(map(id, cap))
+        cap.extend(p for p, st in self.state.items() if st and id(p) not in have)
         for item in self.__dict__.pop('_fill_after_capture', []):
             tab = item[0]
             if item[1] is not None:

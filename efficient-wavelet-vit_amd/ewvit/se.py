@@ -20,13 +20,10 @@ from . import _lib as L
 # the depthwise BatchNorm's apply pass and the SE squeeze as one kernel when the statistics come
 # from the depthwise conv (ewvit_bn_act_se_squeeze; 0: separate passes, A/B)
 _BN_SQUEEZE = os.environ.get('EWVIT_BN_SQUEEZE', '1') != '0'
-# the BatchNorm backward's sums taken by the SE backward's squeeze kernel, per frame
-# (ewvit_se_squeeze_mlp_bwd_bn + ewvit_bn_bwd_se_partials; EWVIT_SE_BN_SUMS=1).  Off: measured
-# slower (SFE piece 14.22-14.25 -> 14.28-14.32 ms, profiles/r03/ab/se_bn_sums_ab.txt) — the
-# squeeze kernel walks one frame's 49-196 rows per block, 1-6 rows per thread, so the third
-# operand's loads, act' and the five-fold LDS tree land on its latency path, while the
-# reduction pass they replace streams the whole map
-_SE_BN_SUMS = os.environ.get('EWVIT_SE_BN_SUMS', '0') == '1'
+# (the BatchNorm backward's sums taken per frame by the SE backward's squeeze kernel measured
+# slower — SFE piece 14.22-14.25 -> 14.28-14.32 ms, profiles/r03/ab/se_bn_sums_ab.txt — and
+# was removed: that kernel walks one frame's 49-196 rows per block, so the extra operand's loads
+# land on its latency path, while the reduction pass they replace streams the whole map)
 
 
 def _rows(x):
@@ -181,20 +178,93 @@ class BnActSEFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
-        if _SE_BN_SUMS:
-            # the SE backward's squeeze kernel also sums the BatchNorm backward's terms per frame
-            # (ewvit_se_squeeze_mlp_bwd_bn): the BatchNorm backward is its dx pass alone
-            mws = torch.empty(L.load().ewvit_se_mlp_bwd_bn_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-            bnpart = torch.empty(N, 2 * C, dtype=torch.float32, device=dev)
-            L.call('ewvit_se_squeeze_mlp_bwd_bn', L.ptr(dyc), L.ptr(x2), L.ptr(xc), L.dt(x2), N, HW, C, L.ptr(sc),
-                   L.ptr(h1), L.ptr(s0), L.ptr(W1), L.ptr(W2), Csq, L.ptr(mean), L.ptr(invstd), L.ptr(gamma),
-                   L.ptr(beta), act, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(bnpart),
-                   L.ptr(mws), L.stream(g), work={'bytes': 3 * x2.numel() * x2.element_size()})
-            L.call('ewvit_bn_bwd_se_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma),
-                   L.ptr(beta), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW,
-                   L.ptr(bnpart), N, L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
-            return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2),
-                    db2, None)
+        mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        # ds = sum_hw dy * x inside the backward MLP's first kernel
+        L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(s), L.ptr(h1), L.ptr(s0),
+               L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
+               L.stream(g), work={'bytes': 2 * xc.numel() * xc.element_size()})
+        dx = torch.empty_like(xc)
+        L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
+               work={'bytes': 2 * xc.numel() * xc.element_size()})
+        return dx, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2
+
+
+class BnActSEFn(torch.autograd.Function):
+    """SE(act(BatchNorm(x))) in training mode — MBConv's depthwise BN + SiLU followed by its
+    squeeze-excitation.  Forward: the BatchNorm statistics + apply passes, then the SE's squeeze
+    MLP and excite pass (the same kernels as batch_norm_act + squeeze_excite).  Backward: the SE
+    MLP backward gives the squeeze term g, and the BatchNorm backward forms its output gradient
+    dy*s + g itself (ewvit_bn_bwd_se) — the SE input-gradient pass and its tensor never exist."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2,
+                partials=None):
+        L.require_gpu(x)
+        xc, N, HW, C = _rows(x)
+        M = N * HW
+        dev = x.device
+        x2 = torch.empty_like(xc)
+        mean = torch.empty(1, C, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        Csq = w1.shape[0]
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
+        h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
+        sc = torch.empty(N, C, dtype=torch.float32, device=dev)
+        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+        y = torch.empty_like(x2)
+        if partials is not None and _BN_SQUEEZE and N <= 65535:
+            # BatchNorm apply + SiLU + the SE squeeze (+ the MLP's first-layer partials) in one
+            # pass, then the gates + excite: 2 launches for the BN and the SE forward
+            part, shifts, nrc = partials
+            L.call('ewvit_bn_act_se_squeeze', L.ptr(xc), L.ptr(x2), L.dt(xc), N, HW, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.ptr(W1), Csq, L.ptr(s0),
+                   L.ptr(fws), L.stream(x2), work={'bytes': 2 * xc.numel() * xc.element_size()})
+            L.call('ewvit_se_gate_excite', L.ptr(fws), L.ptr(_vec(b1)), L.ptr(W2), L.ptr(_vec(b2)), L.ptr(x2),
+                   L.dt(x2), N, HW, C, Csq, L.ptr(h1), L.ptr(sc), L.ptr(y), L.stream(y),
+                   work={'bytes': 2 * x2.numel() * x2.element_size()})
+            ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
+            ctx.cfg = (act, b1 is not None, b2 is not None)
+            return y
+        if partials is not None:
+            # statistics summed by the depthwise conv that produced x: the apply pass only
+            part, shifts, nrc = partials
+            L.call('ewvit_bn_fwd_partials', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), 1, L.stream(x2),
+                   work={'bytes': 2 * xc.numel() * xc.element_size()})
+        else:
+            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
+            L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean),
+                   L.ptr(invstd), 1, L.ptr(counter), L.ptr(ws), L.stream(x2),
+                   work={'bytes': 3 * xc.numel() * xc.element_size()})
+        # squeeze + MLP hidden partials, then the gates and the excite pass in one launch
+        L.call('ewvit_se_forward', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
+               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(y), L.ptr(fws), L.stream(y),
+               work={'bytes': 3 * x2.numel() * x2.element_size()})
+        ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
+        ctx.cfg = (act, b1 is not None, b2 is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc = ctx.saved_tensors
+        act, has_b1, has_b2 = ctx.cfg
+        N, C, H, W = xc.shape
+        HW, M, Csq = H * W, N * H * W, w1.shape[0]
+        dev = xc.device
+        dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
+        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
+        g = torch.empty(N, C, dtype=torch.float32, device=dev)
+        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
+        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
+        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if has_b1 else None
+        db2 = torch.empty(C, dtype=torch.float32, device=dev) if has_b2 else None
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
                L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),

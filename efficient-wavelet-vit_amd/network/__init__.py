@@ -3,8 +3,10 @@
 Same class names, constructor signatures, attribute names and state-dict keys;
 the hot path runs on the ewvit HIP kernels (../ewvit, C-ABI include/ewvit.h).
 """
+import functools
 import os
 
+import torch
 import yaml
 
 _PKG_CONFIG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'config',
@@ -40,3 +42,30 @@ def set_gemm_precision(model, precision='bf16'):
             t.gemm_precision = precision
             n += 1
     return n
+
+
+def _f32(out):
+    if torch.is_tensor(out):
+        return out.float() if out.is_floating_point() and out.dtype != torch.float32 else out
+    if isinstance(out, dict):
+        return type(out)((k, _f32(v)) for k, v in out.items())
+    if isinstance(out, (tuple, list)):
+        return type(out)(_f32(v) for v in out)
+    return out
+
+
+def bf16_compute(forward):
+    """The compute contract of the hot-path modules: they compute in bf16 (MFMA
+    operands; BatchNorm / LayerNorm statistics, softmax and accumulation in fp32), as BASELINE
+    config 2 names.  A caller that has NOT enabled CUDA autocast — the reference's own
+    train.py:100-115 and eval.py:150-160 run fp32 — gets exactly the path an autocast caller
+    gets (autocast(bfloat16) is entered here, so no module falls back to a library conv or
+    BatchNorm) and fp32 outputs, as the reference returns."""
+    @functools.wraps(forward)
+    def wrapper(self, x, *args, **kwargs):
+        if not (torch.is_tensor(x) and x.is_cuda) or torch.is_autocast_enabled('cuda'):
+            return forward(self, x, *args, **kwargs)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = forward(self, x, *args, **kwargs)
+        return _f32(out)
+    return wrapper

@@ -17,7 +17,7 @@ from torch.nn import functional as F
 
 import ewvit
 
-from . import load_config
+from . import bf16_compute, load_config
 from .mwt import MWT
 from .sfe import EfficientViT, LayerNorm, Linear, _fp8, _hooked
 
@@ -25,11 +25,14 @@ from .sfe import EfficientViT, LayerNorm, Linear, _fp8, _hooked
 _SIDE = {}
 
 
-def _side_stream(device):
+def _side_stream(device, main):
+    """The MWT branch's stream, one per (device, main stream): replicas driven from several
+    threads on their own streams (nn.DataParallel) never share one."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _SIDE.get(idx)
+    key = (idx, main.cuda_stream)
+    st = _SIDE.get(key)
     if st is None:
-        st = _SIDE[idx] = torch.cuda.Stream(device=torch.device('cuda', idx))
+        st = _SIDE[key] = torch.cuda.Stream(device=torch.device('cuda', idx))
     return st
 
 
@@ -118,7 +121,8 @@ def _spatial_mean(t):
 
 class FusionGate(nn.Sequential):
     """Conv3x3(2D->D, pad 1) + BN + ReLU (dama.py:124-128).  On a 1x1 map the
-    zero padding leaves only the centre tap: one GEMM with W[:, :, 1, 1]."""
+    zero padding leaves only the centre tap: one GEMM with W[:, :, 1, 1]; the BatchNorm
+    (batch statistics over the chunk's frames) + ReLU on the ewvit BN kernel, fp32."""
 
     def forward(self, x):
         conv, bn, act = self[0], self[1], self[2]
@@ -126,8 +130,10 @@ class FusionGate(nn.Sequential):
             return super().forward(x)
         B = x.shape[0]
         w = conv.weight[:, :, conv.padding[0], conv.padding[1]]
-        y = ewvit.linear(x.reshape(B, -1), w, conv.bias, out_dtype=torch.float32)
-        return act(bn(y.reshape(B, -1, 1, 1)))
+        y = ewvit.linear(x.reshape(B, -1), w, conv.bias, out_dtype=torch.float32).reshape(B, -1, 1, 1)
+        if _hooked(bn) or _hooked(act) or bn.momentum is None or y.shape[1] % 8:
+            return act(bn(y))
+        return ewvit.batch_norm_act(y, bn, 'relu')         # BN + ReLU: one ewvit pass each way
 
 
 class DAMA(nn.Module):                                                     # dama.py:80-206
@@ -164,7 +170,7 @@ class DAMA(nn.Module):                                                     # dam
         if not (frame.is_cuda and _branch_streams()):
             return self.sfe(frame).float(), self.mwt(frame).float()
         main = torch.cuda.current_stream(frame.device)
-        side = _side_stream(frame.device)
+        side = _side_stream(frame.device, main)
         side.wait_stream(main)             # fork before the SFE work is issued on main
         space = self.sfe(frame).float()
         # the MWT ops are recorded after the SFE ops: autograd runs ready backward nodes
@@ -176,6 +182,7 @@ class DAMA(nn.Module):                                                     # dam
         freq.record_stream(main)
         return space, freq
 
+    @bf16_compute
     def _process_frame(self, frame):
         B = frame.shape[0]
         space_feats, freq_feats = self._branches(frame)
@@ -193,6 +200,7 @@ class DAMA(nn.Module):                                                     # dam
         return {'fused': _spatial_mean(weighted), 'space': _spatial_mean(space_feats),
                 'freq': _spatial_mean(freq_feats)}
 
+    @bf16_compute
     def forward(self, x, batch_size=16):
         B, K, C, H, W = x.shape
         if self.training and x.is_cuda:

@@ -224,7 +224,7 @@ class _Block(nn.Module):
             # skip's gradient is added in the first conv's dgrad epilogue (SkipLink)
             link = ewvit.conv.offer_skip_link(x) if torch.is_grad_enabled() and _SKIP_LINK else None
             h = _seq(list(self.block)[:-1], x)
-            ewvit.conv._offered = None
+            ewvit.conv.clear_skip_link()
             return last.forward_drop_add(h, x, self.sd_prob, link)
         r = self.block(x) if self.block._forward_hooks or self.block._forward_pre_hooks else _seq(list(self.block), x)
         if self.use_res_connect:

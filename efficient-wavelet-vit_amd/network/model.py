@@ -19,7 +19,7 @@ from torch import nn
 
 import ewvit
 
-from . import load_config
+from . import bf16_compute, load_config
 from .dama import DAMA
 from .mwt import MWT
 from .sfe import Linear, _hooked
@@ -55,6 +55,7 @@ class DeepfakeDetector(nn.Module):
                          out_dtype=torch.float32)
         return ewvit.linear(h, l2.weight, l2.bias, out_dtype=torch.float32)
 
+    @bf16_compute
     def forward(self, x, batch_size, ablation):
         if batch_size is not None:
             self.batch_size = batch_size

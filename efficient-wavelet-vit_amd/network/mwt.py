@@ -29,6 +29,8 @@ from torch.nn import functional as F
 
 import ewvit
 
+from . import bf16_compute
+
 
 class DWTForward(nn.Module):
     """pytorch_wavelets.DWTForward(J, wave='haar', mode='zero') on the ewvit DWT kernel.
@@ -213,6 +215,7 @@ class MWT(nn.Module):
     def _patched(self):
         return 'wavelet_transform' in self.__dict__ or type(self).wavelet_transform is not MWT.wavelet_transform
 
+    @bf16_compute
     def forward(self, x):
         B, C, H, W = x.shape
         target = (H // 2, W // 2)

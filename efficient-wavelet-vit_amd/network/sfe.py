@@ -20,6 +20,7 @@ from torch.nn import functional as F
 
 import ewvit
 
+from . import bf16_compute
 from .efficientnet import efficientnet_v2_s
 
 
@@ -199,5 +200,6 @@ class EfficientViT(nn.Module):                                             # sfe
         f = ewvit.linear(tok[:, 1:], fm.weight, fm.bias, act=2, out_dtype=torch.float32, fp8=_fp8(fm))
         return f.reshape(Bn, H, W, -1).permute(0, 3, 1, 2)
 
+    @bf16_compute
     def forward(self, img, mask=None):
         return self.head(self.efficient_net.features(img))

@@ -182,17 +182,6 @@ int ewvit_attn_bwd(const void *dout, int64_t sdo_b, int64_t sdo_n, const void *q
                    int64_t sv_b, int64_t sv_n, const float *p, void *dq, void *dk, void *dv,
                    int64_t B, int64_t H, int nq, int nk, int d, float scale, void *stream);
 
-/* Most column segments per output row the depthwise row kernels may use (1..8; default 1 or
- * EWVIT_DW_SEGS): an A/B and test knob, not a numerics switch (every split computes the
- * same sums in the same order). */
-int ewvit_dwconv3x3_set_segs(int max_segs);
-/* Output maps of at most max_pixels per frame (default 0 = never, or EWVIT_DW_PIX) run the
- * depthwise convs on the per-pixel kernel (all 9 taps of a pixel loaded at once, the block's
- * weights staged in LDS) instead of the row kernels: an A/B and test knob (the two compute
- * every output with the same operations in the same order; the per-pixel form measured slower on
- * the backbone's 7^2 / 14^2 maps).  Returns the previous setting. */
-int64_t ewvit_dwconv3x3_set_pix(int64_t max_pixels);
-
 /* ------------------------------------------- depthwise 3x3 conv (backbone) ---
  * The MBConv depthwise convolutions of EfficientNetV2-S (groups = channels,
  * kernel 3, stride 1|2, pad 1, no bias) — the backbone the reference reaches
@@ -292,13 +281,6 @@ int ewvit_bn_bwd_scaled(const void *dy, const void *x, void *dx, int dtype, int6
 int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
                     const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
                     float *dbeta, const float *se_s, const float *se_g, int64_t HW, float *workspace, void *stream);
-/* ewvit_bn_bwd_se's dx pass alone, from the partial rows [nrc][2C] of (sum g, sum g*xhat),
- * g = (dy*se_s + se_g) * act'(z), that ewvit_se_squeeze_mlp_bwd_bn left (one per frame) — the
- * same backward (network/sfe.py:111-113 via torchvision MBConv) without its reduction pass. */
-int ewvit_bn_bwd_se_partials(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
-                             const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
-                             int act, float *dgamma, float *dbeta, const float *se_s, const float *se_g, int64_t HW,
-                             const float *part, int nrc, void *stream);
 /* Training-mode backward whose reduction pass already ran in the kernel that produced dy
  * (ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [groups][nrc][2C] rows of
  * (sum g, sum g*xhat), g = dy * act'(...) or, with row_scale [M / HW] (act 0, one group: the
@@ -364,38 +346,22 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
  * persistently, conv wgrad uses fewer pixel splits, the BatchNorm passes take more rows per
  * workgroup.  For a branch sharing the GPU with another stream (DAMA's MWT beside the
  * backbone: its big launches then leave most CUs to the backbone's latency-bound kernels).
- * Host-side state read at launch time (so a HIP graph records the capped grids).  Returns the
- * previous cap.  ewvit_conv2d_set_grid_cap is the same call. */
+ * Host-side state of the CALLING THREAD, read at launch time (so a HIP graph records the
+ * capped grids; nn.DataParallel's replica threads, reference train.py:249-251, each keep their
+ * own).  Returns the previous cap.  ewvit_conv2d_set_grid_cap is the same call. */
 int ewvit_set_grid_cap(int max_workgroups);
 int ewvit_conv2d_set_grid_cap(int max_workgroups);
 
-/* Kernel-family switch for A/B measurement (not needed for correctness): 0 uses the
- * register-staged kernels everywhere; 1..4 (+8: tap-inner K order; default 9, or
- * EWVIT_CONV_GLDS) select an
- * LDS-DMA tile / ring-depth configuration where the shape allows (csrc/conv.hip).
- * Returns the previous setting. */
+/* Kernel-family test switch (not needed for correctness): 0 runs every shape on the
+ * register-staged kernels — the fallback of the shapes the LDS-DMA kernels refuse — so a test
+ * can check both on one case; 1 (default) the LDS-DMA kernels wherever the shape allows.
+ * Returns the previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_glds(int variant);
-/* Weight-gradient n'-tile width (A/B measurement; default from EWVIT_CONV_WGW, else 4):
- * 0 = 128-column tiles; 1/2/3 = 256-column tiles (each wave 64 x 128) with 64/32/32 pixels
- * per K-tile and ring depth 2/2/3, taken when n' = k*k*Cin >= 256 and the last tile wastes
- * <= 1/8 of it; 4 = auto (2 for n' >= 2048 over >= 64K output pixels, else 0).  Replaces nothing in the reference (tuning knob of csrc/conv.hip).
- * Returns the previous setting. */
+/* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
+ * 64 x 128, 32 pixels per K-tile) for n' = k*k*Cin >= 2048 over >= 64K output pixels, else
+ * 128-column tiles; 2 = 256-column tiles whenever n' >= 256 and the last tile wastes <= 1/8 of
+ * it; 0 = never.  Returns the previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_wgrad_wide(int variant);
-/* Wide-wave fwd / input-gradient blocks for grids of > 4096 128 x 128 tiles with 128-column
- * tiles (A/B measurement; default from EWVIT_CONV_WW, else 0): each wave 64 x 128 of the tile;
- * 1 = 256 x 128 tiles with a 2-deep ring, 2 = 128 x 128 tiles, 3 = 256 x 128 with a 3-deep
- * ring; 0 = off.  Variants 1 / 3 change ewvit_conv2d_fwd_bn_rows to 256.  Replaces nothing in
- * the reference.  Returns the previous setting. */
-int ewvit_conv2d_set_ww(int variant);
-/* The grid size (128 x 128 tiles) above which ewvit_conv2d_set_ww's variant applies (default
- * from EWVIT_CONV_WWMIN, else 4096; tests lower it).  Returns the previous setting. */
-int64_t ewvit_conv2d_set_ww_min(int64_t min_tiles);
-/* Weight-gradient K-groups (A/B measurement; default from EWVIT_CONV_WKG, else 1): 2 = two
- * groups of 4 waves per workgroup, each multiplying every other K-tile of a pixel split and
- * summed through LDS (half the splits and fp32 slabs), for the default 128-column family on
- * an uncapped grid; 1 = one group.  Replaces nothing in the reference.  Returns the previous
- * setting. */
-int ewvit_conv2d_set_wgrad_kgroups(int kgroups);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs
@@ -531,19 +497,6 @@ int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N
                              const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
                              int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,
                              float *workspace, void *stream);
-/* ewvit_se_squeeze_mlp_bwd for an SE whose input a = act(BatchNorm(xb)) (training mode: mean /
- * invstd saved by the forward, affine gamma / beta, act 0/1/2): the same outputs (ds, so g and
- * the MLP gradients, bit-identical), plus that BatchNorm's backward partial rows bnpart [N][2C]
- * (sum g, sum g*xhat per frame, g = (dy*s + g_se) * act'(z)) for ewvit_bn_bwd_se_partials —
- * its first kernel sums the BatchNorm terms over the frame's rows as it reads dy, so the
- * BatchNorm backward's reduction pass never runs (MBConv depthwise BN + SiLU -> SE,
- * network/sfe.py:111-113).  Workspace: ewvit_se_mlp_bwd_bn_workspace bytes. */
-int64_t ewvit_se_mlp_bwd_bn_workspace(int64_t N, int64_t C, int64_t Csq);
-int ewvit_se_squeeze_mlp_bwd_bn(const void *dy, const void *a, const void *xb, int dtype, int64_t N, int64_t HW,
-                                int64_t C, const float *s, const float *h1, const float *s0, const float *w1,
-                                const float *w2, int64_t Csq, const float *mean, const float *invstd,
-                                const float *gamma, const float *beta, int act, float *g, float *dw1, float *db1,
-                                float *dw2, float *db2, float *bnpart, float *workspace, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,

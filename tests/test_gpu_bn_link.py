@@ -253,12 +253,9 @@ def test_mbconv_blocks_linked_vs_unlinked(monkeypatch):
     assert c0.get('ewvit_bn_bwd_partials', 0) == 0
     assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == 4
     assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == 3          # 6.0's depthwise is stride 2
-    # tails of 5.7, 5.8, 6.0 — 6.0's only when 6.1's expand input gradient (K = 1536 over 13 row
-    # tiles) runs on the LDS-DMA kernel, not as the library GEMM (ewvit.conv._libgemm)
-    import ewvit.conv as ec
-    lib = int(ec._libgemm(N * 7 * 7, 256, 1536))
-    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 3 - lib
-    assert c1.get('ewvit_bn_bwd_partials', 0) == 6 - lib
+    # the tails of 5.7, 5.8, 6.0
+    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 3
+    assert c1.get('ewvit_bn_bwd_partials', 0) == 6
     assert _cos(y0, y1) > 0.9999 and float((y0 - y1).abs().max()) <= 5e-2 * float(y0.abs().max())
     assert _cos(gx0, gx1) > 0.9995
     # a BatchNorm bias whose output gradient passes only through train-mode BatchNorms (and
@@ -291,16 +288,12 @@ def test_mbconv_stages_link_count(monkeypatch):
     nblk = 30
     assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == nblk
     assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == nblk - 2          # blocks 4.0 / 6.0 are stride 2
-    # the last tail has no conv after it; the tails before the stage-6 expands that run as the
-    # library GEMM (ewvit.conv._libgemm: K = 1536 over few row tiles) run their own reduction
-    import ewvit.conv as ec
-    lib = 14 if ec._libgemm(N * 7 * 7, 256, 1536) else 0
-    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == nblk - 1 - lib
-    assert c1.get('ewvit_bn_bwd_partials', 0) == 2 * nblk - 3 - lib
+    # the last tail has no conv after it
+    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == nblk - 1
+    assert c1.get('ewvit_bn_bwd_partials', 0) == 2 * nblk - 3
     nbwd = c1.get('ewvit_bn_bwd', 0) + c1.get('ewvit_bn_bwd_scaled', 0) + c1.get('ewvit_bn_bwd_partials', 0)
     assert nbwd == 2 * nblk, c1
-    if not lib:
-        assert c1.get('ewvit_bn_bwd', 0) == 2 and c1.get('ewvit_bn_bwd_scaled', 0) == 1
+    assert c1.get('ewvit_bn_bwd', 0) == 2 and c1.get('ewvit_bn_bwd_scaled', 0) == 1
     assert bool(torch.isfinite(y1).all()) and bool(torch.isfinite(gx1).all())
     assert all(bool(torch.isfinite(v).all()) for v in gp1.values())
 
@@ -440,48 +433,6 @@ def test_conv_dgrad_bn_row_groups(cap):
         assert ea < 1e-5 and eb < 1e-5, (lv, ea, eb)
 
 
-def test_mwt_linked_vs_unlinked(monkeypatch):
-    """The MWT branch (training step of MWT(3, 128, 3) with its convs capped as in DAMA): with
-    the links its hf_conv seperate and fusion BatchNorms (per-level statistics) take their
-    backward sums from the fusion / multiscale convs' input gradients; forward bit-identical,
-    gradients equal to the fp32 summation order."""
-    import ewvit
-    import ewvit.bn as ebn
-    from network.mwt import MWT
-    L = ewvit._lib
-    g = torch.Generator().manual_seed(3)
-    x = torch.randn(4, 3, 64, 64, generator=g).to(DEV)
-    res = {}
-    monkeypatch.setattr(ebn, 'BWD_LINK_BIG', True)       # off by default (measured slower); the path is kept
-    for linked in (False, True):
-        monkeypatch.setattr(ebn, '_BWD_LINK', linked)
-        torch.manual_seed(2)
-        m = MWT(3, 128, 3).to(DEV).train()
-        calls = {}
-        real = L.call
-
-        def count(name, *a, **k):
-            calls[name] = calls.get(name, 0) + 1
-            return real(name, *a, **k)
-        monkeypatch.setattr(L, 'call', count)
-        try:
-            with torch.autocast('cuda', dtype=torch.bfloat16), ewvit._lib.grid_cap(24):
-                y = m(x)
-            y.float().square().mean().backward()
-        finally:
-            monkeypatch.setattr(L, 'call', real)
-        torch.cuda.synchronize()
-        res[linked] = (y.detach().float(), {n: p.grad.float() for n, p in m.named_parameters() if p.grad is not None},
-                       calls)
-    y0, g0, c0 = res[False]
-    y1, g1, c1 = res[True]
-    assert torch.equal(y0, y1)
-    assert c0.get('ewvit_bn_bwd_partials', 0) == 0 and c1.get('ewvit_bn_bwd_partials', 0) == 2
-    assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 2
-    worst = min((_cos(g0[n], g1[n]), n) for n in g0 if g0[n].abs().max() > 0 and not n.endswith('bias'))
-    assert worst[0] > 0.999, worst
-
-
 def test_stale_offer_not_taken():
     """A BatchNorm's link offer dies with its output: a later tensor at the same address and
     shape (the caching allocator reuses blocks) does not pick it up."""
@@ -490,9 +441,43 @@ def test_stale_offer_not_taken():
     x = torch.empty_like(y)
     m = torch.zeros(1, 8, device=DEV)
     ebn.offer_bwd_link(y, x, m, m, None, None, 0)
-    key = ebn._bwd_offered.key
+    key = ebn._tls.offered.key
     del y
     z = torch.empty(2, 8, 4, 4, dtype=torch.bfloat16, device=DEV)
     if (z.data_ptr(), tuple(z.shape), z.dtype) == key:
         assert ebn.take_bwd_link(z) is None
-    ebn._bwd_offered = None
+    ebn._tls.offered = None
+
+
+@pytest.mark.parametrize('kind', ['grouped', 'drop_add'])
+def test_dwconv_refuses_links_it_cannot_sum(kind, monkeypatch):
+    """ewvit_dwconv3x3_bwd_data_bn leaves whole-map, unscaled backward sums, so the
+    depthwise conv must not take the link of a grouped BatchNorm (per-level statistics, e.g.
+    the MWT's) nor of a BNDropAdd tail (drop-path row scale): with the links on, the gradients
+    equal the EWVIT_BN_BWD_LINK=0 ones (the BN's own reduction pass runs)."""
+    import ewvit
+    import ewvit.bn as ebn
+    g = torch.Generator().manual_seed(21)
+    N, C, H = 8, 64, 14
+    x = (torch.randn(N, C, H, H, generator=g) * 0.7 + 0.2).to(DEV, torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    skip = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wdw = (torch.randn(C, 1, 3, 3, generator=g) / 3).to(DEV)
+    dyo = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for linked in (False, True):
+        monkeypatch.setattr(ebn, '_BWD_LINK', linked)
+        torch.manual_seed(4)
+        bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+        xi = x.clone().requires_grad_(True)
+        if kind == 'grouped':
+            h = ewvit.batch_norm_act(xi, bn, 'silu', groups=2)
+        else:
+            h = ewvit.bn.batch_norm_drop_add(xi, bn, skip, 0.5)
+        y = ewvit.dwconv3x3(h, wdw.requires_grad_(True))
+        y.backward(dyo)
+        torch.cuda.synchronize()
+        res.append((xi.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+        wdw = wdw.detach()
+    for a, b in zip(*res):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)

@@ -12,24 +12,20 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.fixture(params=[1, 9, 13, 15, 2, 3, 4, 0, 'w1', 'w2', 'w3', 'k2'],
-                ids=['glds1', 'glds9', 'glds13', 'glds15', 'glds2', 'glds3', 'glds4', 'regstage',
-                     'glds9-wgw1', 'glds9-wgw2', 'glds9-wgw3', 'glds9-wkg2'])
+@pytest.fixture(params=[1, 0, 'wide', 'narrow'], ids=['glds', 'regstage', 'glds-wgrad-wide', 'glds-wgrad-narrow'])
 def glds(request):
-    """Run each case on every LDS-DMA configuration and on the register-staged kernels;
-    'wN': glds9 with 256-column weight-gradient tiles of variant N (the others: auto, 4);
-    'k2': glds9 with two K-groups per weight-gradient workgroup (off by default)."""
+    """Run each case on the LDS-DMA kernels (weight gradient: auto tile width, always the
+    256-column tiles where the shape allows them, never) and on the register-staged kernels
+    (the fallback of the shapes the LDS-DMA kernels refuse)."""
     import ewvit
     lib = ewvit._lib.load()
     p = request.param
-    v, w = (9, int(p[1])) if isinstance(p, str) and p[0] == 'w' else ((9, 4) if p == 'k2' else (p, 4))
+    v, w = (1, {'wide': 2, 'narrow': 0}[p]) if isinstance(p, str) else (p, 4)
     prev = lib.ewvit_conv2d_set_glds(v)
     prevw = lib.ewvit_conv2d_set_wgrad_wide(w)
-    prevk = lib.ewvit_conv2d_set_wgrad_kgroups(2 if p == 'k2' else 1)
     yield v
     lib.ewvit_conv2d_set_glds(prev)
     lib.ewvit_conv2d_set_wgrad_wide(prevw)
-    lib.ewvit_conv2d_set_wgrad_kgroups(prevk)
 
 
 def rel(a, b):
@@ -71,7 +67,7 @@ def rel(a, b):
     (1, 24, 24, 8, 7, 5, 1, 3),          # one 16-wide output tile, rows < the band height
     (2, 16, 16, 64, 10, 16, 1, 3),       # small-channel wgrad (W % 8 == 0): 16 -> 64 with bias
     (3, 24, 24, 24, 7, 24, 1, 3),        # small-channel wgrad, odd H (a 1-row tail band)
-    (64, 160, 160, 960, 14, 14, 1, 1),   # bench-size stage-5 expand: many pixel splits (two K-groups)
+    (64, 160, 160, 960, 14, 14, 1, 1),   # bench-size stage-5 expand: many pixel splits
     (64, 256, 256, 1536, 7, 7, 1, 1),    # bench-size stage-6 expand
 ])
 def test_conv_fwd_bwd(N, Cx, Cin, Cout, H, W, stride, k, glds):
@@ -193,26 +189,18 @@ def test_step_wide_weight_packing():
     assert not torch.equal(ref[0][0], ref2[0][0])
 
 
-@pytest.mark.parametrize('N,Cin,Cout,H', [(64, 1536, 256, 7), (64, 256, 1536, 7), (8, 1024, 64, 14)])
-def test_conv_1x1_library_gemm_route(N, Cin, Cout, H, monkeypatch):
-    """1x1 stride-1 convs with <= 64 128x128 tiles over K >= 1024 (the stage-6 project forward,
-    the stage-6 expand input gradient) run as hipBLASLt GEMMs on the channels-last views: the
-    same results as the LDS-DMA kernel up to fp32 summation order and the bf16 rounding, the skip
-    gradient added before the rounding, and no BatchNorm partial rows offered for the forward."""
+def test_conv_big_narrow_dgrad_256_row_blocks():
+    """A <= 64-column input gradient over > 4096 row tiles takes 256-row blocks (the MWT fusion
+    conv's 56-channel dgrad over 2.4 M pixels): against torch's fp32 conv on the GPU for the same
+    bf16-rounded operands."""
     import ewvit.conv as ec
-    g = torch.Generator().manual_seed(Cin + Cout)
+    g = torch.Generator().manual_seed(56)
+    N, Cin, Cout, H = 44, 56, 128, 112            # 551,936 pixels = 4312 row tiles
     x = torch.randn(N, Cin, H, H, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
-    w = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).to(DEV)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).to(DEV)
     dy = torch.randn(N, Cout, H, H, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
-    outs = []
-    for lib in (False, True):
-        monkeypatch.setattr(ec, '_LIBGEMM', lib)
-        xd, wd = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
-        y = ec.conv2d(xd, wd, None, 1)
-        y.backward(dy)
-        outs.append((y.float(), xd.grad.float(), wd.grad))
-        routed_fwd = ec._libgemm(N * H * H, Cout, Cin)
-        assert (ec.bn_stat_rows(x, w, 1) == 0) == (lib and routed_fwd)
-    for a, b in zip(*outs):
-        assert rel(a, b) < 2 ** -7
-    assert ec._libgemm(N * H * H, Cout, Cin) or ec._libgemm(N * H * H, Cin, Cout)
+    xd = x.clone().requires_grad_(True)
+    ec.conv2d(xd, w, None, 1).backward(dy)
+    xr = x.float().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, w.to(torch.bfloat16).float(), None, padding=1).backward(dy.float())
+    assert rel(xd.grad, xr.grad) < 2 ** -7

@@ -53,7 +53,13 @@ def _mwt_pair():
     return m, copy.deepcopy(m)
 
 
-def test_rccl_collectives_recorded_in_step_graph(nccl_world1):
+@pytest.mark.parametrize('mode', ['relaxed', 'global'])
+def test_rccl_collectives_recorded_in_step_graph(nccl_world1, mode, monkeypatch):
+    """`relaxed` (the default) capture needs no drain: the NCCL watchdog's event queries from
+    its own thread are legal during it.  `global` needs the watchdog's queue empty when the
+    capture begins: TrainStep waits for its progress marker (ewvit.graph.retire_eager_collectives)
+    — no sleep, no timing assumption."""
+    monkeypatch.setenv('EWVIT_CAPTURE_MODE', mode)
     import ewvit
     from ewvit.graph import TrainStep
     a, b = _mwt_pair()

@@ -149,13 +149,12 @@ def test_dropout_mask_changes_per_replay():
     assert not torch.equal(m1, m2)
 
 
-@pytest.mark.parametrize('wgrad_stream', [False, True])
-def test_grad_slots_adopted_and_multi_use(wgrad_stream):
+def test_grad_slots_adopted_and_multi_use():
     """ewvit.grads slots: a conv / linear weight used once gets its gradient written into the
     flat buffer and ADOPTED by AccumulateGrad (no clone: the gradient's storage is the slot's
     when the first post-accumulate hook sees it); a weight used twice in one forward gets the
-    sum of both uses (fresh outputs, not one shared slot).  With the wgrad stream on, the conv
-    wgrads run on the side stream and must give the same gradients."""
+    sum of both uses (fresh outputs, not one shared slot).  The backward runs on autograd's
+    device thread: the ops carry the forward thread's step id to it (ewvit.grads.note_use)."""
     from ewvit import grads, ops
     from ewvit.conv import conv2d
     from ewvit.graph import GradBuckets
@@ -181,15 +180,12 @@ def test_grad_slots_adopted_and_multi_use(wgrad_stream):
     for i, p in enumerate(params):           # registered before GradBuckets' hooks: runs first
         p.register_post_accumulate_grad_hook(lambda q, i=i: stolen.__setitem__(i, q.grad.data_ptr()))
     gb = GradBuckets(params)
-    prev = grads.set_wgrad_stream(wgrad_stream)
     try:
         gb.begin()
         grads.begin_step()
         fwd().backward()
-        grads.wgrad_join()
         torch.cuda.synchronize()
     finally:
-        grads.set_wgrad_stream(prev)
         gb.remove()
     for i, (p, r) in enumerate(zip(params, ref)):
         assert p.grad.data_ptr() == gb.views[i].data_ptr()

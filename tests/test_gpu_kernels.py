@@ -352,66 +352,6 @@ def test_depthwise_fwd_bwd_vs_torch(N, C, H, stride, dtype):
     assert rel_err(wd.grad, wr.grad) < 1e-5 if dtype == torch.float32 else rel_err(wd.grad, wr.grad) < 1e-4
 
 
-@pytest.mark.parametrize('segs', [2, 4])
-@pytest.mark.parametrize('N,C,H,stride', [(8, 64, 7, 1), (8, 64, 9, 1), (8, 32, 14, 1), (4, 32, 28, 2)])
-def test_depthwise_column_segments_identical(segs, N, C, H, stride):
-    """the column-segment split of the row kernels (ewvit_dwconv3x3_set_segs) gives
-    bit-identical results to whole rows, fwd and input gradient, for Wo in {7, 9, 14}."""
-    import ewvit
-    from ewvit import _lib
-    g = torch.Generator().manual_seed(H * 10 + segs)
-    x = torch.randn(N, C, H, H, generator=g).bfloat16().to(DEV).to(memory_format=torch.channels_last)
-    w = torch.randn(C, 1, 3, 3, generator=g).to(DEV)
-    dy = torch.randn(N, C, (H - 1) // stride + 1, (H - 1) // stride + 1, generator=g).bfloat16().to(DEV)
-    outs = []
-    try:
-        for s in (1, segs):
-            _lib.call('ewvit_dwconv3x3_set_segs', s)
-            xd = x.clone().requires_grad_(True)
-            y = ewvit.dwconv3x3(xd, w, stride, 1)
-            y.backward(dy)
-            outs.append((y.detach().clone(), xd.grad.clone()))
-    finally:
-        _lib.call('ewvit_dwconv3x3_set_segs', 1)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize('N,C,H,stride', [(16, 1536, 7, 1), (16, 960, 14, 1), (8, 256, 28, 2), (8, 960, 14, 2),
-                                          (3, 200, 9, 1), (2, 64, 5, 2)])
-def test_depthwise_pixel_kernel_identical_to_rows(N, C, H, stride):
-    """The per-pixel depthwise kernel (ewvit_dwconv3x3_set_pix) gives the row kernels' bits:
-    forward and stride-1 input gradient, with and without the BatchNorm sums (the sums of the
-    same stored values, added in another order: 1e-5)."""
-    import ewvit
-    from ewvit import _lib
-    lib = _lib.load()
-    g = torch.Generator().manual_seed(C + H)
-    x = torch.randn(N, C, H, H, generator=g).bfloat16().to(DEV).to(memory_format=torch.channels_last)
-    w = torch.randn(C, 1, 3, 3, generator=g).to(DEV)
-    Ho = (H - 1) // stride + 1
-    dy = torch.randn(N, C, Ho, Ho, generator=g).bfloat16().to(DEV).to(memory_format=torch.channels_last)
-    outs = []
-    prev = lib.ewvit_dwconv3x3_set_pix(0)
-    try:
-        for pix in (0, 1 << 20):
-            lib.ewvit_dwconv3x3_set_pix(pix)
-            xd = x.clone().requires_grad_(True)
-            y = ewvit.dwconv3x3(xd, w, stride, 1)
-            y.backward(dy)
-            nrc = int(lib.ewvit_dwconv3x3_bn_rows(N, H, H, C, stride, 0))
-            part = torch.empty(nrc, 2 * C, device=DEV)
-            so = torch.empty(C, device=DEV)
-            y2 = torch.empty_like(y)
-            _lib.call('ewvit_dwconv3x3_fwd_bn', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y2), N, H, H, C, stride, None,
-                      _lib.ptr(part), _lib.ptr(so), _lib.stream(x))
-            torch.cuda.synchronize()
-            outs.append((y.detach().clone(), xd.grad.clone(), y2, part.double().sum(0)))
-    finally:
-        lib.ewvit_dwconv3x3_set_pix(prev)
-    a, b = outs
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
-    assert float((a[3] - b[3]).abs().max()) <= 1e-5 * float(a[3].abs().max())
-
 
 def test_hf_upsample_padded_channels():
     """out_channels > 3C: the bands in channels 0..3C-1 (the unpadded result up to one

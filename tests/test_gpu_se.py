@@ -278,48 +278,3 @@ def test_bn_act_se_squeeze_matches_separate_passes(N, C, H, csq, monkeypatch):
         assert torch.equal(u, v)
     for u, v in zip(a[6], b[6]):
         assert torch.equal(u, v)
-
-
-@pytest.mark.parametrize('N,C,H,csq', [(64, 960, 14, 40), (64, 1536, 7, 64), (3, 200, 5, 6)])
-def test_bn_act_se_backward_sums_in_se_squeeze(N, C, H, csq, monkeypatch):
-    """The BatchNorm backward's sums taken per frame by the SE backward's squeeze kernel
-    (ewvit_se_squeeze_mlp_bwd_bn + ewvit_bn_bwd_se_partials) against the reduction pass
-    (ewvit_bn_bwd_se): the SE gradients are bit-identical (same ds), the BatchNorm's input and
-    parameter gradients differ only by the fp32 summation order of sum g, sum g*xhat (frame sums
-    s*A1 + g*A2 instead of row sums of (dy*s + g)*act')."""
-    import ewvit
-    import ewvit.se as ese
-    g = torch.Generator().manual_seed(C + H + 1)
-    x = (torch.randn(N, C, H, H, generator=g) * 0.7 + 0.2).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
-    wd = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV)
-    w1 = (torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5).to(DEV)
-    b1 = (torch.randn(csq, generator=g) * 0.1).to(DEV)
-    w2 = (torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5).to(DEV)
-    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
-    dy = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
-    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.2
-    outs = []
-    for sums in (False, True):
-        monkeypatch.setattr(ese, '_SE_BN_SUMS', sums)
-        bn = torch.nn.BatchNorm2d(C, eps=1e-3).train().to(DEV)
-        with torch.no_grad():
-            bn.weight.copy_(gamma)
-            bn.bias.copy_(beta)
-        xd = x.clone().requires_grad_(True)
-        ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
-        r = ewvit.ops.dwconv3x3_bn_stats(xd, wd, 1, bn.running_mean)
-        assert r is not None
-        y = ewvit.bn_act_se(r[0], bn, 'silu', *ps, partials=r[1:])
-        y.backward(dy)
-        torch.cuda.synchronize()
-        outs.append((y.detach(), [p.grad for p in ps], xd.grad.float(), bn.weight.grad, bn.bias.grad))
-    a, b = outs
-    assert torch.equal(a[0], b[0])
-    for u, v in zip(a[1], b[1]):
-        assert torch.equal(u, v)
-    scale = float(a[2].abs().max())
-    assert float((a[2] - b[2]).abs().max()) <= 2 ** -7 * scale
-    cosv = float(torch.nn.functional.cosine_similarity(a[2].flatten().double(), b[2].flatten().double(), dim=0))
-    assert cosv >= 0.99999, cosv
-    for u, v in zip(a[3:], b[3:]):
-        assert float((u - v).abs().max()) <= 1e-4 * float(u.abs().max()) + 1e-6
