@@ -6,6 +6,11 @@ backward, no optimizer) replayed alone from a HIP graph, timed with events over 
   sfe        the SFE branch (EfficientNetV2-S backbone + ViT head) alone
   full       the whole DeepfakeDetector forward + combined_loss + backward (both streams)
   step       `full` + Adam (the bench's TrainStep)
+  backbone   the EfficientNetV2-S features alone
+  tokens     the token path alone: sfe.head (patch_to_embedding, CLS/pos, ViT) on a fixed
+             backbone map, the cross-attention, gates, classifier and combined_loss, fwd + bwd
+  probe      (--probe-us U) the step with a U-us spin kernel on the main stream right before
+             the cross-attention: how much of a forward token-path microsecond the step pays
 
 Usage: python tools/branch_time.py [--reps 20]
 """
@@ -51,6 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--tables', type=int, default=0, help='also print per-entry tables (N top launch configs)')
+    ap.add_argument('--probe-us', type=float, default=0.0)
     args = ap.parse_args()
     import bench
     import ewvit
@@ -80,6 +86,48 @@ def main():
     out['mwt_cap_ms'] = _time(piece(mwt_capped), args.reps)
     out['mwt_cap'] = cap
     out['sfe_ms'] = _time(piece(lambda: dama.sfe(x)), args.reps)
+    out['backbone_ms'] = _time(piece(lambda: dama.sfe.efficient_net.features(x)), args.reps)
+    from network.losses import combined_loss
+    feat = torch.randn(64, 1280, 7, 7, device=dev).to(memory_format=torch.channels_last).requires_grad_(True)
+    freq0 = torch.randn(64, 128, 1, 1, device=dev).requires_grad_(True)
+    labels = (torch.arange(64, device=dev) % 2).float().view(8, 8)[:, 0]
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
+
+    def tokens():
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            space = dama.sfe.head(feat).float()
+            B = space.shape[0]
+            s_enh, f_enh = dama.cross_att(space.flatten(2).transpose(1, 2), freq0.flatten(2).transpose(1, 2))
+            sp, fr = s_enh.transpose(1, 2).reshape(B, -1, 1, 1), f_enh.transpose(1, 2).reshape(B, -1, 1, 1)
+            cat = torch.cat([sp, fr], dim=1)
+            fused = dama.fusion_gate(cat)
+            gw = dama._gate(cat)
+            wsum = gw[:, 0].view(B, 1, 1, 1) * sp + gw[:, 1].view(B, 1, 1, 1) * fr + gw[:, 2].view(B, 1, 1, 1) * fused
+            d = {k: v.reshape(8, 8, -1).mean(1) for k, v in (('fused', wsum), ('space', sp), ('freq', fr))}
+            out_ = {'logits': model._classify(d['fused']), **d}
+        return combined_loss(out_, labels, crit, 1, 1)[0]
+    out['tokens_ms'] = _time(TrainStep(model, tokens, _NoOpt(model.parameters()), graph=True), args.reps)
+    if args.probe_us > 0:
+        from network import dama as dm
+        cyc = int(args.probe_us * 2100)
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(cyc)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=side):
+                torch.cuda._sleep(cyc)
+        out['probe_alone_ms'] = _time(g.replay, args.reps)
+        orig = dm.BidirectionalCrossTransformer.forward
+
+        def slowed(self, s, f):
+            torch.cuda._sleep(cyc)
+            return orig(self, s, f)
+        dm.BidirectionalCrossTransformer.forward = slowed
+        try:
+            out['step_probe_ms'] = _time(bench.build_step(dev, 64, 0, graph=True, config=2), args.reps)
+        finally:
+            dm.BidirectionalCrossTransformer.forward = orig
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
     if args.tables:
         # per-entry event timings of each piece issued eagerly, one stream, uncapped
