@@ -100,6 +100,9 @@ SIGNATURES = {
                                     _vp],
     'ewvit_bn_bwd_partials': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp,
                               _i32, _i32, _vp],
+    'ewvit_head_fwd': [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_head_bwd': [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
+                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_bwd_data_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
                                  _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
 }
@@ -123,6 +126,7 @@ QUERIES = {
     'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_head_workspace': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
 }
 

