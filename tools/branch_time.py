@@ -8,7 +8,8 @@ backward, no optimizer) replayed alone from a HIP graph, timed with events over 
   step       `full` + Adam (the bench's TrainStep)
   backbone   the EfficientNetV2-S features alone
   tokens     the token path alone: sfe.head (patch_to_embedding, CLS/pos, ViT) on a fixed
-             backbone map, the cross-attention, gates, classifier and combined_loss, fwd + bwd
+             backbone map, then the step's own DAMA head (the fused cross-attention / gates
+             launch when fusable), classifier and combined_loss, fwd + bwd
   probe      (--probe-us U) the step with a U-us spin kernel on the main stream right before
              the cross-attention: how much of a forward token-path microsecond the step pays
 
@@ -93,18 +94,17 @@ def main():
     labels = (torch.arange(64, device=dev) % 2).float().view(8, 8)[:, 0]
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
 
+    xv = torch.zeros(8, 8, 3, 8, 8, device=dev)      # frames are not read: the branches are stubbed
+
     def tokens():
-        with torch.autocast('cuda', dtype=torch.bfloat16):
-            space = dama.sfe.head(feat).float()
-            B = space.shape[0]
-            s_enh, f_enh = dama.cross_att(space.flatten(2).transpose(1, 2), freq0.flatten(2).transpose(1, 2))
-            sp, fr = s_enh.transpose(1, 2).reshape(B, -1, 1, 1), f_enh.transpose(1, 2).reshape(B, -1, 1, 1)
-            cat = torch.cat([sp, fr], dim=1)
-            fused = dama.fusion_gate(cat)
-            gw = dama._gate(cat)
-            wsum = gw[:, 0].view(B, 1, 1, 1) * sp + gw[:, 1].view(B, 1, 1, 1) * fr + gw[:, 2].view(B, 1, 1, 1) * fused
-            d = {k: v.reshape(8, 8, -1).mean(1) for k, v in (('fused', wsum), ('space', sp), ('freq', fr))}
-            out_ = {'logits': model._classify(d['fused']), **d}
+        # the step's own forward after the two branches (DAMA._process_frame: the fused head
+        # when fusable), the classifier and combined_loss, on a fixed backbone map
+        dama._branches = lambda frame: (dama.sfe.head(feat).float(), freq0)
+        try:
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                out_ = model(xv, 8, 'dynamic')
+        finally:
+            del dama._branches
         return combined_loss(out_, labels, crit, 1, 1)[0]
     out['tokens_ms'] = _time(TrainStep(model, tokens, _NoOpt(model.parameters()), graph=True), args.reps)
     if args.probe_us > 0:
