@@ -2,9 +2,11 @@
 branches (reference network/dama.py:143-169): the 2-layer bidirectional cross-attention, the
 fusion gate (centre-tap conv + BatchNorm + ReLU), the gate net and the 3-way weighted sum.
 
-Forward: ONE launch (one workgroup); backward: one workgroup for the activation gradients and
-one grid for the parameter gradients.  The module-by-module path (network/dama.py) issues
-~90 small launches for the same work; it stays for hooked / patched modules, fp8 token GEMMs
+Forward: one workgroup per 16 frames (the attention blocks, fusion conv and gate input layer,
+LDS-resident) + one workgroup for the frame-coupled tail (BatchNorm over the frames, gate
+softmax, weighted sum); backward: the tail, the frame groups in reverse, and one grid for the
+parameter gradients.  The module-by-module path (network/dama.py) issues ~90 small launches
+for the same work; it stays for hooked / patched modules, fp8 token GEMMs
 and shapes outside this kernel's class (dim 128, 4 heads of 32, depth 2, <= 64 frames).
 """
 import ctypes

@@ -69,7 +69,7 @@ def _run(m, s0, f0, fused_path, monkeypatch):
     return {k: v.detach().float() for k, v in out.items()}, s.grad, f.grad, grads, bufs, calls
 
 
-@pytest.mark.parametrize('N', [64, 8, 5])
+@pytest.mark.parametrize('N', [64, 37, 8, 5])
 @pytest.mark.parametrize('training', [True, False])
 def test_head_matches_module_path(N, training, monkeypatch):
     import copy
@@ -142,6 +142,45 @@ def test_head_dropout_fresh_masks_and_consistent_backward(monkeypatch):
         outs.append(fused.detach().clone())
     assert not torch.equal(outs[0], outs[1])
     assert bool(torch.isfinite(outs[0]).all())
+
+
+def test_head_launch_time():
+    """The head's forward (2 launches) and backward (3 launches) at the headline's 64 frames, from
+    a replayed HIP graph (events over 50 replays).  The bound catches a latency-serialised
+    design (a single-workgroup version took 0.39 ms forward / 0.57 ms backward)."""
+    import ewvit
+    m = _dama(True)
+    s0 = torch.randn(64, 128, device=DEV, requires_grad=True)
+    f0 = torch.randn(64, 128, device=DEV, requires_grad=True)
+    gF, gS, gFr = (torch.randn(64, 128, device=DEV) for _ in range(3))
+
+    def step():
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            fused, s, f = ewvit.head.dama_head(m, s0, f0, 0)
+        torch.autograd.backward([fused, s, f], [gF, gS, gFr])
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    for t in [s0, f0, *m.parameters()]:
+        t.grad = None                 # the captured backward assigns .grad (no accumulation kernels)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    times = {}
+    for name, fn in (('fwd+bwd', g.replay),):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        a.record()
+        for _ in range(50):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        times[name] = a.elapsed_time(b) / 50 * 1e3
+    print(f'head fwd+bwd at N=64: {times["fwd+bwd"]:.1f} us per replay (graph)')
+    assert times['fwd+bwd'] < 250.0, times
 
 
 def test_head_refused_for_hooked_modules():

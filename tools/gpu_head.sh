@@ -1,6 +1,8 @@
 #!/bin/bash
 set -o pipefail
 O=gpurun_out; mkdir -p $O
-timeout -k 10 120 python -u tools/fr_probe.py > $O/fr_probe.log 2>&1; echo "probe rc=$?"
+export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_head.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider > $O/head_tests.log 2>&1
-rc=$?; echo "head tests rc=$rc"; tail -4 $O/head_tests.log; exit $rc
+rc=$?; echo "head tests rc=$rc"; grep -E "us per replay|passed|failed|Error" $O/head_tests.log | tail -5
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_head -o run -- python -m pytest tests/test_gpu_head.py -q -k launch_time -p no:cacheprovider > $O/prof_head.log 2>&1
+echo "prof rc=$?"; exit $rc
