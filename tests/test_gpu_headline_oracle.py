@@ -24,7 +24,8 @@ from the fp32 oracle on `fused` and 0.105 on the logits, and its weight-gradient
 0.92-0.99; three more autocast runs on x with 2^-8 relative input noise spread the same way
 (round-4 measurement, profiles/r04/headline.log).  A metric therefore passes when it meets the
 §8c-style bound OR is no further from the oracle than YARD_X x the furthest of those four bf16
-reference runs (measured in this test), and it must always sit inside a fixed floor.
+reference runs (measured in this test; YARD_NORM_X for weight-gradient norm ratios), and it must
+always sit inside a fixed floor.
 """
 import copy
 import os
@@ -64,6 +65,8 @@ GRAD_COS = {
 }
 STAT_TOL = 2e-2
 YARD_X = 1.5      # allowed distance to the oracle, as a multiple of the furthest bf16 reference run
+YARD_NORM_X = 2.0  # ... for a weight gradient's norm ratio: the gate logits' gradients are differences
+                   # of near-equal terms (softmax over 3 gates); the 4 reference runs alone spread 7-14 %
 STATS = ['dama.mwt.hf_conv.fusion.1.running_mean', 'dama.mwt.hf_conv.seperate.2.1.running_var',
          'dama.mwt.multiscale_fusion.1.running_var', 'dama.mwt.freq_pool.2.running_mean',
          'dama.fusion_gate.1.running_mean', 'dama.fusion_gate.1.running_var',
@@ -128,18 +131,18 @@ def test_headline_chunk_train_step_vs_oracle():
 
     fails = []
 
-    def judge(kind, prod, yards, tol, cmin, floor_err, floor_cos):
+    def judge(kind, prod, yards, tol, cmin, floor_err, floor_cos, xe=YARD_X):
         """prod / yards: (err, cos) of the product / of each bf16 yardstick run vs the oracle.
         Pass: within the §8c-style bound (tol, cmin), or no further from the oracle than
         YARD_X x the furthest bf16 reference run — and always inside the absolute floors."""
         ye = max(y[0] for y in yards)
         yc = min(y[1] for y in yards)
-        ok_err = prod[0] <= tol or prod[0] <= YARD_X * ye
+        ok_err = prod[0] <= tol or prod[0] <= xe * ye
         ok_cos = prod[1] >= cmin or (1 - prod[1]) <= YARD_X * (1 - yc)
         ok = ok_err and ok_cos and prod[0] <= floor_err and prod[1] >= floor_cos
         print(f'{"" if ok else "FAIL "}{kind:60s} product err {prod[0]:.4f} cos {prod[1]:.6f} | bf16 reference runs: '
               f'max err {ye:.4f} min cos {yc:.6f}')
-        log('err_of_scale:' + kind, prod[0], max(tol, YARD_X * ye))
+        log('err_of_scale:' + kind, prod[0], max(tol, xe * ye))
         log('cos:' + kind, prod[1], min(cmin, 1 - YARD_X * (1 - yc)))
         if not ok:
             fails.append((kind, prod, ye, yc))
@@ -169,7 +172,7 @@ def test_headline_chunk_train_step_vs_oracle():
     for n, c in GRAD_COS.items():
         assert pp[n].grad is not None and oo[n].grad is not None, n
         judge('grad ' + n + ' (|norm ratio-1|, cos)', gmet(pp[n].grad, n), [gmet(y[2][n].grad, n) for y in yard],
-              0.05, c, 0.25, 0.88)
+              0.05, c, 0.25, 0.88, xe=YARD_NORM_X)
     ps, os_ = p.state_dict(), o.state_dict()
     for k in STATS:
         judge('stat ' + k, _errs(ps[k], os_[k]), [_errs(y[3][k], os_[k]) for y in yard], STAT_TOL, 0.999,
