@@ -101,7 +101,7 @@ __host__ __device__ inline int64_t head_ws_floats() { return W_TOTAL; }
       reinterpret_cast<uint64_t *>(ws_base + W_TOTAL - 256)[(k)] = wall_clock64();                    \
   } while (0)
 #else
-#define HTR(k) do {} while (0)
+#define HTR(k) do { (void)(k); } while (0)
 #endif
 __device__ inline HeadWs head_ws(float *b) { return HeadWs{b}; }
 
@@ -828,7 +828,6 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams p, cons
       D0 = ws.dy(); ldd = HD; o0 = (rr >> 4) * 16; k0 = (rr & 15) * 16;
       X0 = k0 < HD ? ws.st(4) + k0 : ws.st(5) + (k0 - HD); ldx = HD;
       out = g.wfg + 4 * g.fg_tap; ldo = g.fg_so; kstr = g.fg_si;
-      k0 = k0;   // output column; X0 already points at the k block
     } else {
       const int rr = T - 1024 - 128;
       D0 = ws.dh1(); ldd = 64; o0 = (rr >> 4) * 16; k0 = (rr & 15) * 16;
