@@ -1068,6 +1068,35 @@ extern "C" int ewvit_bn_bwd_partials(const void *dy, const void *x, void *dx, in
   return launch_status("bn_bwd_partials");
 }
 
+// The reduction pass of ewvit_bn_bwd alone: part [groups][nrc][2][C] (sum g, sum g * xhat) with
+// nrc = ewvit_bn_bwd_reduce_rows(M, C, groups), for a consumer that forms dx itself.
+extern "C" int ewvit_bn_bwd_reduce_rows(int64_t M, int64_t C, int groups) {
+  if (groups < 1 || M < 1 || C < 8 || C > 4096 || C % 8 || M % groups) return 0;
+  return bn_nrc(bn_geo(C), M / groups, groups);
+}
+
+extern "C" int ewvit_bn_bwd_reduce(const void *dy, const void *x, int dtype, int64_t M, int64_t C, const float *gamma,
+                                   const float *beta, const float *save_mean, const float *save_invstd, int act,
+                                   int groups, float *part, void *stream) {
+  EWVIT_CHECK_ARG(dy && x && save_mean && save_invstd && part && dtype_ok(dtype), "bn_bwd_reduce: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_bwd_reduce: C=%lld", (long long)C);
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd_reduce: act=%d", act);
+  EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M % groups == 0, "bn_bwd_reduce: %d groups", groups);
+  if (M == 0) return 0;
+  const int64_t Mg = M / groups;
+  const BnGeo geo = bn_geo(C);
+  const int nrc = bn_nrc(geo, Mg, groups);
+  const int64_t rpc = (Mg + nrc - 1) / nrc;
+  dim3 grid(nrc, geo.nch, groups);
+  hipStream_t s = as_stream(stream);
+#define BN_RED(DTV, ACTV)                                                                                           \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<DTV, ACTV>), grid, dim3(geo.threads), 0, s, dy, x, save_mean,           \
+                     save_invstd, gamma, beta, Mg, (int)C, geo.CC8, geo.RG, rpc, part)
+  BN_DISPATCH(BN_RED);
+#undef BN_RED
+  return launch_status("bn_bwd_reduce");
+}
+
 extern "C" int ewvit_bn_bwd(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C,
                             const float *gamma, const float *beta, const float *save_mean,
                             const float *save_invstd, int act, float *dgamma, float *dbeta, int accumulate,

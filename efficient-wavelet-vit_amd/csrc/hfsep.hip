@@ -52,7 +52,9 @@ struct HsParams {
 // pixel per 16-channel tile (weights-first MFMA operands), which it stores (8 B) and adds
 // into its running shifted sums; the block reduces them over its pixels at the end:
 // part[l][bx][c] = sum (y - K_c), part[l][bx][64 + c] = sum (y - K_c)^2.
-template <int TH>
+// A band's x rows are staged through registers: XP 16-B pieces per thread, all issued together
+// from clamped in-range addresses (one memory round trip per band, not one per piece).
+template <int TH, int XP>
 __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict__ x, bf16_t *__restrict__ y,
                                                         HsParams p, int Nl, int H, int W,
                                                         const float *__restrict__ shift, float *__restrict__ part,
@@ -99,19 +101,46 @@ __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict
       s2[t][i] = 0.f;
     }
   const int nbh = (H + TH - 1) / TH, nbands = Nl * nbh;
+  const int items = (TH + 2) * Wp * CC;
+  uint4 rx[XP];
+  unsigned okm = 0;                                 // which of this thread's pieces lie in the image
+  auto fetch = [&](int band) {
+    const int img = lvl * Nl + band / nbh, r0 = (band % nbh) * TH;
+    const int rows = H - r0 < TH ? H - r0 : TH;
+    okm = 0;
+    // piece i = tid + 256 k: pixel px = i / CC of the (TH + 2) x Wp halo image, walked
+    // incrementally (256 / CC pixels per step)
+    const int c8 = tid % CC;
+    int tr = (tid / CC) / Wp, tc = (tid / CC) - tr * Wp;
+    const bf16_t *ximg = x + (int64_t)img * H * W * HS_CIN + c8 * 8;
+#pragma unroll
+    for (int k = 0; k < XP; ++k) {
+      const int i = tid + 256 * k;
+      const int ir = r0 - 1 + tr, ic = tc - 1;
+      const bool ok = i < items && (unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && tr < rows + 2;
+      okm |= (unsigned)ok << k;
+      // unconditional load from a clamped address (no branch around the load), zeroed below
+      rx[k] = *reinterpret_cast<const uint4 *>(ximg + (ok ? ((int64_t)ir * W + ic) * HS_CIN : 0));
+      tc += 256 / CC;
+      while (tc >= Wp) { tc -= Wp; ++tr; }
+    }
+  };
   for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
     const int img = lvl * Nl + band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
-    const int items = (TH + 2) * Wp * CC;
+    fetch(band);
     __syncthreads();                               // the previous band's readers are done
-    for (int i = tid; i < items; i += 256) {
-      const int c8 = i % CC, px = i / CC;
-      const int tr = px / Wp, tc = px - tr * Wp;
-      const int ir = r0 - 1 + tr, ic = tc - 1;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if ((unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && tr < rows + 2)
-        v = *reinterpret_cast<const uint4 *>(x + (((int64_t)img * H + ir) * W + ic) * HS_CIN + c8 * 8);
-      *reinterpret_cast<uint4 *>(hs_smem + (size_t)tr * rowb + (tc * HS_CIN + c8 * 8) * 2) = v;
+    {
+      // LDS image offset of piece i: px * 32 + c8 * 16 bytes (rows of Wp pixels, 16 channels)
+      const int c8 = tid % CC;
+#pragma unroll
+      for (int k = 0; k < XP; ++k) {
+        const int i = tid + 256 * k;
+        if (i < items) {
+          const uint4 v = ((okm >> k) & 1u) ? rx[k] : make_uint4(0u, 0u, 0u, 0u);
+          *reinterpret_cast<uint4 *>(hs_smem + (size_t)(i / CC) * HS_CIN * 2 + c8 * 16) = v;
+        }
+      }
     }
     __syncthreads();
     const int npx = rows * W, ngr = (npx + 15) / 16;
@@ -197,9 +226,17 @@ __device__ __forceinline__ int hs_dsw(int r) { return ((r >> 1) & 3) << 1; }
 
 // DYI / XI: register-staged 16-B pieces per thread (dy, x): 7 / 4 cover W <= 112 at TH = 2
 // (the MWT's 112^2 levels), 13 / 7 cover W <= 200 (config 4's 192^2)
-template <int TH, int DYI, int XI>
+// BNB: dy is not given but recomputed per element from the BatchNorm + ReLU that follows the conv
+// (the grouped seperate BN, per-level statistics): dz (the gradient of the BN output), yb (the
+// BN input = this conv's output) and the per-(level, channel) table `bnt` [L][64][8] give
+// dy = gamma invstd (g' - mean(g') - xhat mean(g' xhat)), g' = dz [gamma xhat + beta > 0],
+// xhat = (y - mean) invstd, folded to dy = A g' + B y + C and the mask to P y + Q > 0 (table
+// {A, B, C, P, Q}) — the BN backward's dx pass, so dy never goes through memory.
+template <int TH, int DYI, int XI, bool BNB>
 __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy,
-                                                          float *__restrict__ part, int NI, int H, int W) {
+                                                          float *__restrict__ part, int NI, int H, int W,
+                                                          const bf16_t *__restrict__ yb, const float *__restrict__ bnt,
+                                                          int L, int Nl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char hs_smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);    // dy channels 16 wv .. 16 wv + 15
@@ -215,49 +252,95 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = hf32x4{0.f, 0.f, 0.f, 0.f};
   if (tid < 2) *reinterpret_cast<uint4 *>(ximg + zoff + tid * 16) = make_uint4(0u, 0u, 0u, 0u);
+  float *tab = reinterpret_cast<float *>(hs_smem + Pk * 128 + (nhalo + 1) * 32);   // BNB: [L][64][8]
+  if (BNB)
+    for (int e = tid; e < L * 64 * 8; e += 256) tab[e] = bnt[e];
   const int nbh = (H + TH - 1) / TH, nbands = NI * nbh;
   const int ndy = Pk * 8, nx = nhalo * 2;
-  uint4 rd[DYI], rx[XI];
+  uint4 rd[DYI], ry[BNB ? DYI : 1], rx[XI];
+  unsigned dok = 0, xok = 0;                   // which pieces are real (the loads are unconditional)
   auto fetch = [&](int band) {
     const int img = band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
     const int Pb = rows * W;
-    const bf16_t *dsrc = dy + ((int64_t)img * H + r0) * W * HS_COUT;
+    const int64_t dbase = ((int64_t)img * H + r0) * W * HS_COUT;
+    dok = 0;
+    xok = 0;
 #pragma unroll
     for (int k = 0; k < DYI; ++k) {
       const int i = tid + 256 * k;
-      rd[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < ndy && (i >> 3) < Pb) rd[k] = *reinterpret_cast<const uint4 *>(dsrc + (int64_t)(i >> 3) * HS_COUT + (i & 7) * 8);
+      const bool ok = i < ndy && (i >> 3) < Pb;
+      dok |= (unsigned)ok << k;
+      const int64_t off = ok ? dbase + (int64_t)(i >> 3) * HS_COUT + (i & 7) * 8 : 0;
+      rd[k] = *reinterpret_cast<const uint4 *>(dy + off);
+      if constexpr (BNB) ry[k] = *reinterpret_cast<const uint4 *>(yb + off);
     }
+    // x halo pieces: pixel h = i / 2 of the (TH + 2) x Wp image, walked incrementally
+    int hr = (tid >> 1) / Wp, hc = (tid >> 1) - hr * Wp;
+    const int c = tid & 1;
 #pragma unroll
     for (int k = 0; k < XI; ++k) {
       const int i = tid + 256 * k;
-      rx[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < nx) {
-        const int h = i >> 1, c = i & 1;
-        const int hr = h / Wp, hc = h - hr * Wp;
-        const int ir = r0 - 1 + hr, ic = hc - 1;
-        if ((unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && hr < rows + 2) {
-          rx[k] = *reinterpret_cast<const uint4 *>(x + (((int64_t)img * H + ir) * W + ic) * HS_CIN + c * 8);
-          if (c == 1) rx[k].w = (rx[k].w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
-        }
-      }
+      const int ir = r0 - 1 + hr, ic = hc - 1;
+      const bool ok = i < nx && (unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W && hr < rows + 2;
+      xok |= (unsigned)ok << k;
+      rx[k] = *reinterpret_cast<const uint4 *>(x + (ok ? (((int64_t)img * H + ir) * W + ic) * HS_CIN + c * 8 : 0));
+      hc += 128;
+      while (hc >= Wp) { hc -= Wp; ++hr; }
     }
   };
   if ((int)blockIdx.x < nbands) fetch(blockIdx.x);
   for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
     const int rows = H - (band % nbh) * TH < TH ? H - (band % nbh) * TH : TH;
     const int Pb = rows * W;
+    const int lvl = (band / nbh) / Nl;
+    // BNB: this thread's 8 channels ((tid & 7) * 8 + j: a piece's channels never change with k)
+    // as dy = A g' + B y + C, g' = g [P y + Q > 0]
+    float cst[BNB ? 8 : 1][5];
+    if constexpr (BNB) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int m = 0; m < 5; ++m) cst[j][m] = tab[(lvl * 64 + (tid & 7) * 8 + j) * 8 + m];
+    }
     __syncthreads();                               // the previous band's readers are done
 #pragma unroll
     for (int k = 0; k < DYI; ++k) {
       const int i = tid + 256 * k;
-      if (i < ndy) *reinterpret_cast<uint4 *>(dimg + (i >> 3) * 128 + 16 * ((i & 7) ^ hs_dsw(i >> 3))) = rd[k];
+      if (i < ndy) {
+        uint4 v = ((dok >> k) & 1u) ? rd[k] : make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (BNB) {
+          if ((dok >> k) & 1u) {
+            const unsigned dz[4] = {rd[k].x, rd[k].y, rd[k].z, rd[k].w};
+            const unsigned yv[4] = {ry[k].x, ry[k].y, ry[k].z, ry[k].w};
+            unsigned o[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              float d2[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int j = 2 * h + u;
+                const float g = __uint_as_float(u ? dz[h] & 0xffff0000u : dz[h] << 16);
+                const float yy = __uint_as_float(u ? yv[h] & 0xffff0000u : yv[h] << 16);
+                const float gp = fmaf(cst[j][3], yy, cst[j][4]) > 0.f ? g : 0.f;
+                d2[u] = fmaf(cst[j][0], gp, fmaf(cst[j][1], yy, cst[j][2]));
+              }
+              o[h] = (unsigned)f2bf(d2[0]) | ((unsigned)f2bf(d2[1]) << 16);
+            }
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+          }
+        }
+        *reinterpret_cast<uint4 *>(dimg + (i >> 3) * 128 + 16 * ((i & 7) ^ hs_dsw(i >> 3))) = v;
+      }
     }
 #pragma unroll
     for (int k = 0; k < XI; ++k) {
       const int i = tid + 256 * k;
-      if (i < nx) *reinterpret_cast<uint4 *>(ximg + i * 16) = rx[k];
+      if (i < nx) {
+        uint4 v = ((xok >> k) & 1u) ? rx[k] : make_uint4(0u, 0u, 0u, 0u);
+        if ((i & 1) && ((xok >> k) & 1u)) v.w = (v.w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
+        *reinterpret_cast<uint4 *>(ximg + i * 16) = v;
+      }
     }
     __syncthreads();
     if (band + (int)gridDim.x < nbands) fetch(band + gridDim.x);   // in flight under the MFMAs
@@ -317,11 +400,25 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
 // dW_g[o][ci][tap] = sum_b part[b][18g + o][tap * 16 + 3g + ci]; db_g[o] = sum_b
 // part[b][18g + o][4 * 16 + 15] (the ones channel at the centre tap).  Block: 64 outputs x
 // 4 slab quarters, combined in a fixed order.
-__global__ __launch_bounds__(256) void hfsep_wgrad_reduce_kernel(const float *__restrict__ part, int G, HsParams out) {
+// BNB launches: the last 2 blocks write the grouped BatchNorm's affine gradients, dbeta[c] =
+// sum_l sum g', dgamma[c] = sum_l sum g' xhat (lsum [L][128], levels in order).
+__global__ __launch_bounds__(256) void hfsep_wgrad_reduce_kernel(const float *__restrict__ part, int G, HsParams out,
+                                                                 const float *__restrict__ lsum = nullptr, int L = 0,
+                                                                 float *dgamma = nullptr, float *dbeta = nullptr) {
   __shared__ float red[4][64];
   const int tid = threadIdx.x, o64 = tid & 63, qtr = tid >> 6;
   const int idx = blockIdx.x * 64 + o64;              // 0 .. 54*27 + 54
   constexpr int NW = HS_REAL * 27;
+  if (lsum && (int)blockIdx.x >= (int)gridDim.x - 2) {
+    const int which = (int)gridDim.x - 1 - (int)blockIdx.x;      // 1: dbeta, 0: dgamma
+    if (qtr == 0) {
+      float v = 0.f;
+      for (int l = 0; l < L; ++l) v += lsum[l * 128 + (which ? 0 : 64) + o64];
+      float *dst = which ? dbeta : dgamma;
+      if (dst) dst[o64] = v;
+    }
+    return;
+  }
   int co = 0, col = 0;
   const bool live = idx < NW + HS_REAL;
   if (live) {
@@ -347,6 +444,41 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_reduce_kernel(const float *__
     } else if (out.b[g]) {
       const_cast<float *>(out.b[g])[o] = v;
     }
+  }
+}
+
+// The grouped seperate BatchNorm's backward coefficients per (level, channel) from the partial
+// sums left by the fusion conv's input-gradient epilogue (part [L][nrc][128]: sum g' and sum
+// g' xhat per channel): the table the BNB weight-gradient kernel reads, and the per-level sums
+// for the affine gradients.  One workgroup per level; rows summed in a fixed order.
+__global__ __launch_bounds__(256) void hfsep_bn_coef_kernel(const float *__restrict__ part, int nrc, float n,
+                                                            const float *__restrict__ mean,
+                                                            const float *__restrict__ invstd,
+                                                            const float *__restrict__ gamma,
+                                                            const float *__restrict__ beta, float *__restrict__ tab,
+                                                            float *__restrict__ lsum) {
+  __shared__ float red[2][128];
+  const int l = blockIdx.x, tid = threadIdx.x, col = tid & 127, q = tid >> 7;
+  float v = 0.f;
+  for (int r = q; r < nrc; r += 2) v += part[((int64_t)l * nrc + r) * 128 + col];
+  red[q][col] = v;
+  __syncthreads();
+  if (tid < 128) {
+    const float t = red[0][tid] + red[1][tid];
+    lsum[l * 128 + tid] = t;
+    red[0][tid] = t;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid;
+    const float mu = mean[l * 64 + c], iv = invstd[l * 64 + c];
+    const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+    // dy = gi (g' - a - xhat b) with xhat = (y - mu) iv, gi = gamma iv: A g' + B y + C; the ReLU
+    // mask gamma xhat + beta > 0 as P y + Q > 0
+    const float a = red[0][c] / n, b = red[0][64 + c] / n, gi = ga * iv;
+    float *t = tab + (l * 64 + c) * 8;
+    t[0] = gi; t[1] = -gi * b * iv; t[2] = -gi * a + gi * b * iv * mu; t[3] = gi; t[4] = be - gi * mu;
+    t[5] = 0.f; t[6] = 0.f; t[7] = 0.f;
   }
 }
 
@@ -402,8 +534,14 @@ extern "C" int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int
   const size_t lds = (size_t)(th + 2) * (W + 2) * HS_CIN * 2;
   EWVIT_CHECK_ARG(lds <= 64 * 1024, "hfsep_fwd: W=%lld too wide", (long long)W);
   HsParams p{{w0, w1, w2}, {b0, b1, b2}};
-  hipLaunchKernelGGL(hfsep_fwd_kernel<8>, dim3((unsigned)g, (unsigned)L), dim3(256), lds, as_stream(stream),
-                     (const bf16_t *)x, (bf16_t *)y, p, (int)N, (int)H, (int)W, bn_shift, bn_part, bn_shift_out);
+  // the register stage holds a band's (TH + 2) x (W + 2) x 2 x pieces
+  const int64_t items = (int64_t)(th + 2) * (W + 2) * 2;
+  if (items <= 9 * 256)
+    hipLaunchKernelGGL((hfsep_fwd_kernel<8, 9>), dim3((unsigned)g, (unsigned)L), dim3(256), lds, as_stream(stream),
+                       (const bf16_t *)x, (bf16_t *)y, p, (int)N, (int)H, (int)W, bn_shift, bn_part, bn_shift_out);
+  else
+    hipLaunchKernelGGL((hfsep_fwd_kernel<8, 16>), dim3((unsigned)g, (unsigned)L), dim3(256), lds, as_stream(stream),
+                       (const bf16_t *)x, (bf16_t *)y, p, (int)N, (int)H, (int)W, bn_shift, bn_part, bn_shift_out);
   return launch_status("hfsep_fwd");
 }
 
@@ -428,11 +566,11 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
   hipStream_t s = as_stream(stream);
 #define EWVIT_HS_WG(TH_, D_, X_)                                                                                 \
   do {                                                                                                           \
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_>), \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, false>), \
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
     (void)attr;                                                                                                  \
-    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,           \
-                       (const bf16_t *)dy, workspace, (int)NI, (int)H, (int)W);                                  \
+    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, false>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,    \
+                       (const bf16_t *)dy, workspace, (int)NI, (int)H, (int)W, nullptr, nullptr, 0, 1);          \
   } while (0)
   if (small) EWVIT_HS_WG(2, 7, 4); else EWVIT_HS_WG(2, 13, 7);
 #undef EWVIT_HS_WG
@@ -442,4 +580,50 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
   const int nout = HS_REAL * 27 + HS_REAL;
   hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64), dim3(256), 0, s, workspace, G, out);
   return launch_status("hfsep_bwd_weight reduce");
+}
+
+extern "C" int64_t ewvit_hfsep_bn_bwd_weight_workspace(int64_t L, int64_t N, int64_t H, int64_t W) {
+  if (L < 1 || L > 8 || N < 1 || !hs_geom_ok(L * N, H, W)) return 0;
+  return (int64_t)hs_wg_blocks(L * N, H) * HS_COUT * HS_K * 4 + (int64_t)L * (64 * 8 + 128) * 4;
+}
+
+extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const void *dz, int64_t L, int64_t N, int64_t H,
+                                         int64_t W, const float *mean, const float *invstd, const float *gamma,
+                                         const float *beta, const float *part, int nrc, float *dw0, float *dw1,
+                                         float *dw2, float *db0, float *db1, float *db2, float *dgamma, float *dbeta,
+                                         float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(x && y && dz && mean && invstd && part && workspace, "hfsep_bn_bwd_weight: null pointer");
+  EWVIT_CHECK_ARG(L >= 1 && L <= 8 && N >= 1 && hs_geom_ok(L * N, H, W), "hfsep_bn_bwd_weight: bad geometry");
+  EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 65535, "hfsep_bn_bwd_weight: %d partial rows", nrc);
+  const int64_t NI = L * N;
+  const int th = hs_wg_th();
+  const int G = hs_wg_blocks(NI, H);
+  const int Pk = (int)((th * W + 31) & ~31);
+  const bool small = Pk * 8 <= 7 * 256 && (th + 2) * (W + 2) * 2 <= 4 * 256;
+  EWVIT_CHECK_ARG(small || (Pk * 8 <= 13 * 256 && (th + 2) * (W + 2) * 2 <= 7 * 256),
+                  "hfsep_bn_bwd_weight: W=%lld too wide for TH=%d", (long long)W, th);
+  const size_t lds = (size_t)Pk * 128 + ((size_t)(th + 2) * (W + 2) + 1) * 32 + (size_t)L * 64 * 8 * 4;
+  hipStream_t s = as_stream(stream);
+  float *tab = workspace + (int64_t)G * HS_COUT * HS_K;
+  float *lsum = tab + L * 64 * 8;
+  hipLaunchKernelGGL(hfsep_bn_coef_kernel, dim3((unsigned)L), dim3(256), 0, s, part, nrc, (float)(N * H * W), mean,
+                     invstd, gamma, beta, tab, lsum);
+  if (int rc = launch_status("hfsep_bn_bwd_weight coef")) return rc;
+#define EWVIT_HS_WGB(TH_, D_, X_)                                                                                 \
+  do {                                                                                                            \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, true>), \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
+    (void)attr;                                                                                                   \
+    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, true>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,     \
+                       (const bf16_t *)dz, workspace, (int)NI, (int)H, (int)W, (const bf16_t *)y, tab, (int)L,    \
+                       (int)N);                                                                                   \
+  } while (0)
+  if (small) EWVIT_HS_WGB(2, 7, 4); else EWVIT_HS_WGB(2, 13, 7);
+#undef EWVIT_HS_WGB
+  if (int rc = launch_status("hfsep_bn_bwd_weight")) return rc;
+  HsParams out{{dw0, dw1, dw2}, {db0, db1, db2}};
+  const int nout = HS_REAL * 27 + HS_REAL;
+  hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64 + 2), dim3(256), 0, s, workspace, G, out, lsum,
+                     (int)L, dgamma, dbeta);
+  return launch_status("hfsep_bn_bwd_weight reduce");
 }

@@ -91,6 +91,9 @@ SIGNATURES = {
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_bn_bwd_reduce': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
+    'ewvit_hfsep_bn_bwd_weight': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_bn_act_se_squeeze': [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp,
                                 _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     'ewvit_se_gate_excite': [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
@@ -125,6 +128,8 @@ QUERIES = {
     'ewvit_adam_chunks': (_i64, [_i64]),
     'ewvit_hfsep_fwd_parts': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_hfsep_bwd_weight_workspace': (_i64, [_i64, _i64, _i64]),
+    'ewvit_hfsep_bn_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64]),
+    'ewvit_bn_bwd_reduce_rows': (_i32, [_i64, _i64, _i32]),
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_head_workspace': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),

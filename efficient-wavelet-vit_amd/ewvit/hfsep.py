@@ -95,6 +95,107 @@ def seperate_conv(x, levels, convs, shift=None):
     return y, (part, shifts, part.shape[1])
 
 
+class SeperateBNReLUFn(torch.autograd.Function):
+    """Training: the seperate convs + their grouped BatchNorm (per-level batch statistics,
+    mwt.py:48-59, 84-86) + ReLU.  Forward: ewvit_hfsep_fwd (y and the BN partial sums) and the
+    BN apply pass (ewvit_bn_fwd_partials), offering the BN's backward link to the consumer (the
+    fusion conv).  Backward: when the consumer's input-gradient epilogue left the BN backward
+    sums (the link) — or after the BN backward's own reduction pass (ewvit_bn_bwd_reduce) — ONE
+    pass recomputes the BN backward's dx per element inside the weight-gradient pass
+    (ewvit_hfsep_bn_bwd_weight): the BN's dx tensor is never written nor read back."""
+
+    @staticmethod
+    def forward(ctx, x, levels, cfg, w0, w1, w2, b0, b1, b2, gamma, beta):
+        from .bn import offer_bwd_link
+        running_mean, running_var, momentum, eps = cfg
+        L.require_gpu(x, w0, gamma)
+        params = (w0, w1, w2, b0, b1, b2)
+        ctx.gen = grads.note_use(None)
+        for i, p in enumerate(params):
+            if ctx.needs_input_grad[3 + i]:
+                grads.note_use(p)
+        NL, C, H, W = x.shape
+        if C != 16 or NL % levels or x.dtype != torch.bfloat16 or gamma.numel() != 64:
+            raise ValueError(f'seperate_conv_bn_relu: input {tuple(x.shape)} {x.dtype}, {gamma.numel()} BN channels')
+        xc = x.contiguous(memory_format=torch.channels_last)
+        N = NL // levels
+        ws = [t.detach().contiguous() for t in params]
+        dev = x.device
+        y = torch.empty((NL, 64, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+        z = torch.empty_like(y)
+        mean = torch.empty(levels, 64, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        ctx.cap = L.current_cap()
+        with L.launch_cap(ctx.cap):
+            nparts = int(L.load().ewvit_hfsep_fwd_parts(levels, N, H, W))
+            part = torch.empty(levels, nparts, 128, dtype=torch.float32, device=dev)
+            shifts = torch.empty(levels, 64, dtype=torch.float32, device=dev)
+            sh = running_mean.detach().float().contiguous()
+            npx = NL * H * W
+            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, *[L.ptr(t) for t in ws], L.ptr(sh),
+                   L.ptr(part), L.ptr(shifts), nparts, L.stream(y),
+                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+            L.call('ewvit_bn_fwd_partials', L.ptr(y), L.ptr(z), L.BF16, npx, 64, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), 1, L.ptr(mean),
+                   L.ptr(invstd), None, L.ptr(part), L.ptr(shifts), nparts, levels, L.stream(z),
+                   work={'bytes': 2 * y.numel() * 2})
+        ctx.save_for_backward(xc, y, mean, invstd, gamma, beta)
+        ctx.params, ctx.levels = params, levels
+        ctx.bnlink = offer_bwd_link(z, y, mean, invstd, gamma, beta, 1, None, levels)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        from .bn import fold_bwd_partials
+        with L.launch_cap(L.bwd_cap(ctx.cap)):
+            xc, y, mean, invstd, gamma, beta = ctx.saved_tensors
+            levels = ctx.levels
+            NL, _, H, W = xc.shape
+            N = NL // levels
+            dzc = dz.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            pr = ctx.bnlink.partials_for(dzc) if ctx.bnlink is not None else None
+            ctx.bnlink = None
+            outs = []
+            for i, p in enumerate(ctx.params):
+                if ctx.needs_input_grad[3 + i]:
+                    g = grad_out(p, ctx.gen)
+                    if not g.is_contiguous():
+                        g = torch.empty_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+                    outs.append(g)
+                else:
+                    outs.append(None)
+            dg = torch.empty(64, dtype=torch.float32, device=xc.device) if ctx.needs_input_grad[9] else None
+            db = torch.empty(64, dtype=torch.float32, device=xc.device) if ctx.needs_input_grad[10] else None
+            npx = NL * H * W
+            work = {'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64 + 64) * 2.0}
+            if pr is not None:
+                part, nrc = fold_bwd_partials(pr[0], pr[1], levels, 64)
+            else:
+                # no epilogue sums (the consumer took no link): the BN backward's reduction pass
+                # alone; the dx pass still runs inside the weight gradient
+                nrc = int(L.load().ewvit_bn_bwd_reduce_rows(npx, 64, levels))
+                part = torch.empty(levels * nrc * 128, dtype=torch.float32, device=xc.device)
+                L.call('ewvit_bn_bwd_reduce', L.ptr(dzc), L.ptr(y), L.BF16, npx, 64, L.ptr(gamma), L.ptr(beta),
+                       L.ptr(mean), L.ptr(invstd), 1, levels, L.ptr(part), L.stream(dzc),
+                       work={'bytes': 2 * y.numel() * 2})
+                part, nrc = fold_bwd_partials(part, nrc, levels, 64)
+            ws = torch.empty(int(L.load().ewvit_hfsep_bn_bwd_weight_workspace(levels, N, H, W)) // 4,
+                             dtype=torch.float32, device=xc.device)
+            L.call('ewvit_hfsep_bn_bwd_weight', L.ptr(xc), L.ptr(y), L.ptr(dzc), levels, N, H, W, L.ptr(mean),
+                   L.ptr(invstd), L.ptr(gamma), L.ptr(beta), L.ptr(part), nrc, *[L.ptr(t) for t in outs],
+                   L.ptr(dg), L.ptr(db), L.ptr(ws), L.stream(dzc), work=work)
+        return (None, None, None) + tuple(outs) + (dg, db)
+
+
+def seperate_conv_bn_relu(x, levels, convs, cat, momentum, eps):
+    """Training: relu(BN(seperate_conv(x))) with the grouped BN parameters `cat` = (weight, bias,
+    running_mean, running_var) [64] (the three modules' tensors + identity padding); the running
+    statistics in `cat` are updated in place (the caller copies them back to the modules)."""
+    w, b, rm, rv = cat
+    return SeperateBNReLUFn.apply(x, int(levels), (rm, rv, momentum, eps), *[c.weight for c in convs],
+                                  *[c.bias for c in convs], w, b)
+
+
 _ON = os.environ.get('EWVIT_HFSEP', '1') != '0'      # 0: the block-diagonal dense conv (A/B)
 
 

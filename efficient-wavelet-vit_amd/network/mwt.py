@@ -158,15 +158,20 @@ class _GroupBN:
         y = ewvit.batch_norm_act_params(x, w, bi, rm, rv, training, b0.momentum, b0.eps, 'relu',
                                         levels if training else 1, partials=partials if training else None)
         if training:
-            dst, src, off = [], [], 0
-            for b in bns:
-                n = b.num_features
-                dst += [b.running_mean, b.running_var]
-                src += [rm[off:off + n], rv[off:off + n]]
-                off += n
-            torch._foreach_copy_(dst, src)
-            torch._foreach_add_([b.num_batches_tracked for b in bns], levels)
+            self.writeback(bns, rm, rv, levels)
         return y
+
+    @staticmethod
+    def writeback(bns, rm, rv, levels):
+        """The grouped running statistics back into the modules; their counters += levels."""
+        dst, src, off = [], [], 0
+        for b in bns:
+            n = b.num_features
+            dst += [b.running_mean, b.running_var]
+            src += [rm[off:off + n], rv[off:off + n]]
+            off += n
+        torch._foreach_copy_(dst, src)
+        torch._foreach_add_([b.num_batches_tracked for b in bns], levels)
 
 
 def bn_relu_groups(x, bns, training, pad=0, levels=1, state=None, partials=None, cat=None):
@@ -178,6 +183,10 @@ def bn_relu_groups(x, bns, training, pad=0, levels=1, state=None, partials=None,
 
 def _cdt():
     return torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else torch.float32
+
+
+# tests compare the fused seperate conv + BN node against the two-node path
+_FUSED_SEP_BN = True
 
 
 class MWT(nn.Module):
@@ -255,6 +264,12 @@ class MWT(nn.Module):
             # conv), the BatchNorm statistics per level summed on the way (training)
             bns = [sep[i][1] for i in range(3)]
             cat = self._sep_bn.params(bns, pad, hf.device)
+            if self.training and pad == 10 and _FUSED_SEP_BN:
+                # conv + BN + ReLU as one autograd node: its backward recomputes the BN's dx
+                # inside the weight-gradient pass (ewvit.hfsep.SeperateBNReLUFn)
+                y = ewvit.hfsep.seperate_conv_bn_relu(hf, Lv, convs, cat, bns[0].momentum, bns[0].eps)
+                self._sep_bn.writeback(bns, cat[2], cat[3], Lv)
+                return self._fusion(y, Lv, B)
             if self.training:
                 y, partials = ewvit.hfsep.seperate_conv(hf, Lv, convs, shift=cat[2])
             else:

@@ -576,6 +576,29 @@ int64_t ewvit_hfsep_bwd_weight_workspace(int64_t NI, int64_t H, int64_t W);
 int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, float *dw0, float *dw1,
                            float *dw2, float *db0, float *db1, float *db2, float *workspace, void *stream);
 
+/* The seperate conv's weight gradients THROUGH the grouped BatchNorm + ReLU that follows it
+ * (mwt.py:48-59: Conv -> BatchNorm2d(18) -> ReLU per colour; per-level batch statistics): the
+ * BN backward's dx pass is recomputed per element inside the weight-gradient pass instead of
+ * being written out.  y: the conv output / BN input [L*N][H][W][64] bf16; dz: the gradient of
+ * the BN + ReLU output (same layout); mean / invstd [L][64] the BN forward's batch statistics;
+ * gamma / beta [64]; part [L][nrc][128]: per channel sum g' and sum g' xhat (g' = dz masked by
+ * the ReLU), as the consumer conv's input-gradient epilogue leaves them (ewvit_bn_fold_partials
+ * shape).  Writes dw_g, db_g as ewvit_hfsep_bwd_weight and dgamma = sum g' xhat, dbeta = sum g'
+ * [64] (summed over the levels); any output may be NULL.  workspace:
+ * ewvit_hfsep_bn_bwd_weight_workspace(L, N, H, W) bytes. */
+/* The reduction pass of ewvit_bn_bwd alone, for a consumer that forms the BN's dx itself:
+ * part [groups][nrc][2][C] = per channel sum g and sum g * xhat (g = dy * act'(BN output)),
+ * nrc = ewvit_bn_bwd_reduce_rows(M, C, groups) (0: bad shape). */
+int ewvit_bn_bwd_reduce_rows(int64_t M, int64_t C, int groups);
+int ewvit_bn_bwd_reduce(const void *dy, const void *x, int dtype, int64_t M, int64_t C, const float *gamma,
+                        const float *beta, const float *save_mean, const float *save_invstd, int act, int groups,
+                        float *part, void *stream);
+int64_t ewvit_hfsep_bn_bwd_weight_workspace(int64_t L, int64_t N, int64_t H, int64_t W);
+int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const void *dz, int64_t L, int64_t N, int64_t H, int64_t W,
+                              const float *mean, const float *invstd, const float *gamma, const float *beta,
+                              const float *part, int nrc, float *dw0, float *dw1, float *dw2, float *db0, float *db1,
+                              float *db2, float *dgamma, float *dbeta, float *workspace, void *stream);
+
 /* ------------------------------------------------------ frames (input side) ---
  * The per-frame transform chain of config/transforms.py:81-113 applied by the datasets'
  * __getitem__ (config/data_loader.py:325-337: cv2.imread -> BGR2RGB -> transform(frame) per

@@ -126,17 +126,23 @@ def test_mwt_uses_grouped_seperate_and_matches_block_diagonal():
     o.load_state_dict({k: v.detach().cpu() for k, v in a.state_dict().items()})
     x = torch.randn(4, 3, 64, 64, device=DEV)
     calls = []
-    orig = ewvit.hfsep.SeperateConvFn.apply
+    orig, orig_bn = ewvit.hfsep.SeperateConvFn.apply, ewvit.hfsep.SeperateBNReLUFn.apply
 
     def spy(*args):
         calls.append(1)
         return orig(*args)
+
+    def spy_bn(*args):
+        calls.append(2)
+        return orig_bn(*args)
     ewvit.hfsep.SeperateConvFn.apply = spy
+    ewvit.hfsep.SeperateBNReLUFn.apply = spy_bn
     try:
         with torch.autocast('cuda', dtype=torch.bfloat16):
             ya = a(x)
     finally:
         ewvit.hfsep.SeperateConvFn.apply = orig
+        ewvit.hfsep.SeperateBNReLUFn.apply = orig_bn
     assert calls, 'the grouped seperate conv was not used'
     applies = ewvit.hfsep.applies
     ewvit.hfsep.applies = lambda *_: False            # the block-diagonal dense conv path
@@ -169,3 +175,49 @@ def test_mwt_uses_grouped_seperate_and_matches_block_diagonal():
             torch.testing.assert_close(u, v, rtol=2e-3, atol=2e-3, msg=n)
         else:
             assert torch.equal(u, v), n
+
+
+@pytest.mark.parametrize('hw', [64, 224])
+def test_fused_seperate_bn_node_matches_two_node_path(hw, monkeypatch):
+    """SeperateBNReLUFn (the BN's dx recomputed inside the weight-gradient pass, the BN backward
+    sums taken from the fusion conv's input-gradient epilogue) against the two-node path
+    (SeperateConvFn + the grouped BatchNormActFn): forward bit-identical, the BN running
+    statistics identical, every gradient outside the seperate conv / its BN bit-identical, and
+    the seperate conv's and BN's gradients equal up to the order of fp32 operations before dy's
+    bf16 rounding (cosine >= 0.99999, norms within 1e-4)."""
+    import copy
+    import ewvit
+    from network import mwt as M
+    torch.manual_seed(5)
+    a = M.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 3, hw, hw, device=DEV)
+    names = []
+    real = ewvit._lib.call
+    monkeypatch.setattr(ewvit._lib, 'call', lambda n, *r, **k: (names.append(n), real(n, *r, **k))[1])
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        ya = a(x)
+    ya.float().square().mean().backward()
+    assert 'ewvit_hfsep_bn_bwd_weight' in names and 'ewvit_hfsep_bwd_weight' not in names
+    monkeypatch.setattr(M, '_FUSED_SEP_BN', False)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        yb = b(x)
+    yb.float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb)
+    for (n, u), v in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(u, v), n
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        if p.grad is None:
+            assert q.grad is None, n
+            continue
+        if n.startswith('hf_conv.seperate.'):
+            u, v = p.grad.double().flatten(), q.grad.double().flatten()
+            c = float(u @ v / (u.norm() * v.norm() + 1e-300))
+            r = float(u.norm() / (v.norm() + 1e-300))
+            print(f'{n}: cos {c:.8f} norm ratio {r:.7f}')
+            if n.endswith('0.bias'):        # feeds a train-mode BN: an exact zero, rounding noise
+                continue
+            assert c >= 0.99999 and abs(r - 1) <= 1e-4, (n, c, r)
+        else:
+            assert torch.equal(p.grad, q.grad), n
