@@ -399,21 +399,21 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
 
 // dW_g[o][ci][tap] = sum_b part[b][18g + o][tap * 16 + 3g + ci]; db_g[o] = sum_b
 // part[b][18g + o][4 * 16 + 15] (the ones channel at the centre tap).  Block: 64 outputs x
-// 4 slab quarters, combined in a fixed order.
+// 16 slab groups (8 loads in flight per thread), combined in a fixed order.
 // BNB launches: the last 2 blocks write the grouped BatchNorm's affine gradients, dbeta[c] =
 // sum_l sum g', dgamma[c] = sum_l sum g' xhat (lsum [L][128], levels in order).
-__global__ __launch_bounds__(256) void hfsep_wgrad_reduce_kernel(const float *__restrict__ part, int G, HsParams out,
+__global__ __launch_bounds__(1024) void hfsep_wgrad_reduce_kernel(const float *__restrict__ part, int G, HsParams out,
                                                                  const float *__restrict__ lsum = nullptr, int L = 0,
                                                                  float *dgamma = nullptr, float *dbeta = nullptr) {
-  __shared__ float red[4][64];
-  const int tid = threadIdx.x, o64 = tid & 63, qtr = tid >> 6;
+  __shared__ float red[16][64];
+  const int tid = threadIdx.x, o64 = tid & 63, qtr = tid >> 6;   // 16 slab groups of 64 outputs
   const int idx = blockIdx.x * 64 + o64;              // 0 .. 54*27 + 54
   constexpr int NW = HS_REAL * 27;
   if (lsum && (int)blockIdx.x >= (int)gridDim.x - 2) {
     const int which = (int)gridDim.x - 1 - (int)blockIdx.x;      // 1: dbeta, 0: dgamma
     if (qtr == 0) {
       float v = 0.f;
-      for (int l = 0; l < L; ++l) v += lsum[l * 128 + (which ? 0 : 64) + o64];
+      for (int l = 0; l < L; ++l) v += lsum[l * 128 + (which ? 0 : 64) + o64];   // levels in order
       float *dst = which ? dbeta : dgamma;
       if (dst) dst[o64] = v;
     }
@@ -432,12 +432,26 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_reduce_kernel(const float *__
     }
   }
   float s = 0.f;
-  if (live)
-    for (int b = qtr; b < G; b += 4) s += part[((int64_t)b * HS_COUT + co) * HS_K + col];
+  if (live) {
+    // slabs b = qtr + 16 i, 8 loads in flight per step (fixed order)
+    const float *src = part + (int64_t)co * HS_K + col;
+    const int64_t sstr = (int64_t)HS_COUT * HS_K;
+    int b = qtr;
+    for (; b + 7 * 16 < G; b += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(b + 16 * u) * sstr];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < G; b += 16) s += src[(int64_t)b * sstr];
+  }
   red[qtr][o64] = s;
   __syncthreads();
   if (qtr == 0 && live) {
-    const float v = (red[0][o64] + red[1][o64]) + (red[2][o64] + red[3][o64]);
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += red[q][o64];
     const int g = co / HS_GO, o = co - g * HS_GO;
     if (idx < NW) {
       if (out.w[g]) const_cast<float *>(out.w[g])[o * 27 + (idx - co * 27)] = v;
@@ -578,7 +592,7 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
   if (rc) return rc;
   HsParams out{{dw0, dw1, dw2}, {db0, db1, db2}};
   const int nout = HS_REAL * 27 + HS_REAL;
-  hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64), dim3(256), 0, s, workspace, G, out);
+  hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64), dim3(1024), 0, s, workspace, G, out);
   return launch_status("hfsep_bwd_weight reduce");
 }
 
@@ -623,7 +637,7 @@ extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const voi
   if (int rc = launch_status("hfsep_bn_bwd_weight")) return rc;
   HsParams out{{dw0, dw1, dw2}, {db0, db1, db2}};
   const int nout = HS_REAL * 27 + HS_REAL;
-  hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64 + 2), dim3(256), 0, s, workspace, G, out, lsum,
+  hipLaunchKernelGGL(hfsep_wgrad_reduce_kernel, dim3((nout + 63) / 64 + 2), dim3(1024), 0, s, workspace, G, out, lsum,
                      (int)L, dgamma, dbeta);
   return launch_status("hfsep_bn_bwd_weight reduce");
 }
