@@ -324,11 +324,9 @@ def main():
     args = parse()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         sys.exit(launch_ranks(args.gpus))
-    os.environ.setdefault('TORCH_NCCL_AVOID_RECORD_STREAMS', '1')   # buckets are persistent buffers
-    # process-group status for a global-mode capture's watchdog drain (ewvit.graph)
-    os.environ.setdefault('TORCH_FR_BUFFER_SIZE', '2000')
     import ewvit
     from ewvit import dist as edist
+    edist.rccl_env()        # fresh collective events (no captured event reaches the watchdog), FR status
     rank, world, local = edist.env_ranks()
     if world != args.gpus:
         print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled '

@@ -1,0 +1,1054 @@
+// One pre-norm ViT encoder layer of the spatial branch (gfx950), forward and backward —
+// reference network/sfe.py:72-85 (Transformer), 20-27 (PreNorm), 42-70 (Attention), 29-40
+// (FeedForward):
+//   x1 = x0 + Dropout(to_out(Attention(LN1(x0))))
+//   x2 = x1 + W2 GELU(W1 LN2(x1) + b1) + b2
+// at the hot path's shape: dim 512, 8 heads of 64, mlp 2048, 2 tokens per frame (CLS + the
+// single 7x7 patch), R = 2 x frames <= 128 rows, row 2b + i = token i of frame b.
+//
+// The module path issues 11 forward launches per layer (LayerNorm, to_qkv + split-K reduce,
+// attention, to_out + reduce, LayerNorm, Linear1 + reduce, Linear2 + reduce) and ~25 backward.
+// Every GEMM here is [128 rows] x [<= 2048] x [<= 2048] against fp32 master weights: a few
+// MFLOP and a few MB of weight reads, so each launch is latency: the fusion below cuts the
+// launches, not the bytes.
+//   forward   F1 vit_ln_gemm_kernel<0>   LN1 (statistics per workgroup, all rows) + to_qkv;
+//                                        LN1 output written transposed for the weight gradient
+//             F2 vit_attn_proj_kernel     softmax of the 2x2 scores per (frame, head) + to_out
+//                                        with the attention output formed in the A fragments,
+//                                        bias, dropout, residual
+//             F3 vit_ln_gemm_kernel<1>   LN2 + Linear1 + bias + GELU (pre-activation kept)
+//             F4 vit_mlp2_kernel          Linear2 + bias + residual
+//   backward  B1 vit_mlp2_bwd_kernel      dh = g W2 (rounded like the module path's bf16 dh),
+//                                        g1 = dh GELU'(pre), db1; g transposed, db2
+//             B2 vit_mlp1_bwd_kernel      dLN2 = g1 W1 | dW2 = g^T h | dW1 = g1^T LN2
+//             B3 vit_ln2_bwd_attn_kernel  LN2 backward + residual (dx1), to_out's dropout,
+//                                        d(attention out) = g_o Wo per head, attention
+//                                        backward | dx1, g_o transposed, dbo, dLN2 affine
+//             B4 vit_qkv_bwd_kernel       dLN1 = dqkv Wqkv | dWqkv = dqkv^T LN1 | dWo = g_o^T o
+//             B5 vit_ln1_bwd_kernel       LN1 backward + residual (dx0), dLN1 affine
+// GEMM fragments: v_mfma_f32_16x16x32_bf16, bf16 operands rounded from the fp32 masters /
+// activations exactly where the module path's ewvit_gemm rounds them, fp32 accumulation.
+// Weight gradients reduce over the rows (K = rows): their operands are the activations /
+// gradients stored transposed ([feature][128 rows] bf16, zero past R), written by the kernel
+// that produces them (the MFMA output layout gives a lane 4 consecutive rows of one column).
+// Forward / input-gradient GEMMs read their A fragments straight from global memory (L2) and
+// their B fragments from the fp32 weights (forward) or from an LDS image of the weight slice
+// transposed to k-contiguous bf16 (input gradients reduce over the weight's output index).
+#include "common.h"
+
+namespace ewvit {
+
+constexpr int VD = 512, VQ = 1536, VF = 2048, VH = 8, VDH = 64, VRP = 128;
+constexpr float VSCALE = 0.125f;   // dim_head^-0.5 (sfe.py:50)
+
+typedef ewvit_vit_layer VitP;
+typedef ewvit_vit_grads VitG;
+typedef __attribute__((ext_vector_type(8))) __bf16 vb8;
+typedef __attribute__((ext_vector_type(4))) float vf4;
+
+__device__ __forceinline__ vf4 mma(vb8 a, vb8 b, vf4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ vb8 pack8(const float *v) {
+  vb8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (__bf16)v[e];
+  return r;
+}
+__device__ __forceinline__ void ld8f(const float *p, float *v) {
+  const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ vb8 ld8b(const bf16_t *p) { return *reinterpret_cast<const vb8 *>(p); }
+__device__ __forceinline__ void unpack8(vb8 b, float *v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)b[e];
+}
+__device__ __forceinline__ vb8 zero8() {
+  vb8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (__bf16)0.f;
+  return r;
+}
+__device__ __forceinline__ float rbf(float v) { return bf2f(f2bf(v)); }
+__device__ __forceinline__ float keep_scale(float p, uint64_t sd, uint64_t idx) {
+  return uniform01(sd, idx) >= p ? 1.0f / (1.0f - p) : 0.f;
+}
+
+// ---------------------------------------------------------------- saved state / scratch
+struct VitSaved {
+  float *mu1, *rs1, *mu2, *rs2, *p, *x1;
+  bf16_t *qkv, *aux, *h, *ln1T, *oT, *ln2T, *hT;
+};
+struct VitScratch {
+  bf16_t *gT, *g1, *g1T, *goT, *dqkv, *dqkvT;
+  float *dln2, *dx1, *dln1;
+};
+__host__ __device__ inline int64_t al256(int64_t b) { return (b + 255) / 256 * 256; }
+template <class F> __host__ __device__ inline int64_t saved_layout(F f) {
+  int64_t o = 0;
+  auto put = [&](int idx, int64_t bytes) { f(idx, o); o += al256(bytes); };
+  put(0, 4 * VRP); put(1, 4 * VRP); put(2, 4 * VRP); put(3, 4 * VRP);
+  put(4, 4 * VRP * VH * 2); put(5, 4 * VRP * VD);
+  put(6, 2 * VRP * VQ); put(7, 2 * VRP * VF); put(8, 2 * VRP * VF);
+  put(9, 2 * VD * VRP); put(10, 2 * VD * VRP); put(11, 2 * VD * VRP); put(12, 2 * VF * VRP);
+  return o;
+}
+template <class F> __host__ __device__ inline int64_t scratch_layout(F f) {
+  int64_t o = 0;
+  auto put = [&](int idx, int64_t bytes) { f(idx, o); o += al256(bytes); };
+  put(0, 2 * VD * VRP); put(1, 2 * VRP * VF); put(2, 2 * VF * VRP); put(3, 2 * VD * VRP);
+  put(4, 2 * VRP * VQ); put(5, 2 * VQ * VRP);
+  put(6, 4 * VRP * VD); put(7, 4 * VRP * VD); put(8, 4 * VRP * VD);
+  return o;
+}
+inline VitSaved vit_saved(void *base) {
+  VitSaved s;
+  char *b = reinterpret_cast<char *>(base);
+  saved_layout([&](int i, int64_t o) {
+    void *q = b + o;
+    switch (i) {
+      case 0: s.mu1 = (float *)q; break;
+      case 1: s.rs1 = (float *)q; break;
+      case 2: s.mu2 = (float *)q; break;
+      case 3: s.rs2 = (float *)q; break;
+      case 4: s.p = (float *)q; break;
+      case 5: s.x1 = (float *)q; break;
+      case 6: s.qkv = (bf16_t *)q; break;
+      case 7: s.aux = (bf16_t *)q; break;
+      case 8: s.h = (bf16_t *)q; break;
+      case 9: s.ln1T = (bf16_t *)q; break;
+      case 10: s.oT = (bf16_t *)q; break;
+      case 11: s.ln2T = (bf16_t *)q; break;
+      default: s.hT = (bf16_t *)q; break;
+    }
+  });
+  return s;
+}
+inline VitScratch vit_scratch(void *base) {
+  VitScratch s;
+  char *b = reinterpret_cast<char *>(base);
+  scratch_layout([&](int i, int64_t o) {
+    void *q = b + o;
+    switch (i) {
+      case 0: s.gT = (bf16_t *)q; break;
+      case 1: s.g1 = (bf16_t *)q; break;
+      case 2: s.g1T = (bf16_t *)q; break;
+      case 3: s.goT = (bf16_t *)q; break;
+      case 4: s.dqkv = (bf16_t *)q; break;
+      case 5: s.dqkvT = (bf16_t *)q; break;
+      case 6: s.dln2 = (float *)q; break;
+      case 7: s.dx1 = (float *)q; break;
+      default: s.dln1 = (float *)q; break;
+    }
+  });
+  return s;
+}
+
+// ---------------------------------------------------------------- shared pieces
+// LayerNorm statistics of rows w, w + nw, ... (< 128; rows >= R get 0 / 0): a wave per row,
+// 8 contiguous columns per lane; two-pass mean / centred variance, biased, eps inside the
+// rsqrt (torch's formula, layernorm.hip's)
+__device__ __forceinline__ void ln_stats_rows(const float *x, int R, float eps, float *smu, float *srs, int w,
+                                              int nw, int lane) {
+  for (int r = w; r < VRP; r += nw) {
+    float mu = 0.f, rs = 0.f;
+    if (r < R) {
+      float v[8];
+      ld8f(x + (int64_t)r * VD + lane * 8, v);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e];
+      mu = wave_sum(s) / (float)VD;
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+      rs = rsqrtf(wave_sum(q) / (float)VD + eps);
+    }
+    if (lane == 0) { smu[r] = mu; srs[r] = rs; }
+  }
+}
+
+// A 64 x 64 block of a weight gradient out[r][c] = sum_k AT[r][k] BT[c][k] over the 128 rows
+// k (zero past R in both operands); wave w of 4 takes the 32 x 32 quadrant (w >> 1, w & 1)
+__device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, float *out, int64_t ldo, int r0,
+                                            int c0, int w, int lane) {
+  const int li = lane & 15, lq = lane >> 4;
+  const int rb = r0 + (w >> 1) * 32, cb = c0 + (w & 1) * 32;
+  vb8 a[4][2], b[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a[s][t] = ld8b(AT + (int64_t)(rb + t * 16 + li) * VRP + s * 32 + lq * 8);
+      b[s][t] = ld8b(BT + (int64_t)(cb + t * 16 + li) * VRP + s * 32 + lq * 8);
+    }
+  vf4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mma(a[s][i], b[s][j], acc[i][j]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(int64_t)(rb + i * 16 + lq * 4 + e) * ldo + cb + j * 16 + li] = acc[i][j][e];
+}
+
+// the weight slice W[o][c0 .. c0 + NC) (o < NO, fp32, row stride ldw) as a k-contiguous bf16
+// LDS image wT[c][o] (row pitch NO + 8)
+template <int NC, int NO>
+__device__ __forceinline__ void stage_wT(bf16_t *wT, const float *W, int64_t ldw, int c0, int tid, int nthr) {
+  constexpr int Q = NC / 4;
+  for (int it = tid; it < NO * Q; it += nthr) {
+    const int o = it / Q, q = it - o * Q;
+    const float4 v = *reinterpret_cast<const float4 *>(W + (int64_t)o * ldw + c0 + 4 * q);
+    bf16_t *d = wT + (4 * q) * (NO + 8) + o;
+    d[0] = f2bf(v.x);
+    d[NO + 8] = f2bf(v.y);
+    d[2 * (NO + 8)] = f2bf(v.z);
+    d[3 * (NO + 8)] = f2bf(v.w);
+  }
+}
+
+// ---------------------------------------------------------------- F1 / F3: LN + GEMM
+// MODE 0: qkv = LN1(x0) Wqkv^T (48 workgroups of 32 columns); MODE 1: pre = LN2(x1) W1^T + b1,
+// aux = pre, h = GELU(pre) (64 workgroups).  512 threads: wave (rg = w & 3, kh = w >> 2) owns
+// rows 32 rg .. + 32 and the K half kh; the halves meet in LDS.
+template <int MODE>
+__global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const float *xin, VitSaved s) {
+  __shared__ float smu[VRP], srs[VRP];
+  __shared__ vf4 red[4][2][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float *gw = MODE ? p.ln2_w : p.ln1_w, *gb = MODE ? p.ln2_b : p.ln1_b;
+  const float *W = MODE ? p.w1 : p.wqkv;
+  ln_stats_rows(xin, R, p.ln_eps, smu, srs, w, 8, lane);
+  __syncthreads();
+  if (blockIdx.x == 0 && tid < VRP) {
+    (MODE ? s.mu2 : s.mu1)[tid] = smu[tid];
+    (MODE ? s.rs2 : s.rs1)[tid] = srs[tid];
+  }
+  if (blockIdx.x < 32 && tid < 256) {
+    // the LN output transposed, [k][128 rows] bf16: 16 columns k per workgroup, 8 rows a thread
+    bf16_t *lnT = MODE ? s.ln2T : s.ln1T;
+    const int k = blockIdx.x * 16 + (tid >> 4), r0 = (tid & 15) * 8;
+    const float g = gw[k], bb = gb[k];
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = r0 + e;
+      v[e] = r < R ? (xin[(int64_t)r * VD + k] - smu[r]) * srs[r] * g + bb : 0.f;
+    }
+    *reinterpret_cast<vb8 *>(lnT + (int64_t)k * VRP + r0) = pack8(v);
+  }
+  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int c0 = blockIdx.x * 32;
+  int row[2];
+  float mu[2], rs[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    row[t] = rg * 32 + t * 16 + li;
+    mu[t] = smu[row[t]];
+    rs[t] = srs[row[t]];
+  }
+  vf4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sb = 0; sb < 8; sb += 4) {
+    vb8 af[4][2], bf[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+      float g8[8], b8[8];
+      ld8f(gw + k, g8);
+      ld8f(gb + k, b8);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (row[t] < R) {
+          float v[8];
+          ld8f(xin + (int64_t)row[t] * VD + k, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (v[e] - mu[t]) * rs[t] * g8[e] + b8[e];
+          af[u][t] = pack8(v);
+        } else {
+          af[u][t] = zero8();
+        }
+        float v[8];
+        ld8f(W + (int64_t)(c0 + t * 16 + li) * VD + k, v);
+        bf[u][t] = pack8(v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  if (kh == 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (kh == 1) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const vf4 o = red[rg][i][j][lane];
+      const int col = c0 + j * 16 + li;
+      const int rb = rg * 32 + i * 16 + lq * 4;
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (rb + e < R) s.qkv[(int64_t)(rb + e) * VQ + col] = f2bf(acc[i][j][e] + o[e]);
+      } else {
+        const float bias = p.b1[col];
+        float hv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pre = acc[i][j][e] + o[e] + bias;
+          hv[e] = rb + e < R ? gelu_erf(pre) : 0.f;
+          if (rb + e < R) {
+            s.aux[(int64_t)(rb + e) * VF + col] = f2bf(pre);
+            s.h[(int64_t)(rb + e) * VF + col] = f2bf(hv[e]);
+          }
+        }
+        uint2 pk;
+        pk.x = (unsigned)f2bf(hv[0]) | ((unsigned)f2bf(hv[1]) << 16);
+        pk.y = (unsigned)f2bf(hv[2]) | ((unsigned)f2bf(hv[3]) << 16);
+        *reinterpret_cast<uint2 *>(s.hT + (int64_t)col * VRP + rb) = pk;
+      }
+    }
+}
+
+// ---------------------------------------------------------------- F2: attention + to_out
+// 16 workgroups of 32 output columns, 512 threads.  Each workgroup forms the softmax weights
+// of every (frame, head) — 4 dot products of 64 per pair — in LDS; the attention output
+// o[r][k] = p[r][h][0] v[2f][k] + p[r][h][1] v[2f+1][k] (f = r / 2, h = k / 64) is formed in the
+// A fragments; workgroup b also writes o transposed for columns 32 b .. + 32.
+__global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const float *x0, VitSaved s) {
+  __shared__ float sp[VRP][VH][2];
+  __shared__ vf4 red[4][2][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int B = R >> 1;
+  for (int it = tid >> 3; it < (VRP / 2) * VH; it += 64) {
+    const int b = it >> 3, h = it & 7, d0 = (tid & 7) * 8;
+    float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
+    if (b < B) {
+      float q0[8], q1[8], k0[8], k1[8];
+      unpack8(ld8b(s.qkv + (int64_t)(2 * b) * VQ + h * VDH + d0), q0);
+      unpack8(ld8b(s.qkv + (int64_t)(2 * b + 1) * VQ + h * VDH + d0), q1);
+      unpack8(ld8b(s.qkv + (int64_t)(2 * b) * VQ + VD + h * VDH + d0), k0);
+      unpack8(ld8b(s.qkv + (int64_t)(2 * b + 1) * VQ + VD + h * VDH + d0), k1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s00 += q0[e] * k0[e];
+        s01 += q0[e] * k1[e];
+        s10 += q1[e] * k0[e];
+        s11 += q1[e] * k1[e];
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      s00 += __shfl_xor(s00, m, 64);
+      s01 += __shfl_xor(s01, m, 64);
+      s10 += __shfl_xor(s10, m, 64);
+      s11 += __shfl_xor(s11, m, 64);
+    }
+    if ((tid & 7) == 0) {
+      const float sc[2][2] = {{s00 * VSCALE, s01 * VSCALE}, {s10 * VSCALE, s11 * VSCALE}};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float p0 = 0.f, p1 = 0.f;
+        if (b < B) {
+          const float mx = fmaxf(sc[i][0], sc[i][1]);
+          const float e0 = __expf(sc[i][0] - mx), e1 = __expf(sc[i][1] - mx);
+          const float inv = 1.0f / (e0 + e1);
+          p0 = e0 * inv;
+          p1 = e1 * inv;
+        }
+        sp[2 * b + i][h][0] = p0;
+        sp[2 * b + i][h][1] = p1;
+      }
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int i = tid; i < R * VH * 2; i += 512) s.p[i] = (&sp[0][0][0])[i];
+  {
+    // o transposed: columns k = 32 b + (tid >> 4), rows 8 (tid & 15) .. + 8
+    const int k = blockIdx.x * 32 + (tid >> 4), r0 = (tid & 15) * 8, h = k >> 6;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = r0 + e, f = r >> 1;
+      float o = 0.f;
+      if (r < R) {
+        o = sp[r][h][0] * bf2f(s.qkv[(int64_t)(2 * f) * VQ + 2 * VD + k]);
+        o += sp[r][h][1] * bf2f(s.qkv[(int64_t)(2 * f + 1) * VQ + 2 * VD + k]);
+      }
+      v[e] = o;
+    }
+    *reinterpret_cast<vb8 *>(s.oT + (int64_t)k * VRP + r0) = pack8(v);
+  }
+  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int c0 = blockIdx.x * 32;
+  vf4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sb = 0; sb < 8; sb += 4) {
+    vb8 af[4][2], bf[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = kh * 256 + (sb + u) * 32 + lq * 8, h = k >> 6;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = rg * 32 + t * 16 + li, f = r >> 1;
+        if (r < R) {
+          float v0[8], v1[8], o[8];
+          unpack8(ld8b(s.qkv + (int64_t)(2 * f) * VQ + 2 * VD + k), v0);
+          unpack8(ld8b(s.qkv + (int64_t)(2 * f + 1) * VQ + 2 * VD + k), v1);
+          const float p0 = sp[r][h][0], p1 = sp[r][h][1];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            o[e] = p0 * v0[e];
+            o[e] += p1 * v1[e];
+          }
+          af[u][t] = pack8(o);
+        } else {
+          af[u][t] = zero8();
+        }
+        float v[8];
+        ld8f(p.wo + (int64_t)(c0 + t * 16 + li) * VD + k, v);
+        bf[u][t] = pack8(v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  if (kh == 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (kh == 1) return;
+  const uint64_t sd = step_seed(p.seed, p.seed_off);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const vf4 o = red[rg][i][j][lane];
+      const int col = c0 + j * 16 + li;
+      const float bias = p.bo[col];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = rg * 32 + i * 16 + lq * 4 + e;
+        if (r >= R) continue;
+        float v = acc[i][j][e] + o[e] + bias;
+        if (p.drop_p > 0.f) v = uniform01(sd, (uint64_t)(r * VD + col)) >= p.drop_p ? v * (1.0f / (1.0f - p.drop_p)) : 0.f;
+        v += x0[(int64_t)r * VD + col];
+        s.x1[(int64_t)r * VD + col] = v;
+      }
+    }
+}
+
+// ---------------------------------------------------------------- F4: Linear2 + residual
+// 16 workgroups of 32 columns, 1024 threads: wave (rg = w & 3, kq = w >> 2) owns rows 32 rg ..
+// and the K quarter kq (512 of 2048); the quarters are added in LDS in a fixed order.
+__global__ __launch_bounds__(1024) void vit_mlp2_kernel(VitP p, int R, VitSaved s, float *x2) {
+  __shared__ vf4 red[3][4][2][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rg = w & 3, kq = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int c0 = blockIdx.x * 32;
+  vf4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sb = 0; sb < 16; sb += 4) {
+    vb8 af[4][2], bf[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = kq * 512 + (sb + u) * 32 + lq * 8;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = rg * 32 + t * 16 + li;
+        af[u][t] = r < R ? ld8b(s.h + (int64_t)r * VF + k) : zero8();
+        float v[8];
+        ld8f(p.w2 + (int64_t)(c0 + t * 16 + li) * VF + k, v);
+        bf[u][t] = pack8(v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  if (kq > 0)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[kq - 1][rg][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (kq > 0) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const vf4 a = red[0][rg][i][j][lane], b = red[1][rg][i][j][lane], c = red[2][rg][i][j][lane];
+      const int col = c0 + j * 16 + li;
+      const float bias = p.b2[col];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = rg * 32 + i * 16 + lq * 4 + e;
+        if (r >= R) continue;
+        const float v = (((acc[i][j][e] + a[e]) + b[e]) + c[e]) + bias;
+        x2[(int64_t)r * VD + col] = v + s.x1[(int64_t)r * VD + col];
+      }
+    }
+}
+
+// ---------------------------------------------------------------- B1: Linear2 / GELU backward
+// 64 workgroups of 32 hidden columns J, 512 threads (rg, kh as F1).  dh[:, J] = g W2[:, J]
+// (K = 512 over W2's output index: W2[:, J] staged transposed in LDS), rounded to bf16 like the
+// module path's dh, g1 = dh GELU'(pre) -> g1 (bf16), g1^T, db1[J].  Side job of workgroup b:
+// g's columns 8 b .. + 8 transposed (gT) and their sums (db2).
+__global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
+                                                           VitScratch z) {
+  __shared__ __attribute__((aligned(16))) bf16_t wT[32 * (VD + 8)];
+  __shared__ vf4 red[4][2][2][64];
+  __shared__ float sg[VRP][9];
+  __shared__ float scol[4][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int J0 = blockIdx.x * 32;
+  stage_wT<32, VD>(wT, p.w2, VF, J0, tid, 512);
+  if (tid < VRP) {
+    const int r = tid;
+    float v[8];
+    if (r < R) ld8f(g + (int64_t)r * VD + blockIdx.x * 8, v);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sg[r][e] = v[e];
+      z.gT[(int64_t)(blockIdx.x * 8 + e) * VRP + r] = f2bf(v[e]);
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float a = 0.f;
+    for (int r = 0; r < R; ++r) a += sg[r][tid];
+    G.b2[blockIdx.x * 8 + tid] = a;
+  }
+  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  vf4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sb = 0; sb < 8; sb += 4) {
+    vb8 af[4][2], bf[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = rg * 32 + t * 16 + li;
+        if (r < R) {
+          float v[8];
+          ld8f(g + (int64_t)r * VD + k, v);
+          af[u][t] = pack8(v);
+        } else {
+          af[u][t] = zero8();
+        }
+        bf[u][t] = *reinterpret_cast<const vb8 *>(wT + (t * 16 + li) * (VD + 8) + k);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  if (kh == 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (kh == 0) {
+    float cs[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const vf4 o = red[rg][i][j][lane];
+        const int col = J0 + j * 16 + li;
+        const int rb = rg * 32 + i * 16 + lq * 4;
+        float gv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = rb + e;
+          gv[e] = 0.f;
+          if (r < R) {
+            const float dh = rbf(acc[i][j][e] + o[e]);
+            gv[e] = dh * gelu_erf_grad(bf2f(s.aux[(int64_t)r * VF + col]));
+            z.g1[(int64_t)r * VF + col] = f2bf(gv[e]);
+          }
+          cs[j] += gv[e];
+        }
+        uint2 pk;
+        pk.x = (unsigned)f2bf(gv[0]) | ((unsigned)f2bf(gv[1]) << 16);
+        pk.y = (unsigned)f2bf(gv[2]) | ((unsigned)f2bf(gv[3]) << 16);
+        *reinterpret_cast<uint2 *>(z.g1T + (int64_t)col * VRP + rb) = pk;
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float v = rows_sum4(cs[j]);
+      if (lq == 0) scol[rg][j * 16 + li] = v;
+    }
+  }
+  __syncthreads();
+  if (tid < 32) G.b1[J0 + tid] = ((scol[0][tid] + scol[1][tid]) + scol[2][tid]) + scol[3][tid];
+}
+
+// ---------------------------------------------------------------- B2: Linear1 backward, dW2, dW1
+// 256 threads.  Workgroups 0..31: dLN2[:, I] = g1 W1[:, I], 16 columns I each (W1[:, I] staged
+// transposed; 4 waves = 4 K quarters of 512, added in LDS); 32..287: dW2 = g^T h in 64 x 64
+// blocks; 288..543: dW1 = g1^T LN2.
+__global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[16 * (VF + 8) * 2 + 3 * 8 * 64 * 16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int blk = blockIdx.x;
+  if (blk >= 32 + 256) {
+    const int q = blk - 288;
+    wgrad_block(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    return;
+  }
+  if (blk >= 32) {
+    const int q = blk - 32;
+    wgrad_block(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
+    return;
+  }
+  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
+  vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VF + 8) * 2);
+  const int I0 = blk * 16;
+  stage_wT<16, VF>(wT, p.w1, VD, I0, tid, 256);
+  __syncthreads();
+  const int li = lane & 15, lq = lane >> 4;
+  vf4 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
+  for (int sb = 0; sb < 16; sb += 2) {
+    vb8 af[2][8], bf[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = w * 512 + (sb + u) * 32 + lq * 8;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int r = t * 16 + li;
+        af[u][t] = r < R ? ld8b(z.g1 + (int64_t)r * VF + k) : zero8();
+      }
+      bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VF + 8) + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
+  }
+  if (w > 0)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) red[((w - 1) * 8 + t) * 64 + lane] = acc[t];
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const vf4 a = red[(0 * 8 + t) * 64 + lane], b = red[(1 * 8 + t) * 64 + lane], c = red[(2 * 8 + t) * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = t * 16 + lq * 4 + e;
+      if (r < R) z.dln2[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- LayerNorm backward pieces
+// per-row sums of the LN backward, a wave per row: ma = mean(gamma dY), mb = mean(gamma dY xhat)
+__device__ __forceinline__ void lnb_rows(const float *dY, const float *X, const float *gamma, const float *mu,
+                                         const float *rs, int R, float *sa, float *sb, int w, int nw, int lane) {
+  for (int r = w; r < VRP; r += nw) {
+    float a = 0.f, b = 0.f;
+    if (r < R) {
+      float d[8], x[8], gm[8];
+      ld8f(dY + (int64_t)r * VD + lane * 8, d);
+      ld8f(X + (int64_t)r * VD + lane * 8, x);
+      ld8f(gamma + lane * 8, gm);
+      const float m = mu[r], s = rs[r];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gd = gm[e] * d[e];
+        a += gd;
+        b += gd * ((x[e] - m) * s);
+      }
+      a = wave_sum(a) / (float)VD;
+      b = wave_sum(b) / (float)VD;
+    }
+    if (lane == 0) { sa[r] = a; sb[r] = b; }
+  }
+}
+// columns c0 .. c0 + 32, 512 threads (column tid & 31, rows 8 (tid >> 5) .. + 8):
+// dX = resid + rstd (gamma dY - ma - xhat mb) -> dXout [R][512] f32; the affine gradients
+// (sum dY xhat, sum dY) and, with a dropout (to_out), g_o = dX keep / (1 - p) transposed into
+// goT and its column sums (to_out's bias gradient)
+__device__ __forceinline__ void lnb_cols(const float *dY, const float *X, const float *gamma, const float *mu,
+                                         const float *rs, const float *resid, int R, const float *sa,
+                                         const float *sb, int c0, float *dXout, float *dgamma, float *dbeta,
+                                         bool drop, float dp, uint64_t sd, bf16_t *goT, float *dbo, float *part,
+                                         int tid) {
+  const int c = c0 + (tid & 31), rg = tid >> 5;
+  const float gm = gamma[c];
+  float pg = 0.f, pb = 0.f, po = 0.f, gov[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int r = rg * 8 + e;
+    gov[e] = 0.f;
+    if (r < R) {
+      const float d = dY[(int64_t)r * VD + c];
+      const float xh = (X[(int64_t)r * VD + c] - mu[r]) * rs[r];
+      const float dx = rs[r] * (gm * d - sa[r] - xh * sb[r]) + resid[(int64_t)r * VD + c];
+      dXout[(int64_t)r * VD + c] = dx;
+      pg += d * xh;
+      pb += d;
+      if (drop) {
+        gov[e] = dp > 0.f ? dx * keep_scale(dp, sd, (uint64_t)(r * VD + c)) : dx;
+        po += gov[e];
+      }
+    }
+  }
+  if (drop) *reinterpret_cast<vb8 *>(goT + (int64_t)c * VRP + rg * 8) = pack8(gov);
+  part[(0 * 16 + rg) * 32 + (tid & 31)] = pg;
+  part[(1 * 16 + rg) * 32 + (tid & 31)] = pb;
+  part[(2 * 16 + rg) * 32 + (tid & 31)] = po;
+  __syncthreads();
+  if (tid < 32) {
+    float a = 0.f, b = 0.f, o = 0.f;
+    for (int q = 0; q < 16; ++q) {
+      a += part[(0 * 16 + q) * 32 + tid];
+      b += part[(1 * 16 + q) * 32 + tid];
+      o += part[(2 * 16 + q) * 32 + tid];
+    }
+    dgamma[c0 + tid] = a;
+    dbeta[c0 + tid] = b;
+    if (drop) dbo[c0 + tid] = o;
+  }
+}
+
+// ---------------------------------------------------------------- B3: LN2 backward + attention
+// 512 threads.  Every workgroup takes the per-row LN2 backward sums.  Workgroups 0..7 (head h):
+// d(attention out)[:, head h] = g_o Wo[:, 64 h .. + 64] with g_o = (g + LN2 backward) keep / (1-p)
+// formed in the A fragments (Wo's slice staged transposed), rounded to bf16 like the module
+// path's, then the attention backward of the head over the 2-token frames -> dqkv (bf16) and
+// dqkv^T.  Workgroups 8..23: 32 columns each of dx1, g_o^T, the to_out bias and the LN2 affine
+// gradients.
+__global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
+                                                               VitScratch z) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[64 * (VD + 8) * 2 + VRP * 68 * 4];
+  __shared__ float sa[VRP], sbm[VRP];
+  __shared__ vf4 red[4][2][4][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  lnb_rows(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, R, sa, sbm, w, 8, lane);
+  __syncthreads();
+  const uint64_t sd = step_seed(p.seed, p.seed_off);
+  if (blockIdx.x >= VH) {
+    lnb_cols(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, g, R, sa, sbm, (blockIdx.x - VH) * 32, z.dx1, G.ln2_w, G.ln2_b,
+             true, p.drop_p, sd, z.goT, G.bo, reinterpret_cast<float *>(smem), tid);
+    return;
+  }
+  const int h = blockIdx.x;
+  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
+  float *sdo = reinterpret_cast<float *>(smem + 64 * (VD + 8) * 2);   // [128][68]
+  stage_wT<64, VD>(wT, p.wo, VD, h * VDH, tid, 512);
+  __syncthreads();
+  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  int row[2];
+  float mu[2], rs[2], ma[2], mb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    row[t] = rg * 32 + t * 16 + li;
+    mu[t] = s.mu2[row[t] < R ? row[t] : 0];
+    rs[t] = s.rs2[row[t] < R ? row[t] : 0];
+    ma[t] = sa[row[t]];
+    mb[t] = sbm[row[t]];
+  }
+  vf4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+  for (int sb = 0; sb < 8; sb += 2) {
+    vb8 af[2][2], bf[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+      float gm[8];
+      ld8f(p.ln2_w + k, gm);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = row[t];
+        if (r < R) {
+          float d[8], x[8], gg[8], v[8];
+          ld8f(z.dln2 + (int64_t)r * VD + k, d);
+          ld8f(s.x1 + (int64_t)r * VD + k, x);
+          ld8f(g + (int64_t)r * VD + k, gg);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xh = (x[e] - mu[t]) * rs[t];
+            float dx = rs[t] * (gm[e] * d[e] - ma[t] - xh * mb[t]) + gg[e];
+            if (p.drop_p > 0.f) dx *= keep_scale(p.drop_p, sd, (uint64_t)(r * VD + k + e));
+            v[e] = dx;
+          }
+          af[u][t] = pack8(v);
+        } else {
+          af[u][t] = zero8();
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[u][j] = *reinterpret_cast<const vb8 *>(wT + (j * 16 + li) * (VD + 8) + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  if (kh == 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[rg][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (kh == 0)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const vf4 o = red[rg][i][j][lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sdo[(rg * 32 + i * 16 + lq * 4 + e) * 68 + j * 16 + li] = rbf(acc[i][j][e] + o[e]);
+      }
+  __syncthreads();
+  // attention backward of head h: 8 lanes per frame f (8 head dims each), 64 frames
+  const int f = tid >> 3, d0 = (tid & 7) * 8, B = R >> 1;
+  float q[2][8], kk[2][8], vv[2][8], dO[2][8];
+  float pr[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  if (f < B) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t rb = (int64_t)(2 * f + i) * VQ + h * VDH + d0;
+      unpack8(ld8b(s.qkv + rb), q[i]);
+      unpack8(ld8b(s.qkv + rb + VD), kk[i]);
+      unpack8(ld8b(s.qkv + rb + 2 * VD), vv[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dO[i][e] = sdo[(2 * f + i) * 68 + d0 + e];
+      pr[i][0] = s.p[((2 * f + i) * VH + h) * 2];
+      pr[i][1] = s.p[((2 * f + i) * VH + h) * 2 + 1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { q[i][e] = kk[i][e] = vv[i][e] = dO[i][e] = 0.f; }
+  }
+  float dp[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a += dO[i][e] * vv[j][e];
+#pragma unroll
+      for (int m = 1; m < 8; m <<= 1) a += __shfl_xor(a, m, 64);
+      dp[i][j] = a;
+    }
+  float dq[2][8], dk[2][8], dv[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { dq[i][e] = dk[i][e] = dv[i][e] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float dot = pr[i][0] * dp[i][0] + pr[i][1] * dp[i][1];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float ds = pr[i][j] * (dp[i][j] - dot) * VSCALE;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dq[i][e] += ds * kk[j][e];
+        dk[j][e] += ds * q[i][e];
+        dv[j][e] += pr[i][j] * dO[i][e];
+      }
+    }
+  }
+  // dqkv rows 2f, 2f + 1 (bf16) and dqkv^T [col][rows 2f, 2f + 1]
+#pragma unroll
+  for (int part = 0; part < 3; ++part) {
+    const float(*src)[8] = part == 0 ? dq : part == 1 ? dk : dv;
+    const int cb = part * VD + h * VDH + d0;
+    if (f < B)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) *reinterpret_cast<vb8 *>(z.dqkv + (int64_t)(2 * f + i) * VQ + cb) = pack8(src[i]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const unsigned pk = (unsigned)f2bf(src[0][e]) | ((unsigned)f2bf(src[1][e]) << 16);
+      *reinterpret_cast<unsigned *>(z.dqkvT + (int64_t)(cb + e) * VRP + 2 * f) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- B4: to_qkv backward, dWqkv, dWo
+// 256 threads.  Workgroups 0..31: dLN1[:, I] = dqkv Wqkv[:, I] (16 columns; 4 waves = K
+// quarters of 384, added in LDS); 32..223: dWqkv = dqkv^T LN1; 224..287: dWo = g_o^T o.
+__global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[16 * (VQ + 8) * 2 + 3 * 8 * 64 * 16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int blk = blockIdx.x;
+  if (blk >= 32 + 192) {
+    const int q = blk - 224;
+    wgrad_block(z.goT, s.oT, G.wo, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    return;
+  }
+  if (blk >= 32) {
+    const int q = blk - 32;
+    wgrad_block(z.dqkvT, s.ln1T, G.wqkv, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    return;
+  }
+  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
+  vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VQ + 8) * 2);
+  const int I0 = blk * 16;
+  stage_wT<16, VQ>(wT, p.wqkv, VD, I0, tid, 256);
+  __syncthreads();
+  const int li = lane & 15, lq = lane >> 4;
+  vf4 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
+  for (int sb = 0; sb < 12; sb += 2) {
+    vb8 af[2][8], bf[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = w * 384 + (sb + u) * 32 + lq * 8;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int r = t * 16 + li;
+        af[u][t] = r < R ? ld8b(z.dqkv + (int64_t)r * VQ + k) : zero8();
+      }
+      bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VQ + 8) + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
+  }
+  if (w > 0)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) red[((w - 1) * 8 + t) * 64 + lane] = acc[t];
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const vf4 a = red[(0 * 8 + t) * 64 + lane], b = red[(1 * 8 + t) * 64 + lane], c = red[(2 * 8 + t) * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = t * 16 + lq * 4 + e;
+      if (r < R) z.dln1[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- B5: LN1 backward + residual
+// 16 workgroups of 32 columns, 512 threads: dx0 = dx1 + LN1 backward(dLN1), dLN1 affine.
+__global__ __launch_bounds__(512) void vit_ln1_bwd_kernel(VitP p, VitG G, int R, const float *x0, VitSaved s,
+                                                          VitScratch z, float *dx0) {
+  __shared__ float sa[VRP], sbm[VRP], part[3 * 16 * 32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  lnb_rows(z.dln1, x0, p.ln1_w, s.mu1, s.rs1, R, sa, sbm, w, 8, lane);
+  __syncthreads();
+  lnb_cols(z.dln1, x0, p.ln1_w, s.mu1, s.rs1, z.dx1, R, sa, sbm, blockIdx.x * 32, dx0, G.ln1_w, G.ln1_b, false,
+           0.f, 0, nullptr, nullptr, part, tid);
+}
+
+}  // namespace ewvit
+
+using namespace ewvit;
+
+extern "C" int64_t ewvit_vit_layer_workspace(int which) {
+  return which == 0 ? saved_layout([](int, int64_t) {}) : scratch_layout([](int, int64_t) {});
+}
+
+static int vit_check(const ewvit_vit_layer *p, int R) {
+  EWVIT_CHECK_ARG(p && p->ln1_w && p->ln1_b && p->wqkv && p->wo && p->bo && p->ln2_w && p->ln2_b && p->w1 && p->b1 &&
+                      p->w2 && p->b2,
+                  "vit_layer: null parameter");
+  EWVIT_CHECK_ARG(R >= 2 && R <= VRP && R % 2 == 0, "vit_layer: R=%d rows (2 tokens per frame, <= %d)", R, VRP);
+  EWVIT_CHECK_ARG(p->drop_p >= 0.f && p->drop_p < 1.f, "vit_layer: drop_p=%f", (double)p->drop_p);
+  return 0;
+}
+
+extern "C" int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float *x0, void *saved, float *x2,
+                                   void *stream) {
+  if (int rc = vit_check(p, R)) return rc;
+  EWVIT_CHECK_ARG(x0 && saved && x2, "vit_layer_fwd: null pointer");
+  const VitSaved s = vit_saved(saved);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(vit_ln_gemm_kernel<0>, dim3(VQ / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL(vit_attn_proj_kernel, dim3(VD / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL(vit_ln_gemm_kernel<1>, dim3(VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
+  hipLaunchKernelGGL(vit_mlp2_kernel, dim3(VD / 32), dim3(1024), 0, st, *p, R, s, x2);
+  return launch_status("vit_layer_fwd");
+}
+
+extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float *x0, const void *saved,
+                                   const float *g, void *scratch, float *dx0, const ewvit_vit_grads *G,
+                                   void *stream) {
+  if (int rc = vit_check(p, R)) return rc;
+  EWVIT_CHECK_ARG(x0 && saved && g && scratch && dx0 && G, "vit_layer_bwd: null pointer");
+  EWVIT_CHECK_ARG(G->ln1_w && G->ln1_b && G->wqkv && G->wo && G->bo && G->ln2_w && G->ln2_b && G->w1 && G->b1 &&
+                      G->w2 && G->b2,
+                  "vit_layer_bwd: null gradient");
+  const VitSaved s = vit_saved(const_cast<void *>(saved));
+  const VitScratch z = vit_scratch(scratch);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
+  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(32 + 256 + 256), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
+  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(32 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
+  return launch_status("vit_layer_bwd");
+}

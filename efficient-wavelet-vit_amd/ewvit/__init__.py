@@ -2,7 +2,7 @@
 
 C-ABI: include/ewvit.h, built into ewvit/libewvit.so from csrc/*.hip.
 """
-from . import _lib, head, hfsep, optim
+from . import _lib, head, hfsep, optim, vit
 from .bn import batch_norm_act, batch_norm_act_params, batch_norm_drop_add
 from .conv import conv2d, conv3x3
 from .se import bn_act_se, drop_add, scale_add, squeeze_excite

@@ -108,11 +108,14 @@ SIGNATURES = {
                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_bwd_data_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
                                  _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
+    'ewvit_vit_layer_fwd': [_vp, _i32, _vp, _vp, _vp, _vp],
+    'ewvit_vit_layer_bwd': [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 
 # size queries: name -> (restype, argtypes)
 QUERIES = {
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
+    'ewvit_vit_layer_workspace': (_i64, [_i32]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),

@@ -29,10 +29,31 @@ def env_ranks():
     return rank, world, local
 
 
+def rccl_env():
+    """Process-group settings the captured step needs; they are read when a ProcessGroupNCCL
+    is constructed, so call this before ``init_process_group``.
+
+    * ``TORCH_NCCL_CUDA_EVENT_CACHE=0``: the end event of every collective is a fresh
+      event.  With the cache on, the events of collectives recorded inside a HIP graph
+      capture go back to the cache when their Work objects die, and a later EAGER collective
+      can be handed one of them; ProcessGroupNCCL's watchdog thread then queries it and HIP
+      answers hipErrorCapturedEvent ("operation not permitted on an event last recorded in a
+      capturing stream") — the watchdog rethrows and the process aborts.  Seen on the GPU box
+      as soon as a process issues eager collectives after a captured step (a second
+      TrainStep, the bench's eager timing pass): profiles/r04/dp_abort.log.
+    * ``TORCH_FR_BUFFER_SIZE``: the flight recorder's process-group status, which a
+      global-mode capture waits on (ewvit.graph.retire_eager_collectives).
+    * ``TORCH_NCCL_AVOID_RECORD_STREAMS``: the gradient buckets are persistent buffers."""
+    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
+    os.environ.setdefault('TORCH_FR_BUFFER_SIZE', '2000')
+    os.environ.setdefault('TORCH_NCCL_AVOID_RECORD_STREAMS', '1')
+
+
 def init_from_env(backend=None):
     """Initialise the process group from torchrun's env (MASTER_ADDR/PORT).
     backend: 'nccl' (RCCL) when a GPU is used, 'gloo' otherwise."""
     rank, world, local = env_ranks()
+    rccl_env()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = 'nccl' if torch.cuda.is_available() else 'gloo'

@@ -452,6 +452,11 @@ class TrainStep:
         profiles/r04/fr_probe.log) — so its queue is empty when the capture begins."""
         if not (self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl'):
             return
+        if os.environ.get('TORCH_NCCL_CUDA_EVENT_CACHE', '1') != '0':
+            import warnings
+            warnings.warn('TrainStep: capturing RCCL collectives with the process group\'s event cache on: a '
+                          'later eager collective can reuse a captured event and abort the NCCL watchdog '
+                          '(hipErrorCapturedEvent); call ewvit.dist.rccl_env() before init_process_group')
         if self._capture_mode != 'global':
             return
         retire_eager_collectives()

@@ -1,0 +1,115 @@
+"""One pre-norm ViT encoder layer of the spatial branch on csrc/vit.hip (reference
+network/sfe.py:72-85: x = Attention(LN(x)) + x; x = FeedForward(LN(x)) + x).
+
+At the hot path's shape — dim 512, 8 heads of 64, mlp 2048, 2 tokens per frame, <= 64 frames —
+the layer is 4 forward and 5 backward launches instead of the module path's 11 and ~25
+(LayerNorm, to_qkv, attention, to_out, LayerNorm, two Linears, their split-K reduces, the
+activation / dropout backward and column sums): every GEMM there is 128 rows against a fp32
+weight, so the layer is launch latency, not bytes or flops.  Roundings are the module path's
+(bf16 MFMA operands where ewvit_gemm rounds them, the bf16 attention output and dh), and the
+to_out dropout draws the same host seed and device counter, so the two paths agree to fp32
+summation order.  `network.sfe.Transformer` takes this path when the layer is in its shape
+class and nothing is hooked or patched (EWVIT_VIT_FUSED=0 keeps the module path).
+"""
+import ctypes
+import os
+
+import torch
+
+from . import _lib as L
+from . import grads
+from .grads import grad_out
+
+_vp, _f32, _u64 = ctypes.c_void_p, ctypes.c_float, ctypes.c_uint64
+
+
+class _Params(ctypes.Structure):
+    """include/ewvit.h ewvit_vit_layer."""
+    _fields_ = [('ln1_w', _vp), ('ln1_b', _vp), ('wqkv', _vp), ('wo', _vp), ('bo', _vp), ('ln2_w', _vp),
+                ('ln2_b', _vp), ('w1', _vp), ('b1', _vp), ('w2', _vp), ('b2', _vp), ('ln_eps', _f32),
+                ('drop_p', _f32), ('seed', _u64), ('seed_off', _vp)]
+
+
+class _Grads(ctypes.Structure):
+    """include/ewvit.h ewvit_vit_grads."""
+    _fields_ = [(n, _vp) for n in ('ln1_w', 'ln1_b', 'wqkv', 'wo', 'bo', 'ln2_w', 'ln2_b', 'w1', 'b1', 'w2', 'b2')]
+
+
+_WS = {}
+
+
+def _ws_bytes(which):
+    if which not in _WS:
+        _WS[which] = int(L.load().ewvit_vit_layer_workspace(which))
+    return _WS[which]
+
+
+def enabled():
+    return os.environ.get('EWVIT_VIT_FUSED', '1') != '0'
+
+
+def params_of(attn, ff):
+    """The 11 parameter tensors of one layer (PreNorm(Attention), PreNorm(FeedForward)) in the
+    kernel's order."""
+    a, f = attn.fn, ff.fn
+    return [attn.norm.weight, attn.norm.bias, a.to_qkv.weight, a.to_out[0].weight, a.to_out[0].bias,
+            ff.norm.weight, ff.norm.bias, f.net[0].weight, f.net[0].bias, f.net[3].weight, f.net[3].bias]
+
+
+def _params(ts, eps, drop_p, seed, dev):
+    p = _Params(*[t.data_ptr() for t in ts])
+    p.ln_eps, p.drop_p, p.seed = float(eps), float(drop_p), int(seed)
+    p.seed_off = L.rng_offset(dev).data_ptr() if drop_p > 0 else None
+    return p
+
+
+class ViTLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, x0, *ts):
+        L.require_gpu(x0, *ts)
+        eps, drop_p, seed = cfg
+        B = x0.shape[0]
+        R = 2 * B
+        x0c = x0.float().contiguous()
+        dev = x0.device
+        saved = torch.empty(_ws_bytes(0), dtype=torch.uint8, device=dev)
+        x2 = torch.empty_like(x0c)
+        p = _params(ts, eps, drop_p, seed, dev)
+        ctx.gen = grads.note_use(ts[0])
+        for t in ts[1:]:
+            grads.note_use(t)
+        L.call('ewvit_vit_layer_fwd', ctypes.addressof(p), R, L.ptr(x0c), L.ptr(saved), L.ptr(x2), L.stream(x2),
+               work={'flops': 2.0 * R * 512 * (1536 + 512 + 2 * 2048), 'bytes': 4.0 * sum(t.numel() for t in ts)})
+        ctx.cfg, ctx.R, ctx.ts = cfg, R, ts
+        ctx.save_for_backward(x0c, saved)
+        return x2
+
+    @staticmethod
+    def backward(ctx, g):
+        x0c, saved = ctx.saved_tensors
+        eps, drop_p, seed = ctx.cfg
+        ts, R = ctx.ts, ctx.R
+        dev = x0c.device
+        gc = g.float().contiguous()
+        scratch = torch.empty(_ws_bytes(1), dtype=torch.uint8, device=dev)
+        dx0 = torch.empty_like(x0c)
+        outs = []
+        for k, t in enumerate(ts):
+            # the kernels write every parameter gradient; a frozen one gets a scratch tensor
+            o = grad_out(t, ctx.gen) if ctx.needs_input_grad[2 + k] else torch.empty_like(t)
+            outs.append(o if o.is_contiguous() else torch.empty_like(t, memory_format=torch.contiguous_format))
+        p = _params(ts, eps, drop_p, seed, dev)
+        G = _Grads(*[o.data_ptr() for o in outs])
+        L.call('ewvit_vit_layer_bwd', ctypes.addressof(p), R, L.ptr(x0c), L.ptr(saved), L.ptr(gc), L.ptr(scratch),
+               L.ptr(dx0), ctypes.addressof(G), L.stream(dx0),
+               work={'flops': 4.0 * R * 512 * (1536 + 512 + 2 * 2048), 'bytes': 8.0 * sum(t.numel() for t in ts)})
+        return (None, dx0.reshape(g.shape), *[o if ctx.needs_input_grad[2 + k] else None for k, o in enumerate(outs)])
+
+
+def vit_layer(attn, ff, x, training):
+    """x [B, 2, 512] -> the layer's output [B, 2, 512] f32 (ViTLayerFn with the layer's
+    parameters; the to_out dropout draws its host seed as the module path's Linear does)."""
+    from .ops import _seed
+    drop = attn.fn.to_out[1].p if training else 0.0
+    cfg = (attn.norm.eps, float(drop), _seed() if drop > 0 else 0)
+    return ViTLayerFn.apply(cfg, x, *params_of(attn, ff))

@@ -135,9 +135,49 @@ class Transformer(nn.Module):                                              # sfe
     def forward(self, x):
         x = x.float()
         for attn, ff in self.layers:
+            if _vit_fusable(attn, ff, x):
+                # the layer on csrc/vit.hip: 4 launches forward, 5 backward (ewvit.vit)
+                x = ewvit.vit.vit_layer(attn, ff, x, self.training)
+                continue
             x = attn.forward_residual(x)
             x = ff.forward_residual(x)
         return x
+
+
+
+def _vit_fusable(attn, ff, x):
+    """The shape class of ewvit.vit (csrc/vit.hip): dim 512, 8 heads of 64, mlp 2048, 2 tokens
+    per frame, <= 64 frames, the reference's module structure (no hooks or patched forwards,
+    the FeedForward's dropouts 0 or eval), bf16 token GEMMs."""
+    if not (ewvit.vit.enabled() and x.is_cuda and x.dim() == 3 and x.shape[1] == 2 and x.shape[2] == 512
+            and 1 <= x.shape[0] <= 64):
+        return False
+    if type(attn) is not PreNorm or type(ff) is not PreNorm:
+        return False
+    a, f = attn.fn, ff.fn
+    if (type(a) is not Attention or type(f) is not FeedForward or 'forward' in a.__dict__ or 'forward' in f.__dict__
+            or type(a).forward_residual is not Attention.forward_residual or a.heads != 8 or a.dim_head != 64
+            or not isinstance(a.to_out, nn.Sequential) or len(f.net) != 5
+            or not isinstance(f.net[1], nn.GELU) or f.net[1].approximate != 'none'):
+        return False
+    lins = (a.to_qkv, a.to_out[0], f.net[0], f.net[3])
+    if any(type(m) is not Linear or _fp8(m) for m in lins) or a.to_qkv.bias is not None:
+        return False
+    if (tuple(a.to_qkv.weight.shape) != (1536, 512) or tuple(a.to_out[0].weight.shape) != (512, 512)
+            or tuple(f.net[0].weight.shape) != (2048, 512) or tuple(f.net[3].weight.shape) != (512, 2048)):
+        return False
+    norms = (attn.norm, ff.norm)
+    if any(type(n) not in (LayerNorm, nn.LayerNorm) or n.normalized_shape != (512,) or not n.elementwise_affine
+           for n in norms) or attn.norm.eps != ff.norm.eps:
+        return False
+    if ff.training and (f.net[2].p > 0 or f.net[4].p > 0):
+        return False
+    ts = [attn.norm.weight, attn.norm.bias, a.to_qkv.weight, a.to_out[0].weight, a.to_out[0].bias, ff.norm.weight,
+          ff.norm.bias, f.net[0].weight, f.net[0].bias, f.net[3].weight, f.net[3].bias]
+    if any(t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda for t in ts):
+        return False
+    mods = [attn, ff, a, f, attn.norm, ff.norm, a.to_qkv, a.to_out, *a.to_out, *f.net]
+    return not any(_hooked(m) for m in mods)
 
 
 class EfficientViT(nn.Module):                                             # sfe.py:87-173

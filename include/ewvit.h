@@ -678,6 +678,40 @@ int ewvit_head_bwd(const ewvit_head_params *p, const float *workspace, int N, co
                    float *const *lnb, float *wfg, int64_t fg_so, int64_t fg_si, int64_t fg_tap, float *bfg,
                    float *bn_w, float *bn_b, float *g1w, float *g1b, float *g2w, float *g2b, void *stream);
 
+/* ------------------------------------------------ ViT encoder layer ---
+ * One pre-norm layer of the spatial branch's Transformer (reference network/sfe.py:72-85):
+ *   x1 = x0 + Dropout(to_out(Attention(LayerNorm(x0))))      (sfe.py:20-27, 42-70)
+ *   x2 = x1 + Linear2(GELU(Linear1(LayerNorm(x1))))         (sfe.py:29-40, FeedForward dropout 0)
+ * at the hot path's shape: dim 512, 8 heads of 64, mlp 2048, 2 tokens per frame (CLS + the one
+ * 7x7 patch), R = 2 * frames <= 128 rows (row 2b + i = token i of frame b).  Replaces the 11
+ * forward / ~25 backward module-level launches of the layer (LayerNorm, to_qkv, attention,
+ * to_out, LayerNorm, two Linears, the split-K reduces, act / dropout backward, column sums)
+ * with 4 forward / 5 backward launches.  fp32 master parameters read in place (bf16 MFMA
+ * operands, fp32 accumulation, the module path's roundings); the dropout mask of to_out is the
+ * module path's: keep(seed + *seed_off * golden, row * 512 + col). */
+typedef struct {
+  const float *ln1_w, *ln1_b;   /* layers[i][0].norm: LayerNorm(512) */
+  const float *wqkv;            /* to_qkv.weight [1536][512] (no bias) */
+  const float *wo, *bo;         /* to_out[0]: [512][512], [512] */
+  const float *ln2_w, *ln2_b;   /* layers[i][1].norm */
+  const float *w1, *b1;         /* net[0]: [2048][512], [2048] */
+  const float *w2, *b2;         /* net[3]: [512][2048], [512] */
+  float ln_eps, drop_p;         /* LayerNorm eps; to_out dropout probability (0 in eval) */
+  uint64_t seed;
+  const int64_t *seed_off;
+} ewvit_vit_layer;
+typedef struct {                /* parameter gradients (overwritten), parameter layouts */
+  float *ln1_w, *ln1_b, *wqkv, *wo, *bo, *ln2_w, *ln2_b, *w1, *b1, *w2, *b2;
+} ewvit_vit_grads;
+/* bytes of the forward's saved state (which = 0) and of the backward's scratch (which = 1) */
+int64_t ewvit_vit_layer_workspace(int which);
+/* x0 [R][512] f32 -> x2 [R][512] f32; `saved` (ewvit_vit_layer_workspace(0) bytes) keeps what
+ * the backward reads (LayerNorm statistics, qkv, softmax weights, the GEMM operands). */
+int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float *x0, void *saved, float *x2, void *stream);
+/* g = dL/dx2 [R][512] f32 -> dx0 [R][512] f32 and every parameter gradient. */
+int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float *x0, const void *saved, const float *g,
+                        void *scratch, float *dx0, const ewvit_vit_grads *grads, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,10 +37,11 @@ def _port():
 
 @pytest.fixture(scope='module')
 def nccl_world1():
-    os.environ.setdefault('TORCH_NCCL_AVOID_RECORD_STREAMS', '1')
-    # the flight recorder's process-group status is what a global-mode capture waits on
-    # (ewvit.graph.retire_eager_collectives): enabled before the group exists
-    os.environ.setdefault('TORCH_FR_BUFFER_SIZE', '2000')
+    from ewvit import dist as edist
+    # before the group exists: no event cache (a captured collective's event must never be
+    # handed to a later eager collective the watchdog polls), the flight recorder's
+    # process-group status a global-mode capture waits on (ewvit.graph.retire_eager_collectives)
+    edist.rccl_env()
     os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
     torch.cuda.set_device(0)
     dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{_port()}', rank=0, world_size=1)

@@ -1,0 +1,124 @@
+"""The fused ViT encoder layer (csrc/vit.hip, ewvit.vit) against the module path of
+network/sfe.py (the same reference semantics, sfe.py:72-85, on ewvit GEMM / LayerNorm /
+attention kernels) and against the fp32 oracle.
+
+The fused and module paths round the same operands to bf16 (LN outputs, q/k/v, the attention
+output, h, dh, g1, dqkv) and draw the same to_out dropout mask (host seed + device counter,
+index row * 512 + col); they differ in fp32 summation order only (split-K vs per-wave K
+halves, column sums).  Bounds: outputs max |err| <= 2e-3 of scale and cosine >= 0.99999, every
+parameter and the input gradient cosine >= 0.9999 with the norm within 0.3 %, with dropout on
+and off, for 64 / 37 / 8 / 1 frames.  Against the oracle (fp32 CPU restatement): the bf16
+bounds of the module path's own tests (2e-2 of scale, cosine >= 0.999 / gradients 0.99).
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _cos(a, b):
+    a, b = a.detach().double().flatten(), b.detach().double().flatten()
+    return float(a @ b / (a.norm() * b.norm() + 1e-30))
+
+
+def _vit(drop, seed=0):
+    from network.sfe import Transformer
+    torch.manual_seed(seed)
+    m = Transformer(512, 2, 8, 64, 2048, drop).to(DEV)
+    with torch.no_grad():            # non-trivial LayerNorm affine / biases
+        for n, p in m.named_parameters():
+            if p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+    return m
+
+
+def _run(m, x0, fused, monkeypatch, seed=11):
+    import ewvit
+    monkeypatch.setenv('EWVIT_VIT_FUSED', '1' if fused else '0')
+    calls = {}
+    real = ewvit._lib.call
+
+    def count(name, *a, **k):
+        calls[name] = calls.get(name, 0) + 1
+        return real(name, *a, **k)
+    monkeypatch.setattr(ewvit._lib, 'call', count)
+    x = x0.clone().requires_grad_(True)
+    torch.manual_seed(seed)                  # the to_out dropout's host seeds
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = m(x)
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(y.shape, generator=g).to(DEV)
+    (y.float() * w).sum().backward()
+    torch.cuda.synchronize()
+    monkeypatch.undo()
+    grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+    return y.detach().float(), x.grad.clone(), grads, calls
+
+
+@pytest.mark.parametrize('N', [64, 37, 8, 1])
+@pytest.mark.parametrize('drop', [0.0, 0.15])
+def test_vit_layer_matches_module_path(N, drop, monkeypatch):
+    m0 = _vit(drop).train()
+    g = torch.Generator().manual_seed(N)
+    x0 = (torch.randn(N, 2, 512, generator=g) * 1.5 + 0.3).to(DEV)
+    a, b = copy.deepcopy(m0), copy.deepcopy(m0)
+    ya, dxa, ga, ca = _run(a, x0, True, monkeypatch)
+    yb, dxb, gb, cb = _run(b, x0, False, monkeypatch)
+    assert ca.get('ewvit_vit_layer_fwd') == 2 and ca.get('ewvit_vit_layer_bwd') == 2, ca
+    assert 'ewvit_vit_layer_fwd' not in cb and cb.get('ewvit_gemm', 0) > 0, cb
+    scale = float(yb.abs().max())
+    err = float((ya - yb).abs().max())
+    assert err <= 2e-3 * scale and _cos(ya, yb) >= 0.99999, (err, scale, _cos(ya, yb))
+    assert _cos(dxa, dxb) >= 0.9999
+    assert abs(float(dxa.norm() / dxb.norm()) - 1) < 3e-3
+    for n in gb:
+        c = _cos(ga[n], gb[n])
+        r = float(ga[n].norm() / gb[n].norm())
+        assert c >= 0.9999 and abs(r - 1) < 3e-3, (n, c, r)
+
+
+def test_vit_layer_eval_and_dropout_mask_per_replay(monkeypatch):
+    """Eval mode: no dropout (two calls equal); training mode: the mask follows the device step
+    counter (a new mask per advance), and the module path draws the same one."""
+    import ewvit
+    m = _vit(0.15).eval()
+    x0 = torch.randn(16, 2, 512, device=DEV)
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        y1, y2 = m(x0), m(x0)
+    assert torch.equal(y1, y2)
+    m.train()
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        torch.manual_seed(3)
+        a = m(x0)
+        ewvit._lib.rng_advance(torch.device(DEV))
+        torch.manual_seed(3)
+        b = m(x0)
+    assert not torch.equal(a, b)
+
+
+def test_vit_layer_vs_oracle():
+    """The fused path against the fp32 CPU restatement of sfe.Transformer (oracle/model.py)."""
+    from oracle import model as om
+    from oracle.weights import apply_recipe
+    from network import sfe
+    o = apply_recipe(om.Transformer(512, 2, 8, 64, 2048, 0.0), 3)
+    p = sfe.Transformer(512, 2, 8, 64, 2048, 0.0)
+    p.load_state_dict(o.state_dict())
+    p = p.to(DEV)
+    t = torch.randn(64, 2, 512, generator=torch.Generator().manual_seed(1))
+    to, tp = t.clone().requires_grad_(True), t.to(DEV).requires_grad_(True)
+    yo = o(to)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        yp = p(tp)
+    w = torch.randn(yo.shape, generator=torch.Generator().manual_seed(2))
+    (yo * w).sum().backward()
+    (yp.float() * w.to(DEV)).sum().backward()
+    scale = float(yo.abs().max())
+    assert float((yp.detach().cpu() - yo.detach()).abs().max()) < 2e-2 * scale
+    assert _cos(yp.cpu(), yo) >= 0.999
+    assert _cos(tp.grad.cpu(), to.grad) >= 0.99
+    for (n, a), (_, b) in zip(o.named_parameters(), p.named_parameters()):
+        assert _cos(b.grad.cpu(), a.grad) >= 0.99, n
