@@ -1880,7 +1880,9 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   const int64_t NP = (int64_t)g.ks * g.ks * g.Cin;
   const int64_t tn = wide ? 2 * CBN : CBN;
   const int64_t tiles = ((NP + tn - 1) / tn) * ((g.Cout + CBM - 1) / CBM);
-  int64_t s = 512 / tiles;        // (fewer, longer splits measured slower)
+  // (fewer, longer splits measured slower: 256 / 128 target workgroups for the backbone's
+  // <= 28^2 maps 3231-3233 / 3148 frames/s against 3214-3231 at 512, round 4)
+  int64_t s = 512 / tiles;
   if (g_grid_cap > 0 && s * tiles > g_grid_cap) s = g_grid_cap / tiles;
   const int64_t maxs = M / 256;
   if (s > maxs) s = maxs;

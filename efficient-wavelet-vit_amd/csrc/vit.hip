@@ -149,20 +149,28 @@ inline VitScratch vit_scratch(void *base) {
 // LayerNorm statistics of rows w, w + nw, ... (< 128; rows >= R get 0 / 0): a wave per row,
 // 8 contiguous columns per lane; two-pass mean / centred variance, biased, eps inside the
 // rsqrt (torch's formula, layernorm.hip's)
+template <int NW>
 __device__ __forceinline__ void ln_stats_rows(const float *x, int R, float eps, float *smu, float *srs, int w,
-                                              int nw, int lane) {
-  for (int r = w; r < VRP; r += nw) {
+                                              int lane) {
+  constexpr int NR = VRP / NW;          // rows of this wave: w, w + NW, ... (all loads in flight)
+  float v[NR][8];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = w + i * NW;
+    if (r < R) ld8f(x + (int64_t)r * VD + lane * 8, v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = w + i * NW;
     float mu = 0.f, rs = 0.f;
     if (r < R) {
-      float v[8];
-      ld8f(x + (int64_t)r * VD + lane * 8, v);
       float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[e];
+      for (int e = 0; e < 8; ++e) s += v[i][e];
       mu = wave_sum(s) / (float)VD;
       float q = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+      for (int e = 0; e < 8; ++e) q += (v[i][e] - mu) * (v[i][e] - mu);
       rs = rsqrtf(wave_sum(q) / (float)VD + eps);
     }
     if (lane == 0) { smu[r] = mu; srs[r] = rs; }
@@ -204,17 +212,27 @@ __device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, 
 
 // the weight slice W[o][c0 .. c0 + NC) (o < NO, fp32, row stride ldw) as a k-contiguous bf16
 // LDS image wT[c][o] (row pitch NO + 8)
-template <int NC, int NO>
-__device__ __forceinline__ void stage_wT(bf16_t *wT, const float *W, int64_t ldw, int c0, int tid, int nthr) {
-  constexpr int Q = NC / 4;
-  for (int it = tid; it < NO * Q; it += nthr) {
-    const int o = it / Q, q = it - o * Q;
-    const float4 v = *reinterpret_cast<const float4 *>(W + (int64_t)o * ldw + c0 + 4 * q);
-    bf16_t *d = wT + (4 * q) * (NO + 8) + o;
-    d[0] = f2bf(v.x);
-    d[NO + 8] = f2bf(v.y);
-    d[2 * (NO + 8)] = f2bf(v.z);
-    d[3 * (NO + 8)] = f2bf(v.w);
+template <int NC, int NO, int NTHR>
+__device__ __forceinline__ void stage_wT(bf16_t *wT, const float *W, int64_t ldw, int c0, int tid) {
+  constexpr int Q = NC / 4, IT = NO * Q / NTHR, BT = IT < 8 ? IT : 8;
+  static_assert(IT * NTHR == NO * Q && IT % BT == 0, "stage_wT: shape");
+#pragma unroll
+  for (int b0 = 0; b0 < IT; b0 += BT) {
+    float4 v[BT];
+#pragma unroll
+    for (int u = 0; u < BT; ++u) {
+      const int it = tid + (b0 + u) * NTHR, o = it / Q, q = it - o * Q;
+      v[u] = *reinterpret_cast<const float4 *>(W + (int64_t)o * ldw + c0 + 4 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < BT; ++u) {
+      const int it = tid + (b0 + u) * NTHR, o = it / Q, q = it - o * Q;
+      bf16_t *d = wT + (4 * q) * (NO + 8) + o;
+      d[0] = f2bf(v[u].x);
+      d[NO + 8] = f2bf(v[u].y);
+      d[2 * (NO + 8)] = f2bf(v[u].z);
+      d[3 * (NO + 8)] = f2bf(v[u].w);
+    }
   }
 }
 
@@ -229,7 +247,7 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float *gw = MODE ? p.ln2_w : p.ln1_w, *gb = MODE ? p.ln2_b : p.ln1_b;
   const float *W = MODE ? p.w1 : p.wqkv;
-  ln_stats_rows(xin, R, p.ln_eps, smu, srs, w, 8, lane);
+  ln_stats_rows<8>(xin, R, p.ln_eps, smu, srs, w, lane);
   __syncthreads();
   if (blockIdx.x == 0 && tid < VRP) {
     (MODE ? s.mu2 : s.mu1)[tid] = smu[tid];
@@ -343,45 +361,49 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
   __shared__ vf4 red[4][2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int B = R >> 1;
-  for (int it = tid >> 3; it < (VRP / 2) * VH; it += 64) {
-    const int b = it >> 3, h = it & 7, d0 = (tid & 7) * 8;
+  {
+    // thread = (frame b, head h): the 4 dot products of 64 of the frame's 2x2 scores
+    const int b = tid >> 3, h = tid & 7;
     float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
     if (b < B) {
-      float q0[8], q1[8], k0[8], k1[8];
-      unpack8(ld8b(s.qkv + (int64_t)(2 * b) * VQ + h * VDH + d0), q0);
-      unpack8(ld8b(s.qkv + (int64_t)(2 * b + 1) * VQ + h * VDH + d0), q1);
-      unpack8(ld8b(s.qkv + (int64_t)(2 * b) * VQ + VD + h * VDH + d0), k0);
-      unpack8(ld8b(s.qkv + (int64_t)(2 * b + 1) * VQ + VD + h * VDH + d0), k1);
+      const bf16_t *q0p = s.qkv + (int64_t)(2 * b) * VQ + h * VDH, *q1p = q0p + VQ;
+      vb8 a0[8], a1[8], c0[8], c1[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s00 += q0[e] * k0[e];
-        s01 += q0[e] * k1[e];
-        s10 += q1[e] * k0[e];
-        s11 += q1[e] * k1[e];
+      for (int u = 0; u < 8; ++u) {
+        a0[u] = ld8b(q0p + u * 8);
+        a1[u] = ld8b(q1p + u * 8);
+        c0[u] = ld8b(q0p + VD + u * 8);
+        c1[u] = ld8b(q1p + VD + u * 8);
       }
-    }
 #pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      s00 += __shfl_xor(s00, m, 64);
-      s01 += __shfl_xor(s01, m, 64);
-      s10 += __shfl_xor(s10, m, 64);
-      s11 += __shfl_xor(s11, m, 64);
-    }
-    if ((tid & 7) == 0) {
-      const float sc[2][2] = {{s00 * VSCALE, s01 * VSCALE}, {s10 * VSCALE, s11 * VSCALE}};
+      for (int u = 0; u < 8; ++u) {
+        float q0[8], q1[8], k0[8], k1[8];
+        unpack8(a0[u], q0);
+        unpack8(a1[u], q1);
+        unpack8(c0[u], k0);
+        unpack8(c1[u], k1);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        float p0 = 0.f, p1 = 0.f;
-        if (b < B) {
-          const float mx = fmaxf(sc[i][0], sc[i][1]);
-          const float e0 = __expf(sc[i][0] - mx), e1 = __expf(sc[i][1] - mx);
-          const float inv = 1.0f / (e0 + e1);
-          p0 = e0 * inv;
-          p1 = e1 * inv;
+        for (int e = 0; e < 8; ++e) {
+          s00 += q0[e] * k0[e];
+          s01 += q0[e] * k1[e];
+          s10 += q1[e] * k0[e];
+          s11 += q1[e] * k1[e];
         }
-        sp[2 * b + i][h][0] = p0;
-        sp[2 * b + i][h][1] = p1;
       }
+    }
+    const float sc[2][2] = {{s00 * VSCALE, s01 * VSCALE}, {s10 * VSCALE, s11 * VSCALE}};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float p0 = 0.f, p1 = 0.f;
+      if (b < B) {
+        const float mx = fmaxf(sc[i][0], sc[i][1]);
+        const float e0 = __expf(sc[i][0] - mx), e1 = __expf(sc[i][1] - mx);
+        const float inv = 1.0f / (e0 + e1);
+        p0 = e0 * inv;
+        p1 = e1 * inv;
+      }
+      sp[2 * b + i][h][0] = p0;
+      sp[2 * b + i][h][1] = p1;
     }
   }
   __syncthreads();
@@ -544,7 +566,7 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
   __shared__ float scol[4][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int J0 = blockIdx.x * 32;
-  stage_wT<32, VD>(wT, p.w2, VF, J0, tid, 512);
+  stage_wT<32, VD, 512>(wT, p.w2, VF, J0, tid);
   if (tid < VRP) {
     const int r = tid;
     float v[8];
@@ -659,16 +681,16 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
   bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
   vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VF + 8) * 2);
   const int I0 = blk * 16;
-  stage_wT<16, VF>(wT, p.w1, VD, I0, tid, 256);
+  stage_wT<16, VF, 256>(wT, p.w1, VD, I0, tid);
   __syncthreads();
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
-  for (int sb = 0; sb < 16; sb += 2) {
-    vb8 af[2][8], bf[2];
+  for (int sb = 0; sb < 16; sb += 4) {
+    vb8 af[4][8], bf[4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int k = w * 512 + (sb + u) * 32 + lq * 8;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -678,7 +700,7 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
       bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VF + 8) + k);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
   }
@@ -702,24 +724,35 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
 // per-row sums of the LN backward, a wave per row: ma = mean(gamma dY), mb = mean(gamma dY xhat)
 __device__ __forceinline__ void lnb_rows(const float *dY, const float *X, const float *gamma, const float *mu,
                                          const float *rs, int R, float *sa, float *sb, int w, int nw, int lane) {
-  for (int r = w; r < VRP; r += nw) {
-    float a = 0.f, b = 0.f;
-    if (r < R) {
-      float d[8], x[8], gm[8];
-      ld8f(dY + (int64_t)r * VD + lane * 8, d);
-      ld8f(X + (int64_t)r * VD + lane * 8, x);
-      ld8f(gamma + lane * 8, gm);
-      const float m = mu[r], s = rs[r];
+  float gm[8];
+  ld8f(gamma + lane * 8, gm);
+  for (int r0 = w; r0 < VRP; r0 += 4 * nw) {
+    float d[4][8], x[4][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float gd = gm[e] * d[e];
-        a += gd;
-        b += gd * ((x[e] - m) * s);
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + i * nw;
+      if (r < R) {
+        ld8f(dY + (int64_t)r * VD + lane * 8, d[i]);
+        ld8f(X + (int64_t)r * VD + lane * 8, x[i]);
       }
-      a = wave_sum(a) / (float)VD;
-      b = wave_sum(b) / (float)VD;
     }
-    if (lane == 0) { sa[r] = a; sb[r] = b; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + i * nw;
+      float a = 0.f, b = 0.f;
+      if (r < R) {
+        const float m = mu[r], s = rs[r];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gd = gm[e] * d[i][e];
+          a += gd;
+          b += gd * ((x[i][e] - m) * s);
+        }
+        a = wave_sum(a) / (float)VD;
+        b = wave_sum(b) / (float)VD;
+      }
+      if (lane == 0 && r < VRP) { sa[r] = a; sb[r] = b; }
+    }
   }
 }
 // columns c0 .. c0 + 32, 512 threads (column tid & 31, rows 8 (tid >> 5) .. + 8):
@@ -793,7 +826,7 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
   const int h = blockIdx.x;
   bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
   float *sdo = reinterpret_cast<float *>(smem + 64 * (VD + 8) * 2);   // [128][68]
-  stage_wT<64, VD>(wT, p.wo, VD, h * VDH, tid, 512);
+  stage_wT<64, VD, 512>(wT, p.wo, VD, h * VDH, tid);
   __syncthreads();
   const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
   int row[2];
@@ -953,16 +986,16 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
   bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
   vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VQ + 8) * 2);
   const int I0 = blk * 16;
-  stage_wT<16, VQ>(wT, p.wqkv, VD, I0, tid, 256);
+  stage_wT<16, VQ, 256>(wT, p.wqkv, VD, I0, tid);
   __syncthreads();
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
-  for (int sb = 0; sb < 12; sb += 2) {
-    vb8 af[2][8], bf[2];
+  for (int sb = 0; sb < 12; sb += 4) {
+    vb8 af[4][8], bf[4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int k = w * 384 + (sb + u) * 32 + lq * 8;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -972,7 +1005,7 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
       bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VQ + 8) + k);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
   }
@@ -1002,6 +1035,66 @@ __global__ __launch_bounds__(512) void vit_ln1_bwd_kernel(VitP p, VitG G, int R,
   __syncthreads();
   lnb_cols(z.dln1, x0, p.ln1_w, s.mu1, s.rs1, z.dx1, R, sa, sbm, blockIdx.x * 32, dx0, G.ln1_w, G.ln1_b, false,
            0.f, 0, nullptr, nullptr, part, tid);
+}
+
+
+// ---------------------------------------------------------------- token embedding (sfe.py:155-160)
+// tok[b][0] = drop(cls + pos[b]), tok[b][1] = drop(y[b] + pos[b]) (pos_embedding[0:B] broadcast
+// over the 2 tokens); dropout keep(seed, (b * 2 + i) * 512 + c).  One thread per 4 columns.
+__global__ __launch_bounds__(256) void vit_embed_fwd_kernel(const float *y, const float *cls, const float *pos, int B,
+                                                            float dp, uint64_t seed, const int64_t *seed_off,
+                                                            float *tok) {
+  const int i = blockIdx.x * 256 + threadIdx.x;          // (b, token, column quad)
+  if (i >= B * 2 * (VD / 4)) return;
+  const int c = (i % (VD / 4)) * 4, t = (i / (VD / 4)) & 1, b = i / (2 * (VD / 4));
+  const float4 src = *reinterpret_cast<const float4 *>((t ? y + (int64_t)b * VD : cls) + c);
+  const float4 pe = *reinterpret_cast<const float4 *>(pos + (int64_t)b * VD + c);
+  float v[4] = {src.x + pe.x, src.y + pe.y, src.z + pe.z, src.w + pe.w};
+  if (dp > 0.f) {
+    const uint64_t sd = step_seed(seed, seed_off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= keep_scale(dp, sd, (uint64_t)((b * 2 + t) * VD + c + e));
+  }
+  *reinterpret_cast<float4 *>(tok + ((int64_t)b * 2 + t) * VD + c) = make_float4(v[0], v[1], v[2], v[3]);
+}
+// d y[b] = m dtok[b][1], d pos[b] = m dtok[b][0] + m dtok[b][1] (rows >= B: 0, up to npos <= 64),
+// d cls = sum_b m dtok[b][0] (fixed order).  8 workgroups of 64 columns; thread (column,
+// frame group q) takes frames q, q + 8, ... with all loads in flight.
+__global__ __launch_bounds__(512) void vit_embed_bwd_kernel(const float *dtok, int B, int npos, float dp, uint64_t seed,
+                                                            const int64_t *seed_off, float *dy, float *dcls,
+                                                            float *dpos) {
+  __shared__ float part[8][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  const uint64_t sd = step_seed(seed, seed_off);
+  float g0[8], g1[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int b = q + 8 * u;
+    g0[u] = b < B ? dtok[((int64_t)b * 2) * VD + c] : 0.f;
+    g1[u] = b < B ? dtok[((int64_t)b * 2 + 1) * VD + c] : 0.f;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int b = q + 8 * u;
+    if (b < B) {
+      if (dp > 0.f) {
+        g0[u] *= keep_scale(dp, sd, (uint64_t)((b * 2) * VD + c));
+        g1[u] *= keep_scale(dp, sd, (uint64_t)((b * 2 + 1) * VD + c));
+      }
+      dy[(int64_t)b * VD + c] = g1[u];
+      acc += g0[u];
+    }
+    if (b < npos) dpos[(int64_t)b * VD + c] = g0[u] + g1[u];
+  }
+  part[q][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (q == 0) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += part[k][threadIdx.x];
+    dcls[c] = a;
+  }
 }
 
 }  // namespace ewvit
@@ -1051,4 +1144,22 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(32 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
   hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
   return launch_status("vit_layer_bwd");
+}
+
+extern "C" int ewvit_vit_embed_fwd(const float *y, const float *cls, const float *pos, int B, float drop_p,
+                                   uint64_t seed, const int64_t *seed_off, float *tok, void *stream) {
+  EWVIT_CHECK_ARG(y && cls && pos && tok && B >= 1 && drop_p >= 0.f && drop_p < 1.f, "vit_embed_fwd: bad args");
+  const int n = B * 2 * (VD / 4);
+  hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), y, cls, pos, B, drop_p,
+                     seed, seed_off, tok);
+  return launch_status("vit_embed_fwd");
+}
+
+extern "C" int ewvit_vit_embed_bwd(const float *dtok, int B, int npos, float drop_p, uint64_t seed,
+                                   const int64_t *seed_off, float *dy, float *dcls, float *dpos, void *stream) {
+  EWVIT_CHECK_ARG(dtok && dy && dcls && dpos && B >= 1 && npos >= B && npos <= 64 && drop_p >= 0.f && drop_p < 1.f,
+                  "vit_embed_bwd: bad args");
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, dim3(VD / 64), dim3(512), 0, as_stream(stream), dtok, B, npos, drop_p, seed,
+                     seed_off, dy, dcls, dpos);
+  return launch_status("vit_embed_bwd");
 }

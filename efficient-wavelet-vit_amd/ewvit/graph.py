@@ -440,26 +440,35 @@ class TrainStep:
         """Before a capture that records RCCL collectives.  Every EAGER collective (the warm-up
         steps' bucket all-reduces and buffer broadcasts, the layout broadcast) is queued to
         ProcessGroupNCCL's watchdog thread, which polls the collective's end event
-        (hipEventQuery) until it sees it complete and then drops it.  Collectives issued
-        during a capture are never queued.  Such a poll from another thread while this one
-        captures is illegal in the GLOBAL capture mode (the watchdog's query fails and it
-        aborts the process); in the default RELAXED mode (`EWVIT_CAPTURE_MODE`) it is legal,
-        so nothing has to be drained.  In global mode: after the device has drained, wait
-        until the watchdog has retired every collective enqueued so far — its own progress
-        marker, `last_completed_collective == last_enqueued_collective` of each process group
-        in the flight-recorder status (enabled by TORCH_FR_BUFFER_SIZE > 0 before the group is
-        created; the watchdog polls about every 100 ms: tools/fr_probe.py,
-        profiles/r04/fr_probe.log) — so its queue is empty when the capture begins."""
+        (hipEventQuery) until it sees it complete and then drops it (about every 100 ms:
+        tools/fr_probe.py, profiles/r04/fr_probe.log).  Those events were recorded on the
+        process group's stream, and the first collective of the capture makes that stream
+        part of the capture: a poll of such an event from the watchdog thread while the capture
+        runs fails with hipErrorCapturedEvent ("operation not permitted on an event last
+        recorded in a capturing stream") in EITHER capture mode — the watchdog rethrows and
+        aborts the process, and the capture itself is invalidated (the next launch of the
+        capturing thread reports "operation failed due to a previous error during capture";
+        profiles/r04/dp_abort.log).  So, in both modes: after the device has drained, wait until
+        the watchdog has retired every collective enqueued so far — its own progress marker,
+        `last_completed_collective == last_enqueued_collective` of each process group in the
+        flight-recorder status (TORCH_FR_BUFFER_SIZE > 0 before the group is created:
+        ewvit.dist.rccl_env) — so its queue is empty when the capture begins.  Collectives issued
+        during the capture are never queued."""
         if not (self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl'):
             return
+        import warnings
         if os.environ.get('TORCH_NCCL_CUDA_EVENT_CACHE', '1') != '0':
-            import warnings
             warnings.warn('TrainStep: capturing RCCL collectives with the process group\'s event cache on: a '
                           'later eager collective can reuse a captured event and abort the NCCL watchdog '
                           '(hipErrorCapturedEvent); call ewvit.dist.rccl_env() before init_process_group')
-        if self._capture_mode != 'global':
-            return
-        retire_eager_collectives()
+        try:
+            retire_eager_collectives()
+        except RuntimeError:
+            if self._capture_mode == 'global' or _pg_status():
+                raise
+            warnings.warn('TrainStep: the flight recorder is off (TORCH_FR_BUFFER_SIZE), so the NCCL watchdog '
+                          'queue cannot be drained before the capture; call ewvit.dist.rccl_env() before '
+                          'init_process_group')
 
     def _finish_capture(self, graph):
         fin = getattr(self.opt, 'finish_capture', None)

@@ -113,3 +113,42 @@ def vit_layer(attn, ff, x, training):
     drop = attn.fn.to_out[1].p if training else 0.0
     cfg = (attn.norm.eps, float(drop), _seed() if drop > 0 else 0)
     return ViTLayerFn.apply(cfg, x, *params_of(attn, ff))
+
+
+class EmbedFn(torch.autograd.Function):
+    """tok = Dropout(cat(cls, y) + pos_embedding[0:B]) for one patch per frame (sfe.py:155-160):
+    one launch each way instead of cat / add / dropout and their backward (slice, sums)."""
+
+    @staticmethod
+    def forward(ctx, drop_p, seed, y, cls, pos):
+        L.require_gpu(y, cls, pos)
+        B = y.shape[0]
+        yc = y.float().reshape(B, 512).contiguous()
+        tok = torch.empty(B, 2, 512, dtype=torch.float32, device=y.device)
+        off = L.rng_offset(y.device) if drop_p > 0 else None
+        ctx.gen = grads.note_use(cls)
+        grads.note_use(pos)
+        L.call('ewvit_vit_embed_fwd', L.ptr(yc), L.ptr(cls), L.ptr(pos), B, float(drop_p), int(seed), L.ptr(off),
+               L.ptr(tok), L.stream(tok))
+        ctx.cfg = (float(drop_p), int(seed), B, y.shape)
+        ctx.params = (cls, pos)
+        return tok
+
+    @staticmethod
+    def backward(ctx, g):
+        drop_p, seed, B, yshape = ctx.cfg
+        cls, pos = ctx.params
+        gc = g.float().contiguous()
+        dy = torch.empty(B, 512, dtype=torch.float32, device=g.device)
+        dcls = grad_out(cls, ctx.gen) if ctx.needs_input_grad[3] else torch.empty_like(cls)
+        dpos = grad_out(pos, ctx.gen) if ctx.needs_input_grad[4] else torch.empty_like(pos)
+        off = L.rng_offset(g.device) if drop_p > 0 else None
+        L.call('ewvit_vit_embed_bwd', L.ptr(gc), B, pos.shape[0], drop_p, seed, L.ptr(off), L.ptr(dy), L.ptr(dcls),
+               L.ptr(dpos), L.stream(dy))
+        return (None, None, dy.reshape(yshape), dcls if ctx.needs_input_grad[3] else None,
+                dpos if ctx.needs_input_grad[4] else None)
+
+
+def embed(y, cls, pos, drop_p):
+    from .ops import _seed
+    return EmbedFn.apply(float(drop_p), _seed() if drop_p > 0 else 0, y, cls, pos)

@@ -149,6 +149,8 @@ def _vit_fusable(attn, ff, x):
     """The shape class of ewvit.vit (csrc/vit.hip): dim 512, 8 heads of 64, mlp 2048, 2 tokens
     per frame, <= 64 frames, the reference's module structure (no hooks or patched forwards,
     the FeedForward's dropouts 0 or eval), bf16 token GEMMs."""
+    if torch.compiler.is_compiling():        # traced (torch.compile): the custom-op module path
+        return False
     if not (ewvit.vit.enabled() and x.is_cuda and x.dim() == 3 and x.shape[1] == 2 and x.shape[2] == 512
             and 1 <= x.shape[0] <= 64):
         return False
@@ -229,8 +231,15 @@ class EfficientViT(nn.Module):                                             # sfe
         y = self.patches(x)
         pe = self.patch_to_embedding
         y = ewvit.linear(y, pe.weight, pe.bias, out_dtype=torch.float32, fp8=_fp8(pe))
-        tok = torch.cat((self.cls_token.expand(B, -1, -1), y), 1) + self.pos_embedding[0:B]
-        tok = self.dropout(tok)
+        if (ewvit.vit.enabled() and y.shape[1:] == (1, 512) and self.cls_token.shape == (1, 1, 512)
+                and self.pos_embedding.shape[1:] == (1, 512) and self.pos_embedding.shape[0] <= 64
+                and type(self.dropout) is nn.Dropout
+                and not _hooked(self.dropout) and not torch.compiler.is_compiling()):
+            # CLS concat + pos_embedding[0:B] + emb dropout in one launch (ewvit.vit.embed)
+            tok = ewvit.vit.embed(y, self.cls_token, self.pos_embedding, self.dropout.p if self.training else 0.0)
+        else:
+            tok = torch.cat((self.cls_token.expand(B, -1, -1), y), 1) + self.pos_embedding[0:B]
+            tok = self.dropout(tok)
         tok = self.transformer(tok)
         if self.output_mode == 'cls':
             return self.mlp_head(self.to_cls_token(tok[:, 0]))

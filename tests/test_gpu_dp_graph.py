@@ -59,10 +59,11 @@ def _mwt_pair():
 
 @pytest.mark.parametrize('mode', ['relaxed', 'global'])
 def test_rccl_collectives_recorded_in_step_graph(nccl_world1, mode, monkeypatch):
-    """`relaxed` (the default) capture needs no drain: the NCCL watchdog's event queries from
-    its own thread are legal during it.  `global` needs the watchdog's queue empty when the
-    capture begins: TrainStep waits for its progress marker (ewvit.graph.retire_eager_collectives)
-    — no sleep, no timing assumption."""
+    """Both capture modes need the NCCL watchdog's queue empty when the capture begins (its
+    poll of an eager collective's event on the process group's stream, once that stream has
+    joined the capture, fails with hipErrorCapturedEvent and aborts the process):
+    TrainStep waits for its progress marker (ewvit.graph.retire_eager_collectives) — no sleep,
+    no timing assumption."""
     monkeypatch.setenv('EWVIT_CAPTURE_MODE', mode)
     import ewvit
     from ewvit.graph import TrainStep

@@ -122,3 +122,38 @@ def test_vit_layer_vs_oracle():
     assert _cos(tp.grad.cpu(), to.grad) >= 0.99
     for (n, a), (_, b) in zip(o.named_parameters(), p.named_parameters()):
         assert _cos(b.grad.cpu(), a.grad) >= 0.99, n
+
+
+@pytest.mark.parametrize('B', [64, 13, 1])
+def test_embed_matches_torch(B):
+    """ewvit.vit.embed (CLS concat + pos_embedding[0:B] + emb dropout, sfe.py:155-160) against
+    the torch expression; with dropout every element is 0 or the reference / (1 - p), and the
+    backward applies the forward's mask."""
+    import ewvit
+    g = torch.Generator().manual_seed(B)
+    y = torch.randn(B, 1, 512, generator=g).to(DEV)
+    cls = torch.randn(1, 1, 512, generator=g).to(DEV)
+    pos = torch.randn(64, 1, 512, generator=g).to(DEV)
+    w = torch.randn(B, 2, 512, generator=g).to(DEV)
+    ya, ca, pa = [t.clone().requires_grad_(True) for t in (y, cls, pos)]
+    yb, cb, pb = [t.clone().requires_grad_(True) for t in (y, cls, pos)]
+    ta = ewvit.vit.embed(ya, ca, pa, 0.0)
+    tb = torch.cat((cb.expand(B, -1, -1), yb), 1) + pb[0:B]
+    assert torch.equal(ta, tb)
+    (ta * w).sum().backward()
+    (tb * w).sum().backward()
+    torch.testing.assert_close(ya.grad, yb.grad, rtol=0, atol=0)
+    torch.testing.assert_close(pa.grad, pb.grad, rtol=0, atol=0)
+    torch.testing.assert_close(ca.grad, cb.grad, rtol=1e-6, atol=1e-5)
+    p = 0.15
+    yd, cd, pd = [t.clone().requires_grad_(True) for t in (y, cls, pos)]
+    td = ewvit.vit.embed(yd, cd, pd, p)
+    keep = td != 0
+    frac = float(keep.float().mean())
+    assert abs(frac - (1 - p)) < 0.05 if B > 4 else True
+    torch.testing.assert_close(td[keep], (tb.detach() / (1 - p))[keep], rtol=1e-6, atol=1e-6)
+    (td * w).sum().backward()
+    m = keep.float() / (1 - p)
+    torch.testing.assert_close(yd.grad, (w * m)[:, 1:], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(pd.grad[0:B], (w * m).sum(1, keepdim=True), rtol=1e-6, atol=1e-6)
+    assert float(pd.grad[B:].abs().max()) == 0.0 if B < 64 else True
