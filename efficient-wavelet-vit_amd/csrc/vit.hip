@@ -17,7 +17,9 @@
 //                                        with the attention output formed in the A fragments,
 //                                        bias, dropout, residual
 //             F3 vit_ln_gemm_kernel<1>   LN2 + Linear1 + bias + GELU (pre-activation kept)
-//             F4 vit_mlp2_kernel          Linear2 + bias + residual
+//             F4 ewvit_gemm (split-K)     Linear2 + bias + residual (K = 2048 split over 256
+//                                        workgroups; a column-block kernel reading all of h
+//                                        per workgroup ran 32 us)
 //   backward  B1 vit_mlp2_bwd_kernel      dh = g W2 (rounded like the module path's bf16 dh),
 //                                        g1 = dh GELU'(pre), db1; g transposed, db2
 //             B2 vit_mlp1_bwd_kernel      dLN2 = g1 W1 | dW2 = g^T h | dW1 = g1^T LN2
@@ -40,6 +42,7 @@ namespace ewvit {
 
 constexpr int VD = 512, VQ = 1536, VF = 2048, VH = 8, VDH = 64, VRP = 128;
 constexpr float VSCALE = 0.125f;   // dim_head^-0.5 (sfe.py:50)
+constexpr int VF4_SPLIT = 16;      // K splits of Linear2 (ewvit_gemm, K = 2048: 16 x 128)
 
 typedef ewvit_vit_layer VitP;
 typedef ewvit_vit_grads VitG;
@@ -71,6 +74,9 @@ __device__ __forceinline__ vb8 zero8() {
   return r;
 }
 __device__ __forceinline__ float rbf(float v) { return bf2f(f2bf(v)); }
+// rows >= R are loaded from row R - 1 (in bounds) and masked after the load: a load under a
+// per-lane branch gets its own block and waits, so the epilogues' loads would run one by one
+__device__ __forceinline__ int rclamp(int r, int R) { return r < R ? r : R - 1; }
 __device__ __forceinline__ float keep_scale(float p, uint64_t sd, uint64_t idx) {
   return uniform01(sd, idx) >= p ? 1.0f / (1.0f - p) : 0.f;
 }
@@ -79,11 +85,18 @@ __device__ __forceinline__ float keep_scale(float p, uint64_t sd, uint64_t idx) 
 struct VitSaved {
   float *mu1, *rs1, *mu2, *rs2, *p, *x1;
   bf16_t *qkv, *aux, *h, *ln1T, *oT, *ln2T, *hT;
+  float *ws2;                       // Linear2's split-K slabs (forward only)
 };
 struct VitScratch {
   bf16_t *gT, *g1, *g1T, *goT, *dqkv, *dqkvT;
   float *dln2, *dx1, *dln1;
 };
+// The layer's four weights in bf16, packed once per step by ewvit_vit_pack (fp32 masters read
+// once): each as W [out][in] (forward B fragments, k = in contiguous) and W^T [in][out] (input
+// gradient B fragments, k = out contiguous).  Element offsets within a layer's block:
+constexpr int64_t PK_QKV = 0, PK_QKVT = PK_QKV + (int64_t)VQ * VD, PK_O = PK_QKVT + (int64_t)VQ * VD,
+                  PK_OT = PK_O + (int64_t)VD * VD, PK_1 = PK_OT + (int64_t)VD * VD, PK_1T = PK_1 + (int64_t)VF * VD,
+                  PK_2 = PK_1T + (int64_t)VF * VD, PK_2T = PK_2 + (int64_t)VF * VD, PK_LAYER = PK_2T + (int64_t)VF * VD;
 __host__ __device__ inline int64_t al256(int64_t b) { return (b + 255) / 256 * 256; }
 template <class F> __host__ __device__ inline int64_t saved_layout(F f) {
   int64_t o = 0;
@@ -92,6 +105,7 @@ template <class F> __host__ __device__ inline int64_t saved_layout(F f) {
   put(4, 4 * VRP * VH * 2); put(5, 4 * VRP * VD);
   put(6, 2 * VRP * VQ); put(7, 2 * VRP * VF); put(8, 2 * VRP * VF);
   put(9, 2 * VD * VRP); put(10, 2 * VD * VRP); put(11, 2 * VD * VRP); put(12, 2 * VF * VRP);
+  put(13, 4 * VF4_SPLIT * VRP * VD);
   return o;
 }
 template <class F> __host__ __device__ inline int64_t scratch_layout(F f) {
@@ -120,7 +134,8 @@ inline VitSaved vit_saved(void *base) {
       case 9: s.ln1T = (bf16_t *)q; break;
       case 10: s.oT = (bf16_t *)q; break;
       case 11: s.ln2T = (bf16_t *)q; break;
-      default: s.hT = (bf16_t *)q; break;
+      case 12: s.hT = (bf16_t *)q; break;
+      default: s.ws2 = (float *)q; break;
     }
   });
   return s;
@@ -157,7 +172,7 @@ __device__ __forceinline__ void ln_stats_rows(const float *x, int R, float eps, 
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int r = w + i * NW;
-    if (r < R) ld8f(x + (int64_t)r * VD + lane * 8, v[i]);
+    ld8f(x + (int64_t)rclamp(r, R) * VD + lane * 8, v[i]);
   }
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
@@ -210,32 +225,6 @@ __device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, 
       for (int e = 0; e < 4; ++e) out[(int64_t)(rb + i * 16 + lq * 4 + e) * ldo + cb + j * 16 + li] = acc[i][j][e];
 }
 
-// the weight slice W[o][c0 .. c0 + NC) (o < NO, fp32, row stride ldw) as a k-contiguous bf16
-// LDS image wT[c][o] (row pitch NO + 8)
-template <int NC, int NO, int NTHR>
-__device__ __forceinline__ void stage_wT(bf16_t *wT, const float *W, int64_t ldw, int c0, int tid) {
-  constexpr int Q = NC / 4, IT = NO * Q / NTHR, BT = IT < 8 ? IT : 8;
-  static_assert(IT * NTHR == NO * Q && IT % BT == 0, "stage_wT: shape");
-#pragma unroll
-  for (int b0 = 0; b0 < IT; b0 += BT) {
-    float4 v[BT];
-#pragma unroll
-    for (int u = 0; u < BT; ++u) {
-      const int it = tid + (b0 + u) * NTHR, o = it / Q, q = it - o * Q;
-      v[u] = *reinterpret_cast<const float4 *>(W + (int64_t)o * ldw + c0 + 4 * q);
-    }
-#pragma unroll
-    for (int u = 0; u < BT; ++u) {
-      const int it = tid + (b0 + u) * NTHR, o = it / Q, q = it - o * Q;
-      bf16_t *d = wT + (4 * q) * (NO + 8) + o;
-      d[0] = f2bf(v[u].x);
-      d[NO + 8] = f2bf(v[u].y);
-      d[2 * (NO + 8)] = f2bf(v[u].z);
-      d[3 * (NO + 8)] = f2bf(v[u].w);
-    }
-  }
-}
-
 // ---------------------------------------------------------------- F1 / F3: LN + GEMM
 // MODE 0: qkv = LN1(x0) Wqkv^T (48 workgroups of 32 columns); MODE 1: pre = LN2(x1) W1^T + b1,
 // aux = pre, h = GELU(pre) (64 workgroups).  512 threads: wave (rg = w & 3, kh = w >> 2) owns
@@ -246,7 +235,7 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
   __shared__ vf4 red[4][2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float *gw = MODE ? p.ln2_w : p.ln1_w, *gb = MODE ? p.ln2_b : p.ln1_b;
-  const float *W = MODE ? p.w1 : p.wqkv;
+  const bf16_t *W = reinterpret_cast<const bf16_t *>(p.packed) + (MODE ? PK_1 : PK_QKV);
   ln_stats_rows<8>(xin, R, p.ln_eps, smu, srs, w, lane);
   __syncthreads();
   if (blockIdx.x == 0 && tid < VRP) {
@@ -262,7 +251,8 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int r = r0 + e;
-      v[e] = r < R ? (xin[(int64_t)r * VD + k] - smu[r]) * srs[r] * g + bb : 0.f;
+      const float xv = (xin[(int64_t)rclamp(r, R) * VD + k] - smu[r]) * srs[r] * g + bb;
+      v[e] = r < R ? xv : 0.f;
     }
     *reinterpret_cast<vb8 *>(lnT + (int64_t)k * VRP + r0) = pack8(v);
   }
@@ -281,7 +271,7 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
   for (int sb = 0; sb < 8; sb += 4) {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
@@ -292,18 +282,14 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
       ld8f(gb + k, b8);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (row[t] < R) {
+        {
           float v[8];
-          ld8f(xin + (int64_t)row[t] * VD + k, v);
+          ld8f(xin + (int64_t)rclamp(row[t], R) * VD + k, v);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = (v[e] - mu[t]) * rs[t] * g8[e] + b8[e];
+          for (int e = 0; e < 8; ++e) v[e] = row[t] < R ? (v[e] - mu[t]) * rs[t] * g8[e] + b8[e] : 0.f;
           af[u][t] = pack8(v);
-        } else {
-          af[u][t] = zero8();
         }
-        float v[8];
-        ld8f(W + (int64_t)(c0 + t * 16 + li) * VD + k, v);
-        bf[u][t] = pack8(v);
+        bf[u][t] = ld8b(W + (int64_t)(c0 + t * 16 + li) * VD + k);
       }
     }
 #pragma unroll
@@ -415,13 +401,10 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int r = r0 + e, f = r >> 1;
-      float o = 0.f;
-      if (r < R) {
-        o = sp[r][h][0] * bf2f(s.qkv[(int64_t)(2 * f) * VQ + 2 * VD + k]);
-        o += sp[r][h][1] * bf2f(s.qkv[(int64_t)(2 * f + 1) * VQ + 2 * VD + k]);
-      }
-      v[e] = o;
+      const int r = r0 + e, f = rclamp(r, R) >> 1;
+      float o = sp[r][h][0] * bf2f(s.qkv[(int64_t)(2 * f) * VQ + 2 * VD + k]);
+      o += sp[r][h][1] * bf2f(s.qkv[(int64_t)(2 * f + 1) * VQ + 2 * VD + k]);
+      v[e] = r < R ? o : 0.f;
     }
     *reinterpret_cast<vb8 *>(s.oT + (int64_t)k * VRP + r0) = pack8(v);
   }
@@ -432,7 +415,7 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
   for (int sb = 0; sb < 8; sb += 4) {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
@@ -440,24 +423,20 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
       const int k = kh * 256 + (sb + u) * 32 + lq * 8, h = k >> 6;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int r = rg * 32 + t * 16 + li, f = r >> 1;
-        if (r < R) {
+        const int r = rg * 32 + t * 16 + li, f = rclamp(r, R) >> 1;
+        {
           float v0[8], v1[8], o[8];
           unpack8(ld8b(s.qkv + (int64_t)(2 * f) * VQ + 2 * VD + k), v0);
           unpack8(ld8b(s.qkv + (int64_t)(2 * f + 1) * VQ + 2 * VD + k), v1);
-          const float p0 = sp[r][h][0], p1 = sp[r][h][1];
+          const float p0 = sp[r][h][0], p1 = sp[r][h][1];      // 0 past R
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             o[e] = p0 * v0[e];
             o[e] += p1 * v1[e];
           }
           af[u][t] = pack8(o);
-        } else {
-          af[u][t] = zero8();
         }
-        float v[8];
-        ld8f(p.wo + (int64_t)(c0 + t * 16 + li) * VD + k, v);
-        bf[u][t] = pack8(v);
+        bf[u][t] = ld8b(reinterpret_cast<const bf16_t *>(p.packed) + PK_O + (int64_t)(c0 + t * 16 + li) * VD + k);
       }
     }
 #pragma unroll
@@ -485,70 +464,11 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = rg * 32 + i * 16 + lq * 4 + e;
-        if (r >= R) continue;
+        const float res = x0[(int64_t)rclamp(r, R) * VD + col];
         float v = acc[i][j][e] + o[e] + bias;
         if (p.drop_p > 0.f) v = uniform01(sd, (uint64_t)(r * VD + col)) >= p.drop_p ? v * (1.0f / (1.0f - p.drop_p)) : 0.f;
-        v += x0[(int64_t)r * VD + col];
-        s.x1[(int64_t)r * VD + col] = v;
-      }
-    }
-}
-
-// ---------------------------------------------------------------- F4: Linear2 + residual
-// 16 workgroups of 32 columns, 1024 threads: wave (rg = w & 3, kq = w >> 2) owns rows 32 rg ..
-// and the K quarter kq (512 of 2048); the quarters are added in LDS in a fixed order.
-__global__ __launch_bounds__(1024) void vit_mlp2_kernel(VitP p, int R, VitSaved s, float *x2) {
-  __shared__ vf4 red[3][4][2][2][64];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rg = w & 3, kq = w >> 2, li = lane & 15, lq = lane >> 4;
-  const int c0 = blockIdx.x * 32;
-  vf4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int sb = 0; sb < 16; sb += 4) {
-    vb8 af[4][2], bf[4][2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = kq * 512 + (sb + u) * 32 + lq * 8;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int r = rg * 32 + t * 16 + li;
-        af[u][t] = r < R ? ld8b(s.h + (int64_t)r * VF + k) : zero8();
-        float v[8];
-        ld8f(p.w2 + (int64_t)(c0 + t * 16 + li) * VF + k, v);
-        bf[u][t] = pack8(v);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
-  }
-  if (kq > 0)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) red[kq - 1][rg][i][j][lane] = acc[i][j];
-  __syncthreads();
-  if (kq > 0) return;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const vf4 a = red[0][rg][i][j][lane], b = red[1][rg][i][j][lane], c = red[2][rg][i][j][lane];
-      const int col = c0 + j * 16 + li;
-      const float bias = p.b2[col];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = rg * 32 + i * 16 + lq * 4 + e;
-        if (r >= R) continue;
-        const float v = (((acc[i][j][e] + a[e]) + b[e]) + c[e]) + bias;
-        x2[(int64_t)r * VD + col] = v + s.x1[(int64_t)r * VD + col];
+        v += res;
+        if (r < R) s.x1[(int64_t)r * VD + col] = v;
       }
     }
 }
@@ -560,20 +480,18 @@ __global__ __launch_bounds__(1024) void vit_mlp2_kernel(VitP p, int R, VitSaved 
 // g's columns 8 b .. + 8 transposed (gT) and their sums (db2).
 __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
                                                            VitScratch z) {
-  __shared__ __attribute__((aligned(16))) bf16_t wT[32 * (VD + 8)];
   __shared__ vf4 red[4][2][2][64];
   __shared__ float sg[VRP][9];
   __shared__ float scol[4][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int J0 = blockIdx.x * 32;
-  stage_wT<32, VD, 512>(wT, p.w2, VF, J0, tid);
+  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_2T;    // W2^T [2048][512]
   if (tid < VRP) {
     const int r = tid;
     float v[8];
-    if (r < R) ld8f(g + (int64_t)r * VD + blockIdx.x * 8, v);
-    else
+    ld8f(g + (int64_t)rclamp(r, R) * VD + blockIdx.x * 8, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = r < R ? v[e] : 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       sg[r][e] = v[e];
@@ -592,7 +510,7 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
   for (int sb = 0; sb < 8; sb += 4) {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
@@ -601,14 +519,13 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int r = rg * 32 + t * 16 + li;
-        if (r < R) {
+        {
           float v[8];
-          ld8f(g + (int64_t)r * VD + k, v);
+          ld8f(g + (int64_t)rclamp(r, R) * VD + k, v);
           af[u][t] = pack8(v);
-        } else {
-          af[u][t] = zero8();
+          if (r >= R) af[u][t] = zero8();
         }
-        bf[u][t] = *reinterpret_cast<const vb8 *>(wT + (t * 16 + li) * (VD + 8) + k);
+        bf[u][t] = ld8b(wT + (int64_t)(J0 + t * 16 + li) * VD + k);
       }
     }
 #pragma unroll
@@ -637,12 +554,10 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = rb + e;
-          gv[e] = 0.f;
-          if (r < R) {
-            const float dh = rbf(acc[i][j][e] + o[e]);
-            gv[e] = dh * gelu_erf_grad(bf2f(s.aux[(int64_t)r * VF + col]));
-            z.g1[(int64_t)r * VF + col] = f2bf(gv[e]);
-          }
+          const float a = bf2f(s.aux[(int64_t)rclamp(r, R) * VF + col]);
+          const float dh = rbf(acc[i][j][e] + o[e]);
+          gv[e] = r < R ? dh * gelu_erf_grad(a) : 0.f;
+          if (r < R) z.g1[(int64_t)r * VF + col] = f2bf(gv[e]);
           cs[j] += gv[e];
         }
         uint2 pk;
@@ -665,8 +580,8 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
 // transposed; 4 waves = 4 K quarters of 512, added in LDS); 32..287: dW2 = g^T h in 64 x 64
 // blocks; 288..543: dW1 = g1^T LN2.
 __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[16 * (VF + 8) * 2 + 3 * 8 * 64 * 16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ vf4 red[3 * 8 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int blk = blockIdx.x;
   if (blk >= 32 + 256) {
     const int q = blk - 288;
@@ -678,15 +593,13 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
     wgrad_block(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
     return;
   }
-  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
-  vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VF + 8) * 2);
+  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_1T;    // W1^T [512][2048]
   const int I0 = blk * 16;
-  stage_wT<16, VF, 256>(wT, p.w1, VD, I0, tid);
-  __syncthreads();
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
   for (int sb = 0; sb < 16; sb += 4) {
     vb8 af[4][8], bf[4];
 #pragma unroll
@@ -695,9 +608,10 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int r = t * 16 + li;
-        af[u][t] = r < R ? ld8b(z.g1 + (int64_t)r * VF + k) : zero8();
+        af[u][t] = ld8b(z.g1 + (int64_t)rclamp(r, R) * VF + k);
+        if (r >= R) af[u][t] = zero8();
       }
-      bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VF + 8) + k);
+      bf[u] = ld8b(wT + (int64_t)(I0 + li) * VF + k);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -731,10 +645,8 @@ __device__ __forceinline__ void lnb_rows(const float *dY, const float *X, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + i * nw;
-      if (r < R) {
-        ld8f(dY + (int64_t)r * VD + lane * 8, d[i]);
-        ld8f(X + (int64_t)r * VD + lane * 8, x[i]);
-      }
+      ld8f(dY + (int64_t)rclamp(r, R) * VD + lane * 8, d[i]);
+      ld8f(X + (int64_t)rclamp(r, R) * VD + lane * 8, x[i]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -769,15 +681,15 @@ __device__ __forceinline__ void lnb_cols(const float *dY, const float *X, const 
   float pg = 0.f, pb = 0.f, po = 0.f, gov[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int r = rg * 8 + e;
+    const int r = rg * 8 + e, rr = rclamp(r, R);
+    const float dv = dY[(int64_t)rr * VD + c], xv = X[(int64_t)rr * VD + c], res = resid[(int64_t)rr * VD + c];
     gov[e] = 0.f;
     if (r < R) {
-      const float d = dY[(int64_t)r * VD + c];
-      const float xh = (X[(int64_t)r * VD + c] - mu[r]) * rs[r];
-      const float dx = rs[r] * (gm * d - sa[r] - xh * sb[r]) + resid[(int64_t)r * VD + c];
+      const float xh = (xv - mu[r]) * rs[r];
+      const float dx = rs[r] * (gm * dv - sa[r] - xh * sb[r]) + res;
       dXout[(int64_t)r * VD + c] = dx;
-      pg += d * xh;
-      pb += d;
+      pg += dv * xh;
+      pb += dv;
       if (drop) {
         gov[e] = dp > 0.f ? dx * keep_scale(dp, sd, (uint64_t)(r * VD + c)) : dx;
         po += gov[e];
@@ -803,39 +715,36 @@ __device__ __forceinline__ void lnb_cols(const float *dY, const float *X, const 
 }
 
 // ---------------------------------------------------------------- B3: LN2 backward + attention
-// 512 threads.  Every workgroup takes the per-row LN2 backward sums.  Workgroups 0..7 (head h):
-// d(attention out)[:, head h] = g_o Wo[:, 64 h .. + 64] with g_o = (g + LN2 backward) keep / (1-p)
-// formed in the A fragments (Wo's slice staged transposed), rounded to bf16 like the module
-// path's, then the attention backward of the head over the 2-token frames -> dqkv (bf16) and
-// dqkv^T.  Workgroups 8..23: 32 columns each of dx1, g_o^T, the to_out bias and the LN2 affine
-// gradients.
+// 512 threads.  Every workgroup takes the per-row LN2 backward sums.  Workgroups 0..31 = (head h,
+// row quarter q of 32 rows = 16 frames): d(attention out)[rows, head h] = g_o Wo^T[head h] with
+// g_o = (g + LN2 backward) keep / (1 - p) formed in the A fragments, the 8 waves taking K slices
+// of 64 (added in LDS in a fixed order), rounded to bf16 like the module path's; then the
+// attention backward of the head over the 16 two-token frames -> dqkv (bf16) and dqkv^T.
+// Workgroups 32..47: 32 columns each of dx1, g_o^T, the to_out bias and the LN2 affine gradients.
 __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
                                                                VitScratch z) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[64 * (VD + 8) * 2 + VRP * 68 * 4];
+  __shared__ vf4 red[8][2][4][64];                 // 64 KB: the waves' K-slice partials
+  __shared__ float sdo[32][68];
   __shared__ float sa[VRP], sbm[VRP];
-  __shared__ vf4 red[4][2][4][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   lnb_rows(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, R, sa, sbm, w, 8, lane);
   __syncthreads();
   const uint64_t sd = step_seed(p.seed, p.seed_off);
-  if (blockIdx.x >= VH) {
-    lnb_cols(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, g, R, sa, sbm, (blockIdx.x - VH) * 32, z.dx1, G.ln2_w, G.ln2_b,
-             true, p.drop_p, sd, z.goT, G.bo, reinterpret_cast<float *>(smem), tid);
+  if (blockIdx.x >= 4 * VH) {
+    lnb_cols(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, g, R, sa, sbm, (blockIdx.x - 4 * VH) * 32, z.dx1, G.ln2_w,
+             G.ln2_b, true, p.drop_p, sd, z.goT, G.bo, reinterpret_cast<float *>(&red[0][0][0][0]), tid);
     return;
   }
-  const int h = blockIdx.x;
-  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
-  float *sdo = reinterpret_cast<float *>(smem + 64 * (VD + 8) * 2);   // [128][68]
-  stage_wT<64, VD, 512>(wT, p.wo, VD, h * VDH, tid);
-  __syncthreads();
-  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int h = blockIdx.x >> 2, q = blockIdx.x & 3;
+  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_OT;    // Wo^T [512][512]
+  const int li = lane & 15, lq = lane >> 4;
   int row[2];
   float mu[2], rs[2], ma[2], mb[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    row[t] = rg * 32 + t * 16 + li;
-    mu[t] = s.mu2[row[t] < R ? row[t] : 0];
-    rs[t] = s.rs2[row[t] < R ? row[t] : 0];
+    row[t] = q * 32 + t * 16 + li;
+    mu[t] = s.mu2[rclamp(row[t], R)];
+    rs[t] = s.rs2[rclamp(row[t], R)];
     ma[t] = sa[row[t]];
     mb[t] = sbm[row[t]];
   }
@@ -844,35 +753,31 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-  for (int sb = 0; sb < 8; sb += 2) {
+  {
     vb8 af[2][2], bf[2][4];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+      const int k = w * 64 + u * 32 + lq * 8;
       float gm[8];
       ld8f(p.ln2_w + k, gm);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int r = row[t];
-        if (r < R) {
-          float d[8], x[8], gg[8], v[8];
-          ld8f(z.dln2 + (int64_t)r * VD + k, d);
-          ld8f(s.x1 + (int64_t)r * VD + k, x);
-          ld8f(g + (int64_t)r * VD + k, gg);
+        const int r = row[t], rr = rclamp(r, R);
+        float d[8], x[8], gg[8], v[8];
+        ld8f(z.dln2 + (int64_t)rr * VD + k, d);
+        ld8f(s.x1 + (int64_t)rr * VD + k, x);
+        ld8f(g + (int64_t)rr * VD + k, gg);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float xh = (x[e] - mu[t]) * rs[t];
-            float dx = rs[t] * (gm[e] * d[e] - ma[t] - xh * mb[t]) + gg[e];
-            if (p.drop_p > 0.f) dx *= keep_scale(p.drop_p, sd, (uint64_t)(r * VD + k + e));
-            v[e] = dx;
-          }
-          af[u][t] = pack8(v);
-        } else {
-          af[u][t] = zero8();
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (x[e] - mu[t]) * rs[t];
+          float dx = rs[t] * (gm[e] * d[e] - ma[t] - xh * mb[t]) + gg[e];
+          if (p.drop_p > 0.f) dx *= keep_scale(p.drop_p, sd, (uint64_t)(r * VD + k + e));
+          v[e] = r < R ? dx : 0.f;
         }
+        af[u][t] = pack8(v);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[u][j] = *reinterpret_cast<const vb8 *>(wT + (j * 16 + li) * (VD + 8) + k);
+      for (int j = 0; j < 4; ++j) bf[u][j] = ld8b(wT + (int64_t)(h * VDH + j * 16 + li) * VD + k);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -881,43 +786,40 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
   }
-  if (kh == 1)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) red[rg][i][j][lane] = acc[i][j];
+    for (int j = 0; j < 4; ++j) red[w][i][j][lane] = acc[i][j];
   __syncthreads();
-  if (kh == 0)
+  if (tid < 2 * 4 * 64) {
+    // the 8 K slices added in order; thread (i, j, lane) of the 32 x 64 block
+    const int i = tid >> 8, j = (tid >> 6) & 3, l = tid & 63;
+    vf4 a = red[0][i][j][l];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const vf4 o = red[rg][i][j][lane];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sdo[(rg * 32 + i * 16 + lq * 4 + e) * 68 + j * 16 + li] = rbf(acc[i][j][e] + o[e]);
-      }
-  __syncthreads();
-  // attention backward of head h: 8 lanes per frame f (8 head dims each), 64 frames
-  const int f = tid >> 3, d0 = (tid & 7) * 8, B = R >> 1;
-  float q[2][8], kk[2][8], vv[2][8], dO[2][8];
-  float pr[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  if (f < B) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t rb = (int64_t)(2 * f + i) * VQ + h * VDH + d0;
-      unpack8(ld8b(s.qkv + rb), q[i]);
-      unpack8(ld8b(s.qkv + rb + VD), kk[i]);
-      unpack8(ld8b(s.qkv + rb + 2 * VD), vv[i]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dO[i][e] = sdo[(2 * f + i) * 68 + d0 + e];
-      pr[i][0] = s.p[((2 * f + i) * VH + h) * 2];
-      pr[i][1] = s.p[((2 * f + i) * VH + h) * 2 + 1];
+    for (int k = 1; k < 8; ++k) {
+      const vf4 b = red[k][i][j][l];
+      a = vf4{a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
     }
-  } else {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int e = 0; e < 4; ++e) sdo[i * 16 + (l >> 4) * 4 + e][j * 16 + (l & 15)] = rbf(a[e]);
+  }
+  __syncthreads();
+  if (tid >= 128) return;
+  // attention backward of head h: 8 lanes per frame (8 head dims each), the quarter's 16 frames
+  const int fl = tid >> 3, f = q * 16 + fl, d0 = (tid & 7) * 8, B = R >> 1;
+  const int fc = f < B ? f : B - 1;
+  float qv[2][8], kk[2][8], vv[2][8], dO[2][8];
+  float pr[2][2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { q[i][e] = kk[i][e] = vv[i][e] = dO[i][e] = 0.f; }
+  for (int i = 0; i < 2; ++i) {
+    const int64_t rb = (int64_t)(2 * fc + i) * VQ + h * VDH + d0;
+    unpack8(ld8b(s.qkv + rb), qv[i]);
+    unpack8(ld8b(s.qkv + rb + VD), kk[i]);
+    unpack8(ld8b(s.qkv + rb + 2 * VD), vv[i]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dO[i][e] = f < B ? sdo[2 * fl + i][d0 + e] : 0.f;
+    pr[i][0] = f < B ? s.p[((2 * fc + i) * VH + h) * 2] : 0.f;
+    pr[i][1] = f < B ? s.p[((2 * fc + i) * VH + h) * 2 + 1] : 0.f;
   }
   float dp[2][2];
 #pragma unroll
@@ -945,12 +847,12 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         dq[i][e] += ds * kk[j][e];
-        dk[j][e] += ds * q[i][e];
+        dk[j][e] += ds * qv[i][e];
         dv[j][e] += pr[i][j] * dO[i][e];
       }
     }
   }
-  // dqkv rows 2f, 2f + 1 (bf16) and dqkv^T [col][rows 2f, 2f + 1]
+  // dqkv rows 2f, 2f + 1 (bf16) and dqkv^T [col][rows 2f, 2f + 1] (0 past R)
 #pragma unroll
   for (int part = 0; part < 3; ++part) {
     const float(*src)[8] = part == 0 ? dq : part == 1 ? dk : dv;
@@ -970,8 +872,8 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 // 256 threads.  Workgroups 0..31: dLN1[:, I] = dqkv Wqkv[:, I] (16 columns; 4 waves = K
 // quarters of 384, added in LDS); 32..223: dWqkv = dqkv^T LN1; 224..287: dWo = g_o^T o.
 __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[16 * (VQ + 8) * 2 + 3 * 8 * 64 * 16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ vf4 red[3 * 8 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int blk = blockIdx.x;
   if (blk >= 32 + 192) {
     const int q = blk - 224;
@@ -983,15 +885,13 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
     wgrad_block(z.dqkvT, s.ln1T, G.wqkv, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
-  bf16_t *wT = reinterpret_cast<bf16_t *>(smem);
-  vf4 *red = reinterpret_cast<vf4 *>(smem + 16 * (VQ + 8) * 2);
+  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT;  // Wqkv^T [512][1536]
   const int I0 = blk * 16;
-  stage_wT<16, VQ, 256>(wT, p.wqkv, VD, I0, tid);
-  __syncthreads();
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
   for (int sb = 0; sb < 12; sb += 4) {
     vb8 af[4][8], bf[4];
 #pragma unroll
@@ -1000,9 +900,10 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int r = t * 16 + li;
-        af[u][t] = r < R ? ld8b(z.dqkv + (int64_t)r * VQ + k) : zero8();
+        af[u][t] = ld8b(z.dqkv + (int64_t)rclamp(r, R) * VQ + k);
+        if (r >= R) af[u][t] = zero8();
       }
-      bf[u] = *reinterpret_cast<const vb8 *>(wT + li * (VQ + 8) + k);
+      bf[u] = ld8b(wT + (int64_t)(I0 + li) * VQ + k);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -1097,12 +998,73 @@ __global__ __launch_bounds__(512) void vit_embed_bwd_kernel(const float *dtok, i
   }
 }
 
+// ---------------------------------------------------------------- weight pack (once per step)
+// a workgroup per 64 x 64 tile of one weight: fp32 [out][in] -> bf16 [out][in] and [in][out]
+struct VitPackSrc { const float *w[4 * EWVIT_VIT_PACK_MAX]; };
+__global__ __launch_bounds__(256) void vit_pack_kernel(VitPackSrc src, int nlayers, bf16_t *packed) {
+  __shared__ float tile[64][65];
+  // tiles per layer: qkv 24 x 8, o 8 x 8, w1 32 x 8, w2 8 x 32
+  constexpr int T0 = 24 * 8, T1 = T0 + 64, T2 = T1 + 256, TL = T2 + 256;
+  const int layer = blockIdx.x / TL, t = blockIdx.x % TL;
+  int m, tr, tc, rows, cols;
+  int64_t off, offT;
+  if (t < T0) { m = 0; tr = t / 8; tc = t % 8; rows = VQ; cols = VD; off = PK_QKV; offT = PK_QKVT; }
+  else if (t < T1) { m = 1; tr = (t - T0) / 8; tc = (t - T0) % 8; rows = VD; cols = VD; off = PK_O; offT = PK_OT; }
+  else if (t < T2) { m = 2; tr = (t - T1) / 8; tc = (t - T1) % 8; rows = VF; cols = VD; off = PK_1; offT = PK_1T; }
+  else { m = 3; tr = (t - T2) / 32; tc = (t - T2) % 32; rows = VD; cols = VF; off = PK_2; offT = PK_2T; }
+  const float *W = src.w[layer * 4 + m];
+  bf16_t *dst = packed + (int64_t)layer * PK_LAYER;
+  const int tid = threadIdx.x, r0 = tr * 64, c0 = tc * 64;
+  float4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256, r = i >> 4, q = i & 15;
+    v[u] = *reinterpret_cast<const float4 *>(W + (int64_t)(r0 + r) * cols + c0 + 4 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256, r = i >> 4, q = i & 15;
+    tile[r][4 * q] = v[u].x; tile[r][4 * q + 1] = v[u].y; tile[r][4 * q + 2] = v[u].z; tile[r][4 * q + 3] = v[u].w;
+    uint2 pk;
+    pk.x = (unsigned)f2bf(v[u].x) | ((unsigned)f2bf(v[u].y) << 16);
+    pk.y = (unsigned)f2bf(v[u].z) | ((unsigned)f2bf(v[u].w) << 16);
+    *reinterpret_cast<uint2 *>(dst + off + (int64_t)(r0 + r) * cols + c0 + 4 * q) = pk;
+  }
+  __syncthreads();
+  // transposed: row c (of W^T) = column c of W, 64 rows r per tile
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256, c = i >> 4, q = i & 15;
+    uint2 pk;
+    pk.x = (unsigned)f2bf(tile[4 * q][c]) | ((unsigned)f2bf(tile[4 * q + 1][c]) << 16);
+    pk.y = (unsigned)f2bf(tile[4 * q + 2][c]) | ((unsigned)f2bf(tile[4 * q + 3][c]) << 16);
+    *reinterpret_cast<uint2 *>(dst + offT + (int64_t)(c0 + c) * rows + r0 + 4 * q) = pk;
+  }
+  (void)rows;
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
 
 extern "C" int64_t ewvit_vit_layer_workspace(int which) {
+  if (which == 2) return PK_LAYER * 2;
   return which == 0 ? saved_layout([](int, int64_t) {}) : scratch_layout([](int, int64_t) {});
+}
+
+extern "C" int ewvit_vit_pack(const ewvit_vit_layer *layers, int n, void *packed, void *stream) {
+  EWVIT_CHECK_ARG(layers && packed && n >= 1 && n <= EWVIT_VIT_PACK_MAX, "vit_pack: n=%d", n);
+  VitPackSrc src;
+  for (int i = 0; i < n; ++i) {
+    EWVIT_CHECK_ARG(layers[i].wqkv && layers[i].wo && layers[i].w1 && layers[i].w2, "vit_pack: null weight");
+    src.w[4 * i] = layers[i].wqkv;
+    src.w[4 * i + 1] = layers[i].wo;
+    src.w[4 * i + 2] = layers[i].w1;
+    src.w[4 * i + 3] = layers[i].w2;
+  }
+  hipLaunchKernelGGL(vit_pack_kernel, dim3(n * (24 * 8 + 64 + 256 + 256)), dim3(256), 0, as_stream(stream), src, n,
+                     (bf16_t *)packed);
+  return launch_status("vit_pack");
 }
 
 static int vit_check(const ewvit_vit_layer *p, int R) {
@@ -1111,6 +1073,7 @@ static int vit_check(const ewvit_vit_layer *p, int R) {
                   "vit_layer: null parameter");
   EWVIT_CHECK_ARG(R >= 2 && R <= VRP && R % 2 == 0, "vit_layer: R=%d rows (2 tokens per frame, <= %d)", R, VRP);
   EWVIT_CHECK_ARG(p->drop_p >= 0.f && p->drop_p < 1.f, "vit_layer: drop_p=%f", (double)p->drop_p);
+  EWVIT_CHECK_ARG(p->packed, "vit_layer: no packed weights (ewvit_vit_pack)");
   return 0;
 }
 
@@ -1123,8 +1086,13 @@ extern "C" int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float 
   hipLaunchKernelGGL(vit_ln_gemm_kernel<0>, dim3(VQ / 32), dim3(512), 0, st, *p, R, x0, s);
   hipLaunchKernelGGL(vit_attn_proj_kernel, dim3(VD / 32), dim3(512), 0, st, *p, R, x0, s);
   hipLaunchKernelGGL(vit_ln_gemm_kernel<1>, dim3(VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
-  hipLaunchKernelGGL(vit_mlp2_kernel, dim3(VD / 32), dim3(1024), 0, st, *p, R, s, x2);
-  return launch_status("vit_layer_fwd");
+  if (int rc = launch_status("vit_layer_fwd")) return rc;
+  // Linear2 + bias + residual: K = 2048 against 128 rows wants its K split over many
+  // workgroups (one workgroup per column block reading all of h measured 32 us): the split-K
+  // MFMA GEMM with the packed bf16 W2, its reduce adding b2 and x1
+  return ewvit_gemm(s.h, EWVIT_BF16, VF, 1, reinterpret_cast<const bf16_t *>(p->packed) + PK_2, EWVIT_BF16, 1, VF,
+                    x2, EWVIT_F32, VD, R, VD, VF, 1.f, 0.f, p->b2, 0, nullptr, 0.f, 0, nullptr, s.x1, EWVIT_F32, VD,
+                    VF4_SPLIT, s.ws2, stream);
 }
 
 extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float *x0, const void *saved,
@@ -1140,7 +1108,7 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
   hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(32 + 256 + 256), dim3(256), 0, st, *p, *G, R, s, z);
-  hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
+  hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
   hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(32 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
   hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
   return launch_status("vit_layer_bwd");

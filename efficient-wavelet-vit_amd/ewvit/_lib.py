@@ -110,6 +110,7 @@ SIGNATURES = {
                                  _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     'ewvit_vit_layer_fwd': [_vp, _i32, _vp, _vp, _vp, _vp],
     'ewvit_vit_layer_bwd': [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_vit_pack': [_vp, _i32, _vp, _vp],
     'ewvit_vit_embed_fwd': [_vp, _vp, _vp, _i32, _f32, _u64, _vp, _vp, _vp],
     'ewvit_vit_embed_bwd': [_vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp],
 }

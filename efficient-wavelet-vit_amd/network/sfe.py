@@ -134,10 +134,17 @@ class Transformer(nn.Module):                                              # sfe
 
     def forward(self, x):
         x = x.float()
-        for attn, ff in self.layers:
-            if _vit_fusable(attn, ff, x):
+        fused = [_vit_fusable(attn, ff, x) for attn, ff in self.layers]
+        packed, slot = None, {}
+        if any(fused):
+            # the fused layers' bf16 weights (both orientations), one launch (ewvit.vit.pack)
+            sel = [i for i, f in enumerate(fused) if f][:ewvit.vit.PACK_MAX]
+            packed = ewvit.vit.pack([tuple(self.layers[i]) for i in sel])
+            slot = {i: k for k, i in enumerate(sel)}
+        for i, (attn, ff) in enumerate(self.layers):
+            if i in slot:
                 # the layer on csrc/vit.hip: 4 launches forward, 5 backward (ewvit.vit)
-                x = ewvit.vit.vit_layer(attn, ff, x, self.training)
+                x = ewvit.vit.vit_layer(attn, ff, x, self.training, packed, slot[i])
                 continue
             x = attn.forward_residual(x)
             x = ff.forward_residual(x)

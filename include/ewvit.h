@@ -699,12 +699,20 @@ typedef struct {
   float ln_eps, drop_p;         /* LayerNorm eps; to_out dropout probability (0 in eval) */
   uint64_t seed;
   const int64_t *seed_off;
+  const void *packed;           /* this layer's block of ewvit_vit_pack's output (bf16 weights) */
 } ewvit_vit_layer;
 typedef struct {                /* parameter gradients (overwritten), parameter layouts */
   float *ln1_w, *ln1_b, *wqkv, *wo, *bo, *ln2_w, *ln2_b, *w1, *b1, *w2, *b2;
 } ewvit_vit_grads;
-/* bytes of the forward's saved state (which = 0) and of the backward's scratch (which = 1) */
+/* bytes of the forward's saved state (which = 0), of the backward's scratch (which = 1) and of
+ * one layer's packed weights (which = 2) */
 int64_t ewvit_vit_layer_workspace(int which);
+#define EWVIT_VIT_PACK_MAX 8
+/* The n <= EWVIT_VIT_PACK_MAX layers' to_qkv / to_out / Linear1 / Linear2 weights (fp32, read
+ * from layers[i]) as bf16, each in its own layout and transposed, into n consecutive blocks of
+ * ewvit_vit_layer_workspace(2) bytes: the GEMM operands of ewvit_vit_layer_fwd / _bwd, packed
+ * once per step (the module path rounds the same weights to bf16 inside every GEMM). */
+int ewvit_vit_pack(const ewvit_vit_layer *layers, int n, void *packed, void *stream);
 /* x0 [R][512] f32 -> x2 [R][512] f32; `saved` (ewvit_vit_layer_workspace(0) bytes) keeps what
  * the backward reads (LayerNorm statistics, qkv, softmax weights, the GEMM operands). */
 int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float *x0, void *saved, float *x2, void *stream);

@@ -24,7 +24,7 @@ def main():
     x = torch.randn(args.frames, 2, 512, device=dev, requires_grad=True)
     w = torch.randn(args.frames, 2, 512, device=dev)
     out = {}
-    for mode in ('1', '0'):
+    for mode in os.environ.get('VIT_BENCH_MODES', '1,0').split(','):
         os.environ['EWVIT_VIT_FUSED'] = mode
 
         def step():
