@@ -613,6 +613,45 @@ __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackArgs a) {
   const float *w = a.w[t];
   bf16_t *wp = a.wp[t], *wpt = a.wpt[t];
   const int64_t sco = a.s_co[t], sci = a.s_ci[t], stap = a.s_tap[t];
+  if (sci == 1 && (Cin & 3) == 0 && (Cin_pad & 3) == 0 && (Cout & 3) == 0 && (sco & 3) == 0 && (stap & 3) == 0) {
+    // ci-contiguous weights (the 1x1 convs, channels-last 3x3): 4 channels a thread, float4
+    // loads, 8-byte stores in both layouts — all 4 loads of a thread in flight
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e4 = tid + 256 * u, r = e4 >> 4, c4 = (e4 & 15) * 4;
+      const int co = co0 + r, ci = ci0 + c4;
+      v[u] = co < Cout && ci < Cin ? *reinterpret_cast<const float4 *>(w + co * sco + ci + tap * stap)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e4 = tid + 256 * u, r = e4 >> 4, c4 = (e4 & 15) * 4;
+      const int co = co0 + r, ci = ci0 + c4;
+      const bf16_t b0 = f2bf(v[u].x), b1 = f2bf(v[u].y), b2 = f2bf(v[u].z), b3 = f2bf(v[u].w);
+      tile[r][c4] = b0; tile[r][c4 + 1] = b1; tile[r][c4 + 2] = b2; tile[r][c4 + 3] = b3;
+      if (wp && co < Cout && ci < Cin_pad) {
+        uint2 pk;
+        pk.x = (unsigned)b0 | ((unsigned)b1 << 16);
+        pk.y = (unsigned)b2 | ((unsigned)b3 << 16);
+        *reinterpret_cast<uint2 *>(wp + ((int64_t)co * taps + tap) * Cin_pad + ci) = pk;
+      }
+    }
+    if (!wpt) return;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e4 = tid + 256 * u, r = e4 >> 4, c4 = (e4 & 15) * 4;
+      const int ci = ci0 + r, co = co0 + c4;
+      if (ci < Cin_pad && co < Cout) {
+        uint2 pk;
+        pk.x = (unsigned)tile[c4][r] | ((unsigned)tile[c4 + 1][r] << 16);
+        pk.y = (unsigned)tile[c4 + 2][r] | ((unsigned)tile[c4 + 3][r] << 16);
+        *reinterpret_cast<uint2 *>(wpt + ((int64_t)ci * taps + tap) * Cout + co) = pk;
+      }
+    }
+    return;
+  }
 #pragma unroll 4
   for (int e = tid; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;

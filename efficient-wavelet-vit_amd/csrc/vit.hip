@@ -11,7 +11,7 @@
 // Every GEMM here is [128 rows] x [<= 2048] x [<= 2048] against fp32 master weights: a few
 // MFLOP and a few MB of weight reads, so each launch is latency: the fusion below cuts the
 // launches, not the bytes.
-//   forward   F1 vit_ln_gemm_kernel<0>   LN1 (statistics per workgroup, all rows) + to_qkv;
+//   forward   F1 vit_ln_gemm_kernel<0>   LN1 (statistics per workgroup, its 64 rows) + to_qkv;
 //                                        LN1 output written transposed for the weight gradient
 //             F2 vit_attn_proj_kernel     softmax of the 2x2 scores per (frame, head) + to_out
 //                                        with the attention output formed in the A fragments,
@@ -164,19 +164,19 @@ inline VitScratch vit_scratch(void *base) {
 // LayerNorm statistics of rows w, w + nw, ... (< 128; rows >= R get 0 / 0): a wave per row,
 // 8 contiguous columns per lane; two-pass mean / centred variance, biased, eps inside the
 // rsqrt (torch's formula, layernorm.hip's)
-template <int NW>
+template <int NW, int NROWS = VRP>
 __device__ __forceinline__ void ln_stats_rows(const float *x, int R, float eps, float *smu, float *srs, int w,
-                                              int lane) {
-  constexpr int NR = VRP / NW;          // rows of this wave: w, w + NW, ... (all loads in flight)
+                                              int lane, int r0 = 0) {
+  constexpr int NR = NROWS / NW;        // rows of this wave: r0 + w, r0 + w + NW, ... (all loads in flight)
   float v[NR][8];
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
-    const int r = w + i * NW;
+    const int r = r0 + w + i * NW;
     ld8f(x + (int64_t)rclamp(r, R) * VD + lane * 8, v[i]);
   }
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
-    const int r = w + i * NW;
+    const int r = r0 + w + i * NW;
     float mu = 0.f, rs = 0.f;
     if (r < R) {
       float s = 0.f;
@@ -226,26 +226,30 @@ __device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, 
 }
 
 // ---------------------------------------------------------------- F1 / F3: LN + GEMM
-// MODE 0: qkv = LN1(x0) Wqkv^T (48 workgroups of 32 columns); MODE 1: pre = LN2(x1) W1^T + b1,
-// aux = pre, h = GELU(pre) (64 workgroups).  512 threads: wave (rg = w & 3, kh = w >> 2) owns
-// rows 32 rg .. + 32 and the K half kh; the halves meet in LDS.
+// MODE 0: qkv = LN1(x0) Wqkv^T (48 column blocks of 32); MODE 1: pre = LN2(x1) W1^T + b1,
+// aux = pre, h = GELU(pre) (64 column blocks).  Workgroup (column block cb, row half rh):
+// 64 rows, so a workgroup reads half of the A rows (the workgroups are latency / per-CU
+// bandwidth bound: 48-64 workgroups reading all 128 rows ran 26-30 us).  512 threads: wave
+// (rg = w & 1, kq = w >> 1) owns rows 32 rg .. + 32 of the half and the K quarter kq (4 k-steps,
+// one batch of loads); the quarters meet in LDS in a fixed order.
 template <int MODE>
 __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const float *xin, VitSaved s) {
   __shared__ float smu[VRP], srs[VRP];
-  __shared__ vf4 red[4][2][2][64];
+  __shared__ vf4 red[3][2][2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cb = blockIdx.x >> 1, rh = blockIdx.x & 1, rbase = rh * 64;
   const float *gw = MODE ? p.ln2_w : p.ln1_w, *gb = MODE ? p.ln2_b : p.ln1_b;
   const bf16_t *W = reinterpret_cast<const bf16_t *>(p.packed) + (MODE ? PK_1 : PK_QKV);
-  ln_stats_rows<8>(xin, R, p.ln_eps, smu, srs, w, lane);
+  ln_stats_rows<8, 64>(xin, R, p.ln_eps, smu, srs, w, lane, rbase);
   __syncthreads();
-  if (blockIdx.x == 0 && tid < VRP) {
-    (MODE ? s.mu2 : s.mu1)[tid] = smu[tid];
-    (MODE ? s.rs2 : s.rs1)[tid] = srs[tid];
+  if (cb == 0 && tid < 64) {
+    (MODE ? s.mu2 : s.mu1)[rbase + tid] = smu[rbase + tid];
+    (MODE ? s.rs2 : s.rs1)[rbase + tid] = srs[rbase + tid];
   }
-  if (blockIdx.x < 32 && tid < 256) {
-    // the LN output transposed, [k][128 rows] bf16: 16 columns k per workgroup, 8 rows a thread
+  if (cb < 32 && tid < 128) {
+    // the LN output transposed, [k][128 rows] bf16: 16 columns k per column block, 8 rows a thread
     bf16_t *lnT = MODE ? s.ln2T : s.ln1T;
-    const int k = blockIdx.x * 16 + (tid >> 4), r0 = (tid & 15) * 8;
+    const int k = cb * 16 + (tid >> 3), r0 = rbase + (tid & 7) * 8;
     const float g = gw[k], bb = gb[k];
     float v[8];
 #pragma unroll
@@ -256,13 +260,13 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
     }
     *reinterpret_cast<vb8 *>(lnT + (int64_t)k * VRP + r0) = pack8(v);
   }
-  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
-  const int c0 = blockIdx.x * 32;
+  const int rg = w & 1, kq = w >> 1, li = lane & 15, lq = lane >> 4;
+  const int c0 = cb * 32;
   int row[2];
   float mu[2], rs[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    row[t] = rg * 32 + t * 16 + li;
+    row[t] = rbase + rg * 32 + t * 16 + li;
     mu[t] = smu[row[t]];
     rs[t] = srs[row[t]];
   }
@@ -271,24 +275,21 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int sb = 0; sb < 8; sb += 4) {
+  {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+      const int k = kq * 128 + u * 32 + lq * 8;
       float g8[8], b8[8];
       ld8f(gw + k, g8);
       ld8f(gb + k, b8);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        {
-          float v[8];
-          ld8f(xin + (int64_t)rclamp(row[t], R) * VD + k, v);
+        float v[8];
+        ld8f(xin + (int64_t)rclamp(row[t], R) * VD + k, v);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = row[t] < R ? (v[e] - mu[t]) * rs[t] * g8[e] + b8[e] : 0.f;
-          af[u][t] = pack8(v);
-        }
+        for (int e = 0; e < 8; ++e) v[e] = row[t] < R ? (v[e] - mu[t]) * rs[t] * g8[e] + b8[e] : 0.f;
+        af[u][t] = pack8(v);
         bf[u][t] = ld8b(W + (int64_t)(c0 + t * 16 + li) * VD + k);
       }
     }
@@ -299,30 +300,33 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
   }
-  if (kh == 1)
+  if (kq > 0)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+      for (int j = 0; j < 2; ++j) red[kq - 1][rg][i][j][lane] = acc[i][j];
   __syncthreads();
-  if (kh == 1) return;
+  if (kq > 0) return;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const vf4 o = red[rg][i][j][lane];
+      const vf4 a = red[0][rg][i][j][lane], b = red[1][rg][i][j][lane], c = red[2][rg][i][j][lane];
       const int col = c0 + j * 16 + li;
-      const int rb = rg * 32 + i * 16 + lq * 4;
+      const int rb = rbase + rg * 32 + i * 16 + lq * 4;
+      float v4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = ((acc[i][j][e] + a[e]) + b[e]) + c[e];
       if (MODE == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (rb + e < R) s.qkv[(int64_t)(rb + e) * VQ + col] = f2bf(acc[i][j][e] + o[e]);
+          if (rb + e < R) s.qkv[(int64_t)(rb + e) * VQ + col] = f2bf(v4[e]);
       } else {
         const float bias = p.b1[col];
         float hv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pre = acc[i][j][e] + o[e] + bias;
+          const float pre = v4[e] + bias;
           hv[e] = rb + e < R ? gelu_erf(pre) : 0.f;
           if (rb + e < R) {
             s.aux[(int64_t)(rb + e) * VF + col] = f2bf(pre);
@@ -338,21 +342,23 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
 }
 
 // ---------------------------------------------------------------- F2: attention + to_out
-// 16 workgroups of 32 output columns, 512 threads.  Each workgroup forms the softmax weights
-// of every (frame, head) — 4 dot products of 64 per pair — in LDS; the attention output
-// o[r][k] = p[r][h][0] v[2f][k] + p[r][h][1] v[2f+1][k] (f = r / 2, h = k / 64) is formed in the
-// A fragments; workgroup b also writes o transposed for columns 32 b .. + 32.
+// Workgroup (column block cb of 32 outputs, row half rh = 32 frames), 512 threads.  The
+// workgroup forms the softmax weights of its frames' (frame, head) pairs — 4 dot products of 64
+// per pair — in LDS; the attention output o[r][k] = p[r][h][0] v[2f][k] + p[r][h][1] v[2f+1][k]
+// (f = r / 2, h = k / 64) is formed in the A fragments; column block cb also writes o
+// transposed for its 32 columns and the half's rows.  Waves (rg = w & 1, kq = w >> 1) as F1.
 __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const float *x0, VitSaved s) {
   __shared__ float sp[VRP][VH][2];
-  __shared__ vf4 red[4][2][2][64];
+  __shared__ vf4 red[3][2][2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cb = blockIdx.x >> 1, rh = blockIdx.x & 1, rbase = rh * 64;
   const int B = R >> 1;
-  {
-    // thread = (frame b, head h): the 4 dot products of 64 of the frame's 2x2 scores
-    const int b = tid >> 3, h = tid & 7;
+  if (tid < 256) {
+    // thread = (frame b of the half, head h): the 4 dot products of 64 of the frame's 2x2 scores
+    const int b = rh * 32 + (tid >> 3), h = tid & 7, bc = b < B ? b : B - 1;
     float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
-    if (b < B) {
-      const bf16_t *q0p = s.qkv + (int64_t)(2 * b) * VQ + h * VDH, *q1p = q0p + VQ;
+    {
+      const bf16_t *q0p = s.qkv + (int64_t)(2 * bc) * VQ + h * VDH, *q1p = q0p + VQ;
       vb8 a0[8], a1[8], c0[8], c1[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -393,11 +399,11 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
     }
   }
   __syncthreads();
-  if (blockIdx.x == 0)
-    for (int i = tid; i < R * VH * 2; i += 512) s.p[i] = (&sp[0][0][0])[i];
-  {
-    // o transposed: columns k = 32 b + (tid >> 4), rows 8 (tid & 15) .. + 8
-    const int k = blockIdx.x * 32 + (tid >> 4), r0 = (tid & 15) * 8, h = k >> 6;
+  if (cb == 0)
+    for (int i = rbase * VH * 2 + tid; i < (rbase + 64) * VH * 2 && i < R * VH * 2; i += 512) s.p[i] = (&sp[0][0][0])[i];
+  if (tid < 256) {
+    // o transposed: columns k = 32 cb + (tid >> 3), rows rbase + 8 (tid & 7) .. + 8
+    const int k = cb * 32 + (tid >> 3), r0 = rbase + (tid & 7) * 8, h = k >> 6;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -408,34 +414,31 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
     }
     *reinterpret_cast<vb8 *>(s.oT + (int64_t)k * VRP + r0) = pack8(v);
   }
-  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
-  const int c0 = blockIdx.x * 32;
+  const int rg = w & 1, kq = w >> 1, li = lane & 15, lq = lane >> 4;
+  const int c0 = cb * 32;
   vf4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int sb = 0; sb < 8; sb += 4) {
+  {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int k = kh * 256 + (sb + u) * 32 + lq * 8, h = k >> 6;
+      const int k = kq * 128 + u * 32 + lq * 8, h = k >> 6;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int r = rg * 32 + t * 16 + li, f = rclamp(r, R) >> 1;
-        {
-          float v0[8], v1[8], o[8];
-          unpack8(ld8b(s.qkv + (int64_t)(2 * f) * VQ + 2 * VD + k), v0);
-          unpack8(ld8b(s.qkv + (int64_t)(2 * f + 1) * VQ + 2 * VD + k), v1);
-          const float p0 = sp[r][h][0], p1 = sp[r][h][1];      // 0 past R
+        const int r = rbase + rg * 32 + t * 16 + li, f = rclamp(r, R) >> 1;
+        float v0[8], v1[8], o[8];
+        unpack8(ld8b(s.qkv + (int64_t)(2 * f) * VQ + 2 * VD + k), v0);
+        unpack8(ld8b(s.qkv + (int64_t)(2 * f + 1) * VQ + 2 * VD + k), v1);
+        const float p0 = sp[r][h][0], p1 = sp[r][h][1];      // 0 past R
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            o[e] = p0 * v0[e];
-            o[e] += p1 * v1[e];
-          }
-          af[u][t] = pack8(o);
+        for (int e = 0; e < 8; ++e) {
+          o[e] = p0 * v0[e];
+          o[e] += p1 * v1[e];
         }
+        af[u][t] = pack8(o);
         bf[u][t] = ld8b(reinterpret_cast<const bf16_t *>(p.packed) + PK_O + (int64_t)(c0 + t * 16 + li) * VD + k);
       }
     }
@@ -446,26 +449,26 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
   }
-  if (kh == 1)
+  if (kq > 0)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+      for (int j = 0; j < 2; ++j) red[kq - 1][rg][i][j][lane] = acc[i][j];
   __syncthreads();
-  if (kh == 1) return;
+  if (kq > 0) return;
   const uint64_t sd = step_seed(p.seed, p.seed_off);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const vf4 o = red[rg][i][j][lane];
+      const vf4 a = red[0][rg][i][j][lane], b = red[1][rg][i][j][lane], c = red[2][rg][i][j][lane];
       const int col = c0 + j * 16 + li;
       const float bias = p.bo[col];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int r = rg * 32 + i * 16 + lq * 4 + e;
+        const int r = rbase + rg * 32 + i * 16 + lq * 4 + e;
         const float res = x0[(int64_t)rclamp(r, R) * VD + col];
-        float v = acc[i][j][e] + o[e] + bias;
+        float v = (((acc[i][j][e] + a[e]) + b[e]) + c[e]) + bias;
         if (p.drop_p > 0.f) v = uniform01(sd, (uint64_t)(r * VD + col)) >= p.drop_p ? v * (1.0f / (1.0f - p.drop_p)) : 0.f;
         v += res;
         if (r < R) s.x1[(int64_t)r * VD + col] = v;
@@ -478,9 +481,9 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
 // (K = 512 over W2's output index: W2[:, J] staged transposed in LDS), rounded to bf16 like the
 // module path's dh, g1 = dh GELU'(pre) -> g1 (bf16), g1^T, db1[J].  Side job of workgroup b:
 // g's columns 8 b .. + 8 transposed (gT) and their sums (db2).
-__global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
-                                                           VitScratch z) {
-  __shared__ vf4 red[4][2][2][64];
+__global__ __launch_bounds__(1024) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
+                                                            VitScratch z) {
+  __shared__ vf4 red[3][4][2][2][64];
   __shared__ float sg[VRP][9];
   __shared__ float scol[4][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -504,18 +507,17 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
     for (int r = 0; r < R; ++r) a += sg[r][tid];
     G.b2[blockIdx.x * 8 + tid] = a;
   }
-  const int rg = w & 3, kh = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int rg = w & 3, kq = w >> 2, li = lane & 15, lq = lane >> 4;
   vf4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int sb = 0; sb < 8; sb += 4) {
+  {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int k = kh * 256 + (sb + u) * 32 + lq * 8;
+      const int k = kq * 128 + u * 32 + lq * 8;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int r = rg * 32 + t * 16 + li;
@@ -535,19 +537,21 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
   }
-  if (kh == 1)
+  if (kq > 0)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) red[rg][i][j][lane] = acc[i][j];
+      for (int j = 0; j < 2; ++j) red[kq - 1][rg][i][j][lane] = acc[i][j];
   __syncthreads();
-  if (kh == 0) {
+  if (kq == 0) {
     float cs[2] = {0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const vf4 o = red[rg][i][j][lane];
+        const vf4 ra = red[0][rg][i][j][lane], rb2 = red[1][rg][i][j][lane], rc = red[2][rg][i][j][lane];
+        const vf4 o = vf4{(ra[0] + rb2[0]) + rc[0], (ra[1] + rb2[1]) + rc[1], (ra[2] + rb2[2]) + rc[2],
+                          (ra[3] + rb2[3]) + rc[3]};
         const int col = J0 + j * 16 + li;
         const int rb = rg * 32 + i * 16 + lq * 4;
         float gv[4];
@@ -575,63 +579,72 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
   if (tid < 32) G.b1[J0 + tid] = ((scol[0][tid] + scol[1][tid]) + scol[2][tid]) + scol[3][tid];
 }
 
-// ---------------------------------------------------------------- B2: Linear1 backward, dW2, dW1
-// 256 threads.  Workgroups 0..31: dLN2[:, I] = g1 W1[:, I], 16 columns I each (W1[:, I] staged
-// transposed; 4 waves = 4 K quarters of 512, added in LDS); 32..287: dW2 = g^T h in 64 x 64
-// blocks; 288..543: dW1 = g1^T LN2.
-__global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
-  __shared__ vf4 red[3 * 8 * 64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int blk = blockIdx.x;
-  if (blk >= 32 + 256) {
-    const int q = blk - 288;
-    wgrad_block(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
-    return;
-  }
-  if (blk >= 32) {
-    const int q = blk - 32;
-    wgrad_block(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
-    return;
-  }
-  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_1T;    // W1^T [512][2048]
-  const int I0 = blk * 16;
+// An input-gradient block out[rows 32 rq .. + 32][I0 .. I0 + 16] = A[rows][K] (bf16, row stride
+// K) x BT[I0 .. + 16][K]^T (bf16 k-contiguous weight image), 4 waves = 4 K quarters added in LDS
+// in a fixed order (fp32 out, row stride 512)
+template <int K>
+__device__ __forceinline__ void dgrad_block(const bf16_t *A, const bf16_t *BT, float *out, int R, int I0, int rq,
+                                            int w, int lane, vf4 *red) {
+  constexpr int KQ = K / 4, NS = KQ / 32;
   const int li = lane & 15, lq = lane >> 4;
-  vf4 acc[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
+  vf4 acc[2];
+  acc[0] = acc[1] = vf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-  for (int sb = 0; sb < 16; sb += 4) {
-    vb8 af[4][8], bf[4];
+  for (int sb = 0; sb < NS; sb += 4) {
+    vb8 af[4][2], bf[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int k = w * 512 + (sb + u) * 32 + lq * 8;
+      const int k = w * KQ + (sb + u) * 32 + lq * 8;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int r = t * 16 + li;
-        af[u][t] = ld8b(z.g1 + (int64_t)rclamp(r, R) * VF + k);
+      for (int t = 0; t < 2; ++t) {
+        const int r = rq * 32 + t * 16 + li;
+        af[u][t] = ld8b(A + (int64_t)rclamp(r, R) * K + k);
         if (r >= R) af[u][t] = zero8();
       }
-      bf[u] = ld8b(wT + (int64_t)(I0 + li) * VF + k);
+      bf[u] = ld8b(BT + (int64_t)(I0 + li) * K + k);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
+      for (int t = 0; t < 2; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
   }
   if (w > 0)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) red[((w - 1) * 8 + t) * 64 + lane] = acc[t];
+    for (int t = 0; t < 2; ++t) red[((w - 1) * 2 + t) * 64 + lane] = acc[t];
   __syncthreads();
   if (w > 0) return;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const vf4 a = red[(0 * 8 + t) * 64 + lane], b = red[(1 * 8 + t) * 64 + lane], c = red[(2 * 8 + t) * 64 + lane];
+  for (int t = 0; t < 2; ++t) {
+    const vf4 a = red[(0 * 2 + t) * 64 + lane], b = red[(1 * 2 + t) * 64 + lane], c = red[(2 * 2 + t) * 64 + lane];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int r = t * 16 + lq * 4 + e;
-      if (r < R) z.dln2[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
+      const int r = rq * 32 + t * 16 + lq * 4 + e;
+      if (r < R) out[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
     }
   }
+}
+
+// ---------------------------------------------------------------- B2: Linear1 backward, dW2, dW1
+// 256 threads.  Workgroups 0..127: dLN2 = g1 W1 in (16 columns, 32 rows) blocks (W1^T from the
+// packed image; 4 waves = 4 K quarters of 512, added in LDS); 128..383: dW2 = g^T h in 64 x 64
+// blocks; 384..639: dW1 = g1^T LN2.
+__global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
+  __shared__ vf4 red[3 * 2 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int blk = blockIdx.x;
+  if (blk >= 128 + 256) {
+    const int q = blk - 384;
+    wgrad_block(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    return;
+  }
+  if (blk >= 128) {
+    const int q = blk - 128;
+    wgrad_block(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
+    return;
+  }
+  // input gradient: workgroup (16-column block, row quarter)
+  dgrad_block<VF>(z.g1, reinterpret_cast<const bf16_t *>(p.packed) + PK_1T, z.dln2, R, (blk >> 2) * 16, blk & 3, w,
+                  lane, red);
 }
 
 // ---------------------------------------------------------------- LayerNorm backward pieces
@@ -869,61 +882,25 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 }
 
 // ---------------------------------------------------------------- B4: to_qkv backward, dWqkv, dWo
-// 256 threads.  Workgroups 0..31: dLN1[:, I] = dqkv Wqkv[:, I] (16 columns; 4 waves = K
-// quarters of 384, added in LDS); 32..223: dWqkv = dqkv^T LN1; 224..287: dWo = g_o^T o.
+// 256 threads.  Workgroups 0..127: dLN1 = dqkv Wqkv in (16 columns, 32 rows) blocks (4 waves = K
+// quarters of 384, added in LDS); 128..319: dWqkv = dqkv^T LN1; 320..383: dWo = g_o^T o.
 __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
-  __shared__ vf4 red[3 * 8 * 64];
+  __shared__ vf4 red[3 * 2 * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int blk = blockIdx.x;
-  if (blk >= 32 + 192) {
-    const int q = blk - 224;
+  if (blk >= 128 + 192) {
+    const int q = blk - 320;
     wgrad_block(z.goT, s.oT, G.wo, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
-  if (blk >= 32) {
-    const int q = blk - 32;
+  if (blk >= 128) {
+    const int q = blk - 128;
     wgrad_block(z.dqkvT, s.ln1T, G.wqkv, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
-  const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT;  // Wqkv^T [512][1536]
-  const int I0 = blk * 16;
-  const int li = lane & 15, lq = lane >> 4;
-  vf4 acc[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc[t] = vf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int sb = 0; sb < 12; sb += 4) {
-    vb8 af[4][8], bf[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = w * 384 + (sb + u) * 32 + lq * 8;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int r = t * 16 + li;
-        af[u][t] = ld8b(z.dqkv + (int64_t)rclamp(r, R) * VQ + k);
-        if (r >= R) af[u][t] = zero8();
-      }
-      bf[u] = ld8b(wT + (int64_t)(I0 + li) * VQ + k);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
-  }
-  if (w > 0)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) red[((w - 1) * 8 + t) * 64 + lane] = acc[t];
-  __syncthreads();
-  if (w > 0) return;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const vf4 a = red[(0 * 8 + t) * 64 + lane], b = red[(1 * 8 + t) * 64 + lane], c = red[(2 * 8 + t) * 64 + lane];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = t * 16 + lq * 4 + e;
-      if (r < R) z.dln1[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
-    }
-  }
+  // input gradient: workgroup (16-column block, row quarter)
+  dgrad_block<VQ>(z.dqkv, reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT, z.dln1, R, (blk >> 2) * 16, blk & 3,
+                  w, lane, red);
 }
 
 // ---------------------------------------------------------------- B5: LN1 backward + residual
@@ -1083,9 +1060,9 @@ extern "C" int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float 
   EWVIT_CHECK_ARG(x0 && saved && x2, "vit_layer_fwd: null pointer");
   const VitSaved s = vit_saved(saved);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(vit_ln_gemm_kernel<0>, dim3(VQ / 32), dim3(512), 0, st, *p, R, x0, s);
-  hipLaunchKernelGGL(vit_attn_proj_kernel, dim3(VD / 32), dim3(512), 0, st, *p, R, x0, s);
-  hipLaunchKernelGGL(vit_ln_gemm_kernel<1>, dim3(VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
+  hipLaunchKernelGGL(vit_ln_gemm_kernel<0>, dim3(2 * VQ / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL(vit_attn_proj_kernel, dim3(2 * VD / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL(vit_ln_gemm_kernel<1>, dim3(2 * VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
   if (int rc = launch_status("vit_layer_fwd")) return rc;
   // Linear2 + bias + residual: K = 2048 against 128 rows wants its K split over many
   // workgroups (one workgroup per column block reading all of h measured 32 us): the split-K
@@ -1106,10 +1083,10 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   const VitSaved s = vit_saved(const_cast<void *>(saved));
   const VitScratch z = vit_scratch(scratch);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(32 + 256 + 256), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(VF / 32), dim3(1024), 0, st, *p, *G, R, g, s, z);
+  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(128 + 256 + 256), dim3(256), 0, st, *p, *G, R, s, z);
   hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(32 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
   hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
   return launch_status("vit_layer_bwd");
 }
