@@ -90,6 +90,8 @@ struct VitSaved {
 struct VitScratch {
   bf16_t *gT, *g1, *g1T, *goT, *dqkv, *dqkvT;
   float *dln2, *dx1, *dln1;
+  float *rp2, *rp1;                 // LN backward row partials [32 column blocks][128 rows][2]
+  float *db1p;                      // Linear1 bias gradient per row half [2][2048]
 };
 // The layer's four weights in bf16, packed once per step by ewvit_vit_pack (fp32 masters read
 // once): each as W [out][in] (forward B fragments, k = in contiguous) and W^T [in][out] (input
@@ -114,6 +116,7 @@ template <class F> __host__ __device__ inline int64_t scratch_layout(F f) {
   put(0, 2 * VD * VRP); put(1, 2 * VRP * VF); put(2, 2 * VF * VRP); put(3, 2 * VD * VRP);
   put(4, 2 * VRP * VQ); put(5, 2 * VQ * VRP);
   put(6, 4 * VRP * VD); put(7, 4 * VRP * VD); put(8, 4 * VRP * VD);
+  put(9, 4 * 32 * VRP * 2); put(10, 4 * 32 * VRP * 2); put(11, 4 * 2 * VF);
   return o;
 }
 inline VitSaved vit_saved(void *base) {
@@ -154,7 +157,10 @@ inline VitScratch vit_scratch(void *base) {
       case 5: s.dqkvT = (bf16_t *)q; break;
       case 6: s.dln2 = (float *)q; break;
       case 7: s.dx1 = (float *)q; break;
-      default: s.dln1 = (float *)q; break;
+      case 8: s.dln1 = (float *)q; break;
+      case 9: s.rp2 = (float *)q; break;
+      case 10: s.rp1 = (float *)q; break;
+      default: s.db1p = (float *)q; break;
     }
   });
   return s;
@@ -481,33 +487,37 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
 // (K = 512 over W2's output index: W2[:, J] staged transposed in LDS), rounded to bf16 like the
 // module path's dh, g1 = dh GELU'(pre) -> g1 (bf16), g1^T, db1[J].  Side job of workgroup b:
 // g's columns 8 b .. + 8 transposed (gT) and their sums (db2).
-__global__ __launch_bounds__(1024) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
-                                                            VitScratch z) {
-  __shared__ vf4 red[3][4][2][2][64];
+__global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
+                                                           VitScratch z) {
+  __shared__ vf4 red[3][2][2][2][64];
   __shared__ float sg[VRP][9];
-  __shared__ float scol[4][32];
+  __shared__ float scol[2][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int J0 = blockIdx.x * 32;
+  const int jb = blockIdx.x >> 1, rh = blockIdx.x & 1, rbase = rh * 64;
+  const int J0 = jb * 32;
   const bf16_t *wT = reinterpret_cast<const bf16_t *>(p.packed) + PK_2T;    // W2^T [2048][512]
-  if (tid < VRP) {
-    const int r = tid;
-    float v[8];
-    ld8f(g + (int64_t)rclamp(r, R) * VD + blockIdx.x * 8, v);
+  if (rh == 0) {
+    // side job: g's columns 8 jb .. + 8 transposed (gT) and their sums (db2)
+    if (tid < VRP) {
+      const int r = tid;
+      float v[8];
+      ld8f(g + (int64_t)rclamp(r, R) * VD + jb * 8, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = r < R ? v[e] : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = r < R ? v[e] : 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      sg[r][e] = v[e];
-      z.gT[(int64_t)(blockIdx.x * 8 + e) * VRP + r] = f2bf(v[e]);
+      for (int e = 0; e < 8; ++e) {
+        sg[r][e] = v[e];
+        z.gT[(int64_t)(jb * 8 + e) * VRP + r] = f2bf(v[e]);
+      }
+    }
+    __syncthreads();
+    if (tid < 8) {
+      float a = 0.f;
+      for (int r = 0; r < R; ++r) a += sg[r][tid];
+      G.b2[jb * 8 + tid] = a;
     }
   }
-  __syncthreads();
-  if (tid < 8) {
-    float a = 0.f;
-    for (int r = 0; r < R; ++r) a += sg[r][tid];
-    G.b2[blockIdx.x * 8 + tid] = a;
-  }
-  const int rg = w & 3, kq = w >> 2, li = lane & 15, lq = lane >> 4;
+  const int rg = w & 1, kq = w >> 1, li = lane & 15, lq = lane >> 4;
   vf4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -520,13 +530,11 @@ __global__ __launch_bounds__(1024) void vit_mlp2_bwd_kernel(VitP p, VitG G, int 
       const int k = kq * 128 + u * 32 + lq * 8;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int r = rg * 32 + t * 16 + li;
-        {
-          float v[8];
-          ld8f(g + (int64_t)rclamp(r, R) * VD + k, v);
-          af[u][t] = pack8(v);
-          if (r >= R) af[u][t] = zero8();
-        }
+        const int r = rbase + rg * 32 + t * 16 + li;
+        float v[8];
+        ld8f(g + (int64_t)rclamp(r, R) * VD + k, v);
+        af[u][t] = pack8(v);
+        if (r >= R) af[u][t] = zero8();
         bf[u][t] = ld8b(wT + (int64_t)(J0 + t * 16 + li) * VD + k);
       }
     }
@@ -550,16 +558,14 @@ __global__ __launch_bounds__(1024) void vit_mlp2_bwd_kernel(VitP p, VitG G, int 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const vf4 ra = red[0][rg][i][j][lane], rb2 = red[1][rg][i][j][lane], rc = red[2][rg][i][j][lane];
-        const vf4 o = vf4{(ra[0] + rb2[0]) + rc[0], (ra[1] + rb2[1]) + rc[1], (ra[2] + rb2[2]) + rc[2],
-                          (ra[3] + rb2[3]) + rc[3]};
         const int col = J0 + j * 16 + li;
-        const int rb = rg * 32 + i * 16 + lq * 4;
+        const int rb = rbase + rg * 32 + i * 16 + lq * 4;
         float gv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = rb + e;
           const float a = bf2f(s.aux[(int64_t)rclamp(r, R) * VF + col]);
-          const float dh = rbf(acc[i][j][e] + o[e]);
+          const float dh = rbf(((acc[i][j][e] + ra[e]) + rb2[e]) + rc[e]);
           gv[e] = r < R ? dh * gelu_erf_grad(a) : 0.f;
           if (r < R) z.g1[(int64_t)r * VF + col] = f2bf(gv[e]);
           cs[j] += gv[e];
@@ -576,15 +582,20 @@ __global__ __launch_bounds__(1024) void vit_mlp2_bwd_kernel(VitP p, VitG G, int 
     }
   }
   __syncthreads();
-  if (tid < 32) G.b1[J0 + tid] = ((scol[0][tid] + scol[1][tid]) + scol[2][tid]) + scol[3][tid];
+  // this row half's Linear1 bias-gradient partial (B2 adds the halves)
+  if (tid < 32) z.db1p[rh * VF + J0 + tid] = scol[0][tid] + scol[1][tid];
 }
 
 // An input-gradient block out[rows 32 rq .. + 32][I0 .. I0 + 16] = A[rows][K] (bf16, row stride
 // K) x BT[I0 .. + 16][K]^T (bf16 k-contiguous weight image), 4 waves = 4 K quarters added in LDS
 // in a fixed order (fp32 out, row stride 512)
+// ... and, for the LayerNorm whose output gradient it is, the block's row partials of the LN
+// backward sums over its 16 columns: rpart[I0 / 16][row] = (sum gamma d, sum gamma d xhat)
+// with xhat from X, mu, rs (the consumer adds the 32 column blocks in order)
 template <int K>
 __device__ __forceinline__ void dgrad_block(const bf16_t *A, const bf16_t *BT, float *out, int R, int I0, int rq,
-                                            int w, int lane, vf4 *red) {
+                                            int w, int lane, vf4 *red, const float *X, const float *mu,
+                                            const float *rs, const float *gamma, float *rpart) {
   constexpr int KQ = K / 4, NS = KQ / 32;
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[2];
@@ -613,14 +624,36 @@ __device__ __forceinline__ void dgrad_block(const bf16_t *A, const bf16_t *BT, f
     for (int t = 0; t < 2; ++t) red[((w - 1) * 2 + t) * 64 + lane] = acc[t];
   __syncthreads();
   if (w > 0) return;
+  const float gm = gamma[I0 + li];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const vf4 a = red[(0 * 2 + t) * 64 + lane], b = red[(1 * 2 + t) * 64 + lane], c = red[(2 * 2 + t) * 64 + lane];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int r = rq * 32 + t * 16 + lq * 4 + e;
-      if (r < R) out[(int64_t)r * VD + I0 + li] = ((acc[t][e] + a[e]) + b[e]) + c[e];
+      const int r = rq * 32 + t * 16 + lq * 4 + e, rr = rclamp(r, R);
+      const float d = ((acc[t][e] + a[e]) + b[e]) + c[e];
+      const float xh = (X[(int64_t)rr * VD + I0 + li] - mu[rr]) * rs[rr];
+      if (r < R) out[(int64_t)r * VD + I0 + li] = d;
+      const float ga = row_sum16(r < R ? gm * d : 0.f), gb = row_sum16(r < R ? gm * d * xh : 0.f);
+      if (li == 0) {
+        rpart[((I0 >> 4) * VRP + r) * 2] = ga;
+        rpart[((I0 >> 4) * VRP + r) * 2 + 1] = gb;
+      }
     }
+  }
+}
+
+// the LN backward row sums from the producers' 32 column-block partials, added in order
+__device__ __forceinline__ void lnb_rows_parts(const float *rpart, float *sa, float *sb, int tid) {
+  if (tid < VRP) {
+    float a = 0.f, b = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) {
+      a += rpart[(q * VRP + tid) * 2];
+      b += rpart[(q * VRP + tid) * 2 + 1];
+    }
+    sa[tid] = a / (float)VD;
+    sb[tid] = b / (float)VD;
   }
 }
 
@@ -632,6 +665,12 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
   __shared__ vf4 red[3 * 2 * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int blk = blockIdx.x;
+  if (blk >= 128 + 512) {
+    // Linear1 bias gradient: the two row halves' partials added
+    const int j = (blk - 640) * 256 + threadIdx.x;
+    G.b1[j] = z.db1p[j] + z.db1p[VF + j];
+    return;
+  }
   if (blk >= 128 + 256) {
     const int q = blk - 384;
     wgrad_block(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
@@ -644,42 +683,10 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
   }
   // input gradient: workgroup (16-column block, row quarter)
   dgrad_block<VF>(z.g1, reinterpret_cast<const bf16_t *>(p.packed) + PK_1T, z.dln2, R, (blk >> 2) * 16, blk & 3, w,
-                  lane, red);
+                  lane, red, s.x1, s.mu2, s.rs2, p.ln2_w, z.rp2);
 }
 
 // ---------------------------------------------------------------- LayerNorm backward pieces
-// per-row sums of the LN backward, a wave per row: ma = mean(gamma dY), mb = mean(gamma dY xhat)
-__device__ __forceinline__ void lnb_rows(const float *dY, const float *X, const float *gamma, const float *mu,
-                                         const float *rs, int R, float *sa, float *sb, int w, int nw, int lane) {
-  float gm[8];
-  ld8f(gamma + lane * 8, gm);
-  for (int r0 = w; r0 < VRP; r0 += 4 * nw) {
-    float d[4][8], x[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + i * nw;
-      ld8f(dY + (int64_t)rclamp(r, R) * VD + lane * 8, d[i]);
-      ld8f(X + (int64_t)rclamp(r, R) * VD + lane * 8, x[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + i * nw;
-      float a = 0.f, b = 0.f;
-      if (r < R) {
-        const float m = mu[r], s = rs[r];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float gd = gm[e] * d[i][e];
-          a += gd;
-          b += gd * ((x[i][e] - m) * s);
-        }
-        a = wave_sum(a) / (float)VD;
-        b = wave_sum(b) / (float)VD;
-      }
-      if (lane == 0 && r < VRP) { sa[r] = a; sb[r] = b; }
-    }
-  }
-}
 // columns c0 .. c0 + 32, 512 threads (column tid & 31, rows 8 (tid >> 5) .. + 8):
 // dX = resid + rstd (gamma dY - ma - xhat mb) -> dXout [R][512] f32; the affine gradients
 // (sum dY xhat, sum dY) and, with a dropout (to_out), g_o = dX keep / (1 - p) transposed into
@@ -740,7 +747,7 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
   __shared__ float sdo[32][68];
   __shared__ float sa[VRP], sbm[VRP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  lnb_rows(z.dln2, s.x1, p.ln2_w, s.mu2, s.rs2, R, sa, sbm, w, 8, lane);
+  lnb_rows_parts(z.rp2, sa, sbm, tid);
   __syncthreads();
   const uint64_t sd = step_seed(p.seed, p.seed_off);
   if (blockIdx.x >= 4 * VH) {
@@ -884,7 +891,8 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 // ---------------------------------------------------------------- B4: to_qkv backward, dWqkv, dWo
 // 256 threads.  Workgroups 0..127: dLN1 = dqkv Wqkv in (16 columns, 32 rows) blocks (4 waves = K
 // quarters of 384, added in LDS); 128..319: dWqkv = dqkv^T LN1; 320..383: dWo = g_o^T o.
-__global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
+__global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, const float *x0, VitSaved s,
+                                                          VitScratch z) {
   __shared__ vf4 red[3 * 2 * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int blk = blockIdx.x;
@@ -900,7 +908,7 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
   }
   // input gradient: workgroup (16-column block, row quarter)
   dgrad_block<VQ>(z.dqkv, reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT, z.dln1, R, (blk >> 2) * 16, blk & 3,
-                  w, lane, red);
+                  w, lane, red, x0, s.mu1, s.rs1, p.ln1_w, z.rp1);
 }
 
 // ---------------------------------------------------------------- B5: LN1 backward + residual
@@ -908,8 +916,8 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
 __global__ __launch_bounds__(512) void vit_ln1_bwd_kernel(VitP p, VitG G, int R, const float *x0, VitSaved s,
                                                           VitScratch z, float *dx0) {
   __shared__ float sa[VRP], sbm[VRP], part[3 * 16 * 32];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  lnb_rows(z.dln1, x0, p.ln1_w, s.mu1, s.rs1, R, sa, sbm, w, 8, lane);
+  const int tid = threadIdx.x;
+  lnb_rows_parts(z.rp1, sa, sbm, tid);
   __syncthreads();
   lnb_cols(z.dln1, x0, p.ln1_w, s.mu1, s.rs1, z.dx1, R, sa, sbm, blockIdx.x * 32, dx0, G.ln1_w, G.ln1_b, false,
            0.f, 0, nullptr, nullptr, part, tid);
@@ -1083,10 +1091,10 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   const VitSaved s = vit_saved(const_cast<void *>(saved));
   const VitScratch z = vit_scratch(scratch);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(VF / 32), dim3(1024), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(128 + 256 + 256), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(2 * VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
+  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(128 + 256 + 256 + VF / 256), dim3(256), 0, st, *p, *G, R, s, z);
   hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, s, z);
+  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, x0, s, z);
   hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
   return launch_status("vit_layer_bwd");
 }
