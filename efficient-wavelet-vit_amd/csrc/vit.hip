@@ -1116,3 +1116,103 @@ extern "C" int ewvit_vit_embed_bwd(const float *dtok, int B, int npos, float dro
                      seed_off, dy, dcls, dpos);
   return launch_status("vit_embed_bwd");
 }
+
+// ---------------------------------------------------------------- tall-K, few-row GEMM
+// C[M][N] = A[M][K] (bf16, row stride lda) x W[N][K]^T (fp32 master, rounded to bf16 as
+// ewvit_gemm rounds it) + bias, M <= 64, N % 256 == 0, K % 256 == 0 — the patch_to_embedding
+// forward (sfe.py:155: 64 frames x 62720 x 512, 128 MB of fp32 weight).  The generic split-K
+// GEMM tiles it 64 x 64 and reads the 8 MB activation 8 times (54 us isolated, 69 us in the
+// step); here a workgroup owns a 256-wide K slice and 256 columns (each W element read once, the
+// K slice of A once per wave from L2) and leaves a fp32 partial; the reduce adds the slices in
+// a fixed order with the bias.
+namespace ewvit {
+__global__ __launch_bounds__(256) void tallk_part_kernel(const bf16_t *A, int64_t lda, const float *W, int64_t K,
+                                                         int M, int N, float *part) {
+  const int s = blockIdx.x, ch = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int64_t k0 = (int64_t)s * 256;
+  const int c0 = ch * 256 + w * 64;
+  vf4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int sb = 0; sb < 8; sb += 2) {
+    vb8 af[2][4], bf[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t k = k0 + (sb + u) * 32 + lq * 8;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = t * 16 + li;
+        af[u][t] = ld8b(A + (int64_t)rclamp(r, M) * lda + k);
+        if (r >= M) af[u][t] = zero8();
+        float v[8];
+        ld8f(W + (int64_t)(c0 + t * 16 + li) * K + k, v);
+        bf[u][t] = pack8(v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma(af[u][i], bf[u][j], acc[i][j]);
+  }
+  float *dst = part + (int64_t)s * 64 * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[(int64_t)(i * 16 + lq * 4 + e) * N + c0 + j * 16 + li] = acc[i][j][e];
+}
+
+// out[r][c] = bias[c] + sum_s part[s][r][c]: a workgroup per 64 outputs of one row, 4 slice
+// quarters per output (8 loads in flight per thread), quarters added in order in LDS
+__global__ __launch_bounds__(256) void tallk_reduce_kernel(const float *part, int S, int M, int N, const float *bias,
+                                                           float *C, int64_t ldc) {
+  __shared__ float red[4][64];
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  const int r = o / N, c = o % N;
+  const int sq = (S + 3) / 4, s0 = q * sq, s1 = s0 + sq < S ? s0 + sq : S;
+  float a = 0.f;
+  int sidx = s0;
+  for (; sidx + 8 <= s1; sidx += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[((int64_t)(sidx + u) * 64 + r) * N + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
+  }
+  for (; sidx < s1; ++sidx) a += part[((int64_t)sidx * 64 + r) * N + c];
+  red[q][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (q == 0 && r < M) {
+    const int l = threadIdx.x;
+    C[(int64_t)r * ldc + c] = (((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]) + (bias ? bias[c] : 0.f);
+  }
+}
+}  // namespace ewvit
+
+extern "C" int64_t ewvit_gemm_tallk_workspace(int64_t M, int64_t N, int64_t K) {
+  return (K / 256) * 64 * N * (int64_t)sizeof(float);
+}
+
+extern "C" int ewvit_gemm_tallk(const void *A, int64_t lda, const float *W, const float *bias, float *C, int64_t ldc,
+                                int64_t M, int64_t N, int64_t K, float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(A && W && C && workspace, "gemm_tallk: null pointer");
+  EWVIT_CHECK_ARG(M >= 1 && M <= 64 && N % 256 == 0 && K % 256 == 0 && K / 256 <= 65535 && lda % 8 == 0 &&
+                      lda >= K && ldc >= N,
+                  "gemm_tallk: M=%lld N=%lld K=%lld outside its shape class", (long long)M, (long long)N,
+                  (long long)K);
+  hipStream_t st = as_stream(stream);
+  const int S = (int)(K / 256);
+  hipLaunchKernelGGL(tallk_part_kernel, dim3((unsigned)S, (unsigned)(N / 256)), dim3(256), 0, st, (const bf16_t *)A, lda,
+                     W, K, (int)M, (int)N, workspace);
+  if (int rc = launch_status("gemm_tallk")) return rc;
+  hipLaunchKernelGGL(tallk_reduce_kernel, dim3((unsigned)(64 * N / 64)), dim3(256), 0, st, workspace, S, (int)M, (int)N,
+                     bias, C, ldc);
+  return launch_status("gemm_tallk reduce");
+}

@@ -111,6 +111,7 @@ SIGNATURES = {
     'ewvit_vit_layer_fwd': [_vp, _i32, _vp, _vp, _vp, _vp],
     'ewvit_vit_layer_bwd': [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_vit_pack': [_vp, _i32, _vp, _vp],
+    'ewvit_gemm_tallk': [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp],
     'ewvit_vit_embed_fwd': [_vp, _vp, _vp, _i32, _f32, _u64, _vp, _vp, _vp],
     'ewvit_vit_embed_bwd': [_vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp],
 }
@@ -119,6 +120,7 @@ SIGNATURES = {
 QUERIES = {
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_vit_layer_workspace': (_i64, [_i32]),
+    'ewvit_gemm_tallk_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),

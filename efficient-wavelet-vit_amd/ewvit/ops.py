@@ -94,11 +94,33 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
     return C
 
 
+def _tallk(X, W, out, kw):
+    """The few-row, long-K shape class of ewvit_gemm_tallk (patch_to_embedding's forward,
+    sfe.py:155): bf16 X with at most 64 rows, fp32 W, K and N multiples of 256, K >= 16384,
+    fp32 output, no epilogue but a bias."""
+    M, K = X.shape
+    N = W.shape[0]
+    def unset(v):
+        return v is None or (isinstance(v, (bool, int, float)) and not v)
+    if not all(unset(v) for k, v in kw.items() if k != 'bias'):
+        return False
+    return (M <= 64 and K >= 16384 and K % 256 == 0 and N % 256 == 0 and X.dtype == torch.bfloat16
+            and W.dtype == torch.float32 and W.is_contiguous() and X.stride(0) % 8 == 0 and out.dtype == torch.float32
+            and out.stride(1) == 1)
+
+
 def mm_nt(X, W, out, **kw):
     """out[M,N] = X[M,K] @ W[N,K]^T  (nn.Linear forward)."""
     M, K = X.shape
     N = W.shape[0]
     assert X.stride(1) == 1 and W.stride(1) == 1
+    if _tallk(X, W, out, kw):
+        L.require_gpu(X, W, out)
+        ws = torch.empty(int(L.load().ewvit_gemm_tallk_workspace(M, N, K)) // 4, dtype=torch.float32, device=X.device)
+        bias = kw.get('bias')
+        L.call('ewvit_gemm_tallk', L.ptr(X), X.stride(0), L.ptr(W), L.ptr(bias), L.ptr(out), out.stride(0), M, N, K,
+               L.ptr(ws), L.stream(out), work={'flops': 2.0 * M * N * K, 'bytes': M * K * 2 + N * K * 4 + M * N * 4})
+        return out
     return gemm(X, (X.stride(0), 1), W, (1, W.stride(0)), out, M, N, K, **kw)
 
 

@@ -131,6 +131,14 @@ int ewvit_amax_partials(const void *x, int dtype, int64_t rows, int64_t cols, in
                         void *stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n]  (bias gradients).  accumulate!=0 adds. */
+/* C[M][N] f32 = A[M][K] (bf16, row stride lda) x W[N][K]^T (fp32, rounded to bf16) + bias (may be
+ * NULL) for M <= 64, N % 256 == 0, K % 256 == 0: the patch_to_embedding forward (sfe.py:155,
+ * [64 x 62720] x [62720 x 512]).  A workgroup per (256-wide K slice, 256 columns) leaves a fp32
+ * partial in `workspace` (ewvit_gemm_tallk_workspace bytes), a second launch adds the slices
+ * in a fixed order. */
+int64_t ewvit_gemm_tallk_workspace(int64_t M, int64_t N, int64_t K);
+int ewvit_gemm_tallk(const void *A, int64_t lda, const float *W, const float *bias, float *C, int64_t ldc, int64_t M,
+                     int64_t N, int64_t K, float *workspace, void *stream);
 int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N, float *out,
                  int accumulate, void *stream);
 

@@ -157,3 +157,24 @@ def test_embed_matches_torch(B):
     torch.testing.assert_close(yd.grad, (w * m)[:, 1:], rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(pd.grad[0:B], (w * m).sum(1, keepdim=True), rtol=1e-6, atol=1e-6)
     assert float(pd.grad[B:].abs().max()) == 0.0 if B < 64 else True
+
+
+@pytest.mark.parametrize('M', [64, 37, 1])
+def test_tallk_gemm_patch_embedding_shape(M):
+    """ewvit_gemm_tallk (patch_to_embedding's forward, sfe.py:155: [M, 62720] x [62720, 512] +
+    bias) against torch fp32 on the same bf16-rounded operands (fp32 accumulation, different
+    summation order: 1e-4 of scale) and against the generic split-K GEMM it replaces."""
+    import ewvit
+    g = torch.Generator().manual_seed(M)
+    K, N = 62720, 512
+    x = torch.randn(M, K, generator=g).to(DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.01).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    y = torch.empty(M, N, device=DEV)
+    ewvit.mm_nt(x, w, y, bias=b)
+    ref = x.float() @ w.to(torch.bfloat16).float().t() + b
+    scale = float(ref.abs().max())
+    assert float((y - ref).abs().max()) <= 1e-4 * scale
+    y2 = torch.empty_like(y)
+    ewvit.mm_nt(x, w, y2, bias=b, splitk=64)            # the generic split-K path
+    assert float((y - y2).abs().max()) <= 1e-4 * scale
