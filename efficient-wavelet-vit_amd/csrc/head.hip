@@ -88,7 +88,7 @@ struct HeadWs {
   __device__ float *dh1() const { return dy() + HN * HD; }        // d gate pre-activation [N][64]
   __device__ float *dz2() const { return dh1() + HN * 64; }       // d gate logits [N][4]
   __device__ float *ds(int i) const { return dz2() + HN * 4 + (int64_t)i * HN * HD; }  // d s2, d f2
-  __device__ float *wc() const { return ds(2); }                  // fusion centre tap, packed [128][256]
+  __device__ float *wc() const { return ds(2); }                  // (unused; kept for the layout)
 };
 
 __host__ __device__ inline int64_t head_ws_floats() { return W_TOTAL; }
@@ -104,6 +104,16 @@ __host__ __device__ inline int64_t head_ws_floats() { return W_TOTAL; }
 #define HTR(k) do { (void)(k); } while (0)
 #endif
 __device__ inline HeadWs head_ws(float *b) { return HeadWs{b}; }
+
+// The rows kernels' weights as bf16, packed once per call by ewvit_head_fwd (head_pack_kernel):
+// per attention block i, to_q / to_kv / to_out in their own layout (forward B fragments, k
+// contiguous) and transposed (backward B fragments: the input gradient reduces over the
+// weight's output index); the gate's first layer and the fusion conv's centre tap transposed.
+// The fp32 masters round to the same bf16 values the fragment loaders produced from them.
+constexpr int64_t HP_Q = 0, HP_KV = HP_Q + HD * HD, HP_O = HP_KV + 2 * HD * HD, HP_QT = HP_O + HD * HD,
+                  HP_KVT = HP_QT + HD * HD, HP_OT = HP_KVT + 2 * HD * HD, HP_BLK = HP_OT + HD * HD;
+constexpr int64_t HP_G1T = 4 * HP_BLK, HP_WCT = HP_G1T + 256 * 64, HP_TOTAL = HP_WCT + 256 * HD;
+__device__ __forceinline__ hbf16x8 h_ld8(const bf16_t *p) { return *reinterpret_cast<const hbf16x8 *>(p); }
 
 // attention blocks in forward order: 0 = layer 0 s, 1 = layer 0 f, 2 = layer 1 s, 3 = layer 1 f
 // block i reads state x = st[xin(i)] and context ctx = st[cin(i)], writes st[xout(i)]
@@ -212,13 +222,13 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
   int bi = 0;                                                    // the block the fragment loaders read
   auto nk4 = [](int) { return 4; };
   // to_q (8 tiles) and to_kv of the self token and of the context token (16 + 16 tiles)
+  const bf16_t *pk = reinterpret_cast<const bf16_t *>(p.packed);
   auto frag_qkv = [&](int t, int s, int c, int k0) {
-    const HeadCA &ca = p.ca[bi];
-    const float *wr = t < 8 ? ca.wq + (int64_t)(t * 16 + c) * HD
-                            : ca.wkv + (int64_t)((t < 24 ? t - 8 : t - 24) * 16 + c) * HD;
-    return h_frag_rowk(wr + k0);
+    const bf16_t *wr = t < 8 ? pk + bi * HP_BLK + HP_Q + (int64_t)(t * 16 + c) * HD
+                             : pk + bi * HP_BLK + HP_KV + (int64_t)((t < 24 ? t - 8 : t - 24) * 16 + c) * HD;
+    return h_ld8(wr + k0);
   };
-  auto frag_o = [&](int t, int s, int c, int k0) { return h_frag_rowk(p.ca[bi].wo + (int64_t)(t * 16 + c) * HD + k0); };
+  auto frag_o = [&](int t, int s, int c, int k0) { return h_ld8(pk + bi * HP_BLK + HP_O + (int64_t)(t * 16 + c) * HD + k0); };
   hbf16x8 bA[5][4], bO[1][4];
   for (int e = tid; e < 4 * 3 * HD; e += HT) {
     const int i = e / (3 * HD), j = (e / HD) % 3, c = e % HD;
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
 // fusion_gate centre tap W_c[o][k] = wfg[o * fg_so + k * fg_si + 4 * fg_tap] (8 column tiles) and
 // the gate's first layer W1 [64][256] (4 tiles) over concat = [s2, f2] (dama.py:151), K = 256:
 // one wave per (16 frames, 16 output columns), so the strided centre-tap reads spread over 32+
-// CUs; frame group 0 also leaves the centre tap packed [128][256] for the backward.
+// CUs (the backward reads the tap transposed from the head pack, head_pack_kernel).
 __global__ __launch_bounds__(64) void head_fwd_fuse_kernel(HeadParams p, float *ws_base, int N) {
   const HeadWs ws{ws_base};
   const int t = blockIdx.x % 12, gq = blockIdx.x / 12;
@@ -353,11 +363,6 @@ __global__ __launch_bounds__(64) void head_fwd_fuse_kernel(HeadParams p, float *
 #pragma unroll
       for (int e = 0; e < 8; ++e) w[e] = p.wfg[(int64_t)o * p.fg_so + (int64_t)(k0 + e) * p.fg_si + 4 * p.fg_tap];
       bf[s] = h_pack8(w);
-      if (gq == 0) {
-        float *d = ws.wc() + (int64_t)o * 256 + k0;
-        *reinterpret_cast<float4 *>(d) = make_float4(w[0], w[1], w[2], w[3]);
-        *reinterpret_cast<float4 *>(d + 4) = make_float4(w[4], w[5], w[6], w[7]);
-      }
     } else {
       bf[s] = h_frag_rowk(p.g1w + (int64_t)((t - 8) * 16 + c) * 256 + k0);
     }
@@ -607,19 +612,21 @@ __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *
   auto nk6 = [](int) { return 6; };
   auto nkx = [](int t) { return t < 8 ? 12 : 8; };
   // d concat = dy Wc + dh1 W1 (K = 128 + 64): 16 tiles of concat columns
+  const bf16_t *pk = reinterpret_cast<const bf16_t *>(p.packed);
   auto frag_c = [&](int t, int s, int c, int k0) {
     const int col = t * 16 + c;
-    if (s < 4) return h_frag_colk(ws.wc() + (int64_t)k0 * 256 + col, 256);   // packed by the forward
-    return h_frag_colk(p.g1w + (int64_t)(k0 - HD) * 256 + col, 256);
+    if (s < 4) return h_ld8(pk + HP_WCT + (int64_t)col * HD + k0);           // Wc^T [256][128]
+    return h_ld8(pk + HP_G1T + (int64_t)col * 64 + (k0 - HD));                // W1^T [256][64]
   };
-  auto frag_o = [&](int t, int s, int c, int k0) { return h_frag_colk(p.ca[bi].wo + (int64_t)k0 * HD + t * 16 + c, HD); };
+  auto frag_o = [&](int t, int s, int c, int k0) {
+    return h_ld8(pk + bi * HP_BLK + HP_OT + (int64_t)(t * 16 + c) * HD + k0);
+  };
   // d xn = [dq | dkv_self] [Wq ; Wkv] (8 tiles, K = 384); d ctx = dkv_ctx Wkv (8 tiles, K = 256)
   auto frag_x = [&](int t, int s, int c, int k0) {
-    const HeadCA &ca = p.ca[bi];
     const int col = (t & 7) * 16 + c;
-    if (t < 8 && s < 4) return h_frag_colk(ca.wq + (int64_t)k0 * HD + col, HD);
+    if (t < 8 && s < 4) return h_ld8(pk + bi * HP_BLK + HP_QT + (int64_t)col * HD + k0);
     const int kk = t < 8 ? k0 - HD : k0;
-    return h_frag_colk(ca.wkv + (int64_t)kk * HD + col, HD);
+    return h_ld8(pk + bi * HP_BLK + HP_KVT + (int64_t)col * (2 * HD) + kk);
   };
   hbf16x8 bC[2][6], bO[1][4], bX[2][12];
   for (int e = tid; e < 4 * HD; e += HT) lnw[e] = p.ca[e >> 7].ln_w[e & 127];
@@ -922,6 +929,49 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams p, cons
   }
 }
 
+// one thread per source element: the 4 blocks' to_q / to_kv / to_out (both layouts), the gate's
+// first layer and the fusion conv's centre tap transposed
+__global__ __launch_bounds__(256) void head_pack_kernel(HeadParams p, bf16_t *pk) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  constexpr int64_t PER = 4 * HD * HD;                 // wq + wkv + wo elements of one block
+  if (i < 4 * PER) {
+    const int b = (int)(i / PER);
+    const int64_t e = i - b * PER;
+    const HeadCA &ca = p.ca[b];
+    bf16_t *blk = pk + b * HP_BLK;
+    if (e < HD * HD) {                                  // wq [o][k]
+      const int o = (int)(e / HD), k = (int)(e % HD);
+      const bf16_t v = f2bf(ca.wq[e]);
+      blk[HP_Q + e] = v;
+      blk[HP_QT + (int64_t)k * HD + o] = v;
+    } else if (e < 3 * HD * HD) {                       // wkv [o][k], o < 256
+      const int64_t f = e - HD * HD;
+      const int o = (int)(f / HD), k = (int)(f % HD);
+      const bf16_t v = f2bf(ca.wkv[f]);
+      blk[HP_KV + f] = v;
+      blk[HP_KVT + (int64_t)k * (2 * HD) + o] = v;
+    } else {                                            // wo [o][k]
+      const int64_t f = e - 3 * HD * HD;
+      const int o = (int)(f / HD), k = (int)(f % HD);
+      const bf16_t v = f2bf(ca.wo[f]);
+      blk[HP_O + f] = v;
+      blk[HP_OT + (int64_t)k * HD + o] = v;
+    }
+    return;
+  }
+  const int64_t j = i - 4 * PER;
+  if (j < 64 * 256) {                                   // g1w [o = 64][k = 256] -> [k][o]
+    const int o = (int)(j / 256), k = (int)(j % 256);
+    pk[HP_G1T + (int64_t)k * 64 + o] = f2bf(p.g1w[j]);
+    return;
+  }
+  const int64_t m = j - 64 * 256;
+  if (m < (int64_t)HD * 256) {                          // centre tap Wc[o = 128][k = 256] -> [k][o]
+    const int o = (int)(m / 256), k = (int)(m % 256);
+    pk[HP_WCT + (int64_t)k * HD + o] = f2bf(p.wfg[o * p.fg_so + k * p.fg_si + 4 * p.fg_tap]);
+  }
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -945,6 +995,7 @@ static_assert(HL_FWD_ROWS <= 160 * 1024 && HL_BWD_ROWS <= 64 * 1024 && HL_FWD_TA
 static unsigned head_groups(int N) { return (unsigned)((N + FG - 1) / FG); }
 
 extern "C" int64_t ewvit_head_workspace(void) { return head_ws_floats() * (int64_t)sizeof(float); }
+extern "C" int64_t ewvit_head_pack_bytes(void) { return HP_TOTAL * (int64_t)sizeof(bf16_t); }
 
 extern "C" int ewvit_head_fwd(const HeadParams *params, const float *s0, const float *f0, int N, float *workspace,
                               float *fused, float *s_out, float *f_out, void *stream) {
@@ -953,7 +1004,12 @@ extern "C" int ewvit_head_fwd(const HeadParams *params, const float *s0, const f
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(head_fwd_rows_kernel),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)HL_FWD_ROWS) == hipSuccess;
   (void)attr;
+  EWVIT_CHECK_ARG(params->packed, "head_fwd: no pack buffer (ewvit_head_pack_bytes)");
   hipStream_t s = as_stream(stream);
+  constexpr int64_t npk = 4 * 4 * HD * HD + 64 * 256 + HD * 256;
+  hipLaunchKernelGGL(head_pack_kernel, dim3((unsigned)((npk + 255) / 256)), dim3(256), 0, s, *params,
+                     (bf16_t *)params->packed);
+  if (int rc = launch_status("head_fwd pack")) return rc;
   hipLaunchKernelGGL(head_fwd_rows_kernel, dim3(head_groups(N)), dim3(HT), HL_FWD_ROWS, s, *params, s0, f0, workspace,
                      s_out, f_out, N);
   if (int rc = launch_status("head_fwd rows")) return rc;

@@ -140,6 +140,7 @@ QUERIES = {
     'ewvit_bn_bwd_reduce_rows': (_i32, [_i64, _i64, _i32]),
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_head_workspace': (_i64, []),
+    'ewvit_head_pack_bytes': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
 }
 

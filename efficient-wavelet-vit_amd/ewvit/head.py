@@ -29,7 +29,8 @@ class _Params(ctypes.Structure):
     _fields_ = [('ca', _CA * 4), ('wfg', _vp), ('fg_so', _i64), ('fg_si', _i64), ('fg_tap', _i64), ('bfg', _vp),
                 ('bn_w', _vp), ('bn_b', _vp), ('bn_rm', _vp), ('bn_rv', _vp), ('bn_nbt', _vp), ('bn_mom', _f32),
                 ('bn_eps', _f32), ('g1w', _vp), ('g1b', _vp), ('g2w', _vp), ('g2b', _vp), ('p_ca', _f32),
-                ('p_gate', _f32), ('seed', _u64), ('seed_off', _vp), ('training', _i32), ('ln_eps', _f32)]
+                ('p_gate', _f32), ('seed', _u64), ('seed_off', _vp), ('training', _i32), ('ln_eps', _f32),
+                ('packed', _vp)]
 
 
 class HeadCfg:
@@ -39,8 +40,9 @@ class HeadCfg:
         self.bn, self.ln_eps, self.p_ca, self.p_gate, self.training, self.seed = bn, ln_eps, p_ca, p_gate, training, seed
 
 
-def _params(cfg, ts, dev):
+def _params(cfg, ts, dev, packed=None):
     p = _Params()
+    p.packed = packed
     for i in range(4):
         lw, lb, wq, wkv, wo, bo = ts[6 * i:6 * i + 6]
         p.ca[i] = _CA(lw.data_ptr(), lb.data_ptr(), wq.data_ptr(), wkv.data_ptr(), wo.data_ptr(), bo.data_ptr())
@@ -72,9 +74,10 @@ class DamaHeadFn(torch.autograd.Function):
         ts = tuple(t if t.dtype == torch.float32 else t.float() for t in ts)
         dev = s0.device
         ws = torch.empty(int(L.load().ewvit_head_workspace()) // 4, dtype=torch.float32, device=dev)
+        pk = torch.empty(int(L.load().ewvit_head_pack_bytes()), dtype=torch.uint8, device=dev)
         fused = torch.empty(N, 128, dtype=torch.float32, device=dev)
         so, fo = torch.empty_like(fused), torch.empty_like(fused)
-        p = _params(cfg, ts, dev)
+        p = _params(cfg, ts, dev, pk.data_ptr())
         ctx.gen = grads.note_use(ts[0])
         for t in ts[1:]:
             grads.note_use(t)
@@ -82,12 +85,12 @@ class DamaHeadFn(torch.autograd.Function):
                L.ptr(fo), L.stream(fused), work={'flops': 2.0 * N * 128 * (4 * (128 + 512 + 128) + 256 + 64),
                                                  'bytes': 4.0 * sum(t.numel() for t in ts)})
         ctx.cfg, ctx.N, ctx.ts = cfg, N, ts
-        ctx.save_for_backward(ws)
+        ctx.save_for_backward(ws, pk)
         return fused, so, fo
 
     @staticmethod
     def backward(ctx, g_fused, g_s, g_f):
-        (ws,) = ctx.saved_tensors
+        ws, pk = ctx.saved_tensors
         cfg, N, ts = ctx.cfg, ctx.N, ctx.ts
         dev = ws.device
 
@@ -103,7 +106,7 @@ class DamaHeadFn(torch.autograd.Function):
             if k == 24 and g.stride() != t.stride():
                 g = torch.empty_like(t)
             outs.append(g)
-        p = _params(cfg, ts, dev)
+        p = _params(cfg, ts, dev, pk.data_ptr())
         arr = ctypes.c_void_p * 4
 
         def col(j):

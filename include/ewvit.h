@@ -666,9 +666,13 @@ typedef struct {
   const int64_t *seed_off;
   int training;               /* BatchNorm batch statistics + running-stat update */
   float ln_eps;
+  void *packed;               /* ewvit_head_pack_bytes() of scratch: the weights as bf16, packed
+                               * by ewvit_head_fwd and read by it and by ewvit_head_bwd */
 } ewvit_head_params;
 /* bytes of fp32 workspace the head needs (what the forward saves for the backward) */
 int64_t ewvit_head_workspace(void);
+/* bytes of the bf16 weight pack (ewvit_head_params.packed) */
+int64_t ewvit_head_pack_bytes(void);
 /* s0, f0 [N][128] f32: the space / freq tokens (one per frame) -> fused, s_out, f_out [N][128]
  * (dama.py:165-169's fused / space / freq per frame); the workspace keeps what the backward
  * reads; one workgroup. */
