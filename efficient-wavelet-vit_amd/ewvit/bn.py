@@ -14,6 +14,7 @@ import weakref
 import torch
 
 from . import _lib as L
+from . import grads
 
 ACT = {None: 0, 'none': 0, 'relu': 1, 'silu': 2}
 
@@ -157,6 +158,9 @@ class BatchNormActFn(torch.autograd.Function):
                    L.stream(y), work={'bytes': (2 + int(training)) * xc.numel() * xc.element_size()})
         if training:
             ctx.save_for_backward(xc, weight, bias, mean, invstd)
+            ctx.gen = grads.note_use(weight)
+            grads.note_use(bias)
+            ctx.params = (weight, bias)
         ctx.cfg = (training, act, M, C, groups)
         ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, act, None, groups) if training else None
         return y
@@ -175,8 +179,9 @@ class BatchNormActFn(torch.autograd.Function):
         dyc = dy.to(xc.dtype)
         dyc = dyc.contiguous(memory_format=torch.channels_last) if dyc.dim() == 4 else dyc.contiguous()
         dx = torch.empty_like(xc)
-        dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
+        wp, bp = ctx.params
+        dg = _affine_grad(wp, ctx.gen, C, dy.device)
+        db = _affine_grad(bp, ctx.gen, C, dy.device)
         pr = ctx.bnlink.partials_for(dyc) if ctx.bnlink is not None else None
         ctx.bnlink = None
         if pr is not None:
@@ -184,12 +189,21 @@ class BatchNormActFn(torch.autograd.Function):
             L.call('ewvit_bn_bwd_partials', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight),
                    L.ptr(bias), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), None, 1, L.ptr(pr[0]), pr[1],
                    groups, L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
-            return dx, dg, db, None, None, None, None, None, None, None, None, None
+            return dx, grads.give(wp, dg, ctx.gen), grads.give(bp, db, ctx.gen), *(None,) * 9
         ws = torch.empty(L.load().ewvit_bn_workspace(M, C, groups) // 4, dtype=torch.float32, device=dy.device)
         L.call('ewvit_bn_bwd', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(weight), L.ptr(bias),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), 0, groups, L.ptr(ws), L.stream(dx),
                work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return dx, dg, db, None, None, None, None, None, None, None, None, None
+        return dx, grads.give(wp, dg, ctx.gen), grads.give(bp, db, ctx.gen), *(None,) * 9
+
+
+def _affine_grad(p, gen, C, dev):
+    """The [C] fp32 output for a BatchNorm affine parameter's gradient (its gradient slot when it
+    has one, ewvit.grads), or None without the parameter."""
+    if p is None:
+        return None
+    g = grads.grad_out(p, gen)
+    return g if g.dim() == 1 and g.is_contiguous() and g.dtype == torch.float32 else torch.empty(C, dtype=torch.float32, device=dev)
 
 
 def batch_norm_act(x, bn, act=None, training=None, groups=1, partials=None):
@@ -248,6 +262,9 @@ class BNDropAddFn(torch.autograd.Function):
                L.ptr(L.rng_offset(x.device)), L.ptr(scale), L.ptr(ws), L.stream(y),
                work={'bytes': (3 + int(partials is None)) * xc.numel() * xc.element_size()})
         ctx.save_for_backward(xc, weight, bias, mean, invstd, scale)
+        ctx.gen = grads.note_use(weight)
+        grads.note_use(bias)
+        ctx.params = (weight, bias)
         ctx.cfg = (M, C, M // N, skip.dtype)
         ctx.link = link if link is not None and link.armed else None
         ctx.bnlink = offer_bwd_link(y, xc, mean, invstd, weight, bias, 0, scale)
@@ -259,8 +276,9 @@ class BNDropAddFn(torch.autograd.Function):
         M, C, HW, sdt = ctx.cfg
         dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(xc)
-        dg = torch.empty(C, dtype=torch.float32, device=dy.device) if weight is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=dy.device) if bias is not None else None
+        wp, bp = ctx.params
+        dg = _affine_grad(wp, ctx.gen, C, dy.device)
+        db = _affine_grad(bp, ctx.gen, C, dy.device)
         pr = ctx.bnlink.partials_for(dyc) if ctx.bnlink is not None else None
         ctx.bnlink = None
         if pr is not None:
@@ -280,7 +298,7 @@ class BNDropAddFn(torch.autograd.Function):
             dskip = None
         else:
             dskip = dy.to(sdt)
-        return dx, dskip, dg, db, None, None, None, None, None, None, None, None
+        return dx, dskip, grads.give(wp, dg, ctx.gen), grads.give(bp, db, ctx.gen), *(None,) * 8
 
 
 def batch_norm_drop_add(x, bn, skip, drop_prob, partials=None, link=None):

@@ -297,6 +297,9 @@ class Conv2dFn(torch.autograd.Function):
                                      stride, Ho, Wo, gc, gs)
         if dx is None and skip is not None:       # x needs no gradient through the conv, only the skip's
             dx = skip
+        if dw is not None or db is not None:
+            wparam, bparam = ctx.params
+            dw, db = grads.give(wparam, dw, ctx.gen), grads.give(bparam, db, ctx.gen)
         return dx, dw, db, None, None, None
 
     @staticmethod

@@ -10,11 +10,18 @@ shape and strides), so the wgrad kernel writes into the all-reduce buffer itself
 autograd's AccumulateGrad adopts that view as ``param.grad`` — it steals an incoming
 gradient only when nothing else references the tensor object and its layout matches, so
 the view is built per call rather than kept — no clone, no copy back.
-When the parameter already holds a gradient (gradient accumulation over micro-batches) or
-is used more than once in the step (DAMA's frame chunks run every weight once per chunk:
-autograd sums the uses' gradients before AccumulateGrad, so two uses must not share one
-slot) a fresh tensor is returned and AccumulateGrad adds it as usual.  The uses are
-counted per step: ``begin_step`` opens a step, the ops' forwards call ``note_use``.
+When the parameter already holds a gradient (gradient accumulation over micro-batches) a
+fresh tensor is returned and AccumulateGrad adds it as usual.  The uses are counted per
+step: ``begin_step`` opens a step, the ops' forwards call ``note_use``.
+
+A parameter used more than once in the step (DAMA's frame chunks run every weight once per
+chunk, dama.py:179-186) would have autograd sum its uses' gradients — one add launch per
+parameter per extra use, ~560 small launches per step at config 5 — and AccumulateGrad copy
+the sum into the slot.  Instead the ops hand each use's gradient to ``give``, which keeps it
+and returns None to autograd; the first use in backward order writes straight into the slot
+(``grad_out``), and one callback at the end of the backward pass sums every kept gradient with
+``torch._foreach_add_`` (a few multi-tensor launches for all parameters), sets ``param.grad``
+and runs the parameter's post-accumulate hooks (the data-parallel buckets).
 
 Use counts are per thread: nn.DataParallel runs its replicas' forwards in threads
 (reference train.py:249-251), each with its own parameters.
@@ -62,13 +69,106 @@ def single_use(param, gen=None):
     return g != 0 and getattr(param, '_ewvit_gen', None) == g and param._ewvit_uses == 1
 
 
+def multi_use(param, gen):
+    """True when `param` entered step `gen`'s forward more than once."""
+    return (gen is not None and gen != 0 and getattr(param, '_ewvit_gen', None) == gen and
+            getattr(param, '_ewvit_uses', 0) > 1)
+
+
+def _slot_view(param, dtype=torch.float32):
+    slot = getattr(param, '_ewvit_grad_slot', None)
+    if slot is not None and param.is_leaf and param.grad is None and slot[0].dtype == dtype:
+        return slot[0].as_strided(param.shape, param.stride(), slot[1])
+    return None
+
+
 def grad_out(param, gen=None, dtype=torch.float32):
     """Output tensor for `param`'s gradient (shape and strides of `param`); `gen`: the step id
-    `note_use` returned in the op's forward."""
-    slot = getattr(param, '_ewvit_grad_slot', None)
-    if slot is not None and param.is_leaf and param.grad is None and slot[0].dtype == dtype and single_use(param, gen):
-        return slot[0].as_strided(param.shape, param.stride(), slot[1])
+    `note_use` returned in the op's forward.  The slot itself for a single use, and for the
+    first use in backward order of a parameter used several times (``give`` defers the sum)."""
+    view = _slot_view(param, dtype)
+    if view is not None:
+        if single_use(param, gen):
+            return view
+        if DEFER and multi_use(param, gen) and getattr(param, '_ewvit_slot_gen', None) != gen:
+            param._ewvit_slot_gen = gen
+            return view
     return torch.empty_like(param, dtype=dtype, memory_format=torch.preserve_format)
+
+
+# ---- deferred sums of multi-use parameters' gradients
+DEFER = True            # False: autograd sums the uses (the test switch, tests/test_gpu_grads.py)
+_lock = threading.Lock()
+_pending = {}           # step id -> {id(param): [param, [gradients], {streams}]}
+_queued = set()
+
+
+def give(param, g, gen):
+    """What an op's backward returns to autograd for `param`'s gradient `g`: `g` itself, or —
+    for a parameter used more than once in step `gen` — None, with `g` kept for the sum at the
+    end of the backward pass."""
+    if g is None or param is None or not DEFER or not multi_use(param, gen):
+        return g
+    with _lock:
+        ent = _pending.setdefault(gen, {}).setdefault(id(param), [param, [], set()])
+        ent[1].append(g)
+        if g.is_cuda:
+            ent[2].add(torch.cuda.current_stream(g.device))
+        first = gen not in _queued
+        _queued.add(gen)
+    if first:
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _settle(gen))
+    return None
+
+
+def _settle(gen):
+    """End of the backward pass: every kept gradient summed into its parameter's gradient."""
+    with _lock:
+        ents = list(_pending.pop(gen, {}).values())
+        _queued.discard(gen)
+    if not ents:
+        return
+    cuda = [e for e in ents if e[1][0].is_cuda]
+    if cuda:
+        cur = torch.cuda.current_stream(cuda[0][1][0].device)
+        seen = set()
+        for _, _, streams in cuda:
+            for st in streams:
+                if st != cur and st not in seen:
+                    seen.add(st)
+                    cur.wait_stream(st)
+    copy_dst, copy_src, rounds, finals = [], [], [], []
+    for p, ts, _ in ents:
+        rest = ts
+        if p.grad is not None:                       # accumulation over micro-batches
+            base = p.grad
+        else:
+            view = _slot_view(p)
+            hit = None if view is None else next((i for i, t in enumerate(ts) if t.data_ptr() == view.data_ptr()), None)
+            if hit is not None:                      # the first use wrote into the slot
+                base, rest = ts[hit], ts[:hit] + ts[hit + 1:]
+            elif view is not None:
+                base, rest = view, ts[1:]
+                copy_dst.append(view)
+                copy_src.append(ts[0])
+            else:
+                base, rest = ts[0], ts[1:]
+        finals.append((p, base))
+        for k, t in enumerate(rest):
+            if len(rounds) <= k:
+                rounds.append(([], []))
+            rounds[k][0].append(base)
+            rounds[k][1].append(t)
+    if copy_dst:
+        torch._foreach_copy_(copy_dst, copy_src)
+    for dst, src in rounds:
+        torch._foreach_add_(dst, src)
+    for p, base in finals:
+        if p.grad is None:
+            p.grad = base
+        hooks = getattr(p, '_post_accumulate_grad_hooks', None)
+        for h in (list(hooks.values()) if hooks else []):
+            h(p)
 
 
 def set_slot(param, flat, offset):

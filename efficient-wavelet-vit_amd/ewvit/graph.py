@@ -156,7 +156,9 @@ class GradBuckets:
 
     def _hook(self, i):
         def hook(p):
-            if not self.collect:
+            # (a parameter whose uses all deferred their gradients to ewvit.grads' end-of-backward
+            # sum reaches AccumulateGrad with none: its hook runs again once the sum is in)
+            if not self.collect or p.grad is None:
                 return
             self.observed.append(i)
             v = self.views[i]

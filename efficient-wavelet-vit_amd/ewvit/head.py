@@ -117,7 +117,8 @@ class DamaHeadFn(torch.autograd.Function):
                wfg.stride(3), L.ptr(outs[25]), L.ptr(outs[26]), L.ptr(outs[27]), L.ptr(outs[28]), L.ptr(outs[29]),
                L.ptr(outs[30]), L.ptr(outs[31]), L.stream(ds0),
                work={'flops': 4.0 * N * 128 * (4 * (128 + 512 + 128) + 256 + 64), 'bytes': 8.0 * sum(t.numel() for t in ts)})
-        return (None, ds0, df0, *[g if ctx.needs_input_grad[3 + k] else None for k, g in enumerate(outs)])
+        return (None, ds0, df0, *[grads.give(t, g, ctx.gen) if ctx.needs_input_grad[3 + k] else None
+                                  for k, (t, g) in enumerate(zip(ts, outs))])
 
 
 def params_of(dama):

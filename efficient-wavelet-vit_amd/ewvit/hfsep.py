@@ -79,7 +79,7 @@ class SeperateConvFn(torch.autograd.Function):
             npx = NL * H * W
             L.call('ewvit_hfsep_bwd_weight', L.ptr(xc), L.ptr(dyc), NL, H, W, *[L.ptr(t) for t in outs], L.ptr(ws),
                    L.stream(dyc), work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
-        return (None, None, None) + tuple(outs)
+        return (None, None, None) + tuple(grads.give(p, g, ctx.gen) for p, g in zip(ctx.params, outs))
 
 
 def seperate_conv(x, levels, convs, shift=None):
@@ -184,7 +184,7 @@ class SeperateBNReLUFn(torch.autograd.Function):
             L.call('ewvit_hfsep_bn_bwd_weight', L.ptr(xc), L.ptr(y), L.ptr(dzc), levels, N, H, W, L.ptr(mean),
                    L.ptr(invstd), L.ptr(gamma), L.ptr(beta), L.ptr(part), nrc, *[L.ptr(t) for t in outs],
                    L.ptr(dg), L.ptr(db), L.ptr(ws), L.stream(dzc), work=work)
-        return (None, None, None) + tuple(outs) + (dg, db)
+        return (None, None, None) + tuple(grads.give(p, g, ctx.gen) for p, g in zip(ctx.params, outs)) + (dg, db)
 
 
 def seperate_conv_bn_relu(x, levels, convs, cat, momentum, eps):

@@ -12,6 +12,7 @@ import torch
 
 from . import _lib as L
 from . import bn as _bn
+from . import grads
 from .grads import grad_out, note_use
 
 F32, BF16 = L.F32, L.BF16
@@ -261,6 +262,8 @@ def _linear_backward(ctx, dy, _daux, _dxa):
             db = torch.empty(db.shape[0], dtype=torch.float32, device=dy.device)
     dx = torch.ops.ewvit.linear_backward(dy, x, weight, aux, xa, act, drop_p, seed, bool(need[0]), fp8, dw, db)
     dres = dy if has_res and need[6] else None
+    dw = grads.give(ctx.params[0], dw, ctx.gen)
+    db = grads.give(ctx.params[1], db, ctx.gen)
     return (dx if need[0] else None), dw, db, None, None, None, dres, None, None, None
 
 
@@ -333,6 +336,9 @@ def _ln_setup(ctx, inputs, output):
     ctx.mark_non_differentiable(mean, rstd)
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(x, weight, mean, rstd)
+    ctx.gen = note_use(inputs[1])
+    note_use(inputs[2])
+    ctx.params = (inputs[1], inputs[2])
 
 
 def _ln_backward(ctx, dy, _dm, _dr):
@@ -340,7 +346,7 @@ def _ln_backward(ctx, dy, _dm, _dr):
         return (None,) * 5
     x, weight, mean, rstd = ctx.saved_tensors
     dx, dg, db = torch.ops.ewvit.layer_norm_backward(dy, x, weight, mean, rstd)
-    return dx, dg, db, None, None
+    return dx, grads.give(ctx.params[0], dg, ctx.gen), grads.give(ctx.params[1], db, ctx.gen), None, None
 
 
 _layer_norm_op.register_autograd(_ln_backward, setup_context=_ln_setup)
@@ -607,6 +613,8 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         ctx.save_for_backward(xc, w)
         ctx.cfg = (stride, pad, weight.dtype)
         ctx.wstride = weight.stride()
+        ctx.gen = note_use(weight)
+        ctx.params = (weight,)
         # the backward statistics of the BatchNorm that produced x, summed by the input gradient:
         # ewvit_dwconv3x3_bwd_data_bn leaves whole-map sums with no row scale, so only the link
         # of a one-group BatchNorm without a drop-path scale
@@ -642,17 +650,22 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             wsb = L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, stride, pad)
             ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            dw = torch.empty(C, 1, 3, 3, dtype=torch.float32, device=xc.device)
+            # the gradient slot itself when its layout is the kernel's [C][9] (ewvit.grads)
+            out = grad_out(ctx.params[0], ctx.gen) if wdt == torch.float32 else None
+            direct = out is not None and tuple(out.shape) == (C, 1, 3, 3) and all(
+                a == b for a, b, n in zip(out.stride(), (9, 9, 3, 1), out.shape) if n != 1)
+            dw = out if direct else torch.empty(C, 1, 3, 3, dtype=torch.float32, device=xc.device)
             L.call('ewvit_dwconv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dw), 0, N, H, W, C, stride, pad,
                    L.dt(xc), L.ptr(ws), L.stream(dw),
                    work={'bytes': (dyc.numel() + xc.numel()) * xc.element_size()})
             if wdt != torch.float32:
                 dw = dw.to(wdt)
-            if dw.stride() != ctx.wstride:          # keep the parameter's layout (DDP bucket views)
+            if not direct and dw.stride() != ctx.wstride:    # keep the parameter's layout (DDP bucket views)
                 if all(a == b for a, b, n in zip(dw.stride(), ctx.wstride, dw.shape) if n != 1):
                     dw = dw.as_strided(dw.shape, ctx.wstride)      # same memory, size-1 dims differ only
                 else:
                     dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
+            dw = grads.give(ctx.params[0], dw, ctx.gen)
         return dx, dw, None, None, None
 
 

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib as L
+from . import grads
 
 # the depthwise BatchNorm's apply pass and the SE squeeze as one kernel when the statistics come
 # from the depthwise conv (ewvit_bn_act_se_squeeze; 0: separate passes, A/B)
@@ -56,6 +57,40 @@ def _grad_like(g, p):
     return torch.empty_like(p, dtype=g.dtype).copy_(g)
 
 
+def _dense(o):
+    """True when tensor o's layout is row-major over its non-size-1 dims."""
+    exp, st = [], 1
+    for n in reversed(o.shape):
+        exp.append(st)
+        st *= n
+    return all(a == b for a, b, n in zip(o.stride(), reversed(exp), o.shape) if n != 1)
+
+
+def _mat_out(p, gen, r, c, dev):
+    """([r, c] fp32 matrix the kernel writes, the parameter-shaped gradient it is or None): the
+    parameter's gradient slot (ewvit.grads) when its layout is [r][c] row-major."""
+    o = grads.grad_out(p, gen)
+    if o.dtype == torch.float32 and _dense(o):
+        return o.as_strided((r, c), (c, 1)), o
+    return torch.empty(r, c, dtype=torch.float32, device=dev), None
+
+
+def _vec_out(p, gen, n, dev):
+    if p is None:
+        return None
+    o = grads.grad_out(p, gen)
+    return o if o.dim() == 1 and o.is_contiguous() and o.dtype == torch.float32 else torch.empty(
+        n, dtype=torch.float32, device=dev)
+
+
+def _track(ctx, *params):
+    """Count the uses of the op's parameters (ewvit.grads) and keep them for the backward."""
+    ctx.gen = grads.note_use(None)
+    for p in params:
+        grads.note_use(p)
+    ctx.params = params
+
+
 class SqueezeExciteFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
@@ -76,6 +111,7 @@ class SqueezeExciteFn(torch.autograd.Function):
                work={'bytes': 3 * xc.numel() * xc.element_size()})
         ctx.save_for_backward(xc, w1, w2, s0, h1, s)
         ctx.has_b = (b1 is not None, b2 is not None)
+        _track(ctx, w1, b1, w2, b2)
         return y
 
     @staticmethod
@@ -87,10 +123,11 @@ class SqueezeExciteFn(torch.autograd.Function):
         dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
         W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
         g = torch.empty(N, C, dtype=torch.float32, device=dev)
-        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
-        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
-        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if ctx.has_b[0] else None
-        db2 = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b[1] else None
+        pw1, pb1, pw2, pb2 = ctx.params
+        dW1, o1 = _mat_out(pw1, ctx.gen, Csq, C, dev)
+        dW2, o2 = _mat_out(pw2, ctx.gen, C, Csq, dev)
+        db1 = _vec_out(pb1, ctx.gen, Csq, dev)
+        db2 = _vec_out(pb2, ctx.gen, C, dev)
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         # ds = sum_hw dy * x inside the backward MLP's first kernel
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(s), L.ptr(h1), L.ptr(s0),
@@ -99,7 +136,15 @@ class SqueezeExciteFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
                work={'bytes': 2 * xc.numel() * xc.element_size()})
-        return dx, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2
+        return dx, *_give_se(ctx, dW1, o1, db1, dW2, o2, db2)
+
+
+def _give_se(ctx, dW1, o1, db1, dW2, o2, db2):
+    """The SE parameters' gradients as autograd receives them (ewvit.grads.give)."""
+    pw1, pb1, pw2, pb2 = ctx.params[-4:]
+    g = ctx.gen
+    return (grads.give(pw1, o1 if o1 is not None else _grad_like(dW1, pw1), g), grads.give(pb1, db1, g),
+            grads.give(pw2, o2 if o2 is not None else _grad_like(dW2, pw2), g), grads.give(pb2, db2, g))
 
 
 class BnActSEFn(torch.autograd.Function):
@@ -139,6 +184,7 @@ class BnActSEFn(torch.autograd.Function):
                    work={'bytes': 2 * x2.numel() * x2.element_size()})
             ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
             ctx.cfg = (act, b1 is not None, b2 is not None)
+            _track(ctx, gamma, beta, w1, b1, w2, b2)
             return y
         if partials is not None:
             # statistics summed by the depthwise conv that produced x: the apply pass only
@@ -159,6 +205,7 @@ class BnActSEFn(torch.autograd.Function):
                work={'bytes': 3 * x2.numel() * x2.element_size()})
         ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
         ctx.cfg = (act, b1 is not None, b2 is not None)
+        _track(ctx, gamma, beta, w1, b1, w2, b2)
         return y
 
     @staticmethod
@@ -171,100 +218,14 @@ class BnActSEFn(torch.autograd.Function):
         dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
         W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
         g = torch.empty(N, C, dtype=torch.float32, device=dev)
-        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
-        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
-        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if has_b1 else None
-        db2 = torch.empty(C, dtype=torch.float32, device=dev) if has_b2 else None
+        pg, pb, pw1, pb1, pw2, pb2 = ctx.params
+        dW1, o1 = _mat_out(pw1, ctx.gen, Csq, C, dev)
+        dW2, o2 = _mat_out(pw2, ctx.gen, C, Csq, dev)
+        db1 = _vec_out(pb1, ctx.gen, Csq, dev)
+        db2 = _vec_out(pb2, ctx.gen, C, dev)
         dx = torch.empty_like(xc)
-        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
-        mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-        # ds = sum_hw dy * x inside the backward MLP's first kernel
-        L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(xc), L.dt(xc), N, HW, C, L.ptr(s), L.ptr(h1), L.ptr(s0),
-               L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
-               L.stream(g), work={'bytes': 2 * xc.numel() * xc.element_size()})
-        dx = torch.empty_like(xc)
-        L.call('ewvit_se_scale', L.ptr(dyc), L.dt(xc), L.ptr(s), L.ptr(g), L.ptr(dx), N, HW, C, L.stream(dx),
-               work={'bytes': 2 * xc.numel() * xc.element_size()})
-        return dx, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2
-
-
-class BnActSEFn(torch.autograd.Function):
-    """SE(act(BatchNorm(x))) in training mode — MBConv's depthwise BN + SiLU followed by its
-    squeeze-excitation.  Forward: the BatchNorm statistics + apply passes, then the SE's squeeze
-    MLP and excite pass (the same kernels as batch_norm_act + squeeze_excite).  Backward: the SE
-    MLP backward gives the squeeze term g, and the BatchNorm backward forms its output gradient
-    dy*s + g itself (ewvit_bn_bwd_se) — the SE input-gradient pass and its tensor never exist."""
-
-    @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2,
-                partials=None):
-        L.require_gpu(x)
-        xc, N, HW, C = _rows(x)
-        M = N * HW
-        dev = x.device
-        x2 = torch.empty_like(xc)
-        mean = torch.empty(1, C, dtype=torch.float32, device=dev)
-        invstd = torch.empty_like(mean)
-        Csq = w1.shape[0]
-        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
-        s0 = torch.empty(N, C, dtype=torch.float32, device=dev)
-        h1 = torch.empty(N, Csq, dtype=torch.float32, device=dev)
-        sc = torch.empty(N, C, dtype=torch.float32, device=dev)
-        fws = torch.empty(L.load().ewvit_se_mlp_fwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
-        y = torch.empty_like(x2)
-        if partials is not None and _BN_SQUEEZE and N <= 65535:
-            # BatchNorm apply + SiLU + the SE squeeze (+ the MLP's first-layer partials) in one
-            # pass, then the gates + excite: 2 launches for the BN and the SE forward
-            part, shifts, nrc = partials
-            L.call('ewvit_bn_act_se_squeeze', L.ptr(xc), L.ptr(x2), L.dt(xc), N, HW, C, L.ptr(gamma), L.ptr(beta),
-                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
-                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), L.ptr(W1), Csq, L.ptr(s0),
-                   L.ptr(fws), L.stream(x2), work={'bytes': 2 * xc.numel() * xc.element_size()})
-            L.call('ewvit_se_gate_excite', L.ptr(fws), L.ptr(_vec(b1)), L.ptr(W2), L.ptr(_vec(b2)), L.ptr(x2),
-                   L.dt(x2), N, HW, C, Csq, L.ptr(h1), L.ptr(sc), L.ptr(y), L.stream(y),
-                   work={'bytes': 2 * x2.numel() * x2.element_size()})
-            ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
-            ctx.cfg = (act, b1 is not None, b2 is not None)
-            return y
-        if partials is not None:
-            # statistics summed by the depthwise conv that produced x: the apply pass only
-            part, shifts, nrc = partials
-            L.call('ewvit_bn_fwd_partials', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
-                   L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), act, L.ptr(mean),
-                   L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts), int(nrc), 1, L.stream(x2),
-                   work={'bytes': 2 * xc.numel() * xc.element_size()})
-        else:
-            ws = torch.empty(L.load().ewvit_bn_workspace(M, C, 1) // 4, dtype=torch.float32, device=dev)
-            L.call('ewvit_bn_fwd', L.ptr(xc), L.ptr(x2), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
-                   L.ptr(running_mean), L.ptr(running_var), 1, float(momentum), float(eps), act, L.ptr(mean),
-                   L.ptr(invstd), 1, L.ptr(counter), L.ptr(ws), L.stream(x2),
-                   work={'bytes': 3 * xc.numel() * xc.element_size()})
-        # squeeze + MLP hidden partials, then the gates and the excite pass in one launch
-        L.call('ewvit_se_forward', L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(W1), L.ptr(_vec(b1)), L.ptr(W2),
-               L.ptr(_vec(b2)), Csq, L.ptr(s0), L.ptr(h1), L.ptr(sc), L.ptr(y), L.ptr(fws), L.stream(y),
-               work={'bytes': 3 * x2.numel() * x2.element_size()})
-        ctx.save_for_backward(xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc)
-        ctx.cfg = (act, b1 is not None, b2 is not None)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        xc, gamma, beta, mean, invstd, x2, w1, w2, s0, h1, sc = ctx.saved_tensors
-        act, has_b1, has_b2 = ctx.cfg
-        N, C, H, W = xc.shape
-        HW, M, Csq = H * W, N * H * W, w1.shape[0]
-        dev = xc.device
-        dyc = dy.to(xc.dtype).contiguous(memory_format=torch.channels_last)
-        W1, W2 = _mat(w1, Csq, C), _mat(w2, C, Csq)
-        g = torch.empty(N, C, dtype=torch.float32, device=dev)
-        dW1 = torch.empty(Csq, C, dtype=torch.float32, device=dev)
-        dW2 = torch.empty(C, Csq, dtype=torch.float32, device=dev)
-        db1 = torch.empty(Csq, dtype=torch.float32, device=dev) if has_b1 else None
-        db2 = torch.empty(C, dtype=torch.float32, device=dev) if has_b2 else None
-        dx = torch.empty_like(xc)
-        dg = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=dev) if beta is not None else None
+        dg = _vec_out(pg, ctx.gen, C, dev)
+        db = _vec_out(pb, ctx.gen, C, dev)
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
                L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
@@ -273,8 +234,8 @@ class BnActSEFn(torch.autograd.Function):
         L.call('ewvit_bn_bwd_se', L.ptr(dyc), L.ptr(xc), L.ptr(dx), L.dt(xc), M, C, L.ptr(gamma), L.ptr(beta),
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW, L.ptr(ws),
                L.stream(dx), work={'bytes': 5 * xc.numel() * xc.element_size()})
-        return (dx, dg, db, None, None, None, None, None, None, _grad_like(dW1, w1), db1, _grad_like(dW2, w2), db2,
-                None)
+        return (dx, grads.give(pg, dg, ctx.gen), grads.give(pb, db, ctx.gen), None, None, None, None, None, None,
+                *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None)
 
 
 def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2, partials=None):

@@ -125,7 +125,8 @@ class ViTLayerFn(torch.autograd.Function):
         L.call('ewvit_vit_layer_bwd', ctypes.addressof(p), R, L.ptr(x0c), L.ptr(saved), L.ptr(gc), L.ptr(scratch),
                L.ptr(dx0), ctypes.addressof(G), L.stream(dx0),
                work={'flops': 4.0 * R * 512 * (1536 + 512 + 2 * 2048), 'bytes': 8.0 * sum(t.numel() for t in ts)})
-        return (None, dx0.reshape(g.shape), *[o if ctx.needs_input_grad[2 + k] else None for k, o in enumerate(outs)])
+        return (None, dx0.reshape(g.shape), *[grads.give(t, o, ctx.gen) if ctx.needs_input_grad[2 + k] else None
+                                              for k, (t, o) in enumerate(zip(ts, outs))])
 
 
 def vit_layer(attn, ff, x, training, packed, idx):
@@ -168,8 +169,8 @@ class EmbedFn(torch.autograd.Function):
         off = L.rng_offset(g.device) if drop_p > 0 else None
         L.call('ewvit_vit_embed_bwd', L.ptr(gc), B, pos.shape[0], drop_p, seed, L.ptr(off), L.ptr(dy), L.ptr(dcls),
                L.ptr(dpos), L.stream(dy))
-        return (None, None, dy.reshape(yshape), dcls if ctx.needs_input_grad[3] else None,
-                dpos if ctx.needs_input_grad[4] else None)
+        return (None, None, dy.reshape(yshape), grads.give(cls, dcls, ctx.gen) if ctx.needs_input_grad[3] else None,
+                grads.give(pos, dpos, ctx.gen) if ctx.needs_input_grad[4] else None)
 
 
 def embed(y, cls, pos, drop_p):
