@@ -14,7 +14,9 @@ import bench  # noqa: E402
 
 def main():
     dev = torch.device('cuda', 0)
-    step = bench.build_step(dev, 64, 0, graph=False)
+    config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    frames = bench.CONFIGS[config]['frames'] if 'frames' in bench.CONFIGS[config] else 64
+    step = bench.build_step(dev, frames, 0, graph=False, config=config)
     for _ in range(2):
         step()
     torch.cuda.synchronize()
