@@ -107,7 +107,7 @@ def give(param, g, gen):
     """What an op's backward returns to autograd for `param`'s gradient `g`: `g` itself, or —
     for a parameter used more than once in step `gen` — None, with `g` kept for the sum at the
     end of the backward pass."""
-    if g is None or param is None or not DEFER or not multi_use(param, gen):
+    if g is None or param is None or not DEFER or not param.requires_grad or not multi_use(param, gen):
         return g
     with _lock:
         ent = _pending.setdefault(gen, {}).setdefault(id(param), [param, [], set()])

@@ -88,3 +88,12 @@ def test_multi_use_counts_reset_per_step():
     grads.begin_step()
     g2 = grads.note_use(w)
     assert grads.single_use(w, g2) and not grads.multi_use(w, g2)
+
+
+def test_frozen_parameter_gets_no_gradient():
+    """A parameter that does not require grad, used twice, is never given a .grad."""
+    w = torch.nn.Parameter(torch.randn(4), requires_grad=False)
+    x = torch.randn(3, 4, requires_grad=True)
+    grads.begin_step()
+    (_Scale.apply(x, w).sum() + _Scale.apply(x, w).sum()).backward()
+    assert w.grad is None and x.grad is not None
