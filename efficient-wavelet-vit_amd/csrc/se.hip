@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void scale_add_drop_kernel(const void *__restr
 //   F1 se_mlp_h1_part  grid (N, C/64):  part[n][cb][j] = sum_{c in cb} W1[j][c] s0[n][c]
 //   F2 se_mlp_gate     grid (N, C/256): h1 = b1 + sum_cb part; s = sigmoid(W2 silu(h1) + b2)
 //   B1 se_mlp_dh_part  grid (N, C/64):  dz2 = ds s(1-s); part[n][cb][j] = sum_c W2[c][j] dz2
-//   B2 se_mlp_g        grid (N, C/256): dz1 = (sum_cb part) silu'(h1); g = W1^T dz1 / HW
+//   B2 se_mlp_g        grid (N, C/64):  dz1 = (sum_cb part) silu'(h1); g = W1^T dz1 / HW
 //   B3 se_mlp_wgrad    one thread per dW1 / dW2 / db element, sums over n
 constexpr int SE_CB = 64;
 
@@ -417,12 +417,15 @@ __global__ __launch_bounds__(256) void se_mlp_dh_part_kernel(const float *__rest
   }
 }
 
+// block (n, 64-channel chunk): dz1 for the frame (every block of the frame forms it), then
+// g[c] = sum_j W1[j][c] dz1[j] / HW with the 4 waves on quarters of j, combined in order
 __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__ part, int nb,
                                                        const float *__restrict__ h1,
                                                        const float *__restrict__ w1, int C, int Csq, float inv_hw,
                                                        float *__restrict__ dz1_out, float *__restrict__ g_out) {
   extern __shared__ float dz1[];
-  const int n = blockIdx.x, tid = threadIdx.x;
+  __shared__ float red[4][64];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float *pp = part + (int64_t)n * nb * Csq;
   for (int j = tid; j < Csq; j += 256) {
     const float dh = se_part_sum(pp, nb, Csq, j);
@@ -433,21 +436,26 @@ __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__
     if (blockIdx.y == 0) dz1_out[(int64_t)n * Csq + j] = d;
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + tid;
-  if (c >= C) return;
+  const int c = blockIdx.y * 64 + lane;
+  const int q = (Csq + 3) >> 2, ja = w * q, jb = ja + q < Csq ? ja + q : Csq;
   float acc0 = 0.f, acc1 = 0.f;
-  for (int j0 = 0; j0 < Csq; j0 += 16) {
-    float v[16];
+  if (c < C) {
+    int j = ja;
+    for (; j + 8 <= jb; j += 8) {
+      float v[8];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = j0 + q < Csq ? w1[(int64_t)(j0 + q) * C + c] : 0.f;
+      for (int u = 0; u < 8; ++u) v[u] = w1[(int64_t)(j + u) * C + c];
 #pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      if (j0 + q < Csq) acc0 = fmaf(v[q], dz1[j0 + q], acc0);
-      if (j0 + q + 1 < Csq) acc1 = fmaf(v[q + 1], dz1[j0 + q + 1], acc1);
+      for (int u = 0; u < 8; u += 2) {
+        acc0 = fmaf(v[u], dz1[j + u], acc0);
+        acc1 = fmaf(v[u + 1], dz1[j + u + 1], acc1);
+      }
     }
+    for (; j < jb; ++j) acc0 = fmaf(w1[(int64_t)j * C + c], dz1[j], acc0);
   }
-  const float gq = (acc0 + acc1) * inv_hw;
-  g_out[(int64_t)n * C + c] = gq;
+  red[w][lane] = acc0 + acc1;
+  __syncthreads();
+  if (w == 0 && c < C) g_out[(int64_t)n * C + c] = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) * inv_hw;
 }
 
 // dW2[c][j] = sum_n dz2[n][c] silu(h1[n][j]),  db2[c] = sum_n dz2[n][c]
@@ -741,7 +749,7 @@ extern "C" int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1
   float *dz2 = workspace, *dz1 = workspace + N * C, *part = dz1 + N * Csq;
   hipLaunchKernelGGL(se_mlp_dh_part_kernel, dim3((unsigned)N, (unsigned)nb), dim3(256), 0, st, ds, s, w2, (int)C,
                      (int)Csq, dz2, part);
-  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, inv_hw, dz1, g);
   const int64_t tot = 2 * C * Csq + C + Csq;
   hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
@@ -835,7 +843,7 @@ extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype
   else
     hipLaunchKernelGGL(se_sq_dh_part_kernel<EWVIT_F32>, g1, dim3(256), 0, st, dy, x, (int)HW, s, w2, (int)C,
                        (int)Csq, dz2, part);
-  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, 1.f / (float)HW, dz1, g);
   const int64_t tot = 2 * C * Csq + C + Csq;
   hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
