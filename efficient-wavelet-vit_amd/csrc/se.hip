@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void scale_add_drop_kernel(const void *__restr
 // spreads a frame over many blocks and issues all of a thread's loads back to back.
 // Reductions over c go through fixed-order partial slabs (deterministic).
 //   F1 se_mlp_h1_part  grid (N, C/64):  part[n][cb][j] = sum_{c in cb} W1[j][c] s0[n][c]
-//   F2 se_mlp_gate     grid (N, C/256): h1 = b1 + sum_cb part; s = sigmoid(W2 silu(h1) + b2)
+//   F2 se_mlp_gate     grid (N, C/64):  h1 = b1 + sum_cb part; s = sigmoid(W2 silu(h1) + b2)
 //   B1 se_mlp_dh_part  grid (N, C/64):  dz2 = ds s(1-s); part[n][cb][j] = sum_c W2[c][j] dz2
 //   B2 se_mlp_g        grid (N, C/64):  dz1 = (sum_cb part) silu'(h1); g = W1^T dz1 / HW
 //   B3 se_mlp_wgrad    one thread per dW1 / dW2 / db element, sums over n
@@ -263,40 +263,32 @@ __device__ __forceinline__ float se_part_sum(const float *__restrict__ pp, int n
   return acc;
 }
 
-// a thread's dot of a contiguous fp32 row with the LDS vector a (16-B loads when the
-// rows are 16-B aligned, Csq % 4 == 0)
-__device__ __forceinline__ float se_row_dot(const float *__restrict__ row, const float *a, int Csq) {
+// the pre-activations of a block's 64 gates: z[c] = b2[c] + sum_j W2[c][j] a[j] (a in LDS), lane
+// = channel, the 4 waves on quarters of j, the quarters combined in a fixed order through red —
+// every thread of the block returns its lane's z (one barrier inside)
+__device__ __forceinline__ float se_gate64(const float *__restrict__ w2, const float *__restrict__ b2,
+                                          const float *a, int C, int Csq, int c, float (*red)[64]) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = (Csq + 3) >> 2, ja = w * q, jb = ja + q < Csq ? ja + q : Csq;
   float acc0 = 0.f, acc1 = 0.f;
-  if (Csq & 3) {
-    for (int j0 = 0; j0 < Csq; j0 += 8) {
+  if (c < C) {
+    const float *row = w2 + (int64_t)c * Csq;
+    int j = ja;
+    for (; j + 8 <= jb; j += 8) {
       float v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = j0 + q < Csq ? row[j0 + q] : 0.f;
+      for (int u = 0; u < 8; ++u) v[u] = row[j + u];
 #pragma unroll
-      for (int q = 0; q < 8; q += 2) {
-        if (j0 + q < Csq) acc0 = fmaf(v[q], a[j0 + q], acc0);
-        if (j0 + q + 1 < Csq) acc1 = fmaf(v[q + 1], a[j0 + q + 1], acc1);
+      for (int u = 0; u < 8; u += 2) {
+        acc0 = fmaf(v[u], a[j + u], acc0);
+        acc1 = fmaf(v[u + 1], a[j + u + 1], acc1);
       }
     }
-    return acc0 + acc1;
+    for (; j < jb; ++j) acc0 = fmaf(row[j], a[j], acc0);
   }
-  for (int j0 = 0; j0 < Csq; j0 += 32) {
-    float4 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      v[q] = j0 + 4 * q < Csq ? *reinterpret_cast<const float4 *>(row + j0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int j = j0 + 4 * q;
-      if (j < Csq) {
-        acc0 = fmaf(v[q].x, a[j], acc0);
-        acc1 = fmaf(v[q].y, a[j + 1], acc1);
-        acc0 = fmaf(v[q].z, a[j + 2], acc0);
-        acc1 = fmaf(v[q].w, a[j + 3], acc1);
-      }
-    }
-  }
-  return acc0 + acc1;
+  red[w][lane] = acc0 + acc1;
+  __syncthreads();
+  return ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) + (b2 && c < C ? b2[c] : 0.f);
 }
 
 __global__ __launch_bounds__(256) void se_mlp_gate_kernel(const float *__restrict__ part, int nb,
@@ -305,6 +297,7 @@ __global__ __launch_bounds__(256) void se_mlp_gate_kernel(const float *__restric
                                                           const float *__restrict__ b2, int C, int Csq,
                                                           float *__restrict__ h1_out, float *__restrict__ s_out) {
   extern __shared__ float a1[];
+  __shared__ float red[4][64];
   const int n = blockIdx.x, tid = threadIdx.x;
   const float *pp = part + (int64_t)n * nb * Csq;
   for (int j = tid; j < Csq; j += 256) {
@@ -313,16 +306,15 @@ __global__ __launch_bounds__(256) void se_mlp_gate_kernel(const float *__restric
     if (blockIdx.y == 0) h1_out[(int64_t)n * Csq + j] = h;
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + tid;
-  if (c >= C) return;
-  const float z = se_row_dot(w2 + (int64_t)c * Csq, a1, Csq) + (b2 ? b2[c] : 0.f);
-  s_out[(int64_t)n * C + c] = sigmoid_f(z);
+  const int c = blockIdx.y * 64 + (tid & 63);
+  const float z = se_gate64(w2, b2, a1, C, Csq, c, red);
+  if (tid < 64 && c < C) s_out[(int64_t)n * C + c] = sigmoid_f(z);
 }
 
-// F2 + the excite pass in one launch: block (n, 256-channel chunk) forms the frame's hidden
+// F2 + the excite pass in one launch: block (n, 64-channel chunk) forms the frame's hidden
 // vector and its chunk's gates exactly as se_mlp_gate_kernel does, then scales the chunk's
-// HW rows of x (y = x * s, as se_scale_kernel) — 32 channel vectors x 8 row groups, the first
-// 4 rows of every thread loaded before the gate is known (they do not depend on it)
+// HW rows of x (y = x * s, as se_scale_kernel) — 8 channel vectors x 32 row groups, the first
+// 2 rows of every thread loaded before the gate is known (they do not depend on it)
 template <int DT>
 __global__ __launch_bounds__(256) void se_gate_scale_kernel(const float *__restrict__ part, int nb,
                                                             const float *__restrict__ b1,
@@ -331,17 +323,18 @@ __global__ __launch_bounds__(256) void se_gate_scale_kernel(const float *__restr
                                                             float *__restrict__ h1_out, float *__restrict__ s_out,
                                                             const void *__restrict__ x, void *__restrict__ y, int HW) {
   extern __shared__ float gsm[];
+  __shared__ float red[4][64];
   float *a1 = gsm, *sv = gsm + ((Csq + 3) & ~3);
   const int n = blockIdx.x, tid = threadIdx.x;
-  const int cv = tid & 31, rg = tid >> 5;
-  const int c0 = blockIdx.y * 256 + cv * 8;
+  const int cv = tid & 7, rg = tid >> 3;             // 8 channel vectors x 32 row groups
+  const int c0 = blockIdx.y * 64 + cv * 8;
   const bool active = c0 < C;
   const int64_t base = (int64_t)n * HW * C + c0;
-  constexpr int PF = 4;
+  constexpr int PF = 2, RS = 32;
   float pre[PF][8];
 #pragma unroll
   for (int q = 0; q < PF; ++q) {
-    const int r = rg + 8 * q;
+    const int r = rg + RS * q;
     if (active && r < HW) se_ld8<DT>(x, base + (int64_t)r * C, pre[q]);
   }
   const float *pp = part + (int64_t)n * nb * Csq;
@@ -351,11 +344,11 @@ __global__ __launch_bounds__(256) void se_gate_scale_kernel(const float *__restr
     if (blockIdx.y == 0) h1_out[(int64_t)n * Csq + j] = h;
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + tid;
-  if (c < C) {
-    const float z = se_row_dot(w2 + (int64_t)c * Csq, a1, Csq) + (b2 ? b2[c] : 0.f);
+  const int c = blockIdx.y * 64 + (tid & 63);
+  const float z = se_gate64(w2, b2, a1, C, Csq, c, red);
+  if (tid < 64) {
     const float sg = sigmoid_f(z);
-    s_out[(int64_t)n * C + c] = sg;
+    if (c < C) s_out[(int64_t)n * C + c] = sg;
     sv[tid] = sg;
   }
   __syncthreads();
@@ -365,24 +358,24 @@ __global__ __launch_bounds__(256) void se_gate_scale_kernel(const float *__restr
   for (int j = 0; j < 8; ++j) sc[j] = sv[cv * 8 + j];
 #pragma unroll
   for (int q = 0; q < PF; ++q) {
-    const int r = rg + 8 * q;
+    const int r = rg + RS * q;
     if (r < HW) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) pre[q][j] = fmaf(pre[q][j], sc[j], 0.f);
       se_st8<DT>(y, base + (int64_t)r * C, pre[q]);
     }
   }
-  for (int r0 = rg + 8 * PF; r0 < HW; r0 += 8 * PF) {
+  for (int r0 = rg + RS * PF; r0 < HW; r0 += RS * PF) {
     float v[PF][8];
 #pragma unroll
     for (int q = 0; q < PF; ++q)
-      if (r0 + 8 * q < HW) se_ld8<DT>(x, base + (int64_t)(r0 + 8 * q) * C, v[q]);
+      if (r0 + RS * q < HW) se_ld8<DT>(x, base + (int64_t)(r0 + RS * q) * C, v[q]);
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
-      if (r0 + 8 * q < HW) {
+      if (r0 + RS * q < HW) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[q][j] = fmaf(v[q][j], sc[j], 0.f);
-        se_st8<DT>(y, base + (int64_t)(r0 + 8 * q) * C, v[q]);
+        se_st8<DT>(y, base + (int64_t)(r0 + RS * q) * C, v[q]);
       }
     }
   }
@@ -730,7 +723,7 @@ extern "C" int ewvit_se_mlp_fwd(const float *s0, const float *w1, const float *b
   const int nb = se_nb(C);
   hipLaunchKernelGGL(se_mlp_h1_part_kernel, dim3((unsigned)N, (unsigned)nb), dim3(256), 0, st, s0, w1, (int)C,
                      (int)Csq, workspace);
-  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, workspace, nb, b1, w2, b2, (int)C, (int)Csq, h1, s);
   return launch_status("se_mlp_fwd");
 }
@@ -774,7 +767,7 @@ extern "C" int ewvit_se_squeeze_mlp_fwd(const void *x, int dtype, int64_t N, int
   else
     hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_F32>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
                        (int)C, (int)Csq, s0, workspace);
-  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(se_mlp_gate_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, workspace, nb, b1, w2, b2, (int)C, (int)Csq, h1, s);
   return launch_status("se_squeeze_mlp_fwd");
 }
@@ -790,7 +783,7 @@ extern "C" int ewvit_se_forward(const void *x, int dtype, int64_t N, int64_t HW,
   hipStream_t st = as_stream(stream);
   const int nb = se_nb(C);
   const dim3 g1((unsigned)N, (unsigned)nb);
-  const dim3 g2((unsigned)N, (unsigned)((C + 255) / 256));
+  const dim3 g2((unsigned)N, (unsigned)((C + 63) / 64));
   const size_t lds = (size_t)(((Csq + 3) & ~3) + 256) * sizeof(float);
   if (dtype == EWVIT_BF16) {
     hipLaunchKernelGGL(se_sq_h1_part_kernel<EWVIT_BF16>, g1, dim3(256), 0, st, x, (int)HW, 1.f / (float)HW, w1,
@@ -814,7 +807,7 @@ extern "C" int ewvit_se_gate_excite(const float *part, const float *b1, const fl
   if (int rc = se_check(dtype, N, HW, C, "se_gate_excite")) return rc;
   if (int rc = se_mlp_check(N, C, Csq, "se_gate_excite")) return rc;
   EWVIT_CHECK_ARG(part && w2 && h1 && s && x && y && HW < (1 << 30), "se_gate_excite: bad args");
-  const dim3 g2((unsigned)N, (unsigned)((C + 255) / 256));
+  const dim3 g2((unsigned)N, (unsigned)((C + 63) / 64));
   const size_t lds = (size_t)(((Csq + 3) & ~3) + 256) * sizeof(float);
   if (dtype == EWVIT_BF16)
     hipLaunchKernelGGL(se_gate_scale_kernel<EWVIT_BF16>, g2, dim3(256), lds, as_stream(stream), part, se_nb(C), b1, w2,
