@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void scale_add_drop_kernel(const void *__restr
 //   F2 se_mlp_gate     grid (N, C/64):  h1 = b1 + sum_cb part; s = sigmoid(W2 silu(h1) + b2)
 //   B1 se_mlp_dh_part  grid (N, C/64):  dz2 = ds s(1-s); part[n][cb][j] = sum_c W2[c][j] dz2
 //   B2 se_mlp_g        grid (N, C/64):  dz1 = (sum_cb part) silu'(h1); g = W1^T dz1 / HW
-//   B3 se_mlp_wgrad    one thread per dW1 / dW2 / db element, sums over n
+//   B3 se_mlp_wgrad    64 dW1 / dW2 / db elements per block, the 4 waves on quarters of n
 constexpr int SE_CB = 64;
 
 // lanes = 64 consecutive channels of chunk cb, waves take outputs j = w, w+4, ...
@@ -453,18 +453,23 @@ __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__
 
 // dW2[c][j] = sum_n dz2[n][c] silu(h1[n][j]),  db2[c] = sum_n dz2[n][c]
 // dW1[j][c] = sum_n dz1[n][j] s0[n][c],        db1[j] = sum_n dz1[n][j]
+// block: 64 consecutive outputs (lanes) x 4 waves on quarters of the frames, the quarters
+// combined in a fixed order through LDS (deterministic); a thread's loads of its quarter are
+// issued 8 at a time
 __global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restrict__ dz2,
                                                            const float *__restrict__ dz1,
                                                            const float *__restrict__ h1,
                                                            const float *__restrict__ s0, int N, int C, int Csq,
                                                            float *__restrict__ dw1, float *__restrict__ db1,
                                                            float *__restrict__ dw2, float *__restrict__ db2) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t P = (int64_t)C * Csq;
-  const float *pa, *pb;
-  int64_t sa, sb;                 // strides over n of the two factors
+  const float *pa = nullptr, *pb = nullptr;
+  int64_t sa = 0, sb = 0;
   bool silu_b = false;
-  float *dst;
+  float *dst = nullptr;
   if (i < P) {                    // dW2[c][j], j fastest
     const int c = (int)(i / Csq), j = (int)(i % Csq);
     pa = dz2 + c; sa = C; pb = h1 + j; sb = Csq; silu_b = true; dst = dw2 + i;
@@ -474,31 +479,33 @@ __global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restri
     pa = dz1 + j; sa = Csq; pb = s0 + c; sb = C; dst = dw1 + k;
   } else if (i < 2 * P + C) {
     const int c = (int)(i - 2 * P);
-    pa = dz2 + c; sa = C; pb = nullptr; sb = 0; dst = db2 ? db2 + c : nullptr;
+    pa = dz2 + c; sa = C; dst = db2 ? db2 + c : nullptr;
   } else if (i < 2 * P + C + Csq) {
     const int j = (int)(i - 2 * P - C);
-    pa = dz1 + j; sa = Csq; pb = nullptr; sb = 0; dst = db1 ? db1 + j : nullptr;
-  } else {
-    return;
+    pa = dz1 + j; sa = Csq; dst = db1 ? db1 + j : nullptr;
   }
-  if (!dst) return;
+  const int q = (N + 3) >> 2, na = w * q, nb = na + q < N ? na + q : N;
   float acc0 = 0.f, acc1 = 0.f;
-  for (int n0 = 0; n0 < N; n0 += 16) {
-    float va[16], vb[16];
+  if (dst) {
+    for (int n0 = na; n0 < nb; n0 += 8) {
+      float va[8], vb[8];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const bool ok = n0 + q < N;
-      va[q] = ok ? pa[(int64_t)(n0 + q) * sa] : 0.f;
-      vb[q] = ok ? (pb ? pb[(int64_t)(n0 + q) * sb] : 1.f) : 0.f;
-    }
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = n0 + u < nb;
+        va[u] = ok ? pa[(int64_t)(n0 + u) * sa] : 0.f;
+        vb[u] = ok ? (pb ? pb[(int64_t)(n0 + u) * sb] : 1.f) : 0.f;
+      }
 #pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      const float b0 = silu_b ? silu_f(vb[q]) : vb[q], b1v = silu_b ? silu_f(vb[q + 1]) : vb[q + 1];
-      acc0 = fmaf(va[q], b0, acc0);
-      acc1 = fmaf(va[q + 1], b1v, acc1);
+      for (int u = 0; u < 8; u += 2) {
+        const float b0 = silu_b ? silu_f(vb[u]) : vb[u], b1v = silu_b ? silu_f(vb[u + 1]) : vb[u + 1];
+        acc0 = fmaf(va[u], b0, acc0);
+        acc1 = fmaf(va[u + 1], b1v, acc1);
+      }
     }
   }
-  *dst = acc0 + acc1;
+  red[w][lane] = acc0 + acc1;
+  __syncthreads();
+  if (w == 0 && dst) *dst = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // The squeeze folded into the MLP's first kernel: block (n, chunk) reduces its 64
@@ -745,7 +752,7 @@ extern "C" int ewvit_se_mlp_bwd(const float *ds, const float *s, const float *h1
   hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, inv_hw, dz1, g);
   const int64_t tot = 2 * C * Csq + C + Csq;
-  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
+  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, st, dz2, dz1, h1, s0,
                      (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
   return launch_status("se_mlp_bwd");
 }
@@ -839,7 +846,7 @@ extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype
   hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
                      (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, 1.f / (float)HW, dz1, g);
   const int64_t tot = 2 * C * Csq + C + Csq;
-  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dz2, dz1, h1, s0,
+  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, st, dz2, dz1, h1, s0,
                      (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
   return launch_status("se_squeeze_mlp_bwd");
 }
