@@ -28,64 +28,11 @@
 // (c / gc) * gs + p * gc + c % gc.  gc = C is plain NHWC; gc = 128, gs = B*H*W*128
 // is the MWT's level-major fusion output [L][B][H][W][128] read as the
 // [B][H][W][3*128] concatenation (mwt.py:112) without materialising it.
-#include "common.h"
+#include "conv_common.h"
 
 #include <cstdlib>
 
 namespace ewvit {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 cbf16x8;
-typedef __attribute__((ext_vector_type(4))) float cf32x4;
-typedef __attribute__((ext_vector_type(4))) short cs4;
-
-constexpr int CBM = 128, CBN = 128, CBK = 32;
-
-struct ConvGeom {
-  int N, H, W, Cin;      // x (fwd) / dx (dgrad) grid
-  int Ho, Wo, Cout;      // y / dy grid
-  int stride, ks, pad;   // ks 1|3, pad = ks/2
-};
-
-// ---------------------------------------------------------------- fwd / dgrad
-// A(m, k): m = pixel of the OUTPUT grid of this GEMM (y for fwd, dx for dgrad),
-// k = tap * KC + c (KC = Cin for fwd, Cout for dgrad).  B(k, n) = Wp[n][k].
-struct FwdArgs {
-  const bf16_t *src;     // gathered operand: x (fwd) or dy (dgrad), grouped NHWC
-  const bf16_t *wp;      // packed weights [Ncol][taps][KC]
-  const float *bias;     // [Ncol] or null
-  bf16_t *out;           // [M][Ncol], grouped NHWC
-  ConvGeom g;
-  int64_t M;
-  int Ncol, KC;          // GEMM N and per-tap K
-  int srcH, srcW;        // spatial size of `src`
-  int outH, outW;        // spatial size of the GEMM's output grid
-  int sgc, ogc;          // channel group widths of src / out
-  int64_t sgs, ogs;      // group strides (elements)
-  // optional BatchNorm statistics of the (bf16-rounded) output, LDS-DMA fwd only:
-  // per m-tile t and column c, bn_part[t][c] = sum (y - K[c]), bn_part[t][Ncol + c] =
-  // sum (y - K[c])^2 with K = bn_shift (or 0); tile 0 copies K to bn_shift_out
-  const float *bn_shift = nullptr;
-  float *bn_part = nullptr;
-  float *bn_shift_out = nullptr;
-  // LDS-DMA fwd over a plain NHWC x whose channel count is not a multiple of 64: KC is
-  // the per-tap K padded up to 64 (the weights packed with that many input channels)
-  // and the staging lanes of channels >= KCr (the real count) read zeros
-  int KCr = 0;
-  // optional addend of the output (same layout as out, bf16), added before rounding —
-  // the skip connection's gradient folded into the block input's dgrad
-  const bf16_t *addend = nullptr;
-  // stride-2 3x3 dgrad by output parity class (LDS-DMA kernel): the GEMM rows are the
-  // dx pixels (2i + py, 2j + px) of class pc = 2*py + px on an outH x outW grid, and
-  // only the class's ntap live taps tapl[] run (dy pixel (i + dh, j + dw)); the
-  // epilogue scatters row (n, i, j) to dx pixel (n, 2i + py, 2j + px) of dstH x dstW
-  int pc = -1, ntap = 0;
-  int tapl[4] = {0, 0, 0, 0};
-  int dstH = 0, dstW = 0;
-  // optional (LDS-DMA dgrad, plain NHWC dx, uncapped grid): the backward statistics of the
-  // BatchNorm(+act) whose output this conv read, summed over the bf16-rounded dx per m-tile
-  // (common.h BnBwdStats; bwd.part [m-tiles][2 Ncol])
-  BnBwdStats bwd;
-};
 
 template <bool DGRAD, int BN_, int KS, int BK, int PF>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
@@ -682,36 +629,6 @@ __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackArgs a) {
 // involution).  One K-tile is in flight while the previous one is multiplied; grid
 // order is remapped so that consecutive tiles (which share input halo rows and, for
 // wgrad, the same pixels) run on one XCD and meet in its L2.
-typedef __attribute__((address_space(3))) void lds_t;
-constexpr uint32_t OOB = 0x80000000u;   // any offset >= num_records reads as zero
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void *p, int64_t bytes) {
-  const uint32_t n = bytes >= (int64_t)OOB ? OOB : (uint32_t)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
-}
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, unsigned char *lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t *)lds, 16, voff, 0, 0, 0);
-}
-// bijective XCD remap: blocks b, b+8, b+16 ... (one XCD) get consecutive tile ids
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-// wait until at most the N youngest vector-memory ops (LDS-DMA pieces) are pending,
-// then the workgroup barrier; one asm statement, so hipcc neither drains the DMA
-// queue at the barrier nor moves LDS reads across it
-template <int N> __device__ __forceinline__ void wait_vm_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-// tile kt's pieces landed (L per tile per thread); `rem` younger tiles already issued
-// (at most NS-2 of them) may stay in flight across the barrier
-template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
-  if constexpr (NS >= 4) { if (rem >= 2) { wait_vm_barrier<2 * L>(); return; } }
-  if constexpr (NS >= 3) { if (rem >= 1) { wait_vm_barrier<L>(); return; } }
-  wait_vm_barrier<0>();
-}
-
 // fwd / dgrad: BM x BN_ x 64 tiles, BM/32 waves (BM/64 x 2), NS-deep LDS ring of
 // [row][64 k] images (128-B rows); 16-B chunk c of row r is stored at chunk
 // c ^ ((r >> 1) & 7): conflict-free ds_read_b128 fragment reads
@@ -1676,12 +1593,25 @@ extern "C" int ewvit_conv2d_pack_weights(int n, const float *const *w, const int
 
 // rows per BatchNorm partial that ewvit_conv2d_fwd_bn leaves for this shape (the
 // LDS-DMA kernel's m-tile), or 0 when the shape takes the register-staged kernel
+static FwdArgs fwd_args(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
+  FwdArgs a;
+  a.g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  a.M = (int64_t)a.g.N * a.g.Ho * a.g.Wo; a.Ncol = a.g.Cout; a.KC = a.g.Cin;
+  a.srcH = a.g.H; a.srcW = a.g.W; a.outH = a.g.Ho; a.outW = a.g.Wo;
+  a.sgc = a.g.Cin; a.sgs = 0; a.ogc = a.g.Cout; a.ogs = 0;
+  return a;
+}
+
+// (the windowed kernel, convwin.hip, leaves one partial row per 16 x 16 output block)
 static int fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
   if (!use_glds() || Cin % 64 || Cout % 8 || Cout > 65536) return 0;
   const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t K = (int64_t)ksize * ksize * Cin;
   if (2 * N * H * W * Cin >= (int64_t)OOB || Cout * K * 2 >= (int64_t)OOB || N * Ho * Wo * Cout >= (int64_t)1 << 40)
     return 0;
+  FwdArgs a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
+  a.bn_part = reinterpret_cast<float *>(1);    // (a statistics epilogue)
+  if (win_ok(a, false)) return 256;
   return 128;
 }
 
@@ -1707,7 +1637,10 @@ extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *b
   a.sgc = (int)x_group_c; a.sgs = x_group_stride; a.ogc = g.Cout; a.ogs = 0;
   a.bn_shift = bn_shift; a.bn_part = bn_part; a.bn_shift_out = bn_shift_out;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
-  EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd_bn: LDS-DMA kernel refused the shape");
+  if (fwd_bn_rows(N, H, W, Cin, Cout, ksize, stride) == 256)
+    EWVIT_CHECK_ARG(launch_win(a, xb, false, as_stream(stream)), "conv2d_fwd_bn: windowed kernel refused the shape");
+  else
+    EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd_bn: LDS-DMA kernel refused the shape");
   return launch_status("conv2d_fwd_bn");
 }
 
@@ -1747,7 +1680,8 @@ extern "C" int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias
     // the weights were packed with cp input channels (ewvit_conv2d_fwd_pack_cin)
     a.KC = (int)cp; a.KCr = (int)Cin;
     EWVIT_CHECK_ARG(launch_glds<false>(a, xb, as_stream(stream)), "conv2d_fwd: padded LDS-DMA kernel refused");
-  } else if (!launch_small(a, false, as_stream(stream)) && !launch_glds<false>(a, xb, as_stream(stream))) {
+  } else if (!launch_win(a, xb, false, as_stream(stream)) && !launch_small(a, false, as_stream(stream)) &&
+             !launch_glds<false>(a, xb, as_stream(stream))) {
     launch_fwd<false>(a, as_stream(stream));
   }
   return launch_status("conv2d_fwd");
@@ -1891,8 +1825,8 @@ extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx,
   a.srcH = g.Ho; a.srcW = g.Wo; a.outH = g.H; a.outW = g.W;
   a.sgc = g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
   const int64_t sb = 2 * N * (int64_t)g.Ho * g.Wo * Cout;
-  if (!launch_small(a, true, as_stream(stream)) && !dgrad_by_parity(a, sb, as_stream(stream)) &&
-      !launch_glds<true>(a, sb, as_stream(stream)))
+  if (!launch_win(a, sb, true, as_stream(stream)) && !launch_small(a, true, as_stream(stream)) &&
+      !dgrad_by_parity(a, sb, as_stream(stream)) && !launch_glds<true>(a, sb, as_stream(stream)))
     launch_fwd<true>(a, as_stream(stream));
   return launch_status("conv2d_bwd_data");
 }

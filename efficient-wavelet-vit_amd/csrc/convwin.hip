@@ -1,0 +1,381 @@
+// Windowed 3x3 stride-1 convolution (fwd and input gradient) for the MWT's big maps
+// (gfx950).
+//
+// Callers: the MWT conv stack of network/mwt.py:60-72,112-114 — multiscale_fusion
+// (384 -> 128 over the level-major fusion outputs, 64 x 112^2) and its input
+// gradient (128 -> 384), hf_conv['fusion'] forward (64 -> 128 over 192 x 112^2).  The
+// generic implicit-GEMM kernel (conv.hip conv_glds_kernel) stages every K-tile's
+// A operand as 128 gathered pixel rows — each input pixel crosses L2 -> LDS nine
+// times, once per tap — and runs a 2-deep ring with a full vmcnt drain + barrier per
+// K-tile, the structure whose ceiling is ~0.9 PF/s (cdna_hip_programming.md
+// "The step-3 structure's ~900 TF ceiling").
+//
+// Here a workgroup owns a 16 x 16-pixel output block x 128 output channels and walks
+// the K axis as (64-channel block, tap) — the same K order as conv_glds_kernel's
+// tap_inner walk, and the same MFMA operand order, so results are bit-identical:
+//
+//   * A: the block's 18 x 18-pixel input window of one 64-channel block is staged
+//     ONCE into LDS (41 LDS-DMA pieces of 8 pixels x 128 B); the nine taps read it at
+//     a per-tap pixel offset.  Window pixel p keeps 16-B chunk c at c ^ (p & 7): for
+//     any offset, the 16 consecutive pixels of an MFMA fragment read conflict-free
+//     with ds_read_b128 (brute-forced over all window offsets).  Two window buffers:
+//     the next channel block's (or the next tile's) window lands during taps 0-5 of
+//     the current one.
+//   * B: the packed weights, one 128 x 64 K-tile per tap, in a 4-slot LDS ring; each
+//     K-tile is issued 4 K-tiles ahead.
+//   * One raw s_barrier per K-tile behind a COUNTED s_waitcnt vmcnt(N): the K-tile
+//     after the one being multiplied must have landed, two more stay in flight
+//     across the barrier (N is exact per tap position, epilogue stores included).
+//     The fragments of K-tile i+1 are read into registers while K-tile i's MFMAs
+//     run (register double buffer), so no wave stalls on LDS latency after the
+//     barrier.  All LDS lives in one __shared__ array; the epilogue's bias / BN
+//     shift come from LDS, so no ordinary global load ever waits on the DMA queue
+//     (cdna_hip_programming.md "Projection GEMM at M = 256" item 4 traps).
+//   * 8 waves (4 row groups = 4 image rows each x 2 column halves), 64 x 64 per wave,
+//     one workgroup per CU, persistent over the tiles (XCD-aware order: a spatial
+//     block's column tiles and its neighbours run on one XCD).
+//   * Epilogue straight from the MFMA registers (8-B buffer stores of 4 channels),
+//     optional bias and the BatchNorm statistics of the rounded output per 16 x 16
+//     block (one partial row per block).
+#include "conv_common.h"
+
+#include <type_traits>
+
+namespace ewvit {
+
+int g_win = 1;
+
+namespace {
+constexpr int WT = 16;                    // output block side (pixels)
+constexpr int WW = WT + 2;                // window side
+constexpr int WPIX = WW * WW;             // 324 window pixels
+constexpr int WPIECES = (WPIX + 7) / 8;   // 41 LDS-DMA pieces of 8 pixels x 128 B
+constexpr int WIN_B = WPIECES * 1024;
+constexpr int NSLOT = 4;                  // weight ring slots (K-tiles)
+constexpr int SLOT_B = 128 * 128;         // 128 columns x 64 k, bf16
+constexpr int RING0 = 2 * WIN_B;
+constexpr int SMEM_B = RING0 + NSLOT * SLOT_B;   // 149,504 B: one workgroup per CU
+}  // namespace
+
+// all LDS-DMA pieces except the N youngest landed, LDS reads drained, workgroup barrier
+template <int N> __device__ __forceinline__ void win_sync() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((ext_vector_type(2))) unsigned int cu32x2;
+__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, uint2 v, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b64(cu32x2{v.x, v.y}, r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, float v, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+
+// one unit = (tile, 64-channel block): 9 K-tiles, one per tap
+struct WinUnit {
+  int n0;        // first output column of the tile
+  int kb;        // byte offset of the channel block inside a packed weight row
+  uint32_t wsrc; // byte offset of window pixel (0, 0) and the channel block in src (may wrap: only used with valid pixels)
+  int oh0, ow0;  // window pixel (0, 0) = image pixel (oh0 - 1, ow0 - 1)
+  int img;       // image
+  int part;      // BatchNorm partial row (spatial block index)
+  int last;      // last channel block of the tile
+  int ok;        // the unit exists
+};
+
+template <bool DGRAD, bool STATS>
+__global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_bytes, int64_t out_bytes, int ntn,
+                                                       int ntiles, int ncb) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ws = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave 0..7
+  const int wm = ws >> 1, wn = ws & 1;                        // rows wm*64.., cols wn*64..
+  const int fr = lane & 15, fq = lane >> 4;
+  const int G = gridDim.x;
+  const int ntb = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / G + 1 : 0;
+  const int nu = ntb * ncb;                 // units this workgroup walks
+  if (nu == 0) return;
+  const int H = a.outH, W = a.outW;         // == srcH, srcW (stride 1)
+  const int nbx = W / WT, nbl = (H / WT) * nbx;
+  const int K = 9 * a.KC;
+  const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
+  const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
+  const __amdgpu_buffer_rsrc_t ro = mk_rsrc(a.out, out_bytes);
+
+  if (STATS && blockIdx.x == 0 && a.bn_shift_out)
+    for (int c = tid; c < a.Ncol; c += 512) a.bn_shift_out[c] = a.bn_shift ? a.bn_shift[c] : 0.f;
+  // bias / BN shift of this lane's 16 columns, in registers (a bias or statistics epilogue
+  // needs Ncol == 128: one column tile).  Read from LDS in the epilogue they would make hipcc
+  // drain the LDS-DMA queue (vmcnt(0)) before the read, once per tile
+  float4 bias4[4], shift4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wn * 64 + j * 16 + fq * 4;
+    bias4[j] = a.bias ? *reinterpret_cast<const float4 *>(a.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    shift4[j] = (STATS && a.bn_shift) ? *reinterpret_cast<const float4 *>(a.bn_shift + col)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  auto unit = [&](int u) -> WinUnit {
+    WinUnit d;
+    d.ok = u < nu;
+    const int uu = d.ok ? u : nu - 1;
+    const int k = uu / ncb, cb = uu - k * ncb;
+    const int tile = xcd_remap((int)blockIdx.x + k * G, ntiles);
+    const int jn = tile % ntn, s = tile / ntn;
+    d.img = s / nbl;
+    const int r = s - d.img * nbl;
+    const int by = r / nbx;
+    d.oh0 = by * WT;
+    d.ow0 = (r - by * nbx) * WT;
+    d.part = s;
+    d.n0 = jn * 128;
+    d.kb = cb * 128;                     // 64 channels x 2 B
+    d.last = cb == ncb - 1;
+    const int c = cb * 64, gi = c / a.sgc;
+    const int64_t pix = ((int64_t)d.img * H + (d.oh0 - 1)) * W + (d.ow0 - 1);
+    d.wsrc = (uint32_t)((pix * a.sgc + (int64_t)gi * a.sgs + (c - gi * a.sgc)) * 2);
+    return d;
+  };
+
+  // this lane's B rows (pieces 2ws, 2ws+1: rows 8p + lane/8) — byte offsets in a packed
+  // weight row for column tile 0, chunk-swizzled
+  uint32_t brow[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = (2 * ws + j) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    brow[j] = (uint32_t)((r * K + lc * 8) * 2);
+  }
+  // B(K-tile of unit d, weight tap rt) -> ring slot
+  auto issue_b = [&](const WinUnit &d, int rt, int slot) {
+    unsigned char *dst = smem + RING0 + slot * SLOT_B + ws * 2048;
+    const uint32_t base = (uint32_t)((d.n0 * K + rt * a.KC) * 2 + d.kb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(rw, dst + j * 1024, d.ok ? base + brow[j] : OOB);
+  };
+  // window piece q (8 pixels) of unit d into window buffer wb.  The lane's pixel is
+  // q * 8 + lane / 8 and its source chunk (lane & 7) ^ (pixel & 7) — loop-invariant, since
+  // q * 8 keeps pixel & 7; the pixel's row / column are recomputed per issue (the empty asm
+  // keeps hipcc from hoisting six such sets out of the loop into spilled registers)
+  const int wlc8 = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+  auto issue_w = [&](const WinUnit &d, int q, int wb) {
+    int pl = lane >> 3;
+    asm volatile("" : "+v"(pl));
+    const int p = q * 8 + pl;
+    const int wr = (p * 3641) >> 16;               // p / 18 for p < 328
+    const int wc = p - wr * WW;
+    const int ih = d.oh0 - 1 + wr, iw = d.ow0 - 1 + wc;
+    const bool ok = d.ok && p < WPIX && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    const uint32_t off = d.wsrc + (uint32_t)(((wr * W + wc) * a.sgc + wlc8) * 2);
+    glds16(rs, smem + wb * WIN_B + q * 1024, ok ? off : OOB);
+  };
+
+  // fragment addresses.  A: window pixel (wm*4 + i) * 18 + fr + tap offset, chunk c at
+  // c ^ (pixel & 7); B: ring row wn*64 + j*16 + fr, chunk c at c ^ ((row >> 1) & 7) =
+  // c ^ ((fr >> 1) & 7) for every j, so the 4 column groups are immediate offsets.  The
+  // second k32 half (chunks + 4) is the same address with byte bit 6 flipped.
+  const int apix0 = wm * 4 * WW + fr;
+  const uint32_t bfo = (uint32_t)((wn * 64 + fr) * 128 + 16 * (fq ^ ((fr >> 1) & 7)));
+  cbf16x8 fa[2][4], fb[2][4];
+  // fragments of the K-tile (window buffer wb, tap rt, ring slot) into fa / fb
+  auto read_frags = [&](cbf16x8 (&xa)[2][4], cbf16x8 (&xb)[2][4], int wb, int rt, int slot) {
+    const int kh = rt / 3, kw = rt - kh * 3;
+    const int woff = DGRAD ? (2 - kh) * WW + (2 - kw) : kh * WW + kw;
+    int p0 = apix0;
+    asm volatile("" : "+v"(p0));
+    const unsigned char *wbase = smem + wb * WIN_B;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = p0 + i * WW + woff;
+      const uint32_t o = (uint32_t)(p * 128 + 16 * (fq ^ (p & 7)));
+      xa[0][i] = *reinterpret_cast<const cbf16x8 *>(wbase + o);
+      xa[1][i] = *reinterpret_cast<const cbf16x8 *>(wbase + (o ^ 64));
+    }
+    const unsigned char *bb = smem + RING0 + slot * SLOT_B;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xb[0][j] = *reinterpret_cast<const cbf16x8 *>(bb + bfo + j * 2048);
+      xb[1][j] = *reinterpret_cast<const cbf16x8 *>(bb + (bfo ^ 64) + j * 2048);
+    }
+  };
+
+  cf32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+
+  // tile epilogue: (+ bias) -> bf16, 16 stores per wave; STATS: one more store per wave
+  auto epilogue = [&](const WinUnit &d, int wb) {
+    float cs[4][4], cq[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = wn * 64 + j * 16 + fq * 4;          // column in the tile
+      const int col = d.n0 + cl;
+      const float4 bv = bias4[j], kv = shift4[j];
+      const int gi = col / a.ogc;
+      const int64_t cbase = (int64_t)gi * a.ogs + (col - gi * a.ogc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + i) * W + d.ow0 + fr;
+        const bf16_t h0 = f2bf(acc[i][j][0] + bv.x), h1 = f2bf(acc[i][j][1] + bv.y);
+        const bf16_t h2 = f2bf(acc[i][j][2] + bv.z), h3 = f2bf(acc[i][j][3] + bv.w);
+        uint2 pk;
+        pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
+        bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2));
+        if (STATS) {
+          const float d0 = bf2f(h0) - kv.x, d1 = bf2f(h1) - kv.y, d2 = bf2f(h2) - kv.z, d3 = bf2f(h3) - kv.w;
+          cs[j][0] += d0; cs[j][1] += d1; cs[j][2] += d2; cs[j][3] += d3;
+          cq[j][0] = fmaf(d0, d0, cq[j][0]); cq[j][1] = fmaf(d1, d1, cq[j][1]);
+          cq[j][2] = fmaf(d2, d2, cq[j][2]); cq[j][3] = fmaf(d3, d3, cq[j][3]);
+        }
+        acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if constexpr (STATS) {
+      // the 16 row lanes of each column (DPP), then the 4 row-group waves through LDS (the
+      // finished window buffer wb: every wave's reads of it completed before this K-tile's
+      // barrier, and the next DMA into it is issued after the next barrier)
+      float *red = reinterpret_cast<float *>(smem + wb * WIN_B);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float S = row_sum16(cs[j][r]), Q = row_sum16(cq[j][r]);
+          if (fr == 0) {
+            const int cl = wn * 64 + j * 16 + fq * 4 + r;
+            red[(wm * 128 + cl) * 2] = S;
+            red[(wm * 128 + cl) * 2 + 1] = Q;
+          }
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const int v = tid & 255, cl = v >> 1, w = v & 1;
+      const float t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
+                      (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
+      // threads 256-511 store the same value to the same address: one store per wave
+      bstore32(mk_rsrc(a.bn_part, (int64_t)OOB), t,
+               (uint32_t)(((int64_t)d.part * 2 * a.Ncol + w * a.Ncol + d.n0 + cl) * 4));
+    }
+  };
+  constexpr int ST = 16 + (STATS ? 1 : 0);   // vector-memory ops of one epilogue per wave
+
+  // ---- prologue: unit 0's window, K-tiles 0..3 of unit 0
+  WinUnit cu = unit(0), nx = unit(1);
+#pragma unroll
+  for (int t = 0; t < 6; ++t) issue_w(cu, t * 8 + ws < WPIECES ? t * 8 + ws : WPIECES - 1, 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) issue_b(cu, t, t);
+  win_sync<6>();                            // window 0 and K-tile 0 landed (B 1..3 in flight)
+  read_frags(fa, fb, 0, 0, 0);
+  bool prev_st = false;                     // the previous unit ended a tile (its stores are in flight)
+
+  for (int u = 0; u < nu; ++u) {
+    const int wbuf = u & 1;
+    // one K-tile: wait for K-tile i+1, issue window piece (taps 0-5) and K-tile i+4,
+    // read K-tile i+1's fragments, multiply K-tile i
+    auto step = [&](auto TT) {
+      constexpr int T = decltype(TT)::value;
+      // vector-memory ops younger than K-tile i+1's pieces: the window pieces and weight
+      // K-tiles of iterations i-2, i-1, and the epilogue stores of the previous unit's tap
+      // 8 (iterations i-3 .. i-1 for T = 2, 1, 0)
+      constexpr int NB = 4 + (((T + 7) % 9) < 6 ? 1 : 0) + (((T + 8) % 9) < 6 ? 1 : 0);
+      if constexpr (T <= 2) {
+        if (prev_st) win_sync<NB + ST>();
+        else win_sync<NB>();
+      } else {
+        win_sync<NB>();
+      }
+      if constexpr (T < 6) issue_w(nx, T * 8 + ws < WPIECES ? T * 8 + ws : WPIECES - 1, wbuf ^ 1);
+      const int slot = (u + T) & 3;          // K-tile i = 9u + T; slot(i) == slot(i + 4)
+      if constexpr (T + 4 < 9) issue_b(cu, T + 4, slot);
+      else issue_b(nx, T + 4 - 9, slot);
+      cbf16x8 na[2][4], nb[2][4];
+      if constexpr (T + 1 < 9) read_frags(na, nb, wbuf, T + 1, (slot + 1) & 3);
+      else read_frags(na, nb, wbuf ^ 1, 0, (slot + 1) & 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { fa[ks][q] = na[ks][q]; fb[ks][q] = nb[ks][q]; }
+      if constexpr (T == 8) {
+        prev_st = cu.last;
+        if (cu.last) epilogue(cu, wbuf);
+      }
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
+    cu = nx;
+    nx = unit(u + 2);
+  }
+  // no LDS-DMA may land after the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool win_ok(const FwdArgs &a, bool dgrad) {
+  if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend || a.bwd.part) return false;
+  if (dgrad && a.bn_part) return false;
+  if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
+  if (a.KC % 64 || a.sgc % 64 || (a.KCr && a.KCr != a.KC)) return false;
+  if (a.Ncol % 128 || a.ogc % 128 || ((a.bias || a.bn_part) && a.Ncol != 128)) return false;
+  if (a.M != (int64_t)a.g.N * a.outH * a.outW) return false;
+  const int64_t K = 9LL * a.KC;
+  if (a.Ncol * K * 2 >= (int64_t)OOB) return false;
+  const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
+  if (ob >= (int64_t)OOB) return false;
+  const int64_t nt = a.M / (WT * WT) * (a.Ncol / 128);
+  return nt < (1 << 30);
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) {
+  if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
+  const int ntn = a.Ncol / 128;
+  const int ntiles = (int)(a.M / (WT * WT) * ntn);
+  int G = cu_count();
+  if (g_grid_cap > 0 && g_grid_cap < G) G = g_grid_cap;
+  if (G > ntiles) G = ntiles;
+  const int ncb = a.KC / 64;
+  const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
+  if (dgrad)
+    hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (a.bn_part)
+    hipLaunchKernelGGL((conv_win_kernel<false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else
+    hipLaunchKernelGGL((conv_win_kernel<false, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  return true;
+}
+
+}  // namespace ewvit
+
+extern "C" int ewvit_conv2d_set_win(int variant) {
+  const int prev = ewvit::g_win;
+  ewvit::g_win = variant ? 1 : 0;
+  return prev;
+}

@@ -53,6 +53,7 @@ SIGNATURES = {
     'ewvit_maxpool2_bwd': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp],
     'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
+    'ewvit_conv2d_set_win': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],

@@ -365,6 +365,15 @@ int ewvit_conv2d_set_grid_cap(int max_workgroups);
  * can check both on one case; 1 (default) the LDS-DMA kernels wherever the shape allows.
  * Returns the previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_glds(int variant);
+/* Windowed 3x3 stride-1 kernel switch (test / A-B switch, csrc/convwin.hip): 1 (default) the
+ * forward and input gradient of 3x3 stride-1 convs over maps whose sides are multiples of 16,
+ * with 64-channel input blocks and 128-column output tiles (the MWT's multiscale_fusion and
+ * hf_conv fusion, reference network/mwt.py:60-72,112-114), run one workgroup per 16 x 16
+ * output block with the block's 18 x 18 input window staged once per channel block; 0 the
+ * generic LDS-DMA kernel (bit-identical results).  The forward's BatchNorm partials then
+ * come one row per 16 x 16 block (ewvit_conv2d_fwd_bn_rows answers 256).  Returns the
+ * previous setting.  Replaces nothing in the reference. */
+int ewvit_conv2d_set_win(int variant);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
  * 64 x 128, 32 pixels per K-tile) for n' = k*k*Cin >= 2048 over >= 64K output pixels, else
  * 128-column tiles; 2 = 256-column tiles whenever n' >= 256 and the last tile wastes <= 1/8 of
