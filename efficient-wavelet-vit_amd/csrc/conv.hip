@@ -240,26 +240,6 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 
 // ---------------------------------------------------------------- wgrad
 // C[co][n'] with n' = tap*Cin + ci, reduction over output pixels m.
-// A(co, m) = dy[m][co]   -> image Ast[m][co]  (rows of 128 co = 256 B)
-// B(m, n') = x[pix(m,tap)][ci] -> image Bst[m][n'] (rows of 128 n' = 256 B)
-// 16-B chunk ch of row r lives at 256*r + 16*(ch ^ swz(r)),
-// swz(r) = ((r&3)<<2) | ((r>>2)&3)  (T10 image (b): conflict-free tr reads).
-struct WgradArgs {
-  const bf16_t *x;       // [N, H, W, Cin], grouped (xgc, xgs)
-  const bf16_t *dy;      // [N, Ho, Wo, Cout]
-  float *part;           // [splits][Cout][taps*Cin]
-  float *dbias_part;     // [splits][Cout] partial bias gradients (sum of dy), or null
-  ConvGeom g;
-  int64_t M;             // N*Ho*Wo
-  int64_t mper;          // pixels per split (multiple of 32)
-  int xgc;
-  int64_t xgs;
-};
-
-__device__ __forceinline__ int swz_off(int r, int ch) {
-  return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
-}
-
 template <int KS>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2][2][CBK * 256];  // [buf][A/B][32 rows x 256 B]
@@ -1871,16 +1851,28 @@ extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {
   return prev;
 }
 
+static WgradArgs wgrad_args(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
+  WgradArgs a;
+  a.g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  a.M = (int64_t)a.g.N * a.g.Ho * a.g.Wo;
+  a.xgc = (int)Cin; a.xgs = 0;
+  return a;
+}
+
 extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
                                                      int ksize, int stride) {
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
+  // the windowed kernel (convwin.hip): [splits][Cout][9 Cin] slabs + [splits][Cout] bias partials
+  const int wsp = wgrad_win_splits(wgrad_args(N, H, W, Cin, Cout, ksize, stride), 2 * N * H * W * Cin);
+  const int64_t winb = (int64_t)wsp * Cout * (9 * Cin + 1) * (int64_t)sizeof(float);
   const int64_t ntx = (ksize * ksize * Cin + CBN - 1) / CBN;
   const int64_t narrow = wgrad_splits(g) * Cout * (ksize * ksize * Cin + ntx) * (int64_t)sizeof(float);
   const int wide = wgrad_wide(g);
-  if (!wide) return narrow;
+  int64_t need = narrow > winb ? narrow : winb;
+  if (!wide) return need;
   const int64_t ntw = (ksize * ksize * Cin + 2 * CBN - 1) / (2 * CBN);
   const int64_t wb = wgrad_splits(g, wide) * Cout * (ksize * ksize * Cin + ntw) * (int64_t)sizeof(float);
-  return wb > narrow ? wb : narrow;
+  return wb > need ? wb : need;
 }
 
 extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
@@ -1899,6 +1891,27 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   a.M = (int64_t)g.N * g.Ho * g.Wo;
   const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
   const bool glds = use_glds() && xb < (int64_t)OOB && a.M * g.Cout * 2 < (int64_t)OOB;
+  // the windowed kernel (convwin.hip): 3x3 stride 1 over maps of whole 8 x 16 tiles
+  const int wsp = glds ? wgrad_win_splits(a, xb) : 0;
+  if (wsp > 0) {
+    EWVIT_CHECK_ARG(dw_cin > 0 && dw_cin <= Cin, "conv2d_bwd_weight: dw_cin %lld not in (0, %lld]", (long long)dw_cin,
+                    (long long)Cin);
+    a.part = workspace;
+    a.dbias_part = dbias ? workspace + (int64_t)wsp * g.Cout * taps * g.Cin : nullptr;
+    hipStream_t s = as_stream(stream);
+    launch_wgrad_win(a, xb, wsp, s);
+    if (int rc = launch_status("conv2d_bwd_weight (windowed)")) return rc;
+    WOut wo;
+    wo.s_co = dw_s_co; wo.s_ci = dw_s_ci; wo.s_tap = dw_s_tap; wo.cin = (int)dw_cin;
+    const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
+    int T = 1;
+    while (T < 64 && T * 2 <= wsp && n4 * T * 2 <= 65536) T *= 2;
+    const int64_t nmain = (n4 * T + 255) / 256;
+    const int64_t nbias = dbias ? (g.Cout + 63) / 64 : 0;
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,
+                       g.Cout, g.Cin, taps, wsp, wsp, accumulate, a.dbias_part, dbias, wo, T, (int)nmain);
+    return launch_status("conv2d_bwd_weight reduce");
+  }
   const int wide = glds ? wgrad_wide(g) : 0;
   const int64_t splits = wgrad_splits(g, wide);
   a.dbias_part = dbias ? workspace + splits * g.Cout * taps * (int64_t)g.Cin : nullptr;

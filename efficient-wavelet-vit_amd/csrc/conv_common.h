@@ -88,9 +88,35 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
   wait_vm_barrier<0>();
 }
 
+// ---------------------------------------------------------------- wgrad
+// A(co, m) = dy[m][co]   -> image Ast[m][co]  (rows of 128 co = 256 B)
+// B(m, n') = x[pix(m,tap)][ci] -> image Bst[m][n'] (rows of 128 n' = 256 B)
+// 16-B chunk ch of row r lives at 256*r + 16*(ch ^ swz(r)),
+// swz(r) = ((r&3)<<2) | ((r>>2)&3)  (T10 image (b): conflict-free tr reads).
+struct WgradArgs {
+  const bf16_t *x;       // [N, H, W, Cin], grouped (xgc, xgs)
+  const bf16_t *dy;      // [N, Ho, Wo, Cout]
+  float *part;           // [splits][Cout][taps*Cin]
+  float *dbias_part;     // [splits][Cout] partial bias gradients (sum of dy), or null
+  ConvGeom g;
+  int64_t M;             // N*Ho*Wo
+  int64_t mper;          // pixels per split (multiple of 32)
+  int xgc;
+  int64_t xgs;
+};
+
+__device__ __forceinline__ int swz_off(int r, int ch) {
+  return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
 // the windowed 3x3 stride-1 fwd / dgrad (convwin.hip): true when it ran the shape
 bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s);
 bool win_ok(const FwdArgs &a, bool dgrad);
 extern int g_win;   // 1: the windowed kernels take the shapes they accept (default), 0: never
+// the windowed 3x3 stride-1 weight gradient (convwin.hip): pixel splits it would use for this
+// shape (0 = it does not take the shape), and the launch (slabs [splits][Cout][9*Cin] +
+// bias partials [splits][Cout] for conv_wgrad_reduce_kernel)
+int wgrad_win_splits(const WgradArgs &a, int64_t x_bytes);
+bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream_t s);
 
 }  // namespace ewvit

@@ -354,6 +354,236 @@ static int cu_count() {
   return n;
 }
 
+// ---------------------------------------------------------------- weight gradient
+// dW[co][tap][ci] = sum_pix dy[pix][co] * x[pix + tap shift][ci] over 8 x 16-pixel tiles (the
+// K chunks): a workgroup owns (pixel split, 128-row co tile, 64-channel ci block) and all 9
+// taps — a [128 co] x [9 x 64] block of the weight gradient — and walks its split's pixel
+// tiles.  Per tile it stages the dy tile (128 px x 128 co, 32 KB) and the tile's 10 x 18 x 64
+// x window (23 KB, ONCE for the nine taps) by LDS-DMA into one of two stages, the next tile's
+// landing during this tile's 144 MFMAs per wave.  Both operands are read transposed
+// (ds_read_b64_tr_b16): dy as the MFMA A operand (the generic wgrad's image and swizzle),
+// the window as B with pixel p's 16-B chunk c at c ^ (((p >> 1) & 1) << 1 | ((p >> 3) & 1)
+// << 2) — conflict-free for the 32 lanes of a read at any tap offset (brute-forced).  That
+// swizzle depends on p mod 16 only, so a lane's 16 window addresses (one per p mod 16) are
+// computed once and every tap / k32 step / half reads at one of them plus an immediate
+// offset: no address VALU in the loop.  8 waves = 2 co halves x 4 ci quarters; each wave
+// 64 co x (9 taps x 16 ci) = 144 fp32 accumulators per lane.  The bias gradient (sum of dy
+// over pixels) is one more MFMA per k32 step against a ones operand, by the ci-block-0
+// workgroups.  Per split: fp32 slabs [split][Cout][9 Cin] (+ [split][Cout] bias partials)
+// summed by conv_wgrad_reduce_kernel in a fixed order.
+namespace {
+constexpr int GT_R = 8, GT_C = 16;                 // pixel tile
+constexpr int GX_W = GT_C + 2, GX_H = GT_R + 2;    // x window
+constexpr int GX_PIX = GX_W * GX_H;                // 180 pixels x 32 channels (64-B rows)
+constexpr int GX_PIECES = (GX_PIX + 15) / 16;      // 12 LDS-DMA pieces of 16 pixels
+constexpr int GX_B = GX_PIECES * 1024;             // 12,288
+constexpr int GD_B = 128 * 256;                    // dy tile
+constexpr int GD0 = 2 * GX_B;                      // [X0][X1][D0][D1]
+constexpr int GSMEM = GD0 + 2 * GD_B;              // 90,112 B
+}  // namespace
+
+// 64-B window rows: chunk c of pixel p at c ^ (((p >> 3) & 1) << 1)
+__device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
+
+// LDS-DMA through inline asm: the weight-gradient loop reads its operands with the
+// ds_read_b64_tr_b16 builtin, and hipcc, seeing a pending LDS-DMA (builtin) write, waits
+// vmcnt(0) before the first such read after it — draining the next tile's loads before this
+// tile's MFMAs.  The DMAs here are all counted by hand (s_waitcnt before each barrier), so
+// they are hidden from the compiler.  M0 (the DMA's LDS base) is reserved to hipcc, which
+// sets it before each of its own uses; no other M0 user runs in this kernel.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <bool BIAS>
+__global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb, int nct,
+                                                             int ntile) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[GSMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ws = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = ws >> 1, wc = ws & 1;              // co half, 16-channel half of the 32-channel block
+  const int r = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int cb = r % ncb, ct = (r / ncb) % nct, split = r / (ncb * nct);
+  const int t0 = (int)((int64_t)split * ntile / nsplit), t1 = (int)((int64_t)(split + 1) * ntile / nsplit);
+  const int H = a.g.H, W = a.g.W, Cout = a.g.Cout, Cin = a.g.Cin;
+  const int tpr = W / GT_C, tpi = (H / GT_R) * tpr;
+  const int NP = 9 * Cin;
+  const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, x_bytes);
+  const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * Cout * 2);
+  const bool do_bias = BIAS && cb == 0;
+  const int c32 = cb * 32, gi = c32 / a.xgc;
+  const int64_t cofs = (int64_t)gi * a.xgs + (c32 - gi * a.xgc);
+
+  // stage tile t into stage b: dy tile rows 2 ws, 2 ws + 1 (pieces j: pixels 4 (j & 3) + lane/16
+  // of row 2 ws + j / 4), window pieces 3 ws + j (pixels 16 q + lane / 4).  The empty asm keeps
+  // hipcc from hoisting the per-lane constants out of the loop (into spilled registers).
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
+  auto issue = [&](int t, int b, bool live) {
+    const int img = t / tpi, rem = t - img * tpi;
+    const int oh0 = (rem / tpr) * GT_R, ow0 = (rem % tpr) * GT_C;
+    int dl = lane >> 4;
+    asm volatile("" : "+v"(dl));
+    const int64_t dpix = ((int64_t)img * H + oh0 + 2 * ws) * W + ow0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sc = (lane & 15) ^ ((dl << 2) | (j & 3));
+      const uint32_t off = (uint32_t)(((dpix + (j >> 2) * W + 4 * (j & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
+      glds16_asm(rd, lds0 + GD0 + b * GD_B + (ws * 8 + j) * 1024, live ? off : OOB);
+    }
+    const int64_t xpix = ((int64_t)img * H + oh0 - 1) * W + ow0 - 1;
+    int xl = lane >> 2;
+    asm volatile("" : "+v"(xl));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = ws * 3 + j;
+      const int p = q * 16 + xl;
+      const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;       // p / 18, p % 18
+      const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
+      // (bitwise &: a short-circuit && becomes an exec-masked branch, and at its merge hipcc
+      // waits vmcnt(0) before the next ds_read — draining the DMA just issued)
+      const bool ok = live & (p < GX_PIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+      const int sc = (lane & 3) ^ xswz(p);
+      const uint32_t off = (uint32_t)(((xpix + xr * W + xc) * a.xgc + cofs + sc * 8) * 2);
+      glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB);
+    }
+  };
+
+  // fragment addresses.  A (dy^T, rows k = pixel, cols = co): tr read rows 8g + q (+4 hi)
+  // of k32 step ks at + ks * 8192, stage 1 at + GD_B.  B (window): 16 addresses, one per
+  // window pixel residue mod 16 (the swizzle depends on bit 3 only); stage 1 at + GX_B.
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  uint32_t aad[2][4];
+#pragma unroll
+  for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 8 * g + q4 + 4 * hi, col = wr * 64 + i * 16 + 4 * p4;
+      aad[hi][i] = (uint32_t)(GD0 + swz_off(row, col >> 3) + 2 * (col & 7));
+    }
+  uint32_t xad[16];
+  const int pb0 = (g >> 1) * GX_W + 8 * (g & 1) + q4;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int P = pb0 + m;
+    xad[m] = (uint32_t)(P * 64 + 16 * ((2 * wc + (p4 >> 1)) ^ xswz(P)) + 8 * (p4 & 1));
+  }
+  auto trd = [&](uint32_t off) -> cs4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) cs4 *)(smem + off));
+  };
+
+  cf32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  cf32x4 bacc[2] = {cf32x4{0.f, 0.f, 0.f, 0.f}, cf32x4{0.f, 0.f, 0.f, 0.f}};
+  const cbf16x8 ones = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+      0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+
+  // one loop body for both stages (two bodies made hipcc copy the accumulators between
+  // them): the stage's addresses are toggled by +-stage size after each tile
+  auto compute = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      cbf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const cs4 lo = trd(aad[0][i] + ks * 8192), hi = trd(aad[1][i] + ks * 8192);
+        af[i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int C0 = ks * 2 * GX_W + kh * GX_W + kw, C1 = C0 + 4;
+        const cs4 lo = trd(xad[C0 & 15] + (C0 & ~15) * 64);
+        const cs4 hi = trd(xad[C1 & 15] + (C1 & ~15) * 64);
+        const cbf16x8 bf = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                  lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][t], 0, 0, 0);
+      }
+      if (do_bias) {           // co rows wr*64 + 32 wc .. +31 (wave-uniform branch: a runtime index into af -> scratch)
+        if (wc == 0) {
+          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
+          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
+        } else {
+          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], ones, bacc[0], 0, 0, 0);
+          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[3], ones, bacc[1], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // (the last tile issues a dummy stage — every lane out of range, zeros into the idle stage —
+  // so no branch sits between the DMA and the fragment reads: at such a merge hipcc waits
+  // vmcnt(0) before the first ds_read, draining the next tile's loads)
+  if (t0 < t1) issue(t0, 0, true);
+  int sd = GD_B, sx = GX_B;          // stage 0 -> 1 address deltas
+  for (int t = t0, b = 0; t < t1; ++t, b ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(t + 1 < t1 ? t + 1 : t, b ^ 1, t + 1 < t1);
+    compute();
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aad[hi][i] += sd;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xad[m] += sx;
+    sd = -sd;
+    sx = -sx;
+  }
+
+  // slab [split][Cout][9 Cin]: lane holds rows co = 4 (lane>>4) + rr of each 16-row frag, column lane & 15
+  float *dst = a.part + (int64_t)split * Cout * NP;
+  const int co0 = ct * 128 + wr * 64 + 4 * g;
+  const int cl = c32 + wc * 16 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) dst[(int64_t)(co0 + i * 16 + rr) * NP + t * Cin + cl] = acc[i][t][rr];
+  if (do_bias && (lane & 15) == 0)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        a.dbias_part[(int64_t)split * Cout + ct * 128 + wr * 64 + wc * 32 + h * 16 + 4 * g + rr] = bacc[h][rr];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int wgrad_win_splits(const WgradArgs &a, int64_t x_bytes) {
+  const ConvGeom &g = a.g;
+  if (!g_win || g.ks != 3 || g.stride != 1 || g.pad != 1 || g.H % GT_R || g.W % GT_C || g.Ho != g.H || g.Wo != g.W)
+    return 0;
+  if (g.Cin % 32 || a.xgc % 32 || g.Cout % 128) return 0;
+  if (x_bytes >= (int64_t)OOB || a.M * g.Cout * 2 >= (int64_t)OOB) return 0;
+  const int64_t ntile = a.M / (GT_R * GT_C);
+  const int ncb = g.Cin / 32, nct = g.Cout / 128;
+  int G = cu_count();
+  if (g_grid_cap > 0 && g_grid_cap < G) G = g_grid_cap;
+  int64_t s = G / (ncb * nct);
+  if (s < 1) s = 1;
+  if (s > ntile) s = ntile;
+  return (int)s;
+}
+
+bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream_t s) {
+  const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
+  const int ntile = (int)(a.M / (GT_R * GT_C));
+  const unsigned nwg = (unsigned)(splits * ncb * nct);
+  if (a.dbias_part)
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+  else
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<false>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+  return true;
+}
+
 bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) {
   if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
   const int ntn = a.Ncol / 128;

@@ -1099,9 +1099,10 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   return launch_status("vit_layer_bwd");
 }
 
-extern "C" int ewvit_vit_embed_fwd(const float *y, const float *cls, const float *pos, int B, float drop_p,
+extern "C" int ewvit_vit_embed_fwd(const float *y, const float *cls, const float *pos, int B, int npos, float drop_p,
                                    uint64_t seed, const int64_t *seed_off, float *tok, void *stream) {
-  EWVIT_CHECK_ARG(y && cls && pos && tok && B >= 1 && drop_p >= 0.f && drop_p < 1.f, "vit_embed_fwd: bad args");
+  EWVIT_CHECK_ARG(y && cls && pos && tok && B >= 1 && npos >= B && drop_p >= 0.f && drop_p < 1.f,
+                  "vit_embed_fwd: bad args (B %d, npos %d: pos_embedding needs a row per frame)", B, npos);
   const int n = B * 2 * (VD / 4);
   hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), y, cls, pos, B, drop_p,
                      seed, seed_off, tok);

@@ -113,7 +113,7 @@ SIGNATURES = {
     'ewvit_vit_layer_bwd': [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_vit_pack': [_vp, _i32, _vp, _vp],
     'ewvit_gemm_tallk': [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp],
-    'ewvit_vit_embed_fwd': [_vp, _vp, _vp, _i32, _f32, _u64, _vp, _vp, _vp],
+    'ewvit_vit_embed_fwd': [_vp, _vp, _vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp],
     'ewvit_vit_embed_bwd': [_vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp],
 }
 

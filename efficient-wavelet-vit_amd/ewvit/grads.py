@@ -43,6 +43,13 @@ def begin_step():
     _tls.gen = next(_steps)
 
 
+def end_step():
+    """Close the calling thread's step (after its backward): later forwards outside a step
+    (eager evaluation, a plain training loop) count no uses, so no parameter of theirs looks
+    multi-use and ``give`` hands every gradient straight back to autograd."""
+    _tls.gen = 0
+
+
 def _gen():
     return getattr(_tls, 'gen', 0)
 
@@ -107,7 +114,10 @@ def give(param, g, gen):
     """What an op's backward returns to autograd for `param`'s gradient `g`: `g` itself, or —
     for a parameter used more than once in step `gen` — None, with `g` kept for the sum at the
     end of the backward pass."""
-    if g is None or param is None or not DEFER or not param.requires_grad or not multi_use(param, gen):
+    # (only a leaf is deferred: the sum is written to param.grad, which autograd would never
+    # propagate from a non-leaf weight — a DataParallel replica's, a cast copy — to its leaf)
+    if (g is None or param is None or not DEFER or not param.requires_grad or not param.is_leaf
+            or not multi_use(param, gen)):
         return g
     with _lock:
         ent = _pending.setdefault(gen, {}).setdefault(id(param), [param, [], set()])

@@ -60,10 +60,17 @@ def _backend(group):
 
 
 def _pg_status():
+    """The flight recorder's per-process-group status, {} when this torch build or process
+    group does not provide it (private API: a missing symbol, another signature or an
+    unparsable dump all read as 'unavailable', never as an exception)."""
     import json
-    from torch._C import _distributed_c10d as c10d
-    d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=False, onlyActive=True))
-    return d.get('pg_status') or {}
+    try:
+        from torch._C import _distributed_c10d as c10d
+        d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=False, onlyActive=True))
+        st = d.get('pg_status') if isinstance(d, dict) else None
+        return st if isinstance(st, dict) else {}
+    except Exception:            # noqa: BLE001 — AttributeError / TypeError / ValueError / RuntimeError
+        return {}
 
 
 def retire_eager_collectives(timeout_s=60.0):
@@ -93,11 +100,22 @@ class GradBuckets:
     """Flat, bucketed gradient buffer with all-reduces issued as buckets fill.
 
     ``force=True`` issues the collectives even in a world of one process (a test switch: it
-    puts the RCCL calls inside the captured step graph on a one-GPU box)."""
+    puts the RCCL calls inside the captured step graph on a one-GPU box).
 
-    def __init__(self, params, group=None, bucket_mb=32, first_bucket_mb=4, force=False):
+    ``comm_dtype=torch.bfloat16`` (opt-in; EWVIT_GRAD_COMM_DTYPE=bf16 for TrainStep): each
+    bucket is rounded to bf16 into a communication buffer and all-reduced there — half the
+    xGMI bytes of the fp32 gradient (240 MB -> 120 MB per step at config 2) — and the
+    averaged result is widened back into the fp32 buffer the optimizer reads (fp32 master
+    weights and Adam slots are untouched).  The gradient then carries one bf16 rounding per
+    rank before the sum (a relative error of ~2^-9 per element), which the reference's fp32
+    DataParallel gradient does not; default off."""
+
+    def __init__(self, params, group=None, bucket_mb=32, first_bucket_mb=4, force=False, comm_dtype=None):
         self.params = list(params)
         self.group = group
+        self.comm_dtype = comm_dtype if comm_dtype not in (None, torch.float32) else None
+        if self.comm_dtype is not None and self.comm_dtype != torch.bfloat16:
+            raise ValueError(f'GradBuckets: comm_dtype {comm_dtype} (float32 or bfloat16)')
         self.world = _world(group)
         self.reduce = self.world > 1 or (force and dist.is_available() and dist.is_initialized())
         self.avg_op = not self.reduce or dist.get_backend(group) != 'gloo'   # gloo has no AVG: SUM, then divide
@@ -117,6 +135,7 @@ class GradBuckets:
         n = sum(p.numel() for p in self.params)
         self.order = list(order)
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.comm = torch.zeros(n, dtype=self.comm_dtype, device=dev) if self.comm_dtype is not None else None
         self.views = [None] * len(self.params)
         self.bucket_of = [0] * len(self.params)
         self.buckets = []          # [(start, end, [param idx])]
@@ -184,7 +203,11 @@ class GradBuckets:
                     if st != cur:
                         cur.wait_stream(st)
             op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
-            self.works.append(dist.all_reduce(self.flat[s:e], op=op, group=self.group, async_op=True))
+            buf = self.flat[s:e]
+            if self.comm is not None:
+                buf = self.comm[s:e]
+                buf.copy_(self.flat[s:e])            # round to the communication dtype
+            self.works.append(dist.all_reduce(buf, op=op, group=self.group, async_op=True))
 
     def _fire_ready(self):
         while self.next < len(self.buckets) and self.pending[self.next] == 0:
@@ -205,13 +228,21 @@ class GradBuckets:
         for w in self.works:
             w.wait()
         self.works = []
+        if self.reduce and not self.defer and self.comm is not None:
+            self.flat.copy_(self.comm)               # widen the reduced gradients (one launch)
         if self.reduce and not self.avg_op and not self.defer:
             self.flat.div_(self.world)
 
     def allreduce_all(self):
         """The deferred form: one all-reduce of the whole buffer (between two graphs)."""
         if self.reduce:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM, group=self.group)
+            op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
+            if self.comm is not None:
+                self.comm.copy_(self.flat)
+                dist.all_reduce(self.comm, op=op, group=self.group)
+                self.flat.copy_(self.comm)
+            else:
+                dist.all_reduce(self.flat, op=op, group=self.group)
             if not self.avg_op:
                 self.flat.div_(self.world)
 
@@ -259,11 +290,16 @@ class BufferSync:
 
 class TrainStep:
     def __init__(self, model, forward_loss, optimizer, graph=True, warmup=3, group=None, bucket_mb=32,
-                 accum_steps=1, overlap=True, force_collectives=False):
+                 accum_steps=1, overlap=True, force_collectives=False, grad_comm_dtype=None):
         """``force_collectives``: issue the bucket all-reduces and the buffer broadcast even in
         a world of one (test switch; needs an initialised process group).  A failure to
         capture the collectives raises, unless EWVIT_GRAPH_SPLIT_FALLBACK=1 allows the split,
-        non-overlapped form (graphs around one all-reduce) — never silently."""
+        non-overlapped form (graphs around one all-reduce) — never silently.
+        ``grad_comm_dtype``: None / torch.float32 (default, the reference's fp32 gradient) or
+        torch.bfloat16 — the buckets all-reduced in bf16 (GradBuckets; default from
+        EWVIT_GRAD_COMM_DTYPE=bf16)."""
+        if grad_comm_dtype is None and os.environ.get('EWVIT_GRAD_COMM_DTYPE', 'fp32').lower() in ('bf16', 'bfloat16'):
+            grad_comm_dtype = torch.bfloat16
         self.model, self.forward_loss, self.opt, self.group = model, forward_loss, optimizer, group
         self.world = _world(group)
         forced = bool(force_collectives) and dist.is_available() and dist.is_initialized()
@@ -276,7 +312,7 @@ class TrainStep:
         capturable = backend in (None, 'nccl')
         self.graph = bool(graph) and dev.type == 'cuda' and capturable
         dp = self.world > 1 or forced
-        self.buckets = GradBuckets(self.params, group, bucket_mb, force=forced) if dp else None
+        self.buckets = GradBuckets(self.params, group, bucket_mb, force=forced, comm_dtype=grad_comm_dtype) if dp else None
         if self.buckets is not None:
             self.buckets.defer = not overlap
         self.bufsync = BufferSync(model, group) if dp else None
@@ -325,6 +361,9 @@ class TrainStep:
                     gr.reset()
                     setattr(self, name, None)
             torch.cuda.synchronize()
+            rel = getattr(self.opt, 'release_capture', None)
+            if rel is not None:
+                rel()                        # (the optimizer no longer guards released graphs' state)
         if self.buckets is not None:
             self.buckets.remove()
             self.buckets = None
@@ -357,10 +396,13 @@ class TrainStep:
                 if self.buckets is not None:
                     self.buckets.collect = k == self.accum - 1
                 grads.begin_step()           # parameter use counts (ewvit.grads)
-                lk = self.forward_loss(k) if self.accum > 1 else self.forward_loss()
-                if self.accum > 1:
-                    lk = lk / self.accum                                   # train.py:110
-                lk.backward()
+                try:
+                    lk = self.forward_loss(k) if self.accum > 1 else self.forward_loss()
+                    if self.accum > 1:
+                        lk = lk / self.accum                               # train.py:110
+                    lk.backward()
+                finally:
+                    grads.end_step()
                 loss = lk.detach() if loss is None else loss + lk.detach()
         return loss
 
@@ -458,19 +500,29 @@ class TrainStep:
         during the capture are never queued."""
         if not (self.buckets is not None and self.buckets.reduce and dist.get_backend(self.group) == 'nccl'):
             return
-        import warnings
+        # Both preconditions are hard errors (verdict r4): either one missing brings the round-3
+        # watchdog abort back, later and in another thread.  EWVIT_ALLOW_UNDRAINED_CAPTURE=1
+        # turns them into warnings (a torch build without the flight recorder, at the caller's risk).
+        unsafe = os.environ.get('EWVIT_ALLOW_UNDRAINED_CAPTURE', '0') == '1'
+
+        def refuse(msg):
+            if not unsafe:
+                raise RuntimeError(msg + ' (EWVIT_ALLOW_UNDRAINED_CAPTURE=1 to capture anyway)')
+            import warnings
+            warnings.warn(msg)
+
         if os.environ.get('TORCH_NCCL_CUDA_EVENT_CACHE', '1') != '0':
-            warnings.warn('TrainStep: capturing RCCL collectives with the process group\'s event cache on: a '
-                          'later eager collective can reuse a captured event and abort the NCCL watchdog '
-                          '(hipErrorCapturedEvent); call ewvit.dist.rccl_env() before init_process_group')
-        try:
-            retire_eager_collectives()
-        except RuntimeError:
-            if self._capture_mode == 'global' or _pg_status():
-                raise
-            warnings.warn('TrainStep: the flight recorder is off (TORCH_FR_BUFFER_SIZE), so the NCCL watchdog '
-                          'queue cannot be drained before the capture; call ewvit.dist.rccl_env() before '
-                          'init_process_group')
+            refuse('TrainStep: refusing to capture RCCL collectives with the process group\'s CUDA event cache '
+                   'on: a later eager collective can reuse a captured event and abort the NCCL watchdog '
+                   '(hipErrorCapturedEvent); call ewvit.dist.rccl_env() (or set TORCH_NCCL_CUDA_EVENT_CACHE=0) '
+                   'before init_process_group')
+        if not _pg_status():
+            refuse('TrainStep: refusing to capture RCCL collectives: the flight recorder\'s process-group status '
+                   'is unavailable (TORCH_FR_BUFFER_SIZE unset before init_process_group, or this torch build '
+                   'has no _dump_nccl_trace_json), so the NCCL watchdog queue cannot be drained before the '
+                   'capture; call ewvit.dist.rccl_env() before init_process_group')
+            return
+        retire_eager_collectives()
 
     def _finish_capture(self, graph):
         fin = getattr(self.opt, 'finish_capture', None)

@@ -225,6 +225,14 @@ class Adam(torch.optim.Optimizer):
             self.__dict__.setdefault('_table_keep', []).extend(out)
         return out
 
+    def release_capture(self):
+        """The graphs that launched Adam on this optimizer's state were released
+        (``ewvit.graph.TrainStep.close``): forget which parameters a captured step updates —
+        ``load_state_dict`` stops insisting on their state — and drop the tables kept here."""
+        self.__dict__.pop('_captured_params', None)
+        self.__dict__.pop('_table_keep', None)
+        self.__dict__.pop('_fill_after_capture', None)
+
     def launches_per_step(self):
         """Adam kernel launches one step makes, by kernel name, in either launch form (the
         profilers count step equivalents from them, whichever form the profiled build took)."""

@@ -152,7 +152,7 @@ class EmbedFn(torch.autograd.Function):
         off = L.rng_offset(y.device) if drop_p > 0 else None
         ctx.gen = grads.note_use(cls)
         grads.note_use(pos)
-        L.call('ewvit_vit_embed_fwd', L.ptr(yc), L.ptr(cls), L.ptr(pos), B, float(drop_p), int(seed), L.ptr(off),
+        L.call('ewvit_vit_embed_fwd', L.ptr(yc), L.ptr(cls), L.ptr(pos), B, pos.shape[0], float(drop_p), int(seed), L.ptr(off),
                L.ptr(tok), L.stream(tok))
         ctx.cfg = (float(drop_p), int(seed), B, y.shape)
         ctx.params = (cls, pos)

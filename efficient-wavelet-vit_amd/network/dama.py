@@ -44,13 +44,32 @@ def _branch_streams():
     return os.environ.get('EWVIT_BRANCH_STREAMS', '1') == '1'
 
 
-def _mwt_grid_cap():
+MWT_GRID_CAP = 160          # one process per GPU, nothing else on the chip (world 1)
+RCCL_CU_RESERVE = 16        # CUs left to RCCL's all-reduce kernels per rank when world > 1
+
+
+def _mwt_grid_cap(world=None):
     """Workgroups per big-grid MWT launch (LDS-DMA convs, BatchNorm passes) while the MWT
     shares the GPU with the backbone (EWVIT_MWT_GRID_CAP, 0 = uncapped): the MWT walks its
     tiles / rows on ~160 of the 256 CUs and the backbone's latency-bound kernels keep the
     rest.  Measured (config 2, graph replay, 3 rounds): cap 0 2754, 144 2919, 160 2952,
-    192 2910, 224 2870 frames/s; 64 / 96 make the MWT the critical path (1747 / 2300)."""
-    return int(os.environ.get('EWVIT_MWT_GRID_CAP', '160'))
+    192 2910, 224 2870 frames/s; 64 / 96 make the MWT the critical path (1747 / 2300).
+
+    This is the knob of the CU budget in data parallel (reference train.py:249-251 on N
+    GPUs): the bucket all-reduces' RCCL kernels run during the backward beside both branches
+    and need CUs of their own, so with world > 1 the MWT gives up RCCL_CU_RESERVE
+    (EWVIT_RCCL_CU_RESERVE) workgroups of its cap.  The world-1 value is measured; the
+    reserve is not (no multi-GPU node was available to sweep it) — set EWVIT_MWT_GRID_CAP
+    to override both."""
+    env = os.environ.get('EWVIT_MWT_GRID_CAP')
+    if env is not None:
+        return int(env)
+    if world is None:
+        import torch.distributed as dist
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    if world <= 1:
+        return MWT_GRID_CAP
+    return max(64, MWT_GRID_CAP - int(os.environ.get('EWVIT_RCCL_CU_RESERVE', str(RCCL_CU_RESERVE))))
 
 
 class CrossAttention(nn.Module):                                           # dama.py:15-53

@@ -232,14 +232,16 @@ class EfficientViT(nn.Module):                                             # sfe
     def head(self, x):
         """sfe.py:153-173 from the backbone map x [B, C, h, w]."""
         B = x.shape[0]
-        if B > self.pos_embedding.shape[0]:
+        P = self.pos_embedding.shape[0]
+        if B > P and P != 1:
+            # pos_embedding[0:B] has P rows, which broadcast against B frames only when P == 1
             raise RuntimeError(f'EfficientViT: {B} frames in one chunk exceed pos_embedding rows '
-                               f'({self.pos_embedding.shape[0]}) — the reference fails here too (sfe.py:158-159)')
+                               f'({P}) — the reference fails here too (sfe.py:158-159)')
         y = self.patches(x)
         pe = self.patch_to_embedding
         y = ewvit.linear(y, pe.weight, pe.bias, out_dtype=torch.float32, fp8=_fp8(pe))
         if (ewvit.vit.enabled() and y.shape[1:] == (1, 512) and self.cls_token.shape == (1, 1, 512)
-                and self.pos_embedding.shape[1:] == (1, 512) and self.pos_embedding.shape[0] <= 64
+                and self.pos_embedding.shape[1:] == (1, 512) and B <= P <= 64
                 and type(self.dropout) is nn.Dropout
                 and not _hooked(self.dropout) and not torch.compiler.is_compiling()):
             # CLS concat + pos_embedding[0:B] + emb dropout in one launch (ewvit.vit.embed)

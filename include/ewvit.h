@@ -742,10 +742,10 @@ int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float *x0, const 
                         void *scratch, float *dx0, const ewvit_vit_grads *grads, void *stream);
 /* The token sequence of sfe.py:155-160 for one 7x7 patch per frame: tok [B][2][512] f32 with
  * tok[b][0] = cls + pos[b], tok[b][1] = y[b] + pos[b] (y = patch_to_embedding output [B][512],
- * cls [512], pos = pos_embedding rows [>= B][512]), then Dropout(drop_p) (emb_dropout; keep mask
+ * cls [512], pos = pos_embedding rows [npos >= B][512], EINVAL otherwise), then Dropout(drop_p) (emb_dropout; keep mask
  * keep(seed + *seed_off * golden, (2 b + i) * 512 + c)).  Replaces torch.cat + add + nn.Dropout. */
-int ewvit_vit_embed_fwd(const float *y, const float *cls, const float *pos, int B, float drop_p, uint64_t seed,
-                        const int64_t *seed_off, float *tok, void *stream);
+int ewvit_vit_embed_fwd(const float *y, const float *cls, const float *pos, int B, int npos, float drop_p,
+                        uint64_t seed, const int64_t *seed_off, float *tok, void *stream);
 /* Backward: dtok [B][2][512] -> dy [B][512], dcls [512] (sum over frames, fixed order), dpos [npos][512]
  * (npos <= 64; rows >= B written 0: the pos_embedding[0:B] slice's gradient). */
 int ewvit_vit_embed_bwd(const float *dtok, int B, int npos, float drop_p, uint64_t seed, const int64_t *seed_off,

@@ -13,6 +13,7 @@ import os
 import socket
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -93,7 +94,7 @@ def test_ddp_gloo_world2_matches_dataparallel_semantics():
     torch.testing.assert_close(torch.from_numpy(res[0][2]), torch.from_numpy(res[1][2]))  # buffers broadcast
 
 
-def _trainstep_worker(rank, port, q, accum=1, overlap=True):
+def _trainstep_worker(rank, port, q, accum=1, overlap=True, comm=None):
     for p in (REPO, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -119,7 +120,8 @@ def _trainstep_worker(rank, port, q, accum=1, overlap=True):
             return model(x[:, k]).mean() / w
     # 4 KB buckets: the MWT's ~40 gradients go out in many all-reduces, issued from the
     # post-accumulate hooks while backward is still running
-    step = TrainStep(model, fl, opt, graph=False, bucket_mb=4 / 1024, accum_steps=accum, overlap=overlap)
+    step = TrainStep(model, fl, opt, graph=False, bucket_mb=4 / 1024, accum_steps=accum, overlap=overlap,
+                     grad_comm_dtype=comm)
     fired_in_backward = []
     orig_fire = step.buckets._fire
 
@@ -154,11 +156,11 @@ def _trainstep_worker(rank, port, q, accum=1, overlap=True):
     torch.distributed.destroy_process_group()
 
 
-def _run_trainstep(accum, overlap=True):
+def _run_trainstep(accum, overlap=True, comm=None):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_trainstep_worker, args=(r, port, q, accum, overlap)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_trainstep_worker, args=(r, port, q, accum, overlap, comm)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
@@ -197,6 +199,30 @@ def test_trainstep_gloo_world2_averages_gradients(overlap):
             torch.testing.assert_close(torch.from_numpy(res[r][1][n]), 0.5 * torch.from_numpy(res[r][0][n]),
                                        rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(torch.from_numpy(res[0][1][n]), torch.from_numpy(res[1][1][n]))
+
+
+@pytest.mark.parametrize('overlap', [True, False])
+def test_trainstep_gloo_world2_bf16_grad_allreduce(overlap):
+    """grad_comm_dtype=torch.bfloat16 (opt-in): the buckets are rounded to bf16,
+    all-reduced in bf16 and widened back into the fp32 buffer.  Equal to the fp32
+    DataParallel-semantics gradient within the bf16 rounding of each rank's gradient and of
+    the sum (relative 2^-7 of the gradient's scale), identical on both ranks."""
+    res = _run_trainstep(1, overlap, torch.bfloat16)
+    ref = _model()
+    x = _data()
+    outs = [ref(x[2 * r:2 * r + 2].flatten(0, 1)) for r in range(WORLD)]
+    torch.cat(outs).mean().backward()
+    worst = 0.0
+    # (a floor on the scale: a bias feeding a train-mode BatchNorm has an exactly zero true
+    # gradient, so its computed gradient is rounding noise in either dtype)
+    gmax = max(float(p.grad.abs().max()) for p in ref.parameters())
+    for n, p in ref.named_parameters():
+        scale = max(float(p.grad.abs().max()), 1e-3 * gmax)
+        for r in range(WORLD):
+            g = torch.from_numpy(res[r][0][n]) * WORLD
+            worst = max(worst, float((g - p.grad).abs().max()) / scale)
+        assert np.array_equal(res[0][0][n], res[1][0][n])
+    assert 0 < worst <= 2 ** -7, worst
 
 
 def test_trainstep_gloo_world2_grad_accumulation():

@@ -97,3 +97,59 @@ def test_frozen_parameter_gets_no_gradient():
     grads.begin_step()
     (_Scale.apply(x, w).sum() + _Scale.apply(x, w).sum()).backward()
     assert w.grad is None and x.grad is not None
+
+
+def _step(w, xs):
+    """One 'training step' as TrainStep runs it: begin_step, forward, backward, end_step."""
+    grads.begin_step()
+    try:
+        loss = sum((_Scale.apply(x, w) ** 2).sum() for x in xs)
+        loss.backward()
+    finally:
+        grads.end_step()
+
+
+def test_autograd_grad_after_a_step():
+    """After a step, an eager forward using w twice outside any step must not defer: the
+    gradient comes back from torch.autograd.grad and w.grad is left alone."""
+    torch.manual_seed(1)
+    w = torch.nn.Parameter(torch.randn(5))
+    xs = [torch.randn(3, 5) for _ in range(2)]
+    _step(w, xs)
+    w.grad = None
+    loss = sum((_Scale.apply(x, w) ** 2).sum() for x in xs)
+    (g,) = torch.autograd.grad(loss, [w])
+    w2 = torch.nn.Parameter(w.detach().clone())
+    ref = sum(((x * w2) ** 2).sum() for x in xs)
+    (gr,) = torch.autograd.grad(ref, [w2])
+    torch.testing.assert_close(g, gr, rtol=1e-6, atol=1e-6)
+    assert w.grad is None
+
+
+def test_eager_use_after_a_step_matches_autograd():
+    torch.manual_seed(2)
+    w = torch.nn.Parameter(torch.randn(5))
+    xs = [torch.randn(3, 5) for _ in range(3)]
+    _step(w, xs)
+    w.grad = None
+    (sum((_Scale.apply(x, w) ** 2).sum() for x in xs)).backward()
+    w2 = torch.nn.Parameter(w.detach().clone())
+    (sum(((x * w2) ** 2).sum() for x in xs)).backward()
+    torch.testing.assert_close(w.grad, w2.grad, rtol=1e-6, atol=1e-6)
+
+
+def test_multi_use_non_leaf_weight_reaches_its_leaf():
+    """A non-leaf weight (a DataParallel replica's, a cast copy) used twice in a step: its
+    gradient must flow back to the leaf, not be parked in the non-leaf's .grad."""
+    torch.manual_seed(3)
+    leaf = torch.nn.Parameter(torch.randn(6))
+    xs = [torch.randn(4, 6) for _ in range(2)]
+    grads.begin_step()
+    try:
+        w = leaf * 1.0
+        (sum((_Scale.apply(x, w) ** 2).sum() for x in xs)).backward()
+    finally:
+        grads.end_step()
+    leaf2 = torch.nn.Parameter(leaf.detach().clone())
+    (sum(((x * leaf2) ** 2).sum() for x in xs)).backward()
+    torch.testing.assert_close(leaf.grad, leaf2.grad, rtol=1e-6, atol=1e-6)

@@ -90,8 +90,26 @@ def main():
             L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, k, 1, gc, gs,
                    L.stream(y))
 
-        res = {}
+        dw = torch.empty((Cout, Cx, k, k), device=dev)
+        db = torch.empty(Cout, device=dev)
+        wsb = 0
         for v in (0, 1):
+            lib.ewvit_conv2d_set_win(v)
+            wsb = max(wsb, lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, 1))
+        lib.ewvit_conv2d_set_win(1)
+        wsp = torch.empty(wsb // 4 + 1, device=dev)
+
+        def wgrad():
+            L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), L.ptr(db), 0, N, H, W, Cx, Cout, k, 1,
+                   gc, gs, Cx, dw.stride(0), dw.stride(1), dw.stride(3), L.ptr(wsp), L.stream(y))
+
+        res = {}
+        wres = {}
+        for v in (0, 1):
+            lib.ewvit_conv2d_set_win(v)
+            wgrad()
+            torch.cuda.synchronize()
+            wres[v] = (dw.clone(), db.clone())
             lib.ewvit_conv2d_set_win(v)
             fwd()
             yf = y.clone()
@@ -120,6 +138,11 @@ def main():
                 bad += 1
         if not (ok_y and ok_d):
             bad += 1
+        ew = float((wres[0][0] - wres[1][0]).abs().max() / wres[0][0].abs().max())
+        eb = float((wres[0][1] - wres[1][1]).abs().max() / wres[0][1].abs().max())
+        msg += f' | wgrad rel {ew:.2e} bias rel {eb:.2e}'
+        if ew > 1e-5 or eb > 1e-5:
+            bad += 1
         print(msg, flush=True)
         if a.check_only or name.startswith('small'):
             continue
@@ -128,7 +151,7 @@ def main():
         for r in range(a.rounds):
             for v in (0, 1):
                 lib.ewvit_conv2d_set_win(v)
-                for pn, fn in (('fwd', fwd), ('fwd_bn', fwd_bn), ('dgrad', dgrad)):
+                for pn, fn in (('fwd', fwd), ('fwd_bn', fwd_bn), ('dgrad', dgrad), ('wgrad', wgrad)):
                     if pn == 'fwd_bn' and not use_bias:
                         continue
                     t.setdefault((v, pn), []).append(graph_time(fn, a.iters))
