@@ -51,10 +51,13 @@ constexpr int WW = WT + 2;                // window side
 constexpr int WPIX = WW * WW;             // 324 window pixels
 constexpr int WPIECES = (WPIX + 7) / 8;   // 41 LDS-DMA pieces of 8 pixels x 128 B
 constexpr int WIN_B = WPIECES * 1024;
-constexpr int NSLOT = 4;                  // weight ring slots (K-tiles)
+constexpr int NSLOT = 3;                  // weight ring slots (K-tiles): 9 taps = 3 rounds, so a
+                                          // tap's slot is T % 3 in every unit (immediate offsets)
 constexpr int SLOT_B = 128 * 128;         // 128 columns x 64 k, bf16
-constexpr int RING0 = 2 * WIN_B;
-constexpr int SMEM_B = RING0 + NSLOT * SLOT_B;   // 149,504 B: one workgroup per CU
+constexpr int VEC0 = NSLOT * SLOT_B;      // bias [128] + BN shift [128] floats
+constexpr int RED0 = VEC0 + 1024;         // BN statistics partials [4 row groups][128 cols][2]
+constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1]
+constexpr int SMEM_B = WIN0 + 2 * WIN_B;  // 138,240 B: one workgroup per CU
 }  // namespace
 
 // all LDS-DMA pieces except the N youngest landed, LDS reads drained, workgroup barrier
@@ -69,6 +72,36 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, uint2 v, uint
 __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, float v, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
+
+// LDS-DMA through inline asm.  With the builtin, hipcc tracks the pending LDS write and may
+// wait vmcnt(0) before a later LDS read (it does before every ds_read_b64_tr_b16 builtin of
+// the weight-gradient loop, and after any branch between the DMA and the reads) — draining
+// the loads that should stay in flight.  Every DMA here is counted by hand (s_waitcnt before
+// each barrier), so they are hidden from the compiler.  M0 (the DMA's LDS base) is reserved
+// to hipcc, which sets it before each of its own uses; no other M0 user runs in these kernels.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+// a buffer resource as four dwords (gfx9 layout: base, base_hi | stride << 16, num_records,
+// flags), so the asm operand can be pinned to SGPRs with readfirstlane (hipcc's divergence
+// analysis sometimes leaves uniform values in VGPRs, which an "s" operand then rejects)
+typedef __attribute__((ext_vector_type(4))) int ci32x4;
+__device__ __forceinline__ ci32x4 mk_rsrc4(const void *p, int64_t bytes) {
+  const uint32_t n = bytes >= (int64_t)OOB ? OOB : (uint32_t)bytes;
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return ci32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffff), (int)n, 0x00020000};
+}
+__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void glds16_asm(ci32x4 r, uint32_t lds, uint32_t voff) {
+  const ci32x4 rr = {__builtin_amdgcn_readfirstlane(r[0]), __builtin_amdgcn_readfirstlane(r[1]),
+                     __builtin_amdgcn_readfirstlane(r[2]), __builtin_amdgcn_readfirstlane(r[3])};
+  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(l), "v"(voff), "s"(rr)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
 
 // one unit = (tile, 64-channel block): 9 K-tiles, one per tap
 struct WinUnit {
@@ -97,23 +130,22 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   const int H = a.outH, W = a.outW;         // == srcH, srcW (stride 1)
   const int nbx = W / WT, nbl = (H / WT) * nbx;
   const int K = 9 * a.KC;
-  const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
-  const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
+  const ci32x4 rs = mk_rsrc4(a.src, src_bytes);
+  const ci32x4 rw = mk_rsrc4(a.wp, (int64_t)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t ro = mk_rsrc(a.out, out_bytes);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
 
   if (STATS && blockIdx.x == 0 && a.bn_shift_out)
     for (int c = tid; c < a.Ncol; c += 512) a.bn_shift_out[c] = a.bn_shift ? a.bn_shift[c] : 0.f;
-  // bias / BN shift of this lane's 16 columns, in registers (a bias or statistics epilogue
-  // needs Ncol == 128: one column tile).  Read from LDS in the epilogue they would make hipcc
-  // drain the LDS-DMA queue (vmcnt(0)) before the read, once per tile
-  float4 bias4[4], shift4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = wn * 64 + j * 16 + fq * 4;
-    bias4[j] = a.bias ? *reinterpret_cast<const float4 *>(a.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-    shift4[j] = (STATS && a.bn_shift) ? *reinterpret_cast<const float4 *>(a.bn_shift + col)
-                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  // bias / BN shift (a bias or statistics epilogue needs Ncol == 128: one column tile) in
+  // LDS, staged before any DMA; the epilogue reads them by inline asm (a compiler-visible LDS
+  // read there could be preceded by a vmcnt(0) drain of the DMA queue)
+  float *vec = reinterpret_cast<float *>(smem + VEC0);
+  if (tid < 128) {
+    vec[tid] = a.bias ? a.bias[tid] : 0.f;
+    vec[128 + tid] = (STATS && a.bn_shift) ? a.bn_shift[tid] : 0.f;
   }
+  __syncthreads();
 
   auto unit = [&](int u) -> WinUnit {
     WinUnit d;
@@ -148,54 +180,62 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   }
   // B(K-tile of unit d, weight tap rt) -> ring slot
   auto issue_b = [&](const WinUnit &d, int rt, int slot) {
-    unsigned char *dst = smem + RING0 + slot * SLOT_B + ws * 2048;
+    const uint32_t dst = lds0 + slot * SLOT_B + ws * 2048;
     const uint32_t base = (uint32_t)((d.n0 * K + rt * a.KC) * 2 + d.kb);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(rw, dst + j * 1024, d.ok ? base + brow[j] : OOB);
+    for (int j = 0; j < 2; ++j) glds16_asm(rw, dst + j * 1024, d.ok ? base + brow[j] : OOB);
   };
-  // window piece q (8 pixels) of unit d into window buffer wb.  The lane's pixel is
-  // q * 8 + lane / 8 and its source chunk (lane & 7) ^ (pixel & 7) — loop-invariant, since
-  // q * 8 keeps pixel & 7; the pixel's row / column are recomputed per issue (the empty asm
-  // keeps hipcc from hoisting six such sets out of the loop into spilled registers)
-  const int wlc8 = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+  // window piece q (8 pixels) of unit d into window buffer wb.  The lane's pixel is q * 8 +
+  // lane / 8 and its source chunk (lane & 7) ^ (pixel & 7) — loop-invariant (q * 8 keeps
+  // pixel & 7); the pixel's row / column are recomputed per issue with 24-bit multiplies (the
+  // empty asm keeps hipcc from hoisting the six sets out of the loop into spilled registers)
+  const int wlc16 = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
+  const uint32_t sgc2 = (uint32_t)a.sgc * 2;
   auto issue_w = [&](const WinUnit &d, int q, int wb) {
     int pl = lane >> 3;
     asm volatile("" : "+v"(pl));
-    const int p = q * 8 + pl;
-    const int wr = (p * 3641) >> 16;               // p / 18 for p < 328
-    const int wc = p - wr * WW;
-    const int ih = d.oh0 - 1 + wr, iw = d.ow0 - 1 + wc;
-    const bool ok = d.ok && p < WPIX && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-    const uint32_t off = d.wsrc + (uint32_t)(((wr * W + wc) * a.sgc + wlc8) * 2);
-    glds16(rs, smem + wb * WIN_B + q * 1024, ok ? off : OOB);
+    const uint32_t p = (uint32_t)(q * 8 + pl);
+    const uint32_t wr = __umul24(p, 3641u) >> 16;          // p / 18 for p < 328
+    const uint32_t wc = p - __umul24(wr, (uint32_t)WW);
+    const int ih = d.oh0 - 1 + (int)wr, iw = d.ow0 - 1 + (int)wc;
+    const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+    const uint32_t off = d.wsrc + __umul24(__umul24(wr, (uint32_t)W) + wc, sgc2) + (uint32_t)wlc16;
+    glds16_asm(rs, lds0 + WIN0 + wb * WIN_B + q * 1024, ok ? off : OOB);
   };
 
-  // fragment addresses.  A: window pixel (wm*4 + i) * 18 + fr + tap offset, chunk c at
-  // c ^ (pixel & 7); B: ring row wn*64 + j*16 + fr, chunk c at c ^ ((row >> 1) & 7) =
-  // c ^ ((fr >> 1) & 7) for every j, so the 4 column groups are immediate offsets.  The
-  // second k32 half (chunks + 4) is the same address with byte bit 6 flipped.
-  const int apix0 = wm * 4 * WW + fr;
-  const uint32_t bfo = (uint32_t)((wn * 64 + fr) * 128 + 16 * (fq ^ ((fr >> 1) & 7)));
+  // fragment addresses, no VALU in the loop.  A: window pixel p = p0 + c, p0 = (wm*4)*18 + fr,
+  // c = i*18 + tap offset (compile-time); chunk ch at ch ^ (p & 7) and p & 7 = (fr + c) & 7
+  // (72 = 0 mod 8), so a lane's address is atab[buffer][c & 7] + c * 128 (the k32 half 1 =
+  // chunks + 4: atab[(c + 4) & 7]).  B: ring row wn*64 + j*16 + fr, chunk ch at ch ^ ((fr >> 1)
+  // & 7) for every j; slot / j / half in the immediate.
+  uint32_t atab[2][8];
+  {
+    const int p0 = wm * 4 * WW + fr;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        atab[b][r] = lds0 + WIN0 + b * WIN_B + (uint32_t)(p0 * 128 + 16 * (fq ^ ((fr + r) & 7)));
+  }
+  const uint32_t bfo = lds0 + (uint32_t)((wn * 64 + fr) * 128 + 16 * (fq ^ ((fr >> 1) & 7)));
+  typedef __attribute__((address_space(3))) const cbf16x8 lds_frag;
+  auto ldsr = [&](uint32_t addr) -> cbf16x8 { return *reinterpret_cast<lds_frag *>((uintptr_t)addr); };
   cbf16x8 fa[2][4], fb[2][4];
-  // fragments of the K-tile (window buffer wb, tap rt, ring slot) into fa / fb
-  auto read_frags = [&](cbf16x8 (&xa)[2][4], cbf16x8 (&xb)[2][4], int wb, int rt, int slot) {
-    const int kh = rt / 3, kw = rt - kh * 3;
-    const int woff = DGRAD ? (2 - kh) * WW + (2 - kw) : kh * WW + kw;
-    int p0 = apix0;
-    asm volatile("" : "+v"(p0));
-    const unsigned char *wbase = smem + wb * WIN_B;
+  // fragments of the K-tile (window buffer WB, tap RT, ring slot SL) into xa / xb
+  auto read_frags = [&](auto WBc, auto RTc, auto SLc, cbf16x8 (&xa)[2][4], cbf16x8 (&xb)[2][4]) {
+    constexpr int WB = decltype(WBc)::value, RT = decltype(RTc)::value, SL = decltype(SLc)::value;
+    constexpr int kh = RT / 3, kw = RT % 3;
+    constexpr int woff = DGRAD ? (2 - kh) * WW + (2 - kw) : kh * WW + kw;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int p = p0 + i * WW + woff;
-      const uint32_t o = (uint32_t)(p * 128 + 16 * (fq ^ (p & 7)));
-      xa[0][i] = *reinterpret_cast<const cbf16x8 *>(wbase + o);
-      xa[1][i] = *reinterpret_cast<const cbf16x8 *>(wbase + (o ^ 64));
+      const int c = i * WW + woff;
+      xa[0][i] = ldsr(atab[WB][c & 7] + c * 128);
+      xa[1][i] = ldsr(atab[WB][(c + 4) & 7] + c * 128);
     }
-    const unsigned char *bb = smem + RING0 + slot * SLOT_B;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      xb[0][j] = *reinterpret_cast<const cbf16x8 *>(bb + bfo + j * 2048);
-      xb[1][j] = *reinterpret_cast<const cbf16x8 *>(bb + (bfo ^ 64) + j * 2048);
+      xb[0][j] = ldsr(bfo + SL * SLOT_B + j * 2048);
+      xb[1][j] = ldsr((bfo ^ 64) + SL * SLOT_B + j * 2048);
     }
   };
 
@@ -206,13 +246,20 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
   // tile epilogue: (+ bias) -> bf16, 16 stores per wave; STATS: one more store per wave
-  auto epilogue = [&](const WinUnit &d, int wb) {
+  auto epilogue = [&](const WinUnit &d, int wb) __attribute__((always_inline)) {
     float cs[4][4], cq[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int cl = wn * 64 + j * 16 + fq * 4;          // column in the tile
       const int col = d.n0 + cl;
-      const float4 bv = bias4[j], kv = shift4[j];
+      float4 bv, kv;
+      {
+        const uint32_t va = lds0 + VEC0 + (uint32_t)cl * 4;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bv) : "v"(va) : "memory");
+        if (STATS) asm volatile("ds_read_b128 %0, %1 offset:512\n\ts_waitcnt lgkmcnt(0)" : "=v"(kv) : "v"(va) : "memory");
+        else kv = make_float4(0.f, 0.f, 0.f, 0.f);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       const int gi = col / a.ogc;
       const int64_t cbase = (int64_t)gi * a.ogs + (col - gi * a.ogc);
 #pragma unroll
@@ -236,10 +283,10 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       }
     }
     if constexpr (STATS) {
-      // the 16 row lanes of each column (DPP), then the 4 row-group waves through LDS (the
-      // finished window buffer wb: every wave's reads of it completed before this K-tile's
-      // barrier, and the next DMA into it is issued after the next barrier)
-      float *red = reinterpret_cast<float *>(smem + wb * WIN_B);
+      // the 16 row lanes of each column (DPP) here; the 4 row-group waves' partials are
+      // summed after the NEXT K-tile's barrier (stats_flush), so this epilogue has no barrier
+      // of its own and the MFMAs of the next unit start right away
+      float *red = reinterpret_cast<float *>(smem + RED0);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -251,50 +298,83 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
             red[(wm * 128 + cl) * 2 + 1] = Q;
           }
         }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      const int v = tid & 255, cl = v >> 1, w = v & 1;
-      const float t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
-                      (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
-      // threads 256-511 store the same value to the same address: one store per wave
-      bstore32(mk_rsrc(a.bn_part, (int64_t)OOB), t,
-               (uint32_t)(((int64_t)d.part * 2 * a.Ncol + w * a.Ncol + d.n0 + cl) * 4));
     }
+    (void)wb;
   };
-  constexpr int ST = 16 + (STATS ? 1 : 0);   // vector-memory ops of one epilogue per wave
+  // the BN partial row of the tile whose epilogue ran last: one store per wave (threads
+  // 256-511 store the same value to the same address), after a barrier that every wave
+  // passed with its partials written (lgkmcnt(0))
+  int pend_part = 0, pend_n0 = 0;
+  const __amdgpu_buffer_rsrc_t rp = mk_rsrc(a.bn_part, (int64_t)OOB);
+  const int ncol = a.Ncol;
+  auto stats_flush = [&]() __attribute__((always_inline)) {
+    const float *red = reinterpret_cast<const float *>(smem + RED0);
+    const int v = tid & 255, cl = v >> 1, w = v & 1;
+    const float t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
+                    (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
+    bstore32(rp, t, (uint32_t)((pend_part * 2 * ncol + w * ncol + pend_n0 + cl) * 4));
+  };
+  constexpr int ST = 16;                     // output stores of one epilogue per wave
+  constexpr int SS = STATS ? 1 : 0;          // the statistics store (at the next unit's tap 0)
 
-  // ---- prologue: unit 0's window, K-tiles 0..3 of unit 0
+  // window pieces of the next unit: 2 per wave at taps 0-2 (48 slots for 41 pieces; the extra
+  // slots repeat piece 40), so a unit's window has landed long before its first read
+  constexpr int WPT = 2;
+  auto wpiece = [&](int T, int jj) { const int q = (T * 8 + ws) * WPT + jj; return q < WPIECES ? q : WPIECES - 1; };
+
+  // ---- prologue: unit 0's window (all pieces), K-tiles 0..2 of unit 0
   WinUnit cu = unit(0), nx = unit(1);
 #pragma unroll
-  for (int t = 0; t < 6; ++t) issue_w(cu, t * 8 + ws < WPIECES ? t * 8 + ws : WPIECES - 1, 0);
+  for (int t = 0; t < 3; ++t)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) issue_b(cu, t, t);
-  win_sync<6>();                            // window 0 and K-tile 0 landed (B 1..3 in flight)
-  read_frags(fa, fb, 0, 0, 0);
+    for (int jj = 0; jj < WPT; ++jj) issue_w(cu, wpiece(t, jj), 0);
+#pragma unroll
+  for (int t = 0; t < 3; ++t) issue_b(cu, t, t);
+  win_sync<4>();                            // window 0 and K-tile 0 landed (B 1, 2 in flight)
+  read_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+             fa, fb);
   bool prev_st = false;                     // the previous unit ended a tile (its stores are in flight)
 
-  for (int u = 0; u < nu; ++u) {
-    const int wbuf = u & 1;
-    // one K-tile: wait for K-tile i+1, issue window piece (taps 0-5) and K-tile i+4,
-    // read K-tile i+1's fragments, multiply K-tile i
+  // one unit (window buffer WB): 9 K-tiles.  K-tile i: wait for K-tile i+1 (and its
+  // window), issue the next unit's window pieces (taps 0-2) and K-tile i+3 into slot i % 3,
+  // read K-tile i+1's fragments, multiply K-tile i
+  auto unit_body = [&](auto WBc) {
+    constexpr int WB = decltype(WBc)::value;
     auto step = [&](auto TT) {
       constexpr int T = decltype(TT)::value;
-      // vector-memory ops younger than K-tile i+1's pieces: the window pieces and weight
-      // K-tiles of iterations i-2, i-1, and the epilogue stores of the previous unit's tap
-      // 8 (iterations i-3 .. i-1 for T = 2, 1, 0)
-      constexpr int NB = 4 + (((T + 7) % 9) < 6 ? 1 : 0) + (((T + 8) % 9) < 6 ? 1 : 0);
-      if constexpr (T <= 2) {
-        if (prev_st) win_sync<NB + ST>();
+      // (the address tables re-enter every step: else hipcc hoists every (tap, i) address sum
+      // out of the loop into registers it then spills)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(atab[0][r]), "+v"(atab[1][r]));
+      // vector-memory ops younger than K-tile i+1's pieces (issued at i-2): iteration i-1's
+      // window pieces + weight K-tile, and the previous unit's epilogue stores (tap 8) for
+      // T = 0, 1
+      // (+ the output stores of the previous unit's tap 8 for T = 0, 1 and its statistics
+      // store, issued at this unit's tap 0, for T = 1, 2)
+      constexpr int NB = 2 + (((T + 8) % 9) < 3 ? WPT : 0);
+      constexpr int X = (T <= 1 ? ST : 0) + ((T == 1 || T == 2) ? SS : 0);
+      if constexpr (X > 0) {
+        if (prev_st) win_sync<NB + X>();
         else win_sync<NB>();
       } else {
         win_sync<NB>();
       }
-      if constexpr (T < 6) issue_w(nx, T * 8 + ws < WPIECES ? T * 8 + ws : WPIECES - 1, wbuf ^ 1);
-      const int slot = (u + T) & 3;          // K-tile i = 9u + T; slot(i) == slot(i + 4)
-      if constexpr (T + 4 < 9) issue_b(cu, T + 4, slot);
-      else issue_b(nx, T + 4 - 9, slot);
+      if constexpr (T < 3) {
+#pragma unroll
+        for (int jj = 0; jj < WPT; ++jj) issue_w(nx, wpiece(T, jj), WB ^ 1);
+      }
+      if constexpr (T + 3 < 9) issue_b(cu, T + 3, T % 3);
+      else issue_b(nx, T + 3 - 9, T % 3);
+      if constexpr (STATS && T == 0) {
+        if (prev_st) stats_flush();
+      }
       cbf16x8 na[2][4], nb[2][4];
-      if constexpr (T + 1 < 9) read_frags(na, nb, wbuf, T + 1, (slot + 1) & 3);
-      else read_frags(na, nb, wbuf ^ 1, 0, (slot + 1) & 3);
+      if constexpr (T + 1 < 9)
+        read_frags(std::integral_constant<int, WB>{}, std::integral_constant<int, T + 1>{},
+                   std::integral_constant<int, (T + 1) % 3>{}, na, nb);
+      else
+        read_frags(std::integral_constant<int, WB ^ 1>{}, std::integral_constant<int, 0>{},
+                   std::integral_constant<int, 0>{}, na, nb);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -308,7 +388,11 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         for (int q = 0; q < 4; ++q) { fa[ks][q] = na[ks][q]; fb[ks][q] = nb[ks][q]; }
       if constexpr (T == 8) {
         prev_st = cu.last;
-        if (cu.last) epilogue(cu, wbuf);
+        if (cu.last) {
+          epilogue(cu, WB);
+          pend_part = cu.part;
+          pend_n0 = cu.n0;
+        }
       }
     };
     step(std::integral_constant<int, 0>{});
@@ -320,8 +404,19 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     step(std::integral_constant<int, 6>{});
     step(std::integral_constant<int, 7>{});
     step(std::integral_constant<int, 8>{});
+  };
+  for (int u = 0; u < nu; u += 2) {
+    unit_body(std::integral_constant<int, 0>{});
     cu = nx;
     nx = unit(u + 2);
+    if (u + 1 >= nu) break;
+    unit_body(std::integral_constant<int, 1>{});
+    cu = nx;
+    nx = unit(u + 3);
+  }
+  if constexpr (STATS) {                    // the last tile's statistics
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stats_flush();
   }
   // no LDS-DMA may land after the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -385,19 +480,6 @@ constexpr int GSMEM = GD0 + 2 * GD_B;              // 90,112 B
 // 64-B window rows: chunk c of pixel p at c ^ (((p >> 3) & 1) << 1)
 __device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
 
-// LDS-DMA through inline asm: the weight-gradient loop reads its operands with the
-// ds_read_b64_tr_b16 builtin, and hipcc, seeing a pending LDS-DMA (builtin) write, waits
-// vmcnt(0) before the first such read after it — draining the next tile's loads before this
-// tile's MFMAs.  The DMAs here are all counted by hand (s_waitcnt before each barrier), so
-// they are hidden from the compiler.  M0 (the DMA's LDS base) is reserved to hipcc, which
-// sets it before each of its own uses; no other M0 user runs in this kernel.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
-               : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 template <bool BIAS>
 __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb, int nct,

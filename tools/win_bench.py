@@ -25,6 +25,9 @@ SHAPES = {
 }
 
 
+VARIANTS = (0, 1)      # ewvit_conv2d_set_win: generic LDS-DMA, windowed
+
+
 def graph_time(fn, iters):
     for _ in range(2):
         fn()
@@ -50,6 +53,9 @@ def main():
     ap.add_argument('--only', default=None)
     ap.add_argument('--check-only', action='store_true')
     ap.add_argument('--cap', type=int, default=0, help='grid cap for the timed launches')
+    ap.add_argument('--profile', default=None, help='fwd|fwd_bn|dgrad|wgrad: only run that phase 5x eagerly per '
+                    'variant in --variants (rocprofv3 passes)')
+    ap.add_argument('--variants', default=None, help='comma list of ewvit_conv2d_set_win variants for --profile')
     a = ap.parse_args()
     import ewvit  # noqa: F401
     from ewvit import _lib as L
@@ -103,6 +109,16 @@ def main():
             L.call('ewvit_conv2d_bwd_weight', L.ptr(z), L.ptr(dy), L.ptr(dw), L.ptr(db), 0, N, H, W, Cx, Cout, k, 1,
                    gc, gs, Cx, dw.stride(0), dw.stride(1), dw.stride(3), L.ptr(wsp), L.stream(y))
 
+        if a.profile:
+            fn = dict(fwd=fwd, fwd_bn=fwd_bn, dgrad=dgrad, wgrad=wgrad)[a.profile]
+            for v in ([int(x) for x in a.variants.split(',')] if a.variants else [1]):
+                lib.ewvit_conv2d_set_win(v)
+                for _ in range(5):
+                    fn()
+                torch.cuda.synchronize()
+            lib.ewvit_conv2d_set_win(1)
+            print(f'{name}: profiled {a.profile}', flush=True)
+            continue
         res = {}
         wres = {}
         for v in (0, 1):
@@ -149,7 +165,7 @@ def main():
         t = {}
         prev_cap = lib.ewvit_set_grid_cap(a.cap)
         for r in range(a.rounds):
-            for v in (0, 1):
+            for v in VARIANTS:
                 lib.ewvit_conv2d_set_win(v)
                 for pn, fn in (('fwd', fwd), ('fwd_bn', fwd_bn), ('dgrad', dgrad), ('wgrad', wgrad)):
                     if pn == 'fwd_bn' and not use_bias:
@@ -157,10 +173,10 @@ def main():
                     t.setdefault((v, pn), []).append(graph_time(fn, a.iters))
         lib.ewvit_set_grid_cap(prev_cap)
         lib.ewvit_conv2d_set_win(1)
-        for v in (0, 1):
+        for v in VARIANTS:
             parts = [f'{pn} {min(ts):8.1f} us {flops / min(ts) / 1e6:6.0f} TF/s'
                      for (vv, pn), ts in t.items() if vv == v]
-            print(f'{name:15s} [{"win " if v else "glds"}] ' + ' | '.join(parts), flush=True)
+            print(f'{name:15s} [{("glds", "win ")[v]}] ' + ' | '.join(parts), flush=True)
     print('FAILURES', bad if bad else 'none', flush=True)
     sys.exit(1 if bad else 0)
 
