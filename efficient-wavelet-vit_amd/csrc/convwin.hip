@@ -54,8 +54,9 @@ constexpr int WIN_B = WPIECES * 1024;
 constexpr int NSLOT = 3;                  // weight ring slots (K-tiles): 9 taps = 3 rounds, so a
                                           // tap's slot is T % 3 in every unit (immediate offsets)
 constexpr int SLOT_B = 128 * 128;         // 128 columns x 64 k, bf16
-constexpr int VEC0 = NSLOT * SLOT_B;      // bias [128] + BN shift [128] floats
-constexpr int RED0 = VEC0 + 1024;         // BN statistics partials [4 row groups][128 cols][2]
+constexpr int VEC_N = 512;                // bias / BN shift entries (Ncol <= 512 with either)
+constexpr int VEC0 = NSLOT * SLOT_B;      // bias [512] + BN shift [512] floats
+constexpr int RED0 = VEC0 + 2 * VEC_N * 4; // BN statistics partials [4 row groups][128 cols][2]
 constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1]
 constexpr int SMEM_B = WIN0 + 2 * WIN_B;  // 138,240 B: one workgroup per CU
 }  // namespace
@@ -137,14 +138,16 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 
   if (STATS && blockIdx.x == 0 && a.bn_shift_out)
     for (int c = tid; c < a.Ncol; c += 512) a.bn_shift_out[c] = a.bn_shift ? a.bn_shift[c] : 0.f;
-  // bias / BN shift (a bias or statistics epilogue needs Ncol == 128: one column tile) in
-  // LDS, staged before any DMA; the epilogue reads them by inline asm (a compiler-visible LDS
-  // read there could be preceded by a vmcnt(0) drain of the DMA queue)
+  // bias / BN shift (Ncol <= 512 when either is used) in LDS, staged before any DMA; the
+  // epilogue reads them by inline asm (a compiler-visible LDS read there could be preceded by
+  // a vmcnt(0) drain of the DMA queue)
   float *vec = reinterpret_cast<float *>(smem + VEC0);
-  if (tid < 128) {
-    vec[tid] = a.bias ? a.bias[tid] : 0.f;
-    vec[128 + tid] = (STATS && a.bn_shift) ? a.bn_shift[tid] : 0.f;
-  }
+  const bool has_bias = a.bias != nullptr;   // (Ncol may exceed VEC_N without bias / statistics)
+  if (a.bias || STATS)
+    for (int c = tid; c < a.Ncol && c < VEC_N; c += 512) {
+      vec[c] = a.bias ? a.bias[c] : 0.f;
+      vec[VEC_N + c] = (STATS && a.bn_shift) ? a.bn_shift[c] : 0.f;
+    }
   __syncthreads();
 
   auto unit = [&](int u) -> WinUnit {
@@ -254,9 +257,10 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       const int col = d.n0 + cl;
       float4 bv, kv;
       {
-        const uint32_t va = lds0 + VEC0 + (uint32_t)cl * 4;
-        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bv) : "v"(va) : "memory");
-        if (STATS) asm volatile("ds_read_b128 %0, %1 offset:512\n\ts_waitcnt lgkmcnt(0)" : "=v"(kv) : "v"(va) : "memory");
+        const uint32_t va = lds0 + VEC0 + (uint32_t)col * 4;
+        if (has_bias) asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bv) : "v"(va) : "memory");
+        else bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (STATS) asm volatile("ds_read_b128 %0, %1 offset:2048\n\ts_waitcnt lgkmcnt(0)" : "=v"(kv) : "v"(va) : "memory");
         else kv = make_float4(0.f, 0.f, 0.f, 0.f);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -427,7 +431,7 @@ bool win_ok(const FwdArgs &a, bool dgrad) {
   if (dgrad && a.bn_part) return false;
   if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
   if (a.KC % 64 || a.sgc % 64 || (a.KCr && a.KCr != a.KC)) return false;
-  if (a.Ncol % 128 || a.ogc % 128 || ((a.bias || a.bn_part) && a.Ncol != 128)) return false;
+  if (a.Ncol % 128 || a.ogc % 128 || ((a.bias || a.bn_part) && a.Ncol > VEC_N)) return false;
   if (a.M != (int64_t)a.g.N * a.outH * a.outW) return false;
   const int64_t K = 9LL * a.KC;
   if (a.Ncol * K * 2 >= (int64_t)OOB) return false;

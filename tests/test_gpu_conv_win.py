@@ -52,7 +52,7 @@ def _run(lib, L, win, cap, z, wp, wpt, bias, dy, shift, N, H, W, Cx, Cout, gc, g
     (4, 64, 32, 32, 128, 2, 5),       # 2 levels, persistent walk (cap 5 -> 8 workgroups, 16 tiles)
     (1, 128, 48, 16, 64, 1, 0),       # 64-channel output: forward on the generic kernel, dgrad windowed
     (2, 256, 32, 32, 128, 1, 16),     # 4 channel blocks, capped
-    (1, 128, 16, 16, 256, 3, 0),      # 256 outputs (no bias / stats on the window: generic fwd), dgrad 3 x 128 cols
+    (1, 128, 16, 16, 256, 3, 0),      # 2 column tiles with bias + statistics (config 4), dgrad 3 x 128 cols
 ])
 def test_window_bit_identical(N, Cin, H, W, Cout, levels, cap):
     import ewvit
@@ -69,7 +69,7 @@ def test_window_bit_identical(N, Cin, H, W, Cout, levels, cap):
     shift = (torch.randn(Cout, generator=g) * 0.1).to(DEV)
     gc, gs = (Cin, N * H * W * Cin) if levels > 1 else (0, 0)
     wp, wpt = _pack(w, Cx, True, True)
-    stats = Cout == 128
+    stats = Cout in (128, 256)
     y0, d0, s0 = _run(lib, L, 0, cap, z, wp, wpt, bias, dy, shift, N, H, W, Cx, Cout, gc, gs, stats)
     y1, d1, s1 = _run(lib, L, 1, cap, z, wp, wpt, bias, dy, shift, N, H, W, Cx, Cout, gc, gs, stats)
     assert torch.equal(y0, y1), float((y0.float() - y1.float()).abs().max())

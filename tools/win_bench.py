@@ -82,7 +82,7 @@ def main():
         M = N * H * W
         part = torch.empty((M + 127) // 128, 2 * Cout, device=dev)
         flops = 2.0 * M * Cout * k * k * Cx
-        use_bias = Cout == 128
+        use_bias = Cout <= 512
 
         def fwd():
             L.call('ewvit_conv2d_fwd', L.ptr(z), L.ptr(wp), L.ptr(bias) if use_bias else None, L.ptr(y), N, H, W,
