@@ -1201,6 +1201,121 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
   }
 }
 
+// 1x1 stride-1 weight gradient over a plain NHWC x (the backbone's MBConv expand / project and
+// head convs, sfe.py:111-113): dW[co][ci] = sum_m dy[m][co] * x[m][ci] with no pixel map, so a
+// staging lane's global offset is one register advanced by a scalar stride per K-tile (lanes
+// past Cout / Cin start at OOB and stay there; rows >= M fall past the buffer's end and read
+// zeros) — none of the generic kernel's per-piece address math; the DMAs are asm (glds16_asm),
+// so hipcc does not drain them before the fragment reads.  128 x 128 output tile, 4 waves
+// of 64 x 64, 64-pixel K-tiles in an NS-deep LDS-DMA ring; a K-tile's fragments for both
+// 32-pixel steps are read before its MFMAs, so the second step's reads overlap the first
+// step's MFMAs.  Leaves [splits][Cout][Cin] slabs (conv_wgrad_reduce_kernel), or dW itself for
+// one split.
+template <int NS>
+__global__ __launch_bounds__(256) void conv_wgrad_1x1_kernel(WgradArgs a, int ntx, int nty) {
+  constexpr int BK = 64, IMG = BK * 256, STG = 2 * IMG, P = BK / 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = tile / (ntx * nty);
+  const int tx = tile % ntx, ty = (tile / ntx) % nty;
+  const int co0 = ty * 128, ci0 = tx * 128;
+  const int Cout = a.g.Cout, Cin = a.g.Cin;
+  const int64_t mbeg = (int64_t)split * a.mper;
+  const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
+  const int nk = (int)((mend - mbeg + BK - 1) / BK);
+  const __amdgpu_buffer_rsrc_t rx = mk_rsrc(a.x, a.M * Cin * 2);
+  const __amdgpu_buffer_rsrc_t rd = mk_rsrc(a.dy, a.M * Cout * 2);
+  const int ws = __builtin_amdgcn_readfirstlane(w);
+  const int wm = ws >> 1, wn = ws & 1;
+  // piece j of wave ws: rows 16 ws + 4 j + lane / 16, source chunk (lane % 16) ^ swz(row)
+  uint32_t aoff[P], boff[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int r = ws * 16 + 4 * j + (lane >> 4);
+    const int lc = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    aoff[j] = co0 + lc * 8 < Cout ? (uint32_t)(((mbeg + r) * Cout + co0 + lc * 8) * 2) : OOB;
+    boff[j] = ci0 + lc * 8 < Cin ? (uint32_t)(((mbeg + r) * Cin + ci0 + lc * 8) * 2) : OOB;
+  }
+  const uint32_t adel = (uint32_t)(BK * Cout * 2), bdel = (uint32_t)(BK * Cin * 2);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem + ws * P * 1024;
+  auto stage = [&](int buf) __attribute__((always_inline)) {
+    const uint32_t base = lds0 + buf * STG;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      glds16_asm(rd, base + j * 1024, aoff[j]);
+      glds16_asm(rx, base + IMG + j * 1024, boff[j]);
+      aoff[j] += adel;
+      boff[j] += bdel;
+    }
+  };
+  auto tr_read = [&](const unsigned char *img, int k0, int c0) __attribute__((always_inline)) -> cs4 {
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = c0 + 4 * p;
+    const int off = swz_off(k0 + q, col >> 3) + 2 * (col & 7);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) cs4 *)(img + off));
+  };
+  cf32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const unsigned char *As = smem + buf * STG, *Bs = As + IMG;
+    cbf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const cs4 alo = tr_read(As, ks * 32 + 8 * g, wm * 64 + i * 16);
+        const cs4 ahi = tr_read(As, ks * 32 + 8 * g + 4, wm * 64 + i * 16);
+        af[ks][i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                     alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]});
+        const cs4 blo = tr_read(Bs, ks * 32 + 8 * g, wn * 64 + i * 16);
+        const cs4 bhi = tr_read(Bs, ks * 32 + 8 * g + 4, wn * 64 + i * 16);
+        bfr[ks][i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                      blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]});
+      }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+  };
+  int ld = 0, lbuf = 0;
+  for (; ld < NS - 1 && ld < nk; ++ld) {
+    stage(lbuf);
+    lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+  }
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tile<2 * P, NS>(nk - 1 - kt);
+    if (ld < nk) {
+      stage(lbuf);
+      ++ld;
+      lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
+    }
+    compute(cur);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  float *dst = a.part + (int64_t)split * Cout * Cin;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = ci0 + wn * 64 + j * 16 + (lane & 15);
+    if (col >= Cin) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < Cout) dst[(int64_t)row * Cin + col] = acc[i][j][r];
+      }
+  }
+}
+
 // Kernel family: 1 (default) the LDS-DMA kernels wherever the shape allows them, the
 // register-staged kernels elsewhere; 0 the register-staged kernels everywhere — a test
 // switch (ewvit_conv2d_set_glds): they are the fallback of the shapes the LDS-DMA kernels
@@ -1845,6 +1960,34 @@ static int64_t wgrad_splits(const ConvGeom &g, int wide = 0) {
   return s;
 }
 
+// the 1x1 kernel (conv_wgrad_1x1_kernel): plain NHWC x, stride 1, no bias gradient; splits for
+// ~g_w1_wg workgroups with >= g_w1_minkt K-tiles of 64 pixels each, slabs <= 4x the operands
+// (256 / 8 / 2-deep ring: stage-6 expand 22.2 -> 18.4 us, stage-5 23.7 -> 19.2 us, stage-4
+// 26.6 -> 22.7 us against the generic kernel, profiles/r05/ab/wgrad1x1_kernel.log).
+// ewvit_conv2d_set_wgrad_1x1 (test / tuning): workgroup target (0 = never), min K-tiles, ring.
+static int g_w1_wg = 256, g_w1_minkt = 8, g_w1_ring = 2;
+static bool w1x1_ok(const ConvGeom &g, int64_t x_group_stride, bool has_bias, int64_t M) {
+  return g_w1_wg > 0 && g.ks == 1 && g.stride == 1 && x_group_stride == 0 && !has_bias &&
+         M * g.Cin * 2 < (int64_t)OOB / 2 && M * g.Cout * 2 < (int64_t)OOB / 2;
+}
+static int64_t w1x1_splits(const ConvGeom &g) {
+  const int64_t M = (int64_t)g.N * g.Ho * g.Wo;
+  const int64_t tiles = ((g.Cin + CBN - 1) / CBN) * ((g.Cout + CBM - 1) / CBM);
+  int64_t s = g_w1_wg / tiles;
+  const int64_t maxs = ((M + 63) / 64) / g_w1_minkt;
+  if (s > maxs) s = maxs;
+  const int64_t cap = 2 * M * ((int64_t)g.Cin + g.Cout) / ((int64_t)g.Cout * g.Cin);
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : s;
+}
+extern "C" int ewvit_conv2d_set_wgrad_1x1(int target_wg, int min_ktiles, int ring) {
+  const int prev = g_w1_wg;
+  g_w1_wg = target_wg;
+  g_w1_minkt = min_ktiles >= 1 ? min_ktiles : 4;
+  g_w1_ring = ring == 2 ? 2 : 3;
+  return prev;
+}
+
 extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {
   const int prev = g_wgw;
   g_wgw = variant == 0 || variant == 2 ? variant : 4;
@@ -1869,6 +2012,10 @@ extern "C" int64_t ewvit_conv2d_bwd_weight_workspace(int64_t N, int64_t H, int64
   const int64_t narrow = wgrad_splits(g) * Cout * (ksize * ksize * Cin + ntx) * (int64_t)sizeof(float);
   const int wide = wgrad_wide(g);
   int64_t need = narrow > winb ? narrow : winb;
+  if (w1x1_ok(g, 0, false, (int64_t)N * H * W)) {
+    const int64_t w1 = w1x1_splits(g) * Cout * Cin * (int64_t)sizeof(float);
+    if (w1 > need) need = w1;
+  }
   if (!wide) return need;
   const int64_t ntw = (ksize * ksize * Cin + 2 * CBN - 1) / (2 * CBN);
   const int64_t wb = wgrad_splits(g, wide) * Cout * (ksize * ksize * Cin + ntw) * (int64_t)sizeof(float);
@@ -1910,6 +2057,34 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
     const int64_t nbias = dbias ? (g.Cout + 63) / 64 : 0;
     hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,
                        g.Cout, g.Cin, taps, wsp, wsp, accumulate, a.dbias_part, dbias, wo, T, (int)nmain);
+    return launch_status("conv2d_bwd_weight reduce");
+  }
+  if (glds && w1x1_ok(g, x_group_stride, dbias != nullptr, a.M)) {
+    // the 1x1 kernel: K-tile-aligned splits, slabs + the reduce pass (or dW itself, one split)
+    EWVIT_CHECK_ARG(dw_cin > 0 && dw_cin <= Cin, "conv2d_bwd_weight: dw_cin %lld not in (0, %lld]", (long long)dw_cin,
+                    (long long)Cin);
+    const int ntx = (g.Cin + CBN - 1) / CBN, nty = (g.Cout + CBM - 1) / CBM;
+    const int64_t sp0 = w1x1_splits(g);
+    int64_t mper = (a.M + sp0 - 1) / sp0;
+    a.mper = (mper + 63) / 64 * 64;
+    const int sp = (int)((a.M + a.mper - 1) / a.mper);
+    a.dbias_part = nullptr;
+    const bool direct = sp == 1 && !accumulate && dw_cin == Cin && dw_s_ci == 1 && dw_s_co == Cin;
+    a.part = direct ? dw : workspace;
+    hipStream_t s = as_stream(stream);
+    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
+    if (g_w1_ring == 2) hipLaunchKernelGGL(conv_wgrad_1x1_kernel<2>, dim3(nwg), dim3(256), 0, s, a, ntx, nty);
+    else hipLaunchKernelGGL(conv_wgrad_1x1_kernel<3>, dim3(nwg), dim3(256), 0, s, a, ntx, nty);
+    if (int rc = launch_status("conv2d_bwd_weight (1x1)")) return rc;
+    if (direct) return 0;
+    WOut wo;
+    wo.s_co = dw_s_co; wo.s_ci = dw_s_ci; wo.s_tap = dw_s_tap; wo.cin = (int)dw_cin;
+    const int64_t n4 = (int64_t)g.Cout * g.Cin / 4;
+    int T = 1;
+    while (T < 64 && T * 2 <= sp && n4 * T * 2 <= 65536) T *= 2;
+    const int64_t nmain = (n4 * T + 255) / 256;
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)nmain), dim3(256), 0, s, workspace, dw, g.Cout,
+                       g.Cin, 1, sp, 0, accumulate, nullptr, nullptr, wo, T, (int)nmain);
     return launch_status("conv2d_bwd_weight reduce");
   }
   const int wide = glds ? wgrad_wide(g) : 0;

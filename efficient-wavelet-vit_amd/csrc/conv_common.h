@@ -88,6 +88,35 @@ template <int L, int NS> __device__ __forceinline__ void wait_tile(int rem) {
   wait_vm_barrier<0>();
 }
 
+// LDS-DMA issued from inline asm: hipcc cannot see these, so it neither waits on them before
+// LDS reads (it drains the whole vmcnt queue ahead of any LDS access that may alias a builtin
+// DMA) nor counts them; every kernel using them waits with explicit vmcnt counts (wait_tile,
+// win_sync).  M0 (the DMA's LDS base) is reserved to hipcc, which sets it before each of its
+// own uses; no other M0 user runs in these kernels.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+// a buffer resource as four dwords (gfx9 layout: base, base_hi | stride << 16, num_records,
+// flags), so the asm operand can be pinned to SGPRs with readfirstlane (hipcc's divergence
+// analysis sometimes leaves uniform values in VGPRs, which an "s" operand then rejects)
+typedef __attribute__((ext_vector_type(4))) int ci32x4;
+__device__ __forceinline__ ci32x4 mk_rsrc4(const void *p, int64_t bytes) {
+  const uint32_t n = bytes >= (int64_t)OOB ? OOB : (uint32_t)bytes;
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return ci32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffff), (int)n, 0x00020000};
+}
+__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void glds16_asm(ci32x4 r, uint32_t lds, uint32_t voff) {
+  const ci32x4 rr = {__builtin_amdgcn_readfirstlane(r[0]), __builtin_amdgcn_readfirstlane(r[1]),
+                     __builtin_amdgcn_readfirstlane(r[2]), __builtin_amdgcn_readfirstlane(r[3])};
+  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(l), "v"(voff), "s"(rr)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 // ---------------------------------------------------------------- wgrad
 // A(co, m) = dy[m][co]   -> image Ast[m][co]  (rows of 128 co = 256 B)
 // B(m, n') = x[pix(m,tap)][ci] -> image Bst[m][n'] (rows of 128 n' = 256 B)

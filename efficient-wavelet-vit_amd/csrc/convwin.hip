@@ -74,35 +74,9 @@ __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, float v, uint
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
 
-// LDS-DMA through inline asm.  With the builtin, hipcc tracks the pending LDS write and may
-// wait vmcnt(0) before a later LDS read (it does before every ds_read_b64_tr_b16 builtin of
-// the weight-gradient loop, and after any branch between the DMA and the reads) — draining
-// the loads that should stay in flight.  Every DMA here is counted by hand (s_waitcnt before
-// each barrier), so they are hidden from the compiler.  M0 (the DMA's LDS base) is reserved
-// to hipcc, which sets it before each of its own uses; no other M0 user runs in these kernels.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-// a buffer resource as four dwords (gfx9 layout: base, base_hi | stride << 16, num_records,
-// flags), so the asm operand can be pinned to SGPRs with readfirstlane (hipcc's divergence
-// analysis sometimes leaves uniform values in VGPRs, which an "s" operand then rejects)
-typedef __attribute__((ext_vector_type(4))) int ci32x4;
-__device__ __forceinline__ ci32x4 mk_rsrc4(const void *p, int64_t bytes) {
-  const uint32_t n = bytes >= (int64_t)OOB ? OOB : (uint32_t)bytes;
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  return ci32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffff), (int)n, 0x00020000};
-}
-__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
-               : "memory", "m0");
-}
-__device__ __forceinline__ void glds16_asm(ci32x4 r, uint32_t lds, uint32_t voff) {
-  const ci32x4 rr = {__builtin_amdgcn_readfirstlane(r[0]), __builtin_amdgcn_readfirstlane(r[1]),
-                     __builtin_amdgcn_readfirstlane(r[2]), __builtin_amdgcn_readfirstlane(r[3])};
-  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(l), "v"(voff), "s"(rr)
-               : "memory", "m0");
-}
-#pragma clang diagnostic pop
+// LDS-DMA through inline asm (conv_common.h glds16_asm): with the builtin, hipcc waits vmcnt(0)
+// before every ds_read_b64_tr_b16 of the weight-gradient loop and after any branch between the
+// DMA and the reads, draining the loads that should stay in flight.
 
 // one unit = (tile, 64-channel block): 9 K-tiles, one per tap
 struct WinUnit {

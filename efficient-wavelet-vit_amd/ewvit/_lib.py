@@ -57,6 +57,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
+    'ewvit_conv2d_set_wgrad_1x1': [_i32, _i32, _i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,

@@ -379,6 +379,10 @@ int ewvit_conv2d_set_win(int variant);
  * 128-column tiles; 2 = 256-column tiles whenever n' >= 256 and the last tile wastes <= 1/8 of
  * it; 0 = never.  Returns the previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_wgrad_wide(int variant);
+/* The 1x1 stride-1 weight-gradient kernel (plain NHWC x, no bias gradient): workgroup target of
+ * its pixel splits (0 = never: the generic kernel), fewest 64-pixel K-tiles per split, LDS ring
+ * depth (2 | 3).  Test / tuning switch; returns the previous target. */
+int ewvit_conv2d_set_wgrad_1x1(int target_wg, int min_ktiles, int ring);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs

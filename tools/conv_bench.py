@@ -73,11 +73,17 @@ def main():
                     '+100*w: 256-column wgrad tiles of variant w (e.g. 209)')
     ap.add_argument('--ww', default=None, help='wide-wave fwd/dgrad variants to time per kernel family (ewvit_conv2d_set_ww), e.g. 0,1,2,3')
     ap.add_argument('--bnstats', action='store_true', help='time fwd against fwd with BN statistics in the epilogue')
+    ap.add_argument('--w1', default=None, help='1x1 wgrad kernel settings to time (ewvit_conv2d_set_wgrad_1x1), '
+                    'target_wg:min_ktiles:ring pairs, e.g. 0:4:3,256:4:3,128:4:3 (wgrad only)')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
     a.variants = [int(v) for v in a.variants.split(',')]
+    w1 = None
+    if a.w1:
+        w1 = [tuple(int(q) for q in t.split(':')) for t in a.w1.split(',')]
+        a.variants = [1 + 10000 * i for i in range(len(w1))]
     if a.ww is not None:      # variant v + 1000 * ww
         a.variants = [v + 1000 * int(w) for v in a.variants for w in a.ww.split(',')]
     import ewvit
@@ -105,7 +111,10 @@ def main():
         wsb = 0
         for wv in range(5):                    # largest workspace over the wgrad tile widths
             lib.ewvit_conv2d_set_wgrad_wide(wv)
-            wsb = max(wsb, lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s))
+            for t in (w1 or [(256, 4, 3)]):
+                lib.ewvit_conv2d_set_wgrad_1x1(*t)
+                wsb = max(wsb, lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s))
+        lib.ewvit_conv2d_set_wgrad_1x1(256, 4, 3)
         lib.ewvit_conv2d_set_wgrad_wide(4)
         ws = torch.empty(wsb // 4, device=dev)
 
@@ -134,6 +143,11 @@ def main():
         rows = {}
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
+                if w1:
+                    lib.ewvit_conv2d_set_wgrad_1x1(*w1[v // 10000])
+                    lib.ewvit_conv2d_set_glds(1)
+                    rows.setdefault((v, 'wgrad'), []).append(graph_time(wgrad, a.iters))
+                    continue
                 lib.ewvit_conv2d_set_glds(v % 100)
                 lib.ewvit_conv2d_set_wgrad_wide(v % 1000 // 100)     # 0 = 128-column tiles, 4 = auto
                 if a.ww is not None:
@@ -147,8 +161,14 @@ def main():
         lib.ewvit_conv2d_set_wgrad_wide(4)
         if a.ww is not None:
             lib.ewvit_conv2d_set_ww(0)
+        lib.ewvit_conv2d_set_wgrad_1x1(256, 4, 3)
         for v in a.variants:
             parts = []
+            if w1:
+                t = min(rows[(v, 'wgrad')])
+                print(f'{name:15s} [w1 {":".join(map(str, w1[v // 10000])):>10s}] wgrad {t:8.1f} us {flops / t / 1e6:6.0f} TF/s',
+                      flush=True)
+                continue
             for pn in (('fwd', 'fwd_bn') if a.bnstats and rows_bn > 0 else ('fwd', 'dgrad', 'wgrad')):
                 t = min(rows[(v, pn)])
                 parts.append(f'{pn} {t:8.1f} us {flops / t / 1e6:6.0f} TF/s')
