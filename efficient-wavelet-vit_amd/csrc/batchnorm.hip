@@ -352,7 +352,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
                                                        const float *__restrict__ gamma,
                                                        const float *__restrict__ beta, float *running_mean,
                                                        float *running_var, float momentum, float eps, float *save_mean,
-                                                       float *save_invstd, int64_t *counter, BnDrop dr = BnDrop()) {
+                                                       float *save_invstd, int64_t *counter, BnDrop dr = BnDrop(),
+                                                       float *coef_out = nullptr) {
   __shared__ float red[512];
   __shared__ float coef[2][64];
   const int grp = blockIdx.z, groups = gridDim.z;
@@ -392,6 +393,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
               const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
               coef[0][tid] = ga * inv;
               coef[1][tid] = be - mu * ga * inv;
+              if (coef_out) {
+                coef_out[(2 * grp) * C + cc] = coef[0][tid];
+                coef_out[(2 * grp + 1) * C + cc] = coef[1][tid];
+              }
             }
           }
           bn_sync();
@@ -410,6 +415,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
           const float ga = gamma ? gamma[cc] : 1.f, be = beta ? beta[cc] : 0.f;
           coef[0][tid] = ga * inv;
           coef[1][tid] = be - mu * ga * inv;
+          if (coef_out && blockIdx.x == 0) {
+            coef_out[(2 * grp) * C + cc] = coef[0][tid];
+            coef_out[(2 * grp + 1) * C + cc] = coef[1][tid];
+          }
         }
       }
     } else if (tid < nch_c) {
@@ -903,6 +912,28 @@ extern "C" int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t 
   BN_DISPATCH(BN_APPLY);
 #undef BN_APPLY
   return launch_status("bn_fwd_partials");
+}
+
+// the apply pass's coefficients only, for an op that applies the BatchNorm(+act) itself while
+// reading x (the windowed conv's input transform, ewvit_conv2d_fwd_bn_xf): the training
+// finalisation of ewvit_bn_fwd_partials — same blocks, same reduction order, running statistics,
+// counter, save_mean / save_invstd — with no rows, writing coef[g][0][c] = scale, coef[g][1][c]
+// = shift (y = act(x * scale + shift) is then bit-identical to that apply pass)
+extern "C" int ewvit_bn_coef(int64_t M, int64_t C, const float *gamma, const float *beta, float *running_mean,
+                             float *running_var, float momentum, float eps, float *save_mean, float *save_invstd,
+                             int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc, int groups,
+                             float *coef, void *stream) {
+  EWVIT_CHECK_ARG(part && shifts && coef, "bn_coef: bad args");
+  EWVIT_CHECK_ARG(C > 0 && C % 8 == 0 && C <= 4096, "bn_coef: C=%lld must be a multiple of 8, <= 4096", (long long)C);
+  EWVIT_CHECK_ARG(nrc >= 1 && nrc <= 4096, "bn_coef: %d partial rows", nrc);
+  EWVIT_CHECK_ARG(groups >= 1 && groups <= 65535 && M > 0 && M % groups == 0, "bn_coef: M=%lld, %d groups",
+                  (long long)M, groups);
+  const BnGeo geo = bn_geo(C);
+  dim3 grid(1u, geo.nch, groups);
+  hipLaunchKernelGGL((bn_apply_kernel<EWVIT_BF16, 1>), grid, dim3(geo.threads), 0, as_stream(stream), nullptr, nullptr,
+                     part, shifts, nrc, M / groups, (int)C, geo.CC8, geo.RG, (int64_t)0, 1, gamma, beta, running_mean,
+                     running_var, momentum, eps, save_mean, save_invstd, num_batches_tracked, BnDrop(), coef);
+  return launch_status("bn_coef");
 }
 
 // BatchNorm (no activation) + StochasticDepth(row) + skip add, training, one group:

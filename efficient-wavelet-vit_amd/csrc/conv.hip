@@ -1739,6 +1739,49 @@ extern "C" int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *b
   return launch_status("conv2d_fwd_bn");
 }
 
+// ---- convs reading relu(x * scale + shift): the training BatchNorm + ReLU of x's producer
+// applied in the windowed kernels' operand staging (XF; coefficients from ewvit_bn_coef, one
+// [2][group channels] block per channel group of x), so the normalised tensor is never written.
+// The forward (with the next BatchNorm's statistics) and the weight gradient; the input gradient
+// is the plain conv's (it does not read x).  3x3 stride 1 over maps the windowed kernels take.
+static WgradArgs wgrad_args(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride);
+static bool xf_args(FwdArgs &a, WgradArgs &w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                    int stride, int64_t x_group_c, int64_t x_group_stride) {
+  if (ksize != 3 || stride != 1 || x_group_c <= 0 || Cin % x_group_c || Cin > 512 || !use_glds()) return false;
+  a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
+  a.sgc = (int)x_group_c; a.sgs = x_group_stride;
+  a.bn_part = reinterpret_cast<float *>(1);
+  a.xf = reinterpret_cast<const float *>(1);
+  w = wgrad_args(N, H, W, Cin, Cout, ksize, stride);
+  w.xgc = (int)x_group_c; w.xgs = x_group_stride;
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  return win_ok(a, false) && xb < (int64_t)OOB && wgrad_win_splits(w, xb) > 0;
+}
+extern "C" int ewvit_conv2d_xf_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                                  int64_t x_group_c, int64_t x_group_stride) {
+  FwdArgs a;
+  WgradArgs w;
+  return xf_args(a, w, N, H, W, Cin, Cout, ksize, stride, x_group_c, x_group_stride) ? 1 : 0;
+}
+extern "C" int ewvit_conv2d_fwd_bn_xf(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                                      int64_t W, int64_t Cin, int64_t Cout, int64_t x_group_c, int64_t x_group_stride,
+                                      const float *xf, const float *bn_shift, float *bn_part, float *bn_shift_out,
+                                      void *stream) {
+  EWVIT_CHECK_ARG(x && wp && y && xf && bn_part && bn_shift_out, "conv2d_fwd_bn_xf: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, 3, 1);
+  if (int rc = check_geom(g, "conv2d_fwd_bn_xf")) return rc;
+  if (int rc = check_group(x_group_c, x_group_stride, Cin, N * H * W, "conv2d_fwd_bn_xf", "x")) return rc;
+  FwdArgs a;
+  WgradArgs w;
+  EWVIT_CHECK_ARG(xf_args(a, w, N, H, W, Cin, Cout, 3, 1, x_group_c, x_group_stride),
+                  "conv2d_fwd_bn_xf: shape not taken by the windowed kernels (query ewvit_conv2d_xf_ok)");
+  a.src = (const bf16_t *)x; a.wp = (const bf16_t *)wp; a.bias = bias; a.out = (bf16_t *)y;
+  a.bn_shift = bn_shift; a.bn_part = bn_part; a.bn_shift_out = bn_shift_out; a.xf = xf;
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  EWVIT_CHECK_ARG(launch_win(a, xb, false, as_stream(stream)), "conv2d_fwd_bn_xf: windowed kernel refused the shape");
+  return launch_status("conv2d_fwd_bn_xf");
+}
+
 // input channels per tap the fwd expects its weight pack to have: Cin rounded up to 64
 // when Cin % 64 != 0 (Cin % 16 == 0) and the padded LDS-DMA kernel takes the shape
 static int64_t fwd_pack_cin(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride) {
@@ -2134,4 +2177,43 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,
                      g.Cout, g.Cin, taps, sp, bparts, accumulate, a.dbias_part, dbias, wo, T, (int)nmain);
   return launch_status("conv2d_bwd_weight reduce");
+}
+
+// dW (+ db) of the conv over relu(x * scale + shift) (see ewvit_conv2d_fwd_bn_xf): the windowed
+// kernel with the transform in its x staging, then the split reduction; same workspace as
+// ewvit_conv2d_bwd_weight
+extern "C" int ewvit_conv2d_bwd_weight_xf(const void *x, const void *dy, float *dw, float *dbias, int accumulate,
+                                          int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                          int64_t x_group_c, int64_t x_group_stride, const float *xf, int64_t dw_cin,
+                                          int64_t dw_s_co, int64_t dw_s_ci, int64_t dw_s_tap, float *workspace,
+                                          void *stream) {
+  EWVIT_CHECK_ARG(x && dy && dw && xf && workspace, "conv2d_bwd_weight_xf: null pointer");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, 3, 1);
+  if (int rc = check_geom(g, "conv2d_bwd_weight_xf")) return rc;
+  if (int rc = check_group(x_group_c, x_group_stride, Cin, N * H * W, "conv2d_bwd_weight_xf", "x")) return rc;
+  FwdArgs fa;
+  WgradArgs a;
+  EWVIT_CHECK_ARG(xf_args(fa, a, N, H, W, Cin, Cout, 3, 1, x_group_c, x_group_stride),
+                  "conv2d_bwd_weight_xf: shape not taken by the windowed kernels (query ewvit_conv2d_xf_ok)");
+  EWVIT_CHECK_ARG(dw_cin > 0 && dw_cin <= Cin, "conv2d_bwd_weight_xf: dw_cin %lld not in (0, %lld]", (long long)dw_cin,
+                  (long long)Cin);
+  a.x = (const bf16_t *)x; a.dy = (const bf16_t *)dy; a.xf = xf;
+  const int64_t xb = 2 * (x_group_stride ? (Cin / x_group_c - 1) * x_group_stride + N * H * W * x_group_c : N * H * W * Cin);
+  const int wsp = wgrad_win_splits(a, xb);
+  const int taps = 9;
+  a.part = workspace;
+  a.dbias_part = dbias ? workspace + (int64_t)wsp * g.Cout * taps * g.Cin : nullptr;
+  hipStream_t s = as_stream(stream);
+  launch_wgrad_win(a, xb, wsp, s);
+  if (int rc = launch_status("conv2d_bwd_weight_xf (windowed)")) return rc;
+  WOut wo;
+  wo.s_co = dw_s_co; wo.s_ci = dw_s_ci; wo.s_tap = dw_s_tap; wo.cin = (int)dw_cin;
+  const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
+  int T = 1;
+  while (T < 64 && T * 2 <= wsp && n4 * T * 2 <= 65536) T *= 2;
+  const int64_t nmain = (n4 * T + 255) / 256;
+  const int64_t nbias = dbias ? (g.Cout + 63) / 64 : 0;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,
+                     g.Cout, g.Cin, taps, wsp, wsp, accumulate, a.dbias_part, dbias, wo, T, (int)nmain);
+  return launch_status("conv2d_bwd_weight_xf reduce");
 }

@@ -56,6 +56,11 @@ struct FwdArgs {
   // BatchNorm(+act) whose output this conv read, summed over the bf16-rounded dx per m-tile
   // (common.h BnBwdStats; bwd.part [m-tiles][2 Ncol])
   BnBwdStats bwd;
+  // optional input transform of the windowed fwd (convwin.hip, XF): the conv reads
+  // relu(x * xf[g][0][c] + xf[g][1][c]) — a training BatchNorm + ReLU applied by its producer's
+  // coefficients (ewvit_bn_coef) — instead of x; channel group g = c / sgc, zero padding after
+  // the transform
+  const float *xf = nullptr;
 };
 
 typedef __attribute__((address_space(3))) void lds_t;
@@ -132,6 +137,7 @@ struct WgradArgs {
   int64_t mper;          // pixels per split (multiple of 32)
   int xgc;
   int64_t xgs;
+  const float *xf = nullptr;  // input transform of the windowed wgrad (FwdArgs::xf; groups of xgc)
 };
 
 __device__ __forceinline__ int swz_off(int r, int ch) {

@@ -57,8 +57,10 @@ constexpr int SLOT_B = 128 * 128;         // 128 columns x 64 k, bf16
 constexpr int VEC_N = 512;                // bias / BN shift entries (Ncol <= 512 with either)
 constexpr int VEC0 = NSLOT * SLOT_B;      // bias [512] + BN shift [512] floats
 constexpr int RED0 = VEC0 + 2 * VEC_N * 4; // BN statistics partials [4 row groups][128 cols][2]
-constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1]
-constexpr int SMEM_B = WIN0 + 2 * WIN_B;  // 138,240 B: one workgroup per CU
+constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1][xf][sink]
+constexpr int XF0 = WIN0 + 2 * WIN_B;     // input-transform coefficients [groups][2][sgc] (KC <= 512)
+constexpr int SINK0 = XF0 + 4096;         // 1 KB target of the window slots past the last piece
+constexpr int SMEM_B = SINK0 + 1024;      // 143,360 B: one workgroup per CU
 }  // namespace
 
 // all LDS-DMA pieces except the N youngest landed, LDS reads drained, workgroup barrier
@@ -88,9 +90,15 @@ struct WinUnit {
   int part;      // BatchNorm partial row (spatial block index)
   int last;      // last channel block of the tile
   int ok;        // the unit exists
+  int xo;        // XF: the channel block's first scale in the coefficient table (its shift at + sgc)
 };
 
-template <bool DGRAD, bool STATS>
+// XF (fwd only): the window is staged raw, then each wave rewrites the pieces it staged as
+// relu(x * scale + shift) of the pixel's channel group (FwdArgs::xf; bit-identical to the
+// BatchNorm apply pass the transform replaces), zero outside the image — at tap 6 of the unit
+// before (its pieces landed by then; tap 8's barrier publishes them), in the prologue for the
+// first unit.
+template <bool DGRAD, bool STATS, bool XF = false>
 __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_bytes, int64_t out_bytes, int ntn,
                                                        int ntiles, int ncb) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_B];
@@ -122,6 +130,10 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       vec[c] = a.bias ? a.bias[c] : 0.f;
       vec[VEC_N + c] = (STATS && a.bn_shift) ? a.bn_shift[c] : 0.f;
     }
+  if constexpr (XF) {
+    float *xt = reinterpret_cast<float *>(smem + XF0);
+    for (int c = tid; c < 2 * a.KC; c += 512) xt[c] = a.xf[c];
+  }
   __syncthreads();
 
   auto unit = [&](int u) -> WinUnit {
@@ -143,6 +155,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     const int c = cb * 64, gi = c / a.sgc;
     const int64_t pix = ((int64_t)d.img * H + (d.oh0 - 1)) * W + (d.ow0 - 1);
     d.wsrc = (uint32_t)((pix * a.sgc + (int64_t)gi * a.sgs + (c - gi * a.sgc)) * 2);
+    d.xo = gi * 2 * a.sgc + (c - gi * a.sgc);
     return d;
   };
 
@@ -177,7 +190,43 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     const int ih = d.oh0 - 1 + (int)wr, iw = d.ow0 - 1 + (int)wc;
     const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
     const uint32_t off = d.wsrc + __umul24(__umul24(wr, (uint32_t)W) + wc, sgc2) + (uint32_t)wlc16;
-    glds16_asm(rs, lds0 + WIN0 + wb * WIN_B + q * 1024, ok ? off : OOB);
+    // (slots past the last piece load zeros into the sink, so every wave issues the same count)
+    glds16_asm(rs, q < WPIECES ? lds0 + WIN0 + wb * WIN_B + q * 1024 : lds0 + SINK0, ok ? off : OOB);
+  };
+  // XF: this wave's pieces of unit d's window (buffer wb) -> relu(x * scale + shift), zero
+  // outside the image.  The lane's pixel is 8 q + lane / 8 and its chunk (lane & 7) ^ (lane / 8)
+  // for every piece, so its 8 channels' coefficients are one pair of table rows per unit.
+  auto xform = [&](const WinUnit &d, int wb) __attribute__((always_inline)) {
+    const int lc = (lane & 7) ^ ((lane >> 3) & 7);
+    const float *xt = reinterpret_cast<const float *>(smem + XF0) + d.xo + lc * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = xt[e]; sh[e] = xt[a.sgc + e]; }
+    int pl = lane >> 3;
+    asm volatile("" : "+v"(pl));
+#pragma unroll
+    for (int T = 0; T < 3; ++T)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int q = (T * 8 + ws) * 2 + jj;
+        if (q >= WPIECES) continue;
+        const uint32_t p = (uint32_t)(q * 8 + pl);
+        const uint32_t wr = __umul24(p, 3641u) >> 16;
+        const uint32_t wc = p - __umul24(wr, (uint32_t)WW);
+        const int ih = d.oh0 - 1 + (int)wr, iw = d.ow0 - 1 + (int)wc;
+        const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+        uint4 *ptr = reinterpret_cast<uint4 *>(smem + WIN0 + wb * WIN_B + q * 1024 + lane * 16);
+        const uint4 v = *ptr;
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+        unsigned o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float z0 = fmaf(__uint_as_float(wv[e] << 16), sc[2 * e], sh[2 * e]);
+          const float z1 = fmaf(__uint_as_float(wv[e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
+          o[e] = (unsigned)f2bf(z0 > 0.f ? z0 : 0.f) | ((unsigned)f2bf(z1 > 0.f ? z1 : 0.f) << 16);
+        }
+        *ptr = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
+      }
   };
 
   // fragment addresses, no VALU in the loop.  A: window pixel p = p0 + c, p0 = (wm*4)*18 + fr,
@@ -298,7 +347,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   // window pieces of the next unit: 2 per wave at taps 0-2 (48 slots for 41 pieces; the extra
   // slots repeat piece 40), so a unit's window has landed long before its first read
   constexpr int WPT = 2;
-  auto wpiece = [&](int T, int jj) { const int q = (T * 8 + ws) * WPT + jj; return q < WPIECES ? q : WPIECES - 1; };
+  auto wpiece = [&](int T, int jj) { return (T * 8 + ws) * WPT + jj; };
 
   // ---- prologue: unit 0's window (all pieces), K-tiles 0..2 of unit 0
   WinUnit cu = unit(0), nx = unit(1);
@@ -309,6 +358,10 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 #pragma unroll
   for (int t = 0; t < 3; ++t) issue_b(cu, t, t);
   win_sync<4>();                            // window 0 and K-tile 0 landed (B 1, 2 in flight)
+  if constexpr (XF) {
+    xform(cu, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   read_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
              fa, fb);
   bool prev_st = false;                     // the previous unit ended a tile (its stores are in flight)
@@ -360,6 +413,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
+      if constexpr (XF && T == 6) xform(nx, WB ^ 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -402,6 +456,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 
 bool win_ok(const FwdArgs &a, bool dgrad) {
   if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend || a.bwd.part) return false;
+  if (a.xf && (dgrad || a.KC > 512)) return false;
   if (dgrad && a.bn_part) return false;
   if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
   if (a.KC % 64 || a.sgc % 64 || (a.KCr && a.KCr != a.KC)) return false;
@@ -459,7 +514,10 @@ constexpr int GSMEM = GD0 + 2 * GD_B;              // 90,112 B
 __device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
 
 
-template <bool BIAS>
+// XF: x is read as relu(x * scale + shift) (WgradArgs::xf, the forward's input transform): each
+// wave rewrites its own window pieces of the next tile after its DMAs drained at the end of the
+// current tile (the loop-top barrier publishes them), the first tile's before the loop.
+template <bool BIAS, bool XF = false>
 __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb, int nct,
                                                              int ntile) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[GSMEM];
@@ -509,6 +567,41 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
       const int sc = (lane & 3) ^ xswz(p);
       const uint32_t off = (uint32_t)(((xpix + xr * W + xc) * a.xgc + cofs + sc * 8) * 2);
       glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB);
+    }
+  };
+
+  // XF: the lane's 8 channels are the same in every piece (chunk (lane & 3) ^ xswz(16 q + lane / 4)
+  // = (lane & 3) ^ ((lane >> 5) << 1)), so their coefficients stay in registers
+  float xsc[8], xsh[8];
+  if constexpr (XF) {
+    const int lcx = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const float *xt = a.xf + gi * 2 * a.xgc + (c32 - gi * a.xgc) + lcx * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { xsc[e] = xt[e]; xsh[e] = xt[a.xgc + e]; }
+  }
+  auto xform = [&](int t, int b) __attribute__((always_inline)) {
+    const int img = t / tpi, rem = t - img * tpi;
+    const int oh0 = (rem / tpr) * GT_R, ow0 = (rem % tpr) * GT_C;
+    int xl = lane >> 2;
+    asm volatile("" : "+v"(xl));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = ws * 3 + j;
+      const int p = q * 16 + xl;
+      const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;
+      const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
+      const bool ok = (p < GX_PIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+      uint4 *ptr = reinterpret_cast<uint4 *>(smem + b * GX_B + q * 1024 + lane * 16);
+      const uint4 v = *ptr;
+      const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+      unsigned o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z0 = fmaf(__uint_as_float(wv[e] << 16), xsc[2 * e], xsh[2 * e]);
+        const float z1 = fmaf(__uint_as_float(wv[e] & 0xffff0000u), xsc[2 * e + 1], xsh[2 * e + 1]);
+        o[e] = (unsigned)f2bf(z0 > 0.f ? z0 : 0.f) | ((unsigned)f2bf(z1 > 0.f ? z1 : 0.f) << 16);
+      }
+      *ptr = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
     }
   };
 
@@ -582,12 +675,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
   // (the last tile issues a dummy stage — every lane out of range, zeros into the idle stage —
   // so no branch sits between the DMA and the fragment reads: at such a merge hipcc waits
   // vmcnt(0) before the first ds_read, draining the next tile's loads)
-  if (t0 < t1) issue(t0, 0, true);
+  if (t0 < t1) {
+    issue(t0, 0, true);
+    if constexpr (XF) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      xform(t0, 0);
+    }
+  }
   int sd = GD_B, sx = GX_B;          // stage 0 -> 1 address deltas
   for (int t = t0, b = 0; t < t1; ++t, b ^= 1) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue(t + 1 < t1 ? t + 1 : t, b ^ 1, t + 1 < t1);
     compute();
+    if constexpr (XF) {
+      if (t + 1 < t1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        xform(t + 1, b ^ 1);
+      }
+    }
 #pragma unroll
     for (int hi = 0; hi < 2; ++hi)
 #pragma unroll
@@ -637,7 +742,11 @@ bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream
   const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const unsigned nwg = (unsigned)(splits * ncb * nct);
-  if (a.dbias_part)
+  if (a.xf && a.dbias_part)
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<true, true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+  else if (a.xf)
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<false, true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+  else if (a.dbias_part)
     hipLaunchKernelGGL((conv_wgrad_win_kernel<true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
   else
     hipLaunchKernelGGL((conv_wgrad_win_kernel<false>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
@@ -655,6 +764,10 @@ bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) 
   const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
   if (dgrad)
     hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (a.xf && a.bn_part)
+    hipLaunchKernelGGL((conv_win_kernel<false, true, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (a.xf)
+    hipLaunchKernelGGL((conv_win_kernel<false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (a.bn_part)
     hipLaunchKernelGGL((conv_win_kernel<false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
   else

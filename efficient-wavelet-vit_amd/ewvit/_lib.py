@@ -62,6 +62,12 @@ SIGNATURES = {
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
                             _vp, _vp],
+    'ewvit_conv2d_xf_ok': [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64],
+    'ewvit_conv2d_fwd_bn_xf': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp,
+                               _vp],
+    'ewvit_conv2d_bwd_weight_xf': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
+                                   _i64, _i64, _i64, _vp, _vp],
+    'ewvit_bn_coef': [_i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_bn_fwd_partials': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp, _vp,
                               _vp, _vp, _i32, _i32, _vp],
     'ewvit_bn_fwd_drop_add': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp,

@@ -375,6 +375,150 @@ def conv2d_bn_stats(x, weight, bias, stride, shift, levels=1, groups=1, max_rows
     return y, part, shifts, nrc
 
 
+class BnReluConvFn(torch.autograd.Function):
+    """conv3x3(relu(BatchNorm(z))) in training, the BatchNorm + ReLU applied inside the windowed
+    conv's operand staging (ewvit_conv2d_fwd_bn_xf / ewvit_conv2d_bwd_weight_xf): the normalised
+    map is never written.  z is the level-major producer output [levels*N, C, H, W] whose
+    BatchNorm statistics (per level) its producer's epilogue summed (`zpart` = (part, shifts,
+    nrc)); the conv reads the levels as channel groups (mwt.py:112's concatenation).  Forward:
+    ewvit_bn_coef (the BN's finalisation: batch / running statistics, counter, scale and shift)
+    + the transformed conv with the next BatchNorm's statistics (`ystats`).  Backward: the
+    conv's input gradient (plain dgrad: it does not read z), the transformed weight gradient,
+    then the BatchNorm + ReLU backward on z — the same kernels, in the same order, as
+    BatchNormActFn followed by Conv2dFn, so every result is bit-identical to that pair."""
+
+    @staticmethod
+    def forward(ctx, z, weight, bias, gamma, beta, running_mean, running_var, momentum, eps, counter, levels, zpart,
+                ystats):
+        L.require_gpu(z, weight)
+        ctx.cap = L.current_cap()
+        with L.launch_cap(ctx.cap):
+            return BnReluConvFn._forward(ctx, z, weight, bias, gamma, beta, running_mean, running_var, momentum, eps,
+                                         counter, levels, zpart, ystats)
+
+    @staticmethod
+    def _forward(ctx, z, weight, bias, gamma, beta, running_mean, running_var, momentum, eps, counter, levels, zpart,
+                 ystats):
+        zc = z.contiguous(memory_format=torch.channels_last)
+        NL, C, H, W = zc.shape
+        N, Cx = NL // levels, C * levels
+        Cout = weight.shape[0]
+        dev = z.device
+        part, shifts, nrc = zpart
+        M = NL * H * W
+        coef = torch.empty(levels, 2, C, dtype=torch.float32, device=dev)
+        mean = torch.empty(levels, C, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        L.call('ewvit_bn_coef', M, C, L.ptr(gamma), L.ptr(beta), L.ptr(running_mean), L.ptr(running_var),
+               float(momentum), float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(counter), L.ptr(part), L.ptr(shifts),
+               int(nrc), levels, L.ptr(coef), L.stream(zc))
+        cached = _cached_pack(weight, Cx, True) if weight.dtype == torch.float32 else None
+        if cached is None:
+            wp, wpt = _pack(weight, Cx, True, True)
+            if weight.dtype == torch.float32:
+                _register(weight, Cx, True)
+        else:
+            wp, wpt = cached
+        y = torch.empty((N, Cout, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        shift, ypart, yshift = ystats
+        gs = N * H * W * C
+        L.call('ewvit_conv2d_fwd_bn_xf', L.ptr(zc), L.ptr(wp), L.ptr(b), L.ptr(y), N, H, W, Cx, Cout, C, gs,
+               L.ptr(coef), L.ptr(shift), L.ptr(ypart), L.ptr(yshift), L.stream(y),
+               work={'flops': 2.0 * N * H * W * Cout * 9 * Cx, 'bytes': (zc.numel() + y.numel() + wp.numel()) * 2})
+        ctx.save_for_backward(zc, weight, wpt, coef, gamma, beta, mean, invstd)
+        ctx.gen = grads.note_use(weight)
+        for t in (bias, gamma, beta):
+            grads.note_use(t)
+        ctx.params = (weight, bias, gamma, beta)
+        ctx.cfg = (levels, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        with L.launch_cap(L.bwd_cap(ctx.cap)):
+            return BnReluConvFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
+        zc, weight, wpt, coef, gamma, beta, mean, invstd = ctx.saved_tensors
+        levels, has_bias = ctx.cfg
+        NL, C, H, W = zc.shape
+        N, Cx = NL // levels, C * levels
+        Cout = weight.shape[0]
+        gs = N * H * W * C
+        dev = zc.device
+        dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        # d relu(bn(z)) — the input gradient of the conv, in z's level-major layout
+        da = torch.empty_like(zc, memory_format=torch.channels_last)
+        L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, 3, 1, C, gs, L.stream(da),
+               work={'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + da.numel() + wpt.numel()) * 2})
+        wparam, bparam, gparam, beparam = ctx.params
+        dwf = grad_out(wparam, ctx.gen)
+        s_co, s_ci, s_kh, s_kw = dwf.stride()
+        if s_kh != 3 * s_kw:
+            dwf = torch.empty((Cout, Cx, 3, 3), dtype=torch.float32, device=dev)
+            s_co, s_ci, s_kh, s_kw = dwf.stride()
+        dbf = None
+        if has_bias:
+            dbf = grad_out(bparam, ctx.gen)
+            if dbf.dim() != 1 or not dbf.is_contiguous():
+                dbf = torch.empty(Cout, dtype=torch.float32, device=dev)
+        ws = torch.empty(L.load().ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, 3, 1) // 4, dtype=torch.float32,
+                         device=dev)
+        L.call('ewvit_conv2d_bwd_weight_xf', L.ptr(zc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx, Cout, C, gs,
+               L.ptr(coef), Cx, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf),
+               work={'flops': 2.0 * N * H * W * Cout * 9 * Cx, 'bytes': (dyc.numel() + zc.numel()) * 2})
+        # BatchNorm + ReLU backward on z (per level)
+        M = NL * H * W
+        dz = torch.empty_like(zc)
+        dg = bnmod._affine_grad(gparam, ctx.gen, C, dev)
+        db2 = bnmod._affine_grad(beparam, ctx.gen, C, dev)
+        bws = torch.empty(L.load().ewvit_bn_workspace(M, C, levels) // 4, dtype=torch.float32, device=dev)
+        L.call('ewvit_bn_bwd', L.ptr(da), L.ptr(zc), L.ptr(dz), L.dt(zc), M, C, L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+               L.ptr(invstd), 1, L.ptr(dg), L.ptr(db2), 0, levels, L.ptr(bws), L.stream(dz),
+               work={'bytes': 5 * zc.numel() * zc.element_size()})
+        g = ctx.gen
+        return (dz, grads.give(wparam, dwf, g), grads.give(bparam, dbf, g) if has_bias else None,
+                grads.give(gparam, dg, g), grads.give(beparam, db2, g), *(None,) * 8)
+
+
+def bn_relu_ok(z, weight, levels):
+    """True when bn_relu_conv2d_bn_stats takes this (producer output z, 3x3 conv weight) pair."""
+    if not (z.is_cuda and z.dim() == 4 and z.dtype == torch.bfloat16 and weight.dim() == 4
+            and tuple(weight.shape[2:]) == (3, 3) and weight.dtype == torch.float32 and z.shape[0] % levels == 0
+            and weight.shape[1] == z.shape[1] * levels):
+        return False
+    NL, C, H, W = z.shape
+    N = NL // levels
+    return bool(L.load().ewvit_conv2d_xf_ok(N, H, W, C * levels, weight.shape[0], 3, 1, C, N * H * W * C))
+
+
+def bn_relu_conv2d_bn_stats(z, zpart, bn, weight, bias, shift, levels, max_rows=256):
+    """conv3x3(relu(bn(z)), weight, bias) for a training BatchNorm module `bn` whose batch
+    statistics (one group per level of the level-major z) its producer summed (`zpart`), with
+    the conv's own output statistics for the next BatchNorm: (y, part, shifts, nrc) as
+    conv2d_bn_stats.  See BnReluConvFn."""
+    NL, C, H, W = z.shape
+    N = NL // levels
+    Cout = weight.shape[0]
+    rows = 256
+    nrc = (N * H * W + rows - 1) // rows
+    part = torch.empty(nrc, 2 * Cout, dtype=torch.float32, device=z.device)
+    shifts = torch.empty(Cout, dtype=torch.float32, device=z.device)
+    sh = shift.detach().float().contiguous() if shift is not None else None
+    counter = bn.num_batches_tracked if bn.track_running_stats else None
+    y = BnReluConvFn.apply(z, weight, bias, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                           counter, int(levels), zpart, (sh, part, shifts))
+    if nrc > max_rows:
+        part2 = torch.empty(1, max_rows, 2 * Cout, dtype=torch.float32, device=z.device)
+        shifts2 = torch.empty(1, Cout, dtype=torch.float32, device=z.device)
+        L.call('ewvit_bn_fold_partials', L.ptr(part), nrc, L.ptr(shifts), L.ptr(part2), max_rows, L.ptr(shifts2), Cout,
+               1, L.stream(y))
+        part, shifts, nrc = part2, shifts2, max_rows
+    return y, part, shifts, nrc
+
+
 def stem_ok(x, weight, bias, stride):
     """The frozen backbone stem's shape class (ewvit_conv2d_stem_fwd): 3x3, pad 1, stride
     1|2, Cin 1..4, Cout 8/16/24/32, f32 / bf16 input, no gradient needed anywhere."""

@@ -87,12 +87,50 @@ def _epi_stats(conv, bn, x, levels=1, groups=1):
     return None if r is None else (r[0], r[1:])
 
 
+# the hf_conv['fusion'] BatchNorm + ReLU applied inside multiscale_fusion's conv (ewvit.conv.
+# BnReluConvFn) instead of by its own pass (0: the separate apply pass, A/B and tests)
+_FOLD_FUSION_BN = True
+
+
+class PendingBNReLU:
+    """A training BatchNorm(+ReLU) output not yet materialised: the producer's raw output z,
+    the batch statistics its epilogue summed, the CBR whose BN / ReLU it is and the BN groups
+    (levels).  The consumer either folds it into its conv (CBR.forward -> ewvit.conv.
+    bn_relu_conv2d_bn_stats) or calls materialize()."""
+    __slots__ = ('z', 'partials', 'cbr', 'groups')
+
+    def __init__(self, z, partials, cbr, groups):
+        self.z, self.partials, self.cbr, self.groups = z, partials, cbr, groups
+
+    def materialize(self):
+        return ewvit.batch_norm_act(self.z, self.cbr[1], 'relu', groups=self.groups, partials=self.partials)
+
+
 class CBR(nn.Sequential):
     """Conv3x3 -> BatchNorm2d -> ReLU; BN + ReLU as one fused ewvit pass, its batch
     statistics summed in the conv's epilogue where the conv kernel allows.
-    ``levels``: see Conv3x3.forward."""
+    ``levels``: see Conv3x3.forward.  x may be a PendingBNReLU (the level-major hf fusion
+    output, levels groups): its BatchNorm + ReLU then run inside this conv's operand reads."""
+
+    def _fold(self, p, levels):
+        conv, bn = self[0], self[1]
+        src_bn = p.cbr[1]
+        if not (p.groups == levels and type(conv) is Conv3x3 and bn.training and bn.track_running_stats
+                and bn.momentum is not None and conv.stride[0] == 1 and conv.padding[0] == 1
+                and not (conv._forward_hooks or conv._forward_pre_hooks or bn._forward_hooks or bn._forward_pre_hooks)
+                and conv.weight.requires_grad and src_bn.weight is not None and src_bn.weight.requires_grad
+                and ewvit.conv.bn_relu_ok(p.z, conv.weight, levels)):
+            return None
+        r = ewvit.conv.bn_relu_conv2d_bn_stats(p.z, p.partials, src_bn, conv.weight, conv.bias, bn.running_mean,
+                                               levels)
+        return r[0], r[1:]
 
     def forward(self, x, levels=1):
+        if isinstance(x, PendingBNReLU):
+            r = self._fold(x, levels)
+            if r is not None:
+                return ewvit.batch_norm_act(r[0], self[1], 'relu', partials=r[1])
+            x = x.materialize()
         r = _epi_stats(self[0], self[1], x, levels)
         if r is not None:
             return ewvit.batch_norm_act(r[0], self[1], 'relu', partials=r[1])
@@ -301,6 +339,12 @@ class MWT(nn.Module):
         fus = self.hf_conv['fusion']
         r = _epi_stats(fus[0], fus[1], y, groups=Lv)
         if r is not None:
+            ms = self.multiscale_fusion
+            if (_FOLD_FUSION_BN and Lv > 1 and fus[1].track_running_stats and fus[1].momentum is not None
+                    and not (fus[2]._forward_hooks or fus[2]._forward_pre_hooks or ms._forward_hooks
+                             or ms._forward_pre_hooks)):
+                # consumed by multiscale_fusion (CBR.forward), which applies BN + ReLU itself
+                return PendingBNReLU(r[0], r[1], fus, Lv)
             return ewvit.batch_norm_act(r[0], fus[1], 'relu', groups=Lv, partials=r[1])
         z = fus[0](y)
         z = ewvit.batch_norm_act(z, fus[1], 'relu', groups=Lv) if _fusable(fus[1], z) else \

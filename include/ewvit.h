@@ -257,6 +257,14 @@ int ewvit_bn_fwd_partials(const void *x, void *y, int dtype, int64_t M, int64_t 
                           float eps, int act, float *save_mean, float *save_invstd,
                           int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc,
                           int groups, void *stream);
+/* ewvit_bn_fwd_partials without the apply pass: the same finalisation (batch statistics,
+ * running statistics, counter += groups, save_mean / save_invstd) writing the apply pass's
+ * coefficients coef[g][0][c] = gamma * invstd, coef[g][1][c] = beta - mean * gamma * invstd,
+ * for an op that applies y = act(x * coef0 + coef1) itself (ewvit_conv2d_fwd_bn_xf). */
+int ewvit_bn_coef(int64_t M, int64_t C, const float *gamma, const float *beta, float *running_mean,
+                  float *running_var, float momentum, float eps, float *save_mean, float *save_invstd,
+                  int64_t *num_batches_tracked, const float *part, const float *shifts, int nrc, int groups,
+                  float *coef, void *stream);
 /* part_out[g][k] = sum of part_in[g][k*ch .. k*ch + ch - 1] (ch = ceil(nin / nout); rows
  * of 2C floats, fixed order) and shift_out[g][:] = shift_in[:]: brings a large conv's
  * per-tile partial rows down to what the apply pass finalises from. */
@@ -406,6 +414,23 @@ int ewvit_conv2d_fwd_bn(const void *x, const void *wp, const float *bias, void *
 int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
                      int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride, int64_t x_group_c,
                      int64_t x_group_stride, void *stream);
+/* Convs that read relu(x * scale + shift) instead of x: the training BatchNorm + ReLU of x's
+ * producer (the MWT hf_conv['fusion'] BN, reference network/mwt.py:60-65, ahead of
+ * multiscale_fusion, mwt.py:68-72,114) applied inside the windowed kernels' operand staging,
+ * so the normalised map is never written.  xf: [groups][2][x_group_c] fp32 = per channel group
+ * of x (scale row, shift row), as ewvit_bn_coef writes them; the result is bit-identical to
+ * ewvit_bn_fwd_partials(act = relu) followed by ewvit_conv2d_fwd_bn / ewvit_conv2d_bwd_weight.
+ * 3x3 stride 1 only, where the windowed kernels take the shape (ewvit_conv2d_xf_ok: 1 / 0;
+ * Cin <= 512).  The input gradient of such a conv is the plain ewvit_conv2d_bwd_data. */
+int ewvit_conv2d_xf_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                       int64_t x_group_c, int64_t x_group_stride);
+int ewvit_conv2d_fwd_bn_xf(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,
+                           int64_t W, int64_t Cin, int64_t Cout, int64_t x_group_c, int64_t x_group_stride,
+                           const float *xf, const float *bn_shift, float *bn_part, float *bn_shift_out, void *stream);
+int ewvit_conv2d_bwd_weight_xf(const void *x, const void *dy, float *dw, float *dbias, int accumulate, int64_t N,
+                               int64_t H, int64_t W, int64_t Cin, int64_t Cout, int64_t x_group_c,
+                               int64_t x_group_stride, const float *xf, int64_t dw_cin, int64_t dw_s_co,
+                               int64_t dw_s_ci, int64_t dw_s_tap, float *workspace, void *stream);
 /* The backbone stem, forward only (replaces the library conv of the frozen
  * features.0.0 = Conv2d(3, 24, 3, stride 2, pad 1), reference network/sfe.py:111-119):
  * y [N, Ho, Wo, Cout] bf16 channels-last = conv(x, w) + bias (fp32 operands and accumulation,
