@@ -1950,6 +1950,50 @@ extern "C" int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *
   return launch_status("conv2d_bwd_data_bn");
 }
 
+// the windowed input gradient with the backward statistics of the BatchNorm(+act) whose output
+// the conv read (convwin.hip BST): one partial row per 16 x 16 block per channel group, part
+// [groups][N*H*W / 256][2 group_c]; BatchNorm groups = dx's channel groups (mean / invstd
+// [groups][group_c], gamma / beta [group_c] or null).  ewvit_conv2d_bwd_bn_win_rows: the partial
+// rows per group, 0 when the windowed kernel does not take the shape.
+static bool bst_args(FwdArgs &a, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                     int64_t dx_group_c, int64_t dx_group_stride) {
+  if (ksize != 3 || stride != 1 || dx_group_c <= 0 || Cin % dx_group_c) return false;
+  a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
+  a.M = (int64_t)a.g.N * a.g.H * a.g.W; a.Ncol = a.g.Cin; a.KC = a.g.Cout;
+  a.srcH = a.g.Ho; a.srcW = a.g.Wo; a.outH = a.g.H; a.outW = a.g.W;
+  a.sgc = a.g.Cout; a.sgs = 0; a.ogc = (int)dx_group_c; a.ogs = dx_group_stride;
+  a.bwd.part = reinterpret_cast<float *>(1);
+  a.bwd.x = reinterpret_cast<const bf16_t *>(2);
+  a.bwd.mean = a.bwd.invstd = reinterpret_cast<const float *>(4);
+  const int64_t sb = 2 * N * H * W * Cout;
+  return sb < (int64_t)OOB && win_ok(a, true);
+}
+extern "C" int64_t ewvit_conv2d_bwd_bn_win_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
+                                               int stride, int64_t dx_group_c, int64_t dx_group_stride) {
+  FwdArgs a;
+  return bst_args(a, N, H, W, Cin, Cout, ksize, stride, dx_group_c, dx_group_stride) ? N * H * W / 256 : 0;
+}
+extern "C" int ewvit_conv2d_bwd_data_bn_win(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H,
+                                            int64_t W, int64_t Cin, int64_t Cout, int64_t dx_group_c,
+                                            int64_t dx_group_stride, const void *bx, const float *mean,
+                                            const float *invstd, const float *gamma, const float *beta, int act,
+                                            float *part, void *stream) {
+  EWVIT_CHECK_ARG(dy && wp_t && dx && bx && mean && invstd && part && act >= 0 && act <= 2,
+                  "conv2d_bwd_data_bn_win: bad args");
+  ConvGeom g = mkg(N, H, W, Cin, Cout, 3, 1);
+  if (int rc = check_geom(g, "conv2d_bwd_data_bn_win")) return rc;
+  if (int rc = check_group(dx_group_c, dx_group_stride, Cin, N * H * W, "conv2d_bwd_data_bn_win", "dx")) return rc;
+  FwdArgs a;
+  EWVIT_CHECK_ARG(bst_args(a, N, H, W, Cin, Cout, 3, 1, dx_group_c, dx_group_stride),
+                  "conv2d_bwd_data_bn_win: shape not taken (query ewvit_conv2d_bwd_bn_win_rows)");
+  a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx;
+  a.bwd.part = part; a.bwd.x = (const bf16_t *)bx; a.bwd.mean = mean; a.bwd.invstd = invstd; a.bwd.gamma = gamma;
+  a.bwd.beta = beta; a.bwd.rscale = nullptr; a.bwd.act = act; a.bwd.hw = (int)(H * W); a.bwd.grows = 0;
+  const int64_t sb = 2 * N * H * W * Cout;
+  EWVIT_CHECK_ARG(launch_win(a, sb, true, as_stream(stream)), "conv2d_bwd_data_bn_win: windowed kernel refused");
+  return launch_status("conv2d_bwd_data_bn_win");
+}
+
 extern "C" int ewvit_conv2d_bwd_data(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
                                      int64_t Cin, int64_t Cout, int ksize, int stride, int64_t dx_group_c,
                                      int64_t dx_group_stride, void *stream) {

@@ -58,9 +58,10 @@ constexpr int VEC_N = 512;                // bias / BN shift entries (Ncol <= 51
 constexpr int VEC0 = NSLOT * SLOT_B;      // bias [512] + BN shift [512] floats
 constexpr int RED0 = VEC0 + 2 * VEC_N * 4; // BN statistics partials [4 row groups][128 cols][2]
 constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1][xf][sink]
-constexpr int XF0 = WIN0 + 2 * WIN_B;     // input-transform coefficients [groups][2][sgc] (KC <= 512)
-constexpr int SINK0 = XF0 + 4096;         // 1 KB target of the window slots past the last piece
-constexpr int SMEM_B = SINK0 + 1024;      // 143,360 B: one workgroup per CU
+constexpr int XF0 = WIN0 + 2 * WIN_B;     // fwd: input-transform coefficients [groups][2][sgc] (KC <= 512);
+                                          // dgrad: BatchNorm backward table [4][Ncol] (Ncol <= 512)
+constexpr int SINK0 = XF0 + 8192;         // 1 KB target of the window slots past the last piece
+constexpr int SMEM_B = SINK0 + 1024;      // 147,456 B: one workgroup per CU
 }  // namespace
 
 // all LDS-DMA pieces except the N youngest landed, LDS reads drained, workgroup barrier
@@ -95,10 +96,16 @@ struct WinUnit {
 
 // XF (fwd only): the window is staged raw, then each wave rewrites the pieces it staged as
 // relu(x * scale + shift) of the pixel's channel group (FwdArgs::xf; bit-identical to the
-// BatchNorm apply pass the transform replaces), zero outside the image — at tap 6 of the unit
-// before (its pieces landed by then; tap 8's barrier publishes them), in the prologue for the
-// first unit.
-template <bool DGRAD, bool STATS, bool XF = false>
+// BatchNorm apply pass the transform replaces), zero outside the image — at taps 6 and 7 of the
+// unit before (its pieces landed by then; tap 8's barrier publishes them), in the prologue for
+// the first unit.
+// BST (dgrad only): the backward statistics of the BatchNorm(+act) whose output this conv read
+// (FwdArgs::bwd, common.h BnBwdStats: x = that BN's input in dx's layout, mean / invstd per
+// column, gamma / beta per group channel): per 16 x 16 block and column, sum g and sum g * xhat
+// over the bf16-rounded dx, g = dx * act'(xhat * gamma + beta) — what ewvit_bn_bwd_partials
+// finalises.  The block's BN-input values are loaded at tap 5 of its last channel block (asm,
+// counted in the waits of taps 6, 7; OOB for other units), so the epilogue never waits on them.
+template <bool DGRAD, bool STATS, bool XF = false, bool BST = false>
 __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_bytes, int64_t out_bytes, int ntn,
                                                        int ntiles, int ncb) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_B];
@@ -133,6 +140,16 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   if constexpr (XF) {
     float *xt = reinterpret_cast<float *>(smem + XF0);
     for (int c = tid; c < 2 * a.KC; c += 512) xt[c] = a.xf[c];
+  }
+  if constexpr (BST) {
+    float *bt = reinterpret_cast<float *>(smem + XF0);
+    for (int c = tid; c < a.Ncol; c += 512) {
+      const int cg = c % a.ogc;
+      bt[c] = a.bwd.mean[c];
+      bt[512 + c] = a.bwd.invstd[c];
+      bt[1024 + c] = a.bwd.gamma ? a.bwd.gamma[cg] : 1.f;
+      bt[1536 + c] = a.bwd.beta ? a.bwd.beta[cg] : 0.f;
+    }
   }
   __syncthreads();
 
@@ -196,7 +213,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   // XF: this wave's pieces of unit d's window (buffer wb) -> relu(x * scale + shift), zero
   // outside the image.  The lane's pixel is 8 q + lane / 8 and its chunk (lane & 7) ^ (lane / 8)
   // for every piece, so its 8 channels' coefficients are one pair of table rows per unit.
-  auto xform = [&](const WinUnit &d, int wb) __attribute__((always_inline)) {
+  auto xform = [&](const WinUnit &d, int wb, int half) __attribute__((always_inline)) {
     const int lc = (lane & 7) ^ ((lane >> 3) & 7);
     const float *xt = reinterpret_cast<const float *>(smem + XF0) + d.xo + lc * 8;
     float sc[8], sh[8];
@@ -204,29 +221,30 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     for (int e = 0; e < 8; ++e) { sc[e] = xt[e]; sh[e] = xt[a.sgc + e]; }
     int pl = lane >> 3;
     asm volatile("" : "+v"(pl));
+    // three of the wave's six pieces (half 0 | 1), one after another (batching the reads costs
+    // registers this loop does not have: spills); slots past the last piece skip
 #pragma unroll
-    for (int T = 0; T < 3; ++T)
+    for (int k = 0; k < 3; ++k) {
+      const int kk = half * 3 + k;
+      const int q = ((kk >> 1) * 8 + ws) * 2 + (kk & 1);
+      if (q >= WPIECES) continue;
+      const uint32_t p = (uint32_t)(q * 8 + pl);
+      const uint32_t wr = __umul24(p, 3641u) >> 16;
+      const uint32_t wc = p - __umul24(wr, (uint32_t)WW);
+      const int ih = d.oh0 - 1 + (int)wr, iw = d.ow0 - 1 + (int)wc;
+      const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+      uint4 *ptr = reinterpret_cast<uint4 *>(smem + WIN0 + wb * WIN_B + q * 1024 + lane * 16);
+      const uint4 v = *ptr;
+      const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+      unsigned o[4];
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int q = (T * 8 + ws) * 2 + jj;
-        if (q >= WPIECES) continue;
-        const uint32_t p = (uint32_t)(q * 8 + pl);
-        const uint32_t wr = __umul24(p, 3641u) >> 16;
-        const uint32_t wc = p - __umul24(wr, (uint32_t)WW);
-        const int ih = d.oh0 - 1 + (int)wr, iw = d.ow0 - 1 + (int)wc;
-        const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
-        uint4 *ptr = reinterpret_cast<uint4 *>(smem + WIN0 + wb * WIN_B + q * 1024 + lane * 16);
-        const uint4 v = *ptr;
-        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
-        unsigned o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float z0 = fmaf(__uint_as_float(wv[e] << 16), sc[2 * e], sh[2 * e]);
-          const float z1 = fmaf(__uint_as_float(wv[e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
-          o[e] = (unsigned)f2bf(z0 > 0.f ? z0 : 0.f) | ((unsigned)f2bf(z1 > 0.f ? z1 : 0.f) << 16);
-        }
-        *ptr = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
+      for (int e = 0; e < 4; ++e) {
+        const float z0 = fmaf(__uint_as_float(wv[e] << 16), sc[2 * e], sh[2 * e]);
+        const float z1 = fmaf(__uint_as_float(wv[e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
+        o[e] = (unsigned)f2bf(z0 > 0.f ? z0 : 0.f) | ((unsigned)f2bf(z1 > 0.f ? z1 : 0.f) << 16);
       }
+      *ptr = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
+    }
   };
 
   // fragment addresses, no VALU in the loop.  A: window pixel p = p0 + c, p0 = (wm*4)*18 + fr,
@@ -271,6 +289,25 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
+  // BST: this lane's BN-input values at its 16 epilogue positions of unit d (zeros, no traffic,
+  // unless d ends its tile)
+  uint2 xq[4][4];
+  const __amdgpu_buffer_rsrc_t rbx = mk_rsrc(BST ? (const void *)a.bwd.x : (const void *)a.out, out_bytes);
+  auto issue_x = [&](const WinUnit &d) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = d.n0 + wn * 64 + j * 16 + fq * 4;
+      const int gi = col / a.ogc;
+      const int64_t cbase = (int64_t)gi * a.ogs + (col - gi * a.ogc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + i) * W + d.ow0 + fr;
+        const uint32_t off = d.last ? (uint32_t)((pix * a.ogc + cbase) * 2) : OOB;
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
+      }
+    }
+  };
+
   // tile epilogue: (+ bias) -> bf16, 16 stores per wave; STATS: one more store per wave
   auto epilogue = [&](const WinUnit &d, int wb) __attribute__((always_inline)) {
     float cs[4][4], cq[4][4];
@@ -291,6 +328,12 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       const int64_t cbase = (int64_t)gi * a.ogs + (col - gi * a.ogc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
+      float bmu[4], biv[4], bga[4], bbe[4];
+      if constexpr (BST) {
+        const float *bt = reinterpret_cast<const float *>(smem + XF0) + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { bmu[r] = bt[r]; biv[r] = bt[512 + r]; bga[r] = bt[1024 + r]; bbe[r] = bt[1536 + r]; }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + i) * W + d.ow0 + fr;
@@ -300,6 +343,18 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
         bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2));
+        if constexpr (BST) {
+          const float hv[4] = {bf2f(h0), bf2f(h1), bf2f(h2), bf2f(h3)};
+          const float xv[4] = {__uint_as_float(xq[j][i].x << 16), __uint_as_float(xq[j][i].x & 0xffff0000u),
+                               __uint_as_float(xq[j][i].y << 16), __uint_as_float(xq[j][i].y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xh = (xv[r] - bmu[r]) * biv[r];
+            const float gg = a.bwd.act ? hv[r] * bn_act_grad(a.bwd.act, fmaf(xh, bga[r], bbe[r])) : hv[r];
+            cs[j][r] += gg;
+            cq[j][r] = fmaf(gg, xh, cq[j][r]);
+          }
+        }
         if (STATS) {
           const float d0 = bf2f(h0) - kv.x, d1 = bf2f(h1) - kv.y, d2 = bf2f(h2) - kv.z, d3 = bf2f(h3) - kv.w;
           cs[j][0] += d0; cs[j][1] += d1; cs[j][2] += d2; cs[j][3] += d3;
@@ -309,7 +364,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    if constexpr (STATS) {
+    if constexpr (STATS || BST) {
       // the 16 row lanes of each column (DPP) here; the 4 row-group waves' partials are
       // summed after the NEXT K-tile's barrier (stats_flush), so this epilogue has no barrier
       // of its own and the MFMAs of the next unit start right away
@@ -334,15 +389,24 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   int pend_part = 0, pend_n0 = 0;
   const __amdgpu_buffer_rsrc_t rp = mk_rsrc(a.bn_part, (int64_t)OOB);
   const int ncol = a.Ncol;
+  const __amdgpu_buffer_rsrc_t rq = mk_rsrc(BST ? a.bwd.part : a.bn_part, (int64_t)OOB);
+  const int nblk = (int)(a.M / (WT * WT));
   auto stats_flush = [&]() __attribute__((always_inline)) {
     const float *red = reinterpret_cast<const float *>(smem + RED0);
     const int v = tid & 255, cl = v >> 1, w = v & 1;
     const float t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
                     (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
-    bstore32(rp, t, (uint32_t)((pend_part * 2 * ncol + w * ncol + pend_n0 + cl) * 4));
+    if constexpr (BST) {
+      // [channel group][block][2 group channels]
+      const int gi = pend_n0 / a.ogc;
+      bstore32(rq, t, (uint32_t)((((int64_t)gi * nblk + pend_part) * 2 * a.ogc + w * a.ogc + pend_n0 - gi * a.ogc + cl) * 4));
+    } else {
+      bstore32(rp, t, (uint32_t)((pend_part * 2 * ncol + w * ncol + pend_n0 + cl) * 4));
+    }
   };
   constexpr int ST = 16;                     // output stores of one epilogue per wave
-  constexpr int SS = STATS ? 1 : 0;          // the statistics store (at the next unit's tap 0)
+  constexpr int SS = (STATS || BST) ? 1 : 0; // the statistics store (at the next unit's tap 0)
+  constexpr int XL = BST ? 16 : 0;           // BST: BN-input loads issued at tap 5
 
   // window pieces of the next unit: 2 per wave at taps 0-2 (48 slots for 41 pieces; the extra
   // slots repeat piece 40), so a unit's window has landed long before its first read
@@ -359,7 +423,8 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   for (int t = 0; t < 3; ++t) issue_b(cu, t, t);
   win_sync<4>();                            // window 0 and K-tile 0 landed (B 1, 2 in flight)
   if constexpr (XF) {
-    xform(cu, 0);
+    xform(cu, 0, 0);
+    xform(cu, 0, 1);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   read_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
@@ -382,7 +447,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       // T = 0, 1
       // (+ the output stores of the previous unit's tap 8 for T = 0, 1 and its statistics
       // store, issued at this unit's tap 0, for T = 1, 2)
-      constexpr int NB = 2 + (((T + 8) % 9) < 3 ? WPT : 0);
+      constexpr int NB = 2 + (((T + 8) % 9) < 3 ? WPT : 0) + ((T == 6 || T == 7) ? XL : 0);
       constexpr int X = (T <= 1 ? ST : 0) + ((T == 1 || T == 2) ? SS : 0);
       if constexpr (X > 0) {
         if (prev_st) win_sync<NB + X>();
@@ -396,8 +461,17 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       }
       if constexpr (T + 3 < 9) issue_b(cu, T + 3, T % 3);
       else issue_b(nx, T + 3 - 9, T % 3);
-      if constexpr (STATS && T == 0) {
+      if constexpr ((STATS || BST) && T == 0) {
         if (prev_st) stats_flush();
+      }
+      if constexpr (BST && T == 5) issue_x(cu);
+      if constexpr (BST && T == 8) {
+        // (landed: older than the K-tile this step waited for; the empty asm keeps their
+        // uses below the wait)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(xq[j][i]));
       }
       cbf16x8 na[2][4], nb[2][4];
       if constexpr (T + 1 < 9)
@@ -413,7 +487,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
-      if constexpr (XF && T == 6) xform(nx, WB ^ 1);
+      if constexpr (XF && (T == 6 || T == 7)) xform(nx, WB ^ 1, T - 6);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -446,7 +520,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     cu = nx;
     nx = unit(u + 3);
   }
-  if constexpr (STATS) {                    // the last tile's statistics
+  if constexpr (STATS || BST) {             // the last tile's statistics
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stats_flush();
   }
@@ -455,7 +529,9 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 }
 
 bool win_ok(const FwdArgs &a, bool dgrad) {
-  if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend || a.bwd.part) return false;
+  if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend) return false;
+  if (a.bwd.part && (!dgrad || a.bwd.rscale || a.bwd.grows || !a.bwd.x || !a.bwd.mean || !a.bwd.invstd ||
+                     a.Ncol > 512)) return false;
   if (a.xf && (dgrad || a.KC > 512)) return false;
   if (dgrad && a.bn_part) return false;
   if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
@@ -687,6 +763,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue(t + 1 < t1 ? t + 1 : t, b ^ 1, t + 1 < t1);
     compute();
+    // (transformed after this tile's MFMAs: between its k32 steps measured slower, 948 -> 988 us)
     if constexpr (XF) {
       if (t + 1 < t1) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -762,7 +839,9 @@ bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) 
   if (G > ntiles) G = ntiles;
   const int ncb = a.KC / 64;
   const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
-  if (dgrad)
+  if (dgrad && a.bwd.part)
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (dgrad)
     hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (a.xf && a.bn_part)
     hipLaunchKernelGGL((conv_win_kernel<false, true, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);

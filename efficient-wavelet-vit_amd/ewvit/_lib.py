@@ -67,6 +67,9 @@ SIGNATURES = {
                                _vp],
     'ewvit_conv2d_bwd_weight_xf': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
                                    _i64, _i64, _i64, _vp, _vp],
+    'ewvit_conv2d_bwd_bn_win_rows': [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64],
+    'ewvit_conv2d_bwd_data_bn_win': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                     _i32, _vp, _vp],
     'ewvit_bn_coef': [_i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_bn_fwd_partials': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp, _vp,
                               _vp, _vp, _i32, _i32, _vp],

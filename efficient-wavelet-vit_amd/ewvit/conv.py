@@ -16,6 +16,7 @@ returns the input gradient in z's layout — the concatenation is never built.
 """
 import contextlib
 import ctypes
+import os
 import threading
 import weakref
 
@@ -375,6 +376,11 @@ def conv2d_bn_stats(x, weight, bias, stride, shift, levels=1, groups=1, max_rows
     return y, part, shifts, nrc
 
 
+# BnReluConvFn's BatchNorm backward sums taken by the conv's windowed input-gradient epilogue
+# (ewvit_conv2d_bwd_data_bn_win; False: ewvit_bn_bwd's own reduction pass, A/B and tests)
+_BN_BWD_EPI = os.environ.get('EWVIT_BN_BWD_EPI', '1') != '0'
+
+
 class BnReluConvFn(torch.autograd.Function):
     """conv3x3(relu(BatchNorm(z))) in training, the BatchNorm + ReLU applied inside the windowed
     conv's operand staging (ewvit_conv2d_fwd_bn_xf / ewvit_conv2d_bwd_weight_xf): the normalised
@@ -383,9 +389,11 @@ class BnReluConvFn(torch.autograd.Function):
     nrc)); the conv reads the levels as channel groups (mwt.py:112's concatenation).  Forward:
     ewvit_bn_coef (the BN's finalisation: batch / running statistics, counter, scale and shift)
     + the transformed conv with the next BatchNorm's statistics (`ystats`).  Backward: the
-    conv's input gradient (plain dgrad: it does not read z), the transformed weight gradient,
-    then the BatchNorm + ReLU backward on z — the same kernels, in the same order, as
-    BatchNormActFn followed by Conv2dFn, so every result is bit-identical to that pair."""
+    conv's input gradient (it does not read z) with the BatchNorm backward sums in its epilogue,
+    the transformed weight gradient, then the BatchNorm + ReLU backward's dx pass on z.  With
+    _BN_BWD_EPI off the BN backward runs its own reduction (ewvit_bn_bwd) — then the same
+    kernels in the same order as BatchNormActFn followed by Conv2dFn, every result bit-identical
+    to that pair; with it on the sums are the same values summed in another order."""
 
     @staticmethod
     def forward(ctx, z, weight, bias, gamma, beta, running_mean, running_var, momentum, eps, counter, levels, zpart,
@@ -449,10 +457,20 @@ class BnReluConvFn(torch.autograd.Function):
         gs = N * H * W * C
         dev = zc.device
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        # d relu(bn(z)) — the input gradient of the conv, in z's level-major layout
+        # d relu(bn(z)) — the input gradient of the conv, in z's level-major layout — and the BN
+        # backward's per-block sums of g = da * relu'(.) and g * xhat
         da = torch.empty_like(zc, memory_format=torch.channels_last)
-        L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, 3, 1, C, gs, L.stream(da),
-               work={'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + da.numel() + wpt.numel()) * 2})
+        work = {'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + da.numel() + wpt.numel()) * 2}
+        rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs)) if _BN_BWD_EPI else 0
+        bpart = None
+        if rows > 0:
+            bpart = torch.empty(levels * rows, 2 * C, dtype=torch.float32, device=dev)
+            L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, C, gs,
+                   L.ptr(zc), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, L.ptr(bpart), L.stream(da),
+                   work=work)
+        else:
+            L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, 3, 1, C, gs,
+                   L.stream(da), work=work)
         wparam, bparam, gparam, beparam = ctx.params
         dwf = grad_out(wparam, ctx.gen)
         s_co, s_ci, s_kh, s_kw = dwf.stride()
@@ -474,10 +492,16 @@ class BnReluConvFn(torch.autograd.Function):
         dz = torch.empty_like(zc)
         dg = bnmod._affine_grad(gparam, ctx.gen, C, dev)
         db2 = bnmod._affine_grad(beparam, ctx.gen, C, dev)
-        bws = torch.empty(L.load().ewvit_bn_workspace(M, C, levels) // 4, dtype=torch.float32, device=dev)
-        L.call('ewvit_bn_bwd', L.ptr(da), L.ptr(zc), L.ptr(dz), L.dt(zc), M, C, L.ptr(gamma), L.ptr(beta), L.ptr(mean),
-               L.ptr(invstd), 1, L.ptr(dg), L.ptr(db2), 0, levels, L.ptr(bws), L.stream(dz),
-               work={'bytes': 5 * zc.numel() * zc.element_size()})
+        if bpart is not None:
+            p2, n2 = bnmod.fold_bwd_partials(bpart, rows, levels, C)
+            L.call('ewvit_bn_bwd_partials', L.ptr(da), L.ptr(zc), L.ptr(dz), L.dt(zc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(mean), L.ptr(invstd), 1, L.ptr(dg), L.ptr(db2), None, 1, L.ptr(p2), n2, levels, L.stream(dz),
+                   work={'bytes': 3 * zc.numel() * zc.element_size()})
+        else:
+            bws = torch.empty(L.load().ewvit_bn_workspace(M, C, levels) // 4, dtype=torch.float32, device=dev)
+            L.call('ewvit_bn_bwd', L.ptr(da), L.ptr(zc), L.ptr(dz), L.dt(zc), M, C, L.ptr(gamma), L.ptr(beta),
+                   L.ptr(mean), L.ptr(invstd), 1, L.ptr(dg), L.ptr(db2), 0, levels, L.ptr(bws), L.stream(dz),
+                   work={'bytes': 5 * zc.numel() * zc.element_size()})
         g = ctx.gen
         return (dz, grads.give(wparam, dwf, g), grads.give(bparam, dbf, g) if has_bias else None,
                 grads.give(gparam, dg, g), grads.give(beparam, db2, g), *(None,) * 8)

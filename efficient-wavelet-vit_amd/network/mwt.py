@@ -23,6 +23,8 @@ If ``wavelet_transform`` is overridden on the instance or class (as
 utils/visualize_feature_maps.py:151-158 does), forward falls back to the
 reference's per-level loop calling ``self.wavelet_transform`` (still on GPU).
 """
+import os
+
 import torch
 from torch import nn
 from torch.nn import functional as F
@@ -89,7 +91,7 @@ def _epi_stats(conv, bn, x, levels=1, groups=1):
 
 # the hf_conv['fusion'] BatchNorm + ReLU applied inside multiscale_fusion's conv (ewvit.conv.
 # BnReluConvFn) instead of by its own pass (0: the separate apply pass, A/B and tests)
-_FOLD_FUSION_BN = True
+_FOLD_FUSION_BN = os.environ.get('EWVIT_FOLD_FUSION_BN', '1') != '0'
 
 
 class PendingBNReLU:

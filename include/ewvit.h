@@ -422,6 +422,18 @@ int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, 
  * ewvit_bn_fwd_partials(act = relu) followed by ewvit_conv2d_fwd_bn / ewvit_conv2d_bwd_weight.
  * 3x3 stride 1 only, where the windowed kernels take the shape (ewvit_conv2d_xf_ok: 1 / 0;
  * Cin <= 512).  The input gradient of such a conv is the plain ewvit_conv2d_bwd_data. */
+/* The windowed 3x3 stride-1 input gradient with the backward statistics of the BatchNorm(+act)
+ * whose output the conv read (as ewvit_conv2d_bwd_data_bn, but one partial row per 16 x 16 dx
+ * block: part [groups][N*H*W/256][2 group_c], BatchNorm groups = dx's channel groups, mean /
+ * invstd [groups][group_c], gamma / beta [group_c] or NULL) — the MWT hf fusion BN's backward
+ * sums taken by multiscale_fusion's input gradient (reference network/mwt.py:60-72,114).
+ * ewvit_conv2d_bwd_bn_win_rows: rows per group, 0 when the windowed kernel does not take it. */
+int64_t ewvit_conv2d_bwd_bn_win_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
+                                     int64_t dx_group_c, int64_t dx_group_stride);
+int ewvit_conv2d_bwd_data_bn_win(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
+                                 int64_t Cin, int64_t Cout, int64_t dx_group_c, int64_t dx_group_stride,
+                                 const void *bx, const float *mean, const float *invstd, const float *gamma,
+                                 const float *beta, int act, float *part, void *stream);
 int ewvit_conv2d_xf_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
                        int64_t x_group_c, int64_t x_group_stride);
 int ewvit_conv2d_fwd_bn_xf(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,

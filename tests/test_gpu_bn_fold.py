@@ -27,6 +27,7 @@ def test_mwt_fold_bit_identical(hw, frames, monkeypatch):
     # multiscale conv's input-gradient epilogue (ewvit.bn BwdStatsLink, another summation order);
     # at the model's size (> BWD_LINK_MAX_ROWS tiles) it runs ewvit_bn_bwd, as the fold always does
     monkeypatch.setattr(ewvit.bn, '_BWD_LINK', False)
+    monkeypatch.setattr(ewvit.conv, '_BN_BWD_EPI', False)
     torch.manual_seed(11)
     a = M.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last).train()
     b = copy.deepcopy(a)
@@ -155,3 +156,88 @@ def test_bn_coef_matches_apply_pass():
     assert int((res['coef'][0] != res['apply'][0]).sum()) <= 2
     for u, v, n in zip(res['coef'][1:], res['apply'][1:], ('running_mean', 'running_var', 'counter', 'mean', 'invstd')):
         assert torch.equal(u, v), n
+
+
+@pytest.mark.parametrize('hw,frames', [(224, 2)])
+def test_mwt_fold_bwd_sums_in_dgrad_epilogue(hw, frames, monkeypatch):
+    """The fold with the fusion BN's backward sums taken by multiscale_fusion's windowed input-
+    gradient epilogue (ewvit_conv2d_bwd_data_bn_win + ewvit_bn_bwd_partials) against its own
+    reduction pass (ewvit_bn_bwd): forward and BN state identical; gradients equal up to the fp32
+    summation order of those sums (cosine >= 0.99999, norms within 1e-4; the gradients of biases
+    feeding a train-mode BN are exact zeros up to rounding noise and are skipped)."""
+    import ewvit
+    from network import mwt as M
+    torch.manual_seed(12)
+    a = M.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(frames, 3, hw, hw, device=DEV)
+    names = []
+    real = ewvit._lib.call
+    monkeypatch.setattr(ewvit._lib, 'call', lambda n, *r, **k: (names.append(n), real(n, *r, **k))[1])
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        ya = a(x)
+    ya.float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert 'ewvit_conv2d_bwd_data_bn_win' in names
+    monkeypatch.setattr(ewvit.conv, '_BN_BWD_EPI', False)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        yb = b(x)
+    yb.float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb)
+    for (n, u), v in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(u, v), n
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        if p.grad is None:
+            assert q.grad is None, n
+            continue
+        if n.endswith('0.bias') and not n.startswith('freq_pool'):
+            continue
+        u, v = p.grad.double().flatten(), q.grad.double().flatten()
+        c = float(u @ v / (u.norm() * v.norm() + 1e-300))
+        r = float(u.norm() / (v.norm() + 1e-300))
+        assert c >= 0.99999 and abs(r - 1) <= 1e-4, (n, c, r)
+
+
+def test_dgrad_bn_sums_match_explicit():
+    """ewvit_conv2d_bwd_data_bn_win: dx bit-identical to the plain windowed dgrad, the per-block
+    sums of g and g * xhat equal the float64 sums over the returned dx (1e-5 of scale)."""
+    import ewvit  # noqa: F401
+    from ewvit import _lib as L
+    from ewvit.conv import _pack
+    lib = L.load()
+    g = torch.Generator().manual_seed(21)
+    N, C, H, W, Cout, levels = 2, 128, 32, 48, 128, 3
+    NL, Cx = N * levels, C * levels
+    gc, gs = C, N * H * W * C
+    rows = int(lib.ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, gc, gs))
+    assert rows == N * H * W // 256
+    w = (torch.randn(Cout, Cx, 3, 3, generator=g) / (9 * Cx) ** 0.5).to(DEV)
+    _, wpt = _pack(w, Cx, True, True)
+    dy = torch.randn(N, Cout, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    z = torch.randn(NL, C, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mean = (torch.randn(levels, C, generator=g) * 0.1).to(DEV)
+    inv = (torch.rand(levels, C, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    dx0 = torch.empty_like(z)
+    dx1 = torch.empty_like(z)
+    part = torch.full((levels * rows, 2 * C), float('nan'), device=DEV)
+    L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Cx, Cout, 3, 1, gc, gs, L.stream(dy))
+    L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), N, H, W, Cx, Cout, gc, gs, L.ptr(z),
+           L.ptr(mean), L.ptr(inv), L.ptr(gamma), L.ptr(beta), 1, L.ptr(part), L.stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    zl = z.double().view(levels, N, C, H, W)
+    xh = (zl - mean.double().view(levels, 1, C, 1, 1)) * inv.double().view(levels, 1, C, 1, 1)
+    pre = xh * gamma.double().view(1, 1, C, 1, 1) + beta.double().view(1, 1, C, 1, 1)
+    gg = dx1.double().view(levels, N, C, H, W) * (pre > 0)
+    # per level and 16 x 16 block (image-major, block rows, block columns)
+    def blocks(t):
+        return t.view(levels, N, C, H // 16, 16, W // 16, 16).sum((4, 6)).permute(0, 1, 3, 4, 2).reshape(levels, rows, C)
+    s1, s2 = blocks(gg), blocks(gg * xh)
+    got = part.double().view(levels, rows, 2, C)
+    sc = float(s1.abs().max())
+    assert float((got[:, :, 0] - s1).abs().max()) <= 1e-5 * sc
+    sc2 = float(s2.abs().max())
+    assert float((got[:, :, 1] - s2).abs().max()) <= 1e-5 * sc2
