@@ -649,6 +649,11 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(a.wp, (int64_t)a.Ncol * K * 2);
+  // (builtin DMAs: hipcc then waits vmcnt(4) ahead of each K-tile's fragment reads, so one
+  // K-tile stays in flight whatever NS.  The asm DMAs of the windowed kernels, which leave
+  // NS-1 in flight, measured slower here — the step 18.29 -> 18.56 ms on one box,
+  // profiles/r05/ab/glds_asm_vs_builtin_ab.log: the backbone's small grids share the CUs with
+  // the MWT stream, and deeper DMA queues cost that stream more than they gain)
 
   // A rows staged by this lane: piece p = w*PA + j covers rows 8p..8p+7.  Every tap's
   // source pixel is the row's base pixel plus a tap offset that is the same for all
@@ -688,8 +693,11 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     int by, bx;            // base pixel (may lie outside the image)
     unsigned msk = 0;
     if (cls) {
-      // class taps: dy pixel (oh + dh, ow + dw), dh = (py + 1 - kh) / 2 in {0, 1}
-      for (int lt = 0; lt < a.ntap; ++lt) {
+      // class taps: dy pixel (oh + dh, ow + dw), dh = (py + 1 - kh) / 2 in {0, 1} (unrolled:
+      // a runtime index into the kernel argument's tapl[] puts the argument on the stack)
+#pragma unroll
+      for (int lt = 0; lt < 4; ++lt) {
+        if (lt >= a.ntap) break;
         const int tp = a.tapl[lt], kh = tp / 3, kw = tp - kh * 3;
         const int sh = oh + ((py + 1 - kh) >> 1), sw = ow + ((px + 1 - kw) >> 1);
         if (m < a.M && sh < a.srcH && sw < a.srcW) msk |= 1u << lt;
@@ -737,7 +745,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
         const int tp = dtap[j];
         const int kh = (tp * 11) >> 5, kw = tp - kh * 3;     // tp / 3 for tp < 32 (KS == 3)
         const int dpix = KS == 3 ? kh * a.srcW + kw : 0;
-        const bool ok = tp < KS * KS && ((vmask[j] >> tp) & 1u);
+        const bool ok = (tp < KS * KS) & (((vmask[j] >> tp) & 1u) != 0);
         glds16(rs, base + j * 1024, ok ? (uint32_t)(rb[j] + (dpix * a.sgc + dcc[j] * 8) * 2) : OOB);
         dtap[j] += tq;
         dcc[j] += tr;
@@ -749,7 +757,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
       for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
       return;
     }
-    const int rt = cls ? a.tapl[ltap] : ltap;      // the weight tap
+    const int rt = cls ? (ltap == 0 ? a.tapl[0] : ltap == 1 ? a.tapl[1] : ltap == 2 ? a.tapl[2] : a.tapl[3])
+                       : ltap;                     // the weight tap
     const int kh = rt / KS, kw = rt - kh * KS;
     int dpix;
     if (!DGRAD) dpix = kh * a.srcW + kw;
@@ -773,7 +782,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
 #pragma unroll
     for (int j = 0; j < PA; ++j)
       glds16(rs, base + j * 1024,
-             ((vmask[j] >> tap) & 1u) && c0 + lc8[j] < kcr ? (uint32_t)(rb[j] + sdelta) : OOB);
+                 ((((vmask[j] >> tap) & 1u) != 0) & (c0 + lc8[j] < kcr)) ? (uint32_t)(rb[j] + sdelta) : OOB);
     unsigned char *bb = smem + buf * STG + A_B + ws * PB * 1024;
 #pragma unroll
     for (int j = 0; j < PB; ++j) glds16(rw, bb + j * 1024, boff[j] == OOB ? OOB : boff[j] + kb);
@@ -784,15 +793,20 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   auto frag = [&](const unsigned char *img, int r, int ch) -> cbf16x8 {
     return *reinterpret_cast<const cbf16x8 *>(img + r * 128 + 16 * (ch ^ ((r >> 1) & 7)));
   };
+  // both 32-deep steps' fragments are read before the MFMAs, so the second step's reads run
+  // under the first step's MFMAs
   auto compute = [&](int buf) {
     const unsigned char *As = smem + buf * STG, *Bs = As + A_B;
+    cbf16x8 af[BK / 32][4], bfr[BK / 32][J];
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      cbf16x8 af[4], bfr[J];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(As, wm * 64 + i * 16 + fr, ks * 4 + fq);
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(As, wm * 64 + i * 16 + fr, ks * 4 + fq);
 #pragma unroll
-      for (int j = 0; j < J; ++j) bfr[j] = frag(Bs, wn * WN + j * 16 + fr, ks * 4 + fq);
+      for (int j = 0; j < J; ++j) bfr[ks][j] = frag(Bs, wn * WN + j * 16 + fr, ks * 4 + fq);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -800,8 +814,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
           // operands swapped (B first): the lane holds 4 consecutive output COLUMNS of
           // one row, acc[i][j][r] = C[i*16 + (lane&15)][j*16 + 4*(lane>>4) + r], so the
           // epilogue stores 8 B per lane straight from registers (no LDS image)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
   };
   // `inflight` counts issued K-tiles not yet multiplied (<= NS-1); the buffer refilled is
   // always the one every wave finished reading before the last barrier
@@ -1517,6 +1530,28 @@ static void launch_glds_dense(const FwdArgs &a, int64_t src_bytes, hipStream_t s
 
 // the LDS-DMA fwd/dgrad kernel when every K-tile stays in one tap and one channel
 // group and the operands fit 31-bit buffer offsets; false -> register-staged kernel
+// Tile of the LDS-DMA fwd / dgrad: 128 rows (256 for a <= 64-column dgrad over > 4096 row tiles:
+// the MWT fusion conv's input gradient); grids of < 128 such tiles — the backbone's long-K
+// 1x1 convs at 7^2 (stage 6 project forward / expand input gradient: 3136 x 256 x 1536, 50
+// tiles, 24 K-tiles each) — take 64-row tiles, and 64-column tiles if still < 128 (4x the
+// workgroups).  Any BatchNorm partial rows the kernel leaves follow its row tile.
+static int g_small_tiles = 1;
+extern "C" int ewvit_conv2d_set_small_tiles(int on) {
+  const int prev = g_small_tiles;
+  g_small_tiles = on ? 1 : 0;
+  return prev;
+}
+static void glds_tile(const FwdArgs &a, bool dgrad, int &bm, int &bn) {
+  bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
+  const int64_t ntn = (a.Ncol + bn - 1) / bn, mt = (a.M + 127) / 128;
+  bm = 128;
+  if (dgrad && bn == 64 && mt * ntn > 4096 && !a.bwd.part) { bm = 256; return; }
+  if (g_small_tiles && bn >= 64 && mt * ntn < 128) {
+    bm = 64;
+    if (bn == 128 && (a.M + 63) / 64 * ntn < 128) bn = 64;
+  }
+}
+
 template <bool DGRAD>
 static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int *bm_out = nullptr) {
   const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
@@ -1548,14 +1583,14 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
       a.M * a.ogc >= (int64_t)1 << 40)
     return false;
   const int tap_inner = 1;           // the 9 taps of a 64-channel block are consecutive K-tiles
-  // <= 32 columns (stage 2's entry-conv input gradient, 24 channels): 32-wide column tiles
-  const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
-  const int ntn = (a.Ncol + bn - 1) / bn;
-  // a <= 64-column dgrad over > 4096 row tiles (the MWT fusion conv's 56-channel input
+  // <= 32 columns (stage 2's entry-conv input gradient, 24 channels): 32-wide column tiles.
+  // A <= 64-column dgrad over > 4096 row tiles (the MWT fusion conv's 56-channel input
   // gradient, 2.4 M pixels): 256-row blocks, 535 -> 505 us.  Stage 2's 48-channel 3x3 dgrad
   // (1568 row tiles) runs faster on 8-wave 128-row blocks (96 -> 75 us, tools/dgrad_ab.sh)
-  const bool big = DGRAD && bn == 64 && (a.M + 127) / 128 * ntn > 4096 && !a.bwd.part;
-  const int BM = big ? 256 : 128;
+  int BM, bn;
+  glds_tile(a, DGRAD, BM, bn);
+  const int ntn = (a.Ncol + bn - 1) / bn;
+  const bool big = BM == 256;
   if (bm_out) *bm_out = BM;
   const int64_t mt = (a.M + BM - 1) / BM;
   const int64_t nwg = mt * ntn;
@@ -1580,8 +1615,14 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
   const bool w8 = nwg <= 2048 || (DGRAD && bn == 128);
   const bool sg = nwg <= 256;
   constexpr bool BST = DGRAD;      // (the statistics epilogue is a separate instantiation)
-  if (DGRAD && a.bwd.part) {
-    // the backward-statistics epilogue: 128-row tiles always (the partial rows
+  if (BM == 64) {
+    if (DGRAD && a.bwd.part) {
+      if (bn == 64) EWVIT_GLDS_FWDW(64, 64, 4, 4, BST);
+      else EWVIT_GLDS_FWDW(64, 128, 4, 4, BST);
+    } else if (bn == 64) EWVIT_GLDS_FWDW(64, 64, 4, 4, false);
+    else EWVIT_GLDS_FWDW(64, 128, 4, 4, false);
+  } else if (DGRAD && a.bwd.part) {
+    // the backward-statistics epilogue: 128-row tiles (the partial rows
     // ewvit_conv2d_bwd_bn_rows promised)
     if (bn == 32) EWVIT_GLDS_FWDW(128, 32, 2, 2, BST);
     else if (bn == 64) {
@@ -1707,7 +1748,9 @@ static int fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cou
   FwdArgs a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
   a.bn_part = reinterpret_cast<float *>(1);    // (a statistics epilogue)
   if (win_ok(a, false)) return 256;
-  return 128;
+  int bm, bn;
+  glds_tile(a, false, bm, bn);
+  return bm;
 }
 
 extern "C" int64_t ewvit_conv2d_fwd_bn_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
@@ -1902,7 +1945,12 @@ extern "C" int64_t ewvit_conv2d_bwd_bn_rows(int64_t N, int64_t H, int64_t W, int
   if (stride != 1 || !ewvit_conv2d_bwd_data_add_ok(N, H, W, Cin, Cout, ksize, stride) ||
       Cin > 65536)
     return 0;
-  return (N * H * W + 127) / 128;
+  FwdArgs a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
+  a.M = (int64_t)N * H * W; a.Ncol = (int)Cin; a.KC = (int)Cout;
+  a.bwd.part = reinterpret_cast<float *>(1);
+  int bm, bn;
+  glds_tile(a, true, bm, bn);
+  return (N * H * W + bm - 1) / bm;
 }
 
 // dx = dgrad(dy) (+ addend, when not null; plain dx only) and the backward statistics of the

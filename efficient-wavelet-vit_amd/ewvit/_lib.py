@@ -58,6 +58,7 @@ SIGNATURES = {
     'ewvit_set_grid_cap': [_i32],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_set_wgrad_1x1': [_i32, _i32, _i32],
+    'ewvit_conv2d_set_small_tiles': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -67,7 +68,6 @@ SIGNATURES = {
                                _vp],
     'ewvit_conv2d_bwd_weight_xf': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
                                    _i64, _i64, _i64, _vp, _vp],
-    'ewvit_conv2d_bwd_bn_win_rows': [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64],
     'ewvit_conv2d_bwd_data_bn_win': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
                                      _i32, _vp, _vp],
     'ewvit_bn_coef': [_i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
@@ -129,6 +129,7 @@ SIGNATURES = {
 
 # size queries: name -> (restype, argtypes)
 QUERIES = {
+    'ewvit_conv2d_bwd_bn_win_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64]),
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_vit_layer_workspace': (_i64, [_i32]),
     'ewvit_gemm_tallk_workspace': (_i64, [_i64, _i64, _i64]),
@@ -173,14 +174,22 @@ def load():
     lib.ewvit_last_error.argtypes = []
     if lib.ewvit_abi_version() != ABI_VERSION:
         raise RuntimeError(f'ewvit: ABI {lib.ewvit_abi_version()} != expected {ABI_VERSION}')
+    # (an EWVIT_LIB build for an A/B may predate entry points: those stay unbound)
+    ab = bool(os.environ.get('EWVIT_LIB'))
     for name, args in SIGNATURES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
     for name, (res, args) in QUERIES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    if os.environ.get('EWVIT_SMALL_TILES') == '0' and hasattr(lib, 'ewvit_conv2d_set_small_tiles'):
+        lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
     _lib = lib
     return lib
 

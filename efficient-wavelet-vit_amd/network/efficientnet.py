@@ -95,8 +95,9 @@ class ConvBNAct(nn.Sequential):
                 and conv.padding[0] == conv.kernel_size[0] // 2 and conv.stride[0] == conv.stride[1]
                 and conv.out_channels <= 2048):
             rows = ewvit.conv.bn_stat_rows(x, conv.weight, conv.stride[0])
+            # (counted in 128-row tiles whatever the kernel's row tile: 64 on small grids)
             if rows and (x.shape[0] * ((x.shape[2] - 1) // conv.stride[0] + 1) *
-                         ((x.shape[3] - 1) // conv.stride[0] + 1) + rows - 1) // rows <= _EPI_STATS_MAX_TILES:
+                         ((x.shape[3] - 1) // conv.stride[0] + 1) + 127) // 128 <= _EPI_STATS_MAX_TILES:
                 r = ewvit.conv.conv2d_bn_stats(x, conv.weight, conv.bias, conv.stride[0], bn.running_mean)
                 if r is not None:
                     return r[0], r[1:]

@@ -391,6 +391,9 @@ int ewvit_conv2d_set_wgrad_wide(int variant);
  * its pixel splits (0 = never: the generic kernel), fewest 64-pixel K-tiles per split, LDS ring
  * depth (2 | 3).  Test / tuning switch; returns the previous target. */
 int ewvit_conv2d_set_wgrad_1x1(int target_wg, int min_ktiles, int ring);
+/* LDS-DMA fwd / dgrad on grids of < 128 row tiles: 64-row (and 64-column) tiles, 1 (default),
+ * or the 128-row tiles everywhere, 0 (test switch).  Returns the previous setting. */
+int ewvit_conv2d_set_small_tiles(int on);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs

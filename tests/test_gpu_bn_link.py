@@ -143,7 +143,7 @@ def test_conv_dgrad_bn(N, H, W, Cin, Cout, act, addend, scaled):
         L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Cin, Cout, 1, 1, 0, 0,
                L.stream(dy))
     rows = int(L.load().ewvit_conv2d_bwd_bn_rows(N, H, W, Cin, Cout, 1, 1))
-    assert rows == (N * H * W + 127) // 128
+    assert rows in ((N * H * W + 127) // 128, (N * H * W + 63) // 64)     # 64-row tiles on small grids
     part = torch.full((rows, 2 * Cin), float('nan'), device=DEV)
     nrc = ctypes.c_int(0)
     L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), L.ptr(sk), N, H, W, Cin, Cout, 1, 1, 0, 0,
@@ -362,7 +362,7 @@ def test_conv_dgrad_bn_channel_groups(cap):
         L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Lv * C, Cout, 3, 1, C, gs,
                L.stream(dy))
         tiles = int(lib.ewvit_conv2d_bwd_bn_rows(N, H, W, Lv * C, Cout, 3, 1))
-        assert tiles == (N * H * W + 127) // 128
+        assert tiles in ((N * H * W + 127) // 128, (N * H * W + 63) // 64)
         part = torch.full((Lv * tiles, 2 * C), float('nan'), device=DEV)
         nrc = ctypes.c_int(0)
         L.call('ewvit_conv2d_bwd_data_bn', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), None, N, H, W, Lv * C, Cout, 3, 1, C,
@@ -420,8 +420,8 @@ def test_conv_dgrad_bn_row_groups(cap):
         lib.ewvit_set_grid_cap(prev)
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1)
-    per = M // Lv // 128
-    assert nrc.value == per and tiles == Lv * per
+    per = tiles // Lv                                  # 128-row tiles, or 64 on small grids
+    assert nrc.value == per and tiles == Lv * per and per in (M // Lv // 128, M // Lv // 64)
     for lv in range(Lv):
         sl = slice(lv * N, (lv + 1) * N)
         d, x = dx1[sl].double().cpu(), bx[sl].double().cpu()

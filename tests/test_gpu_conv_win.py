@@ -28,7 +28,7 @@ def _run(lib, L, win, cap, z, wp, wpt, bias, dy, shift, N, H, W, Cx, Cout, gc, g
         sums = None
         if stats:
             rows = int(lib.ewvit_conv2d_fwd_bn_rows(N, H, W, Cx, Cout, 3, 1))
-            assert rows == (256 if win else 128)
+            assert rows == 256 if win else rows in (64, 128)      # the generic kernel: 64-row tiles on small grids
             M = N * H * W
             part = torch.zeros((M + rows - 1) // rows, 2 * Cout, device=DEV)
             so = torch.empty(Cout, device=DEV)

@@ -75,11 +75,16 @@ def main():
     ap.add_argument('--bnstats', action='store_true', help='time fwd against fwd with BN statistics in the epilogue')
     ap.add_argument('--w1', default=None, help='1x1 wgrad kernel settings to time (ewvit_conv2d_set_wgrad_1x1), '
                     'target_wg:min_ktiles:ring pairs, e.g. 0:4:3,256:4:3,128:4:3 (wgrad only)')
+    ap.add_argument('--small', default=None, help='ewvit_conv2d_set_small_tiles settings to time, e.g. 0,1 (replaces --variants)')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
     a.variants = [int(v) for v in a.variants.split(',')]
+    small = None
+    if a.small:
+        small = [int(q) for q in a.small.split(',')]
+        a.variants = [1 + 10000 * i for i in range(len(small))]
     w1 = None
     if a.w1:
         w1 = [tuple(int(q) for q in t.split(':')) for t in a.w1.split(',')]
@@ -143,6 +148,12 @@ def main():
         rows = {}
         for r in range(a.rounds):              # interleaved A/B rounds in one process
             for v in a.variants:
+                if small is not None:
+                    lib.ewvit_conv2d_set_small_tiles(small[v // 10000])
+                    lib.ewvit_conv2d_set_glds(1)
+                    for pn, fn in (('fwd', fwd), ('dgrad', dgrad)):
+                        rows.setdefault((v, pn), []).append(graph_time(fn, a.iters))
+                    continue
                 if w1:
                     lib.ewvit_conv2d_set_wgrad_1x1(*w1[v // 10000])
                     lib.ewvit_conv2d_set_glds(1)
@@ -162,8 +173,13 @@ def main():
         if a.ww is not None:
             lib.ewvit_conv2d_set_ww(0)
         lib.ewvit_conv2d_set_wgrad_1x1(256, 4, 3)
+        lib.ewvit_conv2d_set_small_tiles(1)
         for v in a.variants:
             parts = []
+            if small is not None:
+                print(f'{name:15s} [small {small[v // 10000]}] fwd {min(rows[(v, "fwd")]):8.1f} us | dgrad '
+                      f'{min(rows[(v, "dgrad")]):8.1f} us', flush=True)
+                continue
             if w1:
                 t = min(rows[(v, 'wgrad')])
                 print(f'{name:15s} [w1 {":".join(map(str, w1[v // 10000])):>10s}] wgrad {t:8.1f} us {flops / t / 1e6:6.0f} TF/s',
