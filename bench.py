@@ -370,7 +370,7 @@ def main():
     for r in table.values():
         r['per_step'] = r['launches'] / kt
     # the same pass with the MWT on the main stream and uncapped grids: each kernel on the
-    # whole chip (the timed step runs the MWT's big launches on 160 of the 256 CUs, beside
+    # whole chip (the timed step runs the MWT's big launches on 128 of the 256 CUs, beside
     # the backbone — network/dama.py _mwt_grid_cap — so their as-run durations are longer)
     # (every rank runs it: the eager step issues the gradient all-reduces and the buffer
     # broadcast, so a rank-0-only pass would wait on its peers forever)
@@ -413,7 +413,7 @@ def main():
         res['roofline'] = roofline_for(*dom, config=args.config, adam_per_step=aps) if dom else None
         if res['roofline'] is not None:
             res['roofline']['timing'] = ('HIP events around every launch of an eager pass of the step as it runs '
-                                         '(MWT on its own stream, its big grids capped at 160 workgroups)')
+                                         '(MWT on its own stream, its big grids capped at 128 workgroups)')
         if iso_table and dom and dom[0] in iso_table:
             iso = roofline_for(dom[0], iso_table[dom[0]], config=args.config, adam_per_step=aps)
             iso['timing'] = 'same pass with one stream and uncapped grids (each kernel on the whole chip)'

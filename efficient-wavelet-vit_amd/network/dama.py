@@ -44,16 +44,18 @@ def _branch_streams():
     return os.environ.get('EWVIT_BRANCH_STREAMS', '1') == '1'
 
 
-MWT_GRID_CAP = 160          # one process per GPU, nothing else on the chip (world 1)
+MWT_GRID_CAP = 128          # one process per GPU, nothing else on the chip (world 1)
 RCCL_CU_RESERVE = 16        # CUs left to RCCL's all-reduce kernels per rank when world > 1
 
 
 def _mwt_grid_cap(world=None):
     """Workgroups per big-grid MWT launch (LDS-DMA convs, BatchNorm passes) while the MWT
     shares the GPU with the backbone (EWVIT_MWT_GRID_CAP, 0 = uncapped): the MWT walks its
-    tiles / rows on ~160 of the 256 CUs and the backbone's latency-bound kernels keep the
-    rest.  Measured (config 2, graph replay, 3 rounds): cap 0 2754, 144 2919, 160 2952,
-    192 2910, 224 2870 frames/s; 64 / 96 make the MWT the critical path (1747 / 2300).
+    tiles / rows on 128 of the 256 CUs (16 per XCD) and the backbone's latency-bound kernels
+    keep the rest.  Measured with round 5's windowed MWT convs (config 2, graph replay, same
+    box, 2 rounds each, profiles/r05/ab/cap_sweep*.log): 64 2750, 96 3546, 112 3541, 120 3572,
+    **128 3573-3586**, 136 3507, 144 3513, 160 3519, 192 3464 frames/s (round 4's kernels: 160
+    best, 2952 against 2919 at 144).
 
     This is the knob of the CU budget in data parallel (reference train.py:249-251 on N
     GPUs): the bucket all-reduces' RCCL kernels run during the backward beside both branches
