@@ -2001,10 +2001,13 @@ extern "C" int ewvit_conv2d_bwd_data_bn(const void *dy, const void *wp_t, void *
 // the windowed input gradient with the backward statistics of the BatchNorm(+act) whose output
 // the conv read (convwin.hip BST): one partial row per 16 x 16 block per channel group, part
 // [groups][N*H*W / 256][2 group_c]; BatchNorm groups = dx's channel groups (mean / invstd
-// [groups][group_c], gamma / beta [group_c] or null).  ewvit_conv2d_bwd_bn_win_rows: the partial
-// rows per group, 0 when the windowed kernel does not take the shape.
+// [groups][group_c], gamma / beta [group_c] or null), or — a plain dx (group_c = Cin,
+// group_stride 0) with bn_group_rows > 0 — slices of that many rows (whole images; mean / invstd
+// [N*H*W / bn_group_rows][Cin]), part [slices][bn_group_rows / 256][2 Cin].
+// ewvit_conv2d_bwd_bn_win_rows: N*H*W / 256 (the partial rows per channel group; with row groups
+// the total over the slices), 0 when the windowed kernel does not take the shape.
 static bool bst_args(FwdArgs &a, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
-                     int64_t dx_group_c, int64_t dx_group_stride) {
+                     int64_t dx_group_c, int64_t dx_group_stride, int64_t bn_group_rows) {
   if (ksize != 3 || stride != 1 || dx_group_c <= 0 || Cin % dx_group_c) return false;
   a = fwd_args(N, H, W, Cin, Cout, ksize, stride);
   a.M = (int64_t)a.g.N * a.g.H * a.g.W; a.Ncol = a.g.Cin; a.KC = a.g.Cout;
@@ -2013,30 +2016,34 @@ static bool bst_args(FwdArgs &a, int64_t N, int64_t H, int64_t W, int64_t Cin, i
   a.bwd.part = reinterpret_cast<float *>(1);
   a.bwd.x = reinterpret_cast<const bf16_t *>(2);
   a.bwd.mean = a.bwd.invstd = reinterpret_cast<const float *>(4);
+  if (bn_group_rows < 0 || (bn_group_rows && (dx_group_stride || dx_group_c != Cin))) return false;
+  a.bwd.grows = bn_group_rows;
   const int64_t sb = 2 * N * H * W * Cout;
   return sb < (int64_t)OOB && win_ok(a, true);
 }
 extern "C" int64_t ewvit_conv2d_bwd_bn_win_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize,
-                                               int stride, int64_t dx_group_c, int64_t dx_group_stride) {
+                                               int stride, int64_t dx_group_c, int64_t dx_group_stride,
+                                               int64_t bn_group_rows) {
   FwdArgs a;
-  return bst_args(a, N, H, W, Cin, Cout, ksize, stride, dx_group_c, dx_group_stride) ? N * H * W / 256 : 0;
+  return bst_args(a, N, H, W, Cin, Cout, ksize, stride, dx_group_c, dx_group_stride, bn_group_rows) ? N * H * W / 256
+                                                                                                     : 0;
 }
 extern "C" int ewvit_conv2d_bwd_data_bn_win(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H,
                                             int64_t W, int64_t Cin, int64_t Cout, int64_t dx_group_c,
                                             int64_t dx_group_stride, const void *bx, const float *mean,
                                             const float *invstd, const float *gamma, const float *beta, int act,
-                                            float *part, void *stream) {
+                                            int64_t bn_group_rows, float *part, void *stream) {
   EWVIT_CHECK_ARG(dy && wp_t && dx && bx && mean && invstd && part && act >= 0 && act <= 2,
                   "conv2d_bwd_data_bn_win: bad args");
   ConvGeom g = mkg(N, H, W, Cin, Cout, 3, 1);
   if (int rc = check_geom(g, "conv2d_bwd_data_bn_win")) return rc;
   if (int rc = check_group(dx_group_c, dx_group_stride, Cin, N * H * W, "conv2d_bwd_data_bn_win", "dx")) return rc;
   FwdArgs a;
-  EWVIT_CHECK_ARG(bst_args(a, N, H, W, Cin, Cout, 3, 1, dx_group_c, dx_group_stride),
+  EWVIT_CHECK_ARG(bst_args(a, N, H, W, Cin, Cout, 3, 1, dx_group_c, dx_group_stride, bn_group_rows),
                   "conv2d_bwd_data_bn_win: shape not taken (query ewvit_conv2d_bwd_bn_win_rows)");
   a.src = (const bf16_t *)dy; a.wp = (const bf16_t *)wp_t; a.bias = nullptr; a.out = (bf16_t *)dx;
   a.bwd.part = part; a.bwd.x = (const bf16_t *)bx; a.bwd.mean = mean; a.bwd.invstd = invstd; a.bwd.gamma = gamma;
-  a.bwd.beta = beta; a.bwd.rscale = nullptr; a.bwd.act = act; a.bwd.hw = (int)(H * W); a.bwd.grows = 0;
+  a.bwd.beta = beta; a.bwd.rscale = nullptr; a.bwd.act = act; a.bwd.hw = (int)(H * W); a.bwd.grows = bn_group_rows;
   const int64_t sb = 2 * N * H * W * Cout;
   EWVIT_CHECK_ARG(launch_win(a, sb, true, as_stream(stream)), "conv2d_bwd_data_bn_win: windowed kernel refused");
   return launch_status("conv2d_bwd_data_bn_win");

@@ -21,10 +21,10 @@ struct ConvGeom {
 // A(m, k): m = pixel of the OUTPUT grid of this GEMM (y for fwd, dx for dgrad),
 // k = tap * KC + c (KC = Cin for fwd, Cout for dgrad).  B(k, n) = Wp[n][k].
 struct FwdArgs {
-  const bf16_t *src;     // gathered operand: x (fwd) or dy (dgrad), grouped NHWC
-  const bf16_t *wp;      // packed weights [Ncol][taps][KC]
-  const float *bias;     // [Ncol] or null
-  bf16_t *out;           // [M][Ncol], grouped NHWC
+  const bf16_t *src = nullptr;   // gathered operand: x (fwd) or dy (dgrad), grouped NHWC
+  const bf16_t *wp = nullptr;    // packed weights [Ncol][taps][KC]
+  const float *bias = nullptr;   // [Ncol] or null
+  bf16_t *out = nullptr;         // [M][Ncol], grouped NHWC
   ConvGeom g;
   int64_t M;
   int Ncol, KC;          // GEMM N and per-tap K

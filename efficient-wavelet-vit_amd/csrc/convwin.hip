@@ -105,13 +105,25 @@ struct WinUnit {
 // over the bf16-rounded dx, g = dx * act'(xhat * gamma + beta) — what ewvit_bn_bwd_partials
 // finalises.  The block's BN-input values are loaded at tap 5 of its last channel block (asm,
 // counted in the waits of taps 6, 7; OOB for other units), so the epilogue never waits on them.
-template <bool DGRAD, bool STATS, bool XF = false, bool BST = false>
+// KS (dgrad, 64 output columns: hf_conv['fusion']'s input gradient, 128 -> 64): a tile is the
+// block's 256 pixels x 64 columns and the two waves of a row group split each K-tile's 64 k
+// between them (wn = the k32 half) — the same 64 x 64 wave tile, so the same LDS bytes per
+// MFMA as the 128-column form, over a 64 x 64 weight K-tile (8 KB slots).  At a tile's end
+// each wave hands the partner the two accumulator rows the partner stores (8 KB per wave,
+// through the 24 KB the smaller ring leaves and the just-consumed window buffer) and adds the
+// partner's half of its own two rows: the k-halves summed half 0 + half 1 in fp32, then rounded
+// once as before (not bit-identical to the generic kernel's k order; within its rounding).
+template <bool DGRAD, bool STATS, bool XF = false, bool BST = false, bool KS = false>
 __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_bytes, int64_t out_bytes, int ntn,
                                                        int ntiles, int ncb) {
+  static_assert(!KS || (DGRAD && !STATS && !XF), "k-split: plain / BST dgrad only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_B];
   const int tid = threadIdx.x, lane = tid & 63;
   const int ws = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave 0..7
-  const int wm = ws >> 1, wn = ws & 1;                        // rows wm*64.., cols wn*64..
+  const int wm = ws >> 1, wn = ws & 1;                        // rows wm*64.., cols wn*64.. (KS: k half wn)
+  constexpr int SLB = KS ? 8192 : SLOT_B;                     // ring slot bytes
+  constexpr int BPW = KS ? 1 : 2;                             // weight pieces per wave per K-tile
+  constexpr int NCT = KS ? 64 : 128;                          // columns per tile
   const int fr = lane & 15, fq = lane >> 4;
   const int G = gridDim.x;
   const int ntb = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / G + 1 : 0;
@@ -141,12 +153,18 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     float *xt = reinterpret_cast<float *>(smem + XF0);
     for (int c = tid; c < 2 * a.KC; c += 512) xt[c] = a.xf[c];
   }
+  // BST row groups (a plain dx whose BatchNorm keeps statistics per slice of grows rows,
+  // whole images): mean / invstd [groups][Ncol], groups * Ncol <= 512
+  const int bgi = (BST && a.bwd.grows) ? (int)(a.bwd.grows / ((int64_t)a.outH * a.outW)) : 0;   // images per group
   if constexpr (BST) {
     float *bt = reinterpret_cast<float *>(smem + XF0);
-    for (int c = tid; c < a.Ncol; c += 512) {
-      const int cg = c % a.ogc;
+    const int nst = a.bwd.grows ? (int)(a.M / a.bwd.grows) * a.Ncol : a.Ncol;
+    for (int c = tid; c < nst; c += 512) {
       bt[c] = a.bwd.mean[c];
       bt[512 + c] = a.bwd.invstd[c];
+    }
+    for (int c = tid; c < a.Ncol; c += 512) {
+      const int cg = c % a.ogc;
       bt[1024 + c] = a.bwd.gamma ? a.bwd.gamma[cg] : 1.f;
       bt[1536 + c] = a.bwd.beta ? a.bwd.beta[cg] : 0.f;
     }
@@ -166,7 +184,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     d.oh0 = by * WT;
     d.ow0 = (r - by * nbx) * WT;
     d.part = s;
-    d.n0 = jn * 128;
+    d.n0 = jn * NCT;
     d.kb = cb * 128;                     // 64 channels x 2 B
     d.last = cb == ncb - 1;
     const int c = cb * 64, gi = c / a.sgc;
@@ -178,19 +196,19 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 
   // this lane's B rows (pieces 2ws, 2ws+1: rows 8p + lane/8) — byte offsets in a packed
   // weight row for column tile 0, chunk-swizzled
-  uint32_t brow[2];
+  uint32_t brow[BPW];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (2 * ws + j) * 8 + (lane >> 3);
+  for (int j = 0; j < BPW; ++j) {
+    const int r = (BPW * ws + j) * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((r >> 1) & 7);
     brow[j] = (uint32_t)((r * K + lc * 8) * 2);
   }
   // B(K-tile of unit d, weight tap rt) -> ring slot
   auto issue_b = [&](const WinUnit &d, int rt, int slot) {
-    const uint32_t dst = lds0 + slot * SLOT_B + ws * 2048;
+    const uint32_t dst = lds0 + slot * SLB + ws * (BPW * 1024);
     const uint32_t base = (uint32_t)((d.n0 * K + rt * a.KC) * 2 + d.kb);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16_asm(rw, dst + j * 1024, d.ok ? base + brow[j] : OOB);
+    for (int j = 0; j < BPW; ++j) glds16_asm(rw, dst + j * 1024, d.ok ? base + brow[j] : OOB);
   };
   // window piece q (8 pixels) of unit d into window buffer wb.  The lane's pixel is q * 8 +
   // lane / 8 and its source chunk (lane & 7) ^ (pixel & 7) — loop-invariant (q * 8 keeps
@@ -259,9 +277,9 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 8; ++r)
-        atab[b][r] = lds0 + WIN0 + b * WIN_B + (uint32_t)(p0 * 128 + 16 * (fq ^ ((fr + r) & 7)));
+        atab[b][r] = lds0 + WIN0 + b * WIN_B + (uint32_t)(p0 * 128 + 16 * ((fq | (KS ? 4 * wn : 0)) ^ ((fr + r) & 7)));
   }
-  const uint32_t bfo = lds0 + (uint32_t)((wn * 64 + fr) * 128 + 16 * (fq ^ ((fr >> 1) & 7)));
+  const uint32_t bfo = lds0 + (uint32_t)(((KS ? 0 : wn * 64) + fr) * 128 + 16 * ((fq | (KS ? 4 * wn : 0)) ^ ((fr >> 1) & 7)));
   typedef __attribute__((address_space(3))) const cbf16x8 lds_frag;
   auto ldsr = [&](uint32_t addr) -> cbf16x8 { return *reinterpret_cast<lds_frag *>((uintptr_t)addr); };
   cbf16x8 fa[2][4], fb[2][4];
@@ -274,12 +292,12 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     for (int i = 0; i < 4; ++i) {
       const int c = i * WW + woff;
       xa[0][i] = ldsr(atab[WB][c & 7] + c * 128);
-      xa[1][i] = ldsr(atab[WB][(c + 4) & 7] + c * 128);
+      if constexpr (!KS) xa[1][i] = ldsr(atab[WB][(c + 4) & 7] + c * 128);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      xb[0][j] = ldsr(bfo + SL * SLOT_B + j * 2048);
-      xb[1][j] = ldsr((bfo ^ 64) + SL * SLOT_B + j * 2048);
+      xb[0][j] = ldsr(bfo + SL * SLB + j * 2048);
+      if constexpr (!KS) xb[1][j] = ldsr((bfo ^ 64) + SL * SLB + j * 2048);
     }
   };
 
@@ -291,17 +309,21 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
 
   // BST: this lane's BN-input values at its 16 epilogue positions of unit d (zeros, no traffic,
   // unless d ends its tile)
-  uint2 xq[4][4];
+  // KS: a wave stores rows ER0 .. ER0 + NER - 1 of its row group, all 64 columns
+  constexpr int NER = KS ? 2 : 4;
+  const int ER0 = KS ? 2 * wn : 0;
+  const int ECOL = KS ? 0 : wn * 64;
+  uint2 xq[4][NER];
   const __amdgpu_buffer_rsrc_t rbx = mk_rsrc(BST ? (const void *)a.bwd.x : (const void *)a.out, out_bytes);
   auto issue_x = [&](const WinUnit &d) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = d.n0 + wn * 64 + j * 16 + fq * 4;
+      const int col = d.n0 + ECOL + j * 16 + fq * 4;
       const int gi = col / a.ogc;
       const int64_t cbase = (int64_t)gi * a.ogs + (col - gi * a.ogc);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + i) * W + d.ow0 + fr;
+      for (int i = 0; i < NER; ++i) {
+        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + ER0 + i) * W + d.ow0 + fr;
         const uint32_t off = d.last ? (uint32_t)((pix * a.ogc + cbase) * 2) : OOB;
         asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
       }
@@ -313,7 +335,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     float cs[4][4], cq[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int cl = wn * 64 + j * 16 + fq * 4;          // column in the tile
+      const int cl = ECOL + j * 16 + fq * 4;             // column in the tile
       const int col = d.n0 + cl;
       float4 bv, kv;
       {
@@ -331,12 +353,14 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       float bmu[4], biv[4], bga[4], bbe[4];
       if constexpr (BST) {
         const float *bt = reinterpret_cast<const float *>(smem + XF0) + col;
+        const int so = bgi ? d.img / bgi * a.Ncol : 0;     // the row group's statistics
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { bmu[r] = bt[r]; biv[r] = bt[512 + r]; bga[r] = bt[1024 + r]; bbe[r] = bt[1536 + r]; }
+        for (int r = 0; r < 4; ++r) { bmu[r] = bt[so + r]; biv[r] = bt[512 + so + r]; bga[r] = bt[1024 + r]; bbe[r] = bt[1536 + r]; }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + i) * W + d.ow0 + fr;
+      for (int i = 0; i < NER; ++i) {
+        // (KS: the exchange left the wave's rows ER0, ER0 + 1 in acc[0], acc[1])
+        const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + ER0 + i) * W + d.ow0 + fr;
         const bf16_t h0 = f2bf(acc[i][j][0] + bv.x), h1 = f2bf(acc[i][j][1] + bv.y);
         const bf16_t h2 = f2bf(acc[i][j][2] + bv.z), h3 = f2bf(acc[i][j][3] + bv.w);
         uint2 pk;
@@ -375,9 +399,11 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         for (int r = 0; r < 4; ++r) {
           const float S = row_sum16(cs[j][r]), Q = row_sum16(cq[j][r]);
           if (fr == 0) {
-            const int cl = wn * 64 + j * 16 + fq * 4 + r;
-            red[(wm * 128 + cl) * 2] = S;
-            red[(wm * 128 + cl) * 2 + 1] = Q;
+            // KS: [8 waves][64 columns]; else [4 row groups][128 columns]
+            const int cl = ECOL + j * 16 + fq * 4 + r;
+            const int ro = KS ? ws * 64 : wm * 128;
+            red[(ro + cl) * 2] = S;
+            red[(ro + cl) * 2 + 1] = Q;
           }
         }
     }
@@ -393,20 +419,59 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   const int nblk = (int)(a.M / (WT * WT));
   auto stats_flush = [&]() __attribute__((always_inline)) {
     const float *red = reinterpret_cast<const float *>(smem + RED0);
-    const int v = tid & 255, cl = v >> 1, w = v & 1;
-    const float t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
-                    (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
+    const int v = tid & 255, cl = (v >> 1) & (NCT - 1), w = v & 1;
+    float t;
+    if constexpr (KS) {
+      // the 8 waves' partials of the 64 columns (threads v >= 128 store out of range: every
+      // wave issues the one store the counted waits expect)
+      t = ((red[(0 * 64 + cl) * 2 + w] + red[(1 * 64 + cl) * 2 + w]) +
+           (red[(2 * 64 + cl) * 2 + w] + red[(3 * 64 + cl) * 2 + w])) +
+          ((red[(4 * 64 + cl) * 2 + w] + red[(5 * 64 + cl) * 2 + w]) +
+           (red[(6 * 64 + cl) * 2 + w] + red[(7 * 64 + cl) * 2 + w]));
+    } else {
+      t = (red[(0 * 128 + cl) * 2 + w] + red[(1 * 128 + cl) * 2 + w]) +
+          (red[(2 * 128 + cl) * 2 + w] + red[(3 * 128 + cl) * 2 + w]);
+    }
     if constexpr (BST) {
       // [channel group][block][2 group channels]
       const int gi = pend_n0 / a.ogc;
-      bstore32(rq, t, (uint32_t)((((int64_t)gi * nblk + pend_part) * 2 * a.ogc + w * a.ogc + pend_n0 - gi * a.ogc + cl) * 4));
+      const uint32_t off = (uint32_t)((((int64_t)gi * nblk + pend_part) * 2 * a.ogc + w * a.ogc + pend_n0 - gi * a.ogc + cl) * 4);
+      bstore32(rq, t, (KS && v >= 128) ? OOB : off);
     } else {
       bstore32(rp, t, (uint32_t)((pend_part * 2 * ncol + w * ncol + pend_n0 + cl) * 4));
     }
   };
-  constexpr int ST = 16;                     // output stores of one epilogue per wave
+  // KS: the k-halves of the tile's accumulators meet.  Wave ws writes the two rows its partner
+  // (ws ^ 1) stores — wn 0 sends rows 2, 3, wn 1 rows 0, 1 — to its 8 KB block (blocks 0-2 in
+  // the ring's unused upper 24 KB, 3-7 in window buffer WB: consumed by this unit's last reads,
+  // refilled only after the next unit's first barrier), then adds the partner's block into the
+  // rows it keeps, left in acc[0], acc[1].
+  auto exchange = [&](int wb) __attribute__((always_inline)) {
+    auto blk = [&](int w) -> float4 * {
+      return reinterpret_cast<float4 *>(w < 3 ? smem + 3 * 8192 + w * 8192 : smem + WIN0 + wb * WIN_B + (w - 3) * 8192);
+    };
+    float4 *mine = blk(ws), *theirs = blk(ws ^ 1);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const cf32x4 v = wn ? acc[ii][j] : acc[2 + ii][j];
+        mine[(ii * 4 + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 p = theirs[(ii * 4 + j) * 64 + lane];
+        const cf32x4 k = wn ? acc[2 + ii][j] : acc[ii][j];
+        acc[ii][j] = cf32x4{k[0] + p.x, k[1] + p.y, k[2] + p.z, k[3] + p.w};
+        acc[2 + ii][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  };
+  constexpr int ST = 4 * NER;                // output stores of one epilogue per wave
   constexpr int SS = (STATS || BST) ? 1 : 0; // the statistics store (at the next unit's tap 0)
-  constexpr int XL = BST ? 16 : 0;           // BST: BN-input loads issued at tap 5
+  constexpr int XL = BST ? 4 * NER : 0;      // BST: BN-input loads issued at tap 5
 
   // window pieces of the next unit: 2 per wave at taps 0-2 (48 slots for 41 pieces; the extra
   // slots repeat piece 40), so a unit's window has landed long before its first read
@@ -421,7 +486,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     for (int jj = 0; jj < WPT; ++jj) issue_w(cu, wpiece(t, jj), 0);
 #pragma unroll
   for (int t = 0; t < 3; ++t) issue_b(cu, t, t);
-  win_sync<4>();                            // window 0 and K-tile 0 landed (B 1, 2 in flight)
+  win_sync<2 * BPW>();                      // window 0 and K-tile 0 landed (B 1, 2 in flight)
   if constexpr (XF) {
     xform(cu, 0, 0);
     xform(cu, 0, 1);
@@ -447,7 +512,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       // T = 0, 1
       // (+ the output stores of the previous unit's tap 8 for T = 0, 1 and its statistics
       // store, issued at this unit's tap 0, for T = 1, 2)
-      constexpr int NB = 2 + (((T + 8) % 9) < 3 ? WPT : 0) + ((T == 6 || T == 7) ? XL : 0);
+      constexpr int NB = BPW + (((T + 8) % 9) < 3 ? WPT : 0) + ((T == 6 || T == 7) ? XL : 0);
       constexpr int X = (T <= 1 ? ST : 0) + ((T == 1 || T == 2) ? SS : 0);
       if constexpr (X > 0) {
         if (prev_st) win_sync<NB + X>();
@@ -481,7 +546,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         read_frags(std::integral_constant<int, WB ^ 1>{}, std::integral_constant<int, 0>{},
                    std::integral_constant<int, 0>{}, na, nb);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < (KS ? 1 : 2); ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -495,6 +560,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       if constexpr (T == 8) {
         prev_st = cu.last;
         if (cu.last) {
+          if constexpr (KS) exchange(WB);
           epilogue(cu, WB);
           pend_part = cu.part;
           pend_n0 = cu.n0;
@@ -528,21 +594,31 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// the k-split form: a plain 64-column input gradient
+static bool win_ks(const FwdArgs &a, bool dgrad) {
+  return dgrad && a.Ncol == 64 && a.ogc == 64 && !a.ogs && !a.bias;
+}
+
 bool win_ok(const FwdArgs &a, bool dgrad) {
   if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend) return false;
-  if (a.bwd.part && (!dgrad || a.bwd.rscale || a.bwd.grows || !a.bwd.x || !a.bwd.mean || !a.bwd.invstd ||
-                     a.Ncol > 512)) return false;
+  if (a.bwd.part && (!dgrad || a.bwd.rscale || !a.bwd.x || !a.bwd.mean || !a.bwd.invstd || a.Ncol > 512)) return false;
+  // BatchNorm row groups of whole images, their statistics table in LDS
+  if (a.bwd.part && a.bwd.grows &&
+      (a.ogs || a.bwd.grows % ((int64_t)a.outH * a.outW) || a.M % a.bwd.grows || (a.M / a.bwd.grows) * a.Ncol > 512))
+    return false;
+  const bool ks = win_ks(a, dgrad);
   if (a.xf && (dgrad || a.KC > 512)) return false;
   if (dgrad && a.bn_part) return false;
   if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
   if (a.KC % 64 || a.sgc % 64 || (a.KCr && a.KCr != a.KC)) return false;
-  if (a.Ncol % 128 || a.ogc % 128 || ((a.bias || a.bn_part) && a.Ncol > VEC_N)) return false;
+  if (!ks && (a.Ncol % 128 || a.ogc % 128)) return false;
+  if ((a.bias || a.bn_part) && a.Ncol > VEC_N) return false;
   if (a.M != (int64_t)a.g.N * a.outH * a.outW) return false;
   const int64_t K = 9LL * a.KC;
   if (a.Ncol * K * 2 >= (int64_t)OOB) return false;
   const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
   if (ob >= (int64_t)OOB) return false;
-  const int64_t nt = a.M / (WT * WT) * (a.Ncol / 128);
+  const int64_t nt = a.M / (WT * WT) * (ks ? 1 : a.Ncol / 128);
   return nt < (1 << 30);
 }
 
@@ -832,14 +908,19 @@ bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream
 
 bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) {
   if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
-  const int ntn = a.Ncol / 128;
+  const bool ks = win_ks(a, dgrad);
+  const int ntn = ks ? 1 : a.Ncol / 128;
   const int ntiles = (int)(a.M / (WT * WT) * ntn);
   int G = cu_count();
   if (g_grid_cap > 0 && g_grid_cap < G) G = g_grid_cap;
   if (G > ntiles) G = ntiles;
   const int ncb = a.KC / 64;
   const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
-  if (dgrad && a.bwd.part)
+  if (ks && a.bwd.part)
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (ks)
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+  else if (dgrad && a.bwd.part)
     hipLaunchKernelGGL((conv_win_kernel<true, false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (dgrad)
     hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);

@@ -464,23 +464,33 @@ __global__ __launch_bounds__(1024) void hfsep_wgrad_reduce_kernel(const float *_
 // The grouped seperate BatchNorm's backward coefficients per (level, channel) from the partial
 // sums left by the fusion conv's input-gradient epilogue (part [L][nrc][128]: sum g' and sum
 // g' xhat per channel): the table the BNB weight-gradient kernel reads, and the per-level sums
-// for the affine gradients.  One workgroup per level; rows summed in a fixed order.
-__global__ __launch_bounds__(256) void hfsep_bn_coef_kernel(const float *__restrict__ part, int nrc, float n,
-                                                            const float *__restrict__ mean,
-                                                            const float *__restrict__ invstd,
-                                                            const float *__restrict__ gamma,
-                                                            const float *__restrict__ beta, float *__restrict__ tab,
-                                                            float *__restrict__ lsum) {
-  __shared__ float red[2][128];
+// for the affine gradients.  One workgroup per level: 8 row slices x 4 loads in flight per
+// thread (a latency-bound launch on the MWT's critical path otherwise), summed in a fixed order.
+__global__ __launch_bounds__(1024) void hfsep_bn_coef_kernel(const float *__restrict__ part, int nrc, float n,
+                                                             const float *__restrict__ mean,
+                                                             const float *__restrict__ invstd,
+                                                             const float *__restrict__ gamma,
+                                                             const float *__restrict__ beta, float *__restrict__ tab,
+                                                             float *__restrict__ lsum) {
+  __shared__ float red[8][128];
   const int l = blockIdx.x, tid = threadIdx.x, col = tid & 127, q = tid >> 7;
-  float v = 0.f;
-  for (int r = q; r < nrc; r += 2) v += part[((int64_t)l * nrc + r) * 128 + col];
-  red[q][col] = v;
+  const float *p = part + (int64_t)l * nrc * 128 + col;
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int r = q;
+  for (; r + 24 < nrc; r += 32) {
+    v0 += p[(int64_t)r * 128];
+    v1 += p[(int64_t)(r + 8) * 128];
+    v2 += p[(int64_t)(r + 16) * 128];
+    v3 += p[(int64_t)(r + 24) * 128];
+  }
+  for (; r < nrc; r += 8) v0 += p[(int64_t)r * 128];
+  red[q][col] = (v0 + v1) + (v2 + v3);
   __syncthreads();
   if (tid < 128) {
-    const float t = red[0][tid] + red[1][tid];
+    const float t = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) +
+                    ((red[4][tid] + red[5][tid]) + (red[6][tid] + red[7][tid]));
     lsum[l * 128 + tid] = t;
-    red[0][tid] = t;
+    red[0][tid] = t;                  // (this thread's column only)
   }
   __syncthreads();
   if (tid < 64) {
@@ -620,7 +630,7 @@ extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const voi
   hipStream_t s = as_stream(stream);
   float *tab = workspace + (int64_t)G * HS_COUT * HS_K;
   float *lsum = tab + L * 64 * 8;
-  hipLaunchKernelGGL(hfsep_bn_coef_kernel, dim3((unsigned)L), dim3(256), 0, s, part, nrc, (float)(N * H * W), mean,
+  hipLaunchKernelGGL(hfsep_bn_coef_kernel, dim3((unsigned)L), dim3(1024), 0, s, part, nrc, (float)(N * H * W), mean,
                      invstd, gamma, beta, tab, lsum);
   if (int rc = launch_status("hfsep_bn_bwd_weight coef")) return rc;
 #define EWVIT_HS_WGB(TH_, D_, X_)                                                                                 \

@@ -69,7 +69,7 @@ SIGNATURES = {
     'ewvit_conv2d_bwd_weight_xf': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
                                    _i64, _i64, _i64, _vp, _vp],
     'ewvit_conv2d_bwd_data_bn_win': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
-                                     _i32, _vp, _vp],
+                                     _i32, _i64, _vp, _vp],
     'ewvit_bn_coef': [_i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
     'ewvit_bn_fwd_partials': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp, _vp,
                               _vp, _vp, _i32, _i32, _vp],
@@ -129,7 +129,7 @@ SIGNATURES = {
 
 # size queries: name -> (restype, argtypes)
 QUERIES = {
-    'ewvit_conv2d_bwd_bn_win_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64]),
+    'ewvit_conv2d_bwd_bn_win_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _i64]),
     'ewvit_layernorm_bwd_workspace': (_i64, [_i64, _i64]),
     'ewvit_vit_layer_workspace': (_i64, [_i32]),
     'ewvit_gemm_tallk_workspace': (_i64, [_i64, _i64, _i64]),

@@ -188,6 +188,22 @@ def _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     return bl.groups, (M // bl.groups if bl.groups > 1 else 0), tiles // bl.groups, Cx
 
 
+def _bn_link_win(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
+    """(row-group rows, partial rows) when the windowed input gradient takes the backward sums of
+    the BatchNorm that produced this conv's plain input (hf_conv['fusion']'s 64-channel input:
+    the seperate BNs, per-level statistics over slices of whole images; one partial row per
+    16 x 16 block), else None."""
+    if (bl is None or not _BN_BWD_EPI or levels != 1 or skip is not None or bl.rscale is not None
+            or xdt != torch.bfloat16 or bl.x.shape != xc.shape or k != 3 or stride != 1):
+        return None
+    M = N * H * W
+    if bl.groups > 1 and M % bl.groups:
+        return None
+    grows = M // bl.groups if bl.groups > 1 else 0
+    rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, k, stride, Cx, 0, grows))
+    return (grows, rows) if rows > 0 else None
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, levels, bn_stats=None):
@@ -265,8 +281,17 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
-            lk = _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
-            if lk is not None:
+            lw = _bn_link_win(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            lk = None if lw is not None else _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            if lw is not None:
+                # the windowed input gradient with the producing BatchNorm's per-block sums
+                grows, rows = lw
+                part = torch.empty(rows, 2 * Cx, dtype=torch.float32, device=xc.device)
+                L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dyc), L.ptr(wpt), L.ptr(dx), N, H, W, Cx, Cout, Cx, 0,
+                       L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta), bl.act, grows,
+                       L.ptr(part), L.stream(dx), work=work)
+                bl.fulfil(*bnmod.fold_bwd_partials(part, rows // bl.groups, bl.groups, Cx), dx)
+            elif lk is not None:
                 # dx (+ the skip gradient) and the producing BatchNorm's backward sums in one epilogue
                 groups, grows, rows, Cg = lk
                 sk = skip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if skip is not None else None
@@ -461,12 +486,12 @@ class BnReluConvFn(torch.autograd.Function):
         # backward's per-block sums of g = da * relu'(.) and g * xhat
         da = torch.empty_like(zc, memory_format=torch.channels_last)
         work = {'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + da.numel() + wpt.numel()) * 2}
-        rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs)) if _BN_BWD_EPI else 0
+        rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs, 0)) if _BN_BWD_EPI else 0
         bpart = None
         if rows > 0:
             bpart = torch.empty(levels * rows, 2 * C, dtype=torch.float32, device=dev)
             L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, C, gs,
-                   L.ptr(zc), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, L.ptr(bpart), L.stream(da),
+                   L.ptr(zc), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, 0, L.ptr(bpart), L.stream(da),
                    work=work)
         else:
             L.call('ewvit_conv2d_bwd_data', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, 3, 1, C, gs,

@@ -429,14 +429,20 @@ int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, 
  * whose output the conv read (as ewvit_conv2d_bwd_data_bn, but one partial row per 16 x 16 dx
  * block: part [groups][N*H*W/256][2 group_c], BatchNorm groups = dx's channel groups, mean /
  * invstd [groups][group_c], gamma / beta [group_c] or NULL) — the MWT hf fusion BN's backward
- * sums taken by multiscale_fusion's input gradient (reference network/mwt.py:60-72,114).
- * ewvit_conv2d_bwd_bn_win_rows: rows per group, 0 when the windowed kernel does not take it. */
+ * sums taken by multiscale_fusion's input gradient (reference network/mwt.py:60-72,114).  A
+ * plain dx (dx_group_c = Cin, dx_group_stride 0) may instead carry BatchNorm row groups:
+ * bn_group_rows > 0 rows per slice (whole images, slices * Cin <= 512), mean / invstd
+ * [slices][Cin], part [slices][bn_group_rows/256][2 Cin] — the seperate BNs' per-level
+ * statistics taken by hf_conv['fusion']'s input gradient (a 64-column dx: the k-split form,
+ * reference network/mwt.py:48-65,84-88).
+ * ewvit_conv2d_bwd_bn_win_rows: N*H*W/256 (the rows per channel group; with row groups, the
+ * total over the slices), 0 when the windowed kernel does not take it. */
 int64_t ewvit_conv2d_bwd_bn_win_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
-                                     int64_t dx_group_c, int64_t dx_group_stride);
+                                     int64_t dx_group_c, int64_t dx_group_stride, int64_t bn_group_rows);
 int ewvit_conv2d_bwd_data_bn_win(const void *dy, const void *wp_t, void *dx, int64_t N, int64_t H, int64_t W,
                                  int64_t Cin, int64_t Cout, int64_t dx_group_c, int64_t dx_group_stride,
                                  const void *bx, const float *mean, const float *invstd, const float *gamma,
-                                 const float *beta, int act, float *part, void *stream);
+                                 const float *beta, int act, int64_t bn_group_rows, float *part, void *stream);
 int ewvit_conv2d_xf_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,
                        int64_t x_group_c, int64_t x_group_stride);
 int ewvit_conv2d_fwd_bn_xf(const void *x, const void *wp, const float *bias, void *y, int64_t N, int64_t H,

@@ -210,7 +210,7 @@ def test_dgrad_bn_sums_match_explicit():
     N, C, H, W, Cout, levels = 2, 128, 32, 48, 128, 3
     NL, Cx = N * levels, C * levels
     gc, gs = C, N * H * W * C
-    rows = int(lib.ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, gc, gs))
+    rows = int(lib.ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, gc, gs, 0))
     assert rows == N * H * W // 256
     w = (torch.randn(Cout, Cx, 3, 3, generator=g) / (9 * Cx) ** 0.5).to(DEV)
     _, wpt = _pack(w, Cx, True, True)
@@ -225,7 +225,7 @@ def test_dgrad_bn_sums_match_explicit():
     part = torch.full((levels * rows, 2 * C), float('nan'), device=DEV)
     L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), N, H, W, Cx, Cout, 3, 1, gc, gs, L.stream(dy))
     L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), N, H, W, Cx, Cout, gc, gs, L.ptr(z),
-           L.ptr(mean), L.ptr(inv), L.ptr(gamma), L.ptr(beta), 1, L.ptr(part), L.stream(dy))
+           L.ptr(mean), L.ptr(inv), L.ptr(gamma), L.ptr(beta), 1, 0, L.ptr(part), L.stream(dy))
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1)
     zl = z.double().view(levels, N, C, H, W)
@@ -241,3 +241,57 @@ def test_dgrad_bn_sums_match_explicit():
     assert float((got[:, :, 0] - s1).abs().max()) <= 1e-5 * sc
     sc2 = float(s2.abs().max())
     assert float((got[:, :, 1] - s2).abs().max()) <= 1e-5 * sc2
+
+
+@pytest.mark.parametrize('cap', [0, 5])
+def test_dgrad_bn_sums_row_groups_ksplit(cap):
+    """The k-split 64-column input gradient (hf_conv['fusion'] 128 -> 64) with BatchNorm ROW
+    groups (the seperate BNs' per-level statistics: slices of whole images): dx bit-identical to
+    the plain windowed dgrad, part [levels][blocks per level][2 C] equal to the float64 sums
+    over the returned dx with each level's own mean / invstd (1e-5 of scale); cap 5: the
+    persistent walk."""
+    import ewvit  # noqa: F401
+    from ewvit import _lib as L
+    from ewvit.conv import _pack
+    lib = L.load()
+    g = torch.Generator().manual_seed(23 + cap)
+    levels, N, C, H, W, Cout = 3, 2, 64, 32, 48, 128
+    NL = levels * N
+    grows = N * H * W
+    rows = int(lib.ewvit_conv2d_bwd_bn_win_rows(NL, H, W, C, Cout, 3, 1, C, 0, grows))
+    assert rows == NL * H * W // 256
+    assert int(lib.ewvit_conv2d_bwd_bn_win_rows(NL, H, W, C, Cout, 3, 1, C, 0, grows // 2 + 256)) == 0   # not whole images
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(DEV)
+    _, wpt = _pack(w, C, True, True)
+    dy = torch.randn(NL, Cout, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    z = torch.randn(NL, C, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mean = (torch.randn(levels, C, generator=g) * 0.1).to(DEV)
+    inv = (torch.rand(levels, C, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    dx0 = torch.empty_like(z)
+    dx1 = torch.empty_like(z)
+    part = torch.full((rows, 2 * C), float('nan'), device=DEV)
+    prev = lib.ewvit_set_grid_cap(cap)
+    try:
+        L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), NL, H, W, C, Cout, 3, 1, 0, 0, L.stream(dy))
+        L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dy), L.ptr(wpt), L.ptr(dx1), NL, H, W, C, Cout, C, 0, L.ptr(z),
+               L.ptr(mean), L.ptr(inv), L.ptr(gamma), L.ptr(beta), 1, grows, L.ptr(part), L.stream(dy))
+        torch.cuda.synchronize()
+    finally:
+        lib.ewvit_set_grid_cap(prev)
+    assert torch.equal(dx0, dx1)
+    dref = torch.nn.grad.conv2d_input(z.shape, w.to(torch.bfloat16).float(), dy.float(), padding=1)
+    assert float((dx1.float() - dref).abs().max() / dref.abs().max()) < 2 ** -7
+    zl = z.double().view(levels, N, C, H, W)
+    xh = (zl - mean.double().view(levels, 1, C, 1, 1)) * inv.double().view(levels, 1, C, 1, 1)
+    pre = xh * gamma.double().view(1, 1, C, 1, 1) + beta.double().view(1, 1, C, 1, 1)
+    gg = dx1.double().view(levels, N, C, H, W) * (pre > 0)
+    nb = rows // levels
+
+    def blocks(t):
+        return t.view(levels, N, C, H // 16, 16, W // 16, 16).sum((4, 6)).permute(0, 1, 3, 4, 2).reshape(levels, nb, C)
+    s1, s2 = blocks(gg), blocks(gg * xh)
+    got = part.double().view(levels, nb, 2, C)
+    assert float((got[:, :, 0] - s1).abs().max()) <= 1e-5 * float(s1.abs().max())
+    assert float((got[:, :, 1] - s2).abs().max()) <= 1e-5 * float(s2.abs().max())

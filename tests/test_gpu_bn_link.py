@@ -407,9 +407,13 @@ def test_conv_dgrad_bn_row_groups(cap):
     dx0, dx1 = torch.empty_like(bx), torch.empty_like(bx)
     M = Lv * N * H * W
     prev = lib.ewvit_set_grid_cap(cap)
+    # (the plain dgrad of this 64-column shape would take the windowed k-split kernel, whose k
+    # order differs: the generic LDS-DMA kernel is the bit-identity reference here)
+    lib.ewvit_conv2d_set_win(0)
     try:
         L.call('ewvit_conv2d_bwd_data', L.ptr(dy), L.ptr(wpt), L.ptr(dx0), Lv * N, H, W, C, Cout, 3, 1, 0, 0,
                L.stream(dy))
+        lib.ewvit_conv2d_set_win(1)
         tiles = int(lib.ewvit_conv2d_bwd_bn_rows(Lv * N, H, W, C, Cout, 3, 1))
         part = torch.full((tiles, 2 * C), float('nan'), device=DEV)
         nrc = ctypes.c_int(0)
@@ -418,6 +422,7 @@ def test_conv_dgrad_bn_row_groups(cap):
                ctypes.byref(nrc), L.stream(dy))
     finally:
         lib.ewvit_set_grid_cap(prev)
+        lib.ewvit_conv2d_set_win(1)
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1)
     per = tiles // Lv                                  # 128-row tiles, or 64 on small grids

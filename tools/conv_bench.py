@@ -77,6 +77,8 @@ def main():
                     'target_wg:min_ktiles:ring pairs, e.g. 0:4:3,256:4:3,128:4:3 (wgrad only)')
     ap.add_argument('--small', default=None, help='ewvit_conv2d_set_small_tiles settings to time, e.g. 0,1 (replaces --variants)')
     ap.add_argument('--eager', action='store_true', help='no HIP graph (for rocprofv3 --pmc passes)')
+    ap.add_argument('--win', type=int, default=1, help='ewvit_conv2d_set_win: 1 windowed 3x3 kernels where they apply, 0 off')
+    ap.add_argument('--cap', type=int, default=0, help='ewvit_set_grid_cap (the MWT stream runs under 128)')
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
@@ -96,6 +98,8 @@ def main():
     from ewvit import _lib as L
     from ewvit.conv import _pack
     lib = L.load()
+    lib.ewvit_conv2d_set_win(a.win)
+    lib.ewvit_set_grid_cap(a.cap)
     shapes = SHAPES
     if a.shape:
         shapes = {f'shape{i}': tuple(int(v) for v in sh.split(',')) for i, sh in enumerate(a.shape)}
