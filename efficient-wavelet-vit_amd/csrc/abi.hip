@@ -28,3 +28,25 @@ extern "C" int ewvit_set_grid_cap(int max_workgroups) {
   ewvit::g_grid_cap = max_workgroups > 0 ? (max_workgroups + 7) / 8 * 8 : 0;   // whole XCD rounds
   return prev;
 }
+
+using namespace ewvit;
+
+// Timeline probe (diagnostics, tools/step_timeline.py): when the stream reaches it, one lane
+// writes the device wall clock (ewvit_wall_clock_khz ticks per millisecond) to stamps[idx].
+__global__ void probe_kernel(long long *stamps, int idx) {
+  const int t = (int)threadIdx.x;
+  if (t == 0) stamps[idx + t] = wall_clock64();
+}
+
+extern "C" int ewvit_probe(long long *stamps, int idx, void *stream) {
+  EWVIT_CHECK_ARG(stamps && idx >= 0, "probe: bad args");
+  hipLaunchKernelGGL(probe_kernel, dim3(1), dim3(64), 0, as_stream(stream), stamps, idx);
+  return launch_status("probe");
+}
+
+extern "C" int ewvit_wall_clock_khz(void) {
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+    return 0;
+  return v;
+}

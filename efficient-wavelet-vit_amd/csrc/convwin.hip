@@ -44,6 +44,17 @@
 namespace ewvit {
 
 int g_win = 1;
+// EWVIT_LDS_PAD / ewvit_conv2d_set_lds_pad (A/B): the windowed kernels request the CU's whole
+// 160 KB of LDS (dynamic padding after their static arrays), so no other stream's workgroup
+// can co-reside on a CU one of them holds
+int g_lds_pad = 0;
+template <typename K>
+static size_t lds_pad(K kern, size_t stat) {
+  if (!g_lds_pad || stat >= 160 * 1024) return 0;
+  const size_t d = 160 * 1024 - stat;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)d);
+  return d;
+}
 
 namespace {
 constexpr int WT = 16;                    // output block side (pixels)
@@ -896,13 +907,13 @@ bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const unsigned nwg = (unsigned)(splits * ncb * nct);
   if (a.xf && a.dbias_part)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<true, true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<true, true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<true, true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
   else if (a.xf)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<false, true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<false, true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<false, true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
   else if (a.dbias_part)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<true>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
   else
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<false>), dim3(nwg), dim3(256), 0, s, a, x_bytes, splits, ncb, nct, ntile);
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<false>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<false>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
   return true;
 }
 
@@ -917,25 +928,31 @@ bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) 
   const int ncb = a.KC / 64;
   const int64_t ob = 2 * (a.ogs ? (a.Ncol / a.ogc - 1) * a.ogs + a.M * a.ogc : a.M * a.Ncol);
   if (ks && a.bwd.part)
-    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<true, false, false, true, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (ks)
-    hipLaunchKernelGGL((conv_win_kernel<true, false, false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, false, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<true, false, false, false, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (dgrad && a.bwd.part)
-    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<true, false, false, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<true, false, false, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (dgrad)
-    hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<true, false>), dim3(G), dim3(512), lds_pad(conv_win_kernel<true, false>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (a.xf && a.bn_part)
-    hipLaunchKernelGGL((conv_win_kernel<false, true, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<false, true, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<false, true, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (a.xf)
-    hipLaunchKernelGGL((conv_win_kernel<false, false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<false, false, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<false, false, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else if (a.bn_part)
-    hipLaunchKernelGGL((conv_win_kernel<false, true>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<false, true>), dim3(G), dim3(512), lds_pad(conv_win_kernel<false, true>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   else
-    hipLaunchKernelGGL((conv_win_kernel<false, false>), dim3(G), dim3(512), 0, s, a, src_bytes, ob, ntn, ntiles, ncb);
+    hipLaunchKernelGGL((conv_win_kernel<false, false>), dim3(G), dim3(512), lds_pad(conv_win_kernel<false, false>, SMEM_B), s, a, src_bytes, ob, ntn, ntiles, ncb);
   return true;
 }
 
 }  // namespace ewvit
+
+extern "C" int ewvit_conv2d_set_lds_pad(int on) {
+  const int prev = ewvit::g_lds_pad;
+  ewvit::g_lds_pad = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int ewvit_conv2d_set_win(int variant) {
   const int prev = ewvit::g_win;

@@ -54,8 +54,10 @@ SIGNATURES = {
     'ewvit_adam_step': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
     'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_set_win': [_i32],
+    'ewvit_conv2d_set_lds_pad': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
+    'ewvit_probe': [_vp, _i32, _vp],
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_set_wgrad_1x1': [_i32, _i32, _i32],
     'ewvit_conv2d_set_small_tiles': [_i32],
@@ -154,6 +156,7 @@ QUERIES = {
     'ewvit_head_workspace': (_i64, []),
     'ewvit_head_pack_bytes': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_wall_clock_khz': (_i32, []),
 }
 
 _lib = None
@@ -190,6 +193,8 @@ def load():
         fn.restype = res
     if os.environ.get('EWVIT_SMALL_TILES') == '0' and hasattr(lib, 'ewvit_conv2d_set_small_tiles'):
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
+    if os.environ.get('EWVIT_LDS_PAD') == '1' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
+        lib.ewvit_conv2d_set_lds_pad(1)              # A/B switch (convwin.hip lds_pad)
     _lib = lib
     return lib
 

@@ -16,6 +16,7 @@ from torch import nn
 from torch.nn import functional as F
 
 import ewvit
+from ewvit import probe
 
 from . import bf16_compute, load_config
 from .mwt import MWT
@@ -23,6 +24,10 @@ from .sfe import EfficientViT, LayerNorm, Linear, _fp8, _hooked
 
 
 _SIDE = {}
+
+
+# A/B of the capture order: the MWT forward recorded before the SFE forward
+_MWT_FIRST = os.environ.get('EWVIT_MWT_FIRST', '0') == '1'
 
 
 def _side_stream(device, main):
@@ -192,13 +197,27 @@ class DAMA(nn.Module):                                                     # dam
             return self.sfe(frame).float(), self.mwt(frame).float()
         main = torch.cuda.current_stream(frame.device)
         side = _side_stream(frame.device, main)
+        dev = frame.device
+        probe.stamp(0, dev)                # (timeline probes: no-ops unless EWVIT_PROBE=1)
         side.wait_stream(main)             # fork before the SFE work is issued on main
-        space = self.sfe(frame).float()
-        # the MWT ops are recorded after the SFE ops: autograd runs ready backward nodes
-        # latest-first, so the MWT backward is issued (on `side`) before the SFE backward
-        # fills `main`, and its wait on main covers only the cross-attention backward
-        with torch.cuda.stream(side), ewvit._lib.grid_cap(_mwt_grid_cap()):
-            freq = self.mwt(frame).float()
+
+        def mwt():
+            with torch.cuda.stream(side), ewvit._lib.grid_cap(_mwt_grid_cap()):
+                probe.stamp(2, dev)
+                f = probe.tap(self.mwt(frame).float(), 5)
+                probe.stamp(3, dev)
+            return f
+        if _MWT_FIRST:
+            freq = mwt()
+            space = probe.tap(self.sfe(frame).float(), 4)
+            probe.stamp(1, dev)
+        else:
+            space = probe.tap(self.sfe(frame).float(), 4)
+            probe.stamp(1, dev)
+            # the MWT ops are recorded after the SFE ops: autograd runs ready backward nodes
+            # latest-first, so the MWT backward is issued (on `side`) before the SFE backward
+            # fills `main`, and its wait on main covers only the cross-attention backward
+            freq = mwt()
         main.wait_stream(side)
         freq.record_stream(main)
         return space, freq

@@ -19,6 +19,7 @@ from torch import nn
 from torch.nn import functional as F
 
 import ewvit
+from ewvit import probe
 
 from . import bf16_compute
 from .efficientnet import efficientnet_v2_s
@@ -260,4 +261,6 @@ class EfficientViT(nn.Module):                                             # sfe
 
     @bf16_compute
     def forward(self, img, mask=None):
-        return self.head(self.efficient_net.features(img))
+        f = self.efficient_net.features(img)
+        probe.stamp(7, f.device)           # (timeline probes: no-ops unless EWVIT_PROBE=1)
+        return self.head(probe.tap(f, 6))

@@ -366,6 +366,10 @@ int ewvit_conv2d_pack_weights(int n, const float *const *w, const int64_t *s_co,
  * capped grids; nn.DataParallel's replica threads, reference train.py:249-251, each keep their
  * own).  Returns the previous cap.  ewvit_conv2d_set_grid_cap is the same call. */
 int ewvit_set_grid_cap(int max_workgroups);
+/* Timeline probe (diagnostics): when `stream` reaches it, stamps[idx] = the device wall clock,
+ * ewvit_wall_clock_khz() ticks per millisecond (0 when the device cannot be queried). */
+int ewvit_probe(long long *stamps, int idx, void *stream);
+int ewvit_wall_clock_khz(void);
 int ewvit_conv2d_set_grid_cap(int max_workgroups);
 
 /* Kernel-family test switch (not needed for correctness): 0 runs every shape on the
@@ -382,6 +386,9 @@ int ewvit_conv2d_set_glds(int variant);
  * come one row per 16 x 16 block (ewvit_conv2d_fwd_bn_rows answers 256).  Returns the
  * previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_win(int variant);
+/* A/B: 1 = the windowed kernels request the CU's whole 160 KB of LDS (no co-resident workgroup
+ * of another stream on a CU they hold), 0 = their own footprint (default).  Returns the previous. */
+int ewvit_conv2d_set_lds_pad(int on);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
  * 64 x 128, 32 pixels per K-tile) for n' = k*k*Cin >= 2048 over >= 64K output pixels, else
  * 128-column tiles; 2 = 256-column tiles whenever n' >= 256 and the last tile wastes <= 1/8 of

@@ -1,6 +1,10 @@
-# usage: VAR=name bash ab.sh v1 v2 ...  (two rounds, interleaved)
-O=gpurun_out; mkdir -p $O
-for r in 1 2; do for v in "$@"; do
-  env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 > $O/ab_$v.log 2>&1 || exit 1
-  echo "$VAR=$v $(tail -1 $O/ab_$v.log | python -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
-done; done
+# Same-box A/B of environment switches on the bench: ENVS="A=0 A=1" bash tools/ab_env.sh CONFIG REPS
+# (each word of ENVS is one variant; a variant may join several assignments with commas)
+set -o pipefail
+cfg=${1:-2}; reps=${2:-2}
+for rep in $(seq $reps); do
+  for e in ${ENVS:-NONE=0}; do
+    r=$(env ${e//,/ } timeout -k 10 200 python -u bench.py --config $cfg --no-cpu-baseline 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])") || exit 1
+    echo "cfg $cfg $e rep $rep: $r"
+  done
+done
