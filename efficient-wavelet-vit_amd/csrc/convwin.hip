@@ -44,10 +44,11 @@
 namespace ewvit {
 
 int g_win = 1;
-// EWVIT_LDS_PAD / ewvit_conv2d_set_lds_pad (A/B): the windowed kernels request the CU's whole
-// 160 KB of LDS (dynamic padding after their static arrays), so no other stream's workgroup
-// can co-reside on a CU one of them holds
-int g_lds_pad = 0;
+// The windowed kernels request the CU's whole 160 KB of LDS (dynamic padding after their static
+// arrays), so no workgroup of the other stream co-resides on a CU one of them holds: config 2
+// 3627 -> 3636-3646 frames/s (same box, profiles/r05/ab/lds_pad.log).  EWVIT_LDS_PAD=0 /
+// ewvit_conv2d_set_lds_pad(0): their own footprint.
+int g_lds_pad = 1;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
   if (!g_lds_pad || stat >= 160 * 1024) return 0;

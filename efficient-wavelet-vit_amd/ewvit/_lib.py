@@ -193,8 +193,8 @@ def load():
         fn.restype = res
     if os.environ.get('EWVIT_SMALL_TILES') == '0' and hasattr(lib, 'ewvit_conv2d_set_small_tiles'):
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
-    if os.environ.get('EWVIT_LDS_PAD') == '1' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
-        lib.ewvit_conv2d_set_lds_pad(1)              # A/B switch (convwin.hip lds_pad)
+    if os.environ.get('EWVIT_LDS_PAD') == '0' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
+        lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
     _lib = lib
     return lib
 

@@ -386,8 +386,8 @@ int ewvit_conv2d_set_glds(int variant);
  * come one row per 16 x 16 block (ewvit_conv2d_fwd_bn_rows answers 256).  Returns the
  * previous setting.  Replaces nothing in the reference. */
 int ewvit_conv2d_set_win(int variant);
-/* A/B: 1 = the windowed kernels request the CU's whole 160 KB of LDS (no co-resident workgroup
- * of another stream on a CU they hold), 0 = their own footprint (default).  Returns the previous. */
+/* 1 = the windowed kernels request the CU's whole 160 KB of LDS (no co-resident workgroup of
+ * another stream on a CU they hold; the default), 0 = their own footprint.  Returns the previous. */
 int ewvit_conv2d_set_lds_pad(int on);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
  * 64 x 128, 32 pixels per K-tile) for n' = k*k*Cin >= 2048 over >= 64K output pixels, else
