@@ -71,7 +71,10 @@ constexpr int VEC0 = NSLOT * SLOT_B;      // bias [512] + BN shift [512] floats
 constexpr int RED0 = VEC0 + 2 * VEC_N * 4; // BN statistics partials [4 row groups][128 cols][2]
 constexpr int WIN0 = RED0 + 4096;         // [ring][vec][stats][window 0][window 1][xf][sink]
 constexpr int XF0 = WIN0 + 2 * WIN_B;     // fwd: input-transform coefficients [groups][2][sgc] (KC <= 512);
-                                          // dgrad: BatchNorm backward table [4][Ncol] (Ncol <= 512)
+                                          // dgrad: BatchNorm backward table (BST_N, BST_G below)
+constexpr int BST_N = 768;                // BST: mean / invstd entries (Ncol, or groups x Ncol)
+constexpr int BST_G = 256;                // BST: gamma / beta entries (the group width ogc)
+static_assert((2 * BST_N + 2 * BST_G) * 4 <= 8192, "BST table exceeds the XF0 region");
 constexpr int SINK0 = XF0 + 8192;         // 1 KB target of the window slots past the last piece
 constexpr int SMEM_B = SINK0 + 1024;      // 147,456 B: one workgroup per CU
 }  // namespace
@@ -165,20 +168,20 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     float *xt = reinterpret_cast<float *>(smem + XF0);
     for (int c = tid; c < 2 * a.KC; c += 512) xt[c] = a.xf[c];
   }
-  // BST row groups (a plain dx whose BatchNorm keeps statistics per slice of grows rows,
-  // whole images): mean / invstd [groups][Ncol], groups * Ncol <= 512
+  // BST table (XF0): mean / invstd per column [BST_N] each (row groups — a plain dx whose
+  // BatchNorm keeps statistics per slice of grows rows, whole images — [groups][Ncol]), then
+  // gamma / beta per group channel [256] each (shared by the channel groups)
   const int bgi = (BST && a.bwd.grows) ? (int)(a.bwd.grows / ((int64_t)a.outH * a.outW)) : 0;   // images per group
   if constexpr (BST) {
     float *bt = reinterpret_cast<float *>(smem + XF0);
     const int nst = a.bwd.grows ? (int)(a.M / a.bwd.grows) * a.Ncol : a.Ncol;
     for (int c = tid; c < nst; c += 512) {
       bt[c] = a.bwd.mean[c];
-      bt[512 + c] = a.bwd.invstd[c];
+      bt[BST_N + c] = a.bwd.invstd[c];
     }
-    for (int c = tid; c < a.Ncol; c += 512) {
-      const int cg = c % a.ogc;
-      bt[1024 + c] = a.bwd.gamma ? a.bwd.gamma[cg] : 1.f;
-      bt[1536 + c] = a.bwd.beta ? a.bwd.beta[cg] : 0.f;
+    for (int c = tid; c < a.ogc; c += 512) {
+      bt[2 * BST_N + c] = a.bwd.gamma ? a.bwd.gamma[c] : 1.f;
+      bt[2 * BST_N + BST_G + c] = a.bwd.beta ? a.bwd.beta[c] : 0.f;
     }
   }
   __syncthreads();
@@ -364,10 +367,14 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
       float bmu[4], biv[4], bga[4], bbe[4];
       if constexpr (BST) {
-        const float *bt = reinterpret_cast<const float *>(smem + XF0) + col;
-        const int so = bgi ? d.img / bgi * a.Ncol : 0;     // the row group's statistics
+        const float *bt = reinterpret_cast<const float *>(smem + XF0);
+        const int so = (bgi ? d.img / bgi * a.Ncol : 0) + col;     // the row group's statistics
+        const int cg = col - gi * a.ogc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { bmu[r] = bt[so + r]; biv[r] = bt[512 + so + r]; bga[r] = bt[1024 + r]; bbe[r] = bt[1536 + r]; }
+        for (int r = 0; r < 4; ++r) {
+          bmu[r] = bt[so + r]; biv[r] = bt[BST_N + so + r];
+          bga[r] = bt[2 * BST_N + cg + r]; bbe[r] = bt[2 * BST_N + BST_G + cg + r];
+        }
       }
 #pragma unroll
       for (int i = 0; i < NER; ++i) {
@@ -613,13 +620,18 @@ static bool win_ks(const FwdArgs &a, bool dgrad) {
 
 bool win_ok(const FwdArgs &a, bool dgrad) {
   if (!g_win || a.g.ks != 3 || a.g.stride != 1 || a.g.pad != 1 || a.pc >= 0 || a.addend) return false;
-  if (a.bwd.part && (!dgrad || a.bwd.rscale || !a.bwd.x || !a.bwd.mean || !a.bwd.invstd || a.Ncol > 512)) return false;
+  if (a.bwd.part && (!dgrad || a.bwd.rscale || !a.bwd.x || !a.bwd.mean || !a.bwd.invstd || a.Ncol > BST_N ||
+                     a.ogc > BST_G)) return false;
   // BatchNorm row groups of whole images, their statistics table in LDS
   if (a.bwd.part && a.bwd.grows &&
-      (a.ogs || a.bwd.grows % ((int64_t)a.outH * a.outW) || a.M % a.bwd.grows || (a.M / a.bwd.grows) * a.Ncol > 512))
+      (a.ogs || a.bwd.grows % ((int64_t)a.outH * a.outW) || a.M % a.bwd.grows || (a.M / a.bwd.grows) * a.Ncol > BST_N))
     return false;
   const bool ks = win_ks(a, dgrad);
+  // (the transform and the BST epilogue measured slower at config 4's 768-channel multiscale conv:
+  // 1445 frames/s unfolded, 1391-1396 folded, 1413-1420 folded without BST — two column tiles
+  // transform every window twice; profiles/r05/ab/fold_config4_768.log)
   if (a.xf && (dgrad || a.KC > 512)) return false;
+  if (a.bwd.part && !a.bwd.grows && a.Ncol > 512) return false;
   if (dgrad && a.bn_part) return false;
   if (a.outH != a.srcH || a.outW != a.srcW || a.outH % WT || a.outW % WT) return false;
   if (a.KC % 64 || a.sgc % 64 || (a.KCr && a.KCr != a.KC)) return false;

@@ -438,10 +438,11 @@ int ewvit_conv2d_fwd(const void *x, const void *wp, const float *bias, void *y, 
  * invstd [groups][group_c], gamma / beta [group_c] or NULL) — the MWT hf fusion BN's backward
  * sums taken by multiscale_fusion's input gradient (reference network/mwt.py:60-72,114).  A
  * plain dx (dx_group_c = Cin, dx_group_stride 0) may instead carry BatchNorm row groups:
- * bn_group_rows > 0 rows per slice (whole images, slices * Cin <= 512), mean / invstd
+ * bn_group_rows > 0 rows per slice (whole images, slices * Cin <= 768), mean / invstd
  * [slices][Cin], part [slices][bn_group_rows/256][2 Cin] — the seperate BNs' per-level
  * statistics taken by hf_conv['fusion']'s input gradient (a 64-column dx: the k-split form,
  * reference network/mwt.py:48-65,84-88).
+ * Limits: Cin <= 512 columns (row groups: slices * Cin <= 768), group_c <= 256.
  * ewvit_conv2d_bwd_bn_win_rows: N*H*W/256 (the rows per channel group; with row groups, the
  * total over the slices), 0 when the windowed kernel does not take it. */
 int64_t ewvit_conv2d_bwd_bn_win_rows(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int ksize, int stride,

@@ -19,8 +19,8 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
-@pytest.mark.parametrize('hw,frames', [(224, 2), (64, 4)])
-def test_mwt_fold_bit_identical(hw, frames, monkeypatch):
+@pytest.mark.parametrize('hw,frames,dim', [(224, 2, 128), (64, 4, 128)])
+def test_mwt_fold_bit_identical(hw, frames, dim, monkeypatch):
     import ewvit
     from network import mwt as M
     # the fusion BN's backward sums: at these sizes the two-node path would take them from the
@@ -29,7 +29,7 @@ def test_mwt_fold_bit_identical(hw, frames, monkeypatch):
     monkeypatch.setattr(ewvit.bn, '_BWD_LINK', False)
     monkeypatch.setattr(ewvit.conv, '_BN_BWD_EPI', False)
     torch.manual_seed(11)
-    a = M.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last).train()
+    a = M.MWT(3, dim, 3).to(DEV).to(memory_format=torch.channels_last).train()
     b = copy.deepcopy(a)
     x = torch.randn(frames, 3, hw, hw, device=DEV)
     names = []
@@ -199,15 +199,17 @@ def test_mwt_fold_bwd_sums_in_dgrad_epilogue(hw, frames, monkeypatch):
         assert c >= 0.99999 and abs(r - 1) <= 1e-4, (n, c, r)
 
 
-def test_dgrad_bn_sums_match_explicit():
+@pytest.mark.parametrize('C,Cout', [(128, 128), (128, 256)])
+def test_dgrad_bn_sums_match_explicit(C, Cout):
     """ewvit_conv2d_bwd_data_bn_win: dx bit-identical to the plain windowed dgrad, the per-block
-    sums of g and g * xhat equal the float64 sums over the returned dx (1e-5 of scale)."""
+    sums of g and g * xhat equal the float64 sums over the returned dx (1e-5 of scale); Cout 256:
+    4 K blocks of dy per column tile."""
     import ewvit  # noqa: F401
     from ewvit import _lib as L
     from ewvit.conv import _pack
     lib = L.load()
     g = torch.Generator().manual_seed(21)
-    N, C, H, W, Cout, levels = 2, 128, 32, 48, 128, 3
+    N, H, W, levels = 2, 32, 48, 3
     NL, Cx = N * levels, C * levels
     gc, gs = C, N * H * W * C
     rows = int(lib.ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, gc, gs, 0))
