@@ -456,6 +456,7 @@ def main():
             dr['achieved'] = round(iso[k + '_bytes'] / iso[k + '_us'] / 1e3, 2)
             dr['frac'] = round(dr['achieved'] / HBM_PEAK_GBS, 5)
             dr['timing'] = 'HIP graph of 50 back-to-back launches, events around the replay'
+            dr['channels'] = iso['channels']      # hf_conv input channels written (9: the real bands)
             # the two-launch path it replaces, same frames: DWT (bands to HBM) + upsample
             dr['two_launch'] = {n: {'avg_us': round(iso[n + '_us'], 3), 'work_per_launch': iso[n + '_bytes'],
                                     'achieved': round(iso[n + '_bytes'] / iso[n + '_us'] / 1e3, 2),

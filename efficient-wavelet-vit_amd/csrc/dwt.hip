@@ -281,6 +281,21 @@ __device__ __forceinline__ float rnd_out(float v) {
 // 9 (or 16 with zero padding) channels of one output pixel
 template <int ODT>
 __device__ __forceinline__ void store_px9(void *out, int64_t o, const float (&v)[9], int ocs) {
+  if (ODT == EWVIT_BF16 && ocs == 9) {
+    // the 9 band channels only (18 B per pixel): four 4-B stores and one 2-B store, the 2-B one
+    // first or last as the pixel's offset is odd or even
+    unsigned short h[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) h[k] = f2bf(v[k]);
+    bf16_t *b = reinterpret_cast<bf16_t *>(out) + o;
+    const int s = (int)(o & 1);             // 1: channel 0 alone, then pairs (1,2) .. (7,8)
+    if (s) b[0] = h[0];
+    else b[8] = h[8];
+    unsigned *w = reinterpret_cast<unsigned *>(b + s);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (unsigned)h[s + 2 * k] | ((unsigned)h[s + 2 * k + 1] << 16);
+    return;
+  }
   if (ODT == EWVIT_BF16 && ocs == 16) {
     unsigned w[8];
 #pragma unroll
@@ -306,17 +321,17 @@ __device__ __forceinline__ float2 load2(const void *x, int64_t i) {
   return make_float2(__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u));
 }
 
-template <int XDT, int ODT, int L, int OWMAX, int NT, int ROWS = DWTF_ROWS>
+template <int XDT, int ODT, int L, int OWMAX, int NT, int ROWS = DWTF_ROWS, int PF = 2>
 __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict__ x, void *__restrict__ out,
                                                            int N, int H, int W, int ocs) {
   constexpr int HALO = L > 1 ? (1 << (L - 1)) : 0;      // level-1 rows
   constexpr int R1 = ROWS + 2 * HALO;              // level-1 window rows
   constexpr int R2 = L >= 2 ? R1 / 2 : 1, R3 = L >= 3 ? R1 / 4 : 1;
   constexpr int O2 = OWMAX / 2, O3 = OWMAX / 4;
-  __shared__ float ll1[L >= 2 ? R1 * OWMAX * 3 : 1];
-  __shared__ float b2[L >= 2 ? R2 * O2 * 9 : 1];
-  __shared__ float ll2[L >= 3 ? R2 * O2 * 3 : 1];
-  __shared__ float b3[L >= 3 ? R3 * O3 * 9 : 1];
+  constexpr int S1 = L >= 2 ? R1 * OWMAX * 3 : 1, S2 = L >= 2 ? R2 * O2 * 9 : 1, S3 = L >= 3 ? R2 * O2 * 3 : 1;
+  constexpr int S4 = L >= 3 ? R3 * O3 * 9 : 1;
+  __shared__ __attribute__((aligned(16))) float sm[S1 + S2 + S3 + S4];
+  float *ll1 = sm, *b2 = sm + S1, *ll2 = b2 + S2, *b3 = ll2 + S3;
   const int tid = threadIdx.x, n = blockIdx.y;
   const int OH = H >> 1, OW = W >> 1;
   const int y0 = blockIdx.x * ROWS;                // first level-1 output row
@@ -324,14 +339,28 @@ __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict
   const int64_t plane = (int64_t)H * W;
   const char *xn = reinterpret_cast<const char *>(x) + (int64_t)n * 3 * plane * (XDT == EWVIT_BF16 ? 2 : 4);
   const int64_t lvl = (int64_t)N * OH * OW * ocs;       // one level's output block
+  // 9 output channels (18 B per pixel): a strip level's ROWS x OW x 9 bf16 output is staged in LDS
+  // and written as 16-B vectors (the strip is contiguous in the output) — level 1 through the
+  // b2 / ll2 space (free until level 2), the upsampled levels through ll1 (free after level 2)
+  constexpr int STG = ROWS * OWMAX * 9 / 2;             // staged floats per strip level
+  const bool stg9 = ODT == EWVIT_BF16 && L == 3 && S2 + S3 >= STG && S1 >= STG && ocs == 9 && (OW % 8) == 0;
+  unsigned short *st1 = reinterpret_cast<unsigned short *>(b2), *stu = reinterpret_cast<unsigned short *>(ll1);
+  const int srows = OH - y0 < ROWS ? OH - y0 : ROWS;
+  // copy a staged strip level (srows x OW x 9 bf16) to its contiguous place in the output
+  auto flush9 = [&](const unsigned short *src, int64_t dst_elem) {
+    const int n16 = srows * OW * 9 / 8;
+    const uint4 *sp = reinterpret_cast<const uint4 *>(src);
+    uint4 *dp = reinterpret_cast<uint4 *>(reinterpret_cast<bf16_t *>(out) + dst_elem);
+    for (int t = tid; t < n16; t += NT) dp[t] = sp[t];
+  };
 
-  // ---- level 1 (registers): 4 pixels per thread in flight
+  // ---- level 1 (registers): PF pixels per thread in flight
   {
     const int items = R1 * OW;
-    for (int i0 = tid; i0 < items; i0 += 4 * NT) {
-      float2 r[4][3][2];
+    for (int i0 = tid; i0 < items; i0 += PF * NT) {
+      float2 r[PF][3][2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < PF; ++k) {
         const int it = i0 + k * NT;
         const int i = it / OW, j = it - i * OW, y = ws1 + i;
         if (it < items && y >= 0 && y < OH) {
@@ -344,7 +373,7 @@ __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict
         }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < PF; ++k) {
         const int it = i0 + k * NT;
         const int i = it / OW, j = it - i * OW, y = ws1 + i;
         if (!(it < items && y >= 0 && y < OH)) continue;
@@ -356,13 +385,24 @@ __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict
           v[3 * c] = B0; v[3 * c + 1] = B1; v[3 * c + 2] = B2;
           if (L >= 2) ll1[(i * OWMAX + j) * 3 + c] = LL;
         }
-        if (i >= HALO && i < HALO + ROWS)
-          store_px9<ODT>(out, (((int64_t)n * OH + y) * OW + j) * ocs, v, ocs);
+        if (i >= HALO && i < HALO + ROWS) {
+          if (stg9) {
+            unsigned short *q = st1 + ((i - HALO) * OW + j) * 9;
+#pragma unroll
+            for (int ch = 0; ch < 9; ++ch) q[ch] = f2bf(v[ch]);
+          } else {
+            store_px9<ODT>(out, (((int64_t)n * OH + y) * OW + j) * ocs, v, ocs);
+          }
+        }
       }
     }
   }
   if constexpr (L >= 2) {
     __syncthreads();
+    if (stg9) {
+      flush9(st1, ((int64_t)n * OH + y0) * OW * 9);
+      __syncthreads();                              // b2 / ll2 staged data read before level 2 writes them
+    }
     // ---- level 2 over LDS: window rows ws2 .. ws2 + R2
     const int OH2 = OH >> 1, OW2 = OW >> 1, ws2 = ws1 >> 1;
     for (int it = tid; it < R2 * OW2; it += NT) {
@@ -398,6 +438,27 @@ __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict
     // ---- levels 2..L upsampled to the strip's level-1 rows
     const int rows = OH - y0 < ROWS ? OH - y0 : ROWS;
     const int items = rows * OW;
+    if (stg9) {
+      // one level at a time through ll1 (free now: level 2 has read it)
+      for (int l = 2; l <= L; ++l) {
+        for (int r = tid; r < items; r += NT) {
+          const int oy = y0 + r / OW, ox = r - (r / OW) * OW;
+          const int hl = OH >> (l - 1), wl = OW >> (l - 1);
+          const Lerp ly = lerp_src(oy, hl, OH), lx = lerp_src(ox, wl, OW);
+          const float *bb = l == 2 ? b2 : b3;
+          const int ow = l == 2 ? O2 : O3, ws = l == 2 ? ws2 : (ws1 >> 2);
+          const float *q00 = bb + ((ly.i0 - ws) * ow + lx.i0) * 9;
+          const float *q01 = q00 + lx.ip * 9, *q10 = q00 + ly.ip * ow * 9, *q11 = q10 + lx.ip * 9;
+          unsigned short *q = stu + r * 9;
+#pragma unroll
+          for (int ch = 0; ch < 9; ++ch) q[ch] = f2bf(bilerp(q00[ch], q01[ch], q10[ch], q11[ch], ly, lx));
+        }
+        __syncthreads();
+        flush9(stu, (l - 1) * lvl + ((int64_t)n * OH + y0) * OW * 9);
+        __syncthreads();
+      }
+      return;
+    }
     for (int it = tid; it < (L - 1) * items; it += NT) {
       const int l = 2 + it / items, r = it - (l - 2) * items;
       const int oy = y0 + r / OW, ox = r - (r / OW) * OW;
@@ -490,6 +551,16 @@ extern "C" int ewvit_dwt_hf_fused_ok(int64_t N, int64_t C, int64_t H, int64_t W,
          W % m == 0 && OH == H / 2 && OW == W / 2 && OW <= 112 && out_channels >= 9 && out_channels <= 16;
 }
 
+// level-1 pixels per thread in flight: 2 (104 VGPRs: two 512-thread workgroups per CU, so the 448
+// strips of config 2 are resident at once) measured 30.2 -> 23.5 us (9 channels) and 32.2 -> 25.7 us
+// (16) against 4 (196 VGPRs, one workgroup per CU); EWVIT_DWTF_PF=4: the A/B
+static int g_dwtf_pf = 2;
+extern "C" int ewvit_dwt_set_pf(int pf) {
+  const int prev = g_dwtf_pf;
+  g_dwtf_pf = pf == 4 ? 4 : 2;
+  return prev;
+}
+
 extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, int64_t C, int64_t H, int64_t W,
                                            int levels, int x_dtype, int out_dtype, int64_t out_channels,
                                            void *stream) {
@@ -505,8 +576,14 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
   dim3 grid((unsigned)((OH + rows - 1) / rows), (unsigned)N), block(nt);
   hipStream_t s = as_stream(stream);
 #define DWTF_L(XD, OD, LV)                                                                                    \
-  hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, nt, rows>), grid, block, 0, s, x, out, (int)N, (int)H, \
-                     (int)W, (int)out_channels)
+  do {                                                                                                        \
+    if (g_dwtf_pf == 4)                                                                                       \
+      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, nt, rows, 4>), grid, block, 0, s, x, out, (int)N, \
+                         (int)H, (int)W, (int)out_channels);                                                  \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwt_hf_fused_kernel<XD, OD, LV, 112, nt, rows, 2>), grid, block, 0, s, x, out, (int)N, \
+                         (int)H, (int)W, (int)out_channels);                                                  \
+  } while (0)
 #define DWTF_D(XD, OD)                        \
   do {                                        \
     if (levels == 1) DWTF_L(XD, OD, 1);       \

@@ -46,6 +46,19 @@ struct HsParams {
   const float *b[3];
 };
 
+// 9-channel input (XS 9: the fused DWT front end's 9 real band channels, 18 B per pixel, no zero
+// channels in HBM): a pixel PAIR (2q, 2q+1) of a row is 36 B = 9 dwords at a 4-B aligned offset
+// (W even).  hs_pair9 rewrites it as the two pixels' 16-channel LDS rows (channels 9..15 zero; one
+// = 1.0 at channel 15 for the weight gradient's bias column).
+__device__ __forceinline__ void hs_pair9(const unsigned (&w)[9], uint4 &a0, uint4 &a1, uint4 &b0, uint4 &b1,
+                                         unsigned c15) {
+  a0 = make_uint4(w[0], w[1], w[2], w[3]);
+  a1 = make_uint4(w[4] & 0xffffu, 0u, 0u, c15);
+  b0 = make_uint4((w[4] >> 16) | (w[5] << 16), (w[5] >> 16) | (w[6] << 16), (w[6] >> 16) | (w[7] << 16),
+                  (w[7] >> 16) | (w[8] << 16));
+  b1 = make_uint4(w[8] >> 16, 0u, 0u, c15);
+}
+
 // ---------------------------------------------------------------- forward (+ BN partials)
 // grid (G, L): block (bx, l) walks bands bx, bx + G, ... of level l (TH output rows of one
 // image each).  A lane ends each 16-pixel group with 4 consecutive output channels of one
@@ -54,7 +67,9 @@ struct HsParams {
 // part[l][bx][c] = sum (y - K_c), part[l][bx][64 + c] = sum (y - K_c)^2.
 // A band's x rows are staged through registers: XP 16-B pieces per thread, all issued together
 // from clamped in-range addresses (one memory round trip per band, not one per piece).
-template <int TH, int XP>
+// XS 9: x has 9 channels per pixel; the band is staged as pixel-pair items (hs_pair9), XP of
+// them per thread, plus one zero item per halo row for its two border pixels.
+template <int TH, int XP, int XS = 16>
 __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict__ x, bf16_t *__restrict__ y,
                                                         HsParams p, int Nl, int H, int W,
                                                         const float *__restrict__ shift, float *__restrict__ part,
@@ -102,8 +117,45 @@ __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict
     }
   const int nbh = (H + TH - 1) / TH, nbands = Nl * nbh;
   const int items = (TH + 2) * Wp * CC;
-  uint4 rx[XP];
+  uint4 rx[XP];                                     // (the unused form's registers are dead code)
+  unsigned rq[XP][9];
   unsigned okm = 0;                                 // which of this thread's pieces lie in the image
+  const int npair = W / 2 + 1, items9 = (TH + 2) * npair;
+  auto fetch9 = [&](int band) {
+    const int img = lvl * Nl + band / nbh, r0 = (band % nbh) * TH;
+    const int rows = H - r0 < TH ? H - r0 : TH;
+    okm = 0;
+    const unsigned *ximg = reinterpret_cast<const unsigned *>(x + (int64_t)img * H * W * 9);
+#pragma unroll
+    for (int k = 0; k < XP; ++k) {
+      const int i = tid + 256 * k;
+      const int tr = i / npair, q = i - tr * npair, ir = r0 - 1 + tr;
+      const bool ok = i < items9 && q < W / 2 && (unsigned)ir < (unsigned)H && tr < rows + 2;
+      okm |= (unsigned)ok << k;
+      const unsigned *p = ximg + (ok ? ((int64_t)ir * W + 2 * q) * 9 / 2 : 0);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) rq[k][e] = p[e];
+    }
+  };
+  auto stage9 = [&]() {
+#pragma unroll
+    for (int k = 0; k < XP; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= items9) continue;
+      const int tr = i / npair, q = i - tr * npair;
+      uint4 a0, a1, b0, b1;
+      if ((okm >> k) & 1u) {
+        hs_pair9(rq[k], a0, a1, b0, b1, 0u);
+      } else {
+        a0 = a1 = b0 = b1 = make_uint4(0u, 0u, 0u, 0u);
+      }
+      // halo pixels 2q + 1, 2q + 2 (q = W / 2: the row's two border pixels 0 and W + 1, zero)
+      const int pa = tr * Wp + (q < W / 2 ? 2 * q + 1 : 0), pb = q < W / 2 ? pa + 1 : tr * Wp + W + 1;
+      uint4 *da = reinterpret_cast<uint4 *>(hs_smem + (size_t)pa * HS_CIN * 2);
+      uint4 *db = reinterpret_cast<uint4 *>(hs_smem + (size_t)pb * HS_CIN * 2);
+      da[0] = a0; da[1] = a1; db[0] = b0; db[1] = b1;
+    }
+  };
   auto fetch = [&](int band) {
     const int img = lvl * Nl + band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
@@ -128,9 +180,12 @@ __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict
   for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
     const int img = lvl * Nl + band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
-    fetch(band);
+    if constexpr (XS == 9) fetch9(band);
+    else fetch(band);
     __syncthreads();                               // the previous band's readers are done
-    {
+    if constexpr (XS == 9) {
+      stage9();
+    } else {
       // LDS image offset of piece i: px * 32 + c8 * 16 bytes (rows of Wp pixels, 16 channels)
       const int c8 = tid % CC;
 #pragma unroll
@@ -232,7 +287,8 @@ __device__ __forceinline__ int hs_dsw(int r) { return ((r >> 1) & 3) << 1; }
 // dy = gamma invstd (g' - mean(g') - xhat mean(g' xhat)), g' = dz [gamma xhat + beta > 0],
 // xhat = (y - mean) invstd, folded to dy = A g' + B y + C and the mask to P y + Q > 0 (table
 // {A, B, C, P, Q}) — the BN backward's dx pass, so dy never goes through memory.
-template <int TH, int DYI, int XI, bool BNB>
+// XS 9: 9-channel x staged as pixel-pair items (hs_pair9), XI of them per thread.
+template <int TH, int DYI, int XI, bool BNB, int XS = 16>
 __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy,
                                                           float *__restrict__ part, int NI, int H, int W,
                                                           const bf16_t *__restrict__ yb, const float *__restrict__ bnt,
@@ -258,7 +314,9 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
   const int nbh = (H + TH - 1) / TH, nbands = NI * nbh;
   const int ndy = Pk * 8, nx = nhalo * 2;
   uint4 rd[DYI], ry[BNB ? DYI : 1], rx[XI];
+  unsigned rq[XI][9];                          // XS 9 (the unused form's registers are dead code)
   unsigned dok = 0, xok = 0;                   // which pieces are real (the loads are unconditional)
+  const int npair = W / 2 + 1, items9 = (TH + 2) * npair;
   auto fetch = [&](int band) {
     const int img = band / nbh, r0 = (band % nbh) * TH;
     const int rows = H - r0 < TH ? H - r0 : TH;
@@ -274,6 +332,21 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
       const int64_t off = ok ? dbase + (int64_t)(i >> 3) * HS_COUT + (i & 7) * 8 : 0;
       rd[k] = *reinterpret_cast<const uint4 *>(dy + off);
       if constexpr (BNB) ry[k] = *reinterpret_cast<const uint4 *>(yb + off);
+    }
+    if constexpr (XS == 9) {
+      // pixel pairs (2q, 2q + 1) of the halo rows; item q = W / 2 of a row: its two border pixels
+      const unsigned *xi = reinterpret_cast<const unsigned *>(x + (int64_t)img * H * W * 9);
+#pragma unroll
+      for (int k = 0; k < XI; ++k) {
+        const int i = tid + 256 * k;
+        const int tr = i / npair, q = i - tr * npair, ir = r0 - 1 + tr;
+        const bool ok = i < items9 && q < W / 2 && (unsigned)ir < (unsigned)H && tr < rows + 2;
+        xok |= (unsigned)ok << k;
+        const unsigned *p = xi + (ok ? ((int64_t)ir * W + 2 * q) * 9 / 2 : 0);
+#pragma unroll
+        for (int e = 0; e < 9; ++e) rq[k][e] = p[e];
+      }
+      return;
     }
     // x halo pieces: pixel h = i / 2 of the (TH + 2) x Wp image, walked incrementally
     int hr = (tid >> 1) / Wp, hc = (tid >> 1) - hr * Wp;
@@ -333,13 +406,31 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
         *reinterpret_cast<uint4 *>(dimg + (i >> 3) * 128 + 16 * ((i & 7) ^ hs_dsw(i >> 3))) = v;
       }
     }
+    if constexpr (XS == 9) {
 #pragma unroll
-    for (int k = 0; k < XI; ++k) {
-      const int i = tid + 256 * k;
-      if (i < nx) {
-        uint4 v = ((xok >> k) & 1u) ? rx[k] : make_uint4(0u, 0u, 0u, 0u);
-        if ((i & 1) && ((xok >> k) & 1u)) v.w = (v.w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
-        *reinterpret_cast<uint4 *>(ximg + i * 16) = v;
+      for (int k = 0; k < XI; ++k) {
+        const int i = tid + 256 * k;
+        if (i >= items9) continue;
+        const int tr = i / npair, q = i - tr * npair;
+        uint4 a0, a1, b0, b1;
+        if ((xok >> k) & 1u) {
+          hs_pair9(rq[k], a0, a1, b0, b1, 0x3f800000u);   // channel 15 := 1.0 (bias column)
+        } else {
+          a0 = a1 = b0 = b1 = make_uint4(0u, 0u, 0u, 0u);
+        }
+        const int pa = tr * Wp + (q < W / 2 ? 2 * q + 1 : 0), pb = q < W / 2 ? pa + 1 : tr * Wp + W + 1;
+        uint4 *da = reinterpret_cast<uint4 *>(ximg + pa * 32), *db = reinterpret_cast<uint4 *>(ximg + pb * 32);
+        da[0] = a0; da[1] = a1; db[0] = b0; db[1] = b1;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < XI; ++k) {
+        const int i = tid + 256 * k;
+        if (i < nx) {
+          uint4 v = ((xok >> k) & 1u) ? rx[k] : make_uint4(0u, 0u, 0u, 0u);
+          if ((i & 1) && ((xok >> k) & 1u)) v.w = (v.w & 0xffffu) | 0x3f800000u;   // channel 15 := 1.0 (bias column)
+          *reinterpret_cast<uint4 *>(ximg + i * 16) = v;
+        }
       }
     }
     __syncthreads();
@@ -544,7 +635,7 @@ extern "C" int64_t ewvit_hfsep_fwd_parts(int64_t L, int64_t N, int64_t H, int64_
   return g;
 }
 
-extern "C" int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int64_t H, int64_t W, const float *w0,
+extern "C" int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int64_t H, int64_t W, int x_channels, const float *w0,
                                const float *w1, const float *w2, const float *b0, const float *b1, const float *b2,
                                const float *bn_shift, float *bn_part, float *bn_shift_out, int nparts,
                                void *stream) {
@@ -557,7 +648,21 @@ extern "C" int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int
   const int th = hs_fwd_th();
   const size_t lds = (size_t)(th + 2) * (W + 2) * HS_CIN * 2;
   EWVIT_CHECK_ARG(lds <= 64 * 1024, "hfsep_fwd: W=%lld too wide", (long long)W);
+  EWVIT_CHECK_ARG(x_channels == 16 || (x_channels == 9 && W % 2 == 0), "hfsep_fwd: x_channels %d (16, or 9 with W even)",
+                  x_channels);
   HsParams p{{w0, w1, w2}, {b0, b1, b2}};
+  if (x_channels == 9) {
+    // pixel-pair items: (TH + 2) x (W / 2 + 1)
+    const int64_t items9 = (int64_t)(th + 2) * (W / 2 + 1);
+    EWVIT_CHECK_ARG(items9 <= 4 * 256, "hfsep_fwd: W=%lld too wide for the 9-channel staging", (long long)W);
+    if (items9 <= 3 * 256)
+      hipLaunchKernelGGL((hfsep_fwd_kernel<8, 3, 9>), dim3((unsigned)g, (unsigned)L), dim3(256), lds, as_stream(stream),
+                         (const bf16_t *)x, (bf16_t *)y, p, (int)N, (int)H, (int)W, bn_shift, bn_part, bn_shift_out);
+    else
+      hipLaunchKernelGGL((hfsep_fwd_kernel<8, 4, 9>), dim3((unsigned)g, (unsigned)L), dim3(256), lds, as_stream(stream),
+                         (const bf16_t *)x, (bf16_t *)y, p, (int)N, (int)H, (int)W, bn_shift, bn_part, bn_shift_out);
+    return launch_status("hfsep_fwd");
+  }
   // the register stage holds a band's (TH + 2) x (W + 2) x 2 x pieces
   const int64_t items = (int64_t)(th + 2) * (W + 2) * 2;
   if (items <= 9 * 256)
@@ -574,7 +679,7 @@ extern "C" int64_t ewvit_hfsep_bwd_weight_workspace(int64_t NI, int64_t H, int64
   return (int64_t)hs_wg_blocks(NI, H) * HS_COUT * HS_K * 4;
 }
 
-extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, float *dw0,
+extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, int x_channels, float *dw0,
                                       float *dw1, float *dw2, float *db0, float *db1, float *db2, float *workspace,
                                       void *stream) {
   EWVIT_CHECK_ARG(x && dy && workspace, "hfsep_bwd_weight: null pointer");
@@ -586,17 +691,20 @@ extern "C" int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI,
   const bool small = Pk * 8 <= 7 * 256 && (th + 2) * (W + 2) * 2 <= 4 * 256;
   EWVIT_CHECK_ARG(small || (Pk * 8 <= 13 * 256 && (th + 2) * (W + 2) * 2 <= 7 * 256),
                   "hfsep_bwd_weight: W=%lld too wide for TH=%d", (long long)W, th);
+  EWVIT_CHECK_ARG(x_channels == 16 || (x_channels == 9 && W % 2 == 0), "hfsep_bwd_weight: x_channels %d", x_channels);
   const size_t lds = (size_t)Pk * 128 + ((size_t)(th + 2) * (W + 2) + 1) * 32;
   hipStream_t s = as_stream(stream);
-#define EWVIT_HS_WG(TH_, D_, X_)                                                                                 \
+#define EWVIT_HS_WG(TH_, D_, X_, XS_)                                                                            \
   do {                                                                                                           \
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, false>), \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, false, XS_>), \
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
     (void)attr;                                                                                                  \
-    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, false>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,    \
+    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, false, XS_>), dim3(G), dim3(256), lds, s, (const bf16_t *)x, \
                        (const bf16_t *)dy, workspace, (int)NI, (int)H, (int)W, nullptr, nullptr, 0, 1);          \
   } while (0)
-  if (small) EWVIT_HS_WG(2, 7, 4); else EWVIT_HS_WG(2, 13, 7);
+  // (XS 9: pixel-pair items (TH + 2) x (W / 2 + 1): 1 per thread for W <= 126, 2 for W <= 254)
+  if (x_channels == 9) { if (small) EWVIT_HS_WG(2, 7, 1, 9); else EWVIT_HS_WG(2, 13, 2, 9); }
+  else if (small) EWVIT_HS_WG(2, 7, 4, 16); else EWVIT_HS_WG(2, 13, 7, 16);
 #undef EWVIT_HS_WG
   int rc = launch_status("hfsep_bwd_weight");
   if (rc) return rc;
@@ -612,7 +720,7 @@ extern "C" int64_t ewvit_hfsep_bn_bwd_weight_workspace(int64_t L, int64_t N, int
 }
 
 extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const void *dz, int64_t L, int64_t N, int64_t H,
-                                         int64_t W, const float *mean, const float *invstd, const float *gamma,
+                                         int64_t W, int x_channels, const float *mean, const float *invstd, const float *gamma,
                                          const float *beta, const float *part, int nrc, float *dw0, float *dw1,
                                          float *dw2, float *db0, float *db1, float *db2, float *dgamma, float *dbeta,
                                          float *workspace, void *stream) {
@@ -626,6 +734,7 @@ extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const voi
   const bool small = Pk * 8 <= 7 * 256 && (th + 2) * (W + 2) * 2 <= 4 * 256;
   EWVIT_CHECK_ARG(small || (Pk * 8 <= 13 * 256 && (th + 2) * (W + 2) * 2 <= 7 * 256),
                   "hfsep_bn_bwd_weight: W=%lld too wide for TH=%d", (long long)W, th);
+  EWVIT_CHECK_ARG(x_channels == 16 || (x_channels == 9 && W % 2 == 0), "hfsep_bn_bwd_weight: x_channels %d", x_channels);
   const size_t lds = (size_t)Pk * 128 + ((size_t)(th + 2) * (W + 2) + 1) * 32 + (size_t)L * 64 * 8 * 4;
   hipStream_t s = as_stream(stream);
   float *tab = workspace + (int64_t)G * HS_COUT * HS_K;
@@ -633,16 +742,17 @@ extern "C" int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const voi
   hipLaunchKernelGGL(hfsep_bn_coef_kernel, dim3((unsigned)L), dim3(1024), 0, s, part, nrc, (float)(N * H * W), mean,
                      invstd, gamma, beta, tab, lsum);
   if (int rc = launch_status("hfsep_bn_bwd_weight coef")) return rc;
-#define EWVIT_HS_WGB(TH_, D_, X_)                                                                                 \
+#define EWVIT_HS_WGB(TH_, D_, X_, XS_)                                                                            \
   do {                                                                                                            \
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, true>), \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(hfsep_wgrad_kernel<TH_, D_, X_, true, XS_>), \
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
     (void)attr;                                                                                                   \
-    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, true>), dim3(G), dim3(256), lds, s, (const bf16_t *)x,     \
+    hipLaunchKernelGGL((hfsep_wgrad_kernel<TH_, D_, X_, true, XS_>), dim3(G), dim3(256), lds, s, (const bf16_t *)x, \
                        (const bf16_t *)dz, workspace, (int)NI, (int)H, (int)W, (const bf16_t *)y, tab, (int)L,    \
                        (int)N);                                                                                   \
   } while (0)
-  if (small) EWVIT_HS_WGB(2, 7, 4); else EWVIT_HS_WGB(2, 13, 7);
+  if (x_channels == 9) { if (small) EWVIT_HS_WGB(2, 7, 1, 9); else EWVIT_HS_WGB(2, 13, 2, 9); }
+  else if (small) EWVIT_HS_WGB(2, 7, 4, 16); else EWVIT_HS_WGB(2, 13, 7, 16);
 #undef EWVIT_HS_WGB
   if (int rc = launch_status("hfsep_bn_bwd_weight")) return rc;
   HsParams out{{dw0, dw1, dw2}, {db0, db1, db2}};

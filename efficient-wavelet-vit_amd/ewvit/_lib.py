@@ -55,6 +55,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_set_win': [_i32],
     'ewvit_conv2d_set_lds_pad': [_i32],
+    'ewvit_dwt_set_pf': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
     'ewvit_probe': [_vp, _i32, _vp],
@@ -102,10 +103,10 @@ SIGNATURES = {
     'ewvit_frames_jitter_normalize': [_vp, _vp, _i64, _i32, _vp, _vp, _vp],
     'ewvit_combined_loss': [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp],
     'ewvit_adam_step_table': [_vp, _i32, _i64, _f64, _vp, _f64, _f64, _f32, _f32, _vp],
-    'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
-    'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_hfsep_fwd': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    'ewvit_hfsep_bwd_weight': [_vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_bn_bwd_reduce': [_vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp],
-    'ewvit_hfsep_bn_bwd_weight': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+    'ewvit_hfsep_bn_bwd_weight': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_bn_act_se_squeeze': [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _vp,
                                 _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
@@ -195,6 +196,8 @@ def load():
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
     if os.environ.get('EWVIT_LDS_PAD') == '0' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
+    if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
+        lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
     _lib = lib
     return lib
 

@@ -30,8 +30,8 @@ class SeperateConvFn(torch.autograd.Function):
             if ctx.needs_input_grad[3 + i]:
                 grads.note_use(p)
         NL, C, H, W = x.shape
-        if C != 16 or NL % levels or x.dtype != torch.bfloat16:
-            raise ValueError(f'seperate_conv: input {tuple(x.shape)} {x.dtype} (want [L*N, 16, H, W] bf16)')
+        if C not in (16, 9) or (C == 9 and W % 2) or NL % levels or x.dtype != torch.bfloat16:
+            raise ValueError(f'seperate_conv: input {tuple(x.shape)} {x.dtype} (want [L*N, 16 | 9, H, W] bf16)')
         for w in (w0, w1, w2):
             if tuple(w.shape) != (18, 3, 3, 3) or w.dtype != torch.float32:
                 raise ValueError(f'seperate_conv: weight {tuple(w.shape)} {w.dtype}')
@@ -49,9 +49,9 @@ class SeperateConvFn(torch.autograd.Function):
                 shifts = torch.empty(levels, 64, dtype=torch.float32, device=x.device)
                 sh = shift.detach().float().contiguous()
             npx = NL * H * W
-            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, *[L.ptr(t) for t in ws], L.ptr(sh),
+            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, C, *[L.ptr(t) for t in ws], L.ptr(sh),
                    L.ptr(part), L.ptr(shifts), nparts, L.stream(y),
-                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (C + 64) * 2.0})
         ctx.save_for_backward(xc)
         ctx.params = params
         outs = (y,) if shift is None else (y, part, shifts)
@@ -63,7 +63,7 @@ class SeperateConvFn(torch.autograd.Function):
     def backward(ctx, dy, *_):
         with L.launch_cap(L.bwd_cap(ctx.cap)):
             (xc,) = ctx.saved_tensors
-            NL, _, H, W = xc.shape
+            NL, C, H, W = xc.shape
             dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             outs = []
             for i, p in enumerate(ctx.params):
@@ -77,13 +77,14 @@ class SeperateConvFn(torch.autograd.Function):
             ws = torch.empty(int(L.load().ewvit_hfsep_bwd_weight_workspace(NL, H, W)) // 4, dtype=torch.float32,
                              device=xc.device)
             npx = NL * H * W
-            L.call('ewvit_hfsep_bwd_weight', L.ptr(xc), L.ptr(dyc), NL, H, W, *[L.ptr(t) for t in outs], L.ptr(ws),
-                   L.stream(dyc), work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+            L.call('ewvit_hfsep_bwd_weight', L.ptr(xc), L.ptr(dyc), NL, H, W, C, *[L.ptr(t) for t in outs], L.ptr(ws),
+                   L.stream(dyc), work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (C + 64) * 2.0})
         return (None, None, None) + tuple(grads.give(p, g, ctx.gen) for p, g in zip(ctx.params, outs))
 
 
 def seperate_conv(x, levels, convs, shift=None):
-    """x [levels*N, 16, H, W] bf16 (channels-last storage; channel 3g+ci of colour g) ->
+    """x [levels*N, 16 | 9, H, W] bf16 (channels-last storage; channel 3g+ci of colour g; 16:
+    channels 9..15 zero, 9: W even) ->
     y [levels*N, 64, H, W] bf16 (channel 18g+o, 54..63 zero) with the three Conv2d modules'
     parameters; with ``shift`` (the concatenated BatchNorm running means, training) also
     (part [levels, nparts, 128], shifts [levels, 64], nparts) for ewvit.bn partials."""
@@ -115,7 +116,7 @@ class SeperateBNReLUFn(torch.autograd.Function):
             if ctx.needs_input_grad[3 + i]:
                 grads.note_use(p)
         NL, C, H, W = x.shape
-        if C != 16 or NL % levels or x.dtype != torch.bfloat16 or gamma.numel() != 64:
+        if C not in (16, 9) or (C == 9 and W % 2) or NL % levels or x.dtype != torch.bfloat16 or gamma.numel() != 64:
             raise ValueError(f'seperate_conv_bn_relu: input {tuple(x.shape)} {x.dtype}, {gamma.numel()} BN channels')
         xc = x.contiguous(memory_format=torch.channels_last)
         N = NL // levels
@@ -132,9 +133,9 @@ class SeperateBNReLUFn(torch.autograd.Function):
             shifts = torch.empty(levels, 64, dtype=torch.float32, device=dev)
             sh = running_mean.detach().float().contiguous()
             npx = NL * H * W
-            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, *[L.ptr(t) for t in ws], L.ptr(sh),
+            L.call('ewvit_hfsep_fwd', L.ptr(xc), L.ptr(y), levels, N, H, W, C, *[L.ptr(t) for t in ws], L.ptr(sh),
                    L.ptr(part), L.ptr(shifts), nparts, L.stream(y),
-                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64) * 2.0})
+                   work={'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (C + 64) * 2.0})
             L.call('ewvit_bn_fwd_partials', L.ptr(y), L.ptr(z), L.BF16, npx, 64, L.ptr(gamma), L.ptr(beta),
                    L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps), 1, L.ptr(mean),
                    L.ptr(invstd), None, L.ptr(part), L.ptr(shifts), nparts, levels, L.stream(z),
@@ -150,7 +151,7 @@ class SeperateBNReLUFn(torch.autograd.Function):
         with L.launch_cap(L.bwd_cap(ctx.cap)):
             xc, y, mean, invstd, gamma, beta = ctx.saved_tensors
             levels = ctx.levels
-            NL, _, H, W = xc.shape
+            NL, C, H, W = xc.shape
             N = NL // levels
             dzc = dz.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             pr = ctx.bnlink.partials_for(dzc) if ctx.bnlink is not None else None
@@ -167,7 +168,7 @@ class SeperateBNReLUFn(torch.autograd.Function):
             dg = torch.empty(64, dtype=torch.float32, device=xc.device) if ctx.needs_input_grad[9] else None
             db = torch.empty(64, dtype=torch.float32, device=xc.device) if ctx.needs_input_grad[10] else None
             npx = NL * H * W
-            work = {'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (16 + 64 + 64) * 2.0}
+            work = {'flops': 2.0 * npx * MACS_PER_PIXEL, 'bytes': npx * (C + 64 + 64) * 2.0}
             if pr is not None:
                 part, nrc = fold_bwd_partials(pr[0], pr[1], levels, 64)
             else:
@@ -181,7 +182,7 @@ class SeperateBNReLUFn(torch.autograd.Function):
                 part, nrc = fold_bwd_partials(part, nrc, levels, 64)
             ws = torch.empty(int(L.load().ewvit_hfsep_bn_bwd_weight_workspace(levels, N, H, W)) // 4,
                              dtype=torch.float32, device=xc.device)
-            L.call('ewvit_hfsep_bn_bwd_weight', L.ptr(xc), L.ptr(y), L.ptr(dzc), levels, N, H, W, L.ptr(mean),
+            L.call('ewvit_hfsep_bn_bwd_weight', L.ptr(xc), L.ptr(y), L.ptr(dzc), levels, N, H, W, C, L.ptr(mean),
                    L.ptr(invstd), L.ptr(gamma), L.ptr(beta), L.ptr(part), nrc, *[L.ptr(t) for t in outs],
                    L.ptr(dg), L.ptr(db), L.ptr(ws), L.stream(dzc), work=work)
         return (None, None, None) + tuple(grads.give(p, g, ctx.gen) for p, g in zip(ctx.params, outs)) + (dg, db)
@@ -200,9 +201,20 @@ _ON = os.environ.get('EWVIT_HFSEP', '1') != '0'      # 0: the block-diagonal den
 
 
 def applies(x, convs):
-    """The shape class of seperate_conv: bf16 16-channel HF input on the GPU, three
-    Conv2d(3, 18, 3, padding=1) with biases, no hooks."""
-    return (_ON and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 16 and x.shape[3] <= 200
+    """The shape class of seperate_conv: bf16 16-channel (or 9-channel, W even) HF input on the
+    GPU, three Conv2d(3, 18, 3, padding=1) with biases, no hooks."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] in (16, 9)
+            and not (x.shape[1] == 9 and x.shape[3] % 2) and convs_apply(x.shape[3], convs))
+
+
+# the 9 real band channels in HBM (the kernels zero-pad K in LDS; 0: the 16-channel layout, A/B)
+HF9 = os.environ.get('EWVIT_HF9', '1') != '0'
+
+
+def convs_apply(W, convs):
+    """The module / width part of applies(): whether a W-wide HF input of these three convs takes
+    the hfsep kernels (decidable before the DWT front end writes the input)."""
+    return (_ON and W <= 200
             and len(convs) == 3 and all(
                 type(c) is torch.nn.Conv2d and tuple(c.weight.shape) == (18, 3, 3, 3) and c.bias is not None
                 and c.stride == (1, 1) and c.padding == (1, 1) and c.dilation == (1, 1) and c.groups == 1

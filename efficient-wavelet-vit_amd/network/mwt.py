@@ -290,15 +290,18 @@ class MWT(nn.Module):
         # the seperate conv runs on the ewvit MFMA conv (K = 9 taps x 16 channels)
         cin = 3 * C
         cpad = (cin + 15) // 16 * 16 if cdt == torch.bfloat16 else cin
+        sep = self.hf_conv['seperate']
+        convs = [sep[i][0] for i in range(3)]
+        if (cdt == torch.bfloat16 and C == 3 and ewvit.hfsep.HF9 and x.is_cuda and out_hw[1] % 2 == 0
+                and ewvit.hfsep.convs_apply(out_hw[1], convs)):
+            cpad = 9        # the 9 real band channels: the hfsep kernels zero-pad K in LDS
         hf = ewvit.dwt_hf_features(x, Lv, out_hw, out_dtype=cdt, out_channels=cpad)
         hf = hf.view(Lv * B, out_hw[0], out_hw[1], cpad).permute(0, 3, 1, 2)   # NCHW view, NHWC memory
-        sep = self.hf_conv['seperate']
         if not hasattr(self, '_sep_bn'):
             self._sep_bn = _GroupBN()
         c18 = 18 * C
         pad = (-c18) % 64
-        convs = [sep[i][0] for i in range(3)]
-        if C == 3 and cpad == 16 and ewvit.hfsep.applies(hf, convs):
+        if C == 3 and cpad in (16, 9) and ewvit.hfsep.applies(hf, convs):
             # the grouped conv on csrc/hfsep.hip: 3 x (3 -> 18) for all levels in one launch,
             # 54 channels + 10 zero channels out (whole 64-channel K slices for the fusion
             # conv), the BatchNorm statistics per level summed on the way (training)

@@ -389,6 +389,8 @@ int ewvit_conv2d_set_win(int variant);
 /* 1 = the windowed kernels request the CU's whole 160 KB of LDS (no co-resident workgroup of
  * another stream on a CU they hold; the default), 0 = their own footprint.  Returns the previous. */
 int ewvit_conv2d_set_lds_pad(int on);
+/* A/B: level-1 pixels per thread in flight in ewvit_dwt_hf_upsample_fused (2, the default, or 4); returns the previous. */
+int ewvit_dwt_set_pf(int pf);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
  * 64 x 128, 32 pixels per K-tile) for n' = k*k*Cin >= 2048 over >= 64K output pixels, else
  * 128-column tiles; 2 = 256-column tiles whenever n' >= 256 and the last tile wastes <= 1/8 of
@@ -632,8 +634,9 @@ int ewvit_combined_loss(const float *logits, const float *labels, const float *s
  * hf_conv['seperate'][g] for g = 0..2 (reference network/mwt.py:48-59: Conv2d(3, 18, 3, pad 1) per
  * colour, applied to channels 3g..3g+2 of the level's HF input at mwt.py:84-86, weights shared by the
  * levels, mwt.py:108) for every level in one launch — the grouped conv it is (1458 MACs per pixel).
- *   x   [L*N][H][W][16] bf16 channels-last, level-major (ewvit_dwt_hf_upsample_fused with 16 output
- *       channels: channel 3g+ci real for g, ci < 3, channels 9..15 zero)
+ *   x   [L*N][H][W][x_channels] bf16 channels-last, level-major (ewvit_dwt_hf_upsample_fused's
+ *       output: channel 3g+ci real for g, ci < 3; x_channels 16: channels 9..15 zero, x_channels 9:
+ *       the 9 band channels only, W even — the kernels zero-pad K in LDS)
  *   y   [L*N][H][W][64] bf16: channel 18g+o for o < 18; channels 54..63 written as zero
  *   w_g [18][3][3][3] fp32, b_g [18] fp32 (the three modules' parameters, contiguous)
  * ewvit_hfsep_fwd also leaves, when bn_part is not NULL, the BatchNorm partial statistics of the
@@ -644,11 +647,11 @@ int ewvit_combined_loss(const float *logits, const float *labels, const float *s
  * [L*N][H][W][64] bf16 and x; workspace: ewvit_hfsep_bwd_weight_workspace(L*N, H, W) bytes.
  * W <= 512. */
 int64_t ewvit_hfsep_fwd_parts(int64_t L, int64_t N, int64_t H, int64_t W);
-int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int64_t H, int64_t W, const float *w0,
+int ewvit_hfsep_fwd(const void *x, void *y, int64_t L, int64_t N, int64_t H, int64_t W, int x_channels, const float *w0,
                     const float *w1, const float *w2, const float *b0, const float *b1, const float *b2,
                     const float *bn_shift, float *bn_part, float *bn_shift_out, int nparts, void *stream);
 int64_t ewvit_hfsep_bwd_weight_workspace(int64_t NI, int64_t H, int64_t W);
-int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, float *dw0, float *dw1,
+int ewvit_hfsep_bwd_weight(const void *x, const void *dy, int64_t NI, int64_t H, int64_t W, int x_channels, float *dw0, float *dw1,
                            float *dw2, float *db0, float *db1, float *db2, float *workspace, void *stream);
 
 /* The seperate conv's weight gradients THROUGH the grouped BatchNorm + ReLU that follows it
@@ -670,7 +673,7 @@ int ewvit_bn_bwd_reduce(const void *dy, const void *x, int dtype, int64_t M, int
                         float *part, void *stream);
 int64_t ewvit_hfsep_bn_bwd_weight_workspace(int64_t L, int64_t N, int64_t H, int64_t W);
 int ewvit_hfsep_bn_bwd_weight(const void *x, const void *y, const void *dz, int64_t L, int64_t N, int64_t H, int64_t W,
-                              const float *mean, const float *invstd, const float *gamma, const float *beta,
+                              int x_channels, const float *mean, const float *invstd, const float *gamma, const float *beta,
                               const float *part, int nrc, float *dw0, float *dw1, float *dw2, float *db0, float *db1,
                               float *db2, float *dgamma, float *dbeta, float *workspace, void *stream);
 

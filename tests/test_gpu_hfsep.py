@@ -221,3 +221,80 @@ def test_fused_seperate_bn_node_matches_two_node_path(hw, monkeypatch):
             assert c >= 0.99999 and abs(r - 1) <= 1e-4, (n, c, r)
         else:
             assert torch.equal(p.grad, q.grad), n
+
+
+@pytest.mark.parametrize('L,N,H,W', [(3, 2, 32, 32), (1, 1, 112, 112), (2, 1, 20, 192), (1, 2, 16, 6)])
+def test_nine_channel_input_bit_identical(L, N, H, W):
+    """x with the 9 real band channels only (18 B per pixel; the kernels zero-pad K in LDS)
+    against the 16-channel layout: forward output, BN partial sums and every weight / bias
+    gradient bit-identical (the LDS images the MFMAs read are the same); W 192: the wider
+    staging forms (config 4's 192-wide level maps)."""
+    import ewvit
+    convs = _convs(13)
+    x16 = _input(L, N, H, W, 14)
+    x9 = x16[:, :9].contiguous(memory_format=torch.channels_last)
+    assert x9.stride(1) == 1 and x9.stride(3) == 9
+    shift = torch.randn(64, device=DEV) * 0.1
+    shift[54:] = 0
+    g = torch.Generator(device=DEV).manual_seed(15)
+    out = []
+    for x in (x16, x9):
+        for c in convs:
+            c.weight.grad = None
+            c.bias.grad = None
+        y, (part, shifts, nrc) = ewvit.hfsep.seperate_conv(x, L, convs, shift=shift)
+        dy = torch.randn(y.shape, device=DEV, generator=g.manual_seed(15)).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        out.append((y, part, [c.weight.grad.clone() for c in convs] + [c.bias.grad.clone() for c in convs]))
+    (y0, p0, g0), (y1, p1, g1) = out
+    assert torch.equal(y0, y1)
+    assert torch.equal(p0, p1)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+
+
+def test_dwt_front_end_nine_channels():
+    """ewvit.dwt_hf_features with 9 output channels: the first 9 channels of the 16-channel
+    output, bit for bit, on the fused launch (224^2 frames) and the two-launch path (384^2)."""
+    import ewvit
+    for hw in (224, 384):
+        x = torch.randn(2, 3, hw, hw, device=DEV)
+        a = ewvit.dwt_hf_features(x, 3, (hw // 2, hw // 2), out_dtype=torch.bfloat16, out_channels=16)
+        b = ewvit.dwt_hf_features(x, 3, (hw // 2, hw // 2), out_dtype=torch.bfloat16, out_channels=9)
+        torch.cuda.synchronize()
+        assert b.shape[-1] == 9
+        assert torch.equal(a[..., :9], b), hw
+
+
+@pytest.mark.parametrize('hw', [64, 224])
+def test_mwt_nine_channel_front_end_bit_identical(hw, monkeypatch):
+    """The MWT with the 9-channel HF layout (ewvit.hfsep.HF9) against the 16-channel one: output,
+    BN state and every parameter gradient bit-identical."""
+    import copy
+    import ewvit
+    from network import mwt as M
+    torch.manual_seed(6)
+    a = M.MWT(3, 128, 3).to(DEV).to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(2, 3, hw, hw, device=DEV)
+    shapes = []
+    real = ewvit.hfsep.applies
+    monkeypatch.setattr(ewvit.hfsep, 'applies', lambda t, c: (shapes.append(t.shape[1]), real(t, c))[1])
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        ya = a(x)
+    ya.float().square().mean().backward()
+    monkeypatch.setattr(ewvit.hfsep, 'HF9', False)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        yb = b(x)
+    yb.float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert shapes == [9, 16]
+    assert torch.equal(ya, yb)
+    for (n, u), v in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(u, v), n
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert (p.grad is None) == (q.grad is None), n
+        if p.grad is not None:
+            assert torch.equal(p.grad, q.grad), n

@@ -37,25 +37,29 @@ def graph_us(fn, iters):
     return best
 
 
-def measure(n=64, hw=224, levels=3, iters=50):
-    """-> {'dwt_us', 'dwt_bytes', 'up_us', 'up_bytes', 'fused_us', 'fused_bytes'} (algorithmic
-    bytes per launch)."""
-    from ewvit import ops
+def measure(n=64, hw=224, levels=3, iters=50, channels=None):
+    """-> {'dwt_us', 'dwt_bytes', 'up_us', 'up_bytes', 'fused_us', 'fused_bytes', 'channels'}
+    (algorithmic bytes per launch) for the hf_conv input layout the MWT writes: `channels` = 9
+    (the real band channels, ewvit.hfsep.HF9) or 16 (zero-padded); default: the MWT's own."""
+    from ewvit import hfsep, ops
+    if channels is None:
+        channels = 9 if hfsep.HF9 else 16
     dev = torch.device('cuda', 0)
     x = torch.randn(n, 3, hw, hw, device=dev)
     ll, yh, sizes = ops._dwt_flat(x, levels, torch.bfloat16)
     dwt_bytes = x.numel() * 4 + (yh.numel() + ll.numel()) * 2
     dwt_us = graph_us(lambda: ops._dwt_flat(x, levels, torch.bfloat16), iters)
-    out = ops.hf_upsample(yh, n, 3, hw, hw, levels, (hw // 2, hw // 2), torch.bfloat16, 16)
+    c = channels
+    out = ops.hf_upsample(yh, n, 3, hw, hw, levels, (hw // 2, hw // 2), torch.bfloat16, c)
     up_bytes = yh.numel() * 2 + out.numel() * 2
-    up_us = graph_us(lambda: ops.hf_upsample(yh, n, 3, hw, hw, levels, (hw // 2, hw // 2), torch.bfloat16, 16),
+    up_us = graph_us(lambda: ops.hf_upsample(yh, n, 3, hw, hw, levels, (hw // 2, hw // 2), torch.bfloat16, c),
                      iters)
     fused_us = fused_bytes = None                      # the fused launch takes W <= 224
-    if ops.L.load().ewvit_dwt_hf_fused_ok(n, 3, hw, hw, levels, hw // 2, hw // 2, 16):
-        fused_us = graph_us(lambda: ops._dwt_hf_fused_op(x, levels, torch.bfloat16, 16), iters)
+    if ops.L.load().ewvit_dwt_hf_fused_ok(n, 3, hw, hw, levels, hw // 2, hw // 2, c):
+        fused_us = graph_us(lambda: ops._dwt_hf_fused_op(x, levels, torch.bfloat16, c), iters)
         fused_bytes = x.numel() * 4 + out.numel() * 2  # frames in + hf_conv input out
     return {'dwt_us': dwt_us, 'dwt_bytes': dwt_bytes, 'up_us': up_us, 'up_bytes': up_bytes,
-            'fused_us': fused_us, 'fused_bytes': fused_bytes}
+            'fused_us': fused_us, 'fused_bytes': fused_bytes, 'channels': c}
 
 
 def main():
@@ -64,13 +68,15 @@ def main():
     ap.add_argument('--hw', type=int, default=224)
     ap.add_argument('--levels', type=int, default=3)
     ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--channels', type=int, nargs='*', default=[9, 16])
     a = ap.parse_args()
-    r = measure(a.n, a.hw, a.levels, a.iters)
-    for k in ('dwt', 'up', 'fused'):
-        us, b = r[k + '_us'], r[k + '_bytes']
-        if us is None:
-            continue
-        print(f'{k:5s} {us:8.2f} us  {b / 1e6:7.2f} MB  {b / us / 1e3:7.1f} GB/s', flush=True)
+    for ch in a.channels:
+        r = measure(a.n, a.hw, a.levels, a.iters, ch)
+        for k in ('dwt', 'up', 'fused'):
+            us, b = r[k + '_us'], r[k + '_bytes']
+            if us is None:
+                continue
+            print(f'{ch:2d}ch {k:5s} {us:8.2f} us  {b / 1e6:7.2f} MB  {b / us / 1e3:7.1f} GB/s', flush=True)
 
 
 if __name__ == '__main__':
