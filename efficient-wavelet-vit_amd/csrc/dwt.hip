@@ -332,9 +332,19 @@ __global__ __launch_bounds__(NT) void dwt_hf_fused_kernel(const void *__restrict
   constexpr int S4 = L >= 3 ? R3 * O3 * 9 : 1;
   __shared__ __attribute__((aligned(16))) float sm[S1 + S2 + S3 + S4];
   float *ll1 = sm, *b2 = sm + S1, *ll2 = b2 + S2, *b3 = ll2 + S3;
-  const int tid = threadIdx.x, n = blockIdx.y;
   const int OH = H >> 1, OW = W >> 1;
-  const int y0 = blockIdx.x * ROWS;                // first level-1 output row
+  // one-dimensional grid, XCD-aware: the blocks one XCD receives (b, b + 8, ...) take consecutive
+  // (frame, strip) ids, so a strip's halo rows are mostly the L2 lines its neighbour strip, on the
+  // same XCD, loads (round-robin strips put every neighbour on another XCD's L2)
+  const int nstrip = (OH + ROWS - 1) / ROWS;
+  int sid;
+  {
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    sid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tid = threadIdx.x, n = sid / nstrip;
+  const int y0 = (sid - n * nstrip) * ROWS;        // first level-1 output row
   const int ws1 = y0 - HALO;                            // window origin, level-1 rows
   const int64_t plane = (int64_t)H * W;
   const char *xn = reinterpret_cast<const char *>(x) + (int64_t)n * 3 * plane * (XDT == EWVIT_BF16 ? 2 : 4);
@@ -573,7 +583,7 @@ extern "C" int ewvit_dwt_hf_upsample_fused(const void *x, void *out, int64_t N, 
   // 512 threads over 16-row strips (29.9 -> 26.5 us at config 2 against 256 threads; 1024: 29.7;
   // 8-row strips 31-33 us, 32-row strips on 1024 threads 26.3 us: profiles/r02/ab/dwtf_rows.log)
   constexpr int nt = 512, rows = 16;
-  dim3 grid((unsigned)((OH + rows - 1) / rows), (unsigned)N), block(nt);
+  dim3 grid((unsigned)((OH + rows - 1) / rows * N)), block(nt);
   hipStream_t s = as_stream(stream);
 #define DWTF_L(XD, OD, LV)                                                                                    \
   do {                                                                                                        \
