@@ -67,6 +67,15 @@ CONFIGS = {
 }
 
 
+def _gemm(config):
+    """The token GEMMs' precision of a config; EWVIT_BENCH_GEMM=bf16|fp8 overrides it for A/Bs
+    (the line's dtype and config.token_gemms report what ran)."""
+    g = os.environ.get('EWVIT_BENCH_GEMM') or CONFIGS.get(config, {}).get('gemm', 'bf16')
+    if g not in ('bf16', 'fp8'):
+        raise SystemExit(f'bench.py: EWVIT_BENCH_GEMM={g!r} (bf16 | fp8)')
+    return g
+
+
 def build_mwt_step(dev, frames, rank, graph=True):
     """BASELINE.json configs[3]: the MWT branch (mwt.py:92-119) at 384^2, 32 frames, dim 256,
     3 DWT levels — the reference's SFE cannot run at 384^2 (its 12x12 backbone map is not
@@ -100,12 +109,13 @@ def build_step(dev, frames, rank, graph=True, config=2, force_collectives=False)
     torch.manual_seed(0)                                   # identical init on every rank
     cfg = CONFIGS[config]
     videos = cfg['videos'] * frames // cfg['frames']
+    gemm = _gemm(config)
     per_video = frames // videos
     chunk = cfg['chunk']                                   # frames per video per _process_frame call
     model = DeepfakeDetector(3, 128, batch_size=chunk).to(dev).to(memory_format=torch.channels_last)
-    if cfg['gemm'] != 'bf16':
+    if gemm != 'bf16':
         from network import set_gemm_precision
-        set_gemm_precision(model, cfg['gemm'])
+        set_gemm_precision(model, gemm)
     params = [p for p in model.parameters() if p.requires_grad]
     opt = ewvit.optim.Adam(params, lr=1e-4, weight_decay=1e-4)      # train.py:273-275 on csrc/optim.hip
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([0.5], device=dev))
@@ -297,7 +307,7 @@ def workload(args, world, step):
     cfg = CONFIGS[args.config]
     return {'workload': 'DAMA train step: DeepfakeDetector dynamic fwd + combined_loss + bwd + Adam',
             'image': 224, 'frames_per_gpu': args.frames, 'dim': 128, 'chunk_frames': cfg['videos'] * cfg['chunk'],
-            'token_gemms': cfg['gemm'], 'global_batch': args.frames * world, 'parallelism': f'dp{world}',
+            'token_gemms': _gemm(args.config), 'global_batch': args.frames * world, 'parallelism': f'dp{world}',
             'launch': step.mode, 'baseline_config': 3 if world > 1 else args.config}
 
 
@@ -404,7 +414,7 @@ def main():
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(1e3 * elapsed / args.steps, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                # config 5: the attention / MLP token GEMMs on fp8 e4m3 operands, everything else bf16
-               'dtype': 'fp8e4m3+bf16' if CONFIGS.get(args.config, {}).get('gemm') == 'fp8' else 'bf16',
+               'dtype': 'fp8e4m3+bf16' if _gemm(args.config) == 'fp8' else 'bf16',
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
