@@ -660,18 +660,19 @@ static int cu_count() {
 
 // ---------------------------------------------------------------- weight gradient
 // dW[co][tap][ci] = sum_pix dy[pix][co] * x[pix + tap shift][ci] over 8 x 16-pixel tiles (the
-// K chunks): a workgroup owns (pixel split, 128-row co tile, 64-channel ci block) and all 9
-// taps — a [128 co] x [9 x 64] block of the weight gradient — and walks its split's pixel
-// tiles.  Per tile it stages the dy tile (128 px x 128 co, 32 KB) and the tile's 10 x 18 x 64
-// x window (23 KB, ONCE for the nine taps) by LDS-DMA into one of two stages, the next tile's
-// landing during this tile's 144 MFMAs per wave.  Both operands are read transposed
+// K chunks): a workgroup owns (pixel split, 128-row co tile, 32-channel ci block) and all 9
+// taps — a [128 co] x [9 x 32] block of the weight gradient — and walks its split's pixel
+// tiles.  Per tile it stages the dy tile (128 px x 128 co, 32 KB) and the tile's 10 x 18 x 32
+// x window (11.5 KB, ONCE for the nine taps) by LDS-DMA into one of two stages, the next tile's
+// landing during this tile's MFMAs (144 per wave, 80 / 64 under TS).  Both operands are read transposed
 // (ds_read_b64_tr_b16): dy as the MFMA A operand (the generic wgrad's image and swizzle),
 // the window as B with pixel p's 16-B chunk c at c ^ (((p >> 1) & 1) << 1 | ((p >> 3) & 1)
 // << 2) — conflict-free for the 32 lanes of a read at any tap offset (brute-forced).  That
 // swizzle depends on p mod 16 only, so a lane's 16 window addresses (one per p mod 16) are
 // computed once and every tap / k32 step / half reads at one of them plus an immediate
-// offset: no address VALU in the loop.  8 waves = 2 co halves x 4 ci quarters; each wave
-// 64 co x (9 taps x 16 ci) = 144 fp32 accumulators per lane.  The bias gradient (sum of dy
+// offset: no address VALU in the loop.  4 waves = 2 co halves x 2 ci halves, each wave
+// 64 co x (9 taps x 16 ci) = 144 fp32 accumulators per lane; the default tap-split form (TS)
+// runs 8 waves, the second four repeating those blocks for taps 5-8 (80 accumulators).  The bias gradient (sum of dy
 // over pixels) is one more MFMA per k32 step against a ones operand, by the ci-block-0
 // workgroups.  Per split: fp32 slabs [split][Cout][9 Cin] (+ [split][Cout] bias partials)
 // summed by conv_wgrad_reduce_kernel in a fixed order.
@@ -686,6 +687,8 @@ constexpr int GD0 = 2 * GX_B;                      // [X0][X1][D0][D1]
 constexpr int GSMEM = GD0 + 2 * GD_B;              // 90,112 B
 }  // namespace
 
+template <int V> struct ic_t { static constexpr int value = V; };
+
 // 64-B window rows: chunk c of pixel p at c ^ (((p >> 3) & 1) << 1)
 __device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
 
@@ -693,13 +696,19 @@ __device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
 // XF: x is read as relu(x * scale + shift) (WgradArgs::xf, the forward's input transform): each
 // wave rewrites its own window pieces of the next tile after its DMAs drained at the end of the
 // current tile (the loop-top barrier publishes them), the first tile's before the loop.
-template <bool BIAS, bool XF = false>
-__global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb, int nct,
-                                                             int ntile) {
+// TS (tap split): 8 waves, two per SIMD — waves 4..7 repeat waves 0..3's (co half, ci half) roles
+// for taps 5..8 while waves 0..3 take taps 0..4 (80 accumulators instead of 144, every output
+// still owned by one wave: no cross-wave reduction); the DMA pieces are spread over the 8 waves.
+template <bool BIAS, bool XF = false, bool TS = false>
+__global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb,
+                                                                        int nct, int ntile) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[GSMEM];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int ws = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wsa = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7 (TS) | 0..3
+  const int kq = TS ? wsa >> 2 : 0;                 // TS: tap half (0: taps 0-4, 1: taps 5-8)
+  const int ws = TS ? wsa & 3 : wsa;
   const int wr = ws >> 1, wc = ws & 1;              // co half, 16-channel half of the 32-channel block
+  constexpr int PPW = TS ? 4 : 8, XPW = TS ? 2 : 3;  // dy / x DMA pieces per wave
   const int r = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int cb = r % ncb, ct = (r / ncb) % nct, split = r / (ncb * nct);
   const int t0 = (int)((int64_t)split * ntile / nsplit), t1 = (int)((int64_t)(split + 1) * ntile / nsplit);
@@ -721,19 +730,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
     const int oh0 = (rem / tpr) * GT_R, ow0 = (rem % tpr) * GT_C;
     int dl = lane >> 4;
     asm volatile("" : "+v"(dl));
-    const int64_t dpix = ((int64_t)img * H + oh0 + 2 * ws) * W + ow0;
+    // dy piece P = wsa * PPW + j: tile row P / 4, pixels 4 (P & 3) + lane / 16
+    const int64_t dpix = ((int64_t)img * H + oh0) * W + ow0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int sc = (lane & 15) ^ ((dl << 2) | (j & 3));
-      const uint32_t off = (uint32_t)(((dpix + (j >> 2) * W + 4 * (j & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
-      glds16_asm(rd, lds0 + GD0 + b * GD_B + (ws * 8 + j) * 1024, live ? off : OOB);
+    for (int j = 0; j < PPW; ++j) {
+      const int P = wsa * PPW + j;
+      const int sc = (lane & 15) ^ ((dl << 2) | (P & 3));
+      const uint32_t off = (uint32_t)(((dpix + (P >> 2) * W + 4 * (P & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
+      glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB);
     }
     const int64_t xpix = ((int64_t)img * H + oh0 - 1) * W + ow0 - 1;
     int xl = lane >> 2;
     asm volatile("" : "+v"(xl));
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int q = ws * 3 + j;
+    for (int j = 0; j < XPW; ++j) {
+      if (TS && wsa * XPW + j >= GX_PIECES) continue;   // (TS: waves 6, 7 stage no window piece)
+      const int q = wsa * XPW + j;
       const int p = q * 16 + xl;
       const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;       // p / 18, p % 18
       const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
@@ -761,8 +773,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
     int xl = lane >> 2;
     asm volatile("" : "+v"(xl));
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int q = ws * 3 + j;
+    for (int j = 0; j < XPW; ++j) {
+      if (TS && wsa * XPW + j >= GX_PIECES) continue;
+      const int q = wsa * XPW + j;
       const int p = q * 16 + xl;
       const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;
       const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
@@ -804,49 +817,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) cs4 *)(smem + off));
   };
 
-  cf32x4 acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = cf32x4{0.f, 0.f, 0.f, 0.f};
-  cf32x4 bacc[2] = {cf32x4{0.f, 0.f, 0.f, 0.f}, cf32x4{0.f, 0.f, 0.f, 0.f}};
   const cbf16x8 ones = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
       0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
-
-  // one loop body for both stages (two bodies made hipcc copy the accumulators between
-  // them): the stage's addresses are toggled by +-stage size after each tile
-  auto compute = [&]() {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      cbf16x8 af[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const cs4 lo = trd(aad[0][i] + ks * 8192), hi = trd(aad[1][i] + ks * 8192);
-        af[i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
-                                                lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-      }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int kh = t / 3, kw = t % 3;
-        const int C0 = ks * 2 * GX_W + kh * GX_W + kw, C1 = C0 + 4;
-        const cs4 lo = trd(xad[C0 & 15] + (C0 & ~15) * 64);
-        const cs4 hi = trd(xad[C1 & 15] + (C1 & ~15) * 64);
-        const cbf16x8 bf = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
-                                                  lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][t], 0, 0, 0);
-      }
-      if (do_bias) {           // co rows wr*64 + 32 wc .. +31 (wave-uniform branch: a runtime index into af -> scratch)
-        if (wc == 0) {
-          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
-          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
-        } else {
-          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], ones, bacc[0], 0, 0, 0);
-          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[3], ones, bacc[1], 0, 0, 0);
-        }
-      }
-    }
-  };
 
   // (the last tile issues a dummy stage — every lane out of range, zeros into the idle stage —
   // so no branch sits between the DMA and the fragment reads: at such a merge hipcc waits
@@ -858,44 +830,100 @@ __global__ __launch_bounds__(256) void conv_wgrad_win_kernel(WgradArgs a, int64_
       xform(t0, 0);
     }
   }
-  int sd = GD_B, sx = GX_B;          // stage 0 -> 1 address deltas
-  for (int t = t0, b = 0; t < t1; ++t, b ^= 1) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    issue(t + 1 < t1 ? t + 1 : t, b ^ 1, t + 1 < t1);
-    compute();
-    // (transformed after this tile's MFMAs: between its k32 steps measured slower, 948 -> 988 us)
-    if constexpr (XF) {
-      if (t + 1 < t1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        xform(t + 1, b ^ 1);
-      }
-    }
-#pragma unroll
-    for (int hi = 0; hi < 2; ++hi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) aad[hi][i] += sd;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) xad[m] += sx;
-    sd = -sd;
-    sx = -sx;
-  }
 
-  // slab [split][Cout][9 Cin]: lane holds rows co = 4 (lane>>4) + rr of each 16-row frag, column lane & 15
-  float *dst = a.part + (int64_t)split * Cout * NP;
-  const int co0 = ct * 128 + wr * 64 + 4 * g;
-  const int cl = c32 + wc * 16 + (lane & 15);
+  // the tile loop over taps TB .. TB + NT - 1 (TS: one tap half per wave group, a separate copy
+  // of the loop per half so each keeps its accumulators in fixed registers)
+  auto run = [&](auto KQ) __attribute__((always_inline)) {
+    constexpr int kqc = decltype(KQ)::value;
+    constexpr int TB = 5 * kqc, NT = TS ? (kqc ? 4 : 5) : 9;
+    const bool bias_w = do_bias && kqc == 0;
+    cf32x4 acc[4][NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < NT; ++t) acc[i][t] = cf32x4{0.f, 0.f, 0.f, 0.f};
+    cf32x4 bacc[2] = {cf32x4{0.f, 0.f, 0.f, 0.f}, cf32x4{0.f, 0.f, 0.f, 0.f}};
+
+    // one loop body for both stages (two bodies made hipcc copy the accumulators between
+    // them): the stage's addresses are toggled by +-stage size after each tile
+    auto compute = [&]() {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) dst[(int64_t)(co0 + i * 16 + rr) * NP + t * Cin + cl] = acc[i][t][rr];
-  if (do_bias && (lane & 15) == 0)
+      for (int ks = 0; ks < 4; ++ks) {
+        cbf16x8 af[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 4; ++i) {
+          const cs4 lo = trd(aad[0][i] + ks * 8192), hi = trd(aad[1][i] + ks * 8192);
+          af[i] = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                  lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        }
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        a.dbias_part[(int64_t)split * Cout + ct * 128 + wr * 64 + wc * 32 + h * 16 + 4 * g + rr] = bacc[h][rr];
+        for (int tt = 0; tt < NT; ++tt) {
+          const int t = TB + tt, kh = t / 3, kw = t % 3;
+          const int C0 = ks * 2 * GX_W + kh * GX_W + kw, C1 = C0 + 4;
+          const cs4 lo = trd(xad[C0 & 15] + (C0 & ~15) * 64);
+          const cs4 hi = trd(xad[C1 & 15] + (C1 & ~15) * 64);
+          const cbf16x8 bf = __builtin_bit_cast(cbf16x8, (__attribute__((ext_vector_type(8))) short){
+                                                    lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][tt], 0, 0, 0);
+        }
+        if (bias_w) {          // co rows wr*64 + 32 wc .. +31 (wave-uniform branch: a runtime index into af -> scratch)
+          if (wc == 0) {
+            bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
+            bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
+          } else {
+            bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], ones, bacc[0], 0, 0, 0);
+            bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[3], ones, bacc[1], 0, 0, 0);
+          }
+        }
+      }
+    };
+
+    int sd = GD_B, sx = GX_B;          // stage 0 -> 1 address deltas
+    for (int t = t0, b = 0; t < t1; ++t, b ^= 1) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(t + 1 < t1 ? t + 1 : t, b ^ 1, t + 1 < t1);
+      compute();
+      // (transformed after this tile's MFMAs: between its k32 steps measured slower, 948 -> 988 us)
+      if constexpr (XF) {
+        if (t + 1 < t1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          xform(t + 1, b ^ 1);
+        }
+      }
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) aad[hi][i] += sd;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) xad[m] += sx;
+      sd = -sd;
+      sx = -sx;
+    }
+
+    // slab [split][Cout][9 Cin]: lane holds rows co = 4 (lane>>4) + rr of each 16-row frag, column lane & 15
+    float *dst = a.part + (int64_t)split * Cout * NP;
+    const int co0 = ct * 128 + wr * 64 + 4 * g;
+    const int cl = c32 + wc * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) dst[(int64_t)(co0 + i * 16 + rr) * NP + (TB + tt) * Cin + cl] = acc[i][tt][rr];
+    if (bias_w && (lane & 15) == 0)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          a.dbias_part[(int64_t)split * Cout + ct * 128 + wr * 64 + wc * 32 + h * 16 + 4 * g + rr] = bacc[h][rr];
+  };
+  if constexpr (TS) {
+    if (kq == 0) run(ic_t<0>{});
+    else run(ic_t<1>{});
+  } else {
+    run(ic_t<0>{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -915,18 +943,31 @@ int wgrad_win_splits(const WgradArgs &a, int64_t x_bytes) {
   return (int)s;
 }
 
+// the tap-split 8-wave variant (default): two waves per SIMD hide each other's LDS fragment
+// reads behind MFMAs — config 4 1513 -> 1592 frames/s, config 2 3621 -> 3627 (same box,
+// profiles/r05/ab/wgrad_tap_split.log); 0 (EWVIT_WGWIN_TS=0): the 4-wave kernel
+int g_wgwin_ts = 1;
+
+template <bool BIAS, bool XF, bool TS>
+static void launch_wgrad_win_t(const WgradArgs &a, int64_t x_bytes, int splits, int ncb, int nct, int ntile, hipStream_t s) {
+  const unsigned nwg = (unsigned)(splits * ncb * nct);
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<BIAS, XF, TS>), dim3(nwg), dim3(TS ? 512 : 256),
+                     lds_pad(conv_wgrad_win_kernel<BIAS, XF, TS>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
+}
+
 bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream_t s) {
   const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
   const int ntile = (int)(a.M / (GT_R * GT_C));
-  const unsigned nwg = (unsigned)(splits * ncb * nct);
-  if (a.xf && a.dbias_part)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<true, true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<true, true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
-  else if (a.xf)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<false, true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<false, true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
-  else if (a.dbias_part)
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<true>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<true>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
-  else
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<false>), dim3(nwg), dim3(256), lds_pad(conv_wgrad_win_kernel<false>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
+  const bool b = a.dbias_part != nullptr, x = a.xf != nullptr;
+  auto go = [&](auto TSc) {
+    constexpr bool T = decltype(TSc)::value != 0;
+    if (x && b) launch_wgrad_win_t<true, true, T>(a, x_bytes, splits, ncb, nct, ntile, s);
+    else if (x) launch_wgrad_win_t<false, true, T>(a, x_bytes, splits, ncb, nct, ntile, s);
+    else if (b) launch_wgrad_win_t<true, false, T>(a, x_bytes, splits, ncb, nct, ntile, s);
+    else launch_wgrad_win_t<false, false, T>(a, x_bytes, splits, ncb, nct, ntile, s);
+  };
+  if (g_wgwin_ts) go(ic_t<1>{});
+  else go(ic_t<0>{});
   return true;
 }
 
@@ -960,6 +1001,12 @@ bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) 
 }
 
 }  // namespace ewvit
+
+extern "C" int ewvit_conv2d_set_wgrad_tap_split(int on) {
+  const int prev = ewvit::g_wgwin_ts;
+  ewvit::g_wgwin_ts = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int ewvit_conv2d_set_lds_pad(int on) {
   const int prev = ewvit::g_lds_pad;

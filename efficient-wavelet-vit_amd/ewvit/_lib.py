@@ -55,6 +55,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_glds': [_i32],
     'ewvit_conv2d_set_win': [_i32],
     'ewvit_conv2d_set_lds_pad': [_i32],
+    'ewvit_conv2d_set_wgrad_tap_split': [_i32],
     'ewvit_dwt_set_pf': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
@@ -196,6 +197,8 @@ def load():
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
     if os.environ.get('EWVIT_LDS_PAD') == '0' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
+    if os.environ.get('EWVIT_WGWIN_TS') == '0' and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):
+        lib.ewvit_conv2d_set_wgrad_tap_split(0)      # A/B switch (convwin.hip conv_wgrad_win_kernel TS)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
     _lib = lib
