@@ -188,16 +188,34 @@ ENTRY_KERNELS = {
     'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
     'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
                                    'dw_bwd_weight_reduce_kernel'],
-    'ewvit_conv2d_fwd': ['conv_fwd_kernel<false', 'conv_glds_kernel<false'],
-    'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true', 'conv_glds_kernel<true'],
-    'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_glds_kernel', 'conv_wgrad_reduce_kernel'],
+    'ewvit_conv2d_fwd': ['conv_fwd_kernel<false', 'conv_glds_kernel<false', 'conv_win_kernel<false, false, false'],
+    'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true', 'conv_glds_kernel<true', 'conv_win_kernel<true, false, false, false'],
+    'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_glds_kernel', 'conv_wgrad_1x1_kernel',
+                                'conv_wgrad_win_kernel<true, false', 'conv_wgrad_win_kernel<false, false',
+                                'conv_wgrad_reduce_kernel'],
+    # the windowed MWT convs (csrc/convwin.hip): the input-gradient kernels with the BatchNorm
+    # backward sums in their epilogue, the forward / weight gradient with the folded input
+    # transform (XF); template arguments <DGRAD, STATS, XF, BST, KS> / <BIAS, XF, TS>.  The
+    # weight-gradient slabs' reduce pass is counted under ewvit_conv2d_bwd_weight only
+    'ewvit_conv2d_bwd_data_bn_win': ['conv_win_kernel<true, false, false, true'],
+    'ewvit_conv2d_fwd_bn': ['conv_win_kernel<false, true, false'],
+    'ewvit_conv2d_fwd_bn_xf': ['conv_win_kernel<false, true, true'],
+    'ewvit_conv2d_bwd_weight_xf': ['conv_wgrad_win_kernel<true, true', 'conv_wgrad_win_kernel<false, true'],
     'ewvit_bn_fwd': ['bn_stats_kernel', 'bn_apply_kernel'],
     'ewvit_bn_bwd': ['bn_bwd_reduce_kernel', 'bn_bwd_dx_kernel'],
     'ewvit_se_reduce': ['se_reduce_kernel', 'se_fold_kernel'],
     'ewvit_se_scale': ['se_scale_kernel'],
     'ewvit_scale_add': ['scale_add_kernel'],
 }
-MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_gemm_fp8', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data', 'ewvit_conv2d_bwd_weight')
+MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_gemm_fp8', 'ewvit_gemm_tallk', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data',
+                'ewvit_conv2d_bwd_weight')
+NON_MFMA_CONV = ('ewvit_conv2d_pack_weights', 'ewvit_conv2d_stem_fwd')   # VALU / copy entry points
+
+
+def is_mfma(name):
+    """Entry points whose work is MFMA GEMM: the GEMMs and every implicit-GEMM conv variant
+    (_bn / _xf / _win / _add forms of fwd, bwd_data, bwd_weight)."""
+    return name in MFMA_ENTRIES or (name.startswith('ewvit_conv2d_') and name not in NON_MFMA_CONV)
 def pmc_file(config):
     return os.path.join(REPO, 'profiles', 'pmc_latest.json' if config in (2, 3) else f'pmc_latest_c{config}.json')
 
@@ -235,9 +253,14 @@ def pmc_traffic(entry, per_step, config=2, adam_per_step=None):
     return round(tot / (per_step * steps), 1)
 
 
+def _mwt_cap():
+    from network import dama
+    return dama._mwt_grid_cap()
+
+
 def roofline_for(name, row, config=2, adam_per_step=None):
     traffic = pmc_traffic(name, row.get('per_step'), config, adam_per_step)
-    if name in MFMA_ENTRIES:
+    if is_mfma(name):
         ach = row['TFLOP/s']
         peak = FP8_PEAK_TFS if name == 'ewvit_gemm_fp8' else BF16_PEAK_TFS
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak,
@@ -422,8 +445,9 @@ def main():
         aps = opt.launches_per_step() if hasattr(opt, 'launches_per_step') else None
         res['roofline'] = roofline_for(*dom, config=args.config, adam_per_step=aps) if dom else None
         if res['roofline'] is not None:
+            cap = _mwt_cap()
             res['roofline']['timing'] = ('HIP events around every launch of an eager pass of the step as it runs '
-                                         '(MWT on its own stream, its big grids capped at 128 workgroups)')
+                                         f'(MWT on its own stream, its big grids capped at {cap} workgroups)')
         if iso_table and dom and dom[0] in iso_table:
             iso = roofline_for(dom[0], iso_table[dom[0]], config=args.config, adam_per_step=aps)
             iso['timing'] = 'same pass with one stream and uncapped grids (each kernel on the whole chip)'
