@@ -699,16 +699,23 @@ __device__ __forceinline__ int xswz(int p) { return ((p >> 3) & 1) << 1; }
 // TS (tap split): 8 waves, two per SIMD — waves 4..7 repeat waves 0..3's (co half, ci half) roles
 // for taps 5..8 while waves 0..3 take taps 0..4 (80 accumulators instead of 144, every output
 // still owned by one wave: no cross-wave reduction); the DMA pieces are spread over the 8 waves.
-template <bool BIAS, bool XF = false, bool TS = false>
-__global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb,
-                                                                        int nct, int ntile) {
+// NG = 3: 12 waves, three per SIMD, one kernel row kh per wave group (48 accumulators); the DMA
+// pieces strided over the waves (piece wsa + 12 j).
+template <bool BIAS, bool XF = false, int NG = 1>
+__global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, int64_t x_bytes, int nsplit, int ncb,
+                                                                  int nct, int ntile) {
+  constexpr bool TS = NG > 1;
+  constexpr int NW = 4 * NG;                        // waves
   __shared__ __attribute__((aligned(16))) unsigned char smem[GSMEM];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wsa = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7 (TS) | 0..3
-  const int kq = TS ? wsa >> 2 : 0;                 // TS: tap half (0: taps 0-4, 1: taps 5-8)
+  const int wsa = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..NW-1
+  const int kq = TS ? wsa >> 2 : 0;                 // TS: tap group (NG 2: taps 0-4 | 5-8; NG 3: row kq)
   const int ws = TS ? wsa & 3 : wsa;
   const int wr = ws >> 1, wc = ws & 1;              // co half, 16-channel half of the 32-channel block
-  constexpr int PPW = TS ? 4 : 8, XPW = TS ? 2 : 3;  // dy / x DMA pieces per wave
+  constexpr int PPW = NG == 3 ? 3 : TS ? 4 : 8, XPW = NG == 3 ? 1 : TS ? 2 : 3;  // dy / x DMA pieces per wave
+  // piece ids: contiguous per wave (NG 1, 2), strided (NG 3)
+  auto dpiece = [&](int j) { return NG == 3 ? wsa + NW * j : wsa * PPW + j; };
+  auto xpiece = [&](int j) { return NG == 3 ? wsa : wsa * XPW + j; };
   const int r = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int cb = r % ncb, ct = (r / ncb) % nct, split = r / (ncb * nct);
   const int t0 = (int)((int64_t)split * ntile / nsplit), t1 = (int)((int64_t)(split + 1) * ntile / nsplit);
@@ -734,7 +741,8 @@ __global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArg
     const int64_t dpix = ((int64_t)img * H + oh0) * W + ow0;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-      const int P = wsa * PPW + j;
+      const int P = dpiece(j);
+      if (NG == 3 && P >= 32) continue;               // (NG 3: waves 8-11 stage two dy pieces)
       const int sc = (lane & 15) ^ ((dl << 2) | (P & 3));
       const uint32_t off = (uint32_t)(((dpix + (P >> 2) * W + 4 * (P & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
       glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB);
@@ -744,8 +752,8 @@ __global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArg
     asm volatile("" : "+v"(xl));
 #pragma unroll
     for (int j = 0; j < XPW; ++j) {
-      if (TS && wsa * XPW + j >= GX_PIECES) continue;   // (TS: waves 6, 7 stage no window piece)
-      const int q = wsa * XPW + j;
+      if (TS && xpiece(j) >= GX_PIECES) continue;   // (NG 2: waves 6, 7 stage no window piece)
+      const int q = xpiece(j);
       const int p = q * 16 + xl;
       const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;       // p / 18, p % 18
       const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
@@ -774,8 +782,8 @@ __global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArg
     asm volatile("" : "+v"(xl));
 #pragma unroll
     for (int j = 0; j < XPW; ++j) {
-      if (TS && wsa * XPW + j >= GX_PIECES) continue;
-      const int q = wsa * XPW + j;
+      if (TS && xpiece(j) >= GX_PIECES) continue;
+      const int q = xpiece(j);
       const int p = q * 16 + xl;
       const int xr = (p * 3641) >> 16, xc = p - xr * GX_W;
       const int ih = oh0 - 1 + xr, iw = ow0 - 1 + xc;
@@ -835,7 +843,7 @@ __global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArg
   // of the loop per half so each keeps its accumulators in fixed registers)
   auto run = [&](auto KQ) __attribute__((always_inline)) {
     constexpr int kqc = decltype(KQ)::value;
-    constexpr int TB = 5 * kqc, NT = TS ? (kqc ? 4 : 5) : 9;
+    constexpr int TB = NG == 3 ? 3 * kqc : 5 * kqc, NT = NG == 3 ? 3 : TS ? (kqc ? 4 : 5) : 9;
     const bool bias_w = do_bias && kqc == 0;
     cf32x4 acc[4][NT];
 #pragma unroll
@@ -918,7 +926,11 @@ __global__ __launch_bounds__(TS ? 512 : 256) void conv_wgrad_win_kernel(WgradArg
         for (int rr = 0; rr < 4; ++rr)
           a.dbias_part[(int64_t)split * Cout + ct * 128 + wr * 64 + wc * 32 + h * 16 + 4 * g + rr] = bacc[h][rr];
   };
-  if constexpr (TS) {
+  if constexpr (NG == 3) {
+    if (kq == 0) run(ic_t<0>{});
+    else if (kq == 1) run(ic_t<1>{});
+    else run(ic_t<2>{});
+  } else if constexpr (TS) {
     if (kq == 0) run(ic_t<0>{});
     else run(ic_t<1>{});
   } else {
@@ -945,14 +957,15 @@ int wgrad_win_splits(const WgradArgs &a, int64_t x_bytes) {
 
 // the tap-split 8-wave variant (default): two waves per SIMD hide each other's LDS fragment
 // reads behind MFMAs — config 4 1513 -> 1592 frames/s, config 2 3621 -> 3627 (same box,
-// profiles/r05/ab/wgrad_tap_split.log); 0 (EWVIT_WGWIN_TS=0): the 4-wave kernel
+// profiles/r05/ab/wgrad_tap_split.log); 0 (EWVIT_WGWIN_TS=0): the 4-wave kernel; 2: 12 waves,
+// one kernel row per wave group
 int g_wgwin_ts = 1;
 
-template <bool BIAS, bool XF, bool TS>
+template <bool BIAS, bool XF, int NG>
 static void launch_wgrad_win_t(const WgradArgs &a, int64_t x_bytes, int splits, int ncb, int nct, int ntile, hipStream_t s) {
   const unsigned nwg = (unsigned)(splits * ncb * nct);
-  hipLaunchKernelGGL((conv_wgrad_win_kernel<BIAS, XF, TS>), dim3(nwg), dim3(TS ? 512 : 256),
-                     lds_pad(conv_wgrad_win_kernel<BIAS, XF, TS>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<BIAS, XF, NG>), dim3(nwg), dim3(NG * 256),
+                     lds_pad(conv_wgrad_win_kernel<BIAS, XF, NG>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
 }
 
 bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream_t s) {
@@ -960,14 +973,15 @@ bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const bool b = a.dbias_part != nullptr, x = a.xf != nullptr;
   auto go = [&](auto TSc) {
-    constexpr bool T = decltype(TSc)::value != 0;
+    constexpr int T = decltype(TSc)::value;
     if (x && b) launch_wgrad_win_t<true, true, T>(a, x_bytes, splits, ncb, nct, ntile, s);
     else if (x) launch_wgrad_win_t<false, true, T>(a, x_bytes, splits, ncb, nct, ntile, s);
     else if (b) launch_wgrad_win_t<true, false, T>(a, x_bytes, splits, ncb, nct, ntile, s);
     else launch_wgrad_win_t<false, false, T>(a, x_bytes, splits, ncb, nct, ntile, s);
   };
-  if (g_wgwin_ts) go(ic_t<1>{});
-  else go(ic_t<0>{});
+  if (g_wgwin_ts == 2) go(ic_t<3>{});
+  else if (g_wgwin_ts) go(ic_t<2>{});
+  else go(ic_t<1>{});
   return true;
 }
 
@@ -1004,7 +1018,7 @@ bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) 
 
 extern "C" int ewvit_conv2d_set_wgrad_tap_split(int on) {
   const int prev = ewvit::g_wgwin_ts;
-  ewvit::g_wgwin_ts = on ? 1 : 0;
+  ewvit::g_wgwin_ts = on == 2 ? 2 : on ? 1 : 0;
   return prev;
 }
 

@@ -197,8 +197,8 @@ def load():
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
     if os.environ.get('EWVIT_LDS_PAD') == '0' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
-    if os.environ.get('EWVIT_WGWIN_TS') == '0' and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):
-        lib.ewvit_conv2d_set_wgrad_tap_split(0)      # A/B switch (convwin.hip conv_wgrad_win_kernel TS)
+    if os.environ.get('EWVIT_WGWIN_TS') in ('0', '2') and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):
+        lib.ewvit_conv2d_set_wgrad_tap_split(int(os.environ['EWVIT_WGWIN_TS']))   # A/B (convwin.hip wgrad NG)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
     _lib = lib

@@ -390,8 +390,9 @@ int ewvit_conv2d_set_win(int variant);
  * another stream on a CU they hold; the default), 0 = their own footprint.  Returns the previous. */
 int ewvit_conv2d_set_lds_pad(int on);
 /* The windowed 3x3 weight gradient's tap-split 8-wave variant (two waves per SIMD, taps 0-4 and
- * 5-8 on separate waves; 1 on, the default, 0 the 4-wave kernel); returns the previous setting.
- * Results are bit-identical either way (same per-output MFMA chain).  Env: EWVIT_WGWIN_TS=0. */
+ * 5-8 on separate waves; 1 on, the default, 0 the 4-wave kernel, 2 a 12-wave form with one kernel
+ * row per wave group); returns the previous setting.  Results are bit-identical in every form
+ * (same per-output MFMA chain).  Env: EWVIT_WGWIN_TS=0 / 2. */
 int ewvit_conv2d_set_wgrad_tap_split(int on);
 /* A/B: level-1 pixels per thread in flight in ewvit_dwt_hf_upsample_fused (2, the default, or 4); returns the previous. */
 int ewvit_dwt_set_pf(int pf);

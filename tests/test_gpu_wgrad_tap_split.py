@@ -3,7 +3,8 @@ conv_wgrad_win_kernel<.., TS = true>, ewvit_conv2d_set_wgrad_tap_split): waves 0
 waves 4-7 taps 5-8 of the same (co half, ci half) blocks, so every dW entry is the same MFMA chain
 over the same pixel tiles as the 4-wave kernel — dW and the bias gradient must be BIT-IDENTICAL
 to it, with and without the input transform (XF), under a grid cap (persistent walk), and against
-torch float64 of the same bf16 operands (the MWT conv shapes of reference network/mwt.py:60-72)."""
+torch float64 of the same bf16 operands (the MWT conv shapes of reference network/mwt.py:60-72).
+Setting 2 (12 waves, one kernel row per wave group, strided DMA pieces) is held to the same bar."""
 import pytest
 import torch
 
@@ -33,7 +34,7 @@ def test_tap_split_bit_identical(N, C, H, W, Cout, levels, xf, bias, cap):
     prev_cap = lib.ewvit_set_grid_cap(cap)
     out = {}
     try:
-        for ts in (0, 1):
+        for ts in (0, 1, 2):
             prev = lib.ewvit_conv2d_set_wgrad_tap_split(ts)
             try:
                 dw = torch.full((Cout, Cx, 3, 3), float('nan'), device=DEV)
@@ -53,9 +54,10 @@ def test_tap_split_bit_identical(N, C, H, W, Cout, levels, xf, bias, cap):
                 lib.ewvit_conv2d_set_wgrad_tap_split(prev)
     finally:
         lib.ewvit_set_grid_cap(prev_cap)
-    assert torch.equal(out[0][0], out[1][0]), 'dW'
-    if bias:
-        assert torch.equal(out[0][1], out[1][1]), 'db'
+    for ts in (1, 2):
+        assert torch.equal(out[0][0], out[ts][0]), ('dW', ts)
+        if bias:
+            assert torch.equal(out[0][1], out[ts][1]), ('db', ts)
     # torch (float64) of the same operands (the transform applied in float64, bf16-rounded as the kernel's staging)
     zl = z.double().view(levels, N, C, H, W)
     if xf:
