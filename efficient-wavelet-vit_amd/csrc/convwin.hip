@@ -717,7 +717,9 @@ __global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, i
   auto dpiece = [&](int j) { return NG == 3 ? wsa + NW * j : wsa * PPW + j; };
   auto xpiece = [&](int j) { return NG == 3 ? wsa : wsa * XPW + j; };
   const int r = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-  const int cb = r % ncb, ct = (r / ncb) % nct, split = r / (ncb * nct);
+  // co tile fastest: the nct workgroups sharing a (ci block, split) window stream sit on one XCD
+  // (consecutive remapped ids), so x is fetched into one L2 only
+  const int ct = r % nct, cb = (r / nct) % ncb, split = r / (ncb * nct);
   const int t0 = (int)((int64_t)split * ntile / nsplit), t1 = (int)((int64_t)(split + 1) * ntile / nsplit);
   const int H = a.g.H, W = a.g.W, Cout = a.g.Cout, Cin = a.g.Cin;
   const int tpr = W / GT_C, tpi = (H / GT_R) * tpr;
