@@ -263,14 +263,27 @@ def roofline_for(name, row, config=2, adam_per_step=None):
     if is_mfma(name):
         ach = row['TFLOP/s']
         peak = FP8_PEAK_TFS if name == 'ewvit_gemm_fp8' else BF16_PEAK_TFS
+        # traffic / the bytes the kernels must move (every tensor they read or write once,
+        # including the BatchNorm inputs their epilogues and operand transforms read)
+        ratio = round(traffic / row['bytes_per_launch'], 4) if traffic and row.get('bytes_per_launch') else None
         return {'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak,
                 'unit': 'TFLOP/s', 'frac': round(ach / peak, 5), 'traffic': traffic,
                 'avg_us': round(row['avg_us'], 3), 'work_per_launch': row['flops_per_launch'],
-                'algorithmic_bytes_per_launch': row['bytes_per_launch']}
+                'algorithmic_bytes_per_launch': row['bytes_per_launch'], 'traffic_ratio': ratio}
     ach = row['GB/s']
     return {'kernel': name, 'bound': 'hbm', 'achieved': round(ach, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(ach / HBM_PEAK_GBS, 5), 'traffic': traffic, 'avg_us': round(row['avg_us'], 3),
             'work_per_launch': row['bytes_per_launch']}
+
+
+def mfma_util(table, ms_per_step):
+    """Step-level MFMA utilisation: the algorithmic GEMM / conv flops of one step (every MFMA
+    entry point's launches of the eager pass, per step) over the timed step, against the dense
+    bf16 peak (config 2: ~4.32 TFLOP per 64-frame step)."""
+    fl = sum(r['flops_per_launch'] * r['per_step'] for n, r in table.items() if is_mfma(n))
+    ach = fl / (ms_per_step * 1e-3) / 1e12
+    return {'flops_per_step': fl, 'achieved': round(ach, 2), 'peak': BF16_PEAK_TFS, 'unit': 'TFLOP/s',
+            'frac': round(ach / BF16_PEAK_TFS, 5)}
 
 
 def cpu_baseline(steps, config=2):
@@ -441,6 +454,8 @@ def main():
                'data': 'synthetic N(0,1) frames, random-init weights (no datasets/checkpoints offline)',
                'config': workload(args, world, step)}
         dom = max(table.items(), key=lambda kv: kv[1]['total_ms']) if table else None
+        if table:
+            res['mfma_util'] = mfma_util(table, res['ms_per_step'])
         opt = getattr(step, 'opt', None)
         aps = opt.launches_per_step() if hasattr(opt, 'launches_per_step') else None
         res['roofline'] = roofline_for(*dom, config=args.config, adam_per_step=aps) if dom else None

@@ -2122,12 +2122,18 @@ static int64_t w1x1_splits(const ConvGeom &g) {
   if (s > cap) s = cap;
   return s < 1 ? 1 : s;
 }
+// min_ktiles < 1 / ring not 2 or 3 keep the current value (so a caller can move the workgroup
+// target alone and restore it without knowing the other two knobs)
 extern "C" int ewvit_conv2d_set_wgrad_1x1(int target_wg, int min_ktiles, int ring) {
   const int prev = g_w1_wg;
   g_w1_wg = target_wg;
-  g_w1_minkt = min_ktiles >= 1 ? min_ktiles : 4;
-  g_w1_ring = ring == 2 ? 2 : 3;
+  if (min_ktiles >= 1) g_w1_minkt = min_ktiles;
+  if (ring == 2 || ring == 3) g_w1_ring = ring;
   return prev;
+}
+// the three knobs: 0 workgroup target, 1 min K-tiles, 2 ring slots
+extern "C" int ewvit_conv2d_wgrad_1x1_config(int which) {
+  return which == 0 ? g_w1_wg : which == 1 ? g_w1_minkt : g_w1_ring;
 }
 
 extern "C" int ewvit_conv2d_set_wgrad_wide(int variant) {

@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # EWVIT_LIB: another build of the library (A/B measurements of two kernel versions)
 LIB_PATH = os.environ.get('EWVIT_LIB') or os.path.join(_HERE, 'libewvit.so')
-ABI_VERSION = 2
+ABI_VERSION = 3
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
 PACK_MAX = 32          # EWVIT_PACK_MAX
@@ -159,6 +159,7 @@ QUERIES = {
     'ewvit_head_pack_bytes': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_wall_clock_khz': (_i32, []),
+    'ewvit_conv2d_wgrad_1x1_config': (_i32, [_i32]),
 }
 
 _lib = None

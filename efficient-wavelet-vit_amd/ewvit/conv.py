@@ -283,6 +283,10 @@ class Conv2dFn(torch.autograd.Function):
             work = {'flops': 2.0 * N * Ho * Wo * Cin * k * k * Cout, 'bytes': (dyc.numel() + dx.numel() + wpt.numel()) * 2}
             lw = _bn_link_win(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
             lk = None if lw is not None else _bn_link_plan(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip)
+            if lw is not None or lk is not None:
+                # the backward-statistics epilogue also reads the BatchNorm's input (and the skip
+                # gradient it adds): algorithmic bytes the kernel cannot avoid
+                work['bytes'] += bl.x.numel() * bl.x.element_size() + (skip.numel() * 2 if skip is not None else 0)
             if lw is not None:
                 # the windowed input gradient with the producing BatchNorm's per-block sums
                 grows, rows = lw
@@ -489,6 +493,7 @@ class BnReluConvFn(torch.autograd.Function):
         rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs, 0)) if _BN_BWD_EPI else 0
         bpart = None
         if rows > 0:
+            work['bytes'] += zc.numel() * 2        # the BST epilogue reads the BatchNorm input z
             bpart = torch.empty(levels * rows, 2 * C, dtype=torch.float32, device=dev)
             L.call('ewvit_conv2d_bwd_data_bn_win', L.ptr(dyc), L.ptr(wpt), L.ptr(da), N, H, W, Cx, Cout, C, gs,
                    L.ptr(zc), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 1, 0, L.ptr(bpart), L.stream(da),

@@ -49,15 +49,13 @@ def _branch_streams():
     return os.environ.get('EWVIT_BRANCH_STREAMS', '1') == '1'
 
 
-MWT_GRID_CAP = 96           # one process per GPU, nothing else on the chip (world 1)
-MWT_CU_SHARE = 128          # the half of the chip the MWT may take; RCCL's reserve comes off it
-RCCL_CU_RESERVE = 16        # CUs left to RCCL's all-reduce kernels per rank when world > 1
+MWT_GRID_CAP = 96           # measured at world 1; the same at world > 1 (see _mwt_grid_cap)
 
 
 def _mwt_grid_cap(world=None):
     """Workgroups per big-grid MWT launch (LDS-DMA convs, BatchNorm passes) while the MWT
     shares the GPU with the backbone (EWVIT_MWT_GRID_CAP, 0 = uncapped): the MWT walks its
-    tiles / rows on 128 of the 256 CUs (16 per XCD) and the backbone's latency-bound kernels
+    tiles / rows on 96 of the 256 CUs (12 per XCD) and the backbone's latency-bound kernels
     keep the rest.  With the tap-split windowed weight gradient (8 waves per workgroup) the MWT
     keeps pace on fewer CUs (config 2, same box, 2 rounds each, profiles/r05/ab/cap_sweep_ts.log):
     80 3502-3508, **96 3645-3654**, 104 3603-3606, 112 3604-3608, 128 3614-3621, 160 3539-3545
@@ -65,23 +63,20 @@ def _mwt_grid_cap(world=None):
     2750, 96 3546, 112 3541, 120 3572, 128 3573-3586, 136 3507, 160 3519, 192 3464 (round 4's
     kernels: 160 best, 2952 against 2919 at 144).
 
-    This is the knob of the CU budget in data parallel (reference train.py:249-251 on N
-    GPUs): the bucket all-reduces' RCCL kernels run during the backward beside both branches
-    and need CUs of their own, so with world > 1 the MWT takes at most MWT_CU_SHARE -
-    RCCL_CU_RESERVE (EWVIT_RCCL_CU_RESERVE) workgroups: 112 by default, above the world-1 cap of
-    96, which already leaves the backbone and RCCL 160 CUs (round 5's first 112 at world > 1 left
-    144).  The world-1 value is measured; the reserve is not (no multi-GPU node was available to
-    sweep it) — set EWVIT_MWT_GRID_CAP to override both."""
+    Data parallel (reference train.py:249-251 on N GPUs) uses the SAME cap: the bucket
+    all-reduces' RCCL kernels (one workgroup per RCCL channel) run during the backward on the
+    160 CUs the cap leaves outside the MWT, beside the backbone's backward, whose 7^2-28^2
+    launches fill 50-800 workgroups and leave CU slots between them.  Taking a
+    reserve off the MWT instead would only move the MWT off its measured balance point (cap 80:
+    -4 % at world 1).  No multi-GPU node was available to sweep the world > 1 budget, so the
+    argument is kept for that sweep: EWVIT_MWT_GRID_CAP overrides the cap at every world size."""
     env = os.environ.get('EWVIT_MWT_GRID_CAP')
     if env is not None:
         return int(env)
     if world is None:
         import torch.distributed as dist
         world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-    if world <= 1:
-        return MWT_GRID_CAP
-    reserve = int(os.environ.get('EWVIT_RCCL_CU_RESERVE', str(RCCL_CU_RESERVE)))
-    return max(64, min(MWT_GRID_CAP, MWT_CU_SHARE - reserve))
+    return MWT_GRID_CAP
 
 
 class CrossAttention(nn.Module):                                           # dama.py:15-53

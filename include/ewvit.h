@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EWVIT_ABI_VERSION 2
+#define EWVIT_ABI_VERSION 3
 #define EWVIT_F32 0
 #define EWVIT_BF16 1
 #define EWVIT_EINVAL 1000
@@ -403,8 +403,12 @@ int ewvit_dwt_set_pf(int pf);
 int ewvit_conv2d_set_wgrad_wide(int variant);
 /* The 1x1 stride-1 weight-gradient kernel (plain NHWC x, no bias gradient): workgroup target of
  * its pixel splits (0 = never: the generic kernel), fewest 64-pixel K-tiles per split, LDS ring
- * depth (2 | 3).  Test / tuning switch; returns the previous target. */
+ * depth (2 | 3).  Test / tuning switch; returns the previous target.  min_ktiles < 1 and a ring
+ * other than 2 / 3 keep the current value. */
 int ewvit_conv2d_set_wgrad_1x1(int target_wg, int min_ktiles, int ring);
+/* The current 1x1 weight-gradient knobs: which = 0 workgroup target, 1 min K-tiles, 2 ring
+ * (defaults 256, 8, 2).  Replaces nothing in the reference. */
+int ewvit_conv2d_wgrad_1x1_config(int which);
 /* LDS-DMA fwd / dgrad on grids of < 128 row tiles: 64-row (and 64-column) tiles, 1 (default),
  * or the 128-row tiles everywhere, 0 (test switch).  Returns the previous setting. */
 int ewvit_conv2d_set_small_tiles(int on);

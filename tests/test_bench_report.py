@@ -57,3 +57,35 @@ def test_pmc_patterns_cover_windowed_kernels():
     for k in syms:
         owners = [e for e, pats in bench.ENTRY_KERNELS.items() if any(p in k for p in pats)]
         assert len(owners) == 1, (k, owners)
+
+
+def test_dominant_dgrad_traffic_ratio_matches_hand_count():
+    """The line's traffic / algorithmic-bytes ratio for the windowed input gradient with the
+    BatchNorm-backward sums (ewvit_conv2d_bwd_data_bn_win, 2 launches per config-2 step),
+    recomputed by hand from the shapes: the multiscale dgrad reads dy [64, 112^2, 128] and the
+    BN input z [3 x 64, 112^2, 128], writes dx [3 x 64, 112^2, 128]; the k-split fusion dgrad
+    reads dy [192, 112^2, 128] and the seperate BN's input [192, 112^2, 64], writes dx [192,
+    112^2, 64] (bf16; the packed weights < 1 MB).  Against the committed PMC pass the ratio is
+    ~1.06 (multiscale 1.11, fusion 1.01): the windows' halos, not a missing tensor."""
+    import json
+    import bench
+    px = 64 * 112 * 112
+    ms = (px * 128 + 3 * px * 128 + 3 * px * 128) * 2 + 128 * 384 * 9 * 2
+    fu = (3 * px * 128 + 3 * px * 64 + 3 * px * 64) * 2 + 64 * 128 * 9 * 2
+    hand = (ms + fu) / 2
+    data = json.load(open(bench.pmc_file(2)))
+    adam = {k: v for k, v in data.items() if 'adam_table_kernel' in k}
+    row = dict(_row(300.0, 0.0), per_step=2.0, bytes_per_launch=hand)
+    r = bench.roofline_for('ewvit_conv2d_bwd_data_bn_win', row, config=2,
+                           adam_per_step={'adam_table_kernel': 1} if adam else None)
+    assert r['traffic'] is not None
+    assert r['traffic_ratio'] == round(r['traffic'] / hand, 4)
+    assert 0.95 <= r['traffic_ratio'] <= 1.2, r['traffic_ratio']
+
+
+def test_mfma_util_counts_mfma_entries_only():
+    import bench
+    table = {'ewvit_conv2d_fwd': dict(_row(0, 0), flops_per_launch=1e12, per_step=2.0),
+             'ewvit_bn_bwd': dict(_row(0, 0), flops_per_launch=5e12, per_step=1.0)}
+    u = bench.mfma_util(table, 1.0)          # 2 TFLOP in 1 ms = 2000 TFLOP/s
+    assert u['flops_per_step'] == 2e12 and abs(u['achieved'] - 2000.0) < 1e-6 and abs(u['frac'] - 0.8) < 1e-9

@@ -158,13 +158,15 @@ def test_bn_coef_matches_apply_pass():
         assert torch.equal(u, v), n
 
 
-@pytest.mark.parametrize('hw,frames', [(224, 2)])
+@pytest.mark.parametrize('hw,frames', [(224, 2), (224, 32)])
 def test_mwt_fold_bwd_sums_in_dgrad_epilogue(hw, frames, monkeypatch):
     """The fold with the fusion BN's backward sums taken by multiscale_fusion's windowed input-
     gradient epilogue (ewvit_conv2d_bwd_data_bn_win + ewvit_bn_bwd_partials) against its own
     reduction pass (ewvit_bn_bwd): forward and BN state identical; gradients equal up to the fp32
-    summation order of those sums (cosine >= 0.99999, norms within 1e-4; the gradients of biases
-    feeding a train-mode BN are exact zeros up to rounding noise and are skipped)."""
+    summation order of those sums (cosine >= 0.99999, norms within 1e-4, and element-wise
+    max |d| <= 2^-7 max |ref| — 32 frames: the model's 3 x 32 x 112^2 level maps, the default
+    path of the config-2 step; the gradients of biases feeding a train-mode BN are exact zeros
+    up to rounding noise and are skipped)."""
     import ewvit
     from network import mwt as M
     torch.manual_seed(12)
@@ -196,7 +198,8 @@ def test_mwt_fold_bwd_sums_in_dgrad_epilogue(hw, frames, monkeypatch):
         u, v = p.grad.double().flatten(), q.grad.double().flatten()
         c = float(u @ v / (u.norm() * v.norm() + 1e-300))
         r = float(u.norm() / (v.norm() + 1e-300))
-        assert c >= 0.99999 and abs(r - 1) <= 1e-4, (n, c, r)
+        e = float((u - v).abs().max() / (v.abs().max() + 1e-300))
+        assert c >= 0.99999 and abs(r - 1) <= 1e-4 and e <= 2 ** -7, (n, c, r, e)
 
 
 @pytest.mark.parametrize('C,Cout', [(128, 128), (128, 256)])

@@ -45,14 +45,17 @@ def test_wgrad_1x1(N, Cin, H, W, Cout):
     # transposed view (s_ci = Cout) that cannot take the direct store
     dwt = torch.full((Cin, Cout, 1, 1), float('nan'), device=DEV).permute(1, 0, 2, 3)
     _wgrad(lib, L, x, dy, dwt, ws, N, H, W, Cin, Cout)
-    prev = lib.ewvit_conv2d_set_wgrad_1x1(0, 4, 3)
+    # the shipped knobs (conv.hip g_w1_*) are what the kernel above ran with, on every shape
+    assert [lib.ewvit_conv2d_wgrad_1x1_config(i) for i in range(3)] == [256, 8, 2]
+    prev = lib.ewvit_conv2d_set_wgrad_1x1(0, 0, 0)       # generic kernel; the other knobs kept
     try:
         ws2 = torch.empty(int(lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cin, Cout, 1, 1)) // 4 + 64, device=DEV)
         dw_gen = torch.empty((Cout, Cin, 1, 1), device=DEV)
         _wgrad(lib, L, x, dy, dw_gen, ws2, N, H, W, Cin, Cout)
         torch.cuda.synchronize()
     finally:
-        lib.ewvit_conv2d_set_wgrad_1x1(prev, 4, 3)
+        lib.ewvit_conv2d_set_wgrad_1x1(prev, 0, 0)
+    assert [lib.ewvit_conv2d_wgrad_1x1_config(i) for i in range(3)] == [256, 8, 2]
     ref = dy.double().permute(1, 0, 2, 3).reshape(Cout, -1) @ x.double().permute(0, 2, 3, 1).reshape(-1, Cin)
     ref = ref.float().reshape(Cout, Cin, 1, 1)
     scale = float(ref.abs().max())

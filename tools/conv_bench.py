@@ -123,7 +123,7 @@ def main():
             for t in (w1 or [(256, 4, 3)]):
                 lib.ewvit_conv2d_set_wgrad_1x1(*t)
                 wsb = max(wsb, lib.ewvit_conv2d_bwd_weight_workspace(N, H, W, Cx, Cout, k, s))
-        lib.ewvit_conv2d_set_wgrad_1x1(256, 4, 3)
+        lib.ewvit_conv2d_set_wgrad_1x1(256, 8, 2)
         lib.ewvit_conv2d_set_wgrad_wide(4)
         ws = torch.empty(wsb // 4, device=dev)
 
@@ -176,7 +176,7 @@ def main():
         lib.ewvit_conv2d_set_wgrad_wide(4)
         if a.ww is not None:
             lib.ewvit_conv2d_set_ww(0)
-        lib.ewvit_conv2d_set_wgrad_1x1(256, 4, 3)
+        lib.ewvit_conv2d_set_wgrad_1x1(256, 8, 2)
         lib.ewvit_conv2d_set_small_tiles(1)
         for v in a.variants:
             parts = []
