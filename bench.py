@@ -184,6 +184,7 @@ ENTRY_KERNELS = {
     'ewvit_hf_upsample': ['hf_upsample_kernel'],
     'ewvit_dwt_hf_upsample_fused': ['dwt_hf_fused_kernel'],
     'ewvit_gemm': ['gemm_kernel', 'splitk_reduce_kernel'],
+    'ewvit_gemm_mx8': ['gemm_mx8_kernel'],
     'ewvit_dwconv3x3_fwd': ['dw_row_bf16_kernel<1, false>', 'dw_row_bf16_kernel<2, false>', 'dw_fwd_kernel'],
     'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
     'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
@@ -207,9 +208,11 @@ ENTRY_KERNELS = {
     'ewvit_se_scale': ['se_scale_kernel'],
     'ewvit_scale_add': ['scale_add_kernel'],
 }
-MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_gemm_fp8', 'ewvit_gemm_tallk', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data',
+MFMA_ENTRIES = ('ewvit_gemm', 'ewvit_gemm_mx8', 'ewvit_gemm_tallk', 'ewvit_conv2d_fwd', 'ewvit_conv2d_bwd_data',
                 'ewvit_conv2d_bwd_weight')
 NON_MFMA_CONV = ('ewvit_conv2d_pack_weights', 'ewvit_conv2d_stem_fwd')   # VALU / copy entry points
+# MXFP8 entry points (v_mfma_scale_f32_16x16x128_f8f6f4 runs at the fp8 rate, MI355X_MICROARCH.md)
+FP8_ENTRIES = ('ewvit_gemm_mx8',)
 
 
 def is_mfma(name):
@@ -262,7 +265,7 @@ def roofline_for(name, row, config=2, adam_per_step=None):
     traffic = pmc_traffic(name, row.get('per_step'), config, adam_per_step)
     if is_mfma(name):
         ach = row['TFLOP/s']
-        peak = FP8_PEAK_TFS if name == 'ewvit_gemm_fp8' else BF16_PEAK_TFS
+        peak = FP8_PEAK_TFS if name in FP8_ENTRIES else BF16_PEAK_TFS
         # traffic / the bytes the kernels must move (every tensor they read or write once,
         # including the BatchNorm inputs their epilogues and operand transforms read)
         ratio = round(traffic / row['bytes_per_launch'], 4) if traffic and row.get('bytes_per_launch') else None
@@ -480,7 +483,7 @@ def main():
         # MFMA utilisation of the token path's GEMMs (ViT attention / MLP projections,
         # patch_to_embedding, classifier: north_star's attention/MLP figure); at config 5 the
         # attention / MLP projections are the fp8 entry point, priced against the fp8 peak
-        tok = 'ewvit_gemm_fp8' if (args.config == 5 and 'ewvit_gemm_fp8' in table) else 'ewvit_gemm'
+        tok = 'ewvit_gemm_mx8' if (args.config == 5 and 'ewvit_gemm_mx8' in table) else 'ewvit_gemm'
         if tok in table:
             tg = roofline_for(tok, table[tok], args.config, aps)
             tg['timing'] = res['roofline']['timing'] if res.get('roofline') else None

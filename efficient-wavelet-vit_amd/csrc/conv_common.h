@@ -42,6 +42,7 @@ struct FwdArgs {
   // the per-tap K padded up to 64 (the weights packed with that many input channels)
   // and the staging lanes of channels >= KCr (the real count) read zeros
   int KCr = 0;
+  int nt = 0;            // windowed fwd / dgrad: non-temporal hint on the window DMAs
   // optional addend of the output (same layout as out, bf16), added before rounding —
   // the skip connection's gradient folded into the block input's dgrad
   const bf16_t *addend = nullptr;
@@ -120,6 +121,27 @@ __device__ __forceinline__ void glds16_asm(ci32x4 r, uint32_t lds, uint32_t voff
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(l), "v"(voff), "s"(rr)
                : "memory", "m0");
 }
+// ... with the non-temporal hint when `nt` (a uniform kernel argument: a scalar branch): the
+// windowed MWT convs' activation windows (A/B, ewvit_conv2d_set_win_nt) — streamed once per
+// tile, so they need not keep their L2 lines against the concurrent backbone's working set
+__device__ __forceinline__ void glds16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff, bool nt) {
+  if (nt)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds" ::"s"(lds), "v"(voff),
+                 "s"(r) : "memory", "m0");
+  else
+    glds16_asm(r, lds, voff);
+}
+__device__ __forceinline__ void glds16_asm(ci32x4 r, uint32_t lds, uint32_t voff, bool nt) {
+  if (nt) {
+    const ci32x4 rr = {__builtin_amdgcn_readfirstlane(r[0]), __builtin_amdgcn_readfirstlane(r[1]),
+                       __builtin_amdgcn_readfirstlane(r[2]), __builtin_amdgcn_readfirstlane(r[3])};
+    const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds" ::"s"(l), "v"(voff),
+                 "s"(rr) : "memory", "m0");
+  } else {
+    glds16_asm(r, lds, voff);
+  }
+}
 #pragma clang diagnostic pop
 
 // ---------------------------------------------------------------- wgrad
@@ -138,6 +160,7 @@ struct WgradArgs {
   int xgc;
   int64_t xgs;
   const float *xf = nullptr;  // input transform of the windowed wgrad (FwdArgs::xf; groups of xgc)
+  int nt = 0;                 // windowed wgrad: non-temporal hint on the dy / x window DMAs
 };
 
 __device__ __forceinline__ int swz_off(int r, int ch) {

@@ -49,6 +49,8 @@ int g_win = 1;
 // 3627 -> 3636-3646 frames/s (same box, profiles/r05/ab/lds_pad.log).  EWVIT_LDS_PAD=0 /
 // ewvit_conv2d_set_lds_pad(0): their own footprint.
 int g_lds_pad = 1;
+// the non-temporal hint on the windowed kernels' activation-window DMAs (A/B; 0 = off)
+int g_win_nt = 0;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
   if (!g_lds_pad || stat >= 160 * 1024) return 0;
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
     const bool ok = d.ok & (p < (uint32_t)WPIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
     const uint32_t off = d.wsrc + __umul24(__umul24(wr, (uint32_t)W) + wc, sgc2) + (uint32_t)wlc16;
     // (slots past the last piece load zeros into the sink, so every wave issues the same count)
-    glds16_asm(rs, q < WPIECES ? lds0 + WIN0 + wb * WIN_B + q * 1024 : lds0 + SINK0, ok ? off : OOB);
+    glds16_asm(rs, q < WPIECES ? lds0 + WIN0 + wb * WIN_B + q * 1024 : lds0 + SINK0, ok ? off : OOB, a.nt != 0);
   };
   // XF: this wave's pieces of unit d's window (buffer wb) -> relu(x * scale + shift), zero
   // outside the image.  The lane's pixel is 8 q + lane / 8 and its chunk (lane & 7) ^ (lane / 8)
@@ -747,7 +749,7 @@ __global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, i
       if (NG == 3 && P >= 32) continue;               // (NG 3: waves 8-11 stage two dy pieces)
       const int sc = (lane & 15) ^ ((dl << 2) | (P & 3));
       const uint32_t off = (uint32_t)(((dpix + (P >> 2) * W + 4 * (P & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
-      glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB);
+      glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB, a.nt != 0);
     }
     const int64_t xpix = ((int64_t)img * H + oh0 - 1) * W + ow0 - 1;
     int xl = lane >> 2;
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, i
       const bool ok = live & (p < GX_PIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
       const int sc = (lane & 3) ^ xswz(p);
       const uint32_t off = (uint32_t)(((xpix + xr * W + xc) * a.xgc + cofs + sc * 8) * 2);
-      glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB);
+      glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB, a.nt != 0);
     }
   };
 
@@ -970,7 +972,9 @@ static void launch_wgrad_win_t(const WgradArgs &a, int64_t x_bytes, int splits, 
                      lds_pad(conv_wgrad_win_kernel<BIAS, XF, NG>, GSMEM), s, a, x_bytes, splits, ncb, nct, ntile);
 }
 
-bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream_t s) {
+bool launch_wgrad_win(const WgradArgs &a_in, int64_t x_bytes, int splits, hipStream_t s) {
+  WgradArgs a = a_in;
+  a.nt = g_win_nt;
   const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const bool b = a.dbias_part != nullptr, x = a.xf != nullptr;
@@ -987,7 +991,9 @@ bool launch_wgrad_win(const WgradArgs &a, int64_t x_bytes, int splits, hipStream
   return true;
 }
 
-bool launch_win(const FwdArgs &a, int64_t src_bytes, bool dgrad, hipStream_t s) {
+bool launch_win(const FwdArgs &a_in, int64_t src_bytes, bool dgrad, hipStream_t s) {
+  FwdArgs a = a_in;
+  a.nt = g_win_nt;
   if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
   const bool ks = win_ks(a, dgrad);
   const int ntn = ks ? 1 : a.Ncol / 128;
@@ -1027,6 +1033,13 @@ extern "C" int ewvit_conv2d_set_wgrad_tap_split(int on) {
 extern "C" int ewvit_conv2d_set_lds_pad(int on) {
   const int prev = ewvit::g_lds_pad;
   ewvit::g_lds_pad = on ? 1 : 0;
+  return prev;
+}
+
+// A/B switch: the non-temporal hint on the windowed MWT convs' activation-window DMAs
+extern "C" int ewvit_conv2d_set_win_nt(int on) {
+  const int prev = ewvit::g_win_nt;
+  ewvit::g_win_nt = on ? 1 : 0;
   return prev;
 }
 

@@ -14,7 +14,12 @@
 // flight while the current one feeds the MFMAs.  Operands may be f32 (converted
 // to bf16 while staging: the fp32 master weights are consumed without a cast
 // kernel) or bf16.
+//
+// gemm_mx8_kernel: the same contract with MXFP8 operands (mx8.h: e4m3 elements, one E8M0
+// scale per 32 consecutive K elements, quantized from the f32 / bf16 operands while staging)
+// on v_mfma_scale_f32_16x16x128_f8f6f4 — BASELINE configs[4]'s fp8 token GEMMs.
 #include "common.h"
+#include "mx8.h"
 
 namespace ewvit {
 
@@ -22,7 +27,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int GBM = 64, GBN = 64, GBK = 32, GPAD = 8, GLD = GBK + GPAD;
-constexpr int GLD8 = GBK + 16;   // fp8 LDS image row: 32 k bytes + 16 pad (48-B rows)
+constexpr int MBK = 128, MLD = MBK + 4;   // MX K-tile and its fp32 LDS image row (floats)
 
 struct GemmArgs {
   const void *A; int64_t lda_m, lda_k;
@@ -40,9 +45,6 @@ struct GemmArgs {
   int c_dtype;
   int64_t kper;  // K per split
   float *ws;     // split-K slabs [splitk][M][N]
-  // fp8 path: per-tensor amax of A and B as partial maxima (ewvit_amax_partials)
-  const float *a_amax; int a_nparts;
-  const float *b_amax; int b_nparts;
 };
 
 // Load 8 consecutive elements (along the contiguous dim) starting at flat
@@ -121,25 +123,14 @@ struct Stager {
       load8<DT, VEC>(p, gr + gk * ld_k, n_ok, v);
     }
   }
-  // fp8 e4m3 (OCP) image: v * scale clamped to +-448 (per-tensor scaling keeps |v*scale| <=
-  // 448 up to rounding), round-to-nearest-even by v_cvt_pk_fp8_f32
-  __device__ __forceinline__ void store_q8(uint8_t (*lds)[GLD8], float scale) {
-    unsigned w[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float a = __builtin_amdgcn_fmed3f(v[4 * h] * scale, 448.f, -448.f);
-      const float b = __builtin_amdgcn_fmed3f(v[4 * h + 1] * scale, 448.f, -448.f);
-      const float c = __builtin_amdgcn_fmed3f(v[4 * h + 2] * scale, 448.f, -448.f);
-      const float d = __builtin_amdgcn_fmed3f(v[4 * h + 3] * scale, 448.f, -448.f);
-      int q = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-      q = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, q, true);
-      w[h] = (unsigned)q;
-    }
+  // fp32 image for the MX kernel's block quantization (no rounding while staging)
+  __device__ __forceinline__ void store_f32(float (*lds)[MLD], int k_off) {
     if (KCONTIG) {
-      *reinterpret_cast<uint2 *>(&lds[r][k]) = make_uint2(w[0], w[1]);
+      *reinterpret_cast<float4 *>(&lds[r][k_off + k]) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4 *>(&lds[r][k_off + k + 4]) = make_float4(v[4], v[5], v[6], v[7]);
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) lds[r + i][k] = (uint8_t)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+      for (int i = 0; i < 8; ++i) lds[r + i][k_off + k] = v[i];
     }
   }
   __device__ __forceinline__ void store(bf16_t (*lds)[GLD]) {
@@ -229,134 +220,106 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       }
 }
 
-// Per-tensor amax: each of `nparts` workgroups reduces a contiguous range of rows of the
-// [rows x cols] (row stride ld) matrix to one partial maximum; consumers fold the partials.
-template <int DT>
-__global__ __launch_bounds__(256) void amax_partial_kernel(const void *x, int64_t rows, int64_t cols, int64_t ld,
-                                                          float *part) {
-  float m = 0.f;
-  if (ld == cols && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-    // dense: the flat range split evenly over the workgroups, 16-B loads
-    constexpr int V = DT == EWVIT_F32 ? 4 : 8;
-    const int64_t nv = rows * cols / V;
-    const int64_t per = (nv + gridDim.x - 1) / gridDim.x;
-    const int64_t v0 = (int64_t)blockIdx.x * per, v1 = v0 + per < nv ? v0 + per : nv;
-    for (int64_t v = v0 + threadIdx.x; v < v1; v += 256) {
-      const uint4 q = reinterpret_cast<const uint4 *>(x)[v];
-      const unsigned w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (DT == EWVIT_F32) {
-          m = fmaxf(m, fabsf(__uint_as_float(w[i])));
-        } else {
-          m = fmaxf(m, fabsf(__uint_as_float(w[i] << 16)));
-          m = fmaxf(m, fabsf(__uint_as_float(w[i] & 0xffff0000u)));
-        }
-      }
-    }
-    if (blockIdx.x == gridDim.x - 1)          // the tail past the last whole vector
-      for (int64_t i = nv * V + threadIdx.x; i < rows * cols; i += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, i)));
-  } else {
-    const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
-    const int64_t r0 = (int64_t)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
-    for (int64_t r = r0; r < r1; ++r)
-      for (int64_t c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(Elem<DT>::load(x, r * ld + c)));
-  }
-  __shared__ float red[4];
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-}
-
-// fold the partial maxima into the e4m3 scale 448 / amax (1 for an all-zero tensor)
-__device__ __forceinline__ float fp8_scale(const float *part, int n, float *red) {
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, part[i]);
-  m = wave_max(m);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  return m > 0.f ? 448.f / m : 1.f;
-}
-
-// The gemm_kernel structure with fp8 e4m3 operands (BASELINE configs[4]): operands staged
-// from f32/bf16 memory, multiplied by their per-tensor scale and rounded to OCP e4m3 into
-// the LDS images, v_mfma_f32_16x16x32_fp8_fp8 (8 fp8 of A and of B per lane, the bf16
-// lane map), fp32 accumulation, the product descaled by 1/(sa*sb) before the epilogue.
+// MXFP8 GEMM: 64 x 64 output tile, 128-wide K-tiles.  Per K-tile: A and B are staged as fp32
+// in LDS (the Stager's 64 x 32 pieces, 4 per tile: any operand layout); then each of the 256
+// threads quantizes one 32-element block of A and one of B (row t / 4, block t % 4) into the
+// e4m3 images (two, alternating per K-tile) with its E8M0 scale — every block once; the 4 waves
+// (2 x 2, 32 x 32 each) read their fragments from the images (two 16-B runs per lane, mx8.h's
+// lane map) and run one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 tile (two barriers per
+// K-tile: the fp32 images are rewritten only after every wave quantized them, the e4m3 images
+// only after every wave passed the next K-tile's first barrier, i.e. finished its MFMAs).  The
+// next K-tile's global loads are in flight during the quantization and the MFMAs.  Rows / K past the matrix
+// are zero.  The MFMA applies both block scales, so the epilogue sees the descaled product.
+constexpr int Q8LD = MBK + 16;          // e4m3 image row (bytes): conflict-free 16-B fragment reads
 template <int ADT, int BDT, bool AK, bool BK, bool AV, bool BV>
-__global__ __launch_bounds__(256) void gemm_fp8_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint8_t As[2][GBM][GLD8];
-  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][GBN][GLD8];
-  __shared__ float red[4];
+__global__ __launch_bounds__(256) void gemm_mx8_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[GBM][MLD];
+  __shared__ __attribute__((aligned(16))) float Bs[GBN][MLD];
+  __shared__ __attribute__((aligned(16))) uint8_t Aq[GBM][Q8LD];
+  __shared__ __attribute__((aligned(16))) uint8_t Bq[GBN][Q8LD];
+  __shared__ uint8_t Asc[GBM][4], Bsc[GBN][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
   const int64_t kbeg = (int64_t)blockIdx.z * g.kper;
   const int64_t kend = (kbeg + g.kper < g.K) ? kbeg + g.kper : g.K;
-  const float sa = fp8_scale(g.a_amax, g.a_nparts, red);
-  const float sb = fp8_scale(g.b_amax, g.b_nparts, red);
-
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  Stager<ADT, AK, AV> st_a;
-  Stager<BDT, BK, BV> st_b;
-  const int nk = (int)((kend - kbeg + GBK - 1) / GBK);
-  if (nk > 0) {
-    st_a.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, kbeg, kend, tid);
-    st_b.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, kbeg, kend, tid);
-    st_a.store_q8(As[0], sa);
-    st_b.store_q8(Bs[0], sb);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int64_t k0 = kbeg + (int64_t)(kt + 1) * GBK;
-      st_a.load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, k0, kend, tid);
-      st_b.load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, k0, kend, tid);
+  Stager<ADT, AK, AV> sa[4];
+  Stager<BDT, BK, BV> sb[4];
+  const int nk = (int)((kend - kbeg + MBK - 1) / MBK);
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      sa[p].load(g.A, AK ? g.lda_m : 0, AK ? 0 : g.lda_k, m0, g.M, k0 + p * GBK, kend, tid);
+      sb[p].load(g.B, BK ? g.ldb_n : 0, BK ? 0 : g.ldb_k, n0, g.N, k0 + p * GBK, kend, tid);
     }
-    long af[2], bfr[2];
-    const int fr = lane & 15, fk = (lane >> 4) * 8;
+  };
+  // one 32-element block of an fp32 image row -> its e4m3 bytes and scale
+  auto quant = [&](const float (*src)[MLD], uint8_t (*dst)[Q8LD], uint8_t (*sc)[4]) {
+    const int row = tid >> 2, blk = tid & 3;
+    float v[32];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const long *>(&As[cur][wm * 32 + i * 16 + fr][fk]);
+    for (int q = 0; q < 8; ++q) {
+      const float4 x = *reinterpret_cast<const float4 *>(&src[row][blk * 32 + 4 * q]);
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+    int d[8];
+    sc[row][blk] = (uint8_t)mx_quant_block(v, d);
+    uint4 *o = reinterpret_cast<uint4 *>(&dst[row][blk * 32]);
+    o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+  };
+  auto frag = [&](const uint8_t (*img)[Q8LD], const uint8_t (*sc)[4], int row) {
+    MxFrag f;
+    const uint4 x = *reinterpret_cast<const uint4 *>(&img[row][mx_k0(lane)]);
+    const uint4 y = *reinterpret_cast<const uint4 *>(&img[row][mx_k1(lane)]);
+    f.d[0] = (int)x.x; f.d[1] = (int)x.y; f.d[2] = (int)x.z; f.d[3] = (int)x.w;
+    f.d[4] = (int)y.x; f.d[5] = (int)y.y; f.d[6] = (int)y.z; f.d[7] = (int)y.w;
+    f.sc = sc[row][lane >> 4];
+    return f;
+  };
+  if (nk > 0) load(kbeg);
+  const int r = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const long *>(&Bs[cur][wn * 32 + j * 16 + fr][fk]);
+    for (int p = 0; p < 4; ++p) {
+      sa[p].store_f32(As, p * GBK);
+      sb[p].store_f32(Bs, p * GBK);
+    }
+    __syncthreads();
+    if (kt + 1 < nk) load(kbeg + (int64_t)(kt + 1) * MBK);
+    quant(As, Aq, Asc);
+    quant(Bs, Bq, Bsc);
+    __syncthreads();
+    MxFrag af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(Aq, Asc, wm * 32 + i * 16 + r);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = frag(Bq, Bsc, wn * 32 + j * 16 + r);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) {
-      st_a.store_q8(As[cur ^ 1], sa);
-      st_b.store_q8(Bs[cur ^ 1], sb);
-    }
-    __syncthreads();
-    cur ^= 1;
+      for (int j = 0; j < 2; ++j) acc[i][j] = mx_mma(af[i], bfr[j], acc[i][j]);
   }
 
-  const float descale = 1.f / (sa * sb);
   const bool split = gridDim.z > 1;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + q;
         const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
         if (row < g.M && col < g.N) {
-          const float v = acc[i][j][r] * descale;
           if (split)
-            g.ws[((int64_t)blockIdx.z * g.M + row) * g.N + col] = v;
+            g.ws[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[i][j][q];
           else
-            store_c(g, row, col, epilogue(g, row, col, v));
+            store_c(g, row, col, epilogue(g, row, col, acc[i][j][q]));
         }
       }
 }
@@ -418,10 +381,10 @@ template <int ADT, int BDT, bool AK, bool BK>
 static void launch_typed(const GemmArgs &g, bool av, bool bv, bool q8, dim3 grid, hipStream_t s) {
   dim3 block(256);
   if (q8) {
-    if (av && bv) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
-    else if (av) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, true, false>), grid, block, 0, s, g);
-    else if (bv) hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, false, true>), grid, block, 0, s, g);
-    else hipLaunchKernelGGL((gemm_fp8_kernel<ADT, BDT, AK, BK, false, false>), grid, block, 0, s, g);
+    if (av && bv) hipLaunchKernelGGL((gemm_mx8_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
+    else if (av) hipLaunchKernelGGL((gemm_mx8_kernel<ADT, BDT, AK, BK, true, false>), grid, block, 0, s, g);
+    else if (bv) hipLaunchKernelGGL((gemm_mx8_kernel<ADT, BDT, AK, BK, false, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((gemm_mx8_kernel<ADT, BDT, AK, BK, false, false>), grid, block, 0, s, g);
     return;
   }
   if (av && bv) hipLaunchKernelGGL((gemm_kernel<ADT, BDT, AK, BK, true, true>), grid, block, 0, s, g);
@@ -456,8 +419,7 @@ static int gemm_impl(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, c
                      int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
                      const float *bias, int act, void *aux, float drop_p, uint64_t seed,
                      const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
-                     float *workspace, const float *a_amax, int a_nparts, const float *b_amax, int b_nparts,
-                     bool q8, void *stream) {
+                     float *workspace, bool q8, void *stream) {
   EWVIT_CHECK_ARG(A && B && C, "gemm: null operand");
   EWVIT_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   EWVIT_CHECK_ARG(dtype_ok(a_dtype) && dtype_ok(b_dtype) && dtype_ok(c_dtype), "gemm: bad dtype");
@@ -479,11 +441,11 @@ static int gemm_impl(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, c
   g.alpha = alpha; g.beta = beta; g.bias = bias; g.act = act; g.aux = aux;
   g.drop_p = drop_p; g.seed = seed; g.seed_off = seed_offset; g.resid = resid; g.resid_dtype = resid_dtype; g.ldr = ldr;
   g.c_dtype = c_dtype; g.ws = workspace;
-  g.a_amax = a_amax; g.a_nparts = a_nparts; g.b_amax = b_amax; g.b_nparts = b_nparts;
-  // K per split, a multiple of the K tile
+  // K per split, a multiple of the K tile (128 for the MX kernel)
+  const int kt = q8 ? MBK : GBK;
   int64_t kper = (K + splitk - 1) / splitk;
-  kper = ((kper + GBK - 1) / GBK) * GBK;
-  if (kper == 0) kper = GBK;
+  kper = ((kper + kt - 1) / kt) * kt;
+  if (kper == 0) kper = kt;
   int sk = (int)((K + kper - 1) / kper);
   if (sk < 1) sk = 1;
   g.kper = kper;
@@ -497,7 +459,7 @@ static int gemm_impl(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, c
   else if (a_dtype == EWVIT_BF16) launch_layout<EWVIT_BF16, EWVIT_F32>(g, ak, bk, av, bv, q8, grid, s);
   else if (b_dtype == EWVIT_BF16) launch_layout<EWVIT_F32, EWVIT_BF16>(g, ak, bk, av, bv, q8, grid, s);
   else launch_layout<EWVIT_F32, EWVIT_F32>(g, ak, bk, av, bv, q8, grid, s);
-  int rc = launch_status(q8 ? "gemm_fp8" : "gemm");
+  int rc = launch_status(q8 ? "gemm_mx8" : "gemm");
   if (rc || sk == 1) return rc;
   const int64_t total = M * N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g, sk);
@@ -511,35 +473,17 @@ extern "C" int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda
                           const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
                           float *workspace, void *stream) {
   return gemm_impl(A, a_dtype, lda_m, lda_k, B, b_dtype, ldb_k, ldb_n, C, c_dtype, ldc, M, N, K, alpha, beta, bias,
-                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, nullptr, 0,
-                   nullptr, 0, false, stream);
+                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, false, stream);
 }
 
-extern "C" int ewvit_gemm_fp8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
+extern "C" int ewvit_gemm_mx8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B,
                               int b_dtype, int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype,
                               int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float beta,
                               const float *bias, int act, void *aux, float drop_p, uint64_t seed,
                               const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr,
-                              int splitk, float *workspace, const float *a_amax, int a_nparts,
-                              const float *b_amax, int b_nparts, void *stream) {
-  EWVIT_CHECK_ARG(a_amax && b_amax && a_nparts >= 1 && b_nparts >= 1 && a_nparts <= EWVIT_AMAX_PARTS &&
-                  b_nparts <= EWVIT_AMAX_PARTS, "gemm_fp8: amax partials (%d, %d)", a_nparts, b_nparts);
+                              int splitk, float *workspace, void *stream) {
   return gemm_impl(A, a_dtype, lda_m, lda_k, B, b_dtype, ldb_k, ldb_n, C, c_dtype, ldc, M, N, K, alpha, beta, bias,
-                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, a_amax, a_nparts,
-                   b_amax, b_nparts, true, stream);
-}
-
-extern "C" int ewvit_amax_partials(const void *x, int dtype, int64_t rows, int64_t cols, int64_t ld, float *part,
-                                   int nparts, void *stream) {
-  EWVIT_CHECK_ARG(x && part && dtype_ok(dtype) && rows >= 0 && cols >= 0, "amax_partials: bad args");
-  EWVIT_CHECK_ARG(nparts >= 1 && nparts <= EWVIT_AMAX_PARTS, "amax_partials: nparts=%d", nparts);
-  if (dtype == EWVIT_F32)
-    hipLaunchKernelGGL(amax_partial_kernel<EWVIT_F32>, dim3(nparts), dim3(256), 0, as_stream(stream), x, rows, cols, ld,
-                       part);
-  else
-    hipLaunchKernelGGL(amax_partial_kernel<EWVIT_BF16>, dim3(nparts), dim3(256), 0, as_stream(stream), x, rows, cols,
-                       ld, part);
-  return launch_status("amax_partials");
+                   act, aux, drop_p, seed, seed_offset, resid, resid_dtype, ldr, splitk, workspace, true, stream);
 }
 
 extern "C" int ewvit_colsum(const void *X, int x_dtype, int64_t ldx, int64_t M, int64_t N,

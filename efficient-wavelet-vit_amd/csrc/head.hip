@@ -31,6 +31,7 @@
 // from the fp32 master weights (rounded in registers) before their MFMAs.  Per-row statistics
 // (LayerNorm, softmax, attention) and every accumulation in fp32.
 #include "common.h"
+#include "mx8.h"
 
 namespace ewvit {
 
@@ -199,12 +200,94 @@ __device__ __forceinline__ void g16_mma(const hbf16x8 (&b)[NU][KS], int ntiles, 
   }
 }
 
+// MXFP8 forms (configs[4]): the attention blocks' weights from the MX pack (one 128-wide K step
+// per MxFrag), the activations block-quantized from their bf16 LDS rows in registers
+// (mx_quant).  Image m of block i: 0 Wq [128][128], 1 Wq^T, 2 Wkv [256][128], 3 Wkv^T [128][256],
+// 4 Wo, 5 Wo^T — each e4m3 [rows][cols] + E8M0 [rows][cols / 32] (blocks along the row, the K of
+// the GEMM that reads it).
+__host__ __device__ inline void hmx_dims(int m, int &rows, int &cols) {
+  rows = m == 2 ? 2 * HD : HD;
+  cols = m == 3 ? 2 * HD : HD;
+}
+__host__ __device__ inline int64_t hmx_img(int m) {
+  int64_t o = 0;
+  for (int j = 0; j < m; ++j) {
+    int r, c;
+    hmx_dims(j, r, c);
+    o += (int64_t)r * c + (int64_t)r * (c / 32);
+  }
+  return o;
+}
+constexpr int64_t HMX_BLK = 4 * HD * HD + 4 * HD * (HD / 32) + 2 * (2 * HD * HD + 2 * HD * (HD / 32));
+struct HMxW {
+  const uint8_t *d, *s;
+  int K;
+  __device__ __forceinline__ MxFrag frag(int row, int kstep) const {
+    return mx_load(d + (int64_t)row * K, kstep, s + (int64_t)row * (K / 32));
+  }
+};
+__device__ __forceinline__ HMxW hmx(const void *pk, int blk, int m) {
+  int r, c;
+  hmx_dims(m, r, c);
+  const uint8_t *b = reinterpret_cast<const uint8_t *>(pk) + blk * HMX_BLK + hmx_img(m);
+  return HMxW{b, b + (int64_t)r * c, c};
+}
+template <int NU, int KS, class NkF, class FragF>
+__device__ __forceinline__ void g16_load_mx(MxFrag (&b)[NU][KS], int ntiles, NkF nk, FragF frag) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int t = w + 8 * u;
+    if (t < ntiles) {
+      const int n = nk(t);
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        if (s < n) b[u][s] = frag(t, s, c);
+    }
+  }
+}
+// A rows 0..15 of the tile from LDS (bf16, pitch ap), block-quantized per 128-wide K step
+template <int NU, int KS, class NkF, class AF, class EpiF>
+__device__ __forceinline__ void g16_mma_mx(const MxFrag (&b)[NU][KS], int ntiles, NkF nk, AF afn, EpiF epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int t = w + 8 * u;
+    if (t >= ntiles) break;
+    const int n = nk(t);
+    const bf16_t *A;
+    int ap;
+    afn(t, A, ap);
+    hf32x4 acc = hf32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      if (s < n) {
+        float v[32];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const hbf16x8 x = *reinterpret_cast<const hbf16x8 *>(A + c * ap + s * 128 + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[hh * 16 + q * 8 + e] = (float)x[e];
+          }
+        acc = mx_mma(mx_quant(v), b[u][s], acc);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) epi(t, (lane >> 4) * 4 + r, c, acc[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 extern __shared__ __attribute__((aligned(16))) unsigned char h_smem[];
 
 // ---------------------------------------------------------------- forward, per frame group
 // A phase issues all of its weight fragments before its MFMAs (one L2 round trip per phase);
 // between them the phases touch LDS only (the small parameter vectors are staged there), so no
 // other global load waits behind the fragments.
+template <bool MX>
 __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const float *s0, const float *f0,
                                                            float *ws_base, float *s_out, float *f_out, int N) {
   int trk = 0;
@@ -230,6 +313,12 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
   };
   auto frag_o = [&](int t, int s, int c, int k0) { return h_ld8(pk + bi * HP_BLK + HP_O + (int64_t)(t * 16 + c) * HD + k0); };
   hbf16x8 bA[5][4], bO[1][4];
+  MxFrag mA[5][1], mO[1][1];
+  auto nk1 = [](int) { return 1; };
+  auto mfrag_qkv = [&](int t, int, int c) {
+    return t < 8 ? hmx(p.packed_mx, bi, 0).frag(t * 16 + c, 0) : hmx(p.packed_mx, bi, 2).frag((t < 24 ? t - 8 : t - 24) * 16 + c, 0);
+  };
+  auto mfrag_o = [&](int t, int, int c) { return hmx(p.packed_mx, bi, 4).frag(t * 16 + c, 0); };
   for (int e = tid; e < 4 * 3 * HD; e += HT) {
     const int i = e / (3 * HD), j = (e / HD) % 3, c = e % HD;
     vec[e] = (j == 0 ? p.ca[i].ln_w : j == 1 ? p.ca[i].ln_b : p.ca[i].bo)[c];
@@ -268,12 +357,7 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
     }
     for (int e = tid; e < FG * HD; e += HT) A2[(e >> 7) * HKP + (e & 127)] = f2bf(ctx[e]);
     bi = i;
-    g16_load(bA, 40, nk4, frag_qkv);
-    h_bar();
-    HTR(trk++);
-    g16_mma(
-        bA, 40, nk4, [&](int t, const bf16_t *&A, int &ap) { A = t < 24 ? A1 : A2; ap = HKP; },
-        [&](int t, int row, int c, float v) {
+    auto epi_qkv = [&](int t, int row, int c, float v) {
           const int64_t n = g0 + row;
           if (t < 8) {
             const int col = t * 16 + c;
@@ -284,7 +368,19 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
             kvs[row * 512 + tok * 256 + col] = v;
             if (row < nr) ws.kv(i)[n * 512 + tok * 256 + col] = v;
           }
-        });
+        };
+    auto afn_qkv = [&](int t, const bf16_t *&A, int &ap) { A = t < 24 ? A1 : A2; ap = HKP; };
+    if constexpr (MX) {
+      g16_load_mx(mA, 40, nk1, mfrag_qkv);
+      h_bar();
+      HTR(trk++);
+      g16_mma_mx(mA, 40, nk1, afn_qkv, epi_qkv);
+    } else {
+      g16_load(bA, 40, nk4, frag_qkv);
+      h_bar();
+      HTR(trk++);
+      g16_mma(bA, 40, nk4, afn_qkv, epi_qkv);
+    }
     h_bar();
     HTR(trk++);
     // attention: 1 query x 2 keys per (frame, head); 4 lanes per pair, 8 dims each
@@ -311,20 +407,22 @@ __global__ __launch_bounds__(HT) void head_fwd_rows_kernel(HeadParams p, const f
         if (live) ws.o(i)[gn * HD + d0 + d] = v;
       }
     }
-    g16_load(bO, 8, nk4, frag_o);
+    if constexpr (MX) g16_load_mx(mO, 8, nk1, mfrag_o);
+    else g16_load(bO, 8, nk4, frag_o);
     h_bar();
     HTR(trk++);
     // to_out + bias, dropout, residual (dama.py:50-53, 71-76)
     float *xnew = st + h_xout(i) * FG * HD;
-    g16_mma(
-        bO, 8, nk4, [&](int t, const bf16_t *&A, int &ap) { A = A1; ap = HKP; },
-        [&](int t, int row, int c, float v) {
+    auto afn_o = [&](int t, const bf16_t *&A, int &ap) { A = A1; ap = HKP; };
+    auto epi_o = [&](int t, int row, int c, float v) {
           const int col = t * 16 + c;
           const int64_t n = g0 + row;
           const float y = x[row * HD + col] + (v + bo[col]) * h_drop(sd, i, (int)n, col, p.p_ca);
           xnew[row * HD + col] = y;
           if (row < nr) ws.st(h_xout(i))[n * HD + col] = y;
-        });
+        };
+    if constexpr (MX) g16_mma_mx(mO, 8, nk1, afn_o, epi_o);
+    else g16_mma(bO, 8, nk4, afn_o, epi_o);
     h_bar();
     HTR(trk++);
   }
@@ -592,6 +690,7 @@ __global__ __launch_bounds__(HT) void head_bwd_tail_kernel(HeadParams p, float *
 // As in the forward, a phase issues its weight fragments before its MFMAs and the phases in
 // between touch LDS only; a block's attention / LayerNorm operands (global) are loaded at its
 // start, ahead of its first fragments.
+template <bool MX>
 __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *ws_base, float *ds0, float *df0,
                                                            int N) {
   int trk = 64;
@@ -629,6 +728,15 @@ __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *
     return h_ld8(pk + bi * HP_BLK + HP_KVT + (int64_t)col * (2 * HD) + kk);
   };
   hbf16x8 bC[2][6], bO[1][4], bX[2][12];
+  MxFrag mO[1][1], mX[2][3];
+  auto nk1 = [](int) { return 1; };
+  auto nkxm = [](int t) { return t < 8 ? 3 : 2; };
+  auto mfrag_o = [&](int t, int, int c) { return hmx(p.packed_mx, bi, 5).frag(t * 16 + c, 0); };
+  auto mfrag_x = [&](int t, int s, int c) {
+    const int col = (t & 7) * 16 + c;
+    if (t < 8 && s == 0) return hmx(p.packed_mx, bi, 1).frag(col, 0);
+    return hmx(p.packed_mx, bi, 3).frag(col, (t < 8 ? s - 1 : s) * 128);
+  };
   for (int e = tid; e < 4 * HD; e += HT) lnw[e] = p.ca[e >> 7].ln_w[e & 127];
 #pragma unroll
   for (int u = 0; u < FG * HD / HT; ++u) {
@@ -694,12 +802,14 @@ __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *
       if (r < nr) ws.dpre(i)[(int64_t)g0 * HD + e] = d;
     }
     bi = i;
-    g16_load(bO, 8, nk4, frag_o);
+    if constexpr (MX) g16_load_mx(mO, 8, nk1, mfrag_o);
+    else g16_load(bO, 8, nk4, frag_o);
     h_bar();
     HTR(trk++);
-    g16_mma(
-        bO, 8, nk4, [&](int t, const bf16_t *&A, int &ap) { A = Ac; ap = HKC; },
-        [&](int t, int row, int c, float v) { dO[row * HD + t * 16 + c] = v; });
+    auto afn_c = [&](int t, const bf16_t *&A, int &ap) { A = Ac; ap = HKC; };
+    auto epi_do = [&](int t, int row, int c, float v) { dO[row * HD + t * 16 + c] = v; };
+    if constexpr (MX) g16_mma_mx(mO, 8, nk1, afn_c, epi_do);
+    else g16_mma(bO, 8, nk4, afn_c, epi_do);
     h_bar();
     HTR(trk++);
     // attention backward: 4 lanes per (frame, head), 8 dims each
@@ -731,15 +841,14 @@ __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *
         }
       }
     }
-    g16_load(bX, 16, nkx, frag_x);
+    if constexpr (MX) g16_load_mx(mX, 16, nkxm, mfrag_x);
+    else g16_load(bX, 16, nkx, frag_x);
     h_bar();
     HTR(trk++);
-    g16_mma(
-        bX, 16, nkx,
-        [&](int t, const bf16_t *&A, int &ap) {
+    auto afn_x = [&](int t, const bf16_t *&A, int &ap) {
           if (t < 8) { A = Ac; ap = HKC; } else { A = A3; ap = HKP; }
-        },
-        [&](int t, int row, int c, float v) {
+        };
+    auto epi_x = [&](int t, int row, int c, float v) {
           const int col = (t & 7) * 16 + c;
           if (t < 8) {
             dxs[row * HD + col] = v;
@@ -747,7 +856,9 @@ __global__ __launch_bounds__(HT) void head_bwd_rows_kernel(HeadParams p, float *
           } else {
             dC[row * HD + col] += v;
           }
-        });
+        };
+    if constexpr (MX) g16_mma_mx(mX, 16, nkxm, afn_x, epi_x);
+    else g16_mma(bX, 16, nkx, afn_x, epi_x);
     h_bar();
     HTR(trk++);
     // LayerNorm backward into the own stream (which already holds the residual's gradient):
@@ -803,6 +914,7 @@ constexpr int HW_VBLK = (HW_VEC + 63) / 64;                 // 64 outputs (quads
 constexpr int64_t HW_DEAD = (int64_t)HD * 256 * 8;          // dead-tap zeros
 constexpr int HW_DBLK = (int)((HW_DEAD + 255) / 256);
 
+template <bool MX>
 __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams p, const float *ws_base, HeadGrads g, int N) {
   const uint64_t sd = step_seed(p.seed, p.seed_off);
   const HeadWs ws{const_cast<float *>(ws_base)};
@@ -862,6 +974,25 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams p, cons
       return h_pack8(v);
     };
     const bool two = D1 != nullptr;
+    if (MX && T < 1024) {
+      // one 128-wide MX step over the frames: K = frames of the self token (k < 64) and, for
+      // Wkv, of the context token (k >= 64); zero past N
+      float va[32], vb[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int k = (hh ? mx_k1(lane) : mx_k0(lane)) + e, n = k & 63;
+          const bool ok = n < N && (k < 64 || two);
+          const float *D = k < 64 ? D0 : D1, *X = k < 64 ? X0 : X1;
+          va[hh * 16 + e] = ok ? D[(int64_t)n * ldd + o0 + c] : 0.f;
+          vb[hh * 16 + e] = ok ? X[(int64_t)n * ldx + k0 + c] : 0.f;
+        }
+      const hf32x4 acc = mx_mma(mx_quant(va), mx_quant(vb), hf32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(int64_t)(o0 + (lane >> 4) * 4 + r) * ldo + (int64_t)(k0 + c) * kstr] = acc[r];
+      return;
+    }
     const hbf16x8 a0 = dfrag(D0, 0), a1 = dfrag(D0, 1), b0 = xfrag(X0, 0), b1 = xfrag(X0, 1);
     hbf16x8 a2 = {}, a3 = {}, b2 = {}, b3 = {};
     if (two) { a2 = dfrag(D1, 0); a3 = dfrag(D1, 1); b2 = xfrag(X1, 0); b3 = xfrag(X1, 1); }
@@ -972,6 +1103,43 @@ __global__ __launch_bounds__(256) void head_pack_kernel(HeadParams p, bf16_t *pk
   }
 }
 
+// MXFP8 pack of the attention blocks' weights: one thread per 32-element block of an image
+// (4 blocks x (Wq, Wq^T, Wkv, Wkv^T, Wo, Wo^T)), straight from the fp32 masters
+constexpr int HMX_NB = HD * 4 * 4 + 2 * HD * 4 + HD * 8;    // 32-element blocks per attention block
+__global__ __launch_bounds__(256) void head_pack_mx_kernel(HeadParams p, uint8_t *pk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 4 * HMX_NB) return;
+  const int b = i / HMX_NB;
+  int j = i - b * HMX_NB;
+  // image m, its row and block within the row
+  int m = 0;
+  for (; m < 6; ++m) {
+    int r, c;
+    hmx_dims(m, r, c);
+    if (j < r * (c / 32)) break;
+    j -= r * (c / 32);
+  }
+  int rows, cols;
+  hmx_dims(m, rows, cols);
+  const int row = j / (cols / 32), kb = j % (cols / 32);
+  const HeadCA &ca = p.ca[b];
+  const float *W = m < 2 ? ca.wq : m < 4 ? ca.wkv : ca.wo;    // [out][in = 128]
+  const bool tr = m & 1;
+  float v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) {
+    const int k = kb * 32 + e;
+    v[e] = tr ? W[(int64_t)k * HD + row] : W[(int64_t)row * HD + k];
+  }
+  int d[8];
+  const int ex = mx_quant_block(v, d);
+  uint8_t *img = pk + b * HMX_BLK + hmx_img(m);
+  uint8_t *dst = img + (int64_t)row * cols + kb * 32;
+  *reinterpret_cast<uint4 *>(dst) = make_uint4(d[0], d[1], d[2], d[3]);
+  *reinterpret_cast<uint4 *>(dst + 16) = make_uint4(d[4], d[5], d[6], d[7]);
+  img[(int64_t)rows * cols + (int64_t)row * (cols / 32) + kb] = (uint8_t)ex;
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
@@ -996,13 +1164,16 @@ static unsigned head_groups(int N) { return (unsigned)((N + FG - 1) / FG); }
 
 extern "C" int64_t ewvit_head_workspace(void) { return head_ws_floats() * (int64_t)sizeof(float); }
 extern "C" int64_t ewvit_head_pack_bytes(void) { return HP_TOTAL * (int64_t)sizeof(bf16_t); }
+extern "C" int64_t ewvit_head_pack_bytes_mx(void) { return 4 * HMX_BLK; }
 
 extern "C" int ewvit_head_fwd(const HeadParams *params, const float *s0, const float *f0, int N, float *workspace,
                               float *fused, float *s_out, float *f_out, void *stream) {
   EWVIT_CHECK_ARG(params && s0 && f0 && workspace && fused && s_out && f_out, "head_fwd: null pointer");
   if (int rc = head_check(*params, N, "head_fwd")) return rc;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(head_fwd_rows_kernel),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)HL_FWD_ROWS) == hipSuccess;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(head_fwd_rows_kernel<false>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)HL_FWD_ROWS) == hipSuccess &&
+                           hipFuncSetAttribute(reinterpret_cast<const void *>(head_fwd_rows_kernel<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)HL_FWD_ROWS) == hipSuccess;
   (void)attr;
   EWVIT_CHECK_ARG(params->packed, "head_fwd: no pack buffer (ewvit_head_pack_bytes)");
   hipStream_t s = as_stream(stream);
@@ -1010,8 +1181,15 @@ extern "C" int ewvit_head_fwd(const HeadParams *params, const float *s0, const f
   hipLaunchKernelGGL(head_pack_kernel, dim3((unsigned)((npk + 255) / 256)), dim3(256), 0, s, *params,
                      (bf16_t *)params->packed);
   if (int rc = launch_status("head_fwd pack")) return rc;
-  hipLaunchKernelGGL(head_fwd_rows_kernel, dim3(head_groups(N)), dim3(HT), HL_FWD_ROWS, s, *params, s0, f0, workspace,
-                     s_out, f_out, N);
+  if (params->packed_mx) {
+    hipLaunchKernelGGL(head_pack_mx_kernel, dim3((4 * HMX_NB + 255) / 256), dim3(256), 0, s, *params,
+                       (uint8_t *)params->packed_mx);
+    hipLaunchKernelGGL(head_fwd_rows_kernel<true>, dim3(head_groups(N)), dim3(HT), HL_FWD_ROWS, s, *params, s0, f0,
+                       workspace, s_out, f_out, N);
+  } else {
+    hipLaunchKernelGGL(head_fwd_rows_kernel<false>, dim3(head_groups(N)), dim3(HT), HL_FWD_ROWS, s, *params, s0, f0,
+                       workspace, s_out, f_out, N);
+  }
   if (int rc = launch_status("head_fwd rows")) return rc;
   hipLaunchKernelGGL(head_fwd_fuse_kernel, dim3(12 * head_groups(N)), dim3(64), 0, s, *params, workspace, N);
   if (int rc = launch_status("head_fwd fuse")) return rc;
@@ -1040,9 +1218,18 @@ extern "C" int ewvit_head_bwd(const HeadParams *params, const float *workspace, 
   hipLaunchKernelGGL(head_bwd_tail_kernel, dim3(1), dim3(HT), HL_BWD_TAIL, s, *params, ws, g_fused, g_s, g_f, bn_w,
                      bn_b, N);
   if (int rc = launch_status("head_bwd tail")) return rc;
-  hipLaunchKernelGGL(head_bwd_rows_kernel, dim3(head_groups(N)), dim3(HT), HL_BWD_ROWS, s, *params, ws, ds0, df0, N);
-  if (int rc = launch_status("head_bwd rows")) return rc;
-  hipLaunchKernelGGL(head_bwd_weight_kernel, dim3(HW_TBLK + HW_VBLK + HW_DBLK), dim3(256), 0, s, *params, workspace, g,
-                     N);
+  if (params->packed_mx) {
+    hipLaunchKernelGGL(head_bwd_rows_kernel<true>, dim3(head_groups(N)), dim3(HT), HL_BWD_ROWS, s, *params, ws, ds0,
+                       df0, N);
+    if (int rc = launch_status("head_bwd rows")) return rc;
+    hipLaunchKernelGGL(head_bwd_weight_kernel<true>, dim3(HW_TBLK + HW_VBLK + HW_DBLK), dim3(256), 0, s, *params,
+                       workspace, g, N);
+  } else {
+    hipLaunchKernelGGL(head_bwd_rows_kernel<false>, dim3(head_groups(N)), dim3(HT), HL_BWD_ROWS, s, *params, ws, ds0,
+                       df0, N);
+    if (int rc = launch_status("head_bwd rows")) return rc;
+    hipLaunchKernelGGL(head_bwd_weight_kernel<false>, dim3(HW_TBLK + HW_VBLK + HW_DBLK), dim3(256), 0, s, *params,
+                       workspace, g, N);
+  }
   return launch_status("head_bwd weight");
 }

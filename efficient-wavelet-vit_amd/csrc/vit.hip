@@ -37,6 +37,7 @@
 // their B fragments from the fp32 weights (forward) or from an LDS image of the weight slice
 // transposed to k-contiguous bf16 (input gradients reduce over the weight's output index).
 #include "common.h"
+#include "mx8.h"
 
 namespace ewvit {
 
@@ -100,6 +101,36 @@ constexpr int64_t PK_QKV = 0, PK_QKVT = PK_QKV + (int64_t)VQ * VD, PK_O = PK_QKV
                   PK_OT = PK_O + (int64_t)VD * VD, PK_1 = PK_OT + (int64_t)VD * VD, PK_1T = PK_1 + (int64_t)VF * VD,
                   PK_2 = PK_1T + (int64_t)VF * VD, PK_2T = PK_2 + (int64_t)VF * VD, PK_LAYER = PK_2T + (int64_t)VF * VD;
 __host__ __device__ inline int64_t al256(int64_t b) { return (b + 255) / 256 * 256; }
+// MXFP8 pack (ewvit_vit_pack_mx, configs[4]): the same eight operand images as e4m3 bytes, each
+// row followed (in a separate array) by its E8M0 scales, one per 32 consecutive elements along
+// the row (the GEMM's K): W [out][in] + S [out][in / 32], W^T [in][out] + S^T [in][out / 32].
+// Byte offsets within a layer's block, image m = 0..7 (qkv, qkvT, o, oT, 1, 1T, 2, 2T):
+struct MxW {
+  const uint8_t *d, *s;
+  int K;
+  __device__ __forceinline__ const uint8_t *row(int r) const { return d + (int64_t)r * K; }
+  __device__ __forceinline__ const uint8_t *srow(int r) const { return s + (int64_t)r * (K / 32); }
+};
+__host__ __device__ inline void mx_dims(int m, int &rows, int &cols) {
+  const int R[8] = {VQ, VD, VD, VD, VF, VD, VD, VF}, C[8] = {VD, VQ, VD, VD, VD, VF, VF, VD};
+  rows = R[m];
+  cols = C[m];
+}
+__host__ __device__ inline int64_t mx_off(int m) {     // data at mx_off(m), scales right after
+  int64_t o = 0;
+  for (int i = 0; i < m; ++i) {
+    int r, c;
+    mx_dims(i, r, c);
+    o += al256((int64_t)r * c) + al256((int64_t)r * (c / 32));
+  }
+  return o;
+}
+__device__ __forceinline__ MxW mx_image(const void *packed, int m) {
+  int r, c;
+  mx_dims(m, r, c);
+  const uint8_t *b = reinterpret_cast<const uint8_t *>(packed) + mx_off(m);
+  return MxW{b, b + al256((int64_t)r * c), c};
+}
 template <class F> __host__ __device__ inline int64_t saved_layout(F f) {
   int64_t o = 0;
   auto put = [&](int idx, int64_t bytes) { f(idx, o); o += al256(bytes); };
@@ -200,10 +231,38 @@ __device__ __forceinline__ void ln_stats_rows(const float *x, int R, float eps, 
 
 // A 64 x 64 block of a weight gradient out[r][c] = sum_k AT[r][k] BT[c][k] over the 128 rows
 // k (zero past R in both operands); wave w of 4 takes the 32 x 32 quadrant (w >> 1, w & 1)
+// MX: both operands block-quantized along the 128 rows in registers (4 blocks of 32 rows)
+template <bool MX>
 __device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, float *out, int64_t ldo, int r0,
                                             int c0, int w, int lane) {
   const int li = lane & 15, lq = lane >> 4;
   const int rb = r0 + (w >> 1) * 32, cb = c0 + (w & 1) * 32;
+  if constexpr (MX) {
+    MxFrag fa[2], fb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float va[32], vb[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q;
+          unpack8(ld8b(AT + (int64_t)(rb + t * 16 + li) * VRP + k), va + hh * 16 + q * 8);
+          unpack8(ld8b(BT + (int64_t)(cb + t * 16 + li) * VRP + k), vb + hh * 16 + q * 8);
+        }
+      fa[t] = mx_quant(va);
+      fb[t] = mx_quant(vb);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const vf4 acc = mx_mma(fa[i], fb[j], vf4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[(int64_t)(rb + i * 16 + lq * 4 + e) * ldo + cb + j * 16 + li] = acc[e];
+      }
+    return;
+  }
   vb8 a[4][2], b[4][2];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -238,7 +297,7 @@ __device__ __forceinline__ void wgrad_block(const bf16_t *AT, const bf16_t *BT, 
 // bandwidth bound: 48-64 workgroups reading all 128 rows ran 26-30 us).  512 threads: wave
 // (rg = w & 1, kq = w >> 1) owns rows 32 rg .. + 32 of the half and the K quarter kq (4 k-steps,
 // one batch of loads); the quarters meet in LDS in a fixed order.
-template <int MODE>
+template <int MODE, bool MX>
 __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const float *xin, VitSaved s) {
   __shared__ float smu[VRP], srs[VRP];
   __shared__ vf4 red[3][2][2][2][64];
@@ -281,7 +340,35 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-  {
+  if constexpr (MX) {
+    // the wave's K quarter is one 128-wide MX step: LN output quantized from fp32 in registers
+    const MxW W8 = mx_image(p.packed, MODE ? 4 : 0);
+    MxFrag af[2], bf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float v[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = kq * 128 + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q;
+          float g8[8], b8[8], x8[8];
+          ld8f(gw + k, g8);
+          ld8f(gb + k, b8);
+          ld8f(xin + (int64_t)rclamp(row[t], R) * VD + k, x8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[hh * 16 + q * 8 + e] = row[t] < R ? (x8[e] - mu[t]) * rs[t] * g8[e] + b8[e] : 0.f;
+        }
+      af[t] = mx_quant(v);
+      const int n = c0 + t * 16 + li;
+      bf[t] = mx_load(W8.row(n), kq * 128, W8.srow(n));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mx_mma(af[i], bf[j], acc[i][j]);
+  } else {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -353,6 +440,7 @@ __global__ __launch_bounds__(512) void vit_ln_gemm_kernel(VitP p, int R, const f
 // per pair — in LDS; the attention output o[r][k] = p[r][h][0] v[2f][k] + p[r][h][1] v[2f+1][k]
 // (f = r / 2, h = k / 64) is formed in the A fragments; column block cb also writes o
 // transposed for its 32 columns and the half's rows.  Waves (rg = w & 1, kq = w >> 1) as F1.
+template <bool MX>
 __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const float *x0, VitSaved s) {
   __shared__ float sp[VRP][VH][2];
   __shared__ vf4 red[3][2][2][2][64];
@@ -427,7 +515,38 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-  {
+  if constexpr (MX) {
+    const MxW W8 = mx_image(p.packed, 2);
+    MxFrag af[2], bf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int r = rbase + rg * 32 + t * 16 + li, f = rclamp(r, R) >> 1;
+      float v[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = kq * 128 + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q, h = k >> 6;
+          float v0[8], v1[8];
+          unpack8(ld8b(s.qkv + (int64_t)(2 * f) * VQ + 2 * VD + k), v0);
+          unpack8(ld8b(s.qkv + (int64_t)(2 * f + 1) * VQ + 2 * VD + k), v1);
+          const float p0 = sp[r][h][0], p1 = sp[r][h][1];      // 0 past R
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float o = p0 * v0[e];
+            o += p1 * v1[e];
+            v[hh * 16 + q * 8 + e] = o;
+          }
+        }
+      af[t] = mx_quant(v);
+      const int n = c0 + t * 16 + li;
+      bf[t] = mx_load(W8.row(n), kq * 128, W8.srow(n));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mx_mma(af[i], bf[j], acc[i][j]);
+  } else {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -487,6 +606,7 @@ __global__ __launch_bounds__(512) void vit_attn_proj_kernel(VitP p, int R, const
 // (K = 512 over W2's output index: W2[:, J] staged transposed in LDS), rounded to bf16 like the
 // module path's dh, g1 = dh GELU'(pre) -> g1 (bf16), g1^T, db1[J].  Side job of workgroup b:
 // g's columns 8 b .. + 8 transposed (gT) and their sums (db2).
+template <bool MX>
 __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
                                                            VitScratch z) {
   __shared__ vf4 red[3][2][2][2][64];
@@ -523,7 +643,32 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = vf4{0.f, 0.f, 0.f, 0.f};
-  {
+  if constexpr (MX) {
+    const MxW W8 = mx_image(p.packed, 7);         // W2^T [2048][512]
+    MxFrag af[2], bf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int r = rbase + rg * 32 + t * 16 + li;
+      float v[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = kq * 128 + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q;
+          ld8f(g + (int64_t)rclamp(r, R) * VD + k, v + hh * 16 + q * 8);
+        }
+      if (r >= R)
+#pragma unroll
+        for (int e = 0; e < 32; ++e) v[e] = 0.f;
+      af[t] = mx_quant(v);
+      const int n = J0 + t * 16 + li;
+      bf[t] = mx_load(W8.row(n), kq * 128, W8.srow(n));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mx_mma(af[i], bf[j], acc[i][j]);
+  } else {
     vb8 af[4][2], bf[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -592,32 +737,59 @@ __global__ __launch_bounds__(512) void vit_mlp2_bwd_kernel(VitP p, VitG G, int R
 // ... and, for the LayerNorm whose output gradient it is, the block's row partials of the LN
 // backward sums over its 16 columns: rpart[I0 / 16][row] = (sum gamma d, sum gamma d xhat)
 // with xhat from X, mu, rs (the consumer adds the 32 column blocks in order)
-template <int K>
-__device__ __forceinline__ void dgrad_block(const bf16_t *A, const bf16_t *BT, float *out, int R, int I0, int rq,
-                                            int w, int lane, vf4 *red, const float *X, const float *mu,
-                                            const float *rs, const float *gamma, float *rpart) {
+// MX: A block-quantized in registers, B from the MXFP8 image BT8 of the same weight
+template <int K, bool MX>
+__device__ __forceinline__ void dgrad_block(const bf16_t *A, const bf16_t *BT, const MxW &BT8, float *out, int R,
+                                            int I0, int rq, int w, int lane, vf4 *red, const float *X,
+                                            const float *mu, const float *rs, const float *gamma, float *rpart) {
   constexpr int KQ = K / 4, NS = KQ / 32;
   const int li = lane & 15, lq = lane >> 4;
   vf4 acc[2];
   acc[0] = acc[1] = vf4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (MX) {
 #pragma unroll 1
-  for (int sb = 0; sb < NS; sb += 4) {
-    vb8 af[4][2], bf[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = w * KQ + (sb + u) * 32 + lq * 8;
+    for (int sb = 0; sb < NS; sb += 4) {
+      const int kb = w * KQ + sb * 32;
+      MxFrag af[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int r = rq * 32 + t * 16 + li;
-        af[u][t] = ld8b(A + (int64_t)rclamp(r, R) * K + k);
-        if (r >= R) af[u][t] = zero8();
+        float v[32];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            unpack8(ld8b(A + (int64_t)rclamp(r, R) * K + kb + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q),
+                    v + hh * 16 + q * 8);
+        if (r >= R)
+#pragma unroll
+          for (int e = 0; e < 32; ++e) v[e] = 0.f;
+        af[t] = mx_quant(v);
       }
-      bf[u] = ld8b(BT + (int64_t)(I0 + li) * K + k);
+      const MxFrag bf = mx_load(BT8.row(I0 + li), kb, BT8.srow(I0 + li));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = mx_mma(af[t], bf, acc[t]);
     }
+  } else {
+#pragma unroll 1
+    for (int sb = 0; sb < NS; sb += 4) {
+      vb8 af[4][2], bf[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 4; ++u) {
+        const int k = w * KQ + (sb + u) * 32 + lq * 8;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
+        for (int t = 0; t < 2; ++t) {
+          const int r = rq * 32 + t * 16 + li;
+          af[u][t] = ld8b(A + (int64_t)rclamp(r, R) * K + k);
+          if (r >= R) af[u][t] = zero8();
+        }
+        bf[u] = ld8b(BT + (int64_t)(I0 + li) * K + k);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = mma(af[u][t], bf[u], acc[t]);
+    }
   }
   if (w > 0)
 #pragma unroll
@@ -661,6 +833,7 @@ __device__ __forceinline__ void lnb_rows_parts(const float *rpart, float *sa, fl
 // 256 threads.  Workgroups 0..127: dLN2 = g1 W1 in (16 columns, 32 rows) blocks (W1^T from the
 // packed image; 4 waves = 4 K quarters of 512, added in LDS); 128..383: dW2 = g^T h in 64 x 64
 // blocks; 384..639: dW1 = g1^T LN2.
+template <bool MX>
 __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R, VitSaved s, VitScratch z) {
   __shared__ vf4 red[3 * 2 * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -673,17 +846,18 @@ __global__ __launch_bounds__(256) void vit_mlp1_bwd_kernel(VitP p, VitG G, int R
   }
   if (blk >= 128 + 256) {
     const int q = blk - 384;
-    wgrad_block(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    wgrad_block<MX>(z.g1T, s.ln2T, G.w1, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
   if (blk >= 128) {
     const int q = blk - 128;
-    wgrad_block(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
+    wgrad_block<MX>(z.gT, s.hT, G.w2, VF, (q >> 5) * 64, (q & 31) * 64, w, lane);
     return;
   }
   // input gradient: workgroup (16-column block, row quarter)
-  dgrad_block<VF>(z.g1, reinterpret_cast<const bf16_t *>(p.packed) + PK_1T, z.dln2, R, (blk >> 2) * 16, blk & 3, w,
-                  lane, red, s.x1, s.mu2, s.rs2, p.ln2_w, z.rp2);
+  const MxW W8 = MX ? mx_image(p.packed, 5) : MxW{nullptr, nullptr, 0};
+  dgrad_block<VF, MX>(z.g1, reinterpret_cast<const bf16_t *>(p.packed) + PK_1T, W8, z.dln2, R, (blk >> 2) * 16,
+                      blk & 3, w, lane, red, s.x1, s.mu2, s.rs2, p.ln2_w, z.rp2);
 }
 
 // ---------------------------------------------------------------- LayerNorm backward pieces
@@ -741,6 +915,8 @@ __device__ __forceinline__ void lnb_cols(const float *dY, const float *X, const 
 // of 64 (added in LDS in a fixed order), rounded to bf16 like the module path's; then the
 // attention backward of the head over the 16 two-token frames -> dqkv (bf16) and dqkv^T.
 // Workgroups 32..47: 32 columns each of dx1, g_o^T, the to_out bias and the LN2 affine gradients.
+// MX: the 8 waves as 4 K slices of 128 (one MX step each) x 2 column halves of the head
+template <bool MX>
 __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, int R, const float *g, VitSaved s,
                                                                VitScratch z) {
   __shared__ vf4 red[8][2][4][64];                 // 64 KB: the waves' K-slice partials
@@ -768,6 +944,45 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
     ma[t] = sa[row[t]];
     mb[t] = sbm[row[t]];
   }
+  constexpr int NSL = MX ? 4 : 8;                  // K slices added in the reduction below
+  if constexpr (MX) {
+    const MxW W8 = mx_image(p.packed, 3);          // Wo^T [512][512]
+    const int ks = w & 3, ch = w >> 2;
+    MxFrag af[2], bf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int r = row[t], rr = rclamp(r, R);
+      float v[32];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = ks * 128 + (hh ? mx_k1(lane) : mx_k0(lane)) + 8 * q;
+          float gm[8], d[8], x[8], gg[8];
+          ld8f(p.ln2_w + k, gm);
+          ld8f(z.dln2 + (int64_t)rr * VD + k, d);
+          ld8f(s.x1 + (int64_t)rr * VD + k, x);
+          ld8f(g + (int64_t)rr * VD + k, gg);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xh = (x[e] - mu[t]) * rs[t];
+            float dx = rs[t] * (gm[e] * d[e] - ma[t] - xh * mb[t]) + gg[e];
+            if (p.drop_p > 0.f) dx *= keep_scale(p.drop_p, sd, (uint64_t)(r * VD + k + e));
+            v[hh * 16 + q * 8 + e] = r < R ? dx : 0.f;
+          }
+        }
+      af[t] = mx_quant(v);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int n = h * VDH + (ch * 2 + jj) * 16 + li;
+      bf[jj] = mx_load(W8.row(n), ks * 128, W8.srow(n));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) red[ks][i][ch * 2 + jj][lane] = mx_mma(af[i], bf[jj], vf4{0.f, 0.f, 0.f, 0.f});
+  } else {
   vf4 acc[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -810,13 +1025,14 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[w][i][j][lane] = acc[i][j];
+  }
   __syncthreads();
   if (tid < 2 * 4 * 64) {
-    // the 8 K slices added in order; thread (i, j, lane) of the 32 x 64 block
+    // the K slices added in order; thread (i, j, lane) of the 32 x 64 block
     const int i = tid >> 8, j = (tid >> 6) & 3, l = tid & 63;
     vf4 a = red[0][i][j][l];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) {
+    for (int k = 1; k < NSL; ++k) {
       const vf4 b = red[k][i][j][l];
       a = vf4{a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
     }
@@ -891,6 +1107,7 @@ __global__ __launch_bounds__(512) void vit_ln2_bwd_attn_kernel(VitP p, VitG G, i
 // ---------------------------------------------------------------- B4: to_qkv backward, dWqkv, dWo
 // 256 threads.  Workgroups 0..127: dLN1 = dqkv Wqkv in (16 columns, 32 rows) blocks (4 waves = K
 // quarters of 384, added in LDS); 128..319: dWqkv = dqkv^T LN1; 320..383: dWo = g_o^T o.
+template <bool MX>
 __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R, const float *x0, VitSaved s,
                                                           VitScratch z) {
   __shared__ vf4 red[3 * 2 * 64];
@@ -898,17 +1115,18 @@ __global__ __launch_bounds__(256) void vit_qkv_bwd_kernel(VitP p, VitG G, int R,
   const int blk = blockIdx.x;
   if (blk >= 128 + 192) {
     const int q = blk - 320;
-    wgrad_block(z.goT, s.oT, G.wo, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    wgrad_block<MX>(z.goT, s.oT, G.wo, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
   if (blk >= 128) {
     const int q = blk - 128;
-    wgrad_block(z.dqkvT, s.ln1T, G.wqkv, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
+    wgrad_block<MX>(z.dqkvT, s.ln1T, G.wqkv, VD, (q >> 3) * 64, (q & 7) * 64, w, lane);
     return;
   }
   // input gradient: workgroup (16-column block, row quarter)
-  dgrad_block<VQ>(z.dqkv, reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT, z.dln1, R, (blk >> 2) * 16, blk & 3,
-                  w, lane, red, x0, s.mu1, s.rs1, p.ln1_w, z.rp1);
+  const MxW W8 = MX ? mx_image(p.packed, 1) : MxW{nullptr, nullptr, 0};
+  dgrad_block<VQ, MX>(z.dqkv, reinterpret_cast<const bf16_t *>(p.packed) + PK_QKVT, W8, z.dln1, R, (blk >> 2) * 16,
+                      blk & 3, w, lane, red, x0, s.mu1, s.rs1, p.ln1_w, z.rp1);
 }
 
 // ---------------------------------------------------------------- B5: LN1 backward + residual
@@ -1028,11 +1246,59 @@ __global__ __launch_bounds__(256) void vit_pack_kernel(VitPackSrc src, int nlaye
   (void)rows;
 }
 
+// MXFP8 pack: the same 64 x 64 tiles; threads 0..127 quantize the tile's 64 rows x 2 blocks of
+// W (blocks along in), threads 128..255 its 64 columns x 2 blocks of W^T (blocks along out),
+// straight from the fp32 masters (one rounding)
+__global__ __launch_bounds__(256) void vit_pack_mx_kernel(VitPackSrc src, int nlayers, uint8_t *packed) {
+  __shared__ float tile[64][65];
+  constexpr int T0 = 24 * 8, T1 = T0 + 64, T2 = T1 + 256, TL = T2 + 256;
+  const int layer = blockIdx.x / TL, t = blockIdx.x % TL;
+  int m, tr, tc;
+  if (t < T0) { m = 0; tr = t / 8; tc = t % 8; }
+  else if (t < T1) { m = 1; tr = (t - T0) / 8; tc = (t - T0) % 8; }
+  else if (t < T2) { m = 2; tr = (t - T1) / 8; tc = (t - T1) % 8; }
+  else { m = 3; tr = (t - T2) / 32; tc = (t - T2) % 32; }
+  int rows, cols;
+  mx_dims(2 * m, rows, cols);
+  const float *W = src.w[layer * 4 + m];
+  uint8_t *base = packed + (int64_t)layer * mx_off(8);
+  const int tid = threadIdx.x, r0 = tr * 64, c0 = tc * 64;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256, r = i >> 4, q = i & 15;
+    const float4 v = *reinterpret_cast<const float4 *>(W + (int64_t)(r0 + r) * cols + c0 + 4 * q);
+    tile[r][4 * q] = v.x; tile[r][4 * q + 1] = v.y; tile[r][4 * q + 2] = v.z; tile[r][4 * q + 3] = v.w;
+  }
+  __syncthreads();
+  const int tr_ = tid & 127, hb = tr_ & 1, x = tr_ >> 1;
+  float v[32];
+  int d[8];
+  uint8_t *dst, *sdst;
+  if (tid < 128) {          // W row r0 + x, in-columns c0 + 32 hb ..
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = tile[x][32 * hb + j];
+    uint8_t *img = base + mx_off(2 * m);
+    dst = img + (int64_t)(r0 + x) * cols + c0 + 32 * hb;
+    sdst = img + al256((int64_t)rows * cols) + (int64_t)(r0 + x) * (cols / 32) + c0 / 32 + hb;
+  } else {                  // W^T row c0 + x (= W column), out-rows r0 + 32 hb ..
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = tile[32 * hb + j][x];
+    uint8_t *img = base + mx_off(2 * m + 1);
+    dst = img + (int64_t)(c0 + x) * rows + r0 + 32 * hb;
+    sdst = img + al256((int64_t)cols * rows) + (int64_t)(c0 + x) * (rows / 32) + r0 / 32 + hb;
+  }
+  const int e = mx_quant_block(v, d);
+  *reinterpret_cast<uint4 *>(dst) = make_uint4(d[0], d[1], d[2], d[3]);
+  *reinterpret_cast<uint4 *>(dst + 16) = make_uint4(d[4], d[5], d[6], d[7]);
+  *sdst = (uint8_t)e;
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
 
 extern "C" int64_t ewvit_vit_layer_workspace(int which) {
+  if (which == 3) return mx_off(8);
   if (which == 2) return PK_LAYER * 2;
   return which == 0 ? saved_layout([](int, int64_t) {}) : scratch_layout([](int, int64_t) {});
 }
@@ -1052,6 +1318,21 @@ extern "C" int ewvit_vit_pack(const ewvit_vit_layer *layers, int n, void *packed
   return launch_status("vit_pack");
 }
 
+extern "C" int ewvit_vit_pack_mx(const ewvit_vit_layer *layers, int n, void *packed, void *stream) {
+  EWVIT_CHECK_ARG(layers && packed && n >= 1 && n <= EWVIT_VIT_PACK_MAX, "vit_pack_mx: n=%d", n);
+  VitPackSrc src;
+  for (int i = 0; i < n; ++i) {
+    EWVIT_CHECK_ARG(layers[i].wqkv && layers[i].wo && layers[i].w1 && layers[i].w2, "vit_pack_mx: null weight");
+    src.w[4 * i] = layers[i].wqkv;
+    src.w[4 * i + 1] = layers[i].wo;
+    src.w[4 * i + 2] = layers[i].w1;
+    src.w[4 * i + 3] = layers[i].w2;
+  }
+  hipLaunchKernelGGL(vit_pack_mx_kernel, dim3(n * (24 * 8 + 64 + 256 + 256)), dim3(256), 0, as_stream(stream), src,
+                     n, (uint8_t *)packed);
+  return launch_status("vit_pack_mx");
+}
+
 static int vit_check(const ewvit_vit_layer *p, int R) {
   EWVIT_CHECK_ARG(p && p->ln1_w && p->ln1_b && p->wqkv && p->wo && p->bo && p->ln2_w && p->ln2_b && p->w1 && p->b1 &&
                       p->w2 && p->b2,
@@ -1068,9 +1349,19 @@ extern "C" int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float 
   EWVIT_CHECK_ARG(x0 && saved && x2, "vit_layer_fwd: null pointer");
   const VitSaved s = vit_saved(saved);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(vit_ln_gemm_kernel<0>, dim3(2 * VQ / 32), dim3(512), 0, st, *p, R, x0, s);
-  hipLaunchKernelGGL(vit_attn_proj_kernel, dim3(2 * VD / 32), dim3(512), 0, st, *p, R, x0, s);
-  hipLaunchKernelGGL(vit_ln_gemm_kernel<1>, dim3(2 * VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
+  if (p->mx) {
+    hipLaunchKernelGGL((vit_ln_gemm_kernel<0, true>), dim3(2 * VQ / 32), dim3(512), 0, st, *p, R, x0, s);
+    hipLaunchKernelGGL(vit_attn_proj_kernel<true>, dim3(2 * VD / 32), dim3(512), 0, st, *p, R, x0, s);
+    hipLaunchKernelGGL((vit_ln_gemm_kernel<1, true>), dim3(2 * VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
+    if (int rc = launch_status("vit_layer_fwd")) return rc;
+    // Linear2 on the MXFP8 split-K GEMM (W2 block-quantized from the fp32 master as it is
+    // staged: the same e4m3 values and scales as the pack's image 6)
+    return ewvit_gemm_mx8(s.h, EWVIT_BF16, VF, 1, p->w2, EWVIT_F32, 1, VF, x2, EWVIT_F32, VD, R, VD, VF, 1.f, 0.f,
+                          p->b2, 0, nullptr, 0.f, 0, nullptr, s.x1, EWVIT_F32, VD, VF4_SPLIT, s.ws2, stream);
+  }
+  hipLaunchKernelGGL((vit_ln_gemm_kernel<0, false>), dim3(2 * VQ / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL(vit_attn_proj_kernel<false>, dim3(2 * VD / 32), dim3(512), 0, st, *p, R, x0, s);
+  hipLaunchKernelGGL((vit_ln_gemm_kernel<1, false>), dim3(2 * VF / 32), dim3(512), 0, st, *p, R, (const float *)s.x1, s);
   if (int rc = launch_status("vit_layer_fwd")) return rc;
   // Linear2 + bias + residual: K = 2048 against 128 rows wants its K split over many
   // workgroups (one workgroup per column block reading all of h measured 32 us): the split-K
@@ -1091,10 +1382,17 @@ extern "C" int ewvit_vit_layer_bwd(const ewvit_vit_layer *p, int R, const float 
   const VitSaved s = vit_saved(const_cast<void *>(saved));
   const VitScratch z = vit_scratch(scratch);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(vit_mlp2_bwd_kernel, dim3(2 * VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_mlp1_bwd_kernel, dim3(128 + 256 + 256 + VF / 256), dim3(256), 0, st, *p, *G, R, s, z);
-  hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
-  hipLaunchKernelGGL(vit_qkv_bwd_kernel, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, x0, s, z);
+  if (p->mx) {
+    hipLaunchKernelGGL(vit_mlp2_bwd_kernel<true>, dim3(2 * VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
+    hipLaunchKernelGGL(vit_mlp1_bwd_kernel<true>, dim3(128 + 256 + 256 + VF / 256), dim3(256), 0, st, *p, *G, R, s, z);
+    hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel<true>, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
+    hipLaunchKernelGGL(vit_qkv_bwd_kernel<true>, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, x0, s, z);
+  } else {
+    hipLaunchKernelGGL(vit_mlp2_bwd_kernel<false>, dim3(2 * VF / 32), dim3(512), 0, st, *p, *G, R, g, s, z);
+    hipLaunchKernelGGL(vit_mlp1_bwd_kernel<false>, dim3(128 + 256 + 256 + VF / 256), dim3(256), 0, st, *p, *G, R, s, z);
+    hipLaunchKernelGGL(vit_ln2_bwd_attn_kernel<false>, dim3(4 * VH + 16), dim3(512), 0, st, *p, *G, R, g, s, z);
+    hipLaunchKernelGGL(vit_qkv_bwd_kernel<false>, dim3(128 + 192 + 64), dim3(256), 0, st, *p, *G, R, x0, s, z);
+  }
   hipLaunchKernelGGL(vit_ln1_bwd_kernel, dim3(VD / 32), dim3(512), 0, st, *p, *G, R, x0, s, z, dx0);
   return launch_status("vit_layer_bwd");
 }

@@ -18,7 +18,6 @@ ABI_VERSION = 3
 F32, BF16 = 0, 1
 ADAM_MAX = 48          # EWVIT_ADAM_MAX (include/ewvit.h)
 PACK_MAX = 32          # EWVIT_PACK_MAX
-AMAX_PARTS = 256       # EWVIT_AMAX_PARTS
 ADAM_ENTRY = 7         # EWVIT_ADAM_ENTRY
 
 _i64, _i32, _f32, _u64, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
@@ -31,10 +30,8 @@ SIGNATURES = {
     'ewvit_dwt_hf_upsample_fused': [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i64, _vp],
     'ewvit_gemm': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
                    _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
-    'ewvit_gemm_fp8': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
-                       _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp,
-                       _vp, _i32, _vp, _i32, _vp],
-    'ewvit_amax_partials': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
+    'ewvit_gemm_mx8': [_vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i64,
+                       _f32, _f32, _vp, _i32, _vp, _f32, _u64, _vp, _vp, _i32, _i64, _i32, _vp, _vp],
     'ewvit_colsum': [_vp, _i32, _i64, _i64, _i64, _vp, _i32, _vp],
     'ewvit_dropout_bwd': [_vp, _i32, _i64, _i64, _i64, _f32, _u64, _vp, _vp],
     'ewvit_act_bwd': [_vp, _i32, _i64, _vp, _i32, _f32, _u64, _vp, _vp, _i32, _i64, _i64, _vp],
@@ -56,6 +53,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_win': [_i32],
     'ewvit_conv2d_set_lds_pad': [_i32],
     'ewvit_conv2d_set_wgrad_tap_split': [_i32],
+    'ewvit_conv2d_set_win_nt': [_i32],
     'ewvit_dwt_set_pf': [_i32],
     'ewvit_conv2d_set_grid_cap': [_i32],
     'ewvit_set_grid_cap': [_i32],
@@ -126,6 +124,7 @@ SIGNATURES = {
     'ewvit_vit_layer_fwd': [_vp, _i32, _vp, _vp, _vp, _vp],
     'ewvit_vit_layer_bwd': [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_vit_pack': [_vp, _i32, _vp, _vp],
+    'ewvit_vit_pack_mx': [_vp, _i32, _vp, _vp],
     'ewvit_gemm_tallk': [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp],
     'ewvit_vit_embed_fwd': [_vp, _vp, _vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp],
     'ewvit_vit_embed_bwd': [_vp, _i32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp],
@@ -157,6 +156,7 @@ QUERIES = {
     'ewvit_dwconv3x3_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_head_workspace': (_i64, []),
     'ewvit_head_pack_bytes': (_i64, []),
+    'ewvit_head_pack_bytes_mx': (_i64, []),
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_wall_clock_khz': (_i32, []),
     'ewvit_conv2d_wgrad_1x1_config': (_i32, [_i32]),
@@ -200,6 +200,8 @@ def load():
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
     if os.environ.get('EWVIT_WGWIN_TS') in ('0', '2') and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):
         lib.ewvit_conv2d_set_wgrad_tap_split(int(os.environ['EWVIT_WGWIN_TS']))   # A/B (convwin.hip wgrad NG)
+    if os.environ.get('EWVIT_WIN_NT') in ('0', '1') and hasattr(lib, 'ewvit_conv2d_set_win_nt'):
+        lib.ewvit_conv2d_set_win_nt(int(os.environ['EWVIT_WIN_NT']))   # A/B switch (convwin.hip g_win_nt)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
     _lib = lib

@@ -32,7 +32,7 @@ from .grads import grad_out
 # into persistent bf16 buffers, instead of one pack launch per conv call.
 _registry = {}      # id(weight) -> {'ref', 'cin_pad', 'wp', 'wpt', 'bwd'}
 # per thread (nn.DataParallel replicas run in threads, reference train.py:249-251): the
-# `packed()` scope, the fp8 weight-amax cache of that scope and the offered skip link
+# `packed()` scope and the offered skip link
 _tls = threading.local()
 
 
@@ -121,17 +121,12 @@ def packed():
     """Scope of one forward(+backward) with the weights fixed: packs all registered
     conv weights once on entry; convs inside read the packs."""
     prepack()
-    prev, prev_amax = getattr(_tls, 'active', False), getattr(_tls, 'weight_amax', None)
-    _tls.active, _tls.weight_amax = True, {}     # fp8 weight amax: once per step
+    prev = getattr(_tls, 'active', False)
+    _tls.active = True
     try:
         yield
     finally:
-        _tls.active, _tls.weight_amax = prev, prev_amax
-
-
-def weight_amax_cache():
-    """The fp8 weight-amax cache of the calling thread's `packed()` scope, or None."""
-    return getattr(_tls, 'weight_amax', None)
+        _tls.active = prev
 
 
 def _cached_pack(weight, cin_pad, bwd):

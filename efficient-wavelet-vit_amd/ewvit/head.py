@@ -6,8 +6,9 @@ Forward: one workgroup per 16 frames (the attention blocks, fusion conv and gate
 LDS-resident) + one workgroup for the frame-coupled tail (BatchNorm over the frames, gate
 softmax, weighted sum); backward: the tail, the frame groups in reverse, and one grid for the
 parameter gradients.  The module-by-module path (network/dama.py) issues ~90 small launches
-for the same work; it stays for hooked / patched modules, fp8 token GEMMs
-and shapes outside this kernel's class (dim 128, 4 heads of 32, depth 2, <= 64 frames).
+for the same work; it stays for hooked / patched modules and shapes outside this kernel's
+class (dim 128, 4 heads of 32, depth 2, <= 64 frames).  With fp8 token GEMMs (mx=True) the
+attention blocks' GEMMs run on MXFP8 operands (a second weight pack, ewvit_head_pack_bytes_mx).
 """
 import ctypes
 
@@ -30,19 +31,21 @@ class _Params(ctypes.Structure):
                 ('bn_w', _vp), ('bn_b', _vp), ('bn_rm', _vp), ('bn_rv', _vp), ('bn_nbt', _vp), ('bn_mom', _f32),
                 ('bn_eps', _f32), ('g1w', _vp), ('g1b', _vp), ('g2w', _vp), ('g2b', _vp), ('p_ca', _f32),
                 ('p_gate', _f32), ('seed', _u64), ('seed_off', _vp), ('training', _i32), ('ln_eps', _f32),
-                ('packed', _vp)]
+                ('packed', _vp), ('packed_mx', _vp)]
 
 
 class HeadCfg:
     """The non-tensor state of one call: BatchNorm buffers and hyper-parameters, dropout."""
 
-    def __init__(self, bn, ln_eps, p_ca, p_gate, training, seed):
+    def __init__(self, bn, ln_eps, p_ca, p_gate, training, seed, mx=False):
         self.bn, self.ln_eps, self.p_ca, self.p_gate, self.training, self.seed = bn, ln_eps, p_ca, p_gate, training, seed
+        self.mx = bool(mx)
 
 
-def _params(cfg, ts, dev, packed=None):
+def _params(cfg, ts, dev, packed=None, packed_mx=None):
     p = _Params()
     p.packed = packed
+    p.packed_mx = packed_mx
     for i in range(4):
         lw, lb, wq, wkv, wo, bo = ts[6 * i:6 * i + 6]
         p.ca[i] = _CA(lw.data_ptr(), lb.data_ptr(), wq.data_ptr(), wkv.data_ptr(), wo.data_ptr(), bo.data_ptr())
@@ -75,9 +78,10 @@ class DamaHeadFn(torch.autograd.Function):
         dev = s0.device
         ws = torch.empty(int(L.load().ewvit_head_workspace()) // 4, dtype=torch.float32, device=dev)
         pk = torch.empty(int(L.load().ewvit_head_pack_bytes()), dtype=torch.uint8, device=dev)
+        pkm = torch.empty(int(L.load().ewvit_head_pack_bytes_mx()), dtype=torch.uint8, device=dev) if cfg.mx else None
         fused = torch.empty(N, 128, dtype=torch.float32, device=dev)
         so, fo = torch.empty_like(fused), torch.empty_like(fused)
-        p = _params(cfg, ts, dev, pk.data_ptr())
+        p = _params(cfg, ts, dev, pk.data_ptr(), pkm.data_ptr() if pkm is not None else None)
         ctx.gen = grads.note_use(ts[0])
         for t in ts[1:]:
             grads.note_use(t)
@@ -85,12 +89,12 @@ class DamaHeadFn(torch.autograd.Function):
                L.ptr(fo), L.stream(fused), work={'flops': 2.0 * N * 128 * (4 * (128 + 512 + 128) + 256 + 64),
                                                  'bytes': 4.0 * sum(t.numel() for t in ts)})
         ctx.cfg, ctx.N, ctx.ts = cfg, N, ts
-        ctx.save_for_backward(ws, pk)
+        ctx.save_for_backward(ws, pk, *(() if pkm is None else (pkm,)))
         return fused, so, fo
 
     @staticmethod
     def backward(ctx, g_fused, g_s, g_f):
-        ws, pk = ctx.saved_tensors
+        ws, pk, *pkm = ctx.saved_tensors
         cfg, N, ts = ctx.cfg, ctx.N, ctx.ts
         dev = ws.device
 
@@ -106,7 +110,7 @@ class DamaHeadFn(torch.autograd.Function):
             if k == 24 and g.stride() != t.stride():
                 g = torch.empty_like(t)
             outs.append(g)
-        p = _params(cfg, ts, dev, pk.data_ptr())
+        p = _params(cfg, ts, dev, pk.data_ptr(), pkm[0].data_ptr() if pkm else None)
         arr = ctypes.c_void_p * 4
 
         def col(j):
@@ -134,9 +138,10 @@ def params_of(dama):
     return ts
 
 
-def dama_head(dama, s0, f0, seed):
-    """(fused, space, freq) per frame for s0, f0 [N, 128]: DamaHeadFn with DAMA's parameters."""
+def dama_head(dama, s0, f0, seed, mx=False):
+    """(fused, space, freq) per frame for s0, f0 [N, 128]: DamaHeadFn with DAMA's parameters
+    (mx: the attention blocks' GEMMs on MXFP8 operands)."""
     bn = dama.fusion_gate[1]
     att = dama.cross_att.layers[0][1]
-    cfg = HeadCfg(bn, dama.cross_att.layers[0][0].eps, att.to_out[1].p, dama.gate_net[4].p, dama.training, seed)
+    cfg = HeadCfg(bn, dama.cross_att.layers[0][0].eps, att.to_out[1].p, dama.gate_net[4].p, dama.training, seed, mx)
     return DamaHeadFn.apply(cfg, s0, f0, *params_of(dama))

@@ -28,49 +28,12 @@ def _c(t):
 
 
 # ------------------------------------------------------------------- GEMM
-def amax_partials(X, rows, cols, ld, nparts=None):
-    """Partial maxima of |X| over a [rows x cols] (row stride ld) matrix (ewvit_amax_partials):
-    one workgroup per ~16K elements, at most EWVIT_AMAX_PARTS."""
-    n = nparts or int(max(1, min(L.AMAX_PARTS, (rows * cols + 16383) // 16384)))
-    part = torch.empty(n, dtype=torch.float32, device=X.device)
-    L.call('ewvit_amax_partials', L.ptr(X), L.dt(X), rows, cols, ld, L.ptr(part), n, L.stream(X),
-           work={'bytes': rows * cols * X.element_size()})
-    return part, n
-
-
-def _operand_amax(X, rows_dim, k_dim, ld):
-    """amax partials of a GEMM operand with logical shape (rows_dim, k_dim) and strides ld =
-    (ld_rows, ld_k) — one of them 1."""
-    if ld[1] == 1:
-        return amax_partials(X, rows_dim, k_dim, ld[0])
-    return amax_partials(X, k_dim, rows_dim, ld[1])
-
-
-def weight_amax(W):
-    """amax partials of a whole weight tensor (any layout: the partition does not matter);
-    reused by every fp8 GEMM of one training step (the weights are fixed between optimizer
-    steps) inside ewvit.conv.packed()."""
-    from .conv import weight_amax_cache
-    cache = weight_amax_cache()
-    if cache is not None:
-        e = cache.get(id(W))
-        if e is not None and e[0] is W:
-            return e[1]
-    r = amax_partials(W, 1, W.numel(), W.numel()) if W.is_contiguous() else \
-        amax_partials(W.contiguous(), 1, W.numel(), W.numel())
-    if cache is not None:
-        cache[id(W)] = (W, r)
-    return r
-
-
 def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, aux=None,
-         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None, fp8=False,
-         amax_a=None, amax_b=None):
+         drop_p=0.0, seed=0, seed_offset=None, resid=None, ldr=0, splitk=None, fp8=False):
     """Raw C[M,N] = epi(alpha * A(M,K) @ B(K,N)).  lda = (lda_m, lda_k), ldb = (ldb_k, ldb_n).
     C must be contiguous with row stride N (ldc = C.stride(0)).
-    fp8=True: both operands rounded to OCP e4m3 after per-tensor scaling 448/amax (the amax of
-    each operand is reduced by one launch first unless its partials are given as amax_a /
-    amax_b = (partials, count); ewvit_gemm_fp8)."""
+    fp8=True: MXFP8 operands — every 32-element K run of a row of A / column of B rounded to
+    OCP e4m3 under its own power-of-two scale (ewvit_gemm_mx8, include/ewvit.h)."""
     L.require_gpu(A, B, C)
     if splitk is None:
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
@@ -86,12 +49,7 @@ def gemm(A, lda, B, ldb, C, M, N, K, *, alpha=1.0, beta=0.0, bias=None, act=0, a
             L.ptr(C), L.dt(C), C.stride(0), M, N, K, float(alpha), float(beta), L.ptr(bias), act,
             L.ptr(aux), float(drop_p), seed, L.ptr(seed_offset), L.ptr(resid),
             L.dt(resid) if resid is not None else 0, ldr, splitk, L.ptr(ws))
-    if fp8:
-        pa, na = amax_a if amax_a is not None else _operand_amax(A, M, K, lda)
-        pb, nb = amax_b if amax_b is not None else _operand_amax(B, N, K, (ldb[1], ldb[0]))
-        L.call('ewvit_gemm_fp8', *args, L.ptr(pa), na, L.ptr(pb), nb, L.stream(C), work=work)
-    else:
-        L.call('ewvit_gemm', *args, L.stream(C), work=work)
+    L.call('ewvit_gemm_mx8' if fp8 else 'ewvit_gemm', *args, L.stream(C), work=work)
     return C
 
 
@@ -115,7 +73,7 @@ def mm_nt(X, W, out, **kw):
     M, K = X.shape
     N = W.shape[0]
     assert X.stride(1) == 1 and W.stride(1) == 1
-    if _tallk(X, W, out, kw):
+    if not kw.get('fp8') and _tallk(X, W, out, kw):
         L.require_gpu(X, W, out)
         ws = torch.empty(int(L.load().ewvit_gemm_tallk_workspace(M, N, K)) // 4, dtype=torch.float32, device=X.device)
         bias = kw.get('bias')
@@ -168,7 +126,7 @@ def _linear_op(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     """y = dropout(act(x @ W^T + b)) + resid — nn.Linear (+ReLU/GELU/Dropout/residual) of
     network/sfe.py:29-55,127,134-142 and network/dama.py:25-31,105-113.
     -> (y [*, N], aux = bf16 pre-activation [M, N] (act 1/2 with need_aux, else empty),
-        x amax partials (fp8, else empty))."""
+        an empty float tensor (the per-tensor fp8 amax slot of ABI 2; MXFP8 needs none))."""
     L.require_gpu(x, weight)
     K = x.shape[-1]
     lead = x.shape[:-1]
@@ -178,14 +136,10 @@ def _linear_op(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     aux = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if (need_aux and act in (1, 2)) else None
     soff = L.rng_offset(x.device) if drop_p > 0 else None
     r2 = _c(resid.reshape(M, N)) if resid is not None else None
-    # fp8: the operands' amax partials are taken once and shared — X's by the forward and
-    # the weight gradient, the weight's by every GEMM of the step, dY's by both backward GEMMs
-    xa = amax_partials(x2, M, K, K) if fp8 else None
     mm_nt(x2, _c(weight), y, bias=bias, act=act, aux=aux, drop_p=drop_p, seed=seed, seed_offset=soff,
-          resid=r2, ldr=N if r2 is not None else 0, fp8=fp8, amax_a=xa,
-          amax_b=weight_amax(weight) if fp8 else None)
+          resid=r2, ldr=N if r2 is not None else 0, fp8=fp8)
     e = x.new_empty(_EMPTY, dtype=torch.float32)
-    return y.reshape(*lead, N), (aux if aux is not None else e.to(torch.bfloat16)), (xa[0] if fp8 else e.clone())
+    return y.reshape(*lead, N), (aux if aux is not None else e.to(torch.bfloat16)), e.clone()
 
 
 @_linear_op.register_fake
@@ -193,8 +147,7 @@ def _(x, weight, bias, act, drop_p, seed, resid, out_dtype, fp8, need_aux):
     M = x.numel() // x.shape[-1]
     N = weight.shape[0]
     aux = x.new_empty((M, N) if (need_aux and act in (1, 2)) else _EMPTY, dtype=torch.bfloat16)
-    xa = x.new_empty((int(max(1, min(L.AMAX_PARTS, (x.numel() + 16383) // 16384))),) if fp8 else _EMPTY,
-                     dtype=torch.float32)
+    xa = x.new_empty(_EMPTY, dtype=torch.float32)
     return x.new_empty((*x.shape[:-1], N), dtype=out_dtype), aux, xa
 
 
@@ -215,14 +168,12 @@ def _linear_backward_op(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor,
         soff = L.rng_offset(dy.device) if drop_p > 0 else None
         L.call('ewvit_act_bwd', L.ptr(dy2), L.dt(dy2), N, L.ptr(aux) if aux.numel() else None, act,
                float(drop_p), seed, L.ptr(soff), L.ptr(g), F32, M, N, L.stream(g))
-    ga = amax_partials(g, M, N, N) if fp8 and (need_dx or dw_out is not None) else None
     dx = dy.new_empty(_EMPTY, dtype=x.dtype)
     if need_dx:
-        dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=x.dtype, device=dy.device), fp8=fp8, amax_a=ga,
-                   amax_b=weight_amax(weight) if fp8 else None).reshape(x.shape)
+        dx = mm_nn(g, _c(weight), torch.empty(M, K, dtype=x.dtype, device=dy.device), fp8=fp8).reshape(x.shape)
     if dw_out is not None:
         dw = dw_out if dw_out.is_contiguous() else torch.empty(N, K, dtype=torch.float32, device=dy.device)
-        mm_tn(g, x2, dw, fp8=fp8, amax_a=ga, amax_b=(xa, xa.numel()) if fp8 else None)
+        mm_tn(g, x2, dw, fp8=fp8)
         if dw is not dw_out:
             dw_out.copy_(dw)
     if db_out is not None:
@@ -273,8 +224,8 @@ _linear_op.register_autograd(_linear_backward, setup_context=_linear_setup)
 def linear(x, weight, bias=None, act=0, drop_p=0.0, resid=None, out_dtype=torch.float32, fp8=False):
     """torch.ops.ewvit.linear with autograd.  act 0 none / 1 GELU(erf) / 2 ReLU; dropout and
     the residual add fused in the GEMM epilogue.  fp8=True: the forward and both backward
-    GEMMs take OCP e4m3 operands with per-tensor scaling (BASELINE configs[4]); the epilogue
-    (bias, activation, dropout, residual) is fp32."""
+    GEMMs take MXFP8 operands (OCP e4m3, one power-of-two scale per 32 K elements; BASELINE
+    configs[4]); the epilogue (bias, activation, dropout, residual) is fp32."""
     drop_p = float(drop_p)
     need_aux = act in (1, 2) and torch.is_grad_enabled() and (
         x.requires_grad or weight.requires_grad or (bias is not None and bias.requires_grad))

@@ -27,7 +27,7 @@ class _Params(ctypes.Structure):
     """include/ewvit.h ewvit_vit_layer."""
     _fields_ = [('ln1_w', _vp), ('ln1_b', _vp), ('wqkv', _vp), ('wo', _vp), ('bo', _vp), ('ln2_w', _vp),
                 ('ln2_b', _vp), ('w1', _vp), ('b1', _vp), ('w2', _vp), ('b2', _vp), ('ln_eps', _f32),
-                ('drop_p', _f32), ('seed', _u64), ('seed_off', _vp), ('packed', _vp)]
+                ('drop_p', _f32), ('seed', _u64), ('seed_off', _vp), ('packed', _vp), ('mx', ctypes.c_int)]
 
 
 class _Grads(ctypes.Structure):
@@ -56,31 +56,35 @@ def params_of(attn, ff):
             ff.norm.weight, ff.norm.bias, f.net[0].weight, f.net[0].bias, f.net[3].weight, f.net[3].bias]
 
 
-def _params(ts, eps, drop_p, seed, dev, packed=None):
+def _params(ts, eps, drop_p, seed, dev, packed=None, mx=False):
     p = _Params(*[t.data_ptr() for t in ts])
     p.ln_eps, p.drop_p, p.seed = float(eps), float(drop_p), int(seed)
     p.seed_off = L.rng_offset(dev).data_ptr() if drop_p > 0 else None
     p.packed = packed
+    p.mx = int(bool(mx))
     return p
 
 
 PACK_MAX = 8     # EWVIT_VIT_PACK_MAX
 
 
-def pack(layers):
-    """The bf16 GEMM operands of the given (attn, ff) layers — to_qkv, to_out, Linear1, Linear2,
-    each in its own layout and transposed — packed by one launch (ewvit_vit_pack), once per
-    forward; returns the buffer (one block of ewvit_vit_layer_workspace(2) bytes per layer)."""
+def pack(layers, mx=False):
+    """The GEMM operands of the given (attn, ff) layers — to_qkv, to_out, Linear1, Linear2,
+    each in its own layout and transposed — packed by one launch once per forward: bf16
+    (ewvit_vit_pack), or MXFP8 for fp8 token GEMMs (mx=True, ewvit_vit_pack_mx: e4m3 with one
+    E8M0 scale per 32 elements along each image's K).  Returns the buffer (one block of
+    ewvit_vit_layer_workspace(2 | 3) bytes per layer)."""
     assert 1 <= len(layers) <= PACK_MAX
     ts0 = params_of(*layers[0])
     dev = ts0[0].device
-    blk = _ws_bytes(2)
+    blk = _ws_bytes(3 if mx else 2)
     buf = torch.empty(len(layers) * blk, dtype=torch.uint8, device=dev)
     arr = (_Params * len(layers))()
     for i, (attn, ff) in enumerate(layers):
         arr[i] = _params(params_of(attn, ff), 0.0, 0.0, 0, dev)
-    L.call('ewvit_vit_pack', ctypes.addressof(arr), len(layers), L.ptr(buf), L.stream(buf),
-           work={'bytes': 6.0 * len(layers) * blk / 2})
+    nw = sum(t.numel() for t in params_of(*layers[0])[2:] if t.dim() == 2) * len(layers)
+    L.call('ewvit_vit_pack_mx' if mx else 'ewvit_vit_pack', ctypes.addressof(arr), len(layers), L.ptr(buf),
+           L.stream(buf), work={'bytes': 4.0 * nw + len(layers) * blk})
     return buf
 
 
@@ -88,15 +92,15 @@ class ViTLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, x0, *ts):
         L.require_gpu(x0, *ts)
-        eps, drop_p, seed, buf, idx = cfg
+        eps, drop_p, seed, buf, idx, mx = cfg
         B = x0.shape[0]
         R = 2 * B
         x0c = x0.float().contiguous()
         dev = x0.device
         saved = torch.empty(_ws_bytes(0), dtype=torch.uint8, device=dev)
         x2 = torch.empty_like(x0c)
-        pk = buf.data_ptr() + idx * _ws_bytes(2)
-        p = _params(ts, eps, drop_p, seed, dev, pk)
+        pk = buf.data_ptr() + idx * _ws_bytes(3 if mx else 2)
+        p = _params(ts, eps, drop_p, seed, dev, pk, mx)
         ctx.gen = grads.note_use(ts[0])
         for t in ts[1:]:
             grads.note_use(t)
@@ -109,7 +113,7 @@ class ViTLayerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x0c, saved = ctx.saved_tensors
-        eps, drop_p, seed, buf, idx = ctx.cfg
+        eps, drop_p, seed, buf, idx, mx = ctx.cfg
         ts, R = ctx.ts, ctx.R
         dev = x0c.device
         gc = g.float().contiguous()
@@ -120,7 +124,7 @@ class ViTLayerFn(torch.autograd.Function):
             # the kernels write every parameter gradient; a frozen one gets a scratch tensor
             o = grad_out(t, ctx.gen) if ctx.needs_input_grad[2 + k] else torch.empty_like(t)
             outs.append(o if o.is_contiguous() else torch.empty_like(t, memory_format=torch.contiguous_format))
-        p = _params(ts, eps, drop_p, seed, dev, ctx.pk)
+        p = _params(ts, eps, drop_p, seed, dev, ctx.pk, mx)
         G = _Grads(*[o.data_ptr() for o in outs])
         L.call('ewvit_vit_layer_bwd', ctypes.addressof(p), R, L.ptr(x0c), L.ptr(saved), L.ptr(gc), L.ptr(scratch),
                L.ptr(dx0), ctypes.addressof(G), L.stream(dx0),
@@ -129,13 +133,13 @@ class ViTLayerFn(torch.autograd.Function):
                                               for k, (t, o) in enumerate(zip(ts, outs))])
 
 
-def vit_layer(attn, ff, x, training, packed, idx):
+def vit_layer(attn, ff, x, training, packed, idx, mx=False):
     """x [B, 2, 512] -> the layer's output [B, 2, 512] f32 (ViTLayerFn with the layer's
-    parameters and block `idx` of `packed` (ewvit.vit.pack); the to_out dropout draws its host
-    seed as the module path's Linear does)."""
+    parameters and block `idx` of `packed` (ewvit.vit.pack, MXFP8 GEMMs when mx); the to_out
+    dropout draws its host seed as the module path's Linear does)."""
     from .ops import _seed
     drop = attn.fn.to_out[1].p if training else 0.0
-    cfg = (attn.norm.eps, float(drop), _seed() if drop > 0 else 0, packed, int(idx))
+    cfg = (attn.norm.eps, float(drop), _seed() if drop > 0 else 0, packed, int(idx), bool(mx))
     return ViTLayerFn.apply(cfg, x, *params_of(attn, ff))
 
 

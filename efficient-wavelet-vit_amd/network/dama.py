@@ -226,11 +226,13 @@ class DAMA(nn.Module):                                                     # dam
         """The shape class of ewvit.head (csrc/head.hip): dim 128, 2 bidirectional layers of
         4 x 32-head cross-attention, <= 64 frames of 1x1 maps, the reference's fusion / gate
         modules, no hooks or patched forwards anywhere in the head (the tools of
-        utils/visualize_feature_maps.py hook and patch them), bf16 token GEMMs."""
+        utils/visualize_feature_maps.py hook and patch them), the 12 attention Linears on one
+        GEMM precision.  Returns that precision ('bf16' | 'fp8': MXFP8) or False."""
         if not (space.is_cuda and space.shape[-2:] == (1, 1) and freq.shape[-2:] == (1, 1) and self.dim == 128
                 and space.shape[0] <= 64 and type(self.cross_att).forward is BidirectionalCrossTransformer.forward
                 and len(self.cross_att.layers) == 2):
             return False
+        precs = set()
         mods = [self.cross_att, self.fusion_gate, self.gate_net]
         for layer in self.cross_att.layers:
             mods.append(layer)
@@ -238,9 +240,9 @@ class DAMA(nn.Module):                                                     # dam
                 mods.append(m)
             for att in (layer[1], layer[3]):
                 if (type(att) is not CrossAttention or type(att).forward is not _CA_FORWARD or 'forward' in att.__dict__
-                        or att.heads != 4 or att.dim_head != 32 or not isinstance(att.to_out, nn.Sequential)
-                        or any(_fp8(t) for t in (att.to_q, att.to_kv, att.to_out[0]))):
+                        or att.heads != 4 or att.dim_head != 32 or not isinstance(att.to_out, nn.Sequential)):
                     return False
+                precs.update('fp8' if _fp8(t) else 'bf16' for t in (att.to_q, att.to_kv, att.to_out[0]))
                 mods += [att.to_q, att.to_kv, att.to_out, att.to_out[0], att.to_out[1]]
             if not all(type(layer[j]) in (LayerNorm, nn.LayerNorm) and layer[j].normalized_shape == (128,)
                        and layer[j].elementwise_affine for j in (0, 2)):
@@ -253,18 +255,21 @@ class DAMA(nn.Module):                                                     # dam
                 or tuple(g[5].weight.shape) != (3, 64) or g[2].bias is None or g[5].bias is None):
             return False
         mods += list(self.fusion_gate) + list(g)
-        return not any(_hooked(m) for m in mods)
+        if len(precs) != 1 or any(_hooked(m) for m in mods):
+            return False
+        return precs.pop()
 
     @bf16_compute
     def _process_frame(self, frame):
         B = frame.shape[0]
         space_feats, freq_feats = self._branches(frame)
-        if self._head_fusable(space_feats, freq_feats):
+        prec = self._head_fusable(space_feats, freq_feats)
+        if prec:
             # cross-attention, fusion gate, gate net and weighted sum: ewvit.head (3 launches
-            # forward + backward instead of ~90)
+            # forward + backward instead of ~90; MXFP8 attention GEMMs for fp8 token GEMMs)
             drop = self.training and (self.cross_att.layers[0][1].to_out[1].p > 0 or self.gate_net[4].p > 0)
             fused, s, f = ewvit.head.dama_head(self, space_feats.reshape(B, -1), freq_feats.reshape(B, -1),
-                                               ewvit.ops._seed() if drop else 0)
+                                               ewvit.ops._seed() if drop else 0, mx=prec == 'fp8')
             return {'fused': fused, 'space': s, 'freq': f}
         Ho, Wo = space_feats.shape[-2:]
         s_flat = space_feats.flatten(2).transpose(1, 2)

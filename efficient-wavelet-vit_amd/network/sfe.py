@@ -135,17 +135,20 @@ class Transformer(nn.Module):                                              # sfe
 
     def forward(self, x):
         x = x.float()
-        fused = [_vit_fusable(attn, ff, x) for attn, ff in self.layers]
-        packed, slot = None, {}
-        if any(fused):
-            # the fused layers' bf16 weights (both orientations), one launch (ewvit.vit.pack)
-            sel = [i for i, f in enumerate(fused) if f][:ewvit.vit.PACK_MAX]
-            packed = ewvit.vit.pack([tuple(self.layers[i]) for i in sel])
-            slot = {i: k for k, i in enumerate(sel)}
+        fused = [_vit_fusable(attn, ff, x) for attn, ff in self.layers]     # None | 'bf16' | 'fp8'
+        slot = {}
+        for prec in ('bf16', 'fp8'):
+            sel = [i for i, f in enumerate(fused) if f == prec][:ewvit.vit.PACK_MAX]
+            if sel:
+                # the fused layers' GEMM weights (both orientations; bf16, or MXFP8 for fp8 token
+                # GEMMs), one launch per precision (ewvit.vit.pack)
+                mx = prec == 'fp8'
+                packed = ewvit.vit.pack([tuple(self.layers[i]) for i in sel], mx=mx)
+                slot.update({i: (packed, k, mx) for k, i in enumerate(sel)})
         for i, (attn, ff) in enumerate(self.layers):
             if i in slot:
                 # the layer on csrc/vit.hip: 4 launches forward, 5 backward (ewvit.vit)
-                x = ewvit.vit.vit_layer(attn, ff, x, self.training, packed, slot[i])
+                x = ewvit.vit.vit_layer(attn, ff, x, self.training, *slot[i])
                 continue
             x = attn.forward_residual(x)
             x = ff.forward_residual(x)
@@ -156,9 +159,10 @@ class Transformer(nn.Module):                                              # sfe
 def _vit_fusable(attn, ff, x):
     """The shape class of ewvit.vit (csrc/vit.hip): dim 512, 8 heads of 64, mlp 2048, 2 tokens
     per frame, <= 64 frames, the reference's module structure (no hooks or patched forwards,
-    the FeedForward's dropouts 0 or eval), bf16 token GEMMs."""
+    the FeedForward's dropouts 0 or eval), the four Linears on one GEMM precision.  Returns
+    that precision ('bf16' | 'fp8': MXFP8, network.set_gemm_precision) or None."""
     if torch.compiler.is_compiling():        # traced (torch.compile): the custom-op module path
-        return False
+        return None
     if not (ewvit.vit.enabled() and x.is_cuda and x.dim() == 3 and x.shape[1] == 2 and x.shape[2] == 512
             and 1 <= x.shape[0] <= 64):
         return False
@@ -171,7 +175,10 @@ def _vit_fusable(attn, ff, x):
             or not isinstance(f.net[1], nn.GELU) or f.net[1].approximate != 'none'):
         return False
     lins = (a.to_qkv, a.to_out[0], f.net[0], f.net[3])
-    if any(type(m) is not Linear or _fp8(m) for m in lins) or a.to_qkv.bias is not None:
+    if any(type(m) is not Linear for m in lins) or a.to_qkv.bias is not None:
+        return False
+    prec = {('fp8' if _fp8(m) else 'bf16') for m in lins}
+    if len(prec) != 1:
         return False
     if (tuple(a.to_qkv.weight.shape) != (1536, 512) or tuple(a.to_out[0].weight.shape) != (512, 512)
             or tuple(f.net[0].weight.shape) != (2048, 512) or tuple(f.net[3].weight.shape) != (512, 2048)):
@@ -187,7 +194,7 @@ def _vit_fusable(attn, ff, x):
     if any(t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda for t in ts):
         return False
     mods = [attn, ff, a, f, attn.norm, ff.norm, a.to_qkv, a.to_out, *a.to_out, *f.net]
-    return not any(_hooked(m) for m in mods)
+    return None if any(_hooked(m) for m in mods) else prec.pop()
 
 
 class EfficientViT(nn.Module):                                             # sfe.py:87-173

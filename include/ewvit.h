@@ -32,7 +32,6 @@ extern "C" {
 #define EWVIT_EINVAL 1000
 #define EWVIT_ADAM_MAX 48   /* tensors per ewvit_adam_step launch */
 #define EWVIT_PACK_MAX 32   /* weights per ewvit_conv2d_pack_weights launch */
-#define EWVIT_AMAX_PARTS 256 /* partial maxima per ewvit_amax_partials result */
 
 int ewvit_abi_version(void);
 const char *ewvit_last_error(void);
@@ -110,25 +109,20 @@ int ewvit_gemm(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const v
                const void *resid, int resid_dtype, int64_t ldr, int splitk, float *workspace,
                void *stream);
 
-/* fp8 (BASELINE configs[4]): ewvit_gemm with both operands rounded to OCP e4m3fn
- * (v_mfma_f32_16x16x32_fp8_fp8, fp32 accumulation) after per-tensor scaling s = 448 / amax:
- * C = epi(alpha * sum_k q(A*sa) q(B*sb) / (sa*sb)).  a_amax / b_amax: partial maxima of |A|
- * and |B| over the whole operand (ewvit_amax_partials, <= EWVIT_AMAX_PARTS each), folded by
- * every workgroup in its prologue — so the scaling is current (this call's operands) and the
- * call stays graph-capturable.  Replaces the bf16 GEMMs of the ViT attention / MLP
- * (sfe.py:29-70), the cross-attention projections (dama.py:15-53) and patch_to_embedding
- * (sfe.py:127,155) when the model runs in fp8 (ewvit.set_gemm_precision). */
-int ewvit_gemm_fp8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B, int b_dtype,
+/* fp8 (BASELINE configs[4]): ewvit_gemm with MXFP8 operands — each run of 32 consecutive K
+ * elements of a row of A (and of a column of B) quantized to OCP e4m3fn with one shared E8M0
+ * scale 2^X, X the smallest with max|run| <= 448 * 2^X (round to nearest even, no saturation
+ * needed) — multiplied on v_mfma_scale_f32_16x16x128_f8f6f4 with fp32 accumulation:
+ * C = epi(alpha * sum_k q(A)(m,k) sa(m,k/32) q(B)(k,n) sb(k/32,n)).  The scales are computed
+ * from the operands as they are staged (no amax pass; graph-capturable).  Replaces the bf16
+ * GEMMs of the ViT attention / MLP (sfe.py:29-70), the cross-attention projections
+ * (dama.py:15-53) and patch_to_embedding / feat_map (sfe.py:127,155,168) when the model runs in
+ * fp8 (network.set_gemm_precision) on the module path; same arguments as ewvit_gemm. */
+int ewvit_gemm_mx8(const void *A, int a_dtype, int64_t lda_m, int64_t lda_k, const void *B, int b_dtype,
                    int64_t ldb_k, int64_t ldb_n, void *C, int c_dtype, int64_t ldc, int64_t M, int64_t N, int64_t K,
                    float alpha, float beta, const float *bias, int act, void *aux, float drop_p, uint64_t seed,
                    const int64_t *seed_offset, const void *resid, int resid_dtype, int64_t ldr, int splitk,
-                   float *workspace, const float *a_amax, int a_nparts, const float *b_amax, int b_nparts,
-                   void *stream);
-
-/* max |x| over a [rows x cols] matrix (row stride ld, f32/bf16) as `nparts` partial maxima
- * (workgroup i reduces rows [i*ceil(rows/nparts), ...)); nparts <= EWVIT_AMAX_PARTS. */
-int ewvit_amax_partials(const void *x, int dtype, int64_t rows, int64_t cols, int64_t ld, float *part, int nparts,
-                        void *stream);
+                   float *workspace, void *stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n]  (bias gradients).  accumulate!=0 adds. */
 /* C[M][N] f32 = A[M][K] (bf16, row stride lda) x W[N][K]^T (fp32, rounded to bf16) + bias (may be
@@ -394,6 +388,9 @@ int ewvit_conv2d_set_lds_pad(int on);
  * row per wave group); returns the previous setting.  Results are bit-identical in every form
  * (same per-output MFMA chain).  Env: EWVIT_WGWIN_TS=0 / 2. */
 int ewvit_conv2d_set_wgrad_tap_split(int on);
+/* A/B: the non-temporal cache hint on the windowed MWT convs' activation-window DMAs (1) or not
+ * (0, the default); returns the previous setting.  Env: EWVIT_WIN_NT. */
+int ewvit_conv2d_set_win_nt(int on);
 /* A/B: level-1 pixels per thread in flight in ewvit_dwt_hf_upsample_fused (2, the default, or 4); returns the previous. */
 int ewvit_dwt_set_pf(int pf);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
@@ -747,11 +744,18 @@ typedef struct {
   float ln_eps;
   void *packed;               /* ewvit_head_pack_bytes() of scratch: the weights as bf16, packed
                                * by ewvit_head_fwd and read by it and by ewvit_head_bwd */
+  void *packed_mx;            /* NULL: bf16 attention GEMMs; else ewvit_head_pack_bytes_mx() of
+                               * scratch: to_q / to_kv / to_out as MXFP8 (ewvit_gemm_mx8's
+                               * format, both orientations), packed by ewvit_head_fwd — every
+                               * attention-block GEMM (fwd, input and weight gradients) then runs
+                               * on MXFP8 operands (configs[4]); the fusion conv / gate stay bf16 */
 } ewvit_head_params;
 /* bytes of fp32 workspace the head needs (what the forward saves for the backward) */
 int64_t ewvit_head_workspace(void);
 /* bytes of the bf16 weight pack (ewvit_head_params.packed) */
 int64_t ewvit_head_pack_bytes(void);
+/* bytes of the MXFP8 attention-weight pack (ewvit_head_params.packed_mx) */
+int64_t ewvit_head_pack_bytes_mx(void);
 /* s0, f0 [N][128] f32: the space / freq tokens (one per frame) -> fused, s_out, f_out [N][128]
  * (dama.py:165-169's fused / space / freq per frame); the workspace keeps what the backward
  * reads; one workgroup. */
@@ -790,13 +794,18 @@ typedef struct {
   float ln_eps, drop_p;         /* LayerNorm eps; to_out dropout probability (0 in eval) */
   uint64_t seed;
   const int64_t *seed_off;
-  const void *packed;           /* this layer's block of ewvit_vit_pack's output (bf16 weights) */
+  const void *packed;           /* this layer's block of ewvit_vit_pack's output (bf16 weights), or
+                                   of ewvit_vit_pack_mx's when mx != 0 */
+  int mx;                       /* 1: every GEMM of the layer on MXFP8 operands (configs[4]; see
+                                   ewvit_gemm_mx8): weights from the MX pack, activations and
+                                   gradients block-quantized by the kernels that form their
+                                   fragments, fp32 accumulation; 0: bf16 */
 } ewvit_vit_layer;
 typedef struct {                /* parameter gradients (overwritten), parameter layouts */
   float *ln1_w, *ln1_b, *wqkv, *wo, *bo, *ln2_w, *ln2_b, *w1, *b1, *w2, *b2;
 } ewvit_vit_grads;
-/* bytes of the forward's saved state (which = 0), of the backward's scratch (which = 1) and of
- * one layer's packed weights (which = 2) */
+/* bytes of the forward's saved state (which = 0), of the backward's scratch (which = 1), of
+ * one layer's packed bf16 weights (which = 2) and of one layer's MXFP8 pack (which = 3) */
 int64_t ewvit_vit_layer_workspace(int which);
 #define EWVIT_VIT_PACK_MAX 8
 /* The n <= EWVIT_VIT_PACK_MAX layers' to_qkv / to_out / Linear1 / Linear2 weights (fp32, read
@@ -804,6 +813,11 @@ int64_t ewvit_vit_layer_workspace(int which);
  * ewvit_vit_layer_workspace(2) bytes: the GEMM operands of ewvit_vit_layer_fwd / _bwd, packed
  * once per step (the module path rounds the same weights to bf16 inside every GEMM). */
 int ewvit_vit_pack(const ewvit_vit_layer *layers, int n, void *packed, void *stream);
+/* The same weights as MXFP8 (ewvit_gemm_mx8's format) into n blocks of
+ * ewvit_vit_layer_workspace(3) bytes: per weight W [out][in] the e4m3 image with one E8M0 scale
+ * per 32 consecutive `in` elements, and W^T [in][out] with one per 32 `out` elements (the K of
+ * the forward and of the input-gradient GEMMs), quantized once per step from the fp32 masters. */
+int ewvit_vit_pack_mx(const ewvit_vit_layer *layers, int n, void *packed, void *stream);
 /* x0 [R][512] f32 -> x2 [R][512] f32; `saved` (ewvit_vit_layer_workspace(0) bytes) keeps what
  * the backward reads (LayerNorm statistics, qkv, softmax weights, the GEMM operands). */
 int ewvit_vit_layer_fwd(const ewvit_vit_layer *p, int R, const float *x0, void *saved, float *x2, void *stream);

@@ -13,7 +13,7 @@ def _row(tfs, gbs):
 
 def test_fp8_gemm_priced_against_fp8_peak():
     import bench
-    r = bench.roofline_for('ewvit_gemm_fp8', _row(500.0, 0.0), config=5)
+    r = bench.roofline_for('ewvit_gemm_mx8', _row(500.0, 0.0), config=5)
     assert r['bound'] == 'mfma' and r['peak'] == bench.FP8_PEAK_TFS == 5000.0
     assert abs(r['frac'] - 0.1) < 1e-9
 

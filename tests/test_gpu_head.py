@@ -198,3 +198,49 @@ def test_head_refused_for_hooked_modules():
     assert not m._head_fusable(s, s)
     h.remove()
     assert m._head_fusable(s, s)
+
+
+@pytest.mark.parametrize('N', [64, 21])
+def test_head_mxfp8_vs_module_path_mxfp8(N, monkeypatch):
+    """fp8 token GEMMs: the fused head with its 4 attention blocks' GEMMs on MXFP8 operands
+    (ewvit_head_pack_bytes_mx, the MX forms of csrc/head.hip) against the module path on
+    ewvit_gemm_mx8 (the same block format, quantized from differently rounded intermediates:
+    the fused kernels keep q / kv / the weight-gradient operands in fp32, the module path stores
+    them in bf16), both measured against the bf16 fused head on the same parameters and inputs:
+    the fused MXFP8 head's distance to the bf16 run is at most 1.5x the module path's (max
+    error of scale and the cosine gap, outputs, input and parameter gradients), inside floors
+    (outputs 6e-2 of scale / cosine 0.998, gradients cosine 0.98)."""
+    import copy
+    from network import set_gemm_precision
+    m0 = _dama(True)
+    ref = copy.deepcopy(m0)
+    assert set_gemm_precision(m0, 'fp8') >= 12
+    g = torch.Generator().manual_seed(N + 3)
+    s0 = (torch.randn(N, 128, generator=g) * 2).to(DEV)
+    f0 = torch.randn(N, 128, generator=g).to(DEV)
+    a, b = copy.deepcopy(m0), copy.deepcopy(m0)
+    oa, dsa, dfa, ga, _, ca = _run(a, s0, f0, True, monkeypatch)
+    ob, dsb, dfb, gb, _, cb = _run(b, s0, f0, False, monkeypatch)
+    oc, dsc, dfc, gc, _, cc = _run(ref, s0, f0, True, monkeypatch)
+    assert ca.get('ewvit_head_fwd') == 1 and 'ewvit_gemm_mx8' not in ca and 'ewvit_gemm' not in ca, ca
+    assert cb.get('ewvit_gemm_mx8', 0) >= 36, cb
+    assert cc.get('ewvit_head_fwd') == 1 and 'ewvit_gemm_mx8' not in cc, cc
+
+    def err(u, v):
+        return float((u - v).abs().max()) / max(float(v.abs().max()), 1e-30), _cos(u, v)
+    fails = []
+
+    def judge(name, ea, eb, floor_err, floor_cos):
+        ok = (ea[0] <= max(1.5 * eb[0], 1e-3) and (1 - ea[1]) <= max(1.5 * (1 - eb[1]), 1e-6)
+              and ea[0] <= floor_err and ea[1] >= floor_cos)
+        if not ok:
+            fails.append((name, ea, eb))
+    for k in oc:
+        judge(k, err(oa[k], oc[k]), err(ob[k], oc[k]), 6e-2, 0.998)
+    judge('d s0', err(dsa, dsc), err(dsb, dsc), 1.0, 0.98)
+    judge('d f0', err(dfa, dfc), err(dfb, dfc), 1.0, 0.98)
+    for n in gc:
+        if n.endswith('fusion_gate.0.bias'):          # feeds a train-mode BatchNorm: exact zero + noise
+            continue
+        judge(n, err(ga[n], gc[n]), err(gb[n], gc[n]), 1.0, 0.98)
+    assert not fails, fails

@@ -178,3 +178,32 @@ def test_tallk_gemm_patch_embedding_shape(M):
     y2 = torch.empty_like(y)
     ewvit.mm_nt(x, w, y2, bias=b, splitk=64)            # the generic split-K path
     assert float((y - y2).abs().max()) <= 1e-4 * scale
+
+
+@pytest.mark.parametrize('N', [64, 37, 1])
+def test_vit_layer_mxfp8_matches_module_path(N, monkeypatch):
+    """fp8 token GEMMs (network.set_gemm_precision 'fp8', configs[4]): the fused layer on MXFP8
+    operands (ewvit_vit_pack_mx + the MX kernels of csrc/vit.hip) against the module path, whose
+    Linears run ewvit_gemm_mx8 — the same block format, quantized from the same activations
+    except where the fused kernels keep them in fp32 (LayerNorm outputs, the attention output,
+    the LN2-backward gradient) and the module path has them in bf16, so single e4m3 roundings
+    differ.  Bounds: outputs 3e-2 of scale / cosine >= 0.999, gradients cosine >= 0.995 with
+    norms within 2 %; no bf16 GEMM runs on either side."""
+    from network import set_gemm_precision
+    m0 = _vit(0.0).train()
+    assert set_gemm_precision(m0, 'fp8') == 8
+    g = torch.Generator().manual_seed(N + 1)
+    x0 = (torch.randn(N, 2, 512, generator=g) * 1.5 + 0.3).to(DEV)
+    a, b = copy.deepcopy(m0), copy.deepcopy(m0)
+    ya, dxa, ga, ca = _run(a, x0, True, monkeypatch)
+    yb, dxb, gb, cb = _run(b, x0, False, monkeypatch)
+    assert ca.get('ewvit_vit_layer_fwd') == 2 and ca.get('ewvit_vit_pack_mx') == 1, ca
+    assert 'ewvit_gemm' not in ca and 'ewvit_gemm' not in cb and cb.get('ewvit_gemm_mx8', 0) >= 24, (ca, cb)
+    scale = float(yb.abs().max())
+    err = float((ya - yb).abs().max())
+    assert err <= 3e-2 * scale and _cos(ya, yb) >= 0.999, (err, scale, _cos(ya, yb))
+    assert _cos(dxa, dxb) >= 0.995
+    for n in gb:
+        c = _cos(ga[n], gb[n])
+        r = float(ga[n].norm() / gb[n].norm())
+        assert c >= 0.995 and abs(r - 1) < 2e-2, (n, c, r)
