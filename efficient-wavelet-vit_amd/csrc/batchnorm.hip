@@ -35,14 +35,38 @@ template <int DT> struct Raw8;
 template <> struct Raw8<EWVIT_BF16> { uint4 q; };
 template <> struct Raw8<EWVIT_F32> { float4 a, b; };
 
-template <int DT>
+// NT: the non-temporal hint (global_load / global_store ... nt) — the ReLU instantiations are
+// the MWT's BatchNorms over 0.2-2.4 M-row maps, streamed once per pass with no L2 reuse; the hint
+// keeps them from displacing the concurrent backbone's L2 lines (the windowed convs' window DMAs
+// carry it too, convwin.hip g_win_nt)
+typedef unsigned bn_v4u __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ldq16(const void *p) {
+  if constexpr (NT && EWVIT_MWT_NT) {
+    const bn_v4u v = __builtin_nontemporal_load(reinterpret_cast<const bn_v4u *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4 *>(p);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void stq16(void *p, uint4 v) {
+  if constexpr (NT && EWVIT_MWT_NT) {
+    __builtin_nontemporal_store(bn_v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<bn_v4u *>(p));
+  } else {
+    *reinterpret_cast<uint4 *>(p) = v;
+  }
+}
+template <int DT, bool NT = false>
 __device__ __forceinline__ Raw8<DT> ldraw(const void *p, int64_t i) {
   Raw8<DT> r;
   if constexpr (DT == EWVIT_BF16) {
-    r.q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16_t *>(p) + i);
+    r.q = ldq16<NT>(reinterpret_cast<const bf16_t *>(p) + i);
   } else {
-    const float4 *q = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + i);
-    r.a = q[0]; r.b = q[1];
+    const float *f = reinterpret_cast<const float *>(p) + i;
+    const uint4 a = ldq16<NT>(f), b = ldq16<NT>(f + 4);
+    r.a = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+    r.b = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
   }
   return r;
 }
@@ -76,17 +100,17 @@ __device__ __forceinline__ void ld8(const void *p, int64_t i, float (&v)[8]) {
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   }
 }
-template <int DT>
+template <int DT, bool NT = false>
 __device__ __forceinline__ void st8(void *p, int64_t i, const float (&v)[8]) {
   if (DT == EWVIT_BF16) {
     unsigned w[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf(v[2 * j]) | ((unsigned)f2bf(v[2 * j + 1]) << 16);
-    *reinterpret_cast<uint4 *>(reinterpret_cast<bf16_t *>(p) + i) = make_uint4(w[0], w[1], w[2], w[3]);
+    stq16<NT>(reinterpret_cast<bf16_t *>(p) + i, make_uint4(w[0], w[1], w[2], w[3]));
   } else {
-    float4 *q = reinterpret_cast<float4 *>(reinterpret_cast<float *>(p) + i);
-    q[0] = make_float4(v[0], v[1], v[2], v[3]);
-    q[1] = make_float4(v[4], v[5], v[6], v[7]);
+    float *f = reinterpret_cast<float *>(p) + i;
+    stq16<NT>(f, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
+    stq16<NT>(f + 4, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])));
   }
 }
 
@@ -434,13 +458,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void *__restrict__ 
   };
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < Mg ? r0 + rpb : Mg;
   if constexpr (!DROP) {
-    row_walk_pf<8>(active, r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT>(x, goff + rr * C + c); },
+    row_walk_pf<8>(active, r0, r1, rg, RG, [&](int64_t rr) { return ldraw<DT, ACT == 1>(x, goff + rr * C + c); },
                    [&](int64_t rr, const Raw8<DT> &raw) {
       float v[8];
       unpack<DT>(raw, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(fmaf(v[j], sc[j], sh[j]));
-      st8<DT>(y, goff + rr * C + c, v);
+      st8<DT, ACT == 1>(y, goff + rr * C + c, v);
     }, fin);
   } else {
     const uint64_t sd = step_seed(dr.seed, dr.seed_offset);
@@ -547,7 +571,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const void *__restri
   if (active) {
     row_walk<8>(r0, r1, rg, RG,
                 [&](int64_t rr) {
-                  return Raw8x2s<DT>{ldraw<DT>(x, rr * C + c8 * 8), ldraw<DT>(dy, rr * C + c8 * 8),
+                  return Raw8x2s<DT>{ldraw<DT, ACT == 1>(x, rr * C + c8 * 8), ldraw<DT, ACT == 1>(dy, rr * C + c8 * 8),
                                      SC == 1 ? rscale[(int)rr / HW] : 1.f};
                 },
                 [&](int64_t rr, const Raw8x2s<DT> &raw) {
@@ -640,7 +664,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
   if constexpr (SC == 2) ltab = se_stage(tab, rscale, se_g, r0, r1, HW, C, ch0, nch_c, f0);
   row_walk_pf<8>(active, r0, r1, rg, RG,
                  [&](int64_t rr) {
-                   return Raw8x2s<DT>{ldraw<DT>(x, goff + rr * C + c), ldraw<DT>(dy, goff + rr * C + c),
+                   return Raw8x2s<DT>{ldraw<DT, ACT == 1>(x, goff + rr * C + c), ldraw<DT, ACT == 1>(dy, goff + rr * C + c),
                                       SC == 1 ? rscale[(int)rr / HW] : 1.f};
                  },
                  [&](int64_t rr, const Raw8x2s<DT> &raw) {
@@ -658,7 +682,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const void *__restrict__
       const float g = ACT ? vd[j] * act_grad<ACT>(fmaf(xh, ga[j], be[j])) : vd[j];
       o[j] = ga[j] * iv[j] * (g - c0[j] - xh * c1[j]);
     }
-    st8<DT>(dx, goff + rr * C + c, o);
+    st8<DT, ACT == 1>(dx, goff + rr * C + c, o);
   }, fin);
 }
 

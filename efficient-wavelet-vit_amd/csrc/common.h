@@ -7,6 +7,12 @@
 
 #include "../../include/ewvit.h"
 
+// the non-temporal cache hint on the MWT branch's streaming loads / stores (windowed convs,
+// seperate conv, the ReLU BatchNorm passes): 1 (default); A/B builds compile with -DEWVIT_MWT_NT=0
+#ifndef EWVIT_MWT_NT
+#define EWVIT_MWT_NT 1
+#endif
+
 namespace ewvit {
 
 // ---------------------------------------------------------------- errors

@@ -49,8 +49,11 @@ int g_win = 1;
 // 3627 -> 3636-3646 frames/s (same box, profiles/r05/ab/lds_pad.log).  EWVIT_LDS_PAD=0 /
 // ewvit_conv2d_set_lds_pad(0): their own footprint.
 int g_lds_pad = 1;
-// the non-temporal hint on the windowed kernels' activation-window DMAs (A/B; 0 = off)
-int g_win_nt = 0;
+// the non-temporal hint on the windowed kernels' activation-window DMAs (the windows stream
+// through once per tile; the hint keeps them from displacing the concurrent backbone's L2 lines):
+// config 2 +0.26 / +0.34 / +0.63 % in three interleaved same-box rounds and +0.7 / +0.5 % on
+// another box (profiles/r06/ab/win_nt*.log); EWVIT_WIN_NT=0 / ewvit_conv2d_set_win_nt(0): off
+int g_win_nt = EWVIT_MWT_NT;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
   if (!g_lds_pad || stat >= 160 * 1024) return 0;
@@ -89,6 +92,11 @@ template <int N> __device__ __forceinline__ void win_sync() {
 typedef __attribute__((ext_vector_type(2))) unsigned int cu32x2;
 __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, uint2 v, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b64(cu32x2{v.x, v.y}, r, off, 0, 0);
+}
+// ... with the non-temporal hint (aux 2 = nt on gfx950) when `nt` (uniform): the MWT's output maps
+__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, uint2 v, uint32_t off, bool nt) {
+  if (nt) __builtin_amdgcn_raw_buffer_store_b64(cu32x2{v.x, v.y}, r, off, 0, 2);
+  else __builtin_amdgcn_raw_buffer_store_b64(cu32x2{v.x, v.y}, r, off, 0, 0);
 }
 __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, float v, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
@@ -342,7 +350,8 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       for (int i = 0; i < NER; ++i) {
         const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + ER0 + i) * W + d.ow0 + fr;
         const uint32_t off = d.last ? (uint32_t)((pix * a.ogc + cbase) * 2) : OOB;
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
+        if (a.nt) asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
+        else asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
       }
     }
   };
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         uint2 pk;
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
-        bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2));
+        bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2), a.nt != 0);
         if constexpr (BST) {
           const float hv[4] = {bf2f(h0), bf2f(h1), bf2f(h2), bf2f(h3)};
           const float xv[4] = {__uint_as_float(xq[j][i].x << 16), __uint_as_float(xq[j][i].x & 0xffff0000u),

@@ -18,6 +18,8 @@
 // gemm_mx8_kernel: the same contract with MXFP8 operands (mx8.h: e4m3 elements, one E8M0
 // scale per 32 consecutive K elements, quantized from the f32 / bf16 operands while staging)
 // on v_mfma_scale_f32_16x16x128_f8f6f4 — BASELINE configs[4]'s fp8 token GEMMs.
+#include <type_traits>
+
 #include "common.h"
 #include "mx8.h"
 
@@ -123,15 +125,39 @@ struct Stager {
       load8<DT, VEC>(p, gr + gk * ld_k, n_ok, v);
     }
   }
-  // fp32 image for the MX kernel's block quantization (no rounding while staging)
-  __device__ __forceinline__ void store_f32(float (*lds)[MLD], int k_off) {
+  // the MX kernel's source image for block quantization, in the operand's own dtype (exact):
+  // fp32 for an fp32 operand, bf16 for a bf16 one (no rounding while staging)
+  template <typename T>
+  __device__ __forceinline__ void store_img(T (*lds)[MLD], int k_off) {
     if (KCONTIG) {
-      *reinterpret_cast<float4 *>(&lds[r][k_off + k]) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4 *>(&lds[r][k_off + k + 4]) = make_float4(v[4], v[5], v[6], v[7]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[r][k_off + k + i] = (T)v[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) lds[r + i][k_off + k] = v[i];
+      for (int i = 0; i < 8; ++i) lds[r + i][k_off + k] = (T)v[i];
     }
+  }
+  // MX (KCONTIG only): this thread's 8 values of 32-element block p of row r, quantized with
+  // the block's scale — the block is this row's 4 adjacent lanes (k = 0, 8, 16, 24 of it), so
+  // their maxima meet by two xor shuffles; lane 0 of the four stores the E8M0 byte
+  template <int LDQ>
+  __device__ __forceinline__ void store_mx(uint8_t (*img)[LDQ], uint8_t (*sc)[4], int p) {
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    m = fmaxf(m, __shfl_xor(m, 2, 64));
+    const int e = mx_exp(m);
+    const float s = mx_inv_scale(e);
+    unsigned w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int q = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h] * s, v[4 * h + 1] * s, 0, false);
+      q = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h + 2] * s, v[4 * h + 3] * s, q, true);
+      w[h] = (unsigned)q;
+    }
+    *reinterpret_cast<uint2 *>(&img[r][p * 32 + k]) = make_uint2(w[0], w[1]);
+    if ((threadIdx.x & 3) == 0) sc[r][p] = (uint8_t)e;
   }
   __device__ __forceinline__ void store(bf16_t (*lds)[GLD]) {
     if (KCONTIG) {
@@ -220,24 +246,33 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       }
 }
 
-// MXFP8 GEMM: 64 x 64 output tile, 128-wide K-tiles.  Per K-tile: A and B are staged as fp32
-// in LDS (the Stager's 64 x 32 pieces, 4 per tile: any operand layout); then each of the 256
-// threads quantizes one 32-element block of A and one of B (row t / 4, block t % 4) into the
-// e4m3 images (two, alternating per K-tile) with its E8M0 scale — every block once; the 4 waves
-// (2 x 2, 32 x 32 each) read their fragments from the images (two 16-B runs per lane, mx8.h's
-// lane map) and run one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 tile (two barriers per
-// K-tile: the fp32 images are rewritten only after every wave quantized them, the e4m3 images
-// only after every wave passed the next K-tile's first barrier, i.e. finished its MFMAs).  The
-// next K-tile's global loads are in flight during the quantization and the MFMAs.  Rows / K past the matrix
-// are zero.  The MFMA applies both block scales, so the epilogue sees the descaled product.
+// MXFP8 GEMM: 64 x 64 output tile, 128-wide K-tiles.  An operand stored K-contiguous is
+// quantized in registers as it is staged (a 32-element block is the Stager's 4 adjacent lanes of
+// one row: two xor shuffles) straight into its e4m3 image; an operand stored the other way (the
+// backward products' dY^T / X) is staged as fp32 in LDS first and each of the 256 threads then
+// quantizes one 32-element block of it (row t / 4, block t % 4) — every block once, any layout.
+// The e4m3 images alternate per K-tile, so one or two barriers per K-tile order the phases (the
+// fp32 images are rewritten only after every wave quantized them; an e4m3 image only after every
+// wave passed the next K-tile's first barrier, i.e. finished its MFMAs).  The 4 waves (2 x 2,
+// 32 x 32 each) read their fragments from the images (two 16-B runs per lane, mx8.h's lane map)
+// and run one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 tile; the next K-tile's global
+// loads are in flight meanwhile.  Rows / K past the matrix are zero.  The MFMA applies both
+// block scales, so the epilogue sees the descaled product.
 constexpr int Q8LD = MBK + 16;          // e4m3 image row (bytes): conflict-free 16-B fragment reads
 template <int ADT, int BDT, bool AK, bool BK, bool AV, bool BV>
 __global__ __launch_bounds__(256) void gemm_mx8_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[GBM][MLD];
-  __shared__ __attribute__((aligned(16))) float Bs[GBN][MLD];
-  __shared__ __attribute__((aligned(16))) uint8_t Aq[GBM][Q8LD];
-  __shared__ __attribute__((aligned(16))) uint8_t Bq[GBN][Q8LD];
-  __shared__ uint8_t Asc[GBM][4], Bsc[GBN][4];
+  // source images (non-K-contiguous operands only) in the operand's dtype; e4m3 images doubled
+  // for a K-contiguous operand (written in the staging phase, which may run while a slower wave
+  // still reads the previous K-tile's image), single for the others (written after the barrier
+  // every wave reaches only after its MFMAs)
+  using AT = typename std::conditional<ADT == EWVIT_BF16, __bf16, float>::type;
+  using BT = typename std::conditional<BDT == EWVIT_BF16, __bf16, float>::type;
+  constexpr int NQA = AK ? 2 : 1, NQB = BK ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) AT As[AK ? 1 : GBM][MLD];
+  __shared__ __attribute__((aligned(16))) BT Bs[BK ? 1 : GBN][MLD];
+  __shared__ __attribute__((aligned(16))) uint8_t Aq[NQA][GBM][Q8LD];
+  __shared__ __attribute__((aligned(16))) uint8_t Bq[NQB][GBN][Q8LD];
+  __shared__ uint8_t Asc[NQA][GBM][4], Bsc[NQB][GBN][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
@@ -259,14 +294,11 @@ __global__ __launch_bounds__(256) void gemm_mx8_kernel(GemmArgs g) {
     }
   };
   // one 32-element block of an fp32 image row -> its e4m3 bytes and scale
-  auto quant = [&](const float (*src)[MLD], uint8_t (*dst)[Q8LD], uint8_t (*sc)[4]) {
+  auto quant = [&](const auto (*src)[MLD], uint8_t (*dst)[Q8LD], uint8_t (*sc)[4]) {
     const int row = tid >> 2, blk = tid & 3;
     float v[32];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4 x = *reinterpret_cast<const float4 *>(&src[row][blk * 32 + 4 * q]);
-      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
-    }
+    for (int q = 0; q < 32; ++q) v[q] = (float)src[row][blk * 32 + q];
     int d[8];
     sc[row][blk] = (uint8_t)mx_quant_block(v, d);
     uint4 *o = reinterpret_cast<uint4 *>(&dst[row][blk * 32]);
@@ -285,21 +317,26 @@ __global__ __launch_bounds__(256) void gemm_mx8_kernel(GemmArgs g) {
   if (nk > 0) load(kbeg);
   const int r = lane & 15;
   for (int kt = 0; kt < nk; ++kt) {
+    const int ba = AK ? kt & 1 : 0, bb = BK ? kt & 1 : 0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      sa[p].store_f32(As, p * GBK);
-      sb[p].store_f32(Bs, p * GBK);
+      if constexpr (AK) sa[p].store_mx(Aq[ba], Asc[ba], p);
+      else sa[p].store_img(As, p * GBK);
+      if constexpr (BK) sb[p].store_mx(Bq[bb], Bsc[bb], p);
+      else sb[p].store_img(Bs, p * GBK);
     }
     __syncthreads();
     if (kt + 1 < nk) load(kbeg + (int64_t)(kt + 1) * MBK);
-    quant(As, Aq, Asc);
-    quant(Bs, Bq, Bsc);
-    __syncthreads();
+    if constexpr (!AK || !BK) {
+      if constexpr (!AK) quant(As, Aq[0], Asc[0]);
+      if constexpr (!BK) quant(Bs, Bq[0], Bsc[0]);
+      __syncthreads();
+    }
     MxFrag af[2], bfr[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) af[i] = frag(Aq, Asc, wm * 32 + i * 16 + r);
+    for (int i = 0; i < 2; ++i) af[i] = frag(Aq[ba], Asc[ba], wm * 32 + i * 16 + r);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bfr[j] = frag(Bq, Bsc, wn * 32 + j * 16 + r);
+    for (int j = 0; j < 2; ++j) bfr[j] = frag(Bq[bb], Bsc[bb], wn * 32 + j * 16 + r);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll

@@ -33,6 +33,25 @@
 
 namespace ewvit {
 
+// non-temporal 16-B load / 8-B store (global ... nt): the MWT's 0.3 GB maps stream through once
+typedef __attribute__((ext_vector_type(2))) uint32_t hs_v2u;
+typedef __attribute__((ext_vector_type(4))) uint32_t hs_v4u;
+__device__ __forceinline__ uint4 hs_ldnt(const bf16_t *p) {
+#if EWVIT_MWT_NT
+  const hs_v4u v = __builtin_nontemporal_load(reinterpret_cast<const hs_v4u *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const uint4 *>(p);
+#endif
+}
+__device__ __forceinline__ void hs_stnt(bf16_t *p, hs_v2u v) {
+#if EWVIT_MWT_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<hs_v2u *>(p));
+#else
+  *reinterpret_cast<hs_v2u *>(p) = v;
+#endif
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 hbf16x8;
 typedef __attribute__((ext_vector_type(4))) float hf32x4;
 typedef __attribute__((ext_vector_type(4))) short hs4;
@@ -232,8 +251,8 @@ __global__ __launch_bounds__(256) void hfsep_fwd_kernel(const bf16_t *__restrict
             s2[t][i] += d * d;
           }
           const int n = t * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<uint2 *>(o + n) =
-              make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+          // (non-temporal: the 0.3 GB output map streams to the fusion conv, no L2 reuse)
+          hs_stnt(o + n, hs_v2u{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)});
         }
       }
     }
@@ -330,8 +349,8 @@ __global__ __launch_bounds__(256) void hfsep_wgrad_kernel(const bf16_t *__restri
       const bool ok = i < ndy && (i >> 3) < Pb;
       dok |= (unsigned)ok << k;
       const int64_t off = ok ? dbase + (int64_t)(i >> 3) * HS_COUT + (i & 7) * 8 : 0;
-      rd[k] = *reinterpret_cast<const uint4 *>(dy + off);
-      if constexpr (BNB) ry[k] = *reinterpret_cast<const uint4 *>(yb + off);
+      rd[k] = hs_ldnt(dy + off);
+      if constexpr (BNB) ry[k] = hs_ldnt(yb + off);
     }
     if constexpr (XS == 9) {
       // pixel pairs (2q, 2q + 1) of the halo rows; item q = W / 2 of a row: its two border pixels

@@ -388,8 +388,8 @@ int ewvit_conv2d_set_lds_pad(int on);
  * row per wave group); returns the previous setting.  Results are bit-identical in every form
  * (same per-output MFMA chain).  Env: EWVIT_WGWIN_TS=0 / 2. */
 int ewvit_conv2d_set_wgrad_tap_split(int on);
-/* A/B: the non-temporal cache hint on the windowed MWT convs' activation-window DMAs (1) or not
- * (0, the default); returns the previous setting.  Env: EWVIT_WIN_NT. */
+/* The non-temporal cache hint on the windowed MWT convs' activation-window DMAs: 1 (default) or
+ * 0 (A/B); returns the previous setting.  Env: EWVIT_WIN_NT. */
 int ewvit_conv2d_set_win_nt(int on);
 /* A/B: level-1 pixels per thread in flight in ewvit_dwt_hf_upsample_fused (2, the default, or 4); returns the previous. */
 int ewvit_dwt_set_pf(int pf);
