@@ -35,10 +35,9 @@ template <int DT> struct Raw8;
 template <> struct Raw8<EWVIT_BF16> { uint4 q; };
 template <> struct Raw8<EWVIT_F32> { float4 a, b; };
 
-// NT: the non-temporal hint (global_load / global_store ... nt) — the ReLU instantiations are
-// the MWT's BatchNorms over 0.2-2.4 M-row maps, streamed once per pass with no L2 reuse; the hint
-// keeps them from displacing the concurrent backbone's L2 lines (the windowed convs' window DMAs
-// carry it too, convwin.hip g_win_nt)
+// NT: the non-temporal hint (global_load / global_store ... nt) on the ReLU instantiations (the
+// MWT's BatchNorms over 0.2-2.4 M-row maps, streamed once per pass) — compiled in only with
+// EWVIT_MWT_NT=1: measured a net loss with the other MWT hints (common.h)
 typedef unsigned bn_v4u __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ uint4 ldq16(const void *p) {

@@ -7,10 +7,14 @@
 
 #include "../../include/ewvit.h"
 
-// the non-temporal cache hint on the MWT branch's streaming loads / stores (windowed convs,
-// seperate conv, the ReLU BatchNorm passes): 1 (default); A/B builds compile with -DEWVIT_MWT_NT=0
+// the non-temporal cache hint on the rest of the MWT branch's streaming traffic (the windowed
+// convs' output stores and BN-input loads, the separable conv, the ReLU BatchNorm passes) on top
+// of the window DMAs' (convwin.hip g_win_nt, on): 0 (default).  Measured with it compiled in:
+// config 2 3577-3583 vs 3626-3630 frames/s without any MWT hint, three interleaved same-box
+// rounds (profiles/r06/ab/mwt_nt.log) — the backbone reads those maps' neighbours back through
+// L2 sooner than the hint assumes
 #ifndef EWVIT_MWT_NT
-#define EWVIT_MWT_NT 1
+#define EWVIT_MWT_NT 0
 #endif
 
 namespace ewvit {

@@ -53,7 +53,7 @@ int g_lds_pad = 1;
 // through once per tile; the hint keeps them from displacing the concurrent backbone's L2 lines):
 // config 2 +0.26 / +0.34 / +0.63 % in three interleaved same-box rounds and +0.7 / +0.5 % on
 // another box (profiles/r06/ab/win_nt*.log); EWVIT_WIN_NT=0 / ewvit_conv2d_set_win_nt(0): off
-int g_win_nt = EWVIT_MWT_NT;
+int g_win_nt = 1;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
   if (!g_lds_pad || stat >= 160 * 1024) return 0;
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
       for (int i = 0; i < NER; ++i) {
         const int64_t pix = ((int64_t)d.img * H + d.oh0 + wm * 4 + ER0 + i) * W + d.ow0 + fr;
         const uint32_t off = d.last ? (uint32_t)((pix * a.ogc + cbase) * 2) : OOB;
-        if (a.nt) asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
+        if (EWVIT_MWT_NT && a.nt) asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
         else asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(xq[j][i]) : "v"(off), "s"(rbx) : "memory");
       }
     }
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(512) void conv_win_kernel(FwdArgs a, int64_t src_by
         uint2 pk;
         pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
         pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
-        bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2), a.nt != 0);
+        bstore64(ro, pk, (uint32_t)((pix * a.ogc + cbase) * 2), EWVIT_MWT_NT && a.nt != 0);
         if constexpr (BST) {
           const float hv[4] = {bf2f(h0), bf2f(h1), bf2f(h2), bf2f(h3)};
           const float xv[4] = {__uint_as_float(xq[j][i].x << 16), __uint_as_float(xq[j][i].x & 0xffff0000u),

@@ -128,6 +128,32 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const void *__restrict
 // 3*s new 16-B loads instead of 9 (+72 weight loads) in the generic kernel.
 // ROT: use the 180-degree-rotated kernel — the input gradient of a stride-1
 // conv is the stride-1 conv of dy with the rotated weights (pad 1).
+// The row kernels' window loads are buffer loads: a tap outside the map gets the offset DW_OOB
+// (>= the resource's size), which the hardware returns as zeros — no branch and no select on
+// the loaded value, so the window register carried to the next column is the load's own result
+// and its wait lands at the next column's first use.  (A zeroing select after a global load
+// made every column wait for its loads before the loop back edge: 7^2 / 14^2 depthwise passes
+// 30-60 % slower; the branchy C++ form compiled to FLAT loads from a select between the global
+// address and a private zero.)  Offsets are 32-bit bytes: the host takes the row kernels only
+// for tensors below 2 GB (dw_bufok).
+constexpr uint32_t DW_OOB = 0x80000000u;
+typedef __attribute__((ext_vector_type(4))) unsigned dw_u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned dw_u32x2;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dw_rsrc(const void *p, int64_t elems) {
+  const int64_t bytes = elems * 2;
+  const uint32_t n = bytes >= (int64_t)DW_OOB ? DW_OOB : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ uint4 dw_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const dw_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 dw_ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const dw_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v.x, v.y);
+}
+static inline bool dw_bufok(int64_t elems) { return elems * 2 < (int64_t)DW_OOB; }
+
 __device__ __forceinline__ void bf8_unpack(const uint4 &q, float (&v)[8]) {
   const unsigned w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -168,7 +194,6 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
 #pragma unroll
       for (int k = 0; k < 9; ++k) wr[ROT ? 8 - k : k][j] = t[j * 9 + k];
   }
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
   bool rok[3];
   int64_t rbase[3];
 #pragma unroll
@@ -177,15 +202,19 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
     rok[kh] = hi >= 0 && hi < s.H;
     rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
   }
-  auto ld = [&](int kh, int col) -> uint4 {
-    if (!rok[kh] || col < 0 || col >= s.W) return zero;
-    return *reinterpret_cast<const uint4 *>(x + rbase[kh] + (int64_t)col * s.C);
+  const __amdgpu_buffer_rsrc_t xr = dw_rsrc(x, (int64_t)s.N * s.H * s.W * s.C);
+  auto ld = [&](int kh, int col) -> uint4 {     // zeros outside the map (DW_OOB)
+    return dw_ld16(xr, rok[kh] && col >= 0 && col < s.W ? (uint32_t)((rbase[kh] + (int64_t)col * s.C) * 2) : DW_OOB);
   };
   uint4 win[3][3];  // [kw][kh], column ci = wo*STRIDE - pad + kw
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, wo0 * STRIDE - s.pad + kw);
+  // stride 1: the window's next column loaded one column ahead (its wait lands a column later)
+  uint4 nx[3];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) nx[kh] = STRIDE == 1 ? ld(kh, wo0 + 3 - s.pad) : make_uint4(0u, 0u, 0u, 0u);
   bf16_t *yrow = y + (row * s.Wo) * s.C + c;
   for (int wo = wo0; wo < wo1; ++wo) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -208,7 +237,8 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
       for (int kh = 0; kh < 3; ++kh) {
         win[0][kh] = win[1][kh];
         win[1][kh] = win[2][kh];
-        win[2][kh] = ld(kh, nb + 2);
+        win[2][kh] = nx[kh];
+        nx[kh] = ld(kh, nb + 3);
       }
     } else {
 #pragma unroll
@@ -232,13 +262,15 @@ __global__ __launch_bounds__(256) void dw_row_bf16_kernel(const bf16_t *__restri
 //   ST 2 (input gradient of a stride-1 conv, ROT): sum g, sum g * xhat (BnBwdStats: g =
 //        dx * act'(xhat * gamma + beta), the gradient of the BN(+act) whose output the conv
 //        read) — what ewvit_bn_bwd_partials finalises
-// The 32 row sums of a channel are added in row order through LDS (deterministic).
+// The 32 row sums of a channel are added in row order through LDS (deterministic).  Launched
+// for the stride-2 forward only (the first block of stages 4 and 6); the stride-1 forms run on
+// dw_row4_kernel below.
 struct DwBnFwd {
   float *part = nullptr;
   const float *shift = nullptr;
   float *shift_out = nullptr;
 };
-template <int STRIDE, bool ROT, int ST>
+template <int STRIDE, bool ROT, int ST, int ACT>
 __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict__ x, const float *__restrict__ w,
                                                         bf16_t *__restrict__ y, DwShape s, DwBnFwd f, BnBwdStats b) {
   __shared__ float red[32 * 8 * 16];
@@ -278,8 +310,7 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
         p2[j] = b.gamma ? b.gamma[c + j] : 1.f; p3[j] = b.beta ? b.beta[c + j] : 0.f;
       }
     }
-    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-    bool rok[3];
+      bool rok[3];
     int64_t rbase[3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
@@ -287,28 +318,21 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
       rok[kh] = hi >= 0 && hi < s.H;
       rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
     }
-    auto ld = [&](int kh, int col) -> uint4 {
-      if (!rok[kh] || col < 0 || col >= s.W) return zero;
-      return *reinterpret_cast<const uint4 *>(x + rbase[kh] + (int64_t)col * s.C);
+    const __amdgpu_buffer_rsrc_t xr = dw_rsrc(x, (int64_t)s.N * s.H * s.W * s.C);
+    auto ld = [&](int kh, int col) -> uint4 {   // zeros outside the map (DW_OOB)
+      return dw_ld16(xr, rok[kh] && col >= 0 && col < s.W ? (uint32_t)((rbase[kh] + (int64_t)col * s.C) * 2) : DW_OOB);
     };
-    uint4 win[3][3];
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
     const int64_t ybase = (row * s.Wo) * s.C + c;
-    // ST 2: the BN input at this output pixel, loaded one column ahead with the window's
-    // next column (a load consumed in the same iteration would expose its latency per column)
-    uint4 bxq = zero;
-    if (ST == 2) bxq = *reinterpret_cast<const uint4 *>(b.x + ybase);
-    for (int wo = 0; wo < s.Wo; ++wo) {
+    // one output pixel from the window columns (w0, w1, w2) and the BN input bq (ST 2)
+    auto pixel = [&](const uint4 (&w0)[3], const uint4 (&w1)[3], const uint4 (&w2)[3], const uint4 &bq, int wo) {
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const uint4 *cols[3] = {w0, w1, w2};
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
           float v[8];
-          bf8_unpack(win[kw][kh], v);
+          bf8_unpack(cols[kw][kh], v);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[j]);
         }
@@ -328,24 +352,25 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
         }
       } else {
         float xv[8];
-        bf8_unpack(bxq, xv);
+        bf8_unpack(bq, xv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xh = (xv[j] - p0[j]) * p1[j];
-          const float g = b.act ? v[j] * bn_act_grad(b.act, fmaf(xh, p2[j], p3[j])) : v[j];
+          const float g = ACT ? v[j] * bn_act_grad(ACT, fmaf(xh, p2[j], p3[j])) : v[j];
           sa[j] += g;
           sb[j] = fmaf(g, xh, sb[j]);
         }
       }
-      const int nb = (wo + 1) * STRIDE - s.pad;
-      if (STRIDE == 1) {
+    };
+    {
+      uint4 win[3][3];
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-          win[0][kh] = win[1][kh];
-          win[1][kh] = win[2][kh];
-          win[2][kh] = ld(kh, nb + 2);
-        }
-      } else {
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
+      for (int wo = 0; wo < s.Wo; ++wo) {
+        pixel(win[0], win[1], win[2], make_uint4(0u, 0u, 0u, 0u), wo);
+        const int nb = (wo + 1) * STRIDE - s.pad;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
           win[0][kh] = win[2][kh];
@@ -353,7 +378,6 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
           win[2][kh] = ld(kh, nb + 2);
         }
       }
-      if (ST == 2 && wo + 1 < s.Wo) bxq = *reinterpret_cast<const uint4 *>(b.x + ybase + (int64_t)(wo + 1) * s.C);
     }
   }
   float *q = red + (r * 8 + cv) * 16;
@@ -373,6 +397,193 @@ __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict
       pr[c] = A;
       pr[s.C + c] = B;
       if (ST == 1 && blockIdx.x == 0 && f.shift_out) f.shift_out[c] = f.shift ? f.shift[c] : 0.f;
+    }
+  }
+}
+
+// ---- stride-1 pad-1 row kernel with 4-channel threads: the MBConv depthwise conv of blocks
+// after the first of stages 4-6 (7^2 / 14^2 maps, 28 of the step's 30 depthwise convs).
+//   ST 1: forward + the BatchNorm statistics of y (as dw_row_bn_kernel ST 1);
+//   ST 2: input gradient (the rotated-kernel conv of dy) + the backward sums of the
+//         BatchNorm(+act ACT) whose output the conv read (as dw_row_bn_kernel ST 2), and with
+//         WG also the weight gradient dW[c][kh][kw] = sum dy[h][w] x[h - 1 + kh][w - 1 + kw] —
+//         whose dy is the centre of the dx window, so the whole backward reads dy once, plus an
+//         x window sliding in step, in one launch instead of two.
+// The 8-channel row kernels were latency-bound (0.9-1.9 TB/s: 448 / 896 rows of 7 / 14 columns,
+// ~230 VGPRs, 2 waves per SIMD); a 4-channel thread halves the weights, windows and sums it
+// holds and doubles the waves.  The window's next column is loaded a column ahead.  Block = 32 rows x 8 channel quads (32 channels): one
+// partial row of BN sums per block (part[blockIdx.x][2C], its 32 channels) and with WG one dW
+// slab wpart[blockIdx.x][C][9] for dw_bwd_weight_reduce_kernel; the block's sums over its rows
+// go lane bits 3..5 by DPP / permlane, then the 4 waves in order through LDS (deterministic).
+__device__ __forceinline__ void bf4_unpack(const uint2 &q, float (&v)[4]) {
+  v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+  v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+template <int ST, int ACT, bool WG>
+__global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *__restrict__ in, const bf16_t *__restrict__ x,
+                                                      const float *__restrict__ w, bf16_t *__restrict__ out,
+                                                      DwShape s, DwBnFwd f, BnBwdStats b, float *__restrict__ wpart) {
+  constexpr int NV = 8 + (WG ? 36 : 0);        // per quad: 4 + 4 BN sums (+ 36 dW)
+  __shared__ float red[4][8 * NV];
+  const int tid = threadIdx.x, q = tid & 7, r = tid >> 3, wv = tid >> 6;
+  const int C4 = s.C >> 2;
+  const int c4 = blockIdx.y * 8 + q;
+  const int64_t row = (int64_t)blockIdx.x * 32 + r;          // n*H + h
+  const bool active = c4 < C4 && row < (int64_t)s.N * s.H;
+  float sa[4], sb[4], acc[WG ? 9 : 1][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sa[j] = 0.f; sb[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < (WG ? 9 : 1); ++k) acc[k][j] = 0.f;
+  }
+  if (active) {
+    const int h = (int)(row % s.H);
+    const int n = (int)(row / s.H);
+    const int c = c4 * 4;
+    float wr[9][4];                            // [window tap][channel]; ST 2 rotated
+    {
+      const float4 *wp = reinterpret_cast<const float4 *>(w + (int64_t)c * 9);
+      float t[36];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const float4 v = wp[i];
+        t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wr[ST == 2 ? 8 - k : k][j] = t[j * 9 + k];
+    }
+    float p0[4], p1[4], p2[4], p3[4];          // ST 1: K | ST 2: mean, invstd, gamma, beta
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ST == 1) {
+        p0[j] = f.shift ? f.shift[c + j] : 0.f;
+      } else {
+        p0[j] = b.mean[c + j]; p1[j] = b.invstd[c + j];
+        p2[j] = b.gamma ? b.gamma[c + j] : 1.f; p3[j] = b.beta ? b.beta[c + j] : 0.f;
+      }
+    }
+    bool rok[3];
+    int64_t rbase[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hi = h - 1 + kh;
+      rok[kh] = hi >= 0 && hi < s.H;
+      rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
+    }
+    const int64_t total = (int64_t)s.N * s.H * s.W * s.C;
+    const __amdgpu_buffer_rsrc_t ir = dw_rsrc(in, total);
+    const __amdgpu_buffer_rsrc_t xr = dw_rsrc(WG ? (const void *)x : (const void *)in, total);
+    const __amdgpu_buffer_rsrc_t br = dw_rsrc(ST == 2 ? (const void *)b.x : (const void *)in, total);
+    auto off = [&](int kh, int col) -> uint32_t {  // zeros outside the map (DW_OOB)
+      return rok[kh] && col >= 0 && col < s.W ? (uint32_t)((rbase[kh] + (int64_t)col * s.C) * 2) : DW_OOB;
+    };
+    const int64_t base = (row * s.W) * s.C + c;
+    auto boff = [&](int col) -> uint32_t {
+      return col < s.W ? (uint32_t)((base + (int64_t)col * s.C) * 2) : DW_OOB;
+    };
+    // window columns col - 1 .. col + 1 ([kw][kh]; G the conv input's, X (WG) x's) and the
+    // next column col + 2 loaded a column ahead, like the BN input (ST 2); every load is a
+    // buffer load (zeros outside the map), so the loop has no branch
+    uint2 G[3][3], X[3][3], Gn[3], Xn[3], bq;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        G[kw][kh] = dw_ld8(ir, off(kh, kw - 1));
+        if (WG) X[kw][kh] = dw_ld8(xr, off(kh, kw - 1));
+      }
+      Gn[kh] = dw_ld8(ir, off(kh, 2));
+      if (WG) Xn[kh] = dw_ld8(xr, off(kh, 2));
+    }
+    bq = ST == 2 ? dw_ld8(br, boff(0)) : make_uint2(0u, 0u);
+#pragma unroll 1
+    for (int col = 0; col < s.W; ++col) {
+      float o4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          float v[4];
+          bf4_unpack(G[kw][kh], v);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o4[j] = fmaf(v[j], wr[kh * 3 + kw][j], o4[j]);
+        }
+      if (WG) {
+        float g[4];
+        bf4_unpack(G[1][1], g);                // dy[h][col]: the weight gradient's dy
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh) {
+            float v[4];
+            bf4_unpack(X[kw][kh], v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[WG ? kh * 3 + kw : 0][j] = fmaf(g[j], v[j], acc[WG ? kh * 3 + kw : 0][j]);
+          }
+      }
+      const uint2 oq = make_uint2((unsigned)f2bf(o4[0]) | ((unsigned)f2bf(o4[1]) << 16),
+                                  (unsigned)f2bf(o4[2]) | ((unsigned)f2bf(o4[3]) << 16));
+      *reinterpret_cast<uint2 *>(out + base + (int64_t)col * s.C) = oq;
+      float v[4];
+      bf4_unpack(oq, v);
+      if (ST == 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = v[j] - p0[j];
+          sa[j] += d;
+          sb[j] = fmaf(d, d, sb[j]);
+        }
+      } else {
+        float xv[4];
+        bf4_unpack(bq, xv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (xv[j] - p0[j]) * p1[j];
+          const float gg = ACT ? v[j] * bn_act_grad(ACT, fmaf(xh, p2[j], p3[j])) : v[j];
+          sa[j] += gg;
+          sb[j] = fmaf(gg, xh, sb[j]);
+        }
+        bq = dw_ld8(br, boff(col + 1));
+      }
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const uint32_t o = off(kh, col + 3);
+        G[0][kh] = G[1][kh]; G[1][kh] = G[2][kh]; G[2][kh] = Gn[kh]; Gn[kh] = dw_ld8(ir, o);
+        if (WG) { X[0][kh] = X[1][kh]; X[1][kh] = X[2][kh]; X[2][kh] = Xn[kh]; Xn[kh] = dw_ld8(xr, o); }
+      }
+    }
+  }
+  // the wave's 8 rows (lane bits 3..5) of each quad, then the 4 waves in order
+  float *mine = red[wv] + q * NV;
+  const int lane = tid & 63;
+  auto put = [&](int i, float v) {
+    v += dpp_mov<0x128>(v);                    // row_ror:8 = lane ^ 8 within the row
+    v = rows_sum4(v);
+    if (lane < 8) mine[i] = v;
+  };
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { put(j, sa[j]); put(4 + j, sb[j]); }
+  if (WG) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(8 + j * 9 + k, acc[WG ? k : 0][j]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 8 * NV; i += 256) {
+    const int qq = i / NV, k = i - qq * NV;
+    const int cq = blockIdx.y * 8 + qq;
+    if (cq >= C4) continue;
+    const float t = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    if (k < 8) {
+      float *pr = (ST == 1 ? f.part : b.part) + (int64_t)blockIdx.x * 2 * s.C;
+      pr[(k < 4 ? 0 : s.C) + cq * 4 + (k & 3)] = t;
+      if (ST == 1 && k < 4 && blockIdx.x == 0 && f.shift_out) f.shift_out[cq * 4 + k] = f.shift ? f.shift[cq * 4 + k] : 0.f;
+    } else {
+      wpart[(int64_t)blockIdx.x * s.C * 9 + (int64_t)cq * 36 + (k - 8)] = t;   // [c][tap]
     }
   }
 }
@@ -419,12 +630,11 @@ __global__ __launch_bounds__(256) void dw_row_s2_bwd_kernel(const bf16_t *__rest
   const int hoA = odd ? (hi + 1) >> 1 : hi >> 1, khA = odd ? 0 : 1;
   const int hoB = (hi - 1) >> 1, khB = 2;                            // odd rows only
   const bool okA = hoA < s.Ho, okB = odd && hoB >= 0;
-  const bf16_t *rA = dy + (((int64_t)n * s.Ho + (okA ? hoA : 0)) * s.Wo) * s.C + c;
-  const bf16_t *rB = dy + (((int64_t)n * s.Ho + (okB ? hoB : 0)) * s.Wo) * s.C + c;
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  auto ld = [&](const bf16_t *rp, bool ok, int col) -> uint4 {
-    if (!ok || col < 0 || col >= s.Wo) return zero;
-    return *reinterpret_cast<const uint4 *>(rp + (int64_t)col * s.C);
+  const int64_t rA = (((int64_t)n * s.Ho + (okA ? hoA : 0)) * s.Wo) * s.C + c;
+  const int64_t rB = (((int64_t)n * s.Ho + (okB ? hoB : 0)) * s.Wo) * s.C + c;
+  const __amdgpu_buffer_rsrc_t gr = dw_rsrc(dy, (int64_t)s.N * s.Ho * s.Wo * s.C);
+  auto ld = [&](int64_t rp, bool ok, int col) -> uint4 {   // zeros outside the map (DW_OOB)
+    return dw_ld16(gr, ok && col >= 0 && col < s.Wo ? (uint32_t)((rp + (int64_t)col * s.C) * 2) : DW_OOB);
   };
   uint4 a0 = ld(rA, okA, j0), b0 = ld(rB, okB, j0);                  // dy column j of rows A, B
   bf16_t *xrow = dx + (row * s.W) * s.C + c;
@@ -475,7 +685,6 @@ __global__ __launch_bounds__(512) void dw_wgrad_row_bf16_kernel(const bf16_t *__
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
   const int64_t nrows = (int64_t)s.N * s.Ho;
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
   for (int64_t row = (int64_t)blockIdx.x * R + r; active && row < nrows; row += (int64_t)gridDim.x * R) {
     const int ho = (int)(row % s.Ho);
     const int n = (int)(row / s.Ho);
@@ -487,19 +696,26 @@ __global__ __launch_bounds__(512) void dw_wgrad_row_bf16_kernel(const bf16_t *__
       rok[kh] = hi >= 0 && hi < s.H;
       rbase[kh] = (((int64_t)n * s.H + (rok[kh] ? hi : 0)) * s.W) * s.C + c;
     }
-    auto ld = [&](int kh, int col) -> uint4 {
-      if (!rok[kh] || col < 0 || col >= s.W) return zero;
-      return *reinterpret_cast<const uint4 *>(x + rbase[kh] + (int64_t)col * s.C);
+    const __amdgpu_buffer_rsrc_t xr = dw_rsrc(x, (int64_t)s.N * s.H * s.W * s.C);
+    auto ld = [&](int kh, int col) -> uint4 {   // zeros outside the map (DW_OOB)
+      return dw_ld16(xr, rok[kh] && col >= 0 && col < s.W ? (uint32_t)((rbase[kh] + (int64_t)col * s.C) * 2) : DW_OOB);
     };
     uint4 win[3][3];
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) win[kw][kh] = ld(kh, -s.pad + kw);
-    const bf16_t *gr = dy + (row * s.Wo) * s.C + c;
+    uint4 nx[3];                           // stride 1: the next column, one column ahead
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) nx[kh] = STRIDE == 1 ? ld(kh, 3 - s.pad) : make_uint4(0u, 0u, 0u, 0u);
+    // dy of this output pixel, loaded one column ahead too
+    const __amdgpu_buffer_rsrc_t gr = dw_rsrc(dy, (int64_t)s.N * s.Ho * s.Wo * s.C);
+    const uint32_t gb = (uint32_t)(((row * s.Wo) * s.C + c) * 2), gstep = (uint32_t)s.C * 2;
+    uint4 gq = dw_ld16(gr, gb);
     for (int wo = 0; wo < s.Wo; ++wo) {
       float g[8];
-      bf8_unpack(*reinterpret_cast<const uint4 *>(gr + (int64_t)wo * s.C), g);
+      bf8_unpack(gq, g);
+      gq = dw_ld16(gr, wo + 1 < s.Wo ? gb + (uint32_t)(wo + 1) * gstep : DW_OOB);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -515,7 +731,8 @@ __global__ __launch_bounds__(512) void dw_wgrad_row_bf16_kernel(const bf16_t *__
         for (int kh = 0; kh < 3; ++kh) {
           win[0][kh] = win[1][kh];
           win[1][kh] = win[2][kh];
-          win[2][kh] = ld(kh, nb + 2);
+          win[2][kh] = nx[kh];
+          nx[kh] = ld(kh, nb + 3);
         }
       } else {
 #pragma unroll
@@ -671,7 +888,8 @@ extern "C" int ewvit_dwconv3x3_fwd(const void *x, const float *w, void *y, int64
   EWVIT_CHECK_ARG(x && w && y && dtype_ok(dtype), "dwconv3x3_fwd: bad args");
   DwShape s = mk(N, H, W, C, stride, pad);
   if (int rc = check_shape(s, "dwconv3x3_fwd")) return rc;
-  if (dtype == EWVIT_BF16 && s.C / 8 <= 256 && (s.stride == 1 || s.stride == 2)) {
+  const bool buf = dw_bufok((int64_t)s.N * s.H * s.W * s.C) && dw_bufok((int64_t)s.N * s.Ho * s.Wo * s.C);
+  if (dtype == EWVIT_BF16 && s.C / 8 <= 256 && (s.stride == 1 || s.stride == 2) && buf) {
     const int rpb = 256 / (s.C / 8), segs = 1;
     dim3 grid((unsigned)(((int64_t)s.N * s.Ho + rpb - 1) / rpb));
     if (s.stride == 1)
@@ -696,7 +914,8 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
   EWVIT_CHECK_ARG(dy && w && dx && dtype_ok(dtype), "dwconv3x3_bwd_data: bad args");
   DwShape s = mk(N, H, W, C, stride, pad);
   if (int rc = check_shape(s, "dwconv3x3_bwd_data")) return rc;
-  if (dtype == EWVIT_BF16 && s.stride == 1 && s.pad == 1 && s.C / 8 <= 256) {
+  const bool buf = dw_bufok((int64_t)s.N * s.H * s.W * s.C) && dw_bufok((int64_t)s.N * s.Ho * s.Wo * s.C);
+  if (dtype == EWVIT_BF16 && s.stride == 1 && s.pad == 1 && s.C / 8 <= 256 && buf) {
     // input gradient of a stride-1 pad-1 conv = stride-1 pad-1 conv of dy with the rotated kernel
     DwShape t = s;
     t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
@@ -704,7 +923,7 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
     dim3 grid((unsigned)(((int64_t)t.N * t.Ho + rpb - 1) / rpb));
     hipLaunchKernelGGL((dw_row_bf16_kernel<1, true>), grid, dim3(256), 0, as_stream(stream),
                        (const bf16_t *)dy, w, (bf16_t *)dx, t, rpb, segs);
-  } else if (dtype == EWVIT_BF16 && s.stride == 2 && s.pad == 1 && s.C / 8 <= 256 && s.Ho == (s.H + 1) / 2 &&
+  } else if (dtype == EWVIT_BF16 && s.stride == 2 && s.pad == 1 && s.C / 8 <= 256 && buf && s.Ho == (s.H + 1) / 2 &&
              s.Wo == (s.W + 1) / 2) {
     // stride 2: dx rows in column pairs (dw_row_s2_bwd_kernel)
     const int rpb = 256 / (s.C / 8), segs = 1;
@@ -728,7 +947,7 @@ extern "C" int ewvit_dwconv3x3_bwd_data(const void *dy, const float *w, void *dx
 
 extern "C" int64_t ewvit_dwconv3x3_bn_rows(int64_t N, int64_t H, int64_t W, int64_t C, int stride, int bwd) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || C > 65536 * 8 || (stride != 1 && stride != 2) ||
-      (bwd && stride != 1))
+      (bwd && stride != 1) || !dw_bufok(N * H * W * C))
     return 0;
   const int64_t Ho = bwd ? H : (H - 1) / stride + 1;
   return (N * Ho + 31) / 32;
@@ -747,13 +966,13 @@ extern "C" int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, in
   DwBnFwd f;
   f.part = part; f.shift = shift; f.shift_out = shift_out;
   BnBwdStats b;
-  dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
-  if (stride == 1)
-    hipLaunchKernelGGL((dw_row_bn_kernel<1, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                       (bf16_t *)y, s, f, b);
-  else
-    hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)x, w,
-                       (bf16_t *)y, s, f, b);
+  if (stride == 1) {
+    hipLaunchKernelGGL((dw_row4_kernel<1, 0, false>), dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0,
+                       as_stream(stream), (const bf16_t *)x, nullptr, w, (bf16_t *)y, s, f, b, nullptr);
+    return launch_status("dwconv3x3_fwd_bn");
+  }
+  hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1, 0>), dim3((unsigned)nrc, (unsigned)((C / 8 + 7) / 8)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t *)x, w, (bf16_t *)y, s, f, b);
   return launch_status("dwconv3x3_fwd_bn");
 }
 
@@ -771,23 +990,56 @@ extern "C" int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void 
   EWVIT_CHECK_ARG(nrc > 0 && nrc < 65536, "dwconv3x3_bwd_data_bn: shape not supported");
   DwShape s = mk(N, H, W, C, 1, 1);
   if (int rc = check_shape(s, "dwconv3x3_bwd_data_bn")) return rc;
-  DwShape t = s;                               // the rotated-kernel conv over dy
-  t.H = s.Ho; t.W = s.Wo; t.Ho = s.H; t.Wo = s.W;
   DwBnFwd f;
   BnBwdStats b;
   b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
   b.act = act;
-  dim3 grid((unsigned)nrc, (unsigned)((C / 8 + 7) / 8));
-  hipLaunchKernelGGL((dw_row_bn_kernel<1, true, 2>), grid, dim3(256), 0, as_stream(stream), (const bf16_t *)dy, w,
-                       (bf16_t *)dx, t, f, b);
+  auto kern = act == 2 ? dw_row4_kernel<2, 2, false> : act == 1 ? dw_row4_kernel<2, 1, false> : dw_row4_kernel<2, 0, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t *)dy, nullptr, w, (bf16_t *)dx, s, f, b, nullptr);
   return launch_status("dwconv3x3_bwd_data_bn");
+}
+
+// bytes of f32 workspace ewvit_dwconv3x3_bwd_fused needs: one [C][9] slab per 32 rows
+extern "C" int64_t ewvit_dwconv3x3_bwd_fused_workspace(int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1);
+  return nrc * C * 9 * (int64_t)sizeof(float);
+}
+
+// the stride-1 pad-1 backward in one pass (dw_row4_kernel WG): dx, the producing BatchNorm's
+// backward sums (as ewvit_dwconv3x3_bwd_data_bn: part [ewvit_dwconv3x3_bn_rows(..., 1)][2C])
+// and dW [C][9] (= or += with accumulate) from x, the conv's bf16 input
+extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *dx, const void *x, float *dw,
+                                         int accumulate, int64_t N, int64_t H, int64_t W, int64_t C, const void *bx,
+                                         const float *mean, const float *invstd, const float *gamma,
+                                         const float *beta, int act, float *part, float *workspace, void *stream) {
+  EWVIT_CHECK_ARG(dy && w && dx && x && dw && bx && mean && invstd && part && workspace && act >= 0 && act <= 2,
+                  "dwconv3x3_bwd_fused: bad args");
+  const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1);
+  EWVIT_CHECK_ARG(nrc > 0 && nrc < 65536, "dwconv3x3_bwd_fused: shape not supported");
+  DwShape s = mk(N, H, W, C, 1, 1);
+  if (int rc = check_shape(s, "dwconv3x3_bwd_fused")) return rc;
+  BnBwdStats b;
+  b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
+  b.act = act;
+  hipStream_t st = as_stream(stream);
+  DwBnFwd f;
+  auto kern = act == 2 ? dw_row4_kernel<2, 2, true> : act == 1 ? dw_row4_kernel<2, 1, true> : dw_row4_kernel<2, 0, true>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0, st,
+                     (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace);
+  if (int rc = launch_status("dwconv3x3_bwd_fused")) return rc;
+  const int64_t n = C * 9;
+  hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace, dw, n,
+                     (int)nrc, accumulate);
+  return launch_status("dwconv3x3_bwd_fused reduce");
 }
 
 // weight-gradient plan: row kernel (bf16, C/8 <= 256) with `slabs` blocks, or the
 // generic pixel-slab kernel; the workspace holds one [C][9] f32 slab per block
 static void wgrad_plan(const DwShape &s, int dtype, bool *row, int *R, int64_t *slabs) {
   const int C8 = s.C / 8;
-  *row = dtype == EWVIT_BF16 && C8 <= 256 && (s.stride == 1 || s.stride == 2);
+  *row = dtype == EWVIT_BF16 && C8 <= 256 && (s.stride == 1 || s.stride == 2) &&
+         dw_bufok((int64_t)s.N * s.H * s.W * s.C) && dw_bufok((int64_t)s.N * s.Ho * s.Wo * s.C);
   if (*row) {
     *R = 512 / C8;
     const int64_t nrows = (int64_t)s.N * s.Ho;

@@ -114,6 +114,8 @@ SIGNATURES = {
     'ewvit_dwconv3x3_fwd_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     'ewvit_dwconv3x3_bwd_data_bn': [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp],
+    'ewvit_dwconv3x3_bwd_fused': [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                  _i32, _vp, _vp, _vp],
     'ewvit_bn_bwd_partials': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp,
                               _i32, _i32, _vp],
     'ewvit_head_fwd': [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp],
@@ -137,6 +139,7 @@ QUERIES = {
     'ewvit_vit_layer_workspace': (_i64, [_i32]),
     'ewvit_gemm_tallk_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_dwconv3x3_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i32, _i32]),
+    'ewvit_dwconv3x3_bwd_fused_workspace': (_i64, [_i64, _i64, _i64, _i64]),
     'ewvit_conv2d_bwd_weight_workspace': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_fwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_conv2d_stem_parts': (_i64, [_i64, _i64, _i64, _i32]),

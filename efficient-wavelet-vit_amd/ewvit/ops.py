@@ -539,6 +539,9 @@ def dwt_hf_features(x, levels, out_hw, out_dtype=torch.bfloat16, out_channels=0)
 # the stride-1 input gradient sums the backward statistics of the BatchNorm before the conv
 # (ewvit_dwconv3x3_bwd_data_bn; 0: that BN runs its own reduction pass, A/B)
 _DW_BWD_LINK = os.environ.get('EWVIT_DW_BWD_LINK', '1') != '0'
+# the linked stride-1 input gradient and the weight gradient in one pass
+# (ewvit_dwconv3x3_bwd_fused; 0: two kernels, A/B)
+_DW_BWD_FUSED = os.environ.get('EWVIT_DW_BWD_FUSED', '1') != '0'
 
 
 class DepthwiseConv3x3Fn(torch.autograd.Function):
@@ -584,6 +587,13 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         dx = dw = None
         bl = ctx.bnlink
         ctx.bnlink = None
+        if ctx.needs_input_grad[1]:
+            # the gradient slot itself when its layout is the kernel's [C][9] (ewvit.grads)
+            out = grad_out(ctx.params[0], ctx.gen) if wdt == torch.float32 else None
+            direct = out is not None and tuple(out.shape) == (C, 1, 3, 3) and all(
+                a == b for a, b, n in zip(out.stride(), (9, 9, 3, 1), out.shape) if n != 1)
+            dw = out if direct else torch.empty(C, 1, 3, 3, dtype=torch.float32, device=xc.device)
+        wdone = False
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(xc, memory_format=torch.channels_last)
             rows = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 1)) \
@@ -591,24 +601,30 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
             if 0 < rows <= _bn.BWD_LINK_MAX_ROWS:
                 # dx and the producing BatchNorm(+SiLU)'s backward sums in one pass
                 part = torch.empty(rows, 2 * C, dtype=torch.float32, device=xc.device)
-                L.call('ewvit_dwconv3x3_bwd_data_bn', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, L.ptr(bl.x),
-                       L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta), bl.act, L.ptr(part),
-                       L.stream(dx), work={'bytes': (dyc.numel() + 2 * dx.numel()) * dx.element_size()})
+                if dw is not None and _DW_BWD_FUSED and C % 8 == 0:
+                    # ... and the weight gradient, reading dy once
+                    wsb = L.load().ewvit_dwconv3x3_bwd_fused_workspace(N, H, W, C)
+                    ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
+                    L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dyc), L.ptr(w), L.ptr(dx), L.ptr(xc), L.ptr(dw), 0,
+                           N, H, W, C, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma),
+                           L.ptr(bl.beta), bl.act, L.ptr(part), L.ptr(ws), L.stream(dx),
+                           work={'bytes': (dyc.numel() + 3 * dx.numel()) * dx.element_size()})
+                    wdone = True
+                else:
+                    L.call('ewvit_dwconv3x3_bwd_data_bn', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, L.ptr(bl.x),
+                           L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma), L.ptr(bl.beta), bl.act, L.ptr(part),
+                           L.stream(dx), work={'bytes': (dyc.numel() + 2 * dx.numel()) * dx.element_size()})
                 bl.fulfil(part, rows, dx)
             else:
                 L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, stride, pad,
                        L.dt(xc), L.stream(dx), work={'bytes': (dyc.numel() + dx.numel()) * dx.element_size()})
-        if ctx.needs_input_grad[1]:
-            wsb = L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, stride, pad)
-            ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
-            # the gradient slot itself when its layout is the kernel's [C][9] (ewvit.grads)
-            out = grad_out(ctx.params[0], ctx.gen) if wdt == torch.float32 else None
-            direct = out is not None and tuple(out.shape) == (C, 1, 3, 3) and all(
-                a == b for a, b, n in zip(out.stride(), (9, 9, 3, 1), out.shape) if n != 1)
-            dw = out if direct else torch.empty(C, 1, 3, 3, dtype=torch.float32, device=xc.device)
-            L.call('ewvit_dwconv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dw), 0, N, H, W, C, stride, pad,
-                   L.dt(xc), L.ptr(ws), L.stream(dw),
-                   work={'bytes': (dyc.numel() + xc.numel()) * xc.element_size()})
+        if dw is not None:
+            if not wdone:
+                wsb = L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, stride, pad)
+                ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
+                L.call('ewvit_dwconv3x3_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dw), 0, N, H, W, C, stride, pad,
+                       L.dt(xc), L.ptr(ws), L.stream(dw),
+                       work={'bytes': (dyc.numel() + xc.numel()) * xc.element_size()})
             if wdt != torch.float32:
                 dw = dw.to(wdt)
             if not direct and dw.stride() != ctx.wstride:    # keep the parameter's layout (DDP bucket views)

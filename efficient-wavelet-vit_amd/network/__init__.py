@@ -22,25 +22,26 @@ def load_config(path='config/architecture.yaml'):
 
 
 def set_gemm_precision(model, precision='bf16'):
-    """BASELINE.json configs[4]: run the attention / MLP GEMMs — the ViT's to_qkv, to_out and
-    FeedForward (sfe.py:29-70), patch_to_embedding and feat_map (sfe.py:127,140,155), the
-    cross-attention's to_q, to_kv, to_out (dama.py:15-53) — on fp8 e4m3 operands with
-    per-tensor scaling ('fp8'), or back on bf16 ('bf16').  The conv stacks, the DWT, the
-    gates and the classifier keep bf16.  Returns the number of Linear modules switched."""
+    """BASELINE.json configs[4] ("fp8 (e4m3) MFMA for attention/MLP GEMMs"): run the attention
+    and MLP GEMMs — the ViT's to_qkv, to_out and FeedForward (sfe.py:29-70), the
+    cross-attention's to_q, to_kv, to_out (dama.py:15-53) — on MXFP8 e4m3 operands ('fp8'), or
+    back on bf16 ('bf16').  patch_to_embedding and feat_map (sfe.py:127,140,155), the conv
+    stacks, the DWT, the gates and the classifier keep bf16: the two projections are neither
+    attention nor MLP, and on MXFP8 they measured slower (tools/mx_gemm_bench.py, MI355X:
+    patch_to_embedding forward / dgrad / wgrad 57 / 42 / 130 us against 41 / 33 / 44 us bf16 —
+    bound by the 128 MB fp32 master weight, and the weight gradient's reduction is the 64 frames,
+    half of one 128-wide MX K step).  Returns the number of Linear modules switched."""
     from .dama import CrossAttention
-    from .sfe import Attention, EfficientViT, FeedForward, Linear
+    from .sfe import Attention, FeedForward, Linear
     if precision not in ('bf16', 'fp8'):
         raise ValueError(f'gemm precision {precision!r}: bf16 or fp8')
     n = 0
     for m in model.modules():
-        targets = []
         if isinstance(m, (Attention, FeedForward, CrossAttention)):
-            targets = [c for c in m.modules() if isinstance(c, Linear)]
-        elif isinstance(m, EfficientViT):
-            targets = [m.patch_to_embedding, m.feat_map[0]]
-        for t in targets:
-            t.gemm_precision = precision
-            n += 1
+            for t in m.modules():
+                if isinstance(t, Linear):
+                    t.gemm_precision = precision
+                    n += 1
     return n
 
 

@@ -221,6 +221,15 @@ int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, int64_t N, in
 int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void *dx, int64_t N, int64_t H, int64_t W,
                                 int64_t C, const void *bx, const float *mean, const float *invstd,
                                 const float *gamma, const float *beta, int act, float *part, void *stream);
+/* The whole stride-1 pad-1 backward in one pass: dx and part as bwd_data_bn, plus
+ * dw [C, 3, 3] f32 (= or += when accumulate) as ewvit_dwconv3x3_bwd_weight from x (the conv's
+ * bf16 input [N, H, W, C]), reading dy once; C % 8 == 0.  workspace: ..._bwd_fused_workspace
+ * bytes (one [C][9] slab per partial row). */
+int64_t ewvit_dwconv3x3_bwd_fused_workspace(int64_t N, int64_t H, int64_t W, int64_t C);
+int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *dx, const void *x, float *dw, int accumulate,
+                              int64_t N, int64_t H, int64_t W, int64_t C, const void *bx, const float *mean,
+                              const float *invstd, const float *gamma, const float *beta, int act, float *part,
+                              float *workspace, void *stream);
 
 /* ---------------------------------------------- BatchNorm2d + activation ---
  * BatchNorm2d (batch statistics in training, running statistics in eval) fused

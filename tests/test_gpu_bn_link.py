@@ -77,6 +77,9 @@ def _bwd_ref(dx, bx, mean, invstd, gamma, beta, act, rscale=None, hw=1):
         z = xh * gamma.double().cpu().view(1, C, 1, 1) + beta.double().cpu().view(1, C, 1, 1)
         s = torch.sigmoid(z)
         gr = d * s * (1 + z * (1 - s))
+    elif act == 1:
+        z = xh * gamma.double().cpu().view(1, C, 1, 1) + beta.double().cpu().view(1, C, 1, 1)
+        gr = d * (z > 0).double()
     else:
         gr = d
     if rscale is not None:
@@ -114,6 +117,60 @@ def test_dw_bwd_data_bn(N, C, H, W):
     ra, rb, ma, mb = _bwd_ref(dx1, bx, mean, invstd, gamma, beta, 2)
     ea, eb = sums_close(part, ra, rb, ma, mb)
     assert ea < 1e-5 and eb < 1e-5, (ea, eb)
+
+
+@pytest.mark.parametrize('N,C,H,W,act', [(64, 1536, 7, 7, 2), (64, 960, 14, 14, 2), (4, 200, 9, 11, 2),
+                                         (2, 64, 30, 30, 1), (3, 40, 1, 5, 0), (2, 48, 2, 1, 2)])
+def test_dw_bwd_fused(N, C, H, W, act):
+    """ewvit_dwconv3x3_bwd_fused (dx + the producing BN's backward sums + dW in one pass) against
+    the two kernels it replaces: dx bit-exact (same tap order), the BN sums as
+    test_dw_bwd_data_bn, dW within 1e-5 of its largest entry (fp32, other summation order);
+    accumulate = 1 adds into dW."""
+    L = _L()
+    g = torch.Generator().manual_seed(C * 5 + W)
+    dy = bf(torch.randn(N, C, H, W, generator=g))
+    x = bf(torch.randn(N, C, H, W, generator=g))
+    bx = bf(torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3)
+    w = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV).contiguous()
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    mean, invstd = _bn_stats(bx)
+    dx0, dx1 = torch.empty_like(dy), torch.empty_like(dy)
+    L.call('ewvit_dwconv3x3_bwd_data', L.ptr(dy), L.ptr(w), L.ptr(dx0), N, H, W, C, 1, 1, L.BF16, L.stream(dy))
+    ws0 = torch.empty(int(L.load().ewvit_dwconv3x3_bwd_weight_workspace(N, H, W, C, 1, 1)) // 4, device=DEV)
+    dw0 = torch.empty(C, 1, 3, 3, device=DEV)
+    L.call('ewvit_dwconv3x3_bwd_weight', L.ptr(x), L.ptr(dy), L.ptr(dw0), 0, N, H, W, C, 1, 1, L.BF16, L.ptr(ws0),
+           L.stream(dy))
+    nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1))
+    part = torch.full((nrc, 2 * C), float('nan'), device=DEV)
+    wsb = int(L.load().ewvit_dwconv3x3_bwd_fused_workspace(N, H, W, C))
+    assert wsb == nrc * C * 9 * 4
+    ws = torch.full((wsb // 4,), float('nan'), device=DEV)
+    dw1 = torch.full((C, 1, 3, 3), float('nan'), device=DEV)
+    L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dy), L.ptr(w), L.ptr(dx1), L.ptr(x), L.ptr(dw1), 0, N, H, W, C,
+           L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), act, L.ptr(part), L.ptr(ws), L.stream(dy))
+    dwa = torch.full((C, 1, 3, 3), 0.5, device=DEV)
+    part2 = torch.empty_like(part)
+    L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dy), L.ptr(w), L.ptr(dx1), L.ptr(x), L.ptr(dwa), 1, N, H, W, C,
+           L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), act, L.ptr(part2), L.ptr(ws), L.stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    ra, rb, ma, mb = _bwd_ref(dx1, bx, mean, invstd, gamma, beta, act)
+    ea, eb = sums_close(part, ra, rb, ma, mb)
+    assert ea < 1e-5 and eb < 1e-5, (ea, eb)
+    assert torch.equal(part, part2)
+    ref = torch.zeros(C, 9, dtype=torch.float64)
+    xp = torch.nn.functional.pad(x.double().cpu(), (1, 1, 1, 1))
+    dyd = dy.double().cpu()
+    for kh in range(3):
+        for kw in range(3):
+            ref[:, kh * 3 + kw] = (dyd * xp[:, :, kh:kh + H, kw:kw + W]).sum((0, 2, 3))
+    ref = ref.view(C, 1, 3, 3).float().to(DEV)
+    scale = float(ref.abs().max())
+    assert not torch.isnan(dw1).any()
+    assert float((dw1 - ref).abs().max()) / scale < 1e-5
+    assert float((dw1 - dw0).abs().max()) / scale < 1e-5
+    assert float((dwa - 0.5 - dw1).abs().max()) / scale < 1e-6
 
 
 @pytest.mark.parametrize('N,H,W,Cin,Cout,act,addend,scaled', [
@@ -252,7 +309,9 @@ def test_mbconv_blocks_linked_vs_unlinked(monkeypatch):
     y1, gx1, gp1, bf1, c1 = _run(mods, x0, dyo, True, monkeypatch)
     assert c0.get('ewvit_bn_bwd_partials', 0) == 0
     assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == 4
-    assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == 3          # 6.0's depthwise is stride 2
+    # 6.0's depthwise is stride 2; the stride-1 ones take dx, the link and dW in one pass
+    assert c1.get('ewvit_dwconv3x3_bwd_fused', 0) == 3 and c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == 0
+    assert c1.get('ewvit_dwconv3x3_bwd_weight', 0) == 1 and c0.get('ewvit_dwconv3x3_bwd_weight', 0) == 4
     # the tails of 5.7, 5.8, 6.0
     assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == 3
     assert c1.get('ewvit_bn_bwd_partials', 0) == 6
@@ -287,7 +346,8 @@ def test_mbconv_stages_link_count(monkeypatch):
     y1, gx1, gp1, _, c1 = _run(_features(sl), x0, dyo, True, monkeypatch)
     nblk = 30
     assert c1.get('ewvit_dwconv3x3_fwd_bn', 0) == nblk
-    assert c1.get('ewvit_dwconv3x3_bwd_data_bn', 0) == nblk - 2          # blocks 4.0 / 6.0 are stride 2
+    assert c1.get('ewvit_dwconv3x3_bwd_fused', 0) == nblk - 2            # blocks 4.0 / 6.0 are stride 2
+    assert c1.get('ewvit_dwconv3x3_bwd_weight', 0) == 2
     # the last tail has no conv after it
     assert c1.get('ewvit_conv2d_bwd_data_bn', 0) == nblk - 1
     assert c1.get('ewvit_bn_bwd_partials', 0) == 2 * nblk - 3

@@ -16,7 +16,7 @@ Kernel level (ewvit_gemm_mx8 through the C-ABI):
 
 Module level: the DAMA train step with network.set_gemm_precision(model, 'fp8') against the
 fp32 oracle, bounded by an fp8 YARDSTICK measured in the test (the reference's own module
-sequence on the GPU under torch's bf16 autocast with its 22 token GEMMs' operands cast through
+sequence on the GPU under torch's bf16 autocast with its 20 attention / MLP GEMMs' operands cast through
 torch.float8_e4m3fn, per-tensor scaled, fp32 accumulation — forward and both backward GEMMs);
 and the config-5 chunking (16 videos x 8 frames, batch_size=4 -> two 64-frame chunks) equal to
 composing _process_frame per chunk.
@@ -179,18 +179,18 @@ def _errs(a, b):
 
 
 def test_dama_train_step_fp8_vs_oracle_and_fp8_yardstick():
-    """DAMA train step (2 videos x 8 frames, batch_size 4: two 8-frame chunks) with the 22
-    token GEMMs on MXFP8 (the fused ViT layer and head kernels, ewvit_gemm_mx8 for
-    patch_to_embedding / feat_map) against the fp32 oracle, bounded by the in-test fp8 yardstick."""
+    """DAMA train step (2 videos x 8 frames, batch_size 4: two 8-frame chunks) with the 20
+    attention / MLP GEMMs on MXFP8 (the fused ViT layer and head kernels) against the fp32
+    oracle, bounded by the in-test fp8 yardstick (the same 20 Linears per-tensor e4m3)."""
     from network import dama, set_gemm_precision
     from oracle import model as om
     from oracle.weights import recipe_input
     from test_gpu_modules import pair
     torch.manual_seed(0)
     p, o = pair(dama.DAMA, om.DAMA, (3, 128, 4, 3, 8), 14)
-    assert set_gemm_precision(p, 'fp8') == 22
+    assert set_gemm_precision(p, 'fp8') == 20
     names = [n for n, m in p.named_modules() if getattr(m, 'gemm_precision', 'bf16') == 'fp8']
-    assert len(names) == 22
+    assert len(names) == 20
     p.train(); o.train()
     x = recipe_input((2, 8, 3, 224, 224), seed=4242)
     yards = [_fp8_yardstick(o, names, x, 4)]
@@ -215,10 +215,13 @@ def test_dama_train_step_fp8_vs_oracle_and_fp8_yardstick():
         torch.cuda.synchronize()
     finally:
         ewvit._lib.call = real
-    # the fused MX token kernels ran (and no bf16 GEMM on the token path: every remaining
-    # ewvit_gemm launch would be a bf16 token GEMM)
+    # the fused MX token kernels ran; the generic GEMMs left are the bf16 patch_to_embedding /
+    # feat_map ones (dgrad + wgrad of patch_to_embedding, forward + dgrad + wgrad of feat_map per
+    # chunk; the patch_to_embedding forward is ewvit_gemm_tallk) and the FeedForward's second
+    # MXFP8 GEMM per layer and chunk in the forward
+    print(calls)
     assert calls.get('ewvit_vit_pack_mx') == 2 and calls.get('ewvit_head_fwd') == 2, calls
-    assert 'ewvit_gemm' not in calls and calls.get('ewvit_gemm_mx8', 0) <= 12, calls
+    assert calls.get('ewvit_gemm', 0) <= 10 and calls.get('ewvit_gemm_mx8', 0) <= 12, calls
     fails = []
 
     def judge(kind, prod, ys, floor_err, floor_cos):
@@ -248,8 +251,10 @@ def test_set_gemm_precision_targets():
     from network import set_gemm_precision
     from network.model import DeepfakeDetector
     m = DeepfakeDetector(3, 128, 4)
-    assert set_gemm_precision(m, 'fp8') == 22
-    assert m.dama.sfe.patch_to_embedding.gemm_precision == 'fp8'
+    assert set_gemm_precision(m, 'fp8') == 20
+    assert m.dama.sfe.transformer.layers[0][0].fn.to_qkv.gemm_precision == 'fp8'
+    assert getattr(m.dama.sfe.patch_to_embedding, 'gemm_precision', 'bf16') == 'bf16'
+    assert getattr(m.dama.sfe.feat_map[0], 'gemm_precision', 'bf16') == 'bf16'
     assert getattr(m.classifier[0], 'gemm_precision', 'bf16') == 'bf16'
     assert getattr(m.dama.gate_net[2], 'gemm_precision', 'bf16') == 'bf16'
     with pytest.raises(ValueError):
