@@ -31,6 +31,8 @@
 #include "conv_common.h"
 
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 namespace ewvit {
 
@@ -644,7 +646,8 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   const int py = a.pc >> 1, px = a.pc & 1;
   const int ntaps = cls ? a.ntap : KS * KS;
   const int CC = a.KC >> 3;                // DENSE: 8-channel chunks per tap
-  const int nk = DENSE ? (K + BK - 1) / BK : ntaps * cbn;
+  const int KSP = a.ksplit;                // split K: K-tiles per work item nk / KSP
+  const int nk = (DENSE ? (K + BK - 1) / BK : ntaps * cbn) / KSP;
   const int tq = DENSE ? 8 / CC : 0, tr = DENSE ? 8 % CC : 0;   // DENSE: per-K-tile tap / chunk advance
   const int ls = a.g.stride >> 1, smask = a.g.stride - 1;
   const __amdgpu_buffer_rsrc_t rs = mk_rsrc(a.src, src_bytes);
@@ -676,10 +679,12 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
   // live input window (its pixels + halo, 64 channels) stays small enough for the
   // XCD's L2 to serve the tap re-reads; otherwise taps are outer.
   int ltap = 0, lcb = 0, lgi = 0, lcin = 0;
-  auto setup = [&](int tile) {          // the staged tile's row / column offsets
+  auto setup = [&](int item) {          // the staged tile's row / column offsets
+  const int tile = item / KSP;
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
   ltap = 0; lcb = 0; lgi = 0; lcin = 0;
+  if (KSP > 1) { lcb = (item % KSP) * nk; lcin = lcb * BK; }   // (1x1, one channel group)
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int p = ws * PA + j, r = p * 8 + (lane >> 3);
@@ -826,7 +831,7 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     lbuf = lbuf + 1 == NS ? 0 : lbuf + 1;
   }
   for (int ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
-  const int tile = xcd_remap(ti, ntiles);
+  const int item = xcd_remap(ti, ntiles), tile = item / KSP;
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN_;
 #pragma unroll
@@ -863,6 +868,23 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     }
     compute(cur);
     cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  if (KSP > 1) {
+    // split K: the fp32 partial tile, 16 B (4 columns of one row) per lane and row
+    float *kp = a.kpart + (int64_t)(item % KSP) * a.M * a.Ncol;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int col = n0 + wn * WN + j * 16 + fq * 4;
+      if (col >= a.Ncol) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + wm * 64 + i * 16 + fr;
+        if (row < a.M)
+          *reinterpret_cast<float4 *>(kp + row * a.Ncol + col) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    continue;
   }
   // epilogue: (+ bias) -> bf16, 8-B stores of 4 consecutive channels per lane
   // (Ncol % 8 == 0 and group widths % 32 == 0: a 4-channel run never straddles)
@@ -1019,6 +1041,109 @@ __global__ __launch_bounds__(BM / 64 * WC * 64) void conv_glds_kernel(FwdArgs a,
     }
   }
   }
+  }
+}
+
+// ---- split-K epilogue (conv_glds_kernel with FwdArgs::ksplit > 1; 1x1, plain layouts): block
+// = one bm-row m-tile (the tile the BatchNorm partial rows follow) x 64 columns; thread = 4
+// columns x rows r, r + 16, .. of the tile.  It adds the splits' fp32 partials in split order,
+// then runs conv_glds_kernel's epilogue once: (+ bias, + addend) -> bf16, and MODE 1 the
+// forward statistics sum (y - K), sum (y - K)^2 / MODE 2 the backward statistics (BST: sum g,
+// sum g * xhat) of the tile, its 16 row lanes added in order through LDS.
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_splitk_epi_kernel(FwdArgs a, int bm) {
+  __shared__ float red[16][64][2];
+  const int tid = threadIdx.x, cq = tid & 15, rl = tid >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * bm;
+  const int col = blockIdx.y * 64 + cq * 4;
+  const bool cok = col < a.Ncol;
+  const int64_t plane = a.M * a.Ncol;
+  const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bv = (cok && a.bias) ? *reinterpret_cast<const float4 *>(a.bias + col) : zero;
+  const float4 kv = (MODE == 1 && cok && a.bn_shift) ? *reinterpret_cast<const float4 *>(a.bn_shift + col) : zero;
+  float mu[4] = {0.f, 0.f, 0.f, 0.f}, iv[4] = {0.f, 0.f, 0.f, 0.f};
+  float ga[4] = {1.f, 1.f, 1.f, 1.f}, be[4] = {0.f, 0.f, 0.f, 0.f};
+  if (MODE == 2 && cok) {
+    const int64_t sidx = (a.bwd.grows ? m0 / a.bwd.grows * a.ogc : 0) + col;
+    const float4 mu4 = *reinterpret_cast<const float4 *>(a.bwd.mean + sidx);
+    const float4 iv4 = *reinterpret_cast<const float4 *>(a.bwd.invstd + sidx);
+    mu[0] = mu4.x; mu[1] = mu4.y; mu[2] = mu4.z; mu[3] = mu4.w;
+    iv[0] = iv4.x; iv[1] = iv4.y; iv[2] = iv4.z; iv[3] = iv4.w;
+    if (a.bwd.gamma) {
+      const float4 g4 = *reinterpret_cast<const float4 *>(a.bwd.gamma + col);
+      ga[0] = g4.x; ga[1] = g4.y; ga[2] = g4.z; ga[3] = g4.w;
+    }
+    if (a.bwd.beta) {
+      const float4 b4 = *reinterpret_cast<const float4 *>(a.bwd.beta + col);
+      be[0] = b4.x; be[1] = b4.y; be[2] = b4.z; be[3] = b4.w;
+    }
+  }
+  float cs[4] = {0.f, 0.f, 0.f, 0.f}, cqq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (cok) {
+    for (int r = rl; r < bm; r += 16) {
+      const int64_t row = m0 + r;
+      if (row >= a.M) break;
+      const float *kp = a.kpart + row * a.Ncol + col;
+      float4 t = *reinterpret_cast<const float4 *>(kp);
+      for (int sp = 1; sp < a.ksplit; ++sp) {
+        const float4 u = *reinterpret_cast<const float4 *>(kp + sp * plane);
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      float4 av = bv;
+      if (a.addend) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(a.addend + row * a.ogc + col);
+        av.x += __uint_as_float(q.x << 16); av.y += __uint_as_float(q.x & 0xffff0000u);
+        av.z += __uint_as_float(q.y << 16); av.w += __uint_as_float(q.y & 0xffff0000u);
+      }
+      const bf16_t h0 = f2bf(t.x + av.x), h1 = f2bf(t.y + av.y), h2 = f2bf(t.z + av.z), h3 = f2bf(t.w + av.w);
+      uint2 pk;
+      pk.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      pk.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
+      *reinterpret_cast<uint2 *>(a.out + row * a.ogc + col) = pk;
+      const float hv[4] = {bf2f(h0), bf2f(h1), bf2f(h2), bf2f(h3)};
+      if (MODE == 1) {
+        const float kk[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d = hv[q] - kk[q];
+          cs[q] += d;
+          cqq[q] = fmaf(d, d, cqq[q]);
+        }
+      } else if (MODE == 2) {
+        const uint2 xq = *reinterpret_cast<const uint2 *>(a.bwd.x + row * a.ogc + col);
+        const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
+                             __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
+        const float brs = a.bwd.rscale ? a.bwd.rscale[row / a.bwd.hw] : 1.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float xh = (xv[q] - mu[q]) * iv[q];
+          const float g = a.bwd.act ? hv[q] * bn_act_grad(a.bwd.act, fmaf(xh, ga[q], be[q])) : hv[q] * brs;
+          cs[q] += g;
+          cqq[q] = fmaf(g, xh, cqq[q]);
+        }
+      }
+    }
+  }
+  if (MODE == 0) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { red[rl][cq * 4 + q][0] = cs[q]; red[rl][cq * 4 + q][1] = cqq[q]; }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = blockIdx.y * 64 + tid;
+    if (c < a.Ncol) {
+      float S = 0.f, Q = 0.f;
+      for (int q = 0; q < 16; ++q) { S += red[q][tid][0]; Q += red[q][tid][1]; }
+      const int64_t t = blockIdx.x;
+      if (MODE == 2) {
+        float *pr = a.bwd.part + t * 2 * a.ogc;
+        pr[c] = S;
+        pr[a.ogc + c] = Q;
+      } else {
+        a.bn_part[t * 2 * a.Ncol + c] = S;
+        a.bn_part[t * 2 * a.Ncol + a.Ncol + c] = Q;
+        if (t == 0 && a.bn_shift_out) a.bn_shift_out[c] = a.bn_shift ? a.bn_shift[c] : 0.f;
+      }
+    }
   }
 }
 
@@ -1552,8 +1677,42 @@ static void glds_tile(const FwdArgs &a, bool dgrad, int &bm, int &bn) {
   }
 }
 
+// split K for the LDS-DMA 1x1 fwd / dgrad (FwdArgs::ksplit): the backbone's long-K 1x1 convs
+// over few tiles — stage 6's project forward / expand input gradient (3136 x 256 x 1536: 196
+// workgroups of 24 K-tiles), the head conv (K = 1280) — run their K loop serially per workgroup
+// on < 256 workgroups.  Split into S ranges (S | K-tiles, >= g_ksplit_min_kt K-tiles each, <= 1024
+// work items), fp32 partials in a per-stream scratch buffer, conv_splitk_epi_kernel for the
+// epilogue.  OFF by default: measured slower in the step at every setting — S <= 2 / >= 8 K-tiles
+// 3725-3729, S <= 2 / >= 4 3710, S <= 4 / >= 8 3708-3713, S <= 8 / >= 4 3665-3679 against
+// 3755-3766 frames/s unsplit (same box, profiles/r06/ab/ksplit.log): beside the MWT the step is
+// bound by CU-time and memory traffic, which the partials and the epilogue pass add to, not by
+// these kernels' latency.  ewvit_conv2d_set_ksplit(1) / EWVIT_CONV_KSPLIT=1: on (tests, A/B).
+static int g_ksplit = 0, g_ksplit_max = 2, g_ksplit_min_kt = 8;
+extern "C" int ewvit_conv2d_set_ksplit(int on) {
+  const int prev = g_ksplit;
+  g_ksplit = on ? 1 : 0;
+  if (on > 1) { g_ksplit_max = on & 15; g_ksplit_min_kt = on >> 4; }   // tuning: max S | min K-tiles << 4
+  return prev;
+}
+// the split partials' scratch, one buffer per stream (the branches run convs concurrently),
+// grown outside stream capture only (nullptr -> the caller runs unsplit); a replaced buffer is
+// kept, since kernels queued on the stream may still read it
+static float *ksplit_scratch(hipStream_t s, size_t bytes) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, std::pair<void *, size_t>> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  auto &e = bufs[s];
+  if (e.second >= bytes) return static_cast<float *>(e.first);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  e = {p, bytes};
+  return static_cast<float *>(p);
+}
+
 template <bool DGRAD>
-static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int *bm_out = nullptr) {
+static bool launch_glds(FwdArgs a, int64_t src_bytes, hipStream_t s, int *bm_out = nullptr) {
   const int64_t K = (int64_t)a.g.ks * a.g.ks * a.KC;
   const bool padded = a.KCr && a.KCr != a.KC;     // plain x, channels padded to 64 per tap
   // ragged: plain (ungrouped) x whose per-tap K is not a multiple of 64 — the last
@@ -1593,8 +1752,20 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
   const bool big = BM == 256;
   if (bm_out) *bm_out = BM;
   const int64_t mt = (a.M + BM - 1) / BM;
-  const int64_t nwg = mt * ntn;
+  int64_t nwg = mt * ntn;
   if (nwg >= (int64_t)1 << 31) return false;
+  int S = 1;
+  if (g_ksplit && a.g.ks == 1 && a.pc < 0 && !padded && !ragged && a.sgs == 0 && a.sgc == a.KC && a.ogs == 0 &&
+      a.ogc == a.Ncol && !big && nwg < 256) {
+    const int nkt = a.KC / 64;
+    for (int c = g_ksplit_max; c >= 2; --c)
+      if (nkt % c == 0 && nkt / c >= g_ksplit_min_kt && nwg * c <= 1024) { S = c; break; }
+    if (S > 1) {
+      float *ws = ksplit_scratch(s, (size_t)S * a.M * a.Ncol * sizeof(float));
+      if (ws) { a.ksplit = S; a.kpart = ws; nwg *= S; }
+      else S = 1;
+    }
+  }
   const int ntiles = (int)nwg;
   const dim3 grid((unsigned)(g_grid_cap > 0 && nwg > g_grid_cap ? g_grid_cap : nwg));
 #define EWVIT_GLDS_FWDW(BM_, BN__, NS_, WC_, BST_)                                                                  \
@@ -1615,13 +1786,14 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
   const bool w8 = nwg <= 2048 || (DGRAD && bn == 128);
   const bool sg = nwg <= 256;
   constexpr bool BST = DGRAD;      // (the statistics epilogue is a separate instantiation)
+  const bool bst = DGRAD && a.bwd.part && S == 1;   // (split K: the epilogue kernel sums them)
   if (BM == 64) {
-    if (DGRAD && a.bwd.part) {
+    if (bst) {
       if (bn == 64) EWVIT_GLDS_FWDW(64, 64, 4, 4, BST);
       else EWVIT_GLDS_FWDW(64, 128, 4, 4, BST);
     } else if (bn == 64) EWVIT_GLDS_FWDW(64, 64, 4, 4, false);
     else EWVIT_GLDS_FWDW(64, 128, 4, 4, false);
-  } else if (DGRAD && a.bwd.part) {
+  } else if (bst) {
     // the backward-statistics epilogue: 128-row tiles (the partial rows
     // ewvit_conv2d_bwd_bn_rows promised)
     if (bn == 32) EWVIT_GLDS_FWDW(128, 32, 2, 2, BST);
@@ -1646,6 +1818,12 @@ static bool launch_glds(const FwdArgs &a, int64_t src_bytes, hipStream_t s, int 
     else EWVIT_GLDS_FWDW(128, 128, 2, 2, false);
   }
 #undef EWVIT_GLDS_FWDW
+  if (S > 1) {
+    const dim3 eg((unsigned)mt, (unsigned)((a.Ncol + 63) / 64));
+    if (DGRAD && a.bwd.part) hipLaunchKernelGGL(conv_splitk_epi_kernel<2>, eg, dim3(256), 0, s, a, BM);
+    else if (!DGRAD && a.bn_part) hipLaunchKernelGGL(conv_splitk_epi_kernel<1>, eg, dim3(256), 0, s, a, BM);
+    else hipLaunchKernelGGL(conv_splitk_epi_kernel<0>, eg, dim3(256), 0, s, a, BM);
+  }
   return true;
 }
 

@@ -62,6 +62,11 @@ struct FwdArgs {
   // coefficients (ewvit_bn_coef) — instead of x; channel group g = c / sgc, zero padding after
   // the transform
   const float *xf = nullptr;
+  // split K (LDS-DMA 1x1 fwd / dgrad over few tiles, conv.hip launch_glds): work item i is
+  // (tile i / ksplit, K-range i % ksplit of nk / ksplit K-tiles), which stores its fp32 partial
+  // tile at kpart[split][M][Ncol]; conv_splitk_epi_kernel sums the splits and runs the epilogue
+  int ksplit = 1;
+  float *kpart = nullptr;
 };
 
 typedef __attribute__((address_space(3))) void lds_t;

@@ -61,6 +61,7 @@ SIGNATURES = {
     'ewvit_conv2d_set_wgrad_wide': [_i32],
     'ewvit_conv2d_set_wgrad_1x1': [_i32, _i32, _i32],
     'ewvit_conv2d_set_small_tiles': [_i32],
+    'ewvit_conv2d_set_ksplit': [_i32],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -199,6 +200,8 @@ def load():
         fn.restype = res
     if os.environ.get('EWVIT_SMALL_TILES') == '0' and hasattr(lib, 'ewvit_conv2d_set_small_tiles'):
         lib.ewvit_conv2d_set_small_tiles(0)          # A/B switch (conv.hip glds_tile)
+    if os.environ.get('EWVIT_CONV_KSPLIT') and hasattr(lib, 'ewvit_conv2d_set_ksplit'):
+        lib.ewvit_conv2d_set_ksplit(int(os.environ['EWVIT_CONV_KSPLIT']))   # A/B (conv.hip split K)
     if os.environ.get('EWVIT_LDS_PAD') == '0' and hasattr(lib, 'ewvit_conv2d_set_lds_pad'):
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
     if os.environ.get('EWVIT_WGWIN_TS') in ('0', '2') and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):

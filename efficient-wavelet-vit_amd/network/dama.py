@@ -201,6 +201,17 @@ class DAMA(nn.Module):                                                     # dam
         probe.stamp(0, dev)                # (timeline probes: no-ops unless EWVIT_PROBE=1)
         side.wait_stream(main)             # fork before the SFE work is issued on main
 
+        if probe.ON and not getattr(self, '_probe_hooks', False):
+            # slot 8: the last MWT parameter gradient accumulated (~ the MWT backward's end)
+            for p in self.mwt.parameters():
+                if p.requires_grad:
+                    p.register_post_accumulate_grad_hook(lambda _p: probe.stamp(8, _p.device))
+            # slot 10: the last SFE parameter gradient accumulated (~ the backbone backward's end)
+            for p in self.sfe.parameters():
+                if p.requires_grad:
+                    p.register_post_accumulate_grad_hook(lambda _p: probe.stamp(10, _p.device))
+            self._probe_hooks = True
+
         def mwt():
             with torch.cuda.stream(side), ewvit._lib.grid_cap(_mwt_grid_cap()):
                 probe.stamp(2, dev)

@@ -418,6 +418,13 @@ int ewvit_conv2d_wgrad_1x1_config(int which);
 /* LDS-DMA fwd / dgrad on grids of < 128 row tiles: 64-row (and 64-column) tiles, 1 (default),
  * or the 128-row tiles everywhere, 0 (test switch).  Returns the previous setting. */
 int ewvit_conv2d_set_small_tiles(int on);
+/* Split K (default OFF: measured slower in the step) for the LDS-DMA 1x1 forward / input
+ * gradient over fewer than 256 tiles with >= 8 K-tiles per split (the backbone's long-K 1x1
+ * convs at 7^2): fp32 partials in a per-stream scratch buffer the library owns (allocated
+ * outside stream capture), summed by an epilogue launch that also forms the BatchNorm
+ * statistics.  on > 1 sets the limits too (max splits = on & 15, min K-tiles = on >> 4).
+ * Returns the previous on / off setting. */
+int ewvit_conv2d_set_ksplit(int on);
 /* Input channels per tap the forward expects its packed weights to have (the Cin_pad
  * of ewvit_conv2d_pack_weight for the fwd pack): Cin, or Cin rounded up to 64 when a
  * plain-NHWC input's channel count is not a multiple of 64 and the LDS-DMA kernel runs

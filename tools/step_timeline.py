@@ -5,6 +5,8 @@ the branches overlap as they do in the bench.  Milliseconds since the fork (slot
   1 SFE forward end (main)          2 MWT forward start (side)     3 MWT forward end (side)
   4 SFE backward start (main)       5 MWT backward start (side)       9 step end (after Adam)
   7 backbone forward end (main)     6 token-path backward end = backbone backward start (main)
+  8 last MWT parameter gradient accumulated (~ MWT backward end)
+ 10 last SFE parameter gradient accumulated (~ backbone backward end)
 
 Usage: python tools/step_timeline.py [--steps 5]  (sets EWVIT_PROBE=1 itself)"""
 import argparse
