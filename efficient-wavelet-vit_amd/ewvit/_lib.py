@@ -297,10 +297,14 @@ def grid_cap(n):
         _tls.cap = prev
 
 
+# the backward's cap for ops whose forward ran capped (EWVIT_MWT_BWD_CAP, A/B; unset: the same cap)
+_BWD_CAP = int(os.environ.get('EWVIT_MWT_BWD_CAP', '0') or 0)
+
+
 def bwd_cap(n):
-    """The cap for the backward of an op whose forward ran under cap n: the same (one cap of
-    160 balances both phases)."""
-    return n
+    """The cap for the backward of an op whose forward ran under cap n: the same (one cap
+    balances both phases), or EWVIT_MWT_BWD_CAP when set."""
+    return _BWD_CAP if (n and _BWD_CAP > 0) else n
 
 
 def current_cap():
