@@ -52,7 +52,10 @@ int g_lds_pad = 1;
 // the non-temporal hint on the windowed kernels' activation-window DMAs (the windows stream
 // through once per tile; the hint keeps them from displacing the concurrent backbone's L2 lines):
 // config 2 +0.26 / +0.34 / +0.63 % in three interleaved same-box rounds and +0.7 / +0.5 % on
-// another box (profiles/r06/ab/win_nt*.log); EWVIT_WIN_NT=0 / ewvit_conv2d_set_win_nt(0): off
+// another box (profiles/r06/ab/win_nt*.log).  Only under a grid cap, i.e. beside the other
+// stream: the MWT alone (config 4, uncapped) re-reads the window halos through L2 and lost 3.7 %
+// with the hint (1497 against 1554 frames/s, profiles/r06/ab/win_nt_config4.log).
+// EWVIT_WIN_NT=0 / ewvit_conv2d_set_win_nt(0): off everywhere
 int g_win_nt = 1;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
@@ -983,7 +986,7 @@ static void launch_wgrad_win_t(const WgradArgs &a, int64_t x_bytes, int splits, 
 
 bool launch_wgrad_win(const WgradArgs &a_in, int64_t x_bytes, int splits, hipStream_t s) {
   WgradArgs a = a_in;
-  a.nt = g_win_nt;
+  a.nt = g_win_nt && g_grid_cap > 0;   // beside the backbone only (see g_win_nt)
   const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const bool b = a.dbias_part != nullptr, x = a.xf != nullptr;
@@ -1002,7 +1005,7 @@ bool launch_wgrad_win(const WgradArgs &a_in, int64_t x_bytes, int splits, hipStr
 
 bool launch_win(const FwdArgs &a_in, int64_t src_bytes, bool dgrad, hipStream_t s) {
   FwdArgs a = a_in;
-  a.nt = g_win_nt;
+  a.nt = g_win_nt && g_grid_cap > 0;   // beside the backbone only (see g_win_nt)
   if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
   const bool ks = win_ks(a, dgrad);
   const int ntn = ks ? 1 : a.Ncol / 128;

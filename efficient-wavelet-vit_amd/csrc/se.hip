@@ -613,8 +613,20 @@ __global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restri
     const int j = j0 + lane;
     float acc = 0.f;
     if (j < Csq) {
+      // the wave's 16 channels k = w, w + 4, .. (nc <= SE_CB = 64): all 16 loads issued before
+      // the first FMA (a load-FMA loop waited out each load's latency: 16 serial L2 round
+      // trips), then the FMAs in the same k order (the same bits)
+      // (branch-free: past the chunk's nc channels the load repeats channel nc - 1 and meets
+      // dsh[k] = 0 — d is 0 for channels >= C — so the FMA adds an exact zero)
       const float *wr = w2 + (int64_t)c0 * Csq + j;
-      for (int k = w; k < nc; k += 4) acc = fmaf(wr[(int64_t)k * Csq], dsh[k], acc);
+      float wv[SE_CB / 4];
+#pragma unroll
+      for (int u = 0; u < SE_CB / 4; ++u) {
+        const int k = w + 4 * u;
+        wv[u] = wr[(int64_t)(k < nc ? k : nc - 1) * Csq];
+      }
+#pragma unroll
+      for (int u = 0; u < SE_CB / 4; ++u) acc = fmaf(wv[u], dsh[w + 4 * u], acc);
     }
     red[w][lane] = acc;
     __syncthreads();

@@ -307,6 +307,12 @@ def bwd_cap(n):
     return _BWD_CAP if (n and _BWD_CAP > 0) else n
 
 
+def has(name):
+    """The loaded library exports `name` (an older EWVIT_LIB build for an A/B may not: the
+    callers of entry points added within an ABI version fall back to the older path)."""
+    return hasattr(load(), name)
+
+
 def current_cap():
     return getattr(_tls, 'cap', 0)
 

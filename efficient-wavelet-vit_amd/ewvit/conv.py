@@ -195,6 +195,8 @@ def _bn_link_win(bl, xc, xdt, levels, N, H, W, Cx, Cout, k, stride, skip):
     if bl.groups > 1 and M % bl.groups:
         return None
     grows = M // bl.groups if bl.groups > 1 else 0
+    if not L.has('ewvit_conv2d_bwd_bn_win_rows'):
+        return None
     rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, k, stride, Cx, 0, grows))
     return (grows, rows) if rows > 0 else None
 
@@ -485,7 +487,8 @@ class BnReluConvFn(torch.autograd.Function):
         # backward's per-block sums of g = da * relu'(.) and g * xhat
         da = torch.empty_like(zc, memory_format=torch.channels_last)
         work = {'flops': 2.0 * N * H * W * Cx * 9 * Cout, 'bytes': (dyc.numel() + da.numel() + wpt.numel()) * 2}
-        rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs, 0)) if _BN_BWD_EPI else 0
+        rows = int(L.load().ewvit_conv2d_bwd_bn_win_rows(N, H, W, Cx, Cout, 3, 1, C, gs, 0)) \
+            if _BN_BWD_EPI and L.has('ewvit_conv2d_bwd_bn_win_rows') else 0
         bpart = None
         if rows > 0:
             work['bytes'] += zc.numel() * 2        # the BST epilogue reads the BatchNorm input z

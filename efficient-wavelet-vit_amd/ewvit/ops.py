@@ -601,7 +601,7 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
             if 0 < rows <= _bn.BWD_LINK_MAX_ROWS:
                 # dx and the producing BatchNorm(+SiLU)'s backward sums in one pass
                 part = torch.empty(rows, 2 * C, dtype=torch.float32, device=xc.device)
-                if dw is not None and _DW_BWD_FUSED and C % 8 == 0:
+                if dw is not None and _DW_BWD_FUSED and C % 8 == 0 and L.has('ewvit_dwconv3x3_bwd_fused'):
                     # ... and the weight gradient, reading dy once
                     wsb = L.load().ewvit_dwconv3x3_bwd_fused_workspace(N, H, W, C)
                     ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
