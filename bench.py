@@ -189,7 +189,8 @@ ENTRY_KERNELS = {
     'ewvit_dwconv3x3_bwd_data': ['dw_row_bf16_kernel<1, true>', 'dw_bwd_data_kernel'],
     'ewvit_dwconv3x3_bwd_weight': ['dw_wgrad_row_bf16_kernel', 'dw_bwd_weight_partial_kernel',
                                    'dw_bwd_weight_reduce_kernel'],
-    'ewvit_dwconv3x3_bwd_fused': ['dw_bwd_fused_kernel'],
+    'ewvit_dwconv3x3_bwd_fused': ['dw_row4_kernel<2, 0, true>', 'dw_row4_kernel<2, 1, true>',
+                                  'dw_row4_kernel<2, 2, true>'],
     'ewvit_conv2d_fwd': ['conv_fwd_kernel<false', 'conv_glds_kernel<false', 'conv_win_kernel<false, false, false'],
     'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true', 'conv_glds_kernel<true', 'conv_win_kernel<true, false, false, false'],
     'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_glds_kernel', 'conv_wgrad_1x1_kernel',

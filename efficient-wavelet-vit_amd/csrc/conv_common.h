@@ -165,7 +165,7 @@ struct WgradArgs {
   int xgc;
   int64_t xgs;
   const float *xf = nullptr;  // input transform of the windowed wgrad (FwdArgs::xf; groups of xgc)
-  int nt = 0;                 // windowed wgrad: non-temporal hint on the dy / x window DMAs
+  int nt = 0;                 // windowed wgrad: non-temporal hint, 1 the dy tile DMAs, 2 the x windows'
 };
 
 __device__ __forceinline__ int swz_off(int r, int ch) {

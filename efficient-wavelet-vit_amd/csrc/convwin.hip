@@ -55,8 +55,9 @@ int g_lds_pad = 1;
 // another box (profiles/r06/ab/win_nt*.log).  Only under a grid cap, i.e. beside the other
 // stream: the MWT alone (config 4, uncapped) re-reads the window halos through L2 and lost 3.7 %
 // with the hint (1497 against 1554 frames/s, profiles/r06/ab/win_nt_config4.log).
-// EWVIT_WIN_NT=0 / ewvit_conv2d_set_win_nt(0): off everywhere
-int g_win_nt = 1;
+// A mask: 1 the fwd / dgrad windows, 2 the wgrad dy tiles, 4 the wgrad x windows (default 7);
+// EWVIT_WIN_NT / ewvit_conv2d_set_win_nt(mask), 0 = off everywhere
+int g_win_nt = 7;
 template <typename K>
 static size_t lds_pad(K kern, size_t stat) {
   if (!g_lds_pad || stat >= 160 * 1024) return 0;
@@ -761,7 +762,7 @@ __global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, i
       if (NG == 3 && P >= 32) continue;               // (NG 3: waves 8-11 stage two dy pieces)
       const int sc = (lane & 15) ^ ((dl << 2) | (P & 3));
       const uint32_t off = (uint32_t)(((dpix + (P >> 2) * W + 4 * (P & 3) + dl) * Cout + ct * 128 + sc * 8) * 2);
-      glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB, a.nt != 0);
+      glds16_asm(rd, lds0 + GD0 + b * GD_B + P * 1024, live ? off : OOB, (a.nt & 1) != 0);
     }
     const int64_t xpix = ((int64_t)img * H + oh0 - 1) * W + ow0 - 1;
     int xl = lane >> 2;
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(NG * 256) void conv_wgrad_win_kernel(WgradArgs a, i
       const bool ok = live & (p < GX_PIX) & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
       const int sc = (lane & 3) ^ xswz(p);
       const uint32_t off = (uint32_t)(((xpix + xr * W + xc) * a.xgc + cofs + sc * 8) * 2);
-      glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB, a.nt != 0);
+      glds16_asm(rx, lds0 + b * GX_B + q * 1024, ok ? off : OOB, (a.nt & 2) != 0);
     }
   };
 
@@ -986,7 +987,7 @@ static void launch_wgrad_win_t(const WgradArgs &a, int64_t x_bytes, int splits, 
 
 bool launch_wgrad_win(const WgradArgs &a_in, int64_t x_bytes, int splits, hipStream_t s) {
   WgradArgs a = a_in;
-  a.nt = g_win_nt && g_grid_cap > 0;   // beside the backbone only (see g_win_nt)
+  a.nt = g_grid_cap > 0 ? (g_win_nt >> 1) & 3 : 0;   // beside the backbone only (see g_win_nt)
   const int ncb = a.g.Cin / 32, nct = a.g.Cout / 128;
   const int ntile = (int)(a.M / (GT_R * GT_C));
   const bool b = a.dbias_part != nullptr, x = a.xf != nullptr;
@@ -1005,7 +1006,7 @@ bool launch_wgrad_win(const WgradArgs &a_in, int64_t x_bytes, int splits, hipStr
 
 bool launch_win(const FwdArgs &a_in, int64_t src_bytes, bool dgrad, hipStream_t s) {
   FwdArgs a = a_in;
-  a.nt = g_win_nt && g_grid_cap > 0;   // beside the backbone only (see g_win_nt)
+  a.nt = (g_win_nt & 1) && g_grid_cap > 0;   // beside the backbone only (see g_win_nt)
   if (!win_ok(a, dgrad) || src_bytes >= (int64_t)OOB) return false;
   const bool ks = win_ks(a, dgrad);
   const int ntn = ks ? 1 : a.Ncol / 128;
@@ -1048,10 +1049,11 @@ extern "C" int ewvit_conv2d_set_lds_pad(int on) {
   return prev;
 }
 
-// A/B switch: the non-temporal hint on the windowed MWT convs' activation-window DMAs
-extern "C" int ewvit_conv2d_set_win_nt(int on) {
+// A/B switch: the non-temporal hint on the windowed MWT convs' activation-window DMAs (mask,
+// see g_win_nt)
+extern "C" int ewvit_conv2d_set_win_nt(int mask) {
   const int prev = ewvit::g_win_nt;
-  ewvit::g_win_nt = on ? 1 : 0;
+  ewvit::g_win_nt = mask & 7;
   return prev;
 }
 

@@ -206,7 +206,7 @@ def load():
         lib.ewvit_conv2d_set_lds_pad(0)              # A/B switch (convwin.hip lds_pad)
     if os.environ.get('EWVIT_WGWIN_TS') in ('0', '2') and hasattr(lib, 'ewvit_conv2d_set_wgrad_tap_split'):
         lib.ewvit_conv2d_set_wgrad_tap_split(int(os.environ['EWVIT_WGWIN_TS']))   # A/B (convwin.hip wgrad NG)
-    if os.environ.get('EWVIT_WIN_NT') in ('0', '1') and hasattr(lib, 'ewvit_conv2d_set_win_nt'):
+    if os.environ.get('EWVIT_WIN_NT', '').isdigit() and hasattr(lib, 'ewvit_conv2d_set_win_nt'):
         lib.ewvit_conv2d_set_win_nt(int(os.environ['EWVIT_WIN_NT']))   # A/B switch (convwin.hip g_win_nt)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)

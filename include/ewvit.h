@@ -397,9 +397,11 @@ int ewvit_conv2d_set_lds_pad(int on);
  * row per wave group); returns the previous setting.  Results are bit-identical in every form
  * (same per-output MFMA chain).  Env: EWVIT_WGWIN_TS=0 / 2. */
 int ewvit_conv2d_set_wgrad_tap_split(int on);
-/* The non-temporal cache hint on the windowed MWT convs' activation-window DMAs: 1 (default) or
- * 0 (A/B); returns the previous setting.  Env: EWVIT_WIN_NT. */
-int ewvit_conv2d_set_win_nt(int on);
+/* The non-temporal cache hint on the windowed MWT convs' activation-window DMAs, taken only
+ * under a grid cap (beside the backbone): a mask, 1 the fwd / dgrad windows, 2 the wgrad dy
+ * tiles, 4 the wgrad x windows (7, the default, all; 0 none); returns the previous setting.
+ * Env: EWVIT_WIN_NT. */
+int ewvit_conv2d_set_win_nt(int mask);
 /* A/B: level-1 pixels per thread in flight in ewvit_dwt_hf_upsample_fused (2, the default, or 4); returns the previous. */
 int ewvit_dwt_set_pf(int pf);
 /* Weight-gradient n'-tile width (test switch): 4 (default) auto — 256-column tiles (each wave
