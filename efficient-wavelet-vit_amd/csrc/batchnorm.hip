@@ -1079,6 +1079,25 @@ extern "C" int ewvit_bn_bwd_se(const void *dy, const void *x, void *dx, int dtyp
   return launch_status("bn_bwd_se");
 }
 
+namespace ewvit {
+// the dx pass of ewvit_bn_bwd_se from partial rows another pass left (ewvit_bn_se_bwd, se.hip)
+int bn_bwd_dx_se_launch(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
+                        const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
+                        float *dbeta, const float *se_s, const float *se_g, int64_t HW, const float *part, int nrc,
+                        hipStream_t s) {
+  const BnGeo geo = bn_geo(C);
+  const int64_t rpb = bn_rows_per_block(geo, M, 1);
+  dim3 dgrid((unsigned)((M + rpb - 1) / rpb), geo.nch, 1);
+#define BN_SE_DX(DTV, ACTV)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<DTV, ACTV, 2>), dgrid, dim3(geo.threads), 0, s, dy, x, save_mean, save_invstd, \
+                     gamma, beta, part, nrc, dx, M, (int)C, geo.CC8, geo.RG, rpb, dgamma, dbeta, 0, se_s, (int)HW,   \
+                     se_g)
+  BN_DISPATCH(BN_SE_DX);
+#undef BN_SE_DX
+  return launch_status("bn_se_bwd");
+}
+}  // namespace ewvit
+
 // backward from partial sums left by the kernel that produced dy (the consumer conv's input
 // gradient: ewvit_conv2d_bwd_data_bn, ewvit_dwconv3x3_bwd_data_bn): part [nrc][2C] = per
 // partial row (sum g, sum g * xhat) with g = dy * act'(...) or, row_scale given (the MBConv

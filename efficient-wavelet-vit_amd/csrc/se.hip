@@ -451,6 +451,44 @@ __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__
   if (w == 0 && c < C) g_out[(int64_t)n * C + c] = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) * inv_hw;
 }
 
+// the BN's two channel sums from the per-frame sums (see se_sq_dh_bn_part_kernel): out[c] =
+// sum g', out[C + c] = sum g' xhat — one partial row for bn_bwd_dx_kernel.  Lanes over channels,
+// the 4 waves over quarters of the frames, combined in a fixed order (deterministic).
+// (Extra blocks of se_mlp_wgrad_kernel: no launch of its own.)
+__device__ __forceinline__ void se_bn_sums_block(int bx, const float *__restrict__ bnsum, const float *__restrict__ s,
+                                                 const float *__restrict__ g, int N, int C, float *__restrict__ out,
+                                                 float (*red)[64]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = bx * 64 + lane;                  // 0 .. 2C - 1
+  const int which = k >= C, c = which ? k - C : k;
+  const int q = (N + 3) >> 2, na = w * q, nb = na + q < N ? na + q : N;
+  float acc0 = 0.f, acc1 = 0.f;
+  if (k < 2 * C) {
+    const float *pa = bnsum + (int64_t)(which ? 2 : 0) * N * C + c;    // A or Q
+    const float *pb = bnsum + (int64_t)(which ? 3 : 1) * N * C + c;    // B or D
+    for (int n0 = na; n0 < nb; n0 += 4) {
+      float vs[4], vg[4], va[4], vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = n0 + u < nb;
+        const int64_t o = (int64_t)(ok ? n0 + u : na) * C;
+        vs[u] = ok ? s[o + c] : 0.f; vg[u] = ok ? g[o + c] : 0.f;
+        va[u] = pa[o]; vb[u] = pb[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u += 2) {
+        acc0 = fmaf(vg[u], vb[u], fmaf(vs[u], va[u], acc0));
+        acc1 = fmaf(vg[u + 1], vb[u + 1], fmaf(vs[u + 1], va[u + 1], acc1));
+      }
+    }
+  }
+  red[w][lane] = acc0 + acc1;
+  __syncthreads();
+  if (w == 0 && k < 2 * C) out[k] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+
+
 // dW2[c][j] = sum_n dz2[n][c] silu(h1[n][j]),  db2[c] = sum_n dz2[n][c]
 // dW1[j][c] = sum_n dz1[n][j] s0[n][c],        db1[j] = sum_n dz1[n][j]
 // block: 64 consecutive outputs (lanes) x 4 waves on quarters of the frames, the quarters
@@ -461,8 +499,16 @@ __global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restri
                                                            const float *__restrict__ h1,
                                                            const float *__restrict__ s0, int N, int C, int Csq,
                                                            float *__restrict__ dw1, float *__restrict__ db1,
-                                                           float *__restrict__ dw2, float *__restrict__ db2) {
+                                                           float *__restrict__ dw2, float *__restrict__ db2,
+                                                           const float *__restrict__ bnsum = nullptr,
+                                                           const float *__restrict__ exc = nullptr,
+                                                           const float *__restrict__ gsq = nullptr,
+                                                           float *__restrict__ bnout = nullptr, int nwb = 0) {
   __shared__ float red[4][64];
+  if (bnsum && (int)blockIdx.x >= nwb) {         // the BN sums' blocks (ewvit_bn_se_bwd)
+    se_bn_sums_block((int)blockIdx.x - nwb, bnsum, exc, gsq, N, C, bnout, red);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t P = (int64_t)C * Csq;
@@ -634,6 +680,210 @@ __global__ __launch_bounds__(256) void se_sq_dh_part_kernel(const void *__restri
     __syncthreads();
   }
 }
+
+// the BatchNorm(+act) backward's reduction folded into the SE backward's squeeze pass
+// (ewvit_bn_se_bwd): the BN's output gradient is dy*s[n][c] + g[n][c] (s the excitation, g the
+// squeeze term the MLP backward forms later), so its two channel sums split per frame as
+//   sum g'      = sum_n s[n][c] A[n][c] + g[n][c] B[n][c]
+//   sum g' xhat = sum_n s[n][c] Q[n][c] + g[n][c] D[n][c]
+// with g' = (dy s + g) act'(xhat gamma + beta) and the per-frame sums
+//   A = sum_hw dy t,  B = sum_hw t,  Q = sum_hw dy t xhat,  D = sum_hw t xhat,  t = act'(.).
+// This pass (block: frame n, 64-channel chunk) forms them beside ds = sum_hw dy * a while it
+// streams dy and a anyway; se_mlp_wgrad_kernel, which already sums over the frames, adds the
+// two channel sums; the BN's own reduction pass over dy and z never runs.
+template <int ACT>
+__device__ __forceinline__ float se_act_grad(float z) {   // = batchnorm.hip act_grad
+  if (ACT == 1) return z > 0.f ? 1.f : 0.f;
+  if (ACT == 2) {
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-z));
+    return s * (1.f + z * (1.f - s));
+  }
+  return 1.f;
+}
+
+template <int V> struct se_ic { static constexpr int value = V; };
+// raw 8-channel vectors (bf16: one 16-B load, unpacked at use) for the batched row walks
+template <int DT> struct SeRaw { uint4 a, b; };
+template <int DT>
+__device__ __forceinline__ SeRaw<DT> se_ldraw(const void *p, int64_t i) {
+  SeRaw<DT> r;
+  if constexpr (DT == EWVIT_BF16) {
+    r.a = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16_t *>(p) + i);
+    r.b = r.a;
+  } else {
+    const uint4 *q = reinterpret_cast<const uint4 *>(reinterpret_cast<const float *>(p) + i);
+    r.a = q[0];
+    r.b = q[1];
+  }
+  return r;
+}
+template <int DT>
+__device__ __forceinline__ void se_unpack(const SeRaw<DT> &r, float (&v)[8]) {
+  if constexpr (DT == EWVIT_BF16) {
+    const unsigned w[4] = {r.a.x, r.a.y, r.a.z, r.a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  } else {
+    const unsigned w[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(w[j]);
+  }
+}
+__device__ __forceinline__ void ld8f(const float *p, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4 *>(p)[0], b = reinterpret_cast<const float4 *>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// v + v[lane ^ 8], v + v[lane ^ 16], v + v[lane ^ 32] (fp addition commutes: both lanes
+// of a pair get the same bits)
+__device__ __forceinline__ float xsum8(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int DT, int ACT>
+__global__ __launch_bounds__(256) void se_sq_dh_bn_part_kernel(const void *__restrict__ dy, const void *__restrict__ x,
+                                                               const void *__restrict__ z, int HW,
+                                                               const float *__restrict__ s,
+                                                               const float *__restrict__ w2, int C, int Csq,
+                                                               const float *__restrict__ mean,
+                                                               const float *__restrict__ invstd,
+                                                               const float *__restrict__ gamma,
+                                                               const float *__restrict__ beta,
+                                                               float *__restrict__ dz2_out, float *__restrict__ part,
+                                                               float *__restrict__ bnsum, int N) {
+  __shared__ float wred[4][5][SE_CB];
+  const int n = blockIdx.x, cb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = cb * SE_CB + lane;
+  const int c0 = cb * SE_CB;
+  const int nc = C - c0 < SE_CB ? C - c0 : SE_CB;
+  {
+    const int cv = tid & 7, rg = tid >> 3;
+    const int cc = cb * SE_CB + cv * 8;
+    float acc[5][8];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+    if (cc < C) {
+      float mu[8], iv[8], ga[8], be[8];
+      ld8f(mean + cc, mu);
+      ld8f(invstd + cc, iv);
+      if (gamma) ld8f(gamma + cc, ga);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[j] = 1.f;
+      if (beta) ld8f(beta + cc, be);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) be[j] = 0.f;
+      const int64_t base = (int64_t)n * HW * C + cc;
+      auto use = [&](const SeRaw<DT> &rd, const SeRaw<DT> &ra, const SeRaw<DT> &rz) {
+        float vd[8], va[8], vz[8];
+        se_unpack<DT>(rd, vd);
+        se_unpack<DT>(ra, va);
+        se_unpack<DT>(rz, vz);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          acc[0][j] = fmaf(vd[j], va[j], acc[0][j]);
+          const float xh = (vz[j] - mu[j]) * iv[j];
+          const float t = ACT ? se_act_grad<ACT>(fmaf(xh, ga[j], be[j])) : 1.f;
+          const float dt = vd[j] * t;
+          acc[1][j] += dt;
+          acc[2][j] += t;
+          acc[3][j] = fmaf(dt, xh, acc[3][j]);
+          acc[4][j] = fmaf(t, xh, acc[4][j]);
+        }
+      };
+      // NB rows' 3 NB loads issued before any is used (the sched_barrier keeps hipcc from
+      // sinking them into the uses, where each would wait out its own latency)
+      auto batch = [&](int h0, auto NBc) {
+        constexpr int NB = decltype(NBc)::value;
+        SeRaw<DT> rd[NB], ra[NB], rz[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int64_t o = base + (int64_t)(h0 + 32 * q) * C;
+          rd[q] = se_ldraw<DT>(dy, o);
+          ra[q] = se_ldraw<DT>(x, o);
+          rz[q] = se_ldraw<DT>(z, o);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) use(rd[q], ra[q], rz[q]);
+      };
+      int h = rg;
+      for (; h + 32 < HW; h += 64) batch(h, se_ic<2>{});
+      if (h < HW) batch(h, se_ic<1>{});
+    }
+    // the wave's 8 row groups (lanes cv, cv + 8, .., cv + 56) summed in registers: xor 8 by DPP
+    // row_ror:8, xor 16 / 32 by gfx950's v_permlane16/32_swap (no LDS traffic — an LDS tree over
+    // 40 values per thread was LDS-bandwidth bound), then the 4 waves through LDS in a fixed order
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = xsum32(xsum16(xsum8(acc[k][j])));
+    if (lane < 8)
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wred[w][k][lane * 8 + j] = acc[k][j];
+  }
+  __syncthreads();
+  float tot[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) tot[k] = (wred[0][k][lane] + wred[1][k][lane]) + (wred[2][k][lane] + wred[3][k][lane]);
+  const float dsv = tot[0];
+  if (w == 0 && c < C) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bnsum[((int64_t)k * N + n) * C + c] = tot[k + 1];
+  }
+  float d = 0.f;
+  if (c < C) {
+    const float sv = s[(int64_t)n * C + c];
+    d = dsv * sv * (1.f - sv);
+    if (w == 0) dz2_out[(int64_t)n * C + c] = d;
+  }
+  __shared__ float dsh[SE_CB];
+  __shared__ float red[4][64];
+  if (w == 0) dsh[lane] = d;
+  __syncthreads();
+  float *pp = part + ((int64_t)n * gridDim.y + cb) * Csq;
+  for (int j0 = 0; j0 < Csq; j0 += 64) {     // as se_sq_dh_part_kernel
+    const int j = j0 + lane;
+    float acc = 0.f;
+    if (j < Csq) {
+      float wv[SE_CB / 4];
+      const float *wr = w2 + (int64_t)c0 * Csq + j;
+#pragma unroll
+      for (int u = 0; u < SE_CB / 4; ++u) {
+        const int k = w + 4 * u;
+        wv[u] = wr[(int64_t)(k < nc ? k : nc - 1) * Csq];
+      }
+#pragma unroll
+      for (int u = 0; u < SE_CB / 4; ++u) acc = fmaf(wv[u], dsh[w + 4 * u], acc);
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && j < Csq) pp[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
+  }
+}
+
+// bn_bwd_dx_kernel<DT, ACT, 2> over one partial row (batchnorm.hip)
+int bn_bwd_dx_se_launch(const void *dy, const void *x, void *dx, int dtype, int64_t M, int64_t C, const float *gamma,
+                        const float *beta, const float *save_mean, const float *save_invstd, int act, float *dgamma,
+                        float *dbeta, const float *se_s, const float *se_g, int64_t HW, const float *part, int nrc,
+                        hipStream_t s);
 
 }  // namespace ewvit
 
@@ -861,4 +1111,54 @@ extern "C" int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype
   hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, st, dz2, dz1, h1, s0,
                      (int)N, (int)C, (int)Csq, dw1, db1, dw2, db2);
   return launch_status("se_squeeze_mlp_bwd");
+}
+
+extern "C" int64_t ewvit_bn_se_bwd_workspace(int64_t N, int64_t C, int64_t Csq) {
+  return ewvit_se_mlp_bwd_workspace(N, C, Csq) + (4 * N * C + 2 * C) * (int64_t)sizeof(float);
+}
+
+// The backward of SE(act(BatchNorm(z))) in 4 launches: the SE squeeze pass with the BN's
+// per-frame sums (se_sq_dh_bn_part_kernel), the MLP's g, its weight gradients + the BN's two
+// channel sums (extra blocks), and the BN's dx pass from that one partial row.  Replaces
+// ewvit_se_squeeze_mlp_bwd + ewvit_bn_bwd_se (whose reduction pass re-read dy and z).
+extern "C" int ewvit_bn_se_bwd(const void *dy, const void *a, const void *z, void *dx, int dtype, int64_t N,
+                               int64_t HW, int64_t C, const float *gamma, const float *beta, const float *save_mean,
+                               const float *save_invstd, int act, float *dgamma, float *dbeta, const float *s,
+                               const float *h1, const float *s0, const float *w1, const float *w2, int64_t Csq,
+                               float *g, float *dw1, float *db1, float *dw2, float *db2, float *workspace,
+                               void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "bn_se_bwd")) return rc;
+  if (int rc = se_mlp_check(N, C, Csq, "bn_se_bwd")) return rc;
+  EWVIT_CHECK_ARG(dy && a && z && dx && save_mean && save_invstd && s && h1 && s0 && w1 && w2 && g && dw1 && dw2 &&
+                      workspace && HW < (1 << 30),
+                  "bn_se_bwd: bad args");
+  EWVIT_CHECK_ARG(act >= 0 && act <= 2 && C <= 4096 && N * HW < ((int64_t)1 << 31), "bn_se_bwd: act=%d C=%lld", act,
+                  (long long)C);
+  hipStream_t st = as_stream(stream);
+  const int nb = se_nb(C);
+  float *dz2 = workspace, *dz1 = workspace + N * C, *part = dz1 + N * Csq;
+  float *bnsum = part + N * nb * Csq, *bnrow = bnsum + 4 * N * C;
+  const dim3 g1((unsigned)N, (unsigned)nb);
+#define SE_BN_DH(DTV, ACTV)                                                                                          \
+  hipLaunchKernelGGL((se_sq_dh_bn_part_kernel<DTV, ACTV>), g1, dim3(256), 0, st, dy, a, z, (int)HW, s, w2, (int)C,  \
+                     (int)Csq, save_mean, save_invstd, gamma, beta, dz2, part, bnsum, (int)N)
+  if (dtype == EWVIT_BF16) {
+    if (act == 0) SE_BN_DH(EWVIT_BF16, 0);
+    else if (act == 1) SE_BN_DH(EWVIT_BF16, 1);
+    else SE_BN_DH(EWVIT_BF16, 2);
+  } else {
+    if (act == 0) SE_BN_DH(EWVIT_F32, 0);
+    else if (act == 1) SE_BN_DH(EWVIT_F32, 1);
+    else SE_BN_DH(EWVIT_F32, 2);
+  }
+#undef SE_BN_DH
+  hipLaunchKernelGGL(se_mlp_g_kernel, dim3((unsigned)N, (unsigned)((C + 63) / 64)), dim3(256),
+                     (size_t)Csq * sizeof(float), st, part, nb, h1, w1, (int)C, (int)Csq, 1.f / (float)HW, dz1, g);
+  const int64_t tot = 2 * C * Csq + C + Csq;
+  const int nwb = (int)((tot + 63) / 64), nbn = (int)((2 * C + 63) / 64);
+  hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)(nwb + nbn)), dim3(256), 0, st, dz2, dz1, h1, s0, (int)N,
+                     (int)C, (int)Csq, dw1, db1, dw2, db2, bnsum, s, g, bnrow, nwb);
+  if (int rc = launch_status("bn_se_bwd")) return rc;
+  return bn_bwd_dx_se_launch(dy, z, dx, dtype, N * HW, C, gamma, beta, save_mean, save_invstd, act, dgamma, dbeta, s,
+                             g, HW, bnrow, 1, st);
 }

@@ -21,6 +21,9 @@ from . import grads
 # the depthwise BatchNorm's apply pass and the SE squeeze as one kernel when the statistics come
 # from the depthwise conv (ewvit_bn_act_se_squeeze; 0: separate passes, A/B)
 _BN_SQUEEZE = os.environ.get('EWVIT_BN_SQUEEZE', '1') != '0'
+# the depthwise BN's backward reduction inside the SE backward's squeeze pass (ewvit_bn_se_bwd);
+# EWVIT_BN_SE_FUSED=0: ewvit_se_squeeze_mlp_bwd + ewvit_bn_bwd_se (A/B)
+_BN_SE_FUSED = os.environ.get('EWVIT_BN_SE_FUSED', '1') != '0'
 # (the BatchNorm backward's sums taken per frame by the SE backward's squeeze kernel measured
 # slower — SFE piece 14.22-14.25 -> 14.28-14.32 ms, profiles/r03/ab/se_bn_sums_ab.txt — and
 # was removed: that kernel walks one frame's 49-196 rows per block, so the extra operand's loads
@@ -226,6 +229,15 @@ class BnActSEFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         dg = _vec_out(pg, ctx.gen, C, dev)
         db = _vec_out(pb, ctx.gen, C, dev)
+        if _BN_SE_FUSED and C <= 4096 and L.has('ewvit_bn_se_bwd'):
+            # the BN's reduction inside the SE squeeze pass: 4 launches, dy and z read once fewer
+            mws = torch.empty(L.load().ewvit_bn_se_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+            L.call('ewvit_bn_se_bwd', L.ptr(dyc), L.ptr(x2), L.ptr(xc), L.ptr(dx), L.dt(xc), N, HW, C, L.ptr(gamma),
+                   L.ptr(beta), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(h1),
+                   L.ptr(s0), L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2),
+                   L.ptr(mws), L.stream(dx), work={'bytes': 6 * xc.numel() * xc.element_size()})
+            return (dx, grads.give(pg, dg, ctx.gen), grads.give(pb, db, ctx.gen), None, None, None, None, None, None,
+                    *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None)
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
                L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),

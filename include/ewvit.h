@@ -598,6 +598,20 @@ int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N
                              const float *s, const float *h1, const float *s0, const float *w1, const float *w2,
                              int64_t Csq, float *g, float *dw1, float *db1, float *dw2, float *db2,
                              float *workspace, void *stream);
+/* The backward of SE(act(BatchNorm(z))) (MBConv's depthwise BN + act + SE, network/sfe.py:111-113)
+ * in one call, 4 launches: ewvit_se_squeeze_mlp_bwd's outputs (g, dw1, db1, dw2, db2) and
+ * ewvit_bn_bwd_se's (dx, dgamma, dbeta overwritten), with the BatchNorm's two channel sums split
+ * per frame (sum over rows of (dy s + g) act' = sum_n s A_n + g B_n, likewise for the xhat
+ * moment) and formed in the SE squeeze pass that streams dy and a anyway — the BN's own
+ * reduction pass over dy and z never runs.  a: the SE input act(BN(z)) as the forward stored
+ * it; z: the BN input; save_mean / save_invstd from the forward.  C % 8 == 0, C <= 4096.
+ * workspace: ewvit_bn_se_bwd_workspace(N, C, Csq) bytes. */
+int64_t ewvit_bn_se_bwd_workspace(int64_t N, int64_t C, int64_t Csq);
+int ewvit_bn_se_bwd(const void *dy, const void *a, const void *z, void *dx, int dtype, int64_t N, int64_t HW,
+                    int64_t C, const float *gamma, const float *beta, const float *save_mean,
+                    const float *save_invstd, int act, float *dgamma, float *dbeta, const float *s,
+                    const float *h1, const float *s0, const float *w1, const float *w2, int64_t Csq, float *g,
+                    float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,

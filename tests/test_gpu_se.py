@@ -208,8 +208,10 @@ def test_bn_act_se_matches_two_step_path():
     assert torch.equal(a[0], b[0]) and torch.equal(a[5], b[5])
     assert rel(a[1], b[1]) < 1e-2
     assert rel(a[2], b[2]) < 1e-2 and rel(a[3], b[3]) < 1e-2
+    # the SE squeeze sum ds = sum_hw dy * a: the fused backward (ewvit_bn_se_bwd) adds its row
+    # groups in another (register butterfly) order than the SE-alone pass: fp32 reassociation
     for p, q in zip(a[4], b[4]):
-        assert torch.equal(p, q)
+        assert rel(p, q) < 1e-5
 
 
 @pytest.mark.parametrize('N,C,HW,csq,dtype', [(64, 1536, 49, 64, torch.bfloat16), (64, 960, 196, 40, torch.bfloat16),
@@ -278,3 +280,42 @@ def test_bn_act_se_squeeze_matches_separate_passes(N, C, H, csq, monkeypatch):
         assert torch.equal(u, v)
     for u, v in zip(a[6], b[6]):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize('N,C,H,W,csq,act', [(64, 1536, 7, 7, 64, 'silu'), (64, 960, 14, 14, 40, 'silu'),
+                                             (5, 24, 9, 11, 6, 'relu'), (3, 200, 5, 3, 6, None)])
+def test_bn_se_bwd_matches_two_pass_path(N, C, H, W, csq, act, monkeypatch):
+    """ewvit_bn_se_bwd (the BatchNorm's backward sums split per frame and formed in the SE
+    squeeze pass) against ewvit_se_squeeze_mlp_bwd + ewvit_bn_bwd_se (a reduction pass over the
+    whole map): the same fp32 sums in another order — SE parameter gradients to 1e-5, dgamma /
+    dbeta to 1e-4, dx to one bf16 rounding on < 5 % of its elements."""
+    import ewvit
+    import ewvit.se as ese
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    w1 = (torch.randn(csq, C, 1, 1, generator=g) / C ** 0.5).to(DEV)
+    b1 = (torch.randn(csq, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(C, csq, 1, 1, generator=g) / csq ** 0.5).to(DEV)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    dy = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.2
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(ese, '_BN_SE_FUSED', fused)
+        bn = torch.nn.BatchNorm2d(C, eps=1e-3).train().to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(gam)
+            bn.bias.copy_(bet)
+        xd = x.clone().requires_grad_(True)
+        ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+        y = ewvit.bn_act_se(xd, bn, act, *ps)
+        y.backward(dy)
+        outs.append((y, xd.grad, bn.weight.grad, bn.bias.grad, [p.grad for p in ps]))
+    a, b = outs
+    assert torch.equal(a[0], b[0])
+    for p, q in zip(a[4], b[4]):
+        assert rel(p, q) < 1e-5          # ds summed in another order (fp32 reassociation only)
+    assert rel(a[2], b[2]) < 1e-4 and rel(a[3], b[3]) < 1e-4
+    d = (a[1].float() - b[1].float()).abs()
+    assert float(d.max()) <= 2 ** -7 * float(b[1].float().abs().max())
+    assert float((d > 0).float().mean()) < 0.05
