@@ -29,8 +29,10 @@
 // is the MWT's level-major fusion output [L][B][H][W][128] read as the
 // [B][H][W][3*128] concatenation (mwt.py:112) without materialising it.
 #include "conv_common.h"
+#include "reduce_jobs.h"
 
 #include <cstdlib>
+#include <deque>
 #include <mutex>
 #include <unordered_map>
 
@@ -420,12 +422,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// where dW element (co, ci, tap), ci < cin, lives: the parameter's strides
-struct WOut {
-  int64_t s_co, s_ci, s_tap;
-  int cin;
-};
-
 // dW[co][ci][tap] (= or +=) sum over splits of part[s][co][tap*Cin + ci].  T lanes of a
 // wave share one 4-element output (T = splits fan-in, a power of two <= 64 chosen so
 // ~64K threads run): lane l sums splits l, l+T, ... (4 loads in flight), then an xor
@@ -459,42 +455,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float *__r
     }
     return;
   }
-  const int64_t NP = taps * (int64_t)Cin;
-  const int64_t n = (int64_t)Cout * NP;                                // n % 4 == 0 (Cin % 8 == 0)
-  const int sl = tid & (T - 1);
-  const int64_t i = ((int64_t)blockIdx.x * (256 / T) + tid / T) * 4;
-  const bool ok = i < n;
-  const int64_t ii = ok ? i : 0;
-  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-  int k = sl;
-  for (; k + 3 * T < splits; k += 4 * T) {
-    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + ii);
-    const float4 b = *reinterpret_cast<const float4 *>(part + (int64_t)(k + T) * n + ii);
-    const float4 c = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 2 * T) * n + ii);
-    const float4 d = *reinterpret_cast<const float4 *>(part + (int64_t)(k + 3 * T) * n + ii);
-    s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-    s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
-    s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
-    s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
-  }
-  for (; k < splits; k += T) {
-    const float4 a = *reinterpret_cast<const float4 *>(part + (int64_t)k * n + ii);
-    s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-  }
-  float r[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
-                (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w)};
-  for (int o = T >> 1; o >= 1; o >>= 1)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] += __shfl_xor(r[e], o, 64);
-  if (!ok || sl != 0) return;
-  const int co = (int)(i / NP);
-  const int np = (int)(i % NP);
-  const int tap = np / Cin, ci = np % Cin;
-  // the parameter's own layout (strides), only its real input channels
-  const int64_t o = co * wo.s_co + ci * wo.s_ci + tap * wo.s_tap;
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (ci + e < wo.cin) dw[o + e * wo.s_ci] = accumulate ? dw[o + e * wo.s_ci] + r[e] : r[e];
+  // (the split sums: reduce_jobs.h, shared with the deferred form)
+  wgrad_reduce_block(part, dw, Cin, taps, splits, accumulate, wo, T, (int64_t)Cout * taps * Cin, (int)blockIdx.x);
 }
 
 // pack fp32 W (element (co, ci, tap) at co*s_co + ci*s_ci + tap*s_tap: any of the
@@ -1152,13 +1114,19 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(FwdArgs a, int bm)
 // ds_read_b64_tr_b16).  Bias gradient (sum of dy over pixels): the blocks of n'-tile
 // t sum the dy image of the K-tiles kt = t (mod n'-tiles), spreading the extra reads.
 template <int KS, int BK, int NS, int WJ = 4>
-__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty) {
+__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64_t x_bytes, int ntx, int nty,
+                                                              RedJobs rj) {
   constexpr int NB = WJ / 4;         // 128-column x images per stage (n'-tile of 128 * NB)
   constexpr int IMG = BK * 256, STG = (1 + NB) * IMG;
   constexpr int P = BK / 16;        // pieces (4 rows x 256 B) per wave per image
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
+  // the first rj.nblk workgroups run deferred reductions of earlier weight gradients
+  if ((int)blockIdx.x < rj.nblk) {
+    run_red_jobs(rj, (int)blockIdx.x, reinterpret_cast<float *>(smem));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = xcd_remap((int)blockIdx.x - rj.nblk, (int)gridDim.x - rj.nblk);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
   const int co0 = ty * 128, np0 = tx * 128 * NB;
@@ -1350,11 +1318,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradArgs a, int64
 // step's MFMAs.  Leaves [splits][Cout][Cin] slabs (conv_wgrad_reduce_kernel), or dW itself for
 // one split.
 template <int NS>
-__global__ __launch_bounds__(256) void conv_wgrad_1x1_kernel(WgradArgs a, int ntx, int nty) {
+__global__ __launch_bounds__(256) void conv_wgrad_1x1_kernel(WgradArgs a, int ntx, int nty, RedJobs rj) {
   constexpr int BK = 64, IMG = BK * 256, STG = 2 * IMG, P = BK / 16;
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STG];
+  // the first rj.nblk workgroups run deferred reductions of earlier weight gradients
+  if ((int)blockIdx.x < rj.nblk) {
+    run_red_jobs(rj, (int)blockIdx.x, reinterpret_cast<float *>(smem));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = xcd_remap((int)blockIdx.x - rj.nblk, (int)gridDim.x - rj.nblk);
   const int split = tile / (ntx * nty);
   const int tx = tile % ntx, ty = (tile / ntx) % nty;
   const int co0 = ty * 128, ci0 = tx * 128;
@@ -1853,9 +1826,74 @@ static ConvGeom mkg(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, 
   return g;
 }
 
+// ---- deferred weight-gradient reductions (reduce_jobs.h): per-stream FIFO of jobs
+static thread_local bool t_defer_next = false;
+static std::mutex g_red_mu;
+static std::deque<std::pair<hipStream_t, RedJob>> g_red_q;
+
+bool reduce_take_defer() {
+  const bool d = t_defer_next;
+  t_defer_next = false;
+  return d;
+}
+
+void reduce_defer(hipStream_t s, const RedJob &j) {
+  std::lock_guard<std::mutex> lk(g_red_mu);
+  g_red_q.emplace_back(s, j);
+}
+
+RedJobs reduce_take_jobs(hipStream_t s) {
+  RedJobs r;
+  std::lock_guard<std::mutex> lk(g_red_mu);
+  int q = 0;
+  for (auto it = g_red_q.begin(); it != g_red_q.end() && q < 2;) {
+    if (it->first == s) {
+      r.j[q] = it->second;
+      r.j[q].nblk = red_job_blocks(it->second);
+      r.nblk += r.j[q].nblk;
+      ++q;
+      it = g_red_q.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  r.nblk = (r.nblk + 7) / 8 * 8;
+  return r;
+}
+
+// deferred jobs alone (ewvit_reduce_flush): 2 per launch
+__global__ __launch_bounds__(256) void red_jobs_kernel(RedJobs rj) {
+  __shared__ float red[256];
+  run_red_jobs(rj, (int)blockIdx.x, red);
+}
+
 }  // namespace ewvit
 
 using namespace ewvit;
+
+// ---- deferred reductions (reduce_jobs.h)
+extern "C" int ewvit_reduce_defer_next(int on) {
+  t_defer_next = on != 0;
+  return 0;
+}
+
+extern "C" int ewvit_reduce_pending(void *stream) {
+  std::lock_guard<std::mutex> lk(g_red_mu);
+  int n = 0;
+  for (auto &e : g_red_q)
+    if (!stream || e.first == as_stream(stream)) ++n;
+  return n;
+}
+
+extern "C" int ewvit_reduce_flush(void *stream) {
+  hipStream_t s = as_stream(stream);
+  for (;;) {
+    RedJobs rj = reduce_take_jobs(s);
+    if (rj.nblk == 0) return 0;
+    hipLaunchKernelGGL(red_jobs_kernel, dim3((unsigned)rj.nblk), dim3(256), 0, s, rj);
+    if (int rc = launch_status("reduce_flush")) return rc;
+  }
+}
 
 extern "C" int ewvit_set_grid_cap(int max_workgroups);
 extern "C" int ewvit_conv2d_set_grid_cap(int max_workgroups) { return ewvit_set_grid_cap(max_workgroups); }
@@ -2353,6 +2391,8 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
                                        int stride, int64_t x_group_c, int64_t x_group_stride, int64_t dw_cin,
                                        int64_t dw_s_co, int64_t dw_s_ci, int64_t dw_s_tap, float *workspace,
                                        void *stream) {
+  // (the caller's "defer this reduce" mark is consumed by every call, whatever path it takes)
+  const bool defer_mark = reduce_take_defer();
   EWVIT_CHECK_ARG(x && dy && dw && workspace, "conv2d_bwd_weight: null pointer");
   ConvGeom g = mkg(N, H, W, Cin, Cout, ksize, stride);
   if (int rc = check_geom(g, "conv2d_bwd_weight")) return rc;
@@ -2398,9 +2438,11 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
     const bool direct = sp == 1 && !accumulate && dw_cin == Cin && dw_s_ci == 1 && dw_s_co == Cin;
     a.part = direct ? dw : workspace;
     hipStream_t s = as_stream(stream);
-    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
-    if (g_w1_ring == 2) hipLaunchKernelGGL(conv_wgrad_1x1_kernel<2>, dim3(nwg), dim3(256), 0, s, a, ntx, nty);
-    else hipLaunchKernelGGL(conv_wgrad_1x1_kernel<3>, dim3(nwg), dim3(256), 0, s, a, ntx, nty);
+    // deferred reductions of earlier weight gradients on this stream ride in front of the tiles
+    const RedJobs rj = reduce_take_jobs(s);
+    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp + rj.nblk);
+    if (g_w1_ring == 2) hipLaunchKernelGGL(conv_wgrad_1x1_kernel<2>, dim3(nwg), dim3(256), 0, s, a, ntx, nty, rj);
+    else hipLaunchKernelGGL(conv_wgrad_1x1_kernel<3>, dim3(nwg), dim3(256), 0, s, a, ntx, nty, rj);
     if (int rc = launch_status("conv2d_bwd_weight (1x1)")) return rc;
     if (direct) return 0;
     WOut wo;
@@ -2408,6 +2450,13 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
     const int64_t n4 = (int64_t)g.Cout * g.Cin / 4;
     int T = 1;
     while (T < 64 && T * 2 <= sp && n4 * T * 2 <= 65536) T *= 2;
+    if (defer_mark) {
+      RedJob j;
+      j.kind = 1; j.part = workspace; j.dw = dw; j.n = n4 * 4; j.Cin = g.Cin; j.taps = 1; j.splits = sp;
+      j.accumulate = accumulate; j.T = T; j.wo = wo;
+      reduce_defer(s, j);
+      return 0;
+    }
     const int64_t nmain = (n4 * T + 255) / 256;
     hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)nmain), dim3(256), 0, s, workspace, dw, g.Cout,
                        g.Cin, 1, sp, 0, accumulate, nullptr, nullptr, wo, T, (int)nmain);
@@ -2436,11 +2485,13 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   if (direct) { a.part = dw; a.dbias_part = dbias; }
   hipStream_t s = as_stream(stream);
   if (glds) {
-    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp);
+    // deferred reductions of earlier weight gradients on this stream ride in front of the tiles
+    const RedJobs rj = reduce_take_jobs(s);
+    const unsigned nwg = (unsigned)((int64_t)ntx * nty * sp + rj.nblk);
 #define EWVIT_GLDS_WG(BK_, NS_, WJ_)                                                                        \
   do {                                                                                                    \
-    if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty); \
-    else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty);            \
+    if (ksize == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<1, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty, rj); \
+    else hipLaunchKernelGGL((conv_wgrad_glds_kernel<3, BK_, NS_, WJ_>), dim3(nwg), dim3(256), 0, s, a, xb, ntx, nty, rj);            \
   } while (0)
     if (wide) EWVIT_GLDS_WG(32, 2, 8);
     else EWVIT_GLDS_WG(64, 2, 4);
@@ -2455,6 +2506,13 @@ extern "C" int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw,
   const int64_t n4 = (int64_t)g.Cout * taps * g.Cin / 4;
   int T = 1;                       // split lanes per output: ~64K threads, <= splits, <= 64
   while (T < 64 && T * 2 <= sp && n4 * T * 2 <= 65536) T *= 2;
+  if (defer_mark && glds && !dbias) {
+    RedJob j;
+    j.kind = 1; j.part = workspace; j.dw = dw; j.n = n4 * 4; j.Cin = g.Cin; j.taps = taps; j.splits = sp;
+    j.accumulate = accumulate; j.T = T; j.wo = wo;
+    reduce_defer(s, j);
+    return 0;
+  }
   const int64_t nmain = (n4 * T + 255) / 256;
   const int64_t nbias = dbias ? (g.Cout + 63) / 64 : 0;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((unsigned)(nmain + nbias)), dim3(256), 0, s, workspace, dw,

@@ -15,6 +15,7 @@
 // 1x out.  The weight gradient reduces N*Ho*Wo products per (c, tap) in fp32:
 // per-block partial slabs (deterministic, no atomics) + a second reduction pass.
 #include "common.h"
+#include "reduce_jobs.h"
 
 namespace ewvit {
 
@@ -834,26 +835,8 @@ __global__ __launch_bounds__(256) void dw_bwd_weight_partial_kernel(const void *
 __global__ __launch_bounds__(256) void dw_bwd_weight_reduce_kernel(const float *__restrict__ part,
                                                                    float *__restrict__ dw, int64_t n,
                                                                    int slabs, int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (i < n) {
-    int k = g;
-    for (; k + 12 < slabs; k += 16) {
-      s0 += part[(int64_t)k * n + i];
-      s1 += part[(int64_t)(k + 4) * n + i];
-      s2 += part[(int64_t)(k + 8) * n + i];
-      s3 += part[(int64_t)(k + 12) * n + i];
-    }
-    for (; k < slabs; k += 4) s0 += part[(int64_t)k * n + i];
-  }
-  red[g][lane] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (g == 0 && i < n) {
-    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-    dw[i] = accumulate ? dw[i] + t : t;
-  }
+  __shared__ float red[256];
+  dw_slab_reduce_block(part, dw, n, slabs, accumulate, (int)blockIdx.x, red);   // (reduce_jobs.h)
 }
 
 static int check_shape(const DwShape &s, const char *nm) {
@@ -1013,6 +996,7 @@ extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *d
                                          int accumulate, int64_t N, int64_t H, int64_t W, int64_t C, const void *bx,
                                          const float *mean, const float *invstd, const float *gamma,
                                          const float *beta, int act, float *part, float *workspace, void *stream) {
+  const bool defer_mark = reduce_take_defer();      // (reduce_jobs.h; consumed by every call)
   EWVIT_CHECK_ARG(dy && w && dx && x && dw && bx && mean && invstd && part && workspace && act >= 0 && act <= 2,
                   "dwconv3x3_bwd_fused: bad args");
   const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1);
@@ -1029,6 +1013,12 @@ extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *d
                      (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace);
   if (int rc = launch_status("dwconv3x3_bwd_fused")) return rc;
   const int64_t n = C * 9;
+  if (defer_mark) {                 // the slab sum runs in front of a later weight-gradient launch
+    RedJob j;
+    j.kind = 2; j.part = workspace; j.dw = dw; j.n = n; j.splits = (int)nrc; j.accumulate = accumulate;
+    reduce_defer(st, j);
+    return 0;
+  }
   hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace, dw, n,
                      (int)nrc, accumulate);
   return launch_status("dwconv3x3_bwd_fused reduce");

@@ -62,6 +62,8 @@ SIGNATURES = {
     'ewvit_conv2d_set_wgrad_1x1': [_i32, _i32, _i32],
     'ewvit_conv2d_set_small_tiles': [_i32],
     'ewvit_conv2d_set_ksplit': [_i32],
+    'ewvit_reduce_defer_next': [_i32],
+    'ewvit_reduce_flush': [_vp],
     'ewvit_conv2d_pack_weights': [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'ewvit_conv2d_pack_weight': [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     'ewvit_conv2d_fwd_bn': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp, _vp,
@@ -167,6 +169,7 @@ QUERIES = {
     'ewvit_conv2d_bwd_bn_rows': (_i64, [_i64, _i64, _i64, _i64, _i64, _i32, _i32]),
     'ewvit_wall_clock_khz': (_i32, []),
     'ewvit_conv2d_wgrad_1x1_config': (_i32, [_i32]),
+    'ewvit_reduce_pending': (_i32, [_vp]),
 }
 
 _lib = None

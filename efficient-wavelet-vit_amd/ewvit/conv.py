@@ -24,6 +24,7 @@ import torch
 
 from . import _lib as L
 from . import bn as bnmod
+from . import defer as _defer
 from . import grads
 from .grads import grad_out
 
@@ -347,6 +348,10 @@ class Conv2dFn(torch.autograd.Function):
             if dbf.dim() != 1 or not dbf.is_contiguous():
                 dbf = torch.empty(Cout, dtype=torch.float32, device=xc.device)
         work = {'flops': 2.0 * N * Ho * Wo * Cout * k * k * Cin, 'bytes': (dyc.numel() + xc.numel()) * 2}
+        if ctx.needs_input_grad[1] and dbf is None and grads.deferrable(wparam, dwf, ctx.gen) and _defer.available():
+            # dW is read by nobody before the end of the backward (ewvit.grads.deferrable): the
+            # split-K reduce rides in a later weight-gradient launch (ewvit.defer)
+            _defer.mark(ws, xc.device)
         L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
                Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
         return (dwf if ctx.needs_input_grad[1] else None), dbf

@@ -89,6 +89,33 @@ def _slot_view(param, dtype=torch.float32):
     return None
 
 
+def is_slot(param, t):
+    """True when `t` is `param`'s gradient slot (what ``grad_out`` hands out for it): a tensor
+    AccumulateGrad adopts, or ``give`` keeps for the end-of-backward sum, without reading it."""
+    view = _slot_view(param, t.dtype)
+    return view is not None and view.data_ptr() == t.data_ptr() and view.stride() == t.stride()
+
+
+def deferrable(param, t, gen):
+    """True when nothing reads `t` — the gradient of `param` an op's backward is about to write
+    — before the end of the backward pass, so its last kernel may be deferred (ewvit.defer):
+    the gradient slot (AccumulateGrad adopts it; the data-parallel hook and the multi-use sum
+    flush first), a multi-use parameter's gradient (``give`` keeps it for the end-of-backward
+    sum, which flushes first), or a fresh tensor of a single-use leaf with no gradient and no
+    hooks (AccumulateGrad steals it: default layout, no other reference)."""
+    if param is None or not param.is_leaf or not param.requires_grad:
+        return False
+    if is_slot(param, t):
+        return True
+    if param.grad is not None or getattr(param, '_backward_hooks', None) or \
+            getattr(param, '_post_accumulate_grad_hooks', None):
+        return False
+    if DEFER and multi_use(param, gen):
+        return True
+    return single_use(param, gen) and t.is_contiguous(memory_format=torch.contiguous_format) == \
+        param.is_contiguous(memory_format=torch.contiguous_format) and t.stride() == param.stride()
+
+
 def grad_out(param, gen=None, dtype=torch.float32):
     """Output tensor for `param`'s gradient (shape and strides of `param`); `gen`: the step id
     `note_use` returned in the op's forward.  The slot itself for a single use, and for the
@@ -138,6 +165,8 @@ def _settle(gen):
         _queued.discard(gen)
     if not ents:
         return
+    from . import defer
+    defer.flush()                     # deferred weight-gradient reductions land first
     cuda = [e for e in ents if e[1][0].is_cuda]
     if cuda:
         cur = torch.cuda.current_stream(cuda[0][1][0].device)

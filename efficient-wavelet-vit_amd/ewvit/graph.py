@@ -196,6 +196,8 @@ class GradBuckets:
         s, e, _ = self.buckets[b]
         if self.reduce and not self.defer:
             if self.flat.is_cuda:
+                from . import defer
+                defer.flush()                # deferred weight-gradient reductions land first
                 # the gradients of a bucket may come from several streams (DAMA's MWT branch
                 # runs on its own): the collective, issued on the current stream, waits for all
                 cur = torch.cuda.current_stream(self.flat.device)

@@ -12,6 +12,7 @@ import torch
 
 from . import _lib as L
 from . import bn as _bn
+from . import defer as _defer
 from . import grads
 from .grads import grad_out, note_use
 
@@ -605,6 +606,10 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                     # ... and the weight gradient, reading dy once
                     wsb = L.load().ewvit_dwconv3x3_bwd_fused_workspace(N, H, W, C)
                     ws = torch.empty(wsb // 4, dtype=torch.float32, device=xc.device)
+                    if direct and grads.deferrable(ctx.params[0], dw, ctx.gen) and _defer.available():
+                        # dW is read by nobody before the end of the backward (grads.deferrable):
+                        # its slab sum rides in a later weight-gradient launch (ewvit.defer)
+                        _defer.mark(ws, xc.device)
                     L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dyc), L.ptr(w), L.ptr(dx), L.ptr(xc), L.ptr(dw), 0,
                            N, H, W, C, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma),
                            L.ptr(bl.beta), bl.act, L.ptr(part), L.ptr(ws), L.stream(dx),

@@ -546,6 +546,23 @@ int ewvit_conv2d_bwd_weight(const void *x, const void *dy, float *dw, float *dbi
                             int stride, int64_t x_group_c, int64_t x_group_stride, int64_t dw_cin,
                             int64_t dw_s_co, int64_t dw_s_ci, int64_t dw_s_tap, float *workspace, void *stream);
 
+/* ------------------------------ deferred weight-gradient reductions ---
+ * The split-K weight gradients (ewvit_conv2d_bwd_weight's 1x1 and LDS-DMA forms, no bias) and
+ * ewvit_dwconv3x3_bwd_fused finish with a reduce launch over their fp32 partial slabs.
+ * ewvit_reduce_defer_next(1) marks the calling thread's NEXT such call: its reduce is queued on
+ * its stream instead of launched (the call's workspace must then stay allocated, and dw must not
+ * be read, until the job has run).  Every later ewvit_conv2d_bwd_weight launch of those two
+ * forms on the same stream runs up to 2 queued jobs in extra workgroups ahead of its own tiles;
+ * ewvit_reduce_flush(stream) launches whatever is still queued on `stream`.  Summation order
+ * is the reduce kernel's: results are bit-identical to the immediate form.  The mark is
+ * consumed by the next ewvit_conv2d_bwd_weight / ewvit_dwconv3x3_bwd_fused call whatever path
+ * it takes.  ewvit_reduce_pending(stream) counts queued jobs (stream NULL: all streams).
+ * Replaces the per-call reduce of torch's weight-gradient convs (reached through
+ * network/sfe.py:111-113, the EfficientNetV2-S backbone). */
+int ewvit_reduce_defer_next(int on);
+int ewvit_reduce_flush(void *stream);
+int ewvit_reduce_pending(void *stream);
+
 /* ------------------------------ squeeze-excitation / stochastic-depth add ---
  * The MBConv block tail of the EfficientNetV2-S backbone (torchvision
  * SqueezeExcitation + StochasticDepth, reached via network/sfe.py:111-113) on
