@@ -420,15 +420,24 @@ __device__ __forceinline__ void bf4_unpack(const uint2 &q, float (&v)[4]) {
   v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
   v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
 }
+#ifndef DW_PD
+#define DW_PD 1          // columns loaded ahead (2 / 3 measured slower: profiles/r06/s2/ab/dw_prefetch.log)
+#endif
+#ifndef DW_Q16
+#define DW_Q16 0         // 1: 16 channel quads (128 B of a row) per block row, 512-thread blocks
+#endif
+constexpr int DW_NQ = DW_Q16 ? 16 : 8;           // channel quads per block row
+constexpr int DW_THREADS = 32 * DW_NQ;            // 32 rows per block (ewvit_dwconv3x3_bn_rows)
 template <int ST, int ACT, bool WG>
-__global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *__restrict__ in, const bf16_t *__restrict__ x,
-                                                      const float *__restrict__ w, bf16_t *__restrict__ out,
-                                                      DwShape s, DwBnFwd f, BnBwdStats b, float *__restrict__ wpart) {
+__global__ __launch_bounds__(DW_THREADS, (WG ? 2 : 4) * 256 / DW_THREADS) void dw_row4_kernel(
+    const bf16_t *__restrict__ in, const bf16_t *__restrict__ x, const float *__restrict__ w, bf16_t *__restrict__ out,
+    DwShape s, DwBnFwd f, BnBwdStats b, float *__restrict__ wpart) {
   constexpr int NV = 8 + (WG ? 36 : 0);        // per quad: 4 + 4 BN sums (+ 36 dW)
-  __shared__ float red[4][8 * NV];
-  const int tid = threadIdx.x, q = tid & 7, r = tid >> 3, wv = tid >> 6;
+  constexpr int NW = DW_THREADS / 64;
+  __shared__ float red[NW][DW_NQ * NV];
+  const int tid = threadIdx.x, q = tid % DW_NQ, r = tid / DW_NQ, wv = tid >> 6;
   const int C4 = s.C >> 2;
-  const int c4 = blockIdx.y * 8 + q;
+  const int c4 = blockIdx.y * DW_NQ + q;
   const int64_t row = (int64_t)blockIdx.x * 32 + r;          // n*H + h
   const bool active = c4 < C4 && row < (int64_t)s.N * s.H;
   float sa[4], sb[4], acc[WG ? 9 : 1][4];
@@ -486,9 +495,10 @@ __global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *
       return col < s.W ? (uint32_t)((base + (int64_t)col * s.C) * 2) : DW_OOB;
     };
     // window columns col - 1 .. col + 1 ([kw][kh]; G the conv input's, X (WG) x's) and the
-    // next column col + 2 loaded a column ahead, like the BN input (ST 2); every load is a
-    // buffer load (zeros outside the map), so the loop has no branch
-    uint2 G[3][3], X[3][3], Gn[3], Xn[3], bq;
+    // next DW_PD columns col + 2 .. loaded ahead, like the BN input (ST 2) — DW_PD columns of
+    // loads in flight behind the current one's FMAs; every load is a buffer load (zeros outside
+    // the map), so the loop has no branch
+    uint2 G[3][3], X[3][3], Gn[DW_PD][3], Xn[DW_PD][3], bq[DW_PD];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
 #pragma unroll
@@ -496,10 +506,14 @@ __global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *
         G[kw][kh] = dw_ld8(ir, off(kh, kw - 1));
         if (WG) X[kw][kh] = dw_ld8(xr, off(kh, kw - 1));
       }
-      Gn[kh] = dw_ld8(ir, off(kh, 2));
-      if (WG) Xn[kh] = dw_ld8(xr, off(kh, 2));
+#pragma unroll
+      for (int p = 0; p < DW_PD; ++p) {
+        Gn[p][kh] = dw_ld8(ir, off(kh, 2 + p));
+        if (WG) Xn[p][kh] = dw_ld8(xr, off(kh, 2 + p));
+      }
     }
-    bq = ST == 2 ? dw_ld8(br, boff(0)) : make_uint2(0u, 0u);
+#pragma unroll
+    for (int p = 0; p < DW_PD; ++p) bq[p] = ST == 2 ? dw_ld8(br, boff(p)) : make_uint2(0u, 0u);
 #pragma unroll 1
     for (int col = 0; col < s.W; ++col) {
       float o4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -539,7 +553,7 @@ __global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *
         }
       } else {
         float xv[4];
-        bf4_unpack(bq, xv);
+        bf4_unpack(bq[0], xv);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float xh = (xv[j] - p0[j]) * p1[j];
@@ -547,23 +561,33 @@ __global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *
           sa[j] += gg;
           sb[j] = fmaf(gg, xh, sb[j]);
         }
-        bq = dw_ld8(br, boff(col + 1));
+#pragma unroll
+        for (int p = 0; p + 1 < DW_PD; ++p) bq[p] = bq[p + 1];
+        bq[DW_PD - 1] = dw_ld8(br, boff(col + DW_PD));
       }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        const uint32_t o = off(kh, col + 3);
-        G[0][kh] = G[1][kh]; G[1][kh] = G[2][kh]; G[2][kh] = Gn[kh]; Gn[kh] = dw_ld8(ir, o);
-        if (WG) { X[0][kh] = X[1][kh]; X[1][kh] = X[2][kh]; X[2][kh] = Xn[kh]; Xn[kh] = dw_ld8(xr, o); }
+        const uint32_t o = off(kh, col + 2 + DW_PD);
+        G[0][kh] = G[1][kh]; G[1][kh] = G[2][kh]; G[2][kh] = Gn[0][kh];
+#pragma unroll
+        for (int p = 0; p + 1 < DW_PD; ++p) Gn[p][kh] = Gn[p + 1][kh];
+        Gn[DW_PD - 1][kh] = dw_ld8(ir, o);
+        if (WG) {
+          X[0][kh] = X[1][kh]; X[1][kh] = X[2][kh]; X[2][kh] = Xn[0][kh];
+#pragma unroll
+          for (int p = 0; p + 1 < DW_PD; ++p) Xn[p][kh] = Xn[p + 1][kh];
+          Xn[DW_PD - 1][kh] = dw_ld8(xr, o);
+        }
       }
     }
   }
-  // the wave's 8 rows (lane bits 3..5) of each quad, then the 4 waves in order
+  // the wave's rows of each quad (lane bits 3..5, or 4..5 with 16 quads), then the waves in order
   float *mine = red[wv] + q * NV;
   const int lane = tid & 63;
   auto put = [&](int i, float v) {
-    v += dpp_mov<0x128>(v);                    // row_ror:8 = lane ^ 8 within the row
+    if constexpr (DW_NQ == 8) v += dpp_mov<0x128>(v);    // row_ror:8 = lane ^ 8 within the row
     v = rows_sum4(v);
-    if (lane < 8) mine[i] = v;
+    if (lane < DW_NQ) mine[i] = v;
   };
 #pragma unroll
   for (int j = 0; j < 4; ++j) { put(j, sa[j]); put(4 + j, sb[j]); }
@@ -574,11 +598,12 @@ __global__ __launch_bounds__(256, WG ? 2 : 4) void dw_row4_kernel(const bf16_t *
       for (int j = 0; j < 4; ++j) put(8 + j * 9 + k, acc[WG ? k : 0][j]);
   }
   __syncthreads();
-  for (int i = tid; i < 8 * NV; i += 256) {
+  for (int i = tid; i < DW_NQ * NV; i += DW_THREADS) {
     const int qq = i / NV, k = i - qq * NV;
-    const int cq = blockIdx.y * 8 + qq;
+    const int cq = blockIdx.y * DW_NQ + qq;
     if (cq >= C4) continue;
-    const float t = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    float t = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    if constexpr (NW == 8) t += (red[4 % NW][i] + red[5 % NW][i]) + (red[6 % NW][i] + red[7 % NW][i]);
     if (k < 8) {
       float *pr = (ST == 1 ? f.part : b.part) + (int64_t)blockIdx.x * 2 * s.C;
       pr[(k < 4 ? 0 : s.C) + cq * 4 + (k & 3)] = t;
@@ -950,7 +975,8 @@ extern "C" int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, in
   f.part = part; f.shift = shift; f.shift_out = shift_out;
   BnBwdStats b;
   if (stride == 1) {
-    hipLaunchKernelGGL((dw_row4_kernel<1, 0, false>), dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0,
+    hipLaunchKernelGGL((dw_row4_kernel<1, 0, false>), dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)),
+                       dim3(DW_THREADS), 0,
                        as_stream(stream), (const bf16_t *)x, nullptr, w, (bf16_t *)y, s, f, b, nullptr);
     return launch_status("dwconv3x3_fwd_bn");
   }
@@ -978,8 +1004,8 @@ extern "C" int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void 
   b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
   b.act = act;
   auto kern = act == 2 ? dw_row4_kernel<2, 2, false> : act == 1 ? dw_row4_kernel<2, 1, false> : dw_row4_kernel<2, 0, false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0, as_stream(stream),
-                     (const bf16_t *)dy, nullptr, w, (bf16_t *)dx, s, f, b, nullptr);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)), dim3(DW_THREADS), 0,
+                     as_stream(stream), (const bf16_t *)dy, nullptr, w, (bf16_t *)dx, s, f, b, nullptr);
   return launch_status("dwconv3x3_bwd_data_bn");
 }
 
@@ -1009,7 +1035,7 @@ extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *d
   hipStream_t st = as_stream(stream);
   DwBnFwd f;
   auto kern = act == 2 ? dw_row4_kernel<2, 2, true> : act == 1 ? dw_row4_kernel<2, 1, true> : dw_row4_kernel<2, 0, true>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + 7) / 8)), dim3(256), 0, st,
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)), dim3(DW_THREADS), 0, st,
                      (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace);
   if (int rc = launch_status("dwconv3x3_bwd_fused")) return rc;
   const int64_t n = C * 9;

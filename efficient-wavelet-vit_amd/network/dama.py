@@ -49,14 +49,17 @@ def _branch_streams():
     return os.environ.get('EWVIT_BRANCH_STREAMS', '1') == '1'
 
 
-MWT_GRID_CAP = 96           # measured at world 1; the same at world > 1 (see _mwt_grid_cap)
+MWT_GRID_CAP = 128          # measured at world 1; the same at world > 1 (see _mwt_grid_cap)
 
 
 def _mwt_grid_cap(world=None):
     """Workgroups per big-grid MWT launch (LDS-DMA convs, BatchNorm passes) while the MWT
     shares the GPU with the backbone (EWVIT_MWT_GRID_CAP, 0 = uncapped): the MWT walks its
-    tiles / rows on 96 of the 256 CUs (12 per XCD) and the backbone's latency-bound kernels
-    keep the rest.  With the tap-split windowed weight gradient (8 waves per workgroup) the MWT
+    tiles / rows on 128 of the 256 CUs (16 per XCD) and the backbone's latency-bound kernels
+    keep the rest.  After the deferred weight-gradient reductions shortened the backbone's
+    backward (round 6, config 2, same box, interleaved rounds, profiles/r06/s2/ab/cap_*.log):
+    80 3480-3482, 96 3884-3894, 112 3868-3879, **128 3902-3917** frames/s.  With the tap-split
+    windowed weight gradient (8 waves per workgroup) the MWT
     keeps pace on fewer CUs (config 2, same box, 2 rounds each, profiles/r05/ab/cap_sweep_ts.log):
     80 3502-3508, **96 3645-3654**, 104 3603-3606, 112 3604-3608, 128 3614-3621, 160 3539-3545
     frames/s.  Before it (round 5's first windowed kernels, profiles/r05/ab/cap_sweep*.log): 64
@@ -65,10 +68,10 @@ def _mwt_grid_cap(world=None):
 
     Data parallel (reference train.py:249-251 on N GPUs) uses the SAME cap: the bucket
     all-reduces' RCCL kernels (one workgroup per RCCL channel) run during the backward on the
-    160 CUs the cap leaves outside the MWT, beside the backbone's backward, whose 7^2-28^2
+    128 CUs the cap leaves outside the MWT, beside the backbone's backward, whose 7^2-28^2
     launches fill 50-800 workgroups and leave CU slots between them.  Taking a
-    reserve off the MWT instead would only move the MWT off its measured balance point (cap 80:
-    -4 % at world 1).  No multi-GPU node was available to sweep the world > 1 budget, so the
+    reserve off the MWT instead would only move the MWT off its measured balance point (cap 96:
+    -0.6 %, cap 80: -11 % at world 1).  No multi-GPU node was available to sweep the world > 1 budget, so the
     argument is kept for that sweep: EWVIT_MWT_GRID_CAP overrides the cap at every world size."""
     env = os.environ.get('EWVIT_MWT_GRID_CAP')
     if env is not None:
