@@ -271,6 +271,21 @@ struct DwBnFwd {
   const float *shift = nullptr;
   float *shift_out = nullptr;
 };
+// The BatchNorm(+act) + squeeze-excitation backward of the conv's OUTPUT, folded into the
+// stride-1 fused backward (dw_row4_kernel SE): the conv's output gradient
+//   dz = gamma*invstd*(act'(zhat*gamma + beta) * (dy*s + g) - row/n - zhat * row'/n),
+// zhat = (z - mean)*invstd, is formed from the SE output gradient dy and z as the window loads
+// them — the same operations in the same order as bn_bwd_dx_kernel<bf16, act, 2>, rounded to
+// bf16 as it stores dz — so the dz tensor is never written or read (ewvit_bn_se_bwd with dx
+// NULL leaves `row` and dgamma / dbeta).
+struct DwSe {
+  const bf16_t *z = nullptr;                     // the BatchNorm's input (the conv's output)
+  const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
+  const float *row = nullptr;                    // [2C]: sum g', sum g' zhat
+  const float *s = nullptr, *g = nullptr;        // [N][C]: excitation, squeeze term
+  float n = 1.f;                                 // rows N*H*W
+  int act = 0;
+};
 template <int STRIDE, bool ROT, int ST, int ACT>
 __global__ __launch_bounds__(256) void dw_row_bn_kernel(const bf16_t *__restrict__ x, const float *__restrict__ w,
                                                         bf16_t *__restrict__ y, DwShape s, DwBnFwd f, BnBwdStats b) {
@@ -428,10 +443,11 @@ __device__ __forceinline__ void bf4_unpack(const uint2 &q, float (&v)[4]) {
 #endif
 constexpr int DW_NQ = DW_Q16 ? 16 : 8;           // channel quads per block row
 constexpr int DW_THREADS = 32 * DW_NQ;            // 32 rows per block (ewvit_dwconv3x3_bn_rows)
-template <int ST, int ACT, bool WG>
+template <int ST, int ACT, bool WG, bool SE = false>
 __global__ __launch_bounds__(DW_THREADS, (WG ? 2 : 4) * 256 / DW_THREADS) void dw_row4_kernel(
     const bf16_t *__restrict__ in, const bf16_t *__restrict__ x, const float *__restrict__ w, bf16_t *__restrict__ out,
-    DwShape s, DwBnFwd f, BnBwdStats b, float *__restrict__ wpart) {
+    DwShape s, DwBnFwd f, BnBwdStats b, float *__restrict__ wpart, DwSe e = DwSe()) {
+  static_assert(!SE || (ST == 2 && DW_PD == 1), "the SE fold is the stride-1 backward with one column ahead");
   constexpr int NV = 8 + (WG ? 36 : 0);        // per quad: 4 + 4 BN sums (+ 36 dW)
   constexpr int NW = DW_THREADS / 64;
   __shared__ float red[NW][DW_NQ * NV];
@@ -494,23 +510,54 @@ __global__ __launch_bounds__(DW_THREADS, (WG ? 2 : 4) * 256 / DW_THREADS) void d
     auto boff = [&](int col) -> uint32_t {
       return col < s.W ? (uint32_t)((base + (int64_t)col * s.C) * 2) : DW_OOB;
     };
+    // SE: the folded BN + SE backward's per-channel (and, for this row's frame, per-frame) factors
+    float e_mu[4], e_iv[4], e_ga[4], e_be[4], e_c0[4], e_c1[4], e_sv[4], e_gv[4];
+    if constexpr (SE) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e_mu[j] = e.mean[c + j]; e_iv[j] = e.invstd[c + j];
+        e_ga[j] = e.gamma ? e.gamma[c + j] : 1.f; e_be[j] = e.beta ? e.beta[c + j] : 0.f;
+        e_c0[j] = e.row[c + j] / e.n; e_c1[j] = e.row[s.C + c + j] / e.n;
+        e_sv[j] = e.s[(int64_t)n * s.C + c + j]; e_gv[j] = e.g[(int64_t)n * s.C + c + j];
+      }
+    }
+    const __amdgpu_buffer_rsrc_t zr = dw_rsrc(SE ? (const void *)e.z : (const void *)in, total);
+    // dz of one window element from dy and z (zero outside the map, as the dz tensor's load was)
+    auto xf = [&](uint2 dq, uint2 zq, bool ok) -> uint2 {
+      float vd[4], vz[4], o[4];
+      bf4_unpack(dq, vd);
+      bf4_unpack(zq, vz);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vd[j] = fmaf(vd[j], e_sv[j], e_gv[j]);
+        const float xh = (vz[j] - e_mu[j]) * e_iv[j];
+        const float g = e.act ? vd[j] * bn_act_grad(e.act, fmaf(xh, e_ga[j], e_be[j])) : vd[j];
+        o[j] = e_ga[j] * e_iv[j] * (g - e_c0[j] - xh * e_c1[j]);
+      }
+      return ok ? make_uint2((unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16),
+                             (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16))
+                : make_uint2(0u, 0u);
+    };
     // window columns col - 1 .. col + 1 ([kw][kh]; G the conv input's, X (WG) x's) and the
     // next DW_PD columns col + 2 .. loaded ahead, like the BN input (ST 2) — DW_PD columns of
     // loads in flight behind the current one's FMAs; every load is a buffer load (zeros outside
     // the map), so the loop has no branch
-    uint2 G[3][3], X[3][3], Gn[DW_PD][3], Xn[DW_PD][3], bq[DW_PD];
+    uint2 G[3][3], X[3][3], Gn[DW_PD][3], Xn[DW_PD][3], bq[DW_PD], Zn[3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        G[kw][kh] = dw_ld8(ir, off(kh, kw - 1));
-        if (WG) X[kw][kh] = dw_ld8(xr, off(kh, kw - 1));
+        const uint32_t o = off(kh, kw - 1);
+        G[kw][kh] = dw_ld8(ir, o);
+        if constexpr (SE) G[kw][kh] = xf(G[kw][kh], dw_ld8(zr, o), o != DW_OOB);
+        if (WG) X[kw][kh] = dw_ld8(xr, o);
       }
 #pragma unroll
       for (int p = 0; p < DW_PD; ++p) {
         Gn[p][kh] = dw_ld8(ir, off(kh, 2 + p));
         if (WG) Xn[p][kh] = dw_ld8(xr, off(kh, 2 + p));
       }
+      if constexpr (SE) Zn[kh] = dw_ld8(zr, off(kh, 2));
     }
 #pragma unroll
     for (int p = 0; p < DW_PD; ++p) bq[p] = ST == 2 ? dw_ld8(br, boff(p)) : make_uint2(0u, 0u);
@@ -568,7 +615,13 @@ __global__ __launch_bounds__(DW_THREADS, (WG ? 2 : 4) * 256 / DW_THREADS) void d
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const uint32_t o = off(kh, col + 2 + DW_PD);
-        G[0][kh] = G[1][kh]; G[1][kh] = G[2][kh]; G[2][kh] = Gn[0][kh];
+        G[0][kh] = G[1][kh]; G[1][kh] = G[2][kh];
+        if constexpr (SE) {
+          G[2][kh] = xf(Gn[0][kh], Zn[kh], off(kh, col + 2) != DW_OOB);
+          Zn[kh] = dw_ld8(zr, o);
+        } else {
+          G[2][kh] = Gn[0][kh];
+        }
 #pragma unroll
         for (int p = 0; p + 1 < DW_PD; ++p) Gn[p][kh] = Gn[p + 1][kh];
         Gn[DW_PD - 1][kh] = dw_ld8(ir, o);
@@ -977,7 +1030,7 @@ extern "C" int ewvit_dwconv3x3_fwd_bn(const void *x, const float *w, void *y, in
   if (stride == 1) {
     hipLaunchKernelGGL((dw_row4_kernel<1, 0, false>), dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)),
                        dim3(DW_THREADS), 0,
-                       as_stream(stream), (const bf16_t *)x, nullptr, w, (bf16_t *)y, s, f, b, nullptr);
+                       as_stream(stream), (const bf16_t *)x, nullptr, w, (bf16_t *)y, s, f, b, nullptr, DwSe());
     return launch_status("dwconv3x3_fwd_bn");
   }
   hipLaunchKernelGGL((dw_row_bn_kernel<2, false, 1, 0>), dim3((unsigned)nrc, (unsigned)((C / 8 + 7) / 8)), dim3(256), 0,
@@ -1005,7 +1058,7 @@ extern "C" int ewvit_dwconv3x3_bwd_data_bn(const void *dy, const float *w, void 
   b.act = act;
   auto kern = act == 2 ? dw_row4_kernel<2, 2, false> : act == 1 ? dw_row4_kernel<2, 1, false> : dw_row4_kernel<2, 0, false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)), dim3(DW_THREADS), 0,
-                     as_stream(stream), (const bf16_t *)dy, nullptr, w, (bf16_t *)dx, s, f, b, nullptr);
+                     as_stream(stream), (const bf16_t *)dy, nullptr, w, (bf16_t *)dx, s, f, b, nullptr, DwSe());
   return launch_status("dwconv3x3_bwd_data_bn");
 }
 
@@ -1036,7 +1089,7 @@ extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *d
   DwBnFwd f;
   auto kern = act == 2 ? dw_row4_kernel<2, 2, true> : act == 1 ? dw_row4_kernel<2, 1, true> : dw_row4_kernel<2, 0, true>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)), dim3(DW_THREADS), 0, st,
-                     (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace);
+                     (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace, DwSe());
   if (int rc = launch_status("dwconv3x3_bwd_fused")) return rc;
   const int64_t n = C * 9;
   if (defer_mark) {                 // the slab sum runs in front of a later weight-gradient launch
@@ -1048,6 +1101,49 @@ extern "C" int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *d
   hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace, dw, n,
                      (int)nrc, accumulate);
   return launch_status("dwconv3x3_bwd_fused reduce");
+}
+
+// ewvit_dwconv3x3_bwd_fused with the BatchNorm(+act) + squeeze-excitation backward of the conv's
+// output folded in (DwSe): `dy` is the SE OUTPUT gradient, z / se_* the BN's input, saved
+// statistics, affine and the sums row (ewvit_bn_se_bwd with dx NULL), se_s / se_g [N][C]
+extern "C" int ewvit_dwconv3x3_bwd_fused_se(const void *dy, const float *w, void *dx, const void *x, float *dw,
+                                            int accumulate, int64_t N, int64_t H, int64_t W, int64_t C, const void *bx,
+                                            const float *mean, const float *invstd, const float *gamma,
+                                            const float *beta, int act, float *part, float *workspace, const void *z,
+                                            const float *se_mean, const float *se_invstd, const float *se_gamma,
+                                            const float *se_beta, int se_act, const float *se_row, const float *se_s,
+                                            const float *se_g, void *stream) {
+  const bool defer_mark = reduce_take_defer();      // (reduce_jobs.h; consumed by every call)
+  EWVIT_CHECK_ARG(dy && w && dx && x && dw && bx && mean && invstd && part && workspace && act >= 0 && act <= 2 &&
+                      z && se_mean && se_invstd && se_row && se_s && se_g && se_act >= 0 && se_act <= 2,
+                  "dwconv3x3_bwd_fused_se: bad args");
+  const int64_t nrc = ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1);
+  EWVIT_CHECK_ARG(nrc > 0 && nrc < 65536, "dwconv3x3_bwd_fused_se: shape not supported");
+  DwShape s = mk(N, H, W, C, 1, 1);
+  if (int rc = check_shape(s, "dwconv3x3_bwd_fused_se")) return rc;
+  BnBwdStats b;
+  b.part = part; b.x = (const bf16_t *)bx; b.mean = mean; b.invstd = invstd; b.gamma = gamma; b.beta = beta;
+  b.act = act;
+  DwSe e;
+  e.z = (const bf16_t *)z; e.mean = se_mean; e.invstd = se_invstd; e.gamma = se_gamma; e.beta = se_beta;
+  e.row = se_row; e.s = se_s; e.g = se_g; e.n = (float)(N * H * W); e.act = se_act;
+  hipStream_t st = as_stream(stream);
+  DwBnFwd f;
+  auto kern = act == 2 ? dw_row4_kernel<2, 2, true, true> : act == 1 ? dw_row4_kernel<2, 1, true, true>
+                                                                   : dw_row4_kernel<2, 0, true, true>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrc, (unsigned)((C / 4 + DW_NQ - 1) / DW_NQ)), dim3(DW_THREADS), 0, st,
+                     (const bf16_t *)dy, (const bf16_t *)x, w, (bf16_t *)dx, s, f, b, workspace, e);
+  if (int rc = launch_status("dwconv3x3_bwd_fused_se")) return rc;
+  const int64_t n = C * 9;
+  if (defer_mark) {
+    RedJob j;
+    j.kind = 2; j.part = workspace; j.dw = dw; j.n = n; j.splits = (int)nrc; j.accumulate = accumulate;
+    reduce_defer(st, j);
+    return 0;
+  }
+  hipLaunchKernelGGL(dw_bwd_weight_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace, dw, n,
+                     (int)nrc, accumulate);
+  return launch_status("dwconv3x3_bwd_fused_se reduce");
 }
 
 // weight-gradient plan: row kernel (bf16, C/8 <= 256) with `slabs` blocks, or the

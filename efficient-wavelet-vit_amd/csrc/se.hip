@@ -457,7 +457,8 @@ __global__ __launch_bounds__(256) void se_mlp_g_kernel(const float *__restrict__
 // (Extra blocks of se_mlp_wgrad_kernel: no launch of its own.)
 __device__ __forceinline__ void se_bn_sums_block(int bx, const float *__restrict__ bnsum, const float *__restrict__ s,
                                                  const float *__restrict__ g, int N, int C, float *__restrict__ out,
-                                                 float (*red)[64]) {
+                                                 float (*red)[64], float *__restrict__ dbeta = nullptr,
+                                                 float *__restrict__ dgamma = nullptr) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = bx * 64 + lane;                  // 0 .. 2C - 1
   const int which = k >= C, c = which ? k - C : k;
@@ -484,7 +485,14 @@ __device__ __forceinline__ void se_bn_sums_block(int bx, const float *__restrict
   }
   red[w][lane] = acc0 + acc1;
   __syncthreads();
-  if (w == 0 && k < 2 * C) out[k] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && k < 2 * C) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    out[k] = v;
+    // the BN's parameter gradients are these sums (dbeta = sum g', dgamma = sum g' xhat): written
+    // here when the dx pass is folded into the depthwise backward (ewvit_bn_se_bwd, dx NULL)
+    float *d = which ? dgamma : dbeta;
+    if (d) d[c] = v;
+  }
 }
 
 
@@ -503,10 +511,12 @@ __global__ __launch_bounds__(256) void se_mlp_wgrad_kernel(const float *__restri
                                                            const float *__restrict__ bnsum = nullptr,
                                                            const float *__restrict__ exc = nullptr,
                                                            const float *__restrict__ gsq = nullptr,
-                                                           float *__restrict__ bnout = nullptr, int nwb = 0) {
+                                                           float *__restrict__ bnout = nullptr, int nwb = 0,
+                                                           float *__restrict__ bn_dbeta = nullptr,
+                                                           float *__restrict__ bn_dgamma = nullptr) {
   __shared__ float red[4][64];
   if (bnsum && (int)blockIdx.x >= nwb) {         // the BN sums' blocks (ewvit_bn_se_bwd)
-    se_bn_sums_block((int)blockIdx.x - nwb, bnsum, exc, gsq, N, C, bnout, red);
+    se_bn_sums_block((int)blockIdx.x - nwb, bnsum, exc, gsq, N, C, bnout, red, bn_dbeta, bn_dgamma);
     return;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1117,6 +1127,24 @@ extern "C" int64_t ewvit_bn_se_bwd_workspace(int64_t N, int64_t C, int64_t Csq) 
   return ewvit_se_mlp_bwd_workspace(N, C, Csq) + (4 * N * C + 2 * C) * (int64_t)sizeof(float);
 }
 
+// where ewvit_bn_se_bwd leaves the BN's sums row [2C] (sum g', sum g' zhat) in its workspace (floats)
+extern "C" int64_t ewvit_bn_se_bwd_row_offset(int64_t N, int64_t C, int64_t Csq) {
+  return ewvit_se_mlp_bwd_workspace(N, C, Csq) / (int64_t)sizeof(float) + 4 * N * C;
+}
+
+// the dx pass alone, from the sums row ewvit_bn_se_bwd (dx NULL) left: dx = the BN input gradient
+// of SE(act(BN(z))) given the SE output gradient dy (the form ewvit_dwconv3x3_bwd_fused_se folds)
+extern "C" int ewvit_bn_se_bwd_dx(const void *dy, const void *z, void *dx, int dtype, int64_t N, int64_t HW, int64_t C,
+                                  const float *gamma, const float *beta, const float *save_mean,
+                                  const float *save_invstd, int act, const float *s, const float *g, const float *row,
+                                  void *stream) {
+  if (int rc = se_check(dtype, N, HW, C, "bn_se_bwd_dx")) return rc;
+  EWVIT_CHECK_ARG(dy && z && dx && save_mean && save_invstd && s && g && row && act >= 0 && act <= 2 && C <= 4096,
+                  "bn_se_bwd_dx: bad args");
+  return bn_bwd_dx_se_launch(dy, z, dx, dtype, N * HW, C, gamma, beta, save_mean, save_invstd, act, nullptr, nullptr,
+                             s, g, HW, row, 1, as_stream(stream));
+}
+
 // The backward of SE(act(BatchNorm(z))) in 4 launches: the SE squeeze pass with the BN's
 // per-frame sums (se_sq_dh_bn_part_kernel), the MLP's g, its weight gradients + the BN's two
 // channel sums (extra blocks), and the BN's dx pass from that one partial row.  Replaces
@@ -1129,7 +1157,10 @@ extern "C" int ewvit_bn_se_bwd(const void *dy, const void *a, const void *z, voi
                                void *stream) {
   if (int rc = se_check(dtype, N, HW, C, "bn_se_bwd")) return rc;
   if (int rc = se_mlp_check(N, C, Csq, "bn_se_bwd")) return rc;
-  EWVIT_CHECK_ARG(dy && a && z && dx && save_mean && save_invstd && s && h1 && s0 && w1 && w2 && g && dw1 && dw2 &&
+  // dx NULL: the dx pass is left to the depthwise conv's backward (ewvit_dwconv3x3_bwd_fused_se, which
+  // forms dz from dy and z); dgamma / dbeta come from the sums blocks, the sums row stays in the
+  // workspace at ewvit_bn_se_bwd_row_offset floats
+  EWVIT_CHECK_ARG(dy && a && z && save_mean && save_invstd && s && h1 && s0 && w1 && w2 && g && dw1 && dw2 &&
                       workspace && HW < (1 << 30),
                   "bn_se_bwd: bad args");
   EWVIT_CHECK_ARG(act >= 0 && act <= 2 && C <= 4096 && N * HW < ((int64_t)1 << 31), "bn_se_bwd: act=%d C=%lld", act,
@@ -1157,8 +1188,10 @@ extern "C" int ewvit_bn_se_bwd(const void *dy, const void *a, const void *z, voi
   const int64_t tot = 2 * C * Csq + C + Csq;
   const int nwb = (int)((tot + 63) / 64), nbn = (int)((2 * C + 63) / 64);
   hipLaunchKernelGGL(se_mlp_wgrad_kernel, dim3((unsigned)(nwb + nbn)), dim3(256), 0, st, dz2, dz1, h1, s0, (int)N,
-                     (int)C, (int)Csq, dw1, db1, dw2, db2, bnsum, s, g, bnrow, nwb);
+                     (int)C, (int)Csq, dw1, db1, dw2, db2, bnsum, s, g, bnrow, nwb, dx ? nullptr : dbeta,
+                     dx ? nullptr : dgamma);
   if (int rc = launch_status("bn_se_bwd")) return rc;
+  if (!dx) return 0;
   return bn_bwd_dx_se_launch(dy, z, dx, dtype, N * HW, C, gamma, beta, save_mean, save_invstd, act, dgamma, dbeta, s,
                              g, HW, bnrow, 1, st);
 }

@@ -84,6 +84,9 @@ SIGNATURES = {
     'ewvit_bn_bwd_se': [_vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     'ewvit_bn_se_bwd': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp,
                         _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'ewvit_bn_se_bwd_dx': [_vp, _vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp],
+    'ewvit_dwconv3x3_bwd_fused_se': [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                     _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp],
     'ewvit_bn_fold_partials': [_vp, _i32, _vp, _vp, _i32, _vp, _i64, _i32, _vp],
     'ewvit_conv2d_fwd': [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i64, _i64, _vp],
     'ewvit_conv2d_stem_fwd': [_vp, _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64,
@@ -155,6 +158,7 @@ QUERIES = {
     'ewvit_se_reduce_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_bwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_bn_se_bwd_workspace': (_i64, [_i64, _i64, _i64]),
+    'ewvit_bn_se_bwd_row_offset': (_i64, [_i64, _i64, _i64]),
     'ewvit_se_mlp_fwd_workspace': (_i64, [_i64, _i64, _i64]),
     'ewvit_frames_plan': (_i32, [_vp, _i64, _i32, _i64, _vp]),
     'ewvit_adam_chunks': (_i64, [_i64]),

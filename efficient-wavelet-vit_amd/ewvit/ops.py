@@ -549,8 +549,10 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
     """groups=C 3x3 conv, no bias, channels-last (EfficientNetV2-S MBConv depthwise)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, bn_stats=None):
+    def forward(ctx, x, weight, stride, pad, bn_stats=None, selink=None):
         L.require_gpu(x, weight)
+        # the BN + SE after this conv may hand its dx pass to this backward (ewvit.se.SeDxLink)
+        ctx.selink = selink
         N, C, H, W = x.shape
         xc = x.contiguous(memory_format=torch.channels_last)
         w = weight.detach().float().contiguous()
@@ -582,12 +584,25 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
         xc, w = ctx.saved_tensors
         stride, pad, wdt = ctx.cfg
         N, C, H, W = xc.shape
+        bl = ctx.bnlink
+        ctx.bnlink = None
+        # the BN + SE backward's dx pass left to this conv (ewvit.se.SeDxLink): folded into the
+        # fused backward below when it runs, else formed now (dy is its output, not yet written)
+        sl, fold = ctx.selink, None
+        ctx.selink = None
+        if sl is not None and sl.pending(dy):
+            rows = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, stride, 1)) \
+                if bl is not None and xc.dtype == torch.bfloat16 and bl.x.shape == xc.shape else 0
+            if (ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and 0 < rows <= _bn.BWD_LINK_MAX_ROWS
+                    and wdt == torch.float32 and _DW_BWD_FUSED and C % 8 == 0 and stride == 1 and pad == 1
+                    and L.has('ewvit_dwconv3x3_bwd_fused_se')):
+                fold = sl.take()
+            else:
+                sl.materialize()
         dyc = dy.contiguous(memory_format=torch.channels_last)
         if dyc.dtype != xc.dtype:
             dyc = dyc.to(xc.dtype)
         dx = dw = None
-        bl = ctx.bnlink
-        ctx.bnlink = None
         if ctx.needs_input_grad[1]:
             # the gradient slot itself when its layout is the kernel's [C][9] (ewvit.grads)
             out = grad_out(ctx.params[0], ctx.gen) if wdt == torch.float32 else None
@@ -610,10 +625,21 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                         # dW is read by nobody before the end of the backward (grads.deferrable):
                         # its slab sum rides in a later weight-gradient launch (ewvit.defer)
                         _defer.mark(ws, xc.device)
-                    L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dyc), L.ptr(w), L.ptr(dx), L.ptr(xc), L.ptr(dw), 0,
-                           N, H, W, C, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma),
-                           L.ptr(bl.beta), bl.act, L.ptr(part), L.ptr(ws), L.stream(dx),
-                           work={'bytes': (dyc.numel() + 3 * dx.numel()) * dx.element_size()})
+                    if fold is not None:
+                        # ... with the BN + SE backward of this conv's output folded in: dy is the SE
+                        # output gradient, the conv's output gradient is formed per window element
+                        f = fold
+                        L.call('ewvit_dwconv3x3_bwd_fused_se', L.ptr(f.dy), L.ptr(w), L.ptr(dx), L.ptr(xc),
+                               L.ptr(dw), 0, N, H, W, C, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd),
+                               L.ptr(bl.gamma), L.ptr(bl.beta), bl.act, L.ptr(part), L.ptr(ws), L.ptr(f.z),
+                               L.ptr(f.mean), L.ptr(f.invstd), L.ptr(f.gamma), L.ptr(f.beta), f.act, L.ptr(f.row),
+                               L.ptr(f.s), L.ptr(f.g), L.stream(dx),
+                               work={'bytes': (2 * f.dy.numel() + 3 * dx.numel()) * dx.element_size()})
+                    else:
+                        L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dyc), L.ptr(w), L.ptr(dx), L.ptr(xc), L.ptr(dw), 0,
+                               N, H, W, C, L.ptr(bl.x), L.ptr(bl.mean), L.ptr(bl.invstd), L.ptr(bl.gamma),
+                               L.ptr(bl.beta), bl.act, L.ptr(part), L.ptr(ws), L.stream(dx),
+                               work={'bytes': (dyc.numel() + 3 * dx.numel()) * dx.element_size()})
                     wdone = True
                 else:
                     L.call('ewvit_dwconv3x3_bwd_data_bn', L.ptr(dyc), L.ptr(w), L.ptr(dx), N, H, W, C, L.ptr(bl.x),
@@ -638,7 +664,9 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                 else:
                     dw = torch.empty_strided(dw.shape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
             dw = grads.give(ctx.params[0], dw, ctx.gen)
-        return dx, dw, None, None, None
+        if fold is not None and not wdone:
+            raise RuntimeError('dwconv3x3 backward: the folded BN + SE dx pass did not run')
+        return dx, dw, None, None, None, None
 
 
 def dwconv3x3(x, weight, stride=1, pad=1):
@@ -647,7 +675,7 @@ def dwconv3x3(x, weight, stride=1, pad=1):
     return DepthwiseConv3x3Fn.apply(x, weight, int(stride), int(pad))
 
 
-def dwconv3x3_bn_stats(x, weight, stride, shift):
+def dwconv3x3_bn_stats(x, weight, stride, shift, selink=None):
     """dwconv3x3 (pad 1, bf16) whose kernel also leaves the BatchNorm partial statistics of
     its output centred on `shift` (the BN running mean): (y, part, shifts, nrc) for
     ewvit.bn.batch_norm_act / bn_act_se(..., partials=(part, shifts, nrc)), or None when the
@@ -663,7 +691,7 @@ def dwconv3x3_bn_stats(x, weight, stride, shift):
     part = torch.empty(nrc, 2 * C, dtype=torch.float32, device=x.device)
     shifts = torch.empty(C, dtype=torch.float32, device=x.device)
     sh = shift.detach().float().contiguous() if shift is not None else None
-    y = DepthwiseConv3x3Fn.apply(x, weight, int(stride), 1, (sh, part, shifts))
+    y = DepthwiseConv3x3Fn.apply(x, weight, int(stride), 1, (sh, part, shifts), selink)
     return y, part, shifts, nrc
 
 

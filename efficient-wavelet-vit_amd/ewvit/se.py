@@ -24,6 +24,46 @@ _BN_SQUEEZE = os.environ.get('EWVIT_BN_SQUEEZE', '1') != '0'
 # the depthwise BN's backward reduction inside the SE backward's squeeze pass (ewvit_bn_se_bwd);
 # EWVIT_BN_SE_FUSED=0: ewvit_se_squeeze_mlp_bwd + ewvit_bn_bwd_se (A/B)
 _BN_SE_FUSED = os.environ.get('EWVIT_BN_SE_FUSED', '1') != '0'
+# the BN + SE backward's dx pass folded into the depthwise conv's fused backward (SeDxLink).  Off:
+# measured 2 % slower at config 2 (3834-3842 against 3908-3920 frames/s, same box,
+# profiles/r06/s2/ab/se_dx_fold.log) — the transform (an exp and a reciprocal per element, three
+# times per element across the row windows) and 234 VGPRs cost the depthwise backward more than
+# the dz pass it removes.  EWVIT_SE_DX_FOLD=1: the A/B.
+_SE_DX_FOLD = os.environ.get('EWVIT_SE_DX_FOLD', '0') == '1'
+
+
+class SeDxLink:
+    """MBConv's depthwise conv -> BatchNorm -> SiLU -> SE (reference network/sfe.py:111-113, the
+    torchvision blocks): the BN + SE backward (BnActSEFn) computes its sums but leaves the dx pass
+    to the depthwise conv's backward, which forms dz per window element from the SE output
+    gradient and z (ewvit_dwconv3x3_bwd_fused_se) — the dz tensor is never written or read.
+    BnActSEFn returns an unwritten placeholder for dz; the conv's backward, the only consumer of
+    that gradient (the pair is built by network.efficientnet._seq), either folds it (``take``)
+    or has the dx pass write it first (``materialize``)."""
+
+    def __init__(self):
+        self.dx = None          # the placeholder handed to autograd
+        self.args = None        # what the dx pass needs (SimpleNamespace-like)
+
+    def pending(self, dy):
+        return self.args is not None and self.dx is not None and dy.data_ptr() == self.dx.data_ptr()
+
+    def take(self):
+        a, self.args, self.dx = self.args, None, None
+        return a
+
+    def materialize(self):
+        a, dx = self.args, self.dx
+        self.args = self.dx = None
+        if a is None:
+            return
+        L.call('ewvit_bn_se_bwd_dx', L.ptr(a.dy), L.ptr(a.z), L.ptr(dx), L.dt(a.z), a.N, a.HW, a.C, L.ptr(a.gamma),
+               L.ptr(a.beta), L.ptr(a.mean), L.ptr(a.invstd), a.act, L.ptr(a.s), L.ptr(a.g), L.ptr(a.row),
+               L.stream(dx), work={'bytes': 3 * dx.numel() * dx.element_size()})
+
+
+class _SeDxArgs:
+    __slots__ = ('dy', 'z', 'gamma', 'beta', 'mean', 'invstd', 'act', 's', 'g', 'row', 'N', 'HW', 'C', 'ws')
 # (the BatchNorm backward's sums taken per frame by the SE backward's squeeze kernel measured
 # slower — SFE piece 14.22-14.25 -> 14.28-14.32 ms, profiles/r03/ab/se_bn_sums_ab.txt — and
 # was removed: that kernel walks one frame's 49-196 rows per block, so the extra operand's loads
@@ -159,8 +199,9 @@ class BnActSEFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, counter, act, w1, b1, w2, b2,
-                partials=None):
+                partials=None, link=None):
         L.require_gpu(x)
+        ctx.link = link
         xc, N, HW, C = _rows(x)
         M = N * HW
         dev = x.device
@@ -229,15 +270,30 @@ class BnActSEFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         dg = _vec_out(pg, ctx.gen, C, dev)
         db = _vec_out(pb, ctx.gen, C, dev)
+        link, ctx.link = ctx.link, None
         if _BN_SE_FUSED and C <= 4096 and L.has('ewvit_bn_se_bwd'):
             # the BN's reduction inside the SE squeeze pass: 4 launches, dy and z read once fewer
             mws = torch.empty(L.load().ewvit_bn_se_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
+            if (link is not None and _SE_DX_FOLD and xc.dtype == torch.bfloat16 and
+                    L.has('ewvit_dwconv3x3_bwd_fused_se') and ctx.needs_input_grad[0]):
+                # 3 launches: the sums (and dgamma / dbeta); the dx pass is the depthwise conv's
+                L.call('ewvit_bn_se_bwd', L.ptr(dyc), L.ptr(x2), L.ptr(xc), None, L.dt(xc), N, HW, C, L.ptr(gamma),
+                       L.ptr(beta), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(h1),
+                       L.ptr(s0), L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2),
+                       L.ptr(mws), L.stream(dx), work={'bytes': 3 * xc.numel() * xc.element_size()})
+                off = int(L.load().ewvit_bn_se_bwd_row_offset(N, C, Csq))
+                a = _SeDxArgs()
+                a.dy, a.z, a.gamma, a.beta, a.mean, a.invstd, a.act = dyc, xc, gamma, beta, mean, invstd, act
+                a.s, a.g, a.row, a.N, a.HW, a.C, a.ws = sc, g, mws[off:off + 2 * C], N, HW, C, mws
+                link.args, link.dx = a, dx
+                return (dx, grads.give(pg, dg, ctx.gen), grads.give(pb, db, ctx.gen), None, None, None, None, None,
+                        None, *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None, None)
             L.call('ewvit_bn_se_bwd', L.ptr(dyc), L.ptr(x2), L.ptr(xc), L.ptr(dx), L.dt(xc), N, HW, C, L.ptr(gamma),
                    L.ptr(beta), L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(h1),
                    L.ptr(s0), L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2),
                    L.ptr(mws), L.stream(dx), work={'bytes': 6 * xc.numel() * xc.element_size()})
             return (dx, grads.give(pg, dg, ctx.gen), grads.give(pb, db, ctx.gen), None, None, None, None, None, None,
-                    *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None)
+                    *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None, None)
         mws = torch.empty(L.load().ewvit_se_mlp_bwd_workspace(N, C, Csq) // 4, dtype=torch.float32, device=dev)
         L.call('ewvit_se_squeeze_mlp_bwd', L.ptr(dyc), L.ptr(x2), L.dt(x2), N, HW, C, L.ptr(sc), L.ptr(h1), L.ptr(s0),
                L.ptr(W1), L.ptr(W2), Csq, L.ptr(g), L.ptr(dW1), L.ptr(db1), L.ptr(dW2), L.ptr(db2), L.ptr(mws),
@@ -247,10 +303,10 @@ class BnActSEFn(torch.autograd.Function):
                L.ptr(mean), L.ptr(invstd), act, L.ptr(dg), L.ptr(db), L.ptr(sc), L.ptr(g), HW, L.ptr(ws),
                L.stream(dx), work={'bytes': 5 * xc.numel() * xc.element_size()})
         return (dx, grads.give(pg, dg, ctx.gen), grads.give(pb, db, ctx.gen), None, None, None, None, None, None,
-                *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None)
+                *_give_se(ctx, dW1, o1, db1, dW2, o2, db2), None, None)
 
 
-def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2, partials=None):
+def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2, partials=None, link=None):
     """SE(act(bn(x))) for a training-mode BatchNorm module `bn` (batch statistics, running
     statistics and counter updated like batch_norm_act) and the SE's 1x1 conv parameters
     (fc1 = (se_w1, se_b1), fc2 = (se_w2, se_b2)) — see BnActSEFn.  `partials` = (part,
@@ -263,7 +319,7 @@ def bn_act_se(x, bn, act, se_w1, se_b1, se_w2, se_b2, partials=None):
         x = x.float()
     counter = bn.num_batches_tracked if bn.track_running_stats else None
     return BnActSEFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, counter,
-                           ACT[act], se_w1, se_b1, se_w2, se_b2, partials)
+                           ACT[act], se_w1, se_b1, se_w2, se_b2, partials, link)
 
 
 def squeeze_excite(x, w1, b1, w2, b2):

@@ -103,14 +103,15 @@ class ConvBNAct(nn.Sequential):
                     return r[0], r[1:]
         return None
 
-    def dw_stats(self, x):
+    def dw_stats(self, x, selink=None):
         """(y, part, shifts, nrc): the depthwise conv with its BatchNorm's statistics summed by
-        the conv kernel (ewvit.ops.dwconv3x3_bn_stats), or None."""
+        the conv kernel (ewvit.ops.dwconv3x3_bn_stats), or None.  `selink`: the BN + SE after it
+        may leave its backward's dx pass to the conv (ewvit.se.SeDxLink)."""
         conv, bn = self[0], self[1]
         if not (_DW_STATS and type(conv) is DepthwiseConv2d and conv.padding == (1, 1) and bn.training
                 and bn.track_running_stats and bn.momentum is not None and x.is_cuda and not self._hooked()):
             return None
-        return ewvit.ops.dwconv3x3_bn_stats(x, conv.weight, conv.stride[0], bn.running_mean)
+        return ewvit.ops.dwconv3x3_bn_stats(x, conv.weight, conv.stride[0], bn.running_mean, selink)
 
     def can_bn_se(self, x, se):
         """This block's BatchNorm + act on input x's conv output, then `se`, as one
@@ -201,10 +202,14 @@ def _seq(mods, h):
         m = mods[i]
         if isinstance(m, ConvBNAct) and i + 1 < len(mods) and m.can_bn_se(h, mods[i + 1]):
             se = mods[i + 1]
-            r = m.dw_stats(h)
+            # the BN + SE backward's dx pass folded into the depthwise conv's backward (SeDxLink)
+            link = ewvit.se.SeDxLink() if torch.is_grad_enabled() else None
+            r = m.dw_stats(h, link)
+            if r is None:
+                link = None
             y, part = (r[0], r[1:]) if r is not None else (m[0](h), None)
             h = ewvit.bn_act_se(y, m[1], 'silu' if len(m) > 2 else None, se.fc1.weight, se.fc1.bias,
-                                se.fc2.weight, se.fc2.bias, partials=part)
+                                se.fc2.weight, se.fc2.bias, partials=part, link=link)
             i += 2
             continue
         h = m(h)

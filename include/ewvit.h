@@ -230,6 +230,20 @@ int ewvit_dwconv3x3_bwd_fused(const void *dy, const float *w, void *dx, const vo
                               int64_t N, int64_t H, int64_t W, int64_t C, const void *bx, const float *mean,
                               const float *invstd, const float *gamma, const float *beta, int act, float *part,
                               float *workspace, void *stream);
+/* ewvit_dwconv3x3_bwd_fused with the backward of the BatchNorm(+act se_act) + squeeze-excitation
+ * that consumed the conv's OUTPUT folded in (MBConv: depthwise conv -> BN -> SiLU -> SE): dy is
+ * the SE output gradient; the conv's output gradient dz = gamma*invstd*(act'(zhat*gamma+beta)*
+ * (dy*s + g) - row[c]/n - zhat*row[C+c]/n), zhat = (z - se_mean)*se_invstd, n = N*H*W, is formed
+ * per window element (zero outside the map) and rounded to bf16 — the same operations as
+ * ewvit_bn_se_bwd's dx pass, so the same bits — and never stored.  z: the BN input (the conv's
+ * output) [N,H,W,C] bf16; se_row: the sums row ewvit_bn_se_bwd (dx NULL) leaves in its workspace
+ * at ewvit_bn_se_bwd_row_offset floats; se_s / se_g [N][C]: the excitation and squeeze term. */
+int ewvit_dwconv3x3_bwd_fused_se(const void *dy, const float *w, void *dx, const void *x, float *dw,
+                                 int accumulate, int64_t N, int64_t H, int64_t W, int64_t C, const void *bx,
+                                 const float *mean, const float *invstd, const float *gamma, const float *beta,
+                                 int act, float *part, float *workspace, const void *z, const float *se_mean,
+                                 const float *se_invstd, const float *se_gamma, const float *se_beta, int se_act,
+                                 const float *se_row, const float *se_s, const float *se_g, void *stream);
 
 /* ---------------------------------------------- BatchNorm2d + activation ---
  * BatchNorm2d (batch statistics in training, running statistics in eval) fused
@@ -622,13 +636,20 @@ int ewvit_se_squeeze_mlp_bwd(const void *dy, const void *x, int dtype, int64_t N
  * moment) and formed in the SE squeeze pass that streams dy and a anyway — the BN's own
  * reduction pass over dy and z never runs.  a: the SE input act(BN(z)) as the forward stored
  * it; z: the BN input; save_mean / save_invstd from the forward.  C % 8 == 0, C <= 4096.
- * workspace: ewvit_bn_se_bwd_workspace(N, C, Csq) bytes. */
+ * workspace: ewvit_bn_se_bwd_workspace(N, C, Csq) bytes.  dx NULL: 3 launches, no dx pass —
+ * dgamma / dbeta are written by the sums pass and the sums row [2C] stays in the workspace at
+ * ewvit_bn_se_bwd_row_offset(N, C, Csq) floats for ewvit_dwconv3x3_bwd_fused_se (or
+ * ewvit_bn_se_bwd_dx, the dx pass alone). */
 int64_t ewvit_bn_se_bwd_workspace(int64_t N, int64_t C, int64_t Csq);
+int64_t ewvit_bn_se_bwd_row_offset(int64_t N, int64_t C, int64_t Csq);
 int ewvit_bn_se_bwd(const void *dy, const void *a, const void *z, void *dx, int dtype, int64_t N, int64_t HW,
                     int64_t C, const float *gamma, const float *beta, const float *save_mean,
                     const float *save_invstd, int act, float *dgamma, float *dbeta, const float *s,
                     const float *h1, const float *s0, const float *w1, const float *w2, int64_t Csq, float *g,
                     float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream);
+int ewvit_bn_se_bwd_dx(const void *dy, const void *z, void *dx, int dtype, int64_t N, int64_t HW, int64_t C,
+                       const float *gamma, const float *beta, const float *save_mean, const float *save_invstd,
+                       int act, const float *s, const float *g, const float *row, void *stream);
 /* y = r * scale[n] (+ x when x != NULL) over N rows of row_elems elements (row_elems % 8 == 0):
  * StochasticDepth(mode='row') with its keep/(1-p) factor fused with the skip add. */
 int ewvit_scale_add(const void *r, const void *x, int dtype, const float *scale, void *y, int64_t N,

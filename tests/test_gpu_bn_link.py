@@ -546,3 +546,62 @@ def test_dwconv_refuses_links_it_cannot_sum(kind, monkeypatch):
         wdw = wdw.detach()
     for a, b in zip(*res):
         torch.testing.assert_close(b, a, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize('N,C,H,W,act', [(64, 960, 14, 14, 2), (16, 1536, 7, 7, 2), (4, 200, 9, 11, 1), (2, 64, 30, 30, 0)])
+def test_dw_bwd_fused_se(N, C, H, W, act):
+    """ewvit_dwconv3x3_bwd_fused_se (the BN(+act) + SE backward of the conv's output folded into
+    the fused depthwise backward: dz formed per window element from the SE output gradient and z)
+    against ewvit_bn_se_bwd_dx (that dx pass alone, writing dz) + ewvit_dwconv3x3_bwd_fused on dz:
+    dx, the producing BN's backward sums and dW bit for bit with act 0 / 1; with SiLU (act 2) the
+    compiler schedules the exp / reciprocal differently in the two kernels, so dz may differ by one
+    bf16 rounding: dx within 2 bf16 ulps of its scale, the sums and dW within 1e-3 relative."""
+    L = _L()
+    g = torch.Generator().manual_seed(C * 7 + W)
+    dys = bf(torch.randn(N, C, H, W, generator=g))
+    z = bf(torch.randn(N, C, H, W, generator=g) * 1.3 - 0.2)
+    x = bf(torch.randn(N, C, H, W, generator=g))
+    bx = bf(torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3)
+    w = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).to(DEV).contiguous()
+    gamma = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    g2 = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV)
+    b2 = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    mean, invstd = _bn_stats(bx)
+    m2, i2 = _bn_stats(z)
+    s = torch.rand(N, C, generator=g).to(DEV)
+    gs = (torch.randn(N, C, generator=g) * 0.01).to(DEV)
+    row = (torch.randn(2 * C, generator=g) * N * H * W * 0.01).to(DEV)
+    dz = torch.empty_like(dys)
+    L.call('ewvit_bn_se_bwd_dx', L.ptr(dys), L.ptr(z), L.ptr(dz), L.BF16, N, H * W, C, L.ptr(g2), L.ptr(b2), L.ptr(m2),
+           L.ptr(i2), act, L.ptr(s), L.ptr(gs), L.ptr(row), L.stream(dys))
+    nrc = int(L.load().ewvit_dwconv3x3_bn_rows(N, H, W, C, 1, 1))
+    wsb = int(L.load().ewvit_dwconv3x3_bwd_fused_workspace(N, H, W, C))
+    outs = []
+    for fold in (False, True):
+        dx = torch.full_like(dys, float('nan'))
+        part = torch.full((nrc, 2 * C), float('nan'), device=DEV)
+        ws = torch.full((wsb // 4,), float('nan'), device=DEV)
+        dw = torch.full((C, 1, 3, 3), float('nan'), device=DEV)
+        if fold:
+            L.call('ewvit_dwconv3x3_bwd_fused_se', L.ptr(dys), L.ptr(w), L.ptr(dx), L.ptr(x), L.ptr(dw), 0, N, H, W, C,
+                   L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 2, L.ptr(part), L.ptr(ws),
+                   L.ptr(z), L.ptr(m2), L.ptr(i2), L.ptr(g2), L.ptr(b2), act, L.ptr(row), L.ptr(s), L.ptr(gs),
+                   L.stream(dys))
+        else:
+            L.call('ewvit_dwconv3x3_bwd_fused', L.ptr(dz), L.ptr(w), L.ptr(dx), L.ptr(x), L.ptr(dw), 0, N, H, W, C,
+                   L.ptr(bx), L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), 2, L.ptr(part), L.ptr(ws),
+                   L.stream(dys))
+        outs.append((dx, part, dw))
+    torch.cuda.synchronize()
+    (dx0, p0, w0), (dx1, p1, w1) = outs
+    assert not torch.isnan(dx1).any() and not torch.isnan(w1).any()
+    if act != 2:
+        assert torch.equal(dx0, dx1), float((dx0.float() - dx1.float()).abs().max())
+        assert torch.equal(p0, p1)
+        assert torch.equal(w0, w1)
+        return
+    sc = float(dx0.float().abs().max())
+    assert float((dx0.float() - dx1.float()).abs().max()) <= 2 * sc * 2 ** -8
+    for a, b in ((p0, p1), (w0, w1)):
+        assert float((a - b).abs().max()) <= 1e-3 * float(a.abs().max())
