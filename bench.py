@@ -195,7 +195,7 @@ ENTRY_KERNELS = {
     'ewvit_conv2d_bwd_data': ['conv_fwd_kernel<true', 'conv_glds_kernel<true', 'conv_win_kernel<true, false, false, false'],
     'ewvit_conv2d_bwd_weight': ['conv_wgrad_kernel', 'conv_wgrad_glds_kernel', 'conv_wgrad_1x1_kernel',
                                 'conv_wgrad_win_kernel<true, false', 'conv_wgrad_win_kernel<false, false',
-                                'conv_wgrad_reduce_kernel'],
+                                'conv_wgrad_reduce_kernel', 'red_jobs_kernel'],
     # the windowed MWT convs (csrc/convwin.hip): the input-gradient kernels with the BatchNorm
     # backward sums in their epilogue, the forward / weight gradient with the folded input
     # transform (XF); template arguments <DGRAD, STATS, XF, BST, KS> / <BIAS, XF, TS>.  The
