@@ -135,8 +135,12 @@ def build_step(dev, frames, rank, graph=True, config=2, force_collectives=False)
         loss, _ = combined_loss(out, y, crit, 1, 1, weight=orth_w)
         return loss
     # gradients averaged over ranks by bucketed RCCL all-reduces issued during backward;
-    # the whole iteration replayed from one HIP graph (ewvit/graph.py)
-    return TrainStep(model, forward_loss, opt, graph=graph, force_collectives=force_collectives)
+    # the whole iteration replayed from one HIP graph (ewvit/graph.py).  EWVIT_EARLY_STEP=1 (A/B,
+    # measured slower): everything but the backbone takes its Adam update as soon as its
+    # gradients are final, beside the backbone's backward (TrainStep early_params)
+    backbone = {id(p) for p in model.dama.sfe.efficient_net.parameters()}
+    early = [p for p in params if id(p) not in backbone]
+    return TrainStep(model, forward_loss, opt, graph=graph, force_collectives=force_collectives, early_params=early)
 
 
 def kernel_table(records):

@@ -292,7 +292,7 @@ class BufferSync:
 
 class TrainStep:
     def __init__(self, model, forward_loss, optimizer, graph=True, warmup=3, group=None, bucket_mb=32,
-                 accum_steps=1, overlap=True, force_collectives=False, grad_comm_dtype=None):
+                 accum_steps=1, overlap=True, force_collectives=False, grad_comm_dtype=None, early_params=None):
         """``force_collectives``: issue the bucket all-reduces and the buffer broadcast even in
         a world of one (test switch; needs an initialised process group).  A failure to
         capture the collectives raises, unless EWVIT_GRAPH_SPLIT_FALLBACK=1 allows the split,
@@ -318,6 +318,7 @@ class TrainStep:
         if self.buckets is not None:
             self.buckets.defer = not overlap
         self.bufsync = BufferSync(model, group) if dp else None
+        self._early_init(early_params)
         self.loss = None
         self.mode = 'graph' if self.graph else 'eager'
         self._hyper = optimizer.hyper_signature() if hasattr(optimizer, 'hyper_signature') else None
@@ -350,6 +351,78 @@ class TrainStep:
                 self.fallback = f'{type(e).__name__}: {e}'
                 self._capture_split(warmup)
 
+    # ---- early optimizer step: the parameters whose gradients are final long before the end of
+    # the backward pass (DAMA: everything but the backbone, whose backward is the critical path)
+    # are updated on a side stream as soon as the last of their gradients has been accumulated,
+    # so only the backbone's update remains after the backward pass.  Per-parameter Adam: the
+    # same bits as one step() (tests/test_gpu_graph.py).  World 1, one micro-batch, an optimizer
+    # with step_subset (ewvit.optim.Adam); their weight gradients are never deferred
+    # (ewvit.grads.deferrable), so the last accumulation is the last write.  Opt-in
+    # (EWVIT_EARLY_STEP=1): at config 2 the early update's 1.1 GB of HBM traffic beside the two
+    # branches costs more than the ~190 us it takes off the end of the step (3833-3838 against
+    # 3888-3891 frames/s, profiles/r06/s2/ab/early_step.log).
+    def _early_init(self, early_params):
+        self._early = None
+        if (early_params is None or os.environ.get('EWVIT_EARLY_STEP', '0') != '1' or self.world > 1
+                or self.accum != 1 or not hasattr(self.opt, 'step_subset')):
+            return
+        train = {id(p) for p in self.params}
+        early = [p for p in early_params if id(p) in train]
+        if not early or len(early) == len(self.params):
+            return
+        eids = {id(p) for p in early}
+        self._early = {'ids': eids, 'late': {id(p) for p in self.params if id(p) not in eids}, 'n': len(early),
+                       'left': 0, 'events': {}, 'fired': False, 'on': False, 'stream': None}
+        for p in early:
+            p._ewvit_early = True
+        self._early['hooks'] = [p.register_post_accumulate_grad_hook(self._early_hook) for p in early]
+        self.opt._split_steps = 2
+
+    def _early_hook(self, p):
+        e = self._early
+        if e is None or not e['on'] or p.grad is None:
+            return
+        if p.grad.is_cuda:
+            st = torch.cuda.current_stream(p.grad.device)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            e['events'][st.cuda_stream] = ev         # the stream's latest gradient write
+        e['left'] -= 1
+        if e['left'] == 0:
+            if e['stream'] is None:
+                e['stream'] = torch.cuda.Stream(device=p.device)
+            side = e['stream']
+            for ev in e['events'].values():
+                side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self.opt.step_subset('early', e['ids'])
+            e['fired'] = True
+
+    def _early_close(self):
+        e = getattr(self, '_early', None)
+        if e is None:
+            return
+        for h in e['hooks']:
+            h.remove()
+        for p in self.params:
+            if id(p) in e['ids'] and hasattr(p, '_ewvit_early'):
+                del p._ewvit_early
+        self.opt.__dict__.pop('_split_steps', None)
+        self._early = None
+
+    def _opt_step(self):
+        e = self._early
+        if e is None:
+            self.opt.step()
+            return
+        e['on'] = False
+        if e['fired']:
+            torch.cuda.current_stream().wait_stream(e['stream'])
+            self.opt.step_subset('late', e['late'])
+        else:                                        # not every early gradient arrived: one step
+            self.opt.step_subset('early', e['ids'])
+            self.opt.step_subset('late', e['late'])
+
     def close(self):
         """Release the captured graphs (after the device has drained them) and detach from the
         model: remove the gradient hooks and slots of the buckets.  Call it while the process
@@ -369,6 +442,7 @@ class TrainStep:
         if self.buckets is not None:
             self.buckets.remove()
             self.buckets = None
+        self._early_close()
 
     def describe(self):
         d = {'launch': 'hip-graph' if self.graph else 'eager', 'world': self.world}
@@ -413,10 +487,12 @@ class TrainStep:
         if self.buckets is not None:
             self.bufsync()
             self.buckets.begin()
+        if self._early is not None:
+            self._early.update(left=self._early['n'], events={}, fired=False, on=True)
         loss = self._fwd_bwd()
         if self.buckets is not None:
             self.buckets.finish()
-        self.opt.step()
+        self._opt_step()
         return loss
 
     def _eager(self):

@@ -98,10 +98,10 @@ class Adam(torch.optim.Optimizer):
         """The hyper-parameters a recorded step bakes in as launch constants."""
         return tuple((tuple(g['betas']), float(g['eps']), float(g['weight_decay'])) for g in self.param_groups)
 
-    def _group_step(self, gi, group):
+    def _group_step(self, gi, group, subset=None, tag=None):
         items = []
         for p in group['params']:
-            if p.grad is None:
+            if p.grad is None or (subset is not None and id(p) not in subset):
                 continue
             if p.grad.is_sparse:
                 raise RuntimeError('ewvit.optim.Adam: sparse gradients are not supported')
@@ -128,7 +128,7 @@ class Adam(torch.optim.Optimizer):
             self.sync_hyper()           # raises inside a capture: never record the scalar's fill
         lr_dev = L.ptr(self._lr_dev[gi][0])
         stream = L.stream(items[0][0])
-        if self._table_step(gi, group, items, lr_dev, stream):
+        if self._table_step(gi if tag is None else (gi, tag), group, items, lr_dev, stream):
             return
         for k in range(0, len(items), L.ADAM_MAX):
             chunk = items[k:k + L.ADAM_MAX]
@@ -237,8 +237,20 @@ class Adam(torch.optim.Optimizer):
         """Adam kernel launches one step makes, by kernel name, in either launch form (the
         profilers count step equivalents from them, whichever form the profiled build took)."""
         groups = [sum(1 for p in g['params'] if p.requires_grad) for g in self.param_groups]
-        return {'adam_table_kernel': sum(1 for n in groups if n),
-                'adam_multi_kernel': sum(-(-n // L.ADAM_MAX) for n in groups)}
+        k = int(self.__dict__.get('_split_steps', 1))      # step_subset calls per step (TrainStep early_params)
+        return {'adam_table_kernel': k * sum(1 for n in groups if n),
+                'adam_multi_kernel': sum(-(-n // L.ADAM_MAX) for n in groups) + (k - 1) * sum(1 for n in groups if n)}
+
+    @torch.no_grad()
+    def step_subset(self, tag, params):
+        """``step()`` restricted to `params` (a set of parameter ids): the same per-parameter
+        update, launched on the current stream with its own device table (`tag` names it).  The
+        training step uses it to update the parameters whose gradients are final before the end of
+        the backward pass early, on a side stream (ewvit.graph.TrainStep ``early_params``)."""
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_hyper()
+        for gi, group in enumerate(self.param_groups):
+            self._group_step(gi, group, params, tag)
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -195,3 +195,48 @@ def test_grad_slots_adopted_and_multi_use():
         torch.testing.assert_close(p.grad, r, rtol=1e-5, atol=1e-6)
     for i in (0, 1, 2, 3):                   # written in place (two uses: summed in place), no clone
         assert stolen[i] == gb.views[i].data_ptr(), i
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_trainstep_early_params_same_update(graph):
+    """TrainStep(early_params=...): the parameters whose gradients are final early get their
+    Adam update on a side stream as soon as the last of them is accumulated, the rest after the
+    backward — the same bits as one optimizer step (ewvit.optim.Adam is per-parameter), eager and
+    replayed; the early step really fires before the end of the backward pass."""
+    import ewvit
+    from ewvit.graph import TrainStep
+    a, b = _mwt_pair()
+    x = torch.randn(4, 3, 64, 64, device=DEV)
+
+    def make(m):
+        opt = ewvit.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=3e-3, weight_decay=1e-4)
+
+        def fl():
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                return m(x).float().square().mean()
+        return fl, opt
+    fa, oa = make(a)
+    fb, ob = make(b)
+    import ewvit.graph as egraph
+    import os
+    os.environ['EWVIT_EARLY_STEP'] = '1'
+    sa = TrainStep(a, fa, oa, graph=graph, warmup=2)
+    # the layers nearest the loss finish their gradients first: the last half of the parameters
+    pb = [p for p in b.parameters() if p.requires_grad]
+    try:
+        sb = TrainStep(b, fb, ob, graph=graph, warmup=2, early_params=pb[len(pb) // 2:])
+    finally:
+        del os.environ['EWVIT_EARLY_STEP']
+    del egraph
+    assert sb._early is not None and ob.launches_per_step()['adam_table_kernel'] == 2
+    for _ in range(3):
+        sa()
+        sb()
+    torch.cuda.synchronize()
+    assert sb._early['fired']                       # issued from the backward pass, not the fallback
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
+    for (n, u), v in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(u, v), n
+    sb.close()
+    assert not any(getattr(p, '_ewvit_early', False) for p in b.parameters())
