@@ -219,8 +219,8 @@ def load():
     if os.environ.get('EWVIT_WIN_NT', '').isdigit() and hasattr(lib, 'ewvit_conv2d_set_win_nt'):
         lib.ewvit_conv2d_set_win_nt(int(os.environ['EWVIT_WIN_NT']))   # A/B switch (convwin.hip g_win_nt)
     if os.environ.get('EWVIT_W1X1') and hasattr(lib, 'ewvit_conv2d_set_wgrad_1x1'):
-        # A/B: the 1x1 weight gradient's split rule "workgroup target,min K-tiles per split"
-        wg, mk = (int(v) for v in os.environ['EWVIT_W1X1'].split(','))
+        # A/B: the 1x1 weight gradient's split rule "workgroup target:min K-tiles per split"
+        wg, mk = (int(v) for v in os.environ['EWVIT_W1X1'].split(':'))
         lib.ewvit_conv2d_set_wgrad_1x1(wg, mk, 0)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
