@@ -351,7 +351,7 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] and dbf is None and grads.deferrable(wparam, dwf, ctx.gen) and _defer.available():
             # dW is read by nobody before the end of the backward (ewvit.grads.deferrable): the
             # split-K reduce rides in a later weight-gradient launch (ewvit.defer)
-            _defer.mark(ws, xc.device)
+            _defer.mark(ws, dwf, xc.device)
         L.call('ewvit_conv2d_bwd_weight', L.ptr(xc), L.ptr(dyc), L.ptr(dwf), L.ptr(dbf), 0, N, H, W, Cx,
                Cout, k, stride, gc, gs, Cin, s_co, s_ci, s_kw, L.ptr(ws), L.stream(dwf), work=work)
         return (dwf if ctx.needs_input_grad[1] else None), dbf

@@ -13,7 +13,9 @@ they write a parameter's gradient slot (``ewvit.grads``: AccumulateGrad adopts t
 without reading it).  The readers flush first: the end of the backward pass (an engine
 callback queued by the first deferral), ``grads._settle`` (multi-use sums), and the
 data-parallel bucket all-reduce (``graph.GradBuckets._fire``).  The partial slabs stay
-allocated until ``flush()``.  ``EWVIT_DEFER_REDUCE=0`` turns the deferral off (A/B).
+allocated until ``flush()``, and so do the dW tensors (a backward pass that raises before
+its end leaves jobs that the next deferral flushes into them).  ``EWVIT_DEFER_REDUCE=0``
+turns the deferral off (A/B).
 
 Replaces nothing in the reference: torch's weight-gradient convs inside the backbone
 (network/sfe.py:111-113) reduce internally.
@@ -30,27 +32,41 @@ ENABLED = os.environ.get('EWVIT_DEFER_REDUCE', '1') != '0'
 
 _lock = threading.Lock()
 _held = {}            # stream handle -> (stream, [workspaces kept alive until the flush])
-_queued = False       # an end-of-backward flush is queued (the engine may run it on any thread)
+_queued = -1          # graph task whose end-of-backward flush is queued (the engine may run it on any thread)
 
 
 def available():
     return ENABLED and hasattr(L.load(), 'ewvit_reduce_defer_next')
 
 
-def mark(ws, device):
+def mark(ws, out, device):
     """Make the next reduce-producing library call on this thread defer its reduce, keeping
-    `ws` (its partial-slab workspace) alive until ``flush()``.  Call right before the call.
-    False (nothing marked) outside a backward pass, where no flush would follow."""
+    `ws` (its partial-slab workspace) and the memory of `out` (the dW it writes) alive until
+    ``flush()``.
+    Call right before the call.  False (nothing marked) outside a backward pass, where no
+    flush would follow."""
     global _queued
+    task = torch._C._current_graph_task_id()
+    if task < 0:
+        return False
+    stale = False
     with _lock:
-        if not _queued:
+        if _queued != task:
+            # another graph task: a nested backward (its end flushes everything, which is safe) or
+            # one that raised before its end — its jobs run now, into tensors kept alive here
+            stale = _queued >= 0 and bool(_held)
             try:
                 torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
             except RuntimeError:
                 return False
-            _queued = True
+            _queued = task
+    if stale:
+        flush()
+    with _lock:
         st = torch.cuda.current_stream(device)
-        _held.setdefault(st.cuda_stream, (st, []))[1].append(ws)
+        # (dW's storage, not the tensor: another reference to the tensor object would make
+        # AccumulateGrad clone — read — it instead of adopting it)
+        _held.setdefault(st.cuda_stream, (st, []))[1].extend((ws, out.untyped_storage()))
     L.load().ewvit_reduce_defer_next(1)
     return True
 
@@ -58,7 +74,7 @@ def mark(ws, device):
 def _end_of_backward():
     global _queued
     with _lock:
-        _queued = False
+        _queued = -1
     flush()
 
 

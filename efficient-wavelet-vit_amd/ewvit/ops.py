@@ -624,7 +624,7 @@ class DepthwiseConv3x3Fn(torch.autograd.Function):
                     if direct and grads.deferrable(ctx.params[0], dw, ctx.gen) and _defer.available():
                         # dW is read by nobody before the end of the backward (grads.deferrable):
                         # its slab sum rides in a later weight-gradient launch (ewvit.defer)
-                        _defer.mark(ws, xc.device)
+                        _defer.mark(ws, dw, xc.device)
                     if fold is not None:
                         # ... with the BN + SE backward of this conv's output folded in: dy is the SE
                         # output gradient, the conv's output gradient is formed per window element

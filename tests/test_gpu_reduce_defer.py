@@ -123,8 +123,8 @@ def _grads(m, x, graph, enabled, steps=1):
     calls = []
     real = defer.mark
 
-    def spy(ws, dev):
-        ok = real(ws, dev)
+    def spy(ws, out, dev):
+        ok = real(ws, out, dev)
         calls.append(ok)
         return ok
     old, defer.ENABLED, defer.mark = defer.ENABLED, enabled, spy
@@ -225,3 +225,59 @@ def test_se_dx_fold(graph):
     assert float((va - vb).norm() / va.norm()) < 5e-2        # (measured 1.6e-2)
     dcd = [n for n in gd if not torch.equal(gc[n], gd[n])]
     assert not dcd, dcd[:6]
+
+
+def test_defer_after_failed_backward():
+    """A backward pass that raises after deferring reductions leaves its jobs queued; the next
+    backward's first deferral runs them (into memory kept alive for them) and its own gradients
+    come out right — the same bits as with the deferral off."""
+    import ewvit
+    from ewvit import defer, grads
+    from network.efficientnet import Conv2d
+
+    class Boom(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            raise RuntimeError('boom')
+
+    torch.manual_seed(3)
+    c1 = Conv2d(64, 256, 1, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    c2 = Conv2d(256, 128, 1, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 64, 28, 28, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+
+    def run(fail, enabled):
+        old, defer.ENABLED = defer.ENABLED, enabled
+        try:
+            for p in (*c1.parameters(), *c2.parameters()):
+                p.grad = None
+            grads.begin_step()
+            h = c1(x)
+            y = c2(Boom.apply(h) if fail else h)
+            loss = y.float().square().mean()
+            if fail:
+                with pytest.raises(RuntimeError, match='boom'):
+                    loss.backward()
+            else:
+                loss.backward()
+            grads.end_step()
+        finally:
+            defer.ENABLED = old
+        return c1.weight.grad, c2.weight.grad
+
+    ref = [g.clone() for g in run(False, False)]
+    calls = []
+    real = defer.mark
+    defer.mark = lambda ws, out, dev: calls.append(1) or real(ws, out, dev)
+    try:
+        run(True, True)                                  # c2's wgrad deferred, then the raise
+        assert calls and _pending() >= 1
+        got = run(False, True)
+    finally:
+        defer.mark = real
+    torch.cuda.synchronize()
+    assert _pending() == 0
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
