@@ -22,8 +22,10 @@ import ewvit
 
 # BatchNorm statistics summed in the producing conv's epilogue when the conv has at
 # most this many 128-row output tiles: every BN apply block re-reads all partial rows
-# while finalising, so the fusion pays only for small maps
-_EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '32'))
+# while finalising, so the fusion pays only for small maps.  128 (the stage-5 14^2 maps at 64
+# frames now included) after the deferred reductions: 3904-3916 against 3886-3890 frames/s at 32,
+# 512 3874-3901, unbounded 3898-3899 (profiles/r06/s2/ab/epi_stats_tiles.log)
+_EPI_STATS_MAX_TILES = int(os.environ.get('EWVIT_EPI_STATS_MAX_TILES', '128'))
 # residual blocks hand their skip gradient to the first conv's dgrad epilogue (SkipLink)
 _SKIP_LINK = os.environ.get('EWVIT_SKIP_LINK', '1') != '0'
 # the frozen 3-channel stem on the ewvit direct conv (0: the library conv, A/B)
