@@ -105,6 +105,9 @@ def deferrable(param, t, gen):
     hooks (AccumulateGrad steals it: default layout, no other reference)."""
     if param is None or not param.is_leaf or not param.requires_grad:
         return False
+    if torch.is_grad_enabled():
+        # a create_graph backward: AccumulateGrad clones (reads) the gradient instead of adopting it
+        return False
     if getattr(param, '_ewvit_early', False):        # updated as soon as its gradient lands (TrainStep)
         return False
     if is_slot(param, t):
