@@ -25,7 +25,10 @@ _BWD_LINK = os.environ.get('EWVIT_BN_BWD_LINK', '1') != '0'
 # Links over bigger maps (the MWT's 2.4 M-row convs, partials folded) measured slower — the
 # input-gradient epilogue's BN-input reads under the capped walk cost more than the reduction
 # pass they replace (MWT capped 14.0 -> 15.6 ms) — so those BNs reduce themselves.
-BWD_LINK_MAX_ROWS = 512
+# 128 since round 6 (the 28^2 backbone maps now reduce themselves): 3957-3963 against 3925-3935
+# frames/s at 512, 64 3960-3962, 32 3948-3950, 2048 / 8192 3888-3893 / 3874-3877, no links 3794-3798
+# (profiles/r06/s2/ab/bwd_link_rows.log)
+BWD_LINK_MAX_ROWS = int(os.environ.get('EWVIT_BWD_LINK_MAX_ROWS', '128'))
 
 
 class BwdStatsLink:
