@@ -156,10 +156,22 @@ static BnGeo bn_geo(int64_t C) {
 // BatchNorm cap, 64 - 640 workgroups, measured no better: DESIGN §5.6)
 static int bn_cap() { return g_grid_cap > 0 ? g_grid_cap : 0; }
 
+// (A/B) EWVIT_BN_GEO="reduction blocks:reduction rows per thread:elementwise blocks:elementwise
+// rows per thread" overrides the four constants below (read once)
+static int bn_knob(int which, int dflt) {
+  static int v[4] = {-1, -1, -1, -1};
+  static bool init = false;
+  if (!init) {
+    init = true;
+    if (const char *e = getenv("EWVIT_BN_GEO")) sscanf(e, "%d:%d:%d:%d", &v[0], &v[1], &v[2], &v[3]);
+  }
+  return v[which] > 0 ? v[which] : dflt;
+}
+
 static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
   // <= 256 partial rows, >= 16 rows per thread (8 / 32 measured 0.3-2 % slower on the SFE)
-  constexpr int cap = 256, minr = 16;
-  int64_t nrc = (512 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
+  const int cap = 256, minr = bn_knob(1, 16);
+  int64_t nrc = (bn_knob(0, 512) + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   if (nrc > cap) nrc = cap;
   const int64_t maxr = M / ((int64_t)g.RG * minr);
   if (nrc > maxr) nrc = maxr;
@@ -168,10 +180,11 @@ static int bn_nrc(const BnGeo &g, int64_t M, int groups) {
   return (int)nrc;
 }
 
-// elementwise passes: ~1024 blocks in all, 8..64 rows per thread
+// elementwise passes: ~512 blocks in all, 8..64 rows per thread (round 6: 512 / 384 against the
+// earlier 1024: +0.5-0.7 % at config 2 on three boxes, profiles/r06/s2/ab/bn_geometry.log)
 static int64_t bn_rows_per_block(const BnGeo &g, int64_t M, int groups) {
-  constexpr int minr = 8;          // rows per thread at least (4 / 16 measured slower)
-  int64_t rb = (1024 + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
+  const int minr = bn_knob(3, 8);  // rows per thread at least (4 / 16 measured slower)
+  int64_t rb = (bn_knob(2, 512) + (int64_t)g.nch * groups - 1) / ((int64_t)g.nch * groups);
   int64_t rpt = (M + (int64_t)g.RG * rb - 1) / ((int64_t)g.RG * rb);
   rpt = rpt < minr ? minr : (rpt > 64 ? 64 : rpt);
   if (bn_cap() > 0) {            // capped grid: more rows per block, at most cap blocks in all
