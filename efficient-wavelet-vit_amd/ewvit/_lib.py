@@ -218,10 +218,12 @@ def load():
         lib.ewvit_conv2d_set_wgrad_tap_split(int(os.environ['EWVIT_WGWIN_TS']))   # A/B (convwin.hip wgrad NG)
     if os.environ.get('EWVIT_WIN_NT', '').isdigit() and hasattr(lib, 'ewvit_conv2d_set_win_nt'):
         lib.ewvit_conv2d_set_win_nt(int(os.environ['EWVIT_WIN_NT']))   # A/B switch (convwin.hip g_win_nt)
+    if os.environ.get('EWVIT_WGRAD_WIDE') in ('0', '2') and hasattr(lib, 'ewvit_conv2d_set_wgrad_wide'):
+        lib.ewvit_conv2d_set_wgrad_wide(int(os.environ['EWVIT_WGRAD_WIDE']))   # A/B (conv.hip wgrad_wide)
     if os.environ.get('EWVIT_W1X1') and hasattr(lib, 'ewvit_conv2d_set_wgrad_1x1'):
-        # A/B: the 1x1 weight gradient's split rule "workgroup target:min K-tiles per split"
-        wg, mk = (int(v) for v in os.environ['EWVIT_W1X1'].split(':'))
-        lib.ewvit_conv2d_set_wgrad_1x1(wg, mk, 0)
+        # A/B: the 1x1 weight gradient's split rule "workgroup target:min K-tiles per split[:ring]"
+        v = [int(x) for x in os.environ['EWVIT_W1X1'].split(':')]
+        lib.ewvit_conv2d_set_wgrad_1x1(v[0], v[1], v[2] if len(v) > 2 else 0)
     if os.environ.get('EWVIT_DWTF_PF') in ('2', '4') and hasattr(lib, 'ewvit_dwt_set_pf'):
         lib.ewvit_dwt_set_pf(int(os.environ['EWVIT_DWTF_PF']))   # A/B switch (dwt.hip)
     _lib = lib
